@@ -1,0 +1,164 @@
+"""Native build driver for ptype_amd (no setuptools, no JIT cache).
+
+Builds two in-tree extension modules:
+
+* ``ptype_amd/_core*.so`` -- host-only C++17 control plane (config/YAML, MVCC KV,
+  leases, watch, Raft, TCP transport, registry, KV store, balancer, Go net/rpc
+  gob codec).  Compiled with g++; no HIP dependency so it can be built with
+  host sanitizers (``PTYPE_SANITIZE=thread|address``).
+* ``ptype_amd/_hip*.so`` -- HIP/CDNA4 device runtime (gfx950 only): HBM mailbox
+  rings, GPU registry hash table, route/dispatch/complete kernels, persistent
+  dispatcher, snapshot pack kernels.  Compiled with hipcc ``--offload-arch=gfx950``.
+
+Incremental: an object is rebuilt when its source or any header under ``csrc``
+is newer than the object.  Objects live in ``build/`` (git-ignored).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = "gfx950"
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _pybind_include() -> str:
+    import pybind11
+
+    return pybind11.get_include()
+
+
+def _py_include() -> str:
+    return sysconfig.get_paths()["include"]
+
+
+def _newest_header(d: str) -> float:
+    t = 0.0
+    for h in glob.glob(os.path.join(d, "**", "*.hpp"), recursive=True) + glob.glob(
+        os.path.join(d, "**", "*.h"), recursive=True
+    ):
+        t = max(t, os.path.getmtime(h))
+    return t
+
+
+def _run(cmd: list[str]) -> None:
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if p.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + p.stdout)
+
+
+def _compile_all(jobs, max_workers):
+    with ThreadPoolExecutor(max_workers=max_workers) as ex:
+        list(ex.map(_run, jobs))
+
+
+def _variant_dir(name: str, sanitize: str | None) -> str:
+    d = os.path.join(ROOT, "build", name + (("-" + sanitize) if sanitize else ""))
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def build_core(verbose: bool = False, sanitize: str | None = None, out: str | None = None) -> str:
+    """Build the host-only control-plane module ``_core``."""
+    sanitize = sanitize or os.environ.get("PTYPE_SANITIZE") or None
+    srcs = sorted(glob.glob(os.path.join(CSRC, "core", "*.cpp")))
+    objdir = _variant_dir("core", sanitize)
+    hdr_t = _newest_header(os.path.join(CSRC, "core"))
+    cxx = os.environ.get("CXX", "g++")
+    flags = [
+        "-std=c++17", "-O2", "-g", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+        "-pthread", "-I" + os.path.join(CSRC, "core"), "-I" + _pybind_include(), "-I" + _py_include(),
+    ]
+    if sanitize:
+        flags += ["-fsanitize=" + sanitize, "-fno-omit-frame-pointer", "-O1"]
+    jobs, objs = [], []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_t):
+            jobs.append([cxx] + flags + ["-c", s, "-o", o])
+    _compile_all(jobs, 8)
+    target = out or os.path.join(PKG, "_core" + EXT)
+    if jobs or not os.path.exists(target) or os.path.getmtime(target) < max(os.path.getmtime(o) for o in objs):
+        link = [cxx, "-shared", "-pthread", "-o", target] + objs
+        if sanitize:
+            link += ["-fsanitize=" + sanitize]
+        _run(link)
+    if verbose:
+        print("built", target, "(%d objects recompiled)" % len(jobs))
+    return target
+
+
+def _torch_lib_dir() -> str | None:
+    try:
+        import importlib.util
+
+        spec = importlib.util.find_spec("torch")
+        if spec and spec.origin:
+            d = os.path.join(os.path.dirname(spec.origin), "lib")
+            if os.path.exists(os.path.join(d, "libamdhip64.so")):
+                return d
+    except Exception:
+        pass
+    return None
+
+
+def build_hip(verbose: bool = False) -> str:
+    """Build the gfx950 device-runtime module ``_hip`` with hipcc.
+
+    The module links the HIP runtime that ships inside torch (SONAME
+    libamdhip64.so.7) when present, so a process that imports torch first has
+    exactly ONE HIP runtime (torch's) -- tensors, streams and our kernels share it.
+    """
+    srcs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")) + glob.glob(os.path.join(CSRC, "hip", "*.cpp")))
+    objdir = _variant_dir("hip", None)
+    hdr_t = max(_newest_header(os.path.join(CSRC, "hip")), _newest_header(os.path.join(CSRC, "core")))
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    flags = [
+        "-std=c++17", "-O3", "-fPIC", "-fvisibility=hidden", "--offload-arch=" + ARCH,
+        "-Wno-unused-result", "-munsafe-fp-atomics",
+        "-I" + os.path.join(CSRC, "hip"), "-I" + os.path.join(CSRC, "core"),
+        "-I" + _pybind_include(), "-I" + _py_include(),
+    ]
+    jobs, objs = [], []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
+        objs.append(o)
+        lang = ["-x", "hip"]
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_t):
+            jobs.append([hipcc] + lang + flags + ["-c", s, "-o", o])
+    _compile_all(jobs, 8)
+    target = os.path.join(PKG, "_hip" + EXT)
+    tl = _torch_lib_dir()
+    if jobs or not os.path.exists(target) or os.path.getmtime(target) < max(os.path.getmtime(o) for o in objs):
+        link = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", target] + objs
+        if tl:
+            # bind to torch's runtime first (same SONAME as /opt/rocm's)
+            link += ["-Wl,-rpath," + tl]
+        _run(link)
+    if verbose:
+        print("built", target, "(%d objects recompiled)" % len(jobs))
+    return target
+
+
+def build_all(verbose: bool = False) -> None:
+    build_core(verbose)
+    build_hip(verbose)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what == "core":
+        build_core(True)
+    elif what == "hip":
+        build_hip(True)
+    else:
+        build_all(True)

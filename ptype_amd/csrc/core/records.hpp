@@ -1,0 +1,76 @@
+// Fixed binary message records shared by the host control plane (_core) and
+// the gfx950 device runtime (_hip).
+//
+// These replace the reference's per-call gob payloads on the data plane
+// (reference: cluster/rpc.go:59-105 hands `args`/`reply` to stdlib net/rpc; the
+// calculator payload is example/calculator/calculator.go:3-5 `Args{A, B int}` and
+// the optimus payload example/optimus/prime.go:7-11 `Args{Min, Max, Target int}`).
+// A request is 32 bytes: an 8-byte header plus three machine ints, which covers
+// every payload the reference sends.  Replies are 16 bytes.  Both are sized so a
+// wave moves them with 16-byte (dwordx4) accesses.
+#pragma once
+#include <stdint.h>
+
+namespace ptype {
+
+// Well-known method ids of the compiled-in device handlers (switch in dispatch).
+enum MethodId : uint16_t {
+  kMethodNone = 0,
+  kCalculatorMultiply = 1,  // reply = a0 * a1                      (calculator.go:9-12)
+  kPrimeCheck = 2,          // reply = first divisor in [a0,min(a1,a2)) or a2 (prime.go:15-25)
+  kEcho = 3,                // reply = a0
+  kRetryTest = 4,           // stateful: fails until per-actor count >= a0 (rpc_test.go:55-77)
+  kCounterAdd = 5,          // stateful: state += a0; reply = new state
+  kMethodCount = 6,
+};
+
+enum RecordFlags : uint16_t {
+  kFlagValid = 1,
+  kFlagRouted = 2,  // `actor` holds the destination's local mailbox index
+};
+
+enum ReplyStatus : int32_t {
+  kStatusOk = 0,
+  kStatusNoMethod = 1,      // rpc: can't find method
+  kStatusFailed = 2,        // handler returned an error ("failed", rpc_test.go:76)
+  kStatusNoActor = 3,       // registry lookup miss
+  kStatusOverflow = 4,      // epoch bucket full; message deferred to the next epoch
+  kStatusNotDelivered = 5,  // reply slot never written
+};
+
+struct alignas(16) MsgRecord {
+  uint32_t actor;   // global actor key before routing, local mailbox index after
+  uint16_t method;  // MethodId
+  uint16_t flags;   // RecordFlags
+  int64_t a0, a1, a2;
+};
+static_assert(sizeof(MsgRecord) == 32, "MsgRecord must be 32 bytes");
+
+struct alignas(16) ReplyRecord {
+  int64_t value;
+  int32_t status;
+  uint32_t actor;  // echoes the serving mailbox (debug / audit)
+};
+static_assert(sizeof(ReplyRecord) == 16, "ReplyRecord must be 16 bytes");
+
+// Host<->device latency-path ring slot (fine-grained host memory).  The tag is
+// written last with release semantics; the consumer polls the tag only.
+struct alignas(64) RingSlot {
+  MsgRecord msg;
+  uint64_t tag;   // sequence number + 1 of the request published in this slot
+  uint64_t pad[3];
+};
+static_assert(sizeof(RingSlot) == 64, "RingSlot must be 64 bytes");
+
+struct alignas(32) ReplySlot {
+  ReplyRecord rep;
+  uint64_t tag;
+  uint64_t pad;
+};
+static_assert(sizeof(ReplySlot) == 32, "ReplySlot must be 32 bytes");
+
+// Device-side backend entry point that the host net/rpc server uses to execute a
+// call on a GPU actor (exported by _hip as a C function pointer).
+typedef int (*DeviceSubmitFn)(void* ctx, const MsgRecord* req, ReplyRecord* rep, int n);
+
+}  // namespace ptype

@@ -1,0 +1,127 @@
+// pybind11 bindings for the gfx950 device runtime (_hip).
+//
+// Every launcher takes raw device addresses (torch tensors' data_ptr()) and a
+// raw hipStream_t (torch.cuda.current_stream().cuda_stream), so the module does
+// not link libtorch: it shares torch's HIP runtime, allocator-owned buffers and
+// streams, and keeps compile times at seconds.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "common.hpp"
+#include "server.hpp"
+
+namespace py = pybind11;
+
+namespace ptype {
+void launch_table_upsert(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int64_t,
+                         uintptr_t, uintptr_t);
+void launch_table_delete(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t);
+void launch_table_lookup(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t);
+void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uintptr_t);
+void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void launch_gen_requests(uintptr_t, int64_t, uint32_t, int, uint64_t, uintptr_t);
+void launch_route_bucket(uintptr_t, int64_t, uintptr_t, uint64_t, int, int64_t, uintptr_t, uintptr_t, uintptr_t,
+                         uintptr_t, uintptr_t, int, uintptr_t);
+void launch_dispatch(uintptr_t, int, int64_t, uintptr_t, uintptr_t, uint32_t, uint64_t, uintptr_t, int64_t,
+                     uintptr_t);
+void launch_complete(uintptr_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void launch_snapshot_copy(uintptr_t, uintptr_t, int64_t, uintptr_t);
+}  // namespace ptype
+
+using namespace ptype;
+
+static int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+static uintptr_t pinned_alloc(size_t bytes) {
+  void* p = nullptr;
+  PT_HIP_CHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+  return (uintptr_t)p;
+}
+static void pinned_free(uintptr_t p) { PT_HIP_CHECK(hipHostFree((void*)p)); }
+
+static void memcpy_d2h_async(uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream) {
+  PT_HIP_CHECK(hipMemcpyAsync((void*)dst, (const void*)src, bytes, hipMemcpyDeviceToHost, as_stream(stream)));
+}
+static void memcpy_h2d_async(uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream) {
+  PT_HIP_CHECK(hipMemcpyAsync((void*)dst, (const void*)src, bytes, hipMemcpyHostToDevice, as_stream(stream)));
+}
+static void stream_sync(uintptr_t stream) { PT_HIP_CHECK(hipStreamSynchronize(as_stream(stream))); }
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "ptype_amd gfx950 device runtime: mailboxes, GPU registry, route/dispatch kernels";
+  m.attr("ARCH") = "gfx950";
+  m.attr("MSG_RECORD_BYTES") = (int)sizeof(MsgRecord);
+  m.attr("REPLY_RECORD_BYTES") = (int)sizeof(ReplyRecord);
+  m.attr("TABLE_ENTRY_BYTES") = (int)sizeof(TableEntry);
+  m.attr("MAX_RANKS") = 64;
+  m.def("device_count", &device_count);
+
+  m.def("table_upsert", &launch_table_upsert, py::arg("table"), py::arg("cap"), py::arg("keys"),
+        py::arg("ranks"), py::arg("mboxes"), py::arg("exp_in"), py::arg("exp_tbl"), py::arg("n"),
+        py::arg("stats"), py::arg("stream"));
+  m.def("table_delete", &launch_table_delete, py::arg("table"), py::arg("cap"), py::arg("keys"), py::arg("n"),
+        py::arg("stats"), py::arg("found"), py::arg("stream"));
+  m.def("table_lookup", &launch_table_lookup, py::arg("table"), py::arg("cap"), py::arg("keys"), py::arg("n"),
+        py::arg("out_rank"), py::arg("out_mbox"), py::arg("stream"));
+  m.def("table_sweep", &launch_table_sweep, py::arg("table"), py::arg("cap"), py::arg("exp_tbl"),
+        py::arg("now"), py::arg("stats"), py::arg("stream"));
+  m.def("table_pack", &launch_table_pack, py::arg("table"), py::arg("cap"), py::arg("exp_tbl"), py::arg("out"),
+        py::arg("out_exp"), py::arg("out_count"), py::arg("stream"));
+
+  m.def("gen_requests", &launch_gen_requests, py::arg("out"), py::arg("M"), py::arg("n_actors"),
+        py::arg("method"), py::arg("seed"), py::arg("stream"));
+  m.def("route_bucket", &launch_route_bucket, py::arg("inp"), py::arg("M"), py::arg("table"), py::arg("cap"),
+        py::arg("R"), py::arg("C"), py::arg("sendbuf"), py::arg("perm"), py::arg("counts"), py::arg("ticket"),
+        py::arg("stats"), py::arg("rank_self"), py::arg("stream"));
+  m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("reply"),
+        py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),
+        py::arg("expected_per_rank"), py::arg("stream"));
+  m.def("complete", &launch_complete, py::arg("rep"), py::arg("perm"), py::arg("M"), py::arg("out_val"),
+        py::arg("out_status"), py::arg("checksum"), py::arg("stream"));
+  m.def("snapshot_copy", &launch_snapshot_copy, py::arg("dst"), py::arg("src"), py::arg("n16"),
+        py::arg("stream"));
+
+  m.def("pinned_alloc", &pinned_alloc);
+  m.def("pinned_free", &pinned_free);
+  m.def("memcpy_d2h_async", &memcpy_d2h_async);
+  m.def("memcpy_h2d_async", &memcpy_h2d_async);
+  m.def("stream_sync", &stream_sync, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<DeviceServer>(m, "DeviceServer")
+      .def(py::init<int, uint32_t, uintptr_t, uint32_t, uint64_t, double, double>(), py::arg("device"),
+           py::arg("ring") = 4096, py::arg("state") = 0, py::arg("n_state") = 0, py::arg("delay_us") = 0,
+           py::arg("idle_ms") = 200.0, py::arg("max_s") = 60.0)
+      .def(
+          "call",
+          [](DeviceServer& s, int method, uint32_t actor, int64_t a0, int64_t a1, int64_t a2, double timeout) {
+            MsgRecord m{actor, (uint16_t)method, (uint16_t)kFlagValid, a0, a1, a2};
+            ReplyRecord r;
+            {
+              py::gil_scoped_release nogil;
+              s.call(&m, &r, 1, timeout);
+            }
+            return py::make_tuple(r.value, r.status, r.actor);
+          },
+          py::arg("method"), py::arg("actor"), py::arg("a0") = 0, py::arg("a1") = 0, py::arg("a2") = 0,
+          py::arg("timeout") = 30.0)
+      .def(
+          "call_many",
+          [](DeviceServer& s, uintptr_t req, uintptr_t rep, int n, double timeout) {
+            py::gil_scoped_release nogil;
+            s.call((const MsgRecord*)req, (ReplyRecord*)rep, n, timeout);
+          },
+          py::arg("req"), py::arg("rep"), py::arg("n"), py::arg("timeout") = 30.0)
+      .def("close", &DeviceServer::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("processed", &DeviceServer::processed)
+      .def_property_readonly("launches", &DeviceServer::launches)
+      .def_property_readonly("exits_idle", &DeviceServer::exits_idle)
+      .def_property_readonly("exits_lifetime", &DeviceServer::exits_lifetime)
+      .def_property_readonly("running", &DeviceServer::running)
+      .def("submit_handle", [](DeviceServer& s) {
+        return py::make_tuple((uintptr_t)&DeviceServer::submit_c, (uintptr_t)&s);
+      });
+}

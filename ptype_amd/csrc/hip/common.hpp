@@ -1,0 +1,67 @@
+// Common gfx950 helpers for the ptype device runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+#include "records.hpp"
+
+#define PT_HIP_CHECK(expr)                                                                 \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + " at " \
+                               + __FILE__ + ":" + std::to_string(__LINE__) + " (" #expr ")"); \
+  } while (0)
+
+namespace ptype {
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+// GPU registry table entry: 16 bytes so a lane probes with one dwordx4 load.
+struct alignas(16) TableEntry {
+  uint64_t key;   // 0 = empty, ~0 = tombstone
+  uint32_t rank;  // owning GPU rank (one process per GPU)
+  uint32_t mbox;  // local mailbox / actor-state index on that rank
+};
+static_assert(sizeof(TableEntry) == 16, "TableEntry must be 16 bytes");
+
+constexpr uint64_t kKeyEmpty = 0ull;
+constexpr uint64_t kKeyTomb = ~0ull;
+
+// table stats words (uint64): live entries, tombstones, generation, max probe seen
+enum TableStat { kStatLive = 0, kStatTomb = 1, kStatGen = 2, kStatMaxProbe = 3, kStatWords = 8 };
+
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  // splitmix64 finalizer: full-avalanche, cheap on the SALU/VALU
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  x ^= x >> 31;
+  return x;
+}
+
+// Actor ids used on the batch path map to table keys as id + 1 (0 is "empty").
+__host__ __device__ __forceinline__ uint64_t actor_key(uint32_t actor) { return (uint64_t)actor + 1ull; }
+
+__device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ unsigned mbcnt64(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint64_t realtime_ticks() {  // 100 MHz constant clock
+  return __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ void spin_ticks(uint64_t ticks) {
+  if (!ticks) return;
+  const uint64_t t0 = realtime_ticks();
+  while (realtime_ticks() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+inline hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace ptype

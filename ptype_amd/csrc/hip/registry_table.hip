@@ -1,0 +1,240 @@
+// GPU-resident registry mirror (SURVEY C9 / kernels K5, K6, K7).
+//
+// The authoritative registry lives in the Raft-replicated MVCC store (host);
+// this open-addressing hash table in HBM mirrors it for device-side routing so
+// the batch path never leaves the GPU to resolve a destination.  Reference
+// behaviour it mirrors: Register/Services/nodes (cluster/registry.go:51-166) and
+// lease expiry (cluster/registry.go:59, 2 s TTL).
+//
+// Layout: 16-byte entries {u64 key, u32 rank, u32 mbox}; a side array of u64
+// expiry deadlines (host monotonic ms, 0 = never); capacity is a power of two
+// sized 2x the live count (1M actors -> 2M slots -> 32 MB + 16 MB, trivially
+// resident in 288 GB HBM and mostly in the 256 MB Infinity Cache).
+// Probing is linear; deletes leave tombstones that lookups skip and upserts do
+// not reuse, the host rebuilds (pack -> clear -> upsert) when they pile up.
+#include "common.hpp"
+
+namespace ptype {
+
+__device__ __forceinline__ uint64_t ld_key(const TableEntry* e) {
+  return __hip_atomic_load(&e->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void table_upsert_kernel(TableEntry* __restrict__ t, uint64_t mask,
+                                                           const uint64_t* __restrict__ keys,
+                                                           const uint32_t* __restrict__ ranks,
+                                                           const uint32_t* __restrict__ mboxes,
+                                                           const uint64_t* __restrict__ exp_in,
+                                                           uint64_t* __restrict__ exp_tbl, int64_t n,
+                                                           unsigned long long* __restrict__ stats) {
+  unsigned long long added = 0, maxp = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    if (key == kKeyEmpty || key == kKeyTomb) continue;
+    uint64_t h = mix64(key) & mask;
+    uint64_t probe = 0;
+    bool ok = false;
+    for (; probe <= mask; ++probe, h = (h + 1) & mask) {
+      uint64_t cur = ld_key(&t[h]);
+      if (cur == key) { ok = true; break; }
+      if (cur == kKeyEmpty) {
+        uint64_t expected = kKeyEmpty;
+        if (__hip_atomic_compare_exchange_strong(&t[h].key, &expected, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          ++added;
+          ok = true;
+          break;
+        }
+        if (expected == key) { ok = true; break; }
+      }
+    }
+    if (!ok) continue;  // table full: host sizes capacity >= 2x live, never hit in practice
+    uint64_t v = ((uint64_t)mboxes[i] << 32) | ranks[i];
+    *reinterpret_cast<uint64_t*>(&t[h].rank) = v;
+    if (exp_tbl) exp_tbl[h] = exp_in ? exp_in[i] : 0ull;
+    if (probe > maxp) maxp = probe;
+  }
+  // one atomic per wave for the counters (wave reduce through shuffles)
+  for (int off = 32; off > 0; off >>= 1) {
+    added += __shfl_xor(added, off);
+    unsigned long long o = __shfl_xor(maxp, off);
+    maxp = o > maxp ? o : maxp;
+  }
+  if (lane_id() == 0) {
+    if (added) atomicAdd(&stats[kStatLive], added);
+    atomicMax(&stats[kStatMaxProbe], maxp);
+    atomicAdd(&stats[kStatGen], 1ull);
+  }
+}
+
+__global__ __launch_bounds__(256) void table_delete_kernel(TableEntry* __restrict__ t, uint64_t mask,
+                                                           const uint64_t* __restrict__ keys, int64_t n,
+                                                           unsigned long long* __restrict__ stats,
+                                                           uint8_t* __restrict__ found_out) {
+  unsigned long long removed = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    bool hit = false;
+    if (key != kKeyEmpty && key != kKeyTomb) {
+      uint64_t h = mix64(key) & mask;
+      for (uint64_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+        uint64_t cur = ld_key(&t[h]);
+        if (cur == kKeyEmpty) break;
+        if (cur == key) {
+          uint64_t expected = key;
+          if (__hip_atomic_compare_exchange_strong(&t[h].key, &expected, kKeyTomb, __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            ++removed;
+            hit = true;
+          }
+          break;
+        }
+      }
+    }
+    if (found_out) found_out[i] = hit ? 1 : 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);
+  if (lane_id() == 0 && removed) {
+    atomicAdd(&stats[kStatLive], (unsigned long long)(-(long long)removed));
+    atomicAdd(&stats[kStatTomb], removed);
+    atomicAdd(&stats[kStatGen], 1ull);
+  }
+}
+
+__global__ __launch_bounds__(256) void table_lookup_kernel(const TableEntry* __restrict__ t, uint64_t mask,
+                                                           const uint64_t* __restrict__ keys, int64_t n,
+                                                           int32_t* __restrict__ out_rank,
+                                                           int32_t* __restrict__ out_mbox) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    int32_t rank = -1, mbox = -1;
+    if (key != kKeyEmpty && key != kKeyTomb) {
+      uint64_t h = mix64(key) & mask;
+      for (uint64_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
+        const uint4 e = *reinterpret_cast<const uint4*>(&t[h]);  // one dwordx4
+        const uint64_t k = ((uint64_t)e.y << 32) | e.x;
+        if (k == key) { rank = (int32_t)e.z; mbox = (int32_t)e.w; break; }
+        if (k == kKeyEmpty) break;
+      }
+    }
+    out_rank[i] = rank;
+    if (out_mbox) out_mbox[i] = mbox;
+  }
+}
+
+// K6: lease sweep -- tombstone every entry whose deadline passed.
+__global__ __launch_bounds__(256) void table_sweep_kernel(TableEntry* __restrict__ t, uint64_t cap,
+                                                          const uint64_t* __restrict__ exp_tbl, uint64_t now,
+                                                          unsigned long long* __restrict__ stats) {
+  unsigned long long removed = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = exp_tbl[i];
+    if (e == 0 || e >= now) continue;
+    uint64_t k = ld_key(&t[i]);
+    if (k == kKeyEmpty || k == kKeyTomb) continue;
+    if (__hip_atomic_compare_exchange_strong(&t[i].key, &k, kKeyTomb, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      ++removed;
+  }
+  for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);
+  if (lane_id() == 0 && removed) {
+    atomicAdd(&stats[kStatLive], (unsigned long long)(-(long long)removed));
+    atomicAdd(&stats[kStatTomb], removed);
+    atomicAdd(&stats[kStatGen], 1ull);
+  }
+}
+
+// K7: snapshot pack -- compact live entries (+ deadlines) into a dense buffer
+// that the host copies to pinned DRAM with hipMemcpyAsync.  One wave ballot +
+// one LDS scan per block + one global atomic per block for the output base.
+__global__ __launch_bounds__(256) void table_pack_kernel(const TableEntry* __restrict__ t, uint64_t cap,
+                                                         const uint64_t* __restrict__ exp_tbl,
+                                                         TableEntry* __restrict__ out,
+                                                         uint64_t* __restrict__ out_exp,
+                                                         unsigned long long* __restrict__ out_count) {
+  __shared__ unsigned wave_cnt[4];
+  __shared__ unsigned long long block_base;
+  const unsigned w = threadIdx.x / kWave;
+  for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < cap; base += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = base + threadIdx.x;
+    TableEntry e{};
+    bool live = false;
+    if (i < cap) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&t[i]);
+      e.key = ((uint64_t)v.y << 32) | v.x;
+      e.rank = v.z;
+      e.mbox = v.w;
+      live = e.key != kKeyEmpty && e.key != kKeyTomb;
+    }
+    const uint64_t m = __ballot(live);
+    const unsigned pos = mbcnt64(m);
+    if (lane_id() == 0) wave_cnt[w] = __popcll(m);
+    __syncthreads();
+    unsigned off = 0, tot = 0;
+    for (unsigned k = 0; k < blockDim.x / kWave; ++k) {
+      if (k < w) off += wave_cnt[k];
+      tot += wave_cnt[k];
+    }
+    if (threadIdx.x == 0) block_base = tot ? atomicAdd(out_count, (unsigned long long)tot) : 0ull;
+    __syncthreads();
+    if (live) {
+      const unsigned long long o = block_base + off + pos;
+      out[o] = e;
+      if (out_exp) out_exp[o] = exp_tbl ? exp_tbl[i] : 0ull;
+    }
+    __syncthreads();
+  }
+}
+
+static inline unsigned grid_for(int64_t n, int per_block = 256, unsigned cap = 4096) {
+  int64_t g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// ---- host launchers (pointers are raw device addresses from torch tensors) ----
+void launch_table_upsert(uintptr_t table, uint64_t cap, uintptr_t keys, uintptr_t ranks, uintptr_t mboxes,
+                         uintptr_t exp_in, uintptr_t exp_tbl, int64_t n, uintptr_t stats, uintptr_t stream) {
+  if (n <= 0) return;
+  if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
+  hipLaunchKernelGGL(table_upsert_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream),
+                     (TableEntry*)table, cap - 1, (const uint64_t*)keys, (const uint32_t*)ranks,
+                     (const uint32_t*)mboxes, (const uint64_t*)exp_in, (uint64_t*)exp_tbl, n,
+                     (unsigned long long*)stats);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_table_delete(uintptr_t table, uint64_t cap, uintptr_t keys, int64_t n, uintptr_t stats,
+                         uintptr_t found, uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(table_delete_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), (TableEntry*)table,
+                     cap - 1, (const uint64_t*)keys, n, (unsigned long long*)stats, (uint8_t*)found);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_table_lookup(uintptr_t table, uint64_t cap, uintptr_t keys, int64_t n, uintptr_t out_rank,
+                         uintptr_t out_mbox, uintptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(table_lookup_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream),
+                     (const TableEntry*)table, cap - 1, (const uint64_t*)keys, n, (int32_t*)out_rank,
+                     (int32_t*)out_mbox);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_table_sweep(uintptr_t table, uint64_t cap, uintptr_t exp_tbl, uint64_t now, uintptr_t stats,
+                        uintptr_t stream) {
+  hipLaunchKernelGGL(table_sweep_kernel, dim3(grid_for((int64_t)cap)), dim3(256), 0, as_stream(stream),
+                     (TableEntry*)table, cap, (const uint64_t*)exp_tbl, now, (unsigned long long*)stats);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_table_pack(uintptr_t table, uint64_t cap, uintptr_t exp_tbl, uintptr_t out, uintptr_t out_exp,
+                       uintptr_t out_count, uintptr_t stream) {
+  hipLaunchKernelGGL(table_pack_kernel, dim3(grid_for((int64_t)cap)), dim3(256), 0, as_stream(stream),
+                     (const TableEntry*)table, cap, (const uint64_t*)exp_tbl, (TableEntry*)out, (uint64_t*)out_exp,
+                     (unsigned long long*)out_count);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace ptype

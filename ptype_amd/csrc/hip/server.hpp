@@ -1,0 +1,280 @@
+// Persistent device dispatcher: the latency path of `Client.Call` on a GPU actor
+// (SURVEY C10 / K3 persistent form, K8 fused).
+//
+// Reference: each net/rpc call is one TCP round trip into a goroutine that runs
+// the handler (cluster/rpc.go:59-67 -> stdlib net/rpc server, registered at
+// example/calculator/server/server.go:16-20).  Here the host publishes a 64-B
+// request slot into a ring in fine-grained (coherent) host memory; ONE resident
+// wave polls the ring with relaxed system-scope loads + s_sleep, runs up to 64
+// consecutive requests per poll (one per lane) through the same compiled-in
+// handler table as the batch path, and writes 32-B reply slots back with
+// system-scope stores + a release before each tag.  No kernel launch per call.
+//
+// Liveness: the kernel exits when the host sets `stop`, when it has been idle
+// for `idle_ticks`, or after `max_ticks` (a hard bound so nothing can hang the
+// GPU).  Exit uses a Dekker-style hand-off on `state` so a request published
+// while the kernel retires is never stranded: the kernel stores STOPPED,
+// re-checks the ring, and resumes only by CAS(STOPPED->RUNNING); the host, after
+// publishing, relaunches only by CAS(STOPPED->LAUNCHING).
+#pragma once
+#include <atomic>
+#include <chrono>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "common.hpp"
+#include "handlers.hpp"
+
+namespace ptype {
+
+enum ServerState : uint64_t { kStopped = 0, kRunning = 1, kLaunching = 2 };
+
+struct alignas(64) ServerCtrl {
+  uint64_t stop;
+  uint64_t state;
+  uint64_t resume_head;
+  uint64_t processed;
+  uint64_t exits_idle;
+  uint64_t exits_lifetime;
+  uint64_t pad[2];
+};
+
+__device__ __forceinline__ uint64_t sys_ld(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_st(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __restrict__ req,
+                                                                 ReplySlot* __restrict__ rep, uint64_t ring_mask,
+                                                                 ServerCtrl* __restrict__ ctrl, uint64_t head,
+                                                                 int64_t* __restrict__ state, uint32_t n_state,
+                                                                 uint64_t delay_ticks, uint64_t idle_ticks,
+                                                                 uint64_t max_ticks) {
+  const unsigned lane = lane_id();
+  const uint64_t t_start = realtime_ticks();
+  uint64_t last_work = t_start;
+  uint64_t processed = 0;
+  bool lifetime_exit = false;
+  for (;;) {
+    if (sys_ld(&ctrl->stop)) break;
+    const uint64_t seq = head + lane;
+    RingSlot* s = &req[seq & ring_mask];
+    const bool ready = sys_ld(&s->tag) == seq + 1;
+    const uint64_t m = __ballot(ready);
+    const unsigned n = (m == ~0ull) ? 64u : (unsigned)__builtin_ctzll(~m);
+    if (n == 0) {
+      const uint64_t now = realtime_ticks();
+      const bool idle = idle_ticks && now - last_work > idle_ticks;
+      lifetime_exit = now - t_start > max_ticks;
+      if (idle || lifetime_exit) {
+        int resume = 0;
+        if (lane == 0) {
+          sys_st(&ctrl->resume_head, head);
+          __threadfence_system();
+          sys_st(&ctrl->state, kStopped);
+          __threadfence_system();
+          if (!lifetime_exit && sys_ld(&req[head & ring_mask].tag) == head + 1) {
+            uint64_t expected = kStopped;
+            resume = __hip_atomic_compare_exchange_strong(&ctrl->state, &expected, (uint64_t)kRunning,
+                                                          __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_SYSTEM)
+                         ? 1
+                         : 0;
+          }
+        }
+        resume = __shfl(resume, 0);
+        if (resume) {
+          last_work = realtime_ticks();
+          continue;
+        }
+        if (lane == 0) {
+          __hip_atomic_fetch_add(lifetime_exit ? &ctrl->exits_lifetime : &ctrl->exits_idle, 1ull,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_fetch_add(&ctrl->processed, processed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    if (lane < n) {
+      const uint64_t* w = reinterpret_cast<const uint64_t*>(&s->msg);
+      const uint64_t w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3);
+      MsgRecord msg;
+      msg.actor = (uint32_t)w0;
+      msg.method = (uint16_t)(w0 >> 32);
+      msg.flags = (uint16_t)(w0 >> 48);
+      msg.a0 = (int64_t)w1;
+      msg.a1 = (int64_t)w2;
+      msg.a2 = (int64_t)w3;
+      const ReplyRecord r = run_handler(msg, state, n_state, delay_ticks);
+      ReplySlot* o = &rep[seq & ring_mask];
+      uint64_t* ow = reinterpret_cast<uint64_t*>(&o->rep);
+      sys_st(ow, (uint64_t)r.value);
+      sys_st(ow + 1, (uint64_t)(uint32_t)r.status | ((uint64_t)r.actor << 32));
+      __threadfence_system();
+      sys_st(&o->tag, seq + 1);
+    }
+    head += n;
+    processed += n;
+    last_work = realtime_ticks();
+  }
+  if (lane == 0) {
+    sys_st(&ctrl->resume_head, head);
+    __threadfence_system();
+    sys_st(&ctrl->state, kStopped);
+    __hip_atomic_fetch_add(&ctrl->processed, processed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+class DeviceServer {
+ public:
+  DeviceServer(int device, uint32_t ring, uintptr_t state, uint32_t n_state, uint64_t delay_us, double idle_ms,
+               double max_s)
+      : device_(device), ring_(ring), state_((int64_t*)state), n_state_(n_state) {
+    if (ring == 0 || (ring & (ring - 1))) throw std::invalid_argument("ring size must be a power of two");
+    delay_ticks_ = delay_us * 100;  // s_memrealtime runs at 100 MHz
+    idle_ticks_ = (uint64_t)(idle_ms * 1e5);
+    max_ticks_ = (uint64_t)(max_s * 1e8);
+    PT_HIP_CHECK(hipSetDevice(device_));
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+    PT_HIP_CHECK(hipHostMalloc((void**)&req_, sizeof(RingSlot) * ring_, fl));
+    PT_HIP_CHECK(hipHostMalloc((void**)&rep_, sizeof(ReplySlot) * ring_, fl));
+    PT_HIP_CHECK(hipHostMalloc((void**)&ctrl_, sizeof(ServerCtrl), fl));
+    memset((void*)req_, 0, sizeof(RingSlot) * ring_);
+    memset((void*)rep_, 0, sizeof(ReplySlot) * ring_);
+    memset((void*)ctrl_, 0, sizeof(ServerCtrl));
+    PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dreq_, req_, 0));
+    PT_HIP_CHECK(hipHostGetDevicePointer((void**)&drep_, rep_, 0));
+    PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dctrl_, ctrl_, 0));
+    PT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    owner_.reset(new std::atomic<uint64_t>[ring_]);
+    for (uint32_t i = 0; i < ring_; ++i) owner_[i].store(i, std::memory_order_relaxed);
+  }
+
+  ~DeviceServer() {
+    try {
+      close();
+    } catch (...) {
+    }
+  }
+
+  void close() {
+    if (closed_) return;
+    closed_ = true;
+    __atomic_store_n(&ctrl_->stop, 1ull, __ATOMIC_SEQ_CST);
+    hipSetDevice(device_);
+    hipStreamSynchronize(stream_);
+    hipStreamDestroy(stream_);
+    hipHostFree(req_);
+    hipHostFree(rep_);
+    hipHostFree(ctrl_);
+  }
+
+  // Publish n requests and wait for all replies (any thread).
+  void call(const MsgRecord* in, ReplyRecord* out, int n, double timeout_s) {
+    if (closed_) throw std::runtime_error("device server closed");
+    std::unique_ptr<uint64_t[]> seqs(new uint64_t[n]);
+    int done = 0;
+    while (done < n) {
+      const int batch = std::min<int>(n - done, (int)(ring_ / 2));
+      for (int i = 0; i < batch; ++i) seqs[done + i] = publish(in[done + i]);
+      ensure_running();
+      for (int i = 0; i < batch; ++i) out[done + i] = wait(seqs[done + i], timeout_s);
+      done += batch;
+    }
+  }
+
+  uint64_t processed() const { return __atomic_load_n(&ctrl_->processed, __ATOMIC_ACQUIRE); }
+  uint64_t launches() const { return launches_.load(); }
+  uint64_t exits_idle() const { return __atomic_load_n(&ctrl_->exits_idle, __ATOMIC_ACQUIRE); }
+  uint64_t exits_lifetime() const { return __atomic_load_n(&ctrl_->exits_lifetime, __ATOMIC_ACQUIRE); }
+  bool running() const { return __atomic_load_n(&ctrl_->state, __ATOMIC_ACQUIRE) == kRunning; }
+
+  static int submit_c(void* ctx, const MsgRecord* req, ReplyRecord* rep, int n) {
+    try {
+      static_cast<DeviceServer*>(ctx)->call(req, rep, n, 30.0);
+      return 0;
+    } catch (...) {
+      return -1;
+    }
+  }
+
+ private:
+  uint64_t publish(const MsgRecord& m) {
+    const uint64_t seq = next_seq_.fetch_add(1);
+    const uint32_t idx = (uint32_t)(seq & (ring_ - 1));
+    // wait until the slot's previous occupant (seq - ring) has been consumed
+    for (unsigned spins = 0; owner_[idx].load(std::memory_order_acquire) != seq; ++spins)
+      if (spins > 64) std::this_thread::yield();
+    RingSlot* s = &req_[idx];
+    s->msg = m;
+    __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
+    return seq;
+  }
+
+  ReplyRecord wait(uint64_t seq, double timeout_s) {
+    const uint32_t idx = (uint32_t)(seq & (ring_ - 1));
+    ReplySlot* o = &rep_[idx];
+    auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 0; __atomic_load_n(&o->tag, __ATOMIC_ACQUIRE) != seq + 1; ++spins) {
+      if ((spins & 1023) == 1023) {
+        ensure_running();  // the kernel may have retired on idle/lifetime
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+          throw std::runtime_error("device server: reply timeout");
+        std::this_thread::yield();
+      }
+    }
+    ReplyRecord r = o->rep;
+    owner_[idx].store(seq + ring_, std::memory_order_release);
+    return r;
+  }
+
+  void ensure_running() {
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    for (;;) {
+      uint64_t s = __atomic_load_n(&ctrl_->state, __ATOMIC_SEQ_CST);
+      if (s == kRunning) return;
+      if (s == kStopped) {
+        uint64_t exp = kStopped;
+        if (__atomic_compare_exchange_n(&ctrl_->state, &exp, (uint64_t)kLaunching, false, __ATOMIC_SEQ_CST,
+                                        __ATOMIC_SEQ_CST)) {
+          std::lock_guard<std::mutex> g(launch_mu_);
+          const uint64_t head = __atomic_load_n(&ctrl_->resume_head, __ATOMIC_ACQUIRE);
+          __atomic_store_n(&ctrl_->state, (uint64_t)kRunning, __ATOMIC_SEQ_CST);
+          hipSetDevice(device_);
+          hipLaunchKernelGGL(persistent_dispatch_kernel, dim3(1), dim3(64), 0, stream_, dreq_, drep_,
+                             (uint64_t)(ring_ - 1), dctrl_, head, state_, n_state_, delay_ticks_, idle_ticks_,
+                             max_ticks_);
+          PT_HIP_CHECK(hipGetLastError());
+          launches_.fetch_add(1);
+          return;
+        }
+      }
+      std::this_thread::yield();
+    }
+  }
+
+  int device_;
+  uint32_t ring_;
+  int64_t* state_;
+  uint32_t n_state_;
+  uint64_t delay_ticks_ = 0, idle_ticks_ = 0, max_ticks_ = 0;
+  RingSlot* req_ = nullptr;
+  ReplySlot* rep_ = nullptr;
+  ServerCtrl* ctrl_ = nullptr;
+  RingSlot* dreq_ = nullptr;
+  ReplySlot* drep_ = nullptr;
+  ServerCtrl* dctrl_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  std::atomic<uint64_t> next_seq_{0};
+  std::unique_ptr<std::atomic<uint64_t>[]> owner_;
+  std::atomic<uint64_t> launches_{0};
+  std::mutex launch_mu_;
+  bool closed_ = false;
+};
+
+}  // namespace ptype

@@ -1,0 +1,251 @@
+"""Numerics of the hand-written gfx950 kernels vs plain PyTorch/NumPy references.
+
+GPU tests compare each kernel against the CPU reference of the same op
+(``ptype_amd/ops``); CPU tests pin the reference itself against hand-computed
+expectations (so the references are not self-validating).
+"""
+import pytest
+import torch
+
+from ptype_amd import ops
+from ptype_amd.ops import batch as B
+from ptype_amd.ops.records import (METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD, METHOD_ECHO, METHOD_PRIME_CHECK,
+                                   METHOD_RETRY_TEST, STATUS_FAILED, STATUS_NO_ACTOR, STATUS_OK, STATUS_OVERFLOW,
+                                   make_requests, split_replies)
+from ptype_amd.ops.table import RegistryTable, actor_keys
+
+
+def _populate(table: RegistryTable, n_actors: int, R: int):
+    ids = torch.arange(n_actors, dtype=torch.int64)
+    table.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
+
+
+# ----------------------------------------------------------------- CPU reference
+def test_table_reference_roundtrip():
+    t = RegistryTable(64, device="cpu")
+    _populate(t, 40, 4)
+    assert t.live == 40
+    r, m = t.lookup(actor_keys(torch.tensor([0, 5, 39, 40])))
+    assert r.tolist() == [0, 1, 3, -1]
+    assert m.tolist() == [0, 1, 9, -1]
+    found = t.delete(actor_keys(torch.tensor([5, 77])))
+    assert found.tolist() == [True, False]
+    assert t.live == 39 and t.tombstones == 1
+    r, _ = t.lookup(actor_keys(torch.tensor([5, 6])))
+    assert r.tolist() == [-1, 2]
+    ent, exp = t.pack()
+    assert ent.shape[0] == 39
+    t.rebuild()
+    assert t.live == 39 and t.tombstones == 0
+    r, _ = t.lookup(actor_keys(torch.arange(40)))
+    assert (r[torch.arange(40) != 5] >= 0).all() and r[5] == -1
+
+
+def test_table_reference_sweep():
+    t = RegistryTable(64, device="cpu")
+    ids = torch.arange(8)
+    t.upsert(actor_keys(ids), torch.zeros(8, dtype=torch.int32), ids.to(torch.int32),
+             expiry=torch.tensor([0, 100, 200, 300, 0, 50, 500, 1000]))
+    t.sweep(250)
+    r, _ = t.lookup(actor_keys(ids))
+    assert (r >= 0).tolist() == [True, False, False, True, True, False, True, True]
+
+
+def test_batch_reference_end_to_end():
+    R, C = 3, 64
+    t = RegistryTable(64, device="cpu")
+    _populate(t, 12, R)
+    req = make_requests(torch.tensor([0, 1, 2, 3, 4, 99]), METHOD_CALC_MULTIPLY, torch.tensor([7, 2, 3, 4, 5, 6]),
+                        torch.tensor([8, 3, 4, 5, 6, 7]))
+    send, perm, ws = B.route_bucket(req, t, R, C)
+    assert B.ws_counts(ws, R).tolist() == [2, 2, 1]
+    assert int(B.ws_stats(ws)[B.STAT_NOMATCH]) == 1
+    rep = B.dispatch(send, R, C)
+    val, st = B.complete(rep, perm)
+    assert val.tolist()[:5] == [56, 6, 12, 20, 30]
+    assert st.tolist() == [STATUS_OK] * 5 + [STATUS_NO_ACTOR]
+
+
+def test_batch_reference_overflow_and_handlers():
+    R, C = 1, 2
+    t = RegistryTable(16, device="cpu")
+    _populate(t, 2, 1)
+    state = torch.zeros(2, dtype=torch.int64)
+    req = make_requests(torch.tensor([0, 1, 0]), torch.tensor([METHOD_COUNTER_ADD, METHOD_PRIME_CHECK, METHOD_ECHO]),
+                        torch.tensor([5, 2, 9]), torch.tensor([0, 10, 0]), torch.tensor([0, 21, 0]))
+    send, perm, ws = B.route_bucket(req, t, R, C)
+    rep = B.dispatch(send, R, C, state=state)
+    val, st = B.complete(rep, perm)
+    assert val.tolist()[:2] == [5, 3]  # counter 0+5, 21 = 3*7 -> first divisor 3
+    assert st.tolist() == [STATUS_OK, STATUS_OK, STATUS_OVERFLOW]
+
+
+def test_retry_reference():
+    v, s = B._handler_ref(torch.tensor([METHOD_RETRY_TEST] * 3), torch.tensor([0, 0, 0]), torch.tensor([2, 2, 2]),
+                          torch.zeros(3, dtype=torch.int64), torch.zeros(3, dtype=torch.int64),
+                          torch.zeros(1, dtype=torch.int64))
+    assert s.tolist() == [STATUS_FAILED, STATUS_OK, STATUS_OK]
+    assert v.tolist()[1:] == [2, 3]
+
+
+# ----------------------------------------------------------------- GPU vs reference
+@pytest.mark.gpu
+def test_gpu_table_matches_reference():
+    torch.manual_seed(0)
+    n = 50_000
+    g = RegistryTable(2 * n, device="cuda")
+    c = RegistryTable(2 * n, device="cpu")
+    keys = torch.randperm(10 * n)[:n].to(torch.int64) + 1
+    ranks = torch.randint(0, 8, (n,), dtype=torch.int32)
+    mbox = torch.randint(0, 1 << 20, (n,), dtype=torch.int32)
+    g.upsert(keys.cuda(), ranks.cuda(), mbox.cuda())
+    c.upsert(keys, ranks, mbox)
+    torch.cuda.synchronize()
+    assert g.live == n == c.live
+    # same hash + same probing -> the slot images are identical for a single batch without duplicates
+    probe = torch.cat([keys[::3], torch.arange(10 * n + 5, 10 * n + 1000)])
+    rg, mg = g.lookup(probe.cuda())
+    rc, mc = c.lookup(probe)
+    assert torch.equal(rg.cpu(), rc) and torch.equal(mg.cpu(), mc)
+    dk = keys[::7]
+    fg = g.delete(dk.cuda())
+    fc = c.delete(dk)
+    assert torch.equal(fg.cpu(), fc)
+    assert g.live == c.live and g.tombstones == c.tombstones
+    rg, _ = g.lookup(keys.cuda())
+    rc, _ = c.lookup(keys)
+    assert torch.equal(rg.cpu(), rc)
+    ent, _ = g.pack()
+    assert ent.shape[0] == g.live
+    assert set(ent[:, 0].cpu().tolist()) == set(keys[rc >= 0].tolist())
+    g.rebuild()
+    assert g.tombstones == 0
+    rg2, _ = g.lookup(keys.cuda())
+    assert torch.equal(rg2.cpu(), rc)
+
+
+@pytest.mark.gpu
+def test_gpu_table_sweep_and_snapshot():
+    g = RegistryTable(1024, device="cuda")
+    ids = torch.arange(300)
+    exp = torch.where(ids % 3 == 0, torch.zeros_like(ids), ids * 10)
+    g.upsert(actor_keys(ids).cuda(), torch.zeros(300, dtype=torch.int32).cuda(), ids.to(torch.int32).cuda(),
+             exp.cuda())
+    g.sweep(1500)
+    r, _ = g.lookup(actor_keys(ids).cuda())
+    expect = (exp == 0) | (exp >= 1500)
+    assert torch.equal((r.cpu() >= 0), expect)
+    h_ent, h_exp = g.snapshot_to_host()
+    assert h_ent.is_pinned() and h_ent.shape[0] == int(expect.sum())
+    g2 = RegistryTable(1024, device="cuda")
+    g2.load_packed(h_ent, h_exp)
+    r2, _ = g2.lookup(actor_keys(ids).cuda())
+    assert torch.equal(r2.cpu(), r.cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 2, 8])
+def test_gpu_route_dispatch_complete(R):
+    M, n_actors = 200_003, 4096
+    C = M // R + 4096
+    g = RegistryTable(2 * n_actors, device="cuda")
+    _populate(g, n_actors, R)
+    req = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=1234, device="cuda")
+    ref_req = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=1234, device="cpu")
+    assert torch.equal(req.cpu(), ref_req), "generator kernel differs from reference"
+    send, perm, ws = B.route_bucket(req, g, R, C, rank_self=0)
+    counts = B.ws_counts(ws, R).cpu()
+    actor = ref_req[:, 0] & 0xFFFFFFFF
+    ref_counts = torch.bincount(actor % R, minlength=R)
+    assert torch.equal(counts.to(torch.int64), ref_counts)
+    assert int(B.ws_stats(ws)[B.STAT_OVERFLOW]) == 0
+    # every message lands exactly once
+    p = perm.cpu().to(torch.int64)
+    assert (p >= 0).all() and torch.unique(p).numel() == M
+    # the routed record in the slot is the original with actor -> mailbox
+    s = send.cpu()
+    assert torch.equal(s[p, 1:], ref_req[:, 1:])
+    assert torch.equal(s[p, 0] & 0xFFFFFFFF, actor // R)
+    rep = B.dispatch(send, R, C, expected_per_rank=M // R)
+    val, st = B.complete(rep, perm)
+    torch.cuda.synchronize()
+    assert (st.cpu() == STATUS_OK).all()
+    assert torch.equal(val.cpu(), ref_req[:, 1] * ref_req[:, 2])
+
+
+@pytest.mark.gpu
+def test_gpu_route_overflow_and_unknown():
+    R, C = 2, 1000
+    g = RegistryTable(256, device="cuda")
+    _populate(g, 100, R)
+    actors = torch.cat([torch.zeros(1500, dtype=torch.int64), torch.tensor([555])])  # 1500 -> rank 0 (cap 1000)
+    req = make_requests(actors, METHOD_ECHO, torch.arange(1501)).cuda()
+    send, perm, ws = B.route_bucket(req, g, R, C)
+    rep = B.dispatch(send, R, C)
+    val, st = B.complete(rep, perm)
+    st = st.cpu()
+    assert int((st == STATUS_OVERFLOW).sum()) == 500
+    assert int((st == STATUS_NO_ACTOR).sum()) == 1
+    ok = st == STATUS_OK
+    assert torch.equal(val.cpu()[ok], torch.arange(1501)[ok])
+
+
+@pytest.mark.gpu
+def test_gpu_stateful_handlers_match_reference():
+    R, C = 1, 4096
+    g = RegistryTable(64, device="cuda")
+    _populate(g, 4, 1)
+    n = 1000
+    actors = torch.arange(n) % 4
+    req = make_requests(actors, METHOD_COUNTER_ADD, torch.ones(n, dtype=torch.int64)).cuda()
+    state = torch.zeros(4, dtype=torch.int64, device="cuda")
+    send, perm, _ = B.route_bucket(req, g, R, C)
+    rep = B.dispatch(send, R, C, state=state)
+    val, st = B.complete(rep, perm)
+    assert state.cpu().tolist() == [250] * 4
+    # per-actor values are a permutation of 1..250 (arrival order is the device's)
+    v = val.cpu()
+    for a in range(4):
+        assert sorted(v[actors == a].tolist()) == list(range(1, 251))
+    # prime check vs reference
+    tgt = torch.tensor([97, 91, 221, 1000003, 49])
+    req = make_requests(torch.zeros(5, dtype=torch.int64), METHOD_PRIME_CHECK, torch.full((5,), 2), torch.full((5,), 1 << 40),
+                        tgt).cuda()
+    send, perm, _ = B.route_bucket(req, g, R, C)
+    val, st = B.complete(B.dispatch(send, R, C), perm)
+    assert val.cpu().tolist() == [97, 7, 13, 1000003, 7]
+
+
+@pytest.mark.gpu
+def test_gpu_device_server_latency_path():
+    import time
+
+    state = torch.zeros(8, dtype=torch.int64, device="cuda")
+    srv = ops.hip().DeviceServer(0, 1024, state.data_ptr(), 8, 0, 50.0, 20.0)
+    try:
+        v, s, a = srv.call(METHOD_CALC_MULTIPLY, 0, 7, 8)
+        assert (v, s) == (56, STATUS_OK)
+        # stateful retry actor: fails until count >= 3
+        outs = [srv.call(METHOD_RETRY_TEST, 2, 3)[1] for _ in range(4)]
+        assert outs == [STATUS_FAILED, STATUS_FAILED, STATUS_OK, STATUS_OK]
+        # batched submit through pinned records
+        n = 5000
+        req = make_requests(torch.arange(n) % 8, METHOD_CALC_MULTIPLY, torch.arange(n), torch.full((n,), 3)).pin_memory()
+        rep = torch.zeros(n, 2, dtype=torch.int64).pin_memory()
+        srv.call_many(req.data_ptr(), rep.data_ptr(), n)
+        val, st, _ = split_replies(rep)
+        assert torch.equal(val, torch.arange(n) * 3) and (st == 0).all()
+        # idle exit + transparent relaunch
+        time.sleep(0.3)
+        assert not srv.running
+        assert srv.call(METHOD_ECHO, 1, 42)[0] == 42
+        assert srv.launches >= 2
+        lat = []
+        for i in range(2000):
+            t0 = time.perf_counter()
+            srv.call(METHOD_CALC_MULTIPLY, i % 8, i, 2)
+            lat.append(time.perf_counter() - t0)
+        lat.sort()
+        print("device-server p50 RTT us", lat[len(lat) // 2] * 1e6, "p99", lat[int(len(lat) * 0.99)] * 1e6)
+    finally:
+        srv.close()
