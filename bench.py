@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Headline benchmark: messages/sec (whole node) + p50 RPC RTT, calculator actor.
+
+BASELINE.json metric: "messages/sec (whole node) + p50 RPC RTT, calculator actor
+at 1/2/4/8 MI355X".  One process per GPU (torchrun); every rank hosts a shard of
+the calculator actors and is also a client that sends a batch of synthetic
+``Calculator.Multiply(Args{A, B})`` calls (example/calculator/calculator.go:3-12)
+to uniformly random actors across the whole node each step.
+
+A timed step is the full `Send` path for the batch: generate the requests
+(client), K1 GPU-registry lookup + bucket, RCCL all-to-all over xGMI, K3
+dispatch through the handler table, RCCL all-to-all of replies, K8 completion
+into message order.  Nothing is cached across steps (new args every step) and
+the results of a step are verified against ``A * B``.
+
+p50 RTT: single synchronous ``Call``s to a GPU actor through the persistent
+dispatcher (host-visible ring, no launch per call), measured after the timed
+loop on every rank's own GPU.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]   (N>1 under torchrun)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def _parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--msgs-per-gpu", type=int, default=8 * 1024 * 1024, help="messages each rank sends per step")
+    p.add_argument("--actors-per-gpu", type=int, default=131072)
+    p.add_argument("--chunks", type=int, default=0, help="pipeline chunks per step (0 = auto)")
+    p.add_argument("--rtt-calls", type=int, default=2000)
+    p.add_argument("--cpu", action="store_true", help="gloo/CPU dry run of the same pipeline (tests)")
+    return p.parse_args()
+
+
+def main():
+    args = _parse()
+    import torch
+    import torch.distributed as dist
+
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
+    from ptype_amd.ops.table import RegistryTable, actor_keys
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"--gpus {args.gpus} needs torchrun with {args.gpus} processes", file=sys.stderr)
+            sys.exit(2)
+    use_gpu = not args.cpu
+    if use_gpu:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
+                                device_id=device if use_gpu else None)
+
+    def barrier():
+        if world > 1:
+            if use_gpu:
+                dist.barrier(device_ids=[local])
+            else:
+                dist.barrier()
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize(device)
+
+    M = args.msgs_per_gpu
+    n_actors = args.actors_per_gpu * world
+    chunks = args.chunks or (1 if world == 1 else 4)
+
+    # GPU registry mirror: actor a lives on rank a % world in mailbox a // world
+    table = RegistryTable(2 * n_actors, device=device)
+    ids = torch.arange(n_actors, dtype=torch.int64)
+    table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
+    state = torch.zeros(args.actors_per_gpu, dtype=torch.int64, device=device)
+    ex = ActorExchange(table, M, chunks=chunks, state=state)
+    req = B.MsgBatch(torch.empty(M, dtype=torch.int32, device=device), torch.empty(M, dtype=torch.int64, device=device),
+                     torch.empty(M, dtype=torch.int64, device=device), None, METHOD_CALC_MULTIPLY)
+    val = torch.empty(M, dtype=torch.int64, device=device)
+    st = torch.empty(M, dtype=torch.int32, device=device)
+
+    def step(s):
+        B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=(s * world + rank) * 0x1000193 + 7, device=device,
+                       out=req)
+        ex.send(req, val, st)
+
+    def verify(tag):
+        ok = bool((st == STATUS_OK).all()) and bool(torch.equal(val, req.a0 * req.a1))
+        if not ok:
+            bad = int((st != STATUS_OK).sum())
+            raise SystemExit(f"[rank {rank}] {tag}: verification failed ({bad} non-OK replies)")
+
+    for s in range(args.warmup):
+        step(s)
+    sync()
+    if args.warmup:
+        verify("warmup")
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(args.warmup + s)
+    sync()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if args.steps:
+        verify("timed")
+
+    # p50 RTT of a synchronous Call to a GPU actor (persistent dispatcher)
+    p50 = None
+    if use_gpu and args.rtt_calls > 0:
+        from ptype_amd.ops import hip
+
+        srv = hip().DeviceServer(local, 4096, state.data_ptr(), state.numel(), 0, 200.0, 60.0)
+        try:
+            lat = []
+            for i in range(args.rtt_calls + 100):
+                a = i % state.numel()
+                t = time.perf_counter()
+                v, s_, _ = srv.call(METHOD_CALC_MULTIPLY, a, i, 3)
+                dt = time.perf_counter() - t
+                if v != 3 * i or s_ != STATUS_OK:
+                    raise SystemExit(f"RTT call returned {v}, status {s_}")
+                if i >= 100:
+                    lat.append(dt)
+            lat.sort()
+            p50 = lat[len(lat) // 2] * 1e6
+        finally:
+            srv.close()
+        if world > 1:
+            t = torch.tensor([p50], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            p50 = float(t.item())
+
+    total_msgs = M * world * args.steps
+    value = total_msgs / elapsed if elapsed > 0 else 0.0
+    if rank == 0:
+        out = {
+            "metric": "messages/sec",
+            "value": value,
+            "unit": "msg/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / max(args.steps, 1) * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic",
+            "p50_rtt_us": p50,
+            "config": {
+                "model": "calculator actor (Calculator.Multiply)",
+                "global_batch": M * world,
+                "seq_len": None,
+                "parallelism": f"actors sharded over {world} GPU(s), RCCL all-to-all epochs",
+                "msgs_per_gpu_per_step": M,
+                "actors": n_actors,
+                "chunks": chunks,
+                "record_bytes": 32,
+                "client_batch": "SoA (actor u32, A i64, B i64)",
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,8 +1,8 @@
 // Batch data path of the actor runtime: the device-native `Send` pipeline.
 //
-//   gen_requests   synthetic client load (one MsgRecord per message)
-//   route_bucket   K1: GPU-registry lookup -> destination rank -> LDS-staged
-//                  counting sort -> per-rank epoch slots in HBM (send buffer)
+//   gen_requests   synthetic client load (SoA columns)
+//   route_*        K1: GPU-registry lookup -> destination rank -> stable
+//                  bucketing into per-rank epoch slots in HBM (send buffer)
 //   <RCCL all-to-all of the epoch slots over xGMI; skipped when R == 1>
 //   dispatch       K3: per received record, switch on method id into the
 //                  compiled-in handler, write the reply record in place
@@ -13,192 +13,250 @@
 // (cluster/rpc.go:69-105, :176-183) and the server's goroutine-per-request
 // dispatch (stdlib, wired at example/calculator/server/server.go:16-20).
 //
-// Epoch slot layout, per destination rank d: [C + 1] records, record 0 is a
-// header {actor = delivered count, a0 = raw count incl. overflow, a1 = sender
-// rank}; records 1..C are messages.  Replies use the same [R][C+1] geometry so
-// the reverse all-to-all returns every reply to the slot its request left from;
-// `perm[i]` remembers that slot for message i (or -1 overflow, -2 no actor).
+// Client batches are SoA (GPU-native): actor u32[M], a0/a1/a2 int64[M] (a1/a2
+// optional), method either a column or one uniform id.  A calculator message
+// therefore costs 20 bytes to read, not a 32-byte AoS record.
+//
+// Routing is deterministic and needs no inter-block synchronisation inside a
+// streaming kernel:
+//   route_prep     one coalesced pass: registry lookup -> route word
+//                  (rank | mbox << 8) per message + per-block histogram
+//   route_scan     one block: exclusive scan of the histograms per destination,
+//                  slot headers, overflow / no-actor statistics
+//   route_scatter  same block ranges again, stable in-order placement (wave
+//                  ballots + a small LDS prefix per tile), SoA -> AoS packing
+//                  of the 32-byte wire record
+// Destination slots hold messages in the senders' message order, so the GPU
+// output is bit-identical to the CPU reference.
+//
+// Epoch slot layout, per destination rank d: [C + 1] records; record 0 is a
+// header {u32 delivered, u32 raw count, u32 sender rank, ...}; records 1..C are
+// messages.  Replies use the same [R][C+1] geometry so the reverse all-to-all
+// returns every reply to the slot its request left from; `perm[i]` remembers
+// that slot for message i (-1 overflow, -2 no actor).
 #include "common.hpp"
 #include "handlers.hpp"
 
 namespace ptype {
 
-constexpr int kRouteThreads = 256;
-constexpr int kRouteItems = 4;
-constexpr int kRouteTile = kRouteThreads * kRouteItems;  // 1024 records = 32 KiB of LDS
 constexpr int kMaxRanks = 64;
+constexpr int kRouteThreads = 256;
+constexpr int kScatterItems = 2;
+constexpr int kScatterTile = kRouteThreads * kScatterItems;
+constexpr uint32_t kRouteNoActor = 0xffu;  // route word rank byte for a registry miss
+constexpr uint32_t kMaxMbox = 1u << 24;
+
+// Resolve `key` against one probe group held in registers.  Written with named
+// registers and selects, not an indexed array + early return: that form made
+// hipcc spill the group to scratch and serialise every lookup on vmcnt(0).
+__device__ __forceinline__ void check_entry(const uint4& e, uint64_t key, int& rank, uint32_t& mbox, bool& done) {
+  const uint64_t k = ((uint64_t)e.y << 32) | e.x;
+  const bool hit = !done && k == key;
+  const bool miss = !done && k == kKeyEmpty;
+  rank = hit ? (int)e.z : rank;
+  mbox = hit ? e.w : mbox;
+  done = done || hit || miss;
+}
 
 __device__ __forceinline__ void lookup_entry(const TableEntry* __restrict__ t, uint64_t mask, uint64_t key,
                                              int& rank, uint32_t& mbox) {
   rank = -1;
   mbox = 0;
-  uint64_t h = mix64(key) & mask;
-  for (uint64_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
-    const uint4 e = *reinterpret_cast<const uint4*>(&t[h]);
-    const uint64_t k = ((uint64_t)e.y << 32) | e.x;
-    if (k == key) {
-      rank = (int)e.z;
-      mbox = e.w;
-      return;
-    }
-    if (k == kKeyEmpty) return;
+  bool done = false;
+  uint64_t g = probe_start(key, mask);
+  for (uint64_t step = 0; step <= mask && !done; step += kGroup, g = (g + kGroup) & mask) {
+    const uint4* p = reinterpret_cast<const uint4*>(t + g);
+    const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];  // one 64-B line, four loads in flight
+    check_entry(e0, key, rank, mbox, done);
+    check_entry(e1, key, rank, mbox, done);
+    check_entry(e2, key, rank, mbox, done);
+    check_entry(e3, key, rank, mbox, done);
   }
 }
 
-__global__ __launch_bounds__(256) void gen_requests_kernel(MsgRecord* __restrict__ out, int64_t M,
-                                                           uint32_t n_actors, uint16_t method, uint64_t seed) {
+__global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
+                                                           int64_t* __restrict__ a1, int64_t M, uint32_t n_actors,
+                                                           uint64_t seed) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = mix64(seed ^ (uint64_t)i * 0x9e3779b97f4a7c15ull);
-    uint4 lo, hi;
-    lo.x = (uint32_t)(h % n_actors);
-    lo.y = (uint32_t)method | ((uint32_t)kFlagValid << 16);
-    const int64_t a0 = (int64_t)((h >> 20) & 0xffff) - 0x8000;
-    const int64_t a1 = (int64_t)((h >> 40) & 0xffff);
-    lo.z = (uint32_t)a0;
-    lo.w = (uint32_t)((uint64_t)a0 >> 32);
-    hi.x = (uint32_t)a1;
-    hi.y = (uint32_t)((uint64_t)a1 >> 32);
-    hi.z = 0;
-    hi.w = 0;
-    uint4* o = reinterpret_cast<uint4*>(out + i);
-    o[0] = lo;
-    o[1] = hi;
+    actor[i] = (uint32_t)(h % n_actors);
+    a0[i] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
+    a1[i] = (int64_t)((h >> 40) & 0xffff);
   }
 }
 
-__global__ __launch_bounds__(kRouteThreads) void route_bucket_kernel(
-    const MsgRecord* __restrict__ in, int64_t M, const TableEntry* __restrict__ table, uint64_t mask, int R,
-    int64_t C, MsgRecord* __restrict__ sendbuf, int32_t* __restrict__ perm, unsigned* __restrict__ counts,
-    unsigned* __restrict__ ticket, unsigned long long* __restrict__ stats, int rank_self) {
-  __shared__ uint4 stage[kRouteTile * 2];        // 32 KiB: the tile, sorted by destination
-  __shared__ unsigned wcnt[kRouteThreads / kWave][kMaxRanks];
-  __shared__ unsigned doff[kMaxRanks + 1];       // exclusive prefix of the block's per-dest counts
-  __shared__ unsigned gbase[kMaxRanks];          // reserved global base per dest
-  const unsigned tid = threadIdx.x, w = tid / kWave, lane = lane_id();
-  const uint4* in4 = reinterpret_cast<const uint4*>(in);
-  uint4* out4 = reinterpret_cast<uint4*>(sendbuf);
-  unsigned long long nomatch = 0, overflow = 0;
-
-  for (int64_t tile = blockIdx.x * (int64_t)kRouteTile; tile < M; tile += (int64_t)gridDim.x * kRouteTile) {
-    uint4 lo[kRouteItems], hi[kRouteItems];
-    int dest[kRouteItems];
-    unsigned lrank[kRouteItems];
-#pragma unroll
-    for (int k = 0; k < kRouteItems; ++k) {
-      const int64_t idx = tile + k * kRouteThreads + tid;
-      dest[k] = -2;  // -2: no message in this lane
-      if (idx < M) {
-        lo[k] = in4[idx * 2];
-        hi[k] = in4[idx * 2 + 1];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kRouteItems; ++k) {
-      const int64_t idx = tile + k * kRouteThreads + tid;
-      if (idx < M) {
-        int r;
-        uint32_t mb;
-        lookup_entry(table, mask, actor_key(lo[k].x), r, mb);
-        if (r >= 0 && r < R) {
-          dest[k] = r;
-          lo[k].x = mb;  // route: the receiver indexes its mailbox directly
-          lo[k].y |= (uint32_t)kFlagRouted << 16;
-        } else {
-          dest[k] = -1;
-          perm[idx] = -2;
-          ++nomatch;
-        }
-      }
-    }
-    // wave-level ranking per destination: ballot + mbcnt, no LDS atomics
-    for (int d = 0; d < R; ++d) {
-      unsigned c = 0;
-#pragma unroll
-      for (int k = 0; k < kRouteItems; ++k) {
-        const uint64_t m = __ballot(dest[k] == d);
-        if (dest[k] == d) lrank[k] = c + mbcnt64(m);
-        c += (unsigned)__popcll(m);
-      }
-      if (lane == 0) wcnt[w][d] = c;
-    }
-    __syncthreads();
-    if (tid < (unsigned)R) {
-      unsigned tot = 0;
-      for (unsigned x = 0; x < kRouteThreads / kWave; ++x) tot += wcnt[x][tid];
-      gbase[tid] = tot ? atomicAdd(&counts[tid], tot) : 0u;
-      doff[tid + 1] = tot;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      doff[0] = 0;
-      for (int d = 0; d < R; ++d) doff[d + 1] += doff[d];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kRouteItems; ++k) {
-      const int d = dest[k];
-      if (d < 0) continue;
-      unsigned woff = 0;
-      for (unsigned x = 0; x < w; ++x) woff += wcnt[x][d];
-      const unsigned pin = woff + lrank[k];
-      const unsigned lp = doff[d] + pin;
-      stage[lp * 2] = lo[k];
-      stage[lp * 2 + 1] = hi[k];
-      const int64_t idx = tile + k * kRouteThreads + tid;
-      const int64_t slot = (int64_t)gbase[d] + pin;
-      if (slot < C) {
-        perm[idx] = (int32_t)((int64_t)d * (C + 1) + 1 + slot);
-      } else {
-        perm[idx] = -1;
-        ++overflow;
-      }
-    }
-    __syncthreads();
-    // write-out: consecutive lanes write consecutive 16-B halves of the sorted tile
-    const unsigned nb = doff[R];
-    for (unsigned q = tid; q < nb * 2; q += kRouteThreads) {
-      const unsigned p = q >> 1;
-      int d = 0;
-      while (d + 1 < R && doff[d + 1] <= p) ++d;
-      const int64_t slot = (int64_t)gbase[d] + (p - doff[d]);
-      if (slot < C) out4[((int64_t)d * (C + 1) + 1 + slot) * 2 + (q & 1)] = stage[q];
-    }
-    __syncthreads();
-  }
-
-  for (int off = 32; off > 0; off >>= 1) {
-    nomatch += __shfl_xor(nomatch, off);
-    overflow += __shfl_xor(overflow, off);
-  }
-  if (lane == 0 && (nomatch | overflow)) {
-    atomicAdd(&stats[0], nomatch);
-    atomicAdd(&stats[1], overflow);
-  }
-  // last-arriving block publishes the per-destination headers
+// Pass 1: lookup + histogram.  Block b owns messages [b*P, min(M,(b+1)*P)).
+__global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_t* __restrict__ actor, int64_t M,
+                                                                   int64_t P, const TableEntry* __restrict__ table,
+                                                                   uint64_t mask, int R,
+                                                                   uint32_t* __restrict__ route,
+                                                                   uint32_t* __restrict__ hist) {
+  __shared__ unsigned h[kMaxRanks + 1];
+  for (int d = threadIdx.x; d <= R; d += blockDim.x) h[d] = 0;
   __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    const unsigned prev = atomicAdd(ticket, 1u);
-    if (prev == gridDim.x - 1) {
-      for (int d = 0; d < R; ++d) {
-        const unsigned raw = atomicAdd(&counts[d], 0u);
-        uint4 h0, h1;
-        h0.x = raw < C ? raw : (unsigned)C;
-        h0.y = (uint32_t)kFlagValid << 16;
-        h0.z = raw;
-        h0.w = 0;
-        h1.x = (unsigned)rank_self;
-        h1.y = 0;
-        h1.z = 0;
-        h1.w = 0;
-        out4[(int64_t)d * (C + 1) * 2] = h0;
-        out4[(int64_t)d * (C + 1) * 2 + 1] = h1;
+  const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
+  const unsigned lane = lane_id();
+  for (int64_t base = lo; base < hi; base += blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    int d = -1;  // -1: no message in this lane
+    if (i < hi) {
+      int r;
+      uint32_t mb;
+      lookup_entry(table, mask, actor_key(actor[i]), r, mb);
+      const bool ok = r >= 0 && r < R && mb < kMaxMbox;
+      d = ok ? r : R;  // column R counts registry misses
+      route[i] = ok ? ((uint32_t)r | (mb << 8)) : kRouteNoActor;
+    }
+    // wave histogram: one ballot per destination present in the wave
+    uint64_t active = __ballot(d >= 0);
+    while (active) {
+      const int leader = __builtin_ctzll(active);
+      const int dl = __shfl(d, leader);
+      const uint64_t m = __ballot(d == dl);
+      if (lane == (unsigned)leader) atomicAdd(&h[dl], (unsigned)__popcll(m));
+      active &= ~m;
+    }
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d <= R; d += blockDim.x) hist[(int64_t)blockIdx.x * (R + 1) + d] = h[d];
+}
+
+// Pass 2 (one block): per-destination exclusive scan over blocks; headers; stats.
+__global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__ hist, int G, int R, int64_t C,
+                                                          MsgRecord* __restrict__ sendbuf,
+                                                          unsigned long long* __restrict__ stats, int rank_self) {
+  __shared__ unsigned part[1024];
+  __shared__ unsigned long long overflow_tot, nomatch_tot;
+  if (threadIdx.x == 0) {
+    overflow_tot = 0;
+    nomatch_tot = 0;
+  }
+  __syncthreads();
+  const int per = (G + blockDim.x - 1) / blockDim.x;
+  const int b0 = threadIdx.x * per, b1 = b0 + per < G ? b0 + per : G;
+  for (int d = 0; d <= R; ++d) {
+    unsigned s = 0;
+    for (int b = b0; b < b1; ++b) s += hist[(int64_t)b * (R + 1) + d];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over 1024 partial sums
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+      unsigned v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    unsigned run = part[threadIdx.x] - s;  // exclusive
+    for (int b = b0; b < b1; ++b) {        // hist becomes the per-block base
+      const unsigned c = hist[(int64_t)b * (R + 1) + d];
+      hist[(int64_t)b * (R + 1) + d] = run;
+      run += c;
+    }
+    if (threadIdx.x == blockDim.x - 1) {
+      const unsigned total = part[threadIdx.x];
+      if (d < R) {
+        uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)d * (C + 1));
+        const unsigned delivered = total < C ? total : (unsigned)C;
+        h4[0] = make_uint4(delivered, total, (unsigned)rank_self, (uint32_t)kFlagValid << 16);
+        h4[1] = make_uint4(0, 0, 0, 0);
+        if (total > C) overflow_tot += total - C;
+      } else {
+        nomatch_tot = total;
       }
     }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    stats[0] += nomatch_tot;
+    stats[1] += overflow_tot;
   }
 }
 
-// K3 (batch form).  grid.y = source rank, grid.x tiles the slot range.
+// Pass 3: stable placement + SoA -> AoS packing of the wire records.
+__global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
+    const uint32_t* __restrict__ route, const uint32_t* __restrict__ actor_unused, const int64_t* __restrict__ a0,
+    const int64_t* __restrict__ a1, const int64_t* __restrict__ a2, const uint16_t* __restrict__ method_col,
+    uint32_t method_uniform, int64_t M, int64_t P, int R, int64_t C, const uint32_t* __restrict__ base,
+    MsgRecord* __restrict__ sendbuf, int32_t* __restrict__ perm) {
+  __shared__ unsigned cnt[kScatterItems][kRouteThreads / kWave][kMaxRanks];
+  __shared__ unsigned run[kMaxRanks];
+  const unsigned tid = threadIdx.x, w = tid / kWave, lane = lane_id();
+  for (int d = tid; d < R; d += blockDim.x) run[d] = base[(int64_t)blockIdx.x * (R + 1) + d];
+  const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
+  uint4* out4 = reinterpret_cast<uint4*>(sendbuf);
+  __syncthreads();
+  for (int64_t tile = lo; tile < hi; tile += kScatterTile) {
+    int d[kScatterItems];
+    uint32_t rw[kScatterItems];
+    unsigned rk[kScatterItems];
+#pragma unroll
+    for (int k = 0; k < kScatterItems; ++k) {
+      const int64_t i = tile + k * kRouteThreads + tid;
+      rw[k] = i < hi ? route[i] : kRouteNoActor;
+      d[k] = (i < hi && (rw[k] & 0xff) != kRouteNoActor) ? (int)(rw[k] & 0xff) : -1;
+      rk[k] = 0;
+    }
+    // rank within (item k, wave w, destination): ballots, peeled per present destination
+#pragma unroll
+    for (int k = 0; k < kScatterItems; ++k) {
+      for (int x = lane; x < R; x += kWave) cnt[k][w][x] = 0;
+      uint64_t active = __ballot(d[k] >= 0);
+      while (active) {
+        const int leader = __builtin_ctzll(active);
+        const int dl = __shfl(d[k], leader);
+        const uint64_t m = __ballot(d[k] == dl);
+        if (d[k] == dl) rk[k] = mbcnt64(m);
+        if (lane == (unsigned)leader) cnt[k][w][dl] = (unsigned)__popcll(m);
+        active &= ~m;
+      }
+    }
+    __syncthreads();
+    // per destination: exclusive prefix in message order (k-major, then wave)
+    for (int x = tid; x < R; x += blockDim.x) {
+      unsigned r = run[x];
+      for (int k = 0; k < kScatterItems; ++k)
+        for (int ww = 0; ww < kRouteThreads / kWave; ++ww) {
+          const unsigned c = cnt[k][ww][x];
+          cnt[k][ww][x] = r;
+          r += c;
+        }
+      run[x] = r;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScatterItems; ++k) {
+      const int64_t i = tile + k * kRouteThreads + tid;
+      if (i >= hi) continue;
+      if (d[k] < 0) {
+        perm[i] = -2;
+        continue;
+      }
+      const int64_t pos = (int64_t)cnt[k][w][d[k]] + rk[k];
+      if (pos >= C) {
+        perm[i] = -1;
+        continue;
+      }
+      const int64_t slot = (int64_t)d[k] * (C + 1) + 1 + pos;
+      perm[i] = (int32_t)slot;
+      const uint32_t meth = method_col ? method_col[i] : method_uniform;
+      const int64_t v0 = a0[i], v1 = a1 ? a1[i] : 0, v2 = a2 ? a2[i] : 0;
+      uint4 r0, r1;
+      r0.x = rw[k] >> 8;  // local mailbox index at the destination
+      r0.y = (meth & 0xffff) | ((uint32_t)(kFlagValid | kFlagRouted) << 16);
+      r0.z = (uint32_t)v0;
+      r0.w = (uint32_t)((uint64_t)v0 >> 32);
+      r1.x = (uint32_t)v1;
+      r1.y = (uint32_t)((uint64_t)v1 >> 32);
+      r1.z = (uint32_t)v2;
+      r1.w = (uint32_t)((uint64_t)v2 >> 32);
+      out4[slot * 2] = r0;
+      out4[slot * 2 + 1] = r1;
+    }
+    __syncthreads();
+  }
+}
+
+// K3 (batch form).  grid.y = source rank, grid.x tiles the delivered range.
 __global__ __launch_bounds__(256) void dispatch_kernel(const MsgRecord* __restrict__ recv, int64_t C,
                                                        ReplyRecord* __restrict__ reply, int64_t* __restrict__ state,
                                                        uint32_t n_state, uint64_t delay_ticks,
@@ -206,10 +264,10 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const MsgRecord* __restri
   const int d = blockIdx.y;
   const uint4* r4 = reinterpret_cast<const uint4*>(recv + (int64_t)d * (C + 1));
   const uint4 h = r4[0];
-  const bool valid = (h.y >> 16) & kFlagValid;
+  const bool valid = (h.w >> 16) & kFlagValid;
   const int64_t count = valid ? (int64_t)(h.x < C ? h.x : C) : 0;
   ReplyRecord* rp = reply + (int64_t)d * (C + 1);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // reply header: delivered count (sender audits it)
     ReplyRecord hr;
     hr.value = count;
     hr.status = kStatusOk;
@@ -234,7 +292,7 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const MsgRecord* __restri
   if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);
 }
 
-// K8: replies back to message order.
+// K8: replies back to message order (SoA outputs).
 __global__ __launch_bounds__(256) void complete_kernel(const ReplyRecord* __restrict__ rep,
                                                        const int32_t* __restrict__ perm, int64_t M,
                                                        int64_t* __restrict__ out_val, int32_t* __restrict__ out_st,
@@ -255,9 +313,12 @@ __global__ __launch_bounds__(256) void complete_kernel(const ReplyRecord* __rest
     out_st[i] = st;
     sum += (unsigned long long)v;
   }
-  if (checksum) {
+  if (checksum) {  // block-reduce first: one atomic per block, not per wave
+    __shared__ unsigned long long part[4];
     for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
-    if (lane_id() == 0) atomicAdd(checksum, sum);
+    if (lane_id() == 0) part[threadIdx.x / kWave] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(checksum, part[0] + part[1] + part[2] + part[3]);
   }
 }
 
@@ -268,33 +329,58 @@ static inline unsigned grid_cap(int64_t work, int per, unsigned cap) {
   return (unsigned)g;
 }
 
-void launch_gen_requests(uintptr_t out, int64_t M, uint32_t n_actors, int method, uint64_t seed, uintptr_t stream) {
+void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M, uint32_t n_actors, uint64_t seed,
+                         uintptr_t stream) {
   if (M <= 0) return;
   if (n_actors == 0) throw std::invalid_argument("n_actors must be > 0");
   hipLaunchKernelGGL(gen_requests_kernel, dim3(grid_cap(M, 256, 8192)), dim3(256), 0, as_stream(stream),
-                     (MsgRecord*)out, M, n_actors, (uint16_t)method, seed);
+                     (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed);
   PT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_route_bucket(uintptr_t in, int64_t M, uintptr_t table, uint64_t cap, int R, int64_t C,
-                         uintptr_t sendbuf, uintptr_t perm, uintptr_t counts, uintptr_t ticket, uintptr_t stats,
-                         int rank_self, uintptr_t stream) {
-  if (R < 1 || R > kMaxRanks) throw std::invalid_argument("route_bucket: 1 <= R <= 64");
-  if (C < 1 || C >= (1ll << 31) / R) throw std::invalid_argument("route_bucket: bad capacity");
+// Route blocks: G = ceil(M / P); the scan kernel handles up to 1024 * 64 blocks.
+int64_t route_grid(int64_t M, int64_t* P_out) {
+  int64_t G = (M + 4095) / 4096;  // ~4K messages per block: 8 scatter tiles
+  if (G < 1) G = 1;
+  if (G > 4096) G = 4096;
+  int64_t P = (M + G - 1) / G;
+  P = ((P + 255) / 256) * 256;
+  if (P < 256) P = 256;
+  G = (M + P - 1) / P;
+  if (G < 1) G = 1;
+  *P_out = P;
+  return G;
+}
+
+void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                  int method_uniform, int64_t M, uintptr_t table, uint64_t cap, int R, int64_t C, uintptr_t sendbuf,
+                  uintptr_t perm, uintptr_t route, uintptr_t hist, uintptr_t stats, int rank_self,
+                  uintptr_t stream) {
+  if (R < 1 || R > kMaxRanks) throw std::invalid_argument("route: 1 <= R <= 64");
+  if (C < 1 || C >= (1ll << 31) / R) throw std::invalid_argument("route: bad capacity");
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
-  // >= 1 block even for M == 0 so the last arriver still writes the headers
-  const unsigned g = grid_cap(M, kRouteTile, 2048);
-  hipLaunchKernelGGL(route_bucket_kernel, dim3(g), dim3(kRouteThreads), 0, as_stream(stream), (const MsgRecord*)in,
-                     M, (const TableEntry*)table, cap - 1, R, C, (MsgRecord*)sendbuf, (int32_t*)perm,
-                     (unsigned*)counts, (unsigned*)ticket, (unsigned long long*)stats, rank_self);
+  int64_t P;
+  const int64_t G = route_grid(M, &P);
+  hipStream_t s = as_stream(stream);
+  if (M > 0)
+    hipLaunchKernelGGL(route_prep_kernel, dim3((unsigned)G), dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
+                       (const TableEntry*)table, cap - 1, R, (uint32_t*)route, (uint32_t*)hist);
+  else
+    PT_HIP_CHECK(hipMemsetAsync((void*)hist, 0, sizeof(uint32_t) * (R + 1) * G, s));
+  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, s, (uint32_t*)hist, (int)G, R, C, (MsgRecord*)sendbuf,
+                     (unsigned long long*)stats, rank_self);
+  if (M > 0)
+    hipLaunchKernelGGL(route_scatter_kernel, dim3((unsigned)G), dim3(kRouteThreads), 0, s, (const uint32_t*)route,
+                       (const uint32_t*)actor, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,
+                       (const uint16_t*)method_col, (uint32_t)method_uniform, M, P, R, C, (const uint32_t*)hist,
+                       (MsgRecord*)sendbuf, (int32_t*)perm);
   PT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_dispatch(uintptr_t recv, int R, int64_t C, uintptr_t reply, uintptr_t state, uint32_t n_state,
                      uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank, uintptr_t stream) {
   if (R < 1) throw std::invalid_argument("dispatch: R >= 1");
-  // size the grid for the expected fill, not the capacity, so padding costs no blocks
-  int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
+  const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
   const unsigned gx = grid_cap(per, 256, (unsigned)(4096 / R > 0 ? 4096 / R : 1));
   hipLaunchKernelGGL(dispatch_kernel, dim3(gx, R), dim3(256), 0, as_stream(stream), (const MsgRecord*)recv, C,
                      (ReplyRecord*)reply, (int64_t*)state, n_state, delay_ticks, (unsigned long long*)stats);
@@ -304,9 +390,9 @@ void launch_dispatch(uintptr_t recv, int R, int64_t C, uintptr_t reply, uintptr_
 void launch_complete(uintptr_t rep, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
                      uintptr_t checksum, uintptr_t stream) {
   if (M <= 0) return;
-  hipLaunchKernelGGL(complete_kernel, dim3(grid_cap(M, 256, 8192)), dim3(256), 0, as_stream(stream),
-                     (const ReplyRecord*)rep, (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st,
-                     (unsigned long long*)checksum);
+  hipLaunchKernelGGL(complete_kernel, dim3(grid_cap(M, 256, checksum ? 1024 : 8192)), dim3(256), 0,
+                     as_stream(stream), (const ReplyRecord*)rep, (const int32_t*)perm, M, (int64_t*)out_val,
+                     (int32_t*)out_st, (unsigned long long*)checksum);
   PT_HIP_CHECK(hipGetLastError());
 }
 

@@ -19,9 +19,10 @@ void launch_table_delete(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uin
 void launch_table_lookup(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uintptr_t);
 void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
-void launch_gen_requests(uintptr_t, int64_t, uint32_t, int, uint64_t, uintptr_t);
-void launch_route_bucket(uintptr_t, int64_t, uintptr_t, uint64_t, int, int64_t, uintptr_t, uintptr_t, uintptr_t,
-                         uintptr_t, uintptr_t, int, uintptr_t);
+void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t);
+int64_t route_grid(int64_t, int64_t*);
+void launch_route(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t, int,
+                  int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
 void launch_dispatch(uintptr_t, int, int64_t, uintptr_t, uintptr_t, uint32_t, uint64_t, uintptr_t, int64_t,
                      uintptr_t);
 void launch_complete(uintptr_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
@@ -72,10 +73,16 @@ PYBIND11_MODULE(_hip, m) {
   m.def("table_pack", &launch_table_pack, py::arg("table"), py::arg("cap"), py::arg("exp_tbl"), py::arg("out"),
         py::arg("out_exp"), py::arg("out_count"), py::arg("stream"));
 
-  m.def("gen_requests", &launch_gen_requests, py::arg("out"), py::arg("M"), py::arg("n_actors"),
-        py::arg("method"), py::arg("seed"), py::arg("stream"));
-  m.def("route_bucket", &launch_route_bucket, py::arg("inp"), py::arg("M"), py::arg("table"), py::arg("cap"),
-        py::arg("R"), py::arg("C"), py::arg("sendbuf"), py::arg("perm"), py::arg("counts"), py::arg("ticket"),
+  m.def("gen_requests", &launch_gen_requests, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("M"),
+        py::arg("n_actors"), py::arg("seed"), py::arg("stream"));
+  m.def("route_grid", [](int64_t M) {
+    int64_t P;
+    int64_t G = route_grid(M, &P);
+    return py::make_tuple(G, P);
+  });
+  m.def("route", &launch_route, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"),
+        py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
+        py::arg("R"), py::arg("C"), py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"),
         py::arg("stats"), py::arg("rank_self"), py::arg("stream"));
   m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("reply"),
         py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),

@@ -43,6 +43,14 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
+// Probing starts at the 4-slot group (one 64-B line) the hash lands in, so a
+// lookup issues the whole line as four independent dwordx4 loads and resolves
+// almost every key with ONE memory latency (linear probing, load factor <= 0.5).
+constexpr int kGroup = 4;
+__host__ __device__ __forceinline__ uint64_t probe_start(uint64_t key, uint64_t mask) {
+  return mix64(key) & mask & ~(uint64_t)(kGroup - 1);
+}
+
 // Actor ids used on the batch path map to table keys as id + 1 (0 is "empty").
 __host__ __device__ __forceinline__ uint64_t actor_key(uint32_t actor) { return (uint64_t)actor + 1ull; }
 

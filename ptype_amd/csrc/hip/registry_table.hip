@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void table_upsert_kernel(TableEntry* __restric
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
     if (key == kKeyEmpty || key == kKeyTomb) continue;
-    uint64_t h = mix64(key) & mask;
+    uint64_t h = probe_start(key, mask);
     uint64_t probe = 0;
     bool ok = false;
     for (; probe <= mask; ++probe, h = (h + 1) & mask) {
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void table_delete_kernel(TableEntry* __restric
     const uint64_t key = keys[i];
     bool hit = false;
     if (key != kKeyEmpty && key != kKeyTomb) {
-      uint64_t h = mix64(key) & mask;
+      uint64_t h = probe_start(key, mask);
       for (uint64_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
         uint64_t cur = ld_key(&t[h]);
         if (cur == kKeyEmpty) break;
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void table_lookup_kernel(const TableEntry* __r
     const uint64_t key = keys[i];
     int32_t rank = -1, mbox = -1;
     if (key != kKeyEmpty && key != kKeyTomb) {
-      uint64_t h = mix64(key) & mask;
+      uint64_t h = probe_start(key, mask);
       for (uint64_t probe = 0; probe <= mask; ++probe, h = (h + 1) & mask) {
         const uint4 e = *reinterpret_cast<const uint4*>(&t[h]);  // one dwordx4
         const uint64_t k = ((uint64_t)e.y << 32) | e.x;

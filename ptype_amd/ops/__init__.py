@@ -72,10 +72,10 @@ def _check(t: torch.Tensor, dtype, ndim=None, name="tensor"):
 
 
 from .table import RegistryTable, actor_keys, mix64  # noqa: E402
-from .batch import complete, dispatch, gen_requests, route_bucket  # noqa: E402
+from .batch import MsgBatch, RouteWorkspace, complete, dispatch, gen_requests, route  # noqa: E402
 
 __all__ = [
-    "hip", "records", "RegistryTable", "actor_keys", "mix64", "gen_requests", "route_bucket", "dispatch",
+    "hip", "records", "RegistryTable", "actor_keys", "mix64", "gen_requests", "route", "MsgBatch", "RouteWorkspace", "dispatch",
     "complete", "make_requests", "split_requests", "split_replies", "FLAG_VALID", "FLAG_ROUTED",
     "METHOD_CALC_MULTIPLY", "METHOD_PRIME_CHECK", "METHOD_ECHO", "METHOD_RETRY_TEST", "METHOD_COUNTER_ADD",
     "STATUS_OK", "STATUS_FAILED", "STATUS_NO_ACTOR", "STATUS_NO_METHOD", "STATUS_OVERFLOW",

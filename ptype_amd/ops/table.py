@@ -38,6 +38,13 @@ def mix64(x: np.ndarray) -> np.ndarray:
     return x
 
 
+GROUP = 4  # probe group (kGroup): probing starts at the 64-B line the hash lands in
+
+
+def probe_start(h: np.ndarray, mask: int) -> np.ndarray:
+    return h & np.uint64(mask) & ~np.uint64(GROUP - 1)
+
+
 def actor_keys(actor_ids: torch.Tensor) -> torch.Tensor:
     """Table keys of batch-path actors: id + 1 (0 means empty)."""
     return actor_ids.to(torch.int64) + 1
@@ -230,7 +237,7 @@ class RegistryTable:
             key = int(k_np[i])
             if key in (KEY_EMPTY, KEY_TOMB):
                 continue
-            h = int(h_all[i]) & mask
+            h = int(h_all[i]) & mask & ~(GROUP - 1)
             for probe in range(self.cap):
                 cur = int(tk[h])
                 if cur == key:
@@ -260,7 +267,7 @@ class RegistryTable:
             key = int(k_np[i])
             if key in (KEY_EMPTY, KEY_TOMB):
                 continue
-            h = int(h_all[i]) & mask
+            h = int(h_all[i]) & mask & ~(GROUP - 1)
             for _ in range(self.cap):
                 cur = int(tk[h])
                 if cur == KEY_EMPTY:
@@ -284,7 +291,7 @@ class RegistryTable:
         rank = np.full(n, -1, dtype=np.int32)
         mbox = np.full(n, -1, dtype=np.int32)
         valid = (k_np != KEY_EMPTY) & (k_np != KEY_TOMB)
-        h = (mix64(k_np.view(np.uint64)) & np.uint64(mask)).astype(np.int64)
+        h = probe_start(mix64(k_np.view(np.uint64)), mask).astype(np.int64)
         pending = np.nonzero(valid)[0]
         for _ in range(self.cap):
             if pending.size == 0:

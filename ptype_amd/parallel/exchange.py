@@ -1,0 +1,168 @@
+"""Exchange-epoch engine: remote `Send` between GPUs over RCCL (xGMI).
+
+One process per GPU; every rank is both a client (it sends messages to actors
+anywhere in the node) and a server (it hosts a shard of the actors).  The
+reference moves each call over its own TCP connection (cluster/rpc.go:272-285,
+`rpc.DialHTTP`; calls at :65 and :88).  Here traffic moves in *epochs*: each
+rank buckets its outbound records by destination GPU (K1, LDS-staged counting
+sort), one RCCL all-to-all moves every bucket at once over all 7 xGMI links,
+the receiver runs the handler table over what it got (K3), a second all-to-all
+returns the 16-B replies into the exact slots the requests left from, and K8
+scatters them back to message order.
+
+Fixed-capacity slots (``C + 1`` records per peer, slot 0 a header with the
+count) make both all-to-alls equal-split: no host round trip for sizes, so an
+epoch is launch-only and the host never blocks inside it.  A bucket that
+overflows ``C`` leaves the overflow in the caller's queue for the next epoch
+(``STATUS_OVERFLOW`` until re-sent), which is the actor model's usual
+at-least-once hand-off rather than an error.
+
+Pipelining: ``send()`` splits a batch into chunks; chunk k's all-to-alls run on
+the process group's communication stream while chunk k+1 is routed and chunk
+k-1 is dispatched on the compute stream (RCCL work handles give stream-level,
+not host-level, waits).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from ..ops import batch as B
+from ..ops.records import STATUS_OVERFLOW
+from ..ops.table import RegistryTable
+
+
+def capacity_for(msgs_per_chunk: int, world: int, slack: float = 0.06) -> int:
+    """Per-peer slot capacity for uniformly spread traffic (mean + slack + an
+    8-sigma margin per stripe), so overflow is a statistical non-event."""
+    return B.stripe_capacity(msgs_per_chunk, world, slack)
+
+
+@dataclass
+class EpochStats:
+    sent: int = 0
+    overflow: int = 0
+    nomatch: int = 0
+    failed: int = 0
+
+
+class _ChunkBufs:
+    def __init__(self, R, C, M, device):
+        self.send = torch.empty(R * (C + 1), 4, dtype=torch.int64, device=device)
+        self.recv = torch.empty_like(self.send) if R > 1 else self.send
+        self.reply = torch.empty(R * (C + 1), 2, dtype=torch.int64, device=device)
+        self.back = torch.empty_like(self.reply) if R > 1 else self.reply
+        self.perm = torch.empty(M, dtype=torch.int32, device=device)
+        self.rws = B.RouteWorkspace(M, R, device)
+        self.ws = self.rws.ws
+
+
+class ActorExchange:
+    """Epoch exchange over the default (or given) process group.
+
+    ``table`` is this rank's GPU registry mirror (actor -> rank, mailbox);
+    ``state`` the int64 actor state of the mailboxes this rank hosts.
+    """
+
+    def __init__(self, table: RegistryTable, max_batch: int, chunks: int = 1, group=None, state=None,
+                 delay_us: int = 0, slack: float = 0.06):
+        self.table = table
+        self.device = table.device
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.rank = dist.get_rank(group)
+            self.world = dist.get_world_size(group)
+        else:
+            self.rank, self.world = 0, 1
+        self.chunks = max(1, int(chunks))
+        self.max_chunk = int(math.ceil(max_batch / self.chunks))
+        self.C = capacity_for(self.max_chunk, self.world, slack)
+        self.state = state
+        self.delay_us = delay_us
+        self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device) for _ in range(min(self.chunks, 2))]
+        self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
+
+    # ------------------------------------------------------------------
+    def _a2a(self, out, inp):
+        if self.world == 1:
+            return None
+        return dist.all_to_all_single(out, inp, group=self.group, async_op=True)
+
+    def send(self, req: B.MsgBatch, out_val: torch.Tensor | None = None, out_status: torch.Tensor | None = None):
+        """Deliver every message of ``req`` (a SoA ``MsgBatch``) to its actor and return
+        ``(value int64[M], status int32[M])`` in message order.  Collective:
+        every rank of the group must call it (with its own, possibly empty, batch)
+        the same number of times."""
+        M = req.M
+        if M > self.max_chunk * self.chunks:
+            raise ValueError(f"batch of {M} exceeds max_batch {self.max_chunk * self.chunks}")
+        dev = self.device
+        out_val = torch.empty(M, dtype=torch.int64, device=dev) if out_val is None else out_val
+        out_status = torch.empty(M, dtype=torch.int32, device=dev) if out_status is None else out_status
+        n = self.chunks
+        bounds = [min(M, i * self.max_chunk) for i in range(n + 1)]
+        R, C = self.world, self.C
+        pending_bwd = []  # (chunk index, work handle, bufs)
+
+        def finish(entry):
+            i, work, bufs = entry
+            if work is not None:
+                work.wait()
+            lo, hi = bounds[i], bounds[i + 1]
+            B.complete(bufs.back, bufs.perm[: hi - lo], out_val[lo:hi], out_status[lo:hi], self.checksum)
+
+        fwd = None
+        for i in range(n):
+            bufs = self.bufs[i % len(self.bufs)]
+            lo, hi = bounds[i], bounds[i + 1]
+            # buffer reuse: chunk i-2's replies must be consumed before overwriting
+            while pending_bwd and pending_bwd[0][0] <= i - len(self.bufs):
+                finish(pending_bwd.pop(0))
+            B.route(req.slice(lo, hi), self.table, R, C, self.rank, sendbuf=bufs.send, perm=bufs.perm[: hi - lo],
+                    rws=bufs.rws)
+            work = self._a2a(bufs.recv, bufs.send)
+            if fwd is not None:
+                pending_bwd.append(self._serve(*fwd))
+            fwd = (i, work, bufs, hi - lo)
+        if fwd is not None:
+            pending_bwd.append(self._serve(*fwd))
+        for e in pending_bwd:
+            finish(e)
+        return out_val, out_status
+
+    def _serve(self, i, work, bufs, m):
+        if work is not None:
+            work.wait()
+        B.dispatch(bufs.recv, self.world, self.C, self.state, self.delay_us, reply=bufs.reply, ws=bufs.ws,
+                   expected_per_rank=max(1, m // self.world))
+        return (i, self._a2a(bufs.back, bufs.reply), bufs)
+
+    # ------------------------------------------------------------------
+    def send_all(self, req: B.MsgBatch, max_epochs: int = 16):
+        """`send` + re-send of overflowed messages until every one is delivered
+        (host-synchronising: reads the overflow count once per epoch)."""
+        val, st = self.send(req)
+        for _ in range(max_epochs):
+            over = st == STATUS_OVERFLOW
+            n_over = torch.tensor([int(over.sum())], device=self.device)
+            if self.world > 1:
+                dist.all_reduce(n_over, group=self.group)
+            if int(n_over.item()) == 0:
+                break
+            idx = torch.nonzero(over).flatten()
+            v2, s2 = self.send(req.index_select(idx))
+            val[idx] = v2
+            st[idx] = s2
+        return val, st
+
+    def stats(self) -> EpochStats:
+        s = EpochStats()
+        for b in self.bufs:
+            w = B.ws_stats(b.ws).tolist()
+            s.nomatch += w[B.STAT_NOMATCH]
+            s.overflow += w[B.STAT_OVERFLOW]
+            s.failed += w[B.STAT_FAILED]
+        return s

@@ -51,15 +51,21 @@ def test_table_reference_sweep():
     assert (r >= 0).tolist() == [True, False, False, True, True, False, True, True]
 
 
+def _batch(actors, method, a0, a1=None, a2=None):
+    t = lambda x: None if x is None else torch.as_tensor(x, dtype=torch.int64)
+    m = method if isinstance(method, int) else torch.as_tensor(method, dtype=torch.int16)
+    return B.MsgBatch(torch.as_tensor(actors, dtype=torch.int32), t(a0), t(a1), t(a2), m)
+
+
 def test_batch_reference_end_to_end():
     R, C = 3, 64
     t = RegistryTable(64, device="cpu")
     _populate(t, 12, R)
-    req = make_requests(torch.tensor([0, 1, 2, 3, 4, 99]), METHOD_CALC_MULTIPLY, torch.tensor([7, 2, 3, 4, 5, 6]),
-                        torch.tensor([8, 3, 4, 5, 6, 7]))
-    send, perm, ws = B.route_bucket(req, t, R, C)
-    assert B.ws_counts(ws, R).tolist() == [2, 2, 1]
-    assert int(B.ws_stats(ws)[B.STAT_NOMATCH]) == 1
+    req = _batch([0, 1, 2, 3, 4, 99], METHOD_CALC_MULTIPLY, [7, 2, 3, 4, 5, 6], [8, 3, 4, 5, 6, 7])
+    send, perm, stats = B.route(req, t, R, C)
+    hdr = send[0::C + 1, 0]
+    assert (hdr & 0xFFFFFFFF).tolist() == [2, 2, 1]
+    assert int(stats[B.STAT_NOMATCH]) == 1
     rep = B.dispatch(send, R, C)
     val, st = B.complete(rep, perm)
     assert val.tolist()[:5] == [56, 6, 12, 20, 30]
@@ -67,17 +73,26 @@ def test_batch_reference_end_to_end():
 
 
 def test_batch_reference_overflow_and_handlers():
-    R, C = 1, 2
+    R, C = 1, 8
     t = RegistryTable(16, device="cpu")
     _populate(t, 2, 1)
     state = torch.zeros(2, dtype=torch.int64)
-    req = make_requests(torch.tensor([0, 1, 0]), torch.tensor([METHOD_COUNTER_ADD, METHOD_PRIME_CHECK, METHOD_ECHO]),
-                        torch.tensor([5, 2, 9]), torch.tensor([0, 10, 0]), torch.tensor([0, 21, 0]))
-    send, perm, ws = B.route_bucket(req, t, R, C)
+    methods = [METHOD_COUNTER_ADD, METHOD_PRIME_CHECK] + [METHOD_ECHO] * 8
+    req = _batch([0, 1] + [0] * 8, methods, [5, 2] + list(range(8)), [0, 10] + [0] * 8, [0, 21] + [0] * 8)
+    send, perm, stats = B.route(req, t, R, C)
     rep = B.dispatch(send, R, C, state=state)
     val, st = B.complete(rep, perm)
-    assert val.tolist()[:2] == [5, 3]  # counter 0+5, 21 = 3*7 -> first divisor 3
-    assert st.tolist() == [STATUS_OK, STATUS_OK, STATUS_OVERFLOW]
+    assert val.tolist()[:8] == [5, 3, 0, 1, 2, 3, 4, 5]  # counter 0+5, 21 = 3*7 -> first divisor 3
+    assert st.tolist() == [STATUS_OK] * 8 + [STATUS_OVERFLOW] * 2
+    assert int(stats[B.STAT_OVERFLOW]) == 2
+
+
+def test_msgbatch_records_roundtrip():
+    req = make_requests(torch.tensor([3, 4]), torch.tensor([METHOD_ECHO, METHOD_CALC_MULTIPLY]), torch.tensor([1, 2]),
+                        torch.tensor([5, 6]), torch.tensor([7, 8]))
+    b = B.MsgBatch.from_records(req)
+    assert b.actor.tolist() == [3, 4] and b.method.tolist() == [METHOD_ECHO, METHOD_CALC_MULTIPLY]
+    assert torch.equal(b.to_records(), req)
 
 
 def test_retry_reference():
@@ -147,30 +162,31 @@ def test_gpu_table_sweep_and_snapshot():
 @pytest.mark.parametrize("R", [1, 2, 8])
 def test_gpu_route_dispatch_complete(R):
     M, n_actors = 200_003, 4096
-    C = M // R + 4096
+    C = B.stripe_capacity(M, R)
     g = RegistryTable(2 * n_actors, device="cuda")
+    c = RegistryTable(2 * n_actors, device="cpu")
     _populate(g, n_actors, R)
+    _populate(c, n_actors, R)
     req = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=1234, device="cuda")
-    ref_req = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=1234, device="cpu")
-    assert torch.equal(req.cpu(), ref_req), "generator kernel differs from reference"
-    send, perm, ws = B.route_bucket(req, g, R, C, rank_self=0)
-    counts = B.ws_counts(ws, R).cpu()
-    actor = ref_req[:, 0] & 0xFFFFFFFF
-    ref_counts = torch.bincount(actor % R, minlength=R)
-    assert torch.equal(counts.to(torch.int64), ref_counts)
-    assert int(B.ws_stats(ws)[B.STAT_OVERFLOW]) == 0
-    # every message lands exactly once
-    p = perm.cpu().to(torch.int64)
-    assert (p >= 0).all() and torch.unique(p).numel() == M
-    # the routed record in the slot is the original with actor -> mailbox
-    s = send.cpu()
-    assert torch.equal(s[p, 1:], ref_req[:, 1:])
-    assert torch.equal(s[p, 0] & 0xFFFFFFFF, actor // R)
+    ref = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=1234, device="cpu")
+    assert torch.equal(req.actor.cpu(), ref.actor) and torch.equal(req.a0.cpu(), ref.a0)
+    assert torch.equal(req.a1.cpu(), ref.a1), "generator kernel differs from reference"
+    send, perm, stats = B.route(req, g, R, C, rank_self=0)
+    rsend, rperm, rstats = B.route(ref, c, R, C, rank_self=0)
+    # deterministic stable placement: bit-identical to the CPU reference
+    assert torch.equal(perm.cpu(), rperm)
+    used = rperm.to(torch.int64)
+    hdrs = torch.arange(R) * (C + 1)
+    assert torch.equal(send.cpu()[used], rsend[used])  # every occupied slot
+    assert torch.equal(send.cpu()[hdrs], rsend[hdrs])  # per-destination headers
+    assert stats.cpu().tolist()[:2] == rstats.tolist()[:2] == [0, 0]
     rep = B.dispatch(send, R, C, expected_per_rank=M // R)
     val, st = B.complete(rep, perm)
+    rrep = B.dispatch(rsend, R, C)
+    assert torch.equal(rep.cpu()[used], rrep[used]) and torch.equal(rep.cpu()[hdrs], rrep[hdrs])
     torch.cuda.synchronize()
     assert (st.cpu() == STATUS_OK).all()
-    assert torch.equal(val.cpu(), ref_req[:, 1] * ref_req[:, 2])
+    assert torch.equal(val.cpu(), ref.a0 * ref.a1)
 
 
 @pytest.mark.gpu
@@ -179,27 +195,30 @@ def test_gpu_route_overflow_and_unknown():
     g = RegistryTable(256, device="cuda")
     _populate(g, 100, R)
     actors = torch.cat([torch.zeros(1500, dtype=torch.int64), torch.tensor([555])])  # 1500 -> rank 0 (cap 1000)
-    req = make_requests(actors, METHOD_ECHO, torch.arange(1501)).cuda()
-    send, perm, ws = B.route_bucket(req, g, R, C)
+    req = _batch(actors, METHOD_ECHO, torch.arange(1501))
+    req = B.MsgBatch(req.actor.cuda(), req.a0.cuda(), None, None, METHOD_ECHO)
+    send, perm, stats = B.route(req, g, R, C)
     rep = B.dispatch(send, R, C)
     val, st = B.complete(rep, perm)
     st = st.cpu()
-    assert int((st == STATUS_OVERFLOW).sum()) == 500
-    assert int((st == STATUS_NO_ACTOR).sum()) == 1
-    ok = st == STATUS_OK
-    assert torch.equal(val.cpu()[ok], torch.arange(1501)[ok])
+    # stable order: the first C messages are delivered, the rest overflow to the next epoch
+    assert st[:1000].eq(STATUS_OK).all() and st[1000:1500].eq(STATUS_OVERFLOW).all()
+    assert int(st[1500]) == STATUS_NO_ACTOR
+    assert stats.cpu().tolist()[:2] == [1, 500]
+    assert torch.equal(val.cpu()[:1000], torch.arange(1000))
 
 
 @pytest.mark.gpu
 def test_gpu_stateful_handlers_match_reference():
-    R, C = 1, 4096
+    R, C = 1, 8192
     g = RegistryTable(64, device="cuda")
     _populate(g, 4, 1)
     n = 1000
     actors = torch.arange(n) % 4
-    req = make_requests(actors, METHOD_COUNTER_ADD, torch.ones(n, dtype=torch.int64)).cuda()
+    b = _batch(actors, METHOD_COUNTER_ADD, torch.ones(n, dtype=torch.int64))
+    req = B.MsgBatch(b.actor.cuda(), b.a0.cuda(), None, None, METHOD_COUNTER_ADD)
     state = torch.zeros(4, dtype=torch.int64, device="cuda")
-    send, perm, _ = B.route_bucket(req, g, R, C)
+    send, perm, _ = B.route(req, g, R, C)
     rep = B.dispatch(send, R, C, state=state)
     val, st = B.complete(rep, perm)
     assert state.cpu().tolist() == [250] * 4
@@ -209,9 +228,9 @@ def test_gpu_stateful_handlers_match_reference():
         assert sorted(v[actors == a].tolist()) == list(range(1, 251))
     # prime check vs reference
     tgt = torch.tensor([97, 91, 221, 1000003, 49])
-    req = make_requests(torch.zeros(5, dtype=torch.int64), METHOD_PRIME_CHECK, torch.full((5,), 2), torch.full((5,), 1 << 40),
-                        tgt).cuda()
-    send, perm, _ = B.route_bucket(req, g, R, C)
+    b = _batch(torch.zeros(5, dtype=torch.int64), METHOD_PRIME_CHECK, torch.full((5,), 2), torch.full((5,), 1 << 40), tgt)
+    req = B.MsgBatch(b.actor.cuda(), b.a0.cuda(), b.a1.cuda(), b.a2.cuda(), METHOD_PRIME_CHECK)
+    send, perm, _ = B.route(req, g, R, C)
     val, st = B.complete(B.dispatch(send, R, C), perm)
     assert val.cpu().tolist() == [97, 7, 13, 1000003, 7]
 

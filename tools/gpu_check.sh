@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU validation + bench + kernel profile (run under gpurun from the repo root).
+# usage: tools/gpu_check.sh TAG [pytest-target]
+set -o pipefail
+TAG=${1:-run}
+TARGET=${2:-tests}
+mkdir -p gpurun_out
+timeout -k 10 500 python -m pytest $TARGET -m gpu -x -q > gpurun_out/test_$TAG.log 2>&1 || { echo "TESTS FAILED"; tail -30 gpurun_out/test_$TAG.log; exit 1; }
+tail -1 gpurun_out/test_$TAG.log
+timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "BENCH FAILED"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+cat gpurun_out/bench_$TAG.json
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --rtt-calls 0 > gpurun_out/prof_$TAG.log 2>&1 || { echo "PROFILE FAILED"; exit 1; }
+python - "$TAG" <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(f"gpurun_out/prof_{sys.argv[1]}/run_kernel_stats.csv")))
+for r in rows[:10]:
+    print(r["Name"][:60].ljust(60), r["Calls"].rjust(4), ("%.1f" % (float(r["AverageNs"]) / 1e3)).rjust(9), "us", r["Percentage"][:5], "%")
+PY
