@@ -1,0 +1,76 @@
+// Configuration: the ptype YAML (cluster/config.go:12-21) and the
+// control-plane member YAML that the reference hands to etcd's
+// embed.ConfigFromFile (cluster/config.go:35-43; keys as in
+// cluster/testdata/node1.yml).  Both are parsed by the C++ YAML subset with the
+// YAML->JSON typing rules of sigs.k8s.io/yaml.  A `gpu:` section adds the
+// device-runtime keys (device ordinal, ring slots, actor shard size, ...).
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "yaml.hpp"
+
+namespace ptype {
+
+struct Url {
+  std::string scheme, host, raw;
+  int port = 0;
+};
+Url parse_url(const std::string& s);  // throws kConfig
+
+// Control-plane member settings (the reference's embed.Config subset).
+struct MemberConfig {
+  std::string name = "default";
+  std::string dir;  // data-dir (WAL + snapshots)
+  std::vector<std::string> lpurls{"http://localhost:2380"};  // listen-peer-urls
+  std::vector<std::string> lcurls{"http://localhost:2379"};  // listen-client-urls
+  std::vector<std::string> apurls{"http://localhost:2380"};  // initial-advertise-peer-urls
+  std::vector<std::string> acurls{"http://localhost:2379"};  // advertise-client-urls
+  std::string initial_cluster;                               // name=url,...
+  std::string initial_cluster_token = "etcd-cluster";
+  std::string cluster_state = "new";  // new | existing
+  bool strict_reconfig_check = true;
+  std::string logger = "capnslog";
+  int64_t heartbeat_ms = 100;
+  int64_t election_ms = 1000;
+  uint64_t snapshot_count = 100000;
+  bool unsafe_no_fsync = false;
+
+  void validate() const;  // throws kConfig (etcd's Config.Validate checks)
+  std::string effective_initial_cluster() const;
+  static MemberConfig from_yaml(const YNode& root);
+  static MemberConfig from_file(const std::string& path);
+};
+
+struct GpuConfig {
+  int device = -1;            // -1: LOCAL_RANK (one process per GPU)
+  uint32_t ring = 4096;       // latency-path ring slots (power of two)
+  uint32_t actors = 1024;     // actor mailboxes hosted by this process
+  double idle_ms = 200.0;     // persistent dispatcher idle exit
+  uint64_t delay_us = 0;      // Prime.Check per-candidate delay (250000 in the reference)
+  uint64_t max_batch = 1 << 20;
+};
+
+struct Config {
+  std::string service_name;
+  std::string node_name;
+  int64_t port = 0;
+  std::string etcd_config_file;
+  std::vector<std::string> initial_cluster_client_urls;
+  bool debug = false;
+  bool has_gpu = false;
+  GpuConfig gpu;
+  std::shared_ptr<MemberConfig> member;  // reference: unexported Config.etcdConfig
+};
+
+// ConfigFromFile (cluster/config.go:23-46): ptype YAML, then the member YAML
+// resolved relative to the ptype file's directory, then validation.
+Config config_from_file(const std::string& path);
+Config config_from_yaml(const std::string& text);  // ptype keys only (no member file)
+
+std::string read_file(const std::string& path);
+
+}  // namespace ptype
