@@ -1,0 +1,363 @@
+"""The ptype ``cluster`` API for Python, backed by the C++ control plane.
+
+Names follow the reference package (``cluster.Join``, ``ConfigFromFile``,
+``Cluster.Registry`` / ``Store`` / ``MemberList`` / ``NewClient`` / ``Close``,
+``Client.Call`` / ``Go`` / ``Close`` / ``ConnectionErrs``, ``Registry.Register`` /
+``Services`` / ``WatchService``, ``KVStore.Get`` / ``Put`` / ``Delete``, the
+``With*`` option helpers, ``ErrNoKey``, ``ErrNoClientAvailable``,
+``DefaultConnConfig``), plus the north-star entry points ``New`` (= ``Join``),
+``Client.Send`` (batched device-native submit) and ``Serve`` (server-side
+registration, which the reference leaves to stdlib net/rpc).
+
+Reference: cluster/cluster.go, cluster/config.go, cluster/registry.go,
+cluster/store.go, cluster/store_config.go, cluster/rpc.go.
+"""
+from __future__ import annotations
+
+import dataclasses
+import inspect
+from typing import Any, Callable, Iterable
+
+from . import _core
+from ._core import (  # noqa: F401  (re-exported API surface)
+    CallChannel,
+    ConfigError,
+    ConnConfig,
+    Context,
+    ErrChannel,
+    IntChannel,
+    KvClient,
+    LearnerNotReadyError,
+    MemberConfig,
+    MemberError,
+    NoClientAvailableError,
+    NoKeyError,
+    Node,
+    NodesChannel,
+    PtypeError,
+    RpcError,
+    RpcServer,
+    ShutdownError,
+    TimeoutError,
+    UnavailableError,
+)
+from .gobtypes import GoSlice, GoStruct, GoUint  # noqa: F401
+
+# ---------------------------------------------------------------- sentinels
+ErrNoKey = NoKeyError                       # cluster/store.go:15
+ErrNoClientAvailable = NoClientAvailableError  # cluster/rpc.go:16
+ErrLearnerNotReady = LearnerNotReadyError
+
+# ---------------------------------------------------------------- options (store_config.go)
+SortByKey, SortByVersion, SortByCreateRevision, SortByModRevision, SortByValue = range(5)
+SortNone, SortAscend, SortDescend = range(3)
+
+WithPrefix = _core.with_prefix
+WithLimit = _core.with_limit
+WithRev = _core.with_rev
+WithRange = _core.with_range
+WithFromKey = _core.with_from_key
+WithSerializable = _core.with_serializable
+WithKeysOnly = _core.with_keys_only
+WithCountOnly = _core.with_count_only
+WithLease = _core.with_lease
+
+
+def WithSort(target: int, order: int):
+    return _core.with_sort(int(target), int(order))
+
+
+def GetPrefixRangeEnd(prefix: str) -> str:
+    return _core.prefix_range_end(prefix)
+
+
+def DefaultConnConfig() -> ConnConfig:
+    """{MaxConnections 3, InitialNodeTimeout 5 s, DebounceTime 3 s, Retries 2} (rpc.go:33-38)."""
+    return _core.default_conn_config()
+
+
+def background() -> Context:
+    return Context.background()
+
+
+def _ctx(ctx) -> Context:
+    return ctx if ctx is not None else Context.background()
+
+
+# ---------------------------------------------------------------- config
+Config = _core.Config
+
+
+def ConfigFromFile(path: str) -> Config:
+    """Load the ptype YAML and its member (etcd) YAML (cluster/config.go:23-46)."""
+    return _core.config_from_file(path)
+
+
+config_from_file = ConfigFromFile
+
+
+# ---------------------------------------------------------------- registry
+class Registry:
+    """Service registry over the Raft-replicated store (cluster/registry.go)."""
+
+    def __init__(self, core):
+        self._r = core
+
+    def Register(self, ctx, serviceName: str, nodeName: str, host: str, port: int) -> None:
+        self._r.register(_ctx(ctx), serviceName, nodeName, host, int(port))
+
+    def Services(self, ctx=None) -> dict:
+        return self._r.services(_ctx(ctx))
+
+    def WatchService(self, ctx, serviceName: str) -> NodesChannel:
+        return self._r.watch_service(_ctx(ctx), serviceName)
+
+    def nodes(self, ctx, serviceName: str):
+        return self._r.nodes(_ctx(ctx), serviceName)
+
+    register = Register
+    services = Services
+    watch_service = WatchService
+
+    @property
+    def kv(self):
+        return self._r.kv
+
+    def close(self):
+        self._r.close()
+
+
+def new_etcd_registry(endpoints: list[str]) -> Registry:
+    return Registry(_core.EtcdRegistry(list(endpoints)))
+
+
+class KVStore:
+    """Shared KV store under the ``store/`` prefix (cluster/store.go)."""
+
+    def __init__(self, core):
+        self._s = core
+
+    def Get(self, ctx, key: str, *opts) -> list[str]:
+        return self._s.get(_ctx(ctx), key, *opts)
+
+    def Put(self, ctx, key: str, value: str, *opts) -> None:
+        self._s.put(_ctx(ctx), key, value, *opts)
+
+    def Delete(self, ctx, key: str, *opts) -> None:
+        self._s.delete(_ctx(ctx), key, *opts)
+
+    get, put, delete = Get, Put, Delete
+
+    def close(self):
+        self._s.close()
+
+
+def new_kv_store(endpoints: list[str]) -> KVStore:
+    return KVStore(_core.KVStore(list(endpoints)))
+
+
+# ---------------------------------------------------------------- client
+class Client:
+    """RPC client with the reference's balancer semantics (cluster/rpc.go).
+
+    ``Call`` returns the reply (Go writes it through a pointer); ``Go`` returns
+    a call handle whose ``done`` channel later delivers it; ``Send`` is the
+    batched device-native path (see ``ptype_amd.runtime``).
+    """
+
+    def __init__(self, core: _core.RpcClient, runtime=None, service: str = ""):
+        self._c = core
+        self._rt = runtime
+        self.service = service
+
+    def Call(self, serviceMethod: str, args: Any) -> Any:
+        return self._c.call(serviceMethod, args)
+
+    def Go(self, serviceMethod: str, args: Any, done: CallChannel | None = None):
+        return self._c.go(serviceMethod, args, done)
+
+    def Send(self, batch, **kw):
+        """Batched submit of a ``MsgBatch`` to GPU actors of this service:
+        RCCL epoch exchange across ranks, device dispatch, replies in order."""
+        if self._rt is None:
+            raise RuntimeError("Client.Send needs the cluster's device runtime (Join with a gpu: section)")
+        return self._rt.send(self.service, batch, **kw)
+
+    def Close(self) -> None:
+        self._c.close()
+
+    def ConnectionErrs(self) -> ErrChannel:
+        return self._c.connection_errs()
+
+    call, go, send, close = Call, Go, Send, Close
+
+    @property
+    def conns_updated(self) -> IntChannel:
+        return self._c.conns_updated
+
+    def selected_nodes(self):
+        return self._c.selected_nodes()
+
+    @property
+    def cfg(self) -> ConnConfig:
+        return self._c.cfg
+
+
+def new_client(host: str, serviceName: str, nodes: NodesChannel, cfg: ConnConfig | None = None) -> Client:
+    """newClient(host, serviceName, registry, cfg) taking the WatchService channel."""
+    return Client(_core.RpcClient(host, serviceName, nodes, cfg if cfg is not None else DefaultConnConfig()),
+                  service=serviceName)
+
+
+# ---------------------------------------------------------------- server side
+def _exported_methods(receiver) -> list[tuple[str, Callable]]:
+    out = []
+    for name, fn in inspect.getmembers(receiver, predicate=callable):
+        if name[:1].isupper() and not name.startswith("_"):
+            out.append((name, fn))
+    return out
+
+
+class Server:
+    """net/rpc-compatible server (HTTP CONNECT + gob) for host and GPU actors.
+
+    ``Register(receiver)`` mirrors ``rpc.Register``: every exported (capitalised)
+    method of the receiver becomes ``"<TypeName>.<Method>"``; a method takes the
+    decoded args and returns the reply, raising to return an RPC error.
+    ``RegisterDevice`` binds a method to a compiled-in GPU handler through the
+    persistent dispatcher.
+    """
+
+    def __init__(self):
+        self._s = RpcServer()
+
+    def Register(self, receiver, name: str | None = None) -> None:
+        tname = name or type(receiver).__name__
+        methods = _exported_methods(receiver)
+        if not methods:
+            raise ValueError(f"rpc.Register: type {tname} has no exported methods of suitable type")
+        for mname, fn in methods:
+            self._s.register_method(f"{tname}.{mname}", fn)
+
+    def RegisterFunc(self, service_method: str, fn: Callable) -> None:
+        self._s.register_method(service_method, fn)
+
+    def RegisterDevice(self, service_method: str, device_server, method_id: int, fields: Iterable[str] = (),
+                       actor: int = 0, actor_field: str = "") -> None:
+        fn, ctx = device_server.submit_handle()
+        self._s.register_device_method(service_method, fn, ctx, int(method_id), int(actor), list(fields), actor_field)
+
+    def Listen(self, port: int = 0, host: str = "0.0.0.0", local: bool = True) -> int:
+        return self._s.listen(host, int(port), local)
+
+    def Close(self) -> None:
+        self._s.close()
+
+    def Dispatch(self, service_method: str, args: Any) -> Any:
+        return self._s.dispatch(service_method, args)
+
+    @property
+    def port(self) -> int:
+        return self._s.port
+
+    def call_counts(self) -> dict:
+        return self._s.call_counts()
+
+    def debug_page(self) -> str:
+        return self._s.debug_page()
+
+    register, register_func, register_device, listen, close = Register, RegisterFunc, RegisterDevice, Listen, Close
+
+
+def Serve(port: int, *receivers, host: str = "0.0.0.0") -> Server:
+    """rpc.Register(each receiver) + rpc.HandleHTTP + ListenAndServe(":port")
+    (example/calculator/server/server.go:16-20, :38), non-blocking."""
+    s = Server()
+    for r in receivers:
+        s.Register(r)
+    s.Listen(port, host)
+    return s
+
+
+# ---------------------------------------------------------------- cluster
+class Cluster:
+    """Handle returned by ``Join`` (cluster/cluster.go:20-26)."""
+
+    def __init__(self, core: _core.Cluster, cfg: Config, runtime=None):
+        self._c = core
+        self.cfg = cfg
+        self.Registry = Registry(core.registry)
+        self.Store = KVStore(core.store)
+        self.runtime = runtime
+
+    def MemberList(self, ctx=None):
+        return self._c.member_list(_ctx(ctx))
+
+    def NewClient(self, serviceName: str, cfg: ConnConfig | None = None) -> Client:
+        return Client(self._c.new_client(serviceName, cfg), self.runtime, serviceName)
+
+    def Close(self) -> None:
+        if self.runtime is not None:
+            self.runtime.close()
+        self._c.close()
+
+    @property
+    def local_addr(self) -> str:
+        return self._c.local_addr
+
+    @property
+    def member_id(self) -> int:
+        return self._c.member_id
+
+    def status(self):
+        return self._c.member_status()
+
+    registry = property(lambda self: self.Registry)
+    store = property(lambda self: self.Store)
+    member_list, new_client, close = MemberList, NewClient, Close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.Close()
+
+
+def Join(ctx, cfg: Config, runtime: bool | None = None) -> Cluster:
+    """Join the cluster: start the local control-plane member (as a learner via
+    ``initial_cluster_client_urls`` when ``initial-cluster-state: existing``,
+    promoted once caught up), then register ``services/<service>/<node>/`` with
+    a 2 s lease.  With a ``gpu:`` section (or ``runtime=True``) the process also
+    brings up its GPU actor runtime (persistent dispatcher, registry mirror)."""
+    core = _core.Cluster.join(_ctx(ctx), cfg)
+    rt = None
+    want = cfg.has_gpu if runtime is None else runtime
+    if want:
+        from .runtime import DeviceRuntime
+
+        try:
+            rt = DeviceRuntime.for_cluster(core, cfg)
+        except Exception:
+            core.close()
+            raise
+    return Cluster(core, cfg, rt)
+
+
+def New(cfg: Config, ctx=None, runtime: bool | None = None) -> Cluster:
+    """North-star entry point: ``cluster.New(cfg)`` == ``Join(ctx, cfg)``."""
+    return Join(ctx, cfg, runtime)
+
+
+join = Join
+new = New
+
+
+def member_config(**kw) -> MemberConfig:
+    """Programmatic member config (the reference's tests set the unexported
+    etcdConfig fields directly, cluster/cluster_test.go:73-87)."""
+    m = MemberConfig()
+    for k, v in kw.items():
+        if not hasattr(m, k):
+            raise AttributeError(f"MemberConfig has no field {k}")
+        setattr(m, k, v)
+    return m

@@ -42,6 +42,7 @@ struct ApplyResult {
   Errc code = Errc::kGeneric;
   int64_t rev = 0, deleted = 0, lease_id = 0, ttl = 0;
   uint64_t member_id = 0;
+  int conf_type = -1;
   std::vector<MemberInfo> members;
 };
 

@@ -86,6 +86,55 @@ bool Conn::recv(std::string* payload) {
   return true;
 }
 
+bool Conn::write_raw(const std::string& bytes) {
+  if (!alive_.load()) return false;
+  std::lock_guard<std::mutex> g(wmu_);
+  if (!write_all_fd(fd_, bytes.data(), bytes.size())) {
+    alive_.store(false);
+    return false;
+  }
+  return true;
+}
+
+bool Conn::fill() {
+  if (rpos_ > 0 && rpos_ == rbuf_.size()) {
+    rbuf_.clear();
+    rpos_ = 0;
+  }
+  char tmp[16384];
+  for (;;) {
+    ssize_t k = ::recv(fd_, tmp, sizeof tmp, 0);
+    if (k > 0) {
+      rbuf_.append(tmp, (size_t)k);
+      return true;
+    }
+    if (k < 0 && errno == EINTR) continue;
+    alive_.store(false);
+    return false;
+  }
+}
+
+bool Conn::read_exact(char* p, size_t n) {
+  while (rbuf_.size() - rpos_ < n)
+    if (!fill()) return false;
+  memcpy(p, rbuf_.data() + rpos_, n);
+  rpos_ += n;
+  return true;
+}
+
+bool Conn::read_line(std::string* line) {
+  for (;;) {
+    const size_t nl = rbuf_.find('\n', rpos_);
+    if (nl != std::string::npos) {
+      *line = rbuf_.substr(rpos_, nl - rpos_);
+      rpos_ = nl + 1;
+      if (!line->empty() && line->back() == '\r') line->pop_back();
+      return true;
+    }
+    if (rbuf_.size() - rpos_ > 65536 || !fill()) return false;
+  }
+}
+
 void Conn::shutdown() {
   if (alive_.exchange(false)) ::shutdown(fd_, SHUT_RDWR);
 }

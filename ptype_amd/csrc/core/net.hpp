@@ -23,15 +23,22 @@ class Conn {
   ~Conn();
   bool send(const std::string& payload);      // thread-safe; false when broken
   bool recv(std::string* payload);            // one frame; false on EOF / error
+  // raw byte-stream access (Go net/rpc over HTTP CONNECT is not framed)
+  bool write_raw(const std::string& bytes);   // thread-safe
+  bool read_exact(char* p, size_t n);         // buffered
+  bool read_line(std::string* line);          // up to and excluding '\n'
   void shutdown();
   bool alive() const { return alive_.load(); }
   int fd() const { return fd_; }
   std::string peer() const;
 
  private:
+  bool fill();
   int fd_;
   std::atomic<bool> alive_{true};
   std::mutex wmu_;
+  std::string rbuf_;
+  size_t rpos_ = 0;
 };
 
 // Connect to host:port (ms timeout); nullptr on failure (errno-style message in *err).

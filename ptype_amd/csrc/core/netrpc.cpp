@@ -1,0 +1,364 @@
+#include "netrpc.hpp"
+
+#include <condition_variable>
+#include <set>
+
+#include "config.hpp"
+
+namespace ptype {
+
+// ---------------------------------------------------------------- RpcConn
+RpcOutcome RpcConn::call(const std::string& method, const gob::Value& args, int64_t timeout_ms) {
+  struct Slot {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    RpcOutcome out;
+  };
+  auto s = std::make_shared<Slot>();
+  go(method, args, [s](RpcOutcome o) {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->out = std::move(o);
+    s->done = true;
+    s->cv.notify_all();
+  });
+  std::unique_lock<std::mutex> g(s->mu);
+  if (timeout_ms < 0) {
+    s->cv.wait(g, [&] { return s->done; });
+  } else if (!s->cv.wait_for(g, std::chrono::milliseconds(timeout_ms), [&] { return s->done; })) {
+    RpcOutcome o;
+    o.error = "rpc: call timed out";
+    o.code = Errc::kTimeout;
+    return o;
+  }
+  return s->out;
+}
+
+// ---------------------------------------------------------------- NetRpcConn
+static gob::Value make_request(const std::string& method, uint64_t seq) {
+  gob::Value r = gob::Value::Struct("Request");
+  r.fields.emplace_back("ServiceMethod", gob::Value::String(method));
+  r.fields.emplace_back("Seq", gob::Value::Uint(seq));
+  return r;
+}
+
+std::shared_ptr<NetRpcConn> NetRpcConn::dial_http(const std::string& host, int port, int64_t timeout_ms) {
+  std::string err;
+  auto c = tcp_connect(host, port, timeout_ms, &err);
+  if (!c) fail(Errc::kUnavailable, err);
+  if (!c->write_raw("CONNECT /_goRPC_ HTTP/1.0\n\n")) fail(Errc::kUnavailable, "rpc: handshake write failed");
+  std::string status;
+  if (!c->read_line(&status)) fail(Errc::kUnavailable, "unexpected EOF");
+  for (std::string h; c->read_line(&h) && !h.empty();) {
+  }
+  if (status.find("200 Connected to Go RPC") == std::string::npos)
+    fail(Errc::kUnavailable, "unexpected HTTP response: " + status);
+  std::shared_ptr<NetRpcConn> r(new NetRpcConn());
+  r->conn_ = c;
+  r->target_ = host + ":" + std::to_string(port);
+  NetRpcConn* raw = r.get();
+  r->th_ = std::thread([raw] { raw->reader(); });
+  return r;
+}
+
+NetRpcConn::~NetRpcConn() {
+  close();
+  if (th_.joinable()) th_.join();
+}
+
+void NetRpcConn::go(const std::string& method, const gob::Value& args, RpcDone done) {
+  std::string buf;
+  uint64_t seq;
+  {
+    std::lock_guard<std::mutex> g(pmu_);
+    if (shutdown_) {
+      RpcOutcome o;
+      o.error = "connection is shut down";
+      o.code = Errc::kShutdown;
+      done(o);
+      return;
+    }
+    seq = seq_++;
+    pending_[seq] = std::move(done);
+  }
+  bool ok;
+  {
+    std::lock_guard<std::mutex> g(wmu_);
+    try {
+      enc_.encode(make_request(method, seq), &buf);
+      enc_.encode(args, &buf);
+      ok = conn_->write_raw(buf);
+    } catch (const std::exception& e) {
+      RpcDone d;
+      {
+        std::lock_guard<std::mutex> g2(pmu_);
+        d = std::move(pending_[seq]);
+        pending_.erase(seq);
+      }
+      RpcOutcome o;
+      o.error = std::string("gob: ") + e.what();
+      d(o);
+      return;
+    }
+  }
+  if (!ok) fail_all("connection is shut down", Errc::kShutdown);
+}
+
+void NetRpcConn::reader() {
+  gob::Decoder dec([this](char* p, size_t n) { return conn_->read_exact(p, n); });
+  std::string why = "connection is shut down";
+  try {
+    for (;;) {
+      gob::Value hdr, body;
+      if (!dec.decode(&hdr)) break;
+      if (!dec.decode(&body)) {
+        why = "unexpected EOF";
+        break;
+      }
+      const gob::Value* seqv = hdr.field("Seq");
+      const gob::Value* errv = hdr.field("Error");
+      const uint64_t seq = seqv ? seqv->u : 0;
+      RpcDone d;
+      {
+        std::lock_guard<std::mutex> g(pmu_);
+        auto it = pending_.find(seq);
+        if (it == pending_.end()) continue;
+        d = std::move(it->second);
+        pending_.erase(it);
+      }
+      RpcOutcome o;
+      if (errv && !errv->s.empty()) {
+        o.error = errv->s;
+        o.code = Errc::kRpc;
+      } else {
+        o.reply = std::move(body);
+      }
+      d(std::move(o));
+    }
+  } catch (const std::exception& e) {
+    why = e.what();
+  }
+  fail_all(why, Errc::kShutdown);
+}
+
+void NetRpcConn::fail_all(const std::string& why, Errc code) {
+  std::map<uint64_t, RpcDone> ps;
+  {
+    std::lock_guard<std::mutex> g(pmu_);
+    shutdown_ = true;
+    ps.swap(pending_);
+  }
+  for (auto& kv : ps) {
+    RpcOutcome o;
+    o.error = why;
+    o.code = code;
+    kv.second(o);
+  }
+}
+
+void NetRpcConn::close() {
+  {
+    std::lock_guard<std::mutex> g(pmu_);
+    shutdown_ = true;
+  }
+  if (conn_) conn_->shutdown();
+}
+
+// ---------------------------------------------------------------- server
+RpcServer::~RpcServer() { close(); }
+
+void RpcServer::register_method(const std::string& sm, RpcHandler h) {
+  if (sm.find('.') == std::string::npos) fail("rpc: method name must be Type.Method: " + sm);
+  std::lock_guard<std::mutex> g(mu_);
+  methods_[sm] = std::move(h);
+}
+
+bool RpcServer::has_service(const std::string& service) const {
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& kv : methods_)
+    if (kv.first.compare(0, service.size() + 1, service + ".") == 0) return true;
+  return false;
+}
+
+RpcOutcome RpcServer::dispatch(const std::string& sm, const gob::Value& args) {
+  RpcOutcome o;
+  o.code = Errc::kRpc;
+  const size_t dot = sm.rfind('.');
+  if (dot == std::string::npos || dot == 0 || dot + 1 == sm.size()) {
+    o.error = "rpc: service/method request ill-formed: " + sm;
+    return o;
+  }
+  RpcHandler h;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = methods_.find(sm);
+    if (it == methods_.end()) {
+      const std::string svc = sm.substr(0, dot);
+      bool svc_found = false;
+      for (const auto& kv : methods_)
+        if (kv.first.compare(0, svc.size() + 1, svc + ".") == 0) svc_found = true;
+      o.error = svc_found ? "rpc: can't find method " + sm : "rpc: can't find service " + sm;
+      return o;
+    }
+    h = it->second;
+    ++counts_[sm];
+  }
+  try {
+    o.reply = h(args);
+    o.code = Errc::kGeneric;
+  } catch (const std::exception& e) {
+    o.error = e.what();
+  }
+  return o;
+}
+
+int RpcServer::listen(const std::string& host, int port) {
+  listener_.reset(new Listener(host.empty() ? "0.0.0.0" : host, port,
+                               [this](std::shared_ptr<Conn> c) { serve_conn(c); }));
+  port_ = listener_->port();
+  return port_;
+}
+
+void RpcServer::close() {
+  if (listener_) listener_->close();
+  listener_.reset();
+}
+
+std::map<std::string, uint64_t> RpcServer::call_counts() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return counts_;
+}
+
+std::string RpcServer::debug_page() const {
+  // the spirit of net/rpc's /debug/rpc: services, methods, call counts
+  std::lock_guard<std::mutex> g(mu_);
+  std::string o = "<html><body><title>Services</title>\n";
+  std::string cur;
+  for (const auto& kv : methods_) {
+    const std::string svc = kv.first.substr(0, kv.first.rfind('.'));
+    if (svc != cur) {
+      o += "<hr>Service " + svc + "<hr>\n";
+      cur = svc;
+    }
+    auto c = counts_.find(kv.first);
+    o += "<tr><td>" + kv.first + "</td><td>" + std::to_string(c == counts_.end() ? 0 : c->second) + "</td></tr>\n";
+  }
+  return o + "</body></html>\n";
+}
+
+void RpcServer::serve_conn(std::shared_ptr<Conn> c) {
+  std::string line;
+  if (!c->read_line(&line)) return;
+  for (std::string h; c->read_line(&h) && !h.empty();) {
+  }
+  const auto parts = split(line, ' ');
+  const std::string method = parts.size() > 0 ? parts[0] : "";
+  const std::string path = parts.size() > 1 ? parts[1] : "";
+  if (method == "GET" && path == "/debug/rpc") {
+    const std::string body = debug_page();
+    c->write_raw("HTTP/1.0 200 OK\r\nContent-Type: text/html; charset=utf-8\r\nContent-Length: " +
+                 std::to_string(body.size()) + "\r\n\r\n" + body);
+    return;
+  }
+  if (method != "CONNECT") {
+    c->write_raw("HTTP/1.0 405 Method Not Allowed\r\nContent-Type: text/plain; charset=utf-8\r\n\r\n405 must CONNECT\n");
+    return;
+  }
+  if (path != "/_goRPC_") {
+    c->write_raw("HTTP/1.0 404 Not Found\r\n\r\n404 page not found\n");
+    return;
+  }
+  c->write_raw("HTTP/1.0 200 Connected to Go RPC\n\n");
+  auto enc = std::make_shared<gob::Encoder>();
+  auto emu = std::make_shared<std::mutex>();
+  std::atomic<int> inflight{0};
+  gob::Decoder dec([c](char* p, size_t n) { return c->read_exact(p, n); });
+  try {
+    for (;;) {
+      gob::Value req, args;
+      if (!dec.decode(&req)) break;
+      if (!dec.decode(&args)) break;
+      const gob::Value* smv = req.field("ServiceMethod");
+      const gob::Value* seqv = req.field("Seq");
+      const std::string sm = smv ? smv->s : "";
+      const uint64_t seq = seqv ? seqv->u : 0;
+      ++inflight;
+      std::thread([this, c, enc, emu, sm, seq, args, &inflight] {  // a goroutine per request
+        RpcOutcome o = dispatch(sm, args);
+        gob::Value resp = gob::Value::Struct("Response");
+        resp.fields.emplace_back("ServiceMethod", gob::Value::String(sm));
+        resp.fields.emplace_back("Seq", gob::Value::Uint(seq));
+        resp.fields.emplace_back("Error", gob::Value::String(o.error));
+        std::string buf;
+        {
+          std::lock_guard<std::mutex> g(*emu);
+          try {
+            enc->encode(resp, &buf);
+            enc->encode(o.ok() ? o.reply : gob::Value::Struct(""), &buf);  // invalidRequest = struct{}{}
+          } catch (const std::exception& e) {
+            buf.clear();
+            resp.fields[2].second = gob::Value::String(std::string("gob: ") + e.what());
+            enc->encode(resp, &buf);
+            enc->encode(gob::Value::Struct(""), &buf);
+          }
+          c->write_raw(buf);
+        }
+        --inflight;
+      }).detach();
+    }
+  } catch (const std::exception&) {
+  }
+  c->shutdown();
+  while (inflight.load() > 0) sleep_ms(1);
+}
+
+// ---------------------------------------------------------------- local fast path
+void LocalRpcConn::go(const std::string& method, const gob::Value& args, RpcDone done) {
+  if (closed_.load()) {
+    RpcOutcome o;
+    o.error = "connection is shut down";
+    o.code = Errc::kShutdown;
+    done(o);
+    return;
+  }
+  auto srv = srv_;
+  std::thread([srv, method, args, done] { done(srv->dispatch(method, args)); }).detach();
+}
+
+static std::mutex g_local_mu;
+static std::map<int, std::weak_ptr<RpcServer>> g_local;
+
+void local_server_register(int port, std::shared_ptr<RpcServer> s) {
+  std::lock_guard<std::mutex> g(g_local_mu);
+  g_local[port] = s;
+}
+
+void local_server_unregister(int port) {
+  std::lock_guard<std::mutex> g(g_local_mu);
+  g_local.erase(port);
+}
+
+bool is_local_host(const std::string& host) {
+  if (host == "127.0.0.1" || host == "localhost" || host == "0.0.0.0" || host == "::1") return true;
+  static const std::string self = first_nonloopback_ipv4();
+  return !self.empty() && host == self;
+}
+
+std::shared_ptr<RpcServer> local_server_lookup(const std::string& host, int port) {
+  if (!is_local_host(host)) return nullptr;
+  std::lock_guard<std::mutex> g(g_local_mu);
+  auto it = g_local.find(port);
+  return it == g_local.end() ? nullptr : it->second.lock();
+}
+
+std::shared_ptr<RpcConn> dial_node(const std::string& host, int64_t port, int64_t timeout_ms, bool allow_local) {
+  if (allow_local)
+    if (auto s = local_server_lookup(host, (int)port)) return std::make_shared<LocalRpcConn>(s, host + ":" + std::to_string(port));
+  try {
+    return NetRpcConn::dial_http(host, (int)port, timeout_ms);
+  } catch (const Error& e) {
+    fail(Errc::kUnavailable, "failed to dial service address " + host + ":" + std::to_string(port) + ": " + e.what());
+  }
+}
+
+}  // namespace ptype

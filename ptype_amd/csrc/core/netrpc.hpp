@@ -1,0 +1,135 @@
+// Go net/rpc over HTTP CONNECT + gob, client and server (SURVEY C10/C11/C12,
+// Appendix A.2).  The reference's data plane is exactly this protocol
+// (rpc.DialHTTP at cluster/rpc.go:277; servers call rpc.Register +
+// rpc.HandleHTTP, example/calculator/server/server.go:16-20), so a stock Go
+// client can call ptype_amd services and ptype_amd clients can call Go servers.
+//
+// Server methods are C++ callables: host handlers (e.g. Python callbacks) or
+// device-backed handlers that pack the gob args into a 32-B MsgRecord and run
+// it on a GPU actor through the persistent dispatcher (records.hpp
+// DeviceSubmitFn).  Each request runs on its own thread, as Go runs each
+// request in its own goroutine; responses are serialised per connection.
+#pragma once
+#include <stdint.h>
+
+#include <atomic>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gob.hpp"
+#include "net.hpp"
+#include "util.hpp"
+
+namespace ptype {
+
+// A completed call: reply value or error text (rpc.ServerError / transport error).
+struct RpcOutcome {
+  gob::Value reply;
+  std::string error;
+  Errc code = Errc::kGeneric;
+  bool ok() const { return error.empty(); }
+};
+using RpcDone = std::function<void(RpcOutcome)>;
+
+// What the balancer holds per selected node (the reference's *rpc.Client).
+class RpcConn {
+ public:
+  virtual ~RpcConn() = default;
+  virtual void go(const std::string& method, const gob::Value& args, RpcDone done) = 0;
+  virtual RpcOutcome call(const std::string& method, const gob::Value& args, int64_t timeout_ms = -1);
+  virtual void close() = 0;
+  virtual std::string target() const = 0;
+};
+
+// net/rpc client over TCP (rpc.DialHTTP).
+class NetRpcConn : public RpcConn, public std::enable_shared_from_this<NetRpcConn> {
+ public:
+  static std::shared_ptr<NetRpcConn> dial_http(const std::string& host, int port, int64_t timeout_ms);
+  ~NetRpcConn() override;
+  void go(const std::string& method, const gob::Value& args, RpcDone done) override;
+  void close() override;
+  std::string target() const override { return target_; }
+
+ private:
+  NetRpcConn() = default;
+  void reader();
+  void fail_all(const std::string& why, Errc code);
+  std::shared_ptr<Conn> conn_;
+  std::string target_;
+  std::mutex wmu_;
+  gob::Encoder enc_;
+  std::mutex pmu_;
+  std::map<uint64_t, RpcDone> pending_;
+  uint64_t seq_ = 0;
+  bool shutdown_ = false;
+  std::thread th_;
+};
+
+using RpcHandler = std::function<gob::Value(const gob::Value& args)>;  // throw Error(kRpc, msg) to fail
+
+class RpcServer {
+ public:
+  RpcServer() = default;
+  ~RpcServer();
+  // "Type.Method" (rpc.Register's naming)
+  void register_method(const std::string& service_method, RpcHandler h);
+  bool has_service(const std::string& service) const;
+  // Serve HTTP CONNECT /_goRPC_ (and GET /debug/rpc) on host:port; returns the bound port.
+  int listen(const std::string& host, int port);
+  void close();
+  int port() const { return port_; }
+  // In-process dispatch (the LocalConn fast path and the device bridge use it).
+  RpcOutcome dispatch(const std::string& service_method, const gob::Value& args);
+  std::map<std::string, uint64_t> call_counts() const;
+  std::string debug_page() const;
+
+ private:
+  void serve_conn(std::shared_ptr<Conn> c);
+  mutable std::mutex mu_;
+  std::map<std::string, RpcHandler> methods_;
+  std::map<std::string, uint64_t> counts_;
+  std::unique_ptr<Listener> listener_;
+  int port_ = 0;
+};
+
+// In-process connection to a server living in this process: same semantics as
+// a TCP connection, no sockets (used when the dialled port is served locally).
+class LocalRpcConn : public RpcConn {
+ public:
+  LocalRpcConn(std::shared_ptr<RpcServer> s, std::string target) : srv_(std::move(s)), target_(std::move(target)) {}
+  void go(const std::string& method, const gob::Value& args, RpcDone done) override;
+  RpcOutcome call(const std::string& method, const gob::Value& args, int64_t timeout_ms = -1) override {
+    (void)timeout_ms;  // inline dispatch on the caller's thread: no socket, no thread hop
+    if (closed_.load()) {
+      RpcOutcome o;
+      o.error = "connection is shut down";
+      o.code = Errc::kShutdown;
+      return o;
+    }
+    return srv_->dispatch(method, args);
+  }
+  void close() override { closed_ = true; }
+  std::string target() const override { return target_; }
+
+ private:
+  std::shared_ptr<RpcServer> srv_;
+  std::string target_;
+  std::atomic<bool> closed_{false};
+};
+
+// Process-wide table of servers by port, for the LocalRpcConn fast path.
+void local_server_register(int port, std::shared_ptr<RpcServer> s);
+void local_server_unregister(int port);
+std::shared_ptr<RpcServer> local_server_lookup(const std::string& host, int port);
+bool is_local_host(const std::string& host);
+
+// Dial the way the reference does (rpc.DialHTTP("tcp", host:port)), taking the
+// in-process fast path when the port is served by this process.
+std::shared_ptr<RpcConn> dial_node(const std::string& host, int64_t port, int64_t timeout_ms, bool allow_local);
+
+}  // namespace ptype

@@ -91,8 +91,9 @@ class Context {
   void on_done(std::function<void()> fn);
   std::string err() const;
 
- private:
   struct State;
+
+ private:
   std::shared_ptr<State> st_;
   Context();
   friend struct ContextAccess;

@@ -29,3 +29,28 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+def free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def ports():
+    """Distinct free loopback ports (bound-then-released)."""
+    out = []
+
+    def get():
+        while True:
+            p = free_port()
+            if p not in out:
+                out.append(p)
+                return p
+
+    return get
