@@ -67,8 +67,23 @@ def WithSort(target: int, order: int):
     return _core.with_sort(int(target), int(order))
 
 
-def GetPrefixRangeEnd(prefix: str) -> str:
-    return _core.prefix_range_end(prefix)
+def GetPrefixRangeEnd(prefix: str | bytes) -> str | bytes:
+    """Range end of a prefix on its bytes (store_config.go:41-58); returns str
+    when the result is valid UTF-8, else bytes ("\\x00" when no end exists)."""
+    b = bytearray(prefix.encode() if isinstance(prefix, str) else prefix)
+    for i in range(len(b) - 1, -1, -1):
+        if b[i] < 0xFF:
+            b[i] += 1
+            out = bytes(b[: i + 1])
+            break
+    else:
+        out = b"\x00"
+    if isinstance(prefix, str):
+        try:
+            return out.decode()
+        except UnicodeDecodeError:
+            return out
+    return out
 
 
 def DefaultConnConfig() -> ConnConfig:
