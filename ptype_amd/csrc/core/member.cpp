@@ -835,7 +835,9 @@ void Member::maybe_snapshot() {
   storage_->save_snapshot(idx, term, data, hs, tail);
   last_snap_index_ = idx;
   std::lock_guard<std::mutex> g(in_mu_);
-  const uint64_t keep = 5000;
+  // entries kept in memory for slow followers (etcd's SnapshotCatchUpEntries);
+  // anyone further behind gets the snapshot
+  const uint64_t keep = std::min<uint64_t>(5000, std::max<uint64_t>(1, cfg_.snapshot_count / 2));
   if (idx > keep) node_->compact(idx - keep);
 }
 
