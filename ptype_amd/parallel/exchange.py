@@ -79,6 +79,12 @@ class ActorExchange:
             self.rank, self.world = 0, 1
         self.chunks = max(1, int(chunks))
         self.max_chunk = int(math.ceil(max_batch / self.chunks))
+        # every rank must use the same slot geometry (equal-split all-to-all):
+        # agree on the largest chunk and the chunk count once, collectively
+        if self.world > 1:
+            t = torch.tensor([self.max_chunk, self.chunks], dtype=torch.int64, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            self.max_chunk, self.chunks = int(t[0]), int(t[1])
         self.C = capacity_for(self.max_chunk, self.world, slack)
         self.state = state
         self.delay_us = delay_us

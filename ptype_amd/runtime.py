@@ -1,0 +1,211 @@
+"""Per-process GPU actor runtime: the device side of a cluster member.
+
+One process per GPU.  A ``DeviceRuntime`` owns, on its GPU:
+
+* the actor mailboxes' state (``int64`` per actor, random-init optional),
+* the persistent dispatcher (host-visible request/reply rings) for the
+  single-call latency path -- ``Call`` on a GPU actor needs no kernel launch,
+* the GPU registry mirror (``ops.RegistryTable``) mapping every actor id of a
+  service to (rank, mailbox), kept in step with the authoritative control-plane
+  store, and
+* the exchange engine (``parallel.ActorExchange``) for batched ``Send`` across
+  the GPUs of the node over RCCL.
+
+Actor placement is published in the replicated KV store, one key per rank and
+service (``store/_ptype/actors/<service>/<node>`` -> ``{"rank","world","count"}``,
+strided ids: actor ``a`` lives on rank ``a % world`` in mailbox ``a // world``),
+so the Raft log carries one entry per shard, not one per actor, while the GPU
+table holds every actor (1M actors = 2M slots = 32 MB of HBM).
+
+Reference: the reference has no device side; this realises SURVEY C9/C10/C14
+under the API of cluster/cluster.go and cluster/rpc.go.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import torch
+
+from .ops import batch as B
+from .ops import hip
+from .ops.records import STATUS_OK
+from .ops.table import RegistryTable, actor_keys
+
+ACTORS_PREFIX = "_ptype/actors"
+
+
+def _dist():
+    import torch.distributed as dist
+
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+class DeviceRuntime:
+    def __init__(self, device=None, actors: int = 1024, ring: int = 4096, idle_ms: float = 200.0,
+                 delay_us: int = 0, max_batch: int = 1 << 20, chunks: int = 0, random_state: bool = False,
+                 group=None):
+        if device is None:
+            device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("DeviceRuntime needs a HIP device (use ops.* CPU references for host-only tests)")
+        torch.cuda.set_device(self.device)
+        d = _dist()
+        self.group = group
+        self.rank = d.get_rank(group) if d else 0
+        self.world = d.get_world_size(group) if d else 1
+        self.actors = int(actors)
+        if random_state:
+            g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)
+            self.state = torch.randint(0, 1 << 20, (self.actors,), dtype=torch.int64, device=self.device, generator=g)
+        else:
+            self.state = torch.zeros(self.actors, dtype=torch.int64, device=self.device)
+        self.delay_us = int(delay_us)
+        self.server = hip().DeviceServer(self.device.index or 0, int(ring), self.state.data_ptr(), self.actors,
+                                         self.delay_us, float(idle_ms), 60.0)
+        self.table = RegistryTable(2 * self.actors * self.world, device=self.device)
+        self.max_batch = int(max_batch)
+        self.chunks = chunks or (1 if self.world == 1 else 4)
+        self._exchange = None
+        self.shards: dict[str, list[dict]] = {}
+        self._closed = False
+
+    # ------------------------------------------------------------------ setup
+    @classmethod
+    def for_cluster(cls, core_cluster, cfg) -> "DeviceRuntime":
+        g = cfg.gpu
+        dev = None if g.device < 0 else torch.device("cuda", g.device)
+        rt = cls(dev, actors=g.actors, ring=g.ring, idle_ms=g.idle_ms, delay_us=g.delay_us, max_batch=g.max_batch)
+        rt.publish_shard(core_cluster.store, cfg.service_name, cfg.node_name)
+        rt.sync_registry(core_cluster.store, cfg.service_name)
+        return rt
+
+    def publish_shard(self, store, service: str, node: str) -> None:
+        """Record this rank's actor shard of `service` in the replicated store."""
+        from .cluster import Context
+
+        v = json.dumps({"rank": self.rank, "world": self.world, "count": self.actors})
+        store.put(Context.background(), f"{ACTORS_PREFIX}/{service}/{node}", v)
+
+    def sync_registry(self, store, service: str) -> int:
+        """Rebuild the GPU registry mirror of `service` from the published shards
+        (K5 batch upsert on the device); returns the number of actors."""
+        from .cluster import Context, NoKeyError, WithPrefix
+
+        try:
+            vals = store.get(Context.background(), f"{ACTORS_PREFIX}/{service}/", WithPrefix())
+        except NoKeyError:
+            vals = []
+        shards = [json.loads(v) for v in vals]
+        self.shards[service] = shards
+        self.table.clear()
+        total = 0
+        for s in shards:
+            n, r, w = int(s["count"]), int(s["rank"]), int(s["world"])
+            mbox = torch.arange(n, dtype=torch.int64, device=self.device)
+            ids = r + w * mbox
+            self.table.upsert(actor_keys(ids), torch.full((n,), r, dtype=torch.int32, device=self.device),
+                              mbox.to(torch.int32))
+            total += n
+        return total
+
+    def place_local(self, n_actors_total: int | None = None) -> None:
+        """Strided placement without a control plane (single process / bench):
+        every rank mirrors every rank's shard."""
+        n = self.actors
+        self.table.clear()
+        for r in range(self.world):
+            mbox = torch.arange(n, dtype=torch.int64, device=self.device)
+            self.table.upsert(actor_keys(r + self.world * mbox),
+                              torch.full((n,), r, dtype=torch.int32, device=self.device), mbox.to(torch.int32))
+
+    @property
+    def total_actors(self) -> int:
+        return self.actors * self.world
+
+    @property
+    def exchange(self):
+        if self._exchange is None:
+            from .parallel.exchange import ActorExchange
+
+            self._exchange = ActorExchange(self.table, self.max_batch, chunks=self.chunks, group=self.group,
+                                           state=self.state, delay_us=self.delay_us)
+        return self._exchange
+
+    # ------------------------------------------------------------------ data plane
+    def send(self, service: str | None, batch: B.MsgBatch, resend_overflow: bool = True):
+        """Batched Send: every message to its actor anywhere in the node and the
+        replies back in message order.  Collective across the process group."""
+        ex = self.exchange
+        if resend_overflow:
+            return ex.send_all(batch)
+        return ex.send(batch)
+
+    def call(self, method: int, actor: int, a0: int = 0, a1: int = 0, a2: int = 0, timeout: float = 30.0):
+        """Single synchronous call to a local actor through the persistent dispatcher."""
+        v, st, _ = self.server.call(int(method), int(actor), int(a0), int(a1), int(a2), float(timeout))
+        return v, st
+
+    def serve(self, server, service: str, methods: dict) -> None:
+        """Expose GPU handlers over net/rpc: ``methods`` maps a Go method name to
+        ``(method_id, [arg field names])`` -- e.g. ``{"Multiply": (1, ["A", "B"])}``."""
+        for name, (mid, fields) in methods.items():
+            server.RegisterDevice(f"{service}.{name}", self.server, mid, fields)
+
+    # ------------------------------------------------------------------ snapshots (C14)
+    def snapshot_to_host(self) -> dict:
+        """Actor state + packed registry mirror, staged in pinned host DRAM by
+        hipMemcpyAsync on a side stream (the routing stream keeps running)."""
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        h_state = torch.empty(self.state.shape, dtype=self.state.dtype, pin_memory=True)
+        with torch.cuda.stream(side):
+            h_state.copy_(self.state, non_blocking=True)
+        ent, exp = self.table.snapshot_to_host()
+        side.synchronize()
+        return {"state": h_state, "table": ent, "expiry": exp,
+                "meta": torch.tensor([self.rank, self.world, self.actors], dtype=torch.int64)}
+
+    def save(self, path: str) -> dict:
+        from safetensors.torch import save_file
+
+        t0 = time.perf_counter()
+        snap = self.snapshot_to_host()
+        nbytes = sum(v.numel() * v.element_size() for v in snap.values())
+        save_file({k: v.contiguous() for k, v in snap.items()}, path)
+        return {"bytes": nbytes, "seconds": time.perf_counter() - t0}
+
+    def restore(self, path: str) -> None:
+        from safetensors.torch import load_file
+
+        snap = load_file(path)
+        if int(snap["meta"][2]) != self.actors:
+            raise ValueError("snapshot actor count does not match this runtime")
+        self.state.copy_(snap["state"].to(self.device))
+        self.table.clear()
+        if snap["table"].numel():
+            self.table.load_packed(snap["table"], snap["expiry"])
+
+    # ------------------------------------------------------------------ stats / teardown
+    def stats(self) -> dict:
+        return {"rank": self.rank, "world": self.world, "actors": self.actors,
+                "dispatcher_processed": self.server.processed, "dispatcher_launches": self.server.launches,
+                "registry_live": self.table.live, "registry_tombstones": self.table.tombstones}
+
+    def close(self) -> None:
+        if self._closed:
+            return
+        self._closed = True
+        self.server.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def verify_ok(status: torch.Tensor) -> bool:
+    return bool((status == STATUS_OK).all())
