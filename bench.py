@@ -38,6 +38,9 @@ def _parse():
     p.add_argument("--chunks", type=int, default=0, help="pipeline chunks per step (0 = auto)")
     p.add_argument("--rtt-calls", type=int, default=2000)
     p.add_argument("--cpu", action="store_true", help="gloo/CPU dry run of the same pipeline (tests)")
+    p.add_argument("--force-dist", action="store_true",
+                   help="initialise the process group and run the all-to-alls even for one rank "
+                        "(exercises the RCCL path on a 1-GPU box)")
     return p.parse_args()
 
 
@@ -64,12 +67,15 @@ def main():
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
         dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
                                 device_id=device if use_gpu else None)
 
     def barrier():
-        if world > 1:
+        if dist_on:
             if use_gpu:
                 dist.barrier(device_ids=[local])
             else:
@@ -81,12 +87,13 @@ def main():
 
     M = args.msgs_per_gpu
     n_actors = args.actors_per_gpu * world
-    chunks = args.chunks or (1 if world == 1 else 4)
+    chunks = args.chunks or (4 if dist_on else 1)
 
     # GPU registry mirror: actor a lives on rank a % world in mailbox a // world
     table = RegistryTable(2 * n_actors, device=device)
     ids = torch.arange(n_actors, dtype=torch.int64)
     table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
+    table.enable_directory(n_actors)  # K5b route directory: hot path reads 4 B/message, not a probe line
     state = torch.zeros(args.actors_per_gpu, dtype=torch.int64, device=device)
     ex = ActorExchange(table, M, chunks=chunks, state=state)
     req = B.MsgBatch(torch.empty(M, dtype=torch.int32, device=device), torch.empty(M, dtype=torch.int64, device=device),
@@ -119,7 +126,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -147,7 +154,7 @@ def main():
             p50 = lat[len(lat) // 2] * 1e6
         finally:
             srv.close()
-        if world > 1:
+        if dist_on:
             t = torch.tensor([p50], dtype=torch.float64, device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             p50 = float(t.item())
@@ -173,7 +180,7 @@ def main():
                 "model": "calculator actor (Calculator.Multiply)",
                 "global_batch": M * world,
                 "seq_len": None,
-                "parallelism": f"actors sharded over {world} GPU(s), RCCL all-to-all epochs",
+                "parallelism": f"actors sharded over {world} GPU(s)" + (", RCCL all-to-all epochs" if dist_on else ""),
                 "msgs_per_gpu_per_step": M,
                 "actors": n_actors,
                 "chunks": chunks,
@@ -182,7 +189,7 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

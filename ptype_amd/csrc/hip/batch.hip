@@ -58,19 +58,51 @@ __device__ __forceinline__ void check_entry(const uint4& e, uint64_t key, int& r
   done = done || hit || miss;
 }
 
-__device__ __forceinline__ void lookup_entry(const TableEntry* __restrict__ t, uint64_t mask, uint64_t key,
-                                             int& rank, uint32_t& mbox) {
-  rank = -1;
-  mbox = 0;
-  bool done = false;
-  uint64_t g = probe_start(key, mask);
-  for (uint64_t step = 0; step <= mask && !done; step += kGroup, g = (g + kGroup) & mask) {
+// Linear group probing from group `g` on (the first `skip` slots already checked).
+__device__ __forceinline__ void lookup_from(const TableEntry* __restrict__ t, uint64_t mask, uint64_t key, uint64_t g,
+                                            uint64_t skip, int& rank, uint32_t& mbox, bool& done) {
+  for (uint64_t step = skip; step <= mask && !done; step += kGroup, g = (g + kGroup) & mask) {
     const uint4* p = reinterpret_cast<const uint4*>(t + g);
     const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];  // one 64-B line, four loads in flight
     check_entry(e0, key, rank, mbox, done);
     check_entry(e1, key, rank, mbox, done);
     check_entry(e2, key, rank, mbox, done);
     check_entry(e3, key, rank, mbox, done);
+  }
+}
+
+__device__ __forceinline__ void lookup_entry(const TableEntry* __restrict__ t, uint64_t mask, uint64_t key,
+                                             int& rank, uint32_t& mbox) {
+  rank = -1;
+  mbox = 0;
+  bool done = false;
+  lookup_from(t, mask, key, probe_start(key, mask), 0, rank, mbox, done);
+}
+
+// K independent lookups with all K first-group lines in flight at once (the
+// registry is L2/MALL resident, so a lookup is latency- not bandwidth-bound:
+// memory-level parallelism per thread is what hides it).  Keys that miss their
+// first group (rare at load factor <= 0.5) continue one at a time.
+template <int K>
+__device__ __forceinline__ void lookup_many(const TableEntry* __restrict__ t, uint64_t mask, const uint64_t (&key)[K],
+                                            int (&rank)[K], uint32_t (&mbox)[K]) {
+  uint4 e[K][kGroup];
+  uint64_t g[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    g[k] = probe_start(key[k], mask);
+    const uint4* p = reinterpret_cast<const uint4*>(t + g[k]);
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) e[k][j] = p[j];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    bool done = false;
+    rank[k] = -1;
+    mbox[k] = 0;
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) check_entry(e[k][j], key[k], rank[k], mbox[k], done);
+    if (!done) lookup_from(t, mask, key[k], (g[k] + kGroup) & mask, kGroup, rank[k], mbox[k], done);
   }
 }
 
@@ -86,9 +118,14 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
 }
 
 // Pass 1: lookup + histogram.  Block b owns messages [b*P, min(M,(b+1)*P)).
+// Each thread resolves K messages per tile (coalesced, item-major), with their
+// lookups overlapped.  With a route directory (DIR) an actor id below n_dir costs
+// one 4-B read; the hash table is probed only for ids outside it (or fallbacks).
+template <int K, bool DIR>
 __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_t* __restrict__ actor, int64_t M,
                                                                    int64_t P, const TableEntry* __restrict__ table,
-                                                                   uint64_t mask, int R,
+                                                                   uint64_t mask, const uint32_t* __restrict__ dir,
+                                                                   uint32_t n_dir, int R,
                                                                    uint32_t* __restrict__ route,
                                                                    uint32_t* __restrict__ hist) {
   __shared__ unsigned h[kMaxRanks + 1];
@@ -96,25 +133,52 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
   __syncthreads();
   const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
   const unsigned lane = lane_id();
-  for (int64_t base = lo; base < hi; base += blockDim.x) {
-    const int64_t i = base + threadIdx.x;
-    int d = -1;  // -1: no message in this lane
-    if (i < hi) {
-      int r;
-      uint32_t mb;
-      lookup_entry(table, mask, actor_key(actor[i]), r, mb);
-      const bool ok = r >= 0 && r < R && mb < kMaxMbox;
-      d = ok ? r : R;  // column R counts registry misses
-      route[i] = ok ? ((uint32_t)r | (mb << 8)) : kRouteNoActor;
+  for (int64_t base = lo; base < hi; base += K * kRouteThreads) {
+    uint32_t a[K];
+    int r[K];
+    uint32_t mb[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = base + k * kRouteThreads + threadIdx.x;
+      a[k] = i < hi ? actor[i] : 0u;
     }
-    // wave histogram: one ballot per destination present in the wave
-    uint64_t active = __ballot(d >= 0);
-    while (active) {
-      const int leader = __builtin_ctzll(active);
-      const int dl = __shfl(d, leader);
-      const uint64_t m = __ballot(d == dl);
-      if (lane == (unsigned)leader) atomicAdd(&h[dl], (unsigned)__popcll(m));
-      active &= ~m;
+    if constexpr (DIR) {
+      uint32_t w[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) w[k] = a[k] < n_dir ? dir[a[k]] : kDirFallback;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (w[k] == kDirFallback) {
+          lookup_entry(table, mask, actor_key(a[k]), r[k], mb[k]);
+        } else {
+          r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
+          mb[k] = w[k] >> 8;
+        }
+      }
+    } else {
+      uint64_t key[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) key[k] = actor_key(a[k]);
+      lookup_many<K>(table, mask, key, r, mb);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = base + k * kRouteThreads + threadIdx.x;
+      int d = -1;  // -1: no message in this lane
+      if (i < hi) {
+        const bool ok = r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
+        d = ok ? r[k] : R;  // column R counts registry misses
+        route[i] = ok ? ((uint32_t)r[k] | (mb[k] << 8)) : kRouteNoActor;
+      }
+      // wave histogram: one ballot per destination present in the wave
+      uint64_t active = __ballot(d >= 0);
+      while (active) {
+        const int leader = __builtin_ctzll(active);
+        const int dl = __shfl(d, leader);
+        const uint64_t m = __ballot(d == dl);
+        if (lane == (unsigned)leader) atomicAdd(&h[dl], (unsigned)__popcll(m));
+        active &= ~m;
+      }
     }
   }
   __syncthreads();
@@ -187,13 +251,20 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
   __syncthreads();
   for (int64_t tile = lo; tile < hi; tile += kScatterTile) {
     int d[kScatterItems];
-    uint32_t rw[kScatterItems];
+    uint32_t rw[kScatterItems], meth[kScatterItems];
     unsigned rk[kScatterItems];
+    int64_t v0[kScatterItems], v1[kScatterItems], v2[kScatterItems];
+    // payload loads first, so they are in flight during the ranking phase
 #pragma unroll
     for (int k = 0; k < kScatterItems; ++k) {
       const int64_t i = tile + k * kRouteThreads + tid;
-      rw[k] = i < hi ? route[i] : kRouteNoActor;
-      d[k] = (i < hi && (rw[k] & 0xff) != kRouteNoActor) ? (int)(rw[k] & 0xff) : -1;
+      const bool in = i < hi;
+      rw[k] = in ? route[i] : kRouteNoActor;
+      v0[k] = in ? a0[i] : 0;
+      v1[k] = in && a1 ? a1[i] : 0;
+      v2[k] = in && a2 ? a2[i] : 0;
+      meth[k] = in && method_col ? (uint32_t)method_col[i] : method_uniform;
+      d[k] = (in && (rw[k] & 0xff) != kRouteNoActor) ? (int)(rw[k] & 0xff) : -1;
       rk[k] = 0;
     }
     // rank within (item k, wave w, destination): ballots, peeled per present destination
@@ -238,17 +309,15 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
       }
       const int64_t slot = (int64_t)d[k] * (C + 1) + 1 + pos;
       perm[i] = (int32_t)slot;
-      const uint32_t meth = method_col ? method_col[i] : method_uniform;
-      const int64_t v0 = a0[i], v1 = a1 ? a1[i] : 0, v2 = a2 ? a2[i] : 0;
       uint4 r0, r1;
       r0.x = rw[k] >> 8;  // local mailbox index at the destination
-      r0.y = (meth & 0xffff) | ((uint32_t)(kFlagValid | kFlagRouted) << 16);
-      r0.z = (uint32_t)v0;
-      r0.w = (uint32_t)((uint64_t)v0 >> 32);
-      r1.x = (uint32_t)v1;
-      r1.y = (uint32_t)((uint64_t)v1 >> 32);
-      r1.z = (uint32_t)v2;
-      r1.w = (uint32_t)((uint64_t)v2 >> 32);
+      r0.y = (meth[k] & 0xffff) | ((uint32_t)(kFlagValid | kFlagRouted) << 16);
+      r0.z = (uint32_t)v0[k];
+      r0.w = (uint32_t)((uint64_t)v0[k] >> 32);
+      r1.x = (uint32_t)v1[k];
+      r1.y = (uint32_t)((uint64_t)v1[k] >> 32);
+      r1.z = (uint32_t)v2[k];
+      r1.w = (uint32_t)((uint64_t)v2[k] >> 32);
       out4[slot * 2] = r0;
       out4[slot * 2 + 1] = r1;
     }
@@ -352,20 +421,43 @@ int64_t route_grid(int64_t M, int64_t* P_out) {
   return G;
 }
 
+// Items per thread of route_prep (tuning knob; 0 = default).
+static int g_prep_items = 0;
+void set_route_tuning(int prep_items) { g_prep_items = prep_items; }
+
+template <int K, bool DIR>
+static void launch_prep(dim3 g, hipStream_t s, uintptr_t actor, int64_t M, int64_t P, uintptr_t table, uint64_t cap,
+                        uintptr_t dir, uint32_t n_dir, int R, uintptr_t route, uintptr_t hist) {
+  hipLaunchKernelGGL((route_prep_kernel<K, DIR>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
+                     (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, R, (uint32_t*)route,
+                     (uint32_t*)hist);
+}
+
 void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
-                  int method_uniform, int64_t M, uintptr_t table, uint64_t cap, int R, int64_t C, uintptr_t sendbuf,
-                  uintptr_t perm, uintptr_t route, uintptr_t hist, uintptr_t stats, int rank_self,
-                  uintptr_t stream) {
+                  int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
+                  int64_t C, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist, uintptr_t stats,
+                  int rank_self, uintptr_t stream) {
   if (R < 1 || R > kMaxRanks) throw std::invalid_argument("route: 1 <= R <= 64");
   if (C < 1 || C >= (1ll << 31) / R) throw std::invalid_argument("route: bad capacity");
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
   int64_t P;
   const int64_t G = route_grid(M, &P);
   hipStream_t s = as_stream(stream);
-  if (M > 0)
-    hipLaunchKernelGGL(route_prep_kernel, dim3((unsigned)G), dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
-                       (const TableEntry*)table, cap - 1, R, (uint32_t*)route, (uint32_t*)hist);
-  else
+  if (M > 0) {
+    const dim3 g((unsigned)G);
+    const int k = g_prep_items;
+    if (dir && n_dir) {
+      // measured (tools/route_bench.py): 1/2/4 items within 2% of each other
+      if (k == 1) launch_prep<1, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
+      else if (k == 4) launch_prep<4, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
+      else launch_prep<2, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
+    } else {
+      // probe path: 2 lookups in flight per thread is best; 4 costs occupancy (98 VGPRs)
+      if (k == 1) launch_prep<1, false>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
+      else if (k == 4) launch_prep<4, false>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
+      else launch_prep<2, false>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
+    }
+  } else
     PT_HIP_CHECK(hipMemsetAsync((void*)hist, 0, sizeof(uint32_t) * (R + 1) * G, s));
   hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, s, (uint32_t*)hist, (int)G, R, C, (MsgRecord*)sendbuf,
                      (unsigned long long*)stats, rank_self);

@@ -21,8 +21,10 @@ void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uin
 void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t);
 int64_t route_grid(int64_t, int64_t*);
-void launch_route(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t, int,
-                  int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
+void launch_route(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t, uintptr_t,
+                  uint32_t, int, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
+void set_route_tuning(int);
+void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t);
 void launch_dispatch(uintptr_t, int, int64_t, uintptr_t, uintptr_t, uint32_t, uint64_t, uintptr_t, int64_t,
                      uintptr_t);
 void launch_complete(uintptr_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
@@ -82,8 +84,12 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("route", &launch_route, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"),
         py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
-        py::arg("R"), py::arg("C"), py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"),
+        py::arg("dir"), py::arg("n_dir"), py::arg("R"), py::arg("C"), py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"),
         py::arg("stats"), py::arg("rank_self"), py::arg("stream"));
+  m.def("set_route_tuning", &set_route_tuning, py::arg("prep_items"),
+        "route_prep items per thread (1, 2, 4; 0 = default) -- a tuning knob for experiments");
+  m.def("table_build_dir", &launch_table_build_dir, py::arg("table"), py::arg("cap"), py::arg("dir"),
+        py::arg("n_dir"), py::arg("stream"));
   m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("reply"),
         py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),
         py::arg("expected_per_rank"), py::arg("stream"));

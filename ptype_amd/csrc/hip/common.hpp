@@ -54,6 +54,11 @@ __host__ __device__ __forceinline__ uint64_t probe_start(uint64_t key, uint64_t 
 // Actor ids used on the batch path map to table keys as id + 1 (0 is "empty").
 __host__ __device__ __forceinline__ uint64_t actor_key(uint32_t actor) { return (uint64_t)actor + 1ull; }
 
+// Route directory words (dense actor-id -> route word array, see K5b):
+// 0xFFFFFFFF = not registered; kDirFallback = probe the hash table instead.
+constexpr uint32_t kDirMissing = 0xffffffffu;
+constexpr uint32_t kDirFallback = 0xfffffffeu;
+
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ unsigned mbcnt64(uint64_t mask) {

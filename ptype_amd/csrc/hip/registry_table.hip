@@ -186,6 +186,23 @@ __global__ __launch_bounds__(256) void table_pack_kernel(const TableEntry* __res
   }
 }
 
+// K5b: route directory -- the registry flattened for the dense actor-id range
+// [0, n_dir): dir[id] = rank | mbox << 8 (the route word), 0xFFFFFFFF for an id
+// the registry does not hold, kDirFallback when the entry does not fit a route
+// word (the data path then probes the hash table for that id).  The hash table
+// stays the source of truth; this is its compiled form for the message hot path:
+// a 4-B read per message from an L2-resident array instead of a 64-B probe line.
+// `dir` must be pre-filled with 0xFF bytes.
+__global__ __launch_bounds__(256) void table_build_dir_kernel(const TableEntry* __restrict__ t, uint64_t cap,
+                                                              uint32_t* __restrict__ dir, uint64_t n_dir) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint4 v = *reinterpret_cast<const uint4*>(&t[i]);
+    const uint64_t key = ((uint64_t)v.y << 32) | v.x;
+    if (key == kKeyEmpty || key == kKeyTomb || key > n_dir) continue;  // actor_key(id) = id + 1
+    dir[key - 1] = (v.z < 0xfeu && v.w < (1u << 24)) ? (v.z | (v.w << 8)) : kDirFallback;
+  }
+}
+
 static inline unsigned grid_for(int64_t n, int per_block = 256, unsigned cap = 4096) {
   int64_t g = (n + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -226,6 +243,14 @@ void launch_table_sweep(uintptr_t table, uint64_t cap, uintptr_t exp_tbl, uint64
                         uintptr_t stream) {
   hipLaunchKernelGGL(table_sweep_kernel, dim3(grid_for((int64_t)cap)), dim3(256), 0, as_stream(stream),
                      (TableEntry*)table, cap, (const uint64_t*)exp_tbl, now, (unsigned long long*)stats);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_table_build_dir(uintptr_t table, uint64_t cap, uintptr_t dir, uint64_t n_dir, uintptr_t stream) {
+  hipStream_t s = as_stream(stream);
+  PT_HIP_CHECK(hipMemsetAsync((void*)dir, 0xff, n_dir * sizeof(uint32_t), s));
+  hipLaunchKernelGGL(table_build_dir_kernel, dim3(grid_for((int64_t)cap)), dim3(256), 0, s, (const TableEntry*)table,
+                     cap, (uint32_t*)dir, n_dir);
   PT_HIP_CHECK(hipGetLastError());
 }
 

@@ -139,8 +139,10 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
     uniform = isinstance(batch.method, int)
     if dev.type == "cuda":
         mcol = None if uniform else batch.method.to(torch.int16).contiguous()
+        d, n_dir = table.directory()
         hip().route(_ptr(batch.actor), _ptr(batch.a0), _ptr(batch.a1), _ptr(batch.a2), _ptr(mcol),
-                    int(batch.method) if uniform else 0, M, _ptr(table.table), table.cap, R, C, _ptr(sendbuf),
+                    int(batch.method) if uniform else 0, M, _ptr(table.table), table.cap, _ptr(d), n_dir, R, C,
+                    _ptr(sendbuf),
                     _ptr(perm), _ptr(rws.route), _ptr(rws.hist), _ptr(rws.ws), rank_self, _stream(batch.actor))
         return sendbuf, perm, ws_stats(rws.ws)
     # ---- CPU reference: bit-identical layout (stable message order per destination) ----

@@ -76,6 +76,32 @@ class RegistryTable:
         self.table = torch.zeros(self.cap, 2, dtype=torch.int64, device=self.device)
         self.expiry = torch.zeros(self.cap, dtype=torch.int64, device=self.device)
         self.stats = torch.zeros(8, dtype=torch.int64, device=self.device)
+        self.dir = None  # route directory (K5b), GPU only; see enable_directory
+        self.dir_n = 0
+        self._dir_dirty = True
+
+    # ------------------------------------------------------------------ directory
+    def enable_directory(self, n_ids: int) -> None:
+        """Keep a dense route directory for actor ids ``[0, n_ids)``: the registry
+        flattened to one 4-B route word per id (K5b), rebuilt lazily after any
+        mutation.  The data path reads it instead of probing the hash table; ids
+        outside the range still probe the table, so results are identical."""
+        if not self.is_gpu or n_ids <= 0:
+            return
+        if n_ids > (1 << 30):
+            raise ValueError("directory range too large")
+        self.dir_n = int(n_ids)
+        self.dir = torch.empty(self.dir_n, dtype=torch.int32, device=self.device)
+        self._dir_dirty = True
+
+    def directory(self):
+        """``(dir tensor | None, n)`` -- rebuilt on device if the table changed."""
+        if self.dir is None:
+            return None, 0
+        if self._dir_dirty:
+            hip().table_build_dir(_ptr(self.table), self.cap, _ptr(self.dir), self.dir_n, _stream(self.table))
+            self._dir_dirty = False
+        return self.dir, self.dir_n
 
     # ------------------------------------------------------------------ props
     @property
@@ -109,6 +135,7 @@ class RegistryTable:
             raise ValueError("upsert: keys/ranks/mboxes/expiry must have equal length")
         if self.live + self.tombstones + n > self.cap * 3 // 4:
             self._grow(self.live + n)
+        self._dir_dirty = True
         if self.is_gpu:
             hip().table_upsert(_ptr(self.table), self.cap, _ptr(keys), _ptr(ranks), _ptr(mboxes), _ptr(expiry),
                                _ptr(self.expiry), n, _ptr(self.stats), _stream(self.table))
@@ -118,6 +145,7 @@ class RegistryTable:
     def delete(self, keys: torch.Tensor) -> torch.Tensor:
         keys = keys.to(self.device, torch.int64).contiguous()
         found = torch.zeros(keys.numel(), dtype=torch.uint8, device=self.device)
+        self._dir_dirty = True
         if self.is_gpu:
             hip().table_delete(_ptr(self.table), self.cap, _ptr(keys), keys.numel(), _ptr(self.stats), _ptr(found),
                                _stream(self.table))
@@ -140,6 +168,7 @@ class RegistryTable:
 
     def sweep(self, now_ms: int) -> None:
         """K6: tombstone entries whose deadline (host monotonic ms) has passed."""
+        self._dir_dirty = True
         if self.is_gpu:
             hip().table_sweep(_ptr(self.table), self.cap, _ptr(self.expiry), int(now_ms), _ptr(self.stats),
                               _stream(self.table))
@@ -172,6 +201,7 @@ class RegistryTable:
         return out[:n], out_exp[:n]
 
     def clear(self) -> None:
+        self._dir_dirty = True
         self.table.zero_()
         self.expiry.zero_()
         self.stats[STAT_LIVE] = 0

@@ -50,11 +50,12 @@ class EpochStats:
 
 
 class _ChunkBufs:
-    def __init__(self, R, C, M, device):
+    def __init__(self, R, C, M, device, separate=False):
+        sep = R > 1 or separate
         self.send = torch.empty(R * (C + 1), 4, dtype=torch.int64, device=device)
-        self.recv = torch.empty_like(self.send) if R > 1 else self.send
+        self.recv = torch.empty_like(self.send) if sep else self.send
         self.reply = torch.empty(R * (C + 1), 2, dtype=torch.int64, device=device)
-        self.back = torch.empty_like(self.reply) if R > 1 else self.reply
+        self.back = torch.empty_like(self.reply) if sep else self.reply
         self.perm = torch.empty(M, dtype=torch.int32, device=device)
         self.rws = B.RouteWorkspace(M, R, device)
         self.ws = self.rws.ws
@@ -77,6 +78,9 @@ class ActorExchange:
             self.world = dist.get_world_size(group)
         else:
             self.rank, self.world = 0, 1
+        # run the RCCL all-to-alls even on a single rank (validates the collective
+        # path on a 1-GPU box; a 1-rank all-to-all is a device-local copy)
+        self.force_collectives = bool(dist.is_available() and dist.is_initialized() and self.world == 1)
         self.chunks = max(1, int(chunks))
         self.max_chunk = int(math.ceil(max_batch / self.chunks))
         # every rank must use the same slot geometry (equal-split all-to-all):
@@ -88,12 +92,13 @@ class ActorExchange:
         self.C = capacity_for(self.max_chunk, self.world, slack)
         self.state = state
         self.delay_us = delay_us
-        self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device) for _ in range(min(self.chunks, 2))]
+        self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device, self.force_collectives)
+                     for _ in range(min(self.chunks, 2))]
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
 
     # ------------------------------------------------------------------
     def _a2a(self, out, inp):
-        if self.world == 1:
+        if self.world == 1 and not self.force_collectives:
             return None
         return dist.all_to_all_single(out, inp, group=self.group, async_op=True)
 

@@ -190,6 +190,42 @@ def test_gpu_route_dispatch_complete(R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("items", [1, 2, 4])
+def test_gpu_route_directory_matches_hash_probe(items):
+    """K5b: routing through the dense directory is bit-identical to probing the
+    hash table -- ids inside/outside the directory range, deleted ids, and an
+    entry too wide for a route word (directory fallback to the probe)."""
+    R, n_actors, M = 4, 6000, 100_000
+    C = B.stripe_capacity(M, R)
+    g = RegistryTable(2 * n_actors, device="cuda")
+    c = RegistryTable(2 * n_actors, device="cpu")
+    for t in (g, c):
+        _populate(t, n_actors, R)
+        t.delete(actor_keys(torch.arange(100, 200)))  # registered then removed
+        t.upsert(actor_keys(torch.tensor([7])), torch.tensor([300]), torch.tensor([1]))  # rank 300: fallback
+    g.enable_directory(4096)  # ids 4096.. probe the table
+    req = B.gen_requests(M, n_actors + 50, METHOD_CALC_MULTIPLY, seed=99, device="cuda")  # some ids unregistered
+    ref = B.gen_requests(M, n_actors + 50, METHOD_CALC_MULTIPLY, seed=99, device="cpu")
+    try:
+        ops.hip().set_route_tuning(items)
+        send, perm, stats = B.route(req, g, R, C)
+    finally:
+        ops.hip().set_route_tuning(0)
+    rsend, rperm, rstats = B.route(ref, c, R, C)
+    assert torch.equal(perm.cpu(), rperm)
+    used = rperm[rperm >= 0].to(torch.int64)
+    assert torch.equal(send.cpu()[used], rsend[used])
+    assert stats.cpu().tolist()[:2] == rstats.tolist()[:2]
+    assert rstats.tolist()[0] > 0  # misses were exercised
+    # a later mutation invalidates the directory
+    g.delete(actor_keys(torch.tensor([5])))
+    c.delete(actor_keys(torch.tensor([5])))
+    send, perm, _ = B.route(req, g, R, C)
+    rsend, rperm, _ = B.route(ref, c, R, C)
+    assert torch.equal(perm.cpu(), rperm)
+
+
+@pytest.mark.gpu
 def test_gpu_route_overflow_and_unknown():
     R, C = 2, 1000
     g = RegistryTable(256, device="cuda")

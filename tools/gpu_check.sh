@@ -9,6 +9,9 @@ timeout -k 10 500 python -m pytest $TARGET -m gpu -x -q > gpurun_out/test_$TAG.l
 tail -1 gpurun_out/test_$TAG.log
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "BENCH FAILED"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
+# the RCCL collective path on one rank (all-to-alls + barrier + all_reduce)
+timeout -k 10 300 python bench.py --force-dist --steps 10 --warmup 3 --rtt-calls 0 > gpurun_out/bench_dist_$TAG.json 2> gpurun_out/bench_dist_$TAG.err || { echo "DIST BENCH FAILED"; tail -20 gpurun_out/bench_dist_$TAG.err; exit 1; }
+cat gpurun_out/bench_dist_$TAG.json
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --rtt-calls 0 > gpurun_out/prof_$TAG.log 2>&1 || { echo "PROFILE FAILED"; exit 1; }
 python - "$TAG" <<'PY'
