@@ -184,7 +184,8 @@ def main():
                 "msgs_per_gpu_per_step": M,
                 "actors": n_actors,
                 "chunks": chunks,
-                "record_bytes": 32,
+                "record_bytes": 4 * (ex.fmt or B.WireFormat.for_batch(req)).stride,
+                "reply_bytes": 9,
                 "client_batch": "SoA (actor u32, A i64, B i64)",
             },
         }

@@ -3,9 +3,9 @@
 //   gen_requests   synthetic client load (SoA columns)
 //   route_*        K1: GPU-registry lookup -> destination rank -> stable
 //                  bucketing into per-rank epoch slots in HBM (send buffer)
-//   <RCCL all-to-all of the epoch slots over xGMI; skipped when R == 1>
+//   <RCCL all-to-all of the epoch slots over xGMI>
 //   dispatch       K3: per received record, switch on method id into the
-//                  compiled-in handler, write the reply record in place
+//                  compiled-in handler, write the reply in place
 //   <RCCL all-to-all of the reply slots back to the senders>
 //   complete       K8: scatter replies back to the caller's message order
 //
@@ -14,26 +14,30 @@
 // dispatch (stdlib, wired at example/calculator/server/server.go:16-20).
 //
 // Client batches are SoA (GPU-native): actor u32[M], a0/a1/a2 int64[M] (a1/a2
-// optional), method either a column or one uniform id.  A calculator message
-// therefore costs 20 bytes to read, not a 32-byte AoS record.
+// optional), method either a column or one uniform id.
 //
 // Routing is deterministic and needs no inter-block synchronisation inside a
 // streaming kernel:
-//   route_prep     one coalesced pass: registry lookup -> route word
-//                  (rank | mbox << 8) per message + per-block histogram
+//   route_prep     one coalesced pass: route directory / registry lookup ->
+//                  route word (rank | mbox << 8) per message + block histogram
 //   route_scan     one block: exclusive scan of the histograms per destination,
 //                  slot headers, overflow / no-actor statistics
 //   route_scatter  same block ranges again, stable in-order placement (wave
-//                  ballots + a small LDS prefix per tile), SoA -> AoS packing
-//                  of the 32-byte wire record
+//                  ballots + a small LDS prefix per tile), SoA -> packed records
 // Destination slots hold messages in the senders' message order, so the GPU
 // output is bit-identical to the CPU reference.
 //
-// Epoch slot layout, per destination rank d: [C + 1] records; record 0 is a
-// header {u32 delivered, u32 raw count, u32 sender rank, ...}; records 1..C are
-// messages.  Replies use the same [R][C+1] geometry so the reverse all-to-all
-// returns every reply to the slot its request left from; `perm[i]` remembers
-// that slot for message i (-1 overflow, -2 no actor).
+// Wire format v2 (everything in u32 words; every region starts 16-B aligned):
+//   request region per destination d, REQ = round4(4 + C * stride) words:
+//     header  {delivered, raw count, sender rank, kFlagValid << 16 | method}
+//     records [C] x stride words: mbox, [method if method column], a0 lo/hi,
+//             [a1 lo/hi], [a2 lo/hi]   -> stride = 1 + mc + 2 * nargs
+//   a calculator call (uniform method, two args) is 20 B on the wire, not 32.
+//   reply region per destination, REP = round4(4 + 2C + ceil(C / 4)) words:
+//     header {count, 0, 0, 0}; values int64[C]; statuses u8[C]
+//   i.e. 9 B per reply instead of a 16-B record.  The reverse all-to-all brings
+//   every reply back to the slot its request left from; `perm[i]` remembers it
+//   as d * C + pos (-1 overflow, -2 no actor).
 #include "common.hpp"
 #include "handlers.hpp"
 
@@ -187,7 +191,8 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
 
 // Pass 2 (one block): per-destination exclusive scan over blocks; headers; stats.
 __global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__ hist, int G, int R, int64_t C,
-                                                          MsgRecord* __restrict__ sendbuf,
+                                                          uint32_t* __restrict__ sendbuf, int64_t req_words,
+                                                          uint32_t method_uniform,
                                                           unsigned long long* __restrict__ stats, int rank_self) {
   __shared__ unsigned part[1024];
   __shared__ unsigned long long overflow_tot, nomatch_tot;
@@ -219,10 +224,10 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__
     if (threadIdx.x == blockDim.x - 1) {
       const unsigned total = part[threadIdx.x];
       if (d < R) {
-        uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)d * (C + 1));
+        uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)d * req_words);
         const unsigned delivered = total < C ? total : (unsigned)C;
-        h4[0] = make_uint4(delivered, total, (unsigned)rank_self, (uint32_t)kFlagValid << 16);
-        h4[1] = make_uint4(0, 0, 0, 0);
+        h4[0] = make_uint4(delivered, total, (unsigned)rank_self,
+                           ((uint32_t)kFlagValid << 16) | (method_uniform & 0xffffu));
         if (total > C) overflow_tot += total - C;
       } else {
         nomatch_tot = total;
@@ -236,34 +241,35 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__
   }
 }
 
-// Pass 3: stable placement + SoA -> AoS packing of the wire records.
+// Pass 3: stable placement + SoA -> packed wire records (format <NARGS, MC>).
+template <int NARGS, bool MC>
 __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
-    const uint32_t* __restrict__ route, const uint32_t* __restrict__ actor_unused, const int64_t* __restrict__ a0,
-    const int64_t* __restrict__ a1, const int64_t* __restrict__ a2, const uint16_t* __restrict__ method_col,
-    uint32_t method_uniform, int64_t M, int64_t P, int R, int64_t C, const uint32_t* __restrict__ base,
-    MsgRecord* __restrict__ sendbuf, int32_t* __restrict__ perm) {
+    const uint32_t* __restrict__ route, const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
+    const int64_t* __restrict__ a2, const uint16_t* __restrict__ method_col, uint32_t method_uniform, int64_t M,
+    int64_t P, int R, int64_t C, const uint32_t* __restrict__ base, uint32_t* __restrict__ sendbuf,
+    int64_t req_words, int32_t* __restrict__ perm) {
+  constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
   __shared__ unsigned cnt[kScatterItems][kRouteThreads / kWave][kMaxRanks];
   __shared__ unsigned run[kMaxRanks];
   const unsigned tid = threadIdx.x, w = tid / kWave, lane = lane_id();
   for (int d = tid; d < R; d += blockDim.x) run[d] = base[(int64_t)blockIdx.x * (R + 1) + d];
   const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
-  uint4* out4 = reinterpret_cast<uint4*>(sendbuf);
   __syncthreads();
   for (int64_t tile = lo; tile < hi; tile += kScatterTile) {
     int d[kScatterItems];
     uint32_t rw[kScatterItems], meth[kScatterItems];
     unsigned rk[kScatterItems];
-    int64_t v0[kScatterItems], v1[kScatterItems], v2[kScatterItems];
+    int64_t v[kScatterItems][3];
     // payload loads first, so they are in flight during the ranking phase
 #pragma unroll
     for (int k = 0; k < kScatterItems; ++k) {
       const int64_t i = tile + k * kRouteThreads + tid;
       const bool in = i < hi;
       rw[k] = in ? route[i] : kRouteNoActor;
-      v0[k] = in ? a0[i] : 0;
-      v1[k] = in && a1 ? a1[i] : 0;
-      v2[k] = in && a2 ? a2[i] : 0;
-      meth[k] = in && method_col ? (uint32_t)method_col[i] : method_uniform;
+      v[k][0] = in ? a0[i] : 0;
+      v[k][1] = NARGS > 1 && in && a1 ? a1[i] : 0;
+      v[k][2] = NARGS > 2 && in && a2 ? a2[i] : 0;
+      meth[k] = MC ? (in && method_col ? (uint32_t)method_col[i] : method_uniform) : 0u;
       d[k] = (in && (rw[k] & 0xff) != kRouteNoActor) ? (int)(rw[k] & 0xff) : -1;
       rk[k] = 0;
     }
@@ -307,63 +313,65 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
         perm[i] = -1;
         continue;
       }
-      const int64_t slot = (int64_t)d[k] * (C + 1) + 1 + pos;
-      perm[i] = (int32_t)slot;
-      uint4 r0, r1;
-      r0.x = rw[k] >> 8;  // local mailbox index at the destination
-      r0.y = (meth[k] & 0xffff) | ((uint32_t)(kFlagValid | kFlagRouted) << 16);
-      r0.z = (uint32_t)v0[k];
-      r0.w = (uint32_t)((uint64_t)v0[k] >> 32);
-      r1.x = (uint32_t)v1[k];
-      r1.y = (uint32_t)((uint64_t)v1[k] >> 32);
-      r1.z = (uint32_t)v2[k];
-      r1.w = (uint32_t)((uint64_t)v2[k] >> 32);
-      out4[slot * 2] = r0;
-      out4[slot * 2 + 1] = r1;
+      perm[i] = (int32_t)((int64_t)d[k] * C + pos);
+      uint32_t* o = sendbuf + (int64_t)d[k] * req_words + 4 + pos * kStride;
+      o[0] = rw[k] >> 8;  // local mailbox index at the destination
+      if (MC) o[1] = meth[k] & 0xffffu;
+#pragma unroll
+      for (int j = 0; j < NARGS; ++j) {
+        o[1 + (MC ? 1 : 0) + 2 * j] = (uint32_t)v[k][j];
+        o[2 + (MC ? 1 : 0) + 2 * j] = (uint32_t)((uint64_t)v[k][j] >> 32);
+      }
     }
     __syncthreads();
   }
 }
 
 // K3 (batch form).  grid.y = source rank, grid.x tiles the delivered range.
-__global__ __launch_bounds__(256) void dispatch_kernel(const MsgRecord* __restrict__ recv, int64_t C,
-                                                       ReplyRecord* __restrict__ reply, int64_t* __restrict__ state,
-                                                       uint32_t n_state, uint64_t delay_ticks,
-                                                       unsigned long long* __restrict__ stats) {
+template <int NARGS, bool MC>
+__global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restrict__ recv, int64_t req_words,
+                                                       int64_t C, uint32_t* __restrict__ reply, int64_t rep_words,
+                                                       int64_t* __restrict__ state, uint32_t n_state,
+                                                       uint64_t delay_ticks, unsigned long long* __restrict__ stats) {
+  constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
   const int d = blockIdx.y;
-  const uint4* r4 = reinterpret_cast<const uint4*>(recv + (int64_t)d * (C + 1));
-  const uint4 h = r4[0];
+  const uint32_t* rq = recv + (int64_t)d * req_words;
+  const uint4 h = *reinterpret_cast<const uint4*>(rq);
   const bool valid = (h.w >> 16) & kFlagValid;
   const int64_t count = valid ? (int64_t)(h.x < C ? h.x : C) : 0;
-  ReplyRecord* rp = reply + (int64_t)d * (C + 1);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // reply header: delivered count (sender audits it)
-    ReplyRecord hr;
-    hr.value = count;
-    hr.status = kStatusOk;
-    hr.actor = (uint32_t)count;
-    rp[0] = hr;
-  }
+  uint32_t* rp = reply + (int64_t)d * rep_words;
+  int64_t* vals = reinterpret_cast<int64_t*>(rp + 4);
+  uint8_t* sts = reinterpret_cast<uint8_t*>(rp + 4 + 2 * C);
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // reply header: delivered count (sender audits it)
+    *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
   unsigned long long failed = 0;
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count; s += (int64_t)gridDim.x * blockDim.x) {
-    const uint4 lo = r4[(1 + s) * 2], hi = r4[(1 + s) * 2 + 1];
+    const uint32_t* r = rq + 4 + s * kStride;
+    uint32_t wv[kStride];
+#pragma unroll
+    for (int j = 0; j < kStride; ++j) wv[j] = r[j];
     MsgRecord m;
-    m.actor = lo.x;
-    m.method = (uint16_t)(lo.y & 0xffff);
-    m.flags = (uint16_t)(lo.y >> 16);
-    m.a0 = (int64_t)(((uint64_t)lo.w << 32) | lo.z);
-    m.a1 = (int64_t)(((uint64_t)hi.y << 32) | hi.x);
-    m.a2 = (int64_t)(((uint64_t)hi.w << 32) | hi.z);
-    const ReplyRecord r = run_handler(m, state, n_state, delay_ticks);
-    failed += r.status != kStatusOk;
-    rp[1 + s] = r;
+    m.actor = wv[0];
+    m.method = (uint16_t)(MC ? (wv[1] & 0xffffu) : (h.w & 0xffffu));
+    m.flags = kFlagValid | kFlagRouted;
+    constexpr int o = 1 + (MC ? 1 : 0);
+    m.a0 = (int64_t)(((uint64_t)wv[o + 1] << 32) | wv[o]);
+    m.a1 = 0;
+    m.a2 = 0;
+    if constexpr (NARGS > 1) m.a1 = (int64_t)(((uint64_t)wv[o + 3] << 32) | wv[o + 2]);
+    if constexpr (NARGS > 2) m.a2 = (int64_t)(((uint64_t)wv[o + 5] << 32) | wv[o + 4]);
+    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks);
+    failed += rr.status != kStatusOk;
+    vals[s] = rr.value;
+    sts[s] = (uint8_t)rr.status;
   }
   for (int off = 32; off > 0; off >>= 1) failed += __shfl_xor(failed, off);
   if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);
 }
 
 // K8: replies back to message order (SoA outputs).
-__global__ __launch_bounds__(256) void complete_kernel(const ReplyRecord* __restrict__ rep,
-                                                       const int32_t* __restrict__ perm, int64_t M,
+__global__ __launch_bounds__(256) void complete_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
+                                                       uint32_t C, const int32_t* __restrict__ perm, int64_t M,
                                                        int64_t* __restrict__ out_val, int32_t* __restrict__ out_st,
                                                        unsigned long long* __restrict__ checksum) {
   unsigned long long sum = 0;
@@ -372,9 +380,10 @@ __global__ __launch_bounds__(256) void complete_kernel(const ReplyRecord* __rest
     int64_t v = 0;
     int32_t st;
     if (p >= 0) {
-      const uint4 r = *reinterpret_cast<const uint4*>(rep + p);
-      v = (int64_t)(((uint64_t)r.y << 32) | r.x);
-      st = (int32_t)r.z;
+      const uint32_t d = (uint32_t)p / C, pos = (uint32_t)p - d * C;
+      const uint32_t* rb = rep + (int64_t)d * rep_words;
+      v = reinterpret_cast<const int64_t*>(rb + 4)[pos];
+      st = reinterpret_cast<const uint8_t*>(rb + 4 + 2 * (int64_t)C)[pos];
     } else {
       st = p == -1 ? kStatusOverflow : kStatusNoActor;
     }
@@ -433,13 +442,40 @@ static void launch_prep(dim3 g, hipStream_t s, uintptr_t actor, int64_t M, int64
                      (uint32_t*)hist);
 }
 
-void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
-                  int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
-                  int64_t C, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist, uintptr_t stats,
-                  int rank_self, uintptr_t stream) {
+// Region sizes of wire format v2 (u32 words; see the header comment).
+int64_t wire_req_words(int64_t C, int nargs, bool mc) {
+  const int64_t w = 4 + C * (1 + (mc ? 1 : 0) + 2 * nargs);
+  return (w + 3) & ~3ll;
+}
+int64_t wire_rep_words(int64_t C) {
+  const int64_t w = 4 + 2 * C + (C + 3) / 4;
+  return (w + 3) & ~3ll;
+}
+
+static void check_format(int nargs, int64_t C, int R) {
+  if (nargs < 1 || nargs > 3) throw std::invalid_argument("wire format: 1 <= nargs <= 3");
   if (R < 1 || R > kMaxRanks) throw std::invalid_argument("route: 1 <= R <= 64");
   if (C < 1 || C >= (1ll << 31) / R) throw std::invalid_argument("route: bad capacity");
+}
+
+#define PT_FORMAT_SWITCH(nargs, mc, F) \
+  switch ((nargs) * 2 + ((mc) ? 1 : 0)) { \
+    case 2: F(1, false); break;          \
+    case 3: F(1, true); break;           \
+    case 4: F(2, false); break;          \
+    case 5: F(2, true); break;           \
+    case 6: F(3, false); break;          \
+    default: F(3, true); break;          \
+  }
+
+void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                  int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
+                  int64_t C, int nargs, bool mc, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist,
+                  uintptr_t stats, int rank_self, uintptr_t stream) {
+  check_format(nargs, C, R);
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
+  if (method_col && !mc) throw std::invalid_argument("route: method column needs a method-column wire format");
+  const int64_t req_words = wire_req_words(C, nargs, mc);
   int64_t P;
   const int64_t G = route_grid(M, &P);
   hipStream_t s = as_stream(stream);
@@ -457,34 +493,46 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
       else if (k == 4) launch_prep<4, false>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
       else launch_prep<2, false>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
     }
-  } else
+  } else {
     PT_HIP_CHECK(hipMemsetAsync((void*)hist, 0, sizeof(uint32_t) * (R + 1) * G, s));
-  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, s, (uint32_t*)hist, (int)G, R, C, (MsgRecord*)sendbuf,
-                     (unsigned long long*)stats, rank_self);
-  if (M > 0)
-    hipLaunchKernelGGL(route_scatter_kernel, dim3((unsigned)G), dim3(kRouteThreads), 0, s, (const uint32_t*)route,
-                       (const uint32_t*)actor, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,
-                       (const uint16_t*)method_col, (uint32_t)method_uniform, M, P, R, C, (const uint32_t*)hist,
-                       (MsgRecord*)sendbuf, (int32_t*)perm);
+  }
+  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, s, (uint32_t*)hist, (int)G, R, C, (uint32_t*)sendbuf,
+                     req_words, (uint32_t)method_uniform, (unsigned long long*)stats, rank_self);
+  if (M > 0) {
+#define PT_SCATTER(NA, MCV)                                                                                         \
+  hipLaunchKernelGGL((route_scatter_kernel<NA, MCV>), dim3((unsigned)G), dim3(kRouteThreads), 0, s,                  \
+                     (const uint32_t*)route, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,             \
+                     (const uint16_t*)method_col, (uint32_t)method_uniform, M, P, R, C, (const uint32_t*)hist,      \
+                     (uint32_t*)sendbuf, req_words, (int32_t*)perm)
+    PT_FORMAT_SWITCH(nargs, mc, PT_SCATTER)
+#undef PT_SCATTER
+  }
   PT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_dispatch(uintptr_t recv, int R, int64_t C, uintptr_t reply, uintptr_t state, uint32_t n_state,
-                     uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank, uintptr_t stream) {
-  if (R < 1) throw std::invalid_argument("dispatch: R >= 1");
+void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintptr_t reply, uintptr_t state,
+                     uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
+                     uintptr_t stream) {
+  check_format(nargs, C, R);
   const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
   const unsigned gx = grid_cap(per, 256, (unsigned)(4096 / R > 0 ? 4096 / R : 1));
-  hipLaunchKernelGGL(dispatch_kernel, dim3(gx, R), dim3(256), 0, as_stream(stream), (const MsgRecord*)recv, C,
-                     (ReplyRecord*)reply, (int64_t*)state, n_state, delay_ticks, (unsigned long long*)stats);
+  const int64_t req_words = wire_req_words(C, nargs, mc), rep_words = wire_rep_words(C);
+#define PT_DISPATCH(NA, MCV)                                                                                    \
+  hipLaunchKernelGGL((dispatch_kernel<NA, MCV>), dim3(gx, R), dim3(256), 0, as_stream(stream),                  \
+                     (const uint32_t*)recv, req_words, C, (uint32_t*)reply, rep_words, (int64_t*)state, n_state, \
+                     delay_ticks, (unsigned long long*)stats)
+  PT_FORMAT_SWITCH(nargs, mc, PT_DISPATCH)
+#undef PT_DISPATCH
   PT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_complete(uintptr_t rep, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
+void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
                      uintptr_t checksum, uintptr_t stream) {
   if (M <= 0) return;
+  if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
   hipLaunchKernelGGL(complete_kernel, dim3(grid_cap(M, 256, checksum ? 1024 : 8192)), dim3(256), 0,
-                     as_stream(stream), (const ReplyRecord*)rep, (const int32_t*)perm, M, (int64_t*)out_val,
-                     (int32_t*)out_st, (unsigned long long*)checksum);
+                     as_stream(stream), (const uint32_t*)rep, wire_rep_words(C), (uint32_t)C, (const int32_t*)perm, M,
+                     (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum);
   PT_HIP_CHECK(hipGetLastError());
 }
 

@@ -22,12 +22,15 @@ void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uin
 void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t);
 int64_t route_grid(int64_t, int64_t*);
 void launch_route(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t, uintptr_t,
-                  uint32_t, int, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, uintptr_t);
+                  uint32_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
+                  uintptr_t);
 void set_route_tuning(int);
 void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t);
-void launch_dispatch(uintptr_t, int, int64_t, uintptr_t, uintptr_t, uint32_t, uint64_t, uintptr_t, int64_t,
+void launch_dispatch(uintptr_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uint32_t, uint64_t, uintptr_t, int64_t,
                      uintptr_t);
-void launch_complete(uintptr_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+int64_t wire_req_words(int64_t, int, bool);
+int64_t wire_rep_words(int64_t);
 void launch_snapshot_copy(uintptr_t, uintptr_t, int64_t, uintptr_t);
 }  // namespace ptype
 
@@ -84,17 +87,20 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("route", &launch_route, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"),
         py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
-        py::arg("dir"), py::arg("n_dir"), py::arg("R"), py::arg("C"), py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"),
-        py::arg("stats"), py::arg("rank_self"), py::arg("stream"));
+        py::arg("dir"), py::arg("n_dir"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
+        py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"), py::arg("stats"),
+        py::arg("rank_self"), py::arg("stream"));
+  m.def("wire_req_words", &wire_req_words, py::arg("C"), py::arg("nargs"), py::arg("mc"));
+  m.def("wire_rep_words", &wire_rep_words, py::arg("C"));
   m.def("set_route_tuning", &set_route_tuning, py::arg("prep_items"),
         "route_prep items per thread (1, 2, 4; 0 = default) -- a tuning knob for experiments");
   m.def("table_build_dir", &launch_table_build_dir, py::arg("table"), py::arg("cap"), py::arg("dir"),
         py::arg("n_dir"), py::arg("stream"));
-  m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("reply"),
-        py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),
+  m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
+        py::arg("reply"), py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),
         py::arg("expected_per_rank"), py::arg("stream"));
-  m.def("complete", &launch_complete, py::arg("rep"), py::arg("perm"), py::arg("M"), py::arg("out_val"),
-        py::arg("out_status"), py::arg("checksum"), py::arg("stream"));
+  m.def("complete", &launch_complete, py::arg("rep"), py::arg("C"), py::arg("perm"), py::arg("M"),
+        py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("stream"));
   m.def("snapshot_copy", &launch_snapshot_copy, py::arg("dst"), py::arg("src"), py::arg("n16"),
         py::arg("stream"));
 

@@ -12,8 +12,7 @@ import numpy as np
 import torch
 
 from . import _check, _ptr, _stream, hip
-from .records import (FLAG_ROUTED, FLAG_VALID, METHOD_CALC_MULTIPLY, STATUS_NO_ACTOR, STATUS_OVERFLOW,
-                      make_requests, split_requests)
+from .records import FLAG_VALID, METHOD_CALC_MULTIPLY, STATUS_NO_ACTOR, STATUS_OVERFLOW, make_requests, split_requests
 from .table import RegistryTable, actor_keys, mix64
 
 # workspace words (int64): [0:4) stats [nomatch, overflow, failed, -]
@@ -105,6 +104,40 @@ def gen_requests(M: int, n_actors: int, method: int = METHOD_CALC_MULTIPLY, seed
     return out
 
 
+@dataclass(frozen=True)
+class WireFormat:
+    """Epoch wire format v2 (see csrc/hip/batch.hip): which payload columns a
+    record carries.  ``nargs`` int64 args (1..3) and, with ``method_col``, a
+    per-record method word; otherwise the method is uniform per slot (header).
+    A calculator call (uniform Multiply, A, B) is 5 words = 20 B on the wire."""
+
+    nargs: int = 3
+    method_col: bool = True
+
+    @property
+    def stride(self) -> int:
+        return 1 + int(self.method_col) + 2 * self.nargs
+
+    def req_words(self, C: int) -> int:
+        return (4 + C * self.stride + 3) & ~3
+
+    @staticmethod
+    def rep_words(C: int) -> int:
+        return (4 + 2 * C + (C + 3) // 4 + 3) & ~3
+
+    @staticmethod
+    def for_batch(batch: "MsgBatch") -> "WireFormat":
+        nargs = 3 if batch.a2 is not None else 2 if batch.a1 is not None else 1
+        return WireFormat(nargs, not isinstance(batch.method, int))
+
+    def admits(self, batch: "MsgBatch") -> bool:
+        need = WireFormat.for_batch(batch)
+        return need.nargs <= self.nargs and (self.method_col or not need.method_col)
+
+
+FULL_FORMAT = WireFormat(3, True)  # 32-B records: any batch fits
+
+
 class RouteWorkspace:
     """Per-epoch scratch of the route kernels (route words + block histograms)."""
 
@@ -119,30 +152,37 @@ class RouteWorkspace:
 
 def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int = 0,
           sendbuf: torch.Tensor | None = None, perm: torch.Tensor | None = None,
-          rws: RouteWorkspace | None = None):
+          rws: RouteWorkspace | None = None, fmt: WireFormat = FULL_FORMAT):
     """K1: resolve each message's actor in the GPU registry and place it, in
-    message order, into its destination rank's epoch slot as a 32-B wire record.
+    message order, into its destination rank's epoch slot (wire format ``fmt``).
 
-    Returns ``(sendbuf int64[R*(C+1), 4], perm int32[M], stats int64[4])``.
+    Returns ``(sendbuf int32[R * fmt.req_words(C)], perm int32[M], stats int64[4])``;
+    ``perm[i] = d * C + pos`` (-1 overflow, -2 no actor).
     """
     M = batch.M
     dev = batch.device
     if batch.actor.dtype != torch.int32 or batch.a0.dtype != torch.int64:
         raise TypeError("MsgBatch: actor must be int32 and a0..a2 int64")
+    if not fmt.admits(batch):
+        raise ValueError(f"batch columns do not fit wire format {fmt}")
+    W = fmt.req_words(C)
     if sendbuf is None:
-        sendbuf = torch.empty(R * (C + 1), 4, dtype=torch.int64, device=dev)
+        sendbuf = torch.empty(R * W, dtype=torch.int32, device=dev)
+    _check(sendbuf, torch.int32, 1, "sendbuf")
+    if sendbuf.numel() < R * W:
+        raise ValueError("sendbuf too small for R x req_words(C)")
     if perm is None:
         perm = torch.empty(M, dtype=torch.int32, device=dev)
     if rws is None or rws.M < M or rws.R != R:
         rws = RouteWorkspace(M, R, dev)
     rws.ws.zero_()
     uniform = isinstance(batch.method, int)
+    method_u = int(batch.method) if uniform else 0
     if dev.type == "cuda":
         mcol = None if uniform else batch.method.to(torch.int16).contiguous()
         d, n_dir = table.directory()
-        hip().route(_ptr(batch.actor), _ptr(batch.a0), _ptr(batch.a1), _ptr(batch.a2), _ptr(mcol),
-                    int(batch.method) if uniform else 0, M, _ptr(table.table), table.cap, _ptr(d), n_dir, R, C,
-                    _ptr(sendbuf),
+        hip().route(_ptr(batch.actor), _ptr(batch.a0), _ptr(batch.a1), _ptr(batch.a2), _ptr(mcol), method_u, M,
+                    _ptr(table.table), table.cap, _ptr(d), n_dir, R, C, fmt.nargs, fmt.method_col, _ptr(sendbuf),
                     _ptr(perm), _ptr(rws.route), _ptr(rws.hist), _ptr(rws.ws), rank_self, _stream(batch.actor))
         return sendbuf, perm, ws_stats(rws.ws)
     # ---- CPU reference: bit-identical layout (stable message order per destination) ----
@@ -151,28 +191,40 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
     rank = rank.to(torch.int64)
     mbox = mbox.to(torch.int64)
     ok = (rank >= 0) & (rank < R) & (mbox < MAX_MBOX)
-    method = torch.full((M,), int(batch.method), dtype=torch.int64) if uniform else batch.method.to(torch.int64)
+    cols = [mbox & 0xFFFFFFFF]
+    if fmt.method_col:
+        method = torch.full((M,), method_u, dtype=torch.int64) if uniform else batch.method.to(torch.int64)
+        cols.append(method & 0xFFFF)
     z = torch.zeros(M, dtype=torch.int64)
-    a1 = z if batch.a1 is None else batch.a1
-    a2 = z if batch.a2 is None else batch.a2
-    w0 = (mbox & 0xFFFFFFFF) | ((method & 0xFFFF) << 32) | ((FLAG_VALID | FLAG_ROUTED) << 48)
-    routed = torch.stack([w0, batch.a0, a1, a2], dim=1)
+    for a in [batch.a0, batch.a1, batch.a2][: fmt.nargs]:
+        a = z if a is None else a
+        cols += [a & 0xFFFFFFFF, (a >> 32) & 0xFFFFFFFF]
+    words = _u32(torch.stack(cols, dim=1))  # [M, stride] int32
     perm.fill_(-2)
     overflow = 0
     for d in range(R):
         idx = torch.nonzero(ok & (rank == d)).flatten()
         n = idx.numel()
         k = min(n, C)
-        slot = d * (C + 1) + 1 + torch.arange(k, dtype=torch.int64)
-        sendbuf[slot] = routed[idx[:k]]
-        perm[idx[:k]] = slot.to(torch.int32)
+        region = sendbuf[d * W:(d + 1) * W]
+        region[4:4 + k * fmt.stride] = words[idx[:k]].reshape(-1)
+        perm[idx[:k]] = (d * C + torch.arange(k, dtype=torch.int64)).to(torch.int32)
         perm[idx[k:]] = -1
         overflow += n - k
-        sendbuf[d * (C + 1)] = torch.tensor([k | (n << 32), rank_self | ((FLAG_VALID << 16) << 32), 0, 0])
+        region[:4] = _u32(torch.tensor([k, n, rank_self, (FLAG_VALID << 16) | (method_u & 0xFFFF)]))
     st = ws_stats(rws.ws)
     st[STAT_NOMATCH] = int((~ok).sum())
     st[STAT_OVERFLOW] = overflow
     return sendbuf, perm, st
+
+
+def _u32(x: torch.Tensor) -> torch.Tensor:
+    """int64 values in [0, 2^32) -> the same bits as int32."""
+    return torch.from_numpy(x.numpy().astype(np.uint32).view(np.int32))
+
+
+def _words_i64(lo: torch.Tensor, hi: torch.Tensor) -> torch.Tensor:
+    return (lo.to(torch.int64) & 0xFFFFFFFF) | (hi.to(torch.int64) << 32)
 
 
 def _handler_ref(method, actor, a0, a1, a2, state):
@@ -217,58 +269,69 @@ def _handler_ref(method, actor, a0, a1, a2, state):
 
 
 def dispatch(recv: torch.Tensor, R: int, C: int, state: torch.Tensor | None = None, delay_us: int = 0,
-             reply: torch.Tensor | None = None, ws: torch.Tensor | None = None, expected_per_rank: int = 0):
+             reply: torch.Tensor | None = None, ws: torch.Tensor | None = None, expected_per_rank: int = 0,
+             fmt: WireFormat = FULL_FORMAT):
     """K3 (batch form): run every delivered record through the handler table.
 
-    ``recv`` is ``int64[R*(C+1), 4]`` epoch slots (one per source rank); returns
-    replies ``int64[R*(C+1), 2]`` in the same geometry.
+    ``recv`` is ``int32[R * fmt.req_words(C)]`` (one request region per source
+    rank); returns ``int32[R * rep_words(C)]`` reply regions (header, int64
+    values, u8 statuses) in the same geometry.
     """
-    _check(recv, torch.int64, 2, "recv")
+    _check(recv, torch.int32, 1, "recv")
     dev = recv.device
+    W, Wr = fmt.req_words(C), WireFormat.rep_words(C)
     if reply is None:
-        reply = torch.empty(R * (C + 1), 2, dtype=torch.int64, device=dev)
+        reply = torch.empty(R * Wr, dtype=torch.int32, device=dev)
     if dev.type == "cuda":
         if ws is None:
             ws = new_workspace(dev)
         n_state = 0 if state is None else state.numel()
-        hip().dispatch(_ptr(recv), R, C, _ptr(reply), _ptr(state), n_state, int(delay_us) * 100, _ptr(ws),
-                       int(expected_per_rank), _stream(recv))
+        hip().dispatch(_ptr(recv), R, C, fmt.nargs, fmt.method_col, _ptr(reply), _ptr(state), n_state,
+                       int(delay_us) * 100, _ptr(ws), int(expected_per_rank), _stream(recv))
         return reply
-    from .records import make_replies
     reply.zero_()
     for d in range(R):
-        h = recv[d * (C + 1)]
-        valid = ((int(h[1]) >> 48) & FLAG_VALID) != 0
-        cnt = min(int(h[0]) & 0xFFFFFFFF, C) if valid else 0
-        reply[d * (C + 1), 0] = cnt
-        reply[d * (C + 1), 1] = cnt << 32
+        region = recv[d * W:(d + 1) * W]
+        h = region[:4].to(torch.int64) & 0xFFFFFFFF
+        valid = ((int(h[3]) >> 16) & FLAG_VALID) != 0
+        cnt = min(int(h[0]), C) if valid else 0
+        rr = reply[d * Wr:(d + 1) * Wr]
+        rr[0] = cnt
         if cnt == 0:
             continue
-        lo = d * (C + 1) + 1
-        rows = recv[lo:lo + cnt]
-        w0 = rows[:, 0]
-        actor = w0 & 0xFFFFFFFF
-        method = (w0 >> 32) & 0xFFFF
-        v, stt = _handler_ref(method, actor, rows[:, 1], rows[:, 2], rows[:, 3], state)
-        reply[lo:lo + cnt] = make_replies(v, stt, actor)
+        rows = region[4:4 + cnt * fmt.stride].reshape(cnt, fmt.stride)
+        actor = rows[:, 0].to(torch.int64) & 0xFFFFFFFF
+        o = 1 + int(fmt.method_col)
+        method = (rows[:, 1].to(torch.int64) & 0xFFFF) if fmt.method_col else torch.full((cnt,), int(h[3]) & 0xFFFF)
+        args = [_words_i64(rows[:, o + 2 * j], rows[:, o + 2 * j + 1]) for j in range(fmt.nargs)]
+        args += [torch.zeros(cnt, dtype=torch.int64)] * (3 - fmt.nargs)
+        v, stt = _handler_ref(method, actor, args[0], args[1], args[2], state)
+        rr[4:4 + 2 * C].view(torch.int64)[:cnt] = v
+        rr[4 + 2 * C:].view(torch.uint8)[:cnt] = stt.to(torch.uint8)
     return reply
 
 
-def complete(reply: torch.Tensor, perm: torch.Tensor, out_val: torch.Tensor | None = None,
+def complete(reply: torch.Tensor, perm: torch.Tensor, C: int, out_val: torch.Tensor | None = None,
              out_status: torch.Tensor | None = None, checksum: torch.Tensor | None = None):
-    """K8: ``value[i], status[i] = reply[perm[i]]`` (overflow/no-actor statuses for perm < 0)."""
+    """K8: ``value[i], status[i]`` = the reply at ``perm[i] = d * C + pos`` (overflow /
+    no-actor statuses for perm < 0)."""
     M = perm.numel()
     dev = perm.device
     out_val = torch.empty(M, dtype=torch.int64, device=dev) if out_val is None else out_val
     out_status = torch.empty(M, dtype=torch.int32, device=dev) if out_status is None else out_status
     if dev.type == "cuda":
-        hip().complete(_ptr(reply), _ptr(perm), M, _ptr(out_val), _ptr(out_status), _ptr(checksum), _stream(perm))
+        hip().complete(_ptr(reply), C, _ptr(perm), M, _ptr(out_val), _ptr(out_status), _ptr(checksum), _stream(perm))
         return out_val, out_status
+    Wr = WireFormat.rep_words(C)
+    R = reply.numel() // Wr
+    regions = reply[:R * Wr].reshape(R, Wr)
+    vals = regions[:, 4:4 + 2 * C].contiguous().view(torch.int64).reshape(-1)  # [R*C]
+    sts = regions[:, 4 + 2 * C:].contiguous().view(torch.uint8)[:, :C].reshape(-1)
     p = perm.to(torch.int64)
     ok = p >= 0
     out_val.zero_()
-    out_val[ok] = reply[p[ok], 0]
-    st = reply[p.clamp(min=0), 1] & 0xFFFFFFFF
+    out_val[ok] = vals[p[ok]]
+    st = sts[p.clamp(min=0)].to(torch.int64)
     st = torch.where(p == -1, torch.full_like(st, STATUS_OVERFLOW), st)
     st = torch.where(p == -2, torch.full_like(st, STATUS_NO_ACTOR), st)
     out_status.copy_(st.to(torch.int32))

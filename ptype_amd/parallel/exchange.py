@@ -4,11 +4,17 @@ One process per GPU; every rank is both a client (it sends messages to actors
 anywhere in the node) and a server (it hosts a shard of the actors).  The
 reference moves each call over its own TCP connection (cluster/rpc.go:272-285,
 `rpc.DialHTTP`; calls at :65 and :88).  Here traffic moves in *epochs*: each
-rank buckets its outbound records by destination GPU (K1, LDS-staged counting
-sort), one RCCL all-to-all moves every bucket at once over all 7 xGMI links,
-the receiver runs the handler table over what it got (K3), a second all-to-all
-returns the 16-B replies into the exact slots the requests left from, and K8
-scatters them back to message order.
+rank buckets its outbound records by destination GPU (K1, deterministic
+counting sort), one RCCL all-to-all moves every bucket at once over all 7 xGMI
+links, the receiver runs the handler table over what it got (K3), a second
+all-to-all returns the replies (8-B value + 1-B status) into the exact slots the
+requests left from, and K8 scatters them back to message order.
+
+Wire volume is what bounds an epoch on xGMI, so records carry only the columns
+the batch has (``WireFormat``): a calculator call is 20 B, not a 32-B record.
+Every rank must send batches with the same columns in the same call (the
+all-to-all is equal-split over the format's slot size), or fix the format at
+construction with ``fmt=``.
 
 Fixed-capacity slots (``C + 1`` records per peer, slot 0 a header with the
 count) make both all-to-alls equal-split: no host round trip for sizes, so an
@@ -50,11 +56,13 @@ class EpochStats:
 
 
 class _ChunkBufs:
-    def __init__(self, R, C, M, device, separate=False):
+    """Slot buffers of one in-flight chunk, sized for the widest wire format."""
+
+    def __init__(self, R, C, M, device, separate=False, fmt: B.WireFormat = B.FULL_FORMAT):
         sep = R > 1 or separate
-        self.send = torch.empty(R * (C + 1), 4, dtype=torch.int64, device=device)
+        self.send = torch.empty(R * fmt.req_words(C), dtype=torch.int32, device=device)
         self.recv = torch.empty_like(self.send) if sep else self.send
-        self.reply = torch.empty(R * (C + 1), 2, dtype=torch.int64, device=device)
+        self.reply = torch.empty(R * B.WireFormat.rep_words(C), dtype=torch.int32, device=device)
         self.back = torch.empty_like(self.reply) if sep else self.reply
         self.perm = torch.empty(M, dtype=torch.int32, device=device)
         self.rws = B.RouteWorkspace(M, R, device)
@@ -69,7 +77,7 @@ class ActorExchange:
     """
 
     def __init__(self, table: RegistryTable, max_batch: int, chunks: int = 1, group=None, state=None,
-                 delay_us: int = 0, slack: float = 0.06):
+                 delay_us: int = 0, slack: float = 0.06, fmt: B.WireFormat | None = None):
         self.table = table
         self.device = table.device
         self.group = group
@@ -92,8 +100,9 @@ class ActorExchange:
         self.C = capacity_for(self.max_chunk, self.world, slack)
         self.state = state
         self.delay_us = delay_us
-        self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device, self.force_collectives)
-                     for _ in range(min(self.chunks, 2))]
+        self.fmt = fmt  # None: derived per send() from the batch's columns
+        self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device, self.force_collectives,
+                                fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 2))]
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
 
     # ------------------------------------------------------------------
@@ -116,6 +125,10 @@ class ActorExchange:
         n = self.chunks
         bounds = [min(M, i * self.max_chunk) for i in range(n + 1)]
         R, C = self.world, self.C
+        fmt = self.fmt or B.WireFormat.for_batch(req)
+        if not fmt.admits(req):
+            raise ValueError(f"batch columns do not fit the exchange's wire format {fmt}")
+        wq, wr = R * fmt.req_words(C), R * B.WireFormat.rep_words(C)
         pending_bwd = []  # (chunk index, work handle, bufs)
 
         def finish(entry):
@@ -123,7 +136,7 @@ class ActorExchange:
             if work is not None:
                 work.wait()
             lo, hi = bounds[i], bounds[i + 1]
-            B.complete(bufs.back, bufs.perm[: hi - lo], out_val[lo:hi], out_status[lo:hi], self.checksum)
+            B.complete(bufs.back[:wr], bufs.perm[: hi - lo], C, out_val[lo:hi], out_status[lo:hi], self.checksum)
 
         fwd = None
         for i in range(n):
@@ -132,24 +145,25 @@ class ActorExchange:
             # buffer reuse: chunk i-2's replies must be consumed before overwriting
             while pending_bwd and pending_bwd[0][0] <= i - len(self.bufs):
                 finish(pending_bwd.pop(0))
-            B.route(req.slice(lo, hi), self.table, R, C, self.rank, sendbuf=bufs.send, perm=bufs.perm[: hi - lo],
-                    rws=bufs.rws)
-            work = self._a2a(bufs.recv, bufs.send)
+            B.route(req.slice(lo, hi), self.table, R, C, self.rank, sendbuf=bufs.send[:wq],
+                    perm=bufs.perm[: hi - lo], rws=bufs.rws, fmt=fmt)
+            work = self._a2a(bufs.recv[:wq], bufs.send[:wq])
             if fwd is not None:
-                pending_bwd.append(self._serve(*fwd))
+                pending_bwd.append(self._serve(*fwd, fmt))
             fwd = (i, work, bufs, hi - lo)
         if fwd is not None:
-            pending_bwd.append(self._serve(*fwd))
+            pending_bwd.append(self._serve(*fwd, fmt))
         for e in pending_bwd:
             finish(e)
         return out_val, out_status
 
-    def _serve(self, i, work, bufs, m):
+    def _serve(self, i, work, bufs, m, fmt):
         if work is not None:
             work.wait()
-        B.dispatch(bufs.recv, self.world, self.C, self.state, self.delay_us, reply=bufs.reply, ws=bufs.ws,
-                   expected_per_rank=max(1, m // self.world))
-        return (i, self._a2a(bufs.back, bufs.reply), bufs)
+        wq, wr = self.world * fmt.req_words(self.C), self.world * B.WireFormat.rep_words(self.C)
+        B.dispatch(bufs.recv[:wq], self.world, self.C, self.state, self.delay_us, reply=bufs.reply[:wr], ws=bufs.ws,
+                   expected_per_rank=max(1, m // self.world), fmt=fmt)
+        return (i, self._a2a(bufs.back[:wr], bufs.reply[:wr]), bufs)
 
     # ------------------------------------------------------------------
     def send_all(self, req: B.MsgBatch, max_epochs: int = 16):

@@ -57,19 +57,68 @@ def _batch(actors, method, a0, a1=None, a2=None):
     return B.MsgBatch(torch.as_tensor(actors, dtype=torch.int32), t(a0), t(a1), t(a2), m)
 
 
-def test_batch_reference_end_to_end():
+def _regions_equal(g, c, R, C, fmt):
+    """Compare two request buffers on their defined words: headers + delivered records."""
+    W = fmt.req_words(C)
+    g, c = g.cpu(), c.cpu()
+    for d in range(R):
+        k = int(c[d * W])
+        n = 4 + k * fmt.stride
+        if not torch.equal(g[d * W:d * W + n], c[d * W:d * W + n]):
+            return False
+    return True
+
+
+def _replies_equal(g, c, R, C):
+    Wr = B.WireFormat.rep_words(C)
+    g, c = g.cpu(), c.cpu()
+    for d in range(R):
+        k = int(c[d * Wr])
+        gr, cr = g[d * Wr:(d + 1) * Wr], c[d * Wr:(d + 1) * Wr]
+        if int(gr[0]) != k or not torch.equal(gr[4:4 + 2 * k], cr[4:4 + 2 * k]):
+            return False
+        if not torch.equal(gr[4 + 2 * C:].view(torch.uint8)[:k], cr[4 + 2 * C:].view(torch.uint8)[:k]):
+            return False
+    return True
+
+
+@pytest.mark.parametrize("fmt", [B.FULL_FORMAT, B.WireFormat(2, False)])
+def test_batch_reference_end_to_end(fmt):
     R, C = 3, 64
     t = RegistryTable(64, device="cpu")
     _populate(t, 12, R)
     req = _batch([0, 1, 2, 3, 4, 99], METHOD_CALC_MULTIPLY, [7, 2, 3, 4, 5, 6], [8, 3, 4, 5, 6, 7])
-    send, perm, stats = B.route(req, t, R, C)
-    hdr = send[0::C + 1, 0]
-    assert (hdr & 0xFFFFFFFF).tolist() == [2, 2, 1]
+    send, perm, stats = B.route(req, t, R, C, fmt=fmt)
+    W = fmt.req_words(C)
+    assert send[0::W][:R].tolist() == [2, 2, 1]
     assert int(stats[B.STAT_NOMATCH]) == 1
-    rep = B.dispatch(send, R, C)
-    val, st = B.complete(rep, perm)
+    rep = B.dispatch(send, R, C, fmt=fmt)
+    val, st = B.complete(rep, perm, C)
     assert val.tolist()[:5] == [56, 6, 12, 20, 30]
     assert st.tolist() == [STATUS_OK] * 5 + [STATUS_NO_ACTOR]
+
+
+def test_wire_format_v2_layout():
+    """Pin the v2 wire layout by hand: a calculator call is 5 words (20 B) with
+    the uniform method in the slot header; replies are planar (i64 value + u8 status)."""
+    fmt = B.WireFormat(2, False)
+    assert fmt.stride == 5 and B.FULL_FORMAT.stride == 8 and B.WireFormat(3, False).stride == 7
+    assert fmt.req_words(3) == 20 and B.WireFormat.rep_words(3) == 12
+    t = RegistryTable(16, device="cpu")
+    _populate(t, 4, 2)  # actor a -> rank a % 2, mbox a // 2
+    req = _batch([3, 1, 2], METHOD_CALC_MULTIPLY, [-1, 5, 6], [1 << 33, 7, 8])
+    send, perm, _ = B.route(req, t, 2, 3, rank_self=1, fmt=fmt)
+    assert perm.tolist() == [3, 4, 0]  # d * C + pos; rank 1 gets actors 3 then 1 in message order
+    r1 = send[20:40].tolist()
+    assert r1[:4] == [2, 2, 1, (1 << 16) | METHOD_CALC_MULTIPLY]
+    assert r1[4:9] == [1, -1, -1, 0, 2]  # mbox 1, a0 = -1 (lo, hi), a1 = 2^33 (lo 0, hi 2)
+    rep = B.dispatch(send, 2, 3, fmt=fmt)
+    assert rep.numel() == 2 * 12 and int(rep[12]) == 2
+    assert rep[12 + 4:12 + 10].view(torch.int64)[:2].tolist() == [-(1 << 33), 35]
+    val, st = B.complete(rep, perm, 3)
+    assert val.tolist() == [-(1 << 33), 35, 48] and st.tolist() == [STATUS_OK] * 3
+    with pytest.raises(ValueError):
+        B.route(_batch([0], METHOD_ECHO, [1], [2], [3]), t, 2, 3, fmt=fmt)  # a2 does not fit
 
 
 def test_batch_reference_overflow_and_handlers():
@@ -81,7 +130,7 @@ def test_batch_reference_overflow_and_handlers():
     req = _batch([0, 1] + [0] * 8, methods, [5, 2] + list(range(8)), [0, 10] + [0] * 8, [0, 21] + [0] * 8)
     send, perm, stats = B.route(req, t, R, C)
     rep = B.dispatch(send, R, C, state=state)
-    val, st = B.complete(rep, perm)
+    val, st = B.complete(rep, perm, C)
     assert val.tolist()[:8] == [5, 3, 0, 1, 2, 3, 4, 5]  # counter 0+5, 21 = 3*7 -> first divisor 3
     assert st.tolist() == [STATUS_OK] * 8 + [STATUS_OVERFLOW] * 2
     assert int(stats[B.STAT_OVERFLOW]) == 2
@@ -159,8 +208,9 @@ def test_gpu_table_sweep_and_snapshot():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("R", [1, 2, 8])
-def test_gpu_route_dispatch_complete(R):
+@pytest.mark.parametrize("R,fmt", [(1, B.FULL_FORMAT), (2, B.WireFormat(2, False)), (8, B.WireFormat(2, False)),
+                                   (8, B.WireFormat(3, True)), (3, B.WireFormat(2, True))])
+def test_gpu_route_dispatch_complete(R, fmt):
     M, n_actors = 200_003, 4096
     C = B.stripe_capacity(M, R)
     g = RegistryTable(2 * n_actors, device="cuda")
@@ -171,19 +221,16 @@ def test_gpu_route_dispatch_complete(R):
     ref = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=1234, device="cpu")
     assert torch.equal(req.actor.cpu(), ref.actor) and torch.equal(req.a0.cpu(), ref.a0)
     assert torch.equal(req.a1.cpu(), ref.a1), "generator kernel differs from reference"
-    send, perm, stats = B.route(req, g, R, C, rank_self=0)
-    rsend, rperm, rstats = B.route(ref, c, R, C, rank_self=0)
+    send, perm, stats = B.route(req, g, R, C, rank_self=0, fmt=fmt)
+    rsend, rperm, rstats = B.route(ref, c, R, C, rank_self=0, fmt=fmt)
     # deterministic stable placement: bit-identical to the CPU reference
     assert torch.equal(perm.cpu(), rperm)
-    used = rperm.to(torch.int64)
-    hdrs = torch.arange(R) * (C + 1)
-    assert torch.equal(send.cpu()[used], rsend[used])  # every occupied slot
-    assert torch.equal(send.cpu()[hdrs], rsend[hdrs])  # per-destination headers
+    assert _regions_equal(send, rsend, R, C, fmt)
     assert stats.cpu().tolist()[:2] == rstats.tolist()[:2] == [0, 0]
-    rep = B.dispatch(send, R, C, expected_per_rank=M // R)
-    val, st = B.complete(rep, perm)
-    rrep = B.dispatch(rsend, R, C)
-    assert torch.equal(rep.cpu()[used], rrep[used]) and torch.equal(rep.cpu()[hdrs], rrep[hdrs])
+    rep = B.dispatch(send, R, C, expected_per_rank=M // R, fmt=fmt)
+    val, st = B.complete(rep, perm, C)
+    rrep = B.dispatch(rsend, R, C, fmt=fmt)
+    assert _replies_equal(rep, rrep, R, C)
     torch.cuda.synchronize()
     assert (st.cpu() == STATUS_OK).all()
     assert torch.equal(val.cpu(), ref.a0 * ref.a1)
@@ -213,8 +260,7 @@ def test_gpu_route_directory_matches_hash_probe(items):
         ops.hip().set_route_tuning(0)
     rsend, rperm, rstats = B.route(ref, c, R, C)
     assert torch.equal(perm.cpu(), rperm)
-    used = rperm[rperm >= 0].to(torch.int64)
-    assert torch.equal(send.cpu()[used], rsend[used])
+    assert _regions_equal(send, rsend, R, C, B.FULL_FORMAT)
     assert stats.cpu().tolist()[:2] == rstats.tolist()[:2]
     assert rstats.tolist()[0] > 0  # misses were exercised
     # a later mutation invalidates the directory
@@ -235,7 +281,7 @@ def test_gpu_route_overflow_and_unknown():
     req = B.MsgBatch(req.actor.cuda(), req.a0.cuda(), None, None, METHOD_ECHO)
     send, perm, stats = B.route(req, g, R, C)
     rep = B.dispatch(send, R, C)
-    val, st = B.complete(rep, perm)
+    val, st = B.complete(rep, perm, C)
     st = st.cpu()
     # stable order: the first C messages are delivered, the rest overflow to the next epoch
     assert st[:1000].eq(STATUS_OK).all() and st[1000:1500].eq(STATUS_OVERFLOW).all()
@@ -256,7 +302,7 @@ def test_gpu_stateful_handlers_match_reference():
     state = torch.zeros(4, dtype=torch.int64, device="cuda")
     send, perm, _ = B.route(req, g, R, C)
     rep = B.dispatch(send, R, C, state=state)
-    val, st = B.complete(rep, perm)
+    val, st = B.complete(rep, perm, C)
     assert state.cpu().tolist() == [250] * 4
     # per-actor values are a permutation of 1..250 (arrival order is the device's)
     v = val.cpu()
@@ -267,7 +313,7 @@ def test_gpu_stateful_handlers_match_reference():
     b = _batch(torch.zeros(5, dtype=torch.int64), METHOD_PRIME_CHECK, torch.full((5,), 2), torch.full((5,), 1 << 40), tgt)
     req = B.MsgBatch(b.actor.cuda(), b.a0.cuda(), b.a1.cuda(), b.a2.cuda(), METHOD_PRIME_CHECK)
     send, perm, _ = B.route(req, g, R, C)
-    val, st = B.complete(B.dispatch(send, R, C), perm)
+    val, st = B.complete(B.dispatch(send, R, C), perm, C)
     assert val.cpu().tolist() == [97, 7, 13, 1000003, 7]
 
 
@@ -304,3 +350,13 @@ def test_gpu_device_server_latency_path():
         print("device-server p50 RTT us", lat[len(lat) // 2] * 1e6, "p99", lat[int(len(lat) * 0.99)] * 1e6)
     finally:
         srv.close()
+
+
+def test_wire_sizes_match_kernels():
+    """The Python geometry and the launchers' must agree (the all-to-all splits on it)."""
+    h = ops.hip()
+    for C in (1, 3, 64, 1000, 123457):
+        for nargs in (1, 2, 3):
+            for mc in (False, True):
+                assert h.wire_req_words(C, nargs, mc) == B.WireFormat(nargs, mc).req_words(C)
+        assert h.wire_rep_words(C) == B.WireFormat.rep_words(C)

@@ -39,19 +39,22 @@ def main():
     p.add_argument("--msgs", type=int, default=8 << 20)
     p.add_argument("--iters", type=int, default=20)
     p.add_argument("--ranks", type=int, default=1)
+    p.add_argument("--full", action="store_true", help="32-B records (FULL_FORMAT) instead of the batch's format")
+    p.add_argument("--sizes", default="4096,131072,1048576")
     a = p.parse_args()
     M, R = a.msgs, a.ranks
     C = B.stripe_capacity(M, R)
     rows = []
-    for n_actors in (4096, 131072, 1 << 20):
+    for n_actors in [int(x) for x in a.sizes.split(",")]:
         t = RegistryTable(2 * n_actors, device="cuda")
         ids = torch.arange(n_actors, dtype=torch.int64)
         t.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
         req = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=5, device="cuda")
-        send = torch.empty(R * (C + 1), 4, dtype=torch.int64, device="cuda")
+        fmt = B.WireFormat.for_batch(req) if not a.full else B.FULL_FORMAT
+        send = torch.empty(R * fmt.req_words(C), dtype=torch.int32, device="cuda")
         perm = torch.empty(M, dtype=torch.int32, device="cuda")
         rws = B.RouteWorkspace(M, R, "cuda")
-        reply = torch.empty(R * (C + 1), 2, dtype=torch.int64, device="cuda")
+        reply = torch.empty(R * B.WireFormat.rep_words(C), dtype=torch.int32, device="cuda")
         val = torch.empty(M, dtype=torch.int64, device="cuda")
         st = torch.empty(M, dtype=torch.int32, device="cuda")
         for use_dir in (False, True):
@@ -59,15 +62,16 @@ def main():
                 t.enable_directory(n_actors)
             for items in (1, 2, 4):
                 hip().set_route_tuning(items)
-                us = timed(lambda: B.route(req, t, R, C, sendbuf=send, perm=perm, rws=rws), a.iters)
+                us = timed(lambda: B.route(req, t, R, C, sendbuf=send, perm=perm, rws=rws, fmt=fmt), a.iters)
                 rows.append({"actors": n_actors, "dir": use_dir, "items": items, "route_us": round(us, 1)})
             hip().set_route_tuning(0)
             t.dir = None
-        d_us = timed(lambda: B.dispatch(send, R, C, reply=reply, ws=rws.ws, expected_per_rank=M // R), a.iters)
-        c_us = timed(lambda: B.complete(reply, perm, val, st), a.iters)
+        d_us = timed(lambda: B.dispatch(send, R, C, reply=reply, ws=rws.ws, expected_per_rank=M // R,
+                                          fmt=fmt), a.iters)
+        c_us = timed(lambda: B.complete(reply, perm, C, val, st), a.iters)
         g_us = timed(lambda: B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=6, device="cuda", out=req),
                      a.iters)
-        rows.append({"actors": n_actors, "gen_us": round(g_us, 1), "dispatch_us": round(d_us, 1),
+        rows.append({"actors": n_actors, "ranks": R, "fmt_stride_words": fmt.stride, "gen_us": round(g_us, 1), "dispatch_us": round(d_us, 1),
                      "complete_us": round(c_us, 1)})
     for r in rows:
         print(json.dumps(r))
