@@ -208,7 +208,7 @@ std::string Context::err() const {
 }
 
 // ---------------------------------------------------------------- logging
-static std::atomic<int> g_level{(int)LogLevel::kWarn};
+static std::atomic<int> g_level{(int)LogLevel::kOff};  // zap global default: no-op
 static std::mutex g_log_mu;
 static std::deque<std::string> g_recent;
 

@@ -170,7 +170,7 @@ class Channel {
 };
 
 // ---------------------------------------------------------------- logging
-// Leveled logger with zap-like structured fields.  Off (Warn) by default, as
+// Leveled logger with zap-like structured fields.  Off by default, as
 // zap's global no-op logger is in the reference; `debug: true` in the config
 // switches it to Debug (cluster/cluster.go:29-35).
 enum class LogLevel : int { kDebug = 0, kInfo = 1, kWarn = 2, kError = 3, kOff = 4 };

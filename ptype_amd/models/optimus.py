@@ -124,7 +124,13 @@ class Coordinator:
                     target = int(form.get("target", ["0"])[0])
                 except ValueError:
                     target = 0  # strconv.Atoi error is ignored in the reference
-                body = str(check_fn(target)).encode()
+                try:
+                    body = str(check_fn(target)).encode()
+                except Exception as e:  # the reference log.Fatal()s the coordinator; answer 500 instead
+                    self.send_response(500)
+                    self.end_headers()
+                    self.wfile.write(str(e).encode())
+                    return
                 self.send_response(200)
                 self.end_headers()
                 self.wfile.write(body)
