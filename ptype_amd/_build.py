@@ -149,6 +149,48 @@ def build_hip(verbose: bool = False) -> str:
     return target
 
 
+SANITIZERS = {
+    "thread": ["-fsanitize=thread"],
+    "address": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+}
+
+
+def build_native_test(sanitize: str = "thread", verbose: bool = False) -> str:
+    """Build ``tests/native/core_stress`` -- the host control plane without
+    Python, under a sanitizer (the reference runs ``go test -race``).
+
+    The sanitizer runtime must own the process, which a Python extension cannot
+    give it, so the control-plane sources are linked into a native program.
+    Objects go to ``build/native-<sanitize>/``; returns the executable path.
+    """
+    if sanitize not in SANITIZERS:
+        raise ValueError(f"sanitize must be one of {sorted(SANITIZERS)}")
+    srcs = [s for s in sorted(glob.glob(os.path.join(CSRC, "core", "*.cpp"))) if not s.endswith("bindings.cpp")]
+    srcs.append(os.path.join(ROOT, "tests", "native", "core_stress.cpp"))
+    objdir = _variant_dir("native", sanitize)
+    hdr_t = _newest_header(os.path.join(CSRC, "core"))
+    # LLVM's sanitizer runtimes (ROCm's clang): gcc 11's libtsan lacks the
+    # pthread_cond_clockwait interceptor that libstdc++'s wait_for uses, which
+    # shows up as false "double lock" / race reports on every condition variable
+    clang = os.path.join(ROCM, "lib", "llvm", "bin", "clang++")
+    cxx = os.environ.get("PTYPE_SAN_CXX") or (clang if os.path.exists(clang) else "g++")
+    flags = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-pthread", "-Wall", "-Wno-unused-function",
+             "-I" + os.path.join(CSRC, "core")] + SANITIZERS[sanitize]
+    jobs, objs = [], []
+    for s in srcs:
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_t):
+            jobs.append([cxx] + flags + ["-c", s, "-o", o])
+    _compile_all(jobs, 8)
+    target = os.path.join(objdir, "core_stress")
+    if jobs or not os.path.exists(target) or os.path.getmtime(target) < max(os.path.getmtime(o) for o in objs):
+        _run([cxx, "-pthread", "-o", target] + objs + SANITIZERS[sanitize])
+    if verbose:
+        print("built", target, "(%d objects recompiled)" % len(jobs))
+    return target
+
+
 def build_all(verbose: bool = False) -> None:
     build_core(verbose)
     build_hip(verbose)
@@ -160,5 +202,7 @@ if __name__ == "__main__":
         build_core(True)
     elif what == "hip":
         build_hip(True)
+    elif what.startswith("native-"):
+        build_native_test(what.split("-", 1)[1], True)
     else:
         build_all(True)

@@ -8,17 +8,24 @@
 namespace ptype {
 
 // ---------------------------------------------------------------- crc32c
-uint32_t crc32c(const void* data, size_t n, uint32_t crc) {
-  static uint32_t table[256];
-  static bool init = false;
-  if (!init) {
+namespace {
+struct Crc32cTable {
+  uint32_t t[256];
+  Crc32cTable() {
     for (uint32_t i = 0; i < 256; ++i) {
       uint32_t c = i;
       for (int k = 0; k < 8; ++k) c = (c & 1) ? 0x82F63B78u ^ (c >> 1) : c >> 1;
-      table[i] = c;
+      t[i] = c;
     }
-    init = true;
   }
+};
+}  // namespace
+
+uint32_t crc32c(const void* data, size_t n, uint32_t crc) {
+  // magic static: initialised once, thread-safe (several members may start
+  // concurrently in one process; TSan flagged the old lazy flag)
+  static const Crc32cTable tab;
+  const uint32_t* table = tab.t;
   crc = ~crc;
   const unsigned char* p = (const unsigned char*)data;
   for (size_t i = 0; i < n; ++i) crc = table[(crc ^ p[i]) & 0xff] ^ (crc >> 8);

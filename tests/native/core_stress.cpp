@@ -1,0 +1,389 @@
+// Host control-plane stress program, built with -fsanitize=thread and with
+// -fsanitize=address,undefined (tests/test_sanitizers.py).
+//
+// The reference runs its whole suite under Go's race detector (`go test -race`,
+// Makefile:2).  The C++ control plane is exercised here WITHOUT Python so the
+// sanitizer runtime owns the process: concurrent channels, a 3-member Raft
+// cluster with concurrent clients, watches, leases and a leader failover, the
+// net/rpc server with a balancer-driven client under concurrent Call/Go, and
+// the Cluster facade (Join -> register -> watch -> NewClient -> Call -> Close).
+//
+// usage: core_stress <workdir> [channel|raft|rpc|api|learner ...]   (default: all)
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "api.hpp"
+#include "balancer.hpp"
+#include "config.hpp"
+#include "kvclient.hpp"
+#include "member.hpp"
+#include "netrpc.hpp"
+#include "util.hpp"
+
+using namespace ptype;
+
+namespace {
+
+int g_failures = 0;
+#define CHECK(cond)                                                                \
+  do {                                                                             \
+    if (!(cond)) {                                                                 \
+      std::fprintf(stderr, "CHECK failed at %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      ++g_failures;                                                                \
+    }                                                                              \
+  } while (0)
+
+int free_port() {
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  a.sin_port = 0;
+  ::bind(fd, (sockaddr*)&a, sizeof a);
+  socklen_t n = sizeof a;
+  ::getsockname(fd, (sockaddr*)&a, &n);
+  const int p = ntohs(a.sin_port);
+  ::close(fd);
+  return p;
+}
+
+std::string url(int port) { return "http://127.0.0.1:" + std::to_string(port); }
+
+MemberConfig member_cfg(const std::string& dir, const std::string& name, int pp, int cp, const std::string& ic) {
+  MemberConfig m;
+  m.name = name;
+  m.dir = dir + "/" + name;
+  m.lpurls = m.apurls = {url(pp)};
+  m.lcurls = m.acurls = {url(cp)};
+  m.initial_cluster = ic;
+  m.heartbeat_ms = 20;
+  m.election_ms = 200;
+  m.unsafe_no_fsync = true;
+  return m;
+}
+
+// ---------------------------------------------------------------- scenarios
+void scenario_channel() {
+  auto ch = std::make_shared<Channel<int>>(16);
+  std::atomic<long> sum{0};
+  std::vector<std::thread> prod, cons;
+  for (int p = 0; p < 4; ++p)
+    prod.emplace_back([&, p] {
+      for (int i = 1; i <= 5000; ++i) ch->send(i);
+    });
+  for (int c = 0; c < 3; ++c)
+    cons.emplace_back([&] {
+      for (;;) {
+        bool closed = false;
+        auto v = ch->recv(1000, &closed);
+        if (v) sum += *v;
+        if (closed) return;
+      }
+    });
+  for (auto& t : prod) t.join();
+  ch->close();
+  for (auto& t : cons) t.join();
+  CHECK(sum.load() == 4L * 5000 * 5001 / 2);
+  // rendezvous channel: send returns once taken
+  auto rv = std::make_shared<Channel<std::string>>(0);
+  std::thread taker([&] {
+    auto v = rv->recv(5000);
+    CHECK(v && *v == "x");
+  });
+  CHECK(rv->send("x"));
+  taker.join();
+}
+
+void scenario_raft(const std::string& dir) {
+  const int n = 3;
+  std::vector<int> pp(n), cp(n);
+  std::string ic;
+  for (int i = 0; i < n; ++i) {
+    pp[i] = free_port();
+    cp[i] = free_port();
+    ic += (i ? "," : "") + std::string("m") + std::to_string(i) + "=" + url(pp[i]);
+  }
+  std::vector<std::unique_ptr<Member>> ms;
+  for (int i = 0; i < n; ++i) ms.emplace_back(new Member(member_cfg(dir, "m" + std::to_string(i), pp[i], cp[i], ic)));
+  {
+    std::vector<std::thread> ts;
+    for (auto& m : ms) ts.emplace_back([&m] { m->start(); });
+    for (auto& t : ts) t.join();
+  }
+  for (auto& m : ms) CHECK(m->wait_ready(15000));
+
+  std::vector<std::shared_ptr<KvClient>> cli;
+  for (int i = 0; i < n; ++i) cli.push_back(std::make_shared<KvClient>(std::vector<std::string>{url(cp[i])}));
+
+  // a prefix watch counting events while writers run
+  auto ctx = Context::with_cancel(Context::background());
+  auto wch = cli[0]->watch(ctx, "stress/", "stress0", 0);
+  std::atomic<int> events{0};
+  std::thread watcher([&] {
+    for (;;) {
+      bool closed = false;
+      auto r = wch->recv(200, &closed);
+      if (r) events += (int)r->events.size();
+      if (closed) return;
+    }
+  });
+  // leases: grant + keepalive stream while writes go on
+  int64_t ttl = 0;
+  const int64_t lease = cli[1]->grant(2, &ttl);
+  CHECK(lease != 0);
+  auto kctx = Context::with_cancel(Context::background());
+  auto kch = cli[1]->keepalive(kctx, lease);
+
+  std::atomic<int> ok{0};
+  std::vector<std::thread> writers;
+  for (int w = 0; w < 6; ++w)
+    writers.emplace_back([&, w] {
+      auto& c = cli[w % n];
+      for (int i = 0; i < 40; ++i) {
+        const std::string k = "stress/" + std::to_string(w) + "/" + std::to_string(i);
+        try {
+          c->put(k, "v" + std::to_string(i), (i % 5 == 0) ? lease : 0);
+          RangeOpts o;
+          auto r = c->get(k, o);
+          if (!r.kvs.empty()) ++ok;
+        } catch (const Error& e) {
+          std::fprintf(stderr, "writer %d: %s\n", w, e.what());
+        }
+      }
+    });
+  for (auto& t : writers) t.join();
+  CHECK(ok.load() == 6 * 40);
+  RangeOpts all;
+  all.end = "stress0";
+  all.count_only = true;
+  CHECK(cli[2]->get("stress/", all).count == 240);
+  for (int i = 0; i < 50 && events.load() < 240; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  CHECK(events.load() >= 240);
+  kctx->cancel();
+
+  // leader failover: close the leader, the other two elect a new one and serve writes
+  const uint64_t leader = ms[0]->leader();
+  int li = -1;
+  for (int i = 0; i < n; ++i)
+    if (ms[i]->id() == leader) li = i;
+  CHECK(li >= 0);
+  if (li >= 0) {
+    ms[li]->close();
+    const int s = (li + 1) % n;
+    bool wrote = false;
+    for (int a = 0; a < 100 && !wrote; ++a) {
+      try {
+        cli[s]->put("after/failover", "ok", 0, 1000);
+        wrote = true;
+      } catch (const Error&) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      }
+    }
+    CHECK(wrote);
+    CHECK(ms[s]->leader() != leader);
+  }
+  ctx->cancel();
+  watcher.join();
+  for (auto& c : cli) c->close();
+  for (auto& m : ms) m->close();
+}
+
+void scenario_rpc() {
+  auto srv = std::make_shared<RpcServer>();
+  srv->register_method("Calc.Multiply", [](const gob::Value& a) {
+    const gob::Value* x = a.field("A");
+    const gob::Value* y = a.field("B");
+    if (!x || !y) fail(Errc::kRpc, "bad args");
+    return gob::Value::Int(x->i * y->i);
+  });
+  std::atomic<int> flaky{0};
+  srv->register_method("Calc.Flaky", [&flaky](const gob::Value&) {
+    if (++flaky % 3) fail(Errc::kRpc, "failed");
+    return gob::Value::Int(1);
+  });
+  const int port = srv->listen("127.0.0.1", 0);
+  auto nodes = std::make_shared<NodesChan>(4);
+  nodes->send({Node{"127.0.0.1", port}});
+  ConnConfig cc;
+  cc.retries = 2;
+  cc.allow_local = false;  // force the socket path (HTTP CONNECT + gob)
+  auto client = std::make_shared<RpcClient>("127.0.0.1", "calc", nodes, cc);
+  std::atomic<int> good{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([&, t] {
+      for (int i = 0; i < 100; ++i) {
+        gob::Value args = gob::Value::Struct("Args");
+        args.fields = {{"A", gob::Value::Int(t)}, {"B", gob::Value::Int(i)}};
+        try {
+          if (client->call("Calc.Multiply", args).i == (int64_t)t * i) ++good;
+        } catch (const Error& e) {
+          std::fprintf(stderr, "call: %s\n", e.what());
+        }
+      }
+    });
+  // async Go calls sharing one done channel
+  auto done = std::make_shared<Channel<std::shared_ptr<RpcCall>>>(64);
+  for (int i = 0; i < 50; ++i) {
+    gob::Value args = gob::Value::Struct("Args");
+    args.fields = {{"A", gob::Value::Int(i)}, {"B", gob::Value::Int(2)}};
+    client->go("Calc.Multiply", args, done);
+  }
+  int async_ok = 0;
+  for (int i = 0; i < 50; ++i) {
+    auto c = done->recv(10000);
+    if (c && (*c)->error.empty() && (*c)->reply.i == (*c)->args.field("A")->i * 2) ++async_ok;
+  }
+  for (auto& t : ts) t.join();
+  CHECK(good.load() == 800);
+  CHECK(async_ok == 50);
+  // retry: fails twice, third attempt passes (bounded retries)
+  gob::Value none = gob::Value::Struct("Args");
+  bool passed = false;
+  try {
+    passed = client->call("Calc.Flaky", none).i == 1;
+  } catch (const Error&) {
+  }
+  CHECK(passed);
+  // re-balance while calls are in flight: same node list again, then a new server
+  auto srv2 = std::make_shared<RpcServer>();
+  srv2->register_method("Calc.Multiply", [](const gob::Value& a) { return gob::Value::Int(a.field("A")->i * 1000); });
+  const int port2 = srv2->listen("127.0.0.1", 0);
+  std::thread rebal([&] {
+    nodes->send({Node{"127.0.0.1", port}, Node{"127.0.0.1", port2}});
+    nodes->send({Node{"127.0.0.1", port2}});
+  });
+  for (int i = 0; i < 200; ++i) {
+    gob::Value args = gob::Value::Struct("Args");
+    args.fields = {{"A", gob::Value::Int(3)}, {"B", gob::Value::Int(5)}};
+    try {
+      const int64_t v = client->call("Calc.Multiply", args).i;
+      CHECK(v == 15 || v == 3000);
+    } catch (const Error&) {
+    }
+  }
+  rebal.join();
+  client->close();
+  srv->close();
+  srv2->close();
+}
+
+void scenario_cluster_api(const std::string& dir) {
+  const int pp = free_port(), cp = free_port(), sp = free_port();
+  Config cfg;
+  cfg.service_name = "calculator";
+  cfg.node_name = "node1";
+  cfg.port = sp;
+  cfg.member = std::make_shared<MemberConfig>(member_cfg(dir, "api0", pp, cp, "api0=" + url(pp)));
+  setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1", 1);
+  auto srv = std::make_shared<RpcServer>();
+  srv->register_method("Calculator.Multiply",
+                       [](const gob::Value& a) { return gob::Value::Int(a.field("A")->i * a.field("B")->i); });
+  srv->listen("127.0.0.1", sp);
+  auto c = Cluster::join(Context::background(), cfg);
+  auto svcs = c->registry->services(Context::background());
+  CHECK(svcs.count("calculator") == 1);
+  ConnConfig cc;
+  cc.allow_local = false;
+  auto client = c->new_client("calculator", &cc);
+  std::vector<std::thread> ts;
+  std::atomic<int> good{0};
+  for (int t = 0; t < 4; ++t)
+    ts.emplace_back([&, t] {
+      for (int i = 0; i < 50; ++i) {
+        gob::Value args = gob::Value::Struct("Args");
+        args.fields = {{"A", gob::Value::Int(7)}, {"B", gob::Value::Int(t + i)}};
+        try {
+          if (client->call("Calculator.Multiply", args).i == 7 * (t + i)) ++good;
+        } catch (const Error& e) {
+          std::fprintf(stderr, "api call: %s\n", e.what());
+        }
+      }
+    });
+  // store traffic concurrently with the calls
+  for (int i = 0; i < 50; ++i) c->store->put(Context::background(), "k" + std::to_string(i), "v");
+  CHECK(c->store->get(Context::background(), "k7").size() == 1);
+  for (auto& t : ts) t.join();
+  CHECK(good.load() == 200);
+  client->close();
+  c->close();
+  srv->close();
+}
+
+// Elastic scale-out: a second member joins as a learner through the first one's
+// client URL and is promoted once caught up (cluster/cluster.go:105-147, :183-195).
+void scenario_learner(const std::string& dir) {
+  setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1", 1);
+  const int pp1 = free_port(), cp1 = free_port(), pp2 = free_port(), cp2 = free_port();
+  Config a;
+  a.service_name = "svc";
+  a.node_name = "a";
+  a.port = free_port();
+  a.member = std::make_shared<MemberConfig>(member_cfg(dir, "la", pp1, cp1, "la=" + url(pp1)));
+  auto ca = Cluster::join(Context::background(), a);
+  for (int i = 0; i < 20; ++i) ca->store->put(Context::background(), "pre" + std::to_string(i), "x");
+  Config b;
+  b.service_name = "svc";
+  b.node_name = "b";
+  b.port = free_port();
+  b.initial_cluster_client_urls = {url(cp1)};
+  b.member = std::make_shared<MemberConfig>(member_cfg(dir, "lb", pp2, cp2, ""));
+  b.member->cluster_state = "existing";
+  auto cb = Cluster::join(Context::background(), b);
+  auto ms = cb->member_list(Context::background());
+  CHECK(ms.size() == 2);
+  for (const auto& m : ms) CHECK(!m.is_learner);
+  CHECK(cb->store->get(Context::background(), "pre19").size() == 1);  // caught up before promotion
+  auto nodes = cb->registry->services(Context::background());
+  CHECK(nodes["svc"].size() == 2);
+  cb->close();
+  ca->close();
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s <workdir> [channel|raft|rpc|api]...\n", argv[0]);
+    return 2;
+  }
+  const std::string dir = argv[1];
+  std::vector<std::string> want(argv + 2, argv + argc);
+  if (want.empty()) want = {"channel", "raft", "rpc", "api", "learner"};
+  std::map<std::string, std::function<void()>> all = {
+      {"channel", [] { scenario_channel(); }},
+      {"raft", [&] { scenario_raft(dir); }},
+      {"rpc", [] { scenario_rpc(); }},
+      {"api", [&] { scenario_cluster_api(dir); }},
+      {"learner", [&] { scenario_learner(dir); }},
+  };
+  for (const auto& w : want) {
+    auto it = all.find(w);
+    if (it == all.end()) {
+      std::fprintf(stderr, "unknown scenario %s\n", w.c_str());
+      return 2;
+    }
+    const int before = g_failures;
+    try {
+      it->second();
+    } catch (const std::exception& e) {
+      std::fprintf(stderr, "scenario %s threw: %s\n", w.c_str(), e.what());
+      ++g_failures;
+    }
+    std::printf("%s %s\n", g_failures == before ? "OK" : "FAIL", w.c_str());
+    std::fflush(stdout);
+  }
+  return g_failures ? 1 : 0;
+}
