@@ -281,7 +281,15 @@ class Server:
     def debug_page(self) -> str:
         return self._s.debug_page()
 
+    def ServeDebug(self, stats: Callable[[], dict], path: str = "/debug/ptype") -> None:
+        """``GET <path>`` on this server's port answers ``json.dumps(stats())``
+        (next to net/rpc's ``/debug/rpc``); e.g. ``server.ServeDebug(cluster.Stats)``."""
+        import json
+
+        self._s.set_debug_handler(path, lambda: json.dumps(stats(), default=str))
+
     register, register_func, register_device, listen, close = Register, RegisterFunc, RegisterDevice, Listen, Close
+    serve_debug = ServeDebug
 
 
 def Serve(port: int, *receivers, host: str = "0.0.0.0") -> Server:
@@ -304,12 +312,32 @@ class Cluster:
         self.Registry = Registry(core.registry)
         self.Store = KVStore(core.store)
         self.runtime = runtime
+        self._clients: list[Client] = []
 
     def MemberList(self, ctx=None):
         return self._c.member_list(_ctx(ctx))
 
     def NewClient(self, serviceName: str, cfg: ConnConfig | None = None) -> Client:
-        return Client(self._c.new_client(serviceName, cfg), self.runtime, serviceName)
+        c = Client(self._c.new_client(serviceName, cfg), self.runtime, serviceName)
+        self._clients.append(c)
+        return c
+
+    def Stats(self) -> dict:
+        """Observability snapshot: control-plane member status, the
+        clients' call/attempt counters and selected nodes, and -- with a GPU
+        runtime -- dispatcher, registry-mirror and exchange counters plus the
+        single-call round-trip histogram.  Served as JSON by ``Server.ServeDebug``."""
+        st = self._c.member_status()
+        out = {
+            "service": self.cfg.service_name, "node": self.cfg.node_name, "local_addr": self.local_addr,
+            "member": {"id": st.id, "leader": st.leader, "term": st.term, "commit": st.commit,
+                       "applied": st.applied, "revision": st.revision, "is_learner": st.is_learner},
+            "clients": [{"service": c.service, "calls": c._c.calls, "attempts": c._c.attempts,
+                         "nodes": [f"{n.address}:{n.port}" for n in c.selected_nodes()]} for c in self._clients],
+        }
+        if self.runtime is not None:
+            out["runtime"] = self.runtime.stats()
+        return out
 
     def Close(self) -> None:
         if self.runtime is not None:
@@ -329,7 +357,7 @@ class Cluster:
 
     registry = property(lambda self: self.Registry)
     store = property(lambda self: self.Store)
-    member_list, new_client, close = MemberList, NewClient, Close
+    member_list, new_client, close, stats = MemberList, NewClient, Close, Stats
 
     def __enter__(self):
         return self

@@ -589,7 +589,10 @@ PYBIND11_MODULE(_core, m) {
       .def(py::init<>())
       .def("register_method",
            [](std::shared_ptr<RpcServer> s, const std::string& name, py::function fn) {
-             auto holder = std::make_shared<py::function>(fn);
+             auto holder = std::shared_ptr<py::function>(new py::function(fn), [](py::function* p) {
+               py::gil_scoped_acquire gil;  // a dispatch thread may drop the last reference
+               delete p;
+             });
              s->register_method(name, [holder](const gob::Value& args) -> gob::Value {
                py::gil_scoped_acquire gil;
                try {
@@ -629,6 +632,25 @@ PYBIND11_MODULE(_core, m) {
       .def_property_readonly("port", &RpcServer::port)
       .def("call_counts", &RpcServer::call_counts)
       .def("debug_page", &RpcServer::debug_page)
+      .def("set_debug_handler",
+           [](std::shared_ptr<RpcServer> s, const std::string& path, py::object fn) {
+             if (fn.is_none()) {
+               s->set_debug_handler(path, nullptr);
+               return;
+             }
+             auto holder = std::shared_ptr<py::object>(new py::object(fn), [](py::object* p) {
+               py::gil_scoped_acquire gil;  // the last owner may be a server thread
+               delete p;
+             });
+             s->set_debug_handler(path, [holder]() -> std::string {
+               py::gil_scoped_acquire gil;
+               try {
+                 return (*holder)().cast<std::string>();
+               } catch (py::error_already_set& e) {
+                 throw std::runtime_error(py::str(e.value()).cast<std::string>());
+               }
+             });
+           })
       .def("dispatch", [](RpcServer& s, const std::string& sm, py::object args) {
         gob::Value a = to_gob(args);
         RpcOutcome o;

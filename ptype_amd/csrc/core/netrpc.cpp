@@ -246,6 +246,14 @@ std::string RpcServer::debug_page() const {
   return o + "</body></html>\n";
 }
 
+void RpcServer::set_debug_handler(const std::string& path, std::function<std::string()> fn) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (fn)
+    debug_handlers_[path] = std::move(fn);
+  else
+    debug_handlers_.erase(path);
+}
+
 void RpcServer::serve_conn(std::shared_ptr<Conn> c) {
   std::string line;
   if (!c->read_line(&line)) return;
@@ -259,6 +267,26 @@ void RpcServer::serve_conn(std::shared_ptr<Conn> c) {
     c->write_raw("HTTP/1.0 200 OK\r\nContent-Type: text/html; charset=utf-8\r\nContent-Length: " +
                  std::to_string(body.size()) + "\r\n\r\n" + body);
     return;
+  }
+  if (method == "GET") {
+    std::function<std::string()> fn;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = debug_handlers_.find(path);
+      if (it != debug_handlers_.end()) fn = it->second;
+    }
+    if (fn) {
+      std::string body, status = "200 OK";
+      try {
+        body = fn();
+      } catch (const std::exception& e) {
+        status = "500 Internal Server Error";
+        body = std::string("{\"error\": \"") + e.what() + "\"}";
+      }
+      c->write_raw("HTTP/1.0 " + status + "\r\nContent-Type: application/json\r\nContent-Length: " +
+                   std::to_string(body.size()) + "\r\n\r\n" + body);
+      return;
+    }
   }
   if (method != "CONNECT") {
     c->write_raw("HTTP/1.0 405 Method Not Allowed\r\nContent-Type: text/plain; charset=utf-8\r\n\r\n405 must CONNECT\n");

@@ -87,11 +87,14 @@ class RpcServer {
   RpcOutcome dispatch(const std::string& service_method, const gob::Value& args);
   std::map<std::string, uint64_t> call_counts() const;
   std::string debug_page() const;
+  // Extra GET endpoints answering JSON (e.g. /debug/ptype -> Cluster.Stats()).
+  void set_debug_handler(const std::string& path, std::function<std::string()> fn);
 
  private:
   void serve_conn(std::shared_ptr<Conn> c);
   mutable std::mutex mu_;
   std::map<std::string, RpcHandler> methods_;
+  std::map<std::string, std::function<std::string()>> debug_handlers_;
   std::map<std::string, uint64_t> counts_;
   std::unique_ptr<Listener> listener_;
   int port_ = 0;

@@ -57,8 +57,17 @@ static_assert(sizeof(ReplyRecord) == 16, "ReplyRecord must be 16 bytes");
 // written last with release semantics; the consumer polls the tag only.
 struct alignas(64) RingSlot {
   MsgRecord msg;
-  uint64_t tag;   // sequence number + 1 of the request published in this slot
-  uint64_t pad[3];
+  uint64_t tag;       // sequence number + 1 of the request published in this slot
+  uint64_t t_pub_ns;  // host steady-clock time of publication (latency tracing)
+  uint64_t pad[2];
+};
+
+// One traced request of the persistent dispatcher (host-visible trace ring).
+struct TraceRec {
+  uint64_t seq;
+  uint64_t t_pub_ns;      // host: request published
+  uint64_t t_seen_ticks;  // device s_memrealtime (100 MHz): batch picked up
+  uint64_t t_done_ticks;  // device: reply published
 };
 static_assert(sizeof(RingSlot) == 64, "RingSlot must be 64 bytes");
 

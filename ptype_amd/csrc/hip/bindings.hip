@@ -4,6 +4,7 @@
 // raw hipStream_t (torch.cuda.current_stream().cuda_stream), so the module does
 // not link libtorch: it shares torch's HIP runtime, allocator-owned buffers and
 // streams, and keeps compile times at seconds.
+#include <dlfcn.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -11,6 +12,33 @@
 #include "server.hpp"
 
 namespace py = pybind11;
+
+// roctx ranges for rocprofv3 --marker-trace, resolved at run time
+// so the module has no hard dependency on the profiler SDK; no-ops without it.
+namespace {
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  void (*mark)(const char*) = nullptr;
+  Roctx() {
+    for (const char* lib : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4"}) {
+      void* h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+      if (!h) continue;
+      push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+      pop = (int (*)())dlsym(h, "roctxRangePop");
+      mark = (void (*)(const char*))dlsym(h, "roctxMarkA");
+      if (push && pop) return;
+    }
+    push = nullptr;
+    pop = nullptr;
+    mark = nullptr;
+  }
+};
+Roctx& roctx() {
+  static Roctx r;
+  return r;
+}
+}  // namespace
 
 namespace ptype {
 void launch_table_upsert(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int64_t,
@@ -92,6 +120,12 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("rank_self"), py::arg("stream"));
   m.def("wire_req_words", &wire_req_words, py::arg("C"), py::arg("nargs"), py::arg("mc"));
   m.def("wire_rep_words", &wire_rep_words, py::arg("C"));
+  m.def("roctx_available", [] { return roctx().push != nullptr; });
+  m.def("roctx_push", [](const std::string& s) { return roctx().push ? roctx().push(s.c_str()) : -1; });
+  m.def("roctx_pop", [] { return roctx().pop ? roctx().pop() : -1; });
+  m.def("roctx_mark", [](const std::string& s) {
+    if (roctx().mark) roctx().mark(s.c_str());
+  });
   m.def("set_route_tuning", &set_route_tuning, py::arg("prep_items"),
         "route_prep items per thread (1, 2, 4; 0 = default) -- a tuning knob for experiments");
   m.def("table_build_dir", &launch_table_build_dir, py::arg("table"), py::arg("cap"), py::arg("dir"),
@@ -140,6 +174,18 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("exits_idle", &DeviceServer::exits_idle)
       .def_property_readonly("exits_lifetime", &DeviceServer::exits_lifetime)
       .def_property_readonly("running", &DeviceServer::running)
+      .def("enable_trace", &DeviceServer::enable_trace, py::arg("capacity") = 4096)
+      .def("disable_trace", &DeviceServer::disable_trace)
+      .def("trace_records",
+           [](const DeviceServer& s) {
+             const auto v = s.trace_records();
+             return py::bytes(reinterpret_cast<const char*>(v.data()), v.size() * sizeof(TraceRec));
+           },
+           "raw TraceRec ring: uint64 [seq, t_pub_ns, t_seen_ticks, t_done_ticks] per record")
+      .def("calibrate", &DeviceServer::calibrate, py::arg("timeout") = 2.0,
+           py::call_guard<py::gil_scoped_release>(), "[host_ns, device_ticks, half_window_ns]")
+      .def("rtt_histogram", &DeviceServer::rtt_histogram, "host round-trip counts per log2(ns) bucket")
+      .def_static("now_ns", &DeviceServer::now_ns)
       .def("submit_handle", [](DeviceServer& s) {
         return py::make_tuple((uintptr_t)&DeviceServer::submit_c, (uintptr_t)&s);
       });

@@ -22,6 +22,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <vector>
 
 #include "common.hpp"
 #include "handlers.hpp"
@@ -37,8 +38,13 @@ struct alignas(64) ServerCtrl {
   uint64_t processed;
   uint64_t exits_idle;
   uint64_t exits_lifetime;
-  uint64_t pad[2];
+  uint64_t trace_mask;   // 0: tracing off; else trace ring capacity - 1
+  uint64_t trace_ring;   // device address of the TraceRec ring
+  uint64_t calib_req;    // host sets 1; the kernel answers with calib_ticks and clears it
+  uint64_t calib_ticks;
+  uint64_t pad[6];
 };
+static_assert(sizeof(ServerCtrl) == 128, "ServerCtrl layout");
 
 __device__ __forceinline__ uint64_t sys_ld(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -58,6 +64,10 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
   uint64_t last_work = t_start;
   uint64_t processed = 0;
   bool lifetime_exit = false;
+  // tracing knobs are re-read on the idle path only, never between a request and its reply
+  uint64_t trace_mask = sys_ld(&ctrl->trace_mask);
+  TraceRec* trace = reinterpret_cast<TraceRec*>(sys_ld(&ctrl->trace_ring));
+  unsigned idle_polls = 0;
   for (;;) {
     if (sys_ld(&ctrl->stop)) break;
     const uint64_t seq = head + lane;
@@ -66,6 +76,17 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
     const uint64_t m = __ballot(ready);
     const unsigned n = (m == ~0ull) ? 64u : (unsigned)__builtin_ctzll(~m);
     if (n == 0) {
+      if ((++idle_polls & 3) == 0) {
+        if ((idle_polls & 63) == 0) {
+          trace_mask = sys_ld(&ctrl->trace_mask);
+          trace = reinterpret_cast<TraceRec*>(sys_ld(&ctrl->trace_ring));
+        }
+        if (lane == 0 && sys_ld(&ctrl->calib_req)) {  // clock calibration handshake
+          sys_st(&ctrl->calib_ticks, realtime_ticks());
+          __threadfence_system();
+          sys_st(&ctrl->calib_req, 0);
+        }
+      }
       const uint64_t now = realtime_ticks();
       const bool idle = idle_ticks && now - last_work > idle_ticks;
       lifetime_exit = now - t_start > max_ticks;
@@ -100,6 +121,7 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
+    const uint64_t t_seen = realtime_ticks();
     if (lane < n) {
       const uint64_t* w = reinterpret_cast<const uint64_t*>(&s->msg);
       const uint64_t w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3);
@@ -117,6 +139,14 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
       sys_st(ow + 1, (uint64_t)(uint32_t)r.status | ((uint64_t)r.actor << 32));
       __threadfence_system();
       sys_st(&o->tag, seq + 1);
+      if (trace_mask && trace) {  // after the reply is out: off the request's critical path
+        const uint64_t t_done = realtime_ticks();
+        TraceRec* tr = &trace[seq & trace_mask];
+        sys_st(&tr->seq, seq);
+        sys_st(&tr->t_pub_ns, sys_ld(&s->t_pub_ns));
+        sys_st(&tr->t_seen_ticks, t_seen);
+        sys_st(&tr->t_done_ticks, t_done);
+      }
     }
     head += n;
     processed += n;
@@ -172,6 +202,7 @@ class DeviceServer {
     hipHostFree(req_);
     hipHostFree(rep_);
     hipHostFree(ctrl_);
+    if (trace_) hipHostFree(trace_);
   }
 
   // Publish n requests and wait for all replies (any thread).
@@ -186,6 +217,54 @@ class DeviceServer {
       for (int i = 0; i < batch; ++i) out[done + i] = wait(seqs[done + i], timeout_s);
       done += batch;
     }
+  }
+
+  // ---- tracing (device timestamp ring, enqueue -> dispatch -> reply)
+  void enable_trace(uint32_t capacity) {
+    if (capacity == 0 || (capacity & (capacity - 1))) throw std::invalid_argument("trace capacity: power of two");
+    std::lock_guard<std::mutex> g(launch_mu_);
+    if (!trace_) {
+      const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+      PT_HIP_CHECK(hipHostMalloc((void**)&trace_, sizeof(TraceRec) * capacity, fl));
+      memset((void*)trace_, 0, sizeof(TraceRec) * capacity);
+      PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dtrace_, trace_, 0));
+      trace_cap_ = capacity;
+    }
+    __atomic_store_n(&ctrl_->trace_ring, (uint64_t)(uintptr_t)dtrace_, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&ctrl_->trace_mask, (uint64_t)(trace_cap_ - 1), __ATOMIC_SEQ_CST);
+  }
+  void disable_trace() { __atomic_store_n(&ctrl_->trace_mask, 0ull, __ATOMIC_SEQ_CST); }
+  // Copy of the trace ring (unordered; seq identifies each record).
+  std::vector<TraceRec> trace_records() const {
+    std::vector<TraceRec> v;
+    if (!trace_) return v;
+    v.resize(trace_cap_);
+    memcpy(v.data(), (const void*)trace_, sizeof(TraceRec) * trace_cap_);
+    return v;
+  }
+  // Host steady-clock ns <-> device ticks: the running dispatcher stamps its
+  // clock while the host brackets the handshake.  Returns {host_ns, ticks, err_ns}.
+  std::vector<uint64_t> calibrate(double timeout_s = 2.0) {
+    ensure_running();
+    const uint64_t t0 = now_ns();
+    __atomic_store_n(&ctrl_->calib_req, 1ull, __ATOMIC_SEQ_CST);
+    while (__atomic_load_n(&ctrl_->calib_req, __ATOMIC_ACQUIRE)) {
+      ensure_running();
+      if ((now_ns() - t0) * 1e-9 > timeout_s) throw std::runtime_error("device server: calibration timeout");
+    }
+    const uint64_t t1 = now_ns();
+    return {(t0 + t1) / 2, __atomic_load_n(&ctrl_->calib_ticks, __ATOMIC_ACQUIRE), (t1 - t0) / 2};
+  }
+  // Host-measured round trip of every call, log2(ns) buckets.
+  std::vector<uint64_t> rtt_histogram() const {
+    std::vector<uint64_t> h(kRttBuckets);
+    for (int i = 0; i < kRttBuckets; ++i) h[i] = rtt_hist_[i].load(std::memory_order_relaxed);
+    return h;
+  }
+  static uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
   }
 
   uint64_t processed() const { return __atomic_load_n(&ctrl_->processed, __ATOMIC_ACQUIRE); }
@@ -212,6 +291,7 @@ class DeviceServer {
       if (spins > 64) std::this_thread::yield();
     RingSlot* s = &req_[idx];
     s->msg = m;
+    s->t_pub_ns = now_ns();
     __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
     return seq;
   }
@@ -229,7 +309,10 @@ class DeviceServer {
       }
     }
     ReplyRecord r = o->rep;
+    const uint64_t rtt = now_ns() - req_[idx].t_pub_ns;
     owner_[idx].store(seq + ring_, std::memory_order_release);
+    int b = rtt ? 63 - __builtin_clzll(rtt) : 0;
+    rtt_hist_[b < kRttBuckets ? b : kRttBuckets - 1].fetch_add(1, std::memory_order_relaxed);
     return r;
   }
 
@@ -275,6 +358,11 @@ class DeviceServer {
   std::atomic<uint64_t> launches_{0};
   std::mutex launch_mu_;
   bool closed_ = false;
+  static constexpr int kRttBuckets = 40;
+  std::atomic<uint64_t> rtt_hist_[kRttBuckets] = {};
+  TraceRec* trace_ = nullptr;
+  TraceRec* dtrace_ = nullptr;
+  uint32_t trace_cap_ = 0;
 };
 
 }  // namespace ptype

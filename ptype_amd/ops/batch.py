@@ -152,12 +152,13 @@ class RouteWorkspace:
 
 def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int = 0,
           sendbuf: torch.Tensor | None = None, perm: torch.Tensor | None = None,
-          rws: RouteWorkspace | None = None, fmt: WireFormat = FULL_FORMAT):
+          rws: RouteWorkspace | None = None, fmt: WireFormat = FULL_FORMAT, reset_stats: bool = True):
     """K1: resolve each message's actor in the GPU registry and place it, in
     message order, into its destination rank's epoch slot (wire format ``fmt``).
 
     Returns ``(sendbuf int32[R * fmt.req_words(C)], perm int32[M], stats int64[4])``;
-    ``perm[i] = d * C + pos`` (-1 overflow, -2 no actor).
+    ``perm[i] = d * C + pos`` (-1 overflow, -2 no actor).  The no-actor /
+    overflow counters accumulate in ``rws.ws`` unless ``reset_stats``.
     """
     M = batch.M
     dev = batch.device
@@ -175,7 +176,8 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
         perm = torch.empty(M, dtype=torch.int32, device=dev)
     if rws is None or rws.M < M or rws.R != R:
         rws = RouteWorkspace(M, R, dev)
-    rws.ws.zero_()
+    if reset_stats:
+        rws.ws.zero_()
     uniform = isinstance(batch.method, int)
     method_u = int(batch.method) if uniform else 0
     if dev.type == "cuda":
@@ -213,8 +215,8 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
         overflow += n - k
         region[:4] = _u32(torch.tensor([k, n, rank_self, (FLAG_VALID << 16) | (method_u & 0xFFFF)]))
     st = ws_stats(rws.ws)
-    st[STAT_NOMATCH] = int((~ok).sum())
-    st[STAT_OVERFLOW] = overflow
+    st[STAT_NOMATCH] += int((~ok).sum())
+    st[STAT_OVERFLOW] += overflow
     return sendbuf, perm, st
 
 

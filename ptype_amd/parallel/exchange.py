@@ -39,6 +39,7 @@ import torch.distributed as dist
 from ..ops import batch as B
 from ..ops.records import STATUS_OVERFLOW
 from ..ops.table import RegistryTable
+from ..utils import trace
 
 
 def capacity_for(msgs_per_chunk: int, world: int, slack: float = 0.06) -> int:
@@ -49,8 +50,11 @@ def capacity_for(msgs_per_chunk: int, world: int, slack: float = 0.06) -> int:
 
 @dataclass
 class EpochStats:
-    sent: int = 0
-    overflow: int = 0
+    sent: int = 0  # messages handed to send()
+    epochs: int = 0  # chunk epochs run (one request + one reply all-to-all each)
+    wire_bytes: int = 0  # bytes this rank put on the all-to-alls (requests + replies, padded slots)
+    resends: int = 0  # send_all re-send rounds
+    overflow: int = 0  # device counters (cumulative): overflowed, no-actor, handler-failed
     nomatch: int = 0
     failed: int = 0
 
@@ -104,6 +108,7 @@ class ActorExchange:
         self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device, self.force_collectives,
                                 fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 2))]
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
+        self.counters = EpochStats()
 
     # ------------------------------------------------------------------
     def _a2a(self, out, inp):
@@ -129,6 +134,10 @@ class ActorExchange:
         if not fmt.admits(req):
             raise ValueError(f"batch columns do not fit the exchange's wire format {fmt}")
         wq, wr = R * fmt.req_words(C), R * B.WireFormat.rep_words(C)
+        self.counters.sent += M
+        self.counters.epochs += n
+        if R > 1 or self.force_collectives:
+            self.counters.wire_bytes += n * 4 * (wq + wr)
         pending_bwd = []  # (chunk index, work handle, bufs)
 
         def finish(entry):
@@ -139,30 +148,34 @@ class ActorExchange:
             B.complete(bufs.back[:wr], bufs.perm[: hi - lo], C, out_val[lo:hi], out_status[lo:hi], self.checksum)
 
         fwd = None
-        for i in range(n):
-            bufs = self.bufs[i % len(self.bufs)]
-            lo, hi = bounds[i], bounds[i + 1]
-            # buffer reuse: chunk i-2's replies must be consumed before overwriting
-            while pending_bwd and pending_bwd[0][0] <= i - len(self.bufs):
-                finish(pending_bwd.pop(0))
-            B.route(req.slice(lo, hi), self.table, R, C, self.rank, sendbuf=bufs.send[:wq],
-                    perm=bufs.perm[: hi - lo], rws=bufs.rws, fmt=fmt)
-            work = self._a2a(bufs.recv[:wq], bufs.send[:wq])
+        with trace.range("ptype.send"):
+            for i in range(n):
+                bufs = self.bufs[i % len(self.bufs)]
+                lo, hi = bounds[i], bounds[i + 1]
+                # buffer reuse: chunk i-2's replies must be consumed before overwriting
+                while pending_bwd and pending_bwd[0][0] <= i - len(self.bufs):
+                    finish(pending_bwd.pop(0))
+                with trace.range("ptype.route"):
+                    B.route(req.slice(lo, hi), self.table, R, C, self.rank, sendbuf=bufs.send[:wq],
+                            perm=bufs.perm[: hi - lo], rws=bufs.rws, fmt=fmt, reset_stats=False)
+                work = self._a2a(bufs.recv[:wq], bufs.send[:wq])
+                if fwd is not None:
+                    pending_bwd.append(self._serve(*fwd, fmt))
+                fwd = (i, work, bufs, hi - lo)
             if fwd is not None:
                 pending_bwd.append(self._serve(*fwd, fmt))
-            fwd = (i, work, bufs, hi - lo)
-        if fwd is not None:
-            pending_bwd.append(self._serve(*fwd, fmt))
-        for e in pending_bwd:
-            finish(e)
+            with trace.range("ptype.complete"):
+                for e in pending_bwd:
+                    finish(e)
         return out_val, out_status
 
     def _serve(self, i, work, bufs, m, fmt):
         if work is not None:
             work.wait()
         wq, wr = self.world * fmt.req_words(self.C), self.world * B.WireFormat.rep_words(self.C)
-        B.dispatch(bufs.recv[:wq], self.world, self.C, self.state, self.delay_us, reply=bufs.reply[:wr], ws=bufs.ws,
-                   expected_per_rank=max(1, m // self.world), fmt=fmt)
+        with trace.range("ptype.dispatch"):
+            B.dispatch(bufs.recv[:wq], self.world, self.C, self.state, self.delay_us, reply=bufs.reply[:wr], ws=bufs.ws,
+                       expected_per_rank=max(1, m // self.world), fmt=fmt)
         return (i, self._a2a(bufs.back[:wr], bufs.reply[:wr]), bufs)
 
     # ------------------------------------------------------------------
@@ -178,13 +191,15 @@ class ActorExchange:
             if int(n_over.item()) == 0:
                 break
             idx = torch.nonzero(over).flatten()
+            self.counters.resends += 1
             v2, s2 = self.send(req.index_select(idx))
             val[idx] = v2
             st[idx] = s2
         return val, st
 
     def stats(self) -> EpochStats:
-        s = EpochStats()
+        c = self.counters
+        s = EpochStats(sent=c.sent, epochs=c.epochs, wire_bytes=c.wire_bytes, resends=c.resends)
         for b in self.bufs:
             w = B.ws_stats(b.ws).tolist()
             s.nomatch += w[B.STAT_NOMATCH]

@@ -32,6 +32,7 @@ from .ops import batch as B
 from .ops import hip
 from .ops.records import STATUS_OK
 from .ops.table import RegistryTable, actor_keys
+from .utils import trace
 
 ACTORS_PREFIX = "_ptype/actors"
 
@@ -147,7 +148,8 @@ class DeviceRuntime:
 
     def call(self, method: int, actor: int, a0: int = 0, a1: int = 0, a2: int = 0, timeout: float = 30.0):
         """Single synchronous call to a local actor through the persistent dispatcher."""
-        v, st, _ = self.server.call(int(method), int(actor), int(a0), int(a1), int(a2), float(timeout))
+        with trace.range("ptype.call"):
+            v, st, _ = self.server.call(int(method), int(actor), int(a0), int(a1), int(a2), float(timeout))
         return v, st
 
     def serve(self, server, service: str, methods: dict) -> None:
@@ -192,9 +194,24 @@ class DeviceRuntime:
 
     # ------------------------------------------------------------------ stats / teardown
     def stats(self) -> dict:
-        return {"rank": self.rank, "world": self.world, "actors": self.actors,
-                "dispatcher_processed": self.server.processed, "dispatcher_launches": self.server.launches,
-                "registry_live": self.table.live, "registry_tombstones": self.table.tombstones}
+        from dataclasses import asdict
+
+        from .utils.trace import hist_percentile
+
+        h = self.server.rtt_histogram()
+        out = {"rank": self.rank, "world": self.world, "actors": self.actors,
+               "dispatcher": {"processed": self.server.processed, "launches": self.server.launches,
+                              "exits_idle": self.server.exits_idle, "exits_lifetime": self.server.exits_lifetime,
+                              "running": self.server.running, "calls": int(sum(h)),
+                              "rtt_p50_ns_le": hist_percentile(h, 50), "rtt_p99_ns_le": hist_percentile(h, 99),
+                              "rtt_log2ns_hist": h},
+               "registry": {"live": self.table.live, "tombstones": self.table.tombstones,
+                            "generation": self.table.generation, "capacity": self.table.cap,
+                            "directory_ids": self.table.dir_n},
+               "shards": self.shards}
+        if self._exchange is not None:
+            out["exchange"] = asdict(self._exchange.stats())
+        return out
 
     def close(self) -> None:
         if self._closed:
