@@ -125,7 +125,26 @@ void KvClient::drop_conn(const std::shared_ptr<Conn>& c, const std::string& why)
   }
 }
 
+// Requests rejected with "no leader" were never appended to the log, so they are
+// retried (with backoff) until the call's deadline, as clientv3's retry policy
+// does for Unavailable: an election in progress is not an error to the caller.
 std::string KvClient::call(uint8_t op, const std::string& payload, int64_t timeout_ms) {
+  const int64_t budget = timeout_ms <= 0 ? 5000 : timeout_ms;
+  const int64_t deadline = mono_ms() + budget;
+  int64_t backoff = 10;
+  for (;;) {
+    const int64_t left = deadline - mono_ms();
+    try {
+      return call_once(op, payload, std::max<int64_t>(1, left));
+    } catch (const Error& e) {
+      if (e.code() != Errc::kNotLeader || mono_ms() + backoff >= deadline) throw;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(backoff));
+    backoff = std::min<int64_t>(backoff * 2, 200);
+  }
+}
+
+std::string KvClient::call_once(uint8_t op, const std::string& payload, int64_t timeout_ms) {
   auto c = ensure_conn(timeout_ms);
   auto p = std::make_shared<Pending>();
   const uint64_t id = ++seq_;

@@ -69,6 +69,7 @@ class KvClient : public std::enable_shared_from_this<KvClient> {
     std::string err, payload;
   };
   std::string call(uint8_t op, const std::string& payload, int64_t timeout_ms);
+  std::string call_once(uint8_t op, const std::string& payload, int64_t timeout_ms);
   std::shared_ptr<Conn> ensure_conn(int64_t timeout_ms);
   void reader(std::shared_ptr<Conn> c);
   void drop_conn(const std::shared_ptr<Conn>& c, const std::string& why);

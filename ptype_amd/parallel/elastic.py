@@ -1,0 +1,258 @@
+"""Elastic data plane: rank-failure detection and recovery for the exchange.
+
+SURVEY 5.3.  The reference detects failed service nodes by **lease expiry**
+(2 s TTL + KeepAlive, cluster/registry.go:59-83) observed through a watch, and
+clients re-balance onto the survivors (cluster/rpc.go:197-244).  The data plane
+here is a set of collective process groups (RCCL over xGMI on MI355X, gloo on
+CPU), and a collective with a dead peer fails (gloo: connection reset / timeout;
+RCCL: the watchdog aborts the communicator with
+``TORCH_NCCL_ASYNC_ERROR_HANDLING=2``).  RCCL is not fault tolerant, so a group is
+never repaired in place -- it is aborted and a new *generation* is formed:
+
+1. ``send`` fails -> the survivor aborts its group (``_abort_process_group``),
+2. waits until the control plane's lease-based membership (the service's
+   registry nodes) drops the dead node (bounded by ``grace_s``),
+3. re-rendezvouses through the replicated KV store: the lowest surviving node
+   opens a TCPStore and publishes ``_ptype/dataplane/<svc>/gen/<g>/<node>``
+   ``{addr, port, members}``; the record with the lowest create revision wins
+   (``WithSort(SortByCreateRevision, SortAscend)``), so concurrent candidates
+   with different views still converge on one member list,
+4. re-homes the dead rank's actors by a deterministic ring adoption (the next
+   surviving original rank adopts them into extra mailbox blocks; actors of live
+   ranks never move and keep their state), rebuilds the GPU registry mirror, and
+5. the caller's batch is re-sent (``send_resilient``): delivery is
+   at-least-once, as with the reference's client retries (rpc.go:107-116).
+
+State of the adopted actors restarts from zero unless the application restores
+it (``DeviceRuntime.save/restore`` snapshots); the control plane itself survives
+the loss of a minority of members (Raft quorum).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from datetime import timedelta
+
+import torch
+import torch.distributed as dist
+
+from ..ops import batch as B
+from ..ops.table import RegistryTable, actor_keys
+from .exchange import ActorExchange
+
+PREFIX = "_ptype/dataplane"
+
+
+class RankFailure(RuntimeError):
+    """A collective of the current data-plane generation failed."""
+
+
+class Excluded(RuntimeError):
+    """This node is not a member of the newest generation."""
+
+
+def ring_placement(nodes0: list[str], members: list[str]) -> dict[str, list[int]]:
+    """Original rank -> owner: every surviving node owns its own original rank
+    first, then adopts each dead original rank whose next surviving successor
+    (in original ring order) it is.  Returns ``{node: [original ranks]}``."""
+    alive = set(members)
+    own = {n: ([r] if n in alive else []) for r, n in enumerate(nodes0)}
+    W0 = len(nodes0)
+    for r, n in enumerate(nodes0):
+        if n in alive:
+            continue
+        for k in range(1, W0):
+            succ = nodes0[(r + k) % W0]
+            if succ in alive:
+                own[succ].append(r)
+                break
+    return {n: rs for n, rs in own.items() if n in alive}
+
+
+class ElasticDataPlane:
+    """Batched ``Send`` over a self-healing process group.
+
+    ``cluster`` is a joined ``ptype_amd.cluster.Cluster`` (its node is
+    registered under ``service``); ``world`` the number of data-plane ranks
+    expected at start; ``per_rank`` actors hosted per original rank (actor ``a``
+    belongs to original rank ``a % world``, mailbox ``a // world``).
+    """
+
+    def __init__(self, cluster, service: str, world: int, per_rank: int, device=None, backend: str | None = None,
+                 max_batch: int = 1 << 20, chunks: int = 1, timeout_s: float = 10.0, grace_s: float = 8.0,
+                 rendezvous_timeout_s: float = 60.0):
+        self.cluster = cluster
+        self.service = service
+        self.world0 = int(world)
+        self.per_rank = int(per_rank)
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+        self.max_batch = int(max_batch)
+        self.chunks = int(chunks)
+        self.timeout_s = float(timeout_s)
+        self.grace_s = float(grace_s)
+        self.rdv_timeout_s = float(rendezvous_timeout_s)
+        self.me = f"{cluster.local_addr}:{cluster.cfg.port}"
+        self.gen = -1
+        self.nodes0: list[str] = []
+        self.members: list[str] = []
+        self.blocks: list[int] = []  # original ranks whose actors this node hosts, in mailbox-block order
+        self.state: torch.Tensor | None = None
+        self.table: RegistryTable | None = None
+        self.exchange: ActorExchange | None = None
+        self._tcp_store = None
+        self.recoveries = 0
+        if self.backend == "nccl":
+            # abort the communicator and raise instead of tearing the process down
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+
+    # ------------------------------------------------------------------ membership
+    def alive(self, timeout_s: float = 30.0) -> list[str]:
+        """Nodes of the service whose registry lease is alive (control plane).
+        Retries while the control plane itself is re-electing."""
+        from ..cluster import background
+
+        deadline = time.monotonic() + timeout_s
+        while True:
+            try:
+                nodes = self.cluster.Registry.Services(background()).get(self.service, [])
+                return sorted({f"{n.address}:{n.port}" for n in nodes})
+            except Exception:
+                if time.monotonic() > deadline:
+                    raise
+                time.sleep(0.1)
+
+    def start(self) -> None:
+        """Wait for ``world`` registered nodes and form generation 0."""
+        deadline = time.monotonic() + self.rdv_timeout_s
+        while True:
+            nodes = self.alive()
+            if len(nodes) >= self.world0:
+                break
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"only {len(nodes)} of {self.world0} data-plane nodes registered")
+            time.sleep(0.05)
+        self.nodes0 = nodes[: self.world0]
+        if self.me not in self.nodes0:
+            raise Excluded(f"{self.me} is not among the first {self.world0} nodes of {self.service}")
+        self._form(0, self.nodes0)
+
+    def _form(self, gen: int, proposal: list[str]) -> None:
+        from ..cluster import SortAscend, SortByCreateRevision, WithPrefix, WithSort, background
+
+        prefix = f"{PREFIX}/{self.service}/gen/{gen}/"
+        mine = None
+        if proposal and proposal[0] == self.me:  # candidate rendezvous master
+            host = self.cluster.local_addr
+            mine = dist.TCPStore(host, 0, len(proposal), True, timeout=timedelta(seconds=self.rdv_timeout_s),
+                                 wait_for_workers=False)
+            self.cluster.Store.Put(background(), prefix + self.me,
+                                   json.dumps({"addr": host, "port": mine.port, "members": proposal}))
+        deadline = time.monotonic() + self.rdv_timeout_s
+        rec = None
+        while rec is None:
+            try:
+                vals = self.cluster.Store.Get(background(), prefix, WithPrefix(),
+                                              WithSort(SortByCreateRevision, SortAscend))
+                rec = json.loads(vals[0]) if vals else None
+            except Exception:  # ErrNoKey until a candidate publishes
+                rec = None
+            if rec is None:
+                if time.monotonic() > deadline:
+                    raise TimeoutError(f"no data-plane generation {gen} published")
+                time.sleep(0.05)
+        members = rec["members"]
+        if self.me not in members:
+            raise Excluded(f"{self.me} was left out of generation {gen}: {members}")
+        leader = members[0] == self.me and mine is not None and rec["port"] == mine.port
+        store = mine if leader else dist.TCPStore(rec["addr"], int(rec["port"]), len(members), False,
+                                                  timeout=timedelta(seconds=self.rdv_timeout_s))
+        kw = {"device_id": self.device} if self.backend == "nccl" else {}
+        dist.init_process_group(self.backend, store=dist.PrefixStore(f"ptype/gen{gen}", store),
+                                rank=members.index(self.me), world_size=len(members),
+                                timeout=timedelta(seconds=self.timeout_s), **kw)
+        self._tcp_store = store  # the master keeps the store alive for the group's lifetime
+        self.gen, self.members = gen, members
+        self._rebuild()
+
+    # ------------------------------------------------------------------ placement
+    def _rebuild(self) -> None:
+        own = ring_placement(self.nodes0, self.members)
+        W0, P = self.world0, self.per_rank
+        new_blocks = own[self.me]
+        state = torch.zeros(P * len(new_blocks), dtype=torch.int64, device=self.device)
+        if self.state is not None:  # actors that stay here keep their state
+            for j, r in enumerate(new_blocks):
+                if r in self.blocks:
+                    i = self.blocks.index(r)
+                    state[j * P:(j + 1) * P] = self.state[i * P:(i + 1) * P]
+        self.blocks, self.state = new_blocks, state
+        table = RegistryTable(2 * W0 * P, device=self.device)
+        k = torch.arange(P, dtype=torch.int64)
+        for node, rs in own.items():
+            rank = self.members.index(node)
+            for j, r in enumerate(rs):
+                ids = r + W0 * k
+                table.upsert(actor_keys(ids), torch.full((P,), rank, dtype=torch.int32), (j * P + k).to(torch.int32))
+        table.enable_directory(W0 * P)
+        self.table = table
+        self.exchange = ActorExchange(table, self.max_batch, chunks=self.chunks, state=self.state)
+
+    @property
+    def total_actors(self) -> int:
+        return self.world0 * self.per_rank
+
+    # ------------------------------------------------------------------ data plane
+    def send(self, batch: B.MsgBatch):
+        """One ``send_all`` in the current generation; a collective failure
+        surfaces as ``RankFailure`` (the group is then unusable)."""
+        try:
+            return self.exchange.send_all(batch)
+        except Exception as e:  # gloo/RCCL errors come as RuntimeError / DistBackendError
+            raise RankFailure(f"generation {self.gen}: {e}") from e
+
+    def send_resilient(self, batch: B.MsgBatch, max_recoveries: int = 3):
+        """``send`` + recover-and-resend on rank failure (at-least-once)."""
+        for attempt in range(max_recoveries + 1):
+            try:
+                return self.send(batch)
+            except RankFailure:
+                if attempt == max_recoveries:
+                    raise
+                self.recover()
+
+    def recover(self) -> None:
+        """Abort the failed generation, wait for the lease-driven membership to
+        settle, form the next generation from the survivors, re-home actors."""
+        self._abort()
+        old = set(self.members)
+        deadline = time.monotonic() + self.grace_s
+        alive = self.alive()
+        while set(alive) >= old and time.monotonic() < deadline:  # nobody's lease has expired yet
+            time.sleep(0.1)
+            alive = self.alive()
+        proposal = [n for n in self.members if n in set(alive)]
+        if self.me not in proposal:
+            proposal = sorted(set(proposal) | {self.me})
+        self.recoveries += 1
+        self._form(self.gen + 1, proposal)
+
+    def _abort(self) -> None:
+        if dist.is_initialized():
+            try:
+                dist.distributed_c10d._abort_process_group()
+            except Exception:
+                try:
+                    dist.destroy_process_group()
+                except Exception:
+                    pass
+        self.exchange = None
+
+    def close(self) -> None:
+        if dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                self._abort()
+        self._tcp_store = None
