@@ -38,6 +38,8 @@ def _parse():
     p.add_argument("--chunks", type=int, default=0, help="pipeline chunks per step (0 = auto)")
     p.add_argument("--rtt-calls", type=int, default=2000)
     p.add_argument("--cpu", action="store_true", help="gloo/CPU dry run of the same pipeline (tests)")
+    p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                   help="replay the step as a captured hipGraph (auto: single rank)")
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the process group and run the all-to-alls even for one rank "
                         "(exercises the RCCL path on a 1-GPU box)")
@@ -101,7 +103,23 @@ def main():
     val = torch.empty(M, dtype=torch.int64, device=device)
     st = torch.empty(M, dtype=torch.int32, device=device)
 
+    use_graph = use_gpu and (args.graph == "on" or (args.graph == "auto" and not dist_on))
+    graph = None
+    if use_graph:
+        # the whole step (new requests + Send) as one hipGraph; the generator reads its
+        # seed from device memory and the graph advances it, so every replay is a new batch
+        seed_t = torch.tensor([rank * 0x9E3779B9 + 7], dtype=torch.int64, device=device)
+
+        def prologue():
+            B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, device=device, out=req, seed_tensor=seed_t)
+            seed_t.add_(0x1000193)
+
+        graph = ex.capture(req, val, st, prologue=prologue, allow_collectives=args.graph == "on")
+
     def step(s):
+        if graph is not None:
+            graph.replay()
+            return
         B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=(s * world + rank) * 0x1000193 + 7, device=device,
                        out=req)
         ex.send(req, val, st)
@@ -187,6 +205,7 @@ def main():
                 "record_bytes": 4 * (ex.fmt or B.WireFormat.for_batch(req)).stride,
                 "reply_bytes": 9,
                 "client_batch": "SoA (actor u32, A i64, B i64)",
+                "hip_graph": graph is not None,
             },
         }
         print(json.dumps(out), flush=True)

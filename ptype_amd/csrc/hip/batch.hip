@@ -110,9 +110,11 @@ __device__ __forceinline__ void lookup_many(const TableEntry* __restrict__ t, ui
   }
 }
 
+// `seed_ptr` (optional) lets a captured graph draw a new batch per replay.
 __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
                                                            int64_t* __restrict__ a1, int64_t M, uint32_t n_actors,
-                                                           uint64_t seed) {
+                                                           uint64_t seed, const uint64_t* __restrict__ seed_ptr) {
+  if (seed_ptr) seed = *seed_ptr;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = mix64(seed ^ (uint64_t)i * 0x9e3779b97f4a7c15ull);
     actor[i] = (uint32_t)(h % n_actors);
@@ -408,11 +410,11 @@ static inline unsigned grid_cap(int64_t work, int per, unsigned cap) {
 }
 
 void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M, uint32_t n_actors, uint64_t seed,
-                         uintptr_t stream) {
+                         uintptr_t seed_ptr, uintptr_t stream) {
   if (M <= 0) return;
   if (n_actors == 0) throw std::invalid_argument("n_actors must be > 0");
   hipLaunchKernelGGL(gen_requests_kernel, dim3(grid_cap(M, 256, 8192)), dim3(256), 0, as_stream(stream),
-                     (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed);
+                     (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr);
   PT_HIP_CHECK(hipGetLastError());
 }
 

@@ -47,7 +47,7 @@ void launch_table_delete(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uin
 void launch_table_lookup(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uintptr_t);
 void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
-void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t);
+void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t, uintptr_t);
 int64_t route_grid(int64_t, int64_t*);
 void launch_route(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t, uintptr_t,
                   uint32_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
@@ -107,7 +107,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("out_exp"), py::arg("out_count"), py::arg("stream"));
 
   m.def("gen_requests", &launch_gen_requests, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("M"),
-        py::arg("n_actors"), py::arg("seed"), py::arg("stream"));
+        py::arg("n_actors"), py::arg("seed"), py::arg("seed_ptr"), py::arg("stream"));
   m.def("route_grid", [](int64_t M) {
     int64_t P;
     int64_t G = route_grid(M, &P);

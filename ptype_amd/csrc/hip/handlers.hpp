@@ -28,6 +28,19 @@ __device__ __forceinline__ ReplyRecord run_handler(const MsgRecord& m, int64_t* 
       // for i in [Min, min(Max, Target)): if i != 0 && Target % i == 0 -> i ; else Target
       const int64_t lo = m.a0, hi = m.a1 < m.a2 ? m.a1 : m.a2, target = m.a2;
       r.value = target;
+      if (lo >= 0 && target > 0 && target <= 0xffffffffll) {
+        // 32-bit divisibility: a u32 remainder is a handful of VALU ops, a 64-bit
+        // one a long emulated sequence -- the whole optimus workload lives here
+        const uint32_t t32 = (uint32_t)target;
+        for (int64_t i = lo; i < hi; ++i) {
+          spin_ticks(delay_ticks);
+          if (i != 0 && t32 % (uint32_t)i == 0) {
+            r.value = i;
+            break;
+          }
+        }
+        break;
+      }
       for (int64_t i = lo; i < hi; ++i) {
         spin_ticks(delay_ticks);
         if (i != 0 && target % i == 0) {

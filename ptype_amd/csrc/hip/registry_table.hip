@@ -16,6 +16,38 @@
 
 namespace ptype {
 
+// Block-reduce two counters (sum, max) and publish them with ONE atomic each per
+// block; the generation is bumped once per launch (block 0).  Per-wave atomics
+// on the same words from ~16K waves serialize across the 8 XCDs.
+__device__ __forceinline__ void publish_block_stats(unsigned long long sum, unsigned long long mx,
+                                                    unsigned long long* __restrict__ sum_word,
+                                                    unsigned long long* __restrict__ max_word,
+                                                    unsigned long long* __restrict__ gen_word, bool negate_sum) {
+  __shared__ unsigned long long s_sum[4], s_max[4];
+  for (int off = 32; off > 0; off >>= 1) {
+    sum += __shfl_xor(sum, off);
+    const unsigned long long o = __shfl_xor(mx, off);
+    mx = o > mx ? o : mx;
+  }
+  const unsigned w = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+    s_sum[w] = sum;
+    s_max[w] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long a = 0, m = 0;
+    for (unsigned k = 0; k < blockDim.x / kWave; ++k) {
+      a += s_sum[k];
+      m = s_max[k] > m ? s_max[k] : m;
+    }
+    if (a && sum_word) atomicAdd(sum_word, negate_sum ? (unsigned long long)(-(long long)a) : a);
+    if (m && max_word) atomicMax(max_word, m);
+    if (blockIdx.x == 0 && gen_word) atomicAdd(gen_word, 1ull);
+  }
+  __syncthreads();  // the shared slots may be reused by a following call
+}
+
 __device__ __forceinline__ uint64_t ld_key(const TableEntry* e) {
   return __hip_atomic_load(&e->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -54,17 +86,7 @@ __global__ __launch_bounds__(256) void table_upsert_kernel(TableEntry* __restric
     if (exp_tbl) exp_tbl[h] = exp_in ? exp_in[i] : 0ull;
     if (probe > maxp) maxp = probe;
   }
-  // one atomic per wave for the counters (wave reduce through shuffles)
-  for (int off = 32; off > 0; off >>= 1) {
-    added += __shfl_xor(added, off);
-    unsigned long long o = __shfl_xor(maxp, off);
-    maxp = o > maxp ? o : maxp;
-  }
-  if (lane_id() == 0) {
-    if (added) atomicAdd(&stats[kStatLive], added);
-    atomicMax(&stats[kStatMaxProbe], maxp);
-    atomicAdd(&stats[kStatGen], 1ull);
-  }
+  publish_block_stats(added, maxp, &stats[kStatLive], &stats[kStatMaxProbe], &stats[kStatGen], false);
 }
 
 __global__ __launch_bounds__(256) void table_delete_kernel(TableEntry* __restrict__ t, uint64_t mask,
@@ -93,12 +115,8 @@ __global__ __launch_bounds__(256) void table_delete_kernel(TableEntry* __restric
     }
     if (found_out) found_out[i] = hit ? 1 : 0;
   }
-  for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);
-  if (lane_id() == 0 && removed) {
-    atomicAdd(&stats[kStatLive], (unsigned long long)(-(long long)removed));
-    atomicAdd(&stats[kStatTomb], removed);
-    atomicAdd(&stats[kStatGen], 1ull);
-  }
+  publish_block_stats(removed, 0, &stats[kStatLive], nullptr, &stats[kStatGen], true);
+  publish_block_stats(removed, 0, &stats[kStatTomb], nullptr, nullptr, false);
 }
 
 __global__ __launch_bounds__(256) void table_lookup_kernel(const TableEntry* __restrict__ t, uint64_t mask,
@@ -136,12 +154,8 @@ __global__ __launch_bounds__(256) void table_sweep_kernel(TableEntry* __restrict
                                              __HIP_MEMORY_SCOPE_AGENT))
       ++removed;
   }
-  for (int off = 32; off > 0; off >>= 1) removed += __shfl_xor(removed, off);
-  if (lane_id() == 0 && removed) {
-    atomicAdd(&stats[kStatLive], (unsigned long long)(-(long long)removed));
-    atomicAdd(&stats[kStatTomb], removed);
-    atomicAdd(&stats[kStatGen], 1ull);
-  }
+  publish_block_stats(removed, 0, &stats[kStatLive], nullptr, &stats[kStatGen], true);
+  publish_block_stats(removed, 0, &stats[kStatTomb], nullptr, nullptr, false);
 }
 
 // K7: snapshot pack -- compact live entries (+ deadlines) into a dense buffer

@@ -85,16 +85,20 @@ class MsgBatch:
 
 
 def gen_requests(M: int, n_actors: int, method: int = METHOD_CALC_MULTIPLY, seed: int = 0, device="cuda",
-                 out: MsgBatch | None = None) -> MsgBatch:
-    """Synthetic client load: M calls (A, B) to uniformly hashed actors in [0, n_actors)."""
+                 out: MsgBatch | None = None, seed_tensor: torch.Tensor | None = None) -> MsgBatch:
+    """Synthetic client load: M calls (A, B) to uniformly hashed actors in [0, n_actors).
+    ``seed_tensor`` (GPU int64[1]) is read by the kernel instead of ``seed``, so a
+    captured graph produces a fresh batch on every replay."""
     device = torch.device(device)
     if out is None:
         out = MsgBatch(torch.empty(M, dtype=torch.int32, device=device), torch.empty(M, dtype=torch.int64, device=device),
                        torch.empty(M, dtype=torch.int64, device=device), None, method)
     if device.type == "cuda":
         hip().gen_requests(_ptr(out.actor), _ptr(out.a0), _ptr(out.a1), M, int(n_actors), int(seed) & (2**64 - 1),
-                           _stream(out.actor))
+                           _ptr(seed_tensor), _stream(out.actor))
         return out
+    if seed_tensor is not None:
+        seed = int(seed_tensor.reshape(-1)[0])
     i = np.arange(M, dtype=np.uint64)
     with np.errstate(over="ignore"):
         h = mix64(np.uint64(seed & (2**64 - 1)) ^ (i * np.uint64(0x9E3779B97F4A7C15)))

@@ -179,6 +179,18 @@ class ActorExchange:
         return (i, self._a2a(bufs.back[:wr], bufs.reply[:wr]), bufs)
 
     # ------------------------------------------------------------------
+    def capture(self, req: B.MsgBatch, out_val: torch.Tensor, out_status: torch.Tensor, prologue=None,
+                allow_collectives: bool = False) -> "SendGraph":
+        """Capture ``send(req)`` (plus an optional ``prologue()``, e.g. a kernel
+        that refills ``req``) into a hipGraph for fixed-shape steady-state epochs:
+        one graph launch replaces the ~6 kernel launches + host logic per chunk,
+        which is what bounds small batches.  Single rank by default; RCCL
+        collectives are capturable but opt-in (``allow_collectives``)."""
+        if (self.world > 1 or self.force_collectives) and not allow_collectives:
+            raise RuntimeError("capture: collectives in a graph are opt-in (allow_collectives=True)")
+        return SendGraph(self, req, out_val, out_status, prologue)
+
+    # ------------------------------------------------------------------
     def send_all(self, req: B.MsgBatch, max_epochs: int = 16):
         """`send` + re-send of overflowed messages until every one is delivered
         (host-synchronising: reads the overflow count once per epoch)."""
@@ -206,3 +218,36 @@ class ActorExchange:
             s.overflow += w[B.STAT_OVERFLOW]
             s.failed += w[B.STAT_FAILED]
         return s
+
+
+class SendGraph:
+    """A captured ``ActorExchange.send`` over fixed buffers (``torch.cuda.CUDAGraph``
+    is a hipGraph on ROCm).  ``replay()`` re-runs every kernel of the epoch(s) on
+    whatever ``req`` holds at that moment."""
+
+    def __init__(self, ex: ActorExchange, req: B.MsgBatch, out_val, out_status, prologue=None):
+        self.ex, self.req, self.M = ex, req, req.M
+        dev = ex.device
+
+        def body():
+            if prologue is not None:
+                prologue()
+            ex.send(req, out_val, out_status)
+
+        ex.table.directory()  # build outside the capture if dirty
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # warm allocations / lazy state outside the graph
+                body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            body()
+        self.replays = 0
+
+    def replay(self) -> None:
+        self.graph.replay()
+        self.replays += 1
+        self.ex.counters.sent += self.M
+        self.ex.counters.epochs += self.ex.chunks

@@ -360,3 +360,34 @@ def test_wire_sizes_match_kernels():
             for mc in (False, True):
                 assert h.wire_req_words(C, nargs, mc) == B.WireFormat(nargs, mc).req_words(C)
         assert h.wire_rep_words(C) == B.WireFormat.rep_words(C)
+
+
+@pytest.mark.gpu
+def test_gpu_send_graph_replay():
+    """hipGraph capture of generator + Send: every replay routes a fresh batch."""
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    n_actors, M = 4096, 300_000
+    g = RegistryTable(2 * n_actors, device="cuda")
+    _populate(g, n_actors, 1)
+    g.enable_directory(n_actors)
+    state = torch.zeros(n_actors, dtype=torch.int64, device="cuda")
+    ex = ActorExchange(g, M, state=state)
+    req = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=1, device="cuda")
+    val = torch.empty(M, dtype=torch.int64, device="cuda")
+    st = torch.empty(M, dtype=torch.int32, device="cuda")
+    seed_t = torch.tensor([11], dtype=torch.int64, device="cuda")
+
+    def prologue():
+        B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, device="cuda", out=req, seed_tensor=seed_t)
+        seed_t.add_(1)
+
+    graph = ex.capture(req, val, st, prologue=prologue)
+    seen = []
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1)
+        seen.append(req.actor[:8].cpu().tolist())
+    assert seen[0] != seen[1] != seen[2]
+    assert ex.stats().sent >= 3 * M

@@ -1,0 +1,299 @@
+#!/usr/bin/env python3
+"""The BASELINE.json configs other than the headline (bench.py), one JSON line each.
+
+  host-rpc   example/calculator on the host path: control-plane member + net/rpc
+             (HTTP CONNECT + gob over TCP) -- sync Call p50 RTT and concurrent
+             Go throughput.  CPU only.
+  gpu-1m     calculator actor, 1M synthetic messages per step, 1 MI355X
+             (epoch slots in HBM + GPU registry), full Send path.
+  optimus    optimus fan-out: Prime.Check ranges of many targets as one batch
+             per step across every rank (torchrun for N GPUs: RCCL all-to-all
+             dispatch), per-candidate delay 0.
+  registry   1M-actor registry stress: GPU upsert / probe lookup / directory
+             build / lease sweep / pack + snapshot to pinned host DRAM, and the
+             control-plane store: puts with Raft snapshots + WAL.
+
+usage: python tools/bench_suite.py {host-rpc,gpu-1m,optimus,registry} [...]
+       torchrun --nproc-per-node N --master-addr 127.0.0.1 tools/bench_suite.py optimus
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def _emit(d):
+    print(json.dumps(d), flush=True)
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+# --------------------------------------------------------------------------- host-rpc
+def host_rpc(a):
+    from ptype_amd import cluster as C
+    from ptype_amd.models.calculator import Args, Calculator
+
+    os.environ.setdefault("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    pp, pc, sp = _free_port(), _free_port(), _free_port()
+    d = tempfile.mkdtemp(prefix="hostrpc_")
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "calculator", "n1", sp
+    cfg.member = C.member_config(name="m0", dir=d, lpurls=[f"http://127.0.0.1:{pp}"],
+                                 apurls=[f"http://127.0.0.1:{pp}"], lcurls=[f"http://127.0.0.1:{pc}"],
+                                 acurls=[f"http://127.0.0.1:{pc}"], initial_cluster=f"m0=http://127.0.0.1:{pp}",
+                                 unsafe_no_fsync=True)
+    server = C.Serve(sp, Calculator(), host="127.0.0.1")
+    c = C.Join(C.background(), cfg)
+    try:
+        for local in (False, True):
+            client = c.NewClient("calculator", C.ConnConfig(allow_local=local, retries=0))
+            for i in range(200):
+                client.Call("Calculator.Multiply", Args(i, 3))
+            lat = []
+            for i in range(a.calls):
+                t = time.perf_counter()
+                client.Call("Calculator.Multiply", Args(i, 3))
+                lat.append(time.perf_counter() - t)
+            lat.sort()
+            # throughput: many Go calls in flight from several threads
+            n_threads, per = 8, a.calls // 2
+
+            def worker(k):
+                for i in range(per):
+                    client.Call("Calculator.Multiply", Args(i, k))
+
+            ths = [threading.Thread(target=worker, args=(k,)) for k in range(n_threads)]
+            t0 = time.perf_counter()
+            [t.start() for t in ths]
+            [t.join() for t in ths]
+            el = time.perf_counter() - t0
+            _emit({"config": "example/calculator host path (net/rpc + gob over TCP)" if not local
+                   else "example/calculator host path, in-process fast path (no socket)",
+                   "p50_rtt_us": lat[len(lat) // 2] * 1e6, "p99_rtt_us": lat[int(len(lat) * 0.99)] * 1e6,
+                   "msgs_per_s_8_threads": n_threads * per / el, "handler": "Python receiver (GIL)",
+                   "device": "cpu"})
+            client.Close()
+    finally:
+        c.Close()
+        server.Close()
+
+
+# --------------------------------------------------------------------------- gpu-1m
+def gpu_1m(a):
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--msgs-per-gpu", str(a.msgs),
+                        "--steps", str(a.steps), "--warmup", "5", "--actors-per-gpu", str(a.actors)],
+                       capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise SystemExit(r.stderr[-2000:])
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    line["config_name"] = "calculator actor, 1M synthetic msgs, 1 MI355X"
+    _emit(line)
+
+
+# --------------------------------------------------------------------------- optimus
+def optimus(a):
+    import torch.distributed as dist
+
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.records import METHOD_PRIME_CHECK, STATUS_OK
+    from ptype_amd.ops.table import RegistryTable, actor_keys
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    per = a.actors
+    n = per * world
+    table = RegistryTable(2 * n, device=dev)
+    ids = torch.arange(n, dtype=torch.int64)
+    table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
+    table.enable_directory(n)
+    # targets: odd numbers around `base`, each split into 10-wide ranges [2,10), [10,20), ...
+    T = a.targets
+    tg = torch.arange(T, dtype=torch.int64, device=dev) * 2 + a.base + rank * 2 * T + 1
+    nr = (tg + 9) // 10  # ranges per target (splitWork: i = 10, 20, ... < target + 10)
+    M = int(nr.sum())
+    tid = torch.repeat_interleave(torch.arange(T, device=dev), nr)
+    first = torch.cumsum(nr, 0) - nr
+    k = torch.arange(M, device=dev) - first[tid]
+    lo = torch.where(k == 0, torch.full_like(k, 2), k * 10)
+    hi = (k + 1) * 10
+    batch = B.MsgBatch((torch.arange(M, device=dev) % n).to(torch.int32), lo, hi, tg[tid], METHOD_PRIME_CHECK)
+    ex = ActorExchange(table, M, chunks=4 if world > 1 else 1)
+    tg_rep = tg[tid]
+
+    def step():
+        val, st = ex.send(batch)
+        # gather: per target, the smallest reply that is not the target (watchReplies' winner
+        # when all replies are in); target itself when it is prime
+        # segmented min over each target's contiguous ranges (no contended atomics;
+        # float64 is exact for these magnitudes)
+        cand = torch.where(val != tg_rep, val, torch.full_like(val, 1 << 52)).double()
+        best = torch.segment_reduce(cand, "min", lengths=nr).long()
+        return torch.where(best == (1 << 52), tg, best), st
+
+    for _ in range(3):
+        ans, st = step()
+    torch.cuda.synchronize()
+    assert bool((st == STATUS_OK).all())
+    # check against a CPU trial division on a sample
+    for j in range(0, T, max(1, T // 64)):
+        t = int(tg[j])
+        exp = next((d for d in range(2, t) if t % d == 0), t)
+        assert int(ans[j]) == exp, (t, int(ans[j]), exp)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier(device_ids=[local])
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        _emit({"config": "example/optimus fan-out, RCCL all-to-all dispatch" if world > 1 else
+               "example/optimus fan-out, 1 GPU", "n_gpus": world, "targets_per_gpu_per_step": T,
+               "ranges_per_gpu_per_step": M, "ranges_per_s": M * world * a.steps / el,
+               "targets_per_s": T * world * a.steps / el, "ms_per_step": el / a.steps * 1e3,
+               "candidates_per_range": 10, "delay_per_candidate": 0})
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- registry
+def registry(a):
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.table import RegistryTable, actor_keys
+
+    dev = torch.device("cuda", 0)
+    N = a.actors
+    out = {"config": "1M-actor registry stress + snapshot to pinned host DRAM", "actors": N}
+
+    def timed(fn, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / reps
+
+    keys = actor_keys(torch.arange(N, dtype=torch.int64)).to(dev)
+    ranks = (torch.arange(N, device=dev) % 8).to(torch.int32)
+    mbox = (torch.arange(N, device=dev) // 8).to(torch.int32)
+    exp = torch.full((N,), 1 << 40, dtype=torch.int64, device=dev)
+    # inserts into an empty table (table allocation outside the timed region)
+    ins = []
+    for _ in range(5):
+        t = RegistryTable(4 * N, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        t.upsert(keys, ranks, mbox, exp)
+        torch.cuda.synchronize()
+        ins.append(time.perf_counter() - t0)
+    out["insert_ops_per_s"] = N / min(ins)
+    s = timed(lambda: t.upsert(keys, ranks, mbox, exp))  # every key present: in-place updates
+    out["update_ops_per_s"] = N / s
+    out["table_bytes"] = t.cap * 16
+    q = keys[torch.randperm(N, device=dev)]
+    s = timed(lambda: t.lookup(q))
+    out["lookup_ops_per_s"] = N / s
+
+    def build_dir():
+        t._dir_dirty = True
+        t.directory()
+
+    t.enable_directory(N)
+    s = timed(build_dir)
+    out["directory_build_ms"] = s * 1e3
+    s = timed(lambda: t.sweep(1))  # nothing expires: a full scan
+    out["sweep_scan_ms"] = s * 1e3
+    s = timed(lambda: t.pack())
+    out["pack_ms"] = s * 1e3
+    t0 = time.perf_counter()
+    h_ent, h_exp = t.snapshot_to_host()
+    el = time.perf_counter() - t0
+    nbytes = h_ent.numel() * 8 + h_exp.numel() * 8
+    out["snapshot_to_pinned_ms"] = el * 1e3
+    out["snapshot_bytes"] = nbytes
+    out["snapshot_gb_per_s"] = nbytes / el / 1e9
+    t2 = RegistryTable(2 * N, device=dev)
+    t0 = time.perf_counter()
+    t2.load_packed(h_ent, h_exp)
+    torch.cuda.synchronize()
+    out["restore_ms"] = (time.perf_counter() - t0) * 1e3
+    assert t2.live == N
+    del B
+    # control-plane store: puts through Raft with WAL + periodic snapshots
+    from ptype_amd import cluster as C
+
+    os.environ.setdefault("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    pp, pc = _free_port(), _free_port()
+    d = tempfile.mkdtemp(prefix="regstress_")
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "stress", "n1", _free_port()
+    cfg.member = C.member_config(name="m0", dir=d, lpurls=[f"http://127.0.0.1:{pp}"],
+                                 apurls=[f"http://127.0.0.1:{pp}"], lcurls=[f"http://127.0.0.1:{pc}"],
+                                 acurls=[f"http://127.0.0.1:{pc}"], initial_cluster=f"m0=http://127.0.0.1:{pp}",
+                                 snapshot_count=2000)
+    c = C.Join(C.background(), cfg)
+    try:
+        n_puts = a.puts
+        t0 = time.perf_counter()
+        for i in range(n_puts):
+            c.Store.Put(C.background(), f"actors/{i}", "x" * 32)
+        el = time.perf_counter() - t0
+        out["store_puts_per_s_fsync"] = n_puts / el
+        out["store_snapshot_on_disk"] = os.path.exists(os.path.join(d, "member", "snap.bin"))
+    finally:
+        c.Close()
+    _emit(out)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("which", choices=["host-rpc", "gpu-1m", "optimus", "registry"])
+    p.add_argument("--calls", type=int, default=4000)
+    p.add_argument("--msgs", type=int, default=1 << 20)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--actors", type=int, default=0)
+    p.add_argument("--targets", type=int, default=8192)
+    p.add_argument("--base", type=int, default=100_001)
+    p.add_argument("--puts", type=int, default=5000)
+    a = p.parse_args()
+    if not a.actors:
+        a.actors = {"registry": 1 << 20, "optimus": 65536}.get(a.which, 131072)
+    {"host-rpc": host_rpc, "gpu-1m": gpu_1m, "optimus": optimus, "registry": registry}[a.which](a)
+
+
+if __name__ == "__main__":
+    main()

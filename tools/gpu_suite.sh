@@ -1,0 +1,17 @@
+#!/bin/bash
+# BASELINE configs 2/4/5 on one GPU + hardware counters for the Send kernels.
+# usage (under gpurun): bash tools/gpu_suite.sh TAG
+set -o pipefail
+TAG=${1:-suite}
+mkdir -p gpurun_out
+OUT=gpurun_out/suite_$TAG.jsonl
+: > $OUT
+timeout -k 10 300 python tools/bench_suite.py gpu-1m >> $OUT 2> gpurun_out/suite_$TAG.err || { echo "gpu-1m FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
+timeout -k 10 300 python tools/bench_suite.py optimus >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "optimus FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
+timeout -k 10 300 python tools/bench_suite.py registry >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "registry FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
+cat $OUT
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/pmc_${TAG}_$C -o pmc --output-format csv -- python bench.py --steps 3 --warmup 1 --rtt-calls 0 --graph off > gpurun_out/pmc_${TAG}_$C.log 2>&1 || { echo "PMC $C FAILED"; tail -5 gpurun_out/pmc_${TAG}_$C.log; exit 1; }
+done
+python tools/pmc_summary.py gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE | tee gpurun_out/pmc_${TAG}_summary.txt
