@@ -50,9 +50,10 @@ void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uin
 void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t, uintptr_t);
 int64_t route_grid(int64_t, int64_t*);
 void launch_route(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t, uintptr_t,
-                  uint32_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int,
-                  uintptr_t);
-void set_route_tuning(int);
+                  uint32_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                  int, uintptr_t);
+void set_route_tuning(int, int);
+int64_t route_fused_grid(int64_t, int64_t*);
 void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t);
 void launch_dispatch(uintptr_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uint32_t, uint64_t, uintptr_t, int64_t,
                      uintptr_t);
@@ -116,8 +117,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("route", &launch_route, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"),
         py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
         py::arg("dir"), py::arg("n_dir"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
-        py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"), py::arg("stats"),
+        py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"), py::arg("lb"), py::arg("stats"),
         py::arg("rank_self"), py::arg("stream"));
+  m.def("route_fused_grid", [](int64_t M) {
+    int64_t P;
+    const int64_t G = route_fused_grid(M, &P);
+    return py::make_tuple(G, P);
+  });
   m.def("wire_req_words", &wire_req_words, py::arg("C"), py::arg("nargs"), py::arg("mc"));
   m.def("wire_rep_words", &wire_rep_words, py::arg("C"));
   m.def("roctx_available", [] { return roctx().push != nullptr; });
@@ -126,8 +132,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("roctx_mark", [](const std::string& s) {
     if (roctx().mark) roctx().mark(s.c_str());
   });
-  m.def("set_route_tuning", &set_route_tuning, py::arg("prep_items"),
-        "route_prep items per thread (1, 2, 4; 0 = default) -- a tuning knob for experiments");
+  m.def("set_route_tuning", &set_route_tuning, py::arg("prep_items") = 0, py::arg("mode") = 0,
+        "3-pass route_prep items per thread (1, 2, 4; 0 = default); mode 0 = 3-pass prep/scan/scatter "
+        "(default), 1 = single-pass look-back route -- knobs for experiments");
   m.def("table_build_dir", &launch_table_build_dir, py::arg("table"), py::arg("cap"), py::arg("dir"),
         py::arg("n_dir"), py::arg("stream"));
   m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),

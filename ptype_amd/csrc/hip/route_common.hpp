@@ -1,0 +1,162 @@
+// Route kernels' shared device code: registry lookups (hash probe / route
+// directory) and the stable in-order placement of one tile of messages into the
+// epoch slots (wire format v2, see batch.hip).  Used by the 3-pass route
+// (batch.hip) and the single-pass look-back route (route_fused.hip).
+#pragma once
+#include "common.hpp"
+
+namespace ptype {
+
+constexpr int kMaxRanks = 64;
+constexpr int kRouteThreads = 256;
+constexpr int kScatterItems = 2;
+constexpr int kScatterTile = kRouteThreads * kScatterItems;
+constexpr uint32_t kRouteNoActor = 0xffu;  // route word rank byte for a registry miss
+constexpr uint32_t kMaxMbox = 1u << 24;
+
+// Resolve `key` against one probe group held in registers.  Written with named
+// registers and selects, not an indexed array + early return: that form made
+// hipcc spill the group to scratch and serialise every lookup on vmcnt(0).
+__device__ __forceinline__ void check_entry(const uint4& e, uint64_t key, int& rank, uint32_t& mbox, bool& done) {
+  const uint64_t k = ((uint64_t)e.y << 32) | e.x;
+  const bool hit = !done && k == key;
+  const bool miss = !done && k == kKeyEmpty;
+  rank = hit ? (int)e.z : rank;
+  mbox = hit ? e.w : mbox;
+  done = done || hit || miss;
+}
+
+// Linear group probing from group `g` on (the first `skip` slots already checked).
+__device__ __forceinline__ void lookup_from(const TableEntry* __restrict__ t, uint64_t mask, uint64_t key, uint64_t g,
+                                            uint64_t skip, int& rank, uint32_t& mbox, bool& done) {
+  for (uint64_t step = skip; step <= mask && !done; step += kGroup, g = (g + kGroup) & mask) {
+    const uint4* p = reinterpret_cast<const uint4*>(t + g);
+    const uint4 e0 = p[0], e1 = p[1], e2 = p[2], e3 = p[3];  // one 64-B line, four loads in flight
+    check_entry(e0, key, rank, mbox, done);
+    check_entry(e1, key, rank, mbox, done);
+    check_entry(e2, key, rank, mbox, done);
+    check_entry(e3, key, rank, mbox, done);
+  }
+}
+
+__device__ __forceinline__ void lookup_entry(const TableEntry* __restrict__ t, uint64_t mask, uint64_t key,
+                                             int& rank, uint32_t& mbox) {
+  rank = -1;
+  mbox = 0;
+  bool done = false;
+  lookup_from(t, mask, key, probe_start(key, mask), 0, rank, mbox, done);
+}
+
+// K independent lookups with all K first-group lines in flight at once (the
+// registry is L2/MALL resident, so a lookup is latency- not bandwidth-bound:
+// memory-level parallelism per thread is what hides it).  Keys that miss their
+// first group (rare at load factor <= 0.5) continue one at a time.
+template <int K>
+__device__ __forceinline__ void lookup_many(const TableEntry* __restrict__ t, uint64_t mask, const uint64_t (&key)[K],
+                                            int (&rank)[K], uint32_t (&mbox)[K]) {
+  uint4 e[K][kGroup];
+  uint64_t g[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    g[k] = probe_start(key[k], mask);
+    const uint4* p = reinterpret_cast<const uint4*>(t + g[k]);
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) e[k][j] = p[j];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    bool done = false;
+    rank[k] = -1;
+    mbox[k] = 0;
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) check_entry(e[k][j], key[k], rank[k], mbox[k], done);
+    if (!done) lookup_from(t, mask, key[k], (g[k] + kGroup) & mask, kGroup, rank[k], mbox[k], done);
+  }
+}
+
+// Place the tile [tile, min(tile + kScatterTile, hi)) in message order.
+// `route_at(i)` yields message i's route word; `run[d]` is the next free slot
+// position of destination d for this block and is advanced past the tile.
+// Block-level: every thread of the block must call it (two barriers inside).
+template <int NARGS, bool MC, class RouteAt>
+__device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt route_at,
+                                             const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
+                                             const int64_t* __restrict__ a2,
+                                             const uint16_t* __restrict__ method_col, uint32_t method_uniform,
+                                             int R, int64_t C, uint32_t* __restrict__ sendbuf, int64_t req_words,
+                                             int32_t* __restrict__ perm,
+                                             unsigned (&cnt)[kScatterItems][kRouteThreads / kWave][kMaxRanks],
+                                             unsigned* run) {
+  constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
+  const unsigned tid = threadIdx.x, w = tid / kWave, lane = lane_id();
+  int d[kScatterItems];
+  uint32_t rw[kScatterItems], meth[kScatterItems];
+  unsigned rk[kScatterItems];
+  int64_t v[kScatterItems][3];
+  // payload loads first, so they are in flight during the ranking phase
+#pragma unroll
+  for (int k = 0; k < kScatterItems; ++k) {
+    const int64_t i = tile + k * kRouteThreads + tid;
+    const bool in = i < hi;
+    rw[k] = in ? route_at(i) : kRouteNoActor;
+    v[k][0] = in ? a0[i] : 0;
+    v[k][1] = NARGS > 1 && in && a1 ? a1[i] : 0;
+    v[k][2] = NARGS > 2 && in && a2 ? a2[i] : 0;
+    meth[k] = MC ? (in && method_col ? (uint32_t)method_col[i] : method_uniform) : 0u;
+    d[k] = (in && (rw[k] & 0xff) != kRouteNoActor) ? (int)(rw[k] & 0xff) : -1;
+    rk[k] = 0;
+  }
+  // rank within (item k, wave w, destination): ballots, peeled per present destination
+#pragma unroll
+  for (int k = 0; k < kScatterItems; ++k) {
+    for (int x = lane; x < R; x += kWave) cnt[k][w][x] = 0;
+    uint64_t active = __ballot(d[k] >= 0);
+    while (active) {
+      const int leader = __builtin_ctzll(active);
+      const int dl = __shfl(d[k], leader);
+      const uint64_t m = __ballot(d[k] == dl);
+      if (d[k] == dl) rk[k] = mbcnt64(m);
+      if (lane == (unsigned)leader) cnt[k][w][dl] = (unsigned)__popcll(m);
+      active &= ~m;
+    }
+  }
+  __syncthreads();
+  // per destination: exclusive prefix in message order (k-major, then wave)
+  for (int x = tid; x < R; x += blockDim.x) {
+    unsigned r = run[x];
+    for (int k = 0; k < kScatterItems; ++k)
+      for (int ww = 0; ww < kRouteThreads / kWave; ++ww) {
+        const unsigned c = cnt[k][ww][x];
+        cnt[k][ww][x] = r;
+        r += c;
+      }
+    run[x] = r;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kScatterItems; ++k) {
+    const int64_t i = tile + k * kRouteThreads + tid;
+    if (i >= hi) continue;
+    if (d[k] < 0) {
+      perm[i] = -2;
+      continue;
+    }
+    const int64_t pos = (int64_t)cnt[k][w][d[k]] + rk[k];
+    if (pos >= C) {
+      perm[i] = -1;
+      continue;
+    }
+    perm[i] = (int32_t)((int64_t)d[k] * C + pos);
+    uint32_t* o = sendbuf + (int64_t)d[k] * req_words + 4 + pos * kStride;
+    o[0] = rw[k] >> 8;  // local mailbox index at the destination
+    if (MC) o[1] = meth[k] & 0xffffu;
+#pragma unroll
+    for (int j = 0; j < NARGS; ++j) {
+      o[1 + (MC ? 1 : 0) + 2 * j] = (uint32_t)v[k][j];
+      o[2 + (MC ? 1 : 0) + 2 * j] = (uint32_t)((uint64_t)v[k][j] >> 32);
+    }
+  }
+  __syncthreads();
+}
+
+}  // namespace ptype

@@ -15,9 +15,9 @@ from . import _check, _ptr, _stream, hip
 from .records import FLAG_VALID, METHOD_CALC_MULTIPLY, STATUS_NO_ACTOR, STATUS_OVERFLOW, make_requests, split_requests
 from .table import RegistryTable, actor_keys, mix64
 
-# workspace words (int64): [0:4) stats [nomatch, overflow, failed, -]
+# workspace words (int64): [0:4) stats [nomatch, overflow, failed, route-error flag]
 WS_WORDS = 4
-STAT_NOMATCH, STAT_OVERFLOW, STAT_FAILED = 0, 1, 2
+STAT_NOMATCH, STAT_OVERFLOW, STAT_FAILED, STAT_ROUTE_ERROR = 0, 1, 2, 3
 ROUTE_NO_ACTOR = 0xFF
 MAX_MBOX = 1 << 24  # route word = rank | mbox << 8
 
@@ -143,12 +143,17 @@ FULL_FORMAT = WireFormat(3, True)  # 32-B records: any batch fits
 
 
 class RouteWorkspace:
-    """Per-epoch scratch of the route kernels (route words + block histograms)."""
+    """Per-epoch scratch of the route kernels: the single-pass route's look-back
+    words (ticket/epoch + per-block per-destination prefix states, zeroed once)
+    and the 3-pass route's route words + block histograms."""
 
     def __init__(self, M: int, R: int, device):
         device = torch.device(device)
-        G, _ = hip().route_grid(max(M, 1)) if device.type == "cuda" else (1, M)
+        cuda = device.type == "cuda"
+        G, _ = hip().route_grid(max(M, 1)) if cuda else (1, M)
+        Gf, _ = hip().route_fused_grid(max(M, 1)) if cuda else (1, M)
         self.M, self.R = M, R
+        self.lb = torch.zeros(1 + Gf * (R + 1), dtype=torch.int64, device=device)
         self.route = torch.empty(max(M, 1), dtype=torch.int32, device=device)
         self.hist = torch.empty(G * (R + 1), dtype=torch.int32, device=device)
         self.ws = new_workspace(device)
@@ -189,7 +194,8 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
         d, n_dir = table.directory()
         hip().route(_ptr(batch.actor), _ptr(batch.a0), _ptr(batch.a1), _ptr(batch.a2), _ptr(mcol), method_u, M,
                     _ptr(table.table), table.cap, _ptr(d), n_dir, R, C, fmt.nargs, fmt.method_col, _ptr(sendbuf),
-                    _ptr(perm), _ptr(rws.route), _ptr(rws.hist), _ptr(rws.ws), rank_self, _stream(batch.actor))
+                    _ptr(perm), _ptr(rws.route), _ptr(rws.hist), _ptr(rws.lb), _ptr(rws.ws), rank_self,
+                    _stream(batch.actor))
         return sendbuf, perm, ws_stats(rws.ws)
     # ---- CPU reference: bit-identical layout (stable message order per destination) ----
     actor = batch.actor.to(torch.int64) & 0xFFFFFFFF

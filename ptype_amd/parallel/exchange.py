@@ -217,6 +217,8 @@ class ActorExchange:
             s.nomatch += w[B.STAT_NOMATCH]
             s.overflow += w[B.STAT_OVERFLOW]
             s.failed += w[B.STAT_FAILED]
+            if w[B.STAT_ROUTE_ERROR]:
+                raise RuntimeError("route look-back stalled: epoch results are invalid")
         return s
 
 

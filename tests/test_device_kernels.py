@@ -237,8 +237,8 @@ def test_gpu_route_dispatch_complete(R, fmt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("items", [1, 2, 4])
-def test_gpu_route_directory_matches_hash_probe(items):
+@pytest.mark.parametrize("items,mode", [(0, 1), (1, 0), (2, 0), (4, 0)])
+def test_gpu_route_directory_matches_hash_probe(items, mode):
     """K5b: routing through the dense directory is bit-identical to probing the
     hash table -- ids inside/outside the directory range, deleted ids, and an
     entry too wide for a route word (directory fallback to the probe)."""
@@ -254,10 +254,10 @@ def test_gpu_route_directory_matches_hash_probe(items):
     req = B.gen_requests(M, n_actors + 50, METHOD_CALC_MULTIPLY, seed=99, device="cuda")  # some ids unregistered
     ref = B.gen_requests(M, n_actors + 50, METHOD_CALC_MULTIPLY, seed=99, device="cpu")
     try:
-        ops.hip().set_route_tuning(items)
+        ops.hip().set_route_tuning(items, mode)
         send, perm, stats = B.route(req, g, R, C)
     finally:
-        ops.hip().set_route_tuning(0)
+        ops.hip().set_route_tuning(0, 0)
     rsend, rperm, rstats = B.route(ref, c, R, C)
     assert torch.equal(perm.cpu(), rperm)
     assert _regions_equal(send, rsend, R, C, B.FULL_FORMAT)
@@ -269,6 +269,45 @@ def test_gpu_route_directory_matches_hash_probe(items):
     send, perm, _ = B.route(req, g, R, C)
     rsend, rperm, _ = B.route(ref, c, R, C)
     assert torch.equal(perm.cpu(), rperm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,R,C,fmt", [(0, 3, 64, B.WireFormat(2, False)), (100, 2, 64, B.WireFormat(2, False)),
+                                       (4096, 1, 5000, B.FULL_FORMAT), (70_001, 5, 9000, B.WireFormat(3, False)),
+                                       (1_000_003, 8, 130_000, B.WireFormat(2, True))])
+def test_gpu_route_single_pass_matches_three_pass(M, R, C, fmt):
+    """The 3-pass route (default) and the single-pass look-back route produce the same bytes
+    as the CPU reference: headers, records, perm, statistics -- including empty
+    batches, sub-block batches, overflowing destinations and unknown actors."""
+    n_actors = 3000
+    g = RegistryTable(2 * n_actors, device="cuda")
+    c = RegistryTable(2 * n_actors, device="cpu")
+    _populate(g, n_actors, R)
+    _populate(c, n_actors, R)
+    g.enable_directory(n_actors)
+    req = B.gen_requests(M, n_actors + 100, METHOD_CALC_MULTIPLY, seed=M + R, device="cuda")
+    ref = B.gen_requests(M, n_actors + 100, METHOD_CALC_MULTIPLY, seed=M + R, device="cpu")
+    if fmt.method_col:
+        req.method = (req.actor % 3 + 1).to(torch.int16)
+        ref.method = (ref.actor % 3 + 1).to(torch.int16)
+    if fmt.nargs == 3:
+        req.a2, ref.a2 = req.a1 * 3, ref.a1 * 3
+    rsend, rperm, rstats = B.route(ref, c, R, C, fmt=fmt)
+    outs = []
+    for mode in (0, 1):
+        ops.hip().set_route_tuning(0, mode)
+        try:
+            for _ in range(2):  # twice: the look-back epoch must advance cleanly between launches
+                send, perm, stats = B.route(req, g, R, C, fmt=fmt)
+        finally:
+            ops.hip().set_route_tuning(0, 0)
+        torch.cuda.synchronize()
+        assert torch.equal(perm.cpu(), rperm), f"mode {mode}"
+        assert _regions_equal(send, rsend, R, C, fmt), f"mode {mode}"
+        assert stats.cpu().tolist()[:2] == rstats.tolist()[:2], f"mode {mode}"
+        outs.append(stats.cpu().tolist()[:2])
+    if M > 0:
+        assert rstats.tolist()[0] > 0  # unknown actors were exercised
 
 
 @pytest.mark.gpu

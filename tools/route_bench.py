@@ -60,11 +60,12 @@ def main():
         for use_dir in (False, True):
             if use_dir:
                 t.enable_directory(n_actors)
-            for items in (1, 2, 4):
-                hip().set_route_tuning(items)
+            for mode, items in ((1, 0), (0, 1), (0, 2), (0, 4)):
+                hip().set_route_tuning(items, mode)
                 us = timed(lambda: B.route(req, t, R, C, sendbuf=send, perm=perm, rws=rws, fmt=fmt), a.iters)
-                rows.append({"actors": n_actors, "dir": use_dir, "items": items, "route_us": round(us, 1)})
-            hip().set_route_tuning(0)
+                rows.append({"actors": n_actors, "dir": use_dir, "route": "single-pass" if mode == 1 else "3-pass",
+                             "items": items, "route_us": round(us, 1)})
+            hip().set_route_tuning(0, 0)
             t.dir = None
         d_us = timed(lambda: B.dispatch(send, R, C, reply=reply, ws=rws.ws, expected_per_rank=M // R,
                                           fmt=fmt), a.iters)
