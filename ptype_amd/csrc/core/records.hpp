@@ -21,7 +21,9 @@ enum MethodId : uint16_t {
   kEcho = 3,                // reply = a0
   kRetryTest = 4,           // stateful: fails until per-actor count >= a0 (rpc_test.go:55-77)
   kCounterAdd = 5,          // stateful: state += a0; reply = new state
-  kMethodCount = 6,
+  kForward = 6,             // actor-to-actor "tell": state += 1; if a1 > 0 emit Forward to actor a0
+                            // with (next = (a0 + stride) % n, a1 - 1, a2); a2 = stride | n << 32
+  kMethodCount = 7,
 };
 
 enum RecordFlags : uint16_t {

@@ -38,6 +38,8 @@
 //   i.e. 9 B per reply instead of a 16-B record.  The reverse all-to-all brings
 //   every reply back to the slot its request left from; `perm[i]` remembers it
 //   as d * C + pos (-1 overflow, -2 no actor).
+#include <vector>
+
 #include "common.hpp"
 #include "handlers.hpp"
 #include "route_common.hpp"
@@ -200,7 +202,8 @@ template <int NARGS, bool MC>
 __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restrict__ recv, int64_t req_words,
                                                        int64_t C, uint32_t* __restrict__ reply, int64_t rep_words,
                                                        int64_t* __restrict__ state, uint32_t n_state,
-                                                       uint64_t delay_ticks, unsigned long long* __restrict__ stats) {
+                                                       uint64_t delay_ticks, unsigned long long* __restrict__ stats,
+                                                       OutboxView ob) {
   constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
   const int d = blockIdx.y;
   const uint32_t* rq = recv + (int64_t)d * req_words;
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
     m.a2 = 0;
     if constexpr (NARGS > 1) m.a1 = (int64_t)(((uint64_t)wv[o + 3] << 32) | wv[o + 2]);
     if constexpr (NARGS > 2) m.a2 = (int64_t)(((uint64_t)wv[o + 5] << 32) | wv[o + 4]);
-    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks);
+    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob.cap ? &ob : nullptr);
     failed += rr.status != kStatusOk;
     vals[s] = rr.value;
     sts[s] = (uint8_t)rr.status;
@@ -399,7 +402,18 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
 
 void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintptr_t reply, uintptr_t state,
                      uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
-                     uintptr_t stream) {
+                     const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, uintptr_t stream) {
+  OutboxView ob;
+  if (outbox_cap) {
+    if (outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
+    ob.actor = (uint32_t*)outbox[0];
+    ob.a0 = (int64_t*)outbox[1];
+    ob.a1 = (int64_t*)outbox[2];
+    ob.a2 = (int64_t*)outbox[3];
+    ob.method = (uint16_t*)outbox[4];
+    ob.count = (unsigned long long*)outbox[5];
+    ob.cap = outbox_cap;
+  }
   check_format(nargs, C, R);
   const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
   const unsigned gx = grid_cap(per, 256, (unsigned)(4096 / R > 0 ? 4096 / R : 1));
@@ -407,7 +421,7 @@ void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintp
 #define PT_DISPATCH(NA, MCV)                                                                                    \
   hipLaunchKernelGGL((dispatch_kernel<NA, MCV>), dim3(gx, R), dim3(256), 0, as_stream(stream),                  \
                      (const uint32_t*)recv, req_words, C, (uint32_t*)reply, rep_words, (int64_t*)state, n_state, \
-                     delay_ticks, (unsigned long long*)stats)
+                     delay_ticks, (unsigned long long*)stats, ob)
   PT_FORMAT_SWITCH(nargs, mc, PT_DISPATCH)
 #undef PT_DISPATCH
   PT_HIP_CHECK(hipGetLastError());

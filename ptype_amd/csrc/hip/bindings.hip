@@ -56,7 +56,7 @@ void set_route_tuning(int, int);
 int64_t route_fused_grid(int64_t, int64_t*);
 void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t);
 void launch_dispatch(uintptr_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uint32_t, uint64_t, uintptr_t, int64_t,
-                     uintptr_t);
+                     const std::vector<uintptr_t>&, uint64_t, uintptr_t);
 void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 int64_t wire_req_words(int64_t, int, bool);
 int64_t wire_rep_words(int64_t);
@@ -139,7 +139,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("n_dir"), py::arg("stream"));
   m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
         py::arg("reply"), py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),
-        py::arg("expected_per_rank"), py::arg("stream"));
+        py::arg("expected_per_rank"), py::arg("outbox"), py::arg("outbox_cap"), py::arg("stream"));
   m.def("complete", &launch_complete, py::arg("rep"), py::arg("C"), py::arg("perm"), py::arg("M"),
         py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("stream"));
   m.def("snapshot_copy", &launch_snapshot_copy, py::arg("dst"), py::arg("src"), py::arg("n16"),

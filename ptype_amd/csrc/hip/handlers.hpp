@@ -9,13 +9,50 @@
 
 namespace ptype {
 
+// Device outbox: messages emitted by handlers -- actor-to-actor
+// sends that never leave the GPU until the next exchange epoch routes them.
+// SoA columns in HBM, like a client batch; slots are reserved with ONE atomic
+// per wave (ballot over the emitting lanes, leader adds the popcount, lanes
+// take base + rank).  A full outbox counts drops instead of overwriting.
+struct OutboxView {
+  uint32_t* actor = nullptr;
+  int64_t* a0 = nullptr;
+  int64_t* a1 = nullptr;
+  int64_t* a2 = nullptr;
+  uint16_t* method = nullptr;
+  unsigned long long* count = nullptr;  // [0] reserved slots, [1] dropped
+  uint64_t cap = 0;
+};
+
+// Called by the lanes that emit, from inside a (possibly divergent) branch.
+__device__ __forceinline__ void outbox_emit(const OutboxView& ob, uint32_t actor, uint16_t method, int64_t a0,
+                                            int64_t a1, int64_t a2) {
+  const uint64_t m = __ballot(1);  // the lanes executing this emit
+  const int leader = __builtin_ctzll(m);
+  const unsigned rank = mbcnt64(m);
+  unsigned long long base = 0;
+  if (lane_id() == (unsigned)leader) base = atomicAdd(&ob.count[0], (unsigned long long)__popcll(m));
+  base = __shfl(base, leader);
+  const uint64_t slot = base + rank;
+  if (slot < ob.cap) {
+    ob.actor[slot] = actor;
+    ob.method[slot] = method;
+    ob.a0[slot] = a0;
+    ob.a1[slot] = a1;
+    ob.a2[slot] = a2;
+  } else {
+    atomicAdd(&ob.count[1], 1ull);
+  }
+}
+
 // Runs one request against the actor state of the mailbox it was routed to.
 // `state` holds one int64 per local mailbox (the reference's `type Calculator int`
 // receiver is exactly one machine int of actor state).  `delay_ticks` is the
 // per-candidate delay of Prime.Check in 100 MHz ticks (250 ms in the reference;
 // 0 for throughput runs).
 __device__ __forceinline__ ReplyRecord run_handler(const MsgRecord& m, int64_t* __restrict__ state,
-                                                   uint32_t n_state, uint64_t delay_ticks) {
+                                                   uint32_t n_state, uint64_t delay_ticks,
+                                                   const OutboxView* ob = nullptr) {
   ReplyRecord r;
   r.value = 0;
   r.status = kStatusOk;
@@ -71,6 +108,23 @@ __device__ __forceinline__ ReplyRecord run_handler(const MsgRecord& m, int64_t* 
       if (m.actor < n_state) {
         r.value = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(state + m.actor),
                                      (unsigned long long)m.a0) + m.a0;
+      } else {
+        r.status = kStatusNoActor;
+      }
+      break;
+    case kForward:
+      // a hop of a message chain: count the visit, pass the token on (device-side send)
+      if (m.actor < n_state) {
+        r.value = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(state + m.actor), 1ull) + 1;
+        if (m.a1 > 0) {
+          if (ob && ob->cap) {
+            const uint64_t stride = (uint64_t)m.a2 & 0xffffffffull, n = (uint64_t)m.a2 >> 32;
+            const uint64_t next = n ? ((uint64_t)m.a0 + stride) % n : (uint64_t)m.a0;
+            outbox_emit(*ob, (uint32_t)m.a0, kForward, (int64_t)next, m.a1 - 1, m.a2);
+          } else {
+            r.status = kStatusFailed;  // no outbox bound: the send cannot happen
+          }
+        }
       } else {
         r.status = kStatusNoActor;
       }

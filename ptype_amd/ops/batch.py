@@ -239,11 +239,11 @@ def _words_i64(lo: torch.Tensor, hi: torch.Tensor) -> torch.Tensor:
     return (lo.to(torch.int64) & 0xFFFFFFFF) | (hi.to(torch.int64) << 32)
 
 
-def _handler_ref(method, actor, a0, a1, a2, state):
+def _handler_ref(method, actor, a0, a1, a2, state, outbox=None):
     """Plain-PyTorch reference of the device handler table (handlers.hpp)."""
     from .records import (METHOD_CALC_MULTIPLY as MUL, METHOD_COUNTER_ADD as CADD, METHOD_ECHO as ECHO,
-                          METHOD_PRIME_CHECK as PRIME, METHOD_RETRY_TEST as RETRY, STATUS_FAILED,
-                          STATUS_NO_METHOD)
+                          METHOD_FORWARD as FWD, METHOD_PRIME_CHECK as PRIME, METHOD_RETRY_TEST as RETRY,
+                          STATUS_FAILED, STATUS_NO_METHOD)
     n = method.numel()
     value = torch.zeros(n, dtype=torch.int64)
     status = torch.full((n,), STATUS_NO_METHOD, dtype=torch.int64)
@@ -277,17 +277,33 @@ def _handler_ref(method, actor, a0, a1, a2, state):
         else:
             state[a] += int(a0[i])
             value[i], status[i] = int(state[a]), 0
+    for i in torch.nonzero(method == FWD).flatten().tolist():
+        a = int(actor[i])
+        if state is None or a >= state.numel():
+            status[i] = STATUS_NO_ACTOR
+            continue
+        state[a] += 1
+        value[i], status[i] = int(state[a]), 0
+        if int(a1[i]) > 0:
+            if outbox is None:
+                status[i] = STATUS_FAILED
+                continue
+            w = int(a2[i]) & 0xFFFFFFFFFFFFFFFF
+            stride, n = w & 0xFFFFFFFF, w >> 32
+            nxt = (int(a0[i]) + stride) % n if n else int(a0[i])
+            outbox.emit_cpu(int(a0[i]) & 0xFFFFFFFF, FWD, nxt, int(a1[i]) - 1, int(a2[i]))
     return value, status
 
 
 def dispatch(recv: torch.Tensor, R: int, C: int, state: torch.Tensor | None = None, delay_us: int = 0,
              reply: torch.Tensor | None = None, ws: torch.Tensor | None = None, expected_per_rank: int = 0,
-             fmt: WireFormat = FULL_FORMAT):
+             fmt: WireFormat = FULL_FORMAT, outbox=None):
     """K3 (batch form): run every delivered record through the handler table.
 
     ``recv`` is ``int32[R * fmt.req_words(C)]`` (one request region per source
     rank); returns ``int32[R * rep_words(C)]`` reply regions (header, int64
-    values, u8 statuses) in the same geometry.
+    values, u8 statuses) in the same geometry.  Handlers that send (``Forward``)
+    append to ``outbox`` (a ``DeviceOutbox``).
     """
     _check(recv, torch.int32, 1, "recv")
     dev = recv.device
@@ -298,8 +314,9 @@ def dispatch(recv: torch.Tensor, R: int, C: int, state: torch.Tensor | None = No
         if ws is None:
             ws = new_workspace(dev)
         n_state = 0 if state is None else state.numel()
+        ob, ob_cap = outbox.view() if outbox is not None else ([], 0)
         hip().dispatch(_ptr(recv), R, C, fmt.nargs, fmt.method_col, _ptr(reply), _ptr(state), n_state,
-                       int(delay_us) * 100, _ptr(ws), int(expected_per_rank), _stream(recv))
+                       int(delay_us) * 100, _ptr(ws), int(expected_per_rank), ob, ob_cap, _stream(recv))
         return reply
     reply.zero_()
     for d in range(R):
@@ -317,7 +334,7 @@ def dispatch(recv: torch.Tensor, R: int, C: int, state: torch.Tensor | None = No
         method = (rows[:, 1].to(torch.int64) & 0xFFFF) if fmt.method_col else torch.full((cnt,), int(h[3]) & 0xFFFF)
         args = [_words_i64(rows[:, o + 2 * j], rows[:, o + 2 * j + 1]) for j in range(fmt.nargs)]
         args += [torch.zeros(cnt, dtype=torch.int64)] * (3 - fmt.nargs)
-        v, stt = _handler_ref(method, actor, args[0], args[1], args[2], state)
+        v, stt = _handler_ref(method, actor, args[0], args[1], args[2], state, outbox)
         rr[4:4 + 2 * C].view(torch.int64)[:cnt] = v
         rr[4 + 2 * C:].view(torch.uint8)[:cnt] = stt.to(torch.uint8)
     return reply

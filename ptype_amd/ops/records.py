@@ -9,6 +9,7 @@ METHOD_PRIME_CHECK = 2
 METHOD_ECHO = 3
 METHOD_RETRY_TEST = 4
 METHOD_COUNTER_ADD = 5
+METHOD_FORWARD = 6  # actor-to-actor tell: count the visit, emit Forward to a0 while a1 > 0
 
 FLAG_VALID = 1
 FLAG_ROUTED = 2

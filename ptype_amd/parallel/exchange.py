@@ -110,6 +110,7 @@ class ActorExchange:
         self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device, self.force_collectives,
                                 fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 2))]
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
+        self.outbox = None  # DeviceOutbox that dispatched handlers send into (set by pump)
         self.counters = EpochStats()
 
     # ------------------------------------------------------------------
@@ -177,7 +178,7 @@ class ActorExchange:
         wq, wr = self.world * fmt.req_words(self.C), self.world * B.WireFormat.rep_words(self.C)
         with trace.range("ptype.dispatch"):
             B.dispatch(bufs.recv[:wq], self.world, self.C, self.state, self.delay_us, reply=bufs.reply[:wr], ws=bufs.ws,
-                       expected_per_rank=max(1, m // self.world), fmt=fmt)
+                       expected_per_rank=max(1, m // self.world), fmt=fmt, outbox=self.outbox)
         return (i, self._a2a(bufs.back[:wr], bufs.reply[:wr]), bufs)
 
     # ------------------------------------------------------------------
@@ -191,6 +192,45 @@ class ActorExchange:
         if (self.world > 1 or self.force_collectives) and not allow_collectives:
             raise RuntimeError("capture: collectives in a graph are opt-in (allow_collectives=True)")
         return SendGraph(self, req, out_val, out_status, prologue)
+
+    # ------------------------------------------------------------------
+    def pump(self, outbox, initial: B.MsgBatch | None = None, max_epochs: int = 1 << 20):
+        """Actor-to-actor messaging on the device: deliver ``initial`` (if any),
+        then keep routing whatever the dispatched handlers emitted into
+        ``outbox`` until every rank's outbox is empty.  Fire-and-forget ("tell")
+        semantics: replies of emitted messages are discarded; overflowed slots are
+        re-sent.  Collective; the host reads one count per epoch.
+        Returns ``(epochs, messages delivered by this rank's sends)``."""
+        prev, self.outbox = self.outbox, outbox
+        per_send = self.max_chunk * self.chunks
+        epochs = delivered = 0
+        try:
+            if initial is not None:  # every rank passes one (possibly empty), same columns
+                m0 = mx0 = initial.M
+                if self.world > 1:
+                    t = torch.tensor([m0], dtype=torch.int64, device=self.device)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                    mx0 = int(t.item())
+                for lo in range(0, mx0, per_send):
+                    self.send_all(initial.slice(min(lo, m0), min(m0, lo + per_send)))
+                delivered += m0
+            while epochs < max_epochs:
+                n = outbox.pending()
+                mx = n
+                if self.world > 1:
+                    t = torch.tensor([n], dtype=torch.int64, device=self.device)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                    mx = int(t.item())
+                if mx == 0:
+                    break
+                batch = outbox.take(n)
+                for lo in range(0, mx, per_send):  # same number of collective sends on every rank
+                    self.send_all(batch.slice(min(lo, n), min(n, lo + per_send)))
+                delivered += n
+                epochs += 1
+        finally:
+            self.outbox = prev
+        return epochs, delivered
 
     # ------------------------------------------------------------------
     def send_all(self, req: B.MsgBatch, max_epochs: int = 16):
