@@ -49,10 +49,38 @@ def _newest_header(d: str) -> float:
     return t
 
 
-def _run(cmd: list[str]) -> None:
+def _run(cmd: list[str], log: str | None = None) -> None:
     p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if p.returncode != 0:
         raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + p.stdout)
+    if log:
+        with open(log, "w") as f:
+            f.write(p.stdout)
+
+
+def _compile_logged(jobs, max_workers):
+    with ThreadPoolExecutor(max_workers=max_workers) as ex:
+        list(ex.map(lambda j: _run(j[0], j[1]), jobs))
+
+
+def kernel_resources() -> dict:
+    """Per-kernel VGPRs / scratch / occupancy from the last hipcc compile of each
+    object (``-Rpass-analysis=kernel-resource-usage`` remarks, kept next to the
+    objects).  A kernel with scratch > 0 is a performance bug on gfx950."""
+    import re
+
+    out = {}
+    for res in glob.glob(os.path.join(ROOT, "build", "hip", "*.res")):
+        cur = None
+        for line in open(res):
+            m = re.search(r"Function Name: (\S+)", line)
+            if m:
+                cur = out.setdefault(m.group(1), {})
+                continue
+            m = re.search(r"(VGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\d+)", line)
+            if m and cur is not None:
+                cur[m.group(1).split(" ")[0]] = int(m.group(2))
+    return out
 
 
 def _compile_all(jobs, max_workers):
@@ -134,8 +162,9 @@ def build_hip(verbose: bool = False) -> str:
         objs.append(o)
         lang = ["-x", "hip"]
         if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_t):
-            jobs.append([hipcc] + lang + flags + ["-c", s, "-o", o])
-    _compile_all(jobs, 8)
+            jobs.append(([hipcc] + lang + flags + ["-Rpass-analysis=kernel-resource-usage", "-c", s, "-o", o],
+                         o[:-2] + ".res"))
+    _compile_logged(jobs, 8)
     target = os.path.join(PKG, "_hip" + EXT)
     tl = _torch_lib_dir()
     if jobs or not os.path.exists(target) or os.path.getmtime(target) < max(os.path.getmtime(o) for o in objs):

@@ -198,13 +198,46 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
 }
 
 // K3 (batch form).  grid.y = source rank, grid.x tiles the delivered range.
+// FIXED != 0: the slot's method is known (uniform per source slot, no method
+// column), so the handler switch constant-folds and the loop body is just that
+// handler; FIXED == 0 switches per message.
+template <int NARGS, bool MC, int FIXED>
+__device__ __forceinline__ unsigned long long dispatch_range(const uint32_t* __restrict__ rq, int64_t count,
+                                                             uint32_t hdr_method, int64_t* __restrict__ vals,
+                                                             uint8_t* __restrict__ sts, int64_t* __restrict__ state,
+                                                             uint32_t n_state, uint64_t delay_ticks,
+                                                             OutboxView ob) {
+  constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
+  unsigned long long failed = 0;
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count; s += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t* r = rq + 4 + s * kStride;
+    uint32_t wv[kStride];
+#pragma unroll
+    for (int j = 0; j < kStride; ++j) wv[j] = r[j];
+    MsgRecord m;
+    m.actor = wv[0];
+    m.method = (uint16_t)(FIXED ? FIXED : (MC ? (wv[1] & 0xffffu) : hdr_method));
+    m.flags = kFlagValid | kFlagRouted;
+    constexpr int o = 1 + (MC ? 1 : 0);
+    m.a0 = (int64_t)(((uint64_t)wv[o + 1] << 32) | wv[o]);
+    m.a1 = 0;
+    m.a2 = 0;
+    if constexpr (NARGS > 1) m.a1 = (int64_t)(((uint64_t)wv[o + 3] << 32) | wv[o + 2]);
+    if constexpr (NARGS > 2) m.a2 = (int64_t)(((uint64_t)wv[o + 5] << 32) | wv[o + 4]);
+    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
+    failed += rr.status != kStatusOk;
+    vals[s] = rr.value;
+    sts[s] = (uint8_t)rr.status;
+  }
+  return failed;
+}
+
 template <int NARGS, bool MC>
 __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restrict__ recv, int64_t req_words,
                                                        int64_t C, uint32_t* __restrict__ reply, int64_t rep_words,
                                                        int64_t* __restrict__ state, uint32_t n_state,
                                                        uint64_t delay_ticks, unsigned long long* __restrict__ stats,
                                                        OutboxView ob) {
-  constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
   const int d = blockIdx.y;
   const uint32_t* rq = recv + (int64_t)d * req_words;
   const uint4 h = *reinterpret_cast<const uint4*>(rq);
@@ -215,26 +248,26 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
   uint8_t* sts = reinterpret_cast<uint8_t*>(rp + 4 + 2 * C);
   if (blockIdx.x == 0 && threadIdx.x == 0)  // reply header: delivered count (sender audits it)
     *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
-  unsigned long long failed = 0;
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count; s += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t* r = rq + 4 + s * kStride;
-    uint32_t wv[kStride];
-#pragma unroll
-    for (int j = 0; j < kStride; ++j) wv[j] = r[j];
-    MsgRecord m;
-    m.actor = wv[0];
-    m.method = (uint16_t)(MC ? (wv[1] & 0xffffu) : (h.w & 0xffffu));
-    m.flags = kFlagValid | kFlagRouted;
-    constexpr int o = 1 + (MC ? 1 : 0);
-    m.a0 = (int64_t)(((uint64_t)wv[o + 1] << 32) | wv[o]);
-    m.a1 = 0;
-    m.a2 = 0;
-    if constexpr (NARGS > 1) m.a1 = (int64_t)(((uint64_t)wv[o + 3] << 32) | wv[o + 2]);
-    if constexpr (NARGS > 2) m.a2 = (int64_t)(((uint64_t)wv[o + 5] << 32) | wv[o + 4]);
-    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob.cap ? &ob : nullptr);
-    failed += rr.status != kStatusOk;
-    vals[s] = rr.value;
-    sts[s] = (uint8_t)rr.status;
+  const OutboxView obp = ob;
+  const uint32_t hm = h.w & 0xffffu;
+  unsigned long long failed;
+  if constexpr (!MC) {
+    switch (hm) {  // uniform per slot: one specialised loop per hot method
+      case kCalculatorMultiply:
+        failed = dispatch_range<NARGS, MC, kCalculatorMultiply>(rq, count, hm, vals, sts, state, n_state,
+                                                                delay_ticks, obp);
+        break;
+      case kPrimeCheck:
+        failed = dispatch_range<NARGS, MC, kPrimeCheck>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp);
+        break;
+      case kCounterAdd:
+        failed = dispatch_range<NARGS, MC, kCounterAdd>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp);
+        break;
+      default:
+        failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp);
+    }
+  } else {
+    failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp);
   }
   for (int off = 32; off > 0; off >>= 1) failed += __shfl_xor(failed, off);
   if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);

@@ -24,8 +24,10 @@ struct OutboxView {
   uint64_t cap = 0;
 };
 
-// Called by the lanes that emit, from inside a (possibly divergent) branch.
-__device__ __forceinline__ void outbox_emit(const OutboxView& ob, uint32_t actor, uint16_t method, int64_t a0,
+// Called by the lanes that emit, from inside a (possibly divergent) branch.  The
+// view travels BY VALUE everywhere: taking the address of the kernel argument
+// made hipcc copy it to scratch in every thread (64 B/lane of HBM writes).
+__device__ __forceinline__ void outbox_emit(OutboxView ob, uint32_t actor, uint16_t method, int64_t a0,
                                             int64_t a1, int64_t a2) {
   const uint64_t m = __ballot(1);  // the lanes executing this emit
   const int leader = __builtin_ctzll(m);
@@ -52,7 +54,7 @@ __device__ __forceinline__ void outbox_emit(const OutboxView& ob, uint32_t actor
 // 0 for throughput runs).
 __device__ __forceinline__ ReplyRecord run_handler(const MsgRecord& m, int64_t* __restrict__ state,
                                                    uint32_t n_state, uint64_t delay_ticks,
-                                                   const OutboxView* ob = nullptr) {
+                                                   OutboxView ob = OutboxView()) {
   ReplyRecord r;
   r.value = 0;
   r.status = kStatusOk;
@@ -117,10 +119,10 @@ __device__ __forceinline__ ReplyRecord run_handler(const MsgRecord& m, int64_t* 
       if (m.actor < n_state) {
         r.value = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(state + m.actor), 1ull) + 1;
         if (m.a1 > 0) {
-          if (ob && ob->cap) {
+          if (ob.cap) {
             const uint64_t stride = (uint64_t)m.a2 & 0xffffffffull, n = (uint64_t)m.a2 >> 32;
             const uint64_t next = n ? ((uint64_t)m.a0 + stride) % n : (uint64_t)m.a0;
-            outbox_emit(*ob, (uint32_t)m.a0, kForward, (int64_t)next, m.a1 - 1, m.a2);
+            outbox_emit(ob, (uint32_t)m.a0, kForward, (int64_t)next, m.a1 - 1, m.a2);
           } else {
             r.status = kStatusFailed;  // no outbox bound: the send cannot happen
           }

@@ -42,9 +42,10 @@ def _ring(device, world=1, rank=0, n_per=64, T=20, hops=7, stride=5):
     ids = torch.arange(n, dtype=torch.int64)
     table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
     state = torch.zeros(n_per, dtype=torch.int64, device=device)
-    ex = ActorExchange(table, 4096, chunks=2, state=state)
+    cap = max(4096, T)
+    ex = ActorExchange(table, cap, chunks=2, state=state)
     starts = [(rank * 131 + 17 * t) % n for t in range(T)]
-    outbox = DeviceOutbox(4096, device=device)
+    outbox = DeviceOutbox(cap, device=device)
     epochs, delivered = ex.pump(outbox, initial=_tokens(n, starts, hops, stride, device))
     return ex, state, starts, epochs, delivered, outbox, n
 

@@ -430,3 +430,19 @@ def test_gpu_send_graph_replay():
         seen.append(req.actor[:8].cpu().tolist())
     assert seen[0] != seen[1] != seen[2]
     assert ex.stats().sent >= 3 * M
+
+
+def test_no_kernel_spills_to_scratch():
+    """Every gfx950 kernel compiles without scratch (private memory): twice a
+    silent spill cost 3x (an indexed probe group) and 56 MB of HBM writes per
+    epoch (the address of a by-value kernel argument).  Reads the resource-usage
+    remarks the build keeps next to the objects."""
+    from ptype_amd import _build
+
+    _build.build_hip()
+    res = _build.kernel_resources()
+    assert len(res) >= 20, "resource remarks missing (hipcc -Rpass-analysis=kernel-resource-usage)"
+    spills = {k: v for k, v in res.items() if v.get("ScratchSize", 0) > 0}
+    assert not spills, spills
+    low = {k: v for k, v in res.items() if "route" in k and v.get("Occupancy", 8) < 4}
+    assert not low, low

@@ -9,6 +9,8 @@
   optimus    optimus fan-out: Prime.Check ranges of many targets as one batch
              per step across every rank (torchrun for N GPUs: RCCL all-to-all
              dispatch), per-candidate delay 0.
+  tell       device-side actor-to-actor messaging: token ring of Forward tells
+             emitted by GPU handlers into the HBM outbox, pumped epoch by epoch.
   registry   1M-actor registry stress: GPU upsert / probe lookup / directory
              build / lease sweep / pack + snapshot to pinned host DRAM, and the
              control-plane store: puts with Raft snapshots + WAL.
@@ -189,6 +191,63 @@ def optimus(a):
         dist.destroy_process_group()
 
 
+# --------------------------------------------------------------------------- tell
+def tell(a):
+    """Device-side actor-to-actor messaging: a token ring where every hop is a
+    message emitted by a GPU handler into the HBM outbox and routed by the next
+    exchange epoch (torchrun for N GPUs: hops cross GPUs over RCCL)."""
+    import torch.distributed as dist
+
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.outbox import DeviceOutbox
+    from ptype_amd.ops.records import METHOD_FORWARD
+    from ptype_amd.ops.table import RegistryTable, actor_keys
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    per, T, H = a.actors, a.tokens, a.hops
+    n = per * world
+    table = RegistryTable(2 * n, device=dev)
+    ids = torch.arange(n, dtype=torch.int64)
+    table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
+    table.enable_directory(n)
+    state = torch.zeros(per, dtype=torch.int64, device=dev)
+    ex = ActorExchange(table, T, chunks=1, state=state)
+    outbox = DeviceOutbox(T, device=dev)
+    stride = 7919
+    starts = (torch.arange(T, dtype=torch.int64, device=dev) * 97 + rank * 13) % n
+    init = B.MsgBatch(starts.to(torch.int32), (starts + stride) % n, torch.full((T,), H, dtype=torch.int64, device=dev),
+                      torch.full((T,), stride | (n << 32), dtype=torch.int64, device=dev), METHOD_FORWARD)
+    ex.pump(outbox, initial=init.slice(0, min(T, 1024)))  # warm-up
+    state.zero_()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier(device_ids=[local])
+    t0 = time.perf_counter()
+    epochs, delivered = ex.pump(outbox, initial=init)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    tot = torch.tensor([delivered, int(state.sum())], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    assert int(tot[1]) == T * world * (H + 1) and outbox.dropped == 0, (tot.tolist(), outbox.dropped)
+    if rank == 0:
+        _emit({"config": "device-side actor messaging (token ring, Forward tells via HBM outbox)", "n_gpus": world,
+               "tokens_per_gpu": T, "hops": H, "epochs": epochs, "messages": int(tot[0]),
+               "messages_per_s": int(tot[0]) / el, "ms_per_epoch": el / max(epochs, 1) * 1e3})
+    if world > 1:
+        dist.destroy_process_group()
+
+
 # --------------------------------------------------------------------------- registry
 def registry(a):
     from ptype_amd.ops import batch as B
@@ -281,7 +340,7 @@ def registry(a):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("which", choices=["host-rpc", "gpu-1m", "optimus", "registry"])
+    p.add_argument("which", choices=["host-rpc", "gpu-1m", "optimus", "registry", "tell"])
     p.add_argument("--calls", type=int, default=4000)
     p.add_argument("--msgs", type=int, default=1 << 20)
     p.add_argument("--steps", type=int, default=20)
@@ -289,10 +348,12 @@ def main():
     p.add_argument("--targets", type=int, default=8192)
     p.add_argument("--base", type=int, default=100_001)
     p.add_argument("--puts", type=int, default=5000)
+    p.add_argument("--tokens", type=int, default=1 << 20)
+    p.add_argument("--hops", type=int, default=32)
     a = p.parse_args()
     if not a.actors:
         a.actors = {"registry": 1 << 20, "optimus": 65536}.get(a.which, 131072)
-    {"host-rpc": host_rpc, "gpu-1m": gpu_1m, "optimus": optimus, "registry": registry}[a.which](a)
+    {"host-rpc": host_rpc, "gpu-1m": gpu_1m, "optimus": optimus, "registry": registry, "tell": tell}[a.which](a)
 
 
 if __name__ == "__main__":
