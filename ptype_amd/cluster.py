@@ -198,13 +198,20 @@ class Client:
             raise RuntimeError("Client.Send needs the cluster's device runtime (Join with a gpu: section)")
         return self._rt.send(self.service, batch, **kw)
 
+    def Tell(self, batch, **kw):
+        """Batched fire-and-forget to GPU actors of this service; handlers may send
+        on to other actors (device outbox), which is pumped until quiescent."""
+        if self._rt is None:
+            raise RuntimeError("Client.Tell needs the cluster's device runtime (Join with a gpu: section)")
+        return self._rt.tell(batch, **kw)
+
     def Close(self) -> None:
         self._c.close()
 
     def ConnectionErrs(self) -> ErrChannel:
         return self._c.connection_errs()
 
-    call, go, send, close = Call, Go, Send, Close
+    call, go, send, tell, close = Call, Go, Send, Tell, Close
 
     @property
     def conns_updated(self) -> IntChannel:

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
     const uint32_t* __restrict__ route, const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
     const int64_t* __restrict__ a2, const uint16_t* __restrict__ method_col, uint32_t method_uniform, int64_t M,
     int64_t P, int R, int64_t C, const uint32_t* __restrict__ base, uint32_t* __restrict__ sendbuf,
-    int64_t req_words, int32_t* __restrict__ perm) {
+    int64_t req_words, int32_t* __restrict__ perm, DirectView dv) {
   __shared__ unsigned cnt[kScatterItems][kRouteThreads / kWave][kMaxRanks];
   __shared__ unsigned run[kMaxRanks];
   for (int d = threadIdx.x; d < R; d += blockDim.x) run[d] = base[(int64_t)blockIdx.x * (R + 1) + d];
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
   auto route_at = [route](int64_t i) { return route[i]; };
   for (int64_t tile = lo; tile < hi; tile += kScatterTile)
     scatter_tile<NARGS, MC>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C, sendbuf, req_words,
-                            perm, cnt, run);
+                            perm, cnt, run, dv);
 }
 
 // K3 (batch form).  grid.y = source rank, grid.x tiles the delivered range.
@@ -206,7 +206,7 @@ __device__ __forceinline__ unsigned long long dispatch_range(const uint32_t* __r
                                                              uint32_t hdr_method, int64_t* __restrict__ vals,
                                                              uint8_t* __restrict__ sts, int64_t* __restrict__ state,
                                                              uint32_t n_state, uint64_t delay_ticks,
-                                                             OutboxView ob) {
+                                                             OutboxView ob, DirectView dv, bool direct) {
   constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
   unsigned long long failed = 0;
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count; s += (int64_t)gridDim.x * blockDim.x) {
@@ -226,8 +226,14 @@ __device__ __forceinline__ unsigned long long dispatch_range(const uint32_t* __r
     if constexpr (NARGS > 2) m.a2 = (int64_t)(((uint64_t)wv[o + 5] << 32) | wv[o + 4]);
     const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
     failed += rr.status != kStatusOk;
-    vals[s] = rr.value;
-    sts[s] = (uint8_t)rr.status;
+    if (direct) {  // own slot: straight into the caller's outputs
+      const int32_t i = dv.src[s];
+      dv.out_val[i] = rr.value;
+      dv.out_st[i] = rr.status;
+    } else {
+      vals[s] = rr.value;
+      sts[s] = (uint8_t)rr.status;
+    }
   }
   return failed;
 }
@@ -237,8 +243,9 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
                                                        int64_t C, uint32_t* __restrict__ reply, int64_t rep_words,
                                                        int64_t* __restrict__ state, uint32_t n_state,
                                                        uint64_t delay_ticks, unsigned long long* __restrict__ stats,
-                                                       OutboxView ob) {
+                                                       OutboxView ob, DirectView dv) {
   const int d = blockIdx.y;
+  const bool direct = dv.src != nullptr && d == dv.self;
   const uint32_t* rq = recv + (int64_t)d * req_words;
   const uint4 h = *reinterpret_cast<const uint4*>(rq);
   const bool valid = (h.w >> 16) & kFlagValid;
@@ -255,32 +262,37 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
     switch (hm) {  // uniform per slot: one specialised loop per hot method
       case kCalculatorMultiply:
         failed = dispatch_range<NARGS, MC, kCalculatorMultiply>(rq, count, hm, vals, sts, state, n_state,
-                                                                delay_ticks, obp);
+                                                                delay_ticks, obp, dv, direct);
         break;
       case kPrimeCheck:
-        failed = dispatch_range<NARGS, MC, kPrimeCheck>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp);
+        failed = dispatch_range<NARGS, MC, kPrimeCheck>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct);
         break;
       case kCounterAdd:
-        failed = dispatch_range<NARGS, MC, kCounterAdd>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp);
+        failed = dispatch_range<NARGS, MC, kCounterAdd>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct);
         break;
       default:
-        failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp);
+        failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct);
     }
   } else {
-    failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp);
+    failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct);
   }
   for (int off = 32; off > 0; off >>= 1) failed += __shfl_xor(failed, off);
   if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);
 }
 
 // K8: replies back to message order (SoA outputs).
+// direct: negative perm entries were completed by the scatter / own-slot dispatch.
 __global__ __launch_bounds__(256) void complete_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
                                                        uint32_t C, const int32_t* __restrict__ perm, int64_t M,
                                                        int64_t* __restrict__ out_val, int32_t* __restrict__ out_st,
-                                                       unsigned long long* __restrict__ checksum) {
+                                                       unsigned long long* __restrict__ checksum, bool direct) {
   unsigned long long sum = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t p = perm[i];
+    if (direct && p < 0) {
+      if (checksum) sum += (unsigned long long)out_val[i];
+      continue;
+    }
     int64_t v = 0;
     int32_t st;
     if (p >= 0) {
@@ -350,7 +362,7 @@ void set_route_tuning(int prep_items, int mode) {
 void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
                         int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
                         int R, int64_t C, int nargs, bool mc, int64_t req_words, uintptr_t sendbuf, uintptr_t perm,
-                        uintptr_t lb, uintptr_t stats, int rank_self, uintptr_t stream);
+                        uintptr_t lb, uintptr_t stats, int rank_self, DirectView dv, uintptr_t stream);
 
 template <int K, bool DIR>
 static void launch_prep(dim3 g, hipStream_t s, uintptr_t actor, int64_t M, int64_t P, uintptr_t table, uint64_t cap,
@@ -386,17 +398,31 @@ static void check_format(int nargs, int64_t C, int R) {
     default: F(3, true); break;          \
   }
 
+static DirectView make_direct(const std::vector<uintptr_t>& direct, int self) {
+  DirectView dv;
+  if (!direct.empty()) {
+    if (direct.size() != 3) throw std::invalid_argument("direct: [src, out_val, out_status]");
+    dv.src = (int32_t*)direct[0];
+    dv.out_val = (int64_t*)direct[1];
+    dv.out_st = (int32_t*)direct[2];
+    dv.self = self;
+  }
+  return dv;
+}
+
 void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
                   int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                   int64_t C, int nargs, bool mc, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist,
-                  uintptr_t lb, uintptr_t stats, int rank_self, uintptr_t stream) {
+                  uintptr_t lb, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
+                  uintptr_t stream) {
+  const DirectView dv = make_direct(direct, rank_self);
   check_format(nargs, C, R);
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
   if (method_col && !mc) throw std::invalid_argument("route: method column needs a method-column wire format");
   const int64_t req_words = wire_req_words(C, nargs, mc);
   if (g_route_mode == 1 && lb) {
     launch_route_fused(actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, R, C, nargs, mc,
-                       req_words, sendbuf, perm, lb, stats, rank_self, stream);
+                       req_words, sendbuf, perm, lb, stats, rank_self, dv, stream);
     return;
   }
   int64_t P;
@@ -426,7 +452,7 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
   hipLaunchKernelGGL((route_scatter_kernel<NA, MCV>), dim3((unsigned)G), dim3(kRouteThreads), 0, s,                  \
                      (const uint32_t*)route, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,             \
                      (const uint16_t*)method_col, (uint32_t)method_uniform, M, P, R, C, (const uint32_t*)hist,      \
-                     (uint32_t*)sendbuf, req_words, (int32_t*)perm)
+                     (uint32_t*)sendbuf, req_words, (int32_t*)perm, dv)
     PT_FORMAT_SWITCH(nargs, mc, PT_SCATTER)
 #undef PT_SCATTER
   }
@@ -435,7 +461,9 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
 
 void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintptr_t reply, uintptr_t state,
                      uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
-                     const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, uintptr_t stream) {
+                     const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, const std::vector<uintptr_t>& direct,
+                     int self, uintptr_t stream) {
+  const DirectView dv = make_direct(direct, self);
   OutboxView ob;
   if (outbox_cap) {
     if (outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
@@ -454,19 +482,19 @@ void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintp
 #define PT_DISPATCH(NA, MCV)                                                                                    \
   hipLaunchKernelGGL((dispatch_kernel<NA, MCV>), dim3(gx, R), dim3(256), 0, as_stream(stream),                  \
                      (const uint32_t*)recv, req_words, C, (uint32_t*)reply, rep_words, (int64_t*)state, n_state, \
-                     delay_ticks, (unsigned long long*)stats, ob)
+                     delay_ticks, (unsigned long long*)stats, ob, dv)
   PT_FORMAT_SWITCH(nargs, mc, PT_DISPATCH)
 #undef PT_DISPATCH
   PT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
-                     uintptr_t checksum, uintptr_t stream) {
+                     uintptr_t checksum, bool direct, uintptr_t stream) {
   if (M <= 0) return;
   if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
   hipLaunchKernelGGL(complete_kernel, dim3(grid_cap(M, 256, checksum ? 1024 : 8192)), dim3(256), 0,
                      as_stream(stream), (const uint32_t*)rep, wire_rep_words(C), (uint32_t)C, (const int32_t*)perm, M,
-                     (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum);
+                     (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum, direct);
   PT_HIP_CHECK(hipGetLastError());
 }
 

@@ -74,6 +74,19 @@ __device__ __forceinline__ void lookup_many(const TableEntry* __restrict__ t, ui
   }
 }
 
+// Direct completion of self-directed messages: the scatter records, for every
+// message routed to this rank's own slot, the message index at its slot position
+// (`src`), and writes the no-actor / overflow statuses straight into the caller's
+// outputs; the dispatch of the own slot then writes each reply into the caller's
+// arrays, so no reply staging and no completion pass are needed for them (all of
+// them at N = 1).  Passed BY VALUE (never take the address of a kernel argument).
+struct DirectView {
+  int32_t* src = nullptr;  // [C]: slot position -> message index (self slot)
+  int64_t* out_val = nullptr;
+  int32_t* out_st = nullptr;
+  int self = -1;
+};
+
 // Place the tile [tile, min(tile + kScatterTile, hi)) in message order.
 // `route_at(i)` yields message i's route word; `run[d]` is the next free slot
 // position of destination d for this block and is advanced past the tile.
@@ -86,7 +99,7 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
                                              int R, int64_t C, uint32_t* __restrict__ sendbuf, int64_t req_words,
                                              int32_t* __restrict__ perm,
                                              unsigned (&cnt)[kScatterItems][kRouteThreads / kWave][kMaxRanks],
-                                             unsigned* run) {
+                                             unsigned* run, DirectView dv) {
   constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
   const unsigned tid = threadIdx.x, w = tid / kWave, lane = lane_id();
   int d[kScatterItems];
@@ -139,14 +152,27 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
     if (i >= hi) continue;
     if (d[k] < 0) {
       perm[i] = -2;
+      if (dv.src) {
+        dv.out_val[i] = 0;
+        dv.out_st[i] = kStatusNoActor;
+      }
       continue;
     }
     const int64_t pos = (int64_t)cnt[k][w][d[k]] + rk[k];
     if (pos >= C) {
       perm[i] = -1;
+      if (dv.src) {
+        dv.out_val[i] = 0;
+        dv.out_st[i] = kStatusOverflow;
+      }
       continue;
     }
-    perm[i] = (int32_t)((int64_t)d[k] * C + pos);
+    if (dv.src && d[k] == dv.self) {
+      perm[i] = -3;  // completed by the dispatch of the own slot
+      dv.src[pos] = (int32_t)i;
+    } else {
+      perm[i] = (int32_t)((int64_t)d[k] * C + pos);
+    }
     uint32_t* o = sendbuf + (int64_t)d[k] * req_words + 4 + pos * kStride;
     o[0] = rw[k] >> 8;  // local mailbox index at the destination
     if (MC) o[1] = meth[k] & 0xffffu;

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_fused_kernel(
     int64_t P, const TableEntry* __restrict__ table, uint64_t mask, const uint32_t* __restrict__ dir, uint32_t n_dir,
     int R, int64_t C, uint32_t* __restrict__ sendbuf, int64_t req_words, int32_t* __restrict__ perm,
     unsigned long long* __restrict__ ctrl, uint64_t* __restrict__ status, int G,
-    unsigned long long* __restrict__ stats, int rank_self) {
+    unsigned long long* __restrict__ stats, int rank_self, DirectView dv) {
   extern __shared__ uint32_t lds_route[];  // P route words of this block
   __shared__ unsigned h[kMaxRanks + 1];
   __shared__ unsigned run[kMaxRanks];
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_fused_kernel(
   auto route_at = [lo](int64_t i) { return lds_route[i - lo]; };
   for (int64_t tile = lo; tile < hi; tile += kScatterTile)
     scatter_tile<NARGS, MC>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C, sendbuf, req_words,
-                            perm, cnt, run);
+                            perm, cnt, run, dv);
 }
 
 // Messages per block: 4096 (16 KB of LDS route words); larger for huge batches
@@ -199,21 +199,22 @@ template <int NA, bool MCV, bool D>
 static void launch_fused_t(int64_t G, int64_t P, hipStream_t s, uintptr_t actor, uintptr_t a0, uintptr_t a1,
                            uintptr_t a2, uintptr_t method_col, int method_uniform, int64_t M, uintptr_t table,
                            uint64_t cap, uintptr_t dir, uint32_t n_dir, int R, int64_t C, uintptr_t sendbuf,
-                           int64_t req_words, uintptr_t perm, uintptr_t lb, uintptr_t stats, int rank_self) {
+                           int64_t req_words, uintptr_t perm, uintptr_t lb, uintptr_t stats, int rank_self,
+                           DirectView dv) {
   unsigned long long* ctrl = (unsigned long long*)lb;
   uint64_t* status = (uint64_t*)lb + 1;
   hipLaunchKernelGGL((route_fused_kernel<NA, MCV, D>), dim3((unsigned)G), dim3(kRouteThreads),
                      (size_t)P * sizeof(uint32_t), s, (const uint32_t*)actor, (const int64_t*)a0, (const int64_t*)a1,
                      (const int64_t*)a2, (const uint16_t*)method_col, (uint32_t)method_uniform, M, P,
                      (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, R, C, (uint32_t*)sendbuf,
-                     req_words, (int32_t*)perm, ctrl, status, (int)G, (unsigned long long*)stats, rank_self);
+                     req_words, (int32_t*)perm, ctrl, status, (int)G, (unsigned long long*)stats, rank_self, dv);
 }
 
 // `lb` = workspace of 1 + G * (R + 1) u64 words, zeroed once at allocation.
 void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
                         int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
                         int R, int64_t C, int nargs, bool mc, int64_t req_words, uintptr_t sendbuf, uintptr_t perm,
-                        uintptr_t lb, uintptr_t stats, int rank_self, uintptr_t stream) {
+                        uintptr_t lb, uintptr_t stats, int rank_self, DirectView dv, uintptr_t stream) {
   if (M >= (1ll << 30)) throw std::invalid_argument("route: at most 2^30 messages per epoch");
   int64_t P;
   const int64_t G = route_fused_grid(M, &P);
@@ -221,9 +222,9 @@ void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a
   const bool d = dir && n_dir;
 #define PT_FUSED(NA, MCV)                                                                                      \
   (d ? launch_fused_t<NA, MCV, true>(G, P, s, actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, \
-                                     n_dir, R, C, sendbuf, req_words, perm, lb, stats, rank_self)                \
+                                     n_dir, R, C, sendbuf, req_words, perm, lb, stats, rank_self, dv)            \
      : launch_fused_t<NA, MCV, false>(G, P, s, actor, a0, a1, a2, method_col, method_uniform, M, table, cap, 0, 0, \
-                                      R, C, sendbuf, req_words, perm, lb, stats, rank_self))
+                                      R, C, sendbuf, req_words, perm, lb, stats, rank_self, dv))
   switch (nargs * 2 + (mc ? 1 : 0)) {
     case 2: PT_FUSED(1, false); break;
     case 3: PT_FUSED(1, true); break;

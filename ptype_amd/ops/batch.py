@@ -161,13 +161,19 @@ class RouteWorkspace:
 
 def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int = 0,
           sendbuf: torch.Tensor | None = None, perm: torch.Tensor | None = None,
-          rws: RouteWorkspace | None = None, fmt: WireFormat = FULL_FORMAT, reset_stats: bool = True):
+          rws: RouteWorkspace | None = None, fmt: WireFormat = FULL_FORMAT, reset_stats: bool = True,
+          direct: tuple | None = None):
     """K1: resolve each message's actor in the GPU registry and place it, in
     message order, into its destination rank's epoch slot (wire format ``fmt``).
 
     Returns ``(sendbuf int32[R * fmt.req_words(C)], perm int32[M], stats int64[4])``;
     ``perm[i] = d * C + pos`` (-1 overflow, -2 no actor).  The no-actor /
     overflow counters accumulate in ``rws.ws`` unless ``reset_stats``.
+
+    ``direct = (out_val, out_status, src)``: direct completion -- messages to
+    ``rank_self`` get ``perm = -3`` and ``src[pos] = i`` (the own slot's dispatch
+    then writes their replies straight into the outputs), and no-actor / overflow
+    statuses are written into the outputs here.
     """
     M = batch.M
     dev = batch.device
@@ -192,9 +198,10 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
     if dev.type == "cuda":
         mcol = None if uniform else batch.method.to(torch.int16).contiguous()
         d, n_dir = table.directory()
+        dptr = [] if direct is None else [_ptr(direct[2]), _ptr(direct[0]), _ptr(direct[1])]
         hip().route(_ptr(batch.actor), _ptr(batch.a0), _ptr(batch.a1), _ptr(batch.a2), _ptr(mcol), method_u, M,
                     _ptr(table.table), table.cap, _ptr(d), n_dir, R, C, fmt.nargs, fmt.method_col, _ptr(sendbuf),
-                    _ptr(perm), _ptr(rws.route), _ptr(rws.hist), _ptr(rws.lb), _ptr(rws.ws), rank_self,
+                    _ptr(perm), _ptr(rws.route), _ptr(rws.hist), _ptr(rws.lb), _ptr(rws.ws), rank_self, dptr,
                     _stream(batch.actor))
         return sendbuf, perm, ws_stats(rws.ws)
     # ---- CPU reference: bit-identical layout (stable message order per destination) ----
@@ -220,10 +227,20 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
         k = min(n, C)
         region = sendbuf[d * W:(d + 1) * W]
         region[4:4 + k * fmt.stride] = words[idx[:k]].reshape(-1)
-        perm[idx[:k]] = (d * C + torch.arange(k, dtype=torch.int64)).to(torch.int32)
+        if direct is not None and d == rank_self:
+            perm[idx[:k]] = -3
+            direct[2][:k] = idx[:k].to(torch.int32)
+        else:
+            perm[idx[:k]] = (d * C + torch.arange(k, dtype=torch.int64)).to(torch.int32)
         perm[idx[k:]] = -1
         overflow += n - k
         region[:4] = _u32(torch.tensor([k, n, rank_self, (FLAG_VALID << 16) | (method_u & 0xFFFF)]))
+    if direct is not None:
+        neg = perm < 0
+        neg &= perm != -3
+        direct[0][neg] = 0
+        direct[1][perm == -2] = STATUS_NO_ACTOR
+        direct[1][perm == -1] = STATUS_OVERFLOW
     st = ws_stats(rws.ws)
     st[STAT_NOMATCH] += int((~ok).sum())
     st[STAT_OVERFLOW] += overflow
@@ -297,13 +314,14 @@ def _handler_ref(method, actor, a0, a1, a2, state, outbox=None):
 
 def dispatch(recv: torch.Tensor, R: int, C: int, state: torch.Tensor | None = None, delay_us: int = 0,
              reply: torch.Tensor | None = None, ws: torch.Tensor | None = None, expected_per_rank: int = 0,
-             fmt: WireFormat = FULL_FORMAT, outbox=None):
+             fmt: WireFormat = FULL_FORMAT, outbox=None, direct: tuple | None = None, rank_self: int = 0):
     """K3 (batch form): run every delivered record through the handler table.
 
     ``recv`` is ``int32[R * fmt.req_words(C)]`` (one request region per source
     rank); returns ``int32[R * rep_words(C)]`` reply regions (header, int64
     values, u8 statuses) in the same geometry.  Handlers that send (``Forward``)
-    append to ``outbox`` (a ``DeviceOutbox``).
+    append to ``outbox`` (a ``DeviceOutbox``).  With ``direct = (out_val,
+    out_status, src)`` the own slot (``rank_self``) replies into the outputs.
     """
     _check(recv, torch.int32, 1, "recv")
     dev = recv.device
@@ -315,8 +333,10 @@ def dispatch(recv: torch.Tensor, R: int, C: int, state: torch.Tensor | None = No
             ws = new_workspace(dev)
         n_state = 0 if state is None else state.numel()
         ob, ob_cap = outbox.view() if outbox is not None else ([], 0)
+        dptr = [] if direct is None else [_ptr(direct[2]), _ptr(direct[0]), _ptr(direct[1])]
         hip().dispatch(_ptr(recv), R, C, fmt.nargs, fmt.method_col, _ptr(reply), _ptr(state), n_state,
-                       int(delay_us) * 100, _ptr(ws), int(expected_per_rank), ob, ob_cap, _stream(recv))
+                       int(delay_us) * 100, _ptr(ws), int(expected_per_rank), ob, ob_cap, dptr, int(rank_self),
+                       _stream(recv))
         return reply
     reply.zero_()
     for d in range(R):
@@ -335,21 +355,28 @@ def dispatch(recv: torch.Tensor, R: int, C: int, state: torch.Tensor | None = No
         args = [_words_i64(rows[:, o + 2 * j], rows[:, o + 2 * j + 1]) for j in range(fmt.nargs)]
         args += [torch.zeros(cnt, dtype=torch.int64)] * (3 - fmt.nargs)
         v, stt = _handler_ref(method, actor, args[0], args[1], args[2], state, outbox)
+        if direct is not None and d == rank_self:
+            src = direct[2][:cnt].to(torch.int64)
+            direct[0][src] = v
+            direct[1][src] = stt.to(torch.int32)
+            continue
         rr[4:4 + 2 * C].view(torch.int64)[:cnt] = v
         rr[4 + 2 * C:].view(torch.uint8)[:cnt] = stt.to(torch.uint8)
     return reply
 
 
 def complete(reply: torch.Tensor, perm: torch.Tensor, C: int, out_val: torch.Tensor | None = None,
-             out_status: torch.Tensor | None = None, checksum: torch.Tensor | None = None):
+             out_status: torch.Tensor | None = None, checksum: torch.Tensor | None = None, direct: bool = False):
     """K8: ``value[i], status[i]`` = the reply at ``perm[i] = d * C + pos`` (overflow /
-    no-actor statuses for perm < 0)."""
+    no-actor statuses for perm < 0).  ``direct``: entries with perm < 0 were
+    already completed (route / own-slot dispatch) and are left alone."""
     M = perm.numel()
     dev = perm.device
     out_val = torch.empty(M, dtype=torch.int64, device=dev) if out_val is None else out_val
     out_status = torch.empty(M, dtype=torch.int32, device=dev) if out_status is None else out_status
     if dev.type == "cuda":
-        hip().complete(_ptr(reply), C, _ptr(perm), M, _ptr(out_val), _ptr(out_status), _ptr(checksum), _stream(perm))
+        hip().complete(_ptr(reply), C, _ptr(perm), M, _ptr(out_val), _ptr(out_status), _ptr(checksum), bool(direct),
+                       _stream(perm))
         return out_val, out_status
     Wr = WireFormat.rep_words(C)
     R = reply.numel() // Wr
@@ -358,6 +385,12 @@ def complete(reply: torch.Tensor, perm: torch.Tensor, C: int, out_val: torch.Ten
     sts = regions[:, 4 + 2 * C:].contiguous().view(torch.uint8)[:, :C].reshape(-1)
     p = perm.to(torch.int64)
     ok = p >= 0
+    if direct:
+        out_val[ok] = vals[p[ok]]
+        out_status[ok] = sts[p[ok]].to(torch.int32)
+        if checksum is not None:
+            checksum += out_val.sum()
+        return out_val, out_status
     out_val.zero_()
     out_val[ok] = vals[p[ok]]
     st = sts[p.clamp(min=0)].to(torch.int64)

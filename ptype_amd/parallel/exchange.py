@@ -71,6 +71,7 @@ class _ChunkBufs:
         self.reply = torch.empty(R * B.WireFormat.rep_words(C), dtype=torch.int32, device=device)
         self.back = torch.empty_like(self.reply) if sep else self.reply
         self.perm = torch.empty(M, dtype=torch.int32, device=device)
+        self.src = torch.empty(C, dtype=torch.int32, device=device)  # own slot: position -> message index
         self.rws = B.RouteWorkspace(M, R, device)
         self.ws = self.rws.ws
 
@@ -111,6 +112,9 @@ class ActorExchange:
                                 fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 2))]
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
         self.outbox = None  # DeviceOutbox that dispatched handlers send into (set by pump)
+        # direct completion of self-directed messages (no reply staging, no
+        # completion pass for them; at world 1 no completion kernel at all)
+        self.direct = True
         self.counters = EpochStats()
 
     # ------------------------------------------------------------------
@@ -143,12 +147,19 @@ class ActorExchange:
             self.counters.wire_bytes += n * 4 * (wq + wr)
         pending_bwd = []  # (chunk index, work handle, bufs)
 
+        direct = self.direct
+        local_only = R == 1  # every message is self-directed: nothing comes back
+        self._bounds, self._outs = bounds, (out_val, out_status)
+
         def finish(entry):
             i, work, bufs = entry
             if work is not None:
                 work.wait()
             lo, hi = bounds[i], bounds[i + 1]
-            B.complete(bufs.back[:wr], bufs.perm[: hi - lo], C, out_val[lo:hi], out_status[lo:hi], self.checksum)
+            if direct and local_only and self.checksum is None:
+                return
+            B.complete(bufs.back[:wr], bufs.perm[: hi - lo], C, out_val[lo:hi], out_status[lo:hi], self.checksum,
+                       direct=direct)
 
         fwd = None
         with trace.range("ptype.send"):
@@ -159,8 +170,9 @@ class ActorExchange:
                 while pending_bwd and pending_bwd[0][0] <= i - len(self.bufs):
                     finish(pending_bwd.pop(0))
                 with trace.range("ptype.route"):
+                    dv = (out_val[lo:hi], out_status[lo:hi], bufs.src) if direct else None
                     B.route(req.slice(lo, hi), self.table, R, C, self.rank, sendbuf=bufs.send[:wq],
-                            perm=bufs.perm[: hi - lo], rws=bufs.rws, fmt=fmt, reset_stats=False)
+                            perm=bufs.perm[: hi - lo], rws=bufs.rws, fmt=fmt, reset_stats=False, direct=dv)
                 work = self._a2a(bufs.recv[:wq], bufs.send[:wq])
                 if fwd is not None:
                     pending_bwd.append(self._serve(*fwd, fmt))
@@ -176,9 +188,14 @@ class ActorExchange:
         if work is not None:
             work.wait()
         wq, wr = self.world * fmt.req_words(self.C), self.world * B.WireFormat.rep_words(self.C)
+        dv = None
+        if self.direct:
+            lo, hi = self._bounds[i], self._bounds[i + 1]
+            dv = (self._outs[0][lo:hi], self._outs[1][lo:hi], bufs.src)
         with trace.range("ptype.dispatch"):
             B.dispatch(bufs.recv[:wq], self.world, self.C, self.state, self.delay_us, reply=bufs.reply[:wr], ws=bufs.ws,
-                       expected_per_rank=max(1, m // self.world), fmt=fmt, outbox=self.outbox)
+                       expected_per_rank=max(1, m // self.world), fmt=fmt, outbox=self.outbox, direct=dv,
+                       rank_self=self.rank)
         return (i, self._a2a(bufs.back[:wr], bufs.reply[:wr]), bufs)
 
     # ------------------------------------------------------------------

@@ -146,6 +146,18 @@ class DeviceRuntime:
             return ex.send_all(batch)
         return ex.send(batch)
 
+    def tell(self, batch: B.MsgBatch, outbox_capacity: int | None = None):
+        """Fire-and-forget delivery that lets GPU handlers send on: ``batch`` is
+        delivered, and whatever the handlers emit (actor-to-actor ``Forward``
+        tells) is routed epoch after epoch until every outbox of the group is
+        empty.  Collective.  Returns ``(epochs, messages delivered here)``."""
+        from .ops.outbox import DeviceOutbox
+
+        cap = int(outbox_capacity or self.max_batch)
+        if getattr(self, "_outbox", None) is None or self._outbox.cap < cap:
+            self._outbox = DeviceOutbox(cap, device=self.device)
+        return self.exchange.pump(self._outbox, initial=batch)
+
     def call(self, method: int, actor: int, a0: int = 0, a1: int = 0, a2: int = 0, timeout: float = 30.0):
         """Single synchronous call to a local actor through the persistent dispatcher."""
         with trace.range("ptype.call"):

@@ -446,3 +446,34 @@ def test_no_kernel_spills_to_scratch():
     assert not spills, spills
     low = {k: v for k, v in res.items() if "route" in k and v.get("Occupancy", 8) < 4}
     assert not low, low
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,self_rank,mode", [(1, 0, 0), (3, 1, 0), (8, 5, 0), (3, 2, 1)])
+def test_gpu_direct_completion_matches(R, self_rank, mode):
+    """Direct completion (own slot replies straight into the outputs, statuses of
+    unknown / overflowed messages written by the route) gives exactly the
+    outputs of the staged path -- both route algorithms."""
+    n_actors, M = 5000, 200_000
+    C = B.stripe_capacity(M, R) // 2 if R > 1 else M  # force overflow on multi-rank cases
+    g = RegistryTable(2 * n_actors, device="cuda")
+    _populate(g, n_actors, R)
+    g.enable_directory(n_actors)
+    req = B.gen_requests(M, n_actors + 50, METHOD_CALC_MULTIPLY, seed=R * 7 + self_rank, device="cuda")
+    fmt = B.WireFormat(2, False)
+    ops.hip().set_route_tuning(0, mode)
+    try:
+        send, perm, _ = B.route(req, g, R, C, rank_self=self_rank, fmt=fmt)
+        rep = B.dispatch(send, R, C, fmt=fmt, rank_self=self_rank)
+        ref_val, ref_st = B.complete(rep, perm, C)
+        val = torch.full((M,), -7, dtype=torch.int64, device="cuda")
+        st = torch.full((M,), -7, dtype=torch.int32, device="cuda")
+        src = torch.empty(C, dtype=torch.int32, device="cuda")
+        send2, perm2, _ = B.route(req, g, R, C, rank_self=self_rank, fmt=fmt, direct=(val, st, src))
+        rep2 = B.dispatch(send2, R, C, fmt=fmt, direct=(val, st, src), rank_self=self_rank)
+        B.complete(rep2, perm2, C, val, st, direct=True)
+    finally:
+        ops.hip().set_route_tuning(0, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(val, ref_val) and torch.equal(st, ref_st)
+    assert int((perm2 == -3).sum()) > 0 and bool((st != -7).all())

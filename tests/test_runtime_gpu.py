@@ -104,3 +104,27 @@ def test_snapshot_roundtrip(gpu_cluster, tmp_path):
     assert rt.table.live == rt.actors
     r, _ = rt.table.lookup(torch.arange(1, 100, device=rt.device))
     assert bool((r == 0).all())
+
+
+def test_client_tell_token_ring(gpu_cluster):
+    """Client.Tell: GPU actors pass tokens on through the device outbox."""
+    from ptype_amd.ops.records import METHOD_FORWARD
+
+    c, cfg = gpu_cluster
+    rt = c.runtime
+    server = C.Server()
+    server.Listen(cfg.port, "127.0.0.1")
+    try:
+        client = c.NewClient("calculator", None)
+        n, T, H = rt.total_actors, 1000, 5
+        starts = torch.arange(T, dtype=torch.int64) * 3 % n
+        batch = B.MsgBatch(starts.to(torch.int32).cuda(), ((starts + 1) % n).cuda(),
+                           torch.full((T,), H, dtype=torch.int64, device="cuda"),
+                           torch.full((T,), 1 | (n << 32), dtype=torch.int64, device="cuda"), METHOD_FORWARD)
+        rt.state.zero_()
+        epochs, delivered = client.Tell(batch)
+        torch.cuda.synchronize()
+        assert epochs == H and delivered == T * (H + 1) and int(rt.state.sum()) == T * (H + 1)
+        client.Close()
+    finally:
+        server.Close()
