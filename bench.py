@@ -95,7 +95,7 @@ def main():
     table = RegistryTable(2 * n_actors, device=device)
     ids = torch.arange(n_actors, dtype=torch.int64)
     table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
-    table.enable_directory(n_actors)  # K5b route directory: hot path reads 4 B/message, not a probe line
+    table.enable_directory(n_actors, affine_world=world)  # K5b directory + verified strided placement (no gathers)
     state = torch.zeros(args.actors_per_gpu, dtype=torch.int64, device=device)
     ex = ActorExchange(table, M, chunks=chunks, state=state)
     req = B.MsgBatch(torch.empty(M, dtype=torch.int32, device=device), torch.empty(M, dtype=torch.int64, device=device),

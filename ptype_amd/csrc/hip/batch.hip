@@ -63,13 +63,17 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
 // Each thread resolves K messages per tile (coalesced, item-major), with their
 // lookups overlapped.  With a route directory (DIR) an actor id below n_dir costs
 // one 4-B read; the hash table is probed only for ids outside it (or fallbacks).
-template <int K, bool DIR>
+// MODE 0: hash probe; 1: route directory; 2: affine placement (ids below n_dir
+// verified to sit at rank id % W, mailbox id / W -- route words computed, no
+// gathers; W a power of two uses shifts).
+template <int K, int MODE>
 __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_t* __restrict__ actor, int64_t M,
                                                                    int64_t P, const TableEntry* __restrict__ table,
                                                                    uint64_t mask, const uint32_t* __restrict__ dir,
-                                                                   uint32_t n_dir, int R,
+                                                                   uint32_t n_dir, uint32_t aw, int aw_shift, int R,
                                                                    uint32_t* __restrict__ route,
                                                                    uint32_t* __restrict__ hist) {
+  constexpr bool DIR = MODE == 1;
   __shared__ unsigned h[kMaxRanks + 1];
   for (int d = threadIdx.x; d <= R; d += blockDim.x) h[d] = 0;
   __syncthreads();
@@ -82,9 +86,20 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int64_t i = base + k * kRouteThreads + threadIdx.x;
-      a[k] = i < hi ? actor[i] : 0u;
+      // streaming column: non-temporal, so it does not evict the route directory from L2
+      a[k] = i < hi ? __builtin_nontemporal_load(actor + i) : 0u;
     }
-    if constexpr (DIR) {
+    if constexpr (MODE == 2) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (a[k] < n_dir) {
+          r[k] = aw_shift >= 0 ? (int)(a[k] & (aw - 1)) : (int)(a[k] % aw);
+          mb[k] = aw_shift >= 0 ? a[k] >> aw_shift : a[k] / aw;
+        } else {
+          lookup_entry(table, mask, actor_key(a[k]), r[k], mb[k]);
+        }
+      }
+    } else if constexpr (DIR) {
       uint32_t w[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) w[k] = a[k] < n_dir ? dir[a[k]] : kDirFallback;
@@ -110,7 +125,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
       if (i < hi) {
         const bool ok = r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
         d = ok ? r[k] : R;  // column R counts registry misses
-        route[i] = ok ? ((uint32_t)r[k] | (mb[k] << 8)) : kRouteNoActor;
+        __builtin_nontemporal_store(ok ? ((uint32_t)r[k] | (mb[k] << 8)) : kRouteNoActor, route + i);
       }
       // wave histogram: one ballot per destination present in the wave
       uint64_t active = __ballot(d >= 0);
@@ -364,12 +379,13 @@ void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a
                         int R, int64_t C, int nargs, bool mc, int64_t req_words, uintptr_t sendbuf, uintptr_t perm,
                         uintptr_t lb, uintptr_t stats, int rank_self, DirectView dv, uintptr_t stream);
 
-template <int K, bool DIR>
+template <int K, int MODE>
 static void launch_prep(dim3 g, hipStream_t s, uintptr_t actor, int64_t M, int64_t P, uintptr_t table, uint64_t cap,
-                        uintptr_t dir, uint32_t n_dir, int R, uintptr_t route, uintptr_t hist) {
-  hipLaunchKernelGGL((route_prep_kernel<K, DIR>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
-                     (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, R, (uint32_t*)route,
-                     (uint32_t*)hist);
+                        uintptr_t dir, uint32_t n_dir, int R, uintptr_t route, uintptr_t hist, uint32_t aw = 0) {
+  const int aw_shift = (aw && (aw & (aw - 1)) == 0) ? __builtin_ctz(aw) : -1;
+  hipLaunchKernelGGL((route_prep_kernel<K, MODE>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
+                     (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
+                     (uint32_t*)route, (uint32_t*)hist);
 }
 
 // Region sizes of wire format v2 (u32 words; see the header comment).
@@ -414,7 +430,7 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
                   int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                   int64_t C, int nargs, bool mc, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist,
                   uintptr_t lb, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
-                  uintptr_t stream) {
+                  uint32_t affine_w, uintptr_t stream) {
   const DirectView dv = make_direct(direct, rank_self);
   check_format(nargs, C, R);
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
@@ -431,16 +447,18 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
   if (M > 0) {
     const dim3 g((unsigned)G);
     const int k = g_prep_items;
-    if (dir && n_dir) {
+    if (affine_w && n_dir) {
+      launch_prep<4, 2>(g, s, actor, M, P, table, cap, 0, n_dir, R, route, hist, affine_w);
+    } else if (dir && n_dir) {
       // measured (tools/route_bench.py): 1/2/4 items within 2% of each other
-      if (k == 1) launch_prep<1, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
-      else if (k == 4) launch_prep<4, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
-      else launch_prep<2, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
+      if (k == 1) launch_prep<1, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
+      else if (k == 4) launch_prep<4, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
+      else launch_prep<2, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
     } else {
       // probe path: 2 lookups in flight per thread is best; 4 costs occupancy (98 VGPRs)
-      if (k == 1) launch_prep<1, false>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
-      else if (k == 4) launch_prep<4, false>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
-      else launch_prep<2, false>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
+      if (k == 1) launch_prep<1, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
+      else if (k == 4) launch_prep<4, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
+      else launch_prep<2, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
     }
   } else {
     PT_HIP_CHECK(hipMemsetAsync((void*)hist, 0, sizeof(uint32_t) * (R + 1) * G, s));

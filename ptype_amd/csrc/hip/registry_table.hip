@@ -207,13 +207,30 @@ __global__ __launch_bounds__(256) void table_pack_kernel(const TableEntry* __res
 // stays the source of truth; this is its compiled form for the message hot path:
 // a 4-B read per message from an L2-resident array instead of a 64-B probe line.
 // `dir` must be pre-filled with 0xFF bytes.
+//
+// Affine check (affine_w > 0): count the ids of the range the table holds and
+// the ones NOT placed by the strided rule (rank = id % W, mbox = id / W).  With
+// every id present and no violation, the data path can compute route words
+// arithmetically -- no directory gathers at all (`astats` = {present, violations}).
 __global__ __launch_bounds__(256) void table_build_dir_kernel(const TableEntry* __restrict__ t, uint64_t cap,
-                                                              uint32_t* __restrict__ dir, uint64_t n_dir) {
+                                                              uint32_t* __restrict__ dir, uint64_t n_dir,
+                                                              uint32_t affine_w,
+                                                              unsigned long long* __restrict__ astats) {
+  unsigned long long present = 0, bad = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint4 v = *reinterpret_cast<const uint4*>(&t[i]);
     const uint64_t key = ((uint64_t)v.y << 32) | v.x;
     if (key == kKeyEmpty || key == kKeyTomb || key > n_dir) continue;  // actor_key(id) = id + 1
     dir[key - 1] = (v.z < 0xfeu && v.w < (1u << 24)) ? (v.z | (v.w << 8)) : kDirFallback;
+    if (affine_w) {
+      const uint64_t id = key - 1;
+      ++present;
+      bad += (v.z != id % affine_w || v.w != id / affine_w) ? 1 : 0;
+    }
+  }
+  if (affine_w) {
+    publish_block_stats(present, 0, &astats[0], nullptr, nullptr, false);
+    publish_block_stats(bad, 0, &astats[1], nullptr, nullptr, false);
   }
 }
 
@@ -260,11 +277,13 @@ void launch_table_sweep(uintptr_t table, uint64_t cap, uintptr_t exp_tbl, uint64
   PT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_table_build_dir(uintptr_t table, uint64_t cap, uintptr_t dir, uint64_t n_dir, uintptr_t stream) {
+void launch_table_build_dir(uintptr_t table, uint64_t cap, uintptr_t dir, uint64_t n_dir, uint32_t affine_w,
+                            uintptr_t astats, uintptr_t stream) {
   hipStream_t s = as_stream(stream);
   PT_HIP_CHECK(hipMemsetAsync((void*)dir, 0xff, n_dir * sizeof(uint32_t), s));
+  if (affine_w) PT_HIP_CHECK(hipMemsetAsync((void*)astats, 0, 2 * sizeof(unsigned long long), s));
   hipLaunchKernelGGL(table_build_dir_kernel, dim3(grid_for((int64_t)cap)), dim3(256), 0, s, (const TableEntry*)table,
-                     cap, (uint32_t*)dir, n_dir);
+                     cap, (uint32_t*)dir, n_dir, affine_w, (unsigned long long*)astats);
   PT_HIP_CHECK(hipGetLastError());
 }
 

@@ -88,6 +88,7 @@ struct DirectView {
 };
 
 // Place the tile [tile, min(tile + kScatterTile, hi)) in message order.
+// `perm` may be null only with direct completion at world 1 (nothing comes back).
 // `route_at(i)` yields message i's route word; `run[d]` is the next free slot
 // position of destination d for this block and is advanced past the tile.
 // Block-level: every thread of the block must call it (two barriers inside).
@@ -151,7 +152,7 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
     const int64_t i = tile + k * kRouteThreads + tid;
     if (i >= hi) continue;
     if (d[k] < 0) {
-      perm[i] = -2;
+      if (perm) perm[i] = -2;
       if (dv.src) {
         dv.out_val[i] = 0;
         dv.out_st[i] = kStatusNoActor;
@@ -160,7 +161,7 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
     }
     const int64_t pos = (int64_t)cnt[k][w][d[k]] + rk[k];
     if (pos >= C) {
-      perm[i] = -1;
+      if (perm) perm[i] = -1;
       if (dv.src) {
         dv.out_val[i] = 0;
         dv.out_st[i] = kStatusOverflow;
@@ -168,10 +169,10 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
       continue;
     }
     if (dv.src && d[k] == dv.self) {
-      perm[i] = -3;  // completed by the dispatch of the own slot
+      if (perm) perm[i] = -3;  // completed by the dispatch of the own slot
       dv.src[pos] = (int32_t)i;
     } else {
-      perm[i] = (int32_t)((int64_t)d[k] * C + pos);
+      perm[i] = (int32_t)((int64_t)d[k] * C + pos);  // never null here: remote replies need it
     }
     uint32_t* o = sendbuf + (int64_t)d[k] * req_words + 4 + pos * kStride;
     o[0] = rw[k] >> 8;  // local mailbox index at the destination

@@ -162,7 +162,7 @@ class RouteWorkspace:
 def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int = 0,
           sendbuf: torch.Tensor | None = None, perm: torch.Tensor | None = None,
           rws: RouteWorkspace | None = None, fmt: WireFormat = FULL_FORMAT, reset_stats: bool = True,
-          direct: tuple | None = None):
+          direct: tuple | None = None, write_perm: bool = True):
     """K1: resolve each message's actor in the GPU registry and place it, in
     message order, into its destination rank's epoch slot (wire format ``fmt``).
 
@@ -173,8 +173,11 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
     ``direct = (out_val, out_status, src)``: direct completion -- messages to
     ``rank_self`` get ``perm = -3`` and ``src[pos] = i`` (the own slot's dispatch
     then writes their replies straight into the outputs), and no-actor / overflow
-    statuses are written into the outputs here.
+    statuses are written into the outputs here.  ``write_perm=False`` (only valid
+    with ``direct`` at R == 1, where nothing is completed later) skips ``perm``.
     """
+    if not write_perm and (direct is None or R != 1):
+        raise ValueError("write_perm=False needs direct completion at R == 1")
     M = batch.M
     dev = batch.device
     if batch.actor.dtype != torch.int32 or batch.a0.dtype != torch.int64:
@@ -197,12 +200,12 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
     method_u = int(batch.method) if uniform else 0
     if dev.type == "cuda":
         mcol = None if uniform else batch.method.to(torch.int16).contiguous()
-        d, n_dir = table.directory()
+        d, n_dir, affine = table.directory()
         dptr = [] if direct is None else [_ptr(direct[2]), _ptr(direct[0]), _ptr(direct[1])]
         hip().route(_ptr(batch.actor), _ptr(batch.a0), _ptr(batch.a1), _ptr(batch.a2), _ptr(mcol), method_u, M,
                     _ptr(table.table), table.cap, _ptr(d), n_dir, R, C, fmt.nargs, fmt.method_col, _ptr(sendbuf),
-                    _ptr(perm), _ptr(rws.route), _ptr(rws.hist), _ptr(rws.lb), _ptr(rws.ws), rank_self, dptr,
-                    _stream(batch.actor))
+                    _ptr(perm) if write_perm else 0, _ptr(rws.route), _ptr(rws.hist), _ptr(rws.lb), _ptr(rws.ws),
+                    rank_self, dptr, affine, _stream(batch.actor))
         return sendbuf, perm, ws_stats(rws.ws)
     # ---- CPU reference: bit-identical layout (stable message order per destination) ----
     actor = batch.actor.to(torch.int64) & 0xFFFFFFFF

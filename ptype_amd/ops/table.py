@@ -78,30 +78,46 @@ class RegistryTable:
         self.stats = torch.zeros(8, dtype=torch.int64, device=self.device)
         self.dir = None  # route directory (K5b), GPU only; see enable_directory
         self.dir_n = 0
+        self.affine_world = 0  # strided-rule candidate W (0: no check)
+        self.affine = 0  # W when the last build verified the rule for every id of the range
+        self._astats = None
         self._dir_dirty = True
 
     # ------------------------------------------------------------------ directory
-    def enable_directory(self, n_ids: int) -> None:
+    def enable_directory(self, n_ids: int, affine_world: int = 0) -> None:
         """Keep a dense route directory for actor ids ``[0, n_ids)``: the registry
         flattened to one 4-B route word per id (K5b), rebuilt lazily after any
         mutation.  The data path reads it instead of probing the hash table; ids
-        outside the range still probe the table, so results are identical."""
+        outside the range still probe the table, so results are identical.
+
+        ``affine_world = W``: each rebuild also verifies, on the device, whether
+        every id of the range is registered at rank ``id % W``, mailbox ``id // W``
+        (the runtime's strided placement).  While that holds the route computes
+        the route words -- no directory gathers -- and the first mutation that
+        breaks it (a re-homed or removed actor) falls back to the directory."""
         if not self.is_gpu or n_ids <= 0:
             return
         if n_ids > (1 << 30):
             raise ValueError("directory range too large")
         self.dir_n = int(n_ids)
         self.dir = torch.empty(self.dir_n, dtype=torch.int32, device=self.device)
+        self.affine_world = int(affine_world)
+        self._astats = torch.zeros(2, dtype=torch.int64, device=self.device) if affine_world else None
         self._dir_dirty = True
 
     def directory(self):
-        """``(dir tensor | None, n)`` -- rebuilt on device if the table changed."""
+        """``(dir tensor | None, n, affine W or 0)`` -- rebuilt on device if the table changed."""
         if self.dir is None:
-            return None, 0
+            return None, 0, 0
         if self._dir_dirty:
-            hip().table_build_dir(_ptr(self.table), self.cap, _ptr(self.dir), self.dir_n, _stream(self.table))
+            hip().table_build_dir(_ptr(self.table), self.cap, _ptr(self.dir), self.dir_n, self.affine_world,
+                                  _ptr(self._astats), _stream(self.table))
+            self.affine = 0
+            if self.affine_world:
+                present, bad = (int(x) for x in self._astats.tolist())  # one sync per rebuild
+                self.affine = self.affine_world if present == self.dir_n and bad == 0 else 0
             self._dir_dirty = False
-        return self.dir, self.dir_n
+        return self.dir, self.dir_n, self.affine
 
     # ------------------------------------------------------------------ props
     @property

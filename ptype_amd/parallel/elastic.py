@@ -195,7 +195,7 @@ class ElasticDataPlane:
             for j, r in enumerate(rs):
                 ids = r + W0 * k
                 table.upsert(actor_keys(ids), torch.full((P,), rank, dtype=torch.int32), (j * P + k).to(torch.int32))
-        table.enable_directory(W0 * P)
+        table.enable_directory(W0 * P, affine_world=W0)
         self.table = table
         self.exchange = ActorExchange(table, self.max_batch, chunks=self.chunks, state=self.state)
 

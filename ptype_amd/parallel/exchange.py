@@ -172,7 +172,8 @@ class ActorExchange:
                 with trace.range("ptype.route"):
                     dv = (out_val[lo:hi], out_status[lo:hi], bufs.src) if direct else None
                     B.route(req.slice(lo, hi), self.table, R, C, self.rank, sendbuf=bufs.send[:wq],
-                            perm=bufs.perm[: hi - lo], rws=bufs.rws, fmt=fmt, reset_stats=False, direct=dv)
+                            perm=bufs.perm[: hi - lo], rws=bufs.rws, fmt=fmt, reset_stats=False, direct=dv,
+                            write_perm=not (direct and local_only and self.checksum is None))
                 work = self._a2a(bufs.recv[:wq], bufs.send[:wq])
                 if fwd is not None:
                     pending_bwd.append(self._serve(*fwd, fmt))

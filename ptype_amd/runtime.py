@@ -68,7 +68,7 @@ class DeviceRuntime:
                                          self.delay_us, float(idle_ms), 60.0)
         self.table = RegistryTable(2 * self.actors * self.world, device=self.device)
         # dense actor ids [0, actors*world): route through the compiled directory (K5b)
-        self.table.enable_directory(self.actors * self.world)
+        self.table.enable_directory(self.actors * self.world, affine_world=self.world)
         self.max_batch = int(max_batch)
         self.chunks = chunks or (1 if self.world == 1 else 4)
         self._exchange = None

@@ -477,3 +477,34 @@ def test_gpu_direct_completion_matches(R, self_rank, mode):
     torch.cuda.synchronize()
     assert torch.equal(val, ref_val) and torch.equal(st, ref_st)
     assert int((perm2 == -3).sum()) > 0 and bool((st != -7).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [1, 3, 8])
+def test_gpu_affine_placement_route(W):
+    """Verified strided placement: the route computes route words (no directory
+    gathers) while every id sits at (id % W, id // W); a re-homed or removed actor
+    drops it back to the directory.  Bit-identical to the CPU reference throughout."""
+    n_actors, M = 6000, 150_000
+    C = B.stripe_capacity(M, W)
+    g = RegistryTable(2 * n_actors, device="cuda")
+    c = RegistryTable(2 * n_actors, device="cpu")
+    _populate(g, n_actors, W)
+    _populate(c, n_actors, W)
+    g.enable_directory(n_actors, affine_world=W)
+    req = B.gen_requests(M, n_actors + 70, METHOD_CALC_MULTIPLY, seed=W, device="cuda")
+    ref = B.gen_requests(M, n_actors + 70, METHOD_CALC_MULTIPLY, seed=W, device="cpu")
+    fmt = B.WireFormat(2, False)
+
+    def check():
+        send, perm, st = B.route(req, g, W, C, fmt=fmt)
+        rsend, rperm, rst = B.route(ref, c, W, C, fmt=fmt)
+        assert torch.equal(perm.cpu(), rperm) and _regions_equal(send, rsend, W, C, fmt)
+        assert st.cpu().tolist()[:2] == rst.tolist()[:2]
+
+    check()
+    assert g.affine == W
+    for t in (g, c):  # re-home one actor: the rule no longer holds
+        t.upsert(actor_keys(torch.tensor([10])), torch.tensor([(10 + 1) % W]), torch.tensor([999]))
+    check()
+    assert g.affine == 0

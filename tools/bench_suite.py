@@ -133,7 +133,7 @@ def optimus(a):
     table = RegistryTable(2 * n, device=dev)
     ids = torch.arange(n, dtype=torch.int64)
     table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
-    table.enable_directory(n)
+    table.enable_directory(n, affine_world=world)
     # targets: odd numbers around `base`, each split into 10-wide ranges [2,10), [10,20), ...
     T = a.targets
     tg = torch.arange(T, dtype=torch.int64, device=dev) * 2 + a.base + rank * 2 * T + 1
@@ -216,7 +216,7 @@ def tell(a):
     table = RegistryTable(2 * n, device=dev)
     ids = torch.arange(n, dtype=torch.int64)
     table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
-    table.enable_directory(n)
+    table.enable_directory(n, affine_world=world)
     state = torch.zeros(per, dtype=torch.int64, device=dev)
     ex = ActorExchange(table, T, chunks=1, state=state)
     outbox = DeviceOutbox(T, device=dev)

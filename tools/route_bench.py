@@ -57,9 +57,9 @@ def main():
         reply = torch.empty(R * B.WireFormat.rep_words(C), dtype=torch.int32, device="cuda")
         val = torch.empty(M, dtype=torch.int64, device="cuda")
         st = torch.empty(M, dtype=torch.int32, device="cuda")
-        for use_dir in (False, True):
+        for use_dir in (False, True, "affine"):
             if use_dir:
-                t.enable_directory(n_actors)
+                t.enable_directory(n_actors, affine_world=R if use_dir == "affine" else 0)
             for mode, items in ((1, 0), (0, 1), (0, 2), (0, 4)):
                 hip().set_route_tuning(items, mode)
                 us = timed(lambda: B.route(req, t, R, C, sendbuf=send, perm=perm, rws=rws, fmt=fmt), a.iters)
