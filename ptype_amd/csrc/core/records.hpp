@@ -29,6 +29,7 @@ enum MethodId : uint16_t {
 enum RecordFlags : uint16_t {
   kFlagValid = 1,
   kFlagRouted = 2,  // `actor` holds the destination's local mailbox index
+  kFlagIdentity = 4,  // slot header: slot position == message index (R = 1, no gaps)
 };
 
 enum ReplyStatus : int32_t {

@@ -143,55 +143,59 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
 }
 
 // Pass 2 (one block): per-destination exclusive scan over blocks; headers; stats.
+// Wave-level scans (shuffles) + one LDS exchange of wave totals: 3 barriers per
+// column instead of a 1024-wide Hillis-Steele.  Headers are written after all
+// columns so the no-actor total is known: a batch that maps whole and gap-free
+// onto a single slot (R = 1, no unknown actor, no overflow) is flagged
+// kFlagIdentity -- slot position == message index, which lets direct completion
+// skip the inverse index.
 __global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__ hist, int G, int R, int64_t C,
                                                           uint32_t* __restrict__ sendbuf, int64_t req_words,
                                                           uint32_t method_uniform,
                                                           unsigned long long* __restrict__ stats, int rank_self) {
-  __shared__ unsigned part[1024];
-  __shared__ unsigned long long overflow_tot, nomatch_tot;
-  if (threadIdx.x == 0) {
-    overflow_tot = 0;
-    nomatch_tot = 0;
-  }
-  __syncthreads();
+  __shared__ unsigned wsum[1024 / kWave];
+  __shared__ unsigned tot[kMaxRanks + 1];
+  const unsigned lane = lane_id(), w = threadIdx.x / kWave, nw = blockDim.x / kWave;
   const int per = (G + blockDim.x - 1) / blockDim.x;
   const int b0 = threadIdx.x * per, b1 = b0 + per < G ? b0 + per : G;
   for (int d = 0; d <= R; ++d) {
     unsigned s = 0;
     for (int b = b0; b < b1; ++b) s += hist[(int64_t)b * (R + 1) + d];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over 1024 partial sums
-    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
-      unsigned v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
-      __syncthreads();
-      part[threadIdx.x] += v;
-      __syncthreads();
+    unsigned v = s;  // inclusive scan within the wave
+    for (int off = 1; off < kWave; off <<= 1) {
+      const unsigned t = __shfl_up(v, off);
+      if (lane >= (unsigned)off) v += t;
     }
-    unsigned run = part[threadIdx.x] - s;  // exclusive
-    for (int b = b0; b < b1; ++b) {        // hist becomes the per-block base
+    if (lane == kWave - 1) wsum[w] = v;
+    __syncthreads();
+    if (w == 0) {  // scan of the wave totals
+      unsigned x = lane < nw ? wsum[lane] : 0u;
+      for (int off = 1; off < kWave; off <<= 1) {
+        const unsigned t = __shfl_up(x, off);
+        if (lane >= (unsigned)off) x += t;
+      }
+      if (lane < nw) wsum[lane] = x;
+    }
+    __syncthreads();
+    unsigned run = (w ? wsum[w - 1] : 0u) + v - s;  // exclusive prefix of this thread's first block
+    for (int b = b0; b < b1; ++b) {                   // hist becomes the per-block base
       const unsigned c = hist[(int64_t)b * (R + 1) + d];
       hist[(int64_t)b * (R + 1) + d] = run;
       run += c;
     }
-    if (threadIdx.x == blockDim.x - 1) {
-      const unsigned total = part[threadIdx.x];
-      if (d < R) {
-        uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)d * req_words);
-        const unsigned delivered = total < C ? total : (unsigned)C;
-        h4[0] = make_uint4(delivered, total, (unsigned)rank_self,
-                           ((uint32_t)kFlagValid << 16) | (method_uniform & 0xffffu));
-        if (total > C) overflow_tot += total - C;
-      } else {
-        nomatch_tot = total;
-      }
-    }
+    if (threadIdx.x == 0) tot[d] = wsum[nw - 1];
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    stats[0] += nomatch_tot;
-    stats[1] += overflow_tot;
+  const bool identity = R == 1 && tot[1] == 0 && (int64_t)tot[0] <= C;
+  for (int d = threadIdx.x; d < R; d += blockDim.x) {
+    const unsigned total = tot[d];
+    uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)d * req_words);
+    const unsigned delivered = total < C ? total : (unsigned)C;
+    const uint32_t flags = kFlagValid | (identity ? kFlagIdentity : 0);
+    h4[0] = make_uint4(delivered, total, (unsigned)rank_self, (flags << 16) | (method_uniform & 0xffffu));
+    if (total > C) atomicAdd(&stats[1], (unsigned long long)(total - C));
   }
+  if (threadIdx.x == 0 && tot[R]) stats[0] += tot[R];
 }
 
 // Pass 3: stable placement + SoA -> packed wire records (format <NARGS, MC>).
@@ -205,6 +209,8 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
   __shared__ unsigned run[kMaxRanks];
   for (int d = threadIdx.x; d < R; d += blockDim.x) run[d] = base[(int64_t)blockIdx.x * (R + 1) + d];
   const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
+  if (dv.src)  // the scan flagged a gap-free single slot: positions are message indices
+    dv.identity = ((sendbuf[(int64_t)dv.self * req_words + 3] >> 16) & kFlagIdentity) != 0;
   __syncthreads();
   auto route_at = [route](int64_t i) { return route[i]; };
   for (int64_t tile = lo; tile < hi; tile += kScatterTile)
@@ -221,7 +227,8 @@ __device__ __forceinline__ unsigned long long dispatch_range(const uint32_t* __r
                                                              uint32_t hdr_method, int64_t* __restrict__ vals,
                                                              uint8_t* __restrict__ sts, int64_t* __restrict__ state,
                                                              uint32_t n_state, uint64_t delay_ticks,
-                                                             OutboxView ob, DirectView dv, bool direct) {
+                                                             OutboxView ob, DirectView dv, bool direct,
+                                                             bool ident) {
   constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
   unsigned long long failed = 0;
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count; s += (int64_t)gridDim.x * blockDim.x) {
@@ -242,7 +249,7 @@ __device__ __forceinline__ unsigned long long dispatch_range(const uint32_t* __r
     const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
     failed += rr.status != kStatusOk;
     if (direct) {  // own slot: straight into the caller's outputs
-      const int32_t i = dv.src[s];
+      const int64_t i = ident ? s : (int64_t)dv.src[s];
       dv.out_val[i] = rr.value;
       dv.out_st[i] = rr.status;
     } else {
@@ -272,24 +279,25 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
     *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
   const OutboxView obp = ob;
   const uint32_t hm = h.w & 0xffffu;
+  const bool ident = direct && ((h.w >> 16) & kFlagIdentity);
   unsigned long long failed;
   if constexpr (!MC) {
     switch (hm) {  // uniform per slot: one specialised loop per hot method
       case kCalculatorMultiply:
         failed = dispatch_range<NARGS, MC, kCalculatorMultiply>(rq, count, hm, vals, sts, state, n_state,
-                                                                delay_ticks, obp, dv, direct);
+                                                                delay_ticks, obp, dv, direct, ident);
         break;
       case kPrimeCheck:
-        failed = dispatch_range<NARGS, MC, kPrimeCheck>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct);
+        failed = dispatch_range<NARGS, MC, kPrimeCheck>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct, ident);
         break;
       case kCounterAdd:
-        failed = dispatch_range<NARGS, MC, kCounterAdd>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct);
+        failed = dispatch_range<NARGS, MC, kCounterAdd>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct, ident);
         break;
       default:
-        failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct);
+        failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct, ident);
     }
   } else {
-    failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct);
+    failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct, ident);
   }
   for (int off = 32; off > 0; off >>= 1) failed += __shfl_xor(failed, off);
   if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);

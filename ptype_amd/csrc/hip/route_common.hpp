@@ -85,6 +85,7 @@ struct DirectView {
   int64_t* out_val = nullptr;
   int32_t* out_st = nullptr;
   int self = -1;
+  bool identity = false;  // positions ARE message indices: src is not written
 };
 
 // Place the tile [tile, min(tile + kScatterTile, hi)) in message order.
@@ -170,7 +171,7 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
     }
     if (dv.src && d[k] == dv.self) {
       if (perm) perm[i] = -3;  // completed by the dispatch of the own slot
-      dv.src[pos] = (int32_t)i;
+      if (!dv.identity) dv.src[pos] = (int32_t)i;
     } else {
       perm[i] = (int32_t)((int64_t)d[k] * C + pos);  // never null here: remote replies need it
     }

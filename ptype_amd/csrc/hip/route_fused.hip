@@ -53,6 +53,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_fused_kernel(
   __shared__ unsigned run[kMaxRanks];
   __shared__ unsigned cnt[kScatterItems][kRouteThreads / kWave][kMaxRanks];
   __shared__ unsigned long long s_ticket;
+  __shared__ unsigned s_tot[kMaxRanks + 1];
   const unsigned tid = threadIdx.x, lane = lane_id();
   if (tid == 0) {
     const unsigned long long t = atomicAdd(ctrl, 1ull);
@@ -160,18 +161,23 @@ __global__ __launch_bounds__(kRouteThreads) void route_fused_kernel(
           __hip_atomic_store(mine, lb_pack(epoch, kLbPrefix, excl + agg), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         if (c < R) run[c] = (unsigned)excl;
-        if (b == G - 1) {  // totals: slot headers + statistics
-          const uint64_t total = excl + agg;
-          if (c < R) {
-            uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)c * req_words);
-            const unsigned delivered = total < (uint64_t)C ? (unsigned)total : (unsigned)C;
-            h4[0] = make_uint4(delivered, (unsigned)total, (unsigned)rank_self,
-                               ((uint32_t)kFlagValid << 16) | (method_uniform & 0xffffu));
-            if (total > (uint64_t)C) atomicAdd(&stats[1], (unsigned long long)(total - C));
-          } else if (total) {
-            atomicAdd(&stats[0], (unsigned long long)total);
-          }
-        }
+        if (b == G - 1) s_tot[c] = (unsigned)(excl + agg);
+      }
+    }
+  }
+  __syncthreads();
+  if (b == G - 1) {  // totals: slot headers (+ identity flag, as the 3-pass scan) and statistics
+    const bool identity = R == 1 && s_tot[1] == 0 && (int64_t)s_tot[0] <= C;
+    for (int c = tid; c <= R; c += blockDim.x) {
+      const uint64_t total = s_tot[c];
+      if (c < R) {
+        uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)c * req_words);
+        const unsigned delivered = total < (uint64_t)C ? (unsigned)total : (unsigned)C;
+        const uint32_t flags = kFlagValid | (identity ? kFlagIdentity : 0);
+        h4[0] = make_uint4(delivered, (unsigned)total, (unsigned)rank_self, (flags << 16) | (method_uniform & 0xffffu));
+        if (total > (uint64_t)C) atomicAdd(&stats[1], (unsigned long long)(total - C));
+      } else if (total) {
+        atomicAdd(&stats[0], (unsigned long long)total);
       }
     }
   }

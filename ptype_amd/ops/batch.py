@@ -12,7 +12,8 @@ import numpy as np
 import torch
 
 from . import _check, _ptr, _stream, hip
-from .records import FLAG_VALID, METHOD_CALC_MULTIPLY, STATUS_NO_ACTOR, STATUS_OVERFLOW, make_requests, split_requests
+from .records import (FLAG_IDENTITY, FLAG_VALID, METHOD_CALC_MULTIPLY, STATUS_NO_ACTOR, STATUS_OVERFLOW, make_requests,
+                      split_requests)
 from .table import RegistryTable, actor_keys, mix64
 
 # workspace words (int64): [0:4) stats [nomatch, overflow, failed, route-error flag]
@@ -238,6 +239,8 @@ def route(batch: MsgBatch, table: RegistryTable, R: int, C: int, rank_self: int 
         perm[idx[k:]] = -1
         overflow += n - k
         region[:4] = _u32(torch.tensor([k, n, rank_self, (FLAG_VALID << 16) | (method_u & 0xFFFF)]))
+    if R == 1 and bool(ok.all()) and M <= C:  # gap-free single slot (as the device scan flags it)
+        sendbuf[3] = sendbuf[3] | (FLAG_IDENTITY << 16)
     if direct is not None:
         neg = perm < 0
         neg &= perm != -3
@@ -359,7 +362,8 @@ def dispatch(recv: torch.Tensor, R: int, C: int, state: torch.Tensor | None = No
         args += [torch.zeros(cnt, dtype=torch.int64)] * (3 - fmt.nargs)
         v, stt = _handler_ref(method, actor, args[0], args[1], args[2], state, outbox)
         if direct is not None and d == rank_self:
-            src = direct[2][:cnt].to(torch.int64)
+            ident = ((int(h[3]) >> 16) & FLAG_IDENTITY) != 0
+            src = torch.arange(cnt) if ident else direct[2][:cnt].to(torch.int64)
             direct[0][src] = v
             direct[1][src] = stt.to(torch.int32)
             continue

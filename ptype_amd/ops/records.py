@@ -13,6 +13,7 @@ METHOD_FORWARD = 6  # actor-to-actor tell: count the visit, emit Forward to a0 w
 
 FLAG_VALID = 1
 FLAG_ROUTED = 2
+FLAG_IDENTITY = 4  # slot header: slot position == message index (R = 1, no gaps)
 
 STATUS_OK = 0
 STATUS_NO_METHOD = 1
