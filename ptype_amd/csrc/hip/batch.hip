@@ -234,8 +234,7 @@ __device__ __forceinline__ unsigned long long dispatch_range(const uint32_t* __r
   for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count; s += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t* r = rq + 4 + s * kStride;
     uint32_t wv[kStride];
-#pragma unroll
-    for (int j = 0; j < kStride; ++j) wv[j] = r[j];
+    load_words<kStride>(r, wv);
     MsgRecord m;
     m.actor = wv[0];
     m.method = (uint16_t)(FIXED ? FIXED : (MC ? (wv[1] & 0xffffu) : hdr_method));

@@ -74,6 +74,40 @@ __device__ __forceinline__ void lookup_many(const TableEntry* __restrict__ t, ui
   }
 }
 
+// Records are packed at a stride of 5/6/7/8 dwords, so they are only dword
+// aligned; gfx950 global memory takes dword-aligned multi-dword accesses, so
+// move them as x4/x2/x1 chunks (declared 4-B aligned) instead of one u32 per op.
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+
+template <int K>
+__device__ __forceinline__ void store_words(uint32_t* p, const uint32_t (&w)[K]) {
+  int j = 0;
+#pragma unroll
+  for (; j + 4 <= K; j += 4) *reinterpret_cast<u32x4a*>(p + j) = u32x4a{w[j], w[j + 1], w[j + 2], w[j + 3]};
+  if constexpr (K % 4 >= 2) {
+    *reinterpret_cast<u32x2a*>(p + j) = u32x2a{w[j], w[j + 1]};
+    j += 2;
+  }
+  if constexpr (K % 2 == 1) p[K - 1] = w[K - 1];
+}
+
+template <int K>
+__device__ __forceinline__ void load_words(const uint32_t* p, uint32_t (&w)[K]) {
+  int j = 0;
+#pragma unroll
+  for (; j + 4 <= K; j += 4) {
+    const u32x4a v = *reinterpret_cast<const u32x4a*>(p + j);
+    w[j] = v.x, w[j + 1] = v.y, w[j + 2] = v.z, w[j + 3] = v.w;
+  }
+  if constexpr (K % 4 >= 2) {
+    const u32x2a v = *reinterpret_cast<const u32x2a*>(p + j);
+    w[j] = v.x, w[j + 1] = v.y;
+    j += 2;
+  }
+  if constexpr (K % 2 == 1) w[K - 1] = p[K - 1];
+}
+
 // Direct completion of self-directed messages: the scatter records, for every
 // message routed to this rank's own slot, the message index at its slot position
 // (`src`), and writes the no-actor / overflow statuses straight into the caller's
@@ -176,13 +210,15 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
       perm[i] = (int32_t)((int64_t)d[k] * C + pos);  // never null here: remote replies need it
     }
     uint32_t* o = sendbuf + (int64_t)d[k] * req_words + 4 + pos * kStride;
-    o[0] = rw[k] >> 8;  // local mailbox index at the destination
-    if (MC) o[1] = meth[k] & 0xffffu;
+    uint32_t rec[kStride];
+    rec[0] = rw[k] >> 8;  // local mailbox index at the destination
+    if constexpr (MC) rec[1] = meth[k] & 0xffffu;
 #pragma unroll
     for (int j = 0; j < NARGS; ++j) {
-      o[1 + (MC ? 1 : 0) + 2 * j] = (uint32_t)v[k][j];
-      o[2 + (MC ? 1 : 0) + 2 * j] = (uint32_t)((uint64_t)v[k][j] >> 32);
+      rec[1 + (MC ? 1 : 0) + 2 * j] = (uint32_t)v[k][j];
+      rec[2 + (MC ? 1 : 0) + 2 * j] = (uint32_t)((uint64_t)v[k][j] >> 32);
     }
+    store_words<kStride>(o, rec);
   }
   __syncthreads();
 }
