@@ -268,6 +268,9 @@ class Server:
                        actor: int = 0, actor_field: str = "") -> None:
         fn, ctx = device_server.submit_handle()
         self._s.register_device_method(service_method, fn, ctx, int(method_id), int(actor), list(fields), actor_field)
+        if getattr(device_server, "shm_name", ""):  # same-node processes call it through shared memory
+            device_server.export_method(service_method, int(method_id), int(actor), list(fields), actor_field)
+            self._s.set_shm_segment(device_server.shm_name)
 
     def Listen(self, port: int = 0, host: str = "0.0.0.0", local: bool = True) -> int:
         return self._s.listen(host, int(port), local)

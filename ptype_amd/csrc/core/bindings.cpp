@@ -169,32 +169,12 @@ static RpcHandler device_handler(uintptr_t fn, uintptr_t ctx, int method, uint32
                                  std::vector<std::string> fields, std::string actor_field) {
   auto submit = (DeviceSubmitFn)fn;
   return [submit, ctx, method, actor, fields, actor_field](const gob::Value& args) -> gob::Value {
-    MsgRecord m{};
-    m.actor = actor;
-    m.method = (uint16_t)method;
-    m.flags = kFlagValid;
-    int64_t a[3] = {0, 0, 0};
-    if (args.kind == gob::kStruct) {
-      for (size_t k = 0; k < fields.size() && k < 3; ++k) {
-        const gob::Value* f = args.field(fields[k]);
-        if (f) a[k] = f->kind == gob::kUint ? (int64_t)f->u : f->i;
-      }
-      if (!actor_field.empty())
-        if (const gob::Value* f = args.field(actor_field)) m.actor = (uint32_t)(f->kind == gob::kUint ? f->u : f->i);
-    } else if (args.kind == gob::kInt) {
-      a[0] = args.i;
-    }
-    m.a0 = a[0];
-    m.a1 = a[1];
-    m.a2 = a[2];
+    const MsgRecord m = encode_device_call(args, method, actor, fields, actor_field);
     ReplyRecord r{};
     if (submit((void*)ctx, &m, &r, 1) != 0) fail(Errc::kRpc, "device dispatcher unavailable");
-    switch (r.status) {
-      case kStatusOk: return gob::Value::Int(r.value);
-      case kStatusFailed: fail(Errc::kRpc, "failed");
-      case kStatusNoActor: fail(Errc::kRpc, "no such actor");
-      default: fail(Errc::kRpc, "rpc: device method error status " + std::to_string(r.status));
-    }
+    RpcOutcome o = device_outcome(r);
+    if (!o.ok()) fail(o.code, o.error);
+    return o.reply;
   };
 }
 
@@ -610,6 +590,7 @@ PYBIND11_MODULE(_core, m) {
            },
            py::arg("name"), py::arg("submit_fn"), py::arg("submit_ctx"), py::arg("method"), py::arg("actor") = 0,
            py::arg("fields") = std::vector<std::string>{}, py::arg("actor_field") = "")
+      .def("set_shm_segment", &RpcServer::set_shm_segment, py::arg("name"))
       .def("has_service", &RpcServer::has_service)
       .def(
           "listen",
@@ -664,6 +645,12 @@ PYBIND11_MODULE(_core, m) {
 
   py::class_<RpcConn, std::shared_ptr<RpcConn>>(m, "RpcConn")
       .def_property_readonly("target", &RpcConn::target)
+      .def_property_readonly("transport",
+                             [](RpcConn& c) -> std::string {
+                               if (dynamic_cast<ShmRpcConn*>(&c)) return "shm";
+                               if (dynamic_cast<LocalRpcConn*>(&c)) return "local";
+                               return "tcp";
+                             })
       .def("call",
            [](RpcConn& c, const std::string& method, py::object args) {
              gob::Value a = to_gob(args);

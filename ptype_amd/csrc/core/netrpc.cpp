@@ -216,10 +216,18 @@ int RpcServer::listen(const std::string& host, int port) {
   listener_.reset(new Listener(host.empty() ? "0.0.0.0" : host, port,
                                [this](std::shared_ptr<Conn> c) { serve_conn(c); }));
   port_ = listener_->port();
+  if (!shm_segment_.empty()) {  // same-node clients may call the GPU actors through shared memory
+    shm_locator_publish(port_, shm_segment_);
+    locator_ = true;
+  }
   return port_;
 }
 
 void RpcServer::close() {
+  if (locator_) {
+    shm_locator_remove(port_);
+    locator_ = false;
+  }
   if (listener_) listener_->close();
   listener_.reset();
 }
@@ -379,9 +387,123 @@ std::shared_ptr<RpcServer> local_server_lookup(const std::string& host, int port
   return it == g_local.end() ? nullptr : it->second.lock();
 }
 
+MsgRecord encode_device_call(const gob::Value& args, int method, uint32_t actor,
+                             const std::vector<std::string>& fields, const std::string& actor_field) {
+  MsgRecord m{};
+  m.actor = actor;
+  m.method = (uint16_t)method;
+  m.flags = kFlagValid;
+  int64_t a[3] = {0, 0, 0};
+  if (args.kind == gob::kStruct) {
+    for (size_t k = 0; k < fields.size() && k < 3; ++k) {
+      const gob::Value* f = args.field(fields[k]);
+      if (f) a[k] = f->kind == gob::kUint ? (int64_t)f->u : f->i;
+    }
+    if (!actor_field.empty())
+      if (const gob::Value* f = args.field(actor_field)) m.actor = (uint32_t)(f->kind == gob::kUint ? f->u : f->i);
+  } else if (args.kind == gob::kInt) {
+    a[0] = args.i;
+  }
+  m.a0 = a[0];
+  m.a1 = a[1];
+  m.a2 = a[2];
+  return m;
+}
+
+RpcOutcome device_outcome(const ReplyRecord& r) {
+  RpcOutcome o;
+  switch (r.status) {
+    case kStatusOk:
+      o.reply = gob::Value::Int(r.value);
+      return o;
+    case kStatusFailed:
+      o.error = "failed";
+      break;
+    case kStatusNoActor:
+      o.error = "no such actor";
+      break;
+    default:
+      o.error = "rpc: device method error status " + std::to_string(r.status);
+  }
+  o.code = Errc::kRpc;
+  return o;
+}
+
+// ---- same-node shared-memory connection
+ShmRpcConn::ShmRpcConn(std::shared_ptr<ShmSegment> seg, std::string host, int port, int64_t dial_timeout_ms)
+    : seg_(std::move(seg)), host_(std::move(host)), port_(port), dial_timeout_ms_(dial_timeout_ms) {
+  const ShmHeader* h = static_cast<const ShmHeader*>(seg_->base());
+  if (seg_->size() < sizeof(ShmHeader) || h->magic != kShmMagic || seg_->size() < shm_bytes(h->ring))
+    fail(Errc::kUnavailable, "shared-memory segment " + seg_->name() + " is not a ptype dispatcher");
+  view_ = shm_view(seg_->base(), h->ring);
+}
+
+std::shared_ptr<RpcConn> ShmRpcConn::tcp() {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!tcp_) tcp_ = NetRpcConn::dial_http(host_, port_, dial_timeout_ms_);
+  return tcp_;
+}
+
+RpcOutcome ShmRpcConn::call(const std::string& method, const gob::Value& args, int64_t timeout_ms) {
+  if (closed_.load()) {
+    RpcOutcome o;
+    o.error = "connection is shut down";
+    o.code = Errc::kShutdown;
+    return o;
+  }
+  const ShmHeader* h = view_.hdr;
+  const uint32_t n = std::min<uint32_t>(h->n_methods.load(std::memory_order_acquire), kShmMaxMethods);
+  for (uint32_t k = 0; k < n; ++k) {
+    const ShmMethod& mm = h->methods[k];
+    if (method != mm.name) continue;
+    std::vector<std::string> fields;
+    for (uint32_t f = 0; f < mm.n_fields && f < 3; ++f) fields.emplace_back(mm.fields[f]);
+    const MsgRecord m = encode_device_call(args, (int)mm.method, mm.actor, fields, mm.actor_field);
+    try {
+      const ReplyRecord r = shm_call(view_, m, timeout_ms < 0 ? 30.0 : timeout_ms / 1e3);
+      shm_calls_.fetch_add(1);
+      return device_outcome(r);
+    } catch (const Error& e) {
+      RpcOutcome o;
+      o.error = e.what();
+      o.code = e.code();
+      return o;
+    }
+  }
+  try {  // not a device method: the server's regular net/rpc endpoint
+    return tcp()->call(method, args, timeout_ms);
+  } catch (const Error& e) {
+    RpcOutcome o;
+    o.error = e.what();
+    o.code = e.code();
+    return o;
+  }
+}
+
+void ShmRpcConn::go(const std::string& method, const gob::Value& args, RpcDone done) {
+  auto self = shared_from_this();
+  std::thread([self, method, args, done] { done(self->call(method, args)); }).detach();
+}
+
+void ShmRpcConn::close() {
+  closed_.store(true);
+  std::lock_guard<std::mutex> g(mu_);
+  if (tcp_) tcp_->close();
+}
+
 std::shared_ptr<RpcConn> dial_node(const std::string& host, int64_t port, int64_t timeout_ms, bool allow_local) {
   if (allow_local)
     if (auto s = local_server_lookup(host, (int)port)) return std::make_shared<LocalRpcConn>(s, host + ":" + std::to_string(port));
+  if (allow_local && is_local_host(host)) {  // another process on this node with GPU actors in shared memory
+    const std::string seg = shm_locator_lookup((int)port);
+    if (!seg.empty())
+      if (auto s = ShmSegment::attach(seg)) {
+        try {
+          return std::make_shared<ShmRpcConn>(s, host, (int)port, timeout_ms);
+        } catch (const Error&) {
+        }
+      }
+  }
   try {
     return NetRpcConn::dial_http(host, (int)port, timeout_ms);
   } catch (const Error& e) {

@@ -23,6 +23,8 @@
 
 #include "gob.hpp"
 #include "net.hpp"
+#include "records.hpp"
+#include "shmring.hpp"
 #include "util.hpp"
 
 namespace ptype {
@@ -89,6 +91,9 @@ class RpcServer {
   std::string debug_page() const;
   // Extra GET endpoints answering JSON (e.g. /debug/ptype -> Cluster.Stats()).
   void set_debug_handler(const std::string& path, std::function<std::string()> fn);
+  // The shared-memory segment of this server's GPU actors: published as the
+  // port's locator while listening, so same-node clients call them directly.
+  void set_shm_segment(const std::string& name) { shm_segment_ = name; }
 
  private:
   void serve_conn(std::shared_ptr<Conn> c);
@@ -98,6 +103,40 @@ class RpcServer {
   std::map<std::string, uint64_t> counts_;
   std::unique_ptr<Listener> listener_;
   int port_ = 0;
+  std::string shm_segment_;
+  bool locator_ = false;
+};
+
+// gob args -> device message, and a device reply -> net/rpc outcome: shared by
+// the in-process device bridge and the cross-process shared-memory connection.
+MsgRecord encode_device_call(const gob::Value& args, int method, uint32_t actor,
+                             const std::vector<std::string>& fields, const std::string& actor_field);
+RpcOutcome device_outcome(const ReplyRecord& r);
+
+// Same-node connection to a server process whose GPU actors export their
+// rings in shared memory (shmring.hpp): device methods are published straight
+// into the dispatcher's ring; any other method goes over a lazily dialled TCP
+// net/rpc connection to the same server.
+class ShmRpcConn : public RpcConn, public std::enable_shared_from_this<ShmRpcConn> {
+ public:
+  ShmRpcConn(std::shared_ptr<ShmSegment> seg, std::string host, int port, int64_t dial_timeout_ms);
+  void go(const std::string& method, const gob::Value& args, RpcDone done) override;
+  RpcOutcome call(const std::string& method, const gob::Value& args, int64_t timeout_ms = -1) override;
+  void close() override;
+  std::string target() const override { return host_ + ":" + std::to_string(port_); }
+  uint64_t shm_calls() const { return shm_calls_.load(); }
+
+ private:
+  std::shared_ptr<RpcConn> tcp();
+  std::shared_ptr<ShmSegment> seg_;
+  ShmView view_;
+  std::string host_;
+  int port_;
+  int64_t dial_timeout_ms_;
+  std::mutex mu_;
+  std::shared_ptr<RpcConn> tcp_;
+  std::atomic<bool> closed_{false};
+  std::atomic<uint64_t> shm_calls_{0};
 };
 
 // In-process connection to a server living in this process: same semantics as

@@ -85,4 +85,22 @@ static_assert(sizeof(ReplySlot) == 32, "ReplySlot must be 32 bytes");
 // call on a GPU actor (exported by _hip as a C function pointer).
 typedef int (*DeviceSubmitFn)(void* ctx, const MsgRecord* req, ReplyRecord* rep, int n);
 
+// Control block of the persistent dispatcher (host-visible; the device polls it).
+enum ServerState : uint64_t { kStopped = 0, kRunning = 1, kLaunching = 2 };
+
+struct alignas(64) ServerCtrl {
+  uint64_t stop;
+  uint64_t state;
+  uint64_t resume_head;
+  uint64_t processed;
+  uint64_t exits_idle;
+  uint64_t exits_lifetime;
+  uint64_t trace_mask;   // 0: tracing off; else trace ring capacity - 1
+  uint64_t trace_ring;   // device address of the TraceRec ring
+  uint64_t calib_req;    // host sets 1; the kernel answers with calib_ticks and clears it
+  uint64_t calib_ticks;
+  uint64_t pad[6];
+};
+static_assert(sizeof(ServerCtrl) == 128, "ServerCtrl layout");
+
 }  // namespace ptype

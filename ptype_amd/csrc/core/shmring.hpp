@@ -1,0 +1,105 @@
+// Node-local cross-process path to GPU actors: the persistent dispatcher's
+// request/reply rings in a POSIX shared-memory segment.
+//
+// The reference reaches another process's service over TCP net/rpc even on the
+// same host (cluster/rpc.go:272-285, rpc.DialHTTP; the calculator example runs
+// client and server as two processes, example/calculator/run).  Here a server
+// process that hosts GPU actors places the dispatcher's rings in shared memory
+// registered with HIP (the GPU polls them exactly as it polls its own process's
+// rings), and exports its device methods (name -> method id + argument fields)
+// in the segment header.  A client process on the node maps the segment and
+// publishes calls directly: no socket, no gob, no server thread on the path.
+// The server's launcher thread sleeps on a process-shared futex that clients
+// poke when the dispatcher wave has parked itself.
+//
+// Layout: [ShmHeader, 16 KB][ServerCtrl, 4 KB][RingSlot x ring][ReplySlot x ring][u64 owner x ring]
+#pragma once
+#include <atomic>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "records.hpp"
+
+namespace ptype {
+
+constexpr uint64_t kShmMagic = 0x31736d6570797470ull;  // "ptypems1"
+constexpr int kShmMaxMethods = 32;
+
+struct ShmMethod {
+  char name[96];  // "Service.Method"
+  uint32_t method, actor, n_fields, pad;
+  char fields[3][32];
+  char actor_field[32];
+};
+
+struct alignas(64) ShmHeader {
+  uint64_t magic;
+  uint32_t ring;
+  int32_t owner_pid;
+  std::atomic<uint64_t> next_seq;  // request sequence, shared by every publisher
+  std::atomic<uint32_t> wake;      // futex word: 1 = a publisher found the dispatcher parked
+  std::atomic<uint32_t> n_methods;
+  ShmMethod methods[kShmMaxMethods];
+};
+static_assert(sizeof(ShmHeader) <= 16384, "ShmHeader too large");
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "process-shared atomics must be lock-free");
+
+constexpr size_t kShmHeaderBytes = 16384, kShmCtrlBytes = 4096;
+
+inline size_t shm_bytes(uint32_t ring) {
+  return kShmHeaderBytes + kShmCtrlBytes + (size_t)ring * (sizeof(RingSlot) + sizeof(ReplySlot) + sizeof(uint64_t));
+}
+
+struct ShmView {
+  ShmHeader* hdr = nullptr;
+  ServerCtrl* ctrl = nullptr;
+  RingSlot* req = nullptr;
+  ReplySlot* rep = nullptr;
+  std::atomic<uint64_t>* owner = nullptr;
+};
+
+inline ShmView shm_view(void* base, uint32_t ring) {
+  char* p = static_cast<char*>(base);
+  ShmView v;
+  v.hdr = reinterpret_cast<ShmHeader*>(p);
+  v.ctrl = reinterpret_cast<ServerCtrl*>(p + kShmHeaderBytes);
+  v.req = reinterpret_cast<RingSlot*>(p + kShmHeaderBytes + kShmCtrlBytes);
+  v.rep = reinterpret_cast<ReplySlot*>(reinterpret_cast<char*>(v.req) + (size_t)ring * sizeof(RingSlot));
+  v.owner = reinterpret_cast<std::atomic<uint64_t>*>(reinterpret_cast<char*>(v.rep) + (size_t)ring * sizeof(ReplySlot));
+  return v;
+}
+
+// Process-shared futex on a 32-bit word of the segment.
+void shm_futex_wake(std::atomic<uint32_t>* w);
+void shm_futex_wait(std::atomic<uint32_t>* w, uint32_t expect, int64_t timeout_us);
+
+// A mapping of a named segment (creator: O_CREAT + ftruncate; others: attach).
+class ShmSegment {
+ public:
+  static std::shared_ptr<ShmSegment> create(const std::string& name, size_t bytes);
+  static std::shared_ptr<ShmSegment> attach(const std::string& name);  // nullptr if absent
+  ~ShmSegment();
+  void* base() const { return base_; }
+  size_t size() const { return size_; }
+  const std::string& name() const { return name_; }
+  void unlink_on_close() { unlink_ = true; }
+
+ private:
+  std::string name_;
+  void* base_ = nullptr;
+  size_t size_ = 0;
+  bool unlink_ = false;
+};
+
+// Publish one request into the segment's ring and wait for its reply (any
+// process).  `poke` is called when the dispatcher is not running.
+ReplyRecord shm_call(const ShmView& v, const MsgRecord& m, double timeout_s);
+
+// port -> segment locator written by a listening net/rpc server with
+// shared-memory device methods ("/ptype-port-<port>").
+void shm_locator_publish(int port, const std::string& segment);
+void shm_locator_remove(int port);
+std::string shm_locator_lookup(int port);  // "" if none or its owner is gone
+
+}  // namespace ptype

@@ -153,9 +153,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("stream_sync", &stream_sync, py::call_guard<py::gil_scoped_release>());
 
   py::class_<DeviceServer>(m, "DeviceServer")
-      .def(py::init<int, uint32_t, uintptr_t, uint32_t, uint64_t, double, double>(), py::arg("device"),
-           py::arg("ring") = 4096, py::arg("state") = 0, py::arg("n_state") = 0, py::arg("delay_us") = 0,
-           py::arg("idle_ms") = 200.0, py::arg("max_s") = 60.0)
+      .def(py::init<int, uint32_t, uintptr_t, uint32_t, uint64_t, double, double, const std::string&>(),
+           py::arg("device"), py::arg("ring") = 4096, py::arg("state") = 0, py::arg("n_state") = 0,
+           py::arg("delay_us") = 0, py::arg("idle_ms") = 200.0, py::arg("max_s") = 60.0, py::arg("shm_name") = "")
+      .def("export_method", &DeviceServer::export_method, py::arg("name"), py::arg("method"), py::arg("actor") = 0,
+           py::arg("fields") = std::vector<std::string>{}, py::arg("actor_field") = "")
+      .def_property_readonly("shm_name", &DeviceServer::shm_name)
       .def(
           "call",
           [](DeviceServer& s, int method, uint32_t actor, int64_t a0, int64_t a1, int64_t a2, double timeout) {

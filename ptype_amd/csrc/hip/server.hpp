@@ -21,30 +21,20 @@
 #include <chrono>
 #include <memory>
 #include <mutex>
+#include <string.h>
+#include <unistd.h>
+
+#include <string>
 #include <thread>
 #include <vector>
 
 #include "common.hpp"
 #include "handlers.hpp"
+#include "shmring.hpp"
 
 namespace ptype {
 
-enum ServerState : uint64_t { kStopped = 0, kRunning = 1, kLaunching = 2 };
-
-struct alignas(64) ServerCtrl {
-  uint64_t stop;
-  uint64_t state;
-  uint64_t resume_head;
-  uint64_t processed;
-  uint64_t exits_idle;
-  uint64_t exits_lifetime;
-  uint64_t trace_mask;   // 0: tracing off; else trace ring capacity - 1
-  uint64_t trace_ring;   // device address of the TraceRec ring
-  uint64_t calib_req;    // host sets 1; the kernel answers with calib_ticks and clears it
-  uint64_t calib_ticks;
-  uint64_t pad[6];
-};
-static_assert(sizeof(ServerCtrl) == 128, "ServerCtrl layout");
+// ServerState / ServerCtrl live in records.hpp (shared with the cross-process client).
 
 __device__ __forceinline__ uint64_t sys_ld(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -162,27 +152,57 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
 
 class DeviceServer {
  public:
+  // `shm_name` non-empty: the rings live in a POSIX shared-memory segment of that
+  // name (registered with HIP), so other processes on the node can publish calls
+  // (shmring.hpp); a launcher thread relaunches the parked wave on their poke.
   DeviceServer(int device, uint32_t ring, uintptr_t state, uint32_t n_state, uint64_t delay_us, double idle_ms,
-               double max_s)
+               double max_s, const std::string& shm_name = "")
       : device_(device), ring_(ring), state_((int64_t*)state), n_state_(n_state) {
     if (ring == 0 || (ring & (ring - 1))) throw std::invalid_argument("ring size must be a power of two");
     delay_ticks_ = delay_us * 100;  // s_memrealtime runs at 100 MHz
     idle_ticks_ = (uint64_t)(idle_ms * 1e5);
     max_ticks_ = (uint64_t)(max_s * 1e8);
     PT_HIP_CHECK(hipSetDevice(device_));
-    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
-    PT_HIP_CHECK(hipHostMalloc((void**)&req_, sizeof(RingSlot) * ring_, fl));
-    PT_HIP_CHECK(hipHostMalloc((void**)&rep_, sizeof(ReplySlot) * ring_, fl));
-    PT_HIP_CHECK(hipHostMalloc((void**)&ctrl_, sizeof(ServerCtrl), fl));
-    memset((void*)req_, 0, sizeof(RingSlot) * ring_);
-    memset((void*)rep_, 0, sizeof(ReplySlot) * ring_);
-    memset((void*)ctrl_, 0, sizeof(ServerCtrl));
-    PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dreq_, req_, 0));
-    PT_HIP_CHECK(hipHostGetDevicePointer((void**)&drep_, rep_, 0));
-    PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dctrl_, ctrl_, 0));
-    PT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    owner_.reset(new std::atomic<uint64_t>[ring_]);
+    if (shm_name.empty()) {
+      const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+      PT_HIP_CHECK(hipHostMalloc((void**)&req_, sizeof(RingSlot) * ring_, fl));
+      PT_HIP_CHECK(hipHostMalloc((void**)&rep_, sizeof(ReplySlot) * ring_, fl));
+      PT_HIP_CHECK(hipHostMalloc((void**)&ctrl_, sizeof(ServerCtrl), fl));
+      memset((void*)req_, 0, sizeof(RingSlot) * ring_);
+      memset((void*)rep_, 0, sizeof(ReplySlot) * ring_);
+      memset((void*)ctrl_, 0, sizeof(ServerCtrl));
+      PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dreq_, req_, 0));
+      PT_HIP_CHECK(hipHostGetDevicePointer((void**)&drep_, rep_, 0));
+      PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dctrl_, ctrl_, 0));
+      owner_mem_.reset(new std::atomic<uint64_t>[ring_]);
+      owner_ = owner_mem_.get();
+      seq_ = &local_seq_;
+    } else {
+      seg_ = ShmSegment::create(shm_name, shm_bytes(ring_));
+      const ShmView v = shm_view(seg_->base(), ring_);
+      hdr_ = v.hdr;
+      req_ = v.req;
+      rep_ = v.rep;
+      ctrl_ = v.ctrl;
+      owner_ = v.owner;
+      seq_ = &hdr_->next_seq;
+      PT_HIP_CHECK(hipHostRegister(seg_->base(), seg_->size(), hipHostRegisterMapped | hipHostRegisterPortable));
+      registered_ = true;
+      char* dbase = nullptr;
+      PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dbase, seg_->base(), 0));
+      const char* hbase = static_cast<const char*>(seg_->base());
+      dreq_ = reinterpret_cast<RingSlot*>(dbase + (reinterpret_cast<const char*>(req_) - hbase));
+      drep_ = reinterpret_cast<ReplySlot*>(dbase + (reinterpret_cast<const char*>(rep_) - hbase));
+      dctrl_ = reinterpret_cast<ServerCtrl*>(dbase + (reinterpret_cast<const char*>(ctrl_) - hbase));
+    }
     for (uint32_t i = 0; i < ring_; ++i) owner_[i].store(i, std::memory_order_relaxed);
+    PT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (hdr_) {  // publish the segment only once fully initialised
+      hdr_->ring = ring_;
+      hdr_->owner_pid = (int32_t)getpid();
+      __atomic_store_n(&hdr_->magic, kShmMagic, __ATOMIC_RELEASE);
+      waker_ = std::thread([this] { waker_loop(); });
+    }
   }
 
   ~DeviceServer() {
@@ -193,17 +213,46 @@ class DeviceServer {
   }
 
   void close() {
-    if (closed_) return;
-    closed_ = true;
+    if (closed_.exchange(true)) return;
+    if (hdr_) {
+      hdr_->wake.store(2);
+      shm_futex_wake(&hdr_->wake);
+      if (waker_.joinable()) waker_.join();
+    }
     __atomic_store_n(&ctrl_->stop, 1ull, __ATOMIC_SEQ_CST);
     hipSetDevice(device_);
     hipStreamSynchronize(stream_);
     hipStreamDestroy(stream_);
-    hipHostFree(req_);
-    hipHostFree(rep_);
-    hipHostFree(ctrl_);
+    if (seg_) {
+      if (registered_) hipHostUnregister(seg_->base());
+      seg_.reset();  // unmaps + unlinks the segment
+    } else {
+      hipHostFree(req_);
+      hipHostFree(rep_);
+      hipHostFree(ctrl_);
+    }
     if (trace_) hipHostFree(trace_);
   }
+
+  // Export a device method to same-node client processes (segment header table).
+  void export_method(const std::string& name, uint32_t method, uint32_t actor, const std::vector<std::string>& fields,
+                     const std::string& actor_field) {
+    if (!hdr_) throw std::runtime_error("export_method: server has no shared-memory segment");
+    std::lock_guard<std::mutex> g(launch_mu_);
+    const uint32_t n = hdr_->n_methods.load();
+    if (n >= (uint32_t)kShmMaxMethods) throw std::runtime_error("export_method: method table full");
+    ShmMethod& m = hdr_->methods[n];
+    memset(&m, 0, sizeof m);
+    strncpy(m.name, name.c_str(), sizeof m.name - 1);
+    m.method = method;
+    m.actor = actor;
+    m.n_fields = (uint32_t)std::min<size_t>(fields.size(), 3);
+    for (uint32_t k = 0; k < m.n_fields; ++k) strncpy(m.fields[k], fields[k].c_str(), sizeof m.fields[k] - 1);
+    strncpy(m.actor_field, actor_field.c_str(), sizeof m.actor_field - 1);
+    hdr_->n_methods.store(n + 1, std::memory_order_release);
+  }
+
+  std::string shm_name() const { return seg_ ? seg_->name() : std::string(); }
 
   // Publish n requests and wait for all replies (any thread).
   void call(const MsgRecord* in, ReplyRecord* out, int n, double timeout_s) {
@@ -284,7 +333,7 @@ class DeviceServer {
 
  private:
   uint64_t publish(const MsgRecord& m) {
-    const uint64_t seq = next_seq_.fetch_add(1);
+    const uint64_t seq = seq_->fetch_add(1);
     const uint32_t idx = (uint32_t)(seq & (ring_ - 1));
     // wait until the slot's previous occupant (seq - ring) has been consumed
     for (unsigned spins = 0; owner_[idx].load(std::memory_order_acquire) != seq; ++spins)
@@ -303,8 +352,12 @@ class DeviceServer {
     for (unsigned spins = 0; __atomic_load_n(&o->tag, __ATOMIC_ACQUIRE) != seq + 1; ++spins) {
       if ((spins & 1023) == 1023) {
         ensure_running();  // the kernel may have retired on idle/lifetime
-        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+          // give the slot up: a late reply carries this seq's tag and lands before the
+          // next occupant's (the dispatcher runs in sequence order)
+          owner_[idx].store(seq + ring_, std::memory_order_release);
           throw std::runtime_error("device server: reply timeout");
+        }
         std::this_thread::yield();
       }
     }
@@ -314,6 +367,16 @@ class DeviceServer {
     int b = rtt ? 63 - __builtin_clzll(rtt) : 0;
     rtt_hist_[b < kRttBuckets ? b : kRttBuckets - 1].fetch_add(1, std::memory_order_relaxed);
     return r;
+  }
+
+  // Same-node clients poke the futex when they find the wave parked.
+  void waker_loop() {
+    while (!closed_) {
+      shm_futex_wait(&hdr_->wake, 0, 2000);
+      const uint32_t w = hdr_->wake.exchange(0);
+      if (closed_ || w == 2) break;
+      if (w) ensure_running();
+    }
   }
 
   void ensure_running() {
@@ -353,11 +416,17 @@ class DeviceServer {
   ReplySlot* drep_ = nullptr;
   ServerCtrl* dctrl_ = nullptr;
   hipStream_t stream_ = nullptr;
-  std::atomic<uint64_t> next_seq_{0};
-  std::unique_ptr<std::atomic<uint64_t>[]> owner_;
+  std::atomic<uint64_t> local_seq_{0};
+  std::atomic<uint64_t>* seq_ = nullptr;
+  std::unique_ptr<std::atomic<uint64_t>[]> owner_mem_;
+  std::atomic<uint64_t>* owner_ = nullptr;
+  std::shared_ptr<ShmSegment> seg_;
+  ShmHeader* hdr_ = nullptr;
+  bool registered_ = false;
+  std::thread waker_;
   std::atomic<uint64_t> launches_{0};
   std::mutex launch_mu_;
-  bool closed_ = false;
+  std::atomic<bool> closed_{false};
   static constexpr int kRttBuckets = 40;
   std::atomic<uint64_t> rtt_hist_[kRttBuckets] = {};
   TraceRec* trace_ = nullptr;

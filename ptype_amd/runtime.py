@@ -46,7 +46,7 @@ def _dist():
 class DeviceRuntime:
     def __init__(self, device=None, actors: int = 1024, ring: int = 4096, idle_ms: float = 200.0,
                  delay_us: int = 0, max_batch: int = 1 << 20, chunks: int = 0, random_state: bool = False,
-                 group=None):
+                 group=None, shm: bool = True):
         if device is None:
             device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         self.device = torch.device(device)
@@ -64,8 +64,11 @@ class DeviceRuntime:
         else:
             self.state = torch.zeros(self.actors, dtype=torch.int64, device=self.device)
         self.delay_us = int(delay_us)
+        # dispatcher rings in shared memory: same-node client processes call these
+        # GPU actors without a socket (shmring.hpp)
         self.server = hip().DeviceServer(self.device.index or 0, int(ring), self.state.data_ptr(), self.actors,
-                                         self.delay_us, float(idle_ms), 60.0)
+                                         self.delay_us, float(idle_ms), 60.0,
+                                         f"ptype-{os.getpid()}-{self.device.index or 0}" if shm else "")
         self.table = RegistryTable(2 * self.actors * self.world, device=self.device)
         # dense actor ids [0, actors*world): route through the compiled directory (K5b)
         self.table.enable_directory(self.actors * self.world, affine_world=self.world)

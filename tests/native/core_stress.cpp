@@ -17,6 +17,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <map>
 #include <memory>
@@ -30,6 +31,7 @@
 #include "kvclient.hpp"
 #include "member.hpp"
 #include "netrpc.hpp"
+#include "shmring.hpp"
 #include "util.hpp"
 
 using namespace ptype;
@@ -322,6 +324,90 @@ void scenario_cluster_api(const std::string& dir) {
   srv->close();
 }
 
+// Same-node shared-memory path (shmring.hpp): a CPU thread plays the GPU
+// dispatcher (same protocol: in-order slots, tags, replies), client threads call
+// through dial_node -> ShmRpcConn; a non-device method falls back to TCP.
+void scenario_shm() {
+  const uint32_t ring = 256;
+  auto seg = ShmSegment::create("ptype-stress-" + std::to_string(getpid()), shm_bytes(ring));
+  ShmView v = shm_view(seg->base(), ring);
+  for (uint32_t i = 0; i < ring; ++i) v.owner[i].store(i);
+  v.hdr->ring = ring;
+  v.hdr->owner_pid = (int32_t)getpid();
+  ShmMethod& mm = v.hdr->methods[0];
+  std::strncpy(mm.name, "Calculator.Multiply", sizeof mm.name - 1);
+  mm.method = kCalculatorMultiply;
+  mm.n_fields = 2;
+  std::strncpy(mm.fields[0], "A", 31);
+  std::strncpy(mm.fields[1], "B", 31);
+  v.hdr->n_methods.store(1);
+  __atomic_store_n(&v.hdr->magic, kShmMagic, __ATOMIC_RELEASE);
+  std::atomic<bool> stop{false};
+  std::atomic<int> pokes{0};
+  std::thread disp([&] {  // the "dispatcher": runs while RUNNING, parks after idling
+    uint64_t head = 0;
+    int idle = 0;
+    __atomic_store_n(&v.ctrl->state, (uint64_t)kRunning, __ATOMIC_SEQ_CST);
+    while (!stop.load()) {
+      RingSlot* sl = &v.req[head & (ring - 1)];
+      if (__atomic_load_n(&sl->tag, __ATOMIC_ACQUIRE) != head + 1) {
+        if (++idle > 2000) {  // park as the GPU wave does: STOPPED, re-check, sleep until poked
+          __atomic_store_n(&v.ctrl->state, (uint64_t)kStopped, __ATOMIC_SEQ_CST);
+          while (!stop.load() && __atomic_load_n(&sl->tag, __ATOMIC_SEQ_CST) != head + 1) {
+            shm_futex_wait(&v.hdr->wake, 0, 1000);
+            if (v.hdr->wake.exchange(0)) ++pokes;
+          }
+          __atomic_store_n(&v.ctrl->state, (uint64_t)kRunning, __ATOMIC_SEQ_CST);
+          idle = 0;
+        }
+        std::this_thread::yield();
+        continue;
+      }
+      idle = 0;
+      const MsgRecord m = sl->msg;
+      ReplySlot* o = &v.rep[head & (ring - 1)];
+      o->rep.value = m.method == kCalculatorMultiply ? m.a0 * m.a1 : 0;
+      o->rep.status = m.method == kCalculatorMultiply ? kStatusOk : kStatusNoMethod;
+      o->rep.actor = m.actor;
+      __atomic_store_n(&o->tag, head + 1, __ATOMIC_RELEASE);
+      ++head;
+    }
+  });
+  // the server process side: a net/rpc server on the same port for other methods
+  auto srv = std::make_shared<RpcServer>();
+  srv->register_method("Calculator.Echo", [](const gob::Value& a) { return gob::Value::Int(a.field("A")->i); });
+  srv->set_shm_segment(seg->name());
+  const int port = srv->listen("127.0.0.1", 0);
+  auto conn = dial_node("127.0.0.1", port, 2000, true);
+  CHECK(dynamic_cast<ShmRpcConn*>(conn.get()) != nullptr);
+  std::atomic<int> good{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 6; ++t)
+    ts.emplace_back([&, t] {
+      for (int i = 0; i < 300; ++i) {
+        gob::Value args = gob::Value::Struct("Args");
+        args.fields = {{"A", gob::Value::Int(t + 1)}, {"B", gob::Value::Int(i)}};
+        RpcOutcome o = conn->call("Calculator.Multiply", args, 5000);
+        if (o.ok() && o.reply.i == (int64_t)(t + 1) * i) ++good;
+        if (i % 100 == 99) std::this_thread::sleep_for(std::chrono::milliseconds(30));  // let it park
+      }
+    });
+  for (auto& th : ts) th.join();
+  CHECK(good.load() == 1800);
+  CHECK(pokes.load() > 0);  // calls woke a parked dispatcher
+  gob::Value e = gob::Value::Struct("Args");
+  e.fields = {{"A", gob::Value::Int(42)}};
+  RpcOutcome o = conn->call("Calculator.Echo", e, 5000);  // not exported: TCP fallback
+  CHECK(o.ok() && o.reply.i == 42);
+  CHECK(srv->call_counts()["Calculator.Echo"] == 1 && srv->call_counts().count("Calculator.Multiply") == 0);
+  conn->close();
+  srv->close();
+  CHECK(shm_locator_lookup(port).empty());
+  stop.store(true);
+  shm_futex_wake(&v.hdr->wake);
+  disp.join();
+}
+
 // Elastic scale-out: a second member joins as a learner through the first one's
 // client URL and is promoted once caught up (cluster/cluster.go:105-147, :183-195).
 void scenario_learner(const std::string& dir) {
@@ -361,13 +447,14 @@ int main(int argc, char** argv) {
   }
   const std::string dir = argv[1];
   std::vector<std::string> want(argv + 2, argv + argc);
-  if (want.empty()) want = {"channel", "raft", "rpc", "api", "learner"};
+  if (want.empty()) want = {"channel", "raft", "rpc", "api", "learner", "shm"};
   std::map<std::string, std::function<void()>> all = {
       {"channel", [] { scenario_channel(); }},
       {"raft", [&] { scenario_raft(dir); }},
       {"rpc", [] { scenario_rpc(); }},
       {"api", [&] { scenario_cluster_api(dir); }},
       {"learner", [&] { scenario_learner(dir); }},
+      {"shm", [] { scenario_shm(); }},
   };
   for (const auto& w : want) {
     auto it = all.find(w);
