@@ -11,6 +11,8 @@
              dispatch), per-candidate delay 0.
   tell       device-side actor-to-actor messaging: token ring of Forward tells
              emitted by GPU handlers into the HBM outbox, pumped epoch by epoch.
+  xproc      cross-process Call to a GPU actor on one node: shared-memory rings
+             vs net/rpc over TCP (separate server and client processes).
   registry   1M-actor registry stress: GPU upsert / probe lookup / directory
              build / lease sweep / pack + snapshot to pinned host DRAM, and the
              control-plane store: puts with Raft snapshots + WAL.
@@ -248,6 +250,65 @@ def tell(a):
         dist.destroy_process_group()
 
 
+# --------------------------------------------------------------------------- xproc
+def _xproc_server(port, q, stop):
+    from ptype_amd import cluster as C
+    from ptype_amd.models import calculator
+    from ptype_amd.runtime import DeviceRuntime
+
+    rt = DeviceRuntime(torch.device("cuda", 0), actors=1024, idle_ms=200.0)
+    server = C.Server()
+    calculator.serve_device(rt, server)
+    server.Listen(port, "127.0.0.1")
+    q.put("ready")
+    stop.wait(300)
+    server.Close()
+    rt.close()
+
+
+def _xproc_client(port, calls, q):
+    from ptype_amd import _core
+    from ptype_amd.models.calculator import Args
+
+    out = {}
+    for name, allow in (("shm", True), ("tcp", False)):
+        c = _core.dial_http("127.0.0.1", port, 5.0, allow)
+        for i in range(500):
+            c.call("Calculator.Multiply", Args(i, 2))
+        lat = []
+        for i in range(calls):
+            t = time.perf_counter()
+            c.call("Calculator.Multiply", Args(i, 3))
+            lat.append(time.perf_counter() - t)
+        lat.sort()
+        out[name] = {"transport": c.transport, "p50_us": lat[len(lat) // 2] * 1e6,
+                     "p99_us": lat[int(len(lat) * 0.99)] * 1e6}
+        c.close()
+    q.put(out)
+
+
+def xproc(a):
+    """example/calculator's shape with GPU actors: server and client are separate
+    processes on one node; the client's Call reaches the GPU actor through the
+    shared-memory rings (vs net/rpc over TCP to the same server)."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q, stop = ctx.Queue(), ctx.Event()
+    port = _free_port()
+    sp = ctx.Process(target=_xproc_server, args=(port, q, stop))
+    sp.start()
+    assert q.get(timeout=300) == "ready"
+    cp = ctx.Process(target=_xproc_client, args=(port, a.calls, q))
+    cp.start()
+    out = q.get(timeout=300)
+    cp.join(30)
+    stop.set()
+    sp.join(60)
+    _emit({"config": "cross-process Call to a GPU actor on the same node (calculator server + client processes)",
+           "shm": out["shm"], "tcp_netrpc": out["tcp"]})
+
+
 # --------------------------------------------------------------------------- registry
 def registry(a):
     from ptype_amd.ops import batch as B
@@ -340,7 +401,7 @@ def registry(a):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("which", choices=["host-rpc", "gpu-1m", "optimus", "registry", "tell"])
+    p.add_argument("which", choices=["host-rpc", "gpu-1m", "optimus", "registry", "tell", "xproc"])
     p.add_argument("--calls", type=int, default=4000)
     p.add_argument("--msgs", type=int, default=1 << 20)
     p.add_argument("--steps", type=int, default=20)
@@ -353,7 +414,8 @@ def main():
     a = p.parse_args()
     if not a.actors:
         a.actors = {"registry": 1 << 20, "optimus": 65536}.get(a.which, 131072)
-    {"host-rpc": host_rpc, "gpu-1m": gpu_1m, "optimus": optimus, "registry": registry, "tell": tell}[a.which](a)
+    {"host-rpc": host_rpc, "gpu-1m": gpu_1m, "optimus": optimus, "registry": registry, "tell": tell,
+     "xproc": xproc}[a.which](a)
 
 
 if __name__ == "__main__":

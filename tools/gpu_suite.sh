@@ -9,6 +9,7 @@ OUT=gpurun_out/suite_$TAG.jsonl
 timeout -k 10 300 python tools/bench_suite.py gpu-1m >> $OUT 2> gpurun_out/suite_$TAG.err || { echo "gpu-1m FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 timeout -k 10 300 python tools/bench_suite.py optimus >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "optimus FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 timeout -k 10 300 python tools/bench_suite.py tell >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "tell FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
+timeout -k 10 300 python tools/bench_suite.py xproc >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "xproc FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 timeout -k 10 300 python tools/bench_suite.py registry >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "registry FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 cat $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
