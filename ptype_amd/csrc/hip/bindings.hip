@@ -60,6 +60,7 @@ void launch_dispatch(uintptr_t, int, int64_t, int, bool, uintptr_t, uintptr_t, u
 void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 int64_t wire_req_words(int64_t, int, bool);
 int64_t wire_rep_words(int64_t);
+void launch_records_to_soa(uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 void launch_snapshot_copy(uintptr_t, uintptr_t, int64_t, uintptr_t);
 }  // namespace ptype
 
@@ -143,6 +144,9 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("stream"));
   m.def("complete", &launch_complete, py::arg("rep"), py::arg("C"), py::arg("perm"), py::arg("M"),
         py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"), py::arg("stream"));
+  m.def("records_to_soa", &launch_records_to_soa, py::arg("rec"), py::arg("M"), py::arg("actor"), py::arg("method"),
+        py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("mfma"), py::arg("stream"),
+        "32-B AoS request records -> SoA columns (dwordx4 copy, or MFMA byte transposition)");
   m.def("snapshot_copy", &launch_snapshot_copy, py::arg("dst"), py::arg("src"), py::arg("n16"),
         py::arg("stream"));
 

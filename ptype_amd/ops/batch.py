@@ -74,8 +74,20 @@ class MsgBatch:
         return MsgBatch(self.actor.index_select(0, idx), self.a0.index_select(0, idx), f(self.a1), f(self.a2), m)
 
     @staticmethod
-    def from_records(req: torch.Tensor) -> "MsgBatch":
-        """AoS int64[M,4] records -> SoA batch."""
+    def from_records(req: torch.Tensor, mfma: bool = False) -> "MsgBatch":
+        """AoS int64[M,4] records -> SoA batch (on the GPU: one kernel, see
+        csrc/hip/transpose.hip; ``mfma`` selects the MFMA byte-transposition
+        variant, kept for measurement -- the dwordx4 copy is faster)."""
+        if req.device.type == "cuda":
+            M = req.shape[0]
+            d = req.device
+            out = MsgBatch(torch.empty(M, dtype=torch.int32, device=d), torch.empty(M, dtype=torch.int64, device=d),
+                           torch.empty(M, dtype=torch.int64, device=d), torch.empty(M, dtype=torch.int64, device=d),
+                           torch.empty(M, dtype=torch.int16, device=d))
+            req = req.contiguous()
+            hip().records_to_soa(_ptr(req), M, _ptr(out.actor), _ptr(out.method), _ptr(out.a0), _ptr(out.a1),
+                                 _ptr(out.a2), bool(mfma), _stream(req))
+            return out
         actor, method, _, a0, a1, a2 = split_requests(req)
         return MsgBatch(actor.to(torch.int32).contiguous(), a0.contiguous(), a1.contiguous(), a2.contiguous(),
                         method.to(torch.int16).contiguous())

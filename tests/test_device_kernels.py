@@ -537,3 +537,22 @@ def test_gpu_exactly_once_1m(chunks):
     first = torch.cumsum(counts, 0) - counts
     rank_in_actor = torch.arange(M) - first[a_sorted]
     assert torch.equal(v_sorted, rank_in_actor + 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mfma", [False, True])
+def test_gpu_records_to_soa(mfma):
+    """AoS -> SoA on the device, both the dwordx4 copy and the MFMA byte
+    transposition, equal the CPU split (including negative / high-bit values and
+    a tail that is not a multiple of the 16-record MFMA tile)."""
+    M = 100_003
+    g = torch.Generator().manual_seed(3)
+    actor = torch.randint(0, 1 << 31, (M,), generator=g)
+    method = torch.randint(0, 1 << 15, (M,), generator=g)
+    a0, a1, a2 = (torch.randint(-(1 << 62), 1 << 62, (M,), generator=g) for _ in range(3))
+    req = make_requests(actor, method, a0, a1, a2)
+    ref = B.MsgBatch.from_records(req)
+    out = B.MsgBatch.from_records(req.cuda(), mfma=mfma)
+    torch.cuda.synchronize()
+    assert torch.equal(out.actor.cpu(), ref.actor) and torch.equal(out.method.cpu(), ref.method)
+    assert torch.equal(out.a0.cpu(), ref.a0) and torch.equal(out.a1.cpu(), ref.a1) and torch.equal(out.a2.cpu(), ref.a2)
