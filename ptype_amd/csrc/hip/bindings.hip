@@ -9,6 +9,7 @@
 #include <pybind11/stl.h>
 
 #include "common.hpp"
+#include "engine.hpp"
 #include "server.hpp"
 
 namespace py = pybind11;
@@ -155,6 +156,49 @@ PYBIND11_MODULE(_hip, m) {
   m.def("memcpy_d2h_async", &memcpy_d2h_async);
   m.def("memcpy_h2d_async", &memcpy_h2d_async);
   m.def("stream_sync", &stream_sync, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<EpochEngine>(m, "EpochEngine",
+                          "chunk-pipelined Send (route -> ncclAllToAll -> dispatch -> ncclAllToAll -> complete) "
+                          "enqueued from one host call; comm = raw ncclComm_t or 0 for no collectives")
+      .def(py::init<int, uintptr_t, int, int, int64_t, int64_t, int>(), py::arg("device"), py::arg("comm"),
+           py::arg("R"), py::arg("rank"), py::arg("C"), py::arg("max_chunk"), py::arg("chunks"))
+      .def(
+          "set_bufs",
+          [](EpochEngine& e, int i, uintptr_t send, uintptr_t recv, uintptr_t reply, uintptr_t back, uintptr_t perm,
+             uintptr_t src, uintptr_t route, uintptr_t hist, uintptr_t lb, uintptr_t ws) {
+            e.set_bufs(i, EngineBufs{send, recv, reply, back, perm, src, route, hist, lb, ws});
+          },
+          py::arg("i"), py::arg("send"), py::arg("recv"), py::arg("reply"), py::arg("back"), py::arg("perm"),
+          py::arg("src"), py::arg("route"), py::arg("hist"), py::arg("lb"), py::arg("ws"))
+      .def(
+          "send",
+          [](EpochEngine& e, uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+             int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
+             uint32_t affine_w, int nargs, bool mc, uintptr_t out_val, uintptr_t out_st, uintptr_t state,
+             uint32_t n_state, uint64_t delay_ticks, const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
+             bool direct, uintptr_t checksum, uintptr_t stream) {
+            e.send(EngineSend{actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, affine_w,
+                              nargs, mc, out_val, out_st, state, n_state, delay_ticks, outbox, outbox_cap, direct,
+                              checksum, stream});
+          },
+          py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("method_col"),
+          py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"),
+          py::arg("affine_w"), py::arg("nargs"), py::arg("mc"), py::arg("out_val"), py::arg("out_st"),
+          py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"), py::arg("outbox_cap"),
+          py::arg("direct"), py::arg("checksum"), py::arg("stream"))
+      .def("host_profile",
+           [](const EpochEngine& e) {
+             const auto p = e.host_profile();
+             py::dict d;
+             d["sends"] = p.sends;
+             d["kernels_ns"] = p.kernels_ns;
+             d["a2a_ns"] = p.a2a_ns;
+             d["sync_ns"] = p.sync_ns;
+             d["total_ns"] = p.total_ns;
+             return d;
+           })
+      .def("reset_host_profile", &EpochEngine::reset_host_profile);
+  m.def("rccl_available", [] { return rccl().alltoall != nullptr; });
 
   py::class_<DeviceServer>(m, "DeviceServer")
       .def(py::init<int, uint32_t, uintptr_t, uint32_t, uint64_t, double, double, const std::string&>(),

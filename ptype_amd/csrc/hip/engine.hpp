@@ -1,0 +1,271 @@
+// Native epoch engine: the whole chunk-pipelined Send of ActorExchange in one
+// host call.
+//
+// Per chunk: route kernels on the compute stream -> event -> ncclAllToAll of the
+// request slots on the engine's comm stream -> event -> dispatch on the compute
+// stream -> event -> ncclAllToAll of the reply slots -> event -> completion.
+// Chunk k's collectives overlap chunk k+1's route and chunk k-1's dispatch; the
+// host only enqueues (~10 us per step instead of ~100 us of Python per chunk,
+// which made a multi-GPU step host-bound -- measured with tools/host_overhead.py).
+//
+// RCCL is called directly on the communicator torch's process group already
+// owns (ProcessGroupNCCL._comm_ptr()); the entry points are resolved at run
+// time from the librccl torch loaded, so this module links no second copy.
+// Every rank issues the same collectives in the same order (the pipeline is
+// deterministic in the chunk count, which ActorExchange agrees collectively).
+#pragma once
+#include <dlfcn.h>
+
+#include <chrono>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace ptype {
+
+void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                  int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
+                  int64_t C, int nargs, bool mc, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist,
+                  uintptr_t lb, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
+                  uint32_t affine_w, uintptr_t stream);
+void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintptr_t reply, uintptr_t state,
+                     uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
+                     const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, const std::vector<uintptr_t>& direct,
+                     int self, uintptr_t stream);
+void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
+                     uintptr_t checksum, bool direct, uintptr_t stream);
+int64_t wire_req_words(int64_t C, int nargs, bool mc);
+int64_t wire_rep_words(int64_t C);
+
+// ---- RCCL entry points (from the library torch loaded)
+namespace engine_detail {
+typedef int (*AllToAllFn)(const void*, void*, size_t, int, void*, hipStream_t);
+typedef const char* (*ErrStrFn)(int);
+constexpr int kNcclInt8 = 0;  // ncclDataType_t ncclInt8
+
+struct Rccl {
+  AllToAllFn alltoall = nullptr;
+  ErrStrFn errstr = nullptr;
+  Rccl() {
+    alltoall = (AllToAllFn)dlsym(RTLD_DEFAULT, "ncclAllToAll");
+    errstr = (ErrStrFn)dlsym(RTLD_DEFAULT, "ncclGetErrorString");
+    if (!alltoall)
+      for (const char* lib : {"librccl.so", "librccl.so.1"}) {
+        void* h = dlopen(lib, RTLD_NOW | RTLD_NOLOAD);
+        if (!h) continue;
+        alltoall = (AllToAllFn)dlsym(h, "ncclAllToAll");
+        errstr = (ErrStrFn)dlsym(h, "ncclGetErrorString");
+        if (alltoall) break;
+      }
+  }
+};
+inline Rccl& rccl() {
+  static Rccl r;
+  return r;
+}
+}  // namespace engine_detail
+using engine_detail::rccl;
+using engine_detail::kNcclInt8;
+
+struct EngineBufs {
+  uintptr_t send, recv, reply, back, perm, src, route, hist, lb, ws;
+};
+
+struct EngineSend {  // one Send: the batch, the registry, the outputs
+  uintptr_t actor, a0, a1, a2, method_col;
+  int method_uniform;
+  int64_t M;
+  uintptr_t table;
+  uint64_t cap;
+  uintptr_t dir;
+  uint32_t n_dir, affine_w;
+  int nargs;
+  bool mc;
+  uintptr_t out_val, out_st, state;
+  uint32_t n_state;
+  uint64_t delay_ticks;
+  std::vector<uintptr_t> outbox;
+  uint64_t outbox_cap;
+  bool direct;
+  uintptr_t checksum;
+  uintptr_t stream;  // the caller's compute stream
+};
+
+class EpochEngine {
+ public:
+  EpochEngine(int device, uintptr_t comm, int R, int rank, int64_t C, int64_t max_chunk, int chunks)
+      : device_(device), comm_((void*)comm), R_(R), rank_(rank), C_(C), max_chunk_(max_chunk), chunks_(chunks) {
+    if (R < 1 || chunks < 1 || max_chunk < 1) throw std::invalid_argument("EpochEngine: bad geometry");
+    if (comm_ && !rccl().alltoall) throw std::runtime_error("EpochEngine: ncclAllToAll not found in the process");
+    PT_HIP_CHECK(hipSetDevice(device_));
+    int lo = 0, hi = 0;
+    PT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    PT_HIP_CHECK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));  // comm first
+    for (int i = 0; i < 2; ++i)
+      for (hipEvent_t* e : {&ev_route_[i], &ev_req_[i], &ev_disp_[i], &ev_rep_[i]})
+        PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  ~EpochEngine() {
+    hipSetDevice(device_);
+    hipStreamSynchronize(comm_stream_);
+    for (int i = 0; i < 2; ++i)
+      for (hipEvent_t e : {ev_route_[i], ev_req_[i], ev_disp_[i], ev_rep_[i]}) hipEventDestroy(e);
+    hipStreamDestroy(comm_stream_);
+  }
+
+  void set_bufs(int i, const EngineBufs& b) {
+    if (i < 0 || i > 1) throw std::invalid_argument("EpochEngine: two buffer sets");
+    bufs_[i] = b;
+    nbufs_ = std::max(nbufs_, i + 1);
+  }
+
+  // host-side cost split of the enqueues (ns): kernels, collectives, stream/event ops
+  struct HostProfile {
+    uint64_t sends = 0, kernels_ns = 0, a2a_ns = 0, sync_ns = 0, total_ns = 0;
+  };
+  HostProfile host_profile() const { return prof_; }
+  void reset_host_profile() { prof_ = HostProfile(); }
+
+  void send(const EngineSend& a) {
+    const uint64_t t0 = now();
+    send_impl(a);
+    prof_.total_ns += now() - t0;
+    ++prof_.sends;
+  }
+
+ private:
+  static uint64_t now() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
+  struct Timed {  // adds the scope's duration to one profile bucket
+    uint64_t& acc;
+    uint64_t t0;
+    explicit Timed(uint64_t& a) : acc(a), t0(now()) {}
+    ~Timed() { acc += now() - t0; }
+  };
+
+  void send_impl(const EngineSend& a) {
+    if (a.M > max_chunk_ * chunks_) throw std::invalid_argument("EpochEngine: batch exceeds max_batch");
+    if (nbufs_ < std::min(chunks_, 2)) throw std::runtime_error("EpochEngine: buffers not set");
+    const hipStream_t cs = as_stream(a.stream);
+    const int64_t wq = wire_req_words(C_, a.nargs, a.mc), wr = wire_rep_words(C_);
+    const bool local_only = R_ == 1;
+    const int n = chunks_;
+    std::deque<int> pending;  // chunks whose replies are in flight
+    int fwd = -1;
+    for (int i = 0; i < n; ++i) {
+      const int bi = i % nbufs_;
+      while (!pending.empty() && pending.front() <= i - nbufs_) {  // buffer reuse: replies consumed first
+        finish(a, pending.front(), cs, local_only);
+        pending.pop_front();
+      }
+      route(a, i, bi, cs, local_only);
+      if (comm_) {
+        join(comm_stream_, ev_route_[bi], cs);
+        a2a(bufs_[bi].send, bufs_[bi].recv, wq);
+        record(ev_req_[bi], comm_stream_);
+      }
+      if (fwd >= 0) {
+        serve(a, fwd, cs, wr);
+        pending.push_back(fwd);
+      }
+      fwd = i;
+    }
+    if (fwd >= 0) {
+      serve(a, fwd, cs, wr);
+      pending.push_back(fwd);
+    }
+    for (int j : pending) finish(a, j, cs, local_only);
+  }
+
+  int64_t m_of(const EngineSend& a, int i) const {
+    const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
+    return std::min<int64_t>(a.M, lo + max_chunk_) - lo;
+  }
+  static uintptr_t off(uintptr_t p, int64_t elems, int64_t size) { return p ? p + (uintptr_t)(elems * size) : 0; }
+
+  std::vector<uintptr_t> direct_view(const EngineSend& a, int i, int bi) const {
+    if (!a.direct) return {};
+    const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
+    return {bufs_[bi].src, off(a.out_val, lo, 8), off(a.out_st, lo, 4)};
+  }
+
+  void route(const EngineSend& a, int i, int bi, hipStream_t cs, bool local_only) {
+    const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M), m = m_of(a, i);
+    const bool write_perm = !(a.direct && local_only && !a.checksum);
+    const EngineBufs& b = bufs_[bi];
+    Timed t(prof_.kernels_ns);
+    launch_route(off(a.actor, lo, 4), off(a.a0, lo, 8), off(a.a1, lo, 8), off(a.a2, lo, 8), off(a.method_col, lo, 2),
+                 a.method_uniform, m, a.table, a.cap, a.dir, a.n_dir, R_, C_, a.nargs, a.mc, b.send,
+                 write_perm ? b.perm : 0, b.route, b.hist, b.lb, b.ws, rank_, direct_view(a, i, bi), a.affine_w,
+                 (uintptr_t)cs);
+  }
+
+  void serve(const EngineSend& a, int i, hipStream_t cs, int64_t wr) {
+    const int bi = i % nbufs_;
+    const EngineBufs& b = bufs_[bi];
+    if (comm_) wait(cs, ev_req_[bi]);
+    const int64_t m = m_of(a, i);
+    {
+      Timed t(prof_.kernels_ns);
+      launch_dispatch(comm_ ? b.recv : b.send, R_, C_, a.nargs, a.mc, b.reply, a.state, a.n_state, a.delay_ticks,
+                      b.ws, std::max<int64_t>(1, m / R_), a.outbox, a.outbox_cap, direct_view(a, i, bi), rank_,
+                      (uintptr_t)cs);
+    }
+    if (comm_) {
+      join(comm_stream_, ev_disp_[bi], cs);
+      a2a(b.reply, b.back, wr);
+      record(ev_rep_[bi], comm_stream_);
+    }
+  }
+
+  void finish(const EngineSend& a, int i, hipStream_t cs, bool local_only) {
+    const int bi = i % nbufs_;
+    if (comm_) wait(cs, ev_rep_[bi]);
+    if (a.direct && local_only && !a.checksum) return;  // every reply was written by the own-slot dispatch
+    Timed t(prof_.kernels_ns);
+    const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M), m = m_of(a, i);
+    const EngineBufs& b = bufs_[bi];
+    launch_complete(comm_ ? b.back : b.reply, C_, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4), a.checksum,
+                    a.direct, (uintptr_t)cs);
+  }
+
+  void record(hipEvent_t e, hipStream_t s) {
+    Timed t(prof_.sync_ns);
+    PT_HIP_CHECK(hipEventRecord(e, s));
+  }
+  void wait(hipStream_t s, hipEvent_t e) {
+    Timed t(prof_.sync_ns);
+    PT_HIP_CHECK(hipStreamWaitEvent(s, e, 0));
+  }
+  void join(hipStream_t waiter, hipEvent_t e, hipStream_t producer) {  // waiter runs after producer's work so far
+    record(e, producer);
+    wait(waiter, e);
+  }
+
+  void a2a(uintptr_t src, uintptr_t dst, int64_t words_per_peer) {
+    Timed t(prof_.a2a_ns);
+    const int rc = rccl().alltoall((const void*)src, (void*)dst, (size_t)words_per_peer * 4, kNcclInt8, comm_,
+                                   comm_stream_);
+    if (rc != 0)
+      throw std::runtime_error(std::string("ncclAllToAll failed: ") +
+                               (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+  }
+
+  int device_;
+  void* comm_;
+  int R_, rank_;
+  int64_t C_, max_chunk_;
+  int chunks_;
+  EngineBufs bufs_[2]{};
+  int nbufs_ = 0;
+  hipStream_t comm_stream_ = nullptr;
+  hipEvent_t ev_route_[2]{}, ev_req_[2]{}, ev_disp_[2]{}, ev_rep_[2]{};
+  HostProfile prof_;
+};
+
+}  // namespace ptype
