@@ -107,9 +107,8 @@ class EpochEngine {
       for (hipEvent_t* e : {&ev_route_[i], &ev_req_[i], &ev_disp_[i], &ev_rep_[i]})
         PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
-  ~EpochEngine() {
+  ~EpochEngine() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
     hipSetDevice(device_);
-    hipStreamSynchronize(comm_stream_);
     for (int i = 0; i < 2; ++i)
       for (hipEvent_t e : {ev_route_[i], ev_req_[i], ev_disp_[i], ev_rep_[i]}) hipEventDestroy(e);
     hipStreamDestroy(comm_stream_);

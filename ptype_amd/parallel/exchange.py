@@ -137,12 +137,13 @@ class ActorExchange:
             comm_ptr = backend._comm_ptr
         except (AttributeError, RuntimeError) as e:
             raise RuntimeError(f"native epoch engine needs an RCCL ('nccl') process group: {e}") from e
-        ptr = int(comm_ptr())
-        if ptr == 0:  # lazily created communicator: one collective brings it up
-            t = torch.zeros(1, device=self.device)
-            dist.all_reduce(t, group=self.group)
-            torch.cuda.synchronize(self.device)
+        with torch.cuda.device(self.device):  # _comm_ptr() answers for the current device
             ptr = int(comm_ptr())
+            if ptr == 0:  # lazily created communicator: one collective brings it up
+                t = torch.zeros(1, device=self.device)
+                dist.all_reduce(t, group=self.group)
+                torch.cuda.synchronize(self.device)
+                ptr = int(comm_ptr())
         if ptr == 0:
             raise RuntimeError("process group has no RCCL communicator for this device")
         return ptr
