@@ -15,43 +15,55 @@ from __future__ import annotations
 
 __version__ = "0.1.0"
 
-from . import _core  # noqa: F401  (host control plane; no GPU needed)
-from .cluster import (  # noqa: F401
-    Client,
-    Cluster,
-    Config,
-    ConfigFromFile,
-    ConnConfig,
-    Context,
-    DefaultConnConfig,
-    ErrNoClientAvailable,
-    ErrNoKey,
-    GetPrefixRangeEnd,
-    GoStruct,
-    GoUint,
-    Join,
-    KVStore,
-    New,
-    Node,
-    Registry,
-    Serve,
-    Server,
-    SortAscend,
-    SortByCreateRevision,
-    SortByKey,
-    SortByModRevision,
-    SortByValue,
-    SortByVersion,
-    SortDescend,
-    SortNone,
-    WithCountOnly,
-    WithFromKey,
-    WithKeysOnly,
-    WithLease,
-    WithLimit,
-    WithPrefix,
-    WithRange,
-    WithRev,
-    WithSerializable,
-    WithSort,
+# The public API needs the native control plane (``_core``).  It is imported
+# lazily so that ``python -m ptype_amd._build`` (and the driver's build())
+# works on a fresh checkout where no extension has been compiled yet.
+_API = (
+    "Client",
+    "Cluster",
+    "Config",
+    "ConfigFromFile",
+    "ConnConfig",
+    "Context",
+    "DefaultConnConfig",
+    "ErrNoClientAvailable",
+    "ErrNoKey",
+    "GetPrefixRangeEnd",
+    "GoStruct",
+    "GoUint",
+    "Join",
+    "KVStore",
+    "New",
+    "Node",
+    "Registry",
+    "Serve",
+    "Server",
+    "SortAscend",
+    "SortByCreateRevision",
+    "SortByKey",
+    "SortByModRevision",
+    "SortByValue",
+    "SortByVersion",
+    "SortDescend",
+    "SortNone",
+    "WithCountOnly",
+    "WithFromKey",
+    "WithKeysOnly",
+    "WithLease",
+    "WithLimit",
+    "WithPrefix",
+    "WithRange",
+    "WithRev",
+    "WithSerializable",
+    "WithSort",
 )
+
+__all__ = list(_API)
+
+
+def __getattr__(name):
+    if name in _API:
+        from . import cluster
+
+        return getattr(cluster, name)
+    raise AttributeError(f"module 'ptype_amd' has no attribute {name!r}")
