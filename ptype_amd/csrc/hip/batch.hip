@@ -214,7 +214,8 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
   __syncthreads();
   auto route_at = [route](int64_t i) { return route[i]; };
   for (int64_t tile = lo; tile < hi; tile += kScatterTile)
-    scatter_tile<NARGS, MC>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C, sendbuf, req_words,
+    scatter_tile<NARGS, MC>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C,
+                            V2Emit<NARGS, MC>{sendbuf, req_words},
                             perm, cnt, run, dv);
 }
 
@@ -433,6 +434,11 @@ static DirectView make_direct(const std::vector<uintptr_t>& direct, int self) {
   return dv;
 }
 
+int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir,
+                        uint32_t n_dir, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t route,
+                        uintptr_t hist, uintptr_t stats, int rank_self, uint32_t affine_w, uintptr_t stream,
+                        int64_t* P_out);
+
 void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
                   int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                   int64_t C, int nargs, bool mc, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist,
@@ -449,7 +455,31 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
     return;
   }
   int64_t P;
+  const int64_t G = route_prep_scan(actor, method_uniform, M, table, cap, dir, n_dir, R, C, req_words, sendbuf, route,
+                                    hist, stats, rank_self, affine_w, stream, &P);
+  hipStream_t s = as_stream(stream);
+  if (M > 0) {
+#define PT_SCATTER(NA, MCV)                                                                                         \
+  hipLaunchKernelGGL((route_scatter_kernel<NA, MCV>), dim3((unsigned)G), dim3(kRouteThreads), 0, s,                  \
+                     (const uint32_t*)route, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,             \
+                     (const uint16_t*)method_col, (uint32_t)method_uniform, M, P, R, C, (const uint32_t*)hist,      \
+                     (uint32_t*)sendbuf, req_words, (int32_t*)perm, dv)
+    PT_FORMAT_SWITCH(nargs, mc, PT_SCATTER)
+#undef PT_SCATTER
+  }
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+// Passes 1 + 2 of the 3-pass route (shared by wire formats v2 and v3): route
+// words + block histograms, then per-destination bases and slot headers in
+// regions of `req_words`.  Returns the block count G; *P_out = messages per block.
+int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir,
+                        uint32_t n_dir, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t route,
+                        uintptr_t hist, uintptr_t stats, int rank_self, uint32_t affine_w, uintptr_t stream,
+                        int64_t* P_out) {
+  int64_t P;
   const int64_t G = route_grid(M, &P);
+  *P_out = P;
   hipStream_t s = as_stream(stream);
   if (M > 0) {
     const dim3 g((unsigned)G);
@@ -472,16 +502,8 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
   }
   hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, s, (uint32_t*)hist, (int)G, R, C, (uint32_t*)sendbuf,
                      req_words, (uint32_t)method_uniform, (unsigned long long*)stats, rank_self);
-  if (M > 0) {
-#define PT_SCATTER(NA, MCV)                                                                                         \
-  hipLaunchKernelGGL((route_scatter_kernel<NA, MCV>), dim3((unsigned)G), dim3(kRouteThreads), 0, s,                  \
-                     (const uint32_t*)route, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,             \
-                     (const uint16_t*)method_col, (uint32_t)method_uniform, M, P, R, C, (const uint32_t*)hist,      \
-                     (uint32_t*)sendbuf, req_words, (int32_t*)perm, dv)
-    PT_FORMAT_SWITCH(nargs, mc, PT_SCATTER)
-#undef PT_SCATTER
-  }
   PT_HIP_CHECK(hipGetLastError());
+  return G;
 }
 
 void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintptr_t reply, uintptr_t state,

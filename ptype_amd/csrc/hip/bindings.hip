@@ -61,6 +61,16 @@ void launch_dispatch(uintptr_t, int, int64_t, int, bool, uintptr_t, uintptr_t, u
 void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 int64_t wire_req_words(int64_t, int, bool);
 int64_t wire_rep_words(int64_t);
+void launch_packed_meta(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uint32_t, uint32_t,
+                        uintptr_t, uintptr_t);
+void launch_route_packed(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t,
+                         uintptr_t, uint32_t, int, int64_t, const PackedLayout&, uintptr_t, uintptr_t, uintptr_t,
+                         uintptr_t, uintptr_t, int, const std::vector<uintptr_t>&, uint32_t, uintptr_t);
+void launch_dispatch_packed(uintptr_t, int, int64_t, const PackedLayout&, uintptr_t, uintptr_t, uint32_t, uint64_t,
+                            uintptr_t, int64_t, const std::vector<uintptr_t>&, uint64_t, const std::vector<uintptr_t>&,
+                            int, uintptr_t);
+void launch_complete_packed(uintptr_t, int64_t, int, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool,
+                            uintptr_t);
 void launch_records_to_soa(uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 void launch_snapshot_copy(uintptr_t, uintptr_t, int64_t, uintptr_t);
 }  // namespace ptype
@@ -87,6 +97,33 @@ static void memcpy_h2d_async(uintptr_t dst, uintptr_t src, size_t bytes, uintptr
   PT_HIP_CHECK(hipMemcpyAsync((void*)dst, (const void*)src, bytes, hipMemcpyHostToDevice, as_stream(stream)));
 }
 static void stream_sync(uintptr_t stream) { PT_HIP_CHECK(hipStreamSynchronize(as_stream(stream))); }
+
+namespace ptype {
+void check_packed_layout(const PackedLayout& L, int R, int64_t C);
+}
+
+// v3 layouts cross the binding as dicts {off: [5], w: [5], S, vb}
+static py::dict layout_dict(const PackedLayout& L) {
+  py::dict d;
+  d["off"] = std::vector<int>(L.off, L.off + 5);
+  d["w"] = std::vector<int>(L.w, L.w + 5);
+  d["S"] = (int)L.S;
+  d["vb"] = (int)L.vb;
+  return d;
+}
+static PackedLayout layout_of(const py::dict& d) {
+  PackedLayout L{};
+  const auto off = d["off"].cast<std::vector<int>>(), w = d["w"].cast<std::vector<int>>();
+  if (off.size() != 5 || w.size() != 5) throw std::invalid_argument("layout: off and w need 5 entries");
+  for (int q = 0; q < 5; ++q) {
+    if (off[q] < 0 || off[q] > 255 || w[q] < 0 || w[q] > 64) throw std::invalid_argument("layout: bad field");
+    L.off[q] = (uint8_t)off[q];
+    L.w[q] = (uint8_t)w[q];
+  }
+  L.S = (uint8_t)d["S"].cast<int>();
+  L.vb = (uint8_t)d["vb"].cast<int>();
+  return L;
+}
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "ptype_amd gfx950 device runtime: mailboxes, GPU registry, route/dispatch kernels";
@@ -151,6 +188,53 @@ PYBIND11_MODULE(_hip, m) {
   m.def("snapshot_copy", &launch_snapshot_copy, py::arg("dst"), py::arg("src"), py::arg("n16"),
         py::arg("stream"));
 
+  // ---- wire format v3 (packed.hpp): standalone kernels for tests and tools; the
+  // epoch engine drives them itself (meta all-reduce + layout) in a Send
+  m.attr("PACKED_META_WORDS") = (int)kMetaWords;
+  m.def("packed_meta", &launch_packed_meta, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"),
+        py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("n_dir"), py::arg("affine_w"),
+        py::arg("meta"), py::arg("stream"));
+  m.def(
+      "packed_layout",
+      [](const std::vector<uint64_t>& meta) {
+        if (meta.size() != (size_t)kMetaWords) throw std::invalid_argument("packed_layout: 16 meta words");
+        return layout_dict(packed_layout(meta.data()));
+      },
+      py::arg("meta"));
+  m.def("packed_reply_bits", [](const std::vector<uint64_t>& meta) {
+    if (meta.size() != (size_t)kMetaWords) throw std::invalid_argument("packed_reply_bits: 16 meta words");
+    return packed_reply_bits(meta.data());
+  });
+  m.def("packed_req_words", &packed_req_words, py::arg("C"), py::arg("S"));
+  m.def("packed_rep_words", &packed_rep_words, py::arg("C"), py::arg("vb"));
+  m.def(
+      "route_packed",
+      [](uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col, int method_uniform,
+         int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R, int64_t C,
+         const py::dict& layout, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist, uintptr_t stats,
+         int rank_self, const std::vector<uintptr_t>& direct, uint32_t affine_w, uintptr_t stream) {
+        launch_route_packed(actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, R, C,
+                            layout_of(layout), sendbuf, perm, route, hist, stats, rank_self, direct, affine_w, stream);
+      },
+      py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("method_col"), py::arg("method_uniform"),
+      py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"), py::arg("R"), py::arg("C"),
+      py::arg("layout"), py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"), py::arg("stats"),
+      py::arg("rank_self"), py::arg("direct"), py::arg("affine_w"), py::arg("stream"));
+  m.def(
+      "dispatch_packed",
+      [](uintptr_t recv, int R, int64_t C, const py::dict& layout, uintptr_t reply, uintptr_t state, uint32_t n_state,
+         uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank, const std::vector<uintptr_t>& outbox,
+         uint64_t outbox_cap, const std::vector<uintptr_t>& direct, int self, uintptr_t stream) {
+        launch_dispatch_packed(recv, R, C, layout_of(layout), reply, state, n_state, delay_ticks, stats,
+                               expected_per_rank, outbox, outbox_cap, direct, self, stream);
+      },
+      py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("layout"), py::arg("reply"), py::arg("state"),
+      py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"), py::arg("expected_per_rank"), py::arg("outbox"),
+      py::arg("outbox_cap"), py::arg("direct"), py::arg("self"), py::arg("stream"));
+  m.def("complete_packed", &launch_complete_packed, py::arg("rep"), py::arg("C"), py::arg("vb"), py::arg("perm"),
+        py::arg("M"), py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"),
+        py::arg("stream"));
+
   m.def("pinned_alloc", &pinned_alloc);
   m.def("pinned_free", &pinned_free);
   m.def("memcpy_d2h_async", &memcpy_d2h_async);
@@ -176,16 +260,26 @@ PYBIND11_MODULE(_hip, m) {
              int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
              uint32_t affine_w, int nargs, bool mc, uintptr_t out_val, uintptr_t out_st, uintptr_t state,
              uint32_t n_state, uint64_t delay_ticks, const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
-             bool direct, uintptr_t checksum, uintptr_t stream) {
+             bool direct, uintptr_t checksum, uintptr_t stream, bool packed) {
             e.send(EngineSend{actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, affine_w,
                               nargs, mc, out_val, out_st, state, n_state, delay_ticks, outbox, outbox_cap, direct,
-                              checksum, stream});
+                              checksum, stream, packed});
           },
           py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("method_col"),
           py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"),
           py::arg("affine_w"), py::arg("nargs"), py::arg("mc"), py::arg("out_val"), py::arg("out_st"),
           py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"), py::arg("outbox_cap"),
-          py::arg("direct"), py::arg("checksum"), py::arg("stream"))
+          py::arg("direct"), py::arg("checksum"), py::arg("stream"), py::arg("packed") = false)
+      .def("last_wire",
+           [](const EpochEngine& e) {
+             const auto& w = e.last_wire();
+             py::dict d = layout_dict(w.layout);
+             d["req_words"] = w.req_words;
+             d["rep_words"] = w.rep_words;
+             d["meta"] = std::vector<uint64_t>(w.meta, w.meta + kMetaWords);
+             return d;
+           },
+           "wire format of the last send: v3 layout (S == 0: v2), words per chunk on each all-to-all")
       .def("host_profile",
            [](const EpochEngine& e) {
              const auto p = e.host_profile();
@@ -194,6 +288,7 @@ PYBIND11_MODULE(_hip, m) {
              d["kernels_ns"] = p.kernels_ns;
              d["a2a_ns"] = p.a2a_ns;
              d["sync_ns"] = p.sync_ns;
+             d["meta_ns"] = p.meta_ns;
              d["total_ns"] = p.total_ns;
              return d;
            })

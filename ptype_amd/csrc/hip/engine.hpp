@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "packed.hpp"
 
 namespace ptype {
 
@@ -38,24 +39,45 @@ void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintpt
                      uintptr_t checksum, bool direct, uintptr_t stream);
 int64_t wire_req_words(int64_t C, int nargs, bool mc);
 int64_t wire_rep_words(int64_t C);
+// wire format v3 (packed.hpp / packed.hip)
+void launch_packed_meta(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                        int method_uniform, int64_t M, uint32_t n_dir, uint32_t affine_w, uintptr_t meta,
+                        uintptr_t stream);
+void launch_route_packed(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                         int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
+                         int R, int64_t C, const PackedLayout& L, uintptr_t sendbuf, uintptr_t perm, uintptr_t route,
+                         uintptr_t hist, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
+                         uint32_t affine_w, uintptr_t stream);
+void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout& L, uintptr_t reply, uintptr_t state,
+                            uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
+                            const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
+                            const std::vector<uintptr_t>& direct, int self, uintptr_t stream);
+void launch_complete_packed(uintptr_t rep, int64_t C, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
+                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream);
 
 // ---- RCCL entry points (from the library torch loaded)
 namespace engine_detail {
 typedef int (*AllToAllFn)(const void*, void*, size_t, int, void*, hipStream_t);
+typedef int (*AllReduceFn)(const void*, void*, size_t, int, int, void*, hipStream_t);
 typedef const char* (*ErrStrFn)(int);
-constexpr int kNcclInt8 = 0;  // ncclDataType_t ncclInt8
+constexpr int kNcclInt8 = 0;    // ncclDataType_t ncclInt8
+constexpr int kNcclUint64 = 5;  // ncclDataType_t ncclUint64
+constexpr int kNcclMax = 2;     // ncclRedOp_t ncclMax
 
 struct Rccl {
   AllToAllFn alltoall = nullptr;
+  AllReduceFn allreduce = nullptr;
   ErrStrFn errstr = nullptr;
   Rccl() {
     alltoall = (AllToAllFn)dlsym(RTLD_DEFAULT, "ncclAllToAll");
+    allreduce = (AllReduceFn)dlsym(RTLD_DEFAULT, "ncclAllReduce");
     errstr = (ErrStrFn)dlsym(RTLD_DEFAULT, "ncclGetErrorString");
     if (!alltoall)
       for (const char* lib : {"librccl.so", "librccl.so.1"}) {
         void* h = dlopen(lib, RTLD_NOW | RTLD_NOLOAD);
         if (!h) continue;
         alltoall = (AllToAllFn)dlsym(h, "ncclAllToAll");
+        allreduce = (AllReduceFn)dlsym(h, "ncclAllReduce");
         errstr = (ErrStrFn)dlsym(h, "ncclGetErrorString");
         if (alltoall) break;
       }
@@ -68,6 +90,8 @@ inline Rccl& rccl() {
 }  // namespace engine_detail
 using engine_detail::rccl;
 using engine_detail::kNcclInt8;
+using engine_detail::kNcclMax;
+using engine_detail::kNcclUint64;
 
 struct EngineBufs {
   uintptr_t send, recv, reply, back, perm, src, route, hist, lb, ws;
@@ -91,6 +115,7 @@ struct EngineSend {  // one Send: the batch, the registry, the outputs
   bool direct;
   uintptr_t checksum;
   uintptr_t stream;  // the caller's compute stream
+  bool packed;       // wire format v3 for this Send (needs collectives; not under graph capture)
 };
 
 class EpochEngine {
@@ -106,13 +131,29 @@ class EpochEngine {
     for (int i = 0; i < 2; ++i)
       for (hipEvent_t* e : {&ev_route_[i], &ev_req_[i], &ev_disp_[i], &ev_rep_[i]})
         PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    for (hipEvent_t* e : {&ev_meta_in_, &ev_meta_out_}) PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    PT_HIP_CHECK(hipMalloc(&meta_dev_, kMetaWords * sizeof(uint64_t)));
+    PT_HIP_CHECK(hipHostMalloc(&meta_host_, kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
   }
   ~EpochEngine() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
     hipSetDevice(device_);
     for (int i = 0; i < 2; ++i)
       for (hipEvent_t e : {ev_route_[i], ev_req_[i], ev_disp_[i], ev_rep_[i]}) hipEventDestroy(e);
+    hipEventDestroy(ev_meta_in_);
+    hipEventDestroy(ev_meta_out_);
     hipStreamDestroy(comm_stream_);
+    hipFree(meta_dev_);
+    hipHostFree(meta_host_);
   }
+
+  // Wire format of the last Send: v3 layout (S == 0: v2) and the words this rank
+  // put on each request / reply all-to-all per chunk (all peers, padded slots).
+  struct WireInfo {
+    PackedLayout layout{};
+    int64_t req_words = 0, rep_words = 0;
+    uint64_t meta[kMetaWords] = {};
+  };
+  const WireInfo& last_wire() const { return wire_; }
 
   void set_bufs(int i, const EngineBufs& b) {
     if (i < 0 || i > 1) throw std::invalid_argument("EpochEngine: two buffer sets");
@@ -122,7 +163,7 @@ class EpochEngine {
 
   // host-side cost split of the enqueues (ns): kernels, collectives, stream/event ops
   struct HostProfile {
-    uint64_t sends = 0, kernels_ns = 0, a2a_ns = 0, sync_ns = 0, total_ns = 0;
+    uint64_t sends = 0, kernels_ns = 0, a2a_ns = 0, sync_ns = 0, total_ns = 0, meta_ns = 0;
   };
   HostProfile host_profile() const { return prof_; }
   void reset_host_profile() { prof_ = HostProfile(); }
@@ -147,11 +188,24 @@ class EpochEngine {
     ~Timed() { acc += now() - t0; }
   };
 
-  void send_impl(const EngineSend& a) {
+  void send_impl(const EngineSend& in) {
+    EngineSend a = in;
+    if (a.packed) {  // v3 packs exactly the columns the format names (as v2's scatter reads them)
+      if (a.nargs < 2) a.a1 = 0;
+      if (a.nargs < 3) a.a2 = 0;
+    }
     if (a.M > max_chunk_ * chunks_) throw std::invalid_argument("EpochEngine: batch exceeds max_batch");
     if (nbufs_ < std::min(chunks_, 2)) throw std::runtime_error("EpochEngine: buffers not set");
     const hipStream_t cs = as_stream(a.stream);
-    const int64_t wq = wire_req_words(C_, a.nargs, a.mc), wr = wire_rep_words(C_);
+    packed_ = a.packed && comm_ != nullptr;  // v3 only where bytes cross a collective
+    if (packed_) agree_layout(a, cs);
+    const int64_t wq = packed_ ? packed_req_words(C_, L_.S) : wire_req_words(C_, a.nargs, a.mc);
+    const int64_t wr = packed_ ? packed_rep_words(C_, L_.vb) : wire_rep_words(C_);
+    if (packed_ && (wq > wire_req_words(C_, a.nargs, a.mc) || wr > wire_rep_words(C_)))
+      throw std::logic_error("EpochEngine: packed regions exceed the v2 slot buffers");  // cannot happen (packed.hpp)
+    wire_.layout = packed_ ? L_ : PackedLayout{};
+    wire_.req_words = R_ * wq;
+    wire_.rep_words = R_ * wr;
     const bool local_only = R_ == 1;
     const int n = chunks_;
     std::deque<int> pending;  // chunks whose replies are in flight
@@ -181,6 +235,31 @@ class EpochEngine {
     for (int j : pending) finish(a, j, cs, local_only);
   }
 
+  // v3: column maxima of this rank's batch -> ncclAllReduce(MAX) over the node
+  // -> host.  The one host wait of a packed Send: every rank derives the same
+  // layout from the same agreed vector, so slot geometry stays equal-split.
+  void agree_layout(const EngineSend& a, hipStream_t cs) {
+    if (!rccl().allreduce) throw std::runtime_error("EpochEngine: ncclAllReduce not found in the process");
+    const uint64_t t0 = now();
+    {
+      Timed t(prof_.kernels_ns);
+      launch_packed_meta(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.n_dir, a.affine_w,
+                         (uintptr_t)meta_dev_, (uintptr_t)cs);
+    }
+    join(comm_stream_, ev_meta_in_, cs);
+    const int rc = rccl().allreduce(meta_dev_, meta_dev_, kMetaWords, kNcclUint64, kNcclMax, comm_, comm_stream_);
+    if (rc != 0)
+      throw std::runtime_error(std::string("ncclAllReduce failed: ") +
+                               (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+    PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                comm_stream_));
+    PT_HIP_CHECK(hipEventRecord(ev_meta_out_, comm_stream_));
+    PT_HIP_CHECK(hipEventSynchronize(ev_meta_out_));
+    for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
+    L_ = packed_layout(meta_host_);
+    prof_.meta_ns += now() - t0;
+  }
+
   int64_t m_of(const EngineSend& a, int i) const {
     const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
     return std::min<int64_t>(a.M, lo + max_chunk_) - lo;
@@ -198,6 +277,13 @@ class EpochEngine {
     const bool write_perm = !(a.direct && local_only && !a.checksum);
     const EngineBufs& b = bufs_[bi];
     Timed t(prof_.kernels_ns);
+    if (packed_) {
+      launch_route_packed(off(a.actor, lo, 4), off(a.a0, lo, 8), off(a.a1, lo, 8), off(a.a2, lo, 8),
+                          off(a.method_col, lo, 2), a.method_uniform, m, a.table, a.cap, a.dir, a.n_dir, R_, C_, L_,
+                          b.send, write_perm ? b.perm : 0, b.route, b.hist, b.ws, rank_, direct_view(a, i, bi),
+                          a.affine_w, (uintptr_t)cs);
+      return;
+    }
     launch_route(off(a.actor, lo, 4), off(a.a0, lo, 8), off(a.a1, lo, 8), off(a.a2, lo, 8), off(a.method_col, lo, 2),
                  a.method_uniform, m, a.table, a.cap, a.dir, a.n_dir, R_, C_, a.nargs, a.mc, b.send,
                  write_perm ? b.perm : 0, b.route, b.hist, b.lb, b.ws, rank_, direct_view(a, i, bi), a.affine_w,
@@ -211,9 +297,14 @@ class EpochEngine {
     const int64_t m = m_of(a, i);
     {
       Timed t(prof_.kernels_ns);
-      launch_dispatch(comm_ ? b.recv : b.send, R_, C_, a.nargs, a.mc, b.reply, a.state, a.n_state, a.delay_ticks,
-                      b.ws, std::max<int64_t>(1, m / R_), a.outbox, a.outbox_cap, direct_view(a, i, bi), rank_,
-                      (uintptr_t)cs);
+      if (packed_)
+        launch_dispatch_packed(b.recv, R_, C_, L_, b.reply, a.state, a.n_state, a.delay_ticks, b.ws,
+                               std::max<int64_t>(1, m / R_), a.outbox, a.outbox_cap, direct_view(a, i, bi), rank_,
+                               (uintptr_t)cs);
+      else
+        launch_dispatch(comm_ ? b.recv : b.send, R_, C_, a.nargs, a.mc, b.reply, a.state, a.n_state, a.delay_ticks,
+                        b.ws, std::max<int64_t>(1, m / R_), a.outbox, a.outbox_cap, direct_view(a, i, bi), rank_,
+                        (uintptr_t)cs);
     }
     if (comm_) {
       join(comm_stream_, ev_disp_[bi], cs);
@@ -229,8 +320,12 @@ class EpochEngine {
     Timed t(prof_.kernels_ns);
     const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M), m = m_of(a, i);
     const EngineBufs& b = bufs_[bi];
-    launch_complete(comm_ ? b.back : b.reply, C_, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4), a.checksum,
-                    a.direct, (uintptr_t)cs);
+    if (packed_)
+      launch_complete_packed(b.back, C_, L_.vb, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4), a.checksum,
+                             a.direct, (uintptr_t)cs);
+    else
+      launch_complete(comm_ ? b.back : b.reply, C_, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4),
+                      a.checksum, a.direct, (uintptr_t)cs);
   }
 
   void record(hipEvent_t e, hipStream_t s) {
@@ -264,6 +359,12 @@ class EpochEngine {
   int nbufs_ = 0;
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t ev_route_[2]{}, ev_req_[2]{}, ev_disp_[2]{}, ev_rep_[2]{};
+  hipEvent_t ev_meta_in_{}, ev_meta_out_{};
+  uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)
+  uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
+  bool packed_ = false;
+  PackedLayout L_{};
+  WireInfo wire_;
   HostProfile prof_;
 };
 

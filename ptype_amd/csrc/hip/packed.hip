@@ -1,0 +1,392 @@
+// Wire format v3 kernels (see packed.hpp): the width pass that feeds the
+// per-Send agreement, the packing scatter, the unpacking dispatch with a
+// value-plane + ok-bitmap reply, and the completion that decodes it.
+//
+// Route passes 1 + 2 (route words, histograms, bases, slot headers) are the
+// v2 kernels (batch.hip: route_prep_scan) run with v3 region sizes; only the
+// record writer of the scatter differs (PackedEmit).
+#include <vector>
+
+#include "common.hpp"
+#include "handlers.hpp"
+#include "packed.hpp"
+#include "route_common.hpp"
+
+namespace ptype {
+
+int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir,
+                        uint32_t n_dir, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t route,
+                        uintptr_t hist, uintptr_t stats, int rank_self, uint32_t affine_w, uintptr_t stream,
+                        int64_t* P_out);
+
+constexpr int kStatTooWide = 4;  // workspace stat word: replies that did not fit vb (never, by construction)
+
+// ---- width pass: column maxima of one batch -> meta[kMetaWords] (atomic max)
+__global__ __launch_bounds__(256) void packed_meta_kernel(const uint32_t* __restrict__ actor,
+                                                          const int64_t* __restrict__ a0,
+                                                          const int64_t* __restrict__ a1,
+                                                          const int64_t* __restrict__ a2,
+                                                          const uint16_t* __restrict__ mcol, uint32_t method_uniform,
+                                                          int64_t M, uint32_t n_dir, uint32_t aw,
+                                                          unsigned long long* __restrict__ meta) {
+  uint64_t mb = 0, z0 = 0, z1 = 0, z2 = 0, mm = 0;
+  uint32_t flags = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t a = __builtin_nontemporal_load(actor + i);
+    // affine directory: the route is (a % aw, a / aw); otherwise any mailbox below kMaxMbox
+    const uint64_t m = (aw && a < n_dir) ? a / aw : (uint64_t)(kMaxMbox - 1);
+    mb = m > mb ? m : mb;
+    const uint64_t x0 = zz_enc(__builtin_nontemporal_load(a0 + i));
+    z0 = x0 > z0 ? x0 : z0;
+    if (a1) {
+      const uint64_t x = zz_enc(__builtin_nontemporal_load(a1 + i));
+      z1 = x > z1 ? x : z1;
+    }
+    if (a2) {
+      const uint64_t x = zz_enc(__builtin_nontemporal_load(a2 + i));
+      z2 = x > z2 ? x : z2;
+    }
+    if (mcol) {
+      const uint32_t meth = mcol[i];
+      mm = meth > mm ? meth : mm;
+      flags |= 1u << (meth < 7 ? meth : 7);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    uint64_t t;
+    t = __shfl_xor(mb, off), mb = t > mb ? t : mb;
+    t = __shfl_xor(z0, off), z0 = t > z0 ? t : z0;
+    t = __shfl_xor(z1, off), z1 = t > z1 ? t : z1;
+    t = __shfl_xor(z2, off), z2 = t > z2 ? t : z2;
+    t = __shfl_xor(mm, off), mm = t > mm ? t : mm;
+    flags |= __shfl_xor(flags, off);
+  }
+  __shared__ uint64_t part[256 / kWave][6];
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == 0) {
+    part[w][0] = mb, part[w][1] = z0, part[w][2] = z1, part[w][3] = z2, part[w][4] = mm, part[w][5] = flags;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {  // words 0..3 = mailbox, a0..a2; thread 4 -> kMetaMethod
+    uint64_t v = 0;
+    for (int k = 0; k < 256 / kWave; ++k) v = part[k][threadIdx.x] > v ? part[k][threadIdx.x] : v;
+    if (v) atomicMax(meta + (threadIdx.x == 4 ? (int)kMetaMethod : (int)threadIdx.x), (unsigned long long)v);
+  } else if (threadIdx.x == 5) {
+    uint32_t f = 0;
+    for (int k = 0; k < 256 / kWave; ++k) f |= (uint32_t)part[k][5];
+    if (M > 0 && blockIdx.x == 0) {
+      if (mcol) {
+        atomicMax(meta + kMetaMcol, 1ull);
+      } else {
+        f |= 1u << (method_uniform < 7 ? method_uniform : 7);
+        atomicMax(meta + kMetaMethod, (unsigned long long)method_uniform);
+      }
+    }
+    while (f) {
+      const int b = __builtin_ctz(f);
+      atomicMax(meta + kMetaFlags + b, 1ull);
+      f &= f - 1;
+    }
+  }
+}
+
+// ---- scatter: v3 record writer for scatter_tile
+template <int S>
+struct PackedEmit {
+  uint32_t* sendbuf;
+  int64_t req_words;
+  PackedLayout L;
+  __device__ __forceinline__ void operator()(int d, int64_t pos, uint32_t mbox, const int64_t (&v)[3],
+                                             uint32_t meth) const {
+    const uint64_t f[5] = {meth, mbox, zz_enc(v[0]), zz_enc(v[1]), zz_enc(v[2])};
+    uint32_t rec[S];
+    packed_pack<S>(L, f, rec);
+    store_words<S>(sendbuf + (int64_t)d * req_words + 4 + pos * S, rec);
+  }
+};
+
+template <int S>
+__global__ __launch_bounds__(kRouteThreads) void route_scatter_packed_kernel(
+    const uint32_t* __restrict__ route, const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
+    const int64_t* __restrict__ a2, const uint16_t* __restrict__ method_col, uint32_t method_uniform, int64_t M,
+    int64_t P, int R, int64_t C, const uint32_t* __restrict__ base, uint32_t* __restrict__ sendbuf,
+    int64_t req_words, PackedLayout L, int32_t* __restrict__ perm, DirectView dv) {
+  __shared__ unsigned cnt[kScatterItems][kRouteThreads / kWave][kMaxRanks];
+  __shared__ unsigned run[kMaxRanks];
+  for (int d = threadIdx.x; d < R; d += blockDim.x) run[d] = base[(int64_t)blockIdx.x * (R + 1) + d];
+  const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
+  if (dv.src) dv.identity = ((sendbuf[(int64_t)dv.self * req_words + 3] >> 16) & kFlagIdentity) != 0;
+  __syncthreads();
+  auto route_at = [route](int64_t i) { return route[i]; };
+  // every column is read when present (null-checked): the layout's widths say what is packed
+  for (int64_t tile = lo; tile < hi; tile += kScatterTile)
+    scatter_tile<3, true>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C,
+                          PackedEmit<S>{sendbuf, req_words, L}, perm, cnt, run, dv);
+}
+
+// ---- dispatch: unpack, run the handler, reply into the value plane + ok bitmap
+template <int S, int FIXED>
+__device__ __forceinline__ unsigned long long dispatch_range_packed(
+    const uint32_t* __restrict__ rq, int64_t count, uint32_t hdr_method, PackedLayout L, uint8_t* __restrict__ vals,
+    unsigned long long* __restrict__ okmap, int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks,
+    OutboxView ob, DirectView dv, bool direct, bool ident, unsigned long long& toowide) {
+  unsigned long long failed = 0;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  const unsigned lane = lane_id();
+  // wave-uniform loop: each iteration covers 64 consecutive slots (base % 64 == 0),
+  // so one lane writes the wave's whole ok-bitmap word -- no atomics
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~(kWave - 1)); base < count; base += step) {
+    const int64_t s = base + lane;
+    const bool in = s < count;
+    ReplyRecord rr;
+    rr.value = 0;
+    rr.status = kStatusOk;
+    if (in) {
+      uint32_t wv[S];
+      load_words<S>(rq + 4 + s * S, wv);
+      MsgRecord m;
+      m.actor = (uint32_t)packed_field<S>(L, 1, wv);
+      m.method = (uint16_t)(FIXED ? FIXED : (L.w[0] ? (uint32_t)packed_field<S>(L, 0, wv) : hdr_method));
+      m.flags = kFlagValid | kFlagRouted;
+      m.a0 = zz_dec(packed_field<S>(L, 2, wv));
+      m.a1 = zz_dec(packed_field<S>(L, 3, wv));
+      m.a2 = zz_dec(packed_field<S>(L, 4, wv));
+      rr = run_handler(m, state, n_state, delay_ticks, ob);
+    }
+    if (direct) {  // own slot: straight into the caller's outputs, no wire, no width limit
+      failed += in && rr.status != kStatusOk;
+      if (in) {
+        const int64_t i = ident ? s : (int64_t)dv.src[s];
+        dv.out_val[i] = rr.value;
+        dv.out_st[i] = rr.status;
+      }
+      continue;
+    }
+    bool ok = rr.status == kStatusOk;
+    uint64_t code = ok ? (L.vb == 8 ? (uint64_t)rr.value : zz_enc(rr.value)) : (uint64_t)rr.status;
+    if (ok && L.vb < 8 && (code >> (8 * L.vb))) {  // impossible under the agreed bounds: fail loudly
+      ok = false;
+      code = kStatusFailed;
+      toowide += in;
+    }
+    failed += in && !ok;
+    const unsigned long long bits = __ballot(in && ok);
+    if (in) {
+      switch (L.vb) {
+        case 1: vals[s] = (uint8_t)code; break;
+        case 2: reinterpret_cast<uint16_t*>(vals)[s] = (uint16_t)code; break;
+        case 4: reinterpret_cast<uint32_t*>(vals)[s] = (uint32_t)code; break;
+        default: reinterpret_cast<uint64_t*>(vals)[s] = code;
+      }
+    }
+    if (lane == 0) okmap[base / kWave] = bits;
+  }
+  return failed;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void dispatch_packed_kernel(const uint32_t* __restrict__ recv, int64_t req_words,
+                                                              int64_t C, PackedLayout L, uint32_t* __restrict__ reply,
+                                                              int64_t rep_words, int64_t* __restrict__ state,
+                                                              uint32_t n_state, uint64_t delay_ticks,
+                                                              unsigned long long* __restrict__ stats, OutboxView ob,
+                                                              DirectView dv) {
+  const int d = blockIdx.y;
+  const bool direct = dv.src != nullptr && d == dv.self;
+  const uint32_t* rq = recv + (int64_t)d * req_words;
+  const uint4 h = *reinterpret_cast<const uint4*>(rq);
+  const bool valid = (h.w >> 16) & kFlagValid;
+  const int64_t count = valid ? (int64_t)(h.x < C ? h.x : C) : 0;
+  uint32_t* rp = reply + (int64_t)d * rep_words;
+  uint8_t* vals = reinterpret_cast<uint8_t*>(rp + 4);
+  unsigned long long* okmap = reinterpret_cast<unsigned long long*>(rp + 4 + packed_val_words(C, L.vb));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
+  const uint32_t hm = h.w & 0xffffu;
+  const bool ident = direct && ((h.w >> 16) & kFlagIdentity);
+  unsigned long long toowide = 0, failed;
+  if (!L.w[0] && hm == kCalculatorMultiply)  // uniform hot method: the handler switch constant-folds
+    failed = dispatch_range_packed<S, kCalculatorMultiply>(rq, count, hm, L, vals, okmap, state, n_state, delay_ticks,
+                                                           ob, dv, direct, ident, toowide);
+  else
+    failed = dispatch_range_packed<S, 0>(rq, count, hm, L, vals, okmap, state, n_state, delay_ticks, ob, dv, direct,
+                                         ident, toowide);
+  for (int off = 32; off > 0; off >>= 1) {
+    failed += __shfl_xor(failed, off);
+    toowide += __shfl_xor(toowide, off);
+  }
+  if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);
+  if (lane_id() == 0 && toowide) atomicAdd(&stats[kStatTooWide], toowide);
+}
+
+// ---- K8 for v3 replies
+__global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
+                                                              uint32_t C, int vb, const int32_t* __restrict__ perm,
+                                                              int64_t M, int64_t* __restrict__ out_val,
+                                                              int32_t* __restrict__ out_st,
+                                                              unsigned long long* __restrict__ checksum, bool direct) {
+  const int64_t vw = packed_val_words(C, vb);
+  unsigned long long sum = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t p = perm[i];
+    if (direct && p < 0) {
+      if (checksum) sum += (unsigned long long)out_val[i];
+      continue;
+    }
+    int64_t v = 0;
+    int32_t st;
+    if (p >= 0) {
+      const uint32_t d = (uint32_t)p / C, pos = (uint32_t)p - d * C;
+      const uint32_t* rb = rep + (int64_t)d * rep_words;
+      const uint8_t* vals = reinterpret_cast<const uint8_t*>(rb + 4);
+      const unsigned long long okw = reinterpret_cast<const unsigned long long*>(rb + 4 + vw)[pos / kWave];
+      uint64_t code;
+      switch (vb) {
+        case 1: code = vals[pos]; break;
+        case 2: code = reinterpret_cast<const uint16_t*>(vals)[pos]; break;
+        case 4: code = reinterpret_cast<const uint32_t*>(vals)[pos]; break;
+        default: code = reinterpret_cast<const uint64_t*>(vals)[pos];
+      }
+      if ((okw >> (pos % kWave)) & 1) {
+        v = vb == 8 ? (int64_t)code : zz_dec(code);
+        st = kStatusOk;
+      } else {
+        st = (int32_t)code;
+      }
+    } else {
+      st = p == -1 ? kStatusOverflow : kStatusNoActor;
+    }
+    out_val[i] = v;
+    out_st[i] = st;
+    sum += (unsigned long long)v;
+  }
+  if (checksum) {
+    __shared__ unsigned long long part[4];
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+    if (lane_id() == 0) part[threadIdx.x / kWave] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(checksum, part[0] + part[1] + part[2] + part[3]);
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+static unsigned grid_for(int64_t work, int per, unsigned cap) {
+  const int64_t g = (work + per - 1) / per;
+  return (unsigned)(g < 1 ? 1 : g > cap ? cap : g);
+}
+
+static DirectView direct_of(const std::vector<uintptr_t>& direct, int self) {
+  DirectView dv;
+  if (!direct.empty()) {
+    if (direct.size() != 3) throw std::invalid_argument("direct: [src, out_val, out_status]");
+    dv.src = (int32_t*)direct[0];
+    dv.out_val = (int64_t*)direct[1];
+    dv.out_st = (int32_t*)direct[2];
+    dv.self = self;
+  }
+  return dv;
+}
+
+void check_packed_layout(const PackedLayout& L, int R, int64_t C) {
+  if (L.S < 1 || L.S > 8) throw std::invalid_argument("packed layout: 1 <= S <= 8 dwords");
+  if (L.vb != 1 && L.vb != 2 && L.vb != 4 && L.vb != 8) throw std::invalid_argument("packed layout: vb in {1,2,4,8}");
+  int end = 0;
+  for (int q = 0; q < 5; ++q) {
+    if (L.w[q] > 64) throw std::invalid_argument("packed layout: field wider than 64 bits");
+    end = std::max(end, L.off[q] + L.w[q]);
+  }
+  if (end > 32 * L.S) throw std::invalid_argument("packed layout: fields exceed the record");
+  if (R < 1 || R > kMaxRanks) throw std::invalid_argument("route: 1 <= R <= 64");
+  if (C < 1 || C >= (1ll << 31) / R) throw std::invalid_argument("route: bad capacity");
+}
+
+void launch_packed_meta(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                        int method_uniform, int64_t M, uint32_t n_dir, uint32_t affine_w, uintptr_t meta,
+                        uintptr_t stream) {
+  hipStream_t s = as_stream(stream);
+  PT_HIP_CHECK(hipMemsetAsync((void*)meta, 0, kMetaWords * sizeof(uint64_t), s));
+  if (M > 0 && (!a0 || !actor)) throw std::invalid_argument("packed meta: actor and a0 columns required");
+  hipLaunchKernelGGL(packed_meta_kernel, dim3(grid_for(M, 256 * 8, 2048)), dim3(256), 0, s, (const uint32_t*)actor,
+                     (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col,
+                     (uint32_t)method_uniform, M, n_dir, affine_w, (unsigned long long*)meta);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+#define PT_S_SWITCH(S_, F) \
+  switch (S_) {            \
+    case 1: F(1); break;   \
+    case 2: F(2); break;   \
+    case 3: F(3); break;   \
+    case 4: F(4); break;   \
+    case 5: F(5); break;   \
+    case 6: F(6); break;   \
+    case 7: F(7); break;   \
+    default: F(8); break;  \
+  }
+
+void launch_route_packed(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                         int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
+                         int R, int64_t C, const PackedLayout& L, uintptr_t sendbuf, uintptr_t perm, uintptr_t route,
+                         uintptr_t hist, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
+                         uint32_t affine_w, uintptr_t stream) {
+  check_packed_layout(L, R, C);
+  if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
+  if (method_col && !L.w[0]) throw std::invalid_argument("route: method column needs a method field in the layout");
+  const DirectView dv = direct_of(direct, rank_self);
+  const int64_t req_words = packed_req_words(C, L.S);
+  int64_t P;
+  const int64_t G = route_prep_scan(actor, method_uniform, M, table, cap, dir, n_dir, R, C, req_words, sendbuf, route,
+                                    hist, stats, rank_self, affine_w, stream, &P);
+  if (M > 0) {
+#define PT_SCATTER_P(SV)                                                                                             \
+  hipLaunchKernelGGL((route_scatter_packed_kernel<SV>), dim3((unsigned)G), dim3(kRouteThreads), 0, as_stream(stream), \
+                     (const uint32_t*)route, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,              \
+                     (const uint16_t*)method_col, (uint32_t)method_uniform, M, P, R, C, (const uint32_t*)hist,       \
+                     (uint32_t*)sendbuf, req_words, L, (int32_t*)perm, dv)
+    PT_S_SWITCH(L.S, PT_SCATTER_P)
+#undef PT_SCATTER_P
+  }
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout& L, uintptr_t reply, uintptr_t state,
+                            uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
+                            const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
+                            const std::vector<uintptr_t>& direct, int self, uintptr_t stream) {
+  check_packed_layout(L, R, C);
+  const DirectView dv = direct_of(direct, self);
+  OutboxView ob;
+  if (outbox_cap) {
+    if (outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
+    ob.actor = (uint32_t*)outbox[0];
+    ob.a0 = (int64_t*)outbox[1];
+    ob.a1 = (int64_t*)outbox[2];
+    ob.a2 = (int64_t*)outbox[3];
+    ob.method = (uint16_t*)outbox[4];
+    ob.count = (unsigned long long*)outbox[5];
+    ob.cap = outbox_cap;
+  }
+  const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
+  const unsigned gx = grid_for(per, 256, (unsigned)(4096 / R > 0 ? 4096 / R : 1));
+  const int64_t req_words = packed_req_words(C, L.S), rep_words = packed_rep_words(C, L.vb);
+#define PT_DISPATCH_P(SV)                                                                                          \
+  hipLaunchKernelGGL((dispatch_packed_kernel<SV>), dim3(gx, R), dim3(256), 0, as_stream(stream),                    \
+                     (const uint32_t*)recv, req_words, C, L, (uint32_t*)reply, rep_words, (int64_t*)state, n_state, \
+                     delay_ticks, (unsigned long long*)stats, ob, dv)
+  PT_S_SWITCH(L.S, PT_DISPATCH_P)
+#undef PT_DISPATCH_P
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_complete_packed(uintptr_t rep, int64_t C, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
+                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream) {
+  if (M <= 0) return;
+  if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
+  if (vb != 1 && vb != 2 && vb != 4 && vb != 8) throw std::invalid_argument("complete: vb in {1,2,4,8}");
+  hipLaunchKernelGGL(complete_packed_kernel, dim3(grid_for(M, 256, checksum ? 1024 : 8192)), dim3(256), 0,
+                     as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, vb,
+                     (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum,
+                     direct);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace ptype

@@ -1,0 +1,147 @@
+// Wire format v3 ("packed"): width-adaptive bit-packed epoch records for the
+// multi-GPU exchange, where xGMI bytes -- not kernels -- bound a Send.
+//
+// The reference's wire is gob (encoding/gob behind stdlib net/rpc, used at
+// cluster/rpc.go:65 and :88), which writes every integer as a variable-length
+// value: Args{A: 7, B: 8} costs a few bytes, not two machine words.  A GPU
+// epoch cannot give each record its own length (receivers index records by
+// slot position, and the all-to-all is equal-split), so v3 applies the same
+// idea per *exchange*: before an epoch every rank reduces its batch to column
+// maxima (mailbox bound, zigzag magnitude of each argument, methods present),
+// one 16-word ncclAllReduce(MAX) agrees them across the node, and every record
+// of the Send is packed into the fewest dwords that hold
+//
+//     [method : wm] [mailbox : wx] [a0 : w0] [a1 : w1] [a2 : w2]     (LSB first)
+//
+// with zigzag-encoded arguments (gob's signed-int encoding).  Replies carry a
+// value plane of vb in {1, 2, 4, 8} bytes per record, sized from the methods
+// present and the argument bounds (e.g. Multiply: |A*B| <= |A|max * |B|max), plus
+// an ok-bitmap; a non-OK reply carries its status code in the value field.
+//
+// Calculator.Multiply on the headline bench (A in [-2^15, 2^15), B in
+// [0, 2^16), 131072 mailboxes per rank): 17 + 16 + 17 = 50 bits -> 8 B per
+// request and 4 B + 1 bit per reply, against 20 B + 9 B in v2 -- 2.4x fewer
+// bytes on every all-to-all.  Values that do not fit are impossible by
+// construction (the widths are global maxima); the dispatcher still checks
+// every reply against vb and fails it loudly rather than truncating.
+//
+// Region sizes (u32 words, every region 16-B aligned, like v2):
+//   request per destination: round4(4 + C * S)           header as in v2
+//   reply per destination:   round4(4 + V + 2 * ceil(C / 64))
+//                            header {count,0,0,0}; value plane V = 2 * ceil(C * vb / 8)
+//                            words; ok bitmap as u64 words (bit s = record s ok)
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "records.hpp"
+
+namespace ptype {
+
+// Meta vector reduced per Send (u64 words; ncclAllReduce MAX across ranks).
+enum PackedMeta : int {
+  kMetaMbox = 0,    // largest local mailbox index any record may carry
+  kMetaArg0 = 1,    // largest zigzag(a_j), j = 0..2 -> words 1..3
+  kMetaMethod = 4,  // largest method id sent
+  kMetaMcol = 5,    // 1 if any rank sends a per-record method column (then every record carries one)
+  kMetaFlags = 8,   // words 8..15: 1 if method id (word - 8) occurs; word 15: ids >= 7
+  kMetaWords = 16,
+};
+
+struct PackedLayout {  // passed BY VALUE to kernels (lands in SGPRs)
+  uint8_t off[5];  // bit offsets: 0 method, 1 mailbox, 2..4 args
+  uint8_t w[5];    // bit widths (0 = field absent / all zero)
+  uint8_t S;       // dwords per request record (1..8)
+  uint8_t vb;      // reply value bytes (1, 2, 4, 8)
+};
+
+__host__ __device__ __forceinline__ uint64_t zz_enc(int64_t v) { return ((uint64_t)v << 1) ^ (uint64_t)(v >> 63); }
+__host__ __device__ __forceinline__ int64_t zz_dec(uint64_t z) { return (int64_t)(z >> 1) ^ -(int64_t)(z & 1); }
+__host__ __device__ __forceinline__ uint64_t low_mask(int w) { return w >= 64 ? ~0ull : ((1ull << w) - 1); }
+
+inline int bit_len(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+__host__ __device__ inline int64_t packed_req_words(int64_t C, int S) { return (4 + C * S + 3) & ~3ll; }
+__host__ __device__ inline int64_t packed_val_words(int64_t C, int vb) { return 2 * ((C * vb + 7) / 8); }
+__host__ __device__ inline int64_t packed_rep_words(int64_t C, int vb) {
+  return (4 + packed_val_words(C, vb) + 2 * ((C + 63) / 64) + 3) & ~3ll;
+}
+
+// Reply value bits for the methods present (flags) under argument bounds.
+// Every bound holds for any int64 inputs within the maxima, so a handler's
+// reply never exceeds it (the dispatcher checks again on the device).
+inline int packed_reply_bits(const uint64_t* meta) {
+  auto flag = [&](int m) { return meta[kMetaFlags + m] != 0; };
+  const uint64_t z0 = meta[kMetaArg0], z1 = meta[kMetaArg0 + 1], z2 = meta[kMetaArg0 + 2];
+  auto mag = [](uint64_t z) { return (unsigned __int128)(z / 2 + (z & 1)); };  // |v| <= mag(zz(v))
+  int bits = 0;
+  if (flag(kCalculatorMultiply)) {  // zz(a * b) <= 2 |a| |b|
+    const unsigned __int128 p = 2 * mag(z0) * mag(z1);
+    bits = std::max(bits, (p >> 64) ? 64 : bit_len((uint64_t)p));
+  }
+  if (flag(kEcho)) bits = std::max(bits, bit_len(z0));
+  if (flag(kPrimeCheck)) {  // the target or a divisor in [a0, min(a1, a2)): |reply| <= max |a_j|
+    const uint64_t z = std::max(z0, std::max(z1, z2));
+    bits = std::max(bits, z == ~0ull ? 64 : bit_len(z + 1));
+  }
+  // stateful / forwarding / unknown handlers: state-dependent replies are full width
+  if (flag(kRetryTest) || flag(kCounterAdd) || flag(kForward) || meta[kMetaFlags + 7] != 0) bits = 64;
+  return std::max(bits, 8);  // a non-OK reply carries its status code in the value field
+}
+
+// Layout from the agreed meta vector alone, so every rank derives the same one
+// whatever columns its own batch has (a missing column contributes zeros).
+inline PackedLayout packed_layout(const uint64_t* meta) {
+  PackedLayout L{};
+  int off = 0;
+  auto put = [&](int q, int w) {
+    L.off[q] = (uint8_t)off;
+    L.w[q] = (uint8_t)w;
+    off += w;
+  };
+  put(0, meta[kMetaMcol] ? std::max(1, bit_len(meta[kMetaMethod])) : 0);
+  put(1, bit_len(meta[kMetaMbox]));
+  for (int j = 0; j < 3; ++j) put(2 + j, bit_len(meta[kMetaArg0 + j]));
+  L.S = (uint8_t)std::max(1, (off + 31) / 32);
+  if (L.S > 8) throw std::logic_error("packed layout: record exceeds 8 dwords");
+  const int vbits = packed_reply_bits(meta);
+  L.vb = (uint8_t)(vbits <= 8 ? 1 : vbits <= 16 ? 2 : vbits <= 32 ? 4 : 8);
+  return L;
+}
+
+#ifdef __HIPCC__
+// Dword j of a record from compile-time S and runtime field offsets: every
+// (dword, field) pair is a pair of selects over shifts, never an indexed
+// register array (indexed arrays are what made hipcc spill to scratch before).
+template <int S>
+__device__ __forceinline__ void packed_pack(const PackedLayout L, const uint64_t (&f)[5], uint32_t (&rec)[S]) {
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const int sh = (int)L.off[q] - 32 * j;
+      const uint64_t v = f[q] & low_mask(L.w[q]);
+      if (L.w[q] && sh >= 0 && sh < 32) x |= (uint32_t)(v << sh);
+      else if (L.w[q] && sh < 0 && sh > -64) x |= (uint32_t)(v >> -sh);
+    }
+    rec[j] = x;
+  }
+}
+
+template <int S>
+__device__ __forceinline__ uint64_t packed_field(const PackedLayout L, int q, const uint32_t (&rec)[S]) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int sh = 32 * j - (int)L.off[q];
+    if (sh >= 0 && sh < 64) v |= (uint64_t)rec[j] << sh;
+    else if (sh < 0 && sh > -32) v |= (uint64_t)(rec[j] >> -sh);
+  }
+  return L.w[q] ? (v & low_mask(L.w[q])) : 0ull;
+}
+#endif
+
+}  // namespace ptype

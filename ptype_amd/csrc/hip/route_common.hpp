@@ -127,16 +127,14 @@ struct DirectView {
 // `route_at(i)` yields message i's route word; `run[d]` is the next free slot
 // position of destination d for this block and is advanced past the tile.
 // Block-level: every thread of the block must call it (two barriers inside).
-template <int NARGS, bool MC, class RouteAt>
+template <int NARGS, bool MC, class RouteAt, class Emit>
 __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt route_at,
                                              const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
                                              const int64_t* __restrict__ a2,
                                              const uint16_t* __restrict__ method_col, uint32_t method_uniform,
-                                             int R, int64_t C, uint32_t* __restrict__ sendbuf, int64_t req_words,
-                                             int32_t* __restrict__ perm,
+                                             int R, int64_t C, Emit emit, int32_t* __restrict__ perm,
                                              unsigned (&cnt)[kScatterItems][kRouteThreads / kWave][kMaxRanks],
                                              unsigned* run, DirectView dv) {
-  constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
   const unsigned tid = threadIdx.x, w = tid / kWave, lane = lane_id();
   int d[kScatterItems];
   uint32_t rw[kScatterItems], meth[kScatterItems];
@@ -209,18 +207,31 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
     } else {
       perm[i] = (int32_t)((int64_t)d[k] * C + pos);  // never null here: remote replies need it
     }
-    uint32_t* o = sendbuf + (int64_t)d[k] * req_words + 4 + pos * kStride;
-    uint32_t rec[kStride];
-    rec[0] = rw[k] >> 8;  // local mailbox index at the destination
-    if constexpr (MC) rec[1] = meth[k] & 0xffffu;
-#pragma unroll
-    for (int j = 0; j < NARGS; ++j) {
-      rec[1 + (MC ? 1 : 0) + 2 * j] = (uint32_t)v[k][j];
-      rec[2 + (MC ? 1 : 0) + 2 * j] = (uint32_t)((uint64_t)v[k][j] >> 32);
-    }
-    store_words<kStride>(o, rec);
+    emit(d[k], pos, rw[k] >> 8, v[k], meth[k]);
   }
   __syncthreads();
 }
+
+// Wire format v2 record writer for scatter_tile: mbox, [method], args as lo/hi
+// dword pairs at a fixed stride of 1 + MC + 2 * NARGS dwords.
+template <int NARGS, bool MC>
+struct V2Emit {
+  uint32_t* sendbuf;
+  int64_t req_words;
+  __device__ __forceinline__ void operator()(int d, int64_t pos, uint32_t mbox, const int64_t (&v)[3],
+                                             uint32_t meth) const {
+    constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
+    uint32_t* o = sendbuf + (int64_t)d * req_words + 4 + pos * kStride;
+    uint32_t rec[kStride];
+    rec[0] = mbox;  // local mailbox index at the destination
+    if constexpr (MC) rec[1] = meth & 0xffffu;
+#pragma unroll
+    for (int j = 0; j < NARGS; ++j) {
+      rec[1 + (MC ? 1 : 0) + 2 * j] = (uint32_t)v[j];
+      rec[2 + (MC ? 1 : 0) + 2 * j] = (uint32_t)((uint64_t)v[j] >> 32);
+    }
+    store_words<kStride>(o, rec);
+  }
+};
 
 }  // namespace ptype

@@ -186,7 +186,8 @@ __global__ __launch_bounds__(kRouteThreads) void route_fused_kernel(
   // ---- phase 3: stable placement from the LDS route words
   auto route_at = [lo](int64_t i) { return lds_route[i - lo]; };
   for (int64_t tile = lo; tile < hi; tile += kScatterTile)
-    scatter_tile<NARGS, MC>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C, sendbuf, req_words,
+    scatter_tile<NARGS, MC>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C,
+                            V2Emit<NARGS, MC>{sendbuf, req_words},
                             perm, cnt, run, dv);
 }
 

@@ -17,8 +17,9 @@ from .records import (FLAG_IDENTITY, FLAG_VALID, METHOD_CALC_MULTIPLY, STATUS_NO
 from .table import RegistryTable, actor_keys, mix64
 
 # workspace words (int64): [0:4) stats [nomatch, overflow, failed, route-error flag]
-WS_WORDS = 4
+WS_WORDS = 8
 STAT_NOMATCH, STAT_OVERFLOW, STAT_FAILED, STAT_ROUTE_ERROR = 0, 1, 2, 3
+STAT_TOOWIDE = 4  # wire v3: replies wider than the agreed value plane (never, by construction)
 ROUTE_NO_ACTOR = 0xFF
 MAX_MBOX = 1 << 24  # route word = rank | mbox << 8
 

@@ -67,6 +67,7 @@ class EpochStats:
     overflow: int = 0  # device counters (cumulative): overflowed, no-actor, handler-failed
     nomatch: int = 0
     failed: int = 0
+    toowide: int = 0  # wire v3 replies that did not fit the agreed value plane (must stay 0)
 
 
 class _ChunkBufs:
@@ -92,7 +93,8 @@ class ActorExchange:
     """
 
     def __init__(self, table: RegistryTable, max_batch: int, chunks: int = 1, group=None, state=None,
-                 delay_us: int = 0, slack: float = 0.01, fmt: B.WireFormat | None = None):
+                 delay_us: int = 0, slack: float = 0.01, fmt: B.WireFormat | None = None,
+                 packed: bool | None = None):
         self.table = table
         self.device = table.device
         self.group = group
@@ -126,6 +128,11 @@ class ActorExchange:
         self.counters = EpochStats()
         self._engine = None  # native epoch engine, built on first GPU send
         self.use_engine = self.device.type == "cuda" and os.environ.get("PTYPE_ENGINE", "1") != "0"
+        # wire format v3 (csrc/hip/packed.hpp): width-adaptive packed records on the
+        # all-to-alls, agreed per Send by one 16-word all-reduce (native engine, collectives on)
+        self.packed = os.environ.get("PTYPE_WIRE", "v3") != "v2" if packed is None else bool(packed)
+        self._capturing = False  # a captured graph cannot host the v3 agreement (host wait)
+        self.last_wire = None  # engine.last_wire() of the latest native send
 
     def _comm_ptr(self) -> int:
         """Raw ncclComm_t of the group's RCCL backend (0 without collectives)."""
@@ -174,8 +181,17 @@ class ActorExchange:
             int(req.method) if uniform else 0, req.M, B._ptr(self.table.table), self.table.cap, B._ptr(d), n_dir,
             affine, fmt.nargs, fmt.method_col, B._ptr(out_val), B._ptr(out_status), B._ptr(state),
             0 if state is None else state.numel(), int(self.delay_us) * 100, ob, ob_cap, self.direct,
-            B._ptr(self.checksum), torch.cuda.current_stream(self.device).cuda_stream)
+            B._ptr(self.checksum), torch.cuda.current_stream(self.device).cuda_stream, self.packed_active())
+        if self.world > 1 or self.force_collectives:
+            w = self._engine.last_wire()
+            self.last_wire = w
+            self.counters.wire_bytes += self.chunks * 4 * (w["req_words"] + w["rep_words"])
         return out_val, out_status
+
+    def packed_active(self) -> bool:
+        """Whether the next native send uses wire format v3."""
+        return bool(self.packed and self.use_engine and not self._capturing
+                    and (self.world > 1 or self.force_collectives))
 
     # ------------------------------------------------------------------
     def _a2a(self, out, inp):
@@ -203,8 +219,6 @@ class ActorExchange:
         wq, wr = R * fmt.req_words(C), R * B.WireFormat.rep_words(C)
         self.counters.sent += M
         self.counters.epochs += n
-        if R > 1 or self.force_collectives:
-            self.counters.wire_bytes += n * 4 * (wq + wr)
         if self.use_engine and self._engine is None:
             try:
                 self._get_engine()
@@ -215,6 +229,8 @@ class ActorExchange:
         if self.use_engine:
             with trace.range("ptype.send"):
                 return self._send_native(req, out_val, out_status, fmt)
+        if R > 1 or self.force_collectives:
+            self.counters.wire_bytes += n * 4 * (wq + wr)
         pending_bwd = []  # (chunk index, work handle, bufs)
 
         direct = self.direct
@@ -347,6 +363,7 @@ class ActorExchange:
             s.nomatch += w[B.STAT_NOMATCH]
             s.overflow += w[B.STAT_OVERFLOW]
             s.failed += w[B.STAT_FAILED]
+            s.toowide += int(b.ws[B.STAT_TOOWIDE])
             if w[B.STAT_ROUTE_ERROR]:
                 raise RuntimeError("route look-back stalled: epoch results are invalid")
         return s
@@ -367,6 +384,7 @@ class SendGraph:
             ex.send(req, out_val, out_status)
 
         ex.table.directory()  # build outside the capture if dirty
+        ex._capturing = True  # fixed-geometry v2 slots inside the graph (no host wait)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
