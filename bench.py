@@ -46,6 +46,18 @@ def _parse():
     return p.parse_args()
 
 
+def wire_info(ex, req) -> dict:
+    """Bytes per message on the all-to-alls: wire v3 (packed, agreed per Send) when
+    the exchange ran collectives through the native engine, else wire v2."""
+    from ptype_amd.ops import batch as B
+
+    w = ex.last_wire
+    if w is not None and w["S"]:
+        return {"wire": "v3-packed", "record_bytes": 4 * w["S"], "reply_bytes": w["vb"] + 0.125,
+                "field_bits": w["w"]}
+    return {"wire": "v2", "record_bytes": 4 * (ex.fmt or B.WireFormat.for_batch(req)).stride, "reply_bytes": 9}
+
+
 def main():
     args = _parse()
     import torch
@@ -202,8 +214,7 @@ def main():
                 "msgs_per_gpu_per_step": M,
                 "actors": n_actors,
                 "chunks": chunks,
-                "record_bytes": 4 * (ex.fmt or B.WireFormat.for_batch(req)).stride,
-                "reply_bytes": 9,
+                **wire_info(ex, req),
                 "client_batch": "SoA (actor u32, A i64, B i64)",
                 "hip_graph": graph is not None,
             },

@@ -128,18 +128,23 @@ class EpochEngine {
     int lo = 0, hi = 0;
     PT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     PT_HIP_CHECK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));  // comm first
-    for (int i = 0; i < 2; ++i)
+    // Hand-off events keep the default system-scope release unless
+    // PTYPE_EVENT_SCOPE=device: RCCL may move a buffer with peer reads / writes
+    // over xGMI, which must see (and not be hidden by) this GPU's L2 contents.
+    const char* scope = getenv("PTYPE_EVENT_SCOPE");
+    const unsigned ev_flags =
+        hipEventDisableTiming | ((scope && std::string(scope) == "device") ? hipEventReleaseToDevice : 0u);
+    for (int i = 0; i < kMaxBufs; ++i)
       for (hipEvent_t* e : {&ev_route_[i], &ev_req_[i], &ev_disp_[i], &ev_rep_[i]})
-        PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    for (hipEvent_t* e : {&ev_meta_in_, &ev_meta_out_}) PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        PT_HIP_CHECK(hipEventCreateWithFlags(e, ev_flags));
+    PT_HIP_CHECK(hipEventCreateWithFlags(&ev_meta_out_, hipEventDisableTiming));
     PT_HIP_CHECK(hipMalloc(&meta_dev_, kMetaWords * sizeof(uint64_t)));
     PT_HIP_CHECK(hipHostMalloc(&meta_host_, kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
   }
   ~EpochEngine() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
     hipSetDevice(device_);
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < kMaxBufs; ++i)
       for (hipEvent_t e : {ev_route_[i], ev_req_[i], ev_disp_[i], ev_rep_[i]}) hipEventDestroy(e);
-    hipEventDestroy(ev_meta_in_);
     hipEventDestroy(ev_meta_out_);
     hipStreamDestroy(comm_stream_);
     hipFree(meta_dev_);
@@ -156,7 +161,7 @@ class EpochEngine {
   const WireInfo& last_wire() const { return wire_; }
 
   void set_bufs(int i, const EngineBufs& b) {
-    if (i < 0 || i > 1) throw std::invalid_argument("EpochEngine: two buffer sets");
+    if (i < 0 || i >= kMaxBufs) throw std::invalid_argument("EpochEngine: at most 4 buffer sets");
     bufs_[i] = b;
     nbufs_ = std::max(nbufs_, i + 1);
   }
@@ -195,7 +200,7 @@ class EpochEngine {
       if (a.nargs < 3) a.a2 = 0;
     }
     if (a.M > max_chunk_ * chunks_) throw std::invalid_argument("EpochEngine: batch exceeds max_batch");
-    if (nbufs_ < std::min(chunks_, 2)) throw std::runtime_error("EpochEngine: buffers not set");
+    if (nbufs_ < 1) throw std::runtime_error("EpochEngine: buffers not set");
     const hipStream_t cs = as_stream(a.stream);
     packed_ = a.packed && comm_ != nullptr;  // v3 only where bytes cross a collective
     if (packed_) agree_layout(a, cs);
@@ -246,14 +251,15 @@ class EpochEngine {
       launch_packed_meta(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.n_dir, a.affine_w,
                          (uintptr_t)meta_dev_, (uintptr_t)cs);
     }
-    join(comm_stream_, ev_meta_in_, cs);
-    const int rc = rccl().allreduce(meta_dev_, meta_dev_, kMetaWords, kNcclUint64, kNcclMax, comm_, comm_stream_);
+    // on the compute stream itself: the previous Send's collectives are complete
+    // there already (its completions waited for them), and no cross-stream hop
+    // sits on this, the one host wait of the Send
+    const int rc = rccl().allreduce(meta_dev_, meta_dev_, kMetaWords, kNcclUint64, kNcclMax, comm_, cs);
     if (rc != 0)
       throw std::runtime_error(std::string("ncclAllReduce failed: ") +
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
-    PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                                comm_stream_));
-    PT_HIP_CHECK(hipEventRecord(ev_meta_out_, comm_stream_));
+    PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost, cs));
+    PT_HIP_CHECK(hipEventRecord(ev_meta_out_, cs));
     PT_HIP_CHECK(hipEventSynchronize(ev_meta_out_));
     for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
     L_ = packed_layout(meta_host_);
@@ -355,11 +361,12 @@ class EpochEngine {
   int R_, rank_;
   int64_t C_, max_chunk_;
   int chunks_;
-  EngineBufs bufs_[2]{};
+  static constexpr int kMaxBufs = 4;  // chunks in flight without waiting for buffer reuse
+  EngineBufs bufs_[kMaxBufs]{};
   int nbufs_ = 0;
   hipStream_t comm_stream_ = nullptr;
-  hipEvent_t ev_route_[2]{}, ev_req_[2]{}, ev_disp_[2]{}, ev_rep_[2]{};
-  hipEvent_t ev_meta_in_{}, ev_meta_out_{};
+  hipEvent_t ev_route_[kMaxBufs]{}, ev_req_[kMaxBufs]{}, ev_disp_[kMaxBufs]{}, ev_rep_[kMaxBufs]{};
+  hipEvent_t ev_meta_out_{};
   uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)
   uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
   bool packed_ = false;

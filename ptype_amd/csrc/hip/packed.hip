@@ -31,26 +31,40 @@ __global__ __launch_bounds__(256) void packed_meta_kernel(const uint32_t* __rest
                                                           unsigned long long* __restrict__ meta) {
   uint64_t mb = 0, z0 = 0, z1 = 0, z2 = 0, mm = 0;
   uint32_t flags = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t a = __builtin_nontemporal_load(actor + i);
+  auto take = [&](uint32_t a, int64_t v0, int64_t v1, int64_t v2, uint32_t meth) {
     // affine directory: the route is (a % aw, a / aw); otherwise any mailbox below kMaxMbox
     const uint64_t m = (aw && a < n_dir) ? a / aw : (uint64_t)(kMaxMbox - 1);
     mb = m > mb ? m : mb;
-    const uint64_t x0 = zz_enc(__builtin_nontemporal_load(a0 + i));
+    const uint64_t x0 = zz_enc(v0), x1 = zz_enc(v1), x2 = zz_enc(v2);
     z0 = x0 > z0 ? x0 : z0;
-    if (a1) {
-      const uint64_t x = zz_enc(__builtin_nontemporal_load(a1 + i));
-      z1 = x > z1 ? x : z1;
+    z1 = x1 > z1 ? x1 : z1;
+    z2 = x2 > z2 ? x2 : z2;
+    mm = meth > mm ? meth : mm;
+    flags |= 1u << (meth < 7 ? meth : 7);
+  };
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // 4 elements per iteration, every load issued before any is used: the pass is
+  // one streaming read of the batch and needs the memory-level parallelism
+  for (; i + 3 * stride < M; i += 4 * stride) {
+    uint32_t a[4], me[4] = {0, 0, 0, 0};
+    int64_t v0[4], v1[4] = {0, 0, 0, 0}, v2[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = __builtin_nontemporal_load(actor + i + k * stride);
+      v0[k] = __builtin_nontemporal_load(a0 + i + k * stride);
+      if (a1) v1[k] = __builtin_nontemporal_load(a1 + i + k * stride);
+      if (a2) v2[k] = __builtin_nontemporal_load(a2 + i + k * stride);
+      if (mcol) me[k] = mcol[i + k * stride];
     }
-    if (a2) {
-      const uint64_t x = zz_enc(__builtin_nontemporal_load(a2 + i));
-      z2 = x > z2 ? x : z2;
-    }
-    if (mcol) {
-      const uint32_t meth = mcol[i];
-      mm = meth > mm ? meth : mm;
-      flags |= 1u << (meth < 7 ? meth : 7);
-    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) take(a[k], v0[k], v1[k], v2[k], me[k]);
+  }
+  for (; i < M; i += stride)
+    take(actor[i], a0[i], a1 ? a1[i] : 0, a2 ? a2[i] : 0, mcol ? (uint32_t)mcol[i] : 0u);
+  if (!mcol) {  // uniform method: no column maxima (flagged once per batch below)
+    mm = 0;
+    flags = 0;
   }
   for (int off = 32; off > 0; off >>= 1) {
     uint64_t t;
