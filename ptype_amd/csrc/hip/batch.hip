@@ -211,6 +211,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
   const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
   if (dv.src)  // the scan flagged a gap-free single slot: positions are message indices
     dv.identity = ((sendbuf[(int64_t)dv.self * req_words + 3] >> 16) & kFlagIdentity) != 0;
+  if (dv.identity && dv.zero_copy) return;  // block-uniform: the dispatch reads the batch in place
   __syncthreads();
   auto route_at = [route](int64_t i) { return route[i]; };
   for (int64_t tile = lo; tile < hi; tile += kScatterTile)
@@ -260,12 +261,36 @@ __device__ __forceinline__ unsigned long long dispatch_range(const uint32_t* __r
   return failed;
 }
 
+// Zero-copy local delivery (LocalView): the identity slot's records are the
+// caller's columns; slot position s is message s.
+template <int NARGS, bool MC, int FIXED>
+__device__ __forceinline__ unsigned long long dispatch_local_range(LocalView lv, int64_t count, uint32_t hdr_method,
+                                                                   int64_t* __restrict__ state, uint32_t n_state,
+                                                                   uint64_t delay_ticks, OutboxView ob,
+                                                                   DirectView dv) {
+  unsigned long long failed = 0;
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count; s += (int64_t)gridDim.x * blockDim.x) {
+    MsgRecord m;
+    m.actor = __builtin_nontemporal_load(lv.route + s) >> 8;
+    m.method = (uint16_t)(FIXED ? FIXED : (MC && lv.mcol ? (uint32_t)lv.mcol[s] : hdr_method));
+    m.flags = kFlagValid | kFlagRouted;
+    m.a0 = __builtin_nontemporal_load(lv.a0 + s);
+    m.a1 = NARGS > 1 && lv.a1 ? __builtin_nontemporal_load(lv.a1 + s) : 0;
+    m.a2 = NARGS > 2 && lv.a2 ? __builtin_nontemporal_load(lv.a2 + s) : 0;
+    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
+    failed += rr.status != kStatusOk;
+    __builtin_nontemporal_store(rr.value, dv.out_val + s);
+    __builtin_nontemporal_store((int32_t)rr.status, dv.out_st + s);
+  }
+  return failed;
+}
+
 template <int NARGS, bool MC>
 __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restrict__ recv, int64_t req_words,
                                                        int64_t C, uint32_t* __restrict__ reply, int64_t rep_words,
                                                        int64_t* __restrict__ state, uint32_t n_state,
                                                        uint64_t delay_ticks, unsigned long long* __restrict__ stats,
-                                                       OutboxView ob, DirectView dv) {
+                                                       OutboxView ob, DirectView dv, LocalView lv) {
   const int d = blockIdx.y;
   const bool direct = dv.src != nullptr && d == dv.self;
   const uint32_t* rq = recv + (int64_t)d * req_words;
@@ -281,7 +306,12 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
   const uint32_t hm = h.w & 0xffffu;
   const bool ident = direct && ((h.w >> 16) & kFlagIdentity);
   unsigned long long failed;
-  if constexpr (!MC) {
+  if (ident && lv.route) {  // zero-copy: the scatter left the slot empty
+    failed = (!MC && hm == kCalculatorMultiply)
+                 ? dispatch_local_range<NARGS, MC, kCalculatorMultiply>(lv, count, hm, state, n_state, delay_ticks,
+                                                                         obp, dv)
+                 : dispatch_local_range<NARGS, MC, 0>(lv, count, hm, state, n_state, delay_ticks, obp, dv);
+  } else if constexpr (!MC) {
     switch (hm) {  // uniform per slot: one specialised loop per hot method
       case kCalculatorMultiply:
         failed = dispatch_range<NARGS, MC, kCalculatorMultiply>(rq, count, hm, vals, sts, state, n_state,
@@ -443,13 +473,16 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
                   int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                   int64_t C, int nargs, bool mc, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist,
                   uintptr_t lb, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
-                  uint32_t affine_w, uintptr_t stream) {
-  const DirectView dv = make_direct(direct, rank_self);
+                  uint32_t affine_w, uintptr_t stream, bool zero_copy) {
+  DirectView dv = make_direct(direct, rank_self);
+  if (zero_copy && (R != 1 || !dv.src || perm))
+    throw std::invalid_argument("route: zero-copy local delivery needs R == 1, direct completion and no perm");
+  dv.zero_copy = zero_copy;
   check_format(nargs, C, R);
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
   if (method_col && !mc) throw std::invalid_argument("route: method column needs a method-column wire format");
   const int64_t req_words = wire_req_words(C, nargs, mc);
-  if (g_route_mode == 1 && lb) {
+  if (g_route_mode == 1 && lb && !zero_copy) {
     launch_route_fused(actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, R, C, nargs, mc,
                        req_words, sendbuf, perm, lb, stats, rank_self, dv, stream);
     return;
@@ -509,8 +542,18 @@ int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_
 void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintptr_t reply, uintptr_t state,
                      uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
                      const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, const std::vector<uintptr_t>& direct,
-                     int self, uintptr_t stream) {
+                     int self, uintptr_t stream, const std::vector<uintptr_t>& local) {
   const DirectView dv = make_direct(direct, self);
+  LocalView lv;
+  if (!local.empty()) {
+    if (local.size() != 5) throw std::invalid_argument("local: [route, a0, a1, a2, method_col]");
+    if (!dv.src || R != 1) throw std::invalid_argument("local: zero-copy delivery needs direct completion at R == 1");
+    lv.route = (const uint32_t*)local[0];
+    lv.a0 = (const int64_t*)local[1];
+    lv.a1 = (const int64_t*)local[2];
+    lv.a2 = (const int64_t*)local[3];
+    lv.mcol = (const uint16_t*)local[4];
+  }
   OutboxView ob;
   if (outbox_cap) {
     if (outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
@@ -529,7 +572,7 @@ void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintp
 #define PT_DISPATCH(NA, MCV)                                                                                    \
   hipLaunchKernelGGL((dispatch_kernel<NA, MCV>), dim3(gx, R), dim3(256), 0, as_stream(stream),                  \
                      (const uint32_t*)recv, req_words, C, (uint32_t*)reply, rep_words, (int64_t*)state, n_state, \
-                     delay_ticks, (unsigned long long*)stats, ob, dv)
+                     delay_ticks, (unsigned long long*)stats, ob, dv, lv)
   PT_FORMAT_SWITCH(nargs, mc, PT_DISPATCH)
 #undef PT_DISPATCH
   PT_HIP_CHECK(hipGetLastError());

@@ -50,14 +50,9 @@ void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uin
 void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t, uintptr_t);
 int64_t route_grid(int64_t, int64_t*);
-void launch_route(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t, uintptr_t,
-                  uint32_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
-                  int, const std::vector<uintptr_t>&, uint32_t, uintptr_t);
 void set_route_tuning(int, int);
 int64_t route_fused_grid(int64_t, int64_t*);
 void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uint32_t, uintptr_t, uintptr_t);
-void launch_dispatch(uintptr_t, int, int64_t, int, bool, uintptr_t, uintptr_t, uint32_t, uint64_t, uintptr_t, int64_t,
-                     const std::vector<uintptr_t>&, uint64_t, const std::vector<uintptr_t>&, int, uintptr_t);
 void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 int64_t wire_req_words(int64_t, int, bool);
 int64_t wire_rep_words(int64_t);
@@ -157,7 +152,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
         py::arg("dir"), py::arg("n_dir"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
         py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"), py::arg("lb"), py::arg("stats"),
-        py::arg("rank_self"), py::arg("direct"), py::arg("affine_w"), py::arg("stream"));
+        py::arg("rank_self"), py::arg("direct"), py::arg("affine_w"), py::arg("stream"), py::arg("zero_copy") = false);
   m.def("route_fused_grid", [](int64_t M) {
     int64_t P;
     const int64_t G = route_fused_grid(M, &P);
@@ -179,7 +174,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
         py::arg("reply"), py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),
         py::arg("expected_per_rank"), py::arg("outbox"), py::arg("outbox_cap"), py::arg("direct"), py::arg("self"),
-        py::arg("stream"));
+        py::arg("stream"), py::arg("local") = std::vector<uintptr_t>{});
   m.def("complete", &launch_complete, py::arg("rep"), py::arg("C"), py::arg("perm"), py::arg("M"),
         py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"), py::arg("stream"));
   m.def("records_to_soa", &launch_records_to_soa, py::arg("rec"), py::arg("M"), py::arg("actor"), py::arg("method"),

@@ -103,3 +103,40 @@ def test_gpu_engine_rccl_world1_matches_python():
     r = subprocess.run([sys.executable, "-c", _DIST_SCRIPT], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert '"identical": true, "engine_used": true, "python_used": true' in r.stdout, r.stdout + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunks,mixed", [(1, False), (2, True), (4, False)])
+def test_gpu_engine_zero_copy_identity(chunks, mixed):
+    """World 1, every actor known: the own slot is an identity slot and the
+    engine serves it from the caller's columns (no scatter writes, dispatch reads
+    in place).  Outputs and actor state equal the copying Python pipeline's."""
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    n, M = 5000, 300_007
+    gen = torch.Generator().manual_seed(40 + chunks)
+    actors = torch.randint(0, n, (M,), generator=gen).to(torch.int32)
+    if mixed:
+        method = torch.tensor([METHOD_ECHO, METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD])[torch.randint(0, 3, (M,), generator=gen)]
+    else:
+        method = torch.full((M,), METHOD_CALC_MULTIPLY)
+    a0 = torch.randint(-10**6, 10**6, (M,), generator=gen)
+    a0 = torch.where(method == METHOD_COUNTER_ADD, torch.ones_like(a0), a0)
+    a1 = torch.randint(-10**6, 10**6, (M,), generator=gen)
+    req = B.MsgBatch(actors.cuda(), a0.cuda(), a1.cuda(), None,
+                     method.to(torch.int16).cuda() if mixed else METHOD_CALC_MULTIPLY)
+    outs = {}
+    for engine in (True, False):
+        g = _table(n, True)
+        state = torch.zeros(n, dtype=torch.int64, device="cuda")
+        ex = ActorExchange(g, M, chunks=chunks, state=state)
+        ex.use_engine = engine
+        val, st = ex.send(req)
+        torch.cuda.synchronize()
+        outs[engine] = (val.cpu(), st.cpu(), state.cpu())
+    det = method != METHOD_COUNTER_ADD
+    assert torch.equal(outs[True][1], outs[False][1])
+    assert torch.equal(outs[True][0][det], outs[False][0][det])
+    assert int(outs[True][0][~det].sum()) == int(outs[False][0][~det].sum())
+    assert torch.equal(outs[True][2], outs[False][2])
+    assert bool((outs[True][1] == 0).all())
