@@ -236,11 +236,18 @@ PYBIND11_MODULE(_hip, m) {
   m.def("memcpy_h2d_async", &memcpy_h2d_async);
   m.def("stream_sync", &stream_sync, py::call_guard<py::gil_scoped_release>());
 
+  py::class_<FakeComm, std::shared_ptr<FakeComm>>(m, "FakeComm",
+                                                  "in-process R-rank all-to-all for multi-rank engine tests "
+                                                  "(one host thread + stream per rank on one GPU)")
+      .def(py::init<int>(), py::arg("R"))
+      .def_property_readonly("size", &FakeComm::size);
+
   py::class_<EpochEngine>(m, "EpochEngine",
                           "chunk-pipelined Send (route -> ncclAllToAll -> dispatch -> ncclAllToAll -> complete) "
                           "enqueued from one host call; comm = raw ncclComm_t or 0 for no collectives")
-      .def(py::init<int, uintptr_t, int, int, int64_t, int64_t, int>(), py::arg("device"), py::arg("comm"),
-           py::arg("R"), py::arg("rank"), py::arg("C"), py::arg("max_chunk"), py::arg("chunks"))
+      .def(py::init<int, uintptr_t, int, int, int64_t, int64_t, int, std::shared_ptr<FakeComm>>(), py::arg("device"),
+           py::arg("comm"), py::arg("R"), py::arg("rank"), py::arg("C"), py::arg("max_chunk"), py::arg("chunks"),
+           py::arg("fake") = nullptr)
       .def(
           "set_bufs",
           [](EpochEngine& e, int i, uintptr_t send, uintptr_t recv, uintptr_t reply, uintptr_t back, uintptr_t perm,
@@ -264,7 +271,8 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"),
           py::arg("affine_w"), py::arg("nargs"), py::arg("mc"), py::arg("out_val"), py::arg("out_st"),
           py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"), py::arg("outbox_cap"),
-          py::arg("direct"), py::arg("checksum"), py::arg("stream"), py::arg("packed") = false)
+          py::arg("direct"), py::arg("checksum"), py::arg("stream"), py::arg("packed") = false,
+          py::call_guard<py::gil_scoped_release>())
       .def("last_wire",
            [](const EpochEngine& e) {
              const auto& w = e.last_wire();

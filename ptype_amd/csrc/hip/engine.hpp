@@ -17,7 +17,10 @@
 #include <dlfcn.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <deque>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -93,6 +96,87 @@ using engine_detail::kNcclInt8;
 using engine_detail::kNcclMax;
 using engine_detail::kNcclUint64;
 
+// In-process stand-in for an R-rank communicator (tests only): R engines of one
+// process, each driven by its own host thread and stream on the same GPU, run
+// the exact multi-rank pipeline -- slot geometry, per-peer offsets, direct
+// completion of the own slot, reply routing -- with the all-to-all done as
+// R x R device copies ordered by events.  What RCCL adds on a real node (the
+// xGMI transport) is the only part it does not exercise.
+class FakeComm {
+ public:
+  explicit FakeComm(int R) : R_(R), slots_(R) {
+    if (R < 1 || R > 64) throw std::invalid_argument("FakeComm: 1 <= R <= 64");
+    for (auto& sl : slots_) {
+      PT_HIP_CHECK(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
+      PT_HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    }
+  }
+  ~FakeComm() {
+    for (auto& sl : slots_) {
+      hipEventDestroy(sl.ready);
+      hipEventDestroy(sl.done);
+    }
+  }
+  int size() const { return R_; }
+
+  // recv_r[q] = send_q[r], `bytes` per peer region
+  void alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) {
+    slots_[r].src = src;
+    slots_[r].dst = dst;
+    PT_HIP_CHECK(hipEventRecord(slots_[r].ready, s));
+    barrier();
+    for (int q = 0; q < R_; ++q) {
+      PT_HIP_CHECK(hipStreamWaitEvent(s, slots_[q].ready, 0));
+      PT_HIP_CHECK(hipMemcpyAsync((char*)dst + (size_t)q * bytes, (const char*)slots_[q].src + (size_t)r * bytes, bytes,
+                                  hipMemcpyDeviceToDevice, s));
+    }
+    PT_HIP_CHECK(hipEventRecord(slots_[r].done, s));
+    barrier();
+    for (int q = 0; q < R_; ++q) PT_HIP_CHECK(hipStreamWaitEvent(s, slots_[q].done, 0));  // senders' buffers read
+    barrier();
+  }
+
+  // element-wise max of n u64 on every rank (host-synchronous, like the engine's use)
+  void allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) {
+    slots_[r].host.assign(n, 0);
+    PT_HIP_CHECK(hipMemcpyAsync(slots_[r].host.data(), dev, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    PT_HIP_CHECK(hipStreamSynchronize(s));
+    barrier();
+    std::vector<uint64_t> m(n, 0);
+    for (int q = 0; q < R_; ++q)
+      for (int k = 0; k < n; ++k) m[k] = std::max(m[k], slots_[q].host[k]);
+    barrier();
+    PT_HIP_CHECK(hipMemcpyAsync(dev, m.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    PT_HIP_CHECK(hipStreamSynchronize(s));
+  }
+
+ private:
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu_);
+    const uint64_t gen = gen_;
+    if (++arrived_ == R_) {
+      arrived_ = 0;
+      ++gen_;
+      cv_.notify_all();
+      return;
+    }
+    if (!cv_.wait_for(lk, std::chrono::seconds(60), [&] { return gen_ != gen; }))
+      throw std::runtime_error("FakeComm: a rank did not reach the collective within 60 s");
+  }
+  struct Slot {
+    const void* src = nullptr;
+    void* dst = nullptr;
+    hipEvent_t ready{}, done{};
+    std::vector<uint64_t> host;
+  };
+  int R_;
+  std::vector<Slot> slots_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int arrived_ = 0;
+  uint64_t gen_ = 0;
+};
+
 struct EngineBufs {
   uintptr_t send, recv, reply, back, perm, src, route, hist, lb, ws;
 };
@@ -120,9 +204,13 @@ struct EngineSend {  // one Send: the batch, the registry, the outputs
 
 class EpochEngine {
  public:
-  EpochEngine(int device, uintptr_t comm, int R, int rank, int64_t C, int64_t max_chunk, int chunks)
-      : device_(device), comm_((void*)comm), R_(R), rank_(rank), C_(C), max_chunk_(max_chunk), chunks_(chunks) {
+  EpochEngine(int device, uintptr_t comm, int R, int rank, int64_t C, int64_t max_chunk, int chunks,
+              std::shared_ptr<FakeComm> fake = nullptr)
+      : device_(device), comm_((void*)comm), fake_(std::move(fake)), R_(R), rank_(rank), C_(C),
+        max_chunk_(max_chunk), chunks_(chunks) {
     if (R < 1 || chunks < 1 || max_chunk < 1) throw std::invalid_argument("EpochEngine: bad geometry");
+    if (fake_ && (comm_ || fake_->size() != R || rank < 0 || rank >= R))
+      throw std::invalid_argument("EpochEngine: fake communicator must match R and replace comm");
     if (comm_ && !rccl().alltoall) throw std::runtime_error("EpochEngine: ncclAllToAll not found in the process");
     PT_HIP_CHECK(hipSetDevice(device_));
     int lo = 0, hi = 0;
@@ -202,7 +290,7 @@ class EpochEngine {
     if (a.M > max_chunk_ * chunks_) throw std::invalid_argument("EpochEngine: batch exceeds max_batch");
     if (nbufs_ < 1) throw std::runtime_error("EpochEngine: buffers not set");
     const hipStream_t cs = as_stream(a.stream);
-    packed_ = a.packed && comm_ != nullptr;  // v3 only where bytes cross a collective
+    packed_ = a.packed && collectives();  // v3 only where bytes cross a collective
     if (packed_) agree_layout(a, cs);
     const int64_t wq = packed_ ? packed_req_words(C_, L_.S) : wire_req_words(C_, a.nargs, a.mc);
     const int64_t wr = packed_ ? packed_rep_words(C_, L_.vb) : wire_rep_words(C_);
@@ -222,7 +310,7 @@ class EpochEngine {
         pending.pop_front();
       }
       route(a, i, bi, cs, local_only);
-      if (comm_) {
+      if (collectives()) {
         join(comm_stream_, ev_route_[bi], cs);
         a2a(bufs_[bi].send, bufs_[bi].recv, wq);
         record(ev_req_[bi], comm_stream_);
@@ -244,7 +332,7 @@ class EpochEngine {
   // -> host.  The one host wait of a packed Send: every rank derives the same
   // layout from the same agreed vector, so slot geometry stays equal-split.
   void agree_layout(const EngineSend& a, hipStream_t cs) {
-    if (!rccl().allreduce) throw std::runtime_error("EpochEngine: ncclAllReduce not found in the process");
+    if (!fake_ && !rccl().allreduce) throw std::runtime_error("EpochEngine: ncclAllReduce not found in the process");
     const uint64_t t0 = now();
     {
       Timed t(prof_.kernels_ns);
@@ -254,6 +342,14 @@ class EpochEngine {
     // on the compute stream itself: the previous Send's collectives are complete
     // there already (its completions waited for them), and no cross-stream hop
     // sits on this, the one host wait of the Send
+    if (fake_) {
+      fake_->allreduce_max(rank_, meta_dev_, kMetaWords, cs);
+      PT_HIP_CHECK(hipMemcpy(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
+      L_ = packed_layout(meta_host_);
+      prof_.meta_ns += now() - t0;
+      return;
+    }
     const int rc = rccl().allreduce(meta_dev_, meta_dev_, kMetaWords, kNcclUint64, kNcclMax, comm_, cs);
     if (rc != 0)
       throw std::runtime_error(std::string("ncclAllReduce failed: ") +
@@ -300,7 +396,7 @@ class EpochEngine {
   // collectives, direct completion, no inverse index -- the identity slot is then
   // served from the caller's columns (decided on the device by the scan's flag).
   bool zero_copy(const EngineSend& a, bool local_only, bool write_perm) const {
-    return zero_copy_ && local_only && !comm_ && a.direct && !write_perm;
+    return zero_copy_ && local_only && !collectives() && a.direct && !write_perm;
   }
   std::vector<uintptr_t> local_view(const EngineSend& a, int i, int bi) const {
     const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
@@ -311,7 +407,7 @@ class EpochEngine {
   void serve(const EngineSend& a, int i, hipStream_t cs, int64_t wr) {
     const int bi = i % nbufs_;
     const EngineBufs& b = bufs_[bi];
-    if (comm_) wait(cs, ev_req_[bi]);
+    if (collectives()) wait(cs, ev_req_[bi]);
     const int64_t m = m_of(a, i);
     {
       Timed t(prof_.kernels_ns);
@@ -320,13 +416,13 @@ class EpochEngine {
                                std::max<int64_t>(1, m / R_), a.outbox, a.outbox_cap, direct_view(a, i, bi), rank_,
                                (uintptr_t)cs);
       else
-        launch_dispatch(comm_ ? b.recv : b.send, R_, C_, a.nargs, a.mc, b.reply, a.state, a.n_state, a.delay_ticks,
+        launch_dispatch(collectives() ? b.recv : b.send, R_, C_, a.nargs, a.mc, b.reply, a.state, a.n_state, a.delay_ticks,
                         b.ws, std::max<int64_t>(1, m / R_), a.outbox, a.outbox_cap, direct_view(a, i, bi), rank_,
                         (uintptr_t)cs,
                         zero_copy(a, R_ == 1, !(a.direct && R_ == 1 && !a.checksum)) ? local_view(a, i, bi)
                                                                                   : std::vector<uintptr_t>{});
     }
-    if (comm_) {
+    if (collectives()) {
       join(comm_stream_, ev_disp_[bi], cs);
       a2a(b.reply, b.back, wr);
       record(ev_rep_[bi], comm_stream_);
@@ -335,7 +431,7 @@ class EpochEngine {
 
   void finish(const EngineSend& a, int i, hipStream_t cs, bool local_only) {
     const int bi = i % nbufs_;
-    if (comm_) wait(cs, ev_rep_[bi]);
+    if (collectives()) wait(cs, ev_rep_[bi]);
     if (a.direct && local_only && !a.checksum) return;  // every reply was written by the own-slot dispatch
     Timed t(prof_.kernels_ns);
     const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M), m = m_of(a, i);
@@ -344,7 +440,7 @@ class EpochEngine {
       launch_complete_packed(b.back, C_, L_.vb, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4), a.checksum,
                              a.direct, (uintptr_t)cs);
     else
-      launch_complete(comm_ ? b.back : b.reply, C_, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4),
+      launch_complete(collectives() ? b.back : b.reply, C_, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4),
                       a.checksum, a.direct, (uintptr_t)cs);
   }
 
@@ -363,6 +459,10 @@ class EpochEngine {
 
   void a2a(uintptr_t src, uintptr_t dst, int64_t words_per_peer) {
     Timed t(prof_.a2a_ns);
+    if (fake_) {
+      fake_->alltoall(rank_, (const void*)src, (void*)dst, (size_t)words_per_peer * 4, comm_stream_);
+      return;
+    }
     const int rc = rccl().alltoall((const void*)src, (void*)dst, (size_t)words_per_peer * 4, kNcclInt8, comm_,
                                    comm_stream_);
     if (rc != 0)
@@ -371,7 +471,10 @@ class EpochEngine {
   }
 
   int device_;
+  bool collectives() const { return comm_ != nullptr || fake_ != nullptr; }
+
   void* comm_;
+  std::shared_ptr<FakeComm> fake_;
   int R_, rank_;
   int64_t C_, max_chunk_;
   int chunks_;

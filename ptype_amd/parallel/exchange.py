@@ -94,23 +94,29 @@ class ActorExchange:
 
     def __init__(self, table: RegistryTable, max_batch: int, chunks: int = 1, group=None, state=None,
                  delay_us: int = 0, slack: float = 0.01, fmt: B.WireFormat | None = None,
-                 packed: bool | None = None):
+                 packed: bool | None = None, fake=None):
         self.table = table
         self.device = table.device
         self.group = group
-        if dist.is_available() and dist.is_initialized():
+        # ``fake = (_hip.FakeComm(R), rank)``: one of R in-process ranks on one GPU
+        # (tests drive each from its own thread and stream; geometry must match)
+        self.fake = fake
+        if fake is not None:
+            self.rank, self.world = int(fake[1]), int(fake[0].size)
+        elif dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank(group)
             self.world = dist.get_world_size(group)
         else:
             self.rank, self.world = 0, 1
         # run the RCCL all-to-alls even on a single rank (validates the collective
         # path on a 1-GPU box; a 1-rank all-to-all is a device-local copy)
-        self.force_collectives = bool(dist.is_available() and dist.is_initialized() and self.world == 1)
+        self.force_collectives = bool(fake is None and dist.is_available() and dist.is_initialized()
+                                      and self.world == 1)
         self.chunks = max(1, int(chunks))
         self.max_chunk = int(math.ceil(max_batch / self.chunks))
         # every rank must use the same slot geometry (equal-split all-to-all):
         # agree on the largest chunk and the chunk count once, collectively
-        if self.world > 1:
+        if self.world > 1 and fake is None:
             t = torch.tensor([self.max_chunk, self.chunks], dtype=torch.int64, device=self.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             self.max_chunk, self.chunks = int(t[0]), int(t[1])
@@ -158,8 +164,13 @@ class ActorExchange:
     def _get_engine(self):
         if self._engine is None:
             h = B.hip()
-            eng = h.EpochEngine(self.device.index if self.device.index is not None else torch.cuda.current_device(),
-                                self._comm_ptr(), self.world, self.rank, self.C, self.max_chunk, self.chunks)
+            dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            if self.fake is not None:
+                eng = h.EpochEngine(dev, 0, self.world, self.rank, self.C, self.max_chunk, self.chunks,
+                                    fake=self.fake[0])
+            else:
+                eng = h.EpochEngine(dev, self._comm_ptr(), self.world, self.rank, self.C, self.max_chunk,
+                                    self.chunks)
             for i, b in enumerate(self.bufs):
                 eng.set_bufs(i, b.send.data_ptr(), b.recv.data_ptr(), b.reply.data_ptr(), b.back.data_ptr(),
                              b.perm.data_ptr(), b.src.data_ptr(), b.rws.route.data_ptr(), b.rws.hist.data_ptr(),
