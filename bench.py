@@ -163,31 +163,48 @@ def main():
     if args.steps:
         verify("timed")
 
-    # p50 RTT of a synchronous Call to a GPU actor (persistent dispatcher)
-    p50 = None
+    # p50 RTT of a synchronous Call to a GPU actor (persistent dispatcher, no kernel
+    # launch per call): from this process to its own GPU, and -- with more than one
+    # rank -- from this process to the actors of the NEXT rank's GPU, through that
+    # process's shared-memory rings (the reference's Client.Call to another node,
+    # cluster/rpc.go:59-67; here a node is a GPU of the same host)
+    p50 = p50_remote = None
     if use_gpu and args.rtt_calls > 0:
         from ptype_amd.ops import hip
 
-        srv = hip().DeviceServer(local, 4096, state.data_ptr(), state.numel(), 0, 200.0, 60.0)
-        try:
+        tag = os.environ.get("MASTER_PORT", "0")
+        shm = f"/ptype-bench-{tag}-{rank}" if dist_on else ""
+        srv = hip().DeviceServer(local, 4096, state.data_ptr(), state.numel(), 0, 200.0, 60.0, shm)
+
+        def timed_calls(call):
             lat = []
             for i in range(args.rtt_calls + 100):
                 a = i % state.numel()
                 t = time.perf_counter()
-                v, s_, _ = srv.call(METHOD_CALC_MULTIPLY, a, i, 3)
+                v, s_ = call(METHOD_CALC_MULTIPLY, a, i, 3)[:2]
                 dt = time.perf_counter() - t
                 if v != 3 * i or s_ != STATUS_OK:
                     raise SystemExit(f"RTT call returned {v}, status {s_}")
                 if i >= 100:
                     lat.append(dt)
             lat.sort()
-            p50 = lat[len(lat) // 2] * 1e6
+            return lat[len(lat) // 2] * 1e6
+
+        try:
+            p50 = timed_calls(srv.call)
+            if dist_on:
+                from ptype_amd import _core
+
+                barrier()  # every rank's dispatcher segment exists
+                peer = _core.ShmClient(f"/ptype-bench-{tag}-{(rank + 1) % world}")
+                p50_remote = timed_calls(peer.call)
+                barrier()  # keep serving until every rank is done calling
         finally:
             srv.close()
         if dist_on:
-            t = torch.tensor([p50], dtype=torch.float64, device=device)
+            t = torch.tensor([p50, p50_remote], dtype=torch.float64, device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            p50 = float(t.item())
+            p50, p50_remote = (float(x) for x in t.tolist())
 
     total_msgs = M * world * args.steps
     value = total_msgs / elapsed if elapsed > 0 else 0.0
@@ -205,7 +222,12 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic",
-            "p50_rtt_us": p50,
+            # the cross-GPU call when there is another GPU, else the local one
+            "p50_rtt_us": p50_remote if world > 1 else p50,
+            "p50_rtt_local_us": p50,
+            "p50_rtt_remote_us": p50_remote,
+            "rtt_path": "host -> GPU actor via the persistent dispatcher's rings (remote: the next rank's "
+                        "process, shared-memory rings on its GPU)",
             "config": {
                 "model": "calculator actor (Calculator.Multiply)",
                 "global_batch": M * world,

@@ -663,6 +663,39 @@ PYBIND11_MODULE(_core, m) {
              return from_gob(o.reply);
            })
       .def("close", &RpcConn::close);
+  // A raw handle on another process's dispatcher segment (by name): device calls
+  // straight into the rings that process's GPU polls -- used to time remote calls
+  // between the GPUs of a node (bench.py) without a net/rpc server in the way.
+  struct ShmClient {
+    std::shared_ptr<ShmSegment> seg;
+    ShmView view;
+  };
+  py::class_<ShmClient, std::shared_ptr<ShmClient>>(m, "ShmClient")
+      .def(py::init([](const std::string& name) {
+             auto seg = ShmSegment::attach(name);
+             if (!seg) fail(Errc::kUnavailable, "no dispatcher segment " + name);
+             const ShmHeader* h = static_cast<const ShmHeader*>(seg->base());
+             if (seg->size() < sizeof(ShmHeader) || h->magic != kShmMagic || seg->size() < shm_bytes(h->ring))
+               fail(Errc::kUnavailable, "segment " + name + " is not a ptype dispatcher");
+             auto c = std::make_shared<ShmClient>();
+             c->view = shm_view(seg->base(), h->ring);
+             c->seg = std::move(seg);
+             return c;
+           }),
+           py::arg("name"))
+      .def(
+          "call",
+          [](ShmClient& c, int method, uint32_t actor, int64_t a0, int64_t a1, int64_t a2, double timeout) {
+            MsgRecord m{actor, (uint16_t)method, (uint16_t)kFlagValid, a0, a1, a2};
+            ReplyRecord r;
+            {
+              py::gil_scoped_release nogil;
+              r = shm_call(c.view, m, timeout);
+            }
+            return py::make_tuple(r.value, r.status);
+          },
+          py::arg("method"), py::arg("actor"), py::arg("a0") = 0, py::arg("a1") = 0, py::arg("a2") = 0,
+          py::arg("timeout") = 10.0);
   m.def(
       "dial_http",
       [](const std::string& host, int port, double timeout, bool allow_local) {

@@ -503,13 +503,11 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
   PT_HIP_CHECK(hipGetLastError());
 }
 
-// Passes 1 + 2 of the 3-pass route (shared by wire formats v2 and v3): route
-// words + block histograms, then per-destination bases and slot headers in
-// regions of `req_words`.  Returns the block count G; *P_out = messages per block.
-int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir,
-                        uint32_t n_dir, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t route,
-                        uintptr_t hist, uintptr_t stats, int rank_self, uint32_t affine_w, uintptr_t stream,
-                        int64_t* P_out) {
+// Pass 1 of the 3-pass route (shared by wire formats v2 and v3): route words +
+// block histograms.  Independent of the wire layout, so the v3 engine runs it
+// while the host waits for the layout agreement.  Returns G; *P_out = P.
+int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
+                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out) {
   int64_t P;
   const int64_t G = route_grid(M, &P);
   *P_out = P;
@@ -533,9 +531,24 @@ int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_
   } else {
     PT_HIP_CHECK(hipMemsetAsync((void*)hist, 0, sizeof(uint32_t) * (R + 1) * G, s));
   }
-  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, s, (uint32_t*)hist, (int)G, R, C, (uint32_t*)sendbuf,
-                     req_words, (uint32_t)method_uniform, (unsigned long long*)stats, rank_self);
   PT_HIP_CHECK(hipGetLastError());
+  return G;
+}
+
+// Pass 2: per-destination bases and slot headers in regions of `req_words`.
+void route_scan(int64_t G, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t hist,
+                int method_uniform, uintptr_t stats, int rank_self, uintptr_t stream) {
+  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, as_stream(stream), (uint32_t*)hist, (int)G, R, C,
+                     (uint32_t*)sendbuf, req_words, (uint32_t)method_uniform, (unsigned long long*)stats, rank_self);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir,
+                        uint32_t n_dir, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t route,
+                        uintptr_t hist, uintptr_t stats, int rank_self, uint32_t affine_w, uintptr_t stream,
+                        int64_t* P_out) {
+  const int64_t G = route_prep(actor, M, table, cap, dir, n_dir, R, route, hist, affine_w, stream, P_out);
+  route_scan(G, R, C, req_words, sendbuf, hist, method_uniform, stats, rank_self, stream);
   return G;
 }
 

@@ -58,9 +58,6 @@ int64_t wire_req_words(int64_t, int, bool);
 int64_t wire_rep_words(int64_t);
 void launch_packed_meta(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uint32_t, uint32_t,
                         uintptr_t, uintptr_t);
-void launch_route_packed(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uintptr_t, uint64_t,
-                         uintptr_t, uint32_t, int, int64_t, const PackedLayout&, uintptr_t, uintptr_t, uintptr_t,
-                         uintptr_t, uintptr_t, int, const std::vector<uintptr_t>&, uint32_t, uintptr_t);
 void launch_dispatch_packed(uintptr_t, int, int64_t, const PackedLayout&, uintptr_t, uintptr_t, uint32_t, uint64_t,
                             uintptr_t, int64_t, const std::vector<uintptr_t>&, uint64_t, const std::vector<uintptr_t>&,
                             int, uintptr_t);

@@ -50,7 +50,9 @@ void launch_route_packed(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t 
                          int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
                          int R, int64_t C, const PackedLayout& L, uintptr_t sendbuf, uintptr_t perm, uintptr_t route,
                          uintptr_t hist, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
-                         uint32_t affine_w, uintptr_t stream);
+                         uint32_t affine_w, uintptr_t stream, bool prepped = false);
+int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
+                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out);
 void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout& L, uintptr_t reply, uintptr_t state,
                             uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
                             const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
@@ -342,11 +344,13 @@ class EpochEngine {
     // on the compute stream itself: the previous Send's collectives are complete
     // there already (its completions waited for them), and no cross-stream hop
     // sits on this, the one host wait of the Send
+    prepped_ = 0;
     if (fake_) {
       fake_->allreduce_max(rank_, meta_dev_, kMetaWords, cs);
       PT_HIP_CHECK(hipMemcpy(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
       for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
       L_ = packed_layout(meta_host_);
+      prep_ahead(a, cs);
       prof_.meta_ns += now() - t0;
       return;
     }
@@ -356,10 +360,28 @@ class EpochEngine {
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
     PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost, cs));
     PT_HIP_CHECK(hipEventRecord(ev_meta_out_, cs));
+    prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
     PT_HIP_CHECK(hipEventSynchronize(ev_meta_out_));
     for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
     L_ = packed_layout(meta_host_);
     prof_.meta_ns += now() - t0;
+  }
+
+  // Pass 1 of the route (route words + histograms; layout-independent) for the
+  // first two chunks, queued behind the agreement so the host's wake-up from the
+  // wait (~10-20 us) is hidden behind device work.  Two, not all: every prep run
+  // ahead delays the first all-to-all, which starts the comm-bound critical path.
+  void prep_ahead(const EngineSend& a, hipStream_t cs) {
+    if (nbufs_ < chunks_) return;
+    Timed t(prof_.kernels_ns);
+    const int n = std::min(chunks_, 2);
+    for (int i = 0; i < n; ++i) {
+      const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
+      int64_t P;
+      route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route, bufs_[i].hist,
+                 a.affine_w, (uintptr_t)cs, &P);
+    }
+    prepped_ = n;
   }
 
   int64_t m_of(const EngineSend& a, int i) const {
@@ -383,7 +405,7 @@ class EpochEngine {
       launch_route_packed(off(a.actor, lo, 4), off(a.a0, lo, 8), off(a.a1, lo, 8), off(a.a2, lo, 8),
                           off(a.method_col, lo, 2), a.method_uniform, m, a.table, a.cap, a.dir, a.n_dir, R_, C_, L_,
                           b.send, write_perm ? b.perm : 0, b.route, b.hist, b.ws, rank_, direct_view(a, i, bi),
-                          a.affine_w, (uintptr_t)cs);
+                          a.affine_w, (uintptr_t)cs, i < prepped_ && bi == i);
       return;
     }
     launch_route(off(a.actor, lo, 4), off(a.a0, lo, 8), off(a.a1, lo, 8), off(a.a2, lo, 8), off(a.method_col, lo, 2),
@@ -487,6 +509,7 @@ class EpochEngine {
   uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)
   uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
   bool packed_ = false;
+  int prepped_ = 0;  // chunks whose route pass 1 ran ahead of the agreement wait (this Send)
   bool zero_copy_ = getenv("PTYPE_ZERO_COPY") == nullptr || std::string(getenv("PTYPE_ZERO_COPY")) != "0";
   PackedLayout L_{};
   WireInfo wire_;

@@ -14,10 +14,11 @@
 
 namespace ptype {
 
-int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir,
-                        uint32_t n_dir, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t route,
-                        uintptr_t hist, uintptr_t stats, int rank_self, uint32_t affine_w, uintptr_t stream,
-                        int64_t* P_out);
+int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
+                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out);
+void route_scan(int64_t G, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t hist,
+                int method_uniform, uintptr_t stats, int rank_self, uintptr_t stream);
+int64_t route_grid(int64_t M, int64_t* P_out);
 
 constexpr int kStatTooWide = 4;  // workspace stat word: replies that did not fit vb (never, by construction)
 
@@ -319,7 +320,11 @@ void launch_packed_meta(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a
   hipStream_t s = as_stream(stream);
   PT_HIP_CHECK(hipMemsetAsync((void*)meta, 0, kMetaWords * sizeof(uint64_t), s));
   if (M > 0 && (!a0 || !actor)) throw std::invalid_argument("packed meta: actor and a0 columns required");
-  hipLaunchKernelGGL(packed_meta_kernel, dim3(grid_for(M, 256 * 8, 2048)), dim3(256), 0, s, (const uint32_t*)actor,
+  static const unsigned cap = [] {  // blocks (tuning knob, PTYPE_META_BLOCKS; see tools/meta_bench.py)
+    const char* e = getenv("PTYPE_META_BLOCKS");
+    return e ? (unsigned)atoi(e) : 1024u;  // measured best on MI355X (profiles/r1_meta_sweep.jsonl)
+  }();
+  hipLaunchKernelGGL(packed_meta_kernel, dim3(grid_for(M, 256 * 8, cap)), dim3(256), 0, s, (const uint32_t*)actor,
                      (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col,
                      (uint32_t)method_uniform, M, n_dir, affine_w, (unsigned long long*)meta);
   PT_HIP_CHECK(hipGetLastError());
@@ -341,15 +346,17 @@ void launch_route_packed(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t 
                          int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
                          int R, int64_t C, const PackedLayout& L, uintptr_t sendbuf, uintptr_t perm, uintptr_t route,
                          uintptr_t hist, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
-                         uint32_t affine_w, uintptr_t stream) {
+                         uint32_t affine_w, uintptr_t stream, bool prepped) {
   check_packed_layout(L, R, C);
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
   if (method_col && !L.w[0]) throw std::invalid_argument("route: method column needs a method field in the layout");
   const DirectView dv = direct_of(direct, rank_self);
   const int64_t req_words = packed_req_words(C, L.S);
   int64_t P;
-  const int64_t G = route_prep_scan(actor, method_uniform, M, table, cap, dir, n_dir, R, C, req_words, sendbuf, route,
-                                    hist, stats, rank_self, affine_w, stream, &P);
+  // `prepped`: pass 1 already ran on this stream (route_prep before the agreement wait)
+  const int64_t G = prepped ? route_grid(M, &P)
+                            : route_prep(actor, M, table, cap, dir, n_dir, R, route, hist, affine_w, stream, &P);
+  route_scan(G, R, C, req_words, sendbuf, hist, method_uniform, stats, rank_self, stream);
   if (M > 0) {
 #define PT_SCATTER_P(SV)                                                                                             \
   hipLaunchKernelGGL((route_scatter_packed_kernel<SV>), dim3((unsigned)G), dim3(kRouteThreads), 0, as_stream(stream), \
