@@ -10,11 +10,16 @@ links, the receiver runs the handler table over what it got (K3), a second
 all-to-all returns the replies (8-B value + 1-B status) into the exact slots the
 requests left from, and K8 scatters them back to message order.
 
-Wire volume is what bounds an epoch on xGMI, so records carry only the columns
-the batch has (``WireFormat``): a calculator call is 20 B, not a 32-B record.
-Every rank must send batches with the same columns in the same call (the
-all-to-all is equal-split over the format's slot size), or fix the format at
-construction with ``fmt=``.
+Wire volume is what bounds an epoch on xGMI.  On the native engine with
+collectives (N > 1), records use wire format v3 (``csrc/hip/packed.hpp``,
+``ops/packed.py``): the ranks agree per Send, with one 16-word all-reduce, on
+the bit widths of every column, and records are zigzag bit-packed at them.  A
+calculator call is 8 B plus a 4-B reply, where v2 takes 20 + 9 B.  Elsewhere
+(world 1, the Python/gloo pipeline, a captured graph), v2 records carry only the
+columns the batch has (``WireFormat``).  For v2, every rank must send batches
+with the same columns in the same call (the all-to-all is equal-split over the
+format's slot size), or fix the format at construction with ``fmt=``.  v3
+derives one layout from the agreed maxima, so ranks may differ in their columns.
 
 Fixed-capacity slots (``C + 1`` records per peer, slot 0 a header with the
 count) make both all-to-alls equal-split: no host round trip for sizes, so an
