@@ -387,13 +387,18 @@ void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M,
 
 // Route blocks: G = ceil(M / P); the scan kernel handles up to 1024 * 64 blocks.
 int64_t route_grid(int64_t M, int64_t* P_out) {
-  int64_t G = (M + 4095) / 4096;  // ~4K messages per block: 8 scatter tiles
-  if (G < 1) G = 1;
-  if (G > 4096) G = 4096;
-  int64_t P = (M + G - 1) / G;
-  P = ((P + 255) / 256) * 256;
-  if (P < 256) P = 256;
-  G = (M + P - 1) / P;
+  // ~2048 blocks whatever the batch size (8 per CU): a pipelined chunk of 2 Mi
+  // messages at P = 4096 was only 512 blocks, and the prep / scatter passes --
+  // barrier-separated tiles, latency-bound -- ran at a quarter of the machine.
+  // P is a whole number of scatter tiles (512 messages), at least one.
+  static const int64_t target = [] {
+    const char* e = getenv("PTYPE_ROUTE_BLOCKS");
+    return e ? (int64_t)atoll(e) : (int64_t)2048;
+  }();
+  int64_t P = (M + target - 1) / target;
+  P = ((P + kScatterTile - 1) / kScatterTile) * kScatterTile;
+  if (P < kScatterTile) P = kScatterTile;
+  int64_t G = (M + P - 1) / P;
   if (G < 1) G = 1;
   *P_out = P;
   return G;
