@@ -251,7 +251,7 @@ class EpochEngine {
   const WireInfo& last_wire() const { return wire_; }
 
   void set_bufs(int i, const EngineBufs& b) {
-    if (i < 0 || i >= kMaxBufs) throw std::invalid_argument("EpochEngine: at most 4 buffer sets");
+    if (i < 0 || i >= kMaxBufs) throw std::invalid_argument("EpochEngine: at most 8 buffer sets");
     bufs_[i] = b;
     nbufs_ = std::max(nbufs_, i + 1);
   }
@@ -500,7 +500,7 @@ class EpochEngine {
   int R_, rank_;
   int64_t C_, max_chunk_;
   int chunks_;
-  static constexpr int kMaxBufs = 4;  // chunks in flight without waiting for buffer reuse
+  static constexpr int kMaxBufs = 8;  // chunks in flight without waiting for buffer reuse
   EngineBufs bufs_[kMaxBufs]{};
   int nbufs_ = 0;
   hipStream_t comm_stream_ = nullptr;

@@ -130,7 +130,7 @@ class ActorExchange:
         self.delay_us = delay_us
         self.fmt = fmt  # None: derived per send() from the batch's columns
         self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device, self.force_collectives,
-                                fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 4))]
+                                fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 8))]
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
         self.outbox = None  # DeviceOutbox that dispatched handlers send into (set by pump)
         # direct completion of self-directed messages (no reply staging, no
