@@ -211,7 +211,6 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
   const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
   if (dv.src)  // the scan flagged a gap-free single slot: positions are message indices
     dv.identity = ((sendbuf[(int64_t)dv.self * req_words + 3] >> 16) & kFlagIdentity) != 0;
-  if (dv.identity && dv.zero_copy) return;  // block-uniform: the dispatch reads the batch in place
   __syncthreads();
   auto route_at = [route](int64_t i) { return route[i]; };
   for (int64_t tile = lo; tile < hi; tile += kScatterTile)
@@ -261,36 +260,12 @@ __device__ __forceinline__ unsigned long long dispatch_range(const uint32_t* __r
   return failed;
 }
 
-// Zero-copy local delivery (LocalView): the identity slot's records are the
-// caller's columns; slot position s is message s.
-template <int NARGS, bool MC, int FIXED>
-__device__ __forceinline__ unsigned long long dispatch_local_range(LocalView lv, int64_t count, uint32_t hdr_method,
-                                                                   int64_t* __restrict__ state, uint32_t n_state,
-                                                                   uint64_t delay_ticks, OutboxView ob,
-                                                                   DirectView dv) {
-  unsigned long long failed = 0;
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < count; s += (int64_t)gridDim.x * blockDim.x) {
-    MsgRecord m;
-    m.actor = __builtin_nontemporal_load(lv.route + s) >> 8;
-    m.method = (uint16_t)(FIXED ? FIXED : (MC && lv.mcol ? (uint32_t)lv.mcol[s] : hdr_method));
-    m.flags = kFlagValid | kFlagRouted;
-    m.a0 = __builtin_nontemporal_load(lv.a0 + s);
-    m.a1 = NARGS > 1 && lv.a1 ? __builtin_nontemporal_load(lv.a1 + s) : 0;
-    m.a2 = NARGS > 2 && lv.a2 ? __builtin_nontemporal_load(lv.a2 + s) : 0;
-    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
-    failed += rr.status != kStatusOk;
-    __builtin_nontemporal_store(rr.value, dv.out_val + s);
-    __builtin_nontemporal_store((int32_t)rr.status, dv.out_st + s);
-  }
-  return failed;
-}
-
 template <int NARGS, bool MC>
 __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restrict__ recv, int64_t req_words,
                                                        int64_t C, uint32_t* __restrict__ reply, int64_t rep_words,
                                                        int64_t* __restrict__ state, uint32_t n_state,
                                                        uint64_t delay_ticks, unsigned long long* __restrict__ stats,
-                                                       OutboxView ob, DirectView dv, LocalView lv) {
+                                                       OutboxView ob, DirectView dv) {
   const int d = blockIdx.y;
   const bool direct = dv.src != nullptr && d == dv.self;
   const uint32_t* rq = recv + (int64_t)d * req_words;
@@ -306,12 +281,7 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
   const uint32_t hm = h.w & 0xffffu;
   const bool ident = direct && ((h.w >> 16) & kFlagIdentity);
   unsigned long long failed;
-  if (ident && lv.route) {  // zero-copy: the scatter left the slot empty
-    failed = (!MC && hm == kCalculatorMultiply)
-                 ? dispatch_local_range<NARGS, MC, kCalculatorMultiply>(lv, count, hm, state, n_state, delay_ticks,
-                                                                         obp, dv)
-                 : dispatch_local_range<NARGS, MC, 0>(lv, count, hm, state, n_state, delay_ticks, obp, dv);
-  } else if constexpr (!MC) {
+  if constexpr (!MC) {
     switch (hm) {  // uniform per slot: one specialised loop per hot method
       case kCalculatorMultiply:
         failed = dispatch_range<NARGS, MC, kCalculatorMultiply>(rq, count, hm, vals, sts, state, n_state,
@@ -331,6 +301,85 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
   }
   for (int off = 32; off > 0; off >>= 1) failed += __shfl_xor(failed, off);
   if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);
+}
+
+// World 1, no collectives: the local Send.  With one destination there is
+// nothing to bucket, so resolution and dispatch fuse into one streaming pass:
+// each message is resolved against the registry mirror (affine directory /
+// route directory / hash probe, exactly as route_prep), handed to its
+// mailbox's handler, and its reply written into the caller's outputs.  No
+// epoch slot, no histogram, no scan: 20 B in and 12 B out per calculator call.
+// MODE as route_prep; FIXED != 0: uniform method known at launch (the handler
+// switch constant-folds).
+template <int MODE, int FIXED>
+__global__ __launch_bounds__(256) void local_send_kernel(
+    const uint32_t* __restrict__ actor, const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
+    const int64_t* __restrict__ a2, const uint16_t* __restrict__ mcol, uint32_t method_uniform, int64_t M,
+    const TableEntry* __restrict__ table, uint64_t mask, const uint32_t* __restrict__ dir, uint32_t n_dir,
+    uint32_t aw, int aw_shift, int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
+    int64_t* __restrict__ out_val, int32_t* __restrict__ out_st, unsigned long long* __restrict__ stats,
+    unsigned long long* __restrict__ checksum) {
+  unsigned long long nomatch = 0, failed = 0, sum = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t a = __builtin_nontemporal_load(actor + i);
+    int r;
+    uint32_t mb;
+    if constexpr (MODE == 2) {
+      if (a < n_dir) {
+        r = aw_shift >= 0 ? (int)(a & (aw - 1)) : (int)(a % aw);
+        mb = aw_shift >= 0 ? a >> aw_shift : a / aw;
+      } else {
+        lookup_entry(table, mask, actor_key(a), r, mb);
+      }
+    } else if constexpr (MODE == 1) {
+      const uint32_t w = a < n_dir ? dir[a] : kDirFallback;
+      if (w == kDirFallback) {
+        lookup_entry(table, mask, actor_key(a), r, mb);
+      } else {
+        r = w == kDirMissing ? -1 : (int)(w & 0xff);
+        mb = w >> 8;
+      }
+    } else {
+      lookup_entry(table, mask, actor_key(a), r, mb);
+    }
+    ReplyRecord rr;
+    if (r == 0 && mb < kMaxMbox) {
+      MsgRecord m;
+      m.actor = mb;
+      m.method = (uint16_t)(FIXED ? FIXED : (mcol ? (uint32_t)mcol[i] : method_uniform));
+      m.flags = kFlagValid | kFlagRouted;
+      m.a0 = __builtin_nontemporal_load(a0 + i);
+      m.a1 = a1 ? __builtin_nontemporal_load(a1 + i) : 0;
+      m.a2 = a2 ? __builtin_nontemporal_load(a2 + i) : 0;
+      rr = run_handler(m, state, n_state, delay_ticks, ob);
+      failed += rr.status != kStatusOk;
+    } else {
+      rr.value = 0;
+      rr.status = kStatusNoActor;
+      ++nomatch;
+    }
+    __builtin_nontemporal_store(rr.value, out_val + i);
+    __builtin_nontemporal_store((int32_t)rr.status, out_st + i);
+    sum += (unsigned long long)rr.value;
+  }
+  // counters as the slot path keeps them (ws stats: 0 no-actor, 2 handler-failed),
+  // one atomic per block and only when non-zero
+  __shared__ unsigned long long part[3][256 / kWave];
+  for (int off = 32; off > 0; off >>= 1) {
+    nomatch += __shfl_xor(nomatch, off);
+    failed += __shfl_xor(failed, off);
+    sum += __shfl_xor(sum, off);
+  }
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == 0) part[0][w] = nomatch, part[1][w] = failed, part[2][w] = sum;
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned long long v = 0;
+    for (int k = 0; k < 256 / kWave; ++k) v += part[threadIdx.x][k];
+    if (threadIdx.x == 0 && v) atomicAdd(&stats[0], v);
+    if (threadIdx.x == 1 && v) atomicAdd(&stats[2], v);
+    if (threadIdx.x == 2 && checksum) atomicAdd(checksum, v);
+  }
 }
 
 // K8: replies back to message order (SoA outputs).
@@ -478,16 +527,13 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
                   int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                   int64_t C, int nargs, bool mc, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist,
                   uintptr_t lb, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
-                  uint32_t affine_w, uintptr_t stream, bool zero_copy) {
-  DirectView dv = make_direct(direct, rank_self);
-  if (zero_copy && (R != 1 || !dv.src || perm))
-    throw std::invalid_argument("route: zero-copy local delivery needs R == 1, direct completion and no perm");
-  dv.zero_copy = zero_copy;
+                  uint32_t affine_w, uintptr_t stream) {
+  const DirectView dv = make_direct(direct, rank_self);
   check_format(nargs, C, R);
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
   if (method_col && !mc) throw std::invalid_argument("route: method column needs a method-column wire format");
   const int64_t req_words = wire_req_words(C, nargs, mc);
-  if (g_route_mode == 1 && lb && !zero_copy) {
+  if (g_route_mode == 1 && lb) {
     launch_route_fused(actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, R, C, nargs, mc,
                        req_words, sendbuf, perm, lb, stats, rank_self, dv, stream);
     return;
@@ -560,18 +606,8 @@ int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_
 void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintptr_t reply, uintptr_t state,
                      uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
                      const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, const std::vector<uintptr_t>& direct,
-                     int self, uintptr_t stream, const std::vector<uintptr_t>& local) {
+                     int self, uintptr_t stream) {
   const DirectView dv = make_direct(direct, self);
-  LocalView lv;
-  if (!local.empty()) {
-    if (local.size() != 5) throw std::invalid_argument("local: [route, a0, a1, a2, method_col]");
-    if (!dv.src || R != 1) throw std::invalid_argument("local: zero-copy delivery needs direct completion at R == 1");
-    lv.route = (const uint32_t*)local[0];
-    lv.a0 = (const int64_t*)local[1];
-    lv.a1 = (const int64_t*)local[2];
-    lv.a2 = (const int64_t*)local[3];
-    lv.mcol = (const uint16_t*)local[4];
-  }
   OutboxView ob;
   if (outbox_cap) {
     if (outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
@@ -590,7 +626,7 @@ void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintp
 #define PT_DISPATCH(NA, MCV)                                                                                    \
   hipLaunchKernelGGL((dispatch_kernel<NA, MCV>), dim3(gx, R), dim3(256), 0, as_stream(stream),                  \
                      (const uint32_t*)recv, req_words, C, (uint32_t*)reply, rep_words, (int64_t*)state, n_state, \
-                     delay_ticks, (unsigned long long*)stats, ob, dv, lv)
+                     delay_ticks, (unsigned long long*)stats, ob, dv)
   PT_FORMAT_SWITCH(nargs, mc, PT_DISPATCH)
 #undef PT_DISPATCH
   PT_HIP_CHECK(hipGetLastError());
@@ -603,6 +639,46 @@ void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintpt
   hipLaunchKernelGGL(complete_kernel, dim3(grid_cap(M, 256, checksum ? 1024 : 8192)), dim3(256), 0,
                      as_stream(stream), (const uint32_t*)rep, wire_rep_words(C), (uint32_t)C, (const int32_t*)perm, M,
                      (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum, direct);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                       int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
+                       uint32_t affine_w, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
+                       const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, uintptr_t out_val, uintptr_t out_st,
+                       uintptr_t stats, uintptr_t checksum, uintptr_t stream) {
+  if (M <= 0) return;
+  if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
+  if (!actor || !a0 || !out_val || !out_st || !stats) throw std::invalid_argument("local send: missing column");
+  OutboxView ob;
+  if (outbox_cap) {
+    if (outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
+    ob.actor = (uint32_t*)outbox[0];
+    ob.a0 = (int64_t*)outbox[1];
+    ob.a1 = (int64_t*)outbox[2];
+    ob.a2 = (int64_t*)outbox[3];
+    ob.method = (uint16_t*)outbox[4];
+    ob.count = (unsigned long long*)outbox[5];
+    ob.cap = outbox_cap;
+  }
+  const int aw_shift = (affine_w && (affine_w & (affine_w - 1)) == 0) ? __builtin_ctz(affine_w) : -1;
+  const int mode = (affine_w && n_dir) ? 2 : (dir && n_dir) ? 1 : 0;
+  const bool fixed = !method_col && method_uniform == kCalculatorMultiply;
+  const dim3 g(grid_cap(M, 256 * 4, 8192));
+#define PT_LOCAL(MO, FX)                                                                                              \
+  hipLaunchKernelGGL((local_send_kernel<MO, FX>), g, dim3(256), 0, as_stream(stream), (const uint32_t*)actor,        \
+                     (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col,       \
+                     (uint32_t)method_uniform, M, (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir,     \
+                     affine_w, aw_shift, (int64_t*)state, n_state, delay_ticks, ob, (int64_t*)out_val,              \
+                     (int32_t*)out_st, (unsigned long long*)stats, (unsigned long long*)checksum)
+  if (mode == 2) {
+    if (fixed) PT_LOCAL(2, kCalculatorMultiply); else PT_LOCAL(2, 0);
+  } else if (mode == 1) {
+    if (fixed) PT_LOCAL(1, kCalculatorMultiply); else PT_LOCAL(1, 0);
+  } else {
+    if (fixed) PT_LOCAL(0, kCalculatorMultiply); else PT_LOCAL(0, 0);
+  }
+#undef PT_LOCAL
   PT_HIP_CHECK(hipGetLastError());
 }
 

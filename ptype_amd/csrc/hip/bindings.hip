@@ -149,7 +149,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
         py::arg("dir"), py::arg("n_dir"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
         py::arg("sendbuf"), py::arg("perm"), py::arg("route"), py::arg("hist"), py::arg("lb"), py::arg("stats"),
-        py::arg("rank_self"), py::arg("direct"), py::arg("affine_w"), py::arg("stream"), py::arg("zero_copy") = false);
+        py::arg("rank_self"), py::arg("direct"), py::arg("affine_w"), py::arg("stream"));
   m.def("route_fused_grid", [](int64_t M) {
     int64_t P;
     const int64_t G = route_fused_grid(M, &P);
@@ -171,7 +171,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
         py::arg("reply"), py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),
         py::arg("expected_per_rank"), py::arg("outbox"), py::arg("outbox_cap"), py::arg("direct"), py::arg("self"),
-        py::arg("stream"), py::arg("local") = std::vector<uintptr_t>{});
+        py::arg("stream"));
+  m.def("local_send", &launch_local_send, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"),
+        py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
+        py::arg("dir"), py::arg("n_dir"), py::arg("affine_w"), py::arg("state"), py::arg("n_state"),
+        py::arg("delay_ticks"), py::arg("outbox"), py::arg("outbox_cap"), py::arg("out_val"), py::arg("out_status"),
+        py::arg("stats"), py::arg("checksum"), py::arg("stream"),
+        "world-1 Send: registry resolution + handler dispatch in one pass into the caller's outputs");
   m.def("complete", &launch_complete, py::arg("rep"), py::arg("C"), py::arg("perm"), py::arg("M"),
         py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"), py::arg("stream"));
   m.def("records_to_soa", &launch_records_to_soa, py::arg("rec"), py::arg("M"), py::arg("actor"), py::arg("method"),

@@ -33,11 +33,16 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
                   int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                   int64_t C, int nargs, bool mc, uintptr_t sendbuf, uintptr_t perm, uintptr_t route, uintptr_t hist,
                   uintptr_t lb, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
-                  uint32_t affine_w, uintptr_t stream, bool zero_copy = false);
+                  uint32_t affine_w, uintptr_t stream);
 void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintptr_t reply, uintptr_t state,
                      uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
                      const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, const std::vector<uintptr_t>& direct,
-                     int self, uintptr_t stream, const std::vector<uintptr_t>& local = {});
+                     int self, uintptr_t stream);
+void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                       int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
+                       uint32_t affine_w, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
+                       const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, uintptr_t out_val, uintptr_t out_st,
+                       uintptr_t stats, uintptr_t checksum, uintptr_t stream);
 void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
                      uintptr_t checksum, bool direct, uintptr_t stream);
 int64_t wire_req_words(int64_t C, int nargs, bool mc);
@@ -285,9 +290,19 @@ class EpochEngine {
 
   void send_impl(const EngineSend& in) {
     EngineSend a = in;
-    if (a.packed) {  // v3 packs exactly the columns the format names (as v2's scatter reads them)
+    const bool local = local_ && R_ == 1 && !collectives() && a.direct;
+    if (a.packed || local) {  // exactly the columns the format names (as v2's scatter reads them)
       if (a.nargs < 2) a.a1 = 0;
       if (a.nargs < 3) a.a2 = 0;
+    }
+    if (local) {  // one destination: nothing to bucket or move
+      if (a.M > max_chunk_ * chunks_) throw std::invalid_argument("EpochEngine: batch exceeds max_batch");
+      Timed t(prof_.kernels_ns);
+      wire_ = WireInfo();
+      launch_local_send(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.table, a.cap, a.dir,
+                        a.n_dir, a.affine_w, a.state, a.n_state, a.delay_ticks, a.outbox, a.outbox_cap, a.out_val,
+                        a.out_st, bufs_[0].ws, a.checksum, a.stream);
+      return;
     }
     if (a.M > max_chunk_ * chunks_) throw std::invalid_argument("EpochEngine: batch exceeds max_batch");
     if (nbufs_ < 1) throw std::runtime_error("EpochEngine: buffers not set");
@@ -411,19 +426,7 @@ class EpochEngine {
     launch_route(off(a.actor, lo, 4), off(a.a0, lo, 8), off(a.a1, lo, 8), off(a.a2, lo, 8), off(a.method_col, lo, 2),
                  a.method_uniform, m, a.table, a.cap, a.dir, a.n_dir, R_, C_, a.nargs, a.mc, b.send,
                  write_perm ? b.perm : 0, b.route, b.hist, b.lb, b.ws, rank_, direct_view(a, i, bi), a.affine_w,
-                 (uintptr_t)cs, zero_copy(a, local_only, write_perm));
-  }
-
-  // Zero-copy local delivery (route_common.hpp LocalView): world 1 without
-  // collectives, direct completion, no inverse index -- the identity slot is then
-  // served from the caller's columns (decided on the device by the scan's flag).
-  bool zero_copy(const EngineSend& a, bool local_only, bool write_perm) const {
-    return zero_copy_ && local_only && !collectives() && a.direct && !write_perm;
-  }
-  std::vector<uintptr_t> local_view(const EngineSend& a, int i, int bi) const {
-    const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
-    return {bufs_[bi].route, off(a.a0, lo, 8), off(a.nargs > 1 ? a.a1 : 0, lo, 8), off(a.nargs > 2 ? a.a2 : 0, lo, 8),
-            off(a.method_col, lo, 2)};
+                 (uintptr_t)cs);
   }
 
   void serve(const EngineSend& a, int i, hipStream_t cs, int64_t wr) {
@@ -440,9 +443,7 @@ class EpochEngine {
       else
         launch_dispatch(collectives() ? b.recv : b.send, R_, C_, a.nargs, a.mc, b.reply, a.state, a.n_state, a.delay_ticks,
                         b.ws, std::max<int64_t>(1, m / R_), a.outbox, a.outbox_cap, direct_view(a, i, bi), rank_,
-                        (uintptr_t)cs,
-                        zero_copy(a, R_ == 1, !(a.direct && R_ == 1 && !a.checksum)) ? local_view(a, i, bi)
-                                                                                  : std::vector<uintptr_t>{});
+                        (uintptr_t)cs);
     }
     if (collectives()) {
       join(comm_stream_, ev_disp_[bi], cs);
@@ -510,7 +511,9 @@ class EpochEngine {
   uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
   bool packed_ = false;
   int prepped_ = 0;  // chunks whose route pass 1 ran ahead of the agreement wait (this Send)
-  bool zero_copy_ = getenv("PTYPE_ZERO_COPY") == nullptr || std::string(getenv("PTYPE_ZERO_COPY")) != "0";
+  // world 1 without collectives: the fused local Send (batch.hip local_send_kernel);
+  // PTYPE_LOCAL=0 keeps the epoch-slot pipeline there (A/B and tests)
+  bool local_ = getenv("PTYPE_LOCAL") == nullptr || std::string(getenv("PTYPE_LOCAL")) != "0";
   PackedLayout L_{};
   WireInfo wire_;
   HostProfile prof_;

@@ -120,21 +120,6 @@ struct DirectView {
   int32_t* out_st = nullptr;
   int self = -1;
   bool identity = false;  // positions ARE message indices: src is not written
-  bool zero_copy = false;  // identity slot: dispatch reads the caller's batch in place (LocalView)
-};
-
-// Zero-copy local delivery: when the own slot is an identity slot (world 1, every
-// message known and in capacity), slot position s IS message s, so the slot's
-// records would be a byte-for-byte re-layout of the caller's SoA columns.  The
-// scatter then writes nothing and the dispatch reads the columns (and the route
-// words, for the mailbox) where they already are -- 40 B per message of HBM
-// traffic that only reshuffled data the dispatcher can read directly.
-struct LocalView {
-  const uint32_t* route = nullptr;  // route words (mailbox << 8 | rank) of the chunk
-  const int64_t* a0 = nullptr;
-  const int64_t* a1 = nullptr;
-  const int64_t* a2 = nullptr;
-  const uint16_t* mcol = nullptr;  // per-message methods (null: the slot header's)
 };
 
 // Place the tile [tile, min(tile + kScatterTile, hi)) in message order.

@@ -25,9 +25,14 @@ def _table(n, affine):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("local", ["1", "0"])
 @pytest.mark.parametrize("chunks,affine,mixed", [(1, True, False), (3, True, True), (4, False, True)])
-def test_gpu_engine_matches_python_pipeline(chunks, affine, mixed):
+def test_gpu_engine_matches_python_pipeline(chunks, affine, mixed, local, monkeypatch):
+    """local=1: the engine's fused world-1 Send (local_send_kernel); local=0: its
+    epoch-slot pipeline -- both against the Python slot pipeline."""
     from ptype_amd.parallel.exchange import ActorExchange
+
+    monkeypatch.setenv("PTYPE_LOCAL", local)  # read when the engine is built
 
     n, M = 3000, 250_001
     gen = torch.Generator().manual_seed(chunks)
@@ -108,9 +113,9 @@ def test_gpu_engine_rccl_world1_matches_python():
 @pytest.mark.gpu
 @pytest.mark.parametrize("chunks,mixed", [(1, False), (2, True), (4, False)])
 def test_gpu_engine_zero_copy_identity(chunks, mixed):
-    """World 1, every actor known: the own slot is an identity slot and the
-    engine serves it from the caller's columns (no scatter writes, dispatch reads
-    in place).  Outputs and actor state equal the copying Python pipeline's."""
+    """World 1, every actor known: the engine's fused local Send resolves and
+    dispatches each message straight from the caller's columns (no epoch slot).
+    Outputs and actor state equal the slot-copying Python pipeline's."""
     from ptype_amd.parallel.exchange import ActorExchange
 
     n, M = 5000, 300_007
