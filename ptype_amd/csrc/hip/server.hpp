@@ -57,9 +57,11 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
   // tracing knobs are re-read on the idle path only, never between a request and its reply
   uint64_t trace_mask = sys_ld(&ctrl->trace_mask);
   TraceRec* trace = reinterpret_cast<TraceRec*>(sys_ld(&ctrl->trace_ring));
-  unsigned idle_polls = 0;
+  unsigned idle_polls = 0, iters = 0;
   for (;;) {
-    if (sys_ld(&ctrl->stop)) break;
+    // every poll is a PCIe round trip to host memory: the stop flag is read on
+    // one poll in 16, not before every ring poll (that made a poll two trips)
+    if ((++iters & 15) == 0 && sys_ld(&ctrl->stop)) break;
     const uint64_t seq = head + lane;
     RingSlot* s = &req[seq & ring_mask];
     const bool ready = sys_ld(&s->tag) == seq + 1;
