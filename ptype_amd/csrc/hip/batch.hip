@@ -79,6 +79,10 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
   __syncthreads();
   const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
   const unsigned lane = lane_id();
+  // lane l owns destination l's count for this wave (registers, not LDS atomics:
+  // with 8 destinations, 4 waves' leaders hammering 9 LDS words made the pass
+  // LDS-atomic bound -- SQ_WAIT_INST_LDS 50x the single-destination case)
+  unsigned hc = 0;
   for (int64_t base = lo; base < hi; base += K * kRouteThreads) {
     uint32_t a[K];
     int r[K];
@@ -131,25 +135,126 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
       uint64_t active = __ballot(d >= 0);
       while (active) {
         const int leader = __builtin_ctzll(active);
-        const int dl = __shfl(d, leader);
+        const int dl = __builtin_amdgcn_readlane(d, leader);
         const uint64_t m = __ballot(d == dl);
-        if (lane == (unsigned)leader) atomicAdd(&h[dl], (unsigned)__popcll(m));
+        if (dl < kWave) {
+          if (lane == (unsigned)dl) hc += (unsigned)__popcll(m);
+        } else if (lane == (unsigned)leader) {  // the miss column of a 64-rank world
+          atomicAdd(&h[dl], (unsigned)__popcll(m));
+        }
         active &= ~m;
       }
     }
   }
+  if (hc) atomicAdd(&h[lane], hc);  // lane <= R here: only owned columns are non-zero
   __syncthreads();
-  for (int d = threadIdx.x; d <= R; d += blockDim.x) hist[(int64_t)blockIdx.x * (R + 1) + d] = h[d];
+  // column-major [R + 1][G]: the scan reads each destination's column contiguously
+  for (int d = threadIdx.x; d <= R; d += blockDim.x) hist[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
 }
 
-// Pass 2 (one block): per-destination exclusive scan over blocks; headers; stats.
+// Slot headers + overflow / no-actor statistics from the column totals (block-level;
+// after the barrier that publishes `tot`).
+__device__ __forceinline__ void scan_headers(const unsigned* tot, int R, int64_t C, uint32_t* __restrict__ sendbuf,
+                                             int64_t req_words, uint32_t method_uniform,
+                                             unsigned long long* __restrict__ stats, int rank_self) {
+  const bool identity = R == 1 && tot[1] == 0 && (int64_t)tot[0] <= C;
+  for (int d = threadIdx.x; d < R; d += blockDim.x) {
+    const unsigned total = tot[d];
+    uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)d * req_words);
+    const unsigned delivered = total < C ? total : (unsigned)C;
+    const uint32_t flags = kFlagValid | (identity ? kFlagIdentity : 0);
+    h4[0] = make_uint4(delivered, total, (unsigned)rank_self, (flags << 16) | (method_uniform & 0xffffu));
+    if (total > C) atomicAdd(&stats[1], (unsigned long long)(total - C));
+  }
+  if (threadIdx.x == 0 && tot[R]) stats[0] += tot[R];
+}
+
+// Pass 2 (one block): per-destination exclusive scan over the blocks' histograms
+// -> per-block bases, slot headers, statistics.  Up to 16 ranks (RC = R + 1
+// columns held in registers): every thread loads its ~G/1024 rows whole (all
+// loads in flight at once), each column is scanned by wave shuffles, and ONE
+// block barrier exchanges the wave totals -- the columns no longer go one after
+// another (the column-serial scan took 28 us at 8 ranks: half the route).
+// Headers are written after all columns so the no-actor total is known: a batch
+// that maps whole and gap-free onto a single slot (R = 1, no unknown actor, no
+// overflow) is flagged kFlagIdentity -- slot position == message index, which
+// lets direct completion skip the inverse index.
+template <int RC>
+__global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__ hist, int G, int R, int64_t C,
+                                                          uint32_t* __restrict__ sendbuf, int64_t req_words,
+                                                          uint32_t method_uniform,
+                                                          unsigned long long* __restrict__ stats, int rank_self) {
+  constexpr int kRows = 2;  // rows per thread held in registers (G <= 2048: route_grid's target)
+  __shared__ unsigned wsum[1024 / kWave][RC];
+  __shared__ unsigned tot[kMaxRanks + 1];
+  const unsigned lane = lane_id(), w = threadIdx.x / kWave, nw = blockDim.x / kWave;
+  const int per = (G + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int b0 = threadIdx.x * per, b1 = b0 + per < G ? b0 + per : G;
+  const int cols = R + 1;
+  const bool fast = per <= kRows;
+  unsigned cell[kRows][RC], sum[RC], v[RC];
+#pragma unroll
+  for (int d = 0; d < RC; ++d) sum[d] = 0;
+  if (fast) {  // every load of the thread issued before any is used
+#pragma unroll
+    for (int r = 0; r < kRows; ++r)
+#pragma unroll
+      for (int d = 0; d < RC; ++d) {
+        cell[r][d] = (b0 + r < b1 && d < cols) ? hist[(int64_t)d * G + b0 + r] : 0u;
+        sum[d] += cell[r][d];
+      }
+  } else {
+    for (int b = b0; b < b1; ++b)
+#pragma unroll
+      for (int d = 0; d < RC; ++d) sum[d] += d < cols ? hist[(int64_t)d * G + b] : 0u;
+  }
+#pragma unroll
+  for (int d = 0; d < RC; ++d) {  // inclusive scan of each column across the wave (DPP)
+    v[d] = wave_incl_scan(sum[d]);
+    if (lane == kWave - 1) wsum[w][d] = v[d];
+  }
+  __syncthreads();
+  if (w == 0) {  // exclusive scan of the wave totals, per column (lanes = waves)
+#pragma unroll
+    for (int d = 0; d < RC; ++d) {
+      const unsigned x = lane < nw ? wsum[lane][d] : 0u;
+      const unsigned y = wave_incl_scan(x);
+      if (lane < nw) wsum[lane][d] = y - x;
+      if (lane == nw - 1 && d < cols) tot[d] = y;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int d = 0; d < RC; ++d) {
+    if (d >= cols) continue;
+    unsigned run = wsum[w][d] + v[d] - sum[d];  // exclusive prefix of this thread's first block
+    if (fast) {
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+        if (b0 + r < b1) {
+          hist[(int64_t)d * G + b0 + r] = run;  // hist becomes the per-block base
+          run += cell[r][d];
+        }
+    } else {
+      for (int b = b0; b < b1; ++b) {
+        uint32_t* c = hist + (int64_t)d * G + b;
+        const unsigned x = *c;
+        *c = run;
+        run += x;
+      }
+    }
+  }
+  scan_headers(tot, R, C, sendbuf, req_words, method_uniform, stats, rank_self);
+}
+
+// Pass 2, any R (R + 1 > 17 columns): the columns one after another.
 // Wave-level scans (shuffles) + one LDS exchange of wave totals: 3 barriers per
 // column instead of a 1024-wide Hillis-Steele.  Headers are written after all
 // columns so the no-actor total is known: a batch that maps whole and gap-free
 // onto a single slot (R = 1, no unknown actor, no overflow) is flagged
 // kFlagIdentity -- slot position == message index, which lets direct completion
 // skip the inverse index.
-__global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__ hist, int G, int R, int64_t C,
+__global__ __launch_bounds__(1024) void route_scan_wide_kernel(uint32_t* __restrict__ hist, int G, int R, int64_t C,
                                                           uint32_t* __restrict__ sendbuf, int64_t req_words,
                                                           uint32_t method_uniform,
                                                           unsigned long long* __restrict__ stats, int rank_self) {
@@ -160,7 +265,7 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__
   const int b0 = threadIdx.x * per, b1 = b0 + per < G ? b0 + per : G;
   for (int d = 0; d <= R; ++d) {
     unsigned s = 0;
-    for (int b = b0; b < b1; ++b) s += hist[(int64_t)b * (R + 1) + d];
+    for (int b = b0; b < b1; ++b) s += hist[(int64_t)d * G + b];
     unsigned v = s;  // inclusive scan within the wave
     for (int off = 1; off < kWave; off <<= 1) {
       const unsigned t = __shfl_up(v, off);
@@ -179,23 +284,14 @@ __global__ __launch_bounds__(1024) void route_scan_kernel(uint32_t* __restrict__
     __syncthreads();
     unsigned run = (w ? wsum[w - 1] : 0u) + v - s;  // exclusive prefix of this thread's first block
     for (int b = b0; b < b1; ++b) {                   // hist becomes the per-block base
-      const unsigned c = hist[(int64_t)b * (R + 1) + d];
-      hist[(int64_t)b * (R + 1) + d] = run;
+      const unsigned c = hist[(int64_t)d * G + b];
+      hist[(int64_t)d * G + b] = run;
       run += c;
     }
     if (threadIdx.x == 0) tot[d] = wsum[nw - 1];
     __syncthreads();
   }
-  const bool identity = R == 1 && tot[1] == 0 && (int64_t)tot[0] <= C;
-  for (int d = threadIdx.x; d < R; d += blockDim.x) {
-    const unsigned total = tot[d];
-    uint4* h4 = reinterpret_cast<uint4*>(sendbuf + (int64_t)d * req_words);
-    const unsigned delivered = total < C ? total : (unsigned)C;
-    const uint32_t flags = kFlagValid | (identity ? kFlagIdentity : 0);
-    h4[0] = make_uint4(delivered, total, (unsigned)rank_self, (flags << 16) | (method_uniform & 0xffffu));
-    if (total > C) atomicAdd(&stats[1], (unsigned long long)(total - C));
-  }
-  if (threadIdx.x == 0 && tot[R]) stats[0] += tot[R];
+  scan_headers(tot, R, C, sendbuf, req_words, method_uniform, stats, rank_self);
 }
 
 // Pass 3: stable placement + SoA -> packed wire records (format <NARGS, MC>).
@@ -207,7 +303,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(
     int64_t req_words, int32_t* __restrict__ perm, DirectView dv) {
   __shared__ unsigned cnt[kScatterItems][kRouteThreads / kWave][kMaxRanks];
   __shared__ unsigned run[kMaxRanks];
-  for (int d = threadIdx.x; d < R; d += blockDim.x) run[d] = base[(int64_t)blockIdx.x * (R + 1) + d];
+  for (int d = threadIdx.x; d < R; d += blockDim.x) run[d] = base[(int64_t)d * gridDim.x + blockIdx.x];
   const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
   if (dv.src)  // the scan flagged a gap-free single slot: positions are message indices
     dv.identity = ((sendbuf[(int64_t)dv.self * req_words + 3] >> 16) & kFlagIdentity) != 0;
@@ -589,8 +685,15 @@ int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, ui
 // Pass 2: per-destination bases and slot headers in regions of `req_words`.
 void route_scan(int64_t G, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t hist,
                 int method_uniform, uintptr_t stats, int rank_self, uintptr_t stream) {
-  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1024), 0, as_stream(stream), (uint32_t*)hist, (int)G, R, C,
-                     (uint32_t*)sendbuf, req_words, (uint32_t)method_uniform, (unsigned long long*)stats, rank_self);
+#define PT_SCAN(K)                                                                                              \
+  hipLaunchKernelGGL(K, dim3(1), dim3(1024), 0, as_stream(stream), (uint32_t*)hist, (int)G, R, C, (uint32_t*)sendbuf, \
+                     req_words, (uint32_t)method_uniform, (unsigned long long*)stats, rank_self)
+  if (R + 1 <= 2) PT_SCAN(route_scan_kernel<2>);
+  else if (R + 1 <= 5) PT_SCAN(route_scan_kernel<5>);
+  else if (R + 1 <= 9) PT_SCAN(route_scan_kernel<9>);
+  else if (R + 1 <= 17) PT_SCAN(route_scan_kernel<17>);
+  else PT_SCAN(route_scan_wide_kernel);
+#undef PT_SCAN
   PT_HIP_CHECK(hipGetLastError());
 }
 

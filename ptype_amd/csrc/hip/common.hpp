@@ -65,6 +65,23 @@ __device__ __forceinline__ unsigned mbcnt64(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Inclusive prefix sum across the 64 lanes of a wave with DPP row shifts (VALU,
+// a few cycles each) instead of ds_bpermute shuffles (~100-cycle LDS-path round
+// trips, six of them in a dependent chain): 4 row_shr steps scan each 16-lane
+// row, then the three row totals are read as scalars and added to later rows.
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned v) {
+  const unsigned lane = __lane_id();
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  const unsigned t0 = (unsigned)__builtin_amdgcn_readlane((int)v, 15);
+  const unsigned t1 = (unsigned)__builtin_amdgcn_readlane((int)v, 31);
+  const unsigned t2 = (unsigned)__builtin_amdgcn_readlane((int)v, 47);
+  const unsigned row = lane >> 4;
+  return v + (row > 0 ? t0 : 0u) + (row > 1 ? t1 : 0u) + (row > 2 ? t2 : 0u);
+}
+
 __device__ __forceinline__ uint64_t realtime_ticks() {  // 100 MHz constant clock
   return __builtin_amdgcn_s_memrealtime();
 }

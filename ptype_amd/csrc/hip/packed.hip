@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_packed_kernel(
     int64_t req_words, PackedLayout L, int32_t* __restrict__ perm, DirectView dv) {
   __shared__ unsigned cnt[kScatterItems][kRouteThreads / kWave][kMaxRanks];
   __shared__ unsigned run[kMaxRanks];
-  for (int d = threadIdx.x; d < R; d += blockDim.x) run[d] = base[(int64_t)blockIdx.x * (R + 1) + d];
+  for (int d = threadIdx.x; d < R; d += blockDim.x) run[d] = base[(int64_t)d * gridDim.x + blockIdx.x];
   const int64_t lo = blockIdx.x * P, hi = lo + P < M ? lo + P : M;
   if (dv.src) dv.identity = ((sendbuf[(int64_t)dv.self * req_words + 3] >> 16) & kFlagIdentity) != 0;
   __syncthreads();

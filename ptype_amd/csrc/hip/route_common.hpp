@@ -156,16 +156,17 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
   // rank within (item k, wave w, destination): ballots, peeled per present destination
 #pragma unroll
   for (int k = 0; k < kScatterItems; ++k) {
-    for (int x = lane; x < R; x += kWave) cnt[k][w][x] = 0;
+    unsigned c = 0;  // lane l counts destination l (R <= 64): one LDS store per lane, not one per destination
     uint64_t active = __ballot(d[k] >= 0);
     while (active) {
       const int leader = __builtin_ctzll(active);
-      const int dl = __shfl(d[k], leader);
+      const int dl = __builtin_amdgcn_readlane(d[k], leader);
       const uint64_t m = __ballot(d[k] == dl);
       if (d[k] == dl) rk[k] = mbcnt64(m);
-      if (lane == (unsigned)leader) cnt[k][w][dl] = (unsigned)__popcll(m);
+      if (lane == (unsigned)dl) c = (unsigned)__popcll(m);
       active &= ~m;
     }
+    if (lane < (unsigned)R) cnt[k][w][lane] = c;
   }
   __syncthreads();
   // per destination: exclusive prefix in message order (k-major, then wave)

@@ -209,7 +209,9 @@ def test_gpu_table_sweep_and_snapshot():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("R,fmt", [(1, B.FULL_FORMAT), (2, B.WireFormat(2, False)), (8, B.WireFormat(2, False)),
-                                   (8, B.WireFormat(3, True)), (3, B.WireFormat(2, True))])
+                                   (8, B.WireFormat(3, True)), (3, B.WireFormat(2, True)),
+                                   (16, B.WireFormat(2, False)), (20, B.WireFormat(2, False)),
+                                   (64, B.WireFormat(2, False))])
 def test_gpu_route_dispatch_complete(R, fmt):
     M, n_actors = 200_003, 4096
     C = B.stripe_capacity(M, R)
