@@ -62,8 +62,36 @@ struct alignas(64) RingSlot {
   MsgRecord msg;
   uint64_t tag;       // sequence number + 1 of the request published in this slot
   uint64_t t_pub_ns;  // host steady-clock time of publication (latency tracing)
-  uint64_t pad[2];
+  uint64_t csum;      // ring_csum(seq, msg): lets the device read msg in the same trip as the tag
+  uint64_t pad;
 };
+
+#ifdef __HIPCC__
+#define PT_HD __host__ __device__
+#else
+#define PT_HD
+#endif
+// Checksum binding a ring slot's message words to its sequence number.  The
+// dispatcher reads tag, message and checksum in ONE batch of loads (one PCIe
+// round trip, not two): individual 8-B reads of host memory may be served in
+// any order, so a message word can be older than the tag it was read with --
+// the checksum, written before the tag, exposes that (mismatch -> read again).
+inline PT_HD uint64_t ring_csum(uint64_t seq, uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3) {
+  uint64_t h = seq * 0x9e3779b97f4a7c15ull;
+  for (uint64_t w : {w0, w1, w2, w3}) {
+    h ^= w + 0x632be59bd9b4e019ull + (h << 6) + (h >> 2);
+    h ^= h >> 31;
+    h *= 0xbf58476d1ce4e5b9ull;
+  }
+  return h ^ (h >> 29);
+}
+inline uint64_t ring_csum(uint64_t seq, const MsgRecord& m) {
+  uint64_t w[4];
+  static_assert(sizeof(MsgRecord) == sizeof(w), "MsgRecord is four words");
+  __builtin_memcpy(w, &m, sizeof(w));
+  return ring_csum(seq, w[0], w[1], w[2], w[3]);
+}
+#undef PT_HD
 
 // One traced request of the persistent dispatcher (host-visible trace ring).
 struct TraceRec {
@@ -74,12 +102,20 @@ struct TraceRec {
 };
 static_assert(sizeof(RingSlot) == 64, "RingSlot must be 64 bytes");
 
+// Reply slot of the latency path.  The value and the tag share one aligned
+// 16-B unit that the device writes with ONE 16-byte store: one PCIe write that
+// lands whole, so the host that sees the tag sees the value -- no system fence
+// and no second write for the tag (that pair cost ~0.6 us per call).  The tag
+// carries the status in its low byte: (seq + 1) << 8 | status.
 struct alignas(32) ReplySlot {
-  ReplyRecord rep;
-  uint64_t tag;
-  uint64_t pad;
+  int64_t value;
+  uint64_t tag;    // reply_tag(seq, status)
+  uint64_t pad[2];
 };
 static_assert(sizeof(ReplySlot) == 32, "ReplySlot must be 32 bytes");
+
+inline constexpr uint64_t reply_tag(uint64_t seq, uint32_t status) { return ((seq + 1) << 8) | (status & 0xffu); }
+inline constexpr bool reply_tag_is(uint64_t tag, uint64_t seq) { return (tag >> 8) == ((seq + 1) & (~0ull >> 8)); }
 
 // Device-side backend entry point that the host net/rpc server uses to execute a
 // call on a GPU actor (exported by _hip as a C function pointer).

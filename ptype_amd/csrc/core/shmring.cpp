@@ -103,11 +103,13 @@ ReplyRecord shm_call(const ShmView& v, const MsgRecord& m, double timeout_s) {
     if (spins > 64) std::this_thread::yield();
   RingSlot* s = &v.req[idx];
   s->msg = m;
+  s->csum = ring_csum(seq, m);  // before the tag (release below)
   s->t_pub_ns = t0;
   __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
   poke_if_parked(v);
   ReplySlot* o = &v.rep[idx];
-  for (unsigned spins = 0; __atomic_load_n(&o->tag, __ATOMIC_ACQUIRE) != seq + 1; ++spins) {
+  uint64_t tag;
+  for (unsigned spins = 0; !reply_tag_is(tag = __atomic_load_n(&o->tag, __ATOMIC_ACQUIRE), seq); ++spins) {
     if ((spins & 1023) == 1023) {
       poke_if_parked(v);
       if ((now_ns() - t0) * 1e-9 > timeout_s) {
@@ -119,7 +121,10 @@ ReplyRecord shm_call(const ShmView& v, const MsgRecord& m, double timeout_s) {
       std::this_thread::yield();
     }
   }
-  ReplyRecord r = o->rep;
+  ReplyRecord r;
+  r.value = o->value;  // landed with the tag (one 16-B device store)
+  r.status = (int32_t)(tag & 0xff);
+  r.actor = m.actor;
   v.owner[idx].store(seq + ring, std::memory_order_release);
   return r;
 }

@@ -42,13 +42,34 @@ __device__ __forceinline__ uint64_t sys_ld(const uint64_t* p) {
 __device__ __forceinline__ void sys_st(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// 16 aligned bytes in ONE system-coherent vector store (what sys_st emits for 8 B,
+// `sc0 sc1`, at dwordx4 width): a single write to host memory, not two.
+__device__ __forceinline__ void sys_st16(uint64_t* p, uint64_t lo, uint64_t hi) {
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  const u64x2 v{lo, hi};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+
+// How the wave polls the ring (tuning knobs, PTYPE_POLL_{LANES,FULL,SLEEP}):
+// slots whose tag is read per trip (= most requests taken per batch), whether the
+// head slot's message is read in the same trip (checksum-validated), and how
+// many s_sleep(1) pauses separate empty polls.  Measured on MI355X
+// (tools/latency_sweep.py, profiles/r1_latency_sweep.jsonl): reading the head
+// slot whole in every poll saves the second round trip but costs more than it
+// saves -- p50 6.0 us vs 4.0-4.2 us with tag-only polls (the device's reads of
+// the line the host is writing slow the host's publish) -- so it is off.
+struct PollConfig {
+  uint32_t lanes = 64;
+  uint32_t full = 0;
+  uint32_t sleep = 1;
+};
 
 __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __restrict__ req,
                                                                  ReplySlot* __restrict__ rep, uint64_t ring_mask,
                                                                  ServerCtrl* __restrict__ ctrl, uint64_t head,
                                                                  int64_t* __restrict__ state, uint32_t n_state,
                                                                  uint64_t delay_ticks, uint64_t idle_ticks,
-                                                                 uint64_t max_ticks) {
+                                                                 uint64_t max_ticks, PollConfig poll) {
   const unsigned lane = lane_id();
   const uint64_t t_start = realtime_ticks();
   uint64_t last_work = t_start;
@@ -64,7 +85,15 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
     if ((++iters & 15) == 0 && sys_ld(&ctrl->stop)) break;
     const uint64_t seq = head + lane;
     RingSlot* s = &req[seq & ring_mask];
-    const bool ready = sys_ld(&s->tag) == seq + 1;
+    // Every poll is PCIe reads of host memory.  With `poll.full` the head slot is
+    // read whole in the same trip as its tag and validated by its checksum, so a
+    // lone call costs one round trip to be seen, not two.
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(&s->msg);
+    const bool spec = poll.full && lane == 0;
+    uint64_t tag = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0, cs = 0;
+    if (lane < poll.lanes) tag = sys_ld(&s->tag);
+    if (spec) w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3), cs = sys_ld(&s->csum);
+    const bool ready = tag == seq + 1 && (!spec || cs == ring_csum(seq, w0, w1, w2, w3));
     const uint64_t m = __ballot(ready);
     const unsigned n = (m == ~0ull) ? 64u : (unsigned)__builtin_ctzll(~m);
     if (n == 0) {
@@ -110,13 +139,14 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
         }
         return;
       }
-      __builtin_amdgcn_s_sleep(1);
+      for (uint32_t k = 0; k < poll.sleep; ++k) __builtin_amdgcn_s_sleep(1);
       continue;
     }
     const uint64_t t_seen = realtime_ticks();
     if (lane < n) {
-      const uint64_t* w = reinterpret_cast<const uint64_t*>(&s->msg);
-      const uint64_t w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3);
+      if (!spec) {  // ordered after this lane's tag read (it returned; the branch depends on it)
+        w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3);
+      }
       MsgRecord msg;
       msg.actor = (uint32_t)w0;
       msg.method = (uint16_t)(w0 >> 32);
@@ -125,12 +155,10 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
       msg.a1 = (int64_t)w2;
       msg.a2 = (int64_t)w3;
       const ReplyRecord r = run_handler(msg, state, n_state, delay_ticks);
+      // value + tag in ONE 16-B store (one PCIe write that lands whole): the
+      // host that sees the tag sees the value, so no fence and no second write
       ReplySlot* o = &rep[seq & ring_mask];
-      uint64_t* ow = reinterpret_cast<uint64_t*>(&o->rep);
-      sys_st(ow, (uint64_t)r.value);
-      sys_st(ow + 1, (uint64_t)(uint32_t)r.status | ((uint64_t)r.actor << 32));
-      __threadfence_system();
-      sys_st(&o->tag, seq + 1);
+      sys_st16(reinterpret_cast<uint64_t*>(o), (uint64_t)r.value, reply_tag(seq, (uint32_t)r.status));
       if (trace_mask && trace) {  // after the reply is out: off the request's critical path
         const uint64_t t_done = realtime_ticks();
         TraceRec* tr = &trace[seq & trace_mask];
@@ -342,6 +370,7 @@ class DeviceServer {
       if (spins > 64) std::this_thread::yield();
     RingSlot* s = &req_[idx];
     s->msg = m;
+    s->csum = ring_csum(seq, m);  // before the tag (release below)
     s->t_pub_ns = now_ns();
     __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
     return seq;
@@ -351,7 +380,8 @@ class DeviceServer {
     const uint32_t idx = (uint32_t)(seq & (ring_ - 1));
     ReplySlot* o = &rep_[idx];
     auto t0 = std::chrono::steady_clock::now();
-    for (unsigned spins = 0; __atomic_load_n(&o->tag, __ATOMIC_ACQUIRE) != seq + 1; ++spins) {
+    uint64_t tag;
+    for (unsigned spins = 0; !reply_tag_is(tag = __atomic_load_n(&o->tag, __ATOMIC_ACQUIRE), seq); ++spins) {
       if ((spins & 1023) == 1023) {
         ensure_running();  // the kernel may have retired on idle/lifetime
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
@@ -363,7 +393,10 @@ class DeviceServer {
         std::this_thread::yield();
       }
     }
-    ReplyRecord r = o->rep;
+    ReplyRecord r;
+    r.value = o->value;  // landed with the tag
+    r.status = (int32_t)(tag & 0xff);
+    r.actor = req_[idx].msg.actor;
     const uint64_t rtt = now_ns() - req_[idx].t_pub_ns;
     owner_[idx].store(seq + ring_, std::memory_order_release);
     int b = rtt ? 63 - __builtin_clzll(rtt) : 0;
@@ -396,7 +429,7 @@ class DeviceServer {
           hipSetDevice(device_);
           hipLaunchKernelGGL(persistent_dispatch_kernel, dim3(1), dim3(64), 0, stream_, dreq_, drep_,
                              (uint64_t)(ring_ - 1), dctrl_, head, state_, n_state_, delay_ticks_, idle_ticks_,
-                             max_ticks_);
+                             max_ticks_, poll_);
           PT_HIP_CHECK(hipGetLastError());
           launches_.fetch_add(1);
           return;
@@ -411,6 +444,17 @@ class DeviceServer {
   int64_t* state_;
   uint32_t n_state_;
   uint64_t delay_ticks_ = 0, idle_ticks_ = 0, max_ticks_ = 0;
+  PollConfig poll_ = [] {
+    PollConfig p;
+    auto env = [](const char* k, uint32_t d) {
+      const char* v = getenv(k);
+      return v ? (uint32_t)atoi(v) : d;
+    };
+    p.lanes = std::min<uint32_t>(64, std::max<uint32_t>(1, env("PTYPE_POLL_LANES", p.lanes)));
+    p.full = env("PTYPE_POLL_FULL", p.full);
+    p.sleep = env("PTYPE_POLL_SLEEP", p.sleep);
+    return p;
+  }();
   RingSlot* req_ = nullptr;
   ReplySlot* rep_ = nullptr;
   ServerCtrl* ctrl_ = nullptr;

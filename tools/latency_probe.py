@@ -30,6 +30,12 @@ def main(n=5000):
                 lat.append((time.perf_counter() - t0) * 1e6)
             b = t.breakdown()
         b["python_call_us"] = trace.percentiles(lat)
+        lat = []  # the same loop with tracing off (what bench.py measures)
+        for i in range(n):
+            t0 = time.perf_counter()
+            srv.call(METHOD_CALC_MULTIPLY, i % 1024, i, 3)
+            lat.append((time.perf_counter() - t0) * 1e6)
+        b["python_call_untraced_us"] = trace.percentiles(lat)
         print(json.dumps(b))
     finally:
         srv.close()
