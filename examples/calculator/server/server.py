@@ -21,11 +21,12 @@ def main():
     server = C.Server()
     if not cfg.has_gpu:
         server.Register(calculator.Calculator())
+        server.Listen(cfg.port)  # before registering, so a client that sees the node can dial it
     c = C.Join(C.background(), cfg)
-    if cfg.has_gpu:
+    if cfg.has_gpu:  # device methods need the joined runtime; listen once they are bound
         calculator.serve_device(c.runtime, server)
+        server.Listen(cfg.port)
     print(f"server: services {c.Registry.Services(C.background())}", flush=True)
-    server.Listen(cfg.port)
     try:
         wait_for_signal()
     finally:

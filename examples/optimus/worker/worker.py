@@ -20,11 +20,15 @@ def main():
     server = C.Server()
     if not cfg.has_gpu:
         server.Register(optimus.Prime(delay=float(os.environ.get("PRIME_DELAY", "0.25"))))
+        # listen BEFORE registering: the reference registers first (worker.go Join,
+        # then ListenAndServe), so a mesh client that dials the new node at once can
+        # be refused -- the coordinator's initial connect then fails (rpc.go:278-280)
+        server.Listen(cfg.port)
     c = C.Join(C.background(), cfg)
-    if cfg.has_gpu:
+    if cfg.has_gpu:  # device methods need the joined runtime; listen once they are bound
         c.runtime.serve(server, optimus.SERVICE, optimus.DEVICE_METHODS)
+        server.Listen(cfg.port)
     print(f"worker: services {c.Registry.Services(C.background())}", flush=True)
-    server.Listen(cfg.port)
     try:
         wait_for_signal()
     finally:

@@ -366,10 +366,9 @@ void scenario_shm() {
       idle = 0;
       const MsgRecord m = sl->msg;
       ReplySlot* o = &v.rep[head & (ring - 1)];
-      o->rep.value = m.method == kCalculatorMultiply ? m.a0 * m.a1 : 0;
-      o->rep.status = m.method == kCalculatorMultiply ? kStatusOk : kStatusNoMethod;
-      o->rep.actor = m.actor;
-      __atomic_store_n(&o->tag, head + 1, __ATOMIC_RELEASE);
+      o->value = m.method == kCalculatorMultiply ? m.a0 * m.a1 : 0;
+      const uint32_t st = m.method == kCalculatorMultiply ? kStatusOk : kStatusNoMethod;
+      __atomic_store_n(&o->tag, reply_tag(head, st), __ATOMIC_RELEASE);  // the GPU writes value + tag as one 16-B store
       ++head;
     }
   });
