@@ -163,6 +163,38 @@ def main():
     if args.steps:
         verify("timed")
 
+    # diagnostics, outside the timed region: the step's all-to-all byte volume moved
+    # by RCCL alone (same chunking, same per-peer sizes), so a multi-GPU line says
+    # whether the step is bound by xGMI or by the kernels around it
+    diag = None
+    if dist_on and use_gpu and ex.last_wire is not None and args.steps:
+        w = ex.last_wire
+        sizes = [4 * int(w["req_words"]), 4 * int(w["rep_words"])]  # bytes per chunk, all peers
+        bufs = [(torch.empty(s, dtype=torch.uint8, device=device), torch.empty(s, dtype=torch.uint8, device=device))
+                for s in sizes]
+
+        def a2a_step():
+            for _ in range(chunks):
+                for snd, rcv in bufs:
+                    dist.all_to_all_single(rcv, snd)
+
+        a2a_step()
+        sync()
+        barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 5
+        e0.record()
+        for _ in range(reps):
+            a2a_step()
+        e1.record()
+        sync()
+        a2a_ms = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64, device=device)
+        dist.all_reduce(a2a_ms, op=dist.ReduceOp.MAX)
+        per_step = chunks * sum(sizes)
+        off_rank = per_step * (world - 1) / world
+        diag = {"a2a_only_ms_per_step": float(a2a_ms.item()), "a2a_bytes_per_step_per_rank": per_step,
+                "a2a_offrank_GBps_per_rank": off_rank / (float(a2a_ms.item()) * 1e-3) / 1e9 if world > 1 else None}
+
     # p50 RTT of a synchronous Call to a GPU actor (persistent dispatcher, no kernel
     # launch per call): from this process to its own GPU, and -- with more than one
     # rank -- from this process to the actors of the NEXT rank's GPU, through that
@@ -241,6 +273,8 @@ def main():
                 "hip_graph": graph is not None,
             },
         }
+        if diag is not None:
+            out["diag"] = diag
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()

@@ -1,0 +1,67 @@
+"""bench.py contract: one JSON line from rank 0 with the BASELINE.json metric, the
+whole-job aggregate, and the fields the round driver reads.
+
+CPU: the same pipeline on gloo (world 1 and 2, torchrun on 127.0.0.1).  GPU: the
+real multi-process RCCL path at 2..8 ranks -- only where the box has that many
+GPUs (a 1-GPU box skips it: RCCL refuses two ranks on one device)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT, free_port
+
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "p50_rtt_us"}
+
+
+def _run(nproc, extra, timeout=600):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if nproc == 1:
+        cmd = [sys.executable, "bench.py"]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py"]
+    cmd += ["--gpus", str(nproc)] + extra
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
+    return json.loads(lines[0])
+
+
+SMALL = ["--steps", "2", "--warmup", "1", "--msgs-per-gpu", "20000", "--actors-per-gpu", "1024", "--rtt-calls", "0"]
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_bench_json_contract_cpu(nproc):
+    out = _run(nproc, ["--cpu"] + SMALL)
+    assert REQUIRED <= set(out)
+    assert out["metric"] == "messages/sec" and out["unit"] == "msg/s" and out["higher_is_better"] is True
+    assert out["n_gpus"] == nproc and out["steps"] == 2 and out["warmup"] == 1 and out["scaling"] == "weak"
+    assert out["data"] == "synthetic"
+    assert out["config"]["global_batch"] == 20000 * nproc
+    # value is the whole-job aggregate: every rank's messages over the max rank time
+    assert out["value"] == pytest.approx(20000 * nproc * 2 / (out["ms_per_step"] * 2 / 1e3), rel=1e-6)
+
+
+def _gpus() -> int:
+    try:
+        import torch
+
+        return torch.cuda.device_count() if torch.cuda.is_available() else 0
+    except Exception:
+        return 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nproc", [2, 4, 8])
+def test_bench_multi_gpu(nproc):
+    if _gpus() < nproc:
+        pytest.skip(f"needs {nproc} GPUs (RCCL refuses two ranks on one device)")
+    out = _run(nproc, ["--steps", "3", "--warmup", "2", "--rtt-calls", "200"], timeout=900)
+    assert out["n_gpus"] == nproc and out["value"] > 0
+    assert out["config"]["wire"] == "v3-packed"
+    assert out["p50_rtt_remote_us"] is not None and out["diag"]["a2a_only_ms_per_step"] > 0
