@@ -40,6 +40,11 @@ def _parse():
     p.add_argument("--cpu", action="store_true", help="gloo/CPU dry run of the same pipeline (tests)")
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the step as a captured hipGraph (auto: single rank)")
+    p.add_argument("--loopback", type=int, default=0, metavar="R",
+                   help="profiling only: one GPU runs rank 0 of a symmetric R-rank node with the all-to-alls "
+                        "as local copies (FakeComm loopback) -- the compute side of an R-GPU step")
+    p.add_argument("--link-gbps", type=float, default=0.0,
+                   help="with --loopback: model the all-to-all at this per-rank off-rank bandwidth (GB/s)")
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the process group and run the all-to-alls even for one rank "
                         "(exercises the RCCL path on a 1-GPU box)")
@@ -100,22 +105,33 @@ def main():
             torch.cuda.synchronize(device)
 
     M = args.msgs_per_gpu
-    n_actors = args.actors_per_gpu * world
-    chunks = args.chunks or (4 if dist_on else 1)
+    fake = None
+    if args.loopback > 0:
+        if world != 1 or not use_gpu:
+            raise SystemExit("--loopback is a single-process GPU profiling mode")
+        from ptype_amd.ops import hip
+
+        fake = (hip().FakeComm(args.loopback, loopback=True, link_gbps=args.link_gbps), 0)
+    geo = args.loopback or world  # ranks the actors are sharded over
+    n_actors = args.actors_per_gpu * geo
+    # 2 pipeline chunks on the collective path: measured against 1/4/8 with the
+    # all-to-all modelled at xGMI-like bandwidth (profiles/r1_chunk_model.jsonl)
+    # and on the forced single-rank RCCL path (0.31 vs 0.38-0.40 ms at 4 chunks)
+    chunks = args.chunks or (2 if dist_on or fake else 1)
 
     # GPU registry mirror: actor a lives on rank a % world in mailbox a // world
     table = RegistryTable(2 * n_actors, device=device)
     ids = torch.arange(n_actors, dtype=torch.int64)
-    table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
-    table.enable_directory(n_actors, affine_world=world)  # K5b directory + verified strided placement (no gathers)
+    table.upsert(actor_keys(ids), (ids % geo).to(torch.int32), (ids // geo).to(torch.int32))
+    table.enable_directory(n_actors, affine_world=geo)  # K5b directory + verified strided placement (no gathers)
     state = torch.zeros(args.actors_per_gpu, dtype=torch.int64, device=device)
-    ex = ActorExchange(table, M, chunks=chunks, state=state)
+    ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake)
     req = B.MsgBatch(torch.empty(M, dtype=torch.int32, device=device), torch.empty(M, dtype=torch.int64, device=device),
                      torch.empty(M, dtype=torch.int64, device=device), None, METHOD_CALC_MULTIPLY)
     val = torch.empty(M, dtype=torch.int64, device=device)
     st = torch.empty(M, dtype=torch.int32, device=device)
 
-    use_graph = use_gpu and (args.graph == "on" or (args.graph == "auto" and not dist_on))
+    use_graph = use_gpu and (args.graph == "on" or (args.graph == "auto" and not dist_on and fake is None))
     graph = None
     if use_graph:
         # the whole step (new requests + Send) as one hipGraph; the generator reads its
@@ -201,7 +217,7 @@ def main():
     # process's shared-memory rings (the reference's Client.Call to another node,
     # cluster/rpc.go:59-67; here a node is a GPU of the same host)
     p50 = p50_remote = None
-    if use_gpu and args.rtt_calls > 0:
+    if use_gpu and args.rtt_calls > 0 and fake is None:
         from ptype_amd.ops import hip
 
         tag = os.environ.get("MASTER_PORT", "0")
@@ -271,6 +287,9 @@ def main():
                 **wire_info(ex, req),
                 "client_batch": "SoA (actor u32, A i64, B i64)",
                 "hip_graph": graph is not None,
+                **({"loopback_ranks": args.loopback, "link_gbps": args.link_gbps, "note": "profiling mode: rank 0 of a symmetric "
+                    f"{args.loopback}-rank node, all-to-alls as local copies (not a headline number)"}
+                   if fake else {}),
             },
         }
         if diag is not None:

@@ -42,6 +42,7 @@
 
 #include "common.hpp"
 #include "handlers.hpp"
+#include "packed.hpp"
 #include "route_common.hpp"
 
 namespace ptype {
@@ -66,13 +67,17 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
 // MODE 0: hash probe; 1: route directory; 2: affine placement (ids below n_dir
 // verified to sit at rank id % W, mailbox id / W -- route words computed, no
 // gathers; W a power of two uses shifts).
-template <int K, int MODE>
+//
+// META: the v3 width pass rides along (the batch's argument columns are read in
+// the same tiles, column maxima published per block into mc.meta), so a packed
+// Send reads its batch once before the agreement instead of twice.
+template <int K, int MODE, bool META = false>
 __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_t* __restrict__ actor, int64_t M,
                                                                    int64_t P, const TableEntry* __restrict__ table,
                                                                    uint64_t mask, const uint32_t* __restrict__ dir,
                                                                    uint32_t n_dir, uint32_t aw, int aw_shift, int R,
                                                                    uint32_t* __restrict__ route,
-                                                                   uint32_t* __restrict__ hist) {
+                                                                   uint32_t* __restrict__ hist, MetaCols mc = {}) {
   constexpr bool DIR = MODE == 1;
   __shared__ unsigned h[kMaxRanks + 1];
   for (int d = threadIdx.x; d <= R; d += blockDim.x) h[d] = 0;
@@ -83,6 +88,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
   // with 8 destinations, 4 waves' leaders hammering 9 LDS words made the pass
   // LDS-atomic bound -- SQ_WAIT_INST_LDS 50x the single-destination case)
   unsigned hc = 0;
+  MetaAcc macc;
   for (int64_t base = lo; base < hi; base += K * kRouteThreads) {
     uint32_t a[K];
     int r[K];
@@ -92,6 +98,24 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
       const int64_t i = base + k * kRouteThreads + threadIdx.x;
       // streaming column: non-temporal, so it does not evict the route directory from L2
       a[k] = i < hi ? __builtin_nontemporal_load(actor + i) : 0u;
+    }
+    if constexpr (META) {
+      int64_t v0[K], v1[K], v2[K];
+      uint32_t me[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int64_t i = base + k * kRouteThreads + threadIdx.x;
+        const bool in = i < hi;
+        v0[k] = in ? __builtin_nontemporal_load(mc.a0 + i) : 0;
+        v1[k] = in && mc.a1 ? __builtin_nontemporal_load(mc.a1 + i) : 0;
+        v2[k] = in && mc.a2 ? __builtin_nontemporal_load(mc.a2 + i) : 0;
+        me[k] = in && mc.mcol ? (uint32_t)mc.mcol[i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int64_t i = base + k * kRouteThreads + threadIdx.x;
+        if (i < hi) macc.take(a[k], v0[k], v1[k], v2[k], me[k], mc.n_dir, mc.aw);
+      }
     }
     if constexpr (MODE == 2) {
 #pragma unroll
@@ -150,6 +174,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
   __syncthreads();
   // column-major [R + 1][G]: the scan reads each destination's column contiguously
   for (int d = threadIdx.x; d <= R; d += blockDim.x) hist[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
+  if constexpr (META) meta_publish(macc, mc.mcol != nullptr, mc.method_uniform, M, mc.meta);
 }
 
 // Slot headers + overflow / no-actor statistics from the column totals (block-level;
@@ -569,11 +594,17 @@ void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a
 
 template <int K, int MODE>
 static void launch_prep(dim3 g, hipStream_t s, uintptr_t actor, int64_t M, int64_t P, uintptr_t table, uint64_t cap,
-                        uintptr_t dir, uint32_t n_dir, int R, uintptr_t route, uintptr_t hist, uint32_t aw = 0) {
+                        uintptr_t dir, uint32_t n_dir, int R, uintptr_t route, uintptr_t hist, uint32_t aw = 0,
+                        const MetaCols* mc = nullptr) {
   const int aw_shift = (aw && (aw & (aw - 1)) == 0) ? __builtin_ctz(aw) : -1;
-  hipLaunchKernelGGL((route_prep_kernel<K, MODE>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
-                     (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
-                     (uint32_t*)route, (uint32_t*)hist);
+  if (mc)
+    hipLaunchKernelGGL((route_prep_kernel<K, MODE, true>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
+                       (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
+                       (uint32_t*)route, (uint32_t*)hist, *mc);
+  else
+    hipLaunchKernelGGL((route_prep_kernel<K, MODE>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
+                       (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
+                       (uint32_t*)route, (uint32_t*)hist, MetaCols{});
 }
 
 // Region sizes of wire format v2 (u32 words; see the header comment).
@@ -654,7 +685,8 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
 // block histograms.  Independent of the wire layout, so the v3 engine runs it
 // while the host waits for the layout agreement.  Returns G; *P_out = P.
 int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
-                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out) {
+                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out,
+                   const MetaCols* mc) {
   int64_t P;
   const int64_t G = route_grid(M, &P);
   *P_out = P;
@@ -663,17 +695,17 @@ int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, ui
     const dim3 g((unsigned)G);
     const int k = g_prep_items;
     if (affine_w && n_dir) {
-      launch_prep<4, 2>(g, s, actor, M, P, table, cap, 0, n_dir, R, route, hist, affine_w);
+      launch_prep<4, 2>(g, s, actor, M, P, table, cap, 0, n_dir, R, route, hist, affine_w, mc);
     } else if (dir && n_dir) {
       // measured (tools/route_bench.py): 1/2/4 items within 2% of each other
-      if (k == 1) launch_prep<1, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
-      else if (k == 4) launch_prep<4, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
-      else launch_prep<2, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist);
+      if (k == 1) launch_prep<1, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc);
+      else if (k == 4) launch_prep<4, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc);
+      else launch_prep<2, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc);
     } else {
       // probe path: 2 lookups in flight per thread is best; 4 costs occupancy (98 VGPRs)
-      if (k == 1) launch_prep<1, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
-      else if (k == 4) launch_prep<4, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
-      else launch_prep<2, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist);
+      if (k == 1) launch_prep<1, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc);
+      else if (k == 4) launch_prep<4, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc);
+      else launch_prep<2, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc);
     }
   } else {
     PT_HIP_CHECK(hipMemsetAsync((void*)hist, 0, sizeof(uint32_t) * (R + 1) * G, s));
@@ -701,7 +733,7 @@ int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_
                         uint32_t n_dir, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t route,
                         uintptr_t hist, uintptr_t stats, int rank_self, uint32_t affine_w, uintptr_t stream,
                         int64_t* P_out) {
-  const int64_t G = route_prep(actor, M, table, cap, dir, n_dir, R, route, hist, affine_w, stream, P_out);
+  const int64_t G = route_prep(actor, M, table, cap, dir, n_dir, R, route, hist, affine_w, stream, P_out, nullptr);
   route_scan(G, R, C, req_words, sendbuf, hist, method_uniform, stats, rank_self, stream);
   return G;
 }

@@ -242,8 +242,9 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<FakeComm, std::shared_ptr<FakeComm>>(m, "FakeComm",
                                                   "in-process R-rank all-to-all for multi-rank engine tests "
                                                   "(one host thread + stream per rank on one GPU)")
-      .def(py::init<int>(), py::arg("R"))
-      .def_property_readonly("size", &FakeComm::size);
+      .def(py::init<int, bool, double>(), py::arg("R"), py::arg("loopback") = false, py::arg("link_gbps") = 0.0)
+      .def_property_readonly("size", &FakeComm::size)
+      .def_property_readonly("loopback", &FakeComm::loopback);
 
   py::class_<EpochEngine>(m, "EpochEngine",
                           "chunk-pipelined Send (route -> ncclAllToAll -> dispatch -> ncclAllToAll -> complete) "
@@ -276,6 +277,7 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"), py::arg("outbox_cap"),
           py::arg("direct"), py::arg("checksum"), py::arg("stream"), py::arg("packed") = false,
           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("stream_values", &EpochEngine::stream_values)
       .def("last_wire",
            [](const EpochEngine& e) {
              const auto& w = e.last_wire();

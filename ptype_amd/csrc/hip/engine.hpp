@@ -57,7 +57,8 @@ void launch_route_packed(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t 
                          uintptr_t hist, uintptr_t stats, int rank_self, const std::vector<uintptr_t>& direct,
                          uint32_t affine_w, uintptr_t stream, bool prepped = false);
 int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
-                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out);
+                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out,
+                   const MetaCols* mc = nullptr);
 void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout& L, uintptr_t reply, uintptr_t state,
                             uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
                             const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
@@ -109,9 +110,26 @@ using engine_detail::kNcclUint64;
 // completion of the own slot, reply routing -- with the all-to-all done as
 // R x R device copies ordered by events.  What RCCL adds on a real node (the
 // xGMI transport) is the only part it does not exercise.
+//
+// Loopback mode (bench/profiling only): ONE driving rank stands for every rank of
+// a symmetric R-rank node -- each rank sends the same traffic pattern, so what
+// rank q would send this rank is exactly what this rank sends q (recv = send, one
+// copy) and the all-reduce is the identity.  The rank runs the full R-rank kernel
+// pipeline with an HBM-speed interconnect: the compute side of an R-GPU step.
+// link_gbps > 0 also models the interconnect: after each loopback copy, one wave
+// holds the comm stream for the time the off-rank bytes (R - 1 peer regions)
+// would take at that per-rank egress bandwidth, so chunk-pipelining choices can
+// be compared against an xGMI-like all-to-all (compute contention from RCCL's
+// own kernels is not modelled).
+__global__ void fake_link_kernel(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
+}
+
 class FakeComm {
  public:
-  explicit FakeComm(int R) : R_(R), slots_(R) {
+  explicit FakeComm(int R, bool loopback = false, double link_gbps = 0.0)
+      : R_(R), loopback_(loopback), link_gbps_(link_gbps), slots_(R) {
     if (R < 1 || R > 64) throw std::invalid_argument("FakeComm: 1 <= R <= 64");
     for (auto& sl : slots_) {
       PT_HIP_CHECK(hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming));
@@ -125,9 +143,20 @@ class FakeComm {
     }
   }
   int size() const { return R_; }
+  bool loopback() const { return loopback_; }
 
   // recv_r[q] = send_q[r], `bytes` per peer region
   void alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) {
+    if (loopback_) {
+      PT_HIP_CHECK(hipMemcpyAsync(dst, src, bytes * R_, hipMemcpyDeviceToDevice, s));
+      if (link_gbps_ > 0) {
+        const double secs = (double)bytes * (R_ - 1) / (link_gbps_ * 1e9);
+        const uint64_t ticks = (uint64_t)std::min(secs * 1e8, 1e7);  // at most 100 ms
+        hipLaunchKernelGGL(fake_link_kernel, dim3(1), dim3(64), 0, s, ticks);
+        PT_HIP_CHECK(hipGetLastError());
+      }
+      return;
+    }
     slots_[r].src = src;
     slots_[r].dst = dst;
     PT_HIP_CHECK(hipEventRecord(slots_[r].ready, s));
@@ -145,6 +174,7 @@ class FakeComm {
 
   // element-wise max of n u64 on every rank (host-synchronous, like the engine's use)
   void allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) {
+    if (loopback_) return;  // every rank holds the same maxima
     slots_[r].host.assign(n, 0);
     PT_HIP_CHECK(hipMemcpyAsync(slots_[r].host.data(), dev, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     PT_HIP_CHECK(hipStreamSynchronize(s));
@@ -177,6 +207,8 @@ class FakeComm {
     std::vector<uint64_t> host;
   };
   int R_;
+  bool loopback_;
+  double link_gbps_;
   std::vector<Slot> slots_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -233,6 +265,14 @@ class EpochEngine {
       for (hipEvent_t* e : {&ev_route_[i], &ev_req_[i], &ev_disp_[i], &ev_rep_[i]})
         PT_HIP_CHECK(hipEventCreateWithFlags(e, ev_flags));
     PT_HIP_CHECK(hipEventCreateWithFlags(&ev_meta_out_, hipEventDisableTiming));
+    int wv = 0;
+    const char* sync = getenv("PTYPE_STREAM_SYNC");
+    if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device_) == hipSuccess && wv &&
+        !(sync && std::string(sync) == "events")) {
+      PT_HIP_CHECK(hipMalloc(&flags_dev_, sizeof(flag_seq_)));
+      PT_HIP_CHECK(hipMemset(flags_dev_, 0, sizeof(flag_seq_)));
+      use_values_ = true;
+    }
     PT_HIP_CHECK(hipMalloc(&meta_dev_, kMetaWords * sizeof(uint64_t)));
     PT_HIP_CHECK(hipHostMalloc(&meta_host_, kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
   }
@@ -244,6 +284,7 @@ class EpochEngine {
     hipStreamDestroy(comm_stream_);
     hipFree(meta_dev_);
     hipHostFree(meta_host_);
+    if (flags_dev_) hipFree(flags_dev_);
   }
 
   // Wire format of the last Send: v3 layout (S == 0: v2) and the words this rank
@@ -254,6 +295,7 @@ class EpochEngine {
     uint64_t meta[kMetaWords] = {};
   };
   const WireInfo& last_wire() const { return wire_; }
+  bool stream_values() const { return use_values_; }  // hand-offs via stream wait-value packets
 
   void set_bufs(int i, const EngineBufs& b) {
     if (i < 0 || i >= kMaxBufs) throw std::invalid_argument("EpochEngine: at most 8 buffer sets");
@@ -328,9 +370,9 @@ class EpochEngine {
       }
       route(a, i, bi, cs, local_only);
       if (collectives()) {
-        join(comm_stream_, ev_route_[bi], cs);
+        handoff(kRouted, bi, cs, comm_stream_);
         a2a(bufs_[bi].send, bufs_[bi].recv, wq);
-        record(ev_req_[bi], comm_stream_);
+        signal(kReqIn, bi, comm_stream_);
       }
       if (fwd >= 0) {
         serve(a, fwd, cs, wr);
@@ -351,31 +393,41 @@ class EpochEngine {
   void agree_layout(const EngineSend& a, hipStream_t cs) {
     if (!fake_ && !rccl().allreduce) throw std::runtime_error("EpochEngine: ncclAllReduce not found in the process");
     const uint64_t t0 = now();
+    // With a buffer set per chunk, the width pass rides in route pass 1 of every
+    // chunk (route_prep_kernel<..., META>): the batch is read once before the
+    // agreement, and every chunk's pass 1 is done by the time it returns.
+    // Otherwise a separate width pass, and pass 1 of two chunks runs ahead.
+    prepped_ = 0;
+    const bool fused = nbufs_ >= chunks_ && meta_fused_;
     {
       Timed t(prof_.kernels_ns);
-      launch_packed_meta(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.n_dir, a.affine_w,
-                         (uintptr_t)meta_dev_, (uintptr_t)cs);
+      if (fused) {
+        PT_HIP_CHECK(hipMemsetAsync(meta_dev_, 0, kMetaWords * sizeof(uint64_t), cs));
+        prep_with_meta(a, cs);
+      } else {
+        launch_packed_meta(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.n_dir, a.affine_w,
+                           (uintptr_t)meta_dev_, (uintptr_t)cs);
+      }
     }
     // on the compute stream itself: the previous Send's collectives are complete
     // there already (its completions waited for them), and no cross-stream hop
     // sits on this, the one host wait of the Send
-    prepped_ = 0;
-    if (fake_) {
+    if (fake_ && !fake_->loopback()) {
       fake_->allreduce_max(rank_, meta_dev_, kMetaWords, cs);
       PT_HIP_CHECK(hipMemcpy(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
       for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
       L_ = packed_layout(meta_host_);
-      prep_ahead(a, cs);
+      if (!fused) prep_ahead(a, cs);
       prof_.meta_ns += now() - t0;
       return;
     }
-    const int rc = rccl().allreduce(meta_dev_, meta_dev_, kMetaWords, kNcclUint64, kNcclMax, comm_, cs);
+    const int rc = fake_ ? 0 : rccl().allreduce(meta_dev_, meta_dev_, kMetaWords, kNcclUint64, kNcclMax, comm_, cs);
     if (rc != 0)
       throw std::runtime_error(std::string("ncclAllReduce failed: ") +
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
     PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost, cs));
     PT_HIP_CHECK(hipEventRecord(ev_meta_out_, cs));
-    prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
+    if (!fused) prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
     PT_HIP_CHECK(hipEventSynchronize(ev_meta_out_));
     for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
     L_ = packed_layout(meta_host_);
@@ -397,6 +449,21 @@ class EpochEngine {
                  a.affine_w, (uintptr_t)cs, &P);
     }
     prepped_ = n;
+  }
+
+  // Route pass 1 + the width pass, every chunk (one buffer set each).
+  void prep_with_meta(const EngineSend& a, hipStream_t cs) {
+    if (a.M > 0 && (!a.a0 || !a.actor)) throw std::invalid_argument("packed meta: actor and a0 columns required");
+    for (int i = 0; i < chunks_; ++i) {
+      const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
+      const MetaCols mc{(const int64_t*)off(a.a0, lo, 8), (const int64_t*)off(a.a1, lo, 8),
+                        (const int64_t*)off(a.a2, lo, 8), (const uint16_t*)off(a.method_col, lo, 2),
+                        (uint32_t)a.method_uniform, a.n_dir, a.affine_w, (unsigned long long*)meta_dev_};
+      int64_t P;
+      route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route, bufs_[i].hist,
+                 a.affine_w, (uintptr_t)cs, &P, &mc);
+    }
+    prepped_ = chunks_;
   }
 
   int64_t m_of(const EngineSend& a, int i) const {
@@ -432,7 +499,7 @@ class EpochEngine {
   void serve(const EngineSend& a, int i, hipStream_t cs, int64_t wr) {
     const int bi = i % nbufs_;
     const EngineBufs& b = bufs_[bi];
-    if (collectives()) wait(cs, ev_req_[bi]);
+    if (collectives()) await(cs, kReqIn, bi);
     const int64_t m = m_of(a, i);
     {
       Timed t(prof_.kernels_ns);
@@ -446,15 +513,15 @@ class EpochEngine {
                         (uintptr_t)cs);
     }
     if (collectives()) {
-      join(comm_stream_, ev_disp_[bi], cs);
+      handoff(kServed, bi, cs, comm_stream_);
       a2a(b.reply, b.back, wr);
-      record(ev_rep_[bi], comm_stream_);
+      signal(kRepIn, bi, comm_stream_);
     }
   }
 
   void finish(const EngineSend& a, int i, hipStream_t cs, bool local_only) {
     const int bi = i % nbufs_;
-    if (collectives()) wait(cs, ev_rep_[bi]);
+    if (collectives()) await(cs, kRepIn, bi);
     if (a.direct && local_only && !a.checksum) return;  // every reply was written by the own-slot dispatch
     Timed t(prof_.kernels_ns);
     const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M), m = m_of(a, i);
@@ -475,9 +542,44 @@ class EpochEngine {
     Timed t(prof_.sync_ns);
     PT_HIP_CHECK(hipStreamWaitEvent(s, e, 0));
   }
-  void join(hipStream_t waiter, hipEvent_t e, hipStream_t producer) {  // waiter runs after producer's work so far
-    record(e, producer);
-    wait(waiter, e);
+  // Cross-stream hand-offs, 4 per chunk: route -> request all-to-all -> dispatch
+  // -> reply all-to-all -> completion.  Default: a monotonic 64-bit sequence word
+  // per (hand-off, buffer set) written by the producer stream
+  // (hipStreamWriteValue64) and waited on by the consumer stream
+  // (hipStreamWaitValue64, a CP wait packet).  Measured on gfx950
+  // (tools/event_gap_bench.hip, profiles/r1_event_gap.jsonl): a kernel ->
+  // other-stream kernel hop costs +3.6 us this way vs +10.5 us through
+  // hipEventRecord / hipStreamWaitEvent.  The kernels on both sides carry the
+  // runtime's agent-scope kernel-boundary fences (release at the producer's end,
+  // acquire at the consumer's start), so the data the word orders is visible
+  // across XCDs; RCCL orders its own xGMI traffic.  PTYPE_STREAM_SYNC=events, a
+  // stream under graph capture, or a device without stream wait-value support use
+  // the events.
+  enum Handoff { kRouted = 0, kReqIn = 1, kServed = 2, kRepIn = 3 };
+  hipEvent_t& event_of(Handoff h, int bi) {
+    return h == kRouted ? ev_route_[bi] : h == kReqIn ? ev_req_[bi] : h == kServed ? ev_disp_[bi] : ev_rep_[bi];
+  }
+  bool values_on(hipStream_t s) const {
+    if (!use_values_) return false;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusNone;
+  }
+  void signal(Handoff h, int bi, hipStream_t producer) {
+    const int k = (int)h * kMaxBufs + bi;
+    value_mode_[k] = values_on(producer);
+    if (!value_mode_[k]) return record(event_of(h, bi), producer);
+    Timed t(prof_.sync_ns);
+    PT_HIP_CHECK(hipStreamWriteValue64(producer, flags_dev_ + k, ++flag_seq_[k], 0));
+  }
+  void await(hipStream_t waiter, Handoff h, int bi) {
+    const int k = (int)h * kMaxBufs + bi;
+    if (!value_mode_[k]) return wait(waiter, event_of(h, bi));
+    Timed t(prof_.sync_ns);
+    PT_HIP_CHECK(hipStreamWaitValue64(waiter, flags_dev_ + k, flag_seq_[k], hipStreamWaitValueGte, ~0ull));
+  }
+  void handoff(Handoff h, int bi, hipStream_t producer, hipStream_t waiter) {  // waiter runs after producer's work so far
+    signal(h, bi, producer);
+    await(waiter, h, bi);
   }
 
   void a2a(uintptr_t src, uintptr_t dst, int64_t words_per_peer) {
@@ -507,6 +609,10 @@ class EpochEngine {
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t ev_route_[kMaxBufs]{}, ev_req_[kMaxBufs]{}, ev_disp_[kMaxBufs]{}, ev_rep_[kMaxBufs]{};
   hipEvent_t ev_meta_out_{};
+  bool use_values_ = false;              // hand-offs through stream wait-value packets (see handoff)
+  uint64_t* flags_dev_ = nullptr;        // [4 hand-offs][kMaxBufs] sequence words
+  uint64_t flag_seq_[4 * kMaxBufs] = {};  // last value written per word
+  bool value_mode_[4 * kMaxBufs] = {};    // how the pending hand-off on that word was signalled
   uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)
   uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
   bool packed_ = false;
@@ -514,6 +620,11 @@ class EpochEngine {
   // world 1 without collectives: the fused local Send (batch.hip local_send_kernel);
   // PTYPE_LOCAL=0 keeps the epoch-slot pipeline there (A/B and tests)
   bool local_ = getenv("PTYPE_LOCAL") == nullptr || std::string(getenv("PTYPE_LOCAL")) != "0";
+  // v3: width pass fused into route pass 1 of every chunk (PTYPE_META_FUSED=1).
+  // Off by default: measured 1-3% slower than the separate pass + two preps run
+  // ahead (profiles/r1_multirank_ab.txt) -- the fused pass 1 holds 3 more int64
+  // columns per item, and every chunk's pass 1 lands before the first scatter.
+  bool meta_fused_ = getenv("PTYPE_META_FUSED") != nullptr && std::string(getenv("PTYPE_META_FUSED")) == "1";
   PackedLayout L_{};
   WireInfo wire_;
   HostProfile prof_;

@@ -15,7 +15,8 @@
 namespace ptype {
 
 int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
-                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out);
+                   uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out,
+                   const MetaCols* mc = nullptr);
 void route_scan(int64_t G, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t hist,
                 int method_uniform, uintptr_t stats, int rank_self, uintptr_t stream);
 int64_t route_grid(int64_t M, int64_t* P_out);
@@ -30,19 +31,7 @@ __global__ __launch_bounds__(256) void packed_meta_kernel(const uint32_t* __rest
                                                           const uint16_t* __restrict__ mcol, uint32_t method_uniform,
                                                           int64_t M, uint32_t n_dir, uint32_t aw,
                                                           unsigned long long* __restrict__ meta) {
-  uint64_t mb = 0, z0 = 0, z1 = 0, z2 = 0, mm = 0;
-  uint32_t flags = 0;
-  auto take = [&](uint32_t a, int64_t v0, int64_t v1, int64_t v2, uint32_t meth) {
-    // affine directory: the route is (a % aw, a / aw); otherwise any mailbox below kMaxMbox
-    const uint64_t m = (aw && a < n_dir) ? a / aw : (uint64_t)(kMaxMbox - 1);
-    mb = m > mb ? m : mb;
-    const uint64_t x0 = zz_enc(v0), x1 = zz_enc(v1), x2 = zz_enc(v2);
-    z0 = x0 > z0 ? x0 : z0;
-    z1 = x1 > z1 ? x1 : z1;
-    z2 = x2 > z2 ? x2 : z2;
-    mm = meth > mm ? meth : mm;
-    flags |= 1u << (meth < 7 ? meth : 7);
-  };
+  MetaAcc acc;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   // 4 elements per iteration, every load issued before any is used: the pass is
@@ -59,50 +48,11 @@ __global__ __launch_bounds__(256) void packed_meta_kernel(const uint32_t* __rest
       if (mcol) me[k] = mcol[i + k * stride];
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) take(a[k], v0[k], v1[k], v2[k], me[k]);
+    for (int k = 0; k < 4; ++k) acc.take(a[k], v0[k], v1[k], v2[k], me[k], n_dir, aw);
   }
   for (; i < M; i += stride)
-    take(actor[i], a0[i], a1 ? a1[i] : 0, a2 ? a2[i] : 0, mcol ? (uint32_t)mcol[i] : 0u);
-  if (!mcol) {  // uniform method: no column maxima (flagged once per batch below)
-    mm = 0;
-    flags = 0;
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    uint64_t t;
-    t = __shfl_xor(mb, off), mb = t > mb ? t : mb;
-    t = __shfl_xor(z0, off), z0 = t > z0 ? t : z0;
-    t = __shfl_xor(z1, off), z1 = t > z1 ? t : z1;
-    t = __shfl_xor(z2, off), z2 = t > z2 ? t : z2;
-    t = __shfl_xor(mm, off), mm = t > mm ? t : mm;
-    flags |= __shfl_xor(flags, off);
-  }
-  __shared__ uint64_t part[256 / kWave][6];
-  const int w = threadIdx.x / kWave;
-  if (lane_id() == 0) {
-    part[w][0] = mb, part[w][1] = z0, part[w][2] = z1, part[w][3] = z2, part[w][4] = mm, part[w][5] = flags;
-  }
-  __syncthreads();
-  if (threadIdx.x < 5) {  // words 0..3 = mailbox, a0..a2; thread 4 -> kMetaMethod
-    uint64_t v = 0;
-    for (int k = 0; k < 256 / kWave; ++k) v = part[k][threadIdx.x] > v ? part[k][threadIdx.x] : v;
-    if (v) atomicMax(meta + (threadIdx.x == 4 ? (int)kMetaMethod : (int)threadIdx.x), (unsigned long long)v);
-  } else if (threadIdx.x == 5) {
-    uint32_t f = 0;
-    for (int k = 0; k < 256 / kWave; ++k) f |= (uint32_t)part[k][5];
-    if (M > 0 && blockIdx.x == 0) {
-      if (mcol) {
-        atomicMax(meta + kMetaMcol, 1ull);
-      } else {
-        f |= 1u << (method_uniform < 7 ? method_uniform : 7);
-        atomicMax(meta + kMetaMethod, (unsigned long long)method_uniform);
-      }
-    }
-    while (f) {
-      const int b = __builtin_ctz(f);
-      atomicMax(meta + kMetaFlags + b, 1ull);
-      f &= f - 1;
-    }
-  }
+    acc.take(actor[i], a0[i], a1 ? a1[i] : 0, a2 ? a2[i] : 0, mcol ? (uint32_t)mcol[i] : 0u, n_dir, aw);
+  meta_publish(acc, mcol != nullptr, method_uniform, M, meta);
 }
 
 // ---- scatter: v3 record writer for scatter_tile

@@ -37,6 +37,9 @@
 #include <stdexcept>
 
 #include "records.hpp"
+#ifdef __HIPCC__
+#include "route_common.hpp"  // kMaxMbox (the width pass bounds unresolved mailboxes by it)
+#endif
 
 namespace ptype {
 
@@ -128,6 +131,89 @@ __device__ __forceinline__ void packed_pack(const PackedLayout L, const uint64_t
       else if (L.w[q] && sh < 0 && sh > -64) x |= (uint32_t)(v >> -sh);
     }
     rec[j] = x;
+  }
+}
+
+// Width-pass accumulator: column maxima of the records one thread saw.
+struct MetaAcc {
+  uint64_t mb = 0, z0 = 0, z1 = 0, z2 = 0, mm = 0;
+  uint32_t flags = 0;
+  __device__ __forceinline__ void take(uint32_t a, int64_t v0, int64_t v1, int64_t v2, uint32_t meth, uint32_t n_dir,
+                                       uint32_t aw) {
+    // affine directory: the route is (a % aw, a / aw); otherwise any mailbox below kMaxMbox
+    const uint64_t m = (aw && a < n_dir) ? a / aw : (uint64_t)(kMaxMbox - 1);
+    mb = m > mb ? m : mb;
+    const uint64_t x0 = zz_enc(v0), x1 = zz_enc(v1), x2 = zz_enc(v2);
+    z0 = x0 > z0 ? x0 : z0;
+    z1 = x1 > z1 ? x1 : z1;
+    z2 = x2 > z2 ? x2 : z2;
+    mm = meth > mm ? meth : mm;
+    flags |= 1u << (meth < 7 ? meth : 7);
+  }
+};
+
+// The width-pass columns, passed BY VALUE to route pass 1 when it also runs the
+// width pass (the v3 engine fuses them: one read of the batch instead of two).
+struct MetaCols {
+  const int64_t* a0;
+  const int64_t* a1;
+  const int64_t* a2;
+  const uint16_t* mcol;
+  uint32_t method_uniform, n_dir, aw;
+  unsigned long long* meta;
+};
+
+// Block-wide reduction of every thread's accumulator into meta[] (atomic max).
+// Every thread of the (256-thread) block must call it.  A block only issues the
+// atomic when its value beats what meta[] already holds (a relaxed read, at worst
+// stale-low, i.e. one unneeded atomic): thousands of blocks hitting the same 16
+// words with atomics serialise at L2, and on random data the maxima settle after
+// the first few blocks.
+__device__ __forceinline__ void meta_max(unsigned long long* p, uint64_t v) {
+  if (v > __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(p, (unsigned long long)v);
+}
+__device__ __forceinline__ void meta_publish(MetaAcc acc, bool has_mcol, uint32_t method_uniform, int64_t M,
+                                             unsigned long long* __restrict__ meta) {
+  if (!has_mcol) {  // uniform method: no column maxima (flagged once per batch below)
+    acc.mm = 0;
+    acc.flags = 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    uint64_t t;
+    t = __shfl_xor(acc.mb, off), acc.mb = t > acc.mb ? t : acc.mb;
+    t = __shfl_xor(acc.z0, off), acc.z0 = t > acc.z0 ? t : acc.z0;
+    t = __shfl_xor(acc.z1, off), acc.z1 = t > acc.z1 ? t : acc.z1;
+    t = __shfl_xor(acc.z2, off), acc.z2 = t > acc.z2 ? t : acc.z2;
+    t = __shfl_xor(acc.mm, off), acc.mm = t > acc.mm ? t : acc.mm;
+    acc.flags |= __shfl_xor(acc.flags, off);
+  }
+  __shared__ uint64_t part[256 / 64][6];
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) {
+    part[w][0] = acc.mb, part[w][1] = acc.z0, part[w][2] = acc.z1, part[w][3] = acc.z2, part[w][4] = acc.mm,
+    part[w][5] = acc.flags;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5) {  // words 0..3 = mailbox, a0..a2; thread 4 -> kMetaMethod
+    uint64_t v = 0;
+    for (int k = 0; k < 256 / 64; ++k) v = part[k][threadIdx.x] > v ? part[k][threadIdx.x] : v;
+    if (v) meta_max(meta + (threadIdx.x == 4 ? (int)kMetaMethod : (int)threadIdx.x), v);
+  } else if (threadIdx.x == 5) {
+    uint32_t f = 0;
+    for (int k = 0; k < 256 / 64; ++k) f |= (uint32_t)part[k][5];
+    if (M > 0 && blockIdx.x == 0) {
+      if (has_mcol) {
+        meta_max(meta + kMetaMcol, 1);
+      } else {
+        f |= 1u << (method_uniform < 7 ? method_uniform : 7);
+        meta_max(meta + kMetaMethod, method_uniform);
+      }
+    }
+    while (f) {
+      const int b = __builtin_ctz(f);
+      meta_max(meta + kMetaFlags + b, 1);
+      f &= f - 1;
+    }
   }
 }
 

@@ -103,3 +103,29 @@ def test_gpu_engine_multirank(R, packed, chunks, mixed, big):
         assert all(w["S"] == L["S"] and w["vb"] == L["vb"] for w in wires), "ranks disagree on the layout"
         if not mixed and not big:
             assert L["S"] == 2 and L["vb"] == 4, L  # 8-B requests, 4-B replies
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,chunks,sync,link", [(8, 2, "values", 0.0), (8, 4, "events", 0.0), (4, 2, "values", 400.0),
+                                                (2, 1, "values", 0.0)])
+def test_gpu_engine_loopback(R, chunks, sync, link, monkeypatch):
+    """FakeComm loopback (the bench's --loopback profiling mode): one rank runs an
+    R-rank step with recv = send; every reply must still be its handler's value,
+    with either cross-stream hand-off form and with the modelled link delay."""
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    monkeypatch.setenv("PTYPE_STREAM_SYNC", sync)
+    n, M = 4096 * R, 300_000
+    tab = RegistryTable(2 * n, device="cuda")
+    ids = torch.arange(n)
+    tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
+    tab.enable_directory(n, affine_world=R)
+    ex = ActorExchange(tab, M, chunks=chunks, state=torch.zeros(n // R, dtype=torch.int64, device="cuda"),
+                       fake=(hip().FakeComm(R, loopback=True, link_gbps=link), 0))
+    for seed in (3, 4):
+        req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=seed, device="cuda")
+        val, st = ex.send(req)
+        torch.cuda.synchronize()
+        assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1)
+    assert ex.last_wire["S"] == 2
+    assert ex._engine.stream_values == (sync == "values")
