@@ -217,6 +217,7 @@ def main():
     # process's shared-memory rings (the reference's Client.Call to another node,
     # cluster/rpc.go:59-67; here a node is a GPU of the same host)
     p50 = p50_remote = None
+    ring_on_device = None
     if use_gpu and args.rtt_calls > 0 and fake is None:
         from ptype_amd.ops import hip
 
@@ -238,6 +239,7 @@ def main():
             lat.sort()
             return lat[len(lat) // 2] * 1e6
 
+        ring_on_device = bool(srv.ring_on_device)
         try:
             p50 = timed_calls(srv.call)
             if dist_on:
@@ -276,6 +278,8 @@ def main():
             "p50_rtt_remote_us": p50_remote,
             "rtt_path": "host -> GPU actor via the persistent dispatcher's rings (remote: the next rank's "
                         "process, shared-memory rings on its GPU)",
+            "rtt_request_ring": None if ring_on_device is None else ("device (host writes via BAR)" if ring_on_device
+                                                                      else "pinned host"),
             "config": {
                 "model": "calculator actor (Calculator.Multiply)",
                 "global_batch": M * world,

@@ -168,7 +168,10 @@ def build_hip(verbose: bool = False) -> str:
     target = os.path.join(PKG, "_hip" + EXT)
     tl = _torch_lib_dir()
     if jobs or not os.path.exists(target) or os.path.getmtime(target) < max(os.path.getmtime(o) for o in objs):
-        link = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", target] + objs
+        # libhsa-runtime64 (soname .so.1) for hsa_amd_pointer_info: resolved through the
+        # RUNPATH to the runtime torch's HIP already loaded
+        link = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", target] + objs + [
+            "-L" + os.path.join(ROCM, "lib"), "-lhsa-runtime64"]
         if tl:
             # bind to torch's runtime first (same SONAME as /opt/rocm's)
             link += ["-Wl,-rpath," + tl]

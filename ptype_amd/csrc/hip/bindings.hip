@@ -332,6 +332,7 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("req"), py::arg("rep"), py::arg("n"), py::arg("timeout") = 30.0)
       .def("close", &DeviceServer::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("processed", &DeviceServer::processed)
+      .def_property_readonly("ring_on_device", &DeviceServer::ring_on_device)
       .def_property_readonly("launches", &DeviceServer::launches)
       .def_property_readonly("exits_idle", &DeviceServer::exits_idle)
       .def_property_readonly("exits_lifetime", &DeviceServer::exits_lifetime)

@@ -4,11 +4,14 @@
 // Reference: each net/rpc call is one TCP round trip into a goroutine that runs
 // the handler (cluster/rpc.go:59-67 -> stdlib net/rpc server, registered at
 // example/calculator/server/server.go:16-20).  Here the host publishes a 64-B
-// request slot into a ring in fine-grained (coherent) host memory; ONE resident
+// request slot into a ring; ONE resident
 // wave polls the ring with relaxed system-scope loads + s_sleep, runs up to 64
 // consecutive requests per poll (one per lane) through the same compiled-in
-// handler table as the batch path, and writes 32-B reply slots back with
-// system-scope stores + a release before each tag.  No kernel launch per call.
+// handler table as the batch path, and writes reply slots back as single 16-B
+// system-scope stores.  No kernel launch per call.  In-process, the request
+// ring is fine-grained DEVICE memory the host writes through its BAR mapping
+// (polls and payload reads stay on the GPU: p50 RTT 4.0-4.5 -> 3.1 us,
+// profiles/r1_ring_placement_ab.txt); the cross-process ring is host shm.
 //
 // Liveness: the kernel exits when the host sets `stop`, when it has been idle
 // for `idle_ticks`, or after `max_ticks` (a hard bound so nothing can hang the
@@ -28,11 +31,68 @@
 #include <thread>
 #include <vector>
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <immintrin.h>
+
 #include "common.hpp"
 #include "handlers.hpp"
 #include "shmring.hpp"
 
 namespace ptype {
+
+// Whether the host CPU can read and write `p` directly (device memory mapped
+// through the BAR): the pointer's accessible agents include a CPU agent.  The
+// module links libhsa-runtime64.so.1, which resolves (RUNPATH, same soname) to
+// the HSA runtime torch's HIP already loaded -- one runtime in the process.
+inline bool cpu_can_access(const void* p);
+
+inline hsa_status_t find_cpu_agent(hsa_agent_t a, void* out) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t*>(out) = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// Open device allocation `p` to the host CPU (large-BAR mapping) and confirm it.
+inline bool open_to_cpu(const void* p) {
+  hsa_agent_t cpu{};
+  hsa_iterate_agents(find_cpu_agent, &cpu);
+  if (!cpu.handle) return false;
+  const hsa_status_t st = hsa_amd_agents_allow_access(1, &cpu, nullptr, p);
+  if (st != HSA_STATUS_SUCCESS) {
+    if (getenv("PTYPE_RING_DEBUG")) fprintf(stderr, "ptype: hsa_amd_agents_allow_access -> %d\n", (int)st);
+    return false;
+  }
+  // (the pointer's accessible-agent list does not name the CPU for device
+  // memory even after this succeeds; success is the runtime's mapping promise)
+  cpu_can_access(p);  // debug report only
+  return true;
+}
+
+inline bool cpu_can_access(const void* p) {
+  const bool dbg = getenv("PTYPE_RING_DEBUG") != nullptr;
+  hsa_amd_pointer_info_t info{};
+  info.size = sizeof(info);
+  uint32_t n = 0;
+  hsa_agent_t* agents = nullptr;
+  const hsa_status_t st = hsa_amd_pointer_info(p, &info, malloc, &n, &agents);
+  if (st != HSA_STATUS_SUCCESS) {
+    if (dbg) fprintf(stderr, "ptype: hsa_amd_pointer_info -> %d\n", (int)st);
+    return false;
+  }
+  bool cpu = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(agents[i], HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU)
+      cpu = true;
+  }
+  free(agents);
+  if (dbg) fprintf(stderr, "ptype: ring %p type %d, %u accessible agents, cpu %d\n", p, (int)info.type, n, (int)cpu);
+  return cpu;
+}
 
 // ServerState / ServerCtrl live in records.hpp (shared with the cross-process client).
 
@@ -189,19 +249,49 @@ class DeviceServer {
                double max_s, const std::string& shm_name = "")
       : device_(device), ring_(ring), state_((int64_t*)state), n_state_(n_state) {
     if (ring == 0 || (ring & (ring - 1))) throw std::invalid_argument("ring size must be a power of two");
+    pub_actor_.assign(ring_, 0);
+    pub_ns_.assign(ring_, 0);
     delay_ticks_ = delay_us * 100;  // s_memrealtime runs at 100 MHz
     idle_ticks_ = (uint64_t)(idle_ms * 1e5);
     max_ticks_ = (uint64_t)(max_s * 1e8);
     PT_HIP_CHECK(hipSetDevice(device_));
     if (shm_name.empty()) {
       const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
-      PT_HIP_CHECK(hipHostMalloc((void**)&req_, sizeof(RingSlot) * ring_, fl));
+      // Request ring in fine-grained DEVICE memory that the host writes through
+      // its BAR mapping: the wave's polls and payload reads stay on the GPU
+      // instead of crossing PCIe (tools/ring_latency_probe.hip: ping-pong floor
+      // 2.14 vs 2.38 us, and a call's payload read is a second round trip).
+      // Replies and the control block (host-polled; CAS hand-off) stay in host
+      // memory.  PTYPE_RING_MEM=host, or a device the CPU cannot map, keeps the
+      // ring in pinned host memory.
+      const char* rm = getenv("PTYPE_RING_MEM");
+      if (!(rm && std::string(rm) == "host")) {
+        if (hipExtMallocWithFlags((void**)&req_, sizeof(RingSlot) * ring_, hipDeviceMallocFinegrained) == hipSuccess) {
+          if (open_to_cpu(req_)) {
+            req_on_device_ = true;
+          } else {
+            PT_HIP_CHECK(hipFree(req_));
+            req_ = nullptr;
+          }
+        } else {
+          if (getenv("PTYPE_RING_DEBUG")) fprintf(stderr, "ptype: fine-grained device ring allocation failed\n");
+          (void)hipGetLastError();
+          req_ = nullptr;
+        }
+      }
+      if (req_on_device_) {
+        PT_HIP_CHECK(hipMemset(req_, 0, sizeof(RingSlot) * ring_));
+        PT_HIP_CHECK(hipDeviceSynchronize());
+        dreq_ = req_;
+      } else {
+        PT_HIP_CHECK(hipHostMalloc((void**)&req_, sizeof(RingSlot) * ring_, fl));
+        memset((void*)req_, 0, sizeof(RingSlot) * ring_);
+        PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dreq_, req_, 0));
+      }
       PT_HIP_CHECK(hipHostMalloc((void**)&rep_, sizeof(ReplySlot) * ring_, fl));
       PT_HIP_CHECK(hipHostMalloc((void**)&ctrl_, sizeof(ServerCtrl), fl));
-      memset((void*)req_, 0, sizeof(RingSlot) * ring_);
       memset((void*)rep_, 0, sizeof(ReplySlot) * ring_);
       memset((void*)ctrl_, 0, sizeof(ServerCtrl));
-      PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dreq_, req_, 0));
       PT_HIP_CHECK(hipHostGetDevicePointer((void**)&drep_, rep_, 0));
       PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dctrl_, ctrl_, 0));
       owner_mem_.reset(new std::atomic<uint64_t>[ring_]);
@@ -242,6 +332,8 @@ class DeviceServer {
     }
   }
 
+  bool ring_on_device() const { return req_on_device_; }  // request ring in device memory (host writes via BAR)
+
   void close() {
     if (closed_.exchange(true)) return;
     if (hdr_) {
@@ -257,7 +349,8 @@ class DeviceServer {
       if (registered_) hipHostUnregister(seg_->base());
       seg_.reset();  // unmaps + unlinks the segment
     } else {
-      hipHostFree(req_);
+      if (req_on_device_) hipFree(req_);
+      else hipHostFree(req_);
       hipHostFree(rep_);
       hipHostFree(ctrl_);
     }
@@ -369,10 +462,17 @@ class DeviceServer {
     for (unsigned spins = 0; owner_[idx].load(std::memory_order_acquire) != seq; ++spins)
       if (spins > 64) std::this_thread::yield();
     RingSlot* s = &req_[idx];
+    const uint64_t t = now_ns();
+    pub_actor_[idx] = m.actor;  // host-side copies: the ring may be device memory (slow to read back)
+    pub_ns_[idx] = t;
     s->msg = m;
     s->csum = ring_csum(seq, m);  // before the tag (release below)
-    s->t_pub_ns = now_ns();
+    s->t_pub_ns = t;
+    // the ring may be a write-combined BAR mapping: the payload must be out before
+    // the tag, and the tag out now rather than when the WC buffer drains
+    if (req_on_device_) _mm_sfence();
     __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
+    if (req_on_device_) _mm_sfence();
     return seq;
   }
 
@@ -396,8 +496,8 @@ class DeviceServer {
     ReplyRecord r;
     r.value = o->value;  // landed with the tag
     r.status = (int32_t)(tag & 0xff);
-    r.actor = req_[idx].msg.actor;
-    const uint64_t rtt = now_ns() - req_[idx].t_pub_ns;
+    r.actor = pub_actor_[idx];
+    const uint64_t rtt = now_ns() - pub_ns_[idx];
     owner_[idx].store(seq + ring_, std::memory_order_release);
     int b = rtt ? 63 - __builtin_clzll(rtt) : 0;
     rtt_hist_[b < kRttBuckets ? b : kRttBuckets - 1].fetch_add(1, std::memory_order_relaxed);
@@ -456,6 +556,9 @@ class DeviceServer {
     return p;
   }();
   RingSlot* req_ = nullptr;
+  bool req_on_device_ = false;     // request ring in fine-grained device memory (host writes via BAR)
+  std::vector<uint32_t> pub_actor_;  // per slot: actor / publish time of the call this process published
+  std::vector<uint64_t> pub_ns_;
   ReplySlot* rep_ = nullptr;
   ServerCtrl* ctrl_ = nullptr;
   RingSlot* dreq_ = nullptr;
