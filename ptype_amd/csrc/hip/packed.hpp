@@ -118,8 +118,21 @@ inline PackedLayout packed_layout(const uint64_t* meta) {
 // Dword j of a record from compile-time S and runtime field offsets: every
 // (dword, field) pair is a pair of selects over shifts, never an indexed
 // register array (indexed arrays are what made hipcc spill to scratch before).
+//
+// Records of up to 64 bits (S <= 2, the calculator's 50-bit record) are built
+// and read as one u64: a field is one 64-bit shift + mask, not a select chain
+// per (dword, field) -- the unpacking dispatch was VALU-bound on those chains.
 template <int S>
 __device__ __forceinline__ void packed_pack(const PackedLayout L, const uint64_t (&f)[5], uint32_t (&rec)[S]) {
+  if constexpr (S <= 2) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+      if (L.w[q]) v |= (f[q] & low_mask(L.w[q])) << L.off[q];  // off + w <= 64 here
+    rec[0] = (uint32_t)v;
+    if constexpr (S == 2) rec[1] = (uint32_t)(v >> 32);
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < S; ++j) {
     uint32_t x = 0;
@@ -219,6 +232,10 @@ __device__ __forceinline__ void meta_publish(MetaAcc acc, bool has_mcol, uint32_
 
 template <int S>
 __device__ __forceinline__ uint64_t packed_field(const PackedLayout L, int q, const uint32_t (&rec)[S]) {
+  if constexpr (S <= 2) {
+    const uint64_t r = S == 2 ? ((uint64_t)rec[S - 1] << 32 | rec[0]) : (uint64_t)rec[0];
+    return L.w[q] ? (r >> L.off[q]) & low_mask(L.w[q]) : 0ull;
+  }
   uint64_t v = 0;
 #pragma unroll
   for (int j = 0; j < S; ++j) {

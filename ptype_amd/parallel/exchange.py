@@ -134,8 +134,14 @@ class ActorExchange:
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
         self.outbox = None  # DeviceOutbox that dispatched handlers send into (set by pump)
         # direct completion of self-directed messages (no reply staging, no
-        # completion pass for them; at world 1 no completion kernel at all)
-        self.direct = True
+        # completion pass for them; at world 1 no completion kernel at all).
+        # Default on at world 1 only: with more ranks the completion pass runs
+        # anyway, and the own slot's replies written from the dispatcher land
+        # scattered (message index through the inverse index, ~R messages apart)
+        # -- the completion's gather writes them coalesced instead (bench
+        # --loopback 8: 0.360 -> 0.337 ms/step).  PTYPE_DIRECT=0/1 overrides.
+        d = os.environ.get("PTYPE_DIRECT")
+        self.direct = (d != "0") if d is not None else (self.world == 1)
         self.counters = EpochStats()
         self._engine = None  # native epoch engine, built on first GPU send
         self.use_engine = self.device.type == "cuda" and os.environ.get("PTYPE_ENGINE", "1") != "0"
