@@ -554,7 +554,10 @@ class EpochEngine {
   // acquire at the consumer's start), so the data the word orders is visible
   // across XCDs; RCCL orders its own xGMI traffic.  PTYPE_STREAM_SYNC=events, a
   // stream under graph capture, or a device without stream wait-value support use
-  // the events.
+  // the events (and so do rocprofv3 --pmc passes: there the wait-value hand-offs
+  // were observed to hang).  Deadlock-free when streams share a hardware queue:
+  // every await is enqueued after its signal in host order and queues are FIFO,
+  // so a wait only ever depends on packets enqueued before it.
   enum Handoff { kRouted = 0, kReqIn = 1, kServed = 2, kRepIn = 3 };
   hipEvent_t& event_of(Handoff h, int bi) {
     return h == kRouted ? ev_route_[bi] : h == kReqIn ? ev_req_[bi] : h == kServed ? ev_disp_[bi] : ev_rep_[bi];

@@ -1,7 +1,7 @@
 #!/bin/bash
 # DRAM bytes per kernel on the RCCL path (--force-dist, wire v3), one counter per pass.
-# Event hand-offs: counter collection serialises kernels, and a stream wait-value hand-off
-# between the compute and comm streams cannot complete under serialisation.
+# Event hand-offs: with the default stream wait-value hand-offs a --pmc pass hung silently
+# (observed); with PTYPE_STREAM_SYNC=events it completes in seconds.
 # usage (under gpurun): bash tools/gpu_pmc_dist.sh TAG
 set -o pipefail
 TAG=${1:-pmcd}

@@ -17,10 +17,10 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/pmc_${TAG}_$C -o pmc --output-format csv -- python bench.py --steps 3 --warmup 1 --rtt-calls 0 --graph off > gpurun_out/pmc_${TAG}_$C.log 2>&1 || { echo "PMC $C FAILED"; tail -5 gpurun_out/pmc_${TAG}_$C.log; exit 1; }
 done
 python tools/pmc_summary.py gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE | tee gpurun_out/pmc_${TAG}_summary.txt
-# the RCCL path (wire v3) with collectives forced on at world 1.  Counter collection
-# serialises kernels, and a stream wait-value hand-off (a kernel on one stream waits for a
-# word a kernel on the other stream writes) then never completes: the pass hung silently
-# with the default hand-offs.  Counter passes use event hand-offs (PTYPE_STREAM_SYNC=events).
+# the RCCL path (wire v3) with collectives forced on at world 1.  Under --pmc counter
+# collection the default stream wait-value hand-offs hung silently (observed on the box;
+# plain --kernel-trace runs are fine); with event hand-offs (PTYPE_STREAM_SYNC=events) the
+# pass completes in seconds, so counter passes use events.
 for C in FETCH_SIZE WRITE_SIZE; do
   PTYPE_STREAM_SYNC=events timeout -k 10 150 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/pmcd_${TAG}_$C -o pmc --output-format csv -- python bench.py --force-dist --steps 3 --warmup 1 --rtt-calls 0 > gpurun_out/pmcd_${TAG}_$C.log 2>&1 || { echo "PMC dist $C FAILED"; tail -5 gpurun_out/pmcd_${TAG}_$C.log; exit 1; }
 done
