@@ -17,7 +17,17 @@ p50 RTT: single synchronous ``Call``s to a GPU actor through the persistent
 dispatcher (host-visible ring, no launch per call), measured after the timed
 loop on every rank's own GPU.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]   (N>1 under torchrun)
+Placement: actors are spread over the ranks and their mailboxes by a random
+permutation (``--placement random``, the default), so every message's route is
+read from the GPU registry mirror (the compiled route directory; ``--lookup hash``
+probes the hash table instead).  ``--placement affine`` (actor a on rank a % N,
+mailbox a / N) lets the route be computed without registry reads; it is reported
+as a secondary figure, never as the headline.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+  N > 1 without torchrun: bench.py starts torch.distributed.run with N rank
+  processes itself (a child process, before anything touches a GPU) and exits
+  with its status.
 """
 from __future__ import annotations
 
@@ -48,7 +58,45 @@ def _parse():
     p.add_argument("--force-dist", action="store_true",
                    help="initialise the process group and run the all-to-alls even for one rank "
                         "(exercises the RCCL path on a 1-GPU box)")
+    p.add_argument("--placement", choices=["random", "affine"], default="random",
+                   help="actor -> (rank, mailbox) placement: a random permutation (routes read the registry) "
+                        "or the strided rule (routes computed)")
+    p.add_argument("--lookup", choices=["directory", "hash"], default="directory",
+                   help="registry mirror read on the route: compiled route directory or hash-table probe")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip the secondary (affine placement) measurement after the headline")
     return p.parse_args()
+
+
+def _spawn_ranks(args) -> int:
+    """`--gpus N` outside torchrun: run this script under torch.distributed.run with
+    N local rank processes (127.0.0.1 rendezvous) as a child; return its status.
+    Runs before anything initialises a GPU in this process (no exec)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def place_actors(n_actors: int, world: int, placement: str, seed: int = 1234):
+    """(rank, mailbox) of every actor id: the same on every rank (CPU generator).
+    random: a uniformly random bijection onto rank-major mailbox slots, so each
+    rank hosts exactly n_actors / world mailboxes."""
+    import torch
+
+    ids = torch.arange(n_actors, dtype=torch.int64)
+    if placement == "affine":
+        slot = ids
+    else:
+        slot = torch.randperm(n_actors, generator=torch.Generator().manual_seed(seed))
+    return (slot % world).to(torch.int32), (slot // world).to(torch.int32)
 
 
 def wire_info(ex, req) -> dict:
@@ -65,6 +113,8 @@ def wire_info(ex, req) -> dict:
 
 def main():
     args = _parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_spawn_ranks(args))
     import torch
     import torch.distributed as dist
 
@@ -77,9 +127,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"--gpus {args.gpus} needs torchrun with {args.gpus} processes", file=sys.stderr)
-            sys.exit(2)
+        print(f"--gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     use_gpu = not args.cpu
     if use_gpu:
         torch.cuda.set_device(local)
@@ -119,38 +168,23 @@ def main():
     # and on the forced single-rank RCCL path (0.31 vs 0.38-0.40 ms at 4 chunks)
     chunks = args.chunks or (2 if dist_on or fake else 1)
 
-    # GPU registry mirror: actor a lives on rank a % world in mailbox a // world
-    table = RegistryTable(2 * n_actors, device=device)
-    ids = torch.arange(n_actors, dtype=torch.int64)
-    table.upsert(actor_keys(ids), (ids % geo).to(torch.int32), (ids // geo).to(torch.int32))
-    table.enable_directory(n_actors, affine_world=geo)  # K5b directory + verified strided placement (no gathers)
+    def build_table(placement):
+        # GPU registry mirror: every actor of the node -> (rank, mailbox)
+        t = RegistryTable(2 * n_actors, device=device)
+        ids = torch.arange(n_actors, dtype=torch.int64)
+        r, mb = place_actors(n_actors, geo, placement)
+        t.upsert(actor_keys(ids), r, mb)
+        if args.lookup == "directory":
+            # K5b route directory; the device verifies the strided rule (affine placement only)
+            t.enable_directory(n_actors, affine_world=geo)
+        return t
+
     state = torch.zeros(args.actors_per_gpu, dtype=torch.int64, device=device)
-    ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake)
     req = B.MsgBatch(torch.empty(M, dtype=torch.int32, device=device), torch.empty(M, dtype=torch.int64, device=device),
                      torch.empty(M, dtype=torch.int64, device=device), None, METHOD_CALC_MULTIPLY)
     val = torch.empty(M, dtype=torch.int64, device=device)
     st = torch.empty(M, dtype=torch.int32, device=device)
-
     use_graph = use_gpu and (args.graph == "on" or (args.graph == "auto" and not dist_on and fake is None))
-    graph = None
-    if use_graph:
-        # the whole step (new requests + Send) as one hipGraph; the generator reads its
-        # seed from device memory and the graph advances it, so every replay is a new batch
-        seed_t = torch.tensor([rank * 0x9E3779B9 + 7], dtype=torch.int64, device=device)
-
-        def prologue():
-            B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, device=device, out=req, seed_tensor=seed_t)
-            seed_t.add_(0x1000193)
-
-        graph = ex.capture(req, val, st, prologue=prologue, allow_collectives=args.graph == "on")
-
-    def step(s):
-        if graph is not None:
-            graph.replay()
-            return
-        B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=(s * world + rank) * 0x1000193 + 7, device=device,
-                       out=req)
-        ex.send(req, val, st)
 
     def verify(tag):
         ok = bool((st == STATUS_OK).all()) and bool(torch.equal(val, req.a0 * req.a1))
@@ -158,26 +192,69 @@ def main():
             bad = int((st != STATUS_OK).sum())
             raise SystemExit(f"[rank {rank}] {tag}: verification failed ({bad} non-OK replies)")
 
-    for s in range(args.warmup):
-        step(s)
-    sync()
-    if args.warmup:
-        verify("warmup")
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(args.warmup + s)
-    sync()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist_on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    if args.steps:
-        verify("timed")
+    def measure(table, steps, warmup):
+        """Warm up, then time `steps` Sends (barrier + synchronize on both sides,
+        max over ranks); returns (seconds, exchange, graph used)."""
+        ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake)
+        graph = None
+        if use_graph:
+            # the whole step (new requests + Send) as one hipGraph; the generator reads its
+            # seed from device memory and the graph advances it, so every replay is a new batch
+            seed_t = torch.tensor([rank * 0x9E3779B9 + 7], dtype=torch.int64, device=device)
+
+            def prologue():
+                B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, device=device, out=req, seed_tensor=seed_t)
+                seed_t.add_(0x1000193)
+
+            graph = ex.capture(req, val, st, prologue=prologue, allow_collectives=args.graph == "on")
+
+        def step(s):
+            if graph is not None:
+                graph.replay()
+                return
+            B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=(s * world + rank) * 0x1000193 + 7, device=device,
+                           out=req)
+            ex.send(req, val, st)
+
+        for s in range(warmup):
+            step(s)
+        sync()
+        if warmup:
+            verify("warmup")
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        for s in range(steps):
+            step(warmup + s)
+        sync()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if dist_on:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        if steps:
+            verify("timed")
+        return elapsed, ex, graph is not None
+
+    table = build_table(args.placement)
+    elapsed, ex, graphed = measure(table, args.steps, args.warmup)
+    def lookup_mode(t):
+        if t.dir is None:
+            return "hash-table probe"
+        t.directory()
+        return "computed (verified strided rule)" if t.affine else "route directory gather"
+
+    route_mode = lookup_mode(table)
+    secondary = None
+    if args.placement != "affine" and not args.no_secondary and args.steps:
+        # secondary figure only: the same step with the strided placement, whose routes
+        # need no registry reads (what round 1 reported as its headline)
+        t2 = build_table("affine")
+        e2, _, _ = measure(t2, args.steps, max(1, args.warmup))
+        secondary = {"placement": "affine", "registry_lookup": lookup_mode(t2),
+                     "value": M * world * args.steps / e2 if e2 > 0 else 0.0,
+                     "ms_per_step": e2 / args.steps * 1e3}
 
     # diagnostics, outside the timed region: the step's all-to-all byte volume moved
     # by RCCL alone (same chunking, same per-peer sizes), so a multi-GPU line says
@@ -284,13 +361,17 @@ def main():
                 "model": "calculator actor (Calculator.Multiply)",
                 "global_batch": M * world,
                 "seq_len": None,
-                "parallelism": f"actors sharded over {world} GPU(s)" + (", RCCL all-to-all epochs" if dist_on else ""),
+                "parallelism": f"actors sharded over {world} GPU(s)" + ((", RCCL all-to-all epochs" if use_gpu
+                                                                           else ", gloo all-to-all epochs (CPU)")
+                                                                          if dist_on else ""),
                 "msgs_per_gpu_per_step": M,
                 "actors": n_actors,
                 "chunks": chunks,
                 **wire_info(ex, req),
                 "client_batch": "SoA (actor u32, A i64, B i64)",
-                "hip_graph": graph is not None,
+                "hip_graph": graphed,
+                "placement": args.placement,
+                "registry_lookup": route_mode,
                 **({"loopback_ranks": args.loopback, "link_gbps": args.link_gbps, "note": "profiling mode: rank 0 of a symmetric "
                     f"{args.loopback}-rank node, all-to-alls as local copies (not a headline number)"}
                    if fake else {}),
@@ -298,6 +379,8 @@ def main():
         }
         if diag is not None:
             out["diag"] = diag
+        if secondary is not None:
+            out["secondary"] = secondary
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()

@@ -265,10 +265,11 @@ class EpochEngine {
       for (hipEvent_t* e : {&ev_route_[i], &ev_req_[i], &ev_disp_[i], &ev_rep_[i]})
         PT_HIP_CHECK(hipEventCreateWithFlags(e, ev_flags));
     PT_HIP_CHECK(hipEventCreateWithFlags(&ev_meta_out_, hipEventDisableTiming));
+    // Cross-stream hand-offs use events unless PTYPE_STREAM_SYNC=values (see handoff()).
     int wv = 0;
     const char* sync = getenv("PTYPE_STREAM_SYNC");
-    if (hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device_) == hipSuccess && wv &&
-        !(sync && std::string(sync) == "events")) {
+    if (sync && std::string(sync) == "values" &&
+        hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device_) == hipSuccess && wv) {
       PT_HIP_CHECK(hipMalloc(&flags_dev_, sizeof(flag_seq_)));
       PT_HIP_CHECK(hipMemset(flags_dev_, 0, sizeof(flag_seq_)));
       use_values_ = true;
@@ -543,21 +544,31 @@ class EpochEngine {
     PT_HIP_CHECK(hipStreamWaitEvent(s, e, 0));
   }
   // Cross-stream hand-offs, 4 per chunk: route -> request all-to-all -> dispatch
-  // -> reply all-to-all -> completion.  Default: a monotonic 64-bit sequence word
-  // per (hand-off, buffer set) written by the producer stream
-  // (hipStreamWriteValue64) and waited on by the consumer stream
-  // (hipStreamWaitValue64, a CP wait packet).  Measured on gfx950
-  // (tools/event_gap_bench.hip, profiles/r1_event_gap.jsonl): a kernel ->
-  // other-stream kernel hop costs +3.6 us this way vs +10.5 us through
-  // hipEventRecord / hipStreamWaitEvent.  The kernels on both sides carry the
-  // runtime's agent-scope kernel-boundary fences (release at the producer's end,
-  // acquire at the consumer's start), so the data the word orders is visible
-  // across XCDs; RCCL orders its own xGMI traffic.  PTYPE_STREAM_SYNC=events, a
-  // stream under graph capture, or a device without stream wait-value support use
-  // the events (and so do rocprofv3 --pmc passes: there the wait-value hand-offs
-  // were observed to hang).  Deadlock-free when streams share a hardware queue:
-  // every await is enqueued after its signal in host order and queues are FIFO,
-  // so a wait only ever depends on packets enqueued before it.
+  // -> reply all-to-all -> completion.
+  //
+  // Default: hipEventRecord on the producer stream + hipStreamWaitEvent on the
+  // consumer (barrier-AND packets on HSA completion signals).
+  //
+  // Opt-in (PTYPE_STREAM_SYNC=values): a monotonic 64-bit sequence word per
+  // (hand-off, buffer set) written by the producer stream (hipStreamWriteValue64)
+  // and waited on by the consumer stream (hipStreamWaitValue64, a CP wait-value
+  // packet).  Measured on gfx950 (tools/event_gap_bench.hip,
+  // profiles/r1_event_gap.jsonl) a kernel -> other-stream kernel hop costs +3.6 us
+  // this way vs +10.5 us with events, i.e. ~7 us per hop on a ~0.3 ms step.
+  //
+  // Why events are the default: a rocprofv3 --pmc pass over the RCCL path hung
+  // with the wait-value hand-offs and completed with events.  A wait-value packet
+  // blocks its hardware queue on a memory word that the runtime and tools know
+  // nothing about; anything that serialises or re-orders dispatches across queues
+  // (counter collection serialises kernels device-wide, and at N > 1 RCCL's and
+  // torch's streams share the process's 4 hardware queues with ours) can hold the
+  // producer's write-value packet behind the blocked waiter.  Host enqueue order
+  // (every await enqueued after its signal) is NOT enough when two streams map to
+  // one hardware queue in a different order than the host issued them, or when a
+  // tool's queue interception releases packets one dispatch at a time.  Events
+  // carry HSA signals that the runtime and profilers track, so they cannot
+  // deadlock that way.  The gain of wait-value packets (~7 us per hop) is not
+  // worth a hang at N = 8.
   enum Handoff { kRouted = 0, kReqIn = 1, kServed = 2, kRepIn = 3 };
   hipEvent_t& event_of(Handoff h, int bi) {
     return h == kRouted ? ev_route_[bi] : h == kReqIn ? ev_req_[bi] : h == kServed ? ev_disp_[bi] : ev_rep_[bi];

@@ -406,16 +406,21 @@ class SendGraph:
             ex.send(req, out_val, out_status)
 
         ex.table.directory()  # build outside the capture if dirty
-        ex._capturing = True  # fixed-geometry v2 slots inside the graph (no host wait)
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(2):  # warm allocations / lazy state outside the graph
+        # fixed-geometry v2 slots inside the graph (no host wait); the flag covers
+        # only the warm-up and the capture, so eager sends afterwards keep wire v3
+        prev, ex._capturing = ex._capturing, True
+        try:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):  # warm allocations / lazy state outside the graph
+                    body()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
                 body()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            body()
+        finally:
+            ex._capturing = prev
         self.replays = 0
 
     def replay(self) -> None:

@@ -17,9 +17,11 @@ REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
             "vs_baseline", "dtype", "data", "config", "p50_rtt_us"}
 
 
-def _run(nproc, extra, timeout=600):
+def _run(nproc, extra, timeout=600, launcher="torchrun"):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    if nproc == 1:
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    if nproc == 1 or launcher == "self":  # bench.py starts torch.distributed.run itself for N > 1
         cmd = [sys.executable, "bench.py"]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
@@ -35,14 +37,17 @@ def _run(nproc, extra, timeout=600):
 SMALL = ["--steps", "2", "--warmup", "1", "--msgs-per-gpu", "20000", "--actors-per-gpu", "1024", "--rtt-calls", "0"]
 
 
-@pytest.mark.parametrize("nproc", [1, 2])
-def test_bench_json_contract_cpu(nproc):
-    out = _run(nproc, ["--cpu"] + SMALL)
+@pytest.mark.parametrize("nproc,launcher", [(1, "self"), (2, "torchrun"), (2, "self")])
+def test_bench_json_contract_cpu(nproc, launcher):
+    out = _run(nproc, ["--cpu"] + SMALL, launcher=launcher)
     assert REQUIRED <= set(out)
     assert out["metric"] == "messages/sec" and out["unit"] == "msg/s" and out["higher_is_better"] is True
     assert out["n_gpus"] == nproc and out["steps"] == 2 and out["warmup"] == 1 and out["scaling"] == "weak"
     assert out["data"] == "synthetic"
     assert out["config"]["global_batch"] == 20000 * nproc
+    # headline placement reads the registry mirror; the strided figure is secondary only
+    assert out["config"]["placement"] == "random" and out["config"]["registry_lookup"] != "computed (verified strided rule)"
+    assert out["secondary"]["placement"] == "affine"
     # value is the whole-job aggregate: every rank's messages over the max rank time
     assert out["value"] == pytest.approx(20000 * nproc * 2 / (out["ms_per_step"] * 2 / 1e3), rel=1e-6)
 
