@@ -63,6 +63,9 @@ def _parse():
                         "or the strided rule (routes computed)")
     p.add_argument("--lookup", choices=["directory", "hash"], default="directory",
                    help="registry mirror read on the route: compiled route directory or hash-table probe")
+    p.add_argument("--delivery", choices=["direct", "mailbox"], default="direct",
+                   help="how a message reaches its actor on its GPU: one fused pass, or through the HBM "
+                        "mailboxes (K2 enqueue + K3 drain; world 1)")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary (affine placement) measurement after the headline")
     return p.parse_args()
@@ -192,10 +195,10 @@ def main():
             bad = int((st != STATUS_OK).sum())
             raise SystemExit(f"[rank {rank}] {tag}: verification failed ({bad} non-OK replies)")
 
-    def measure(table, steps, warmup):
+    def measure(table, steps, warmup, delivery=args.delivery):
         """Warm up, then time `steps` Sends (barrier + synchronize on both sides,
         max over ranks); returns (seconds, exchange, graph used)."""
-        ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake)
+        ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake, delivery=delivery)
         graph = None
         if use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
@@ -255,6 +258,19 @@ def main():
         secondary = {"placement": "affine", "registry_lookup": lookup_mode(t2),
                      "value": M * world * args.steps / e2 if e2 > 0 else 0.0,
                      "ms_per_step": e2 / args.steps * 1e3}
+
+    mailbox = None
+    if world == 1 and not dist_on and fake is None and not args.no_secondary and args.steps:
+        # the same step through the HBM mailboxes (K2 enqueue + K3 drain) or, when the
+        # headline already used them, through the fused direct pass
+        other = "direct" if args.delivery == "mailbox" else "mailbox"
+        e3, ex3, _ = measure(table, args.steps, max(1, args.warmup), delivery=other)
+        mailbox = {"delivery": other, "placement": args.placement, "value": M * args.steps / e3 if e3 > 0 else 0.0,
+                   "ms_per_step": e3 / args.steps * 1e3}
+        if ex3.mailboxes is not None:
+            mailbox.update(shards=ex3.mailboxes.shards, slots=ex3.mailboxes.slots,
+                           ring_bytes=ex3.mailboxes.bytes)
+            del ex3
 
     # diagnostics, outside the timed region: the step's all-to-all byte volume moved
     # by RCCL alone (same chunking, same per-peer sizes), so a multi-GPU line says
@@ -372,6 +388,7 @@ def main():
                 "hip_graph": graphed,
                 "placement": args.placement,
                 "registry_lookup": route_mode,
+                "delivery": args.delivery if world == 1 and not dist_on else "direct",
                 **({"loopback_ranks": args.loopback, "link_gbps": args.link_gbps, "note": "profiling mode: rank 0 of a symmetric "
                     f"{args.loopback}-rank node, all-to-alls as local copies (not a headline number)"}
                    if fake else {}),
@@ -381,6 +398,8 @@ def main():
             out["diag"] = diag
         if secondary is not None:
             out["secondary"] = secondary
+        if mailbox is not None:
+            out["secondary_delivery"] = mailbox
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()

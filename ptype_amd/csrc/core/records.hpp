@@ -23,13 +23,24 @@ enum MethodId : uint16_t {
   kCounterAdd = 5,          // stateful: state += a0; reply = new state
   kForward = 6,             // actor-to-actor "tell": state += 1; if a1 > 0 emit Forward to actor a0
                             // with (next = (a0 + stride) % n, a1 - 1, a2); a2 = stride | n << 32
-  kMethodCount = 7,
+  kSeqFold = 7,             // ORDERED stateful: reply = state; state = state * kFoldMul + a0 (wrapping).
+                            // Non-commutative, so the final state and the replies expose the exact
+                            // order an actor processed its messages in (mailbox FIFO audit)
+  kMethodCount = 8,
 };
+
+// Multiplier of kSeqFold (odd, so the fold is a bijection of the prior state).
+constexpr uint64_t kFoldMul = 0x100000001b3ull;
+
+// Methods whose handler is a non-commutative read-modify-write of actor state:
+// they must run one at a time per actor, in mailbox order (HBM mailboxes, K2/K3).
+inline constexpr bool method_ordered(uint32_t m) { return m == kSeqFold; }
 
 enum RecordFlags : uint16_t {
   kFlagValid = 1,
   kFlagRouted = 2,  // `actor` holds the destination's local mailbox index
   kFlagIdentity = 4,  // slot header: slot position == message index (R = 1, no gaps)
+  kFlagA2 = 8,        // mailbox record: the third argument is in the ring's a2 side array
 };
 
 enum ReplyStatus : int32_t {

@@ -432,7 +432,14 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
 // epoch slot, no histogram, no scan: 20 B in and 12 B out per calculator call.
 // MODE as route_prep; FIXED != 0: uniform method known at launch (the handler
 // switch constant-folds).
-template <int MODE, int FIXED>
+//
+// K messages per thread per tile (item-major, so every column access stays
+// coalesced), with ALL of a tile's streaming loads issued before the first
+// registry read is used: with one message per iteration the chain was
+// actor load -> directory gather -> (branch) -> argument loads, three
+// dependent memory latencies per message, and the random-placement step ran
+// the pass at 59 us vs 38 us for the gather-free affine rule (profiles/README.md).
+template <int MODE, int FIXED, int K = 4>
 __global__ __launch_bounds__(256) void local_send_kernel(
     const uint32_t* __restrict__ actor, const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
     const int64_t* __restrict__ a2, const uint16_t* __restrict__ mcol, uint32_t method_uniform, int64_t M,
@@ -441,47 +448,71 @@ __global__ __launch_bounds__(256) void local_send_kernel(
     int64_t* __restrict__ out_val, int32_t* __restrict__ out_st, unsigned long long* __restrict__ stats,
     unsigned long long* __restrict__ checksum) {
   unsigned long long nomatch = 0, failed = 0, sum = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t a = __builtin_nontemporal_load(actor + i);
-    int r;
-    uint32_t mb;
-    if constexpr (MODE == 2) {
-      if (a < n_dir) {
-        r = aw_shift >= 0 ? (int)(a & (aw - 1)) : (int)(a % aw);
-        mb = aw_shift >= 0 ? a >> aw_shift : a / aw;
-      } else {
-        lookup_entry(table, mask, actor_key(a), r, mb);
-      }
-    } else if constexpr (MODE == 1) {
-      const uint32_t w = a < n_dir ? dir[a] : kDirFallback;
-      if (w == kDirFallback) {
-        lookup_entry(table, mask, actor_key(a), r, mb);
-      } else {
-        r = w == kDirMissing ? -1 : (int)(w & 0xff);
-        mb = w >> 8;
-      }
-    } else {
-      lookup_entry(table, mask, actor_key(a), r, mb);
+  const int64_t tile = (int64_t)K * blockDim.x;
+  for (int64_t base = blockIdx.x * tile; base < M; base += (int64_t)gridDim.x * tile) {
+    uint32_t a[K];
+    int64_t x0[K], x1[K], x2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = base + k * (int64_t)blockDim.x + threadIdx.x;
+      const bool in = i < M;
+      a[k] = in ? __builtin_nontemporal_load(actor + i) : 0xffffffffu;
+      x0[k] = in ? __builtin_nontemporal_load(a0 + i) : 0;
+      x1[k] = in && a1 ? __builtin_nontemporal_load(a1 + i) : 0;
+      x2[k] = in && a2 ? __builtin_nontemporal_load(a2 + i) : 0;
     }
-    ReplyRecord rr;
-    if (r == 0 && mb < kMaxMbox) {
-      MsgRecord m;
-      m.actor = mb;
-      m.method = (uint16_t)(FIXED ? FIXED : (mcol ? (uint32_t)mcol[i] : method_uniform));
-      m.flags = kFlagValid | kFlagRouted;
-      m.a0 = __builtin_nontemporal_load(a0 + i);
-      m.a1 = a1 ? __builtin_nontemporal_load(a1 + i) : 0;
-      m.a2 = a2 ? __builtin_nontemporal_load(a2 + i) : 0;
-      rr = run_handler(m, state, n_state, delay_ticks, ob);
-      failed += rr.status != kStatusOk;
+    int r[K];
+    uint32_t mb[K];
+    if constexpr (MODE == 1) {
+      uint32_t w[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) w[k] = a[k] < n_dir ? dir[a[k]] : kDirFallback;  // K gathers in flight
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
+        mb[k] = w[k] >> 8;
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k)  // (a tail lane's id 0xffffffff resolves to nothing: no probe)
+        if (w[k] == kDirFallback && a[k] != 0xffffffffu) lookup_entry(table, mask, actor_key(a[k]), r[k], mb[k]);
     } else {
-      rr.value = 0;
-      rr.status = kStatusNoActor;
-      ++nomatch;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (MODE == 2 && a[k] < n_dir) {
+          r[k] = aw_shift >= 0 ? (int)(a[k] & (aw - 1)) : (int)(a[k] % aw);
+          mb[k] = aw_shift >= 0 ? a[k] >> aw_shift : a[k] / aw;
+        } else if (a[k] == 0xffffffffu) {
+          r[k] = -1;
+          mb[k] = 0;
+        } else {
+          lookup_entry(table, mask, actor_key(a[k]), r[k], mb[k]);
+        }
+      }
     }
-    __builtin_nontemporal_store(rr.value, out_val + i);
-    __builtin_nontemporal_store((int32_t)rr.status, out_st + i);
-    sum += (unsigned long long)rr.value;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = base + k * (int64_t)blockDim.x + threadIdx.x;
+      if (i >= M) continue;
+      ReplyRecord rr;
+      if (r[k] == 0 && mb[k] < kMaxMbox) {
+        MsgRecord m;
+        m.actor = mb[k];
+        m.method = (uint16_t)(FIXED ? FIXED : (mcol ? (uint32_t)mcol[i] : method_uniform));
+        m.flags = kFlagValid | kFlagRouted;
+        m.a0 = x0[k];
+        m.a1 = x1[k];
+        m.a2 = x2[k];
+        rr = run_handler(m, state, n_state, delay_ticks, ob);
+        failed += rr.status != kStatusOk;
+      } else {
+        rr.value = 0;
+        rr.status = kStatusNoActor;
+        ++nomatch;
+      }
+      __builtin_nontemporal_store(rr.value, out_val + i);
+      __builtin_nontemporal_store((int32_t)rr.status, out_st + i);
+      sum += (unsigned long long)rr.value;
+    }
   }
   // counters as the slot path keeps them (ws stats: 0 no-actor, 2 handler-failed),
   // one atomic per block and only when non-zero

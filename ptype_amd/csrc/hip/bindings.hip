@@ -10,6 +10,7 @@
 
 #include "common.hpp"
 #include "engine.hpp"
+#include "mailbox.hpp"
 #include "server.hpp"
 
 namespace py = pybind11;
@@ -301,6 +302,31 @@ PYBIND11_MODULE(_hip, m) {
              return d;
            })
       .def("reset_host_profile", &EpochEngine::reset_host_profile);
+  py::class_<Mailboxes>(m, "Mailboxes",
+                        "HBM actor mailboxes: S shard rings of Q 32-B tagged records (K2 enqueue, K3 epoch drain, "
+                        "K3 persistent consumer); see csrc/hip/mailbox.hpp")
+      .def(py::init<int, uint32_t, uint32_t, bool>(), py::arg("device"), py::arg("shards") = 256,
+           py::arg("slots") = 65536, py::arg("with_a2") = true)
+      .def("enqueue", &Mailboxes::enqueue, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"),
+           py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
+           py::arg("dir"), py::arg("n_dir"), py::arg("affine_w"), py::arg("rank_self"), py::arg("origin_base"),
+           py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("live"), py::arg("stream"))
+      .def("drain", &Mailboxes::drain, py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"),
+           py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("ordered"), py::arg("stream"),
+           py::arg("outbox") = std::vector<uintptr_t>{}, py::arg("outbox_cap") = 0)
+      .def("start", &Mailboxes::start, py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"),
+           py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("blocks") = 16, py::arg("idle_ms") = 0.0,
+           py::arg("max_s") = 60.0)
+      .def("stop", &Mailboxes::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("running", &Mailboxes::running)
+      .def("reset", &Mailboxes::reset, py::arg("stream"))
+      .def("stats", &Mailboxes::stats)
+      .def("shard_counters", &Mailboxes::shard_counters)
+      .def_property_readonly("shards", &Mailboxes::shards)
+      .def_property_readonly("slots", &Mailboxes::slots)
+      .def_property_readonly("bytes", &Mailboxes::bytes)
+      .def_property_readonly("consumer_processed", &Mailboxes::consumer_processed)
+      .def_property_readonly("launches", &Mailboxes::launches);
   m.def("rccl_available", [] { return rccl().alltoall != nullptr; });
 
   py::class_<DeviceServer>(m, "DeviceServer")

@@ -52,9 +52,15 @@ __device__ __forceinline__ void outbox_emit(OutboxView ob, uint32_t actor, uint1
 // receiver is exactly one machine int of actor state).  `delay_ticks` is the
 // per-candidate delay of Prime.Check in 100 MHz ticks (250 ms in the reference;
 // 0 for throughput runs).
+//
+// `exclusive`: the caller owns the actor for this call (the mailbox consumer that
+// owns its shard, runs ordered methods one at a time per actor, in mailbox order),
+// so an ordered method is a plain read-modify-write.  Elsewhere (the parallel
+// batch dispatch, the latency-path wave) an ordered method is a CAS loop: still
+// linearizable -- no update is lost -- just not in any defined order.
 __device__ __forceinline__ ReplyRecord run_handler(const MsgRecord& m, int64_t* __restrict__ state,
                                                    uint32_t n_state, uint64_t delay_ticks,
-                                                   OutboxView ob = OutboxView()) {
+                                                   OutboxView ob = OutboxView(), bool exclusive = false) {
   ReplyRecord r;
   r.value = 0;
   r.status = kStatusOk;
@@ -126,6 +132,27 @@ __device__ __forceinline__ ReplyRecord run_handler(const MsgRecord& m, int64_t* 
           } else {
             r.status = kStatusFailed;  // no outbox bound: the send cannot happen
           }
+        }
+      } else {
+        r.status = kStatusNoActor;
+      }
+      break;
+    case kSeqFold:
+      if (m.actor < n_state) {
+        unsigned long long* p = reinterpret_cast<unsigned long long*>(state + m.actor);
+        if (exclusive) {
+          const uint64_t prev = *p;
+          *p = prev * kFoldMul + (uint64_t)m.a0;
+          r.value = (int64_t)prev;
+        } else {
+          unsigned long long prev = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (;;) {
+            const unsigned long long next = prev * kFoldMul + (uint64_t)m.a0;
+            if (__hip_atomic_compare_exchange_weak(p, &prev, next, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT))
+              break;
+          }
+          r.value = (int64_t)prev;
         }
       } else {
         r.status = kStatusNoActor;

@@ -1,0 +1,676 @@
+// HBM actor mailboxes: K2 enqueue, K3 epoch drain, K3 persistent consumer.
+// Design and protocol: mailbox.hpp.
+#include <string.h>
+
+#include <vector>
+
+#include "mailbox.hpp"
+#include "route_common.hpp"
+
+namespace ptype {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Write-through (sc1) 16-B store / load: the record halves a concurrent
+// consumer on another XCD reads (MI355X_MICROARCH.md, hand-off forms: sc1
+// payload stores drained before the signal, sc1 loads on the consumer).
+__device__ __forceinline__ void st16_sc1(void* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ u32x4 ld16_sc1(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t sys_ld64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ unsigned long long* ctr_tail(const MboxView& mv, uint32_t s) {
+  return mv.ctr + (uint64_t)s * kMboxCtrStride;
+}
+__device__ __forceinline__ unsigned long long* ctr_done(const MboxView& mv, uint32_t s) {
+  return mv.ctr + (uint64_t)s * kMboxCtrStride + 1;
+}
+__device__ __forceinline__ unsigned long long* ctr_head(const MboxView& mv, uint32_t s) {
+  return mv.ctr + (uint64_t)s * kMboxCtrStride + 16;
+}
+__device__ __forceinline__ uint32_t* rec_at(const MboxView& mv, uint32_t s, uint64_t pos) {
+  const uint64_t slot = ((uint64_t)s << mv.log_q) | (pos & ((1ull << mv.log_q) - 1));
+  return mv.rec + slot * 8;
+}
+__device__ __forceinline__ uint32_t lap_tag(const MboxView& mv, uint64_t pos) {
+  return (uint32_t)(pos >> mv.log_q) + 1u;
+}
+
+__device__ __forceinline__ void block_add_stats(unsigned long long* stats, unsigned long long v0, int w0,
+                                                unsigned long long v1, int w1, unsigned long long v2, int w2) {
+  __shared__ unsigned long long part[3][4];
+  for (int off = 32; off > 0; off >>= 1) {
+    v0 += __shfl_xor(v0, off);
+    v1 += __shfl_xor(v1, off);
+    v2 += __shfl_xor(v2, off);
+  }
+  const int w = threadIdx.x / kWave;
+  if (lane_id() == 0) part[0][w] = v0, part[1][w] = v1, part[2][w] = v2;
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    unsigned long long v = 0;
+    for (int k = 0; k < (int)(blockDim.x / kWave); ++k) v += part[threadIdx.x][k];
+    const int word = threadIdx.x == 0 ? w0 : threadIdx.x == 1 ? w1 : w2;
+    if (v && word >= 0) atomicAdd(&stats[word], v);
+  }
+}
+
+// ---------------------------------------------------------------- K2 enqueue
+// One tile = K * 256 messages per block (item-major, coalesced).  LDS holds the
+// tile's per-shard counts, then each shard's reserved base and capacity limit.
+template <int MODE, bool LIVE, int K>
+__global__ __launch_bounds__(256) void mailbox_enqueue_kernel(
+    MboxView mv, const uint32_t* __restrict__ actor, const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
+    const int64_t* __restrict__ a2, const uint16_t* __restrict__ mcol, uint32_t method_uniform, int64_t M,
+    const TableEntry* __restrict__ table, uint64_t mask, const uint32_t* __restrict__ dir, uint32_t n_dir,
+    uint32_t aw, int aw_shift, int rank_self, uint32_t origin_base, ReplyView rv) {
+  extern __shared__ unsigned long long lds_mb[];
+  const uint32_t S = 1u << mv.log_s;
+  const uint64_t Q = 1ull << mv.log_q;
+  unsigned long long* base = lds_mb;      // [S]
+  unsigned long long* lim = lds_mb + S;   // [S]
+  unsigned* hist = reinterpret_cast<unsigned*>(lds_mb + 2 * S);  // [S]
+  const int64_t tile = (int64_t)K * blockDim.x;
+  unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0;
+  for (int64_t tb = blockIdx.x * tile; tb < M; tb += (int64_t)gridDim.x * tile) {
+    for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) hist[s] = 0;
+    uint32_t a[K];
+    int64_t x0[K], x1[K], x2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = tb + k * (int64_t)blockDim.x + threadIdx.x;
+      const bool in = i < M;
+      a[k] = in ? __builtin_nontemporal_load(actor + i) : 0xffffffffu;
+      x0[k] = in ? __builtin_nontemporal_load(a0 + i) : 0;
+      x1[k] = in && a1 ? __builtin_nontemporal_load(a1 + i) : 0;
+      x2[k] = in && a2 ? __builtin_nontemporal_load(a2 + i) : 0;
+    }
+    int r[K];
+    uint32_t mb[K];
+    if constexpr (MODE == 1) {
+      uint32_t w[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) w[k] = a[k] < n_dir ? dir[a[k]] : kDirFallback;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
+        mb[k] = w[k] >> 8;
+        if (w[k] == kDirFallback) {
+          if (a[k] != 0xffffffffu) lookup_entry(table, mask, actor_key(a[k]), r[k], mb[k]);
+          else r[k] = -1;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        if (MODE == 2 && a[k] < n_dir) {
+          r[k] = aw_shift >= 0 ? (int)(a[k] & (aw - 1)) : (int)(a[k] % aw);
+          mb[k] = aw_shift >= 0 ? a[k] >> aw_shift : a[k] / aw;
+        } else if (a[k] == 0xffffffffu) {
+          r[k] = -1;
+          mb[k] = 0;
+        } else {
+          lookup_entry(table, mask, actor_key(a[k]), r[k], mb[k]);
+        }
+      }
+    }
+    __syncthreads();  // hist zeroed
+    unsigned off[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const bool ok = r[k] == rank_self && mb[k] < kMaxMbox;
+      off[k] = ok ? atomicAdd(&hist[mb[k] & (S - 1)], 1u) : 0xffffffffu;
+    }
+    __syncthreads();
+    // ONE reservation per (tile, shard), and the capacity limit from the shard's head
+    for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
+      const unsigned c = hist[s];
+      if (c) {
+        base[s] = atomicAdd(ctr_tail(mv, s), (unsigned long long)c);
+        lim[s] = ld_agent(ctr_head(mv, s)) + Q;
+      }
+    }
+    __syncthreads();
+    // half B (and a2) first; with a live consumer they are drained before any tag goes out
+    uint64_t pos[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = tb + k * (int64_t)blockDim.x + threadIdx.x;
+      pos[k] = ~0ull;
+      if (i >= M) continue;
+      if (off[k] == 0xffffffffu) {
+        ++n_miss;
+        if ((uint64_t)(origin_base + i) < rv.n) {
+          rv.val[origin_base + i] = 0;
+          rv.st[origin_base + i] = kStatusNoActor;
+        }
+        continue;
+      }
+      const uint32_t s = mb[k] & (S - 1);
+      const uint64_t p = base[s] + off[k];
+      if (p >= lim[s]) {  // would overwrite an unconsumed record: a hole, answered now
+        ++n_ovf;
+        if ((uint64_t)(origin_base + i) < rv.n) {
+          rv.val[origin_base + i] = 0;
+          rv.st[origin_base + i] = kStatusOverflow;
+        }
+        continue;
+      }
+      pos[k] = p;
+      uint32_t* rc = rec_at(mv, s, p);
+      const u32x4 hb = {(uint32_t)x0[k], (uint32_t)((uint64_t)x0[k] >> 32), (uint32_t)x1[k],
+                        (uint32_t)((uint64_t)x1[k] >> 32)};
+      const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
+      if constexpr (LIVE) {
+        st16_sc1(rc + 4, hb);
+        if (a2) __hip_atomic_store(reinterpret_cast<unsigned long long*>(mv.a2 + slot), (unsigned long long)x2[k],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        *reinterpret_cast<u32x4*>(rc + 4) = hb;
+        if (a2) mv.a2[slot] = x2[k];
+      }
+    }
+    if constexpr (LIVE) vm_drain();  // every B half of this wave is out before its tags
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (pos[k] == ~0ull) continue;
+      const int64_t i = tb + k * (int64_t)blockDim.x + threadIdx.x;
+      const uint32_t s = mb[k] & (S - 1);
+      const uint32_t meth = mcol ? (uint32_t)mcol[i] : method_uniform;
+      const u32x4 ha = {lap_tag(mv, pos[k]), mb[k], (uint32_t)(origin_base + i),
+                        (meth & 0xffffu) | ((uint32_t)(kFlagValid | kFlagRouted | (a2 ? kFlagA2 : 0)) << 16)};
+      uint32_t* rc = rec_at(mv, s, pos[k]);
+      if constexpr (LIVE) st16_sc1(rc, ha);
+      else *reinterpret_cast<u32x4*>(rc) = ha;
+      ++n_enq;
+    }
+    if constexpr (LIVE) vm_drain();
+    __syncthreads();  // every wave's records are out: the tile's positions are done
+    if constexpr (LIVE) {
+      for (uint32_t s = threadIdx.x; s < S; s += blockDim.x)
+        if (hist[s]) atomicAdd(ctr_done(mv, s), (unsigned long long)hist[s]);
+    }
+    __syncthreads();  // LDS reused by the next tile
+  }
+  block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
+}
+
+// ---------------------------------------------------------------- record decode + reply
+struct MboxMsg {
+  MsgRecord m;
+  uint32_t origin;
+  bool valid;
+};
+
+__device__ __forceinline__ MboxMsg decode(const u32x4& ha, const u32x4& hb, const int64_t* a2v) {
+  MboxMsg x;
+  x.m.actor = ha.y;
+  x.origin = ha.z;
+  x.m.method = (uint16_t)(ha.w & 0xffffu);
+  x.m.flags = (uint16_t)(ha.w >> 16);
+  x.m.a0 = (int64_t)(((uint64_t)hb.y << 32) | hb.x);
+  x.m.a1 = (int64_t)(((uint64_t)hb.w << 32) | hb.z);
+  x.m.a2 = (x.m.flags & kFlagA2) && a2v ? *a2v : 0;
+  x.valid = true;
+  return x;
+}
+
+__device__ __forceinline__ void write_reply(const ReplyView& rv, uint32_t origin, const ReplyRecord& r) {
+  if ((uint64_t)origin < rv.n) {
+    rv.val[origin] = r.value;
+    rv.st[origin] = r.status;
+  }
+}
+
+// Run one window of up to 64 records (lane l holds ring position h + l) in ring
+// order per actor.  Lanes whose actor appears once in the window run together;
+// lanes of an actor that appears more than once (found through a 128-entry LDS
+// owner table per wave) run one at a time in lane order afterwards.
+__device__ __forceinline__ unsigned long long run_window_ordered(const MboxMsg& x, int64_t* __restrict__ state,
+                                                                  uint32_t n_state, uint64_t delay_ticks,
+                                                                  OutboxView ob, const ReplyView& rv,
+                                                                  volatile uint32_t* owner, volatile uint32_t* conf,
+                                                                  unsigned long long& failed, uint32_t log_s) {
+  const unsigned lane = lane_id();
+  const uint32_t h = (x.m.actor >> log_s) & 127u;
+  if (x.valid) conf[h] = 0u;
+  if (x.valid) owner[h] = lane;
+  const bool lost = x.valid && owner[h] != lane;
+  if (lost) conf[h] = 1u;
+  const bool serial = x.valid && conf[h] != 0u;
+  uint64_t ser = __ballot(serial);
+  if (x.valid && !serial) {
+    const ReplyRecord r = run_handler(x.m, state, n_state, delay_ticks, ob, true);
+    failed += r.status != kStatusOk;
+    write_reply(rv, x.origin, r);
+  }
+  const unsigned long long n_serial = (unsigned long long)__popcll(ser);
+  while (ser) {
+    vm_drain();  // the previous lane's state store has landed before the next one reads
+    const int l = __builtin_ctzll(ser);
+    if ((int)lane == l) {
+      const ReplyRecord r = run_handler(x.m, state, n_state, delay_ticks, ob, true);
+      failed += r.status != kStatusOk;
+      write_reply(rv, x.origin, r);
+    }
+    ser &= ser - 1;
+  }
+  vm_drain();  // this window's state stores land before the next window's loads
+  return n_serial;
+}
+
+// ---------------------------------------------------------------- K3 epoch drain (parallel)
+// grid (X, S): block (x, s) strides over shard s's queued positions.  Stateless
+// and commutative methods only (the host picks the ordered form otherwise).  The
+// last block to finish commits every shard's head (ticket self-resets).
+template <int FIXED, int K>
+__global__ __launch_bounds__(256) void mailbox_drain_kernel(MboxView mv, int64_t* __restrict__ state,
+                                                            uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
+                                                            ReplyView rv) {
+  const uint32_t s = blockIdx.y;
+  const uint64_t Q = 1ull << mv.log_q;
+  const uint64_t h = *ctr_head(mv, s), t = *ctr_tail(mv, s);
+  const uint64_t end = t < h + Q ? t : h + Q;
+  unsigned long long done = 0, failed = 0, holes = 0;
+  const uint64_t step = (uint64_t)gridDim.x * K * blockDim.x;
+  for (uint64_t p0 = h + (uint64_t)blockIdx.x * K * blockDim.x; p0 < end; p0 += step) {
+    u32x4 ha[K], hb[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t p = p0 + (uint64_t)k * blockDim.x + threadIdx.x;
+      if (p < end) {
+        const uint32_t* rc = rec_at(mv, s, p);
+        ha[k] = *reinterpret_cast<const u32x4*>(rc);
+        hb[k] = *reinterpret_cast<const u32x4*>(rc + 4);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t p = p0 + (uint64_t)k * blockDim.x + threadIdx.x;
+      if (p >= end) continue;
+      if (ha[k].x != lap_tag(mv, p)) {
+        ++holes;
+        continue;
+      }
+      const uint64_t slot = (uint64_t)(rec_at(mv, s, p) - mv.rec) / 8;
+      MboxMsg x = decode(ha[k], hb[k], mv.a2 ? mv.a2 + slot : nullptr);
+      if (FIXED) x.m.method = FIXED;
+      const ReplyRecord r = run_handler(x.m, state, n_state, delay_ticks, ob);
+      failed += r.status != kStatusOk;
+      write_reply(rv, x.origin, r);
+      ++done;
+    }
+  }
+  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
+  // last block out commits the heads (every block has read its shard's head by now)
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned long long total = (unsigned long long)gridDim.x * gridDim.y;
+    last = atomicAdd(&mv.stats[kMbTicket], 1ull) == total - 1;
+  }
+  __syncthreads();
+  if (last) {
+    const uint32_t S = 1u << mv.log_s;
+    for (uint32_t q = threadIdx.x; q < S; q += blockDim.x) {
+      const unsigned long long t = *ctr_tail(mv, q);
+      *ctr_head(mv, q) = t;
+      *ctr_done(mv, q) = t;  // epoch enqueues do not count `done`; the drain settles it
+    }
+    if (threadIdx.x == 0) mv.stats[kMbTicket] = 0;
+  }
+}
+
+// ---------------------------------------------------------------- K3 epoch drain (ordered)
+// One wave per shard; windows of 64 consecutive positions in ring order.
+__global__ __launch_bounds__(256) void mailbox_drain_ordered_kernel(MboxView mv, int64_t* __restrict__ state,
+                                                                    uint32_t n_state, uint64_t delay_ticks,
+                                                                    OutboxView ob, ReplyView rv) {
+  __shared__ uint32_t owner_tab[4][128], conf_tab[4][128];
+  const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t s = blockIdx.x * 4 + w;
+  const uint32_t S = 1u << mv.log_s;
+  if (s >= S) return;  // whole wave: no barrier follows
+  const uint64_t Q = 1ull << mv.log_q;
+  const uint64_t h = *ctr_head(mv, s), t = *ctr_tail(mv, s);
+  const uint64_t end = t < h + Q ? t : h + Q;
+  unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
+  for (uint64_t p0 = h; p0 < end; p0 += kWave) {
+    const uint64_t p = p0 + lane;
+    MboxMsg x;
+    x.valid = false;
+    if (p < end) {
+      const uint32_t* rc = rec_at(mv, s, p);
+      const u32x4 ha = *reinterpret_cast<const u32x4*>(rc);
+      const u32x4 hb = *reinterpret_cast<const u32x4*>(rc + 4);
+      if (ha.x == lap_tag(mv, p)) {
+        const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
+        x = decode(ha, hb, mv.a2 ? mv.a2 + slot : nullptr);
+        ++done;
+      } else {
+        ++holes;
+      }
+    }
+    serial += run_window_ordered(x, state, n_state, delay_ticks, ob, rv, owner_tab[w], conf_tab[w], failed,
+                                 mv.log_s);
+  }
+  if (lane == 0) *ctr_head(mv, s) = t, *ctr_done(mv, s) = t;
+  for (int off = 32; off > 0; off >>= 1) {
+    done += __shfl_xor(done, off);
+    failed += __shfl_xor(failed, off);
+    holes += __shfl_xor(holes, off);
+  }
+  if (lane == 0) {
+    if (done) atomicAdd(&mv.stats[kMbProcessed], done);
+    if (failed) atomicAdd(&mv.stats[kMbFailed], failed);
+    if (holes) atomicAdd(&mv.stats[kMbHoles], holes);
+    if (serial) atomicAdd(&mv.stats[kMbSerial], serial);
+  }
+}
+
+// ---------------------------------------------------------------- K3 persistent consumer
+// Wave g of G owns shards g, g + G, ...  Polls the next window's tags with sc1
+// loads; a window is the run of consecutive published records (up to 64).  A
+// position whose tag has not arrived while the shard is quiescent (done ==
+// tail, read after the tag) is a hole and is skipped.  Exits on: the host's
+// stop flag once its shards are empty and quiescent, `idle_ticks` without work,
+// or `max_ticks` (hard bound: nothing can spin forever).
+__global__ __launch_bounds__(256) void mailbox_consumer_kernel(MboxView mv, MboxCtrl* __restrict__ ctrl,
+                                                               int64_t* __restrict__ state, uint32_t n_state,
+                                                               uint64_t delay_ticks, ReplyView rv,
+                                                               uint64_t idle_ticks, uint64_t max_ticks) {
+  __shared__ uint32_t owner_tab[4][128], conf_tab[4][128];
+  const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t g = blockIdx.x * 4 + w, G = gridDim.x * 4;
+  const uint32_t S = 1u << mv.log_s;
+  const uint64_t t_start = realtime_ticks();
+  uint64_t last_work = t_start;
+  unsigned long long processed = 0, failed = 0, holes = 0, serial = 0;
+  bool stopping = false, lifetime = false;
+  unsigned sweeps = 0;
+  for (;;) {
+    bool work = false, pending = false;
+    for (uint32_t s = g; s < S; s += G) {
+      unsigned long long* hp = ctr_head(mv, s);
+      const uint64_t h = ld_agent(hp);
+      const uint64_t p = h + lane;
+      const uint32_t* rc = rec_at(mv, s, p);
+      const u32x4 ha = ld16_sc1(rc);
+      const bool ready = ha.x == lap_tag(mv, p);
+      const uint64_t m = __ballot(ready);
+      unsigned n = m == ~0ull ? 64u : (unsigned)__builtin_ctzll(~m);
+      if (n == 0) {
+        const uint64_t t = ld_agent(ctr_tail(mv, s));
+        if (h < t) {
+          pending = true;
+          // quiescent shard (every reserved position finished) and still no tag: a hole
+          const uint64_t d = ld_agent(ctr_done(mv, s));
+          if (d == t && ld16_sc1(rec_at(mv, s, h)).x != lap_tag(mv, h)) {
+            if (lane == 0) st_agent(hp, h + 1);
+            ++holes;
+            work = true;
+          }
+        }
+        continue;
+      }
+      MboxMsg x;
+      x.valid = false;
+      if (lane < n) {
+        const u32x4 hb = ld16_sc1(rc + 4);
+        const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
+        int64_t a2v = 0;
+        if (((ha.w >> 16) & kFlagA2) && mv.a2)
+          a2v = (int64_t)__hip_atomic_load(reinterpret_cast<unsigned long long*>(mv.a2 + slot), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        x = decode(ha, hb, &a2v);
+      }
+      serial += run_window_ordered(x, state, n_state, delay_ticks, OutboxView(), rv, owner_tab[w], conf_tab[w],
+                                   failed, mv.log_s);
+      processed += n;
+      if (lane == 0) st_agent(hp, h + n);  // the slots are free again (their loads have returned)
+      work = true;
+    }
+    const uint64_t now = realtime_ticks();
+    if (work) {
+      last_work = now;
+      continue;
+    }
+    if ((++sweeps & 15) == 0 && !stopping) stopping = sys_ld64(&ctrl->stop) != 0;
+    lifetime = now - t_start > max_ticks;
+    if ((stopping && !pending) || lifetime || (idle_ticks && now - last_work > idle_ticks && !pending)) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  for (int off = 32; off > 0; off >>= 1) failed += __shfl_xor(failed, off);
+  if (lane == 0) {
+    atomicAdd(&mv.stats[kMbProcessed], processed);
+    if (failed) atomicAdd(&mv.stats[kMbFailed], failed);
+    if (holes) atomicAdd(&mv.stats[kMbHoles], holes);
+    if (serial) atomicAdd(&mv.stats[kMbSerial], serial);
+    __hip_atomic_fetch_add(&ctrl->processed, (uint64_t)processed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_add(lifetime ? &ctrl->exits_lifetime : &ctrl->exits_idle, (uint64_t)1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_add(&ctrl->live_waves, (uint64_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Before a persistent session: positions reserved by epoch enqueues (which do
+// not count `done`) are all finished once those kernels have completed.
+__global__ void mailbox_settle_kernel(MboxView mv) {
+  const uint32_t S = 1u << mv.log_s;
+  for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < S; s += gridDim.x * blockDim.x)
+    *ctr_done(mv, s) = *ctr_tail(mv, s);
+}
+
+// ---------------------------------------------------------------- launchers
+static unsigned mb_grid(int64_t work, int per, unsigned cap) {
+  int64_t g = (work + per - 1) / per;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2,
+                            uintptr_t method_col, int method_uniform, int64_t M, uintptr_t table, uint64_t cap,
+                            uintptr_t dir, uint32_t n_dir, uint32_t affine_w, int rank_self, uint32_t origin_base,
+                            const ReplyView& rv, bool live, uintptr_t stream) {
+  if (M <= 0) return;
+  if (!actor || !a0) throw std::invalid_argument("mailbox enqueue: missing column");
+  if (a2 && !mv.a2) throw std::invalid_argument("mailbox enqueue: 3-argument batch but the rings have no a2 array");
+  if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
+  if ((uint64_t)origin_base + (uint64_t)M > rv.n) throw std::invalid_argument("mailbox enqueue: reply view too small");
+  if ((uint64_t)origin_base + (uint64_t)M > 0xffffffffull) throw std::invalid_argument("mailbox enqueue: origin > u32");
+  constexpr int K = 8;
+  const int aw_shift = (affine_w && (affine_w & (affine_w - 1)) == 0) ? __builtin_ctz(affine_w) : -1;
+  const int mode = (affine_w && n_dir) ? 2 : (dir && n_dir) ? 1 : 0;
+  const uint32_t S = 1u << mv.log_s;
+  const size_t lds = (size_t)S * (8 + 8 + 4);
+  const dim3 g(mb_grid(M, 256 * K, 4096));
+#define PT_ENQ(MO, LV)                                                                                                \
+  hipLaunchKernelGGL((mailbox_enqueue_kernel<MO, LV, K>), g, dim3(256), lds, as_stream(stream), mv,                \
+                     (const uint32_t*)actor, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,           \
+                     (const uint16_t*)method_col, (uint32_t)method_uniform, M, (const TableEntry*)table, cap - 1,  \
+                     (const uint32_t*)dir, n_dir, affine_w, aw_shift, rank_self, origin_base, rv)
+  if (live) {
+    if (mode == 2) PT_ENQ(2, true); else if (mode == 1) PT_ENQ(1, true); else PT_ENQ(0, true);
+  } else {
+    if (mode == 2) PT_ENQ(2, false); else if (mode == 1) PT_ENQ(1, false); else PT_ENQ(0, false);
+  }
+#undef PT_ENQ
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_mailbox_drain(const MboxView& mv, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
+                          const OutboxView& ob, const ReplyView& rv, bool ordered, uintptr_t stream) {
+  const uint32_t S = 1u << mv.log_s;
+  hipStream_t st = as_stream(stream);
+  if (ordered) {
+    hipLaunchKernelGGL(mailbox_drain_ordered_kernel, dim3((S + 3) / 4), dim3(256), 0, st, mv, (int64_t*)state,
+                       n_state, delay_ticks, ob, rv);
+  } else {
+    // ~2048 blocks over the shards (each block strides over its shard's queue)
+    const unsigned X = S >= 2048 ? 1u : 2048u / S;
+    hipLaunchKernelGGL((mailbox_drain_kernel<0, 2>), dim3(X, S), dim3(256), 0, st, mv, (int64_t*)state, n_state,
+                       delay_ticks, ob, rv);
+  }
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_mailbox_consumer(const MboxView& mv, MboxCtrl* ctrl, uintptr_t state, uint32_t n_state,
+                             uint64_t delay_ticks, const ReplyView& rv, int blocks, uint64_t idle_ticks,
+                             uint64_t max_ticks, uintptr_t stream) {
+  hipLaunchKernelGGL(mailbox_consumer_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), mv, ctrl,
+                     (int64_t*)state, n_state, delay_ticks, rv, idle_ticks, max_ticks);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------- host class
+static uint32_t log2_exact(uint32_t v, const char* what) {
+  if (v == 0 || (v & (v - 1))) throw std::invalid_argument(std::string(what) + " must be a power of two");
+  return (uint32_t)__builtin_ctz(v);
+}
+
+Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) : device_(device) {
+  mv_.log_s = log2_exact(shards, "mailbox shards");
+  mv_.log_q = log2_exact(slots, "mailbox slots per shard");
+  if (shards > (uint32_t)kMboxMaxShards) throw std::invalid_argument("mailbox shards <= 4096");
+  if (slots < 64) throw std::invalid_argument("mailbox slots per shard >= 64");
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  const uint64_t n = (uint64_t)shards * slots;
+  PT_HIP_CHECK(hipMalloc((void**)&mv_.rec, n * 32));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, n * 32, stream_));  // tag 0 = never published
+  bytes_ = n * 32;
+  if (with_a2) {
+    PT_HIP_CHECK(hipMalloc((void**)&mv_.a2, n * 8));
+    bytes_ += n * 8;
+  }
+  const size_t ctr_bytes = (size_t)shards * kMboxCtrStride * 8;
+  PT_HIP_CHECK(hipMalloc((void**)&mv_.ctr, ctr_bytes));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, ctr_bytes, stream_));
+  PT_HIP_CHECK(hipMalloc((void**)&mv_.stats, kMbStatWords * 8));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStatWords * 8, stream_));
+  bytes_ += ctr_bytes + kMbStatWords * 8;
+  const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+  PT_HIP_CHECK(hipHostMalloc((void**)&ctrl_, sizeof(MboxCtrl), fl));
+  memset((void*)ctrl_, 0, sizeof(MboxCtrl));
+  PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dctrl_, ctrl_, 0));
+  // (not a device-wide sync: a persistent dispatcher may be running)
+  PT_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+Mailboxes::~Mailboxes() {
+  try {
+    if (started_) stop();
+  } catch (...) {
+  }
+  (void)hipSetDevice(device_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+  (void)hipFree(mv_.rec);
+  if (mv_.a2) (void)hipFree(mv_.a2);
+  (void)hipFree(mv_.ctr);
+  (void)hipFree(mv_.stats);
+  if (ctrl_) (void)hipHostFree(ctrl_);
+}
+
+void Mailboxes::enqueue(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+                        int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
+                        uint32_t affine_w, int rank_self, uint32_t origin_base, uintptr_t out_val, uintptr_t out_st,
+                        uint64_t out_n, bool live, uintptr_t stream) {
+  ReplyView rv{(int64_t*)out_val, (int32_t*)out_st, out_n};
+  if (!out_val || !out_st) throw std::invalid_argument("mailbox enqueue: reply outputs required");
+  launch_mailbox_enqueue(mv_, actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, affine_w,
+                         rank_self, origin_base, rv, live, stream);
+}
+
+void Mailboxes::drain(uintptr_t state, uint32_t n_state, uint64_t delay_ticks, uintptr_t out_val, uintptr_t out_st,
+                      uint64_t out_n, bool ordered, uintptr_t stream, const std::vector<uintptr_t>& outbox,
+                      uint64_t outbox_cap) {
+  if (started_ && running()) throw std::runtime_error("mailbox drain: a persistent consumer owns the rings");
+  OutboxView ob;
+  if (outbox_cap) {
+    if (outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
+    ob.actor = (uint32_t*)outbox[0];
+    ob.a0 = (int64_t*)outbox[1];
+    ob.a1 = (int64_t*)outbox[2];
+    ob.a2 = (int64_t*)outbox[3];
+    ob.method = (uint16_t*)outbox[4];
+    ob.count = (unsigned long long*)outbox[5];
+    ob.cap = outbox_cap;
+  }
+  launch_mailbox_drain(mv_, state, n_state, delay_ticks, ob, ReplyView{(int64_t*)out_val, (int32_t*)out_st, out_n},
+                       ordered, stream);
+}
+
+void Mailboxes::start(uintptr_t state, uint32_t n_state, uint64_t delay_ticks, uintptr_t out_val, uintptr_t out_st,
+                      uint64_t out_n, int blocks, double idle_ms, double max_s) {
+  if (started_ && running()) throw std::runtime_error("mailbox consumer already running");
+  if (blocks < 1 || blocks > 256) throw std::invalid_argument("consumer blocks: 1..256 (stay below residency)");
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipStreamSynchronize(stream_));
+  __atomic_store_n(&ctrl_->stop, 0ull, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&ctrl_->live_waves, (uint64_t)blocks * 4, __ATOMIC_SEQ_CST);
+  hipLaunchKernelGGL(mailbox_settle_kernel, dim3(1), dim3(256), 0, stream_, mv_);
+  launch_mailbox_consumer(mv_, dctrl_, state, n_state, delay_ticks,
+                          ReplyView{(int64_t*)out_val, (int32_t*)out_st, out_n}, blocks,
+                          (uint64_t)(idle_ms * 1e5), (uint64_t)(max_s * 1e8), (uintptr_t)stream_);
+  started_ = true;
+  ++launches_;
+}
+
+void Mailboxes::stop() {
+  if (!started_) return;
+  __atomic_store_n(&ctrl_->stop, 1ull, __ATOMIC_SEQ_CST);
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipStreamSynchronize(stream_));
+  started_ = false;
+}
+
+bool Mailboxes::running() const { return __atomic_load_n(&ctrl_->live_waves, __ATOMIC_ACQUIRE) != 0; }
+
+uint64_t Mailboxes::consumer_processed() const { return __atomic_load_n(&ctrl_->processed, __ATOMIC_ACQUIRE); }
+
+void Mailboxes::reset(uintptr_t stream) {
+  if (started_ && running()) throw std::runtime_error("mailbox reset: consumer running");
+  hipStream_t s = as_stream(stream);
+  const uint64_t n = (uint64_t)shards() * slots();
+  PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, n * 32, s));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, (size_t)shards() * kMboxCtrStride * 8, s));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStatWords * 8, s));
+}
+
+std::vector<uint64_t> Mailboxes::stats() const {
+  std::vector<uint64_t> v(kMbStatWords);
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipMemcpy(v.data(), mv_.stats, kMbStatWords * 8, hipMemcpyDeviceToHost));
+  return v;
+}
+
+std::vector<uint64_t> Mailboxes::shard_counters() const {
+  const uint32_t S = shards();
+  std::vector<uint64_t> raw((size_t)S * kMboxCtrStride), out((size_t)S * 3);
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipMemcpy(raw.data(), mv_.ctr, raw.size() * 8, hipMemcpyDeviceToHost));
+  for (uint32_t s = 0; s < S; ++s) {
+    out[3 * s] = raw[(size_t)s * kMboxCtrStride];
+    out[3 * s + 1] = raw[(size_t)s * kMboxCtrStride + 1];
+    out[3 * s + 2] = raw[(size_t)s * kMboxCtrStride + 16];
+  }
+  return out;
+}
+
+}  // namespace ptype

@@ -1,0 +1,141 @@
+// HBM actor mailboxes (SURVEY K2 `mailbox_enqueue`, K3 `dispatch` in epoch and
+// persistent form): the queue between a message's arrival on a GPU and its
+// actor running it.
+//
+// Reference: net/rpc gives every request its own goroutine on the server
+// (stdlib; registered at example/calculator/server/server.go:16-20, served at
+// :38; calls leave the client at cluster/rpc.go:65 and :88).  Here the queue is
+// explicit and lives in HBM:
+//
+//   * S shards per GPU (power of two); actor (local mailbox) m belongs to shard
+//     m & (S - 1), so an actor's messages always meet in one ring.
+//   * each shard is a ring of Q 32-B records:  half A {tag, mbox, origin,
+//     method | flags << 16}, half B {a0, a1}; a2 (3-argument methods) in a side
+//     array.  tag = (position >> log2 Q) + 1: the lap the slot was published in,
+//     so a consumer tells a fresh record from last lap's without any flag word.
+//   * per-shard counters on their own cache lines: tail (reservations), done
+//     (positions a producer has finished: written, or given up as overflow),
+//     head (consumed; the consumer's, read by producers for the capacity check).
+//
+// Producers (K2) reserve ring positions with ONE atomicAdd per (tile, shard):
+// a block stages a tile of messages, ranks them per shard with LDS atomics and
+// reserves each shard's run at once.  A position that would overwrite an
+// unconsumed record is not written: that message is answered
+// kStatusOverflow on the spot (the Send re-sends it), its position becomes a
+// hole, and `done` still counts it.  A consumer treats a position whose tag
+// never arrives as a hole once the shard is quiescent (done == tail).
+//
+// Consumers (K3) run handlers in ring order per actor:
+//   * epoch form: launched behind the enqueue on the same stream (graph-
+//     capturable); stateless / commutative methods drain every shard with the
+//     whole grid, ordered methods (records.hpp method_ordered) one wave per
+//     shard;
+//   * persistent form: a grid well below residency (RCCL keeps its CUs) whose
+//     waves each own a set of shards, poll tags with relaxed write-through
+//     (sc1) loads + s_sleep, and drain concurrently with producers on other
+//     streams; the host's stop flag makes them drain what is left and exit.
+// Within a 64-record window the owning wave finds actors that appear twice
+// (an LDS owner table) and runs just those lanes one at a time, in lane = ring
+// order; everything else runs in parallel.
+#pragma once
+#include <memory>
+
+#include "common.hpp"
+#include "handlers.hpp"
+
+namespace ptype {
+
+constexpr int kMboxCtrStride = 32;  // u64 words per shard: [0] tail, [1] done (one line), [16] head (another)
+constexpr int kMboxMaxShards = 4096;
+enum MboxStat : int {
+  kMbEnqueued = 0,   // records written into rings
+  kMbOverflow = 1,   // messages answered kStatusOverflow (ring full)
+  kMbNoActor = 2,    // registry miss / not this rank's actor
+  kMbProcessed = 3,  // records run by a consumer
+  kMbFailed = 4,     // handler status != ok
+  kMbHoles = 5,      // positions skipped as holes
+  kMbSerial = 6,     // records run serialised (same actor twice in a window)
+  kMbTicket = 8,     // epoch drain: last-block ticket (self-resetting)
+  kMbStatWords = 16,
+};
+
+struct MboxView {
+  uint32_t* rec = nullptr;  // [S * Q * 8] words
+  int64_t* a2 = nullptr;    // [S * Q]
+  unsigned long long* ctr = nullptr;
+  unsigned long long* stats = nullptr;
+  uint32_t log_s = 0, log_q = 0;
+};
+
+// Host-visible control block of the persistent consumer.
+struct alignas(64) MboxCtrl {
+  uint64_t stop;
+  uint64_t live_waves;  // waves still running
+  uint64_t processed;
+  uint64_t exits_idle;
+  uint64_t exits_lifetime;
+  uint64_t pad[3];
+};
+
+// Where replies go: SoA outputs indexed by the record's origin (out_n bounds it).
+struct ReplyView {
+  int64_t* val = nullptr;
+  int32_t* st = nullptr;
+  uint64_t n = 0;
+};
+
+void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2,
+                            uintptr_t method_col, int method_uniform, int64_t M, uintptr_t table, uint64_t cap,
+                            uintptr_t dir, uint32_t n_dir, uint32_t affine_w, int rank_self, uint32_t origin_base,
+                            const ReplyView& rv, bool live, uintptr_t stream);
+void launch_mailbox_drain(const MboxView& mv, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
+                          const OutboxView& ob, const ReplyView& rv, bool ordered, uintptr_t stream);
+void launch_mailbox_consumer(const MboxView& mv, MboxCtrl* ctrl, uintptr_t state, uint32_t n_state,
+                             uint64_t delay_ticks, const ReplyView& rv, int blocks, uint64_t idle_ticks,
+                             uint64_t max_ticks, uintptr_t stream);
+
+class Mailboxes {
+ public:
+  Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2);
+  ~Mailboxes();
+
+  // K2 from a SoA client batch resolved against the registry mirror (this rank's
+  // actors only); origin of message i = origin_base + i.  `live`: a persistent
+  // consumer may be draining concurrently (write-through, ordered publication).
+  void enqueue(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col, int method_uniform,
+               int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, uint32_t affine_w,
+               int rank_self, uint32_t origin_base, uintptr_t out_val, uintptr_t out_st, uint64_t out_n, bool live,
+               uintptr_t stream);
+  // K3 epoch form: drain everything enqueued before it on `stream`.
+  void drain(uintptr_t state, uint32_t n_state, uint64_t delay_ticks, uintptr_t out_val, uintptr_t out_st,
+             uint64_t out_n, bool ordered, uintptr_t stream, const std::vector<uintptr_t>& outbox = {},
+             uint64_t outbox_cap = 0);
+  // K3 persistent form on its own stream.
+  void start(uintptr_t state, uint32_t n_state, uint64_t delay_ticks, uintptr_t out_val, uintptr_t out_st,
+             uint64_t out_n, int blocks, double idle_ms, double max_s);
+  // Ask the persistent consumer to drain what is queued and exit; waits for it.
+  void stop();
+  bool running() const;
+  void reset(uintptr_t stream);  // counters and rings to empty (no consumer may be running)
+
+  std::vector<uint64_t> stats() const;            // kMbStatWords device counters
+  std::vector<uint64_t> shard_counters() const;   // [tail, done, head] per shard
+  uint32_t shards() const { return 1u << mv_.log_s; }
+  uint32_t slots() const { return 1u << mv_.log_q; }
+  uint64_t bytes() const { return bytes_; }
+  uint64_t consumer_processed() const;
+  uint64_t launches() const { return launches_; }
+  const MboxView& view() const { return mv_; }
+
+ private:
+  int device_;
+  MboxView mv_;
+  uint64_t bytes_ = 0;
+  MboxCtrl* ctrl_ = nullptr;   // pinned host
+  MboxCtrl* dctrl_ = nullptr;  // its device address
+  hipStream_t stream_ = nullptr;
+  bool started_ = false;
+  uint64_t launches_ = 0;
+};
+
+}  // namespace ptype

@@ -275,11 +275,19 @@ def _words_i64(lo: torch.Tensor, hi: torch.Tensor) -> torch.Tensor:
     return (lo.to(torch.int64) & 0xFFFFFFFF) | (hi.to(torch.int64) << 32)
 
 
+def fold_step(prev: int, a0: int) -> int:
+    """One kSeqFold application on int64 state: prev * FOLD_MUL + a0, wrapped to int64."""
+    from .records import FOLD_MUL
+
+    v = (prev * FOLD_MUL + a0) & 0xFFFFFFFFFFFFFFFF
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
 def _handler_ref(method, actor, a0, a1, a2, state, outbox=None):
     """Plain-PyTorch reference of the device handler table (handlers.hpp)."""
     from .records import (METHOD_CALC_MULTIPLY as MUL, METHOD_COUNTER_ADD as CADD, METHOD_ECHO as ECHO,
                           METHOD_FORWARD as FWD, METHOD_PRIME_CHECK as PRIME, METHOD_RETRY_TEST as RETRY,
-                          STATUS_FAILED, STATUS_NO_METHOD)
+                          METHOD_SEQ_FOLD as FOLD, STATUS_FAILED, STATUS_NO_METHOD)
     n = method.numel()
     value = torch.zeros(n, dtype=torch.int64)
     status = torch.full((n,), STATUS_NO_METHOD, dtype=torch.int64)
@@ -313,6 +321,13 @@ def _handler_ref(method, actor, a0, a1, a2, state, outbox=None):
         else:
             state[a] += int(a0[i])
             value[i], status[i] = int(state[a]), 0
+    for i in torch.nonzero(method == FOLD).flatten().tolist():  # in message order: a serial execution
+        a = int(actor[i])
+        if state is None or a >= state.numel():
+            status[i] = STATUS_NO_ACTOR
+            continue
+        value[i], status[i] = int(state[a]), 0
+        state[a] = fold_step(int(state[a]), int(a0[i]))
     for i in torch.nonzero(method == FWD).flatten().tolist():
         a = int(actor[i])
         if state is None or a >= state.numel():

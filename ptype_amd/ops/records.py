@@ -10,10 +10,19 @@ METHOD_ECHO = 3
 METHOD_RETRY_TEST = 4
 METHOD_COUNTER_ADD = 5
 METHOD_FORWARD = 6  # actor-to-actor tell: count the visit, emit Forward to a0 while a1 > 0
+METHOD_SEQ_FOLD = 7  # ORDERED: reply = state; state = state * FOLD_MUL + a0 (mod 2**64)
+
+FOLD_MUL = 0x100000001B3
+ORDERED_METHODS = frozenset({METHOD_SEQ_FOLD})  # one at a time per actor, in mailbox order
+
+
+def method_ordered(m: int) -> bool:
+    return int(m) in ORDERED_METHODS
 
 FLAG_VALID = 1
 FLAG_ROUTED = 2
 FLAG_IDENTITY = 4  # slot header: slot position == message index (R = 1, no gaps)
+FLAG_A2 = 8  # mailbox record: third argument in the ring's a2 side array
 
 STATUS_OK = 0
 STATUS_NO_METHOD = 1

@@ -50,7 +50,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import batch as B
-from ..ops.records import STATUS_OVERFLOW
+from ..ops.records import STATUS_OVERFLOW, method_ordered
 from ..ops.table import RegistryTable
 from ..utils import trace
 
@@ -73,6 +73,7 @@ class EpochStats:
     nomatch: int = 0
     failed: int = 0
     toowide: int = 0  # wire v3 replies that did not fit the agreed value plane (must stay 0)
+    mailbox: dict | None = None  # HBM mailbox counters (mailbox delivery)
 
 
 class _ChunkBufs:
@@ -99,7 +100,20 @@ class ActorExchange:
 
     def __init__(self, table: RegistryTable, max_batch: int, chunks: int = 1, group=None, state=None,
                  delay_us: int = 0, slack: float = 0.01, fmt: B.WireFormat | None = None,
-                 packed: bool | None = None, fake=None):
+                 packed: bool | None = None, fake=None, delivery: str = "auto", mailbox_shards: int = 256,
+                 mailbox_slots: int = 0):
+        if delivery not in ("auto", "direct", "mailbox"):
+            raise ValueError("delivery: 'auto', 'direct' or 'mailbox'")
+        # How a message reaches its actor on the GPU that hosts it (world 1):
+        #   direct  -- resolved and run in one streaming pass (no queue): stateless and
+        #              commutative methods, and ordered ones as linearizable CAS updates
+        #   mailbox -- through the HBM mailboxes (ops/mailbox.py): FIFO per actor, ordered
+        #              methods one at a time per actor
+        #   auto    -- mailbox for a uniform ordered method, direct otherwise
+        self.delivery = delivery
+        self.mailbox_shards = int(mailbox_shards)
+        self.mailbox_slots = int(mailbox_slots)
+        self.mailboxes = None
         self.table = table
         self.device = table.device
         self.group = group
@@ -210,6 +224,31 @@ class ActorExchange:
             self.counters.wire_bytes += self.chunks * 4 * (w["req_words"] + w["rep_words"])
         return out_val, out_status
 
+    def _use_mailbox(self, req: B.MsgBatch) -> bool:
+        if self.device.type != "cuda" or self.world > 1 or self.force_collectives or self.delivery == "direct":
+            return False
+        if self.delivery == "mailbox":
+            return True
+        return isinstance(req.method, int) and method_ordered(req.method)
+
+    def _mailboxes(self):
+        if self.mailboxes is None:
+            from ..ops.mailbox import Mailboxes
+
+            S = self.mailbox_shards
+            per = self.max_chunk * self.chunks / S
+            # twice the uniform load per shard: a Send's messages fit at once; skew
+            # overflows into send_all's re-send rounds
+            Q = self.mailbox_slots or 1 << max(6, math.ceil(math.log2(2 * per + 256)))
+            self.mailboxes = Mailboxes(self.device, S, Q, with_a2=True)
+        return self.mailboxes
+
+    def _send_mailbox(self, req: B.MsgBatch, out_val, out_status):
+        """World-1 Send through the HBM mailboxes: K2 enqueue + K3 drain."""
+        self._mailboxes().send(req, self.table, self.state, out_val, out_status, rank_self=self.rank,
+                               delay_us=self.delay_us, outbox=self.outbox)
+        return out_val, out_status
+
     def packed_active(self) -> bool:
         """Whether the next native send uses wire format v3."""
         return bool(self.packed and self.use_engine and not self._capturing
@@ -241,6 +280,9 @@ class ActorExchange:
         wq, wr = R * fmt.req_words(C), R * B.WireFormat.rep_words(C)
         self.counters.sent += M
         self.counters.epochs += n
+        if self._use_mailbox(req):
+            with trace.range("ptype.send.mailbox"):
+                return self._send_mailbox(req, out_val, out_status)
         if self.use_engine and self._engine is None:
             try:
                 self._get_engine()
@@ -388,6 +430,12 @@ class ActorExchange:
             s.toowide += int(b.ws[B.STAT_TOOWIDE])
             if w[B.STAT_ROUTE_ERROR]:
                 raise RuntimeError("route look-back stalled: epoch results are invalid")
+        if self.mailboxes is not None:
+            m = self.mailboxes.stats()
+            s.nomatch += m["no_actor"]
+            s.overflow += m["overflow"]
+            s.failed += m["failed"]
+            s.mailbox = m
         return s
 
 
