@@ -49,6 +49,8 @@ void ConnectionBalancer::close() {
   {
     std::lock_guard<std::mutex> g(mu_);
     cs.swap(clients_);
+    for (auto& r : retired_) cs.push_back(std::move(r));
+    retired_.clear();
   }
   for (auto& c : cs) c->close();
   errs_->close();
@@ -82,15 +84,35 @@ void ConnectionBalancer::set_clients_for_test(std::vector<std::shared_ptr<RpcCon
 
 void ConnectionBalancer::handle_new_nodes(const std::vector<Node>& nodes) {
   std::vector<Node> sel = select_nodes(local_addr_, nodes, cfg_.max_connections);
+  // connections to nodes that stay selected are kept (their in-flight calls go on);
+  // only newly selected nodes are dialled -- the reference re-dials every node and
+  // keeps the old clients open (rpc.go:226-236)
+  std::vector<std::pair<Node, std::shared_ptr<RpcConn>>> have;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t i = 0; i < selected_.size() && i < clients_.size(); ++i) have.emplace_back(selected_[i], clients_[i]);
+  }
+  auto find = [](const std::vector<std::pair<Node, std::shared_ptr<RpcConn>>>& v, const Node& n) {
+    for (const auto& e : v)
+      if (e.first == n) return e.second;
+    return std::shared_ptr<RpcConn>();
+  };
+  std::vector<std::pair<Node, std::shared_ptr<RpcConn>>> dialled;
   std::vector<std::shared_ptr<RpcConn>> fresh;
   fresh.reserve(sel.size());
   for (const auto& n : sel) {
-    try {
-      fresh.push_back(dialer_(n, cfg_));
-    } catch (const Error& e) {
-      for (auto& c : fresh) c->close();
-      fail(Errc::kUnavailable, e.what());
+    std::shared_ptr<RpcConn> c = find(have, n);
+    if (!c) c = find(dialled, n);  // a duplicate pick shares its connection
+    if (!c) {
+      try {
+        c = dialer_(n, cfg_);
+      } catch (const Error& e) {
+        for (auto& d : dialled) d.second->close();
+        fail(Errc::kUnavailable, e.what());
+      }
+      dialled.emplace_back(n, c);
     }
+    fresh.push_back(c);
   }
   std::vector<std::shared_ptr<RpcConn>> old;
   {
@@ -98,9 +120,41 @@ void ConnectionBalancer::handle_new_nodes(const std::vector<Node>& nodes) {
     old.swap(clients_);
     clients_ = std::move(fresh);
     selected_ = sel;
+    // connections no longer selected close once no call holds them (see reap_retired)
+    for (auto& c : old) {
+      bool kept = false;
+      for (auto& k : clients_) kept = kept || k == c;
+      bool queued = false;
+      for (auto& r : retired_) queued = queued || r == c;
+      if (!kept && !queued) retired_.push_back(c);
+    }
   }
-  for (auto& c : old) c->close();  // the reference leaks these (rpc.go:233-236)
+  old.clear();
+  reap_retired();
   updated_->try_send(1);
+}
+
+// A retired connection is closed when the balancer's reference is the only one
+// left: every call holds the connection it was handed by get() until it returns.
+void ConnectionBalancer::reap_retired() {
+  std::vector<std::shared_ptr<RpcConn>> idle;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto it = retired_.begin(); it != retired_.end();) {
+      if (it->use_count() == 1) {
+        idle.push_back(std::move(*it));
+        it = retired_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  for (auto& c : idle) c->close();
+}
+
+size_t ConnectionBalancer::retired_count() {
+  std::lock_guard<std::mutex> g(mu_);
+  return retired_.size();
 }
 
 void ConnectionBalancer::watch_loop() {
@@ -108,6 +162,7 @@ void ConnectionBalancer::watch_loop() {
   bool have = false;
   int64_t deadline = mono_ms() + cfg_.debounce_ms;
   while (!stop_.load()) {
+    reap_retired();
     const int64_t left = deadline - mono_ms();
     if (left <= 0) {
       if (have) {

@@ -13,9 +13,10 @@
 // Documented fixes: at most 1 + Retries attempts, each
 // re-selected round robin (the reference's `retries := 0` inside the loop
 // retries forever); `Go` delivers the final error (the reference tests the
-// outer call's nil error and never retries); replaced clients are closed and
-// Close takes the lock; a closed registry channel stops the watcher instead of
-// spinning.
+// outer call's nil error and never retries); a re-balance keeps the connections
+// of nodes that stay selected and closes a deselected one only once no call
+// holds it (the reference leaks them); Close takes the lock; a closed registry
+// channel stops the watcher instead of spinning.
 #pragma once
 #include <stdint.h>
 
@@ -68,10 +69,12 @@ class ConnectionBalancer {
   static int hash_index(const std::string& local_addr, int conn_number, int node_count);
   // test hook mirroring rpc_test.go:390-425 (clients set directly)
   void set_clients_for_test(std::vector<std::shared_ptr<RpcConn>> clients);
+  size_t retired_count();  // deselected connections still serving in-flight calls
 
  private:
   void handle_new_nodes(const std::vector<Node>& nodes);  // throws on dial failure
   void watch_loop();
+  void reap_retired();
 
   std::string local_addr_, service_;
   std::shared_ptr<NodesChan> nodes_;
@@ -81,6 +84,7 @@ class ConnectionBalancer {
   std::mutex mu_;
   std::vector<Node> selected_;
   std::vector<std::shared_ptr<RpcConn>> clients_;
+  std::vector<std::shared_ptr<RpcConn>> retired_;  // deselected, closed when no call holds them
   std::shared_ptr<Channel<std::string>> errs_;
   std::shared_ptr<Channel<int>> updated_;
   std::atomic<bool> stop_{false};

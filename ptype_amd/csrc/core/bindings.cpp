@@ -287,7 +287,13 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("actors", &GpuConfig::actors)
       .def_readwrite("idle_ms", &GpuConfig::idle_ms)
       .def_readwrite("delay_us", &GpuConfig::delay_us)
-      .def_readwrite("max_batch", &GpuConfig::max_batch);
+      .def_readwrite("max_batch", &GpuConfig::max_batch)
+      .def_readwrite("world", &GpuConfig::world)
+      .def_readwrite("backend", &GpuConfig::backend)
+      .def_readwrite("cpu", &GpuConfig::cpu)
+      .def_readwrite("mailbox_shards", &GpuConfig::mailbox_shards)
+      .def_readwrite("mailbox_slots", &GpuConfig::mailbox_slots)
+      .def_readwrite("watch", &GpuConfig::watch);
   py::class_<MemberConfig, std::shared_ptr<MemberConfig>>(m, "MemberConfig")
       .def(py::init<>())
       .def_readwrite("name", &MemberConfig::name)
@@ -767,6 +773,7 @@ PYBIND11_MODULE(_core, m) {
       .def_property_readonly("calls", &RpcClient::calls)
       .def_property_readonly("attempts", &RpcClient::attempts)
       .def("selected_nodes", [](RpcClient& c) { return c.balancer().selected_nodes(); })
+      .def_property_readonly("retired_conns", [](RpcClient& c) { return c.balancer().retired_count(); })
       .def_property_readonly("conns_updated", [](RpcClient& c) { return c.balancer().conns_updated(); });
 
   // ---------------------------------------------------------------- cluster

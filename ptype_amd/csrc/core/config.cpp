@@ -123,7 +123,16 @@ void decode_ptype(const YNode& root, Config& c) {
         else if (g.first == "idle_ms") c.gpu.idle_ms = want_float(G, g.first, g.second);
         else if (g.first == "delay_us") c.gpu.delay_us = (uint64_t)want_int(G, g.first, g.second);
         else if (g.first == "max_batch") c.gpu.max_batch = (uint64_t)want_int(G, g.first, g.second);
+        else if (g.first == "world") c.gpu.world = (int)want_int(G, g.first, g.second);
+        else if (g.first == "backend") c.gpu.backend = want_string(G, g.first, g.second);
+        else if (g.first == "cpu") c.gpu.cpu = want_bool(G, g.first, g.second);
+        else if (g.first == "mailbox_shards") c.gpu.mailbox_shards = (uint32_t)want_int(G, g.first, g.second);
+        else if (g.first == "mailbox_slots") c.gpu.mailbox_slots = (uint32_t)want_int(G, g.first, g.second);
+        else if (g.first == "watch") c.gpu.watch = want_bool(G, g.first, g.second);
       }
+      if (c.gpu.mailbox_shards == 0 || (c.gpu.mailbox_shards & (c.gpu.mailbox_shards - 1)))
+        fail(Errc::kConfig, "gpu.mailbox_shards must be a power of two");
+      if (c.gpu.world < 0) fail(Errc::kConfig, "gpu.world must be >= 0");
       if (c.gpu.ring == 0 || (c.gpu.ring & (c.gpu.ring - 1)))
         fail(Errc::kConfig, "gpu.ring must be a power of two");
     }

@@ -52,6 +52,12 @@ struct GpuConfig {
   double idle_ms = 200.0;     // persistent dispatcher idle exit
   uint64_t delay_us = 0;      // Prime.Check per-candidate delay (250000 in the reference)
   uint64_t max_batch = 1 << 20;
+  int world = 0;              // data-plane ranks of the service: > 1 makes Join form the group
+  std::string backend;        // "" = nccl (RCCL) on a GPU, gloo with cpu
+  bool cpu = false;           // actor runtime on the host reference path (tests, GPU-less hosts)
+  uint32_t mailbox_shards = 256;
+  uint32_t mailbox_slots = 0;  // 0: sized from max_batch
+  bool watch = true;          // follow the store (shard records, leases) into the GPU registry mirror
 };
 
 struct Config {

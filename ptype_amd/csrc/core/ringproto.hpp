@@ -1,0 +1,147 @@
+// Host side of the single-call request ring (the persistent dispatcher's
+// latency path), shared by the in-process DeviceServer (csrc/hip/server.hpp)
+// and same-node client processes (shmring.cpp).
+//
+// Publishers take sequence numbers from one shared counter; the dispatcher
+// consumes strictly in sequence order, so every taken sequence number MUST end
+// up published, and a slot may only be reused once its previous occupant's
+// reply has landed.  owner[slot] is the slot's state word:
+//
+//   s              free for sequence s (nobody has claimed it yet)
+//   s | kBusy      claimed by s's publisher: published, or about to be; freed
+//                  (-> s + ring) when s's reply has been taken
+//   s | kRescued   s's publisher stalled or died before publishing; a rescuer
+//                  published a no-op (method 0 -> kStatusNoMethod) in its place
+//
+// A timed-out caller does NOT free its slot (the dispatcher may not have read
+// the request yet): the slot stays busy until the late reply lands, and the
+// next occupant takes it over then.  A caller whose reply is overdue rescues
+// the unclaimed sequence numbers in front of it, so a publisher that died
+// between taking a number and publishing wedges the ring for a bounded time
+// only.  (the old protocol freed a timed-out slot at once and
+// waited for owners without a bound.)
+#pragma once
+#include <immintrin.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <chrono>
+#include <functional>
+#include <thread>
+
+#include "records.hpp"
+
+namespace ptype {
+
+constexpr uint64_t kOwnerBusy = 1ull << 62;
+constexpr uint64_t kOwnerRescued = 1ull << 63;
+constexpr uint64_t kOwnerSeq = kOwnerBusy - 1;
+
+struct RingRefs {
+  RingSlot* req = nullptr;      // host-writable view of the request ring
+  ReplySlot* rep = nullptr;     // host view of the reply ring
+  std::atomic<uint64_t>* owner = nullptr;
+  uint32_t ring = 0;            // power of two
+  bool bar = false;             // request ring is device memory written through the BAR
+  std::function<void()> poke;   // make sure the dispatcher runs (relaunch / wake its server)
+};
+
+inline uint64_t ring_now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// Write request `m` for `seq` into its slot (the slot is claimed) and publish the tag.
+inline void ring_write(const RingRefs& r, uint64_t seq, const MsgRecord& m, uint64_t t_ns) {
+  RingSlot* s = &r.req[seq & (r.ring - 1)];
+  s->msg = m;
+  s->csum = ring_csum(seq, m);  // before the tag (release below)
+  s->t_pub_ns = t_ns;
+  // a BAR mapping is write-combined: the payload must be out before the tag
+  if (r.bar) _mm_sfence();
+  __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
+  if (r.bar) {
+    _mm_sfence();
+    // a posted write can still be in flight when the caller checks whether the
+    // dispatcher is running (Dekker hand-off); a read of the same line is
+    // non-posted and returns only after it has landed
+    (void)__atomic_load_n(&s->tag, __ATOMIC_ACQUIRE);
+  }
+}
+
+inline bool reply_landed(const RingRefs& r, uint64_t seq) {
+  return reply_tag_is(__atomic_load_n(&r.rep[seq & (r.ring - 1)].tag, __ATOMIC_ACQUIRE), seq);
+}
+
+// Publish a no-op for `p` if nobody has claimed it; true if this call did.
+inline bool ring_rescue(const RingRefs& r, uint64_t p) {
+  uint64_t exp = p;
+  if (!r.owner[p & (r.ring - 1)].compare_exchange_strong(exp, p | kOwnerRescued, std::memory_order_acq_rel))
+    return false;
+  MsgRecord noop{};
+  noop.method = kMethodNone;
+  noop.flags = kFlagValid;
+  ring_write(r, p, noop, ring_now_ns());
+  return true;
+}
+
+// Claim the slot of `seq` (its previous occupant's reply taken, or taken over).
+// Returns false if `seq` was rescued by someone else (the call must fail) or the
+// wait exceeded `timeout_s` (then `seq` stays unclaimed; a later caller rescues it).
+inline bool ring_claim(const RingRefs& r, uint64_t seq, double timeout_s) {
+  std::atomic<uint64_t>& o = r.owner[seq & (r.ring - 1)];
+  const uint64_t prev = seq - r.ring;
+  const uint64_t t0 = ring_now_ns();
+  for (unsigned spins = 0;; ++spins) {
+    uint64_t cur = o.load(std::memory_order_acquire);
+    if (cur == seq) {
+      if (o.compare_exchange_strong(cur, seq | kOwnerBusy, std::memory_order_acq_rel)) return true;
+      continue;
+    }
+    if (cur == (seq | kOwnerRescued)) return false;
+    if ((spins & 255) == 255) {
+      // the previous occupant published (or was rescued) and its reply landed, but
+      // nobody took it: a caller that timed out or died -- take the slot over
+      if (seq >= r.ring && (cur == (prev | kOwnerBusy) || cur == (prev | kOwnerRescued)) && reply_landed(r, prev)) {
+        if (o.compare_exchange_strong(cur, seq | kOwnerBusy, std::memory_order_acq_rel)) return true;
+        continue;
+      }
+      if (r.poke) r.poke();
+      if ((ring_now_ns() - t0) * 1e-9 > timeout_s) return false;
+      std::this_thread::yield();
+    }
+  }
+}
+
+// Wait for the reply of `seq`; true with the slot freed, false on timeout (the
+// slot stays busy: the late reply lands before the next occupant takes over).
+// While the reply is overdue, unclaimed sequence numbers in front of `seq` are
+// rescued: the dispatcher runs in order and would otherwise wait for them forever.
+inline bool ring_wait(const RingRefs& r, uint64_t seq, double timeout_s, int64_t* value, uint32_t* status) {
+  ReplySlot* out = &r.rep[seq & (r.ring - 1)];
+  const uint64_t t0 = ring_now_ns();
+  const double rescue_after = timeout_s < 0.2 ? timeout_s / 2 : 0.1;
+  bool rescued = false;
+  uint64_t tag;
+  for (unsigned spins = 0; !reply_tag_is(tag = __atomic_load_n(&out->tag, __ATOMIC_ACQUIRE), seq); ++spins) {
+    if ((spins & 1023) == 1023) {
+      if (r.poke) r.poke();
+      const double waited = (ring_now_ns() - t0) * 1e-9;
+      if (!rescued && waited > rescue_after) {
+        rescued = true;
+        const uint64_t lo = seq >= r.ring ? seq - r.ring + 1 : 0;
+        for (uint64_t p = seq; p-- > lo;)
+          if ((r.owner[p & (r.ring - 1)].load(std::memory_order_acquire) & kOwnerSeq) == p) ring_rescue(r, p);
+      }
+      if (waited > timeout_s) return false;
+      std::this_thread::yield();
+    }
+  }
+  *value = out->value;  // landed with the tag (one 16-B device store)
+  *status = (uint32_t)(tag & 0xff);
+  r.owner[seq & (r.ring - 1)].store(seq + r.ring, std::memory_order_release);
+  return true;
+}
+
+}  // namespace ptype

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <thread>
 
+#include "ringproto.hpp"
 #include "util.hpp"
 
 namespace ptype {
@@ -93,40 +94,25 @@ static void poke_if_parked(const ShmView& v) {
 }
 
 ReplyRecord shm_call(const ShmView& v, const MsgRecord& m, double timeout_s) {
-  const uint32_t ring = v.hdr->ring;
+  RingRefs r;
+  r.req = v.req;
+  r.rep = v.rep;
+  r.owner = v.owner;
+  r.ring = v.hdr->ring;
+  r.poke = [&v] { poke_if_parked(v); };
   const uint64_t seq = v.hdr->next_seq.fetch_add(1);
-  const uint32_t idx = (uint32_t)(seq & (ring - 1));
-  const uint64_t t0 = now_ns();
-  // the slot's previous occupant (seq - ring) must have taken its reply; once we
-  // hold a sequence number we MUST publish (the dispatcher consumes in order)
-  for (unsigned spins = 0; v.owner[idx].load(std::memory_order_acquire) != seq; ++spins)
-    if (spins > 64) std::this_thread::yield();
-  RingSlot* s = &v.req[idx];
-  s->msg = m;
-  s->csum = ring_csum(seq, m);  // before the tag (release below)
-  s->t_pub_ns = t0;
-  __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
+  if (!ring_claim(r, seq, timeout_s))
+    fail(Errc::kTimeout, "device actor call: request slot not free in time (left for rescue)");
+  ring_write(r, seq, m, now_ns());
   poke_if_parked(v);
-  ReplySlot* o = &v.rep[idx];
-  uint64_t tag;
-  for (unsigned spins = 0; !reply_tag_is(tag = __atomic_load_n(&o->tag, __ATOMIC_ACQUIRE), seq); ++spins) {
-    if ((spins & 1023) == 1023) {
-      poke_if_parked(v);
-      if ((now_ns() - t0) * 1e-9 > timeout_s) {
-        // give the slot up: a late reply carries this seq's tag and lands before
-        // the next occupant's (the dispatcher runs in sequence order)
-        v.owner[idx].store(seq + ring, std::memory_order_release);
-        fail(Errc::kTimeout, "device actor call: reply timeout");
-      }
-      std::this_thread::yield();
-    }
-  }
-  ReplyRecord r;
-  r.value = o->value;  // landed with the tag (one 16-B device store)
-  r.status = (int32_t)(tag & 0xff);
-  r.actor = m.actor;
-  v.owner[idx].store(seq + ring, std::memory_order_release);
-  return r;
+  int64_t value = 0;
+  uint32_t status = 0;
+  if (!ring_wait(r, seq, timeout_s, &value, &status)) fail(Errc::kTimeout, "device actor call: reply timeout");
+  ReplyRecord out;
+  out.value = value;
+  out.status = (int32_t)status;
+  out.actor = m.actor;
+  return out;
 }
 
 // ---- locator: "/ptype-port-<port>" holds {pid, segment name}

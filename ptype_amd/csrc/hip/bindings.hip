@@ -310,10 +310,11 @@ PYBIND11_MODULE(_hip, m) {
       .def("enqueue", &Mailboxes::enqueue, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"),
            py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
            py::arg("dir"), py::arg("n_dir"), py::arg("affine_w"), py::arg("rank_self"), py::arg("origin_base"),
-           py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("live"), py::arg("stream"))
+           py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("live"), py::arg("stream"),
+           py::arg("arrival") = false)
       .def("drain", &Mailboxes::drain, py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"),
            py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("ordered"), py::arg("stream"),
-           py::arg("outbox") = std::vector<uintptr_t>{}, py::arg("outbox_cap") = 0)
+           py::arg("outbox") = std::vector<uintptr_t>{}, py::arg("outbox_cap") = 0, py::arg("fixed_method") = 0)
       .def("start", &Mailboxes::start, py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"),
            py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("blocks") = 16, py::arg("idle_ms") = 0.0,
            py::arg("max_s") = 60.0)

@@ -87,9 +87,10 @@ struct ReplyView {
 void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2,
                             uintptr_t method_col, int method_uniform, int64_t M, uintptr_t table, uint64_t cap,
                             uintptr_t dir, uint32_t n_dir, uint32_t affine_w, int rank_self, uint32_t origin_base,
-                            const ReplyView& rv, bool live, uintptr_t stream);
+                            const ReplyView& rv, bool live, uintptr_t stream, bool arrival = false);
 void launch_mailbox_drain(const MboxView& mv, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
-                          const OutboxView& ob, const ReplyView& rv, bool ordered, uintptr_t stream);
+                          const OutboxView& ob, const ReplyView& rv, bool ordered, uintptr_t stream,
+                          int fixed_method = 0);
 void launch_mailbox_consumer(const MboxView& mv, MboxCtrl* ctrl, uintptr_t state, uint32_t n_state,
                              uint64_t delay_ticks, const ReplyView& rv, int blocks, uint64_t idle_ticks,
                              uint64_t max_ticks, uintptr_t stream);
@@ -102,14 +103,15 @@ class Mailboxes {
   // K2 from a SoA client batch resolved against the registry mirror (this rank's
   // actors only); origin of message i = origin_base + i.  `live`: a persistent
   // consumer may be draining concurrently (write-through, ordered publication).
+  // `arrival`: shard by arrival tile, not by actor (batches without ordered methods).
   void enqueue(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col, int method_uniform,
                int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, uint32_t affine_w,
                int rank_self, uint32_t origin_base, uintptr_t out_val, uintptr_t out_st, uint64_t out_n, bool live,
-               uintptr_t stream);
+               uintptr_t stream, bool arrival = false);
   // K3 epoch form: drain everything enqueued before it on `stream`.
   void drain(uintptr_t state, uint32_t n_state, uint64_t delay_ticks, uintptr_t out_val, uintptr_t out_st,
              uint64_t out_n, bool ordered, uintptr_t stream, const std::vector<uintptr_t>& outbox = {},
-             uint64_t outbox_cap = 0);
+             uint64_t outbox_cap = 0, int fixed_method = 0);
   // K3 persistent form on its own stream.
   void start(uintptr_t state, uint32_t n_state, uint64_t delay_ticks, uintptr_t out_val, uintptr_t out_st,
              uint64_t out_n, int blocks, double idle_ms, double max_s);

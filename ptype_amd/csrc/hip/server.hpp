@@ -37,6 +37,7 @@
 
 #include "common.hpp"
 #include "handlers.hpp"
+#include "ringproto.hpp"
 #include "shmring.hpp"
 
 namespace ptype {
@@ -384,7 +385,7 @@ class DeviceServer {
     int done = 0;
     while (done < n) {
       const int batch = std::min<int>(n - done, (int)(ring_ / 2));
-      for (int i = 0; i < batch; ++i) seqs[done + i] = publish(in[done + i]);
+      for (int i = 0; i < batch; ++i) seqs[done + i] = publish(in[done + i], timeout_s);
       ensure_running();
       for (int i = 0; i < batch; ++i) out[done + i] = wait(seqs[done + i], timeout_s);
       done += batch;
@@ -455,50 +456,45 @@ class DeviceServer {
   }
 
  private:
-  uint64_t publish(const MsgRecord& m) {
+  RingRefs refs() {
+    RingRefs r;
+    r.req = req_;
+    r.rep = rep_;
+    r.owner = owner_;
+    r.ring = ring_;
+    r.bar = req_on_device_;
+    r.poke = [this] { ensure_running(); };
+    return r;
+  }
+
+  // Claim the next sequence number's slot and publish (ringproto.hpp protocol).
+  uint64_t publish(const MsgRecord& m, double timeout_s) {
+    const RingRefs r = refs();
     const uint64_t seq = seq_->fetch_add(1);
+    if (!ring_claim(r, seq, timeout_s))
+      throw std::runtime_error("device server: request slot not free in time (left for rescue)");
     const uint32_t idx = (uint32_t)(seq & (ring_ - 1));
-    // wait until the slot's previous occupant (seq - ring) has been consumed
-    for (unsigned spins = 0; owner_[idx].load(std::memory_order_acquire) != seq; ++spins)
-      if (spins > 64) std::this_thread::yield();
-    RingSlot* s = &req_[idx];
     const uint64_t t = now_ns();
     pub_actor_[idx] = m.actor;  // host-side copies: the ring may be device memory (slow to read back)
     pub_ns_[idx] = t;
-    s->msg = m;
-    s->csum = ring_csum(seq, m);  // before the tag (release below)
-    s->t_pub_ns = t;
-    // the ring may be a write-combined BAR mapping: the payload must be out before
-    // the tag, and the tag out now rather than when the WC buffer drains
-    if (req_on_device_) _mm_sfence();
-    __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
-    if (req_on_device_) _mm_sfence();
+    ring_write(r, seq, m, t);
     return seq;
   }
 
   ReplyRecord wait(uint64_t seq, double timeout_s) {
     const uint32_t idx = (uint32_t)(seq & (ring_ - 1));
-    ReplySlot* o = &rep_[idx];
-    auto t0 = std::chrono::steady_clock::now();
-    uint64_t tag;
-    for (unsigned spins = 0; !reply_tag_is(tag = __atomic_load_n(&o->tag, __ATOMIC_ACQUIRE), seq); ++spins) {
-      if ((spins & 1023) == 1023) {
-        ensure_running();  // the kernel may have retired on idle/lifetime
-        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
-          // give the slot up: a late reply carries this seq's tag and lands before the
-          // next occupant's (the dispatcher runs in sequence order)
-          owner_[idx].store(seq + ring_, std::memory_order_release);
-          throw std::runtime_error("device server: reply timeout");
-        }
-        std::this_thread::yield();
-      }
-    }
+    const uint32_t actor = pub_actor_[idx];
+    const uint64_t t_pub = pub_ns_[idx];
+    int64_t value = 0;
+    uint32_t status = 0;
+    // a timed-out call keeps its slot busy until the late reply lands (no reuse
+    // while the dispatcher may still read the request)
+    if (!ring_wait(refs(), seq, timeout_s, &value, &status)) throw std::runtime_error("device server: reply timeout");
     ReplyRecord r;
-    r.value = o->value;  // landed with the tag
-    r.status = (int32_t)(tag & 0xff);
-    r.actor = pub_actor_[idx];
-    const uint64_t rtt = now_ns() - pub_ns_[idx];
-    owner_[idx].store(seq + ring_, std::memory_order_release);
+    r.value = value;
+    r.status = (int32_t)status;
+    r.actor = actor;
+    const uint64_t rtt = now_ns() - t_pub;
     int b = rtt ? 63 - __builtin_clzll(rtt) : 0;
     rtt_hist_[b < kRttBuckets ? b : kRttBuckets - 1].fetch_add(1, std::memory_order_relaxed);
     return r;

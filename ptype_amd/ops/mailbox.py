@@ -58,9 +58,11 @@ class Mailboxes:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def enqueue(self, batch: MsgBatch, table, out_val: torch.Tensor, out_status: torch.Tensor, rank_self: int = 0,
-                origin_base: int = 0, live: bool = False) -> None:
+                origin_base: int = 0, live: bool = False, arrival: bool = False) -> None:
         """K2 on the current stream: replies for messages that never enter a ring
-        (no actor on this rank, ring full -> STATUS_OVERFLOW) are written at once."""
+        (no actor on this rank, ring full -> STATUS_OVERFLOW) are written at once.
+        ``arrival``: shard by arrival tile instead of by actor -- only for batches
+        without ordered methods, whose actors need no single ring."""
         if batch.actor.dtype != torch.int32 or batch.a0.dtype != torch.int64:
             raise TypeError("MsgBatch: actor must be int32 and a0..a2 int64")
         uniform = isinstance(batch.method, int)
@@ -69,14 +71,16 @@ class Mailboxes:
         self._m.enqueue(_ptr(batch.actor), _ptr(batch.a0), _ptr(batch.a1), _ptr(batch.a2), _ptr(mcol),
                         int(batch.method) if uniform else 0, batch.M, _ptr(table.table), table.cap, _ptr(d), n_dir,
                         affine, int(rank_self), int(origin_base), _ptr(out_val), _ptr(out_status), out_val.numel(),
-                        bool(live), self._stream())
+                        bool(live), self._stream(), bool(arrival))
 
     def drain(self, state: torch.Tensor | None, out_val: torch.Tensor, out_status: torch.Tensor,
-              ordered: bool = True, delay_us: int = 0, outbox=None) -> None:
-        """K3 epoch form on the current stream: run everything queued."""
+              ordered: bool = True, delay_us: int = 0, outbox=None, fixed_method: int = 0) -> None:
+        """K3 epoch form on the current stream: run everything queued.
+        ``fixed_method``: every queued record is known to carry this method."""
         ob, ob_cap = outbox.view() if outbox is not None else ([], 0)
         self._m.drain(_ptr(state), 0 if state is None else state.numel(), int(delay_us) * 100, _ptr(out_val),
-                      _ptr(out_status), out_val.numel(), bool(ordered), self._stream(), ob, ob_cap)
+                      _ptr(out_status), out_val.numel(), bool(ordered), self._stream(), ob, ob_cap,
+                      int(fixed_method))
 
     def send(self, batch: MsgBatch, table, state: torch.Tensor | None, out_val: torch.Tensor | None = None,
              out_status: torch.Tensor | None = None, rank_self: int = 0, delay_us: int = 0,
@@ -87,9 +91,11 @@ class Mailboxes:
         out_status = torch.empty(M, dtype=torch.int32, device=self.device) if out_status is None else out_status
         if M == 0:
             return out_val, out_status
-        self.enqueue(batch, table, out_val, out_status, rank_self=rank_self)
-        self.drain(state, out_val, out_status, ordered=batch_ordered(batch) if ordered is None else ordered,
-                   delay_us=delay_us, outbox=outbox)
+        ordered = batch_ordered(batch) if ordered is None else ordered
+        self.enqueue(batch, table, out_val, out_status, rank_self=rank_self, arrival=not ordered)
+        # the rings are empty between Sends, so a uniform batch fixes every queued method
+        fixed = int(batch.method) if isinstance(batch.method, int) else 0
+        self.drain(state, out_val, out_status, ordered=ordered, delay_us=delay_us, outbox=outbox, fixed_method=fixed)
         return out_val, out_status
 
     # ---- persistent consumer ("tell" sessions)

@@ -393,6 +393,27 @@ def test_gpu_device_server_latency_path():
         srv.close()
 
 
+@pytest.mark.gpu
+def test_gpu_device_server_timeout_does_not_wedge_ring():
+    """a timed-out call must not hand its slot to the next occupant while
+    the dispatcher may still read it.  One slow call (Prime.Check with a per-candidate
+    delay) times out; the next `ring` calls -- the last one reusing the timed-out
+    slot -- all complete, and the late reply is taken over, not lost."""
+    from ptype_amd.ops.records import METHOD_PRIME_CHECK
+
+    ring = 64
+    state = torch.zeros(8, dtype=torch.int64, device="cuda")
+    srv = ops.hip().DeviceServer(0, ring, state.data_ptr(), 8, 20_000, 200.0, 20.0)  # 20 ms per candidate
+    try:
+        with pytest.raises(RuntimeError, match="timeout"):
+            srv.call(METHOD_PRIME_CHECK, 0, 2, 10, 101, 0.05)  # 8 candidates x 20 ms > 50 ms
+        for i in range(ring + 8):
+            v, s, _ = srv.call(METHOD_CALC_MULTIPLY, i % 8, i, 5, 0, 10.0)
+            assert (v, s) == (5 * i, STATUS_OK)
+    finally:
+        srv.close()
+
+
 def test_wire_sizes_match_kernels():
     """The Python geometry and the launchers' must agree (the all-to-all splits on it)."""
     h = ops.hip()

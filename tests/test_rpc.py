@@ -371,3 +371,33 @@ def test_concurrent_calls_pipelined(servers):
         assert got == sorted(f"who's n{i}" for i in range(200))
     finally:
         c.Close()
+
+
+def test_rebalance_keeps_in_flight_calls(servers):
+    """a re-balance must not cut calls in flight.  Connections of nodes
+    that stay selected are kept; a deselected node's connection closes only after
+    its pending call returned -- so a non-idempotent handler runs exactly once."""
+    slow = RPCRetryTest(0)
+    n1, n2 = servers(slow), servers(RPCTest())
+    ch = mock_registry([n1])
+    cfg = C.ConnConfig(max_connections=0, initial_node_timeout=1.0, debounce_time=0.2, retries=2, allow_local=False)
+    c = C.new_client("", "foo", ch, cfg)
+    try:
+        call = c.Go("RPCRetryTest.Go", "")  # sleeps 1 s on n1
+        time.sleep(0.1)
+        ch.send([n1, n2])  # n1 stays selected
+        assert c.conns_updated.recv(3.0) is not None
+        time.sleep(0.1)
+        ch.send([n2])  # n1 deselected while its call is still running
+        assert c.conns_updated.recv(3.0) is not None
+        assert c._c.retired_conns == 1
+        done = call.done.recv(5.0)
+        assert done.error is None and done.reply == 1  # completed on the retired connection
+        assert slow.called == 1  # ran once: no retry after a cut connection
+        deadline = time.time() + 3
+        while c._c.retired_conns and time.time() < deadline:
+            time.sleep(0.05)
+        assert c._c.retired_conns == 0  # closed once idle
+        assert c.Call("RPCTest.Call", "x") == "who's x"
+    finally:
+        c.Close()
