@@ -11,24 +11,25 @@ namespace ptype {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// Write-through (sc1) 16-B store / load: the record halves a concurrent
-// consumer on another XCD reads (MI355X_MICROARCH.md, hand-off forms: sc1
-// payload stores drained before the signal, sc1 loads on the consumer).
+// Write-through (sc1) 16-B store: the record halves a concurrent consumer on
+// another XCD reads (MI355X_MICROARCH.md, hand-off forms: sc1 payload stores
+// drained before the signal).
 __device__ __forceinline__ void st16_sc1(void* p, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
 }
-__device__ __forceinline__ u32x4 ld16_sc1(const void* p) {
-  u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// A read that cannot be served by a stale L2 line: the per-XCD L2s are not
+// coherent with each other while a kernel runs, and a word another XCD keeps
+// rewriting (a tail, a ring slot) can sit in this XCD's L2 from an earlier
+// read.  A no-op atomic executes at the memory side and returns memory's value.
+__device__ __forceinline__ unsigned long long ld_fresh(unsigned long long* p) {
+  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ u32x4 ld16_fresh(uint32_t* p) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  const unsigned long long lo = ld_fresh(q), hi = ld_fresh(q + 1);
+  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 }
 __device__ __forceinline__ uint64_t sys_ld64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(256) void mailbox_enqueue_kernel(
       const unsigned c = hist[s];
       if (c) {
         base[s] = atomicAdd(ctr_tail(mv, s), (unsigned long long)c);
-        lim[s] = ld_agent(ctr_head(mv, s)) + Q;
+        lim[s] = (LIVE ? ld_fresh(ctr_head(mv, s)) : *ctr_head(mv, s)) + Q;
       }
     }
     __syncthreads();
@@ -448,21 +449,21 @@ __global__ __launch_bounds__(256) void mailbox_consumer_kernel(MboxView mv, Mbox
     bool work = false, pending = false;
     for (uint32_t s = g; s < S; s += G) {
       unsigned long long* hp = ctr_head(mv, s);
-      const uint64_t h = ld_agent(hp);
+      const uint64_t h = ld_fresh(hp);
       const uint64_t p = h + lane;
-      const uint32_t* rc = rec_at(mv, s, p);
-      const u32x4 ha = ld16_sc1(rc);
+      uint32_t* rc = rec_at(mv, s, p);
+      const u32x4 ha = ld16_fresh(rc);
       const bool ready = ha.x == lap_tag(mv, p);
       const uint64_t m = __ballot(ready);
       unsigned n = m == ~0ull ? 64u : (unsigned)__builtin_ctzll(~m);
       if (n == 0) {
-        const uint64_t t = ld_agent(ctr_tail(mv, s));
+        const uint64_t t = ld_fresh(ctr_tail(mv, s));
         if (h < t) {
           pending = true;
           // quiescent shard (every reserved position finished) and still no tag: a hole
-          const uint64_t d = ld_agent(ctr_done(mv, s));
-          if (d == t && ld16_sc1(rec_at(mv, s, h)).x != lap_tag(mv, h)) {
-            if (lane == 0) st_agent(hp, h + 1);
+          const uint64_t d = ld_fresh(ctr_done(mv, s));
+          if (d == t && ld16_fresh(rec_at(mv, s, h)).x != lap_tag(mv, h)) {
+            if (lane == 0) __hip_atomic_exchange(hp, (unsigned long long)(h + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ++holes;
             work = true;
           }
@@ -472,18 +473,16 @@ __global__ __launch_bounds__(256) void mailbox_consumer_kernel(MboxView mv, Mbox
       MboxMsg x;
       x.valid = false;
       if (lane < n) {
-        const u32x4 hb = ld16_sc1(rc + 4);
+        const u32x4 hb = ld16_fresh(rc + 4);
         const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
         int64_t a2v = 0;
-        if (((ha.w >> 16) & kFlagA2) && mv.a2)
-          a2v = (int64_t)__hip_atomic_load(reinterpret_cast<unsigned long long*>(mv.a2 + slot), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+        if (((ha.w >> 16) & kFlagA2) && mv.a2) a2v = (int64_t)ld_fresh(reinterpret_cast<unsigned long long*>(mv.a2 + slot));
         x = decode(ha, hb, &a2v);
       }
       serial += run_window_ordered(x, state, n_state, delay_ticks, OutboxView(), rv, owner_tab[w], conf_tab[w],
                                    failed, mv.log_s);
       processed += n;
-      if (lane == 0) st_agent(hp, h + n);  // the slots are free again (their loads have returned)
+      if (lane == 0) __hip_atomic_exchange(hp, (unsigned long long)(h + n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // slots free again
       work = true;
     }
     const uint64_t now = realtime_ticks();

@@ -31,9 +31,14 @@
 //     whole grid, ordered methods (records.hpp method_ordered) one wave per
 //     shard;
 //   * persistent form: a grid well below residency (RCCL keeps its CUs) whose
-//     waves each own a set of shards, poll tags with relaxed write-through
-//     (sc1) loads + s_sleep, and drain concurrently with producers on other
-//     streams; the host's stop flag makes them drain what is left and exit.
+//     waves each own a set of shards, poll tags + s_sleep, and drain
+//     concurrently with producers on other streams; the host's stop flag makes
+//     them drain what is left and exit.  Producers store records write-through
+//     (sc1, B half drained before the tag half); the consumer reads tags,
+//     counters and records with no-op atomics, which execute at the memory side:
+//     an sc1 load is served by the reading XCD's own (non-coherent) L2, and a
+//     line it cached before the producer wrote stays stale there (observed: a
+//     consumer that never saw its records).
 // Within a 64-record window the owning wave finds actors that appear twice
 // (an LDS owner table) and runs just those lanes one at a time, in lane = ring
 // order; everything else runs in parallel.

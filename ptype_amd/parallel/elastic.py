@@ -12,9 +12,10 @@ never repaired in place -- it is aborted and a new *generation* is formed:
 1. ``send`` fails -> the survivor aborts its group (``_abort_process_group``),
 2. waits until the control plane's lease-based membership (the service's
    registry nodes) drops the dead node (bounded by ``grace_s``),
-3. re-rendezvouses through the replicated KV store: the lowest surviving node
-   opens a TCPStore and publishes ``_ptype/dataplane/<svc>/gen/<g>/<node>``
-   ``{addr, port, members}``; the record with the lowest create revision wins
+3. re-rendezvouses through the replicated KV store (``bootstrap.form_group``,
+   the same path ``Join`` forms epoch 0 with): the lowest surviving node opens a
+   TCPStore and publishes ``_ptype/nccl/<svc>/<gen>/<node>`` ``{addr, port,
+   members}``; the record with the lowest create revision wins
    (``WithSort(SortByCreateRevision, SortAscend)``), so concurrent candidates
    with different views still converge on one member list,
 4. re-homes the dead rank's actors by a deterministic ring adoption (the next
@@ -29,10 +30,8 @@ the loss of a minority of members (Raft quorum).
 """
 from __future__ import annotations
 
-import json
 import os
 import time
-from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -41,7 +40,6 @@ from ..ops import batch as B
 from ..ops.table import RegistryTable, actor_keys
 from .exchange import ActorExchange
 
-PREFIX = "_ptype/dataplane"
 
 
 class RankFailure(RuntimeError):
@@ -111,17 +109,9 @@ class ElasticDataPlane:
     def alive(self, timeout_s: float = 30.0) -> list[str]:
         """Nodes of the service whose registry lease is alive (control plane).
         Retries while the control plane itself is re-electing."""
-        from ..cluster import background
+        from .bootstrap import alive_nodes
 
-        deadline = time.monotonic() + timeout_s
-        while True:
-            try:
-                nodes = self.cluster.Registry.Services(background()).get(self.service, [])
-                return sorted({f"{n.address}:{n.port}" for n in nodes})
-            except Exception:
-                if time.monotonic() > deadline:
-                    raise
-                time.sleep(0.1)
+        return alive_nodes(self.cluster.Registry, self.service, timeout_s)
 
     def start(self) -> None:
         """Wait for ``world`` registered nodes and form generation 0."""
@@ -139,39 +129,11 @@ class ElasticDataPlane:
         self._form(0, self.nodes0)
 
     def _form(self, gen: int, proposal: list[str]) -> None:
-        from ..cluster import SortAscend, SortByCreateRevision, WithPrefix, WithSort, background
+        from .bootstrap import form_group
 
-        prefix = f"{PREFIX}/{self.service}/gen/{gen}/"
-        mine = None
-        if proposal and proposal[0] == self.me:  # candidate rendezvous master
-            host = self.cluster.local_addr
-            mine = dist.TCPStore(host, 0, len(proposal), True, timeout=timedelta(seconds=self.rdv_timeout_s),
-                                 wait_for_workers=False)
-            self.cluster.Store.Put(background(), prefix + self.me,
-                                   json.dumps({"addr": host, "port": mine.port, "members": proposal}))
-        deadline = time.monotonic() + self.rdv_timeout_s
-        rec = None
-        while rec is None:
-            try:
-                vals = self.cluster.Store.Get(background(), prefix, WithPrefix(),
-                                              WithSort(SortByCreateRevision, SortAscend))
-                rec = json.loads(vals[0]) if vals else None
-            except Exception:  # ErrNoKey until a candidate publishes
-                rec = None
-            if rec is None:
-                if time.monotonic() > deadline:
-                    raise TimeoutError(f"no data-plane generation {gen} published")
-                time.sleep(0.05)
-        members = rec["members"]
-        if self.me not in members:
-            raise Excluded(f"{self.me} was left out of generation {gen}: {members}")
-        leader = members[0] == self.me and mine is not None and rec["port"] == mine.port
-        store = mine if leader else dist.TCPStore(rec["addr"], int(rec["port"]), len(members), False,
-                                                  timeout=timedelta(seconds=self.rdv_timeout_s))
-        kw = {"device_id": self.device} if self.backend == "nccl" else {}
-        dist.init_process_group(self.backend, store=dist.PrefixStore(f"ptype/gen{gen}", store),
-                                rank=members.index(self.me), world_size=len(members),
-                                timeout=timedelta(seconds=self.timeout_s), **kw)
+        members, store = form_group(self.cluster.Store, self.cluster.local_addr, self.me, self.service, gen,
+                                    proposal, self.backend, lambda r: self.device if self.backend == "nccl" else None,
+                                    timeout_s=self.timeout_s, rdv_timeout_s=self.rdv_timeout_s)
         self._tcp_store = store  # the master keeps the store alive for the group's lifetime
         self.gen, self.members = gen, members
         self._rebuild()

@@ -14,8 +14,11 @@ One process per GPU.  A ``DeviceRuntime`` owns, on its GPU:
 Actor placement is published in the replicated KV store, one key per rank and
 service (``store/_ptype/actors/<service>/<node>`` -> ``{"rank","world","count"}``,
 strided ids: actor ``a`` lives on rank ``a % world`` in mailbox ``a // world``),
-so the Raft log carries one entry per shard, not one per actor, while the GPU
-table holds every actor (1M actors = 2M slots = 32 MB of HBM).
+attached to a lease this process keeps alive, so the Raft log carries one
+entry per shard, not one per actor, while the GPU table holds every actor (1M
+actors = 2M slots = 32 MB of HBM).  ``mirror.RegistryMirror`` follows those
+records (watch + lease expiry) into the table; with ``gpu.world > 1`` Join
+forms the data-plane group through the store first (parallel/bootstrap.py).
 
 Reference: the reference has no device side; this realises SURVEY C9/C10/C14
 under the API of cluster/cluster.go and cluster/rpc.go.
@@ -46,17 +49,21 @@ def _dist():
 class DeviceRuntime:
     def __init__(self, device=None, actors: int = 1024, ring: int = 4096, idle_ms: float = 200.0,
                  delay_us: int = 0, max_batch: int = 1 << 20, chunks: int = 0, random_state: bool = False,
-                 group=None, shm: bool = True):
+                 group=None, shm: bool = True, service: str = "", mailbox_shards: int = 256,
+                 mailbox_slots: int = 0):
         if device is None:
             device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         self.device = torch.device(device)
-        if self.device.type != "cuda":
-            raise RuntimeError("DeviceRuntime needs a HIP device (use ops.* CPU references for host-only tests)")
-        torch.cuda.set_device(self.device)
+        # a CPU runtime runs the handler table's host reference (tests, GPU-less hosts):
+        # no persistent dispatcher, no HBM mailboxes, gloo collectives
+        self.on_gpu = self.device.type == "cuda"
+        if self.on_gpu:
+            torch.cuda.set_device(self.device)
         d = _dist()
         self.group = group
         self.rank = d.get_rank(group) if d else 0
         self.world = d.get_world_size(group) if d else 1
+        self.service = service
         self.actors = int(actors)
         if random_state:
             g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)
@@ -64,40 +71,98 @@ class DeviceRuntime:
         else:
             self.state = torch.zeros(self.actors, dtype=torch.int64, device=self.device)
         self.delay_us = int(delay_us)
-        # dispatcher rings in shared memory: same-node client processes call these
-        # GPU actors without a socket (shmring.hpp)
-        self.server = hip().DeviceServer(self.device.index or 0, int(ring), self.state.data_ptr(), self.actors,
-                                         self.delay_us, float(idle_ms), 60.0,
-                                         f"ptype-{os.getpid()}-{self.device.index or 0}" if shm else "")
+        self.server = None
+        if self.on_gpu:
+            # dispatcher rings in shared memory: same-node client processes call these
+            # GPU actors without a socket (shmring.hpp)
+            self.server = hip().DeviceServer(self.device.index or 0, int(ring), self.state.data_ptr(), self.actors,
+                                             self.delay_us, float(idle_ms), 60.0,
+                                             f"ptype-{os.getpid()}-{self.device.index or 0}" if shm else "")
         self.table = RegistryTable(2 * self.actors * self.world, device=self.device)
         # dense actor ids [0, actors*world): route through the compiled directory (K5b)
         self.table.enable_directory(self.actors * self.world, affine_world=self.world)
         self.max_batch = int(max_batch)
         self.chunks = chunks or (1 if self.world == 1 else 4)
+        self.mailbox_shards, self.mailbox_slots = int(mailbox_shards), int(mailbox_slots)
         self._exchange = None
         self.shards: dict[str, list[dict]] = {}
+        self.mirror = None  # RegistryMirror (watch-driven) once attached to a control plane
+        self.shard_lease = None
+        self._tcp_store = None  # rendezvous store of a group this runtime formed (kept alive)
+        self._owns_group = False
         self._closed = False
 
     # ------------------------------------------------------------------ setup
     @classmethod
     def for_cluster(cls, core_cluster, cfg) -> "DeviceRuntime":
+        """The device side of ``Join``: form the service's data plane through the
+        store when ``gpu.world > 1`` (parallel/bootstrap.py), start the runtime on
+        this rank's device, publish the actor shard under a lease and mirror every
+        shard of the service into the registry table (mirror.py)."""
+        import torch.distributed as dist
+
+        from .cluster import KVStore, Registry
+
         g = cfg.gpu
-        dev = None if g.device < 0 else torch.device("cuda", g.device)
-        rt = cls(dev, actors=g.actors, ring=g.ring, idle_ms=g.idle_ms, delay_us=g.delay_us, max_batch=g.max_batch)
-        rt.publish_shard(core_cluster.store, cfg.service_name, cfg.node_name)
-        rt.sync_registry(core_cluster.store, cfg.service_name)
+        owns = False
+        tcp = None
+        ndev = 0 if g.cpu else torch.cuda.device_count()
+
+        def device_for_rank(r: int):
+            if g.cpu:
+                return torch.device("cpu")
+            if g.device >= 0:
+                return torch.device("cuda", g.device)
+            lr = os.environ.get("LOCAL_RANK")
+            return torch.device("cuda", int(lr) if lr is not None else r % max(ndev, 1))
+
+        if g.world > 1 and not (dist.is_available() and dist.is_initialized()):
+            from .parallel.bootstrap import form_group, node_id, wait_nodes
+
+            me = node_id(core_cluster.local_addr, cfg.port)
+            registry = Registry(core_cluster.registry)
+            nodes = wait_nodes(registry, cfg.service_name, g.world)
+            backend = g.backend or ("gloo" if g.cpu else "nccl")
+            members, tcp = form_group(KVStore(core_cluster.store), core_cluster.local_addr, me, cfg.service_name, 0,
+                                      nodes, backend, device_for_rank)
+            owns = True
+        d = _dist()
+        rank = d.get_rank() if d else 0
+        rt = cls(device_for_rank(rank), actors=g.actors, ring=g.ring, idle_ms=g.idle_ms, delay_us=g.delay_us,
+                 max_batch=g.max_batch, service=cfg.service_name, mailbox_shards=g.mailbox_shards,
+                 mailbox_slots=g.mailbox_slots)
+        rt._tcp_store, rt._owns_group = tcp, owns
+        rt.attach(core_cluster.registry.kv, cfg.service_name, cfg.node_name, watch=g.watch)
+        # Send needs every rank's routes: wait until all shards of the group are mirrored
+        rt.mirror.wait_shards(rt.world)
         return rt
 
+    def attach(self, kv, service: str, node: str, watch: bool = True) -> None:
+        """Publish this rank's shard (lease-attached) and follow every shard of
+        ``service`` into the registry table."""
+        from .mirror import RegistryMirror, ShardLease
+
+        self.service = service
+        self.shard_lease = ShardLease(kv, service, node, self.rank, self.world, self.actors)
+        self.table.clear()
+        self.mirror = RegistryMirror(self.table, kv, service, watch=watch)
+        self.mirror.apply()
+
+    def sync(self) -> int:
+        """Apply pending registry changes (joins, leaves, lease expiries) now."""
+        return self.mirror.apply() if self.mirror is not None else 0
+
     def publish_shard(self, store, service: str, node: str) -> None:
-        """Record this rank's actor shard of `service` in the replicated store."""
+        """Record this rank's actor shard of `service` in the replicated store
+        (without a lease; ``attach`` keeps a lease-attached record instead)."""
         from .cluster import Context
 
-        v = json.dumps({"rank": self.rank, "world": self.world, "count": self.actors})
+        v = json.dumps({"rank": self.rank, "world": self.world, "count": self.actors, "node": node})
         store.put(Context.background(), f"{ACTORS_PREFIX}/{service}/{node}", v)
 
     def sync_registry(self, store, service: str) -> int:
-        """Rebuild the GPU registry mirror of `service` from the published shards
-        (K5 batch upsert on the device); returns the number of actors."""
+        """One-shot rebuild of the GPU registry mirror of `service` from the
+        published shards (K5 batch upsert on the device); returns the number of actors."""
         from .cluster import Context, NoKeyError, WithPrefix
 
         try:
@@ -137,13 +202,22 @@ class DeviceRuntime:
             from .parallel.exchange import ActorExchange
 
             self._exchange = ActorExchange(self.table, self.max_batch, chunks=self.chunks, group=self.group,
-                                           state=self.state, delay_us=self.delay_us)
+                                           state=self.state, delay_us=self.delay_us,
+                                           mailbox_shards=self.mailbox_shards, mailbox_slots=self.mailbox_slots)
         return self._exchange
 
     # ------------------------------------------------------------------ data plane
+    def _check_service(self, service: str | None) -> None:
+        if service and self.service and service != self.service:
+            raise ValueError(f"Send to {service!r}: this process's data plane hosts {self.service!r} "
+                             "(one GPU actor service per runtime)")
+
     def send(self, service: str | None, batch: B.MsgBatch, resend_overflow: bool = True):
         """Batched Send: every message to its actor anywhere in the node and the
-        replies back in message order.  Collective across the process group."""
+        replies back in message order.  Collective across the process group.
+        Registry changes seen since the last Send are applied first."""
+        self._check_service(service)
+        self.sync()
         ex = self.exchange
         if resend_overflow:
             return ex.send_all(batch)
@@ -162,10 +236,35 @@ class DeviceRuntime:
         return self.exchange.pump(self._outbox, initial=batch)
 
     def call(self, method: int, actor: int, a0: int = 0, a1: int = 0, a2: int = 0, timeout: float = 30.0):
-        """Single synchronous call to a local actor through the persistent dispatcher."""
+        """Single synchronous call to a local actor.  Through the persistent
+        dispatcher (no kernel launch) -- except ordered methods, which must queue
+        behind the actor's other messages: those go through its HBM mailbox."""
+        from .ops.records import method_ordered
+
+        if not self.on_gpu or method_ordered(method):
+            b = B.MsgBatch(torch.tensor([actor], dtype=torch.int32, device=self.device),
+                           torch.tensor([a0], dtype=torch.int64, device=self.device),
+                           torch.tensor([a1], dtype=torch.int64, device=self.device),
+                           torch.tensor([a2], dtype=torch.int64, device=self.device), int(method))
+            if self.on_gpu:
+                mb = self.exchange._mailboxes()
+                v, st = mb.send(b, self._local_table(), self.state, rank_self=0, delay_us=self.delay_us, ordered=True)
+                return int(v.item()), int(st.item())
+            v, st = B._handler_ref(torch.tensor([int(method)]), torch.tensor([actor]), b.a0, b.a1, b.a2, self.state)
+            return int(v[0]), int(st[0])
         with trace.range("ptype.call"):
             v, st, _ = self.server.call(int(method), int(actor), int(a0), int(a1), int(a2), float(timeout))
         return v, st
+
+    def _local_table(self):
+        """Identity table of this rank's mailboxes (a local call names the mailbox)."""
+        if getattr(self, "_ltable", None) is None:
+            t = RegistryTable(2 * self.actors, device=self.device)
+            ids = torch.arange(self.actors, dtype=torch.int64)
+            t.upsert(actor_keys(ids), torch.zeros(self.actors, dtype=torch.int32), ids.to(torch.int32))
+            t.enable_directory(self.actors)
+            self._ltable = t
+        return self._ltable
 
     def serve(self, server, service: str, methods: dict) -> None:
         """Expose GPU handlers over net/rpc: ``methods`` maps a Go method name to
@@ -213,17 +312,21 @@ class DeviceRuntime:
 
         from .utils.trace import hist_percentile
 
-        h = self.server.rtt_histogram()
-        out = {"rank": self.rank, "world": self.world, "actors": self.actors,
-               "dispatcher": {"processed": self.server.processed, "launches": self.server.launches,
-                              "exits_idle": self.server.exits_idle, "exits_lifetime": self.server.exits_lifetime,
-                              "running": self.server.running, "calls": int(sum(h)),
-                              "rtt_p50_ns_le": hist_percentile(h, 50), "rtt_p99_ns_le": hist_percentile(h, 99),
-                              "rtt_log2ns_hist": h},
-               "registry": {"live": self.table.live, "tombstones": self.table.tombstones,
-                            "generation": self.table.generation, "capacity": self.table.cap,
-                            "directory_ids": self.table.dir_n},
-               "shards": self.shards}
+        out = {"rank": self.rank, "world": self.world, "actors": self.actors, "device": str(self.device)}
+        if self.server is not None:
+            h = self.server.rtt_histogram()
+            out["dispatcher"] = {"processed": self.server.processed, "launches": self.server.launches,
+                                 "exits_idle": self.server.exits_idle, "exits_lifetime": self.server.exits_lifetime,
+                                 "running": self.server.running, "calls": int(sum(h)),
+                                 "rtt_p50_ns_le": hist_percentile(h, 50), "rtt_p99_ns_le": hist_percentile(h, 99),
+                                 "rtt_log2ns_hist": h}
+        out["registry"] = {"live": self.table.live, "tombstones": self.table.tombstones,
+                           "generation": self.table.generation, "capacity": self.table.cap,
+                           "directory_ids": self.table.dir_n}
+        out["shards"] = ({k: v["record"] for k, v in self.mirror.shards.items()} if self.mirror is not None
+                         else self.shards)
+        if self.mirror is not None:
+            out["mirror"] = {"applies": self.mirror.applies, "actors": self.mirror.actors}
         if self._exchange is not None:
             out["exchange"] = asdict(self._exchange.stats())
         return out
@@ -232,7 +335,21 @@ class DeviceRuntime:
         if self._closed:
             return
         self._closed = True
-        self.server.close()
+        if self.mirror is not None:
+            self.mirror.close()
+        if self.shard_lease is not None:
+            self.shard_lease.close()
+        if self.server is not None:
+            self.server.close()
+        if self._owns_group:
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                try:
+                    dist.destroy_process_group()
+                except Exception:
+                    pass
+            self._tcp_store = None
 
     def __del__(self):
         try:

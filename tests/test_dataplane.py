@@ -1,0 +1,194 @@
+"""Join brings up the data plane; the registry mirror follows the store.
+
+* Three processes, each ``Join`` with a ``gpu:`` section (``cpu: true``, gloo,
+  ``world: 3``) and nothing else: Join rendezvouses through the replicated store
+  (parallel/bootstrap.py), every rank publishes its lease-attached actor shard
+  and mirrors the others (mirror.py), and ``NewClient(svc).Send`` moves a batch
+  to actors on every rank -- no torchrun, no init_process_group by the caller.
+  Reference: one call joins a node (cluster/cluster.go:28-84).
+* One process, two control-plane members: a node that publishes its shard
+  after this runtime joined becomes routable without a manual sync, and a node
+  whose lease lapses leaves the mirror within TTL + the re-list period
+  (cluster/registry.go:59-83, :119-150; cluster/rpc.go:197-244).
+"""
+import os
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import free_port
+
+
+def _member(C, i, pp, pc, ic, tmp):
+    return C.member_config(name=f"e{i}", dir=os.path.join(tmp, f"m{i}"), lpurls=[f"http://127.0.0.1:{pp[i]}"],
+                           apurls=[f"http://127.0.0.1:{pp[i]}"], lcurls=[f"http://127.0.0.1:{pc[i]}"],
+                           acurls=[f"http://127.0.0.1:{pc[i]}"], initial_cluster=ic, heartbeat_ms=20,
+                           election_ms=200, unsafe_no_fsync=True)
+
+
+class Host:
+    """A host-side receiver so NewClient's balancer has a net/rpc server to dial."""
+
+    def Ping(self, x):
+        return x
+
+
+def _worker(i, pp, pc, sp, tmp, q):
+    os.environ["PTYPE_ADVERTISE_ADDR"] = "127.0.0.1"
+    from ptype_amd import cluster as C
+    from ptype_amd.ops.batch import MsgBatch
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD, STATUS_OK
+
+    c = None
+    try:
+        ic = ",".join(f"e{j}=http://127.0.0.1:{pp[j]}" for j in range(3))
+        cfg = C.Config()
+        cfg.service_name, cfg.node_name, cfg.port = "calc", f"n{i}", sp[i]
+        cfg.member = _member(C, i, pp, pc, ic, tmp)
+        cfg.has_gpu = True
+        cfg.gpu.cpu, cfg.gpu.world, cfg.gpu.actors, cfg.gpu.max_batch = True, 3, 32, 4096
+        srv = C.Serve(sp[i], Host(), host="127.0.0.1")
+        c = C.Join(C.background(), cfg)  # forms the gloo group through the store
+        rt = c.runtime
+        client = c.NewClient("calc", C.ConnConfig(retries=0, allow_local=False))
+        n = rt.total_actors
+        ids = torch.arange(n, dtype=torch.int32)
+        a = ids.to(torch.int64) + 100 * i
+        val, st = client.Send(MsgBatch(ids, a, torch.full((n,), 3, dtype=torch.int64), None, METHOD_CALC_MULTIPLY))
+        ok_mul = bool((st == STATUS_OK).all()) and torch.equal(val, a * 3)
+        # every rank adds 1 to every actor: each actor, wherever it lives, counts 3
+        _, st = client.Send(MsgBatch(ids, torch.ones(n, dtype=torch.int64), None, None, METHOD_COUNTER_ADD))
+        ok_add = bool((st == STATUS_OK).all())
+        import torch.distributed as dist
+
+        dist.barrier()
+        q.put((i, rt.rank, rt.world, ok_mul, ok_add, bool((rt.state == 3).all()), len(rt.mirror.shards),
+               client.Call("Host.Ping", "x")))
+        dist.barrier()
+        client.Close()
+        srv.Close()
+        c.Close()
+    except Exception as e:
+        import traceback
+
+        q.put(("error", i, repr(e), traceback.format_exc()[-2000:]))
+        if c is not None:
+            c.Close()
+
+
+@pytest.mark.timeout(180)
+def test_join_forms_data_plane_and_send(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pp, pc, sp = ([free_port() for _ in range(3)] for _ in range(3))
+    procs = [ctx.Process(target=_worker, args=(i, pp, pc, sp, str(tmp_path), q)) for i in range(3)]
+    [p.start() for p in procs]
+    res = [q.get(timeout=150) for _ in range(3)]
+    [p.join(30) for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    errors = [r for r in res if r[0] == "error"]
+    assert not errors, "\n".join("\n".join(map(str, r)) for r in errors)
+    assert sorted(r[1] for r in res) == [0, 1, 2]  # ranks assigned by the rendezvous
+    for i, rank, world, ok_mul, ok_add, counted, shards, ping in res:
+        assert world == 3 and ok_mul and ok_add and counted and shards == 3 and ping == "x", res
+
+
+def test_mirror_follows_joins_and_lease_expiry(tmp_path, ports, monkeypatch):
+    monkeypatch.setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    from ptype_amd import cluster as C
+    from ptype_amd.mirror import ShardLease
+    from ptype_amd.ops.table import actor_keys
+
+    pp, pc = [ports(), ports()], [ports(), ports()]
+    ic = ",".join(f"e{j}=http://127.0.0.1:{pp[j]}" for j in range(2))
+    cfgs = []
+    for i in range(2):
+        cfg = C.Config()
+        cfg.service_name, cfg.node_name, cfg.port = "calc", f"n{i}", ports()
+        cfg.member = _member(C, i, pp, pc, ic, str(tmp_path))
+        cfgs.append(cfg)
+    import threading
+
+    joined = [None, None]
+
+    def join(i, rt):
+        joined[i] = C.Join(C.background(), cfgs[i], runtime=rt)
+
+    cfgs[0].has_gpu = True
+    cfgs[0].gpu.cpu, cfgs[0].gpu.actors = True, 16
+    ts = [threading.Thread(target=join, args=(i, i == 0)) for i in range(2)]  # static 2-member cluster
+    [t.start() for t in ts]
+    [t.join(30) for t in ts]
+    a, b = joined
+    try:
+        rt = a.runtime
+        # this node's shard publishes rank 0 of a 2-rank layout: ids 0, 2, 4, ...
+        rt.shard_lease.close()
+        rt.mirror.apply()
+        mine = ShardLease(b.registry.kv, "calc", "n0", 0, 2, 16)
+        rt.mirror.wait_shards(1, 10)
+        rank, _ = rt.table.lookup(actor_keys(torch.tensor([4, 5])))
+        assert rank.tolist() == [0, -1]  # odd ids: nobody yet
+        # a node that joins later: its shard (rank 1, ids 1, 3, 5, ...) becomes routable at the next apply
+        other = ShardLease(b.registry.kv, "calc", "n1", 1, 2, 16)
+        deadline = time.time() + 5
+        while time.time() < deadline:
+            rt.sync()
+            if rt.table.lookup(actor_keys(torch.tensor([5])))[0].tolist() == [1]:
+                break
+            time.sleep(0.05)
+        rank, mbox = rt.table.lookup(actor_keys(torch.tensor([4, 5, 31])))
+        assert rank.tolist() == [0, 1, 1] and mbox.tolist() == [2, 2, 15]
+        # its lease lapses (no revoke: a crash) -> gone within TTL + re-list period
+        other.stop_keepalive()
+        t0 = time.time()
+        while time.time() - t0 < 8:
+            rt.sync()
+            if rt.table.lookup(actor_keys(torch.tensor([5])))[0].tolist() == [-1]:
+                break
+            time.sleep(0.1)
+        gone = time.time() - t0
+        assert rt.table.lookup(actor_keys(torch.tensor([4, 5])))[0].tolist() == [0, -1]
+        assert gone < 2 + 3 + 1, gone  # TTL 2 s + debounce (reference: 3 s) + slack
+        assert len(rt.mirror.shards) == 1
+        mine.close()
+    finally:
+        a.Close()
+        b.Close()
+
+
+def test_mirror_k6_sweeps_shards_not_seen(tmp_path, ports, monkeypatch):
+    """K6 backstop: with no watch stream, a shard whose record vanished expires by
+    its deadline (last seen + TTL + grace) through the table sweep."""
+    monkeypatch.setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    from ptype_amd import cluster as C
+    from ptype_amd.mirror import RegistryMirror, ShardLease
+    from ptype_amd.ops.table import RegistryTable, actor_keys
+
+    pp, pc = ports(), ports()
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "svc", "n0", ports()
+    cfg.member = _member(C, 0, [pp], [pc], f"e0=http://127.0.0.1:{pp}", str(tmp_path))
+    c = C.Join(C.background(), cfg, runtime=False)
+    try:
+        kv = c._c.registry.kv
+        lease = ShardLease(kv, "svc", "x", 0, 1, 8)
+        t = RegistryTable(64, device="cpu")
+        # no watch and no re-list within the test: nothing refreshes the shard's deadline
+        m = RegistryMirror(t, kv, "svc", ttl_ms=300, grace_ms=100, relist_s=1000.0, watch=False)
+        m.wait_shards(1, 5)
+        assert t.live == 8
+        t0 = time.time()
+        lease.close()
+        while t.live and time.time() - t0 < 5:
+            m.apply()
+            time.sleep(0.02)
+        assert t.live == 0 and not m.shards and t.tombstones == 8  # swept (K6), not deleted by an event
+        assert time.time() - t0 < 1.0
+        m.close()
+    finally:
+        c.Close()

@@ -129,19 +129,21 @@ def test_mailbox_overflow_is_answered_and_resent():
     assert ex.counters.resends > 0
 
 
-def test_mailbox_persistent_consumer_live_enqueue():
+@pytest.mark.parametrize("shards,slots,blocks", [(128, 1 << 12, 8), (256, 1 << 10, 16), (64, 1 << 13, 4)])
+def test_mailbox_persistent_consumer_live_enqueue(shards, slots, blocks):
     """The persistent consumer drains while batches keep arriving from another stream;
-    after stop() every message ran exactly once, batches in submission order."""
+    after stop() every message ran exactly once, batches in submission order.  Rings
+    smaller than the traffic: slots are recycled while the consumer runs."""
     n, M, batches = 2048, 1 << 16, 6
     t, perm = placed_table(n)
     state = torch.randint(0, 1 << 20, (n,), dtype=torch.int64, device=DEV)
     s0 = state.cpu().clone()
-    mb = Mailboxes(DEV, shards=128, slots=1 << 12)  # smaller than the traffic: the ring must recycle
+    mb = Mailboxes(DEV, shards=shards, slots=slots)
     out_v = torch.full((M * batches,), -1, dtype=torch.int64, device=DEV)
     out_s = torch.full((M * batches,), -1, dtype=torch.int32, device=DEV)
     reqs = [fold_batch(M, n, 100 + b) for b in range(batches)]
     torch.cuda.synchronize()
-    mb.start(state, out_v, out_s, blocks=8, max_s=20.0)
+    mb.start(state, out_v, out_s, blocks=blocks, max_s=20.0)
     prod = torch.cuda.Stream(DEV)
     with torch.cuda.stream(prod):
         for b, r in enumerate(reqs):

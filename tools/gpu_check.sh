@@ -5,6 +5,8 @@ set -o pipefail
 TAG=${1:-run}
 TARGET=${2:-tests}
 mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo "SMOKE FAILED"; tail -30 gpurun_out/smoke_$TAG.log; exit 1; }
+tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 700 python -u -m pytest $TARGET -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1 || { echo "TESTS FAILED"; tail -30 gpurun_out/test_$TAG.log; exit 1; }
 tail -1 gpurun_out/test_$TAG.log
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "BENCH FAILED"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
