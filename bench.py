@@ -66,6 +66,10 @@ def _parse():
     p.add_argument("--delivery", choices=["direct", "mailbox"], default="direct",
                    help="how a message reaches its actor on its GPU: one fused pass, or through the HBM "
                         "mailboxes (K2 enqueue + K3 drain; world 1)")
+    p.add_argument("--zipf", type=float, default=0.0, metavar="S",
+                   help="skewed load: actor popularity Zipf(S) (hot actors scattered over the GPUs); batches "
+                        "pre-generated outside the timed loop, so compare against --zipf 0 --pregen")
+    p.add_argument("--pregen", action="store_true", help="uniform load, pre-generated like --zipf (A/B baseline)")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary (affine placement) measurement after the headline")
     return p.parse_args()
@@ -187,10 +191,18 @@ def main():
                      torch.empty(M, dtype=torch.int64, device=device), None, METHOD_CALC_MULTIPLY)
     val = torch.empty(M, dtype=torch.int64, device=device)
     st = torch.empty(M, dtype=torch.int32, device=device)
-    use_graph = use_gpu and (args.graph == "on" or (args.graph == "auto" and not dist_on and fake is None))
+    pregen = args.zipf > 0 or args.pregen
+    use_graph = use_gpu and not pregen and (args.graph == "on" or (args.graph == "auto" and not dist_on and fake is None))
+    pre = []
+    if pregen:  # 4 distinct batches per rank, generated before any timing
+        for k in range(4):
+            sd = (k * world + rank) * 7919 + 13
+            pre.append(B.gen_zipf_requests(M, n_actors, args.zipf, seed=sd, device=device) if args.zipf > 0 else
+                       B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=sd, device=device))
 
-    def verify(tag):
-        ok = bool((st == STATUS_OK).all()) and bool(torch.equal(val, req.a0 * req.a1))
+    def verify(tag, r=None):
+        r = req if r is None else r
+        ok = bool((st == STATUS_OK).all()) and bool(torch.equal(val, r.a0 * r.a1))
         if not ok:
             bad = int((st != STATUS_OK).sum())
             raise SystemExit(f"[rank {rank}] {tag}: verification failed ({bad} non-OK replies)")
@@ -215,6 +227,9 @@ def main():
             if graph is not None:
                 graph.replay()
                 return
+            if pre:
+                ex.send_all(pre[s % len(pre)], out=(val, st))
+                return
             B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=(s * world + rank) * 0x1000193 + 7, device=device,
                            out=req)
             ex.send(req, val, st)
@@ -223,7 +238,7 @@ def main():
             step(s)
         sync()
         if warmup:
-            verify("warmup")
+            verify("warmup", pre[(warmup - 1) % len(pre)] if pre else None)
         barrier()
         sync()
         t0 = time.perf_counter()
@@ -237,7 +252,7 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         if steps:
-            verify("timed")
+            verify("timed", pre[(warmup + steps - 1) % len(pre)] if pre else None)
         return elapsed, ex, graph is not None
 
     table = build_table(args.placement)
@@ -386,6 +401,10 @@ def main():
                 **wire_info(ex, req),
                 "client_batch": "SoA (actor u32, A i64, B i64)",
                 "hip_graph": graphed,
+                **({"load": f"zipf({args.zipf})" if args.zipf > 0 else "uniform", "pregenerated": True,
+                    "resend_rounds": ex.counters.resends} if pregen else {}),
+                **({"slot_capacity": ex.last_wire.get("C"), "slot_capacity_alloc": ex.last_wire.get("C_alloc"),
+                    "slot_capacity_static": ex.C} if ex.last_wire is not None else {}),
                 "placement": args.placement,
                 "registry_lookup": route_mode,
                 "delivery": args.delivery if world == 1 and not dist_on else "direct",

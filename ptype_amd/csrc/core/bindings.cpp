@@ -415,7 +415,8 @@ PYBIND11_MODULE(_core, m) {
       .def("status", &Member::status)
       .def("client_ports", &Member::client_ports)
       .def("member_list", &Member::member_list)
-      .def("lease_list", &Member::lease_list);
+      .def("lease_list", &Member::lease_list)
+      .def_property_readonly("reads_served", &Member::reads_served);
 
   py::class_<KvClient, std::shared_ptr<KvClient>>(m, "KvClient")
       .def(py::init<std::vector<std::string>, int64_t>(), py::arg("endpoints"), py::arg("dial_timeout_ms") = 5000)

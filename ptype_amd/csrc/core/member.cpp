@@ -315,6 +315,10 @@ void Member::close() {
     std::lock_guard<std::mutex> g(note_mu_);
     note_cv_.notify_all();
   }
+  {
+    std::lock_guard<std::mutex> g(read_mu_);
+    read_cv_.notify_all();
+  }
   if (raft_th_.joinable()) raft_th_.join();
   if (note_th_.joinable()) note_th_.join();
   // fail every outstanding waiter
@@ -388,8 +392,9 @@ void Member::raft_loop() {
     {
       std::unique_lock<std::mutex> g(in_mu_);
       const int64_t wait = std::max<int64_t>(1, last_tick_ms_ + cfg_.heartbeat_ms - mono_ms());
-      in_cv_.wait_for(g, std::chrono::milliseconds(wait),
-                      [&] { return stop_.load() || !inbox_.msgs.empty() || !inbox_.props.empty(); });
+      in_cv_.wait_for(g, std::chrono::milliseconds(wait), [&] {
+        return stop_.load() || !inbox_.msgs.empty() || !inbox_.props.empty() || !inbox_.reads.empty();
+      });
       std::swap(in, inbox_);
     }
     if (stop_.load()) break;
@@ -424,6 +429,7 @@ void Member::raft_loop() {
         lk.lock();
       }
     }
+    for (const auto& ctx : in.reads) node_->read_index(ctx);
     const int64_t now = mono_ms();
     while (now - last_tick_ms_ >= cfg_.heartbeat_ms) {
       node_->tick();
@@ -486,10 +492,26 @@ void Member::process_ready() {
   storage_->append(ents, hs_changed ? &hs : nullptr);
   std::vector<raft::Message> msgs = node_->take_messages();
   std::vector<raft::Entry> committed = node_->take_committed();
+  std::vector<raft::ReadState> reads = node_->take_read_states();
   const bool is_leader = node_->role() == raft::kLeader;
   lk.unlock();
   for (const auto& m : msgs) send_raft(m);
   for (const auto& e : committed) apply_entry(e);
+  {
+    std::lock_guard<std::mutex> g(read_mu_);
+    for (const auto& rs : reads) {
+      auto it = read_waiters_.find(rs.ctx);
+      if (it == read_waiters_.end()) continue;
+      it->second.done = true;
+      it->second.ok = rs.ok;
+      it->second.index = rs.index;
+    }
+    {
+      std::lock_guard<std::mutex> g2(sm_mu_);
+      applied_pub_.store(applied_);
+    }
+  }
+  read_cv_.notify_all();
   if (is_leader != was_leader_) {
     std::lock_guard<std::mutex> g(sm_mu_);
     if (is_leader) {
@@ -755,6 +777,42 @@ void Member::resolve(uint64_t reqid, ApplyResult r) {
   w->cv.notify_all();
 }
 
+void Member::read_barrier(int64_t timeout_ms) {
+  if (stop_.load()) fail(Errc::kShutdown, "etcdserver: server stopped");
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(clamp_timeout(timeout_ms));
+  for (;;) {
+    const std::string ctx = std::to_string(id_) + "/" + std::to_string(++read_seq_);
+    {
+      std::lock_guard<std::mutex> g(read_mu_);
+      read_waiters_[ctx] = ReadWaiter{};
+    }
+    {
+      std::lock_guard<std::mutex> g(in_mu_);
+      inbox_.reads.push_back(ctx);
+      in_cv_.notify_all();
+    }
+    std::unique_lock<std::mutex> g(read_mu_);
+    // a round that gets no answer (leader lost, message dropped) is retried
+    const auto round_end = std::min(deadline, std::chrono::steady_clock::now() +
+                                                  std::chrono::milliseconds(std::max<int64_t>(50, 4 * cfg_.heartbeat_ms)));
+    read_cv_.wait_until(g, round_end, [&] { return read_waiters_[ctx].done || stop_.load(); });
+    const ReadWaiter w = read_waiters_[ctx];
+    read_waiters_.erase(ctx);
+    if (w.done && w.ok) {
+      // serve once this member's state machine has caught up with the read index
+      if (!read_cv_.wait_until(g, deadline, [&] { return applied_pub_.load() >= w.index || stop_.load(); }))
+        fail(Errc::kTimeout, "etcdserver: request timed out");
+      if (stop_.load()) fail(Errc::kShutdown, "etcdserver: server stopped");
+      ++reads_served_;
+      return;
+    }
+    if (stop_.load()) fail(Errc::kShutdown, "etcdserver: server stopped");
+    if (std::chrono::steady_clock::now() >= deadline) fail(Errc::kTimeout, "etcdserver: request timed out");
+    g.unlock();
+    if (w.done) sleep_ms(std::max<int64_t>(1, cfg_.heartbeat_ms / 2));  // no leader / no term commit yet
+  }
+}
+
 ApplyResult Member::propose_wait(uint8_t etype, uint8_t op, const std::string& payload, int64_t timeout_ms) {
   if (stop_.load()) fail(Errc::kShutdown, "etcdserver: server stopped");
   auto w = std::make_shared<Waiter>();
@@ -911,7 +969,7 @@ void Member::cancel_watch(int64_t wid) {
 
 // ---------------------------------------------------------------- local API
 RangeResult Member::range(const std::string& key, const RangeOpts& o, int64_t timeout_ms) {
-  if (!o.serializable) propose_wait(raft::kEntryNormal, kApplyNoop, "", timeout_ms);  // linearizable read barrier
+  if (!o.serializable) read_barrier(timeout_ms);  // linearizable: ReadIndex, not a log write
   std::lock_guard<std::mutex> g(sm_mu_);
   return kv_.range(key, o);
 }

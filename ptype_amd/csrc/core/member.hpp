@@ -63,6 +63,7 @@ class Member {
   StatusInfo status();
   const MemberConfig& config() const { return cfg_; }
   std::vector<int> client_ports() const;
+  uint64_t reads_served() const { return reads_served_.load(); }  // linearizable reads through ReadIndex
 
   // ---- local API (also what the TCP handler calls)
   RangeResult range(const std::string& key, const RangeOpts& o, int64_t timeout_ms = 5000);
@@ -92,6 +93,11 @@ class Member {
   struct Inbox {
     std::vector<raft::Message> msgs;
     std::vector<std::pair<uint8_t, std::string>> props;  // (entry type, data)
+    std::vector<std::string> reads;                       // ReadIndex request ids
+  };
+  struct ReadWaiter {
+    bool done = false, ok = false;
+    uint64_t index = 0;
   };
   struct Watcher {
     std::string key, end;
@@ -101,6 +107,9 @@ class Member {
   struct Peer;
 
   ApplyResult propose_wait(uint8_t etype, uint8_t op, const std::string& payload, int64_t timeout_ms);
+  // Linearizable read barrier (ReadIndex): returns once this member has applied
+  // everything committed when the read arrived -- no log entry, no fsync.
+  void read_barrier(int64_t timeout_ms);
   void raft_loop();
   void notifier_loop();
   void process_ready();
@@ -141,6 +150,12 @@ class Member {
 
   std::mutex wait_mu_;
   std::map<uint64_t, std::shared_ptr<Waiter>> waiters_;
+  std::mutex read_mu_;
+  std::condition_variable read_cv_;  // a read state arrived or applied_ advanced
+  std::map<std::string, ReadWaiter> read_waiters_;
+  std::atomic<uint64_t> applied_pub_{0};  // applied_, readable without sm_mu_
+  std::atomic<uint64_t> read_seq_{0};
+  std::atomic<uint64_t> reads_served_{0};
   std::atomic<uint64_t> reqseq_{0};
   std::atomic<int64_t> lease_seq_{0};
 

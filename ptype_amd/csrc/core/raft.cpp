@@ -104,7 +104,16 @@ const Entry* Node::entry_at(uint64_t i) const {
   return &log_[i - snap_index_ - 1];
 }
 
+std::vector<ReadState> Node::take_read_states() {
+  std::vector<ReadState> v;
+  v.swap(read_states_);
+  return v;
+}
+
 void Node::reset(uint64_t term) {
+  // pending reads of a leadership that ends fail; their owners retry
+  for (auto& kv : reads_) read_done(kv.first, 0, kv.second.from, false);
+  reads_.clear();
   if (term_ != term) {
     term_ = term;
     vote_ = 0;
@@ -115,6 +124,60 @@ void Node::reset(uint64_t term) {
   reset_randomized_timeout();
   votes_granted_.clear();
   votes_rejected_.clear();
+}
+
+void Node::read_index(const std::string& ctx) {
+  if (role_ == kLeader) {
+    leader_read(ctx, opt_.id);
+  } else if (lead_ != 0) {
+    Message m;
+    m.type = kMsgReadIndex;
+    m.to = lead_;
+    m.context = ctx;
+    send(std::move(m));
+  } else {
+    read_states_.push_back(ReadState{ctx, 0, false});
+  }
+}
+
+void Node::read_done(const std::string& ctx, uint64_t index, uint64_t from, bool ok) {
+  if (from == opt_.id) {
+    read_states_.push_back(ReadState{ctx, index, ok});
+    return;
+  }
+  Message r;
+  r.type = kMsgReadIndexResp;
+  r.to = from;
+  r.index = index;
+  r.reject = !ok;
+  r.context = ctx;
+  send(std::move(r));
+}
+
+void Node::leader_read(const std::string& ctx, uint64_t from) {
+  // a new leader does not know what is committed until an entry of its own term
+  // is (become_leader appends an empty one for exactly this)
+  if (term_at(commit_) != term_) {
+    read_done(ctx, 0, from, false);
+    return;
+  }
+  if (quorum() <= 1) {
+    read_done(ctx, commit_, from, true);
+    return;
+  }
+  PendingRead& pr = reads_[ctx];
+  pr.index = commit_;
+  pr.from = from;
+  pr.acks = {opt_.id};
+  for (auto& kv : prs_) {
+    if (kv.first == opt_.id) continue;
+    Message m;
+    m.type = kMsgHeartbeat;
+    m.to = kv.first;
+    m.commit = std::min(kv.second.match, commit_);
+    m.context = ctx;
+    send(std::move(m));
+  }
 }
 
 void Node::become_follower(uint64_t term, uint64_t lead) {
@@ -425,10 +488,26 @@ void Node::step_leader(const Message& m) {
       }
       break;
     }
+    case kMsgReadIndex:
+      leader_read(m.context, m.from);
+      break;
     case kMsgHeartbeatResp: {
       auto it = prs_.find(m.from);
       if (it == prs_.end()) return;
       it->second.recent_active = true;
+      if (!m.context.empty()) {  // a ReadIndex round: count the ack
+        auto rd = reads_.find(m.context);
+        if (rd != reads_.end() && voters_.count(m.from)) {
+          rd->second.acks.insert(m.from);
+          size_t n = 0;
+          for (uint64_t a : rd->second.acks) n += voters_.count(a);
+          if (n >= quorum()) {
+            const PendingRead pr = rd->second;
+            reads_.erase(rd);
+            read_done(m.context, pr.index, pr.from, true);
+          }
+        }
+      }
       if (it->second.match < last_index()) {
         if (it->second.next > last_index()) it->second.next = it->second.match + 1;
         send_append(m.from);
@@ -483,9 +562,16 @@ void Node::step_follower(const Message& m) {
       Message r;
       r.type = kMsgHeartbeatResp;
       r.to = m.from;
+      r.context = m.context;  // echo a ReadIndex round's id
       send(r);
       break;
     }
+    case kMsgReadIndex:  // we are not the leader (any more): the requester retries
+      read_done(m.context, 0, m.from, false);
+      break;
+    case kMsgReadIndexResp:
+      read_states_.push_back(ReadState{m.context, m.index, !m.reject});
+      break;
     case kMsgSnap:
       elapsed_ = 0;
       lead_ = m.from;

@@ -44,6 +44,17 @@ enum MsgType : uint8_t {
   kMsgSnap = 8,
   kMsgPropReject = 9,   // leader -> proposer: conf change refused (context = reason)
   kMsgLeaseRenew = 10,  // follower -> leader: keepalive forwarded (context = lease id)
+  kMsgReadIndex = 11,      // follower -> leader: linearizable read request (context = request id)
+  kMsgReadIndexResp = 12,  // leader -> follower: index = read index (reject: no leader term commit yet)
+};
+
+// A linearizable read confirmed by a quorum (ReadIndex): serve it locally once
+// the state machine has applied `index`.  ok == false: no leader, or the leader
+// has not committed an entry of its term yet -- retry.
+struct ReadState {
+  std::string ctx;
+  uint64_t index = 0;
+  bool ok = false;
 };
 
 struct Message {
@@ -100,6 +111,11 @@ class Node {
   void step(const Message& m);
   std::string propose(uint8_t type, const std::string& data);  // "" = accepted / forwarded
   void campaign();
+  // ReadIndex (Raft thesis 6.4): the leader records its commit index, confirms
+  // it is still the leader with one heartbeat round acknowledged by a quorum,
+  // and answers the index -- no log entry, no fsync.  A follower forwards the
+  // request to the leader.  Results come out of take_read_states().
+  void read_index(const std::string& ctx);
 
   // ---- outputs (drained by the owner)
   std::vector<Message> take_messages();
@@ -107,6 +123,7 @@ class Node {
   bool take_hardstate(HardState* hs);  // true if changed since the last take
   std::vector<Entry> take_committed(size_t max = 4096);  // (applied, commit]; advances applied
   bool take_snapshot(uint64_t* index, uint64_t* term, std::string* data);  // follower: install this first
+  std::vector<ReadState> take_read_states();
 
   // ---- membership (called by the applier when a conf change commits)
   void apply_conf_change(uint8_t type, uint64_t node);
@@ -152,6 +169,8 @@ class Node {
   void step_candidate(const Message& m);
   void step_follower(const Message& m);
   void reset_randomized_timeout();
+  void leader_read(const std::string& ctx, uint64_t from);
+  void read_done(const std::string& ctx, uint64_t index, uint64_t from, bool ok);
 
   Options opt_;
   uint64_t term_ = 0, vote_ = 0, lead_ = 0, commit_ = 0, applied_ = 0;
@@ -164,6 +183,13 @@ class Node {
   int elapsed_ = 0, hb_elapsed_ = 0, randomized_timeout_ = 10;
   uint64_t pending_conf_index_ = 0;
   std::mt19937_64 rng_;
+
+  struct PendingRead {
+    uint64_t index = 0, from = 0;
+    std::set<uint64_t> acks;
+  };
+  std::map<std::string, PendingRead> reads_;  // leader: awaiting a quorum of heartbeat acks
+  std::vector<ReadState> read_states_;
 
   std::vector<Message> msgs_;
   std::vector<Entry> unstable_;

@@ -46,6 +46,7 @@ namespace ptype {
 void launch_table_upsert(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int64_t,
                          uintptr_t, uintptr_t);
 void launch_table_delete(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t);
+void launch_table_upsert_packed(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, int64_t, uintptr_t, uintptr_t);
 void launch_table_lookup(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uintptr_t);
 void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
@@ -130,6 +131,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("table_upsert", &launch_table_upsert, py::arg("table"), py::arg("cap"), py::arg("keys"),
         py::arg("ranks"), py::arg("mboxes"), py::arg("exp_in"), py::arg("exp_tbl"), py::arg("n"),
         py::arg("stats"), py::arg("stream"));
+  m.def("table_upsert_packed", &launch_table_upsert_packed, py::arg("table"), py::arg("cap"), py::arg("entries"),
+        py::arg("exp_in"), py::arg("exp_tbl"), py::arg("n"), py::arg("stats"), py::arg("stream"));
   m.def("table_delete", &launch_table_delete, py::arg("table"), py::arg("cap"), py::arg("keys"), py::arg("n"),
         py::arg("stats"), py::arg("found"), py::arg("stream"));
   m.def("table_lookup", &launch_table_lookup, py::arg("table"), py::arg("cap"), py::arg("keys"), py::arg("n"),
@@ -250,9 +253,9 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<EpochEngine>(m, "EpochEngine",
                           "chunk-pipelined Send (route -> ncclAllToAll -> dispatch -> ncclAllToAll -> complete) "
                           "enqueued from one host call; comm = raw ncclComm_t or 0 for no collectives")
-      .def(py::init<int, uintptr_t, int, int, int64_t, int64_t, int, std::shared_ptr<FakeComm>>(), py::arg("device"),
-           py::arg("comm"), py::arg("R"), py::arg("rank"), py::arg("C"), py::arg("max_chunk"), py::arg("chunks"),
-           py::arg("fake") = nullptr)
+      .def(py::init<int, uintptr_t, int, int, int64_t, int64_t, int, std::shared_ptr<FakeComm>, bool, int64_t>(),
+           py::arg("device"), py::arg("comm"), py::arg("R"), py::arg("rank"), py::arg("C"), py::arg("max_chunk"),
+           py::arg("chunks"), py::arg("fake") = nullptr, py::arg("adaptive") = false, py::arg("c_fixed") = 0)
       .def(
           "set_bufs",
           [](EpochEngine& e, int i, uintptr_t send, uintptr_t recv, uintptr_t reply, uintptr_t back, uintptr_t perm,
@@ -285,6 +288,8 @@ PYBIND11_MODULE(_hip, m) {
              py::dict d = layout_dict(w.layout);
              d["req_words"] = w.req_words;
              d["rep_words"] = w.rep_words;
+             d["C"] = w.C;
+             d["C_alloc"] = w.C_alloc;
              d["meta"] = std::vector<uint64_t>(w.meta, w.meta + kMetaWords);
              return d;
            },

@@ -65,6 +65,7 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
                             const std::vector<uintptr_t>& direct, int self, uintptr_t stream);
 void launch_complete_packed(uintptr_t rep, int64_t C, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
                             uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream);
+void launch_hist_cap(uintptr_t hist, int64_t G, int R, uintptr_t meta, uintptr_t stream);
 
 // ---- RCCL entry points (from the library torch loaded)
 namespace engine_detail {
@@ -243,10 +244,15 @@ struct EngineSend {  // one Send: the batch, the registry, the outputs
 
 class EpochEngine {
  public:
+  // `C`: per-peer slot capacity the buffers were allocated for.  `adaptive`: with
+  // wire v3, each Send's slots are sized by the busiest bucket of the node,
+  // agreed in the same all-reduce as the layout (never above `C`).
+  // `c_fixed` (0: C): the capacity of Sends that do not adapt (wire v2).
   EpochEngine(int device, uintptr_t comm, int R, int rank, int64_t C, int64_t max_chunk, int chunks,
-              std::shared_ptr<FakeComm> fake = nullptr)
-      : device_(device), comm_((void*)comm), fake_(std::move(fake)), R_(R), rank_(rank), C_(C),
-        max_chunk_(max_chunk), chunks_(chunks) {
+              std::shared_ptr<FakeComm> fake = nullptr, bool adaptive = false, int64_t c_fixed = 0)
+      : device_(device), comm_((void*)comm), fake_(std::move(fake)), R_(R), rank_(rank), C_(C), C_alloc_(C),
+        C_fixed_(c_fixed > 0 && c_fixed <= C ? c_fixed : C), max_chunk_(max_chunk), chunks_(chunks),
+        adaptive_(adaptive) {
     if (R < 1 || chunks < 1 || max_chunk < 1) throw std::invalid_argument("EpochEngine: bad geometry");
     if (fake_ && (comm_ || fake_->size() != R || rank < 0 || rank >= R))
       throw std::invalid_argument("EpochEngine: fake communicator must match R and replace comm");
@@ -293,6 +299,8 @@ class EpochEngine {
   struct WireInfo {
     PackedLayout layout{};
     int64_t req_words = 0, rep_words = 0;
+    int64_t C = 0;        // per-peer slot capacity this Send used
+    int64_t C_alloc = 0;  // what the buffers hold
     uint64_t meta[kMetaWords] = {};
   };
   const WireInfo& last_wire() const { return wire_; }
@@ -351,7 +359,10 @@ class EpochEngine {
     if (nbufs_ < 1) throw std::runtime_error("EpochEngine: buffers not set");
     const hipStream_t cs = as_stream(a.stream);
     packed_ = a.packed && collectives();  // v3 only where bytes cross a collective
+    C_ = packed_ && adaptive_ && nbufs_ >= chunks_ ? C_alloc_ : C_fixed_;
     if (packed_) agree_layout(a, cs);
+    wire_.C = C_;
+    wire_.C_alloc = C_alloc_;
     const int64_t wq = packed_ ? packed_req_words(C_, L_.S) : wire_req_words(C_, a.nargs, a.mc);
     const int64_t wr = packed_ ? packed_rep_words(C_, L_.vb) : wire_rep_words(C_);
     if (packed_ && (wq > wire_req_words(C_, a.nargs, a.mc) || wr > wire_rep_words(C_)))
@@ -400,6 +411,9 @@ class EpochEngine {
     // Otherwise a separate width pass, and pass 1 of two chunks runs ahead.
     prepped_ = 0;
     const bool fused = nbufs_ >= chunks_ && meta_fused_;
+    // adaptive capacity needs every chunk's histograms before the agreement (a
+    // buffer set per chunk keeps them until its scatter)
+    const bool adapt = adaptive_ && nbufs_ >= chunks_;
     {
       Timed t(prof_.kernels_ns);
       if (fused) {
@@ -408,7 +422,10 @@ class EpochEngine {
       } else {
         launch_packed_meta(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.n_dir, a.affine_w,
                            (uintptr_t)meta_dev_, (uintptr_t)cs);
+        if (adapt) prep_all(a, cs);
       }
+      if (adapt)
+        for (int i = 0; i < chunks_; ++i) launch_hist_cap(bufs_[i].hist, prep_G_[i], R_, (uintptr_t)meta_dev_, (uintptr_t)cs);
     }
     // on the compute stream itself: the previous Send's collectives are complete
     // there already (its completions waited for them), and no cross-stream hop
@@ -418,7 +435,8 @@ class EpochEngine {
       PT_HIP_CHECK(hipMemcpy(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
       for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
       L_ = packed_layout(meta_host_);
-      if (!fused) prep_ahead(a, cs);
+      if (adapt) adapt_capacity();
+      else if (!fused) prep_ahead(a, cs);
       prof_.meta_ns += now() - t0;
       return;
     }
@@ -428,11 +446,33 @@ class EpochEngine {
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
     PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost, cs));
     PT_HIP_CHECK(hipEventRecord(ev_meta_out_, cs));
-    if (!fused) prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
+    if (!fused && !adapt) prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
     PT_HIP_CHECK(hipEventSynchronize(ev_meta_out_));
     for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
     L_ = packed_layout(meta_host_);
+    if (adapt) adapt_capacity();
     prof_.meta_ns += now() - t0;
+  }
+
+  // This Send's slot capacity: the node's busiest bucket, rounded up to 64 (at
+  // least 64, at most what the buffers hold -- beyond that the excess overflows
+  // into send_all's re-send rounds as before).
+  void adapt_capacity() {
+    const int64_t need = (int64_t)meta_host_[kMetaCap];
+    int64_t c = ((need + 63) / 64) * 64;
+    c = std::max<int64_t>(64, std::min<int64_t>(c, C_alloc_));
+    C_ = c;
+  }
+
+  // Route pass 1 of every chunk (adaptive capacity reads all histograms).
+  void prep_all(const EngineSend& a, hipStream_t cs) {
+    for (int i = 0; i < chunks_; ++i) {
+      const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
+      int64_t P;
+      prep_G_[i] = route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route,
+                              bufs_[i].hist, a.affine_w, (uintptr_t)cs, &P);
+    }
+    prepped_ = chunks_;
   }
 
   // Pass 1 of the route (route words + histograms; layout-independent) for the
@@ -461,8 +501,8 @@ class EpochEngine {
                         (const int64_t*)off(a.a2, lo, 8), (const uint16_t*)off(a.method_col, lo, 2),
                         (uint32_t)a.method_uniform, a.n_dir, a.affine_w, (unsigned long long*)meta_dev_};
       int64_t P;
-      route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route, bufs_[i].hist,
-                 a.affine_w, (uintptr_t)cs, &P, &mc);
+      prep_G_[i] = route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route,
+                              bufs_[i].hist, a.affine_w, (uintptr_t)cs, &P, &mc);
     }
     prepped_ = chunks_;
   }
@@ -615,8 +655,10 @@ class EpochEngine {
   void* comm_;
   std::shared_ptr<FakeComm> fake_;
   int R_, rank_;
-  int64_t C_, max_chunk_;
+  int64_t C_, C_alloc_, C_fixed_, max_chunk_;
   int chunks_;
+  bool adaptive_ = false;
+  int64_t prep_G_[8] = {};  // route blocks of each chunk's pass 1 (kMaxBufs)
   static constexpr int kMaxBufs = 8;  // chunks in flight without waiting for buffer reuse
   EngineBufs bufs_[kMaxBufs]{};
   int nbufs_ = 0;

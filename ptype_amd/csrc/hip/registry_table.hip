@@ -52,16 +52,33 @@ __device__ __forceinline__ uint64_t ld_key(const TableEntry* e) {
   return __hip_atomic_load(&e->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(256) void table_upsert_kernel(TableEntry* __restrict__ t, uint64_t mask,
-                                                           const uint64_t* __restrict__ keys,
-                                                           const uint32_t* __restrict__ ranks,
-                                                           const uint32_t* __restrict__ mboxes,
+// Upsert input: either SoA columns (keys / ranks / mboxes) or packed TableEntry
+// records as K7 writes them (`packed`, a restore: no host-side column split).
+struct UpsertIn {
+  const uint64_t* keys = nullptr;
+  const uint32_t* ranks = nullptr;
+  const uint32_t* mboxes = nullptr;
+  const TableEntry* packed = nullptr;
+  __device__ __forceinline__ void get(int64_t i, uint64_t& key, uint64_t& val) const {
+    if (packed) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&packed[i]);
+      key = ((uint64_t)v.y << 32) | v.x;
+      val = ((uint64_t)v.w << 32) | v.z;
+    } else {
+      key = keys[i];
+      val = ((uint64_t)mboxes[i] << 32) | ranks[i];
+    }
+  }
+};
+
+__global__ __launch_bounds__(256) void table_upsert_kernel(TableEntry* __restrict__ t, uint64_t mask, UpsertIn in,
                                                            const uint64_t* __restrict__ exp_in,
                                                            uint64_t* __restrict__ exp_tbl, int64_t n,
                                                            unsigned long long* __restrict__ stats) {
   unsigned long long added = 0, maxp = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t key = keys[i];
+    uint64_t key, v;
+    in.get(i, key, v);
     if (key == kKeyEmpty || key == kKeyTomb) continue;
     uint64_t h = probe_start(key, mask);
     uint64_t probe = 0;
@@ -81,7 +98,6 @@ __global__ __launch_bounds__(256) void table_upsert_kernel(TableEntry* __restric
       }
     }
     if (!ok) continue;  // table full: host sizes capacity >= 2x live, never hit in practice
-    uint64_t v = ((uint64_t)mboxes[i] << 32) | ranks[i];
     *reinterpret_cast<uint64_t*>(&t[h].rank) = v;
     if (exp_tbl) exp_tbl[h] = exp_in ? exp_in[i] : 0ull;
     if (probe > maxp) maxp = probe;
@@ -246,10 +262,24 @@ void launch_table_upsert(uintptr_t table, uint64_t cap, uintptr_t keys, uintptr_
                          uintptr_t exp_in, uintptr_t exp_tbl, int64_t n, uintptr_t stats, uintptr_t stream) {
   if (n <= 0) return;
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
-  hipLaunchKernelGGL(table_upsert_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream),
-                     (TableEntry*)table, cap - 1, (const uint64_t*)keys, (const uint32_t*)ranks,
-                     (const uint32_t*)mboxes, (const uint64_t*)exp_in, (uint64_t*)exp_tbl, n,
-                     (unsigned long long*)stats);
+  UpsertIn in;
+  in.keys = (const uint64_t*)keys;
+  in.ranks = (const uint32_t*)ranks;
+  in.mboxes = (const uint32_t*)mboxes;
+  hipLaunchKernelGGL(table_upsert_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), (TableEntry*)table,
+                     cap - 1, in, (const uint64_t*)exp_in, (uint64_t*)exp_tbl, n, (unsigned long long*)stats);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+// Restore (K7 inverse): re-insert packed TableEntry records (+ their deadlines).
+void launch_table_upsert_packed(uintptr_t table, uint64_t cap, uintptr_t entries, uintptr_t exp_in,
+                                uintptr_t exp_tbl, int64_t n, uintptr_t stats, uintptr_t stream) {
+  if (n <= 0) return;
+  if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
+  UpsertIn in;
+  in.packed = (const TableEntry*)entries;
+  hipLaunchKernelGGL(table_upsert_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), (TableEntry*)table,
+                     cap - 1, in, (const uint64_t*)exp_in, (uint64_t*)exp_tbl, n, (unsigned long long*)stats);
   PT_HIP_CHECK(hipGetLastError());
 }
 

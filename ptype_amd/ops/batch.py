@@ -122,6 +122,39 @@ def gen_requests(M: int, n_actors: int, method: int = METHOD_CALC_MULTIPLY, seed
     return out
 
 
+_ZIPF_CDF: dict = {}
+
+
+def zipf_actors(M: int, n_actors: int, s: float = 1.1, seed: int = 0, device="cuda",
+                scatter_seed: int = 99) -> torch.Tensor:
+    """Skewed client load: M actor ids with P(rank k) ~ 1 / k^s over n_actors (Zipf),
+    the popularity ranks scattered over the id space by a fixed permutation (hot
+    actors land on arbitrary GPUs).  int32[M] on ``device``."""
+    device = torch.device(device)
+    key = (int(n_actors), float(s), int(scatter_seed), str(device))
+    if key not in _ZIPF_CDF:
+        w = torch.arange(1, n_actors + 1, dtype=torch.float64).pow(-float(s))
+        cdf = torch.cumsum(w, 0)
+        cdf = (cdf / cdf[-1]).to(device)
+        perm = torch.randperm(n_actors, generator=torch.Generator().manual_seed(scatter_seed)).to(device)
+        _ZIPF_CDF[key] = (cdf, perm)
+    cdf, perm = _ZIPF_CDF[key]
+    g = torch.Generator(device=device).manual_seed(int(seed))
+    u = torch.rand(M, dtype=torch.float64, device=device, generator=g)
+    k = torch.searchsorted(cdf, u).clamp_(max=n_actors - 1)
+    return perm[k].to(torch.int32)
+
+
+def gen_zipf_requests(M: int, n_actors: int, s: float = 1.1, method: int = METHOD_CALC_MULTIPLY, seed: int = 0,
+                      device="cuda") -> MsgBatch:
+    """``gen_requests`` with Zipf(s) actor popularity."""
+    device = torch.device(device)
+    g = torch.Generator(device=device).manual_seed(int(seed) + 1)
+    a0 = torch.randint(-0x8000, 0x8000, (M,), dtype=torch.int64, device=device, generator=g)
+    a1 = torch.randint(0, 0x10000, (M,), dtype=torch.int64, device=device, generator=g)
+    return MsgBatch(zipf_actors(M, n_actors, s, seed, device), a0, a1, None, method)
+
+
 @dataclass(frozen=True)
 class WireFormat:
     """Epoch wire format v2 (see csrc/hip/batch.hip): which payload columns a

@@ -225,12 +225,24 @@ class RegistryTable:
         self.stats[STAT_GEN] += 1
 
     def load_packed(self, entries: torch.Tensor, expiry: torch.Tensor | None = None) -> None:
-        entries = entries.to(self.device)
-        keys = entries[:, 0].contiguous()
-        v = entries[:, 1]
-        ranks = (v & 0xFFFFFFFF).to(torch.int32)
-        mboxes = ((v >> 32) & 0xFFFFFFFF).to(torch.int32)
-        self.upsert(keys, ranks, mboxes, expiry)
+        """Re-insert packed K7 records (``int64[n, 2]`` = TableEntry, + deadlines).
+        On a GPU table: one host->device copy of each array (pinned sources copy
+        asynchronously) and one upsert kernel reading the records as they are."""
+        n = entries.shape[0]
+        if n == 0:
+            return
+        if not self.is_gpu:
+            keys = entries[:, 0].contiguous()
+            v = entries[:, 1]
+            self.upsert(keys, (v & 0xFFFFFFFF).to(torch.int32), ((v >> 32) & 0xFFFFFFFF).to(torch.int32), expiry)
+            return
+        ent = entries.to(self.device, non_blocking=True).contiguous()
+        exp = expiry.to(self.device, non_blocking=True).contiguous() if expiry is not None else None
+        if self.live + self.tombstones + n > self.cap * 3 // 4:
+            self._grow(self.live + n)
+        self._dir_dirty = True
+        hip().table_upsert_packed(_ptr(self.table), self.cap, _ptr(ent), _ptr(exp), _ptr(self.expiry), n,
+                                  _ptr(self.stats), _stream(self.table))
 
     def rebuild(self, min_capacity: int | None = None) -> None:
         """Drop tombstones: pack -> (resize) -> clear -> re-insert."""
@@ -251,22 +263,34 @@ class RegistryTable:
         self.rebuild(min_capacity=max(self.cap, 2 * need))
 
     # ---------------------------------------------------------- snapshot
-    def snapshot_to_host(self):
-        """Pack on device, then hipMemcpyAsync into pinned host DRAM on a side stream."""
-        entries, exp = self.pack()
+    def snapshot_to_host(self, stream: "torch.cuda.Stream | None" = None):
+        """K7 straight into pinned host DRAM: the pack kernel writes the live
+        entries and deadlines over PCIe into pinned buffers allocated ONCE per
+        table (reused by every later snapshot), so a snapshot is one kernel + an
+        8-B count read back -- no device staging, no per-snapshot pinned
+        allocation.  Runs on ``stream`` (default: a side stream behind the
+        current one); returns views ``(entries int64[n, 2], expiry int64[n])``
+        valid until the next snapshot of this table."""
         if not self.is_gpu:
+            entries, exp = self.pack()
             return entries.clone(), exp.clone()
-        side = torch.cuda.Stream(self.device)
+        if getattr(self, "_snap_cap", 0) < self.cap:
+            self._snap_ent = torch.empty(self.cap, 2, dtype=torch.int64, pin_memory=True)
+            self._snap_exp = torch.empty(self.cap, dtype=torch.int64, pin_memory=True)
+            self._snap_cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._snap_cnt_h = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._snap_cap = self.cap
+        side = stream if stream is not None else torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
-        h_ent = torch.empty(entries.shape, dtype=torch.int64, pin_memory=True)
-        h_exp = torch.empty(exp.shape, dtype=torch.int64, pin_memory=True)
         with torch.cuda.stream(side):
-            h_ent.copy_(entries, non_blocking=True)
-            h_exp.copy_(exp, non_blocking=True)
-            entries.record_stream(side)
-            exp.record_stream(side)
+            self._snap_cnt.zero_()
+            # the kernel stores through the pinned buffers' device mapping (UVA)
+            hip().table_pack(_ptr(self.table), self.cap, _ptr(self.expiry), _ptr(self._snap_ent),
+                             _ptr(self._snap_exp), _ptr(self._snap_cnt), side.cuda_stream)
+            self._snap_cnt_h.copy_(self._snap_cnt, non_blocking=True)
         side.synchronize()
-        return h_ent, h_exp
+        n = int(self._snap_cnt_h[0])
+        return self._snap_ent[:n], self._snap_exp[:n]
 
     # ---------------------------------------------------------- CPU reference
     def _slots(self):

@@ -44,6 +44,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 from dataclasses import dataclass
 
 import torch
@@ -143,7 +144,21 @@ class ActorExchange:
         self.state = state
         self.delay_us = delay_us
         self.fmt = fmt  # None: derived per send() from the batch's columns
-        self.bufs = [_ChunkBufs(self.world, self.C, self.max_chunk, self.device, self.force_collectives,
+        self.use_engine = self.device.type == "cuda" and os.environ.get("PTYPE_ENGINE", "1") != "0"
+        # wire format v3 (csrc/hip/packed.hpp): width-adaptive packed records on the
+        # all-to-alls, agreed per Send by one 16-word all-reduce (native engine, collectives on)
+        self.packed = os.environ.get("PTYPE_WIRE", "v3") != "v2" if packed is None else bool(packed)
+        # Adaptive slot capacity (native engine + wire v3): every Send's slots are sized
+        # by the node's busiest (rank, destination) bucket, agreed in the layout
+        # all-reduce; the buffers hold `skew_room` x the uniform share per peer, so
+        # skewed (Zipf) traffic fits without re-send rounds and uniform traffic moves
+        # less padding than the static mean + 8 sigma capacity
+        self.adaptive = bool(self.use_engine and self.packed and self.world > 1 and self.chunks <= 8
+                             and os.environ.get("PTYPE_ADAPTIVE_C", "1") != "0")
+        room = float(os.environ.get("PTYPE_SKEW_ROOM", "4"))
+        self.C_alloc = (max(self.C, min(self.max_chunk, int(math.ceil(room * self.max_chunk / self.world))))
+                        if self.adaptive else self.C)
+        self.bufs = [_ChunkBufs(self.world, self.C_alloc, self.max_chunk, self.device, self.force_collectives,
                                 fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 8))]
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
         self.outbox = None  # DeviceOutbox that dispatched handlers send into (set by pump)
@@ -158,10 +173,6 @@ class ActorExchange:
         self.direct = (d != "0") if d is not None else (self.world == 1)
         self.counters = EpochStats()
         self._engine = None  # native epoch engine, built on first GPU send
-        self.use_engine = self.device.type == "cuda" and os.environ.get("PTYPE_ENGINE", "1") != "0"
-        # wire format v3 (csrc/hip/packed.hpp): width-adaptive packed records on the
-        # all-to-alls, agreed per Send by one 16-word all-reduce (native engine, collectives on)
-        self.packed = os.environ.get("PTYPE_WIRE", "v3") != "v2" if packed is None else bool(packed)
         self._capturing = False  # a captured graph cannot host the v3 agreement (host wait)
         self.last_wire = None  # engine.last_wire() of the latest native send
 
@@ -191,11 +202,11 @@ class ActorExchange:
             h = B.hip()
             dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
             if self.fake is not None:
-                eng = h.EpochEngine(dev, 0, self.world, self.rank, self.C, self.max_chunk, self.chunks,
-                                    fake=self.fake[0])
+                eng = h.EpochEngine(dev, 0, self.world, self.rank, self.C_alloc, self.max_chunk, self.chunks,
+                                    fake=self.fake[0], adaptive=self.adaptive, c_fixed=self.C)
             else:
-                eng = h.EpochEngine(dev, self._comm_ptr(), self.world, self.rank, self.C, self.max_chunk,
-                                    self.chunks)
+                eng = h.EpochEngine(dev, self._comm_ptr(), self.world, self.rank, self.C_alloc, self.max_chunk,
+                                    self.chunks, adaptive=self.adaptive, c_fixed=self.C)
             for i, b in enumerate(self.bufs):
                 eng.set_bufs(i, b.send.data_ptr(), b.recv.data_ptr(), b.reply.data_ptr(), b.back.data_ptr(),
                              b.perm.data_ptr(), b.src.data_ptr(), b.rws.route.data_ptr(), b.rws.hist.data_ptr(),
@@ -401,16 +412,18 @@ class ActorExchange:
         return epochs, delivered
 
     # ------------------------------------------------------------------
-    def send_all(self, req: B.MsgBatch, max_epochs: int = 16):
-        """`send` + re-send of overflowed messages until every one is delivered
-        (host-synchronising: reads the overflow count once per epoch)."""
-        val, st = self.send(req)
+    def send_all(self, req: B.MsgBatch, max_epochs: int = 16, out: tuple | None = None):
+        """`send` + re-send of overflowed messages until every one is delivered.
+        Reads the overflow count once per epoch (a host round trip); with adaptive
+        slot capacity (native engine, wire v3) skewed traffic fits in the first
+        epoch and no re-send round runs."""
+        val, st = self.send(req, *(out or ()))
         for _ in range(max_epochs):
             over = st == STATUS_OVERFLOW
-            n_over = torch.tensor([int(over.sum())], device=self.device)
+            n_over = int(over.sum())
             if self.world > 1:
-                dist.all_reduce(n_over, group=self.group)
-            if int(n_over.item()) == 0:
+                n_over = self._agree_max(n_over)
+            if n_over == 0:
                 break
             idx = torch.nonzero(over).flatten()
             self.counters.resends += 1
@@ -418,6 +431,19 @@ class ActorExchange:
             val[idx] = v2
             st[idx] = s2
         return val, st
+
+    def _agree_max(self, v: int) -> int:
+        """Max of ``v`` over the group (every rank must take the same number of
+        re-send rounds).  In-process FakeComm ranks agree through a barrier; the
+        loopback stand-in is one rank that speaks for a symmetric node."""
+        if self.fake is None:
+            t = torch.tensor([v], dtype=torch.int64, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            return int(t.item())
+        fc = self.fake[0]
+        if fc.loopback:
+            return v
+        return _FakeAgree.of(fc).max(self.rank, v)
 
     def stats(self) -> EpochStats:
         c = self.counters
@@ -437,6 +463,33 @@ class ActorExchange:
             s.failed += m["failed"]
             s.mailbox = m
         return s
+
+
+class _FakeAgree:
+    """Max-agreement among the in-process ranks of one FakeComm (one thread each)."""
+
+    _by_comm: dict = {}
+    _lock = threading.Lock()
+
+    def __init__(self, R: int):
+        self.R = R
+        self.vals = [0] * R
+        self.barrier = threading.Barrier(R)
+
+    @classmethod
+    def of(cls, fc) -> "_FakeAgree":
+        with cls._lock:
+            a = cls._by_comm.get(id(fc))
+            if a is None:
+                a = cls._by_comm[id(fc)] = cls(int(fc.size))
+            return a
+
+    def max(self, rank: int, v: int) -> int:
+        self.vals[rank] = v
+        self.barrier.wait()
+        out = max(self.vals)
+        self.barrier.wait()  # nobody overwrites a value before every rank has read them
+        return out
 
 
 class SendGraph:

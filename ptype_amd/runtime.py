@@ -274,15 +274,22 @@ class DeviceRuntime:
 
     # ------------------------------------------------------------------ snapshots (C14)
     def snapshot_to_host(self) -> dict:
-        """Actor state + packed registry mirror, staged in pinned host DRAM by
-        hipMemcpyAsync on a side stream (the routing stream keeps running)."""
-        side = torch.cuda.Stream(self.device)
-        side.wait_stream(torch.cuda.current_stream(self.device))
-        h_state = torch.empty(self.state.shape, dtype=self.state.dtype, pin_memory=True)
-        with torch.cuda.stream(side):
-            h_state.copy_(self.state, non_blocking=True)
-        ent, exp = self.table.snapshot_to_host()
-        side.synchronize()
+        """Actor state + packed registry mirror in pinned host DRAM, on a side
+        stream (the routing stream keeps running): the state by one DMA copy, the
+        mirror by K7 writing straight into its pinned buffers.  The pinned
+        buffers are allocated once and reused; the returned tensors are views
+        valid until the next snapshot."""
+        side = torch.cuda.Stream(self.device) if self.on_gpu else None
+        if self.on_gpu:
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            if getattr(self, "_snap_state", None) is None or self._snap_state.numel() != self.state.numel():
+                self._snap_state = torch.empty(self.state.shape, dtype=self.state.dtype, pin_memory=True)
+            with torch.cuda.stream(side):
+                self._snap_state.copy_(self.state, non_blocking=True)
+            h_state = self._snap_state
+        else:
+            h_state = self.state.clone()
+        ent, exp = self.table.snapshot_to_host(side)
         return {"state": h_state, "table": ent, "expiry": exp,
                 "meta": torch.tensor([self.rank, self.world, self.actors], dtype=torch.int64)}
 
@@ -301,10 +308,21 @@ class DeviceRuntime:
         snap = load_file(path)
         if int(snap["meta"][2]) != self.actors:
             raise ValueError("snapshot actor count does not match this runtime")
-        self.state.copy_(snap["state"].to(self.device))
+        self.restore_from(snap)
+
+    def restore_from(self, snap: dict) -> None:
+        """Actor state and registry mirror from a snapshot dict (``snapshot_to_host``
+        output): one host->device copy each, the mirror re-inserted by one packed
+        upsert kernel."""
+        pin = self.on_gpu and not snap["state"].is_pinned()
+        st = snap["state"].pin_memory() if pin else snap["state"]
+        self.state.copy_(st, non_blocking=self.on_gpu)
         self.table.clear()
         if snap["table"].numel():
-            self.table.load_packed(snap["table"], snap["expiry"])
+            ent, exp = snap["table"], snap["expiry"]
+            if self.on_gpu and not ent.is_pinned():
+                ent, exp = ent.pin_memory(), exp.pin_memory()
+            self.table.load_packed(ent, exp)
 
     # ------------------------------------------------------------------ stats / teardown
     def stats(self) -> dict:

@@ -70,3 +70,10 @@ def test_bench_multi_gpu(nproc):
     assert out["n_gpus"] == nproc and out["value"] > 0
     assert out["config"]["wire"] == "v3-packed"
     assert out["p50_rtt_remote_us"] is not None and out["diag"]["a2a_only_ms_per_step"] > 0
+
+
+def test_bench_zipf_cpu():
+    """Skewed load (Zipf 1.1, pre-generated) through the 2-rank gloo pipeline."""
+    out = _run(2, ["--cpu", "--zipf", "1.1", "--no-secondary"] + SMALL, launcher="self")
+    assert out["config"]["load"] == "zipf(1.1)" and out["config"]["pregenerated"] is True
+    assert out["value"] > 0

@@ -129,3 +129,57 @@ def test_gpu_engine_loopback(R, chunks, sync, link, monkeypatch):
         assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1)
     assert ex.last_wire["S"] == 2
     assert ex._engine.stream_values == (sync == "values")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("adaptive", [True, False])
+def test_gpu_engine_zipf_skew_no_resend(adaptive, monkeypatch):
+    """Zipf(1.1) traffic on the R = 8 pipeline.  With adaptive capacity the agreed
+    slot size covers the busiest bucket: every message is delivered in ONE pass
+    (no overflow, no host re-send round); the static capacity (mean + 8 sigma)
+    overflows and needs send_all's rounds."""
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    monkeypatch.setenv("PTYPE_ADAPTIVE_C", "1" if adaptive else "0")
+    R, n, M = 8, 1 << 15, 200_000
+    fc = hip().FakeComm(R)
+    out, errors = [None] * R, []
+    start = threading.Barrier(R)
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                tab = RegistryTable(2 * n, device="cuda")
+                ids = torch.arange(n)
+                tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
+                tab.enable_directory(n, affine_world=R)
+                st = torch.zeros(n // R, dtype=torch.int64, device="cuda")
+                ex = ActorExchange(tab, M, chunks=2, state=st, fake=(fc, r))
+                req = B.gen_zipf_requests(M, n, 1.1, seed=10 + r, device="cuda")
+                start.wait()
+                v, sts = ex.send(req)  # one pass, no host re-send loop
+                s.synchronize()
+                over = int((sts == 4).sum())
+                ok = bool(torch.equal(v[sts == STATUS_OK], (req.a0 * req.a1)[sts == STATUS_OK]))
+                out[r] = (over, ok, ex.last_wire["C"], ex.last_wire["C_alloc"], ex.C)
+        except BaseException as e:  # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(R)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not errors, errors
+    Cs = {o[2] for o in out}
+    assert len(Cs) == 1  # every rank agreed on one capacity
+    for over, ok, C, C_alloc, C_static in out:
+        assert ok
+        if adaptive:
+            assert over == 0 and C > C_static  # the hot bucket needed more than mean + 8 sigma
+        else:
+            assert C == C_static
+    if not adaptive:
+        assert sum(o[0] for o in out) > 0  # static slots overflow under this skew

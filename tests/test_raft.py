@@ -167,3 +167,36 @@ def test_watch_on_follower_and_compaction(tmp_path, ports):
 
 class _Empty:
     events = []
+
+
+def test_linearizable_reads_use_read_index(tmp_path, ports):
+    """A linearizable Get is a ReadIndex round (leader commit index confirmed by a
+    quorum of heartbeat acks), not a log entry: reads leave the log untouched, and
+    a read on any member -- follower included -- sees every write acknowledged
+    before it started (reference: etcd's default linearizable Range,
+    cluster/store.go:38-53)."""
+    cfgs, ms = static_cluster(3, ports, tmp_path)
+    try:
+        leader_id = ms[0].leader()
+        follower = [i for i, m in enumerate(ms) if m.id != leader_id][0]
+        leader = [i for i, m in enumerate(ms) if m.id == leader_id][0]
+        w = _core.KvClient(eps(cfgs[leader]))
+        r = _core.KvClient(eps(cfgs[follower]))
+        w.put("x", b"0")
+        assert wait_for(lambda: ms[follower].status().applied == ms[leader].status().applied)
+        before = ms[leader].status().commit
+        for i in range(1, 40):
+            w.put("x", str(i).encode())  # acknowledged by the leader ...
+            assert [kv.value for kv in r.get("x").kvs] == [str(i).encode()]  # ... visible on the follower
+        after_writes = ms[leader].status().commit
+        assert after_writes - before == 39  # one entry per put, none per get
+        for _ in range(50):
+            r.get("x")
+        time.sleep(0.1)
+        assert ms[leader].status().commit == after_writes  # 50 linearizable reads: no log growth
+        assert ms[follower].reads_served >= 89
+        w.close()
+        r.close()
+    finally:
+        for m in ms:
+            m.close()

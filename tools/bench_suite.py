@@ -359,19 +359,36 @@ def registry(a):
     out["sweep_scan_ms"] = s * 1e3
     s = timed(lambda: t.pack())
     out["pack_ms"] = s * 1e3
+    # K7 straight into pinned host DRAM; the pinned buffers are allocated by the
+    # first snapshot of a table and reused (the first call is timed separately)
+    side = torch.cuda.Stream(dev)
     t0 = time.perf_counter()
-    h_ent, h_exp = t.snapshot_to_host()
-    el = time.perf_counter() - t0
+    h_ent, h_exp = t.snapshot_to_host(side)
+    out["snapshot_first_ms_incl_pinned_alloc"] = (time.perf_counter() - t0) * 1e3
+    els = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h_ent, h_exp = t.snapshot_to_host(side)
+        els.append(time.perf_counter() - t0)
+    el = min(els)
     nbytes = h_ent.numel() * 8 + h_exp.numel() * 8
     out["snapshot_to_pinned_ms"] = el * 1e3
+    out["snapshot_to_pinned_ms_median"] = sorted(els)[len(els) // 2] * 1e3
     out["snapshot_bytes"] = nbytes
     out["snapshot_gb_per_s"] = nbytes / el / 1e9
-    t2 = RegistryTable(2 * N, device=dev)
-    t0 = time.perf_counter()
-    t2.load_packed(h_ent, h_exp)
-    torch.cuda.synchronize()
-    out["restore_ms"] = (time.perf_counter() - t0) * 1e3
-    assert t2.live == N
+    out["table_scanned_bytes"] = t.cap * 24
+    rest = []
+    for _ in range(3):
+        t2 = RegistryTable(2 * N, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        t2.load_packed(h_ent, h_exp)  # one H2D copy per array + one packed upsert kernel
+        torch.cuda.synchronize()
+        rest.append(time.perf_counter() - t0)
+        assert t2.live == N
+    out["restore_ms"] = min(rest) * 1e3
+    out["restore_gb_per_s"] = nbytes / min(rest) / 1e9
     del B
     # control-plane store: puts through Raft with WAL + periodic snapshots
     from ptype_amd import cluster as C
@@ -393,6 +410,25 @@ def registry(a):
             c.Store.Put(C.background(), f"actors/{i}", "x" * 32)
         el = time.perf_counter() - t0
         out["store_puts_per_s_fsync"] = n_puts / el
+        # group commit: concurrent writers share one WAL fdatasync per raft-loop round
+        import threading
+
+        def writer(k):
+            for i in range(n_puts // 8):
+                c.Store.Put(C.background(), f"g{k}/{i}", "x" * 32)
+
+        ths = [threading.Thread(target=writer, args=(k,)) for k in range(8)]
+        t0 = time.perf_counter()
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        out["store_puts_per_s_fsync_8_writers"] = 8 * (n_puts // 8) / (time.perf_counter() - t0)
+        # linearizable reads: a ReadIndex round each, no log entry
+        c0 = c._c.member_status().commit
+        t0 = time.perf_counter()
+        for i in range(n_puts):
+            c.Store.Get(C.background(), f"actors/{i % 100}")
+        out["store_linearizable_gets_per_s"] = n_puts / (time.perf_counter() - t0)
+        out["store_log_entries_per_get"] = (c._c.member_status().commit - c0) / n_puts
         out["store_snapshot_on_disk"] = os.path.exists(os.path.join(d, "member", "snap.bin"))
     finally:
         c.Close()
