@@ -210,7 +210,8 @@ def main():
     def measure(table, steps, warmup, delivery=args.delivery):
         """Warm up, then time `steps` Sends (barrier + synchronize on both sides,
         max over ranks); returns (seconds, exchange, graph used)."""
-        ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake, delivery=delivery)
+        # the bench sends Calculator.Multiply only (stateless): mailboxes shard by arrival
+        ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake, delivery=delivery, mailbox_ordered=False)
         graph = None
         if use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
@@ -407,7 +408,7 @@ def main():
                     "slot_capacity_static": ex.C} if ex.last_wire is not None else {}),
                 "placement": args.placement,
                 "registry_lookup": route_mode,
-                "delivery": args.delivery if world == 1 and not dist_on else "direct",
+                "delivery": args.delivery,
                 **({"loopback_ranks": args.loopback, "link_gbps": args.link_gbps, "note": "profiling mode: rank 0 of a symmetric "
                     f"{args.loopback}-rank node, all-to-alls as local copies (not a headline number)"}
                    if fake else {}),

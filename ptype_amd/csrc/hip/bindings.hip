@@ -270,17 +270,17 @@ PYBIND11_MODULE(_hip, m) {
              int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
              uint32_t affine_w, int nargs, bool mc, uintptr_t out_val, uintptr_t out_st, uintptr_t state,
              uint32_t n_state, uint64_t delay_ticks, const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
-             bool direct, uintptr_t checksum, uintptr_t stream, bool packed) {
+             bool direct, uintptr_t checksum, uintptr_t stream, bool packed, uintptr_t mailboxes, bool ordered) {
             e.send(EngineSend{actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, affine_w,
                               nargs, mc, out_val, out_st, state, n_state, delay_ticks, outbox, outbox_cap, direct,
-                              checksum, stream, packed});
+                              checksum, stream, packed, mailboxes, ordered});
           },
           py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("method_col"),
           py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"),
           py::arg("affine_w"), py::arg("nargs"), py::arg("mc"), py::arg("out_val"), py::arg("out_st"),
           py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"), py::arg("outbox_cap"),
           py::arg("direct"), py::arg("checksum"), py::arg("stream"), py::arg("packed") = false,
-          py::call_guard<py::gil_scoped_release>())
+          py::arg("mailboxes") = 0, py::arg("ordered") = false, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("stream_values", &EpochEngine::stream_values)
       .def("last_wire",
            [](const EpochEngine& e) {
@@ -332,7 +332,9 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("slots", &Mailboxes::slots)
       .def_property_readonly("bytes", &Mailboxes::bytes)
       .def_property_readonly("consumer_processed", &Mailboxes::consumer_processed)
-      .def_property_readonly("launches", &Mailboxes::launches);
+      .def_property_readonly("launches", &Mailboxes::launches)
+      .def_property_readonly("handle", [](Mailboxes& m) { return (uintptr_t)&m; },
+                             "address of the C++ object (the epoch engine delivers into these mailboxes)");
   m.def("rccl_available", [] { return rccl().alltoall != nullptr; });
 
   py::class_<DeviceServer>(m, "DeviceServer")

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "mailbox.hpp"
 #include "packed.hpp"
 
 namespace ptype {
@@ -240,6 +241,8 @@ struct EngineSend {  // one Send: the batch, the registry, the outputs
   uintptr_t checksum;
   uintptr_t stream;  // the caller's compute stream
   bool packed;       // wire format v3 for this Send (needs collectives; not under graph capture)
+  uintptr_t mailboxes = 0;  // Mailboxes*: deliver on receipt through the HBM mailboxes (wire v2, no direct)
+  bool ordered = false;     // the batch may carry ordered methods (actor-sharded rings, ordered drain)
 };
 
 class EpochEngine {
@@ -542,7 +545,30 @@ class EpochEngine {
     const EngineBufs& b = bufs_[bi];
     if (collectives()) await(cs, kReqIn, bi);
     const int64_t m = m_of(a, i);
-    {
+    if (a.mailboxes) {  // K2 on receipt + K3: replies land in the reply regions
+      Timed t(prof_.kernels_ns);
+      const Mailboxes* mb = reinterpret_cast<const Mailboxes*>(a.mailboxes);
+      ReplyView rv;
+      rv.slots = (uint32_t*)b.reply;
+      rv.rep_words = wr;  // words per source region
+      rv.C = (uint32_t)C_;
+      rv.n = (uint64_t)R_ * (uint64_t)C_;
+      const uintptr_t src = collectives() ? b.recv : b.send;
+      launch_mailbox_enqueue_slots(mb->view(), src, R_, C_, a.nargs, a.mc, rv, std::max<int64_t>(1, m / R_),
+                                   !a.ordered, (uintptr_t)cs);
+      OutboxView ob;
+      if (a.outbox_cap) {
+        ob.actor = (uint32_t*)a.outbox[0];
+        ob.a0 = (int64_t*)a.outbox[1];
+        ob.a1 = (int64_t*)a.outbox[2];
+        ob.a2 = (int64_t*)a.outbox[3];
+        ob.method = (uint16_t*)a.outbox[4];
+        ob.count = (unsigned long long*)a.outbox[5];
+        ob.cap = a.outbox_cap;
+      }
+      // (no fixed-method drain: other ranks' slots may carry other methods)
+      launch_mailbox_drain(mb->view(), a.state, a.n_state, a.delay_ticks, ob, rv, a.ordered, (uintptr_t)cs, 0);
+    } else {
       Timed t(prof_.kernels_ns);
       if (packed_)
         launch_dispatch_packed(b.recv, R_, C_, L_, b.reply, a.state, a.n_state, a.delay_ticks, b.ws,

@@ -7,7 +7,11 @@
 #include "mailbox.hpp"
 #include "route_common.hpp"
 
+#include <algorithm>
+
 namespace ptype {
+
+int64_t wire_req_words(int64_t C, int nargs, bool mc);
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -72,6 +76,124 @@ __device__ __forceinline__ void block_add_stats(unsigned long long* stats, unsig
 }
 
 // ---------------------------------------------------------------- K2 enqueue
+// Reply of a message that never enters a ring, written at enqueue.
+__device__ __forceinline__ void write_status(const ReplyView& rv, uint32_t origin, int32_t status);
+
+// The common part of K2 for one tile of K * 256 messages already resolved to
+// (ok, mailbox, method, args, origin): per-shard ranks in LDS, ONE reservation
+// per (tile, shard), capacity check against the shard's head, the records
+// (B half + a2 first; with a live consumer drained before any tag half).
+// `hist` must hold zeros for this tile when called (the caller zeroed it
+// before its own loads; the barrier below orders that).
+template <bool LIVE, int K, bool ARRIVAL>
+__device__ __forceinline__ void enqueue_tile(const MboxView& mv, unsigned long long* base, unsigned long long* lim,
+                                             unsigned* hist, uint32_t tile_index, const bool (&in)[K],
+                                             const bool (&ok)[K], const uint32_t (&mb)[K],
+                                             const uint32_t (&meth)[K], const int64_t (&x0)[K],
+                                             const int64_t (&x1)[K], const int64_t (&x2)[K],
+                                             const uint32_t (&origin)[K], bool has_a2, const ReplyView& rv,
+                                             unsigned long long& n_enq, unsigned long long& n_ovf,
+                                             unsigned long long& n_miss) {
+  const uint32_t S = 1u << mv.log_s;
+  const uint64_t Q = 1ull << mv.log_q;
+  __syncthreads();  // hist zeroed
+  unsigned off[K];
+  const uint32_t tile_shard = tile_index & (S - 1);
+  if constexpr (ARRIVAL) {
+    // message-order compaction: rank = (item k, wave, lane) prefix of the valid flags
+    __shared__ unsigned wcnt[K][4];
+    const unsigned w = threadIdx.x / kWave;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t bal = __ballot(ok[k]);
+      off[k] = ok[k] ? mbcnt64(bal) : 0xffffffffu;
+      if (lane_id() == 0) wcnt[k][w] = (unsigned)__popcll(bal);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned run = 0;
+      for (int k = 0; k < K; ++k)
+        for (int q = 0; q < 4; ++q) {
+          const unsigned c = wcnt[k][q];
+          wcnt[k][q] = run;
+          run += c;
+        }
+      hist[tile_shard] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (off[k] != 0xffffffffu) off[k] += wcnt[k][w];
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) off[k] = ok[k] ? atomicAdd(&hist[mb[k] & (S - 1)], 1u) : 0xffffffffu;
+  }
+  __syncthreads();
+  uint32_t sh[K];  // ring of each message
+#pragma unroll
+  for (int k = 0; k < K; ++k) sh[k] = ARRIVAL ? tile_shard : mb[k] & (S - 1);
+  // ONE reservation per (tile, shard), and the capacity limit from the shard's head
+  for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
+    const unsigned c = hist[s];
+    if (c) {
+      base[s] = atomicAdd(ctr_tail(mv, s), (unsigned long long)c);
+      lim[s] = (LIVE ? ld_fresh(ctr_head(mv, s)) : *ctr_head(mv, s)) + Q;
+    }
+  }
+  __syncthreads();
+  uint64_t pos[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    pos[k] = ~0ull;
+    if (!in[k]) continue;
+    if (off[k] == 0xffffffffu) {
+      ++n_miss;
+      write_status(rv, origin[k], kStatusNoActor);
+      continue;
+    }
+    const uint32_t s = sh[k];
+    const uint64_t p = base[s] + off[k];
+    if (p >= lim[s]) {  // would overwrite an unconsumed record: a hole, answered now
+      ++n_ovf;
+      write_status(rv, origin[k], kStatusOverflow);
+      continue;
+    }
+    pos[k] = p;
+    uint32_t* rc = rec_at(mv, s, p);
+    const u32x4 hb = {(uint32_t)x0[k], (uint32_t)((uint64_t)x0[k] >> 32), (uint32_t)x1[k],
+                      (uint32_t)((uint64_t)x1[k] >> 32)};
+    const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
+    if constexpr (LIVE) {
+      st16_sc1(rc + 4, hb);
+      if (has_a2)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(mv.a2 + slot), (unsigned long long)x2[k],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *reinterpret_cast<u32x4*>(rc + 4) = hb;
+      if (has_a2) mv.a2[slot] = x2[k];
+    }
+  }
+  if constexpr (LIVE) vm_drain();  // every B half of this wave is out before its tags
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (pos[k] == ~0ull) continue;
+    const u32x4 ha = {lap_tag(mv, pos[k]), mb[k], origin[k],
+                      (meth[k] & 0xffffu) | ((uint32_t)(kFlagValid | kFlagRouted | (has_a2 ? kFlagA2 : 0)) << 16)};
+    uint32_t* rc = rec_at(mv, sh[k], pos[k]);
+    if constexpr (LIVE) st16_sc1(rc, ha);
+    else *reinterpret_cast<u32x4*>(rc) = ha;
+    ++n_enq;
+  }
+  if constexpr (LIVE) vm_drain();
+  __syncthreads();  // every wave's records are out: the tile's positions are done
+  if constexpr (LIVE) {
+    for (uint32_t s = threadIdx.x; s < S; s += blockDim.x)
+      if (hist[s]) atomicAdd(ctr_done(mv, s), (unsigned long long)hist[s]);
+  }
+  __syncthreads();  // LDS reused by the next tile
+}
+
+
 // One tile = K * 256 messages per block (item-major, coalesced).  LDS holds the
 // tile's per-shard counts, then each shard's reserved base and capacity limit.
 //
@@ -89,7 +211,6 @@ __global__ __launch_bounds__(256) void mailbox_enqueue_kernel(
     uint32_t aw, int aw_shift, int rank_self, uint32_t origin_base, ReplyView rv) {
   extern __shared__ unsigned long long lds_mb[];
   const uint32_t S = 1u << mv.log_s;
-  const uint64_t Q = 1ull << mv.log_q;
   unsigned long long* base = lds_mb;      // [S]
   unsigned long long* lim = lds_mb + S;   // [S]
   unsigned* hist = reinterpret_cast<unsigned*>(lds_mb + 2 * S);  // [S]
@@ -137,115 +258,73 @@ __global__ __launch_bounds__(256) void mailbox_enqueue_kernel(
         }
       }
     }
-    __syncthreads();  // hist zeroed
-    unsigned off[K];
-    const uint32_t tile_shard = (uint32_t)(tb / tile) & (S - 1);
-    if constexpr (ARRIVAL) {
-      // message-order compaction: rank = (item k, wave, lane) prefix of the valid flags
-      __shared__ unsigned wcnt[K][4];
-      const unsigned w = threadIdx.x / kWave;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const bool ok = r[k] == rank_self && mb[k] < kMaxMbox;
-        const uint64_t bal = __ballot(ok);
-        off[k] = ok ? mbcnt64(bal) : 0xffffffffu;
-        if (lane_id() == 0) wcnt[k][w] = (unsigned)__popcll(bal);
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        unsigned run = 0;
-        for (int k = 0; k < K; ++k)
-          for (int q = 0; q < 4; ++q) {
-            const unsigned c = wcnt[k][q];
-            wcnt[k][q] = run;
-            run += c;
-          }
-        hist[tile_shard] = run;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (off[k] != 0xffffffffu) off[k] += wcnt[k][w];
-    } else {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const bool ok = r[k] == rank_self && mb[k] < kMaxMbox;
-        off[k] = ok ? atomicAdd(&hist[mb[k] & (S - 1)], 1u) : 0xffffffffu;
-      }
-    }
-    __syncthreads();
-    uint32_t sh[K];  // ring of each message
-#pragma unroll
-    for (int k = 0; k < K; ++k) sh[k] = ARRIVAL ? tile_shard : mb[k] & (S - 1);
-    // ONE reservation per (tile, shard), and the capacity limit from the shard's head
-    for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
-      const unsigned c = hist[s];
-      if (c) {
-        base[s] = atomicAdd(ctr_tail(mv, s), (unsigned long long)c);
-        lim[s] = (LIVE ? ld_fresh(ctr_head(mv, s)) : *ctr_head(mv, s)) + Q;
-      }
-    }
-    __syncthreads();
-    // half B (and a2) first; with a live consumer they are drained before any tag goes out
-    uint64_t pos[K];
+    bool in[K], ok[K];
+    uint32_t meth[K], org[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int64_t i = tb + k * (int64_t)blockDim.x + threadIdx.x;
-      pos[k] = ~0ull;
-      if (i >= M) continue;
-      if (off[k] == 0xffffffffu) {
-        ++n_miss;
-        if ((uint64_t)(origin_base + i) < rv.n) {
-          rv.val[origin_base + i] = 0;
-          rv.st[origin_base + i] = kStatusNoActor;
-        }
-        continue;
-      }
-      const uint32_t s = sh[k];
-      const uint64_t p = base[s] + off[k];
-      if (p >= lim[s]) {  // would overwrite an unconsumed record: a hole, answered now
-        ++n_ovf;
-        if ((uint64_t)(origin_base + i) < rv.n) {
-          rv.val[origin_base + i] = 0;
-          rv.st[origin_base + i] = kStatusOverflow;
-        }
-        continue;
-      }
-      pos[k] = p;
-      uint32_t* rc = rec_at(mv, s, p);
-      const u32x4 hb = {(uint32_t)x0[k], (uint32_t)((uint64_t)x0[k] >> 32), (uint32_t)x1[k],
-                        (uint32_t)((uint64_t)x1[k] >> 32)};
-      const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
-      if constexpr (LIVE) {
-        st16_sc1(rc + 4, hb);
-        if (a2) __hip_atomic_store(reinterpret_cast<unsigned long long*>(mv.a2 + slot), (unsigned long long)x2[k],
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      in[k] = i < M;
+      ok[k] = in[k] && r[k] == rank_self && mb[k] < kMaxMbox;
+      meth[k] = in[k] ? (mcol ? (uint32_t)mcol[i] : method_uniform) : 0u;
+      org[k] = origin_base + (uint32_t)i;
+    }
+    enqueue_tile<LIVE, K, ARRIVAL>(mv, base, lim, hist, (uint32_t)(tb / tile), in, ok, mb, meth, x0, x1, x2, org,
+                                   a2 != nullptr, rv, n_enq, n_ovf, n_miss);
+  }
+  block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
+}
+
+// ---------------------------------------------------------------- K2 on receipt
+// At N > 1 the records arrive in the epoch's request regions (wire v2, already
+// routed by the sender: word 0 is the local mailbox).  grid (X, R): block (x, d)
+// tiles source rank d's region; origin = d * C + slot position, so the drain
+// answers straight into the reply region the reverse all-to-all returns.
+template <int NARGS, bool MC, int K, bool ARRIVAL>
+__global__ __launch_bounds__(256) void mailbox_enqueue_slots_kernel(MboxView mv, const uint32_t* __restrict__ recv,
+                                                                    int64_t req_words, uint32_t C, ReplyView rv) {
+  extern __shared__ unsigned long long lds_mb[];
+  const uint32_t S = 1u << mv.log_s;
+  unsigned long long* base = lds_mb;
+  unsigned long long* lim = lds_mb + S;
+  unsigned* hist = reinterpret_cast<unsigned*>(lds_mb + 2 * S);
+  constexpr int kStride = 1 + (MC ? 1 : 0) + 2 * NARGS;
+  const int d = blockIdx.y;
+  const uint32_t* rq = recv + (int64_t)d * req_words;
+  const uint4 h = *reinterpret_cast<const uint4*>(rq);
+  const bool valid = (h.w >> 16) & kFlagValid;
+  const int64_t count = valid ? (int64_t)(h.x < C ? h.x : C) : 0;
+  const uint32_t hm = h.w & 0xffffu;
+  if (blockIdx.x == 0 && threadIdx.x == 0)  // reply header: delivered count (as the dispatch writes it)
+    *reinterpret_cast<uint4*>(rv.slots + (int64_t)d * rv.rep_words) = make_uint4((uint32_t)count, 0u, 0u, 0u);
+  const int64_t tile = (int64_t)K * blockDim.x;
+  unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0;
+  for (int64_t tb = blockIdx.x * tile; tb < count; tb += (int64_t)gridDim.x * tile) {
+    for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) hist[s] = 0;
+    bool in[K], ok[K];
+    uint32_t mb[K], meth[K], org[K];
+    int64_t x0[K], x1[K], x2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = tb + k * (int64_t)blockDim.x + threadIdx.x;
+      in[k] = i < count;
+      uint32_t wv[kStride];
+      if (in[k]) {
+        load_words<kStride>(rq + 4 + i * kStride, wv);
       } else {
-        *reinterpret_cast<u32x4*>(rc + 4) = hb;
-        if (a2) mv.a2[slot] = x2[k];
-      }
-    }
-    if constexpr (LIVE) vm_drain();  // every B half of this wave is out before its tags
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (pos[k] == ~0ull) continue;
-      const int64_t i = tb + k * (int64_t)blockDim.x + threadIdx.x;
-      const uint32_t s = sh[k];
-      const uint32_t meth = mcol ? (uint32_t)mcol[i] : method_uniform;
-      const u32x4 ha = {lap_tag(mv, pos[k]), mb[k], (uint32_t)(origin_base + i),
-                        (meth & 0xffffu) | ((uint32_t)(kFlagValid | kFlagRouted | (a2 ? kFlagA2 : 0)) << 16)};
-      uint32_t* rc = rec_at(mv, s, pos[k]);
-      if constexpr (LIVE) st16_sc1(rc, ha);
-      else *reinterpret_cast<u32x4*>(rc) = ha;
-      ++n_enq;
+        for (int j = 0; j < kStride; ++j) wv[j] = 0;
+      }
+      constexpr int o = 1 + (MC ? 1 : 0);
+      mb[k] = wv[0];
+      meth[k] = MC ? (wv[1] & 0xffffu) : hm;
+      x0[k] = (int64_t)(((uint64_t)wv[o + 1] << 32) | wv[o]);
+      x1[k] = NARGS > 1 ? (int64_t)(((uint64_t)wv[o + 3] << 32) | wv[o + 2]) : 0;
+      x2[k] = NARGS > 2 ? (int64_t)(((uint64_t)wv[o + 5] << 32) | wv[o + 4]) : 0;
+      ok[k] = in[k] && mb[k] < kMaxMbox;
+      org[k] = (uint32_t)d * C + (uint32_t)i;
     }
-    if constexpr (LIVE) vm_drain();
-    __syncthreads();  // every wave's records are out: the tile's positions are done
-    if constexpr (LIVE) {
-      for (uint32_t s = threadIdx.x; s < S; s += blockDim.x)
-        if (hist[s]) atomicAdd(ctr_done(mv, s), (unsigned long long)hist[s]);
-    }
-    __syncthreads();  // LDS reused by the next tile
+    enqueue_tile<false, K, ARRIVAL>(mv, base, lim, hist, (uint32_t)(d * 4096 + tb / tile), in, ok, mb, meth, x0, x1,
+                                    x2, org, NARGS > 2, rv, n_enq, n_ovf, n_miss);
   }
   block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
 }
@@ -270,11 +349,23 @@ __device__ __forceinline__ MboxMsg decode(const u32x4& ha, const u32x4& hb, cons
   return x;
 }
 
-__device__ __forceinline__ void write_reply(const ReplyView& rv, uint32_t origin, const ReplyRecord& r) {
-  if ((uint64_t)origin < rv.n) {
-    rv.val[origin] = r.value;
-    rv.st[origin] = r.status;
+__device__ __forceinline__ void put_reply(const ReplyView& rv, uint32_t origin, int64_t value, int32_t status) {
+  if ((uint64_t)origin >= rv.n) return;
+  if (rv.slots) {  // wire v2 reply regions: values int64[C] then statuses u8[C] per source rank
+    const uint32_t d = origin / rv.C, pos = origin - d * rv.C;
+    uint32_t* rb = rv.slots + (int64_t)d * rv.rep_words;
+    reinterpret_cast<int64_t*>(rb + 4)[pos] = value;
+    reinterpret_cast<uint8_t*>(rb + 4 + 2 * (int64_t)rv.C)[pos] = (uint8_t)status;
+    return;
   }
+  rv.val[origin] = value;
+  rv.st[origin] = status;
+}
+__device__ __forceinline__ void write_reply(const ReplyView& rv, uint32_t origin, const ReplyRecord& r) {
+  put_reply(rv, origin, r.value, r.status);
+}
+__device__ __forceinline__ void write_status(const ReplyView& rv, uint32_t origin, int32_t status) {
+  put_reply(rv, origin, 0, status);
 }
 
 // Run one window of up to 64 records (lane l holds ring position h + l) in ring
@@ -561,6 +652,36 @@ void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, u
   }
 #undef PT_ENQ
 #undef PT_ENQA
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_mailbox_enqueue_slots(const MboxView& mv, uintptr_t recv, int R, int64_t C, int nargs, bool mc,
+                                  const ReplyView& rv, int64_t expected_per_rank, bool arrival, uintptr_t stream) {
+  if (R < 1 || C < 1 || !rv.slots || rv.C != (uint32_t)C) throw std::invalid_argument("mailbox enqueue slots: geometry");
+  if (nargs > 2 && !mv.a2) throw std::invalid_argument("mailbox enqueue: 3-argument records but no a2 array");
+  if ((uint64_t)R * (uint64_t)C > 0xffffffffull) throw std::invalid_argument("mailbox enqueue: origin > u32");
+  constexpr int K = 4;
+  const int64_t req_words = wire_req_words(C, nargs, mc);
+  const uint32_t S = 1u << mv.log_s;
+  const size_t lds = (size_t)S * (8 + 8 + 4);
+  const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
+  const dim3 g(mb_grid(per, 256 * K, (unsigned)std::max(1, 4096 / R)), (unsigned)R);
+#define PT_ENQS(NA, MCV)                                                                                           \
+  if (arrival)                                                                                                    \
+    hipLaunchKernelGGL((mailbox_enqueue_slots_kernel<NA, MCV, K, true>), g, dim3(256), lds, as_stream(stream), mv, \
+                       (const uint32_t*)recv, req_words, (uint32_t)C, rv);                                        \
+  else                                                                                                            \
+    hipLaunchKernelGGL((mailbox_enqueue_slots_kernel<NA, MCV, K, false>), g, dim3(256), lds, as_stream(stream), mv, \
+                       (const uint32_t*)recv, req_words, (uint32_t)C, rv);
+  switch (nargs * 2 + (mc ? 1 : 0)) {
+    case 2: PT_ENQS(1, false) break;
+    case 3: PT_ENQS(1, true) break;
+    case 4: PT_ENQS(2, false) break;
+    case 5: PT_ENQS(2, true) break;
+    case 6: PT_ENQS(3, false) break;
+    default: PT_ENQS(3, true) break;
+  }
+#undef PT_ENQS
   PT_HIP_CHECK(hipGetLastError());
 }
 

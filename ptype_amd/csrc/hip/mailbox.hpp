@@ -82,17 +82,25 @@ struct alignas(64) MboxCtrl {
   uint64_t pad[3];
 };
 
-// Where replies go: SoA outputs indexed by the record's origin (out_n bounds it).
+// Where replies go, indexed by the record's origin (< n): SoA outputs (a local
+// Send: origin = message index), or -- mailbox delivery on receipt at N > 1 --
+// the epoch's wire-v2 reply regions (origin = source rank * C + slot position),
+// which the reverse all-to-all takes back to the senders.
 struct ReplyView {
   int64_t* val = nullptr;
   int32_t* st = nullptr;
   uint64_t n = 0;
+  uint32_t* slots = nullptr;
+  int64_t rep_words = 0;
+  uint32_t C = 0;
 };
 
 void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2,
                             uintptr_t method_col, int method_uniform, int64_t M, uintptr_t table, uint64_t cap,
                             uintptr_t dir, uint32_t n_dir, uint32_t affine_w, int rank_self, uint32_t origin_base,
                             const ReplyView& rv, bool live, uintptr_t stream, bool arrival = false);
+void launch_mailbox_enqueue_slots(const MboxView& mv, uintptr_t recv, int R, int64_t C, int nargs, bool mc,
+                                  const ReplyView& rv, int64_t expected_per_rank, bool arrival, uintptr_t stream);
 void launch_mailbox_drain(const MboxView& mv, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
                           const OutboxView& ob, const ReplyView& rv, bool ordered, uintptr_t stream,
                           int fixed_method = 0);

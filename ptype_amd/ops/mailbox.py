@@ -54,6 +54,11 @@ class Mailboxes:
     def bytes(self) -> int:
         return int(self._m.bytes)
 
+    @property
+    def handle(self) -> int:
+        """Address of the native object: the epoch engine delivers received records into it."""
+        return int(self._m.handle)
+
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 

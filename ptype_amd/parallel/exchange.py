@@ -102,7 +102,7 @@ class ActorExchange:
     def __init__(self, table: RegistryTable, max_batch: int, chunks: int = 1, group=None, state=None,
                  delay_us: int = 0, slack: float = 0.01, fmt: B.WireFormat | None = None,
                  packed: bool | None = None, fake=None, delivery: str = "auto", mailbox_shards: int = 256,
-                 mailbox_slots: int = 0):
+                 mailbox_slots: int = 0, mailbox_ordered: bool | None = None):
         if delivery not in ("auto", "direct", "mailbox"):
             raise ValueError("delivery: 'auto', 'direct' or 'mailbox'")
         # How a message reaches its actor on the GPU that hosts it (world 1):
@@ -111,7 +111,14 @@ class ActorExchange:
         #   mailbox -- through the HBM mailboxes (ops/mailbox.py): FIFO per actor, ordered
         #              methods one at a time per actor
         #   auto    -- mailbox for a uniform ordered method, direct otherwise
+        # With more ranks the receiver cannot see what the other ranks sent, so there
+        # the choice is the exchange's (same on every rank): "mailbox" delivers on
+        # receipt (K2 from the request regions, wire v2) into actor-sharded rings with
+        # the ordered drain -- unless `mailbox_ordered=False` promises that no ordered
+        # method is ever sent (then arrival-sharded rings, streaming drain); "auto"
+        # and "direct" dispatch directly (ordered methods as linearizable CAS updates).
         self.delivery = delivery
+        self.mailbox_ordered = True if mailbox_ordered is None else bool(mailbox_ordered)
         self.mailbox_shards = int(mailbox_shards)
         self.mailbox_slots = int(mailbox_slots)
         self.mailboxes = None
@@ -223,17 +230,24 @@ class ActorExchange:
         d, n_dir, affine = self.table.directory()
         ob, ob_cap = self.outbox.view() if self.outbox is not None else ([], 0)
         state = self.state
+        mb = self._mailboxes().handle if self._mailbox_on_receipt() else 0
         self._get_engine().send(
             B._ptr(req.actor), B._ptr(req.a0), B._ptr(req.a1), B._ptr(req.a2), B._ptr(mcol),
             int(req.method) if uniform else 0, req.M, B._ptr(self.table.table), self.table.cap, B._ptr(d), n_dir,
             affine, fmt.nargs, fmt.method_col, B._ptr(out_val), B._ptr(out_status), B._ptr(state),
-            0 if state is None else state.numel(), int(self.delay_us) * 100, ob, ob_cap, self.direct,
-            B._ptr(self.checksum), torch.cuda.current_stream(self.device).cuda_stream, self.packed_active())
+            0 if state is None else state.numel(), int(self.delay_us) * 100, ob, ob_cap, self.direct and not mb,
+            B._ptr(self.checksum), torch.cuda.current_stream(self.device).cuda_stream, self.packed_active() and not mb,
+            mb, self.mailbox_ordered)
         if self.world > 1 or self.force_collectives:
             w = self._engine.last_wire()
             self.last_wire = w
             self.counters.wire_bytes += self.chunks * 4 * (w["req_words"] + w["rep_words"])
         return out_val, out_status
+
+    def _mailbox_on_receipt(self) -> bool:
+        """N > 1 (or forced collectives): received records go through the mailboxes."""
+        return (self.delivery == "mailbox" and self.device.type == "cuda"
+                and (self.world > 1 or self.force_collectives))
 
     def _use_mailbox(self, req: B.MsgBatch) -> bool:
         if self.device.type != "cuda" or self.world > 1 or self.force_collectives or self.delivery == "direct":
@@ -263,7 +277,7 @@ class ActorExchange:
     def packed_active(self) -> bool:
         """Whether the next native send uses wire format v3."""
         return bool(self.packed and self.use_engine and not self._capturing
-                    and (self.world > 1 or self.force_collectives))
+                    and (self.world > 1 or self.force_collectives) and not self._mailbox_on_receipt())
 
     # ------------------------------------------------------------------
     def _a2a(self, out, inp):

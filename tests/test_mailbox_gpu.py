@@ -183,3 +183,66 @@ def test_mailbox_send_graph_replay():
         g.replay()
         torch.cuda.synchronize()
         assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1)
+
+
+@pytest.mark.parametrize("R,ordered", [(4, True), (3, False)])
+def test_mailbox_delivery_on_receipt_multirank(R, ordered):
+    """N > 1: every rank's received records go through its HBM mailboxes (K2 on
+    receipt from the request regions, K3 into the reply regions), on the engine's
+    real multi-rank pipeline (FakeComm ranks, one GPU).  Ordered: SeqFold traffic
+    from every rank to every rank's actors, audited per actor across all senders
+    (exactly once, serialised).  Unordered: calculator replies exact."""
+    import threading
+
+    from ptype_amd.ops import hip
+
+    n, M = 4096, 60_000
+    fc = hip().FakeComm(R)
+    res, errors = [None] * R, []
+    start = threading.Barrier(R)
+    states0 = [torch.randint(0, 1 << 30, (n // R + 1,), dtype=torch.int64, generator=torch.Generator().manual_seed(r))
+               for r in range(R)]
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                tab = RegistryTable(2 * n, device="cuda")
+                ids = torch.arange(n)
+                tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
+                tab.enable_directory(n, affine_world=R)
+                st = states0[r].to("cuda")
+                ex = ActorExchange(tab, M, chunks=2, state=st, fake=(fc, r), delivery="mailbox",
+                                   mailbox_ordered=ordered, mailbox_shards=64)
+                req = fold_batch(M, n, 300 + r) if ordered else B.gen_requests(M, n, METHOD_CALC_MULTIPLY,
+                                                                                 seed=300 + r, device="cuda")
+                start.wait()
+                v, sts = ex.send(req)
+                s.synchronize()
+                res[r] = (req.actor.cpu().long(), req.a0.cpu(), None if ordered else req.a1.cpu(), v.cpu(), sts.cpu(),
+                          st.cpu(), ex.stats().mailbox)
+        except BaseException as e:  # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    ths = [threading.Thread(target=run, args=(r,)) for r in range(R)]
+    [t.start() for t in ths]
+    [t.join(timeout=240) for t in ths]
+    assert not errors, errors
+    for r in range(R):
+        assert res[r][6]["processed"] > 0 and res[r][6]["enqueued"] == res[r][6]["processed"]
+    if not ordered:
+        for actor, a0, a1, v, sts, _, _ in res:
+            assert bool((sts == STATUS_OK).all()) and torch.equal(v, a0 * a1)
+        return
+    actor = torch.cat([x[0] for x in res])
+    a0 = torch.cat([x[1] for x in res])
+    v = torch.cat([x[3] for x in res])
+    sts = torch.cat([x[4] for x in res])
+    # global mailbox key: owner rank * (n // R + 1) + local mailbox
+    P = n // R + 1
+    key = (actor % R) * P + actor // R
+    before = torch.cat(states0)
+    after = torch.cat([x[5] for x in res])
+    ok, info = audit_fold(key, a0, v, sts, before, after)
+    assert ok, info

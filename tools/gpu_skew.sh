@@ -20,6 +20,8 @@ PTYPE_ADAPTIVE_C=0 timeout -k 10 200 python bench.py $COMMON --pregen >> $OUT 2>
 python - "$OUT" <<'PY'
 import json, sys
 for ln in open(sys.argv[1]):
+    if not ln.startswith("{"):
+        continue
     d = json.loads(ln); c = d["config"]
     print(c.get("load"), "C", c.get("slot_capacity"), "/", c.get("slot_capacity_alloc"), "static", c.get("slot_capacity_static"),
           "resends", c.get("resend_rounds"), "ms/step %.3f" % d["ms_per_step"], "G msg/s %.1f" % (d["value"] / 1e9))
