@@ -92,6 +92,41 @@ def _spawn_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+_LIVE_EXCHANGES: list = []  # for the hang watchdog
+
+
+def _hang_watchdog(after_s: float, rank: int) -> None:
+    """Diagnosis mode (PTYPE_HANG_DIAG=<seconds>): if the run has not finished
+    after that long, print every engine's hand-off words (signalled sequence vs
+    value the GPU wrote) and whether its streams drained, then exit -- the main
+    thread is blocked inside a synchronisation and cannot report."""
+    import threading
+
+    import torch
+
+    def dump():
+        print(f"[rank {rank}] HANG after {after_s:.0f} s", file=sys.stderr, flush=True)
+        names = ["routed", "req_in", "served", "rep_in"]
+        for ex in _LIVE_EXCHANGES:
+            eng = ex._engine
+            if eng is None:
+                continue
+            st = eng.hang_state(torch.cuda.current_stream(ex.device).cuda_stream)
+            for k in range(32):
+                seq, val = st[2 * k], st[2 * k + 1]
+                if seq or val > 0:
+                    print(f"  {names[k // 8]}[buf {k % 8}]: signalled {seq}, GPU wrote {val}"
+                          + ("   <-- behind" if val >= 0 and val < seq else ""), file=sys.stderr, flush=True)
+            print(f"  compute stream drained: {bool(st[64])}, comm stream drained: {bool(st[65])}, "
+                  f"layout agreement done: {bool(st[66])}, route kernels done per chunk: {st[67:75]}",
+                  file=sys.stderr, flush=True)
+        os._exit(3)
+
+    t = threading.Timer(after_s, dump)
+    t.daemon = True
+    t.start()
+
+
 def place_actors(n_actors: int, world: int, placement: str, seed: int = 1234):
     """(rank, mailbox) of every actor id: the same on every rank (CPU generator).
     random: a uniformly random bijection onto rank-major mailbox slots, so each
@@ -212,6 +247,8 @@ def main():
         max over ranks); returns (seconds, exchange, graph used)."""
         # the bench sends Calculator.Multiply only (stateless): mailboxes shard by arrival
         ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake, delivery=delivery, mailbox_ordered=False)
+        if os.environ.get("PTYPE_HANG_DIAG"):
+            _LIVE_EXCHANGES.append(ex)
         graph = None
         if use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
@@ -257,6 +294,8 @@ def main():
         return elapsed, ex, graph is not None
 
     table = build_table(args.placement)
+    if os.environ.get("PTYPE_HANG_DIAG"):
+        _hang_watchdog(float(os.environ.get("PTYPE_HANG_DIAG") or 30), rank)
     elapsed, ex, graphed = measure(table, args.steps, args.warmup)
     def lookup_mode(t):
         if t.dir is None:

@@ -56,7 +56,9 @@ extern const char* kStorePrefix;  // "store"
 
 // clientv3.OpOption equivalents (cluster/store_config.go:33-103)
 struct OpOption {
-  enum Kind { kPrefix, kLimit, kRev, kRange, kFromKey, kSerializable, kKeysOnly, kCountOnly, kSort, kLease } kind;
+  enum Kind { kPrefix, kLimit, kRev, kRange, kFromKey, kSerializable, kKeysOnly, kCountOnly, kSort, kLease };
+  OpOption(Kind k = kPrefix) : kind(k) {}  // NOLINT: implicit from a kind, as the option helpers build them
+  Kind kind;
   int64_t n = 0;
   std::string s;
   int target = 0, order = 0;

@@ -71,7 +71,7 @@ static gob::Value to_gob(py::handle o) {
   if (py::isinstance<py::bytes>(o)) return gob::Value::Bytes(o.cast<std::string>());
   if (py::hasattr(o, "__dataclass_fields__")) {
     py::object fields = py::module_::import("dataclasses").attr("fields")(o);
-    gob::Value v = gob::Value::Struct(py::str(o.get_type().attr("__name__")).cast<std::string>());
+    gob::Value v = gob::Value::Struct(py::str(py::type::handle_of(o).attr("__name__")).cast<std::string>());
     for (auto f : fields) {
       const std::string n = f.attr("name").cast<std::string>();
       v.fields.emplace_back(n, to_gob(o.attr(n.c_str())));
@@ -95,7 +95,7 @@ static gob::Value to_gob(py::handle o) {
     }
     return v;
   }
-  fail("gob: cannot encode Python type " + py::str(o.get_type()).cast<std::string>());
+  fail("gob: cannot encode Python type " + py::str(py::type::handle_of(o)).cast<std::string>());
 }
 
 static py::object from_gob(const gob::Value& v) {

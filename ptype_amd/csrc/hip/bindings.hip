@@ -282,6 +282,7 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("direct"), py::arg("checksum"), py::arg("stream"), py::arg("packed") = false,
           py::arg("mailboxes") = 0, py::arg("ordered") = false, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("stream_values", &EpochEngine::stream_values)
+      .def("hang_state", &EpochEngine::hang_state, py::arg("compute_stream"))
       .def("last_wire",
            [](const EpochEngine& e) {
              const auto& w = e.last_wire();

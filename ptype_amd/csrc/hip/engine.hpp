@@ -140,8 +140,8 @@ class FakeComm {
   }
   ~FakeComm() {
     for (auto& sl : slots_) {
-      hipEventDestroy(sl.ready);
-      hipEventDestroy(sl.done);
+      (void)hipEventDestroy(sl.ready);
+      (void)hipEventDestroy(sl.done);
     }
   }
   int size() const { return R_; }
@@ -279,22 +279,30 @@ class EpochEngine {
     const char* sync = getenv("PTYPE_STREAM_SYNC");
     if (sync && std::string(sync) == "values" &&
         hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device_) == hipSuccess && wv) {
-      PT_HIP_CHECK(hipMalloc(&flags_dev_, sizeof(flag_seq_)));
-      PT_HIP_CHECK(hipMemset(flags_dev_, 0, sizeof(flag_seq_)));
+      if (getenv("PTYPE_HANG_DIAG")) {
+        // diagnosis: the words in pinned host memory, readable while a queue is stuck
+        PT_HIP_CHECK(hipHostMalloc((void**)&flags_host_, sizeof(flag_seq_), hipHostMallocMapped));
+        memset((void*)flags_host_, 0, sizeof(flag_seq_));
+        PT_HIP_CHECK(hipHostGetDevicePointer((void**)&flags_dev_, flags_host_, 0));
+      } else {
+        PT_HIP_CHECK(hipMalloc(&flags_dev_, sizeof(flag_seq_)));
+        PT_HIP_CHECK(hipMemset(flags_dev_, 0, sizeof(flag_seq_)));
+      }
       use_values_ = true;
     }
     PT_HIP_CHECK(hipMalloc(&meta_dev_, kMetaWords * sizeof(uint64_t)));
     PT_HIP_CHECK(hipHostMalloc(&meta_host_, kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
   }
   ~EpochEngine() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
-    hipSetDevice(device_);
+    (void)hipSetDevice(device_);
     for (int i = 0; i < kMaxBufs; ++i)
-      for (hipEvent_t e : {ev_route_[i], ev_req_[i], ev_disp_[i], ev_rep_[i]}) hipEventDestroy(e);
-    hipEventDestroy(ev_meta_out_);
-    hipStreamDestroy(comm_stream_);
-    hipFree(meta_dev_);
-    hipHostFree(meta_host_);
-    if (flags_dev_) hipFree(flags_dev_);
+      for (hipEvent_t e : {ev_route_[i], ev_req_[i], ev_disp_[i], ev_rep_[i]}) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(ev_meta_out_);
+    (void)hipStreamDestroy(comm_stream_);
+    (void)hipFree(meta_dev_);
+    (void)hipHostFree(meta_host_);
+    if (flags_host_) (void)hipHostFree(flags_host_);
+    else if (flags_dev_) (void)hipFree(flags_dev_);
   }
 
   // Wire format of the last Send: v3 layout (S == 0: v2) and the words this rank
@@ -308,6 +316,28 @@ class EpochEngine {
   };
   const WireInfo& last_wire() const { return wire_; }
   bool stream_values() const { return use_values_; }  // hand-offs via stream wait-value packets
+  // Hang diagnosis (PTYPE_HANG_DIAG with PTYPE_STREAM_SYNC=values): for every
+  // (hand-off, buffer set) word its last signalled sequence and, when the words
+  // live in pinned host memory, the value the GPU has written so far; plus
+  // whether the compute / comm streams have drained (hipStreamQuery).
+  std::vector<int64_t> hang_state(uintptr_t compute_stream) const {
+    std::vector<int64_t> v;
+    for (int k = 0; k < 4 * kMaxBufs; ++k) {
+      v.push_back((int64_t)flag_seq_[k]);
+      v.push_back(flags_host_ ? (int64_t)__atomic_load_n(&flags_host_[k], __ATOMIC_SEQ_CST) : -1);
+    }
+    v.push_back(hipStreamQuery(as_stream(compute_stream)) == hipSuccess ? 1 : 0);
+    v.push_back(hipStreamQuery(comm_stream_) == hipSuccess ? 1 : 0);
+    v.push_back(hipEventQuery(ev_meta_out_) == hipSuccess ? 1 : 0);
+    for (int i = 0; i < kMaxBufs; ++i)  // 1: the chunk's route kernels completed, 0: not yet, -1: not marked
+      v.push_back(diag_ev_[i] ? (hipEventQuery(diag_ev_[i]) == hipSuccess ? 1 : 0) : -1);
+    return v;
+  }
+  void diag_mark(int i, hipStream_t s) {
+    if (i >= kMaxBufs) return;
+    if (!diag_ev_[i]) PT_HIP_CHECK(hipEventCreateWithFlags(&diag_ev_[i], hipEventDisableTiming));
+    PT_HIP_CHECK(hipEventRecord(diag_ev_[i], s));
+  }
 
   void set_bufs(int i, const EngineBufs& b) {
     if (i < 0 || i >= kMaxBufs) throw std::invalid_argument("EpochEngine: at most 8 buffer sets");
@@ -384,6 +414,7 @@ class EpochEngine {
         pending.pop_front();
       }
       route(a, i, bi, cs, local_only);
+      if (flags_host_) diag_mark(i, cs);  // PTYPE_HANG_DIAG: did this chunk's route kernels finish?
       if (collectives()) {
         handoff(kRouted, bi, cs, comm_stream_);
         a2a(bufs_[bi].send, bufs_[bi].recv, wq);
@@ -693,6 +724,8 @@ class EpochEngine {
   hipEvent_t ev_meta_out_{};
   bool use_values_ = false;              // hand-offs through stream wait-value packets (see handoff)
   uint64_t* flags_dev_ = nullptr;        // [4 hand-offs][kMaxBufs] sequence words
+  uint64_t* flags_host_ = nullptr;       // the same words in pinned host memory (PTYPE_HANG_DIAG)
+  hipEvent_t diag_ev_[8] = {};           // PTYPE_HANG_DIAG: after each chunk's route kernels
   uint64_t flag_seq_[4 * kMaxBufs] = {};  // last value written per word
   bool value_mode_[4 * kMaxBufs] = {};    // how the pending hand-off on that word was signalled
   uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)

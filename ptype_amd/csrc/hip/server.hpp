@@ -343,19 +343,19 @@ class DeviceServer {
       if (waker_.joinable()) waker_.join();
     }
     __atomic_store_n(&ctrl_->stop, 1ull, __ATOMIC_SEQ_CST);
-    hipSetDevice(device_);
-    hipStreamSynchronize(stream_);
-    hipStreamDestroy(stream_);
+    (void)hipSetDevice(device_);
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
     if (seg_) {
-      if (registered_) hipHostUnregister(seg_->base());
+      if (registered_) (void)hipHostUnregister(seg_->base());
       seg_.reset();  // unmaps + unlinks the segment
     } else {
-      if (req_on_device_) hipFree(req_);
-      else hipHostFree(req_);
-      hipHostFree(rep_);
-      hipHostFree(ctrl_);
+      if (req_on_device_) (void)hipFree(req_);
+      else (void)hipHostFree(req_);
+      (void)hipHostFree(rep_);
+      (void)hipHostFree(ctrl_);
     }
-    if (trace_) hipHostFree(trace_);
+    if (trace_) (void)hipHostFree(trace_);
   }
 
   // Export a device method to same-node client processes (segment header table).
@@ -522,7 +522,7 @@ class DeviceServer {
           std::lock_guard<std::mutex> g(launch_mu_);
           const uint64_t head = __atomic_load_n(&ctrl_->resume_head, __ATOMIC_ACQUIRE);
           __atomic_store_n(&ctrl_->state, (uint64_t)kRunning, __ATOMIC_SEQ_CST);
-          hipSetDevice(device_);
+          (void)hipSetDevice(device_);
           hipLaunchKernelGGL(persistent_dispatch_kernel, dim3(1), dim3(64), 0, stream_, dreq_, drep_,
                              (uint64_t)(ring_ - 1), dctrl_, head, state_, n_state_, delay_ticks_, idle_ticks_,
                              max_ticks_, poll_);
