@@ -14,7 +14,6 @@ cluster/store.go, cluster/store_config.go, cluster/rpc.go.
 """
 from __future__ import annotations
 
-import dataclasses
 import inspect
 from typing import Any, Callable, Iterable
 

@@ -15,7 +15,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _check, _ptr, _stream, hip
+from . import _ptr, _stream, hip
 
 KEY_EMPTY = 0
 KEY_TOMB = -1  # ~0 as int64

@@ -10,7 +10,7 @@ import torch
 
 from ptype_amd.ops import batch as B
 from ptype_amd.ops.mailbox import audit_fold, batch_ordered, send_ref
-from ptype_amd.ops.records import (METHOD_CALC_MULTIPLY, METHOD_SEQ_FOLD, STATUS_NO_ACTOR, STATUS_OK, method_ordered)
+from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_SEQ_FOLD, STATUS_NO_ACTOR, method_ordered
 
 
 def serial_run(mbox, a0, state0, order):

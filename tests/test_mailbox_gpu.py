@@ -6,7 +6,6 @@ reference; ordered (SeqFold) traffic is audited by chain reconstruction
 before to after the Send through every message exactly once, which also
 exposes the order each actor ran its messages in (FIFO checks).
 """
-import numpy as np
 import pytest
 import torch
 

@@ -1,7 +1,6 @@
 """Registry + KV store parity against a real control-plane member (reference
 cluster/registry_test.go and cluster/store_test.go, EtcdDependentSuite: one
 embedded member in a temp dir, `services` and `store` wiped before each test)."""
-import threading
 import time
 
 import pytest
