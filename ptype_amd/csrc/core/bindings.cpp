@@ -4,6 +4,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <unordered_map>
+
 #include "api.hpp"
 #include "gob.hpp"
 #include "json.hpp"
@@ -48,10 +50,48 @@ static gob::Value struct_from(const std::string& name, py::iterable pairs) {
   return v;
 }
 
+// Per-type facts to_gob needs for class instances (whether the type has a
+// __gob_value__ helper, or its dataclass name and field names), computed once per
+// type: `dataclasses.fields` and a failing hasattr cost microseconds per call on
+// the single-call path (a same-node device call is ~3 us end to end).
+struct GobTypeInfo {
+  py::object type;  // keeps the type alive, so its address is not reused
+  bool helper = false, dataclass = false;
+  std::string name;
+  std::vector<std::pair<std::string, py::str>> fields;
+};
+
+static const GobTypeInfo& gob_type_info(py::handle o) {
+  static std::unordered_map<PyTypeObject*, std::unique_ptr<GobTypeInfo>> cache;  // under the GIL
+  PyTypeObject* t = Py_TYPE(o.ptr());
+  auto it = cache.find(t);
+  if (it != cache.end()) return *it->second;
+  auto info = std::make_unique<GobTypeInfo>();
+  info->type = py::reinterpret_borrow<py::object>(reinterpret_cast<PyObject*>(t));
+  info->helper = py::hasattr(info->type, "__gob_value__");
+  info->dataclass = !info->helper && py::hasattr(info->type, "__dataclass_fields__");
+  if (info->dataclass) {
+    info->name = py::str(info->type.attr("__name__")).cast<std::string>();
+    for (auto f : py::module_::import("dataclasses").attr("fields")(info->type)) {
+      const std::string n = f.attr("name").cast<std::string>();
+      info->fields.emplace_back(n, py::str(n));
+    }
+  }
+  return *cache.emplace(t, std::move(info)).first->second;
+}
+
 static gob::Value to_gob(py::handle o) {
   if (o.is_none()) fail("gob: cannot encode None");
   if (py::isinstance<py::bool_>(o)) return gob::Value::Bool(o.cast<bool>());
-  if (py::hasattr(o, "__gob_value__")) {  // GoUint / GoStruct helpers (ptype_amd.gobtypes)
+  if (PyLong_CheckExact(o.ptr())) return gob::Value::Int(o.cast<int64_t>());  // hot: plain ints
+  const GobTypeInfo& ti = gob_type_info(o);
+  if (ti.dataclass) {
+    gob::Value v = gob::Value::Struct(ti.name);
+    v.fields.reserve(ti.fields.size());
+    for (const auto& f : ti.fields) v.fields.emplace_back(f.first, to_gob(o.attr(f.second)));
+    return v;
+  }
+  if (ti.helper) {  // GoUint / GoStruct helpers (ptype_amd.gobtypes)
     py::tuple t = o.attr("__gob_value__")();
     const std::string tag = t[0].cast<std::string>();
     if (tag == "uint") return gob::Value::Uint(t[1].cast<uint64_t>());
@@ -69,15 +109,6 @@ static gob::Value to_gob(py::handle o) {
   if (py::isinstance<py::float_>(o)) return gob::Value::Float(o.cast<double>());
   if (py::isinstance<py::str>(o)) return gob::Value::String(o.cast<std::string>());
   if (py::isinstance<py::bytes>(o)) return gob::Value::Bytes(o.cast<std::string>());
-  if (py::hasattr(o, "__dataclass_fields__")) {
-    py::object fields = py::module_::import("dataclasses").attr("fields")(o);
-    gob::Value v = gob::Value::Struct(py::str(py::type::handle_of(o).attr("__name__")).cast<std::string>());
-    for (auto f : fields) {
-      const std::string n = f.attr("name").cast<std::string>();
-      v.fields.emplace_back(n, to_gob(o.attr(n.c_str())));
-    }
-    return v;
-  }
   if (py::isinstance<py::list>(o) || py::isinstance<py::tuple>(o)) {
     gob::Value v;
     v.kind = gob::kSlice;
@@ -658,6 +689,11 @@ PYBIND11_MODULE(_core, m) {
                                if (dynamic_cast<LocalRpcConn*>(&c)) return "local";
                                return "tcp";
                              })
+      .def_property_readonly("ring_placement",
+                             [](RpcConn& c) -> py::object {
+                               if (auto* s = dynamic_cast<ShmRpcConn*>(&c)) return py::str(s->ring_placement());
+                               return py::none();
+                             })
       .def("call",
            [](RpcConn& c, const std::string& method, py::object args) {
              gob::Value a = to_gob(args);
@@ -675,21 +711,21 @@ PYBIND11_MODULE(_core, m) {
   // between the GPUs of a node (bench.py) without a net/rpc server in the way.
   struct ShmClient {
     std::shared_ptr<ShmSegment> seg;
+    std::shared_ptr<DevRingMap> devmap;
     ShmView view;
   };
   py::class_<ShmClient, std::shared_ptr<ShmClient>>(m, "ShmClient")
       .def(py::init([](const std::string& name) {
              auto seg = ShmSegment::attach(name);
              if (!seg) fail(Errc::kUnavailable, "no dispatcher segment " + name);
-             const ShmHeader* h = static_cast<const ShmHeader*>(seg->base());
-             if (seg->size() < sizeof(ShmHeader) || h->magic != kShmMagic || seg->size() < shm_bytes(h->ring))
-               fail(Errc::kUnavailable, "segment " + name + " is not a ptype dispatcher");
              auto c = std::make_shared<ShmClient>();
-             c->view = shm_view(seg->base(), h->ring);
+             c->view = shm_attach_view(seg, &c->devmap);
              c->seg = std::move(seg);
              return c;
            }),
            py::arg("name"))
+      .def_property_readonly("ring_placement",
+                             [](const ShmClient& c) { return std::string(c.view.bar ? "device" : "host"); })
       .def(
           "call",
           [](ShmClient& c, int method, uint32_t actor, int64_t a0, int64_t a1, int64_t a2, double timeout) {
@@ -703,6 +739,24 @@ PYBIND11_MODULE(_core, m) {
           },
           py::arg("method"), py::arg("actor"), py::arg("a0") = 0, py::arg("a1") = 0, py::arg("a2") = 0,
           py::arg("timeout") = 10.0);
+  // the dma-buf fd hand-off of the cross-process device ring, bound for tests
+  py::class_<FdHandoff, std::shared_ptr<FdHandoff>>(m, "FdHandoff")
+      .def(py::init([](const std::string& name, int fd) { return std::make_shared<FdHandoff>(name, fd); }),
+           py::arg("name"), py::arg("fd"))
+      .def_property_readonly("handed", &FdHandoff::handed);
+  m.def(
+      "fd_receive",
+      [](const std::string& name) {
+        std::string why;
+        int fd;
+        {
+          py::gil_scoped_release nogil;
+          fd = shm_receive_fd(name, &why);
+        }
+        if (fd < 0) fail(Errc::kUnavailable, "fd hand-off " + name + ": " + why);
+        return fd;
+      },
+      py::arg("name"));
   m.def(
       "dial_http",
       [](const std::string& host, int port, double timeout, bool allow_local) {

@@ -432,10 +432,28 @@ RpcOutcome device_outcome(const ReplyRecord& r) {
 // ---- same-node shared-memory connection
 ShmRpcConn::ShmRpcConn(std::shared_ptr<ShmSegment> seg, std::string host, int port, int64_t dial_timeout_ms)
     : seg_(std::move(seg)), host_(std::move(host)), port_(port), dial_timeout_ms_(dial_timeout_ms) {
-  const ShmHeader* h = static_cast<const ShmHeader*>(seg_->base());
-  if (seg_->size() < sizeof(ShmHeader) || h->magic != kShmMagic || seg_->size() < shm_bytes(h->ring))
-    fail(Errc::kUnavailable, "shared-memory segment " + seg_->name() + " is not a ptype dispatcher");
-  view_ = shm_view(seg_->base(), h->ring);
+  view_ = shm_attach_view(seg_, &devmap_);
+}
+
+// The segment's export of `method`, resolved once per name (exports are only
+// ever appended, so a resolved entry stays valid; a miss re-scans the table).
+const ShmRpcConn::DevMethod* ShmRpcConn::device_method(const std::string& method) {
+  std::lock_guard<std::mutex> g(methods_mu_);
+  auto it = methods_.find(method);
+  if (it != methods_.end()) return &it->second;
+  const ShmHeader* h = view_.hdr;
+  const uint32_t n = std::min<uint32_t>(h->n_methods.load(std::memory_order_acquire), kShmMaxMethods);
+  for (uint32_t k = 0; k < n; ++k) {
+    const ShmMethod& mm = h->methods[k];
+    if (method != mm.name) continue;
+    DevMethod d;
+    d.method = mm.method;
+    d.actor = mm.actor;
+    for (uint32_t f = 0; f < mm.n_fields && f < 3; ++f) d.fields.emplace_back(mm.fields[f]);
+    d.actor_field = mm.actor_field;
+    return &methods_.emplace(method, std::move(d)).first->second;
+  }
+  return nullptr;
 }
 
 std::shared_ptr<RpcConn> ShmRpcConn::tcp() {
@@ -451,14 +469,8 @@ RpcOutcome ShmRpcConn::call(const std::string& method, const gob::Value& args, i
     o.code = Errc::kShutdown;
     return o;
   }
-  const ShmHeader* h = view_.hdr;
-  const uint32_t n = std::min<uint32_t>(h->n_methods.load(std::memory_order_acquire), kShmMaxMethods);
-  for (uint32_t k = 0; k < n; ++k) {
-    const ShmMethod& mm = h->methods[k];
-    if (method != mm.name) continue;
-    std::vector<std::string> fields;
-    for (uint32_t f = 0; f < mm.n_fields && f < 3; ++f) fields.emplace_back(mm.fields[f]);
-    const MsgRecord m = encode_device_call(args, (int)mm.method, mm.actor, fields, mm.actor_field);
+  if (const DevMethod* dm = device_method(method)) {
+    const MsgRecord m = encode_device_call(args, (int)dm->method, dm->actor, dm->fields, dm->actor_field);
     try {
       const ReplyRecord r = shm_call(view_, m, timeout_ms < 0 ? 30.0 : timeout_ms / 1e3);
       shm_calls_.fetch_add(1);

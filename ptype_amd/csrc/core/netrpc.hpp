@@ -18,6 +18,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -125,10 +126,21 @@ class ShmRpcConn : public RpcConn, public std::enable_shared_from_this<ShmRpcCon
   void close() override;
   std::string target() const override { return host_ + ":" + std::to_string(port_); }
   uint64_t shm_calls() const { return shm_calls_.load(); }
+  // where the requests go: "device" (the server GPU's ring, mapped from its dma-buf) or "host" (the segment)
+  const char* ring_placement() const { return view_.bar ? "device" : "host"; }
 
  private:
+  struct DevMethod {
+    uint32_t method = 0, actor = 0;
+    std::vector<std::string> fields;
+    std::string actor_field;
+  };
+  const DevMethod* device_method(const std::string& method);
   std::shared_ptr<RpcConn> tcp();
   std::shared_ptr<ShmSegment> seg_;
+  std::shared_ptr<DevRingMap> devmap_;
+  std::mutex methods_mu_;
+  std::unordered_map<std::string, DevMethod> methods_;  // node-stable: pointers stay valid
   ShmView view_;
   std::string host_;
   int port_;

@@ -4,14 +4,20 @@
 #include <fcntl.h>
 #include <linux/futex.h>
 #include <signal.h>
+#include <stddef.h>
 #include <sys/mman.h>
+#include <sys/select.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
+#include <sys/un.h>
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "ringproto.hpp"
@@ -80,6 +86,145 @@ ShmSegment::~ShmSegment() {
   if (unlink_) shm_unlink(name_.c_str());
 }
 
+bool xproc_device_ring_enabled() {
+  const char* v = getenv("PTYPE_XPROC_RING");
+  return !(v && std::string(v) == "host");
+}
+
+// ---- dma-buf fd hand-off (abstract unix socket, SCM_RIGHTS).  pidfd_getfd
+// would need ptrace rights over the server (Yama scope 1 denies it between
+// sibling processes); a socket the server answers works for any same-uid peer.
+static sockaddr_un abstract_addr(const std::string& name, socklen_t* len) {
+  sockaddr_un a{};
+  a.sun_family = AF_UNIX;
+  const size_t n = std::min(name.size(), sizeof(a.sun_path) - 2);
+  std::memcpy(a.sun_path + 1, name.data(), n);  // sun_path[0] = 0: abstract namespace
+  *len = (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + n);
+  return a;
+}
+
+FdHandoff::FdHandoff(const std::string& name, int fd) : fd_(fd) {
+  listen_fd_ = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  socklen_t len;
+  const sockaddr_un a = abstract_addr(name, &len);
+  if (listen_fd_ < 0 || bind(listen_fd_, (const sockaddr*)&a, len) != 0 || listen(listen_fd_, 64) != 0) {
+    const std::string e = std::strerror(errno);
+    if (listen_fd_ >= 0) close(listen_fd_);
+    fail(Errc::kGeneric, "fd hand-off socket " + name + ": " + e);
+  }
+  thread_ = std::thread([this] { loop(); });
+}
+
+FdHandoff::~FdHandoff() {
+  stop_.store(true);
+  if (thread_.joinable()) thread_.join();
+  close(listen_fd_);
+}
+
+void FdHandoff::loop() {
+  while (!stop_.load()) {
+    fd_set rs;
+    FD_ZERO(&rs);
+    FD_SET(listen_fd_, &rs);
+    timeval tv{0, 100000};
+    if (select(listen_fd_ + 1, &rs, nullptr, nullptr, &tv) <= 0) continue;
+    const int c = accept4(listen_fd_, nullptr, nullptr, SOCK_CLOEXEC);
+    if (c < 0) continue;
+    ucred cred{};
+    socklen_t cl = sizeof cred;
+    if (getsockopt(c, SOL_SOCKET, SO_PEERCRED, &cred, &cl) == 0 && cred.uid == getuid()) {
+      char b = 'r';
+      iovec io{&b, 1};
+      char ctl[CMSG_SPACE(sizeof(int))] = {};
+      msghdr m{};
+      m.msg_iov = &io;
+      m.msg_iovlen = 1;
+      m.msg_control = ctl;
+      m.msg_controllen = sizeof ctl;
+      cmsghdr* cm = CMSG_FIRSTHDR(&m);
+      cm->cmsg_level = SOL_SOCKET;
+      cm->cmsg_type = SCM_RIGHTS;
+      cm->cmsg_len = CMSG_LEN(sizeof(int));
+      std::memcpy(CMSG_DATA(cm), &fd_, sizeof(int));
+      if (sendmsg(c, &m, MSG_NOSIGNAL) == 1) handed_.fetch_add(1);
+    }
+    close(c);
+  }
+}
+
+int shm_receive_fd(const std::string& name, std::string* why) {
+  const int s = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  socklen_t len;
+  const sockaddr_un a = abstract_addr(name, &len);
+  if (s < 0 || connect(s, (const sockaddr*)&a, len) != 0) {
+    if (why) *why = std::string("connect: ") + std::strerror(errno);
+    if (s >= 0) close(s);
+    return -1;
+  }
+  timeval tv{2, 0};
+  setsockopt(s, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  char b = 0;
+  iovec io{&b, 1};
+  char ctl[CMSG_SPACE(sizeof(int))] = {};
+  msghdr m{};
+  m.msg_iov = &io;
+  m.msg_iovlen = 1;
+  m.msg_control = ctl;
+  m.msg_controllen = sizeof ctl;
+  int fd = -1;
+  if (recvmsg(s, &m, MSG_CMSG_CLOEXEC) == 1)
+    for (cmsghdr* cm = CMSG_FIRSTHDR(&m); cm; cm = CMSG_NXTHDR(&m, cm))
+      if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS) std::memcpy(&fd, CMSG_DATA(cm), sizeof(int));
+  if (fd < 0 && why) *why = "no fd received (different user?)";
+  close(s);
+  return fd;
+}
+
+std::shared_ptr<DevRingMap> DevRingMap::attach(const ShmHeader* h, std::string* why) {
+  if (!h->req_dev) {
+    if (why) *why = "the server's ring is in the segment";
+    return nullptr;
+  }
+  const std::string name(h->req_sock, strnlen(h->req_sock, sizeof h->req_sock));
+  const int fd = shm_receive_fd(name, why);
+  if (fd < 0) return nullptr;
+  const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+  const uint64_t off = h->req_dev_off;
+  const size_t lead = (size_t)(off & (pg - 1));
+  const size_t len = (lead + (size_t)h->req_dev_bytes + pg - 1) & ~(pg - 1);
+  void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)(off - lead));
+  const int err = errno;
+  close(fd);  // the mapping holds the buffer
+  if (p == MAP_FAILED) {
+    if (why) *why = std::string("mmap of the device ring: ") + std::strerror(err);
+    return nullptr;
+  }
+  auto m = std::shared_ptr<DevRingMap>(new DevRingMap());
+  m->map_ = p;
+  m->len_ = len;
+  m->req_ = reinterpret_cast<RingSlot*>(static_cast<char*>(p) + lead);
+  return m;
+}
+
+DevRingMap::~DevRingMap() {
+  if (map_) munmap(map_, len_);
+}
+
+ShmView shm_attach_view(const std::shared_ptr<ShmSegment>& seg, std::shared_ptr<DevRingMap>* devmap) {
+  const ShmHeader* h = static_cast<const ShmHeader*>(seg->base());
+  if (seg->size() < sizeof(ShmHeader) || h->magic != kShmMagic || seg->size() < shm_bytes(h->ring))
+    fail(Errc::kUnavailable, "shared-memory segment " + seg->name() + " is not a ptype dispatcher");
+  ShmView v = shm_view(seg->base(), h->ring);
+  if (h->req_dev) {
+    std::string why;
+    *devmap = DevRingMap::attach(h, &why);
+    if (!*devmap) fail(Errc::kUnavailable, "dispatcher " + seg->name() + ": device request ring: " + why);
+    v.req = (*devmap)->req();
+    v.bar = true;
+  }
+  return v;
+}
+
 static uint64_t now_ns() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch())
@@ -99,6 +244,7 @@ ReplyRecord shm_call(const ShmView& v, const MsgRecord& m, double timeout_s) {
   r.rep = v.rep;
   r.owner = v.owner;
   r.ring = v.hdr->ring;
+  r.bar = v.bar;
   r.poke = [&v] { poke_if_parked(v); };
   const uint64_t seq = v.hdr->next_seq.fetch_add(1);
   if (!ring_claim(r, seq, timeout_s))

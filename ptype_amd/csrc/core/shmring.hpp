@@ -13,17 +13,29 @@
 // poke when the dispatcher wave has parked itself.
 //
 // Layout: [ShmHeader, 16 KB][ServerCtrl, 4 KB][RingSlot x ring][ReplySlot x ring][u64 owner x ring]
+//
+// Request ring placement: by default the ring the dispatcher
+// polls is NOT the segment's RingSlot area but fine-grained memory on the
+// server's GPU.  The server exports it as a dma-buf and hands the fd to client
+// processes over an abstract unix socket (SCM_RIGHTS; same uid only); a client
+// maps it with plain mmap -- no HIP in the client -- and writes requests through
+// the BAR, so the polling wave's tag and payload reads stay in HBM instead of
+// crossing PCIe twice per call.  Replies, the owner words and the control block
+// stay in host memory (the client polls them).  GPU peers can import the same
+// ring with the hipIpcMemHandle in the header.  PTYPE_XPROC_RING=host keeps the
+// ring in the segment (either side).
 #pragma once
 #include <atomic>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "records.hpp"
 
 namespace ptype {
 
-constexpr uint64_t kShmMagic = 0x31736d6570797470ull;  // "ptypems1"
+constexpr uint64_t kShmMagic = 0x32736d6570797470ull;  // "ptypems2"
 constexpr int kShmMaxMethods = 32;
 
 struct ShmMethod {
@@ -41,6 +53,14 @@ struct alignas(64) ShmHeader {
   std::atomic<uint32_t> wake;      // futex word: 1 = a publisher found the dispatcher parked
   std::atomic<uint32_t> n_methods;
   ShmMethod methods[kShmMaxMethods];
+  // device-memory request ring (0: the ring is the segment's own RingSlot area)
+  uint32_t req_dev;
+  int32_t ipc_device;     // the server's HIP device ordinal
+  uint64_t req_dev_off;   // offset of the ring in the dma-buf
+  uint64_t req_dev_bytes;
+  char req_sock[64];      // abstract unix socket handing out the dma-buf fd
+  uint8_t ipc_handle[64]; // hipIpcMemHandle_t of the ring (GPU peers)
+  uint32_t ipc_valid, pad2;
 };
 static_assert(sizeof(ShmHeader) <= 16384, "ShmHeader too large");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "process-shared atomics must be lock-free");
@@ -57,6 +77,7 @@ struct ShmView {
   RingSlot* req = nullptr;
   ReplySlot* rep = nullptr;
   std::atomic<uint64_t>* owner = nullptr;
+  bool bar = false;  // `req` is device memory written through a BAR mapping
 };
 
 inline ShmView shm_view(void* base, uint32_t ring) {
@@ -91,6 +112,49 @@ class ShmSegment {
   size_t size_ = 0;
   bool unlink_ = false;
 };
+
+// Whether a server places its request ring on the device (PTYPE_XPROC_RING != host).
+bool xproc_device_ring_enabled();
+
+// Server side: hands `fd` to every same-uid process that connects to the
+// abstract unix socket `name` (one thread; stops on destruction).
+class FdHandoff {
+ public:
+  FdHandoff(const std::string& name, int fd);
+  ~FdHandoff();
+  FdHandoff(const FdHandoff&) = delete;
+  FdHandoff& operator=(const FdHandoff&) = delete;
+  uint64_t handed() const { return handed_.load(); }
+
+ private:
+  void loop();
+  int listen_fd_ = -1, fd_;
+  std::atomic<bool> stop_{false};
+  std::atomic<uint64_t> handed_{0};
+  std::thread thread_;
+};
+
+// Client side of FdHandoff: the fd (owned by the caller), or -1 with `why` set.
+int shm_receive_fd(const std::string& name, std::string* why = nullptr);
+
+// Client side: the server's device request ring mapped into this process.
+class DevRingMap {
+ public:
+  // nullptr if the header names no device ring or any step fails (`why` says which)
+  static std::shared_ptr<DevRingMap> attach(const ShmHeader* h, std::string* why = nullptr);
+  ~DevRingMap();
+  RingSlot* req() const { return req_; }
+
+ private:
+  void* map_ = nullptr;
+  size_t len_ = 0;
+  RingSlot* req_ = nullptr;
+};
+
+// Attach to a dispatcher segment: the view (with the device ring mapped when the
+// server placed it there) and the mapping that keeps it alive.  Throws when the
+// server's ring is on the device and cannot be mapped here.
+ShmView shm_attach_view(const std::shared_ptr<ShmSegment>& seg, std::shared_ptr<DevRingMap>* devmap);
 
 // Publish one request into the segment's ring and wait for its reply (any
 // process).  `poke` is called when the dispatcher is not running.

@@ -368,6 +368,7 @@ PYBIND11_MODULE(_hip, m) {
       .def("close", &DeviceServer::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("processed", &DeviceServer::processed)
       .def_property_readonly("ring_on_device", &DeviceServer::ring_on_device)
+      .def_property_readonly("ring_fds_handed", &DeviceServer::ring_fds_handed)
       .def_property_readonly("launches", &DeviceServer::launches)
       .def_property_readonly("exits_idle", &DeviceServer::exits_idle)
       .def_property_readonly("exits_lifetime", &DeviceServer::exits_lifetime)

@@ -11,7 +11,8 @@
 // system-scope stores.  No kernel launch per call.  In-process, the request
 // ring is fine-grained DEVICE memory the host writes through its BAR mapping
 // (polls and payload reads stay on the GPU: p50 RTT 4.0-4.5 -> 3.1 us,
-// profiles/r1_ring_placement_ab.txt); the cross-process ring is host shm.
+// profiles/r1_ring_placement_ab.txt); for other processes the same device ring
+// is exported as a dma-buf they map (shmring.hpp), with replies in host shm.
 //
 // Liveness: the kernel exits when the host sets `stop`, when it has been idle
 // for `idle_ticks`, or after `max_ticks` (a hard bound so nothing can hang the
@@ -315,6 +316,7 @@ class DeviceServer {
       dreq_ = reinterpret_cast<RingSlot*>(dbase + (reinterpret_cast<const char*>(req_) - hbase));
       drep_ = reinterpret_cast<ReplySlot*>(dbase + (reinterpret_cast<const char*>(rep_) - hbase));
       dctrl_ = reinterpret_cast<ServerCtrl*>(dbase + (reinterpret_cast<const char*>(ctrl_) - hbase));
+      if (xproc_device_ring_enabled()) export_device_ring();
     }
     for (uint32_t i = 0; i < ring_; ++i) owner_[i].store(i, std::memory_order_relaxed);
     PT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -347,6 +349,9 @@ class DeviceServer {
     (void)hipStreamSynchronize(stream_);
     (void)hipStreamDestroy(stream_);
     if (seg_) {
+      handoff_.reset();  // no new client maps the ring (mapped ones keep the buffer alive)
+      if (dmabuf_fd_ >= 0) (void)hsa_amd_portable_close_dmabuf(dmabuf_fd_);
+      if (req_on_device_) (void)hipFree(req_);
       if (registered_) (void)hipHostUnregister(seg_->base());
       seg_.reset();  // unmaps + unlinks the segment
     } else {
@@ -377,6 +382,7 @@ class DeviceServer {
   }
 
   std::string shm_name() const { return seg_ ? seg_->name() : std::string(); }
+  uint64_t ring_fds_handed() const { return handoff_ ? handoff_->handed() : 0; }  // client processes that mapped the ring
 
   // Publish n requests and wait for all replies (any thread).
   void call(const MsgRecord* in, ReplyRecord* out, int n, double timeout_s) {
@@ -500,6 +506,60 @@ class DeviceServer {
     return r;
   }
 
+  // Cross-process request ring in device memory (shmring.hpp):
+  // fine-grained HBM that this process writes through its BAR mapping, client
+  // processes through an mmap of its dma-buf (fd handed over a unix socket), and
+  // GPU peers through its IPC handle.  Any failure leaves the segment's ring.
+  void export_device_ring() {
+    const size_t bytes = sizeof(RingSlot) * ring_;
+    RingSlot* d = nullptr;
+    const auto dbg = [](const char* what, int st) {
+      if (getenv("PTYPE_RING_DEBUG")) fprintf(stderr, "ptype: device ring export: %s -> %d\n", what, st);
+    };
+    if (hipExtMallocWithFlags((void**)&d, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+      (void)hipGetLastError();
+      return dbg("hipExtMallocWithFlags", -1);
+    }
+    int fd = -1;
+    uint64_t off = 0;
+    hsa_status_t st = HSA_STATUS_ERROR;
+    if (!open_to_cpu(d) || (st = hsa_amd_portable_export_dmabuf(d, bytes, &fd, &off)) != HSA_STATUS_SUCCESS) {
+      dbg("open_to_cpu / hsa_amd_portable_export_dmabuf", (int)st);
+      (void)hipFree(d);
+      return;
+    }
+    static std::atomic<uint32_t> counter{0};
+    const std::string sock = "ptype-ring-" + std::to_string(getpid()) + "-" + std::to_string(counter.fetch_add(1));
+    try {
+      handoff_.reset(new FdHandoff(sock, fd));
+    } catch (const std::exception& e) {
+      dbg(e.what(), -1);
+      (void)hsa_amd_portable_close_dmabuf(fd);
+      (void)hipFree(d);
+      return;
+    }
+    PT_HIP_CHECK(hipMemset(d, 0, bytes));
+    PT_HIP_CHECK(hipDeviceSynchronize());
+    hipIpcMemHandle_t ipc;
+    if (hipIpcGetMemHandle(&ipc, d) == hipSuccess) {
+      static_assert(sizeof(ipc) <= sizeof(hdr_->ipc_handle), "IPC handle size");
+      memcpy(hdr_->ipc_handle, &ipc, sizeof ipc);
+      hdr_->ipc_valid = 1;
+    } else {
+      (void)hipGetLastError();
+    }
+    dmabuf_fd_ = fd;
+    req_ = d;
+    dreq_ = d;
+    req_on_device_ = true;
+    hdr_->ipc_device = device_;
+    hdr_->req_dev_off = off;
+    hdr_->req_dev_bytes = bytes;
+    memset(hdr_->req_sock, 0, sizeof hdr_->req_sock);
+    strncpy(hdr_->req_sock, sock.c_str(), sizeof hdr_->req_sock - 1);
+    hdr_->req_dev = 1;  // published with the magic (release) at the end of construction
+  }
+
   // Same-node clients poke the futex when they find the wave parked.
   void waker_loop() {
     while (!closed_) {
@@ -566,6 +626,8 @@ class DeviceServer {
   std::unique_ptr<std::atomic<uint64_t>[]> owner_mem_;
   std::atomic<uint64_t>* owner_ = nullptr;
   std::shared_ptr<ShmSegment> seg_;
+  std::unique_ptr<FdHandoff> handoff_;
+  int dmabuf_fd_ = -1;
   ShmHeader* hdr_ = nullptr;
   bool registered_ = false;
   std::thread waker_;

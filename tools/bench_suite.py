@@ -260,15 +260,24 @@ def _xproc_server(port, q, stop):
     server = C.Server()
     calculator.serve_device(rt, server)
     server.Listen(port, "127.0.0.1")
-    q.put("ready")
+    q.put(("ready", rt.server.shm_name))
     stop.wait(300)
+    q.put(("server", {"ring_on_device": bool(rt.server.ring_on_device), "ring_fds_handed": rt.server.ring_fds_handed}))
     server.Close()
     rt.close()
 
 
-def _xproc_client(port, calls, q):
+def _pcts(lat):
+    lat.sort()
+    return {"p50_us": lat[len(lat) // 2] * 1e6, "p90_us": lat[int(len(lat) * 0.9)] * 1e6,
+            "p99_us": lat[int(len(lat) * 0.99)] * 1e6}
+
+
+def _xproc_client(port, seg, calls, q):
+    os.environ["HIP_VISIBLE_DEVICES"] = ""  # the client process never touches a GPU
     from ptype_amd import _core
     from ptype_amd.models.calculator import Args
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY
 
     out = {}
     for name, allow in (("shm", True), ("tcp", False)):
@@ -280,17 +289,26 @@ def _xproc_client(port, calls, q):
             t = time.perf_counter()
             c.call("Calculator.Multiply", Args(i, 3))
             lat.append(time.perf_counter() - t)
-        lat.sort()
-        out[name] = {"transport": c.transport, "p50_us": lat[len(lat) // 2] * 1e6,
-                     "p99_us": lat[int(len(lat) * 0.99)] * 1e6}
+        out[name] = {"transport": c.transport, "ring": c.ring_placement, **_pcts(lat)}
         c.close()
-    q.put(out)
+    # the same ring without net/rpc's name lookup and gob argument encoding
+    raw = _core.ShmClient(seg)
+    lat = []
+    for i in range(calls + 500):
+        t = time.perf_counter()
+        raw.call(METHOD_CALC_MULTIPLY, i % 1024, i, 3)
+        if i >= 500:
+            lat.append(time.perf_counter() - t)
+    out["raw"] = {"ring": raw.ring_placement, **_pcts(lat)}
+    q.put(("client", out))
 
 
 def xproc(a):
     """example/calculator's shape with GPU actors: server and client are separate
     processes on one node; the client's Call reaches the GPU actor through the
-    shared-memory rings (vs net/rpc over TCP to the same server)."""
+    dispatcher's rings (request ring in the server GPU's memory, mapped from its
+    dma-buf; replies in shared memory) vs net/rpc over TCP to the same server.
+    `raw` is the same ring called without net/rpc's method lookup and gob args."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
@@ -298,15 +316,19 @@ def xproc(a):
     port = _free_port()
     sp = ctx.Process(target=_xproc_server, args=(port, q, stop))
     sp.start()
-    assert q.get(timeout=300) == "ready"
-    cp = ctx.Process(target=_xproc_client, args=(port, a.calls, q))
+    kind, seg = q.get(timeout=300)
+    assert kind == "ready"
+    cp = ctx.Process(target=_xproc_client, args=(port, seg, a.calls, q))
     cp.start()
-    out = q.get(timeout=300)
+    kind, out = q.get(timeout=300)
+    assert kind == "client", out
     cp.join(30)
     stop.set()
+    _, srv = q.get(timeout=60)
     sp.join(60)
     _emit({"config": "cross-process Call to a GPU actor on the same node (calculator server + client processes)",
-           "shm": out["shm"], "tcp_netrpc": out["tcp"]})
+           "request_ring": os.environ.get("PTYPE_XPROC_RING", "device"), "server": srv,
+           "shm": out["shm"], "shm_raw": out["raw"], "tcp_netrpc": out["tcp"]})
 
 
 # --------------------------------------------------------------------------- registry
