@@ -54,12 +54,14 @@ static gob::Value struct_from(const std::string& name, py::iterable pairs) {
 // __gob_value__ helper, or its dataclass name and field names), computed once per
 // type: `dataclasses.fields` and a failing hasattr cost microseconds per call on
 // the single-call path (a same-node device call is ~3 us end to end).
+namespace {  // internal linkage: pybind11 types are hidden-visibility
 struct GobTypeInfo {
   py::object type;  // keeps the type alive, so its address is not reused
   bool helper = false, dataclass = false;
   std::string name;
   std::vector<std::pair<std::string, py::str>> fields;
 };
+}  // namespace
 
 static const GobTypeInfo& gob_type_info(py::handle o) {
   static std::unordered_map<PyTypeObject*, std::unique_ptr<GobTypeInfo>> cache;  // under the GIL
