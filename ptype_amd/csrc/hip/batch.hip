@@ -48,6 +48,9 @@
 namespace ptype {
 
 // `seed_ptr` (optional) lets a captured graph draw a new batch per replay.
+// (Advancing the seed inside this kernel, last block out, was measured slower than
+// the separate one-element add it replaces: 8192 blocks ending on a ticket round
+// trip cost more than the ~4 us launch; fewer, longer blocks stream slower.)
 __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
                                                            int64_t* __restrict__ a1, int64_t M, uint32_t n_actors,
                                                            uint64_t seed, const uint64_t* __restrict__ seed_ptr) {
@@ -77,7 +80,8 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
                                                                    uint64_t mask, const uint32_t* __restrict__ dir,
                                                                    uint32_t n_dir, uint32_t aw, int aw_shift, int R,
                                                                    uint32_t* __restrict__ route,
-                                                                   uint32_t* __restrict__ hist, MetaCols mc = {}) {
+                                                                   uint32_t* __restrict__ hist, MetaCols mc = {},
+                                                                   CapFold cf = {}) {
   constexpr bool DIR = MODE == 1;
   __shared__ unsigned h[kMaxRanks + 1];
   for (int d = threadIdx.x; d <= R; d += blockDim.x) h[d] = 0;
@@ -175,6 +179,26 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
   // column-major [R + 1][G]: the scan reads each destination's column contiguously
   for (int d = threadIdx.x; d <= R; d += blockDim.x) hist[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
   if constexpr (META) meta_publish(macc, mc.mcol != nullptr, mc.method_uniform, M, mc.meta);
+  if (cf.tot) {  // adaptive capacity (CapFold): column totals, then the last block takes the max
+    __shared__ unsigned s_last;
+    const unsigned tid = threadIdx.x;
+    unsigned* tot = cf.tot + (blockIdx.x % kCapCopies) * kMaxCapCols;  // spread: same-address atomics serialise
+    if (tid <= (unsigned)R && h[tid]) {
+      // device-scope atomics complete at the memory side (coherent across XCDs); the
+      // returned value is consumed so the add has landed before the barrier below
+      const unsigned old = atomicAdd(&tot[tid], h[tid]);
+      if (old == 0xffffffffu) h[tid] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) s_last = last_block_ticket(cf.ticket);
+    __syncthreads();
+    if (s_last && tid <= (unsigned)R) {
+      unsigned t = 0;
+      for (unsigned c = 0; c < kCapCopies; ++c)  // memory-side read + reset for the next launch
+        t += atomicExch(&cf.tot[c * kMaxCapCols + tid], 0u);
+      if (tid < (unsigned)R && t) atomicMax(&cf.meta[kMetaCap], (unsigned long long)t);
+    }
+  }
 }
 
 // Slot headers + overflow / no-actor statistics from the column totals (block-level;
@@ -626,16 +650,17 @@ void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a
 template <int K, int MODE>
 static void launch_prep(dim3 g, hipStream_t s, uintptr_t actor, int64_t M, int64_t P, uintptr_t table, uint64_t cap,
                         uintptr_t dir, uint32_t n_dir, int R, uintptr_t route, uintptr_t hist, uint32_t aw = 0,
-                        const MetaCols* mc = nullptr) {
+                        const MetaCols* mc = nullptr, const CapFold* cf = nullptr) {
   const int aw_shift = (aw && (aw & (aw - 1)) == 0) ? __builtin_ctz(aw) : -1;
+  const CapFold fold = cf ? *cf : CapFold{};
   if (mc)
     hipLaunchKernelGGL((route_prep_kernel<K, MODE, true>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
                        (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
-                       (uint32_t*)route, (uint32_t*)hist, *mc);
+                       (uint32_t*)route, (uint32_t*)hist, *mc, fold);
   else
     hipLaunchKernelGGL((route_prep_kernel<K, MODE>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
                        (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
-                       (uint32_t*)route, (uint32_t*)hist, MetaCols{});
+                       (uint32_t*)route, (uint32_t*)hist, MetaCols{}, fold);
 }
 
 // Region sizes of wire format v2 (u32 words; see the header comment).
@@ -717,7 +742,8 @@ void launch_route(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uin
 // while the host waits for the layout agreement.  Returns G; *P_out = P.
 int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                    uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out,
-                   const MetaCols* mc) {
+                   const MetaCols* mc, const CapFold* cf) {
+  if (cf && R + 1 > kMaxCapCols) throw std::invalid_argument("route_prep: capacity fold needs R <= 64");
   int64_t P;
   const int64_t G = route_grid(M, &P);
   *P_out = P;
@@ -726,17 +752,17 @@ int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, ui
     const dim3 g((unsigned)G);
     const int k = g_prep_items;
     if (affine_w && n_dir) {
-      launch_prep<4, 2>(g, s, actor, M, P, table, cap, 0, n_dir, R, route, hist, affine_w, mc);
+      launch_prep<4, 2>(g, s, actor, M, P, table, cap, 0, n_dir, R, route, hist, affine_w, mc, cf);
     } else if (dir && n_dir) {
       // measured (tools/route_bench.py): 1/2/4 items within 2% of each other
-      if (k == 1) launch_prep<1, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc);
-      else if (k == 4) launch_prep<4, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc);
-      else launch_prep<2, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc);
+      if (k == 1) launch_prep<1, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
+      else if (k == 4) launch_prep<4, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
+      else launch_prep<2, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
     } else {
       // probe path: 2 lookups in flight per thread is best; 4 costs occupancy (98 VGPRs)
-      if (k == 1) launch_prep<1, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc);
-      else if (k == 4) launch_prep<4, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc);
-      else launch_prep<2, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc);
+      if (k == 1) launch_prep<1, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc, cf);
+      else if (k == 4) launch_prep<4, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc, cf);
+      else launch_prep<2, 0>(g, s, actor, M, P, table, cap, 0, 0, R, route, hist, 0, mc, cf);
     }
   } else {
     PT_HIP_CHECK(hipMemsetAsync((void*)hist, 0, sizeof(uint32_t) * (R + 1) * G, s));
@@ -764,7 +790,7 @@ int64_t route_prep_scan(uintptr_t actor, int method_uniform, int64_t M, uintptr_
                         uint32_t n_dir, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t route,
                         uintptr_t hist, uintptr_t stats, int rank_self, uint32_t affine_w, uintptr_t stream,
                         int64_t* P_out) {
-  const int64_t G = route_prep(actor, M, table, cap, dir, n_dir, R, route, hist, affine_w, stream, P_out, nullptr);
+  const int64_t G = route_prep(actor, M, table, cap, dir, n_dir, R, route, hist, affine_w, stream, P_out, nullptr, nullptr);
   route_scan(G, R, C, req_words, sendbuf, hist, method_uniform, stats, rank_self, stream);
   return G;
 }

@@ -291,6 +291,7 @@ PYBIND11_MODULE(_hip, m) {
              d["rep_words"] = w.rep_words;
              d["C"] = w.C;
              d["C_alloc"] = w.C_alloc;
+             d["adapted"] = w.adapted;
              d["meta"] = std::vector<uint64_t>(w.meta, w.meta + kMetaWords);
              return d;
            },
@@ -369,6 +370,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("processed", &DeviceServer::processed)
       .def_property_readonly("ring_on_device", &DeviceServer::ring_on_device)
       .def_property_readonly("ring_fds_handed", &DeviceServer::ring_fds_handed)
+      .def_property_readonly("stream_priority", &DeviceServer::stream_priority)
       .def_property_readonly("launches", &DeviceServer::launches)
       .def_property_readonly("exits_idle", &DeviceServer::exits_idle)
       .def_property_readonly("exits_lifetime", &DeviceServer::exits_lifetime)

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <stdexcept>
 #include <string>
 
@@ -93,5 +94,66 @@ __device__ __forceinline__ void spin_ticks(uint64_t ticks) {
 }
 
 inline hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Two-level "last block out" ticket.  Same-address atomics serialise at the
+// memory side (~8-10 ns each on MI355X: 8192 blocks taking one ticket word cost
+// ~80 us, measured), so block b counts itself in group word b % kTicketGroups and
+// the last block of each group counts the group in the top word: no word sees
+// more than G / kTicketGroups + kTicketGroups atomics.  `words` holds
+// kTicketWords u32, zero between launches (the winners reset them).  Call from
+// ONE thread per block, after that block's own device-scope atomics have landed
+// (their returned values consumed); returns true in exactly one block.
+constexpr unsigned kTicketGroups = 64;
+constexpr unsigned kTicketWords = kTicketGroups + 1;
+__device__ __forceinline__ bool last_block_ticket(unsigned* words) {
+  const unsigned G = gridDim.x, g = blockIdx.x % kTicketGroups;
+  const unsigned in_group = (G - g + kTicketGroups - 1) / kTicketGroups;
+  if (atomicAdd(&words[g], 1u) != in_group - 1) return false;
+  atomicExch(&words[g], 0u);
+  const unsigned groups = G < kTicketGroups ? G : kTicketGroups;
+  if (atomicAdd(&words[kTicketGroups], 1u) != groups - 1) return false;
+  atomicExch(&words[kTicketGroups], 0u);
+  return true;
+}
+
+// A stream for PERSISTENT kernels (the dispatcher wave, the mailbox consumer).
+// HIP maps ordinary streams round-robin onto a small pool of hardware queues per
+// priority level (GPU_MAX_HW_QUEUES, 4 on the box), so a persistent kernel on a
+// pooled stream sits in an in-order queue AHEAD of work that later streams put
+// on the same queue -- including the very enqueue it waits for (a live mailbox
+// session then stalls until the consumer's lifetime bound; a Send behind the
+// dispatcher waits for its idle exit: measured 2975 ms, tools/pstream_probe.py).
+// PTYPE_PERSISTENT_STREAM selects the placement:
+//   low    (default) a non-blocking stream at the lowest priority: its own queue
+//          pool, which only persistent kernels use
+//   cumask a CU-masked stream (a dedicated queue, never pooled) -- but HIP makes
+//          it a BLOCKING stream, so legacy null-stream work waits for the
+//          resident kernel (torch's default stream is the null stream)
+//   pooled an ordinary non-blocking stream (the hazard above)
+inline hipStream_t dedicated_stream(int device) {
+  hipStream_t s = nullptr;
+  const char* env = getenv("PTYPE_PERSISTENT_STREAM");
+  const std::string mode = env ? env : "low";
+  if (mode == "cumask") {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {
+      uint32_t mask[32];
+      const uint32_t words = (uint32_t)((cus + 31) / 32) < 32u ? (uint32_t)((cus + 31) / 32) : 32u;
+      for (uint32_t i = 0; i < words; ++i) mask[i] = 0xffffffffu;
+      if (hipExtStreamCreateWithCUMask(&s, words, mask) == hipSuccess) return s;
+    }
+    (void)hipGetLastError();
+  } else if (mode != "pooled") {
+    // HIP reports the range [0 (normal), -1 (high)]; a value above 0 selects the
+    // runtime's low-priority level, whose queue pool ordinary streams never use
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+        hipStreamCreateWithPriority(&s, hipStreamNonBlocking, mode == "high" ? greatest : least + 1) == hipSuccess)
+      return s;
+    (void)hipGetLastError();
+  }
+  PT_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return s;
+}
 
 }  // namespace ptype

@@ -59,14 +59,13 @@ void launch_route_packed(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t 
                          uint32_t affine_w, uintptr_t stream, bool prepped = false);
 int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                    uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out,
-                   const MetaCols* mc = nullptr);
+                   const MetaCols* mc = nullptr, const CapFold* cf = nullptr);
 void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout& L, uintptr_t reply, uintptr_t state,
                             uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
                             const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
                             const std::vector<uintptr_t>& direct, int self, uintptr_t stream);
 void launch_complete_packed(uintptr_t rep, int64_t C, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
                             uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream);
-void launch_hist_cap(uintptr_t hist, int64_t G, int R, uintptr_t meta, uintptr_t stream);
 
 // ---- RCCL entry points (from the library torch loaded)
 namespace engine_detail {
@@ -291,6 +290,8 @@ class EpochEngine {
       use_values_ = true;
     }
     PT_HIP_CHECK(hipMalloc(&meta_dev_, kMetaWords * sizeof(uint64_t)));
+    PT_HIP_CHECK(hipMalloc(&capfold_dev_, kCapFoldWords * sizeof(unsigned)));  // column totals + ticket, self-resetting
+    PT_HIP_CHECK(hipMemset(capfold_dev_, 0, kCapFoldWords * sizeof(unsigned)));
     PT_HIP_CHECK(hipHostMalloc(&meta_host_, kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
   }
   ~EpochEngine() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
@@ -300,6 +301,7 @@ class EpochEngine {
     (void)hipEventDestroy(ev_meta_out_);
     (void)hipStreamDestroy(comm_stream_);
     (void)hipFree(meta_dev_);
+    (void)hipFree(capfold_dev_);
     (void)hipHostFree(meta_host_);
     if (flags_host_) (void)hipHostFree(flags_host_);
     else if (flags_dev_) (void)hipFree(flags_dev_);
@@ -312,6 +314,7 @@ class EpochEngine {
     int64_t req_words = 0, rep_words = 0;
     int64_t C = 0;        // per-peer slot capacity this Send used
     int64_t C_alloc = 0;  // what the buffers hold
+    bool adapted = false; // C was sized from the agreed busiest bucket (meta[kMetaCap])
     uint64_t meta[kMetaWords] = {};
   };
   const WireInfo& last_wire() const { return wire_; }
@@ -393,6 +396,7 @@ class EpochEngine {
     const hipStream_t cs = as_stream(a.stream);
     packed_ = a.packed && collectives();  // v3 only where bytes cross a collective
     C_ = packed_ && adaptive_ && nbufs_ >= chunks_ ? C_alloc_ : C_fixed_;
+    wire_.adapted = false;
     if (packed_) agree_layout(a, cs);
     wire_.C = C_;
     wire_.C_alloc = C_alloc_;
@@ -450,16 +454,16 @@ class EpochEngine {
     const bool adapt = adaptive_ && nbufs_ >= chunks_;
     {
       Timed t(prof_.kernels_ns);
+      // (adaptive: every chunk's pass 1 also folds its busiest column into
+      // meta[kMetaCap] -- CapFold -- so no separate histogram pass runs)
       if (fused) {
         PT_HIP_CHECK(hipMemsetAsync(meta_dev_, 0, kMetaWords * sizeof(uint64_t), cs));
-        prep_with_meta(a, cs);
+        prep_with_meta(a, cs, adapt);
       } else {
         launch_packed_meta(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.n_dir, a.affine_w,
                            (uintptr_t)meta_dev_, (uintptr_t)cs);
         if (adapt) prep_all(a, cs);
       }
-      if (adapt)
-        for (int i = 0; i < chunks_; ++i) launch_hist_cap(bufs_[i].hist, prep_G_[i], R_, (uintptr_t)meta_dev_, (uintptr_t)cs);
     }
     // on the compute stream itself: the previous Send's collectives are complete
     // there already (its completions waited for them), and no cross-stream hop
@@ -496,15 +500,25 @@ class EpochEngine {
     int64_t c = ((need + 63) / 64) * 64;
     c = std::max<int64_t>(64, std::min<int64_t>(c, C_alloc_));
     C_ = c;
+    wire_.adapted = true;
   }
 
-  // Route pass 1 of every chunk (adaptive capacity reads all histograms).
+  CapFold cap_fold() const {
+    CapFold f;
+    f.tot = capfold_dev_;
+    f.ticket = capfold_dev_ + kCapCopies * kMaxCapCols;
+    f.meta = (unsigned long long*)meta_dev_;
+    return f;
+  }
+
+  // Route pass 1 of every chunk, each folding its busiest bucket into the agreement.
   void prep_all(const EngineSend& a, hipStream_t cs) {
+    const CapFold cf = cap_fold();
     for (int i = 0; i < chunks_; ++i) {
       const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
       int64_t P;
       prep_G_[i] = route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route,
-                              bufs_[i].hist, a.affine_w, (uintptr_t)cs, &P);
+                              bufs_[i].hist, a.affine_w, (uintptr_t)cs, &P, nullptr, &cf);
     }
     prepped_ = chunks_;
   }
@@ -527,8 +541,9 @@ class EpochEngine {
   }
 
   // Route pass 1 + the width pass, every chunk (one buffer set each).
-  void prep_with_meta(const EngineSend& a, hipStream_t cs) {
+  void prep_with_meta(const EngineSend& a, hipStream_t cs, bool adapt) {
     if (a.M > 0 && (!a.a0 || !a.actor)) throw std::invalid_argument("packed meta: actor and a0 columns required");
+    const CapFold cf = cap_fold();
     for (int i = 0; i < chunks_; ++i) {
       const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
       const MetaCols mc{(const int64_t*)off(a.a0, lo, 8), (const int64_t*)off(a.a1, lo, 8),
@@ -536,7 +551,7 @@ class EpochEngine {
                         (uint32_t)a.method_uniform, a.n_dir, a.affine_w, (unsigned long long*)meta_dev_};
       int64_t P;
       prep_G_[i] = route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route,
-                              bufs_[i].hist, a.affine_w, (uintptr_t)cs, &P, &mc);
+                              bufs_[i].hist, a.affine_w, (uintptr_t)cs, &P, &mc, adapt ? &cf : nullptr);
     }
     prepped_ = chunks_;
   }
@@ -730,6 +745,7 @@ class EpochEngine {
   bool value_mode_[4 * kMaxBufs] = {};    // how the pending hand-off on that word was signalled
   uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)
   uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
+  unsigned* capfold_dev_ = nullptr;  // CapFold words: column totals [kCapCopies][kMaxCapCols] + ticket
   bool packed_ = false;
   int prepped_ = 0;  // chunks whose route pass 1 ran ahead of the agreement wait (this Send)
   // world 1 without collectives: the fused local Send (batch.hip local_send_kernel);

@@ -728,7 +728,7 @@ Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) 
   if (shards > (uint32_t)kMboxMaxShards) throw std::invalid_argument("mailbox shards <= 4096");
   if (slots < 64) throw std::invalid_argument("mailbox slots per shard >= 64");
   PT_HIP_CHECK(hipSetDevice(device_));
-  PT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  stream_ = dedicated_stream(device_);  // the persistent consumer runs here
   const uint64_t n = (uint64_t)shards * slots;
   PT_HIP_CHECK(hipMalloc((void**)&mv_.rec, n * 32));
   PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, n * 32, stream_));  // tag 0 = never published

@@ -16,7 +16,7 @@ namespace ptype {
 
 int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir, int R,
                    uintptr_t route, uintptr_t hist, uint32_t affine_w, uintptr_t stream, int64_t* P_out,
-                   const MetaCols* mc = nullptr);
+                   const MetaCols* mc = nullptr, const CapFold* cf = nullptr);
 void route_scan(int64_t G, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t hist,
                 int method_uniform, uintptr_t stats, int rank_self, uintptr_t stream);
 int64_t route_grid(int64_t M, int64_t* P_out);
@@ -397,38 +397,4 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int vb, uintptr_t perm, in
                      direct);
   PT_HIP_CHECK(hipGetLastError());
 }
-
-
-// Adaptive slot capacity: the largest destination column total of one chunk's
-// route histograms ([R + 1][G] column-major, column R = registry misses) folded
-// into meta[kMetaCap] (atomic max).  One block per chunk; the engine all-reduces
-// the meta vector, so every rank sizes this Send's slots by the busiest
-// (rank, destination) bucket of the node -- skewed traffic gets the room it
-// needs instead of overflowing into re-send rounds, uniform traffic less padding.
-__global__ __launch_bounds__(1024) void hist_cap_kernel(const uint32_t* __restrict__ hist, int G, int R,
-                                                        unsigned long long* __restrict__ meta) {
-  __shared__ unsigned long long part[1024 / kWave];
-  unsigned long long best = 0;
-  for (int d = 0; d < R; ++d) {
-    unsigned long long s = 0;
-    for (int b = threadIdx.x; b < G; b += blockDim.x) s += hist[(int64_t)d * G + b];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (lane_id() == 0) part[threadIdx.x / kWave] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      unsigned long long t = 0;
-      for (int k = 0; k < (int)(blockDim.x / kWave); ++k) t += part[k];
-      best = t > best ? t : best;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0 && best) atomicMax(&meta[kMetaCap], best);
-}
-
-void launch_hist_cap(uintptr_t hist, int64_t G, int R, uintptr_t meta, uintptr_t stream) {
-  hipLaunchKernelGGL(hist_cap_kernel, dim3(1), dim3(1024), 0, as_stream(stream), (const uint32_t*)hist, (int)G, R,
-                     (unsigned long long*)meta);
-  PT_HIP_CHECK(hipGetLastError());
-}
-
 }  // namespace ptype

@@ -177,6 +177,20 @@ struct MetaCols {
   unsigned long long* meta;
 };
 
+// Adaptive slot capacity folded into route pass 1 (replaces the one-block
+// hist_cap pass: a launch and ~12 us per chunk).  Every block adds its column
+// counts into `tot`; the last block out (ticket) takes the busiest destination
+// column into meta[kMetaCap] (atomic max) and resets `tot` and the ticket, so the
+// words are zero again for the next launch.  Passed BY VALUE.
+struct CapFold {
+  unsigned* tot = nullptr;     // [kCapCopies][kMaxCapCols], zero between launches
+  unsigned* ticket = nullptr;  // [kTicketWords] (last_block_ticket), zero between launches
+  unsigned long long* meta = nullptr;
+};
+constexpr int kMaxCapCols = 65;   // R + 1 <= 64 + 1 (the registry-miss column)
+constexpr unsigned kCapCopies = 16;  // block b adds into copy b % 16 (same-address atomics serialise)
+constexpr size_t kCapFoldWords = kCapCopies * kMaxCapCols + kTicketWords;
+
 // Block-wide reduction of every thread's accumulator into meta[] (atomic max).
 // Every thread of the (256-thread) block must call it.  A block only issues the
 // atomic when its value beats what meta[] already holds (a relaxed read, at worst

@@ -319,7 +319,7 @@ class DeviceServer {
       if (xproc_device_ring_enabled()) export_device_ring();
     }
     for (uint32_t i = 0; i < ring_; ++i) owner_[i].store(i, std::memory_order_relaxed);
-    PT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    stream_ = dedicated_stream(device_);  // the persistent dispatcher runs here
     if (hdr_) {  // publish the segment only once fully initialised
       hdr_->ring = ring_;
       hdr_->owner_pid = (int32_t)getpid();
@@ -335,7 +335,11 @@ class DeviceServer {
     }
   }
 
-  bool ring_on_device() const { return req_on_device_; }  // request ring in device memory (host writes via BAR)
+  bool ring_on_device() const { return req_on_device_; }
+  int stream_priority() const {  // the dispatcher stream's priority (dedicated_stream)
+    int p = 0;
+    return hipStreamGetPriority(stream_, &p) == hipSuccess ? p : -99;
+  }  // request ring in device memory (host writes via BAR)
 
   void close() {
     if (closed_.exchange(true)) return;

@@ -97,7 +97,9 @@ def make_batch(target: int, n_actors: int, device) -> MsgBatch:
 
 
 def check_device(runtime, target: int) -> int:
-    """One batched Send + a device-side gather (smallest divisor found)."""
+    """One batched Send + a device-side gather (smallest divisor found).  The
+    prime workers are co-hosted on the runtime's GPU actors."""
+    runtime.host(SERVICE)
     batch = make_batch(target, runtime.total_actors, runtime.device)
     val, st = runtime.send(SERVICE, batch)
     if not bool((st == STATUS_OK).all()):

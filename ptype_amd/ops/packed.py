@@ -27,7 +27,7 @@ from .records import (METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD, METHOD_ECHO, MET
 from .table import RegistryTable
 
 META_WORDS = 16
-META_MBOX, META_ARG0, META_METHOD, META_MCOL, META_FLAGS = 0, 1, 4, 5, 8
+META_MBOX, META_ARG0, META_METHOD, META_MCOL, META_CAP, META_FLAGS = 0, 1, 4, 5, 6, 8
 
 _U64 = np.uint64
 

@@ -51,6 +51,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import batch as B
+from ..ops.packed import META_CAP
 from ..ops.records import STATUS_OVERFLOW, method_ordered
 from ..ops.table import RegistryTable
 from ..utils import trace
@@ -432,6 +433,8 @@ class ActorExchange:
         slot capacity (native engine, wire v3) skewed traffic fits in the first
         epoch and no re-send round runs."""
         val, st = self.send(req, *(out or ()))
+        if self._fits_for_sure():
+            return val, st
         for _ in range(max_epochs):
             over = st == STATUS_OVERFLOW
             n_over = int(over.sum())
@@ -445,6 +448,16 @@ class ActorExchange:
             val[idx] = v2
             st[idx] = s2
         return val, st
+
+    def _fits_for_sure(self) -> bool:
+        """Whether the last native send provably overflowed no slot on any rank: its
+        capacity was sized from the agreed busiest (rank, destination) bucket of the
+        node and that bucket fit.  Every rank holds the same agreed vector, so all
+        take this exit together -- no count, no host round trip, no agreement."""
+        w = self.last_wire
+        if not (self.use_engine and w is not None and w.get("adapted")):
+            return False
+        return int(w["meta"][META_CAP]) <= int(w["C"])
 
     def _agree_max(self, v: int) -> int:
         """Max of ``v`` over the group (every rank must take the same number of

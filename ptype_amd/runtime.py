@@ -64,6 +64,9 @@ class DeviceRuntime:
         self.rank = d.get_rank(group) if d else 0
         self.world = d.get_world_size(group) if d else 1
         self.service = service
+        # services whose actors are this runtime's actors: the one it joined as, plus
+        # any co-hosted through host()/serve() (one actor id space per runtime)
+        self.hosted: set[str] = {service} if service else set()
         self.actors = int(actors)
         if random_state:
             g = torch.Generator(device=self.device).manual_seed(1234 + self.rank)
@@ -143,6 +146,7 @@ class DeviceRuntime:
         from .mirror import RegistryMirror, ShardLease
 
         self.service = service
+        self.hosted.add(service)
         self.shard_lease = ShardLease(kv, service, node, self.rank, self.world, self.actors)
         self.table.clear()
         self.mirror = RegistryMirror(self.table, kv, service, watch=watch)
@@ -207,10 +211,16 @@ class DeviceRuntime:
         return self._exchange
 
     # ------------------------------------------------------------------ data plane
+    def host(self, service: str) -> None:
+        """Co-host ``service`` on this runtime's actors (the reference registers
+        several net/rpc services on one server; here they share the GPU actors and
+        the registry mirror, and a Send names which one it addresses)."""
+        self.hosted.add(service)
+
     def _check_service(self, service: str | None) -> None:
-        if service and self.service and service != self.service:
-            raise ValueError(f"Send to {service!r}: this process's data plane hosts {self.service!r} "
-                             "(one GPU actor service per runtime)")
+        if service and self.hosted and service not in self.hosted:
+            raise ValueError(f"Send to {service!r}: this process's data plane hosts {sorted(self.hosted)} "
+                             "(co-host more services with DeviceRuntime.host)")
 
     def send(self, service: str | None, batch: B.MsgBatch, resend_overflow: bool = True):
         """Batched Send: every message to its actor anywhere in the node and the
@@ -269,6 +279,7 @@ class DeviceRuntime:
     def serve(self, server, service: str, methods: dict) -> None:
         """Expose GPU handlers over net/rpc: ``methods`` maps a Go method name to
         ``(method_id, [arg field names])`` -- e.g. ``{"Multiply": (1, ["A", "B"])}``."""
+        self.host(service)
         for name, (mid, fields) in methods.items():
             server.RegisterDevice(f"{service}.{name}", self.server, mid, fields)
 

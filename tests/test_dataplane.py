@@ -192,3 +192,25 @@ def test_mirror_k6_sweeps_shards_not_seen(tmp_path, ports, monkeypatch):
         m.close()
     finally:
         c.Close()
+
+
+def test_send_names_a_hosted_service():
+    """A Send names its service: the runtime's own, or one co-hosted on its actors
+    (host() / serve()); anything else is refused instead of silently routed."""
+    import torch
+
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY
+    from ptype_amd.runtime import DeviceRuntime
+
+    rt = DeviceRuntime(torch.device("cpu"), actors=16, service="calculator")
+    rt.place_local()
+    b = B.gen_requests(64, 16, METHOD_CALC_MULTIPLY, seed=3, device="cpu")
+    v, st = rt.send("calculator", b)
+    assert torch.equal(v, b.a0 * b.a1)
+    with pytest.raises(ValueError, match="co-host"):
+        rt.send("Prime", b)
+    rt.host("Prime")
+    v, _ = rt.send("Prime", b)
+    assert torch.equal(v, b.a0 * b.a1)
+    rt.close()
