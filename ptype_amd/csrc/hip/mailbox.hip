@@ -48,9 +48,24 @@ __device__ __forceinline__ unsigned long long* ctr_done(const MboxView& mv, uint
 __device__ __forceinline__ unsigned long long* ctr_head(const MboxView& mv, uint32_t s) {
   return mv.ctr + (uint64_t)s * kMboxCtrStride + 16;
 }
+// A record is two 16-B halves in two planes: plane A {tag, mailbox, origin,
+// method | flags} at rec[slot], plane B {a0, a1} at rec[b_off + slot], so a
+// wave's store of one half covers 64 consecutive 16-B cells -- whole lines.  As
+// one 32-B record per slot (PTYPE_MBOX_PLANAR=0) each store instruction wrote
+// every other 16 B of 64 records: the enqueue's DRAM writes were 419 MB for 268 MB
+// of records (PMC WRITE_SIZE).  Bench mailbox step: 0.247 ms (32-B records) ->
+// 0.215 ms (planes, de-aliased; see the pad below).
+__device__ __forceinline__ uint64_t slot_at(const MboxView& mv, uint32_t s, uint64_t pos) {
+  return ((uint64_t)s << mv.log_q) | (pos & ((1ull << mv.log_q) - 1));
+}
+__device__ __forceinline__ uint32_t* rec_a(const MboxView& mv, uint64_t slot) {
+  return mv.rec + slot * (mv.planar ? 4 : 8);
+}
+__device__ __forceinline__ uint32_t* rec_b(const MboxView& mv, uint64_t slot) {
+  return mv.planar ? mv.rec + mv.b_off + slot * 4 : mv.rec + slot * 8 + 4;
+}
 __device__ __forceinline__ uint32_t* rec_at(const MboxView& mv, uint32_t s, uint64_t pos) {
-  const uint64_t slot = ((uint64_t)s << mv.log_q) | (pos & ((1ull << mv.log_q) - 1));
-  return mv.rec + slot * 8;
+  return rec_a(mv, slot_at(mv, s, pos));
 }
 __device__ __forceinline__ uint32_t lap_tag(const MboxView& mv, uint64_t pos) {
   return (uint32_t)(pos >> mv.log_q) + 1u;
@@ -159,17 +174,16 @@ __device__ __forceinline__ void enqueue_tile(const MboxView& mv, unsigned long l
       continue;
     }
     pos[k] = p;
-    uint32_t* rc = rec_at(mv, s, p);
+    const uint64_t slot = slot_at(mv, s, p);
     const u32x4 hb = {(uint32_t)x0[k], (uint32_t)((uint64_t)x0[k] >> 32), (uint32_t)x1[k],
                       (uint32_t)((uint64_t)x1[k] >> 32)};
-    const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
     if constexpr (LIVE) {
-      st16_sc1(rc + 4, hb);
+      st16_sc1(rec_b(mv, slot), hb);
       if (has_a2)
         __hip_atomic_store(reinterpret_cast<unsigned long long*>(mv.a2 + slot), (unsigned long long)x2[k],
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      *reinterpret_cast<u32x4*>(rc + 4) = hb;
+      *reinterpret_cast<u32x4*>(rec_b(mv, slot)) = hb;
       if (has_a2) mv.a2[slot] = x2[k];
     }
   }
@@ -425,9 +439,9 @@ __global__ __launch_bounds__(256) void mailbox_drain_kernel(MboxView mv, int64_t
     for (int k = 0; k < K; ++k) {
       const uint64_t p = p0 + (uint64_t)k * blockDim.x + threadIdx.x;
       if (p < end) {
-        const uint32_t* rc = rec_at(mv, s, p);
-        ha[k] = *reinterpret_cast<const u32x4*>(rc);
-        hb[k] = *reinterpret_cast<const u32x4*>(rc + 4);
+        const uint64_t slot = slot_at(mv, s, p);
+        ha[k] = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
+        hb[k] = *reinterpret_cast<const u32x4*>(rec_b(mv, slot));
       }
     }
 #pragma unroll
@@ -438,7 +452,7 @@ __global__ __launch_bounds__(256) void mailbox_drain_kernel(MboxView mv, int64_t
         ++holes;
         continue;
       }
-      const uint64_t slot = (uint64_t)(rec_at(mv, s, p) - mv.rec) / 8;
+      const uint64_t slot = slot_at(mv, s, p);
       MboxMsg x = decode(ha[k], hb[k], mv.a2 ? mv.a2 + slot : nullptr);
       if (FIXED) x.m.method = FIXED;
       const ReplyRecord r = run_handler(x.m, state, n_state, delay_ticks, ob);
@@ -488,11 +502,10 @@ __global__ __launch_bounds__(256) void mailbox_drain_ordered_kernel(MboxView mv,
     MboxMsg x;
     x.valid = false;
     if (p < end) {
-      const uint32_t* rc = rec_at(mv, s, p);
-      const u32x4 ha = *reinterpret_cast<const u32x4*>(rc);
-      const u32x4 hb = *reinterpret_cast<const u32x4*>(rc + 4);
+      const uint64_t slot = slot_at(mv, s, p);
+      const u32x4 ha = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
+      const u32x4 hb = *reinterpret_cast<const u32x4*>(rec_b(mv, slot));
       if (ha.x == lap_tag(mv, p)) {
-        const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
         x = decode(ha, hb, mv.a2 ? mv.a2 + slot : nullptr);
         ++done;
       } else {
@@ -564,8 +577,8 @@ __global__ __launch_bounds__(256) void mailbox_consumer_kernel(MboxView mv, Mbox
       MboxMsg x;
       x.valid = false;
       if (lane < n) {
-        const u32x4 hb = ld16_fresh(rc + 4);
-        const uint64_t slot = (uint64_t)(rc - mv.rec) / 8;
+        const uint64_t slot = slot_at(mv, s, p);
+        const u32x4 hb = ld16_fresh(rec_b(mv, slot));
         int64_t a2v = 0;
         if (((ha.w >> 16) & kFlagA2) && mv.a2) a2v = (int64_t)ld_fresh(reinterpret_cast<unsigned long long*>(mv.a2 + slot));
         x = decode(ha, hb, &a2v);
@@ -694,8 +707,11 @@ void launch_mailbox_drain(const MboxView& mv, uintptr_t state, uint32_t n_state,
     hipLaunchKernelGGL(mailbox_drain_ordered_kernel, dim3((S + 3) / 4), dim3(256), 0, st, mv, (int64_t*)state,
                        n_state, delay_ticks, ob, rv);
   } else {
-    // ~2048 blocks over the shards (each block strides over its shard's queue)
-    const unsigned X = S >= 2048 ? 1u : 2048u / S;
+    // ~1024 blocks over the shards (each block strides over its shard's queue).
+    // Measured (8 Mi records, 256 shards): 1024 / 2048 / 4096 blocks 0.232 / 0.237 /
+    // 0.240 ms per mailbox step; 4 records per thread instead of 2: no change.
+    static const unsigned target = getenv("PTYPE_DRAIN_BLOCKS") ? (unsigned)atoi(getenv("PTYPE_DRAIN_BLOCKS")) : 1024u;
+    const unsigned X = S >= target ? 1u : target / S;
     // a Send that knows every queued record's method (uniform batch) drains with
     // that handler constant-folded
     if (fixed_method == kCalculatorMultiply)
@@ -725,14 +741,23 @@ static uint32_t log2_exact(uint32_t v, const char* what) {
 Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) : device_(device) {
   mv_.log_s = log2_exact(shards, "mailbox shards");
   mv_.log_q = log2_exact(slots, "mailbox slots per shard");
+  mv_.planar = !(getenv("PTYPE_MBOX_PLANAR") && std::string(getenv("PTYPE_MBOX_PLANAR")) == "0");
   if (shards > (uint32_t)kMboxMaxShards) throw std::invalid_argument("mailbox shards <= 4096");
   if (slots < 64) throw std::invalid_argument("mailbox slots per shard >= 64");
   PT_HIP_CHECK(hipSetDevice(device_));
   stream_ = dedicated_stream(device_);  // the persistent consumer runs here
   const uint64_t n = (uint64_t)shards * slots;
-  PT_HIP_CHECK(hipMalloc((void**)&mv_.rec, n * 32));
-  PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, n * 32, stream_));  // tag 0 = never published
-  bytes_ = n * 32;
+  // plane B starts past plane A plus a pad: A[slot] and B[slot] are read together,
+  // and a power-of-two distance between them aliases in the HBM address mapping.
+  // Measured (bench mailbox step, PTYPE_MBOX_BPAD sweep): pad 0 / 4.3 KB / 65 KB /
+  // 2 MB / 8 MB / 128 MB: 0.234-0.238 ms; 1 MB + 3.4 KB: 0.215-0.217; 33 MB: 0.219.
+  const uint64_t pad = mv_.planar ? (getenv("PTYPE_MBOX_BPAD") ? (uint64_t)atoll(getenv("PTYPE_MBOX_BPAD")) & ~15ull
+                                                               : 1052032ull) : 0ull;
+  mv_.b_off = (n * 16 + pad) / 4;
+  rec_bytes_ = n * 32 + pad;
+  PT_HIP_CHECK(hipMalloc((void**)&mv_.rec, rec_bytes_));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, rec_bytes_, stream_));  // tag 0 = never published
+  bytes_ = rec_bytes_;
   if (with_a2) {
     PT_HIP_CHECK(hipMalloc((void**)&mv_.a2, n * 8));
     bytes_ += n * 8;
@@ -826,7 +851,7 @@ void Mailboxes::reset(uintptr_t stream) {
   if (started_ && running()) throw std::runtime_error("mailbox reset: consumer running");
   hipStream_t s = as_stream(stream);
   const uint64_t n = (uint64_t)shards() * slots();
-  PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, n * 32, s));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, rec_bytes_, s));
   PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, (size_t)shards() * kMboxCtrStride * 8, s));
   PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStatWords * 8, s));
 }

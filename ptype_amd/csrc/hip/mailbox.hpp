@@ -65,11 +65,15 @@ enum MboxStat : int {
 };
 
 struct MboxView {
-  uint32_t* rec = nullptr;  // [S * Q * 8] words
+  // records: half A {tag, mailbox, origin, method | flags}, half B {a0, a1}, 16 B
+  // each; `planar`: [2][S * Q][4] words (two planes), else [S * Q][8] (32-B records)
+  uint32_t* rec = nullptr;
   int64_t* a2 = nullptr;    // [S * Q]
   unsigned long long* ctr = nullptr;
   unsigned long long* stats = nullptr;
   uint32_t log_s = 0, log_q = 0;
+  uint32_t planar = 0;
+  uint64_t b_off = 0;  // planar: word offset of plane B (past plane A + a de-aliasing pad)
 };
 
 // Host-visible control block of the persistent consumer.
@@ -146,6 +150,7 @@ class Mailboxes {
   int device_;
   MboxView mv_;
   uint64_t bytes_ = 0;
+  uint64_t rec_bytes_ = 0;  // the record planes (+ pad)
   MboxCtrl* ctrl_ = nullptr;   // pinned host
   MboxCtrl* dctrl_ = nullptr;  // its device address
   hipStream_t stream_ = nullptr;
