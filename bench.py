@@ -366,6 +366,8 @@ def main():
     # cluster/rpc.go:59-67; here a node is a GPU of the same host)
     p50 = p50_remote = None
     ring_on_device = None
+    remote_ring = None
+    rtt_errors: list[str] = []
     if use_gpu and args.rtt_calls > 0 and fake is None:
         from ptype_amd.ops import hip
 
@@ -381,28 +383,41 @@ def main():
                 v, s_ = call(METHOD_CALC_MULTIPLY, a, i, 3)[:2]
                 dt = time.perf_counter() - t
                 if v != 3 * i or s_ != STATUS_OK:
-                    raise SystemExit(f"RTT call returned {v}, status {s_}")
+                    raise RuntimeError(f"RTT call returned {v}, status {s_}")
                 if i >= 100:
                     lat.append(dt)
             lat.sort()
             return lat[len(lat) // 2] * 1e6
 
         ring_on_device = bool(srv.ring_on_device)
+        # a failed call is reported, never raised between the barriers: the other
+        # ranks would wait there forever
         try:
             p50 = timed_calls(srv.call)
-            if dist_on:
-                from ptype_amd import _core
-
-                barrier()  # every rank's dispatcher segment exists
-                peer = _core.ShmClient(f"/ptype-bench-{tag}-{(rank + 1) % world}")
-                p50_remote = timed_calls(peer.call)
-                barrier()  # keep serving until every rank is done calling
-        finally:
-            srv.close()
+        except Exception as e:
+            rtt_errors.append(f"local: {e}")
+            p50 = -1.0
         if dist_on:
-            t = torch.tensor([p50, p50_remote], dtype=torch.float64, device=device)
+            from ptype_amd import _core
+
+            barrier()  # every rank's dispatcher segment exists
+            try:
+                peer = _core.ShmClient(f"/ptype-bench-{tag}-{(rank + 1) % world}")
+                remote_ring = peer.ring_placement
+                p50_remote = timed_calls(peer.call)
+            except Exception as e:
+                rtt_errors.append(f"remote: {e}")
+                p50_remote = -1.0
+            barrier()  # keep serving until every rank is done calling
+        srv.close()
+        if dist_on:
+            t = torch.tensor([p50, p50_remote, float(len(rtt_errors))], dtype=torch.float64, device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            p50, p50_remote = (float(x) for x in t.tolist())
+            p50, p50_remote, n_err = (float(x) for x in t.tolist())
+            if n_err and not rtt_errors:
+                rtt_errors.append("on another rank")
+        if rtt_errors:
+            p50 = p50_remote = None
 
     total_msgs = M * world * args.steps
     value = total_msgs / elapsed if elapsed > 0 else 0.0
@@ -425,9 +440,12 @@ def main():
             "p50_rtt_local_us": p50,
             "p50_rtt_remote_us": p50_remote,
             "rtt_path": "host -> GPU actor via the persistent dispatcher's rings (remote: the next rank's "
-                        "process, shared-memory rings on its GPU)",
+                        "process: its GPU's request ring mapped from a dma-buf, replies in shared memory)",
             "rtt_request_ring": None if ring_on_device is None else ("device (host writes via BAR)" if ring_on_device
                                                                       else "pinned host"),
+            # remote: the next rank's GPU ring, mapped here from its dma-buf ("device") or its shm segment
+            "rtt_remote_request_ring": remote_ring,
+            "rtt_error": "; ".join(rtt_errors) if rtt_errors else None,
             "config": {
                 "model": "calculator actor (Calculator.Multiply)",
                 "global_batch": M * world,
