@@ -52,6 +52,10 @@ void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uin
 void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t, uintptr_t);
 int64_t route_grid(int64_t, int64_t*);
+int64_t gob_max_bytes(int64_t, int, uint32_t);
+int64_t gob_ws_words(int64_t);
+void launch_gob_encode(const std::vector<uintptr_t>&, int64_t, uint32_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
+void launch_gob_decode(uintptr_t, uintptr_t, int64_t, uint32_t, const std::vector<uintptr_t>&, uintptr_t, uintptr_t);
 void set_route_tuning(int, int);
 int64_t route_fused_grid(int64_t, int64_t*);
 void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uint32_t, uintptr_t, uintptr_t);
@@ -142,6 +146,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("table_pack", &launch_table_pack, py::arg("table"), py::arg("cap"), py::arg("exp_tbl"), py::arg("out"),
         py::arg("out_exp"), py::arg("out_count"), py::arg("stream"));
 
+  // K4: gob value messages of fixed-schema int structs (csrc/hip/gob.hip)
+  m.def("gob_max_bytes", &gob_max_bytes, py::arg("M"), py::arg("nf"), py::arg("type_id"));
+  m.def("gob_ws_words", &gob_ws_words, py::arg("M"));
+  m.def("gob_encode", &launch_gob_encode, py::arg("cols"), py::arg("M"), py::arg("type_id"), py::arg("out"),
+        py::arg("offsets"), py::arg("ws"), py::arg("stream"));
+  m.def("gob_decode", &launch_gob_decode, py::arg("buf"), py::arg("offsets"), py::arg("M"), py::arg("type_id"),
+        py::arg("cols"), py::arg("status"), py::arg("stream"));
   m.def("gen_requests", &launch_gen_requests, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("M"),
         py::arg("n_actors"), py::arg("seed"), py::arg("seed_ptr"), py::arg("stream"));
   m.def("route_grid", [](int64_t M) {

@@ -457,9 +457,41 @@ def registry(a):
     _emit(out)
 
 
+# --------------------------------------------------------------------------- gob (K4)
+def gob(a):
+    """K4: gob value messages of calculator Args{A, B} for a batch in HBM --
+    encode (size / scan / write passes) and decode (one message per lane)."""
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops import gob as G
+
+    M = a.msgs
+    req = B.gen_requests(M, 1 << 17, seed=5, device="cuda")
+    cols = [req.a0.contiguous(), req.a1.contiguous()]
+    buf, offs = G.encode_structs(cols, 65)
+    back, st = G.decode_structs(buf, offs, 2, 65)
+    torch.cuda.synchronize()
+    assert not bool(st.any()) and torch.equal(back[0], cols[0]) and torch.equal(back[1], cols[1])
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / a.steps
+
+    te = timed(lambda: G.encode_structs(cols, 65))
+    td = timed(lambda: G.decode_structs(buf, offs, 2, 65))
+    nbytes = int(buf.numel())
+    _emit({"config": "K4 gob value messages, calculator Args{A, B}", "messages": M, "gob_bytes": nbytes,
+           "bytes_per_message": nbytes / M, "encode_ms": te * 1e3, "encode_msgs_per_s": M / te,
+           "decode_ms": td * 1e3, "decode_msgs_per_s": M / td, "decode_gob_GBps": nbytes / td / 1e9})
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("which", choices=["host-rpc", "gpu-1m", "optimus", "registry", "tell", "xproc"])
+    p.add_argument("which", choices=["host-rpc", "gpu-1m", "optimus", "registry", "tell", "xproc", "gob"])
     p.add_argument("--calls", type=int, default=4000)
     p.add_argument("--msgs", type=int, default=1 << 20)
     p.add_argument("--steps", type=int, default=20)
@@ -473,7 +505,7 @@ def main():
     if not a.actors:
         a.actors = {"registry": 1 << 20, "optimus": 65536}.get(a.which, 131072)
     {"host-rpc": host_rpc, "gpu-1m": gpu_1m, "optimus": optimus, "registry": registry, "tell": tell,
-     "xproc": xproc}[a.which](a)
+     "xproc": xproc, "gob": gob}[a.which](a)
 
 
 if __name__ == "__main__":
