@@ -303,6 +303,7 @@ PYBIND11_MODULE(_hip, m) {
              d["C"] = w.C;
              d["C_alloc"] = w.C_alloc;
              d["adapted"] = w.adapted;
+             d["exact"] = w.exact;
              d["meta"] = std::vector<uint64_t>(w.meta, w.meta + kMetaWords);
              return d;
            },

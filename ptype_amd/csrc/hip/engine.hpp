@@ -71,29 +71,42 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int vb, uintptr_t perm, in
 namespace engine_detail {
 typedef int (*AllToAllFn)(const void*, void*, size_t, int, void*, hipStream_t);
 typedef int (*AllReduceFn)(const void*, void*, size_t, int, int, void*, hipStream_t);
+typedef int (*SendFn)(const void*, size_t, int, int, void*, hipStream_t);
+typedef int (*RecvFn)(void*, size_t, int, int, void*, hipStream_t);
+typedef int (*GroupFn)();
 typedef const char* (*ErrStrFn)(int);
 constexpr int kNcclInt8 = 0;    // ncclDataType_t ncclInt8
+constexpr int kNcclUint32 = 3;  // ncclDataType_t ncclUint32
 constexpr int kNcclUint64 = 5;  // ncclDataType_t ncclUint64
 constexpr int kNcclMax = 2;     // ncclRedOp_t ncclMax
 
 struct Rccl {
   AllToAllFn alltoall = nullptr;
   AllReduceFn allreduce = nullptr;
+  SendFn send = nullptr;
+  RecvFn recv = nullptr;
+  GroupFn group_start = nullptr, group_end = nullptr;
   ErrStrFn errstr = nullptr;
+  void bind(void* h) {
+    alltoall = (AllToAllFn)dlsym(h, "ncclAllToAll");
+    allreduce = (AllReduceFn)dlsym(h, "ncclAllReduce");
+    send = (SendFn)dlsym(h, "ncclSend");
+    recv = (RecvFn)dlsym(h, "ncclRecv");
+    group_start = (GroupFn)dlsym(h, "ncclGroupStart");
+    group_end = (GroupFn)dlsym(h, "ncclGroupEnd");
+    errstr = (ErrStrFn)dlsym(h, "ncclGetErrorString");
+  }
   Rccl() {
-    alltoall = (AllToAllFn)dlsym(RTLD_DEFAULT, "ncclAllToAll");
-    allreduce = (AllReduceFn)dlsym(RTLD_DEFAULT, "ncclAllReduce");
-    errstr = (ErrStrFn)dlsym(RTLD_DEFAULT, "ncclGetErrorString");
+    bind(RTLD_DEFAULT);
     if (!alltoall)
       for (const char* lib : {"librccl.so", "librccl.so.1"}) {
         void* h = dlopen(lib, RTLD_NOW | RTLD_NOLOAD);
         if (!h) continue;
-        alltoall = (AllToAllFn)dlsym(h, "ncclAllToAll");
-        allreduce = (AllReduceFn)dlsym(h, "ncclAllReduce");
-        errstr = (ErrStrFn)dlsym(h, "ncclGetErrorString");
+        bind(h);
         if (alltoall) break;
       }
   }
+  bool p2p() const { return send && recv && group_start && group_end; }
 };
 inline Rccl& rccl() {
   static Rccl r;
@@ -102,6 +115,7 @@ inline Rccl& rccl() {
 }  // namespace engine_detail
 using engine_detail::rccl;
 using engine_detail::kNcclInt8;
+using engine_detail::kNcclUint32;
 using engine_detail::kNcclMax;
 using engine_detail::kNcclUint64;
 
@@ -127,6 +141,19 @@ __global__ void fake_link_kernel(uint64_t ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
 }
 
+// Loopback exact-size all-to-all as ONE launch: region q's first sizes[q] bytes
+// (a multiple of 16) from src + q * stride to dst + q * stride.
+struct RegionSizes {
+  uint32_t n[64];
+};
+__global__ __launch_bounds__(256) void fake_copy_regions_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                                size_t stride16, RegionSizes sz) {
+  const uint32_t q = blockIdx.y, n16 = sz.n[q] / 16;
+  const uint4* s = src + (size_t)q * stride16;
+  uint4* d = dst + (size_t)q * stride16;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) d[i] = s[i];
+}
+
 class FakeComm {
  public:
   explicit FakeComm(int R, bool loopback = false, double link_gbps = 0.0)
@@ -148,10 +175,33 @@ class FakeComm {
 
   // recv_r[q] = send_q[r], `bytes` per peer region
   void alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) {
+    alltoallv(r, src, dst, bytes, nullptr, s);
+  }
+  // Regions `stride` bytes apart; only the first `recv_bytes[q]` of region q move
+  // (nullptr: whole regions).  Loopback: this rank stands for all, recv = send.
+  void alltoallv(int r, const void* src, void* dst, size_t stride, const size_t* recv_bytes, hipStream_t s) {
     if (loopback_) {
-      PT_HIP_CHECK(hipMemcpyAsync(dst, src, bytes * R_, hipMemcpyDeviceToDevice, s));
+      size_t off_rank = 0;
+      if (!recv_bytes) {
+        PT_HIP_CHECK(hipMemcpyAsync(dst, src, stride * R_, hipMemcpyDeviceToDevice, s));
+        off_rank = stride * (R_ - 1);
+      } else {
+        RegionSizes sz{};
+        size_t biggest = 0;
+        for (int q = 0; q < R_; ++q) {
+          if (recv_bytes[q] % 16 || stride % 16 || recv_bytes[q] > 0xffffffffu)
+            throw std::invalid_argument("FakeComm: regions must be 16-B multiples below 4 GB");
+          sz.n[q] = (uint32_t)recv_bytes[q];
+          biggest = std::max(biggest, recv_bytes[q]);
+          if (q != r) off_rank += recv_bytes[q];
+        }
+        const unsigned gx = (unsigned)std::min<size_t>(std::max<size_t>((biggest / 16 + 255) / 256, 1), 1024);
+        hipLaunchKernelGGL(fake_copy_regions_kernel, dim3(gx, R_), dim3(256), 0, s, (const uint4*)src, (uint4*)dst,
+                           stride / 16, sz);
+        PT_HIP_CHECK(hipGetLastError());
+      }
       if (link_gbps_ > 0) {
-        const double secs = (double)bytes * (R_ - 1) / (link_gbps_ * 1e9);
+        const double secs = (double)off_rank / (link_gbps_ * 1e9);
         const uint64_t ticks = (uint64_t)std::min(secs * 1e8, 1e7);  // at most 100 ms
         hipLaunchKernelGGL(fake_link_kernel, dim3(1), dim3(64), 0, s, ticks);
         PT_HIP_CHECK(hipGetLastError());
@@ -164,8 +214,10 @@ class FakeComm {
     barrier();
     for (int q = 0; q < R_; ++q) {
       PT_HIP_CHECK(hipStreamWaitEvent(s, slots_[q].ready, 0));
-      PT_HIP_CHECK(hipMemcpyAsync((char*)dst + (size_t)q * bytes, (const char*)slots_[q].src + (size_t)r * bytes, bytes,
-                                  hipMemcpyDeviceToDevice, s));
+      const size_t n = recv_bytes ? recv_bytes[q] : stride;
+      if (n)
+        PT_HIP_CHECK(hipMemcpyAsync((char*)dst + (size_t)q * stride, (const char*)slots_[q].src + (size_t)r * stride, n,
+                                    hipMemcpyDeviceToDevice, s));
     }
     PT_HIP_CHECK(hipEventRecord(slots_[r].done, s));
     barrier();
@@ -292,6 +344,10 @@ class EpochEngine {
     PT_HIP_CHECK(hipMalloc(&meta_dev_, kMetaWords * sizeof(uint64_t)));
     PT_HIP_CHECK(hipMalloc(&capfold_dev_, kCapFoldWords * sizeof(unsigned)));  // column totals + ticket, self-resetting
     PT_HIP_CHECK(hipMemset(capfold_dev_, 0, kCapFoldWords * sizeof(unsigned)));
+    // exact-size exchange: per chunk, the counts this rank sends each peer and receives from each
+    PT_HIP_CHECK(hipMalloc(&xcnt_dev_, kXcntWords * sizeof(unsigned)));
+    PT_HIP_CHECK(hipMemset(xcnt_dev_, 0, kXcntWords * sizeof(unsigned)));
+    PT_HIP_CHECK(hipHostMalloc(&xcnt_host_, kXcntWords * sizeof(unsigned), hipHostMallocDefault));
     PT_HIP_CHECK(hipHostMalloc(&meta_host_, kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
   }
   ~EpochEngine() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
@@ -302,6 +358,8 @@ class EpochEngine {
     (void)hipStreamDestroy(comm_stream_);
     (void)hipFree(meta_dev_);
     (void)hipFree(capfold_dev_);
+    (void)hipFree(xcnt_dev_);
+    (void)hipHostFree(xcnt_host_);
     (void)hipHostFree(meta_host_);
     if (flags_host_) (void)hipHostFree(flags_host_);
     else if (flags_dev_) (void)hipFree(flags_dev_);
@@ -315,6 +373,7 @@ class EpochEngine {
     int64_t C = 0;        // per-peer slot capacity this Send used
     int64_t C_alloc = 0;  // what the buffers hold
     bool adapted = false; // C was sized from the agreed busiest bucket (meta[kMetaCap])
+    bool exact = false;   // regions moved at their used size (counts all-to-all + grouped send / recv)
     uint64_t meta[kMetaWords] = {};
   };
   const WireInfo& last_wire() const { return wire_; }
@@ -397,6 +456,9 @@ class EpochEngine {
     packed_ = a.packed && collectives();  // v3 only where bytes cross a collective
     C_ = packed_ && adaptive_ && nbufs_ >= chunks_ ? C_alloc_ : C_fixed_;
     wire_.adapted = false;
+    // exact-size exchange (SURVEY X1 + X2): needs every chunk's counts before the
+    // agreement (adaptive mode preps all chunks) and RCCL's p2p calls
+    exact_ = packed_ && adaptive_ && nbufs_ >= chunks_ && exact_enabled_ && (fake_ || rccl().p2p());
     if (packed_) agree_layout(a, cs);
     wire_.C = C_;
     wire_.C_alloc = C_alloc_;
@@ -407,6 +469,17 @@ class EpochEngine {
     wire_.layout = packed_ ? L_ : PackedLayout{};
     wire_.req_words = R_ * wq;
     wire_.rep_words = R_ * wr;
+    wire_.exact = exact_;
+    if (exact_) {  // what actually moves: the used prefixes, averaged over the chunks
+      int64_t rq = 0, rp = 0;
+      for (int i = 0; i < chunks_; ++i)
+        for (int q = 0; q < R_; ++q) {
+          rq += packed_req_words(std::min<int64_t>(send_count(i, q), C_), L_.S);
+          rp += packed_rep_words(std::min<int64_t>(recv_count(i, q), C_), L_.vb);
+        }
+      wire_.req_words = rq / chunks_;
+      wire_.rep_words = rp / chunks_;
+    }
     const bool local_only = R_ == 1;
     const int n = chunks_;
     std::deque<int> pending;  // chunks whose replies are in flight
@@ -421,7 +494,15 @@ class EpochEngine {
       if (flags_host_) diag_mark(i, cs);  // PTYPE_HANG_DIAG: did this chunk's route kernels finish?
       if (collectives()) {
         handoff(kRouted, bi, cs, comm_stream_);
-        a2a(bufs_[bi].send, bufs_[bi].recv, wq);
+        if (exact_) {
+          for (int q = 0; q < R_; ++q) {
+            xs_[q] = (size_t)packed_req_words(std::min<int64_t>(send_count(i, q), C_), L_.S) * 4;
+            xr_[q] = (size_t)packed_req_words(std::min<int64_t>(recv_count(i, q), C_), L_.S) * 4;
+          }
+          a2av(bufs_[bi].send, bufs_[bi].recv, wq);
+        } else {
+          a2a(bufs_[bi].send, bufs_[bi].recv, wq);
+        }
         signal(kReqIn, bi, comm_stream_);
       }
       if (fwd >= 0) {
@@ -470,7 +551,12 @@ class EpochEngine {
     // sits on this, the one host wait of the Send
     if (fake_ && !fake_->loopback()) {
       fake_->allreduce_max(rank_, meta_dev_, kMetaWords, cs);
+      if (exact_) {
+        exchange_counts(cs);
+        PT_HIP_CHECK(hipStreamSynchronize(cs));  // the copies are on cs; hipMemcpy below does not order after them
+      }
       PT_HIP_CHECK(hipMemcpy(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
+      if (exact_) PT_HIP_CHECK(hipMemcpy(xcnt_host_, xcnt_dev_, kXcntWords * sizeof(unsigned), hipMemcpyDeviceToHost));
       for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
       L_ = packed_layout(meta_host_);
       if (adapt) adapt_capacity();
@@ -482,7 +568,10 @@ class EpochEngine {
     if (rc != 0)
       throw std::runtime_error(std::string("ncclAllReduce failed: ") +
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+    if (exact_) exchange_counts(cs);
     PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost, cs));
+    if (exact_)
+      PT_HIP_CHECK(hipMemcpyAsync(xcnt_host_, xcnt_dev_, kXcntWords * sizeof(unsigned), hipMemcpyDeviceToHost, cs));
     PT_HIP_CHECK(hipEventRecord(ev_meta_out_, cs));
     if (!fused && !adapt) prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
     PT_HIP_CHECK(hipEventSynchronize(ev_meta_out_));
@@ -503,18 +592,40 @@ class EpochEngine {
     wire_.adapted = true;
   }
 
-  CapFold cap_fold() const {
+  CapFold cap_fold(int chunk) const {
     CapFold f;
     f.tot = capfold_dev_;
     f.ticket = capfold_dev_ + kCapCopies * kMaxCapCols;
     f.meta = (unsigned long long*)meta_dev_;
+    f.counts = xcnt_dev_ + (size_t)chunk * kMaxCapCols;  // this chunk's per-destination totals (X1 input)
     return f;
   }
 
+  // X1: every rank learns, per chunk, how many records each peer sends it -- one
+  // 1-word all-to-all per chunk on the counts route pass 1 left behind, queued
+  // before the agreement's D2H copy (so it adds no host wait of its own).
+  void exchange_counts(hipStream_t cs) {
+    for (int i = 0; i < chunks_; ++i) {
+      unsigned* snd = xcnt_dev_ + (size_t)i * kMaxCapCols;
+      unsigned* rcv = xcnt_dev_ + (size_t)(kMaxBufs + i) * kMaxCapCols;
+      if (fake_) {
+        if (fake_->loopback()) PT_HIP_CHECK(hipMemcpyAsync(rcv, snd, R_ * sizeof(unsigned), hipMemcpyDeviceToDevice, cs));
+        else fake_->alltoall(rank_, snd, rcv, sizeof(unsigned), cs);
+        continue;
+      }
+      const int rc = rccl().alltoall(snd, rcv, 1, kNcclUint32, comm_, cs);
+      if (rc != 0)
+        throw std::runtime_error(std::string("ncclAllToAll (counts) failed: ") +
+                                 (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+    }
+  }
+  int64_t send_count(int chunk, int q) const { return xcnt_host_[(size_t)chunk * kMaxCapCols + q]; }
+  int64_t recv_count(int chunk, int q) const { return xcnt_host_[(size_t)(kMaxBufs + chunk) * kMaxCapCols + q]; }
+
   // Route pass 1 of every chunk, each folding its busiest bucket into the agreement.
   void prep_all(const EngineSend& a, hipStream_t cs) {
-    const CapFold cf = cap_fold();
     for (int i = 0; i < chunks_; ++i) {
+      const CapFold cf = cap_fold(i);
       const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
       int64_t P;
       prep_G_[i] = route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route,
@@ -543,8 +654,8 @@ class EpochEngine {
   // Route pass 1 + the width pass, every chunk (one buffer set each).
   void prep_with_meta(const EngineSend& a, hipStream_t cs, bool adapt) {
     if (a.M > 0 && (!a.a0 || !a.actor)) throw std::invalid_argument("packed meta: actor and a0 columns required");
-    const CapFold cf = cap_fold();
     for (int i = 0; i < chunks_; ++i) {
+      const CapFold cf = cap_fold(i);
       const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
       const MetaCols mc{(const int64_t*)off(a.a0, lo, 8), (const int64_t*)off(a.a1, lo, 8),
                         (const int64_t*)off(a.a2, lo, 8), (const uint16_t*)off(a.method_col, lo, 2),
@@ -627,7 +738,15 @@ class EpochEngine {
     }
     if (collectives()) {
       handoff(kServed, bi, cs, comm_stream_);
-      a2a(b.reply, b.back, wr);
+      if (exact_) {  // replies go back to whoever sent: sizes by the received counts
+        for (int q = 0; q < R_; ++q) {
+          xs_[q] = (size_t)packed_rep_words(std::min<int64_t>(recv_count(i, q), C_), L_.vb) * 4;
+          xr_[q] = (size_t)packed_rep_words(std::min<int64_t>(send_count(i, q), C_), L_.vb) * 4;
+        }
+        a2av(b.reply, b.back, wr);
+      } else {
+        a2a(b.reply, b.back, wr);
+      }
       signal(kRepIn, bi, comm_stream_);
     }
   }
@@ -721,6 +840,28 @@ class EpochEngine {
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
   }
 
+  // X2: the regions' used prefixes (xs_ bytes to each peer, xr_ bytes from each)
+  // as grouped ncclSend / ncclRecv; regions stay `stride_words` apart.
+  void a2av(uintptr_t src, uintptr_t dst, int64_t stride_words) {
+    Timed t(prof_.a2a_ns);
+    const size_t stride = (size_t)stride_words * 4;
+    if (fake_) {
+      fake_->alltoallv(rank_, (const void*)src, (void*)dst, stride, xr_, comm_stream_);
+      return;
+    }
+    auto check = [](int rc, const char* what) {
+      if (rc != 0)
+        throw std::runtime_error(std::string(what) + " failed: " +
+                                 (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+    };
+    check(rccl().group_start(), "ncclGroupStart");
+    for (int q = 0; q < R_; ++q) {
+      check(rccl().send((const char*)src + (size_t)q * stride, xs_[q], kNcclInt8, q, comm_, comm_stream_), "ncclSend");
+      check(rccl().recv((char*)dst + (size_t)q * stride, xr_[q], kNcclInt8, q, comm_, comm_stream_), "ncclRecv");
+    }
+    check(rccl().group_end(), "ncclGroupEnd");
+  }
+
   int device_;
   bool collectives() const { return comm_ != nullptr || fake_ != nullptr; }
 
@@ -746,6 +887,13 @@ class EpochEngine {
   uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)
   uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
   unsigned* capfold_dev_ = nullptr;  // CapFold words: column totals [kCapCopies][kMaxCapCols] + ticket
+  // exact-size exchange: [send | recv][kMaxBufs chunks][kMaxCapCols] counts (device, pinned host copy)
+  static constexpr size_t kXcntWords = 2 * kMaxBufs * kMaxCapCols;
+  unsigned* xcnt_dev_ = nullptr;
+  unsigned* xcnt_host_ = nullptr;
+  size_t xs_[kMaxCapCols] = {}, xr_[kMaxCapCols] = {};  // bytes to / from each peer for the a2av in flight
+  bool exact_ = false;  // this Send
+  bool exact_enabled_ = !(getenv("PTYPE_EXCHANGE") && std::string(getenv("PTYPE_EXCHANGE")) == "padded");
   bool packed_ = false;
   int prepped_ = 0;  // chunks whose route pass 1 ran ahead of the agreement wait (this Send)
   // world 1 without collectives: the fused local Send (batch.hip local_send_kernel);

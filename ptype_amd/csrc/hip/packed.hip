@@ -182,8 +182,8 @@ __global__ __launch_bounds__(256) void dispatch_packed_kernel(const uint32_t* __
   const bool valid = (h.w >> 16) & kFlagValid;
   const int64_t count = valid ? (int64_t)(h.x < C ? h.x : C) : 0;
   uint32_t* rp = reply + (int64_t)d * rep_words;
-  uint8_t* vals = reinterpret_cast<uint8_t*>(rp + 4);
-  unsigned long long* okmap = reinterpret_cast<unsigned long long*>(rp + 4 + packed_val_words(C, L.vb));
+  unsigned long long* okmap = reinterpret_cast<unsigned long long*>(rp + 4);  // sized by the count (packed.hpp)
+  uint8_t* vals = reinterpret_cast<uint8_t*>(rp + 4 + packed_ok_words(count));
   if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
   const uint32_t hm = h.w & 0xffffu;
   const bool ident = direct && ((h.w >> 16) & kFlagIdentity);
@@ -212,7 +212,6 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
                                                               int64_t M, int64_t* __restrict__ out_val,
                                                               int32_t* __restrict__ out_st,
                                                               unsigned long long* __restrict__ checksum, bool direct) {
-  const int64_t vw = packed_val_words(C, vb);
   unsigned long long sum = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < M; i0 += stride * kCompU) {
@@ -231,8 +230,9 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
       if (p[u] >= 0) {
         const uint32_t d = (uint32_t)p[u] / C, pos = (uint32_t)p[u] - d * C;
         const uint32_t* rb = rep + (int64_t)d * rep_words;
-        const uint8_t* vals = reinterpret_cast<const uint8_t*>(rb + 4);
-        okw[u] = reinterpret_cast<const unsigned long long*>(rb + 4 + vw)[pos / kWave] >> (pos % kWave);
+        // [header][ok bitmap sized by the region's count][values]
+        const uint8_t* vals = reinterpret_cast<const uint8_t*>(rb + 4 + packed_ok_words(rb[0]));
+        okw[u] = reinterpret_cast<const unsigned long long*>(rb + 4)[pos / kWave] >> (pos % kWave);
         switch (vb) {
           case 1: code[u] = vals[pos]; break;
           case 2: code[u] = reinterpret_cast<const uint16_t*>(vals)[pos]; break;

@@ -67,10 +67,17 @@ __host__ __device__ __forceinline__ uint64_t low_mask(int w) { return w >= 64 ? 
 
 inline int bit_len(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
 
-__host__ __device__ inline int64_t packed_req_words(int64_t C, int S) { return (4 + C * S + 3) & ~3ll; }
-__host__ __device__ inline int64_t packed_val_words(int64_t C, int vb) { return 2 * ((C * vb + 7) / 8); }
-__host__ __device__ inline int64_t packed_rep_words(int64_t C, int vb) {
-  return (4 + packed_val_words(C, vb) + 2 * ((C + 63) / 64) + 3) & ~3ll;
+// Region sizes in u32 words.  A request region of n records: [header 4][n * S];
+// a reply region of n replies: [header 4][ok bitmap 2 * ceil(n / 64)][values
+// n * vb bytes, 8-B padded].  The ok bitmap comes FIRST and both parts are sized
+// by the count, so the used part of a region is a prefix whose length both ends
+// know from the count alone -- what the exact-size exchange (grouped
+// ncclSend / ncclRecv, engine.hpp) moves.  Allocation size: the same with n = C.
+__host__ __device__ inline int64_t packed_req_words(int64_t n, int S) { return (4 + n * S + 3) & ~3ll; }
+__host__ __device__ inline int64_t packed_val_words(int64_t n, int vb) { return 2 * ((n * vb + 7) / 8); }
+__host__ __device__ inline int64_t packed_ok_words(int64_t n) { return 2 * ((n + 63) / 64); }
+__host__ __device__ inline int64_t packed_rep_words(int64_t n, int vb) {
+  return (4 + packed_ok_words(n) + packed_val_words(n, vb) + 3) & ~3ll;
 }
 
 // Reply value bits for the methods present (flags) under argument bounds.
@@ -186,6 +193,7 @@ struct CapFold {
   unsigned* tot = nullptr;     // [kCapCopies][kMaxCapCols], zero between launches
   unsigned* ticket = nullptr;  // [kTicketWords] (last_block_ticket), zero between launches
   unsigned long long* meta = nullptr;
+  unsigned* counts = nullptr;  // optional [R + 1]: this launch's column totals (the exact-size exchange's X1 input)
 };
 constexpr int kMaxCapCols = 65;   // R + 1 <= 64 + 1 (the registry-miss column)
 constexpr unsigned kCapCopies = 16;  // block b adds into copy b % 16 (same-address atomics serialise)

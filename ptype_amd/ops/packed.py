@@ -119,8 +119,13 @@ def val_words(C: int, vb: int) -> int:
     return 2 * ((C * vb + 7) // 8)
 
 
+def ok_words(n: int) -> int:
+    return 2 * ((n + 63) // 64)
+
+
 def rep_words(C: int, vb: int) -> int:
-    return (4 + val_words(C, vb) + 2 * ((C + 63) // 64) + 3) & ~3
+    """[header 4][ok bitmap ok_words(n)][values val_words(n, vb)] (packed.hpp)."""
+    return (4 + ok_words(C) + val_words(C, vb) + 3) & ~3
 
 
 def pack_reference(fields: list[np.ndarray], L: dict) -> np.ndarray:
@@ -259,9 +264,9 @@ def reply_regions(reply: torch.Tensor, R: int, C: int, vb: int):
     for d in range(R):
         reg = buf[d * Wr:(d + 1) * Wr]
         cnt = int(reg[0])
-        vw = val_words(C, vb)
-        codes = reg[4:4 + vw].view(dt)[:cnt].astype(_U64)
-        okw = reg[4 + vw:].view(_U64)
+        ow = ok_words(cnt)
+        codes = reg[4 + ow:4 + ow + val_words(cnt, vb)].view(dt)[:cnt].astype(_U64)
+        okw = reg[4:4 + ow].view(_U64)
         ok = ((okw[np.arange(cnt) // 64] >> (np.arange(cnt) % 64).astype(_U64)) & _U64(1)).astype(bool)
         out.append((cnt, codes, ok))
     return out

@@ -161,8 +161,11 @@ class ActorExchange:
         # all-reduce; the buffers hold `skew_room` x the uniform share per peer, so
         # skewed (Zipf) traffic fits without re-send rounds and uniform traffic moves
         # less padding than the static mean + 8 sigma capacity
-        self.adaptive = bool(self.use_engine and self.packed and self.world > 1 and self.chunks <= 8
-                             and os.environ.get("PTYPE_ADAPTIVE_C", "1") != "0")
+        # (PTYPE_ADAPTIVE_C=force: also at world 1 with forced collectives -- runs the
+        # counts all-to-all and the grouped ncclSend / ncclRecv on a 1-GPU box)
+        ad = os.environ.get("PTYPE_ADAPTIVE_C", "1")
+        self.adaptive = bool(self.use_engine and self.packed and self.chunks <= 8 and ad != "0"
+                             and (self.world > 1 or (ad == "force" and self.force_collectives)))
         room = float(os.environ.get("PTYPE_SKEW_ROOM", "4"))
         self.C_alloc = (max(self.C, min(self.max_chunk, int(math.ceil(room * self.max_chunk / self.world))))
                         if self.adaptive else self.C)

@@ -304,18 +304,22 @@ _ENGINE_SCRIPT = textwrap.dedent("""
         if not det:
             same = same and int(a[0].sum()) == int(b[0].sum())
         out[name] = {"same": bool(same), "S": a[5]["S"], "vb": a[5]["vb"], "toowide": a[6],
-                     "req_words": a[5]["req_words"], "rep_words": a[5]["rep_words"]}
+                     "req_words": a[5]["req_words"], "rep_words": a[5]["rep_words"], "exact": a[5]["exact"]}
     print("RESULT " + json.dumps(out))
     dist.destroy_process_group()
 """)
 
 
 @pytest.mark.gpu
-def test_gpu_engine_packed_rccl_world1():
+@pytest.mark.parametrize("adaptive", ["1", "force"])
+def test_gpu_engine_packed_rccl_world1(adaptive):
     """The native engine with wire v3 over RCCL (agreement all-reduce, packed
     all-to-alls) matches the v2 Python pipeline exactly, and sizes records as
-    packed.hpp says (calculator: 2 dwords + 4-B replies)."""
-    env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT="29563")
+    packed.hpp says (calculator: 2 dwords + 4-B replies).  ``force``: adaptive
+    capacity at world 1, so the exact-size exchange runs on real RCCL -- the
+    counts all-to-all and the grouped ncclSend / ncclRecv (to self)."""
+    env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1",
+               MASTER_PORT="29563" if adaptive == "1" else "29564", PTYPE_ADAPTIVE_C=adaptive)
     r = subprocess.run([sys.executable, "-c", _ENGINE_SCRIPT], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
@@ -327,3 +331,4 @@ def test_gpu_engine_packed_rccl_world1():
     assert out["calc"]["S"] == 2 and out["calc"]["vb"] == 4, out["calc"]
     assert out["calc_unknown"]["S"] == 2 and out["calc_unknown"]["vb"] == 4  # 24-bit mailbox field still fits
     assert out["mixed_big"]["vb"] == 8 and out["counter"]["vb"] == 8
+    assert all(o["exact"] == (adaptive == "force") for o in out.values()), out
