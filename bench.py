@@ -336,7 +336,8 @@ def main():
     diag = None
     if dist_on and use_gpu and ex.last_wire is not None and args.steps:
         w = ex.last_wire
-        sizes = [4 * int(w["req_words"]), 4 * int(w["rep_words"])]  # bytes per chunk, all peers
+        # bytes per chunk, all peers (rounded to a multiple of the world: equal splits)
+        sizes = [(4 * int(w[k]) + world - 1) // world * world for k in ("req_words", "rep_words")]
         bufs = [(torch.empty(s, dtype=torch.uint8, device=device), torch.empty(s, dtype=torch.uint8, device=device))
                 for s in sizes]
 
