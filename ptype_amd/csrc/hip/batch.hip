@@ -197,7 +197,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
       for (unsigned c = 0; c < kCapCopies; ++c)  // memory-side read + reset for the next launch
         t += atomicExch(&cf.tot[c * kMaxCapCols + tid], 0u);
       if (tid < (unsigned)R && t) atomicMax(&cf.meta[kMetaCap], (unsigned long long)t);
-      if (cf.counts) cf.counts[tid] = t;
+      if (cf.counts && tid < (unsigned)R) cf.counts[(size_t)tid * cf.count_stride] = t;
     }
   }
 }

@@ -76,7 +76,6 @@ typedef int (*RecvFn)(void*, size_t, int, int, void*, hipStream_t);
 typedef int (*GroupFn)();
 typedef const char* (*ErrStrFn)(int);
 constexpr int kNcclInt8 = 0;    // ncclDataType_t ncclInt8
-constexpr int kNcclUint32 = 3;  // ncclDataType_t ncclUint32
 constexpr int kNcclUint64 = 5;  // ncclDataType_t ncclUint64
 constexpr int kNcclMax = 2;     // ncclRedOp_t ncclMax
 
@@ -115,7 +114,6 @@ inline Rccl& rccl() {
 }  // namespace engine_detail
 using engine_detail::rccl;
 using engine_detail::kNcclInt8;
-using engine_detail::kNcclUint32;
 using engine_detail::kNcclMax;
 using engine_detail::kNcclUint64;
 
@@ -341,14 +339,15 @@ class EpochEngine {
       }
       use_values_ = true;
     }
-    PT_HIP_CHECK(hipMalloc(&meta_dev_, kMetaWords * sizeof(uint64_t)));
+    // the agreement vector: the v3 column maxima, then (exact-size exchange) the
+    // node's count matrix [src rank][dst rank][chunk] -- one all-reduce(MAX) carries
+    // both, since every rank fills only its own row
+    agree_words_ = kMetaWords + (int64_t)R * R * chunks;
+    PT_HIP_CHECK(hipMalloc(&meta_dev_, agree_words_ * sizeof(uint64_t)));
     PT_HIP_CHECK(hipMalloc(&capfold_dev_, kCapFoldWords * sizeof(unsigned)));  // column totals + ticket, self-resetting
     PT_HIP_CHECK(hipMemset(capfold_dev_, 0, kCapFoldWords * sizeof(unsigned)));
-    // exact-size exchange: per chunk, the counts this rank sends each peer and receives from each
-    PT_HIP_CHECK(hipMalloc(&xcnt_dev_, kXcntWords * sizeof(unsigned)));
-    PT_HIP_CHECK(hipMemset(xcnt_dev_, 0, kXcntWords * sizeof(unsigned)));
-    PT_HIP_CHECK(hipHostMalloc(&xcnt_host_, kXcntWords * sizeof(unsigned), hipHostMallocDefault));
-    PT_HIP_CHECK(hipHostMalloc(&meta_host_, kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
+
+    PT_HIP_CHECK(hipHostMalloc(&meta_host_, agree_words_ * sizeof(uint64_t), hipHostMallocDefault));
   }
   ~EpochEngine() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
     (void)hipSetDevice(device_);
@@ -358,8 +357,7 @@ class EpochEngine {
     (void)hipStreamDestroy(comm_stream_);
     (void)hipFree(meta_dev_);
     (void)hipFree(capfold_dev_);
-    (void)hipFree(xcnt_dev_);
-    (void)hipHostFree(xcnt_host_);
+
     (void)hipHostFree(meta_host_);
     if (flags_host_) (void)hipHostFree(flags_host_);
     else if (flags_dev_) (void)hipFree(flags_dev_);
@@ -537,6 +535,8 @@ class EpochEngine {
       Timed t(prof_.kernels_ns);
       // (adaptive: every chunk's pass 1 also folds its busiest column into
       // meta[kMetaCap] -- CapFold -- so no separate histogram pass runs)
+      if (exact_)  // other ranks' rows of the count matrix must be zero for the MAX
+        PT_HIP_CHECK(hipMemsetAsync(meta_dev_ + kMetaWords, 0, (agree_words_ - kMetaWords) * sizeof(uint64_t), cs));
       if (fused) {
         PT_HIP_CHECK(hipMemsetAsync(meta_dev_, 0, kMetaWords * sizeof(uint64_t), cs));
         prep_with_meta(a, cs, adapt);
@@ -549,14 +549,10 @@ class EpochEngine {
     // on the compute stream itself: the previous Send's collectives are complete
     // there already (its completions waited for them), and no cross-stream hop
     // sits on this, the one host wait of the Send
+    const int64_t n_agree = exact_ ? agree_words_ : kMetaWords;
     if (fake_ && !fake_->loopback()) {
-      fake_->allreduce_max(rank_, meta_dev_, kMetaWords, cs);
-      if (exact_) {
-        exchange_counts(cs);
-        PT_HIP_CHECK(hipStreamSynchronize(cs));  // the copies are on cs; hipMemcpy below does not order after them
-      }
-      PT_HIP_CHECK(hipMemcpy(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
-      if (exact_) PT_HIP_CHECK(hipMemcpy(xcnt_host_, xcnt_dev_, kXcntWords * sizeof(unsigned), hipMemcpyDeviceToHost));
+      fake_->allreduce_max(rank_, meta_dev_, (int)n_agree, cs);
+      PT_HIP_CHECK(hipMemcpy(meta_host_, meta_dev_, n_agree * sizeof(uint64_t), hipMemcpyDeviceToHost));
       for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
       L_ = packed_layout(meta_host_);
       if (adapt) adapt_capacity();
@@ -564,14 +560,11 @@ class EpochEngine {
       prof_.meta_ns += now() - t0;
       return;
     }
-    const int rc = fake_ ? 0 : rccl().allreduce(meta_dev_, meta_dev_, kMetaWords, kNcclUint64, kNcclMax, comm_, cs);
+    const int rc = fake_ ? 0 : rccl().allreduce(meta_dev_, meta_dev_, n_agree, kNcclUint64, kNcclMax, comm_, cs);
     if (rc != 0)
       throw std::runtime_error(std::string("ncclAllReduce failed: ") +
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
-    if (exact_) exchange_counts(cs);
-    PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, kMetaWords * sizeof(uint64_t), hipMemcpyDeviceToHost, cs));
-    if (exact_)
-      PT_HIP_CHECK(hipMemcpyAsync(xcnt_host_, xcnt_dev_, kXcntWords * sizeof(unsigned), hipMemcpyDeviceToHost, cs));
+    PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, n_agree * sizeof(uint64_t), hipMemcpyDeviceToHost, cs));
     PT_HIP_CHECK(hipEventRecord(ev_meta_out_, cs));
     if (!fused && !adapt) prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
     PT_HIP_CHECK(hipEventSynchronize(ev_meta_out_));
@@ -592,35 +585,29 @@ class EpochEngine {
     wire_.adapted = true;
   }
 
+  // Route pass 1 of chunk `chunk` folds its busiest bucket into meta[kMetaCap] and,
+  // for the exact-size exchange, writes its per-destination totals into this
+  // rank's row of the count matrix (X1: the same all-reduce then tells every rank
+  // what each peer sends it -- no count all-to-all, no extra host wait).
   CapFold cap_fold(int chunk) const {
     CapFold f;
     f.tot = capfold_dev_;
     f.ticket = capfold_dev_ + kCapCopies * kMaxCapCols;
     f.meta = (unsigned long long*)meta_dev_;
-    f.counts = xcnt_dev_ + (size_t)chunk * kMaxCapCols;  // this chunk's per-destination totals (X1 input)
+    if (exact_) {
+      f.counts = (unsigned long long*)meta_dev_ + kMetaWords + (size_t)rank_ * R_ * chunks_ + chunk;
+      f.count_stride = (uint32_t)chunks_;
+    }
     return f;
   }
-
-  // X1: every rank learns, per chunk, how many records each peer sends it -- one
-  // 1-word all-to-all per chunk on the counts route pass 1 left behind, queued
-  // before the agreement's D2H copy (so it adds no host wait of its own).
-  void exchange_counts(hipStream_t cs) {
-    for (int i = 0; i < chunks_; ++i) {
-      unsigned* snd = xcnt_dev_ + (size_t)i * kMaxCapCols;
-      unsigned* rcv = xcnt_dev_ + (size_t)(kMaxBufs + i) * kMaxCapCols;
-      if (fake_) {
-        if (fake_->loopback()) PT_HIP_CHECK(hipMemcpyAsync(rcv, snd, R_ * sizeof(unsigned), hipMemcpyDeviceToDevice, cs));
-        else fake_->alltoall(rank_, snd, rcv, sizeof(unsigned), cs);
-        continue;
-      }
-      const int rc = rccl().alltoall(snd, rcv, 1, kNcclUint32, comm_, cs);
-      if (rc != 0)
-        throw std::runtime_error(std::string("ncclAllToAll (counts) failed: ") +
-                                 (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
-    }
+  int64_t send_count(int chunk, int q) const {
+    return (int64_t)meta_host_[kMetaWords + ((size_t)rank_ * R_ + q) * chunks_ + chunk];
   }
-  int64_t send_count(int chunk, int q) const { return xcnt_host_[(size_t)chunk * kMaxCapCols + q]; }
-  int64_t recv_count(int chunk, int q) const { return xcnt_host_[(size_t)(kMaxBufs + chunk) * kMaxCapCols + q]; }
+  int64_t recv_count(int chunk, int p) const {
+    // loopback: this rank stands for every rank of a symmetric node (recv = send)
+    if (fake_ && fake_->loopback()) return send_count(chunk, p);
+    return (int64_t)meta_host_[kMetaWords + ((size_t)p * R_ + rank_) * chunks_ + chunk];
+  }
 
   // Route pass 1 of every chunk, each folding its busiest bucket into the agreement.
   void prep_all(const EngineSend& a, hipStream_t cs) {
@@ -887,10 +874,7 @@ class EpochEngine {
   uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)
   uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
   unsigned* capfold_dev_ = nullptr;  // CapFold words: column totals [kCapCopies][kMaxCapCols] + ticket
-  // exact-size exchange: [send | recv][kMaxBufs chunks][kMaxCapCols] counts (device, pinned host copy)
-  static constexpr size_t kXcntWords = 2 * kMaxBufs * kMaxCapCols;
-  unsigned* xcnt_dev_ = nullptr;
-  unsigned* xcnt_host_ = nullptr;
+  int64_t agree_words_ = kMetaWords;  // meta + count matrix [R][R][chunks]
   size_t xs_[kMaxCapCols] = {}, xr_[kMaxCapCols] = {};  // bytes to / from each peer for the a2av in flight
   bool exact_ = false;  // this Send
   bool exact_enabled_ = !(getenv("PTYPE_EXCHANGE") && std::string(getenv("PTYPE_EXCHANGE")) == "padded");

@@ -193,7 +193,10 @@ struct CapFold {
   unsigned* tot = nullptr;     // [kCapCopies][kMaxCapCols], zero between launches
   unsigned* ticket = nullptr;  // [kTicketWords] (last_block_ticket), zero between launches
   unsigned long long* meta = nullptr;
-  unsigned* counts = nullptr;  // optional [R + 1]: this launch's column totals (the exact-size exchange's X1 input)
+  // optional: this launch's destination totals, counts[q * count_stride] for q < R
+  // (this rank's row of the agreement's count matrix: the exact-size exchange's X1)
+  unsigned long long* counts = nullptr;
+  uint32_t count_stride = 1;
 };
 constexpr int kMaxCapCols = 65;   // R + 1 <= 64 + 1 (the registry-miss column)
 constexpr unsigned kCapCopies = 16;  // block b adds into copy b % 16 (same-address atomics serialise)
