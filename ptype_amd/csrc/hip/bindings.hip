@@ -67,7 +67,7 @@ void launch_packed_meta(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, i
 void launch_dispatch_packed(uintptr_t, int, int64_t, const PackedLayout&, uintptr_t, uintptr_t, uint32_t, uint64_t,
                             uintptr_t, int64_t, const std::vector<uintptr_t>&, uint64_t, const std::vector<uintptr_t>&,
                             int, uintptr_t);
-void launch_complete_packed(uintptr_t, int64_t, int, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool,
+void launch_complete_packed(uintptr_t, int64_t, int, int, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool,
                             uintptr_t);
 void launch_records_to_soa(uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 void launch_snapshot_copy(uintptr_t, uintptr_t, int64_t, uintptr_t);
@@ -244,7 +244,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("layout"), py::arg("reply"), py::arg("state"),
       py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"), py::arg("expected_per_rank"), py::arg("outbox"),
       py::arg("outbox_cap"), py::arg("direct"), py::arg("self"), py::arg("stream"));
-  m.def("complete_packed", &launch_complete_packed, py::arg("rep"), py::arg("C"), py::arg("vb"), py::arg("perm"),
+  m.def("complete_packed", &launch_complete_packed, py::arg("rep"), py::arg("C"), py::arg("R"), py::arg("vb"), py::arg("perm"),
         py::arg("M"), py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"),
         py::arg("stream"));
 

@@ -64,7 +64,7 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
                             uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
                             const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
                             const std::vector<uintptr_t>& direct, int self, uintptr_t stream);
-void launch_complete_packed(uintptr_t rep, int64_t C, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
+void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
                             uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream);
 
 // ---- RCCL entry points (from the library torch loaded)
@@ -746,7 +746,7 @@ class EpochEngine {
     const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M), m = m_of(a, i);
     const EngineBufs& b = bufs_[bi];
     if (packed_)
-      launch_complete_packed(b.back, C_, L_.vb, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4), a.checksum,
+      launch_complete_packed(b.back, C_, R_, L_.vb, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4), a.checksum,
                              a.direct, (uintptr_t)cs);
     else
       launch_complete(collectives() ? b.back : b.reply, C_, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4),

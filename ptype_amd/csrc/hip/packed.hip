@@ -208,10 +208,16 @@ constexpr int kCompU = 4;
 constexpr int32_t kPastBatch = INT32_MIN;  // (perm codes: >= 0 slot position, -1 overflow, -2 no actor, -3 direct)
 
 __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
-                                                              uint32_t C, int vb, const int32_t* __restrict__ perm,
-                                                              int64_t M, int64_t* __restrict__ out_val,
+                                                              uint32_t C, int R, int vb,
+                                                              const int32_t* __restrict__ perm, int64_t M,
+                                                              int64_t* __restrict__ out_val,
                                                               int32_t* __restrict__ out_st,
                                                               unsigned long long* __restrict__ checksum, bool direct) {
+  // each source region's value plane starts past its count-sized ok bitmap: the
+  // offsets once per block in LDS, not a dependent header load per message
+  __shared__ uint32_t voff[kMaxRanks];
+  for (int d = threadIdx.x; d < R; d += blockDim.x) voff[d] = 4 + (uint32_t)packed_ok_words(rep[(int64_t)d * rep_words]);
+  __syncthreads();
   unsigned long long sum = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < M; i0 += stride * kCompU) {
@@ -231,7 +237,7 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
         const uint32_t d = (uint32_t)p[u] / C, pos = (uint32_t)p[u] - d * C;
         const uint32_t* rb = rep + (int64_t)d * rep_words;
         // [header][ok bitmap sized by the region's count][values]
-        const uint8_t* vals = reinterpret_cast<const uint8_t*>(rb + 4 + packed_ok_words(rb[0]));
+        const uint8_t* vals = reinterpret_cast<const uint8_t*>(rb + voff[d]);
         okw[u] = reinterpret_cast<const unsigned long long*>(rb + 4)[pos / kWave] >> (pos % kWave);
         switch (vb) {
           case 1: code[u] = vals[pos]; break;
@@ -390,13 +396,14 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
   PT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_complete_packed(uintptr_t rep, int64_t C, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
+void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
                             uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream) {
   if (M <= 0) return;
   if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
+  if (R < 1 || R > kMaxRanks) throw std::invalid_argument("complete: 1 <= R <= 64");
   if (vb != 1 && vb != 2 && vb != 4 && vb != 8) throw std::invalid_argument("complete: vb in {1,2,4,8}");
   hipLaunchKernelGGL(complete_packed_kernel, dim3(grid_for(M, 256 * kCompU, checksum ? 1024 : 8192)), dim3(256), 0,
-                     as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, vb,
+                     as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R, vb,
                      (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum,
                      direct);
   PT_HIP_CHECK(hipGetLastError());

@@ -250,7 +250,8 @@ def complete(reply: torch.Tensor, perm: torch.Tensor, C: int, vb: int, direct: b
     dev = perm.device
     out_val = torch.empty(M, dtype=torch.int64, device=dev) if out_val is None else out_val
     out_status = torch.empty(M, dtype=torch.int32, device=dev) if out_status is None else out_status
-    hip().complete_packed(_ptr(reply), C, vb, _ptr(perm), M, _ptr(out_val), _ptr(out_status), 0, bool(direct),
+    R = reply.numel() // rep_words(C, vb)
+    hip().complete_packed(_ptr(reply), C, R, vb, _ptr(perm), M, _ptr(out_val), _ptr(out_status), 0, bool(direct),
                           _stream(perm))
     return out_val, out_status
 
