@@ -464,13 +464,7 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
 // actor load -> directory gather -> (branch) -> argument loads, three
 // dependent memory latencies per message, and the random-placement step ran
 // the pass at 59 us vs 38 us for the gather-free affine rule (profiles/README.md).
-//
-// PIPE: a grid of ~one resident wave set that loops over tiles, issuing the NEXT
-// tile's column loads after this tile's directory gathers (so the gathers' wait
-// does not also wait for them: vector memory counters retire in order) and before
-// this tile's gathers are consumed -- the next tile's DRAM latency overlaps this
-// tile's gather latency and compute.
-template <int MODE, int FIXED, int K = 4, bool PIPE = false>
+template <int MODE, int FIXED, int K = 4>
 __global__ __launch_bounds__(256) void local_send_kernel(
     const uint32_t* __restrict__ actor, const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
     const int64_t* __restrict__ a2, const uint16_t* __restrict__ mcol, uint32_t method_uniform, int64_t M,
@@ -480,34 +474,24 @@ __global__ __launch_bounds__(256) void local_send_kernel(
     unsigned long long* __restrict__ checksum) {
   unsigned long long nomatch = 0, failed = 0, sum = 0;
   const int64_t tile = (int64_t)K * blockDim.x;
-  uint32_t a[K];
-  int64_t x0[K], x1[K], x2[K];
-  auto load_tile = [&](int64_t b, uint32_t (&ta)[K], int64_t (&t0)[K], int64_t (&t1)[K], int64_t (&t2)[K]) {
+  for (int64_t base = blockIdx.x * tile; base < M; base += (int64_t)gridDim.x * tile) {
+    uint32_t a[K];
+    int64_t x0[K], x1[K], x2[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int64_t i = b + k * (int64_t)blockDim.x + threadIdx.x;
+      const int64_t i = base + k * (int64_t)blockDim.x + threadIdx.x;
       const bool in = i < M;
-      ta[k] = in ? __builtin_nontemporal_load(actor + i) : 0xffffffffu;
-      t0[k] = in ? __builtin_nontemporal_load(a0 + i) : 0;
-      t1[k] = in && a1 ? __builtin_nontemporal_load(a1 + i) : 0;
-      t2[k] = in && a2 ? __builtin_nontemporal_load(a2 + i) : 0;
+      a[k] = in ? __builtin_nontemporal_load(actor + i) : 0xffffffffu;
+      x0[k] = in ? __builtin_nontemporal_load(a0 + i) : 0;
+      x1[k] = in && a1 ? __builtin_nontemporal_load(a1 + i) : 0;
+      x2[k] = in && a2 ? __builtin_nontemporal_load(a2 + i) : 0;
     }
-  };
-  if (PIPE && (int64_t)blockIdx.x * tile < M) load_tile(blockIdx.x * tile, a, x0, x1, x2);
-  for (int64_t base = blockIdx.x * tile; base < M; base += (int64_t)gridDim.x * tile) {
-    if constexpr (!PIPE) load_tile(base, a, x0, x1, x2);
-    uint32_t na[K];
-    int64_t n0[K], n1[K], n2[K];
-    const int64_t next = base + (int64_t)gridDim.x * tile;
     int r[K];
     uint32_t mb[K];
     if constexpr (MODE == 1) {
       uint32_t w[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) w[k] = a[k] < n_dir ? dir[a[k]] : kDirFallback;  // K gathers in flight
-      if constexpr (PIPE) {  // next tile's columns: issued after the gathers, in flight across them
-        if (next < M) load_tile(next, na, n0, n1, n2);
-      }
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
@@ -517,9 +501,6 @@ __global__ __launch_bounds__(256) void local_send_kernel(
       for (int k = 0; k < K; ++k)  // (a tail lane's id 0xffffffff resolves to nothing: no probe)
         if (w[k] == kDirFallback && a[k] != 0xffffffffu) lookup_entry(table, mask, actor_key(a[k]), r[k], mb[k]);
     } else {
-      if constexpr (PIPE) {
-        if (next < M) load_tile(next, na, n0, n1, n2);
-      }
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         if (MODE == 2 && a[k] < n_dir) {
@@ -556,10 +537,6 @@ __global__ __launch_bounds__(256) void local_send_kernel(
       __builtin_nontemporal_store(rr.value, out_val + i);
       __builtin_nontemporal_store((int32_t)rr.status, out_st + i);
       sum += (unsigned long long)rr.value;
-    }
-    if constexpr (PIPE) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) a[k] = na[k], x0[k] = n0[k], x1[k] = n1[k], x2[k] = n2[k];
     }
   }
   // counters as the slot path keeps them (ws stats: 0 no-actor, 2 handler-failed),
@@ -665,9 +642,6 @@ void set_route_tuning(int prep_items, int mode) {
   g_prep_items = prep_items;
   g_route_mode = mode;
 }
-// local_send_kernel PIPE grid (blocks; 0 = the one-tile-per-block form)
-static unsigned g_local_pipe = getenv("PTYPE_LOCAL_PIPE") ? (unsigned)atoi(getenv("PTYPE_LOCAL_PIPE")) : 0u;
-void set_local_tuning(unsigned pipe_blocks) { g_local_pipe = pipe_blocks; }
 
 void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
                         int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
@@ -883,17 +857,8 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
   const int aw_shift = (affine_w && (affine_w & (affine_w - 1)) == 0) ? __builtin_ctz(affine_w) : -1;
   const int mode = (affine_w && n_dir) ? 2 : (dir && n_dir) ? 1 : 0;
   const bool fixed = !method_col && method_uniform == kCalculatorMultiply;
-  // pipelined variant over `pipe` blocks (0: one tile per block); set_local_tuning / PTYPE_LOCAL_PIPE
-  const unsigned pipe = g_local_pipe;
-  const dim3 g(grid_cap(M, 256 * 4, pipe ? pipe : 8192));
+  const dim3 g(grid_cap(M, 256 * 4, 8192));
 #define PT_LOCAL(MO, FX)                                                                                              \
-  if (pipe)                                                                                                           \
-    hipLaunchKernelGGL((local_send_kernel<MO, FX, 4, true>), g, dim3(256), 0, as_stream(stream), (const uint32_t*)actor, \
-                       (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col,     \
-                       (uint32_t)method_uniform, M, (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir,   \
-                       affine_w, aw_shift, (int64_t*)state, n_state, delay_ticks, ob, (int64_t*)out_val,            \
-                       (int32_t*)out_st, (unsigned long long*)stats, (unsigned long long*)checksum);                \
-  else                                                                                                                \
   hipLaunchKernelGGL((local_send_kernel<MO, FX>), g, dim3(256), 0, as_stream(stream), (const uint32_t*)actor,        \
                      (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col,       \
                      (uint32_t)method_uniform, M, (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir,     \

@@ -57,7 +57,6 @@ int64_t gob_ws_words(int64_t);
 void launch_gob_encode(const std::vector<uintptr_t>&, int64_t, uint32_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_gob_decode(uintptr_t, uintptr_t, int64_t, uint32_t, const std::vector<uintptr_t>&, uintptr_t, uintptr_t);
 void set_route_tuning(int, int);
-void set_local_tuning(unsigned);
 int64_t route_fused_grid(int64_t, int64_t*);
 void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uint32_t, uintptr_t, uintptr_t);
 void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
@@ -154,8 +153,6 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("offsets"), py::arg("ws"), py::arg("stream"));
   m.def("gob_decode", &launch_gob_decode, py::arg("buf"), py::arg("offsets"), py::arg("M"), py::arg("type_id"),
         py::arg("cols"), py::arg("status"), py::arg("stream"));
-  m.def("set_local_tuning", &set_local_tuning, py::arg("pipe_blocks"),
-        "world-1 fused Send: 0 = one tile per block; N = the software-pipelined form over N blocks");
   m.def("gen_requests", &launch_gen_requests, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("M"),
         py::arg("n_actors"), py::arg("seed"), py::arg("seed_ptr"), py::arg("stream"));
   m.def("route_grid", [](int64_t M) {

@@ -25,17 +25,14 @@ def _table(n, affine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("local", ["1", "0", "pipe"])
+@pytest.mark.parametrize("local", ["1", "0"])
 @pytest.mark.parametrize("chunks,affine,mixed", [(1, True, False), (3, True, True), (4, False, True)])
 def test_gpu_engine_matches_python_pipeline(chunks, affine, mixed, local, monkeypatch):
-    """local=1: the engine's fused world-1 Send (local_send_kernel); pipe: its
-    software-pipelined form over a small odd grid (many tiles per block);
-    local=0: the epoch-slot pipeline -- all against the Python slot pipeline."""
-    from ptype_amd.ops import hip
+    """local=1: the engine's fused world-1 Send (local_send_kernel); local=0: its
+    epoch-slot pipeline -- both against the Python slot pipeline."""
     from ptype_amd.parallel.exchange import ActorExchange
 
-    monkeypatch.setenv("PTYPE_LOCAL", "0" if local == "0" else "1")  # read when the engine is built
-    hip().set_local_tuning(37 if local == "pipe" else 0)
+    monkeypatch.setenv("PTYPE_LOCAL", local)  # read when the engine is built
 
     n, M = 3000, 250_001
     gen = torch.Generator().manual_seed(chunks)
@@ -71,7 +68,6 @@ def test_gpu_engine_matches_python_pipeline(chunks, affine, mixed, local, monkey
             a, b = a[det], b[det]
         assert (a == b) if isinstance(a, int) else torch.equal(a, b), k
     assert int((outs[True][1] == STATUS_NO_ACTOR).sum()) > 0
-    hip().set_local_tuning(0)
 
 
 _DIST_SCRIPT = textwrap.dedent("""
