@@ -67,9 +67,14 @@ def test_bench_multi_gpu(nproc):
     if _gpus() < nproc:
         pytest.skip(f"needs {nproc} GPUs (RCCL refuses two ranks on one device)")
     out = _run(nproc, ["--steps", "3", "--warmup", "2", "--rtt-calls", "200"], timeout=900)
-    assert out["n_gpus"] == nproc and out["value"] > 0
-    assert out["config"]["wire"] == "v3-packed"
+    assert out["n_gpus"] == nproc and out["value"] > 0  # (the bench verifies every reply itself)
+    assert out["config"]["wire"] == "v3-packed" and out["config"]["exchange"] == "exact"
     assert out["p50_rtt_remote_us"] is not None and out["diag"]["a2a_only_ms_per_step"] > 0
+    assert out["rtt_error"] is None and out["rtt_remote_request_ring"] == "device"
+    # skewed traffic through the exact-size exchange: no re-send rounds
+    z = _run(nproc, ["--steps", "3", "--warmup", "1", "--rtt-calls", "0", "--zipf", "1.1", "--no-secondary"],
+             timeout=900)
+    assert z["config"]["resend_rounds"] == 0 and z["value"] > 0
 
 
 def test_bench_zipf_cpu():
