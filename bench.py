@@ -50,6 +50,9 @@ def _parse():
     p.add_argument("--cpu", action="store_true", help="gloo/CPU dry run of the same pipeline (tests)")
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the step as a captured hipGraph (auto: single rank)")
+    p.add_argument("--steps-per-graph", type=int, default=1,
+                   help="whole steps per graph replay (small batches: the graph launch shows); "
+                        "steps and warmup must be multiples")
     p.add_argument("--loopback", type=int, default=0, metavar="R",
                    help="profiling only: one GPU runs rank 0 of a symmetric R-rank node with the all-to-alls "
                         "as local copies (FakeComm loopback) -- the compute side of an R-GPU step")
@@ -231,6 +234,9 @@ def main():
     st = torch.empty(M, dtype=torch.int32, device=device)
     pregen = args.zipf > 0 or args.pregen
     use_graph = use_gpu and not pregen and (args.graph == "on" or (args.graph == "auto" and not dist_on and fake is None))
+    if args.steps_per_graph < 1 or (args.steps_per_graph > 1 and (
+            not use_graph or args.steps % args.steps_per_graph or args.warmup % args.steps_per_graph)):
+        raise SystemExit("--steps-per-graph: needs the graph path, and steps / warmup multiples of it")
     pre = []
     if pregen:  # 4 distinct batches per rank, generated before any timing
         for k in range(4):
@@ -256,17 +262,22 @@ def main():
         if use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
             # seed from device memory and the graph advances it, so every replay is a new batch
-            seed_t = torch.tensor([rank * 0x9E3779B9 + 7], dtype=torch.int64, device=device)
+            U = args.steps_per_graph
+            seed_t = torch.tensor([rank * 0x9E3779B9 + 7 + j * 0x1000193 for j in range(U)], dtype=torch.int64,
+                                  device=device)
 
-            def prologue():
-                B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, device=device, out=req, seed_tensor=seed_t)
-                seed_t.add_(0x1000193)
+            def prologue(j=0):  # step j of a replay draws from seed j; the last one advances them all
+                B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, device=device, out=req, seed_tensor=seed_t[j:j + 1])
+                if j == U - 1:
+                    seed_t.add_(U * 0x1000193)
 
-            graph = ex.capture(req, val, st, prologue=prologue, allow_collectives=args.graph == "on")
+            graph = ex.capture(req, val, st, prologue=prologue, allow_collectives=args.graph == "on",
+                               repeat=args.steps_per_graph)
 
         def step(s):
             if graph is not None:
-                graph.replay()
+                if s % args.steps_per_graph == 0:  # one replay runs steps_per_graph whole steps
+                    graph.replay()
                 return
             if pre:
                 ex.send_all(pre[s % len(pre)], out=(val, st))
@@ -463,6 +474,7 @@ def main():
                 **wire_info(ex, req),
                 "client_batch": "SoA (actor u32, A i64, B i64)",
                 "hip_graph": graphed,
+                "steps_per_graph": args.steps_per_graph if graphed else None,
                 **({"load": f"zipf({args.zipf})" if args.zipf > 0 else "uniform", "pregenerated": True,
                     "resend_rounds": ex.counters.resends} if pregen else {}),
                 **({"slot_capacity": ex.last_wire.get("C"), "slot_capacity_alloc": ex.last_wire.get("C_alloc"),

@@ -380,15 +380,18 @@ class ActorExchange:
 
     # ------------------------------------------------------------------
     def capture(self, req: B.MsgBatch, out_val: torch.Tensor, out_status: torch.Tensor, prologue=None,
-                allow_collectives: bool = False) -> "SendGraph":
+                allow_collectives: bool = False, repeat: int = 1) -> "SendGraph":
         """Capture ``send(req)`` (plus an optional ``prologue()``, e.g. a kernel
         that refills ``req``) into a hipGraph for fixed-shape steady-state epochs:
         one graph launch replaces the ~6 kernel launches + host logic per chunk,
-        which is what bounds small batches.  Single rank by default; RCCL
-        collectives are capturable but opt-in (``allow_collectives``)."""
+        which is what bounds small batches.  ``repeat``: that many (prologue +
+        Send) rounds in one graph -- one replay per ``repeat`` steps, for batches
+        small enough that the graph launch itself shows; ``prologue(j)`` then gets
+        the step's index j within the replay.  Single rank by default;
+        RCCL collectives are capturable but opt-in (``allow_collectives``)."""
         if (self.world > 1 or self.force_collectives) and not allow_collectives:
             raise RuntimeError("capture: collectives in a graph are opt-in (allow_collectives=True)")
-        return SendGraph(self, req, out_val, out_status, prologue)
+        return SendGraph(self, req, out_val, out_status, prologue, repeat)
 
     # ------------------------------------------------------------------
     def pump(self, outbox, initial: B.MsgBatch | None = None, max_epochs: int = 1 << 20):
@@ -527,14 +530,23 @@ class SendGraph:
     is a hipGraph on ROCm).  ``replay()`` re-runs every kernel of the epoch(s) on
     whatever ``req`` holds at that moment."""
 
-    def __init__(self, ex: ActorExchange, req: B.MsgBatch, out_val, out_status, prologue=None):
-        self.ex, self.req, self.M = ex, req, req.M
+    def __init__(self, ex: ActorExchange, req: B.MsgBatch, out_val, out_status, prologue=None, repeat: int = 1):
+        if repeat < 1:
+            raise ValueError("repeat >= 1")
+        self.ex, self.req, self.M, self.repeat = ex, req, req.M, int(repeat)
         dev = ex.device
 
-        def body():
+        def one(j=0):
             if prologue is not None:
-                prologue()
+                if self.repeat > 1:
+                    prologue(j)  # the step's index within the replay
+                else:
+                    prologue()
             ex.send(req, out_val, out_status)
+
+        def body():
+            for j in range(self.repeat):
+                one(j)
 
         ex.table.directory()  # build outside the capture if dirty
         # fixed-geometry v2 slots inside the graph (no host wait); the flag covers
@@ -545,7 +557,7 @@ class SendGraph:
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 for _ in range(2):  # warm allocations / lazy state outside the graph
-                    body()
+                    one()
             torch.cuda.current_stream(dev).wait_stream(side)
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
@@ -555,7 +567,8 @@ class SendGraph:
         self.replays = 0
 
     def replay(self) -> None:
+        """One graph launch: ``repeat`` steps."""
         self.graph.replay()
         self.replays += 1
-        self.ex.counters.sent += self.M
-        self.ex.counters.epochs += self.ex.chunks
+        self.ex.counters.sent += self.M * self.repeat
+        self.ex.counters.epochs += self.ex.chunks * self.repeat

@@ -455,6 +455,41 @@ def test_gpu_send_graph_replay():
     assert ex.stats().sent >= 3 * M
 
 
+@pytest.mark.gpu
+def test_gpu_send_graph_repeat():
+    """A graph holding 3 whole steps (prologue + Send each): one replay advances the
+    generator 3 times, and the last step's replies are the ones left in the outputs."""
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    n_actors, M = 2048, 100_000
+    g = RegistryTable(2 * n_actors, device="cuda")
+    _populate(g, n_actors, 1)
+    g.enable_directory(n_actors)
+    ex = ActorExchange(g, M, state=torch.zeros(n_actors, dtype=torch.int64, device="cuda"))
+    req = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=1, device="cuda")
+    val = torch.empty(M, dtype=torch.int64, device="cuda")
+    st = torch.empty(M, dtype=torch.int32, device="cuda")
+    seed_t = torch.tensor([100, 101, 102], dtype=torch.int64, device="cuda")
+    steps = []
+
+    def prologue(j):
+        steps.append(j)
+        B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, device="cuda", out=req, seed_tensor=seed_t[j:j + 1])
+        if j == 2:
+            seed_t.add_(3)
+
+    graph = ex.capture(req, val, st, prologue=prologue, repeat=3)
+    assert steps[-3:] == [0, 1, 2]  # the captured body: steps 0, 1, 2 of a replay
+    s0 = int(seed_t[2].item())
+    sent0 = ex.stats().sent
+    graph.replay()
+    torch.cuda.synchronize()
+    assert int(seed_t[2].item()) == s0 + 3
+    ref = B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=s0, device="cuda")  # the replay's last batch
+    assert torch.equal(req.actor, ref.actor) and torch.equal(val, ref.a0 * ref.a1) and bool((st == STATUS_OK).all())
+    assert ex.stats().sent - sent0 == 3 * M
+
+
 def test_no_kernel_spills_to_scratch():
     """Every gfx950 kernel compiles without scratch (private memory): twice a
     silent spill cost 3x (an indexed probe group) and 56 MB of HBM writes per

@@ -104,8 +104,10 @@ def gpu_1m(a):
     import subprocess
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # 8 whole steps per graph replay: at 1 Mi messages the graph launch is a third of a step
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--msgs-per-gpu", str(a.msgs),
-                        "--steps", str(a.steps), "--warmup", "5", "--actors-per-gpu", str(a.actors)],
+                        "--steps", str(8 * max(1, a.steps // 8)), "--warmup", "8", "--steps-per-graph", "8",
+                        "--actors-per-gpu", str(a.actors)],
                        capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         raise SystemExit(r.stderr[-2000:])
