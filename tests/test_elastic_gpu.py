@@ -1,0 +1,76 @@
+"""The elastic data plane's RCCL branch on HIP, on one GPU.
+
+tests/test_elastic.py kills a rank of a 3-process gloo group.  A real RCCL
+group needs a GPU per rank, so here one process runs the RCCL-specific steps
+the recovery takes: form generation 0 through the replicated store (RCCL
+communicator on this GPU, collectives forced on at world 1), Send, ABORT the
+communicator (``_abort_process_group`` -- what a survivor does when a
+collective fails), form generation 1 through the store, and Send again: the
+actors kept their state and every reply is right.
+"""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+from conftest import ROOT, free_port
+
+_SCRIPT = textwrap.dedent("""
+    import json, os, sys, tempfile, torch
+    sys.path.insert(0, os.environ["PTYPE_ROOT"])
+    os.environ["PTYPE_ADVERTISE_ADDR"] = "127.0.0.1"
+    from ptype_amd import cluster as C
+    from ptype_amd.ops.batch import MsgBatch
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD, STATUS_OK
+    from ptype_amd.parallel.elastic import ElasticDataPlane
+    pp, pc, sp = (int(x) for x in os.environ["PORTS"].split(","))
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "dpg", "g0", sp
+    cfg.member = C.member_config(name="g0", dir=tempfile.mkdtemp(prefix="elg_"),
+                                 lpurls=[f"http://127.0.0.1:{pp}"], apurls=[f"http://127.0.0.1:{pp}"],
+                                 lcurls=[f"http://127.0.0.1:{pc}"], acurls=[f"http://127.0.0.1:{pc}"],
+                                 initial_cluster=f"g0=http://127.0.0.1:{pp}", unsafe_no_fsync=True)
+    c = C.Join(C.background(), cfg)
+    dp = ElasticDataPlane(c, "dpg", world=1, per_rank=4096, device="cuda:0", timeout_s=10.0, grace_s=0.5)
+    dp.start()
+    out = {"backend": dp.backend, "gen0": dp.gen}
+    n = dp.total_actors
+    ids = torch.arange(n, dtype=torch.int32, device="cuda")
+    add = MsgBatch(ids, torch.ones(n, dtype=torch.int64, device="cuda"), None, None, METHOD_COUNTER_ADD)
+    _, st = dp.send_resilient(add)
+    torch.cuda.synchronize()
+    out["forced_collectives"] = bool(dp.exchange.force_collectives)
+    out["ok1"] = bool((st == STATUS_OK).all())
+    dp.recover()  # abort the RCCL communicator, form the next generation through the store
+    out["gen1"] = dp.gen
+    mul = MsgBatch(ids, ids.to(torch.int64), torch.full((n,), 7, dtype=torch.int64, device="cuda"), None,
+                   METHOD_CALC_MULTIPLY)
+    val, st = dp.send_resilient(mul)
+    _, st2 = dp.send_resilient(add)
+    torch.cuda.synchronize()
+    out["ok2"] = bool((st == STATUS_OK).all()) and torch.equal(val, ids.to(torch.int64) * 7)
+    out["ok3"] = bool((st2 == STATUS_OK).all())
+    out["state"] = sorted(int(x) for x in dp.state.unique().tolist())
+    out["recoveries"] = dp.recoveries
+    print("RESULT " + json.dumps(out))
+    dp.close()
+    c.Close()
+""")
+
+
+@pytest.mark.gpu
+def test_elastic_rccl_abort_and_reform_world1():
+    env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1",
+               PORTS=",".join(str(free_port()) for _ in range(3)))
+    r = subprocess.run([sys.executable, "-c", _SCRIPT], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads(line[0][7:])
+    assert out["backend"] == "nccl" and out["forced_collectives"], out
+    assert out["gen0"] == 0 and out["gen1"] == 1 and out["recoveries"] == 1, out
+    assert out["ok1"] and out["ok2"] and out["ok3"], out
+    assert out["state"] == [2], out  # both CounterAdd rounds landed on state kept across the re-formation
