@@ -24,8 +24,15 @@ never repaired in place -- it is aborted and a new *generation* is formed:
 5. the caller's batch is re-sent (``send_resilient``): delivery is
    at-least-once, as with the reference's client retries (rpc.go:107-116).
 
-State of the adopted actors restarts from zero unless the application restores
-it (``DeviceRuntime.save/restore`` snapshots); the control plane itself survives
+Actor state survives a rank loss through **buddy replicas** kept in HBM:
+``replicate()`` (collective; also run every ``replicate_every`` sends) ships
+every block a node hosts to its *buddy* -- the next surviving node after it in
+the original ring -- with one ``ncclSend``/``ncclRecv`` pair per neighbour
+(``batch_isend_irecv``: a point-to-point xGMI copy, no collective over the whole
+group).  The buddy is by construction the node ``ring_placement`` makes adopt
+those blocks if their host dies, so an adopted block resumes from its replica
+(the state as of the last ``replicate``); a block with no replica (two
+neighbours lost at once) restarts from zero.  The control plane itself survives
 the loss of a minority of members (Raft quorum).
 """
 from __future__ import annotations
@@ -68,6 +75,18 @@ def ring_placement(nodes0: list[str], members: list[str]) -> dict[str, list[int]
     return {n: rs for n, rs in own.items() if n in alive}
 
 
+def buddy(nodes0: list[str], members: list[str], node: str) -> str:
+    """The next surviving node after ``node`` in original ring order: the one
+    ``ring_placement`` hands ``node``'s blocks to if ``node`` dies."""
+    alive = set(members)
+    i = nodes0.index(node)
+    for k in range(1, len(nodes0)):
+        n = nodes0[(i + k) % len(nodes0)]
+        if n in alive:
+            return n
+    return node
+
+
 class ElasticDataPlane:
     """Batched ``Send`` over a self-healing process group.
 
@@ -79,7 +98,7 @@ class ElasticDataPlane:
 
     def __init__(self, cluster, service: str, world: int, per_rank: int, device=None, backend: str | None = None,
                  max_batch: int = 1 << 20, chunks: int = 1, timeout_s: float = 10.0, grace_s: float = 8.0,
-                 rendezvous_timeout_s: float = 60.0):
+                 rendezvous_timeout_s: float = 60.0, replicate_every: int = 0):
         self.cluster = cluster
         self.service = service
         self.world0 = int(world)
@@ -101,6 +120,10 @@ class ElasticDataPlane:
         self.exchange: ActorExchange | None = None
         self._tcp_store = None
         self.recoveries = 0
+        self.replicate_every = int(replicate_every)
+        self.replicas: dict[int, torch.Tensor] = {}  # original rank -> its block as of the last replicate()
+        self.restored: list[int] = []  # blocks the last re-formation resumed from a replica
+        self._sends = 0
         if self.backend == "nccl":
             # abort the communicator and raise instead of tearing the process down
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
@@ -144,12 +167,17 @@ class ElasticDataPlane:
         W0, P = self.world0, self.per_rank
         new_blocks = own[self.me]
         state = torch.zeros(P * len(new_blocks), dtype=torch.int64, device=self.device)
+        self.restored = []
         if self.state is not None:  # actors that stay here keep their state
             for j, r in enumerate(new_blocks):
                 if r in self.blocks:
                     i = self.blocks.index(r)
                     state[j * P:(j + 1) * P] = self.state[i * P:(i + 1) * P]
+                elif r in self.replicas:  # adopted: resume from the buddy replica
+                    state[j * P:(j + 1) * P] = self.replicas[r]
+                    self.restored.append(r)
         self.blocks, self.state = new_blocks, state
+        self.replicas = {}  # the ring changed: replicas are re-taken by the next replicate()
         table = RegistryTable(2 * W0 * P, device=self.device)
         k = torch.arange(P, dtype=torch.int64)
         for node, rs in own.items():
@@ -175,14 +203,39 @@ class ElasticDataPlane:
             raise RankFailure(f"generation {self.gen}: {e}") from e
 
     def send_resilient(self, batch: B.MsgBatch, max_recoveries: int = 3):
-        """``send`` + recover-and-resend on rank failure (at-least-once)."""
+        """``send`` + recover-and-resend on rank failure (at-least-once);
+        replicates state every ``replicate_every`` successful sends."""
         for attempt in range(max_recoveries + 1):
             try:
-                return self.send(batch)
+                out = self.send(batch)
+                self._sends += 1
+                if self.replicate_every and self._sends % self.replicate_every == 0:
+                    self.replicate()
+                return out
             except RankFailure:
                 if attempt == max_recoveries:
                     raise
                 self.recover()
+
+    def replicate(self) -> None:
+        """Collective over the current generation: every node sends the blocks
+        it hosts to its buddy and keeps the blocks of the node whose buddy it is,
+        as resident device tensors.  Point-to-point only (two neighbours)."""
+        own = ring_placement(self.nodes0, self.members)
+        dst = buddy(self.nodes0, self.members, self.me)
+        if dst == self.me:  # alone: nothing can adopt these blocks
+            return
+        src = next(n for n in self.members if buddy(self.nodes0, self.members, n) == self.me)
+        P = self.per_rank
+        recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=self.device)
+        ops = [dist.P2POp(dist.isend, self.state, self.members.index(dst)),
+               dist.P2POp(dist.irecv, recv, self.members.index(src))]
+        try:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        except Exception as e:
+            raise RankFailure(f"generation {self.gen}: replicate: {e}") from e
+        self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(own[src])}
 
     def recover(self) -> None:
         """Abort the failed generation, wait for the lease-driven membership to

@@ -6,7 +6,8 @@ its Raft member and registry lease die with it).  The survivors' next ``Send``
 fails inside the collective, they abort the group, wait for the dead node's
 lease to expire, form generation 1 through the replicated store, re-home the
 dead rank's actors and re-send: every actor is reachable again, actors of live
-ranks kept their state, adopted actors restarted from zero.
+ranks kept their state, and the adopted actors resumed from the buddy replica
+taken before the crash (``replicate``), not from zero.
 """
 import os
 
@@ -14,7 +15,7 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from ptype_amd.parallel.elastic import ring_placement
+from ptype_amd.parallel.elastic import buddy, ring_placement
 
 
 def test_ring_placement():
@@ -23,6 +24,14 @@ def test_ring_placement():
     assert ring_placement(n, ["a", "b", "d"]) == {"a": [0], "b": [1], "d": [3, 2]}
     assert ring_placement(n, ["a", "c"]) == {"a": [0, 3], "c": [2, 1]}
     assert ring_placement(n, ["d"]) == {"d": [3, 0, 1, 2]}
+    # the buddy of a node is the adopter of everything it hosts
+    for alive in (n, ["a", "b", "d"], ["a", "c"]):
+        own = ring_placement(n, alive)
+        for h in alive:
+            rest = [x for x in alive if x != h]  # h dies
+            assert buddy(n, alive, h) in rest
+            assert set(own[h]) <= set(ring_placement(n, rest)[buddy(n, alive, h)])
+    assert buddy(n, ["c"], "c") == "c"
 
 
 def _worker(i, pp, pc, sp, crash, q):
@@ -50,6 +59,7 @@ def _worker(i, pp, pc, sp, crash, q):
         add = MsgBatch(ids, torch.ones(n, dtype=torch.int64), None, None, METHOD_COUNTER_ADD)
         _, st = dp.send_resilient(add)
         ok1 = bool((st == STATUS_OK).all()) and bool((dp.state == 3).all())
+        dp.replicate()  # every block now has a copy on its buddy
         if dp.me == dp.nodes0[crash]:
             os._exit(0)  # crash: no group teardown, no lease revoke, member gone
         mul = MsgBatch(ids, ids.to(torch.int64), torch.full((n,), 7, dtype=torch.int64), None, METHOD_CALC_MULTIPLY)
@@ -57,11 +67,11 @@ def _worker(i, pp, pc, sp, crash, q):
         ok2 = bool((st == STATUS_OK).all()) and torch.equal(val, ids.to(torch.int64) * 7)
         _, st = dp.send_resilient(add)
         ok3 = bool((st == STATUS_OK).all())
-        # own block: 3 + 2 increments; adopted block (if any): 2 increments from a fresh start
+        # own block: 3 + 2 increments; adopted block (if any): its replica (3) + 2 increments
         P = dp.per_rank
         own = bool((dp.state[:P] == 5).all())
         adopted = [int(x) for x in dp.state[P:].unique().tolist()]
-        q.put((dp.me, ok1, ok2, ok3, own, adopted, len(dp.members), dp.recoveries, dp.blocks))
+        q.put((dp.me, ok1, ok2, ok3, own, adopted, dp.restored, len(dp.members), dp.recoveries, dp.blocks))
         dp.close()
         c.Close()
     except Exception as e:
@@ -92,9 +102,9 @@ def test_rank_failure_recovery():
             p.kill()
     errors = [r for r in res if r[0] == "error"]
     assert not errors, "\n".join("\n".join(map(str, r)) for r in errors)
-    for me, ok1, ok2, ok3, own, adopted, world, recoveries, blocks in res:
+    for me, ok1, ok2, ok3, own, adopted, restored, world, recoveries, blocks in res:
         assert ok1 and ok2 and ok3 and own, (me, ok1, ok2, ok3, own)
         assert world == 2 and recoveries == 1
         if len(blocks) > 1:
-            assert blocks[1] == crash and adopted == [2]
+            assert blocks[1] == crash and restored == [crash] and adopted == [5], (blocks, restored, adopted)
     assert sorted(len(r[-1]) for r in res) == [1, 2]  # exactly one survivor adopted the dead rank
