@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
 // META: the v3 width pass rides along (the batch's argument columns are read in
 // the same tiles, column maxima published per block into mc.meta), so a packed
 // Send reads its batch once before the agreement instead of twice.
-template <int K, int MODE, bool META = false>
+template <int K, int MODE, bool META = false, bool PIPE = false>
 __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_t* __restrict__ actor, int64_t M,
                                                                    int64_t P, const TableEntry* __restrict__ table,
                                                                    uint64_t mask, const uint32_t* __restrict__ dir,
@@ -93,6 +93,16 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
   // LDS-atomic bound -- SQ_WAIT_INST_LDS 50x the single-destination case)
   unsigned hc = 0;
   MetaAcc macc;
+  // PIPE: the next tile's actor ids are loaded before this tile's directory
+  // gathers, so a wave's HBM latency overlaps its gather latency
+  uint32_t an[K];
+  if constexpr (PIPE) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = lo + k * kRouteThreads + threadIdx.x;
+      an[k] = i < hi ? __builtin_nontemporal_load(actor + i) : 0u;
+    }
+  }
   for (int64_t base = lo; base < hi; base += K * kRouteThreads) {
     uint32_t a[K];
     int r[K];
@@ -101,7 +111,13 @@ __global__ __launch_bounds__(kRouteThreads) void route_prep_kernel(const uint32_
     for (int k = 0; k < K; ++k) {
       const int64_t i = base + k * kRouteThreads + threadIdx.x;
       // streaming column: non-temporal, so it does not evict the route directory from L2
-      a[k] = i < hi ? __builtin_nontemporal_load(actor + i) : 0u;
+      if constexpr (PIPE) {
+        a[k] = an[k];
+        const int64_t j = i + K * kRouteThreads;
+        an[k] = j < hi ? __builtin_nontemporal_load(actor + j) : 0u;
+      } else {
+        a[k] = i < hi ? __builtin_nontemporal_load(actor + i) : 0u;
+      }
     }
     if constexpr (META) {
       int64_t v0[K], v1[K], v2[K];
@@ -638,9 +654,11 @@ int64_t route_grid(int64_t M, int64_t* P_out) {
 // loses (189 vs 139 us at 8 Mi messages); the 3-pass route is the default.
 static int g_prep_items = 0;
 static int g_route_mode = 0;
-void set_route_tuning(int prep_items, int mode) {
+static int g_prep_pipe = 0;  // directory path: >= 0 next tile's ids loaded ahead (default), -1 off
+void set_route_tuning(int prep_items, int mode, int prep_pipe) {
   g_prep_items = prep_items;
   g_route_mode = mode;
+  g_prep_pipe = prep_pipe;
 }
 
 void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
@@ -648,19 +666,19 @@ void launch_route_fused(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a
                         int R, int64_t C, int nargs, bool mc, int64_t req_words, uintptr_t sendbuf, uintptr_t perm,
                         uintptr_t lb, uintptr_t stats, int rank_self, DirectView dv, uintptr_t stream);
 
-template <int K, int MODE>
+template <int K, int MODE, bool PIPE = false>
 static void launch_prep(dim3 g, hipStream_t s, uintptr_t actor, int64_t M, int64_t P, uintptr_t table, uint64_t cap,
                         uintptr_t dir, uint32_t n_dir, int R, uintptr_t route, uintptr_t hist, uint32_t aw = 0,
                         const MetaCols* mc = nullptr, const CapFold* cf = nullptr) {
   const int aw_shift = (aw && (aw & (aw - 1)) == 0) ? __builtin_ctz(aw) : -1;
   const CapFold fold = cf ? *cf : CapFold{};
   if (mc)
-    hipLaunchKernelGGL((route_prep_kernel<K, MODE, true>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
-                       (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
+    hipLaunchKernelGGL((route_prep_kernel<K, MODE, true, PIPE>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor,
+                       M, P, (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
                        (uint32_t*)route, (uint32_t*)hist, *mc, fold);
   else
-    hipLaunchKernelGGL((route_prep_kernel<K, MODE>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor, M, P,
-                       (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
+    hipLaunchKernelGGL((route_prep_kernel<K, MODE, false, PIPE>), g, dim3(kRouteThreads), 0, s, (const uint32_t*)actor,
+                       M, P, (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, aw, aw_shift, R,
                        (uint32_t*)route, (uint32_t*)hist, MetaCols{}, fold);
 }
 
@@ -755,9 +773,18 @@ int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, ui
     if (affine_w && n_dir) {
       launch_prep<4, 2>(g, s, actor, M, P, table, cap, 0, n_dir, R, route, hist, affine_w, mc, cf);
     } else if (dir && n_dir) {
-      // measured (tools/route_bench.py): 1/2/4 items within 2% of each other
-      if (k == 1) launch_prep<1, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
+      // measured (tools/prep_sweep.py, 4 Mi messages, 1M-actor directory, R = 8): prep
+      // 33.3 us at 2 items, 30.3 at 4 items with the next tile's ids loaded ahead
+      // (profiles/r2_prep_sweep.txt) -- the gathers into a directory that does not
+      // fit one XCD's L2 next to the streams bound it, not the id-load latency
+      if (g_prep_pipe >= 0) {
+        if (k == 4) launch_prep<4, 1, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
+        else if (k == 8) launch_prep<8, 1, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
+        else if (k == 2) launch_prep<2, 1, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
+        else launch_prep<4, 1, true>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
+      } else if (k == 1) launch_prep<1, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
       else if (k == 4) launch_prep<4, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
+      else if (k == 8) launch_prep<8, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
       else launch_prep<2, 1>(g, s, actor, M, P, table, cap, dir, n_dir, R, route, hist, 0, mc, cf);
     } else {
       // probe path: 2 lookups in flight per thread is best; 4 costs occupancy (98 VGPRs)

@@ -56,7 +56,7 @@ int64_t gob_max_bytes(int64_t, int, uint32_t);
 int64_t gob_ws_words(int64_t);
 void launch_gob_encode(const std::vector<uintptr_t>&, int64_t, uint32_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_gob_decode(uintptr_t, uintptr_t, int64_t, uint32_t, const std::vector<uintptr_t>&, uintptr_t, uintptr_t);
-void set_route_tuning(int, int);
+void set_route_tuning(int, int, int);
 int64_t route_fused_grid(int64_t, int64_t*);
 void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uint32_t, uintptr_t, uintptr_t);
 void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
@@ -179,8 +179,10 @@ PYBIND11_MODULE(_hip, m) {
     if (roctx().mark) roctx().mark(s.c_str());
   });
   m.def("set_route_tuning", &set_route_tuning, py::arg("prep_items") = 0, py::arg("mode") = 0,
-        "3-pass route_prep items per thread (1, 2, 4; 0 = default); mode 0 = 3-pass prep/scan/scatter "
-        "(default), 1 = single-pass look-back route -- knobs for experiments");
+        py::arg("prep_pipe") = 0,
+        "3-pass route_prep items per thread (1, 2, 4, 8; 0 = default); mode 0 = 3-pass prep/scan/scatter "
+        "(default), 1 = single-pass look-back route; prep_pipe: 0 = default (directory path: next tile's ids "
+        "loaded before this tile's gathers), -1 = off -- knobs for experiments");
   m.def("table_build_dir", &launch_table_build_dir, py::arg("table"), py::arg("cap"), py::arg("dir"),
         py::arg("n_dir"), py::arg("affine_w"), py::arg("affine_stats"), py::arg("stream"));
   m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),

@@ -239,8 +239,9 @@ def test_gpu_route_dispatch_complete(R, fmt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("items,mode", [(0, 1), (1, 0), (2, 0), (4, 0)])
-def test_gpu_route_directory_matches_hash_probe(items, mode):
+@pytest.mark.parametrize("items,mode,pipe", [(0, 1, 0), (1, 0, -1), (2, 0, -1), (4, 0, -1), (8, 0, -1), (0, 0, 0),
+                                             (2, 0, 0), (8, 0, 0)])
+def test_gpu_route_directory_matches_hash_probe(items, mode, pipe):
     """K5b: routing through the dense directory is bit-identical to probing the
     hash table -- ids inside/outside the directory range, deleted ids, and an
     entry too wide for a route word (directory fallback to the probe)."""
@@ -256,10 +257,10 @@ def test_gpu_route_directory_matches_hash_probe(items, mode):
     req = B.gen_requests(M, n_actors + 50, METHOD_CALC_MULTIPLY, seed=99, device="cuda")  # some ids unregistered
     ref = B.gen_requests(M, n_actors + 50, METHOD_CALC_MULTIPLY, seed=99, device="cpu")
     try:
-        ops.hip().set_route_tuning(items, mode)
+        ops.hip().set_route_tuning(items, mode, pipe)
         send, perm, stats = B.route(req, g, R, C)
     finally:
-        ops.hip().set_route_tuning(0, 0)
+        ops.hip().set_route_tuning(0, 0, 0)
     rsend, rperm, rstats = B.route(ref, c, R, C)
     assert torch.equal(perm.cpu(), rperm)
     assert _regions_equal(send, rsend, R, C, B.FULL_FORMAT)
