@@ -487,9 +487,18 @@ __global__ __launch_bounds__(256) void local_send_kernel(
     const TableEntry* __restrict__ table, uint64_t mask, const uint32_t* __restrict__ dir, uint32_t n_dir,
     uint32_t aw, int aw_shift, int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
     int64_t* __restrict__ out_val, int32_t* __restrict__ out_st, unsigned long long* __restrict__ stats,
-    unsigned long long* __restrict__ checksum) {
+    unsigned long long* __restrict__ checksum, unsigned stage_cap, const unsigned long long* __restrict__ m_dev) {
+  if (m_dev) {  // device-counted batch (an outbox bank): M is its capacity, the count says how many
+    const unsigned long long n = *m_dev;
+    if ((int64_t)n < M) M = (int64_t)n;
+  }
   unsigned long long nomatch = 0, failed = 0, sum = 0;
   const int64_t tile = (int64_t)K * blockDim.x;
+  extern __shared__ __align__(16) unsigned char smem[];
+  if (stage_cap) {  // handlers' outbox sends staged per tile (one reservation per block, handlers.hpp)
+    ob.stg = outbox_stage(smem, stage_cap);
+    __syncthreads();
+  }
   for (int64_t base = blockIdx.x * tile; base < M; base += (int64_t)gridDim.x * tile) {
     uint32_t a[K];
     int64_t x0[K], x1[K], x2[K];
@@ -554,6 +563,7 @@ __global__ __launch_bounds__(256) void local_send_kernel(
       __builtin_nontemporal_store((int32_t)rr.status, out_st + i);
       sum += (unsigned long long)rr.value;
     }
+    if (stage_cap) outbox_flush(ob);  // block-uniform: the tile loop bound is the block's
   }
   // counters as the slot path keeps them (ws stats: 0 no-actor, 2 handler-failed),
   // one atomic per block and only when non-zero
@@ -866,7 +876,7 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
                        int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
                        uint32_t affine_w, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
                        const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, uintptr_t out_val, uintptr_t out_st,
-                       uintptr_t stats, uintptr_t checksum, uintptr_t stream) {
+                       uintptr_t stats, uintptr_t checksum, uintptr_t stream, uintptr_t m_dev) {
   if (M <= 0) return;
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
   if (!actor || !a0 || !out_val || !out_st || !stats) throw std::invalid_argument("local send: missing column");
@@ -885,12 +895,16 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
   const int mode = (affine_w && n_dir) ? 2 : (dir && n_dir) ? 1 : 0;
   const bool fixed = !method_col && method_uniform == kCalculatorMultiply;
   const dim3 g(grid_cap(M, 256 * 4, 8192));
+  // outbox sends staged in LDS per 1024-message tile (the hot calculator method never sends)
+  const unsigned stage_cap = outbox_cap && !fixed ? 256 * 4 : 0;
+  const size_t smem = stage_cap ? outbox_stage_bytes(stage_cap) : 0;
 #define PT_LOCAL(MO, FX)                                                                                              \
-  hipLaunchKernelGGL((local_send_kernel<MO, FX>), g, dim3(256), 0, as_stream(stream), (const uint32_t*)actor,        \
+  hipLaunchKernelGGL((local_send_kernel<MO, FX>), g, dim3(256), smem, as_stream(stream), (const uint32_t*)actor,     \
                      (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col,       \
                      (uint32_t)method_uniform, M, (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir,     \
                      affine_w, aw_shift, (int64_t*)state, n_state, delay_ticks, ob, (int64_t*)out_val,              \
-                     (int32_t*)out_st, (unsigned long long*)stats, (unsigned long long*)checksum)
+                     (int32_t*)out_st, (unsigned long long*)stats, (unsigned long long*)checksum, stage_cap,       \
+                     (const unsigned long long*)m_dev)
   if (mode == 2) {
     if (fixed) PT_LOCAL(2, kCalculatorMultiply); else PT_LOCAL(2, 0);
   } else if (mode == 1) {
@@ -899,6 +913,22 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
     if (fixed) PT_LOCAL(0, kCalculatorMultiply); else PT_LOCAL(0, 0);
   }
 #undef PT_LOCAL
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+// Device-driven pump epochs (ActorExchange.pump at world 1): the consumed outbox
+// bank's count becomes the epoch's record and is reset for the bank's next turn.
+__global__ void outbox_advance_kernel(unsigned long long* __restrict__ count, uint64_t cap,
+                                      long long* __restrict__ epoch_m, int64_t j) {
+  const unsigned long long n = count[0];
+  epoch_m[j] = (long long)(n < cap ? n : cap);
+  count[0] = 0;
+}
+
+void launch_outbox_advance(uintptr_t count, uint64_t cap, uintptr_t epoch_m, int64_t j, uintptr_t stream) {
+  if (!count || !epoch_m || j < 0) throw std::invalid_argument("outbox_advance: null buffer or negative index");
+  hipLaunchKernelGGL(outbox_advance_kernel, dim3(1), dim3(1), 0, as_stream(stream), (unsigned long long*)count, cap,
+                     (long long*)epoch_m, j);
   PT_HIP_CHECK(hipGetLastError());
 }
 

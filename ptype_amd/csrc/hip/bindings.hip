@@ -193,8 +193,12 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("method_col"), py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"),
         py::arg("dir"), py::arg("n_dir"), py::arg("affine_w"), py::arg("state"), py::arg("n_state"),
         py::arg("delay_ticks"), py::arg("outbox"), py::arg("outbox_cap"), py::arg("out_val"), py::arg("out_status"),
-        py::arg("stats"), py::arg("checksum"), py::arg("stream"),
-        "world-1 Send: registry resolution + handler dispatch in one pass into the caller's outputs");
+        py::arg("stats"), py::arg("checksum"), py::arg("stream"), py::arg("m_dev") = 0,
+        "world-1 Send: registry resolution + handler dispatch in one pass into the caller's outputs "
+        "(m_dev: a device u64 holding the batch's real length <= M, read by the kernel)");
+  m.def("outbox_advance", &launch_outbox_advance, py::arg("count"), py::arg("cap"), py::arg("epoch_m"), py::arg("j"),
+        py::arg("stream"),
+        "after a device-counted epoch: epoch_m[j] = min(count[0], cap), count[0] = 0 (the consumed bank)");
   m.def("complete", &launch_complete, py::arg("rep"), py::arg("C"), py::arg("perm"), py::arg("M"),
         py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"), py::arg("stream"));
   m.def("records_to_soa", &launch_records_to_soa, py::arg("rec"), py::arg("M"), py::arg("actor"), py::arg("method"),
@@ -283,17 +287,19 @@ PYBIND11_MODULE(_hip, m) {
              int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
              uint32_t affine_w, int nargs, bool mc, uintptr_t out_val, uintptr_t out_st, uintptr_t state,
              uint32_t n_state, uint64_t delay_ticks, const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
-             bool direct, uintptr_t checksum, uintptr_t stream, bool packed, uintptr_t mailboxes, bool ordered) {
+             bool direct, uintptr_t checksum, uintptr_t stream, bool packed, uintptr_t mailboxes, bool ordered,
+             uintptr_t m_dev) {
             e.send(EngineSend{actor, a0, a1, a2, method_col, method_uniform, M, table, cap, dir, n_dir, affine_w,
                               nargs, mc, out_val, out_st, state, n_state, delay_ticks, outbox, outbox_cap, direct,
-                              checksum, stream, packed, mailboxes, ordered});
+                              checksum, stream, packed, mailboxes, ordered, m_dev});
           },
           py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("method_col"),
           py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"),
           py::arg("affine_w"), py::arg("nargs"), py::arg("mc"), py::arg("out_val"), py::arg("out_st"),
           py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"), py::arg("outbox_cap"),
           py::arg("direct"), py::arg("checksum"), py::arg("stream"), py::arg("packed") = false,
-          py::arg("mailboxes") = 0, py::arg("ordered") = false, py::call_guard<py::gil_scoped_release>())
+          py::arg("mailboxes") = 0, py::arg("ordered") = false, py::arg("m_dev") = 0,
+          py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("stream_values", &EpochEngine::stream_values)
       .def("hang_state", &EpochEngine::hang_state, py::arg("compute_stream"))
       .def("last_wire",

@@ -43,7 +43,8 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
                        int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
                        uint32_t affine_w, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
                        const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, uintptr_t out_val, uintptr_t out_st,
-                       uintptr_t stats, uintptr_t checksum, uintptr_t stream);
+                       uintptr_t stats, uintptr_t checksum, uintptr_t stream, uintptr_t m_dev = 0);
+void launch_outbox_advance(uintptr_t count, uint64_t cap, uintptr_t epoch_m, int64_t j, uintptr_t stream);
 void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
                      uintptr_t checksum, bool direct, uintptr_t stream);
 int64_t wire_req_words(int64_t C, int nargs, bool mc);
@@ -292,6 +293,7 @@ struct EngineSend {  // one Send: the batch, the registry, the outputs
   bool packed;       // wire format v3 for this Send (needs collectives; not under graph capture)
   uintptr_t mailboxes = 0;  // Mailboxes*: deliver on receipt through the HBM mailboxes (wire v2, no direct)
   bool ordered = false;     // the batch may carry ordered methods (actor-sharded rings, ordered drain)
+  uintptr_t m_dev = 0;      // u64 on the device: the batch's real length (<= M), read by the kernel (local path)
 };
 
 class EpochEngine {
@@ -445,9 +447,10 @@ class EpochEngine {
       wire_ = WireInfo();
       launch_local_send(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.table, a.cap, a.dir,
                         a.n_dir, a.affine_w, a.state, a.n_state, a.delay_ticks, a.outbox, a.outbox_cap, a.out_val,
-                        a.out_st, bufs_[0].ws, a.checksum, a.stream);
+                        a.out_st, bufs_[0].ws, a.checksum, a.stream, a.m_dev);
       return;
     }
+    if (a.m_dev) throw std::invalid_argument("EpochEngine: a device-counted batch needs the single-rank local path");
     if (a.M > max_chunk_ * chunks_) throw std::invalid_argument("EpochEngine: batch exceeds max_batch");
     if (nbufs_ < 1) throw std::runtime_error("EpochEngine: buffers not set");
     const hipStream_t cs = as_stream(a.stream);

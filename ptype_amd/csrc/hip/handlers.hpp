@@ -14,6 +14,24 @@ namespace ptype {
 // SoA columns in HBM, like a client batch; slots are reserved with ONE atomic
 // per wave (ballot over the emitting lanes, leader adds the popcount, lanes
 // take base + rank).  A full outbox counts drops instead of overwriting.
+//
+// Block staging (OutboxStage, kernels that pass one): the lanes append to an LDS
+// copy of the columns instead, and the block publishes the tile's records with
+// ONE global reservation and coalesced copies (outbox_flush).  Every wave's
+// reservation is an atomic on the same word, and same-address atomics serialise
+// device-wide (~7 ns each): 16 K wave reservations per Mi emitted messages were
+// the whole 113 us of a token-ring epoch.
+struct OutboxStage {
+  unsigned* n = nullptr;  // LDS: records staged (may pass cap: the excess went straight to HBM)
+  unsigned long long* base = nullptr;  // LDS: the block's global reservation
+  uint32_t* actor = nullptr;
+  uint16_t* method = nullptr;
+  int64_t* a0 = nullptr;
+  int64_t* a1 = nullptr;
+  int64_t* a2 = nullptr;
+  unsigned cap = 0;
+};
+
 struct OutboxView {
   uint32_t* actor = nullptr;
   int64_t* a0 = nullptr;
@@ -22,13 +40,79 @@ struct OutboxView {
   uint16_t* method = nullptr;
   unsigned long long* count = nullptr;  // [0] reserved slots, [1] dropped
   uint64_t cap = 0;
+  OutboxStage stg;  // block staging in LDS (stg.n null: off)
 };
+
+// LDS bytes of a stage of `cap` records (the layout outbox_stage() carves).
+__host__ __device__ constexpr size_t outbox_stage_bytes(unsigned cap) {
+  return 16 + (size_t)cap * (3 * sizeof(int64_t) + sizeof(uint32_t) + sizeof(uint16_t)) + 16;
+}
+
+// Carve a stage out of dynamic LDS (`smem`, 16-B aligned) and empty it; call
+// before the first emit and follow with a barrier.
+__device__ __forceinline__ OutboxStage outbox_stage(unsigned char* smem, unsigned cap) {
+  OutboxStage s;
+  s.base = reinterpret_cast<unsigned long long*>(smem);
+  s.n = reinterpret_cast<unsigned*>(smem + 8);
+  s.a0 = reinterpret_cast<int64_t*>(smem + 16);
+  s.a1 = s.a0 + cap;
+  s.a2 = s.a1 + cap;
+  s.actor = reinterpret_cast<uint32_t*>(s.a2 + cap);
+  s.method = reinterpret_cast<uint16_t*>(s.actor + cap);
+  s.cap = cap;
+  if (threadIdx.x == 0) *s.n = 0;
+  return s;
+}
+
+// Block-wide (every thread, block-uniform control flow): one reservation for the
+// staged records, coalesced copies to HBM, stage emptied for the next tile.
+__device__ __forceinline__ void outbox_flush(OutboxView ob) {  // by value, like outbox_emit
+  const OutboxStage s = ob.stg;
+  __syncthreads();  // every emit of the tile has landed in LDS
+  const unsigned n = *s.n < s.cap ? *s.n : s.cap;
+  if (threadIdx.x == 0) *s.base = n ? atomicAdd(&ob.count[0], (unsigned long long)n) : 0ull;
+  __syncthreads();
+  const unsigned long long base = *s.base;
+  unsigned long long drop = 0;
+  for (unsigned j = threadIdx.x; j < n; j += blockDim.x) {
+    const unsigned long long slot = base + j;
+    if (slot < ob.cap) {
+      ob.actor[slot] = s.actor[j];
+      ob.method[slot] = s.method[j];
+      ob.a0[slot] = s.a0[j];
+      ob.a1[slot] = s.a1[j];
+      ob.a2[slot] = s.a2[j];
+    } else {
+      ++drop;
+    }
+  }
+  if (drop) atomicAdd(&ob.count[1], drop);
+  __syncthreads();  // copies read the stage before it is reset
+  if (threadIdx.x == 0) *s.n = 0;
+  __syncthreads();
+}
 
 // Called by the lanes that emit, from inside a (possibly divergent) branch.  The
 // view travels BY VALUE everywhere: taking the address of the kernel argument
 // made hipcc copy it to scratch in every thread (64 B/lane of HBM writes).
 __device__ __forceinline__ void outbox_emit(OutboxView ob, uint32_t actor, uint16_t method, int64_t a0,
                                             int64_t a1, int64_t a2) {
+  if (ob.stg.n) {  // block staging: an LDS atomic per wave
+    const uint64_t sm = __ballot(1);
+    const int sl = __builtin_ctzll(sm);
+    unsigned li = 0;
+    if (lane_id() == (unsigned)sl) li = atomicAdd(ob.stg.n, (unsigned)__popcll(sm));
+    li = __shfl(li, sl) + mbcnt64(sm);
+    if (li < ob.stg.cap) {
+      ob.stg.actor[li] = actor;
+      ob.stg.method[li] = method;
+      ob.stg.a0[li] = a0;
+      ob.stg.a1[li] = a1;
+      ob.stg.a2[li] = a2;
+      return;
+    }
+    // stage full (a handler emitting more than one record per message): straight to HBM
+  }
   const uint64_t m = __ballot(1);  // the lanes executing this emit
   const int leader = __builtin_ctzll(m);
   const unsigned rank = mbcnt64(m);

@@ -185,6 +185,8 @@ class ActorExchange:
         self.counters = EpochStats()
         self._engine = None  # native epoch engine, built on first GPU send
         self._capturing = False  # a captured graph cannot host the v3 agreement (host wait)
+        self._last_mailbox = True  # whether the last send went through the mailboxes (until known: assume so)
+        self._pump_graph = None  # (key, hipGraph of a group of device-pump epochs, its buffers)
         self.last_wire = None  # engine.last_wire() of the latest native send
 
     def _comm_ptr(self) -> int:
@@ -309,7 +311,8 @@ class ActorExchange:
         wq, wr = R * fmt.req_words(C), R * B.WireFormat.rep_words(C)
         self.counters.sent += M
         self.counters.epochs += n
-        if self._use_mailbox(req):
+        self._last_mailbox = self._use_mailbox(req)
+        if self._last_mailbox:
             with trace.range("ptype.send.mailbox"):
                 return self._send_mailbox(req, out_val, out_status)
         if self.use_engine and self._engine is None:
@@ -394,12 +397,15 @@ class ActorExchange:
         return SendGraph(self, req, out_val, out_status, prologue, repeat)
 
     # ------------------------------------------------------------------
-    def pump(self, outbox, initial: B.MsgBatch | None = None, max_epochs: int = 1 << 20):
+    def pump(self, outbox, initial: B.MsgBatch | None = None, max_epochs: int = 1 << 20, check_every: int = 8):
         """Actor-to-actor messaging on the device: deliver ``initial`` (if any),
         then keep routing whatever the dispatched handlers emitted into
         ``outbox`` until every rank's outbox is empty.  Fire-and-forget ("tell")
         semantics: replies of emitted messages are discarded; overflowed slots are
-        re-sent.  Collective; the host reads one count per epoch.
+        re-sent.  Collective; the host reads one count per epoch -- on one rank
+        (native engine, direct delivery) once per ``check_every`` epochs: each
+        epoch's kernel reads its batch length from the outbox bank's device
+        counter, so epochs queue back to back without a host round trip.
         Returns ``(epochs, messages delivered by this rank's sends)``."""
         prev, self.outbox = self.outbox, outbox
         per_send = self.max_chunk * self.chunks
@@ -414,6 +420,9 @@ class ActorExchange:
                 for lo in range(0, mx0, per_send):
                     self.send_all(initial.slice(min(lo, m0), min(m0, lo + per_send)))
                 delivered += m0
+            if self._device_pump_ok(outbox):
+                e, d = self._pump_device(outbox, max_epochs, check_every)
+                return epochs + e, delivered + d
             while epochs < max_epochs:
                 n = outbox.pending()
                 mx = n
@@ -430,6 +439,98 @@ class ActorExchange:
                 epochs += 1
         finally:
             self.outbox = prev
+        return epochs, delivered
+
+    def _device_pump_ok(self, outbox) -> bool:
+        """The single-rank local path (one fused kernel per epoch, no slots) with
+        an outbox whose banks fit one Send."""
+        return bool(self.use_engine and self.world == 1 and not self.force_collectives and self.direct
+                    and self.delivery != "mailbox" and outbox.cap <= self.max_chunk * self.chunks
+                    and os.environ.get("PTYPE_DEVICE_PUMP", "1") != "0" and os.environ.get("PTYPE_LOCAL", "1") != "0")
+
+    def _pump_device(self, outbox, max_epochs: int, check_every: int):
+        """World-1 pump without a host round trip per epoch.  Epoch j sends the
+        active bank's full capacity with its device count as the length
+        (``m_dev``); the handlers emit into the other bank; one tiny kernel
+        records the count and empties the consumed bank.  Epochs go in groups of
+        ``check_every`` (even: a group starts and ends on the same bank), and the
+        host reads a group's counts -- copied to pinned memory behind an event --
+        while the NEXT group already runs, so the GPU never waits for the host.
+        After the first groups, a group is one hipGraph replay (cached while the
+        buffers it points at are unchanged).  ``max_epochs`` is rounded up to a
+        whole group; trailing epochs of an empty outbox are no-op launches."""
+        from ..ops import hip
+
+        k = max(2, check_every + (check_every & 1))
+        cap = outbox.cap
+        dev = self.device
+        d, n_dir, affine = self.table.directory()
+        state = self.state
+        engine = self._get_engine()
+        p0 = outbox.active
+        key = (id(outbox), p0, cap, k, B._ptr(self.table.table), B._ptr(d), n_dir, affine, B._ptr(state),
+               B._ptr(self.checksum), int(self.delay_us))
+        c = self._pump_graph
+        if c is None or c["key"] != key:
+            c = self._pump_graph = {
+                "key": key, "graphs": [None, None],
+                "val": torch.empty(cap, dtype=torch.int64, device=dev),  # replies of tells: discarded
+                "st": torch.empty(cap, dtype=torch.int32, device=dev),
+                "ms": torch.zeros(2, k, dtype=torch.int64, device=dev),
+                "host": torch.zeros(2, k + 1, dtype=torch.int64, pin_memory=True),
+                "ev": [torch.cuda.Event(), torch.cuda.Event()]}
+        val, st, ms, host, ev = c["val"], c["st"], c["ms"], c["host"], c["ev"]
+        start_count = outbox.banks[p0]["count"]  # active again after every (even) group
+
+        def group(h):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            for j in range(k):
+                b = outbox.bank
+                outbox.active ^= 1  # the handlers emit into the other bank (emptied when it was consumed)
+                ob, ob_cap = outbox.view()
+                engine.send(B._ptr(b["actor"]), B._ptr(b["a0"]), B._ptr(b["a1"]), B._ptr(b["a2"]),
+                            B._ptr(b["method"]), 0, cap, B._ptr(self.table.table), self.table.cap, B._ptr(d), n_dir,
+                            affine, 3, True, B._ptr(val), B._ptr(st), B._ptr(state),
+                            0 if state is None else state.numel(), int(self.delay_us) * 100, ob, ob_cap, True,
+                            B._ptr(self.checksum), stream, False, 0, False, B._ptr(b["count"]))
+                hip().outbox_advance(B._ptr(b["count"]), cap, B._ptr(ms[h]), j, stream)
+
+        def launch(h):
+            if c["graphs"][h] is not None:
+                c["graphs"][h].replay()
+            else:
+                group(h)
+            host[h, :k].copy_(ms[h], non_blocking=True)
+            host[h, k:].copy_(start_count[:1], non_blocking=True)  # what is left to pump
+            ev[h].record()
+
+        use_graphs = os.environ.get("PTYPE_PUMP_GRAPH", "1") != "0"
+        epochs = delivered = 0
+        launch(0)
+        launched, h = k, 1
+        while True:
+            more = launched < max_epochs
+            if more:  # the next group runs while this one's counts are read
+                launch(h)
+                launched += k
+            ev[h ^ 1].synchronize()
+            counts = host[h ^ 1, :k].tolist()
+            left = int(host[h ^ 1, k])
+            n_ep = sum(1 for m in counts if m)
+            epochs += n_ep
+            delivered += sum(counts)
+            self.counters.sent += sum(counts)
+            self.counters.epochs += n_ep
+            if not more:
+                break
+            if left == 0:  # the group in flight has nothing to deliver
+                break
+            if use_graphs and c["graphs"][h ^ 1] is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    group(h ^ 1)
+                c["graphs"][h ^ 1] = g
+            h ^= 1
         return epochs, delivered
 
     # ------------------------------------------------------------------
@@ -460,6 +561,8 @@ class ActorExchange:
         capacity was sized from the agreed busiest (rank, destination) bucket of the
         node and that bucket fit.  Every rank holds the same agreed vector, so all
         take this exit together -- no count, no host round trip, no agreement."""
+        if self.world == 1 and not self.force_collectives and not self._last_mailbox and self.C >= self.max_chunk:
+            return True  # one destination whose slot holds a whole chunk: nothing can overflow
         w = self.last_wire
         if not (self.use_engine and w is not None and w.get("adapted")):
             return False
