@@ -427,7 +427,12 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
                                                        int64_t C, uint32_t* __restrict__ reply, int64_t rep_words,
                                                        int64_t* __restrict__ state, uint32_t n_state,
                                                        uint64_t delay_ticks, unsigned long long* __restrict__ stats,
-                                                       OutboxView ob, DirectView dv) {
+                                                       OutboxView ob, DirectView dv, unsigned stage_cap) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  if (stage_cap) {  // handlers' outbox sends staged in LDS, published once per block (handlers.hpp)
+    ob.stg = outbox_stage(smem, stage_cap);
+    __syncthreads();
+  }
   const int d = blockIdx.y;
   const bool direct = dv.src != nullptr && d == dv.self;
   const uint32_t* rq = recv + (int64_t)d * req_words;
@@ -461,6 +466,7 @@ __global__ __launch_bounds__(256) void dispatch_kernel(const uint32_t* __restric
   } else {
     failed = dispatch_range<NARGS, MC, 0>(rq, count, hm, vals, sts, state, n_state, delay_ticks, obp, dv, direct, ident);
   }
+  if (stage_cap) outbox_flush(ob);  // every thread of the block reaches here
   for (int off = 32; off > 0; off >>= 1) failed += __shfl_xor(failed, off);
   if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);
 }
@@ -853,10 +859,12 @@ void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintp
   const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
   const unsigned gx = grid_cap(per, 256, (unsigned)(4096 / R > 0 ? 4096 / R : 1));
   const int64_t req_words = wire_req_words(C, nargs, mc), rep_words = wire_rep_words(C);
+  const unsigned stage_cap = outbox_cap ? kOutboxStage : 0;  // LDS stage only where handlers can send
+  const size_t smem = stage_cap ? outbox_stage_bytes(stage_cap) : 0;
 #define PT_DISPATCH(NA, MCV)                                                                                    \
-  hipLaunchKernelGGL((dispatch_kernel<NA, MCV>), dim3(gx, R), dim3(256), 0, as_stream(stream),                  \
+  hipLaunchKernelGGL((dispatch_kernel<NA, MCV>), dim3(gx, R), dim3(256), smem, as_stream(stream),               \
                      (const uint32_t*)recv, req_words, C, (uint32_t*)reply, rep_words, (int64_t*)state, n_state, \
-                     delay_ticks, (unsigned long long*)stats, ob, dv)
+                     delay_ticks, (unsigned long long*)stats, ob, dv, stage_cap)
   PT_FORMAT_SWITCH(nargs, mc, PT_DISPATCH)
 #undef PT_DISPATCH
   PT_HIP_CHECK(hipGetLastError());
@@ -896,7 +904,7 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
   const bool fixed = !method_col && method_uniform == kCalculatorMultiply;
   const dim3 g(grid_cap(M, 256 * 4, 8192));
   // outbox sends staged in LDS per 1024-message tile (the hot calculator method never sends)
-  const unsigned stage_cap = outbox_cap && !fixed ? 256 * 4 : 0;
+  const unsigned stage_cap = outbox_cap && !fixed ? kOutboxStage : 0;
   const size_t smem = stage_cap ? outbox_stage_bytes(stage_cap) : 0;
 #define PT_LOCAL(MO, FX)                                                                                              \
   hipLaunchKernelGGL((local_send_kernel<MO, FX>), g, dim3(256), smem, as_stream(stream), (const uint32_t*)actor,     \

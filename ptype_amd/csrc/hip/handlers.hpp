@@ -43,6 +43,10 @@ struct OutboxView {
   OutboxStage stg;  // block staging in LDS (stg.n null: off)
 };
 
+// Records a block stages (one 1024-message tile of local_send; a dispatch block
+// publishes at its end, anything past the stage goes straight to HBM): 30 KB.
+constexpr unsigned kOutboxStage = 1024;
+
 // LDS bytes of a stage of `cap` records (the layout outbox_stage() carves).
 __host__ __device__ constexpr size_t outbox_stage_bytes(unsigned cap) {
   return 16 + (size_t)cap * (3 * sizeof(int64_t) + sizeof(uint32_t) + sizeof(uint16_t)) + 16;

@@ -174,7 +174,12 @@ __global__ __launch_bounds__(256) void dispatch_packed_kernel(const uint32_t* __
                                                               int64_t rep_words, int64_t* __restrict__ state,
                                                               uint32_t n_state, uint64_t delay_ticks,
                                                               unsigned long long* __restrict__ stats, OutboxView ob,
-                                                              DirectView dv) {
+                                                              DirectView dv, unsigned stage_cap) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  if (stage_cap) {  // handlers' outbox sends staged in LDS, published once per block (handlers.hpp)
+    ob.stg = outbox_stage(smem, stage_cap);
+    __syncthreads();
+  }
   const int d = blockIdx.y;
   const bool direct = dv.src != nullptr && d == dv.self;
   const uint32_t* rq = recv + (int64_t)d * req_words;
@@ -194,6 +199,7 @@ __global__ __launch_bounds__(256) void dispatch_packed_kernel(const uint32_t* __
   else
     failed = dispatch_range_packed<S, 0>(rq, count, hm, L, vals, okmap, state, n_state, delay_ticks, ob, dv, direct,
                                          ident, toowide);
+  if (stage_cap) outbox_flush(ob);  // every thread of the block reaches here
   for (int off = 32; off > 0; off >>= 1) {
     failed += __shfl_xor(failed, off);
     toowide += __shfl_xor(toowide, off);
@@ -387,10 +393,12 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
   const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
   const unsigned gx = grid_for(per, 256, (unsigned)(4096 / R > 0 ? 4096 / R : 1));
   const int64_t req_words = packed_req_words(C, L.S), rep_words = packed_rep_words(C, L.vb);
+  const unsigned stage_cap = outbox_cap ? kOutboxStage : 0;  // LDS stage only where handlers can send
+  const size_t smem = stage_cap ? outbox_stage_bytes(stage_cap) : 0;
 #define PT_DISPATCH_P(SV)                                                                                          \
-  hipLaunchKernelGGL((dispatch_packed_kernel<SV>), dim3(gx, R), dim3(256), 0, as_stream(stream),                    \
+  hipLaunchKernelGGL((dispatch_packed_kernel<SV>), dim3(gx, R), dim3(256), smem, as_stream(stream),                 \
                      (const uint32_t*)recv, req_words, C, L, (uint32_t*)reply, rep_words, (int64_t*)state, n_state, \
-                     delay_ticks, (unsigned long long*)stats, ob, dv)
+                     delay_ticks, (unsigned long long*)stats, ob, dv, stage_cap)
   PT_S_SWITCH(L.S, PT_DISPATCH_P)
 #undef PT_DISPATCH_P
   PT_HIP_CHECK(hipGetLastError());

@@ -412,11 +412,8 @@ class ActorExchange:
         epochs = delivered = 0
         try:
             if initial is not None:  # every rank passes one (possibly empty), same columns
-                m0 = mx0 = initial.M
-                if self.world > 1:
-                    t = torch.tensor([m0], dtype=torch.int64, device=self.device)
-                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-                    mx0 = int(t.item())
+                m0 = initial.M
+                mx0 = self._agree_max(m0) if self.world > 1 else m0
                 for lo in range(0, mx0, per_send):
                     self.send_all(initial.slice(min(lo, m0), min(m0, lo + per_send)))
                 delivered += m0
@@ -425,11 +422,7 @@ class ActorExchange:
                 return epochs + e, delivered + d
             while epochs < max_epochs:
                 n = outbox.pending()
-                mx = n
-                if self.world > 1:
-                    t = torch.tensor([n], dtype=torch.int64, device=self.device)
-                    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-                    mx = int(t.item())
+                mx = self._agree_max(n) if self.world > 1 else n
                 if mx == 0:
                     break
                 batch = outbox.take(n)

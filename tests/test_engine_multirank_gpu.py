@@ -183,3 +183,62 @@ def test_gpu_engine_zipf_skew_no_resend(adaptive, monkeypatch):
             assert C == C_static
     if not adaptive:
         assert sum(o[0] for o in out) > 0  # static slots overflow under this skew
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("packed", [True, False])
+def test_gpu_multirank_tells(packed):
+    """Device tells across R = 4 in-process ranks: a token ring whose every hop is
+    a ``Forward`` emitted by a dispatch kernel into the (LDS-staged) outbox and
+    routed by the next epoch's exchange; every actor counts exactly the visits a
+    plain simulation predicts."""
+    from ptype_amd.ops.outbox import DeviceOutbox
+    from ptype_amd.ops.records import METHOD_FORWARD
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    R, n_per, T, hops, stride = 4, 5000, 3000, 9, 7
+    n = n_per * R
+    fc = hip().FakeComm(R)
+    starts = [[(r * 1009 + 13 * t) % n for t in range(T)] for r in range(R)]
+    states, errors, epochs = [None] * R, [], [None] * R
+    start = threading.Barrier(R)
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                tab = RegistryTable(4 * n, device="cuda")
+                ids = torch.arange(n)
+                tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
+                st = torch.zeros(n_per, dtype=torch.int64, device="cuda")
+                ex = ActorExchange(tab, 2 * T, chunks=2, state=st, packed=packed, fake=(fc, r))
+                ob = DeviceOutbox(2 * T, device="cuda")
+                s0 = torch.tensor(starts[r], dtype=torch.int64)
+                init = B.MsgBatch(s0.to(torch.int32).cuda(), ((s0 + stride) % n).cuda(),
+                                  torch.full((T,), hops, dtype=torch.int64, device="cuda"),
+                                  torch.full((T,), stride | (n << 32), dtype=torch.int64, device="cuda"),
+                                  METHOD_FORWARD)
+                start.wait()
+                epochs[r], _ = ex.pump(ob, initial=init)
+                s.synchronize()
+                states[r] = st.cpu()
+                assert ob.dropped == 0
+        except BaseException as e:  # noqa: BLE001 - surfaced below
+            errors.append((r, repr(e)))
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(R)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not errors, errors
+    exp = torch.zeros(n, dtype=torch.int64)
+    for ss in starts:
+        for a in ss:
+            for _ in range(hops + 1):
+                exp[a] += 1
+                a = (a + stride) % n
+    for r in range(R):
+        assert torch.equal(states[r], exp[r::R]), r  # actor a -> rank a % R, mailbox a // R
+    assert all(e == hops for e in epochs), epochs
