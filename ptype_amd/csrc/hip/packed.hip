@@ -391,7 +391,11 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
     ob.cap = outbox_cap;
   }
   const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
-  const unsigned gx = grid_for(per, 256, (unsigned)(4096 / R > 0 ? 4096 / R : 1));
+  static const unsigned target = [] {  // blocks over all sources (PTYPE_DISPATCH_BLOCKS: tuning knob)
+    const char* e = getenv("PTYPE_DISPATCH_BLOCKS");
+    return e ? (unsigned)atoi(e) : 4096u;
+  }();
+  const unsigned gx = grid_for(per, 256, (unsigned)(target / R > 0 ? target / R : 1));
   const int64_t req_words = packed_req_words(C, L.S), rep_words = packed_rep_words(C, L.vb);
   const unsigned stage_cap = outbox_cap ? kOutboxStage : 0;  // LDS stage only where handlers can send
   const size_t smem = stage_cap ? outbox_stage_bytes(stage_cap) : 0;
