@@ -45,6 +45,8 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
                        const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, uintptr_t out_val, uintptr_t out_st,
                        uintptr_t stats, uintptr_t checksum, uintptr_t stream, uintptr_t m_dev = 0);
 void launch_outbox_advance(uintptr_t count, uint64_t cap, uintptr_t epoch_m, int64_t j, uintptr_t stream);
+void launch_pack_replies(uintptr_t v2, int R, int64_t C, uintptr_t reply, int vb, uintptr_t stats,
+                         int64_t expected_per_rank, uintptr_t stream);
 void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
                      uintptr_t checksum, bool direct, uintptr_t stream);
 int64_t wire_req_words(int64_t C, int nargs, bool mc);
@@ -291,7 +293,7 @@ struct EngineSend {  // one Send: the batch, the registry, the outputs
   uintptr_t checksum;
   uintptr_t stream;  // the caller's compute stream
   bool packed;       // wire format v3 for this Send (needs collectives; not under graph capture)
-  uintptr_t mailboxes = 0;  // Mailboxes*: deliver on receipt through the HBM mailboxes (wire v2, no direct)
+  uintptr_t mailboxes = 0;  // Mailboxes*: deliver on receipt through the HBM mailboxes (no direct)
   bool ordered = false;     // the batch may carry ordered methods (actor-sharded rings, ordered drain)
   uintptr_t m_dev = 0;      // u64 on the device: the batch's real length (<= M), read by the kernel (local path)
 };
@@ -359,6 +361,7 @@ class EpochEngine {
     (void)hipStreamDestroy(comm_stream_);
     (void)hipFree(meta_dev_);
     (void)hipFree(capfold_dev_);
+    if (mb_stage_) (void)hipFree(mb_stage_);
 
     (void)hipHostFree(meta_host_);
     if (flags_host_) (void)hipHostFree(flags_host_);
@@ -701,8 +704,15 @@ class EpochEngine {
       rv.C = (uint32_t)C_;
       rv.n = (uint64_t)R_ * (uint64_t)C_;
       const uintptr_t src = collectives() ? b.recv : b.send;
-      launch_mailbox_enqueue_slots(mb->view(), src, R_, C_, a.nargs, a.mc, rv, std::max<int64_t>(1, m / R_),
-                                   !a.ordered, (uintptr_t)cs);
+      if (packed_) {  // v3 records in; the drain answers in v2 geometry into a staging set, packed below
+        rv.slots = mb_stage(cs);
+        rv.rep_words = wire_rep_words(C_);
+        launch_mailbox_enqueue_slots_packed(mb->view(), src, R_, C_, L_, rv, std::max<int64_t>(1, m / R_),
+                                            !a.ordered, (uintptr_t)cs);
+      } else {
+        launch_mailbox_enqueue_slots(mb->view(), src, R_, C_, a.nargs, a.mc, rv, std::max<int64_t>(1, m / R_),
+                                     !a.ordered, (uintptr_t)cs);
+      }
       OutboxView ob;
       if (a.outbox_cap) {
         ob.actor = (uint32_t*)a.outbox[0];
@@ -715,6 +725,9 @@ class EpochEngine {
       }
       // (no fixed-method drain: other ranks' slots may carry other methods)
       launch_mailbox_drain(mb->view(), a.state, a.n_state, a.delay_ticks, ob, rv, a.ordered, (uintptr_t)cs, 0);
+      if (packed_)
+        launch_pack_replies((uintptr_t)rv.slots, R_, C_, b.reply, L_.vb, b.ws, std::max<int64_t>(1, m / R_),
+                            (uintptr_t)cs);
     } else {
       Timed t(prof_.kernels_ns);
       if (packed_)
@@ -877,6 +890,17 @@ class EpochEngine {
   uint64_t* meta_dev_ = nullptr;   // v3 column maxima (device, all-reduced in place)
   uint64_t* meta_host_ = nullptr;  // pinned copy the host derives the layout from
   unsigned* capfold_dev_ = nullptr;  // CapFold words: column totals [kCapCopies][kMaxCapCols] + ticket
+  uint32_t* mb_stage_ = nullptr;     // v2-geometry reply staging for mailbox delivery with wire v3 (lazy)
+
+  // One staging set serves every chunk: each chunk's enqueue, drain and pack run
+  // in order on the compute stream.
+  uint32_t* mb_stage(hipStream_t cs) {
+    (void)cs;
+    if (!mb_stage_) {
+      PT_HIP_CHECK(hipMalloc(&mb_stage_, (size_t)R_ * (size_t)wire_rep_words(C_alloc_) * sizeof(uint32_t)));
+    }
+    return mb_stage_;
+  }
   int64_t agree_words_ = kMetaWords;  // meta + count matrix [R][R][chunks]
   size_t xs_[kMaxCapCols] = {}, xr_[kMaxCapCols] = {};  // bytes to / from each peer for the a2av in flight
   bool exact_ = false;  // this Send

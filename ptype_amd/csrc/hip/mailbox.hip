@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "mailbox.hpp"
+#include "packed.hpp"
 #include "route_common.hpp"
 
 #include <algorithm>
@@ -339,6 +340,61 @@ __global__ __launch_bounds__(256) void mailbox_enqueue_slots_kernel(MboxView mv,
     }
     enqueue_tile<false, K, ARRIVAL>(mv, base, lim, hist, (uint32_t)(d * 4096 + tb / tile), in, ok, mb, meth, x0, x1,
                                     x2, org, NARGS > 2, rv, n_enq, n_ovf, n_miss);
+  }
+  block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
+}
+
+// The same from wire v3 request regions (packed.hpp): S dwords per record, fields
+// at the agreed bit offsets, arguments zigzag-coded.  The drain still answers in
+// wire v2 geometry (into a staging region set); pack_replies then writes the v3
+// reply regions the reverse all-to-all moves.
+template <int S, int K, bool ARRIVAL>
+__global__ __launch_bounds__(256) void mailbox_enqueue_slots_packed_kernel(MboxView mv,
+                                                                           const uint32_t* __restrict__ recv,
+                                                                           int64_t req_words, uint32_t C,
+                                                                           PackedLayout L, ReplyView rv) {
+  extern __shared__ unsigned long long lds_mb[];
+  const uint32_t NS = 1u << mv.log_s;
+  unsigned long long* base = lds_mb;
+  unsigned long long* lim = lds_mb + NS;
+  unsigned* hist = reinterpret_cast<unsigned*>(lds_mb + 2 * NS);
+  const int d = blockIdx.y;
+  const uint32_t* rq = recv + (int64_t)d * req_words;
+  const uint4 h = *reinterpret_cast<const uint4*>(rq);
+  const bool valid = (h.w >> 16) & kFlagValid;
+  const int64_t count = valid ? (int64_t)(h.x < C ? h.x : C) : 0;
+  const uint32_t hm = h.w & 0xffffu;
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    *reinterpret_cast<uint4*>(rv.slots + (int64_t)d * rv.rep_words) = make_uint4((uint32_t)count, 0u, 0u, 0u);
+  const int64_t tile = (int64_t)K * blockDim.x;
+  const bool has_a2 = L.w[4] != 0;
+  unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0;
+  for (int64_t tb = blockIdx.x * tile; tb < count; tb += (int64_t)gridDim.x * tile) {
+    for (uint32_t s = threadIdx.x; s < NS; s += blockDim.x) hist[s] = 0;
+    bool in[K], ok[K];
+    uint32_t mb[K], meth[K], org[K];
+    int64_t x0[K], x1[K], x2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int64_t i = tb + k * (int64_t)blockDim.x + threadIdx.x;
+      in[k] = i < count;
+      uint32_t wv[S];
+      if (in[k]) {
+        load_words<S>(rq + 4 + i * S, wv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < S; ++j) wv[j] = 0;
+      }
+      mb[k] = (uint32_t)packed_field<S>(L, 1, wv);
+      meth[k] = L.w[0] ? (uint32_t)packed_field<S>(L, 0, wv) : hm;
+      x0[k] = zz_dec(packed_field<S>(L, 2, wv));
+      x1[k] = zz_dec(packed_field<S>(L, 3, wv));
+      x2[k] = zz_dec(packed_field<S>(L, 4, wv));
+      ok[k] = in[k] && mb[k] < kMaxMbox;
+      org[k] = (uint32_t)d * C + (uint32_t)i;
+    }
+    enqueue_tile<false, K, ARRIVAL>(mv, base, lim, hist, (uint32_t)(d * 4096 + tb / tile), in, ok, mb, meth, x0, x1,
+                                    x2, org, has_a2, rv, n_enq, n_ovf, n_miss);
   }
   block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
 }
@@ -695,6 +751,40 @@ void launch_mailbox_enqueue_slots(const MboxView& mv, uintptr_t recv, int R, int
     default: PT_ENQS(3, true) break;
   }
 #undef PT_ENQS
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_mailbox_enqueue_slots_packed(const MboxView& mv, uintptr_t recv, int R, int64_t C, const PackedLayout& L,
+                                         const ReplyView& rv, int64_t expected_per_rank, bool arrival,
+                                         uintptr_t stream) {
+  if (R < 1 || C < 1 || !rv.slots || rv.C != (uint32_t)C) throw std::invalid_argument("mailbox enqueue slots: geometry");
+  if (L.w[4] && !mv.a2) throw std::invalid_argument("mailbox enqueue: 3-argument records but no a2 array");
+  if (L.S < 1 || L.S > 8) throw std::invalid_argument("mailbox enqueue: packed record of 1..8 dwords");
+  if ((uint64_t)R * (uint64_t)C > 0xffffffffull) throw std::invalid_argument("mailbox enqueue: origin > u32");
+  constexpr int K = 4;
+  const int64_t req_words = packed_req_words(C, L.S);
+  const uint32_t NS = 1u << mv.log_s;
+  const size_t lds = (size_t)NS * (8 + 8 + 4);
+  const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
+  const dim3 g(mb_grid(per, 256 * K, (unsigned)std::max(1, 4096 / R)), (unsigned)R);
+#define PT_ENQP(SV)                                                                                                  \
+  if (arrival)                                                                                                       \
+    hipLaunchKernelGGL((mailbox_enqueue_slots_packed_kernel<SV, K, true>), g, dim3(256), lds, as_stream(stream), mv, \
+                       (const uint32_t*)recv, req_words, (uint32_t)C, L, rv);                                        \
+  else                                                                                                               \
+    hipLaunchKernelGGL((mailbox_enqueue_slots_packed_kernel<SV, K, false>), g, dim3(256), lds, as_stream(stream),    \
+                       mv, (const uint32_t*)recv, req_words, (uint32_t)C, L, rv);
+  switch (L.S) {
+    case 1: PT_ENQP(1) break;
+    case 2: PT_ENQP(2) break;
+    case 3: PT_ENQP(3) break;
+    case 4: PT_ENQP(4) break;
+    case 5: PT_ENQP(5) break;
+    case 6: PT_ENQP(6) break;
+    case 7: PT_ENQP(7) break;
+    default: PT_ENQP(8) break;
+  }
+#undef PT_ENQP
   PT_HIP_CHECK(hipGetLastError());
 }
 

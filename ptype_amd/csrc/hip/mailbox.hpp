@@ -99,6 +99,10 @@ struct ReplyView {
   uint32_t C = 0;
 };
 
+struct PackedLayout;
+void launch_mailbox_enqueue_slots_packed(const MboxView& mv, uintptr_t recv, int R, int64_t C, const PackedLayout& L,
+                                         const ReplyView& rv, int64_t expected_per_rank, bool arrival,
+                                         uintptr_t stream);
 void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2,
                             uintptr_t method_col, int method_uniform, int64_t M, uintptr_t table, uint64_t cap,
                             uintptr_t dir, uint32_t n_dir, uint32_t affine_w, int rank_self, uint32_t origin_base,

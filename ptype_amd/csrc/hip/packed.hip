@@ -20,6 +20,7 @@ int64_t route_prep(uintptr_t actor, int64_t M, uintptr_t table, uint64_t cap, ui
 void route_scan(int64_t G, int R, int64_t C, int64_t req_words, uintptr_t sendbuf, uintptr_t hist,
                 int method_uniform, uintptr_t stats, int rank_self, uintptr_t stream);
 int64_t route_grid(int64_t M, int64_t* P_out);
+int64_t wire_rep_words(int64_t C);
 
 constexpr int kStatTooWide = 4;  // workspace stat word: replies that did not fit vb (never, by construction)
 
@@ -206,6 +207,51 @@ __global__ __launch_bounds__(256) void dispatch_packed_kernel(const uint32_t* __
   }
   if (lane_id() == 0 && failed) atomicAdd(&stats[2], failed);
   if (lane_id() == 0 && toowide) atomicAdd(&stats[kStatTooWide], toowide);
+}
+
+// ---- v2 reply regions -> v3 reply regions (mailbox delivery on receipt at N > 1:
+// the drain answers in v2 geometry, in ring order; this pass writes what the
+// reverse all-to-all moves).  grid (X, R), 64-slot groups per wave as dispatch.
+__global__ __launch_bounds__(256) void pack_replies_kernel(const uint32_t* __restrict__ v2, int64_t v2_words,
+                                                           int64_t C, uint32_t* __restrict__ reply, int64_t rep_words,
+                                                           int vb, unsigned long long* __restrict__ stats) {
+  const int d = blockIdx.y;
+  const uint32_t* src = v2 + (int64_t)d * v2_words;
+  const int64_t count = std::min<int64_t>(src[0], C);
+  const int64_t* sval = reinterpret_cast<const int64_t*>(src + 4);
+  const uint8_t* sst = reinterpret_cast<const uint8_t*>(src + 4 + 2 * C);
+  uint32_t* rp = reply + (int64_t)d * rep_words;
+  unsigned long long* okmap = reinterpret_cast<unsigned long long*>(rp + 4);
+  uint8_t* vals = reinterpret_cast<uint8_t*>(rp + 4 + packed_ok_words(count));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
+  const unsigned lane = lane_id();
+  unsigned long long toowide = 0;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t gb = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~(kWave - 1)); gb < count; gb += step) {
+    const int64_t s = gb + lane;
+    const bool in = s < count;
+    const int64_t value = in ? sval[s] : 0;
+    const int32_t status = in ? (int32_t)sst[s] : kStatusOk;
+    bool ok = status == kStatusOk;
+    uint64_t code = ok ? (vb == 8 ? (uint64_t)value : zz_enc(value)) : (uint64_t)status;
+    if (ok && vb < 8 && (code >> (8 * vb))) {  // impossible under the agreed bounds: fail loudly
+      ok = false;
+      code = kStatusFailed;
+      toowide += in;
+    }
+    const unsigned long long bits = __ballot(in && ok);
+    if (in) {
+      switch (vb) {
+        case 1: vals[s] = (uint8_t)code; break;
+        case 2: reinterpret_cast<uint16_t*>(vals)[s] = (uint16_t)code; break;
+        case 4: reinterpret_cast<uint32_t*>(vals)[s] = (uint32_t)code; break;
+        default: reinterpret_cast<uint64_t*>(vals)[s] = code;
+      }
+    }
+    if (lane == 0) okmap[gb / kWave] = bits;
+  }
+  for (int off = 32; off > 0; off >>= 1) toowide += __shfl_xor(toowide, off);
+  if (lane == 0 && toowide) atomicAdd(&stats[kStatTooWide], toowide);
 }
 
 // ---- K8 for v3 replies: a gather per message (coalesced outputs); kCompU
@@ -420,4 +466,16 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t p
                      direct);
   PT_HIP_CHECK(hipGetLastError());
 }
+void launch_pack_replies(uintptr_t v2, int R, int64_t C, uintptr_t reply, int vb, uintptr_t stats,
+                         int64_t expected_per_rank, uintptr_t stream) {
+  if (R < 1 || C < 1 || !v2 || !reply || !stats) throw std::invalid_argument("pack_replies: geometry");
+  if (vb != 1 && vb != 2 && vb != 4 && vb != 8) throw std::invalid_argument("pack_replies: vb in {1, 2, 4, 8}");
+  const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
+  const unsigned gx = grid_for(per, 256, (unsigned)(4096 / R > 0 ? 4096 / R : 1));
+  hipLaunchKernelGGL(pack_replies_kernel, dim3(gx, R), dim3(256), 0, as_stream(stream), (const uint32_t*)v2,
+                     wire_rep_words(C), C, (uint32_t*)reply, packed_rep_words(C, vb), vb,
+                     (unsigned long long*)stats);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace ptype

@@ -242,7 +242,7 @@ class ActorExchange:
             int(req.method) if uniform else 0, req.M, B._ptr(self.table.table), self.table.cap, B._ptr(d), n_dir,
             affine, fmt.nargs, fmt.method_col, B._ptr(out_val), B._ptr(out_status), B._ptr(state),
             0 if state is None else state.numel(), int(self.delay_us) * 100, ob, ob_cap, self.direct and not mb,
-            B._ptr(self.checksum), torch.cuda.current_stream(self.device).cuda_stream, self.packed_active() and not mb,
+            B._ptr(self.checksum), torch.cuda.current_stream(self.device).cuda_stream, self.packed_active(),
             mb, self.mailbox_ordered)
         if self.world > 1 or self.force_collectives:
             w = self._engine.last_wire()
@@ -283,7 +283,7 @@ class ActorExchange:
     def packed_active(self) -> bool:
         """Whether the next native send uses wire format v3."""
         return bool(self.packed and self.use_engine and not self._capturing
-                    and (self.world > 1 or self.force_collectives) and not self._mailbox_on_receipt())
+                    and (self.world > 1 or self.force_collectives))
 
     # ------------------------------------------------------------------
     def _a2a(self, out, inp):

@@ -184,13 +184,15 @@ def test_mailbox_send_graph_replay():
         assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1)
 
 
-@pytest.mark.parametrize("R,ordered", [(4, True), (3, False)])
-def test_mailbox_delivery_on_receipt_multirank(R, ordered):
+@pytest.mark.parametrize("R,ordered,packed", [(4, True, True), (3, False, True), (4, True, False), (3, False, False)])
+def test_mailbox_delivery_on_receipt_multirank(R, ordered, packed):
     """N > 1: every rank's received records go through its HBM mailboxes (K2 on
     receipt from the request regions, K3 into the reply regions), on the engine's
     real multi-rank pipeline (FakeComm ranks, one GPU).  Ordered: SeqFold traffic
     from every rank to every rank's actors, audited per actor across all senders
-    (exactly once, serialised).  Unordered: calculator replies exact."""
+    (exactly once, serialised).  Unordered: calculator replies exact.  ``packed``:
+    wire v3 records are enqueued straight from the packed regions and the drain's
+    replies are packed into v3 reply regions; else wire v2."""
     import threading
 
     from ptype_amd.ops import hip
@@ -213,12 +215,13 @@ def test_mailbox_delivery_on_receipt_multirank(R, ordered):
                 tab.enable_directory(n, affine_world=R)
                 st = states0[r].to("cuda")
                 ex = ActorExchange(tab, M, chunks=2, state=st, fake=(fc, r), delivery="mailbox",
-                                   mailbox_ordered=ordered, mailbox_shards=64)
+                                   mailbox_ordered=ordered, mailbox_shards=64, packed=packed)
                 req = fold_batch(M, n, 300 + r) if ordered else B.gen_requests(M, n, METHOD_CALC_MULTIPLY,
                                                                                  seed=300 + r, device="cuda")
                 start.wait()
                 v, sts = ex.send(req)
                 s.synchronize()
+                assert (ex.last_wire["S"] > 0) == packed, ex.last_wire
                 res[r] = (req.actor.cpu().long(), req.a0.cpu(), None if ordered else req.a1.cpu(), v.cpu(), sts.cpu(),
                           st.cpu(), ex.stats().mailbox)
         except BaseException as e:  # noqa: BLE001
