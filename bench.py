@@ -42,7 +42,7 @@ def _parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--msgs-per-gpu", type=int, default=8 * 1024 * 1024, help="messages each rank sends per step")
     p.add_argument("--actors-per-gpu", type=int, default=131072)
     p.add_argument("--chunks", type=int, default=0, help="pipeline chunks per step (0 = auto)")
@@ -50,9 +50,9 @@ def _parse():
     p.add_argument("--cpu", action="store_true", help="gloo/CPU dry run of the same pipeline (tests)")
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the step as a captured hipGraph (auto: single rank)")
-    p.add_argument("--steps-per-graph", type=int, default=1,
-                   help="whole steps per graph replay (small batches: the graph launch shows); "
-                        "steps and warmup must be multiples")
+    p.add_argument("--steps-per-graph", type=int, default=0,
+                   help="whole steps per graph replay (the graph launch and the seed advance show per replay); "
+                        "steps and warmup must be multiples.  0 = auto: the largest of 4, 2, 1 dividing both")
     p.add_argument("--loopback", type=int, default=0, metavar="R",
                    help="profiling only: one GPU runs rank 0 of a symmetric R-rank node with the all-to-alls "
                         "as local copies (FakeComm loopback) -- the compute side of an R-GPU step")
@@ -234,6 +234,9 @@ def main():
     st = torch.empty(M, dtype=torch.int32, device=device)
     pregen = args.zipf > 0 or args.pregen
     use_graph = use_gpu and not pregen and (args.graph == "on" or (args.graph == "auto" and not dist_on and fake is None))
+    if args.steps_per_graph == 0:  # auto (measured at 8 Mi msgs: 1 -> 89-90, 2 -> 93.8, 4 -> 94.8 G msg/s)
+        args.steps_per_graph = next((u for u in (4, 2) if use_graph and args.steps % u == 0
+                                     and args.warmup % u == 0), 1)
     if args.steps_per_graph < 1 or (args.steps_per_graph > 1 and (
             not use_graph or args.steps % args.steps_per_graph or args.warmup % args.steps_per_graph)):
         raise SystemExit("--steps-per-graph: needs the graph path, and steps / warmup multiples of it")
