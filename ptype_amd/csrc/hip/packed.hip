@@ -80,7 +80,7 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_packed_kernel(
     const uint32_t* __restrict__ route, const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
     const int64_t* __restrict__ a2, const uint16_t* __restrict__ method_col, uint32_t method_uniform, int64_t M,
     int64_t P, int R, int64_t C, const uint32_t* __restrict__ base, uint32_t* __restrict__ sendbuf,
-    int64_t req_words, PackedLayout L, int32_t* __restrict__ perm, DirectView dv) {
+    int64_t req_words, PackedLayout L, int32_t* __restrict__ perm, DirectView dv, bool pipe) {
   __shared__ unsigned cnt[kScatterItems][kRouteThreads / kWave][kMaxRanks];
   __shared__ unsigned run[kMaxRanks];
   for (int d = threadIdx.x; d < R; d += blockDim.x) run[d] = base[(int64_t)d * gridDim.x + blockIdx.x];
@@ -88,10 +88,21 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_packed_kernel(
   if (dv.src) dv.identity = ((sendbuf[(int64_t)dv.self * req_words + 3] >> 16) & kFlagIdentity) != 0;
   __syncthreads();
   auto route_at = [route](int64_t i) { return route[i]; };
+  const PackedEmit<S> emit{sendbuf, req_words, L};
   // every column is read when present (null-checked): the layout's widths say what is packed
+  if (pipe) {  // the next tile's loads in flight across this tile's ranking barriers
+    ScatterIn cur, nxt;
+    if (lo < hi) scatter_load<3, true>(lo, hi, route_at, a0, a1, a2, method_col, method_uniform, cur);
+    for (int64_t tile = lo; tile < hi; tile += kScatterTile) {
+      if (tile + kScatterTile < hi)  // block-uniform
+        scatter_load<3, true>(tile + kScatterTile, hi, route_at, a0, a1, a2, method_col, method_uniform, nxt);
+      scatter_place(tile, hi, cur, R, C, emit, perm, cnt, run, dv);
+      cur = nxt;
+    }
+    return;
+  }
   for (int64_t tile = lo; tile < hi; tile += kScatterTile)
-    scatter_tile<3, true>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C,
-                          PackedEmit<S>{sendbuf, req_words, L}, perm, cnt, run, dv);
+    scatter_tile<3, true>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, R, C, emit, perm, cnt, run, dv);
 }
 
 // ---- dispatch: unpack, run the handler, reply into the value plane + ok bitmap
@@ -407,12 +418,16 @@ void launch_route_packed(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t 
   const int64_t G = prepped ? route_grid(M, &P)
                             : route_prep(actor, M, table, cap, dir, n_dir, R, route, hist, affine_w, stream, &P);
   route_scan(G, R, C, req_words, sendbuf, hist, method_uniform, stats, rank_self, stream);
+  static const bool scatter_pipe = [] {  // PTYPE_SCATTER_PIPE=0: tiles load-then-place one at a time
+    const char* e = getenv("PTYPE_SCATTER_PIPE");
+    return !(e && e[0] == '0');
+  }();
   if (M > 0) {
 #define PT_SCATTER_P(SV)                                                                                             \
   hipLaunchKernelGGL((route_scatter_packed_kernel<SV>), dim3((unsigned)G), dim3(kRouteThreads), 0, as_stream(stream), \
                      (const uint32_t*)route, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,              \
                      (const uint16_t*)method_col, (uint32_t)method_uniform, M, P, R, C, (const uint32_t*)hist,       \
-                     (uint32_t*)sendbuf, req_words, L, (int32_t*)perm, dv)
+                     (uint32_t*)sendbuf, req_words, L, (int32_t*)perm, dv, scatter_pipe)
     PT_S_SWITCH(L.S, PT_SCATTER_P)
 #undef PT_SCATTER_P
   }

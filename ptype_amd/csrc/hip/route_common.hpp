@@ -122,35 +122,49 @@ struct DirectView {
   bool identity = false;  // positions ARE message indices: src is not written
 };
 
-// Place the tile [tile, min(tile + kScatterTile, hi)) in message order.
-// `perm` may be null only with direct completion at world 1 (nothing comes back).
-// `route_at(i)` yields message i's route word; `run[d]` is the next free slot
-// position of destination d for this block and is advanced past the tile.
-// Block-level: every thread of the block must call it (two barriers inside).
-template <int NARGS, bool MC, class RouteAt, class Emit>
-__device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt route_at,
+// One scatter tile's inputs, loaded ahead of its placement (scatter_load), so a
+// block can have the next tile's loads in flight across this tile's barriers.
+struct ScatterIn {
+  uint32_t rw[kScatterItems];
+  uint32_t meth[kScatterItems];
+  int64_t v[kScatterItems][3];
+};
+
+template <int NARGS, bool MC, class RouteAt>
+__device__ __forceinline__ void scatter_load(int64_t tile, int64_t hi, RouteAt route_at,
                                              const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
                                              const int64_t* __restrict__ a2,
                                              const uint16_t* __restrict__ method_col, uint32_t method_uniform,
-                                             int R, int64_t C, Emit emit, int32_t* __restrict__ perm,
-                                             unsigned (&cnt)[kScatterItems][kRouteThreads / kWave][kMaxRanks],
-                                             unsigned* run, DirectView dv) {
+                                             ScatterIn& x) {
+#pragma unroll
+  for (int k = 0; k < kScatterItems; ++k) {
+    const int64_t i = tile + k * kRouteThreads + threadIdx.x;
+    const bool in = i < hi;
+    x.rw[k] = in ? route_at(i) : kRouteNoActor;
+    x.v[k][0] = in ? a0[i] : 0;
+    x.v[k][1] = NARGS > 1 && in && a1 ? a1[i] : 0;
+    x.v[k][2] = NARGS > 2 && in && a2 ? a2[i] : 0;
+    x.meth[k] = MC ? (in && method_col ? (uint32_t)method_col[i] : method_uniform) : 0u;
+  }
+}
+
+// Place the tile [tile, min(tile + kScatterTile, hi)) in message order.
+// `perm` may be null only with direct completion at world 1 (nothing comes back).
+// `run[d]` is the next free slot position of destination d for this block and
+// is advanced past the tile.  Block-level: every thread of the block must call
+// it (two barriers inside).
+template <class Emit>
+__device__ __forceinline__ void scatter_place(int64_t tile, int64_t hi, const ScatterIn& x, int R, int64_t C,
+                                              Emit emit, int32_t* __restrict__ perm,
+                                              unsigned (&cnt)[kScatterItems][kRouteThreads / kWave][kMaxRanks],
+                                              unsigned* run, DirectView dv) {
   const unsigned tid = threadIdx.x, w = tid / kWave, lane = lane_id();
   int d[kScatterItems];
-  uint32_t rw[kScatterItems], meth[kScatterItems];
   unsigned rk[kScatterItems];
-  int64_t v[kScatterItems][3];
-  // payload loads first, so they are in flight during the ranking phase
 #pragma unroll
   for (int k = 0; k < kScatterItems; ++k) {
     const int64_t i = tile + k * kRouteThreads + tid;
-    const bool in = i < hi;
-    rw[k] = in ? route_at(i) : kRouteNoActor;
-    v[k][0] = in ? a0[i] : 0;
-    v[k][1] = NARGS > 1 && in && a1 ? a1[i] : 0;
-    v[k][2] = NARGS > 2 && in && a2 ? a2[i] : 0;
-    meth[k] = MC ? (in && method_col ? (uint32_t)method_col[i] : method_uniform) : 0u;
-    d[k] = (in && (rw[k] & 0xff) != kRouteNoActor) ? (int)(rw[k] & 0xff) : -1;
+    d[k] = (i < hi && (x.rw[k] & 0xff) != kRouteNoActor) ? (int)(x.rw[k] & 0xff) : -1;
     rk[k] = 0;
   }
   // rank within (item k, wave w, destination): ballots, peeled per present destination
@@ -170,15 +184,15 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
   }
   __syncthreads();
   // per destination: exclusive prefix in message order (k-major, then wave)
-  for (int x = tid; x < R; x += blockDim.x) {
-    unsigned r = run[x];
+  for (int q = tid; q < R; q += blockDim.x) {
+    unsigned r = run[q];
     for (int k = 0; k < kScatterItems; ++k)
       for (int ww = 0; ww < kRouteThreads / kWave; ++ww) {
-        const unsigned c = cnt[k][ww][x];
-        cnt[k][ww][x] = r;
+        const unsigned c = cnt[k][ww][q];
+        cnt[k][ww][q] = r;
         r += c;
       }
-    run[x] = r;
+    run[q] = r;
   }
   __syncthreads();
 #pragma unroll
@@ -208,9 +222,24 @@ __device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt r
     } else {
       perm[i] = (int32_t)((int64_t)d[k] * C + pos);  // never null here: remote replies need it
     }
-    emit(d[k], pos, rw[k] >> 8, v[k], meth[k]);
+    emit(d[k], pos, x.rw[k] >> 8, x.v[k], x.meth[k]);
   }
   __syncthreads();
+}
+
+
+// Load + place in one call (callers without cross-tile prefetch).
+template <int NARGS, bool MC, class RouteAt, class Emit>
+__device__ __forceinline__ void scatter_tile(int64_t tile, int64_t hi, RouteAt route_at,
+                                             const int64_t* __restrict__ a0, const int64_t* __restrict__ a1,
+                                             const int64_t* __restrict__ a2,
+                                             const uint16_t* __restrict__ method_col, uint32_t method_uniform,
+                                             int R, int64_t C, Emit emit, int32_t* __restrict__ perm,
+                                             unsigned (&cnt)[kScatterItems][kRouteThreads / kWave][kMaxRanks],
+                                             unsigned* run, DirectView dv) {
+  ScatterIn x;
+  scatter_load<NARGS, MC>(tile, hi, route_at, a0, a1, a2, method_col, method_uniform, x);
+  scatter_place(tile, hi, x, R, C, emit, perm, cnt, run, dv);
 }
 
 // Wire format v2 record writer for scatter_tile: mbox, [method], args as lo/hi
