@@ -114,7 +114,7 @@ class ActorExchange:
         #   auto    -- mailbox for a uniform ordered method, direct otherwise
         # With more ranks the receiver cannot see what the other ranks sent, so there
         # the choice is the exchange's (same on every rank): "mailbox" delivers on
-        # receipt (K2 from the request regions, wire v2) into actor-sharded rings with
+        # receipt (K2 from the request regions, v3 or v2 records) into actor-sharded rings with
         # the ordered drain -- unless `mailbox_ordered=False` promises that no ordered
         # method is ever sent (then arrival-sharded rings, streaming drain); "auto"
         # and "direct" dispatch directly (ordered methods as linearizable CAS updates).
