@@ -51,13 +51,25 @@ namespace ptype {
 // (Advancing the seed inside this kernel, last block out, was measured slower than
 // the separate one-element add it replaces: 8192 blocks ending on a ticket round
 // trip cost more than the ~4 us launch; fewer, longer blocks stream slower.)
+// h % n without a 64-bit divide (gfx950 has no integer divider: `%` expands to a
+// long dependent sequence): q = mulhi(h, floor((2^64 - 1) / n)) undershoots
+// floor(h / n) by at most 2, so at most two corrections make it exact.
+__device__ __forceinline__ uint32_t mod_u64_u32(uint64_t h, uint32_t n, uint64_t magic) {
+  const uint64_t q = __umul64hi(h, magic);
+  uint64_t r = h - q * n;
+  r = r >= n ? r - n : r;
+  r = r >= n ? r - n : r;
+  return (uint32_t)r;
+}
+
 __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
                                                            int64_t* __restrict__ a1, int64_t M, uint32_t n_actors,
-                                                           uint64_t seed, const uint64_t* __restrict__ seed_ptr) {
+                                                           uint64_t seed, const uint64_t* __restrict__ seed_ptr,
+                                                           uint64_t magic) {
   if (seed_ptr) seed = *seed_ptr;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = mix64(seed ^ (uint64_t)i * 0x9e3779b97f4a7c15ull);
-    actor[i] = (uint32_t)(h % n_actors);
+    actor[i] = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
     a0[i] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
     a1[i] = (int64_t)((h >> 40) & 0xffff);
   }
@@ -638,8 +650,17 @@ void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M,
                          uintptr_t seed_ptr, uintptr_t stream) {
   if (M <= 0) return;
   if (n_actors == 0) throw std::invalid_argument("n_actors must be > 0");
-  hipLaunchKernelGGL(gen_requests_kernel, dim3(grid_cap(M, 256, 8192)), dim3(256), 0, as_stream(stream),
-                     (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr);
+  static const int variant = [] {  // tuning knobs: PTYPE_GEN_DIV=1 plain `%`; PTYPE_GEN_BLOCKS grid cap
+    const char* e = getenv("PTYPE_GEN_DIV");
+    return e ? atoi(e) : 0;
+  }();
+  static const unsigned cap_blocks = [] {
+    const char* e = getenv("PTYPE_GEN_BLOCKS");
+    return e ? (unsigned)atoi(e) : 8192u;
+  }();
+  const uint64_t magic = variant == 1 ? 0ull : ~0ull / n_actors;
+  hipLaunchKernelGGL(gen_requests_kernel, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
+                     (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr, magic);
   PT_HIP_CHECK(hipGetLastError());
 }
 
