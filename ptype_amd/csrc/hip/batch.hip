@@ -932,41 +932,39 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
     const char* e = getenv("PTYPE_LOCAL_BLOCKS");
     return e ? (unsigned)atoi(e) : 16384u;
   }();
-  // fixed-method directory path (the calculator hot path): one tile per block,
-  // 8-16 K blocks -- measured (profiles/r2_local_items_sweep.txt) 2 Mi msgs: 1 item
-  // x 8192 blocks 67.4 G msg/s vs 4 x 2048 59.1; 8 Mi: 2 x 16384 101.1 vs 4 x 8192
-  // 94.8 (a grid-stride loop or fewer, longer blocks leave latency exposed)
-  int kk = 4;
-  if (fixed && mode == 1) kk = items ? items : M <= 256ll * 8192 ? 1 : M <= 2ll * 256 * 16384 ? 2 : 4;
-  const dim3 g(grid_cap(M, 256 * kk, fixed && mode == 1 ? max_blocks : 8192u));
-  // outbox sends staged in LDS per 1024-message tile (the hot calculator method never sends)
-  const unsigned stage_cap = outbox_cap && !fixed ? kOutboxStage : 0;
+  // The calculator on the directory path (the gather-bound hot path): one tile per
+  // block, 8-16 K blocks -- measured (profiles/r2_local_items_sweep.txt) 2 Mi msgs:
+  // 1 item x 8192 blocks 67.4 G msg/s vs 4 x 2048 59.1; 8 Mi: 2 x 16384 101.1 vs
+  // 4 x 8192 94.8.  The gather-free affine path and outbox-sending handlers keep
+  // 4 items x <= 8192 blocks (8 Mi affine: 122 vs 112; token-ring tells: 14.8 vs
+  // 11.3 G msg/s -- smaller tiles mean more outbox reservations).
+  const bool hot = fixed && mode == 1;
+  const int kk = items ? items : !hot ? 4 : M <= 256ll * 8192 ? 1 : M <= 2ll * 256 * 16384 ? 2 : 4;
+  const dim3 g(grid_cap(M, 256 * kk, hot ? max_blocks : 8192u));
+  // outbox sends staged in LDS per tile (the hot calculator method never sends)
+  const unsigned stage_cap = outbox_cap && !fixed ? 256u * kk : 0;
   const size_t smem = stage_cap ? outbox_stage_bytes(stage_cap) : 0;
-  if (kk != 4) {  // (the fixed-method directory path only)
-    auto k = kk == 1 ? local_send_kernel<1, kCalculatorMultiply, 1> : local_send_kernel<1, kCalculatorMultiply, 2>;
-    hipLaunchKernelGGL(k, g, dim3(256), smem, as_stream(stream), (const uint32_t*)actor, (const int64_t*)a0,
-                       (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col, (uint32_t)method_uniform, M,
-                       (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir, affine_w, aw_shift,
-                       (int64_t*)state, n_state, delay_ticks, ob, (int64_t*)out_val, (int32_t*)out_st,
-                       (unsigned long long*)stats, (unsigned long long*)checksum, stage_cap,
-                       (const unsigned long long*)m_dev);
-    PT_HIP_CHECK(hipGetLastError());
-    return;
-  }
-#define PT_LOCAL(MO, FX)                                                                                              \
-  hipLaunchKernelGGL((local_send_kernel<MO, FX>), g, dim3(256), smem, as_stream(stream), (const uint32_t*)actor,     \
+#define PT_LOCAL_K(MO, FX, KK)                                                                                        \
+  hipLaunchKernelGGL((local_send_kernel<MO, FX, KK>), g, dim3(256), smem, as_stream(stream), (const uint32_t*)actor, \
                      (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col,       \
                      (uint32_t)method_uniform, M, (const TableEntry*)table, cap - 1, (const uint32_t*)dir, n_dir,     \
                      affine_w, aw_shift, (int64_t*)state, n_state, delay_ticks, ob, (int64_t*)out_val,              \
                      (int32_t*)out_st, (unsigned long long*)stats, (unsigned long long*)checksum, stage_cap,       \
                      (const unsigned long long*)m_dev)
-  if (mode == 2) {
-    if (fixed) PT_LOCAL(2, kCalculatorMultiply); else PT_LOCAL(2, 0);
-  } else if (mode == 1) {
-    if (fixed) PT_LOCAL(1, kCalculatorMultiply); else PT_LOCAL(1, 0);
-  } else {
-    if (fixed) PT_LOCAL(0, kCalculatorMultiply); else PT_LOCAL(0, 0);
+#define PT_LOCAL(MO, FX)                  \
+  switch (kk) {                           \
+    case 1: PT_LOCAL_K(MO, FX, 1); break; \
+    case 2: PT_LOCAL_K(MO, FX, 2); break; \
+    default: PT_LOCAL_K(MO, FX, 4);       \
   }
+  if (mode == 2) {
+    if (fixed) PT_LOCAL(2, kCalculatorMultiply) else PT_LOCAL(2, 0)
+  } else if (mode == 1) {
+    if (fixed) PT_LOCAL(1, kCalculatorMultiply) else PT_LOCAL(1, 0)
+  } else {
+    if (fixed) PT_LOCAL(0, kCalculatorMultiply) else PT_LOCAL(0, 0)
+  }
+#undef PT_LOCAL_K
 #undef PT_LOCAL
   PT_HIP_CHECK(hipGetLastError());
 }
