@@ -701,7 +701,8 @@ void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, u
   const int mode = (affine_w && n_dir) ? 2 : (dir && n_dir) ? 1 : 0;
   const uint32_t S = 1u << mv.log_s;
   const size_t lds = (size_t)S * (8 + 8 + 4);
-  const dim3 g(mb_grid(M, 256 * (arrival ? KA : K), 4096));
+  static const unsigned enq_blocks = getenv("PTYPE_ENQ_BLOCKS") ? (unsigned)atoi(getenv("PTYPE_ENQ_BLOCKS")) : 4096u;
+  const dim3 g(mb_grid(M, 256 * (arrival ? KA : K), enq_blocks));
 #define PT_ENQ(MO, LV)                                                                                                \
   hipLaunchKernelGGL((mailbox_enqueue_kernel<MO, LV, K>), g, dim3(256), lds, as_stream(stream), mv,                \
                      (const uint32_t*)actor, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,           \
