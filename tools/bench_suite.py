@@ -132,12 +132,19 @@ def optimus(a):
     torch.cuda.set_device(dev)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    fake = None
+    geo = world
+    if a.loopback > 0:  # rank 0 of a symmetric R-rank node; all-to-alls as local copies (FakeComm)
+        from ptype_amd.ops import hip
+
+        fake = (hip().FakeComm(a.loopback, loopback=True, link_gbps=a.link_gbps), 0)
+        geo = a.loopback
     per = a.actors
-    n = per * world
+    n = per * geo
     table = RegistryTable(2 * n, device=dev)
     ids = torch.arange(n, dtype=torch.int64)
-    table.upsert(actor_keys(ids), (ids % world).to(torch.int32), (ids // world).to(torch.int32))
-    table.enable_directory(n, affine_world=world)
+    table.upsert(actor_keys(ids), (ids % geo).to(torch.int32), (ids // geo).to(torch.int32))
+    table.enable_directory(n, affine_world=geo)
     # targets: odd numbers around `base`, each split into 10-wide ranges [2,10), [10,20), ...
     T = a.targets
     tg = torch.arange(T, dtype=torch.int64, device=dev) * 2 + a.base + rank * 2 * T + 1
@@ -149,7 +156,7 @@ def optimus(a):
     lo = torch.where(k == 0, torch.full_like(k, 2), k * 10)
     hi = (k + 1) * 10
     batch = B.MsgBatch((torch.arange(M, device=dev) % n).to(torch.int32), lo, hi, tg[tid], METHOD_PRIME_CHECK)
-    ex = ActorExchange(table, M, chunks=4 if world > 1 else 1)
+    ex = ActorExchange(table, M, chunks=4 if geo > 1 else 1, fake=fake)
     tg_rep = tg[tid]
 
     def step():
@@ -186,7 +193,13 @@ def optimus(a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     if rank == 0:
-        _emit({"config": "example/optimus fan-out, RCCL all-to-all dispatch" if world > 1 else
+        extra = {}
+        if fake is not None:
+            extra = {"loopback_ranks": a.loopback, "link_gbps": a.link_gbps, "wire": (ex.last_wire or {}).get("S"),
+                     "note": "profiling mode: rank 0 of a symmetric R-rank node, all-to-alls as local copies "
+                             "(modelled link bandwidth if link_gbps > 0); per-GPU rates, not a node total"}
+        _emit({**extra, "config": "example/optimus fan-out, RCCL all-to-all dispatch" if world > 1 else
+               "example/optimus fan-out, %d-rank loopback on 1 GPU" % geo if fake else
                "example/optimus fan-out, 1 GPU", "n_gpus": world, "targets_per_gpu_per_step": T,
                "ranges_per_gpu_per_step": M, "ranges_per_s": M * world * a.steps / el,
                "targets_per_s": T * world * a.steps / el, "ms_per_step": el / a.steps * 1e3,
@@ -499,6 +512,8 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--actors", type=int, default=0)
     p.add_argument("--targets", type=int, default=8192)
+    p.add_argument("--loopback", type=int, default=0, metavar="R", help="optimus: R-rank loopback (FakeComm)")
+    p.add_argument("--link-gbps", type=float, default=0.0, help="optimus --loopback: modelled link bandwidth")
     p.add_argument("--base", type=int, default=100_001)
     p.add_argument("--puts", type=int, default=5000)
     p.add_argument("--tokens", type=int, default=1 << 20)

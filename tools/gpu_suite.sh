@@ -9,6 +9,9 @@ OUT=gpurun_out/suite_$TAG.jsonl
 timeout -k 10 300 python tools/bench_suite.py host-rpc >> $OUT 2> gpurun_out/suite_$TAG.err || { echo "host-rpc FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 timeout -k 10 300 python tools/bench_suite.py gpu-1m >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "gpu-1m FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 timeout -k 10 300 python tools/bench_suite.py optimus >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "optimus FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
+# config 4's 8-GPU step on one GPU: rank 0 of an 8-rank node (FakeComm loopback), links unmodelled / at 120 GB/s
+timeout -k 10 300 python tools/bench_suite.py optimus --loopback 8 >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "optimus loopback FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
+timeout -k 10 300 python tools/bench_suite.py optimus --loopback 8 --link-gbps 120 >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "optimus loopback link FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 timeout -k 10 300 python tools/bench_suite.py tell >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "tell FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 timeout -k 10 300 python tools/bench_suite.py xproc >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "xproc FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
 timeout -k 10 300 python tools/bench_suite.py registry >> $OUT 2>> gpurun_out/suite_$TAG.err || { echo "registry FAILED"; tail -5 gpurun_out/suite_$TAG.err; exit 1; }
