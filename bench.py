@@ -418,7 +418,16 @@ def main():
         if dist_on:
             from ptype_amd import _core
 
-            barrier()  # every rank's dispatcher segment exists
+            # host-side barriers through the rendezvous store: no collective kernel
+            # sits on any GPU while the peers' dispatchers must (re)launch to serve
+            def host_barrier(key):
+                store = dist.distributed_c10d._get_default_store()
+                store.add(key, 1)
+                t_end = time.monotonic() + 120.0
+                while store.add(key, 0) < world and time.monotonic() < t_end:
+                    time.sleep(0.001)
+
+            host_barrier("ptype/bench/rtt/ready")  # every rank's dispatcher segment exists
             try:
                 peer = _core.ShmClient(f"/ptype-bench-{tag}-{(rank + 1) % world}")
                 remote_ring = peer.ring_placement
@@ -426,7 +435,7 @@ def main():
             except Exception as e:
                 rtt_errors.append(f"remote: {e}")
                 p50_remote = -1.0
-            barrier()  # keep serving until every rank is done calling
+            host_barrier("ptype/bench/rtt/done")  # keep serving until every rank is done calling
         srv.close()
         if dist_on:
             t = torch.tensor([p50, p50_remote, float(len(rtt_errors))], dtype=torch.float64, device=device)

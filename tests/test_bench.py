@@ -77,6 +77,18 @@ def test_bench_multi_gpu(nproc):
     assert z["config"]["resend_rounds"] == 0 and z["value"] > 0
 
 
+@pytest.mark.gpu
+def test_bench_force_dist_remote_rtt():
+    """World 1 with the RCCL process group up: the multi-rank RTT phase (store
+    barriers, the "next rank's" dispatcher mapped from its dma-buf -- here this
+    rank's own) runs as it does at N > 1."""
+    out = _run(1, ["--force-dist", "--steps", "2", "--warmup", "1", "--rtt-calls", "200", "--no-secondary"],
+               timeout=300)
+    assert out["rtt_error"] is None, out["rtt_error"]
+    assert out["p50_rtt_remote_us"] is not None and out["p50_rtt_remote_us"] > 0
+    assert out["rtt_remote_request_ring"] == "device"
+
+
 def test_bench_zipf_cpu():
     """Skewed load (Zipf 1.1, pre-generated) through the 2-rank gloo pipeline."""
     out = _run(2, ["--cpu", "--zipf", "1.1", "--no-secondary"] + SMALL, launcher="self")
