@@ -36,6 +36,7 @@ import json
 import os
 import sys
 import time
+import weakref
 
 
 def _parse():
@@ -99,10 +100,12 @@ _LIVE_EXCHANGES: list = []  # for the hang watchdog
 
 
 def _hang_watchdog(after_s: float, rank: int) -> None:
-    """Diagnosis mode (PTYPE_HANG_DIAG=<seconds>): if the run has not finished
-    after that long, print every engine's hand-off words (signalled sequence vs
-    value the GPU wrote) and whether its streams drained, then exit -- the main
-    thread is blocked inside a synchronisation and cannot report."""
+    """Hang watchdog (PTYPE_HANG_DIAG=<seconds>; on by default with more than one
+    rank, PTYPE_HANG_DIAG=0 turns it off): if the run has not finished after that
+    long, print every engine's hand-off words (signalled sequence vs value the GPU
+    wrote) and whether its streams drained, then exit 3 -- the main thread is
+    blocked inside a synchronisation and cannot report, and a multi-GPU run that
+    hangs should end with a diagnosis rather than at the launcher's time limit."""
     import threading
 
     import torch
@@ -110,8 +113,9 @@ def _hang_watchdog(after_s: float, rank: int) -> None:
     def dump():
         print(f"[rank {rank}] HANG after {after_s:.0f} s", file=sys.stderr, flush=True)
         names = ["routed", "req_in", "served", "rep_in"]
-        for ex in _LIVE_EXCHANGES:
-            eng = ex._engine
+        for ref in _LIVE_EXCHANGES:
+            ex = ref()
+            eng = ex._engine if ex is not None else None
             if eng is None:
                 continue
             st = eng.hang_state(torch.cuda.current_stream(ex.device).cuda_stream)
@@ -259,8 +263,7 @@ def main():
         max over ranks); returns (seconds, exchange, graph used)."""
         # the bench sends Calculator.Multiply only (stateless): mailboxes shard by arrival
         ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake, delivery=delivery, mailbox_ordered=False)
-        if os.environ.get("PTYPE_HANG_DIAG"):
-            _LIVE_EXCHANGES.append(ex)
+        _LIVE_EXCHANGES.append(weakref.ref(ex))  # (weak: a finished measurement's buffers stay freeable)
         graph = None
         if use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
@@ -311,8 +314,11 @@ def main():
         return elapsed, ex, graph is not None
 
     table = build_table(args.placement)
-    if os.environ.get("PTYPE_HANG_DIAG"):
-        _hang_watchdog(float(os.environ.get("PTYPE_HANG_DIAG") or 30), rank)
+    hang_s = os.environ.get("PTYPE_HANG_DIAG")
+    if hang_s is None and world > 1 and use_gpu:  # generous: RCCL set-up, secondaries, RTT calls included
+        hang_s = str(300 + 0.2 * (args.steps + args.warmup) * (3 if not args.no_secondary else 1))
+    if hang_s and float(hang_s) > 0:
+        _hang_watchdog(float(hang_s), rank)
     elapsed, ex, graphed = measure(table, args.steps, args.warmup)
     def lookup_mode(t):
         if t.dir is None:
