@@ -5,7 +5,7 @@
 set -o pipefail
 TAG=${1:-wd}
 mkdir -p gpurun_out
-PTYPE_HANG_DIAG=1 timeout -k 10 120 python bench.py --force-dist --steps 400 --warmup 2 --rtt-calls 0 --no-secondary > gpurun_out/wd_$TAG.out 2> gpurun_out/wd_$TAG.err
+PTYPE_HANG_DIAG=2 timeout -k 10 120 python bench.py --force-dist --steps 20000 --warmup 2 --rtt-calls 0 --no-secondary > gpurun_out/wd_$TAG.out 2> gpurun_out/wd_$TAG.err
 rc=$?
 echo "watchdog run exit: $rc"; grep -E "HANG|signalled|drained" gpurun_out/wd_$TAG.err | head -12
 [ $rc -eq 3 ] || { echo "WATCHDOG DID NOT FIRE AS EXPECTED"; tail -20 gpurun_out/wd_$TAG.err; exit 1; }
