@@ -478,7 +478,7 @@ __device__ __forceinline__ unsigned long long run_window_ordered(const MboxMsg& 
 // ---------------------------------------------------------------- K3 epoch drain (parallel)
 // grid (X, S): block (x, s) strides over shard s's queued positions.  Stateless
 // and commutative methods only (the host picks the ordered form otherwise).  The
-// last block to finish commits every shard's head (ticket self-resets).
+// last block of each shard commits that shard's head (per-shard ticket, self-resetting).
 template <int FIXED, int K>
 __global__ __launch_bounds__(256) void mailbox_drain_kernel(MboxView mv, int64_t* __restrict__ state,
                                                             uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
@@ -517,25 +517,26 @@ __global__ __launch_bounds__(256) void mailbox_drain_kernel(MboxView mv, int64_t
       ++done;
     }
   }
-  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
-  // last block out commits the heads (every block has read its shard's head by
-  // now).  No fence: nothing is handed over but the ticket itself, and an agent
-  // release per block wrote back the XCD's L2 -- half-written reply lines
-  // included -- 2048 times per drain
+  // `processed` is counted per shard by its last block (positions - holes), not by
+  // every block: 1024 same-address atomics at the kernel's end serialise (~9 ns
+  // each) in its tail.  A block with holes takes them back out of the count.
+  (void)done;
+  block_add_stats(mv.stats, holes ? (unsigned long long)(-(long long)holes) : 0ull, kMbProcessed, failed, kMbFailed,
+                  holes, kMbHoles);
+  // the last block of this shard commits its head (every block of the shard has
+  // read the head by now).  A ticket per shard: one word for the whole grid
+  // serialised 1024 returning atomics.  No fence: nothing is handed over but the
+  // ticket itself, and an agent release per block wrote back the XCD's L2 --
+  // half-written reply lines included -- 2048 times per drain
   __shared__ int last;
-  if (threadIdx.x == 0) {
-    const unsigned long long total = (unsigned long long)gridDim.x * gridDim.y;
-    last = atomicAdd(&mv.stats[kMbTicket], 1ull) == total - 1;
-  }
+  unsigned long long* tk = mv.ctr + (uint64_t)s * kMboxCtrStride + kMboxCtrTicket;
+  if (threadIdx.x == 0) last = atomicAdd(tk, 1ull) == gridDim.x - 1;
   __syncthreads();
-  if (last) {
-    const uint32_t S = 1u << mv.log_s;
-    for (uint32_t q = threadIdx.x; q < S; q += blockDim.x) {
-      const unsigned long long t = *ctr_tail(mv, q);
-      *ctr_head(mv, q) = t;
-      *ctr_done(mv, q) = t;  // epoch enqueues do not count `done`; the drain settles it
-    }
-    if (threadIdx.x == 0) mv.stats[kMbTicket] = 0;
+  if (last && threadIdx.x == 0) {
+    *ctr_head(mv, s) = t;
+    *ctr_done(mv, s) = t;  // epoch enqueues do not count `done`; the drain settles it
+    if (end > h) atomicAdd(&mv.stats[kMbProcessed], (unsigned long long)(end - h));
+    *tk = 0;
   }
 }
 

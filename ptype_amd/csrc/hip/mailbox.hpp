@@ -51,6 +51,7 @@
 namespace ptype {
 
 constexpr int kMboxCtrStride = 32;  // u64 words per shard: [0] tail, [1] done (one line), [16] head (another)
+constexpr int kMboxCtrTicket = 24;  // [24]: the epoch drain's per-shard last-block ticket (self-resetting)
 constexpr int kMboxMaxShards = 4096;
 enum MboxStat : int {
   kMbEnqueued = 0,   // records written into rings
@@ -60,7 +61,7 @@ enum MboxStat : int {
   kMbFailed = 4,     // handler status != ok
   kMbHoles = 5,      // positions skipped as holes
   kMbSerial = 6,     // records run serialised (same actor twice in a window)
-  kMbTicket = 8,     // epoch drain: last-block ticket (self-resetting)
+  kMbTicket = 8,     // reserved (the epoch drain's tickets are per shard: kMboxCtrTicket)
   kMbStatWords = 16,
 };
 
