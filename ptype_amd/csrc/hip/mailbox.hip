@@ -87,7 +87,10 @@ __device__ __forceinline__ void block_add_stats(unsigned long long* stats, unsig
     unsigned long long v = 0;
     for (int k = 0; k < (int)(blockDim.x / kWave); ++k) v += part[threadIdx.x][k];
     const int word = threadIdx.x == 0 ? w0 : threadIdx.x == 1 ? w1 : w2;
-    if (v && word >= 0) atomicAdd(&stats[word], v);
+    // striped by block: one word for the whole grid serialised thousands of
+    // same-address atomics (~9 ns each) at the kernel's end (readers sum stripes)
+    const size_t stripe = (size_t)((blockIdx.x + blockIdx.y * gridDim.x) % kMbStripes) * kMbStatWords;
+    if (v && word >= 0) atomicAdd(&stats[stripe + word], v);
   }
 }
 
@@ -697,7 +700,11 @@ void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, u
   if ((uint64_t)origin_base + (uint64_t)M > rv.n) throw std::invalid_argument("mailbox enqueue: reply view too small");
   if ((uint64_t)origin_base + (uint64_t)M > 0xffffffffull) throw std::invalid_argument("mailbox enqueue: origin > u32");
   constexpr int K = 8;   // actor sharding: a big tile amortises the (tile, shard) reservations
-  constexpr int KA = 4;  // arrival sharding: one reservation per tile anyway; 64 VGPRs, 8 waves/SIMD
+  // arrival sharding: 4 items per thread (one reservation per tile; 64 VGPRs, 8
+  // waves/SIMD); 1 and 2 measured slower at 1 Mi and 8 Mi messages
+  // (profiles/r2_enq_items_sweep.txt).  PTYPE_ENQ_ITEMS overrides.
+  static const int ka_env = getenv("PTYPE_ENQ_ITEMS") ? atoi(getenv("PTYPE_ENQ_ITEMS")) : 0;
+  const int KA = ka_env == 1 || ka_env == 2 || ka_env == 4 ? ka_env : 4;
   const int aw_shift = (affine_w && (affine_w & (affine_w - 1)) == 0) ? __builtin_ctz(affine_w) : -1;
   const int mode = (affine_w && n_dir) ? 2 : (dir && n_dir) ? 1 : 0;
   const uint32_t S = 1u << mv.log_s;
@@ -709,11 +716,20 @@ void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, u
                      (const uint32_t*)actor, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,           \
                      (const uint16_t*)method_col, (uint32_t)method_uniform, M, (const TableEntry*)table, cap - 1,  \
                      (const uint32_t*)dir, n_dir, affine_w, aw_shift, rank_self, origin_base, rv)
-#define PT_ENQA(MO)                                                                                                   \
-  hipLaunchKernelGGL((mailbox_enqueue_kernel<MO, false, KA, true>), g, dim3(256), lds, as_stream(stream), mv,       \
+#define PT_ENQA_K(MO, KV)                                                                                             \
+  hipLaunchKernelGGL((mailbox_enqueue_kernel<MO, false, KV, true>), g, dim3(256), lds, as_stream(stream), mv,       \
                      (const uint32_t*)actor, (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2,           \
                      (const uint16_t*)method_col, (uint32_t)method_uniform, M, (const TableEntry*)table, cap - 1,  \
                      (const uint32_t*)dir, n_dir, affine_w, aw_shift, rank_self, origin_base, rv)
+#define PT_ENQA(MO)     \
+  do {                  \
+    if (KA == 1)        \
+      PT_ENQA_K(MO, 1); \
+    else if (KA == 2)   \
+      PT_ENQA_K(MO, 2); \
+    else                \
+      PT_ENQA_K(MO, 4); \
+  } while (0)
   if (live) {
     if (mode == 2) PT_ENQ(2, true); else if (mode == 1) PT_ENQ(1, true); else PT_ENQ(0, true);
   } else if (arrival) {
@@ -723,6 +739,7 @@ void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, u
   }
 #undef PT_ENQ
 #undef PT_ENQA
+#undef PT_ENQA_K
   PT_HIP_CHECK(hipGetLastError());
 }
 
@@ -857,8 +874,8 @@ Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) 
   const size_t ctr_bytes = (size_t)shards * kMboxCtrStride * 8;
   PT_HIP_CHECK(hipMalloc((void**)&mv_.ctr, ctr_bytes));
   PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, ctr_bytes, stream_));
-  PT_HIP_CHECK(hipMalloc((void**)&mv_.stats, kMbStatWords * 8));
-  PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStatWords * 8, stream_));
+  PT_HIP_CHECK(hipMalloc((void**)&mv_.stats, kMbStripes * kMbStatWords * 8));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStripes * kMbStatWords * 8, stream_));
   bytes_ += ctr_bytes + kMbStatWords * 8;
   const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
   PT_HIP_CHECK(hipHostMalloc((void**)&ctrl_, sizeof(MboxCtrl), fl));
@@ -945,13 +962,15 @@ void Mailboxes::reset(uintptr_t stream) {
   const uint64_t n = (uint64_t)shards() * slots();
   PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, rec_bytes_, s));
   PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, (size_t)shards() * kMboxCtrStride * 8, s));
-  PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStatWords * 8, s));
+  PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStripes * kMbStatWords * 8, s));
 }
 
 std::vector<uint64_t> Mailboxes::stats() const {
-  std::vector<uint64_t> v(kMbStatWords);
+  std::vector<uint64_t> raw((size_t)kMbStripes * kMbStatWords), v(kMbStatWords, 0);
   PT_HIP_CHECK(hipSetDevice(device_));
-  PT_HIP_CHECK(hipMemcpy(v.data(), mv_.stats, kMbStatWords * 8, hipMemcpyDeviceToHost));
+  PT_HIP_CHECK(hipMemcpy(raw.data(), mv_.stats, raw.size() * 8, hipMemcpyDeviceToHost));
+  for (int k = 0; k < kMbStripes; ++k)
+    for (int w = 0; w < kMbStatWords; ++w) v[w] += raw[(size_t)k * kMbStatWords + w];
   return v;
 }
 

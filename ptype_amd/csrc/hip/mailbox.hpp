@@ -64,6 +64,7 @@ enum MboxStat : int {
   kMbTicket = 8,     // reserved (the epoch drain's tickets are per shard: kMboxCtrTicket)
   kMbStatWords = 16,
 };
+constexpr int kMbStripes = 32;  // stats copies (block-striped atomics; stats() sums them)
 
 struct MboxView {
   // records: half A {tag, mailbox, origin, method | flags}, half B {a0, a1}, 16 B
