@@ -250,6 +250,16 @@ __global__ __launch_bounds__(256) void table_build_dir_kernel(const TableEntry* 
   }
 }
 
+// Blocks of the upsert / delete passes (PTYPE_TABLE_BLOCKS: tuning knob): each
+// block publishes its counters with one same-address atomic, and those serialise
+// at L2.  1M-actor inserts: 4096 blocks 5.7-5.9 G/s, 1024 7.5, 512 8.5, 256 7.9
+// (profiles/r2_table_grid_sweep.txt).  (Skipping the max atomic behind an
+// agent-scope read made it worse: 3.0 G/s at 4096.)
+static unsigned table_blocks() {
+  static const unsigned b = getenv("PTYPE_TABLE_BLOCKS") ? (unsigned)atoi(getenv("PTYPE_TABLE_BLOCKS")) : 512u;
+  return b ? b : 512u;
+}
+
 static inline unsigned grid_for(int64_t n, int per_block = 256, unsigned cap = 4096) {
   int64_t g = (n + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -266,8 +276,8 @@ void launch_table_upsert(uintptr_t table, uint64_t cap, uintptr_t keys, uintptr_
   in.keys = (const uint64_t*)keys;
   in.ranks = (const uint32_t*)ranks;
   in.mboxes = (const uint32_t*)mboxes;
-  hipLaunchKernelGGL(table_upsert_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), (TableEntry*)table,
-                     cap - 1, in, (const uint64_t*)exp_in, (uint64_t*)exp_tbl, n, (unsigned long long*)stats);
+  hipLaunchKernelGGL(table_upsert_kernel, dim3(grid_for(n, 256, table_blocks())), dim3(256), 0, as_stream(stream),
+                     (TableEntry*)table, cap - 1, in, (const uint64_t*)exp_in, (uint64_t*)exp_tbl, n, (unsigned long long*)stats);
   PT_HIP_CHECK(hipGetLastError());
 }
 
@@ -278,15 +288,16 @@ void launch_table_upsert_packed(uintptr_t table, uint64_t cap, uintptr_t entries
   if (cap == 0 || (cap & (cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
   UpsertIn in;
   in.packed = (const TableEntry*)entries;
-  hipLaunchKernelGGL(table_upsert_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), (TableEntry*)table,
-                     cap - 1, in, (const uint64_t*)exp_in, (uint64_t*)exp_tbl, n, (unsigned long long*)stats);
+  hipLaunchKernelGGL(table_upsert_kernel, dim3(grid_for(n, 256, table_blocks())), dim3(256), 0, as_stream(stream),
+                     (TableEntry*)table, cap - 1, in, (const uint64_t*)exp_in, (uint64_t*)exp_tbl, n, (unsigned long long*)stats);
   PT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_table_delete(uintptr_t table, uint64_t cap, uintptr_t keys, int64_t n, uintptr_t stats,
                          uintptr_t found, uintptr_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(table_delete_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), (TableEntry*)table,
+  hipLaunchKernelGGL(table_delete_kernel, dim3(grid_for(n, 256, table_blocks())), dim3(256), 0, as_stream(stream),
+                     (TableEntry*)table,
                      cap - 1, (const uint64_t*)keys, n, (unsigned long long*)stats, (uint8_t*)found);
   PT_HIP_CHECK(hipGetLastError());
 }
