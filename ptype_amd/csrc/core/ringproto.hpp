@@ -121,7 +121,11 @@ inline bool ring_claim(const RingRefs& r, uint64_t seq, double timeout_s) {
 inline bool ring_wait(const RingRefs& r, uint64_t seq, double timeout_s, int64_t* value, uint32_t* status) {
   ReplySlot* out = &r.rep[seq & (r.ring - 1)];
   const uint64_t t0 = ring_now_ns();
-  const double rescue_after = timeout_s < 0.2 ? timeout_s / 2 : 0.1;
+  // A publisher between taking its number and claiming its slot can be merely
+  // descheduled: rescuing it fails a live call.  100 ms was too eager on a loaded
+  // host (the ASan stress run on 8 busy CPUs lost calls), so a dead publisher now
+  // wedges the ring for up to 1 s (or half the caller's timeout, if shorter).
+  const double rescue_after = timeout_s < 2.0 ? timeout_s / 2 : 1.0;
   bool rescued = false;
   uint64_t tag;
   for (unsigned spins = 0; !reply_tag_is(tag = __atomic_load_n(&out->tag, __ATOMIC_ACQUIRE), seq); ++spins) {
