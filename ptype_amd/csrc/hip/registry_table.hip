@@ -177,39 +177,60 @@ __global__ __launch_bounds__(256) void table_sweep_kernel(TableEntry* __restrict
 // K7: snapshot pack -- compact live entries (+ deadlines) into a dense buffer
 // that the host copies to pinned DRAM with hipMemcpyAsync.  One wave ballot +
 // one LDS scan per block + one global atomic per block for the output base.
+// K tiles of 256 entries per block trip, item-major (coalesced reads): per-(tile,
+// wave) counts in LDS, one block scan, ONE output reservation per trip.  One
+// returning atomic per 256 entries (8 K per 2M-entry table, all on one word)
+// serialised at L2: that was most of the pass.
+template <int K>
 __global__ __launch_bounds__(256) void table_pack_kernel(const TableEntry* __restrict__ t, uint64_t cap,
                                                          const uint64_t* __restrict__ exp_tbl,
                                                          TableEntry* __restrict__ out,
                                                          uint64_t* __restrict__ out_exp,
                                                          unsigned long long* __restrict__ out_count) {
-  __shared__ unsigned wave_cnt[4];
+  __shared__ unsigned wave_cnt[K][4];
   __shared__ unsigned long long block_base;
   const unsigned w = threadIdx.x / kWave;
-  for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < cap; base += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t i = base + threadIdx.x;
-    TableEntry e{};
-    bool live = false;
-    if (i < cap) {
-      const uint4 v = *reinterpret_cast<const uint4*>(&t[i]);
-      e.key = ((uint64_t)v.y << 32) | v.x;
-      e.rank = v.z;
-      e.mbox = v.w;
-      live = e.key != kKeyEmpty && e.key != kKeyTomb;
+  const uint64_t trip = (uint64_t)K * blockDim.x;
+  for (uint64_t base = blockIdx.x * trip; base < cap; base += (uint64_t)gridDim.x * trip) {
+    TableEntry e[K];
+    bool live[K];
+    unsigned pos[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t i = base + (uint64_t)k * blockDim.x + threadIdx.x;
+      live[k] = false;
+      if (i < cap) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&t[i]);
+        e[k].key = ((uint64_t)v.y << 32) | v.x;
+        e[k].rank = v.z;
+        e[k].mbox = v.w;
+        live[k] = e[k].key != kKeyEmpty && e[k].key != kKeyTomb;
+      }
     }
-    const uint64_t m = __ballot(live);
-    const unsigned pos = mbcnt64(m);
-    if (lane_id() == 0) wave_cnt[w] = __popcll(m);
-    __syncthreads();
-    unsigned off = 0, tot = 0;
-    for (unsigned k = 0; k < blockDim.x / kWave; ++k) {
-      if (k < w) off += wave_cnt[k];
-      tot += wave_cnt[k];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t m = __ballot(live[k]);
+      pos[k] = mbcnt64(m);
+      if (lane_id() == 0) wave_cnt[k][w] = __popcll(m);
     }
-    if (threadIdx.x == 0) block_base = tot ? atomicAdd(out_count, (unsigned long long)tot) : 0ull;
     __syncthreads();
-    if (live) {
-      const unsigned long long o = block_base + off + pos;
-      out[o] = e;
+    if (threadIdx.x == 0) {  // exclusive scan over (tile, wave), then the trip's reservation
+      unsigned run = 0;
+      for (int k = 0; k < K; ++k)
+        for (unsigned q = 0; q < blockDim.x / kWave; ++q) {
+          const unsigned c = wave_cnt[k][q];
+          wave_cnt[k][q] = run;
+          run += c;
+        }
+      block_base = run ? atomicAdd(out_count, (unsigned long long)run) : 0ull;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (!live[k]) continue;
+      const uint64_t i = base + (uint64_t)k * blockDim.x + threadIdx.x;
+      const unsigned long long o = block_base + wave_cnt[k][w] + pos[k];
+      out[o] = e[k];
       if (out_exp) out_exp[o] = exp_tbl ? exp_tbl[i] : 0ull;
     }
     __syncthreads();
@@ -330,7 +351,9 @@ void launch_table_build_dir(uintptr_t table, uint64_t cap, uintptr_t dir, uint64
 
 void launch_table_pack(uintptr_t table, uint64_t cap, uintptr_t exp_tbl, uintptr_t out, uintptr_t out_exp,
                        uintptr_t out_count, uintptr_t stream) {
-  hipLaunchKernelGGL(table_pack_kernel, dim3(grid_for((int64_t)cap)), dim3(256), 0, as_stream(stream),
+  constexpr int K = 8;  // 2048 entries per reservation
+  hipLaunchKernelGGL(table_pack_kernel<K>, dim3(grid_for((int64_t)cap, 256 * K, 1024)), dim3(256), 0,
+                     as_stream(stream),
                      (const TableEntry*)table, cap, (const uint64_t*)exp_tbl, (TableEntry*)out, (uint64_t*)out_exp,
                      (unsigned long long*)out_count);
   PT_HIP_CHECK(hipGetLastError());
