@@ -876,7 +876,7 @@ Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) 
   PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, ctr_bytes, stream_));
   PT_HIP_CHECK(hipMalloc((void**)&mv_.stats, kMbStripes * kMbStatWords * 8));
   PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStripes * kMbStatWords * 8, stream_));
-  bytes_ += ctr_bytes + kMbStatWords * 8;
+  bytes_ += ctr_bytes + kMbStripes * kMbStatWords * 8;
   const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
   PT_HIP_CHECK(hipHostMalloc((void**)&ctrl_, sizeof(MboxCtrl), fl));
   memset((void*)ctrl_, 0, sizeof(MboxCtrl));
