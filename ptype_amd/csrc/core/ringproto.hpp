@@ -121,11 +121,7 @@ inline bool ring_claim(const RingRefs& r, uint64_t seq, double timeout_s) {
 inline bool ring_wait(const RingRefs& r, uint64_t seq, double timeout_s, int64_t* value, uint32_t* status) {
   ReplySlot* out = &r.rep[seq & (r.ring - 1)];
   const uint64_t t0 = ring_now_ns();
-  // A publisher between taking its number and claiming its slot can be merely
-  // descheduled: rescuing it fails a live call.  100 ms was too eager on a loaded
-  // host (the ASan stress run on 8 busy CPUs lost calls), so a dead publisher now
-  // wedges the ring for up to 1 s (or half the caller's timeout, if shorter).
-  const double rescue_after = timeout_s < 2.0 ? timeout_s / 2 : 1.0;
+  const double rescue_after = timeout_s < 0.2 ? timeout_s / 2 : 0.1;
   bool rescued = false;
   uint64_t tag;
   for (unsigned spins = 0; !reply_tag_is(tag = __atomic_load_n(&out->tag, __ATOMIC_ACQUIRE), seq); ++spins) {
@@ -144,7 +140,13 @@ inline bool ring_wait(const RingRefs& r, uint64_t seq, double timeout_s, int64_t
   }
   *value = out->value;  // landed with the tag (one 16-B device store)
   *status = (uint32_t)(tag & 0xff);
-  r.owner[seq & (r.ring - 1)].store(seq + r.ring, std::memory_order_release);
+  // Free the slot only if it is still ours: once the reply has landed, the next
+  // occupant may already have taken the slot over (ring_claim's takeover for a
+  // caller that looks gone).  A blind store here handed its claimed slot back as
+  // unclaimed, and a rescuer then overwrote its published request with a no-op
+  // (a lost call and two writers on one slot: TSan / ASan stress under load).
+  uint64_t mine = seq | kOwnerBusy;
+  r.owner[seq & (r.ring - 1)].compare_exchange_strong(mine, seq + r.ring, std::memory_order_acq_rel);
   return true;
 }
 

@@ -380,6 +380,8 @@ void scenario_shm() {
   auto conn = dial_node("127.0.0.1", port, 2000, true);
   CHECK(dynamic_cast<ShmRpcConn*>(conn.get()) != nullptr);
   std::atomic<int> good{0};
+  std::mutex bad_mu;
+  std::string first_bad;
   std::vector<std::thread> ts;
   for (int t = 0; t < 6; ++t)
     ts.emplace_back([&, t] {
@@ -387,11 +389,19 @@ void scenario_shm() {
         gob::Value args = gob::Value::Struct("Args");
         args.fields = {{"A", gob::Value::Int(t + 1)}, {"B", gob::Value::Int(i)}};
         RpcOutcome o = conn->call("Calculator.Multiply", args, 5000);
-        if (o.ok() && o.reply.i == (int64_t)(t + 1) * i) ++good;
+        if (o.ok() && o.reply.i == (int64_t)(t + 1) * i) {
+          ++good;
+        } else {
+          std::lock_guard<std::mutex> g(bad_mu);
+          if (first_bad.empty())
+            first_bad = "call " + std::to_string(t) + "/" + std::to_string(i) + ": ok=" + std::to_string(o.ok()) +
+                        " err=" + o.error + " reply=" + std::to_string(o.reply.i);
+        }
         if (i % 100 == 99) std::this_thread::sleep_for(std::chrono::milliseconds(30));  // let it park
       }
     });
   for (auto& th : ts) th.join();
+  if (good.load() != 1800) fprintf(stderr, "shm: %d of 1800 good; first failure %s\n", good.load(), first_bad.c_str());
   CHECK(good.load() == 1800);
   CHECK(pokes.load() > 0);  // calls woke a parked dispatcher
   gob::Value e = gob::Value::Struct("Args");
