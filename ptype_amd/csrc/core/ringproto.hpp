@@ -11,7 +11,8 @@
 //   s | kBusy      claimed by s's publisher: published, or about to be; freed
 //                  (-> s + ring) when s's reply has been taken
 //   s | kRescued   s's publisher stalled or died before publishing; a rescuer
-//                  published a no-op (method 0 -> kStatusNoMethod) in its place
+//                  published a no-op (method 0 -> kStatusNoMethod) in its place;
+//                  or s's caller timed out waiting (nobody reads s's reply)
 //
 // A timed-out caller does NOT free its slot (the dispatcher may not have read
 // the request yet): the slot stays busy until the late reply lands, and the
@@ -31,7 +32,39 @@
 
 #include "records.hpp"
 
+// The request ring's real synchronisation runs through its consumer -- a GPU
+// wave in production, another mapping of the segment in the stress test --
+// which ThreadSanitizer cannot see: a slot taken over after its reply landed is
+// ordered behind the previous occupant's request only by that consumer.  These
+// annotations state that edge (publish = release of the slot, reply observed
+// before a takeover = acquire of it).
+#if defined(__SANITIZE_THREAD__)
+#define PT_TSAN_RING 1
+#elif defined(__has_feature)
+#if __has_feature(thread_sanitizer)
+#define PT_TSAN_RING 1
+#endif
+#endif
+#ifdef PT_TSAN_RING
+#include <sanitizer/tsan_interface.h>
+#endif
+
 namespace ptype {
+
+inline void ring_tsan_release(const void* slot) {
+#ifdef PT_TSAN_RING
+  __tsan_release(const_cast<void*>(slot));
+#else
+  (void)slot;
+#endif
+}
+inline void ring_tsan_acquire(const void* slot) {
+#ifdef PT_TSAN_RING
+  __tsan_acquire(const_cast<void*>(slot));
+#else
+  (void)slot;
+#endif
+}
 
 constexpr uint64_t kOwnerBusy = 1ull << 62;
 constexpr uint64_t kOwnerRescued = 1ull << 63;
@@ -60,6 +93,7 @@ inline void ring_write(const RingRefs& r, uint64_t seq, const MsgRecord& m, uint
   s->t_pub_ns = t_ns;
   // a BAR mapping is write-combined: the payload must be out before the tag
   if (r.bar) _mm_sfence();
+  ring_tsan_release(s);
   __atomic_store_n(&s->tag, seq + 1, __ATOMIC_RELEASE);
   if (r.bar) {
     _mm_sfence();
@@ -93,6 +127,7 @@ inline bool ring_claim(const RingRefs& r, uint64_t seq, double timeout_s) {
   std::atomic<uint64_t>& o = r.owner[seq & (r.ring - 1)];
   const uint64_t prev = seq - r.ring;
   const uint64_t t0 = ring_now_ns();
+  const double takeover_after = timeout_s < 2.0 ? timeout_s / 2 : 1.0;
   for (unsigned spins = 0;; ++spins) {
     uint64_t cur = o.load(std::memory_order_acquire);
     if (cur == seq) {
@@ -101,10 +136,18 @@ inline bool ring_claim(const RingRefs& r, uint64_t seq, double timeout_s) {
     }
     if (cur == (seq | kOwnerRescued)) return false;
     if ((spins & 255) == 255) {
-      // the previous occupant published (or was rescued) and its reply landed, but
-      // nobody took it: a caller that timed out or died -- take the slot over
-      if (seq >= r.ring && (cur == (prev | kOwnerBusy) || cur == (prev | kOwnerRescued)) && reply_landed(r, prev)) {
-        if (o.compare_exchange_strong(cur, seq | kOwnerBusy, std::memory_order_acq_rel)) return true;
+      // the previous occupant's reply landed but nobody took it.  Rescued (a no-op
+      // nobody waits for) or abandoned (its caller timed out and marked it): take
+      // the slot over now.  Merely busy: its caller may be alive and just slow to
+      // read the reply -- taking over at once let the next reply overwrite it (a
+      // lost call under load) -- so only after a grace period (a caller that died)
+      const bool gone = cur == (prev | kOwnerRescued) ||
+                        (cur == (prev | kOwnerBusy) && (ring_now_ns() - t0) * 1e-9 > takeover_after);
+      if (seq >= r.ring && gone && reply_landed(r, prev)) {
+        if (o.compare_exchange_strong(cur, seq | kOwnerBusy, std::memory_order_acq_rel)) {
+          ring_tsan_acquire(&r.req[seq & (r.ring - 1)]);  // prev's request was consumed before its reply
+          return true;
+        }
         continue;
       }
       if (r.poke) r.poke();
@@ -121,20 +164,29 @@ inline bool ring_claim(const RingRefs& r, uint64_t seq, double timeout_s) {
 inline bool ring_wait(const RingRefs& r, uint64_t seq, double timeout_s, int64_t* value, uint32_t* status) {
   ReplySlot* out = &r.rep[seq & (r.ring - 1)];
   const uint64_t t0 = ring_now_ns();
-  const double rescue_after = timeout_s < 0.2 ? timeout_s / 2 : 0.1;
-  bool rescued = false;
+  const double rescue_every = timeout_s < 0.2 ? timeout_s / 2 : 0.1;
+  // the scan repeats: a number that was not yet rescuable at one scan (its slot
+  // still held by the previous occupant) can be stranded later, when its
+  // publisher gives up claiming -- a single early scan left the ring wedged
+  double next_rescue = rescue_every;
   uint64_t tag;
   for (unsigned spins = 0; !reply_tag_is(tag = __atomic_load_n(&out->tag, __ATOMIC_ACQUIRE), seq); ++spins) {
     if ((spins & 1023) == 1023) {
       if (r.poke) r.poke();
       const double waited = (ring_now_ns() - t0) * 1e-9;
-      if (!rescued && waited > rescue_after) {
-        rescued = true;
+      if (waited > next_rescue) {
+        next_rescue = waited + rescue_every;
         const uint64_t lo = seq >= r.ring ? seq - r.ring + 1 : 0;
         for (uint64_t p = seq; p-- > lo;)
           if ((r.owner[p & (r.ring - 1)].load(std::memory_order_acquire) & kOwnerSeq) == p) ring_rescue(r, p);
       }
-      if (waited > timeout_s) return false;
+      if (waited > timeout_s) {
+        // abandoned: the next occupant may take the slot over as soon as the late
+        // reply lands (nobody will read it)
+        uint64_t mine = seq | kOwnerBusy;
+        r.owner[seq & (r.ring - 1)].compare_exchange_strong(mine, seq | kOwnerRescued, std::memory_order_acq_rel);
+        return false;
+      }
       std::this_thread::yield();
     }
   }
