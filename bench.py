@@ -67,9 +67,11 @@ def _parse():
                         "or the strided rule (routes computed)")
     p.add_argument("--lookup", choices=["directory", "hash"], default="directory",
                    help="registry mirror read on the route: compiled route directory or hash-table probe")
-    p.add_argument("--delivery", choices=["direct", "mailbox"], default="direct",
-                   help="how a message reaches its actor on its GPU: one fused pass, or through the HBM "
-                        "mailboxes (K2 enqueue + K3 drain; world 1)")
+    p.add_argument("--delivery", choices=["direct", "mailbox"], default="mailbox",
+                   help="how a message reaches its actor on its GPU: through the HBM mailboxes (BASELINE config "
+                        "2: K2 enqueue + K3 drain; at N > 1 on receipt), or one fused resolve-and-run pass")
+    p.add_argument("--sharding", choices=["actor", "arrival"], default="actor",
+                   help="mailbox rings: per actor (every actor's messages FIFO in one ring) or per arrival tile")
     p.add_argument("--zipf", type=float, default=0.0, metavar="S",
                    help="skewed load: actor popularity Zipf(S) (hot actors scattered over the GPUs); batches "
                         "pre-generated outside the timed loop, so compare against --zipf 0 --pregen")
@@ -171,7 +173,7 @@ def main():
     import torch.distributed as dist
 
     from ptype_amd.ops import batch as B
-    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_SEQ_FOLD, STATUS_OK
     from ptype_amd.ops.table import RegistryTable, actor_keys
     from ptype_amd.parallel.exchange import ActorExchange
 
@@ -251,19 +253,33 @@ def main():
             pre.append(B.gen_zipf_requests(M, n_actors, args.zipf, seed=sd, device=device) if args.zipf > 0 else
                        B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=sd, device=device))
 
-    def verify(tag, r=None):
-        r = req if r is None else r
-        ok = bool((st == STATUS_OK).all()) and bool(torch.equal(val, r.a0 * r.a1))
+    def verify(tag, r, v, t, method):
+        ok = bool((t == STATUS_OK).all())
+        if ok and method == METHOD_CALC_MULTIPLY:
+            ok = bool(torch.equal(v, r.a0 * r.a1))
         if not ok:
-            bad = int((st != STATUS_OK).sum())
+            bad = int((t != STATUS_OK).sum())
             raise SystemExit(f"[rank {rank}] {tag}: verification failed ({bad} non-OK replies)")
 
-    def measure(table, steps, warmup, delivery=args.delivery):
-        """Warm up, then time `steps` Sends (barrier + synchronize on both sides,
-        max over ranks); returns (seconds, exchange, graph used)."""
-        # the bench sends Calculator.Multiply only (stateless): mailboxes shard by arrival
-        ex = ActorExchange(table, M, chunks=chunks, state=state, fake=fake, delivery=delivery, mailbox_ordered=False)
+    def measure(table, steps, warmup, delivery=args.delivery, sharding=args.sharding, Mq=M,
+                method=METHOD_CALC_MULTIPLY):
+        """Warm up, then time `steps` Sends of `Mq` messages (barrier + synchronize
+        on both sides, max over ranks); returns (seconds, exchange, graph used).
+        Replies are verified after the warm-up and after the timed steps: every
+        status OK and, for Calculator.Multiply, every value == A * B."""
+        # mailbox delivery: actor-sharded rings (each actor's messages in message
+        # order in one ring) unless --sharding arrival (tile-sharded queues)
+        ex = ActorExchange(table, Mq, chunks=chunks, state=state, fake=fake, delivery=delivery,
+                           mailbox_ordered=sharding == "actor")
         _LIVE_EXCHANGES.append(weakref.ref(ex))  # (weak: a finished measurement's buffers stay freeable)
+        if Mq == M and method == METHOD_CALC_MULTIPLY:
+            rq, v, t = req, val, st
+        else:
+            rq = B.MsgBatch(torch.empty(Mq, dtype=torch.int32, device=device),
+                            torch.empty(Mq, dtype=torch.int64, device=device),
+                            torch.empty(Mq, dtype=torch.int64, device=device), None, method)
+            v = torch.empty(Mq, dtype=torch.int64, device=device)
+            t = torch.empty(Mq, dtype=torch.int32, device=device)
         graph = None
         if use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
@@ -273,45 +289,53 @@ def main():
                                   device=device)
 
             def prologue(j=0):  # step j of a replay draws from seed j; the last one advances them all
-                B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, device=device, out=req, seed_tensor=seed_t[j:j + 1])
+                B.gen_requests(Mq, n_actors, method, device=device, out=rq, seed_tensor=seed_t[j:j + 1])
                 if j == U - 1:
                     seed_t.add_(U * 0x1000193)
 
-            graph = ex.capture(req, val, st, prologue=prologue, allow_collectives=args.graph == "on",
+            graph = ex.capture(rq, v, t, prologue=prologue, allow_collectives=args.graph == "on",
                                repeat=args.steps_per_graph)
 
-        def step(s):
+        def step(s_):
             if graph is not None:
-                if s % args.steps_per_graph == 0:  # one replay runs steps_per_graph whole steps
+                if s_ % args.steps_per_graph == 0:  # one replay runs steps_per_graph whole steps
                     graph.replay()
                 return
-            if pre:
-                ex.send_all(pre[s % len(pre)], out=(val, st))
+            if pre and Mq == M and method == METHOD_CALC_MULTIPLY:
+                ex.send_all(pre[s_ % len(pre)], out=(v, t))
                 return
-            B.gen_requests(M, n_actors, METHOD_CALC_MULTIPLY, seed=(s * world + rank) * 0x1000193 + 7, device=device,
-                           out=req)
-            ex.send(req, val, st)
+            B.gen_requests(Mq, n_actors, method, seed=(s_ * world + rank) * 0x1000193 + 7, device=device, out=rq)
+            ex.send(rq, v, t)
 
-        for s in range(warmup):
-            step(s)
+        def last(k):
+            return pre[(k - 1) % len(pre)] if pre and Mq == M and method == METHOD_CALC_MULTIPLY else rq
+
+        for s_ in range(warmup):
+            step(s_)
         sync()
         if warmup:
-            verify("warmup", pre[(warmup - 1) % len(pre)] if pre else None)
+            verify("warmup", last(warmup), v, t, method)
         barrier()
         sync()
         t0 = time.perf_counter()
-        for s in range(steps):
-            step(warmup + s)
+        for s_ in range(steps):
+            step(warmup + s_)
         sync()
         barrier()
         elapsed = time.perf_counter() - t0
         if dist_on:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
         if steps:
-            verify("timed", pre[(warmup + steps - 1) % len(pre)] if pre else None)
+            verify("timed", last(warmup + steps), v, t, method)
         return elapsed, ex, graph is not None
+
+    def mailbox_info(ex_):
+        mb = ex_.mailboxes
+        if mb is None:
+            return {}
+        return {"mailbox_shards": mb.shards, "mailbox_slots": mb.slots, "mailbox_ring_bytes": mb.bytes}
 
     table = build_table(args.placement)
     hang_s = os.environ.get("PTYPE_HANG_DIAG")
@@ -327,27 +351,40 @@ def main():
         return "computed (verified strided rule)" if t.affine else "route directory gather"
 
     route_mode = lookup_mode(table)
-    secondary = None
+    head_mailbox = mailbox_info(ex)
+    secondaries = {}
     if args.placement != "affine" and not args.no_secondary and args.steps:
-        # secondary figure only: the same step with the strided placement, whose routes
-        # need no registry reads (what round 1 reported as its headline)
+        # the same step with the strided placement, whose routes need no registry reads
         t2 = build_table("affine")
         e2, _, _ = measure(t2, args.steps, max(1, args.warmup))
-        secondary = {"placement": "affine", "registry_lookup": lookup_mode(t2),
-                     "value": M * world * args.steps / e2 if e2 > 0 else 0.0,
-                     "ms_per_step": e2 / args.steps * 1e3}
-
-    mailbox = None
+        secondaries["affine_placement"] = {"placement": "affine", "registry_lookup": lookup_mode(t2),
+                                           "delivery": args.delivery, "msgs_per_gpu_per_step": M,
+                                           "value": M * world * args.steps / e2 if e2 > 0 else 0.0,
+                                           "ms_per_step": e2 / args.steps * 1e3}
+        del t2
     if world == 1 and not dist_on and fake is None and not args.no_secondary and args.steps:
-        # the same step through the HBM mailboxes (K2 enqueue + K3 drain) or, when the
-        # headline already used them, through the fused direct pass
-        other = "direct" if args.delivery == "mailbox" else "mailbox"
-        e3, ex3, _ = measure(table, args.steps, max(1, args.warmup), delivery=other)
-        mailbox = {"delivery": other, "placement": args.placement, "value": M * args.steps / e3 if e3 > 0 else 0.0,
-                   "ms_per_step": e3 / args.steps * 1e3}
-        if ex3.mailboxes is not None:
-            mailbox.update(shards=ex3.mailboxes.shards, slots=ex3.mailboxes.slots,
-                           ring_bytes=ex3.mailboxes.bytes)
+        runs = []
+        if args.delivery == "mailbox" and args.sharding == "actor":
+            # BASELINE config 2 at its own size: 1 Mi messages per step
+            runs.append(("config2_1m", dict(delivery="mailbox", sharding="actor", Mq=min(M, 1 << 20))))
+            runs.append(("arrival_sharded", dict(delivery="mailbox", sharding="arrival")))
+            # an ORDERED stateful method (SeqFold: state = state * K + a0, non-commutative):
+            # every actor runs its messages one at a time in ring (= message) order
+            runs.append(("ordered_seqfold", dict(delivery="mailbox", sharding="actor", method=METHOD_SEQ_FOLD)))
+        if args.delivery != "direct":
+            runs.append(("direct", dict(delivery="direct")))
+        else:
+            runs.append(("mailbox", dict(delivery="mailbox", sharding=args.sharding)))
+        for name, kw in runs:
+            e3, ex3, _ = measure(table, args.steps, max(1, args.warmup), **kw)
+            Mq = kw.get("Mq", M)
+            secondaries[name] = {"delivery": kw["delivery"], "placement": args.placement, "msgs_per_gpu_per_step": Mq,
+                                 "value": Mq * args.steps / e3 if e3 > 0 else 0.0,
+                                 "ms_per_step": e3 / args.steps * 1e3, **mailbox_info(ex3)}
+            if kw["delivery"] == "mailbox":
+                secondaries[name]["sharding"] = kw.get("sharding", "actor")
+                secondaries[name]["method"] = "SeqFold (ordered)" if kw.get("method") == METHOD_SEQ_FOLD \
+                    else "Calculator.Multiply"
             del ex3
 
     # diagnostics, outside the timed region: the step's all-to-all byte volume moved
@@ -500,6 +537,7 @@ def main():
                 "placement": args.placement,
                 "registry_lookup": route_mode,
                 "delivery": args.delivery,
+                **({"sharding": args.sharding, **head_mailbox} if args.delivery == "mailbox" else {}),
                 **({"loopback_ranks": args.loopback, "link_gbps": args.link_gbps, "note": "profiling mode: rank 0 of a symmetric "
                     f"{args.loopback}-rank node, all-to-alls as local copies (not a headline number)"}
                    if fake else {}),
@@ -507,10 +545,8 @@ def main():
         }
         if diag is not None:
             out["diag"] = diag
-        if secondary is not None:
-            out["secondary"] = secondary
-        if mailbox is not None:
-            out["secondary_delivery"] = mailbox
+        if secondaries:
+            out["secondaries"] = secondaries
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()

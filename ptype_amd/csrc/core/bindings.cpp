@@ -741,6 +741,13 @@ PYBIND11_MODULE(_core, m) {
           },
           py::arg("method"), py::arg("actor"), py::arg("a0") = 0, py::arg("a1") = 0, py::arg("a2") = 0,
           py::arg("timeout") = 10.0);
+  py::class_<HostDispatcher, std::shared_ptr<HostDispatcher>>(
+      m, "HostDispatcher", "CPU stand-in for the GPU dispatcher on a shared-memory segment of its own")
+      .def(py::init([](const std::string& name, uint32_t ring) { return std::make_shared<HostDispatcher>(name, ring); }),
+           py::arg("name"), py::arg("ring") = 64)
+      .def_property_readonly("name", &HostDispatcher::name)
+      .def_property_readonly("processed", &HostDispatcher::processed)
+      .def_property_readonly("noops", &HostDispatcher::noops);
   // the dma-buf fd hand-off of the cross-process device ring, bound for tests
   py::class_<FdHandoff, std::shared_ptr<FdHandoff>>(m, "FdHandoff")
       .def(py::init([](const std::string& name, int fd) { return std::make_shared<FdHandoff>(name, fd); }),

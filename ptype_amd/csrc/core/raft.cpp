@@ -349,6 +349,16 @@ void Node::tick() {
   if (role_ == kLeader) {
     ++hb_elapsed_;
     ++elapsed_;
+    // ReadIndex rounds whose acks never came (dropped heartbeats, a requester
+    // that re-asked with a fresh ctx) expire instead of piling up
+    for (auto it = reads_.begin(); it != reads_.end();) {
+      if (++it->second.age > kReadExpiryElections * opt_.election_tick) {
+        read_done(it->first, 0, it->second.from, false);
+        it = reads_.erase(it);
+      } else {
+        ++it;
+      }
+    }
     if (hb_elapsed_ >= opt_.heartbeat_tick) {
       hb_elapsed_ = 0;
       broadcast_heartbeat();
@@ -542,6 +552,12 @@ void Node::step_candidate(const Message& m) {
         become_leader();
       else if (votes_rejected_.size() >= quorum())
         become_follower(term_, 0);
+      break;
+    case kMsgReadIndex:  // no leader to ask: the requester retries (instead of waiting out its round)
+      read_done(m.context, 0, m.from, false);
+      break;
+    case kMsgReadIndexResp:  // an answer to a read asked while this node was a follower
+      read_states_.push_back(ReadState{m.context, m.index, !m.reject});
       break;
     default:
       break;

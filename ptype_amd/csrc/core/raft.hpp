@@ -186,8 +186,10 @@ class Node {
 
   struct PendingRead {
     uint64_t index = 0, from = 0;
+    int age = 0;  // leader ticks since the round started (expired past kReadExpiryElections elections)
     std::set<uint64_t> acks;
   };
+  static constexpr int kReadExpiryElections = 4;
   std::map<std::string, PendingRead> reads_;  // leader: awaiting a quorum of heartbeat acks
   std::vector<ReadState> read_states_;
 

@@ -243,16 +243,27 @@ ReplyRecord shm_call(const ShmView& v, const MsgRecord& m, double timeout_s) {
   r.req = v.req;
   r.rep = v.rep;
   r.owner = v.owner;
+  r.takers = v.takers;
+  r.next_seq = &v.hdr->next_seq;
   r.ring = v.hdr->ring;
   r.bar = v.bar;
   r.poke = [&v] { poke_if_parked(v); };
-  const uint64_t seq = v.hdr->next_seq.fetch_add(1);
+  RingTicket t = ring_take(r, 1, timeout_s);
+  RingTicketGuard guard{r, t};
+  const uint64_t seq = t.seq;
+  ring_test_stop("took");
   if (!ring_claim(r, seq, timeout_s))
     fail(Errc::kTimeout, "device actor call: request slot not free in time (left for rescue)");
+  ring_test_stop("claimed");
   ring_write(r, seq, m, now_ns());
   poke_if_parked(v);
   int64_t value = 0;
   uint32_t status = 0;
+  if (getenv("PTYPE_RING_TEST_STOP")) {  // test hook: stop once the reply has landed, before reading it
+    const uint64_t t0 = now_ns();
+    while (!reply_landed(r, seq) && (now_ns() - t0) * 1e-9 < timeout_s) std::this_thread::yield();
+    ring_test_stop("landed");
+  }
   if (!ring_wait(r, seq, timeout_s, &value, &status)) fail(Errc::kTimeout, "device actor call: reply timeout");
   ReplyRecord out;
   out.value = value;
@@ -287,6 +298,59 @@ std::string shm_locator_lookup(int port) {
   std::memcpy(&pid, b, sizeof pid);
   if (pid <= 0 || (kill(pid, 0) != 0 && errno == ESRCH)) return "";  // its server is gone
   return std::string(b + 8, strnlen(b + 8, 240));
+}
+
+}  // namespace ptype
+
+namespace ptype {
+
+// ---- HostDispatcher
+HostDispatcher::HostDispatcher(const std::string& name, uint32_t ring) {
+  if (ring < 2 || (ring & (ring - 1))) throw std::invalid_argument("HostDispatcher: ring must be a power of two");
+  seg_ = ShmSegment::create(name, shm_bytes(ring));
+  seg_->unlink_on_close();
+  v_ = shm_view(seg_->base(), ring);
+  for (uint32_t i = 0; i < ring; ++i) v_.owner[i].store(i, std::memory_order_relaxed);
+  v_.hdr->ring = ring;
+  v_.hdr->owner_pid = (int32_t)getpid();
+  __atomic_store_n(&v_.ctrl->state, (uint64_t)kRunning, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&v_.hdr->magic, kShmMagic, __ATOMIC_RELEASE);
+  thread_ = std::thread([this] { loop(); });
+}
+
+HostDispatcher::~HostDispatcher() {
+  stop_.store(true);
+  if (thread_.joinable()) thread_.join();
+}
+
+void HostDispatcher::loop() {
+  const uint32_t ring = v_.hdr->ring;
+  uint64_t head = 0;
+  unsigned idle = 0;
+  while (!stop_.load(std::memory_order_relaxed)) {
+    RingSlot* sl = &v_.req[head & (ring - 1)];
+    if (__atomic_load_n(&sl->tag, __ATOMIC_ACQUIRE) != head + 1) {
+      if (++idle > 4096) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      else std::this_thread::yield();
+      continue;
+    }
+    idle = 0;
+    const MsgRecord m = sl->msg;
+    if (ring_csum(head, m) != sl->csum) continue;  // payload not yet visible with its tag: read again
+    int64_t value = 0;
+    uint32_t st = kStatusOk;
+    switch (m.method) {
+      case kCalculatorMultiply: value = m.a0 * m.a1; break;
+      case kEcho: value = m.a0; break;
+      default: st = kStatusNoMethod; break;
+    }
+    if (m.method == kMethodNone) noops_.fetch_add(1);
+    ReplySlot* o = &v_.rep[head & (ring - 1)];
+    o->value = value;
+    __atomic_store_n(&o->tag, reply_tag(head, st), __ATOMIC_RELEASE);
+    processed_.fetch_add(1);
+    ++head;
+  }
 }
 
 }  // namespace ptype

@@ -13,6 +13,7 @@
 // poke when the dispatcher wave has parked itself.
 //
 // Layout: [ShmHeader, 16 KB][ServerCtrl, 4 KB][RingSlot x ring][ReplySlot x ring][u64 owner x ring]
+//         [RingTaker x kRingTakers] (ringproto.hpp: who holds which sequence numbers)
 //
 // Request ring placement: by default the ring the dispatcher
 // polls is NOT the segment's RingSlot area but fine-grained memory on the
@@ -32,10 +33,11 @@
 #include <vector>
 
 #include "records.hpp"
+#include "ringproto.hpp"
 
 namespace ptype {
 
-constexpr uint64_t kShmMagic = 0x32736d6570797470ull;  // "ptypems2"
+constexpr uint64_t kShmMagic = 0x33736d6570797470ull;  // "ptypems3" (taker entries)
 constexpr int kShmMaxMethods = 32;
 
 struct ShmMethod {
@@ -68,7 +70,8 @@ static_assert(std::atomic<uint64_t>::is_always_lock_free, "process-shared atomic
 constexpr size_t kShmHeaderBytes = 16384, kShmCtrlBytes = 4096;
 
 inline size_t shm_bytes(uint32_t ring) {
-  return kShmHeaderBytes + kShmCtrlBytes + (size_t)ring * (sizeof(RingSlot) + sizeof(ReplySlot) + sizeof(uint64_t));
+  return kShmHeaderBytes + kShmCtrlBytes + (size_t)ring * (sizeof(RingSlot) + sizeof(ReplySlot) + sizeof(uint64_t)) +
+         (size_t)kRingTakers * sizeof(RingTaker);
 }
 
 struct ShmView {
@@ -77,6 +80,7 @@ struct ShmView {
   RingSlot* req = nullptr;
   ReplySlot* rep = nullptr;
   std::atomic<uint64_t>* owner = nullptr;
+  RingTaker* takers = nullptr;
   bool bar = false;  // `req` is device memory written through a BAR mapping
 };
 
@@ -88,6 +92,7 @@ inline ShmView shm_view(void* base, uint32_t ring) {
   v.req = reinterpret_cast<RingSlot*>(p + kShmHeaderBytes + kShmCtrlBytes);
   v.rep = reinterpret_cast<ReplySlot*>(reinterpret_cast<char*>(v.req) + (size_t)ring * sizeof(RingSlot));
   v.owner = reinterpret_cast<std::atomic<uint64_t>*>(reinterpret_cast<char*>(v.rep) + (size_t)ring * sizeof(ReplySlot));
+  v.takers = reinterpret_cast<RingTaker*>(reinterpret_cast<char*>(v.owner) + (size_t)ring * sizeof(uint64_t));
   return v;
 }
 
@@ -159,6 +164,30 @@ ShmView shm_attach_view(const std::shared_ptr<ShmSegment>& seg, std::shared_ptr<
 // Publish one request into the segment's ring and wait for its reply (any
 // process).  `poke` is called when the dispatcher is not running.
 ReplyRecord shm_call(const ShmView& v, const MsgRecord& m, double timeout_s);
+
+// A CPU stand-in for the GPU's persistent dispatcher on a segment of its own:
+// the same protocol (requests strictly in sequence order, 16-B reply tag +
+// value), stateless handlers only (Calculator.Multiply, Echo; anything else
+// answers kStatusNoMethod).  For GPU-less hosts and the ring-protocol tests
+// (liveness with stopped and killed callers).
+class HostDispatcher {
+ public:
+  HostDispatcher(const std::string& name, uint32_t ring);
+  ~HostDispatcher();
+  HostDispatcher(const HostDispatcher&) = delete;
+  HostDispatcher& operator=(const HostDispatcher&) = delete;
+  const std::string& name() const { return seg_->name(); }
+  uint64_t processed() const { return processed_.load(); }
+  uint64_t noops() const { return noops_.load(); }  // rescued numbers (method 0) answered
+
+ private:
+  void loop();
+  std::shared_ptr<ShmSegment> seg_;
+  ShmView v_;
+  std::atomic<bool> stop_{false};
+  std::atomic<uint64_t> processed_{0}, noops_{0};
+  std::thread thread_;
+};
 
 // port -> segment locator written by a listening net/rpc server with
 // shared-memory device methods ("/ptype-port-<port>").

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "mailbox.hpp"
+#include "mailbox_dev.hpp"
 #include "packed.hpp"
 #include "route_common.hpp"
 
@@ -14,90 +15,7 @@ namespace ptype {
 
 int64_t wire_req_words(int64_t C, int nargs, bool mc);
 
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-// Write-through (sc1) 16-B store: the record halves a concurrent consumer on
-// another XCD reads (MI355X_MICROARCH.md, hand-off forms: sc1 payload stores
-// drained before the signal).
-__device__ __forceinline__ void st16_sc1(void* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// A read that cannot be served by a stale L2 line: the per-XCD L2s are not
-// coherent with each other while a kernel runs, and a word another XCD keeps
-// rewriting (a tail, a ring slot) can sit in this XCD's L2 from an earlier
-// read.  A no-op atomic executes at the memory side and returns memory's value.
-__device__ __forceinline__ unsigned long long ld_fresh(unsigned long long* p) {
-  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u32x4 ld16_fresh(uint32_t* p) {
-  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-  const unsigned long long lo = ld_fresh(q), hi = ld_fresh(q + 1);
-  return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-}
-__device__ __forceinline__ uint64_t sys_ld64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ unsigned long long* ctr_tail(const MboxView& mv, uint32_t s) {
-  return mv.ctr + (uint64_t)s * kMboxCtrStride;
-}
-__device__ __forceinline__ unsigned long long* ctr_done(const MboxView& mv, uint32_t s) {
-  return mv.ctr + (uint64_t)s * kMboxCtrStride + 1;
-}
-__device__ __forceinline__ unsigned long long* ctr_head(const MboxView& mv, uint32_t s) {
-  return mv.ctr + (uint64_t)s * kMboxCtrStride + 16;
-}
-// A record is two 16-B halves in two planes: plane A {tag, mailbox, origin,
-// method | flags} at rec[slot], plane B {a0, a1} at rec[b_off + slot], so a
-// wave's store of one half covers 64 consecutive 16-B cells -- whole lines.  As
-// one 32-B record per slot (PTYPE_MBOX_PLANAR=0) each store instruction wrote
-// every other 16 B of 64 records: the enqueue's DRAM writes were 419 MB for 268 MB
-// of records (PMC WRITE_SIZE).  Bench mailbox step: 0.247 ms (32-B records) ->
-// 0.215 ms (planes, de-aliased; see the pad below).
-__device__ __forceinline__ uint64_t slot_at(const MboxView& mv, uint32_t s, uint64_t pos) {
-  return ((uint64_t)s << mv.log_q) | (pos & ((1ull << mv.log_q) - 1));
-}
-__device__ __forceinline__ uint32_t* rec_a(const MboxView& mv, uint64_t slot) {
-  return mv.rec + slot * (mv.planar ? 4 : 8);
-}
-__device__ __forceinline__ uint32_t* rec_b(const MboxView& mv, uint64_t slot) {
-  return mv.planar ? mv.rec + mv.b_off + slot * 4 : mv.rec + slot * 8 + 4;
-}
-__device__ __forceinline__ uint32_t* rec_at(const MboxView& mv, uint32_t s, uint64_t pos) {
-  return rec_a(mv, slot_at(mv, s, pos));
-}
-__device__ __forceinline__ uint32_t lap_tag(const MboxView& mv, uint64_t pos) {
-  return (uint32_t)(pos >> mv.log_q) + 1u;
-}
-
-__device__ __forceinline__ void block_add_stats(unsigned long long* stats, unsigned long long v0, int w0,
-                                                unsigned long long v1, int w1, unsigned long long v2, int w2) {
-  __shared__ unsigned long long part[3][4];
-  for (int off = 32; off > 0; off >>= 1) {
-    v0 += __shfl_xor(v0, off);
-    v1 += __shfl_xor(v1, off);
-    v2 += __shfl_xor(v2, off);
-  }
-  const int w = threadIdx.x / kWave;
-  if (lane_id() == 0) part[0][w] = v0, part[1][w] = v1, part[2][w] = v2;
-  __syncthreads();
-  if (threadIdx.x < 3) {
-    unsigned long long v = 0;
-    for (int k = 0; k < (int)(blockDim.x / kWave); ++k) v += part[threadIdx.x][k];
-    const int word = threadIdx.x == 0 ? w0 : threadIdx.x == 1 ? w1 : w2;
-    // striped by block: one word for the whole grid serialised thousands of
-    // same-address atomics (~9 ns each) at the kernel's end (readers sum stripes)
-    const size_t stripe = (size_t)((blockIdx.x + blockIdx.y * gridDim.x) % kMbStripes) * kMbStatWords;
-    if (v && word >= 0) atomicAdd(&stats[stripe + word], v);
-  }
-}
-
 // ---------------------------------------------------------------- K2 enqueue
-// Reply of a message that never enters a ring, written at enqueue.
-__device__ __forceinline__ void write_status(const ReplyView& rv, uint32_t origin, int32_t status);
-
 // The common part of K2 for one tile of K * 256 messages already resolved to
 // (ok, mailbox, method, args, origin): per-shard ranks in LDS, ONE reservation
 // per (tile, shard), capacity check against the shard's head, the records
@@ -155,8 +73,26 @@ __device__ __forceinline__ void enqueue_tile(const MboxView& mv, unsigned long l
   for (uint32_t s = threadIdx.x; s < S; s += blockDim.x) {
     const unsigned c = hist[s];
     if (c) {
-      base[s] = atomicAdd(ctr_tail(mv, s), (unsigned long long)c);
-      lim[s] = (LIVE ? ld_fresh(ctr_head(mv, s)) : *ctr_head(mv, s)) + Q;
+      if constexpr (LIVE) {
+        // clamped to the ring's free space (a CAS bounded by head + Q): a full ring
+        // reserves nothing, so overflow leaves no hole a live consumer would have
+        // to wait out -- under producers that never pause it never could
+        // (the unclamped add made consumption crawl under overload)
+        unsigned long long t = ld_fresh(ctr_tail(mv, s)), take = 0;
+        for (;;) {
+          const unsigned long long room = ld_fresh(ctr_head(mv, s)) + Q;
+          take = t < room ? (room - t < c ? room - t : c) : 0ull;
+          if (!take) break;
+          const unsigned long long seen = atomicCAS(ctr_tail(mv, s), t, t + take);
+          if (seen == t) break;
+          t = seen;
+        }
+        base[s] = t;
+        lim[s] = t + take;  // offsets >= take overflow (answered now, never reserved)
+      } else {
+        base[s] = atomicAdd(ctr_tail(mv, s), (unsigned long long)c);
+        lim[s] = *ctr_head(mv, s) + Q;
+      }
     }
   }
   __syncthreads();
@@ -204,9 +140,9 @@ __device__ __forceinline__ void enqueue_tile(const MboxView& mv, unsigned long l
   }
   if constexpr (LIVE) vm_drain();
   __syncthreads();  // every wave's records are out: the tile's positions are done
-  if constexpr (LIVE) {
+  if constexpr (LIVE) {  // the reserved positions are written: done catches up with tail
     for (uint32_t s = threadIdx.x; s < S; s += blockDim.x)
-      if (hist[s]) atomicAdd(ctr_done(mv, s), (unsigned long long)hist[s]);
+      if (hist[s] && lim[s] > base[s]) atomicAdd(ctr_done(mv, s), lim[s] - base[s]);
   }
   __syncthreads();  // LDS reused by the next tile
 }
@@ -400,45 +336,6 @@ __global__ __launch_bounds__(256) void mailbox_enqueue_slots_packed_kernel(MboxV
                                     x2, org, has_a2, rv, n_enq, n_ovf, n_miss);
   }
   block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
-}
-
-// ---------------------------------------------------------------- record decode + reply
-struct MboxMsg {
-  MsgRecord m;
-  uint32_t origin;
-  bool valid;
-};
-
-__device__ __forceinline__ MboxMsg decode(const u32x4& ha, const u32x4& hb, const int64_t* a2v) {
-  MboxMsg x;
-  x.m.actor = ha.y;
-  x.origin = ha.z;
-  x.m.method = (uint16_t)(ha.w & 0xffffu);
-  x.m.flags = (uint16_t)(ha.w >> 16);
-  x.m.a0 = (int64_t)(((uint64_t)hb.y << 32) | hb.x);
-  x.m.a1 = (int64_t)(((uint64_t)hb.w << 32) | hb.z);
-  x.m.a2 = (x.m.flags & kFlagA2) && a2v ? *a2v : 0;
-  x.valid = true;
-  return x;
-}
-
-__device__ __forceinline__ void put_reply(const ReplyView& rv, uint32_t origin, int64_t value, int32_t status) {
-  if ((uint64_t)origin >= rv.n) return;
-  if (rv.slots) {  // wire v2 reply regions: values int64[C] then statuses u8[C] per source rank
-    const uint32_t d = origin / rv.C, pos = origin - d * rv.C;
-    uint32_t* rb = rv.slots + (int64_t)d * rv.rep_words;
-    reinterpret_cast<int64_t*>(rb + 4)[pos] = value;
-    reinterpret_cast<uint8_t*>(rb + 4 + 2 * (int64_t)rv.C)[pos] = (uint8_t)status;
-    return;
-  }
-  rv.val[origin] = value;
-  rv.st[origin] = status;
-}
-__device__ __forceinline__ void write_reply(const ReplyView& rv, uint32_t origin, const ReplyRecord& r) {
-  put_reply(rv, origin, r.value, r.status);
-}
-__device__ __forceinline__ void write_status(const ReplyView& rv, uint32_t origin, int32_t status) {
-  put_reply(rv, origin, 0, status);
 }
 
 // Run one window of up to 64 records (lane l holds ring position h + l) in ring
@@ -874,6 +771,9 @@ Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) 
   const size_t ctr_bytes = (size_t)shards * kMboxCtrStride * 8;
   PT_HIP_CHECK(hipMalloc((void**)&mv_.ctr, ctr_bytes));
   PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, ctr_bytes, stream_));
+  PT_HIP_CHECK(hipMalloc((void**)&sort_hist_, (size_t)kMboxSortHistWords * sizeof(uint32_t)));
+  PT_HIP_CHECK(hipMalloc((void**)&sort_tot_, (size_t)shards * sizeof(uint32_t)));
+  bytes_ += (size_t)kMboxSortHistWords * sizeof(uint32_t) + (size_t)shards * sizeof(uint32_t);
   PT_HIP_CHECK(hipMalloc((void**)&mv_.stats, kMbStripes * kMbStatWords * 8));
   PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStripes * kMbStatWords * 8, stream_));
   bytes_ += ctr_bytes + kMbStripes * kMbStatWords * 8;
@@ -896,6 +796,8 @@ Mailboxes::~Mailboxes() {
   if (mv_.a2) (void)hipFree(mv_.a2);
   (void)hipFree(mv_.ctr);
   (void)hipFree(mv_.stats);
+  if (sort_hist_) (void)hipFree(sort_hist_);
+  if (sort_tot_) (void)hipFree(sort_tot_);
   if (ctrl_) (void)hipHostFree(ctrl_);
 }
 

@@ -44,6 +44,7 @@
 // order; everything else runs in parallel.
 #pragma once
 #include <memory>
+#include <vector>
 
 #include "common.hpp"
 #include "handlers.hpp"
@@ -53,6 +54,10 @@ namespace ptype {
 constexpr int kMboxCtrStride = 32;  // u64 words per shard: [0] tail, [1] done (one line), [16] head (another)
 constexpr int kMboxCtrTicket = 24;  // [24]: the epoch drain's per-shard last-block ticket (self-resetting)
 constexpr int kMboxMaxShards = 4096;
+// Sorted epoch mailboxes (mailbox_sort.hip): shard limit, and the per-(block,
+// shard) histogram's size -- it bounds the count / scatter grid (G <= words / S)
+constexpr int kMboxSortMaxShards = 1024;
+constexpr uint32_t kMboxSortHistWords = 1u << 18;
 enum MboxStat : int {
   kMbEnqueued = 0,   // records written into rings
   kMbOverflow = 1,   // messages answered kStatusOverflow (ring full)
@@ -118,10 +123,40 @@ void launch_mailbox_consumer(const MboxView& mv, MboxCtrl* ctrl, uintptr_t state
                              uint64_t delay_ticks, const ReplyView& rv, int blocks, uint64_t idle_ticks,
                              uint64_t max_ticks, uintptr_t stream);
 
+// One epoch Send through the sorted mailboxes (Mailboxes::send_sorted).
+struct MboxSend {
+  uintptr_t actor = 0, a0 = 0, a1 = 0, a2 = 0, method_col = 0;
+  int method_uniform = 0;
+  int64_t M = 0;
+  uintptr_t table = 0;
+  uint64_t cap = 0;
+  uintptr_t dir = 0;
+  uint32_t n_dir = 0, affine_w = 0;
+  int rank_self = 0;
+  uint32_t origin_base = 0;
+  uintptr_t out_val = 0, out_st = 0;
+  uint64_t out_n = 0;
+  uintptr_t state = 0;
+  uint32_t n_state = 0;
+  uint64_t delay_ticks = 0;
+  std::vector<uintptr_t> outbox;
+  uint64_t outbox_cap = 0;
+  bool arrival = false;  // shard by arrival tile (batches without ordered methods)
+  bool ordered = true;   // ordered drain: per-actor serial, FIFO; else the parallel drain
+  int fixed_method = 0;  // every message carries this method (constant-folded handler)
+  uintptr_t stream = 0;
+};
+
 class Mailboxes {
  public:
   Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2);
   ~Mailboxes();
+
+  // Epoch Send (mailbox_sort.hip): K2 as a stable counting sort of the batch into
+  // the shard rings (count, scan, scatter: every ring in message order), then
+  // the ordered or parallel K3 drain; replies at origin_base + message index.
+  // The rings must be empty of live records (no persistent session running).
+  void send_sorted(const MboxSend& a);
 
   // K2 from a SoA client batch resolved against the registry mirror (this rank's
   // actors only); origin of message i = origin_base + i.  `live`: a persistent
@@ -162,6 +197,8 @@ class Mailboxes {
   hipStream_t stream_ = nullptr;
   bool started_ = false;
   uint64_t launches_ = 0;
+  uint32_t* sort_hist_ = nullptr;  // [G][S] per-block shard counts -> prefixes (send_sorted)
+  uint32_t* sort_tot_ = nullptr;   // [S] the epoch's total per shard
 };
 
 }  // namespace ptype

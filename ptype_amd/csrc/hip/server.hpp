@@ -298,6 +298,13 @@ class DeviceServer {
       PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dctrl_, ctrl_, 0));
       owner_mem_.reset(new std::atomic<uint64_t>[ring_]);
       owner_ = owner_mem_.get();
+      takers_mem_.reset(new RingTaker[kRingTakers]);
+      takers_ = takers_mem_.get();
+      for (uint32_t i = 0; i < kRingTakers; ++i) {
+        takers_[i].token.store(0, std::memory_order_relaxed);
+        takers_[i].range.store(0, std::memory_order_relaxed);
+        takers_[i].state.store(kTakerIdle, std::memory_order_relaxed);
+      }
       seq_ = &local_seq_;
     } else {
       seg_ = ShmSegment::create(shm_name, shm_bytes(ring_));
@@ -307,6 +314,7 @@ class DeviceServer {
       rep_ = v.rep;
       ctrl_ = v.ctrl;
       owner_ = v.owner;
+      takers_ = v.takers;  // zero-filled with the new segment
       seq_ = &hdr_->next_seq;
       PT_HIP_CHECK(hipHostRegister(seg_->base(), seg_->size(), hipHostRegisterMapped | hipHostRegisterPortable));
       registered_ = true;
@@ -391,13 +399,16 @@ class DeviceServer {
   // Publish n requests and wait for all replies (any thread).
   void call(const MsgRecord* in, ReplyRecord* out, int n, double timeout_s) {
     if (closed_) throw std::runtime_error("device server closed");
-    std::unique_ptr<uint64_t[]> seqs(new uint64_t[n]);
     int done = 0;
     while (done < n) {
-      const int batch = std::min<int>(n - done, (int)(ring_ / 2));
-      for (int i = 0; i < batch; ++i) seqs[done + i] = publish(in[done + i], timeout_s);
+      const int batch = std::min<int>({n - done, (int)(ring_ / 2), (int)kRingMaxTake});
+      const RingRefs r = refs();
+      // one taker entry names the batch's numbers until every reply is read
+      RingTicket t = ring_take(r, (uint32_t)batch, timeout_s);
+      RingTicketGuard guard{r, t};
+      for (int i = 0; i < batch; ++i) publish(r, t.seq + (uint64_t)i, in[done + i], timeout_s);
       ensure_running();
-      for (int i = 0; i < batch; ++i) out[done + i] = wait(seqs[done + i], timeout_s);
+      for (int i = 0; i < batch; ++i) out[done + i] = wait(t.seq + (uint64_t)i, timeout_s);
       done += batch;
     }
   }
@@ -471,6 +482,8 @@ class DeviceServer {
     r.req = req_;
     r.rep = rep_;
     r.owner = owner_;
+    r.takers = takers_;
+    r.next_seq = seq_;
     r.ring = ring_;
     r.bar = req_on_device_;
     r.poke = [this] { ensure_running(); };
@@ -478,9 +491,7 @@ class DeviceServer {
   }
 
   // Claim the next sequence number's slot and publish (ringproto.hpp protocol).
-  uint64_t publish(const MsgRecord& m, double timeout_s) {
-    const RingRefs r = refs();
-    const uint64_t seq = seq_->fetch_add(1);
+  void publish(const RingRefs& r, uint64_t seq, const MsgRecord& m, double timeout_s) {
     if (!ring_claim(r, seq, timeout_s))
       throw std::runtime_error("device server: request slot not free in time (left for rescue)");
     const uint32_t idx = (uint32_t)(seq & (ring_ - 1));
@@ -488,7 +499,6 @@ class DeviceServer {
     pub_actor_[idx] = m.actor;  // host-side copies: the ring may be device memory (slow to read back)
     pub_ns_[idx] = t;
     ring_write(r, seq, m, t);
-    return seq;
   }
 
   ReplyRecord wait(uint64_t seq, double timeout_s) {
@@ -628,6 +638,8 @@ class DeviceServer {
   std::atomic<uint64_t> local_seq_{0};
   std::atomic<uint64_t>* seq_ = nullptr;
   std::unique_ptr<std::atomic<uint64_t>[]> owner_mem_;
+  std::unique_ptr<RingTaker[]> takers_mem_;
+  RingTaker* takers_ = nullptr;
   std::atomic<uint64_t>* owner_ = nullptr;
   std::shared_ptr<ShmSegment> seg_;
   std::unique_ptr<FdHandoff> handoff_;

@@ -32,6 +32,7 @@ from .batch import MsgBatch, _handler_ref, fold_step
 from .records import STATUS_NO_ACTOR, STATUS_OK, method_ordered
 
 STAT_NAMES = ("enqueued", "overflow", "no_actor", "processed", "failed", "holes", "serialised")
+SORT_MAX_SHARDS = 1024  # csrc/hip/mailbox.hpp kMboxSortMaxShards
 
 
 def batch_ordered(batch: MsgBatch) -> bool:
@@ -89,18 +90,47 @@ class Mailboxes:
 
     def send(self, batch: MsgBatch, table, state: torch.Tensor | None, out_val: torch.Tensor | None = None,
              out_status: torch.Tensor | None = None, rank_self: int = 0, delay_us: int = 0,
-             ordered: bool | None = None, outbox=None):
-        """World-1 Send through the mailboxes: K2 + K3, replies in message order."""
+             ordered: bool | None = None, outbox=None, sharding: str = "actor", sort: bool | None = None):
+        """World-1 Send through the mailboxes: K2 + K3, replies in message order.
+
+        ``sharding``: ``"actor"`` (every actor's messages in one ring, FIFO in
+        message order) or ``"arrival"`` (a tile's messages in one ring: only for
+        batches without ordered methods).  ``ordered`` (default: whether the batch
+        may carry an ordered method): drain each actor's records one at a time in
+        ring order; otherwise every record runs in parallel.  ``sort`` (default on):
+        the sorted epoch kernels (csrc/hip/mailbox_sort.hip: counting-sort enqueue,
+        16-B records); off: the tagged reservation kernels of mailbox.hip."""
         M = batch.M
         out_val = torch.empty(M, dtype=torch.int64, device=self.device) if out_val is None else out_val
         out_status = torch.empty(M, dtype=torch.int32, device=self.device) if out_status is None else out_status
         if M == 0:
             return out_val, out_status
-        ordered = batch_ordered(batch) if ordered is None else ordered
-        self.enqueue(batch, table, out_val, out_status, rank_self=rank_self, arrival=not ordered)
+        if sharding not in ("actor", "arrival"):
+            raise ValueError("sharding: 'actor' or 'arrival'")
+        ordered = batch_ordered(batch) if ordered is None else bool(ordered)
+        arrival = sharding == "arrival"
+        if arrival and ordered:
+            raise ValueError("arrival sharding cannot serve ordered methods (an actor's messages meet in no one ring)")
         # the rings are empty between Sends, so a uniform batch fixes every queued method
         fixed = int(batch.method) if isinstance(batch.method, int) else 0
-        self.drain(state, out_val, out_status, ordered=ordered, delay_us=delay_us, outbox=outbox, fixed_method=fixed)
+        if sort is None:
+            sort = self.shards <= SORT_MAX_SHARDS
+        if not sort:
+            self.enqueue(batch, table, out_val, out_status, rank_self=rank_self, arrival=arrival)
+            self.drain(state, out_val, out_status, ordered=ordered, delay_us=delay_us, outbox=outbox,
+                       fixed_method=fixed)
+            return out_val, out_status
+        if batch.actor.dtype != torch.int32 or batch.a0.dtype != torch.int64:
+            raise TypeError("MsgBatch: actor must be int32 and a0..a2 int64")
+        uniform = isinstance(batch.method, int)
+        mcol = None if uniform else batch.method.to(torch.int16).contiguous()
+        d, n_dir, affine = table.directory()
+        ob, ob_cap = outbox.view() if outbox is not None else ([], 0)
+        self._m.send_sorted(_ptr(batch.actor), _ptr(batch.a0), _ptr(batch.a1), _ptr(batch.a2), _ptr(mcol),
+                            int(batch.method) if uniform else 0, M, _ptr(table.table), table.cap, _ptr(d), n_dir,
+                            affine, int(rank_self), 0, _ptr(out_val), _ptr(out_status), out_val.numel(), _ptr(state),
+                            0 if state is None else state.numel(), int(delay_us) * 100, ob, ob_cap, arrival, ordered,
+                            fixed, self._stream())
         return out_val, out_status
 
     # ---- persistent consumer ("tell" sessions)

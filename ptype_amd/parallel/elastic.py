@@ -208,14 +208,20 @@ class ElasticDataPlane:
         for attempt in range(max_recoveries + 1):
             try:
                 out = self.send(batch)
-                self._sends += 1
-                if self.replicate_every and self._sends % self.replicate_every == 0:
-                    self.replicate()
-                return out
             except RankFailure:
                 if attempt == max_recoveries:
                     raise
                 self.recover()
+                continue
+            self._sends += 1
+            if self.replicate_every and self._sends % self.replicate_every == 0:
+                try:
+                    self.replicate()
+                except RankFailure:
+                    # the batch WAS delivered: recover the group, never re-send it
+                    # (non-commutative methods would run twice -- ADVICE r2)
+                    self.recover()
+            return out
 
     def replicate(self) -> None:
         """Collective over the current generation: every node sends the blocks

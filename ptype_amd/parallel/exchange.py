@@ -275,9 +275,16 @@ class ActorExchange:
         return self.mailboxes
 
     def _send_mailbox(self, req: B.MsgBatch, out_val, out_status):
-        """World-1 Send through the HBM mailboxes: K2 enqueue + K3 drain."""
+        """World-1 Send through the HBM mailboxes: K2 enqueue (a stable counting sort
+        into the shard rings) + K3 drain (per-actor serial in ring order when the
+        batch may carry ordered methods, else every record in parallel).
+        Actor-sharded rings unless ``mailbox_ordered=False`` promised a batch
+        without ordered methods (then arrival-sharded)."""
+        from ..ops.mailbox import batch_ordered
+
         self._mailboxes().send(req, self.table, self.state, out_val, out_status, rank_self=self.rank,
-                               delay_us=self.delay_us, outbox=self.outbox)
+                               delay_us=self.delay_us, outbox=self.outbox, ordered=batch_ordered(req),
+                               sharding="actor" if self.mailbox_ordered else "arrival")
         return out_val, out_status
 
     def packed_active(self) -> bool:
@@ -556,6 +563,10 @@ class ActorExchange:
         take this exit together -- no count, no host round trip, no agreement."""
         if self.world == 1 and not self.force_collectives and not self._last_mailbox and self.C >= self.max_chunk:
             return True  # one destination whose slot holds a whole chunk: nothing can overflow
+        if self._mailbox_on_receipt():
+            # the slots fit, but K2 on receipt can still answer STATUS_OVERFLOW when a
+            # receiver's rings fill (skewed traffic to one shard): count them (ADVICE r2)
+            return False
         w = self.last_wire
         if not (self.use_engine and w is not None and w.get("adapted")):
             return False

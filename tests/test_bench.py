@@ -47,7 +47,7 @@ def test_bench_json_contract_cpu(nproc, launcher):
     assert out["config"]["global_batch"] == 20000 * nproc
     # headline placement reads the registry mirror; the strided figure is secondary only
     assert out["config"]["placement"] == "random" and out["config"]["registry_lookup"] != "computed (verified strided rule)"
-    assert out["secondary"]["placement"] == "affine"
+    assert out["secondaries"]["affine_placement"]["placement"] == "affine"
     # value is the whole-job aggregate: every rank's messages over the max rank time
     assert out["value"] == pytest.approx(20000 * nproc * 2 / (out["ms_per_step"] * 2 / 1e3), rel=1e-6)
 
