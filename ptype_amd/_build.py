@@ -102,7 +102,7 @@ def build_core(verbose: bool = False, sanitize: str | None = None, out: str | No
     hdr_t = _newest_header(os.path.join(CSRC, "core"))
     cxx = os.environ.get("CXX", "g++")
     flags = [
-        "-std=c++17", "-O2", "-g", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+        "-std=c++17", "-O2", "-g1", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
         "-pthread", "-I" + os.path.join(CSRC, "core"), "-I" + _pybind_include(), "-I" + _py_include(),
     ]
     if sanitize:

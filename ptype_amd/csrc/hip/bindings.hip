@@ -10,6 +10,7 @@
 
 #include "common.hpp"
 #include "engine.hpp"
+#include "exchange_sorted.hpp"
 #include "mailbox.hpp"
 #include "server.hpp"
 
@@ -329,6 +330,45 @@ PYBIND11_MODULE(_hip, m) {
              return d;
            })
       .def("reset_host_profile", &EpochEngine::reset_host_profile);
+  py::class_<SortedExchange>(m, "SortedExchange",
+                             "multi-GPU Send with mailbox delivery: the sender's counting sort by (rank, actor shard) "
+                             "fills the peers' mailboxes directly; see csrc/hip/exchange_sorted.hpp")
+      .def(py::init<int, uintptr_t, int, int, int64_t, int, int64_t, int64_t, std::shared_ptr<FakeComm>>(),
+           py::arg("device"), py::arg("comm"), py::arg("R"), py::arg("rank"), py::arg("max_chunk"), py::arg("chunks"),
+           py::arg("C_alloc"), py::arg("C0"), py::arg("fake") = nullptr)
+      .def(
+          "send",
+          [](SortedExchange& e, uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
+             int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
+             uint32_t affine_w, uintptr_t out_val, uintptr_t out_st, uintptr_t state, uint32_t n_state,
+             uint64_t delay_ticks, bool ordered, uintptr_t stream) {
+            SxSend a;
+            a.actor = actor, a.a0 = a0, a.a1 = a1, a.a2 = a2, a.method_col = method_col;
+            a.method_uniform = method_uniform, a.M = M, a.table = table, a.cap = cap, a.dir = dir, a.n_dir = n_dir;
+            a.affine_w = affine_w, a.out_val = out_val, a.out_st = out_st, a.state = state, a.n_state = n_state;
+            a.delay_ticks = delay_ticks, a.ordered = ordered, a.stream = stream;
+            e.send(a);
+          },
+          py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("method_col"),
+          py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"),
+          py::arg("affine_w"), py::arg("out_val"), py::arg("out_st"), py::arg("state"), py::arg("n_state"),
+          py::arg("delay_ticks"), py::arg("ordered"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())
+      .def("last_wire",
+           [](const SortedExchange& e) {
+             const auto& w = e.last_wire();
+             py::dict d = layout_dict(w.L);
+             d["S"] = w.S;  // as moved (the layout's dwords rounded to a kernel variant)
+             d["req_words"] = w.req_words;
+             d["rep_words"] = w.rep_words;
+             d["C"] = w.C;
+             d["agreed"] = w.agreed;
+             d["spec_from"] = w.spec_from;
+             d["meta"] = std::vector<uint64_t>(w.meta, w.meta + kMetaWords);
+             return d;
+           },
+           "geometry of the last send (per peer and chunk); agreed: from the agreement of Send spec_from")
+      .def("stats", &SortedExchange::stats)
+      .def_property_readonly("sends", &SortedExchange::sends);
   py::class_<Mailboxes>(m, "Mailboxes",
                         "HBM actor mailboxes: S shard rings of Q 32-B tagged records (K2 enqueue, K3 epoch drain, "
                         "K3 persistent consumer); see csrc/hip/mailbox.hpp")

@@ -137,7 +137,7 @@ using engine_detail::kNcclUint64;
 // would take at that per-rank egress bandwidth, so chunk-pipelining choices can
 // be compared against an xGMI-like all-to-all (compute contention from RCCL's
 // own kernels is not modelled).
-__global__ void fake_link_kernel(uint64_t ticks) {
+static __global__ void fake_link_kernel(uint64_t ticks) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
 }
@@ -147,7 +147,7 @@ __global__ void fake_link_kernel(uint64_t ticks) {
 struct RegionSizes {
   uint32_t n[64];
 };
-__global__ __launch_bounds__(256) void fake_copy_regions_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+static __global__ __launch_bounds__(256) void fake_copy_regions_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                                 size_t stride16, RegionSizes sz) {
   const uint32_t q = blockIdx.y, n16 = sz.n[q] / 16;
   const uint4* s = src + (size_t)q * stride16;

@@ -1,0 +1,801 @@
+// Sorted exchange (design: exchange_sorted.hpp).
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "exchange_sorted.hpp"
+#include "mailbox.hpp"
+#include "mailbox_dev.hpp"
+#include "sort_common.hpp"
+
+namespace ptype {
+
+namespace {
+constexpr int kXOrdThreads = 512;  // receiver ordered drain: one block per wire shard, one bin per thread
+constexpr int kXOrdK = 4;
+constexpr int kXOrdWin = kXOrdThreads * kXOrdK;
+constexpr int kXOrdWaves = kXOrdThreads / kWave;
+constexpr uint32_t kXOrdStateMax = 4096;
+constexpr int kXDispU = 4;
+constexpr int kXMaxBuckets = kSxMaxRanks * kSxShards;
+}  // namespace
+
+// ---------------------------------------------------------------- layout
+PackedLayout sx_layout(const uint64_t* meta) {
+  uint64_t m[kMetaWords];
+  std::copy(meta, meta + kMetaWords, m);
+  m[kMetaMbox] = meta[kMetaMbox] + 1;  // one more value: all-ones is the null record
+  return packed_layout(m);
+}
+
+static int sx_round_S(int S) { return S <= 4 ? S : S <= 6 ? 6 : 8; }
+
+// A field fits the layout in force (the mailbox all-ones value is reserved).
+__device__ __forceinline__ bool sx_fits(const PackedLayout& L, uint32_t meth, uint32_t hdr_method, uint32_t mb,
+                                        uint64_t z0, uint64_t z1, uint64_t z2) {
+  auto fits = [&](int q, uint64_t v) { return L.w[q] >= 64 || (v >> L.w[q]) == 0; };
+  if (L.w[0] ? !fits(0, meth) : meth != hdr_method) return false;
+  if (L.w[1] == 0 || (uint64_t)mb >= low_mask(L.w[1])) return false;
+  return fits(2, z0) && fits(3, z1) && fits(4, z2);
+}
+
+// Whether the received regions of a chunk may hold ordered methods: a method
+// column on the wire, or a sender whose uniform method is ordered.
+__device__ __forceinline__ bool sx_need_order(const uint32_t* recv, int64_t req_stride, int R, const PackedLayout& L) {
+  if (L.w[0]) return true;
+  for (int p = 0; p < R; ++p) {
+    const uint32_t hw = recv[(int64_t)p * req_stride + 3];
+    if (((hw >> 16) & kFlagValid) && recv[(int64_t)p * req_stride] && method_ordered(hw & 0xffffu)) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t t = (uint32_t)__shfl_xor((int)v, off);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------- sender: count
+template <int MODE>
+__global__ __launch_bounds__(kST) void sx_count_kernel(SortIn in, int R, uint32_t* __restrict__ hist,
+                                                       unsigned long long* __restrict__ meta) {
+  __shared__ uint32_t cnt[kXMaxBuckets];
+  __shared__ uint32_t mbmax_s;
+  const uint32_t B = (uint32_t)R * kSxShards;
+  const uint32_t v = virt_block(blockIdx.x, in.G);
+  for (uint32_t b = threadIdx.x; b < B; b += kST) cnt[b] = 0;
+  if (threadIdx.x == 0) mbmax_s = 0;
+  __syncthreads();
+  uint32_t mbmax = 0;
+  const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
+  uint32_t a[kSK];
+  if (t0 < t1) load_actors(in, t0, a);
+  for (uint32_t t = t0; t < t1; ++t) {
+    int r[kSK];
+    uint32_t mb[kSK];
+    resolve_k<MODE>(in, a, r, mb);
+    if (t + 1 < t1) load_actors(in, t + 1, a);
+#pragma unroll
+    for (int k = 0; k < kSK; ++k)
+      if (r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox) {
+        atomicAdd(&cnt[(uint32_t)r[k] * kSxShards + (mb[k] & (kSxShards - 1))], 1u);
+        mbmax = mb[k] > mbmax ? mb[k] : mbmax;
+      }
+  }
+  mbmax = wave_max(mbmax);
+  if (lane_id() == 0 && mbmax) atomicMax(&mbmax_s, mbmax);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < B; b += kST) hist[(size_t)v * B + b] = cnt[b];
+  if (threadIdx.x == 0 && mbmax_s) meta_max(meta + kMetaMbox, mbmax_s);
+}
+
+// ---------------------------------------------------------------- sender: scan + region tables
+// Block d owns region d's 64 shard columns of hist [G][R * 64]: exclusive prefix
+// over blocks (in place), then the shard offsets within the region, its shard
+// table (clamped to C) and header, and the region total into meta[kMetaCap].
+__global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hist, uint32_t G, int R,
+                                                       uint32_t* __restrict__ sendbuf, int64_t req_stride,
+                                                       int64_t tab_off, uint32_t C, uint32_t method_uniform,
+                                                       uint32_t hdr_flags, int rank_self,
+                                                       unsigned long long* __restrict__ meta,
+                                                       uint32_t* __restrict__ boff) {
+  __shared__ uint32_t part[16][64];
+  const uint32_t B = (uint32_t)R * kSxShards;
+  const uint32_t lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const uint32_t d = blockIdx.x, c = d * kSxShards + lane;
+  const uint32_t rows = (G + 15) / 16, r0 = min(G, g * rows), r1 = min(G, r0 + rows);
+  uint32_t sum = 0;
+  {
+    uint32_t r = r0;
+    for (; r + 8 <= r1; r += 8) {
+      uint32_t x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = hist[(size_t)(r + j) * B + c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += x[j];
+    }
+    for (; r < r1; ++r) sum += hist[(size_t)r * B + c];
+  }
+  part[g][lane] = sum;
+  __syncthreads();
+  uint32_t run = 0, total = 0;
+  for (uint32_t j = 0; j < 16; ++j) {
+    if (j < g) run += part[j][lane];
+    total += part[j][lane];
+  }
+  for (uint32_t r = r0; r < r1; ++r) {
+    const uint32_t x = hist[(size_t)r * B + c];
+    hist[(size_t)r * B + c] = run;
+    run += x;
+  }
+  if (g == 0) {
+    const uint32_t inc = wave_incl_scan(total);
+    const uint32_t off = inc - total;
+    const uint32_t all = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    boff[c] = off;
+    uint32_t* region = sendbuf + (int64_t)d * req_stride;
+    region[tab_off + lane] = off < C ? off : C;
+    if (lane == 0) {
+      const uint32_t n = all < C ? all : C;
+      region[tab_off + kSxShards] = n;
+      *reinterpret_cast<uint4*>(region) = make_uint4(n, all, (uint32_t)rank_self, (hdr_flags << 16) | method_uniform);
+      if (all) meta_max(meta + kMetaCap, all);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- sender: scatter
+template <int MODE, int S>
+__global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, const uint32_t* __restrict__ hist,
+                                                         const uint32_t* __restrict__ boff,
+                                                         uint32_t* __restrict__ sendbuf, int64_t req_stride,
+                                                         uint32_t C, PackedLayout L, int32_t* __restrict__ perm,
+                                                         unsigned long long* __restrict__ meta) {
+  __shared__ uint32_t run[kXMaxBuckets];
+  __shared__ uint32_t bo[kXMaxBuckets];
+  __shared__ uint32_t wcnt[kST / kWave][kXMaxBuckets];
+  const uint32_t B = (uint32_t)R * kSxShards;
+  const uint32_t bbits = 32 - __builtin_clz(B - 1);  // bucket index bits (B >= 64)
+  const uint32_t v = virt_block(blockIdx.x, in.G);
+  const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  for (uint32_t b = threadIdx.x; b < B; b += kST) {
+    run[b] = hist[(size_t)v * B + b];
+    bo[b] = boff[b];
+  }
+  MetaAcc acc;
+  const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
+  SortTileIn x;
+  if (t0 < t1) load_args(in, t0, x);
+  for (uint32_t t = t0; t < t1; ++t) {
+    for (uint32_t b = lane; b < B; b += kWave) wcnt[w][b] = 0;
+    int r[kSK];
+    uint32_t mb[kSK];
+    resolve_k<MODE>(in, x.a, r, mb);
+    int64_t v0[kSK], v1[kSK], v2[kSK];
+    uint32_t meth[kSK];
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      v0[k] = x.x0[k], v1[k] = x.x1[k], v2[k] = x.x2[k];
+      const int64_t i = tile_index(t, k);
+      meth[k] = in.mcol && i < in.M ? (uint32_t)in.mcol[i] : in.method_uniform;
+    }
+    if (t + 1 < t1) load_args(in, t + 1, x);
+    uint32_t wr[kSK], bk[kSK];
+    bool ok[kSK];
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      ok[k] = r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
+      bk[k] = ok[k] ? (uint32_t)r[k] * kSxShards + (mb[k] & (kSxShards - 1)) : 0u;
+      if (ok[k]) {
+        const uint64_t z0 = zz_enc(v0[k]), z1 = zz_enc(v1[k]), z2 = zz_enc(v2[k]);
+        acc.z0 = z0 > acc.z0 ? z0 : acc.z0;
+        acc.z1 = z1 > acc.z1 ? z1 : acc.z1;
+        acc.z2 = z2 > acc.z2 ? z2 : acc.z2;
+        acc.mm = meth[k] > acc.mm ? meth[k] : acc.mm;
+        acc.flags |= 1u << (meth[k] < 7 ? meth[k] : 7);
+      }
+      const uint64_t peers = match_bits(bk[k], bbits, __ballot(ok[k]));
+      const unsigned below = mbcnt64(peers);
+      const int leader = peers ? __builtin_ctzll(peers) : 0;
+      unsigned old = 0;
+      if (ok[k] && below == 0) {
+        old = wcnt[w][bk[k]];
+        wcnt[w][bk[k]] = old + (unsigned)__popcll(peers);
+      }
+      wr[k] = (unsigned)__shfl((int)old, leader) + below;
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < B; b += kST) {
+      uint32_t rr = run[b];
+#pragma unroll
+      for (int ww = 0; ww < kST / kWave; ++ww) {
+        const uint32_t c = wcnt[ww][b];
+        wcnt[ww][b] = rr;
+        rr += c;
+      }
+      run[b] = rr;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      const int64_t i = tile_index(t, k);
+      if (i >= in.M) continue;
+      if (!ok[k]) {
+        perm[i] = -2;  // no such actor: the completion answers kStatusNoActor
+        continue;
+      }
+      const uint32_t pos = bo[bk[k]] + wcnt[w][bk[k]] + wr[k];
+      if (pos >= C) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
+        perm[i] = -1;
+        continue;
+      }
+      const uint64_t z0 = zz_enc(v0[k]), z1 = zz_enc(v1[k]), z2 = zz_enc(v2[k]);
+      uint64_t f[5];
+      const bool fit = sx_fits(L, meth[k], in.method_uniform, mb[k], z0, z1, z2);
+      if (fit) {
+        f[0] = meth[k], f[1] = mb[k], f[2] = z0, f[3] = z1, f[4] = z2;
+        perm[i] = (int32_t)((uint32_t)r[k] * C + pos);
+      } else {  // wider than the layout in force: a null record holds the slot
+        f[0] = 0, f[1] = low_mask(L.w[1]), f[2] = 0, f[3] = 0, f[4] = 0;
+        perm[i] = -1;
+      }
+      uint32_t rec[S];
+      packed_pack<S>(L, f, rec);
+      store_words<S>(sendbuf + (int64_t)r[k] * req_stride + 4 + (int64_t)pos * S, rec);
+    }
+    __syncthreads();
+  }
+  acc.mb = 0;  // the count pass folds the mailboxes
+  meta_publish(acc, in.mcol != nullptr, in.method_uniform, in.M, meta);
+}
+
+// ---------------------------------------------------------------- receiver: parallel drain
+// grid (X, R): block (x, p) strides over source p's region in 64-record groups
+// per wave; a reply lands at its request's position (one ok-bitmap word per group).
+template <int S, int FIXED>
+__device__ __forceinline__ unsigned long long sx_drain_range(const uint32_t* rq, int64_t count, uint32_t hm,
+                                                             const PackedLayout& L, uint8_t* vals,
+                                                             unsigned long long* okmap, int64_t* state,
+                                                             uint32_t n_state, uint64_t delay_ticks,
+                                                             unsigned long long& toowide) {
+  unsigned long long failed = 0;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  const unsigned lane = lane_id();
+  const uint64_t null_mb = low_mask(L.w[1]);
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~(kWave - 1)); base < count;
+       base += step * kXDispU) {
+    uint32_t wv[kXDispU][S];
+#pragma unroll
+    for (int u = 0; u < kXDispU; ++u) {
+      const int64_t s = base + u * step + lane;
+      if (s < count) load_words<S>(rq + 4 + s * S, wv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kXDispU; ++u) {
+      const int64_t gb = base + u * step;
+      if (gb >= count) break;
+      const int64_t s = gb + lane;
+      const bool in = s < count;
+      ReplyRecord rr;
+      rr.value = 0;
+      rr.status = kStatusOk;
+      bool null = false;
+      if (in) {
+        const uint64_t mbf = packed_field<S>(L, 1, wv[u]);
+        null = mbf == null_mb;
+        if (!null) {
+          MsgRecord m;
+          m.actor = (uint32_t)mbf;
+          m.method = (uint16_t)(FIXED ? FIXED : (L.w[0] ? (uint32_t)packed_field<S>(L, 0, wv[u]) : hm));
+          m.flags = kFlagValid | kFlagRouted;
+          m.a0 = zz_dec(packed_field<S>(L, 2, wv[u]));
+          m.a1 = zz_dec(packed_field<S>(L, 3, wv[u]));
+          m.a2 = zz_dec(packed_field<S>(L, 4, wv[u]));
+          rr = run_handler(m, state, n_state, delay_ticks);
+        } else {
+          rr.status = kStatusOverflow;  // nobody reads it: the sender answered this one itself
+        }
+      }
+      bool ok = rr.status == kStatusOk;
+      uint64_t code = ok ? (L.vb == 8 ? (uint64_t)rr.value : zz_enc(rr.value)) : (uint64_t)rr.status;
+      if (ok && L.vb < 8 && (code >> (8 * L.vb))) {  // impossible under the agreed bounds: fail loudly
+        ok = false;
+        code = kStatusFailed;
+        toowide += in;
+      }
+      failed += in && !ok && !null;
+      const unsigned long long bits = __ballot(in && ok);
+      if (in) {
+        switch (L.vb) {
+          case 1: vals[s] = (uint8_t)code; break;
+          case 2: reinterpret_cast<uint16_t*>(vals)[s] = (uint16_t)code; break;
+          case 4: reinterpret_cast<uint32_t*>(vals)[s] = (uint32_t)code; break;
+          default: reinterpret_cast<uint64_t*>(vals)[s] = code;
+        }
+      }
+      if (lane == 0) okmap[gb / kWave] = bits;
+    }
+  }
+  return failed;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void sx_drain_par_kernel(const uint32_t* __restrict__ recv, int64_t req_stride,
+                                                           int64_t C, PackedLayout L, int R, bool may_order,
+                                                           uint32_t* __restrict__ reply, int64_t rep_stride,
+                                                           int64_t* __restrict__ state, uint32_t n_state,
+                                                           uint64_t delay_ticks, unsigned long long* __restrict__ stats) {
+  if (may_order && sx_need_order(recv, req_stride, R, L)) return;  // the ordered drain serves this chunk
+  const int p = blockIdx.y;
+  const uint32_t* rq = recv + (int64_t)p * req_stride;
+  const uint4 h = *reinterpret_cast<const uint4*>(rq);
+  const int64_t count = ((h.w >> 16) & kFlagValid) ? (int64_t)(h.x < C ? h.x : C) : 0;
+  const uint32_t hm = h.w & 0xffffu;
+  uint32_t* rp = reply + (int64_t)p * rep_stride;
+  unsigned long long* okmap = reinterpret_cast<unsigned long long*>(rp + 4);
+  uint8_t* vals = reinterpret_cast<uint8_t*>(rp + 4 + packed_ok_words(count));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
+  unsigned long long toowide = 0, failed;
+  if (!L.w[0] && hm == kCalculatorMultiply)
+    failed = sx_drain_range<S, kCalculatorMultiply>(rq, count, hm, L, vals, okmap, state, n_state, delay_ticks, toowide);
+  else
+    failed = sx_drain_range<S, 0>(rq, count, hm, L, vals, okmap, state, n_state, delay_ticks, toowide);
+  for (int off = 32; off > 0; off >>= 1) {
+    failed += __shfl_xor(failed, off);
+    toowide += __shfl_xor(toowide, off);
+  }
+  if (lane_id() == 0 && failed) atomicAdd(&stats[0], failed);
+  if (lane_id() == 0 && toowide) atomicAdd(&stats[1], toowide);
+}
+
+// ---------------------------------------------------------------- receiver: ordered drain
+// Reply headers and zeroed ok bitmaps first (the ordered drain sets ok bits one
+// record at a time).  grid R.
+__global__ __launch_bounds__(256) void sx_reply_init_kernel(const uint32_t* __restrict__ recv, int64_t req_stride,
+                                                            int64_t C, PackedLayout L, int R,
+                                                            uint32_t* __restrict__ reply, int64_t rep_stride) {
+  if (!sx_need_order(recv, req_stride, R, L)) return;
+  const int p = blockIdx.x;
+  const uint4 h = *reinterpret_cast<const uint4*>(recv + (int64_t)p * req_stride);
+  const int64_t count = ((h.w >> 16) & kFlagValid) ? (int64_t)(h.x < C ? h.x : C) : 0;
+  uint32_t* rp = reply + (int64_t)p * rep_stride;
+  if (threadIdx.x == 0) *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
+  for (int64_t j = threadIdx.x; j < packed_ok_words(count); j += blockDim.x) rp[4 + j] = 0u;
+}
+
+struct SxOrdLds {
+  uint32_t wcnt[kXOrdWaves][kXOrdThreads];
+  uint32_t bstart[kXOrdThreads];
+  uint32_t bcount[kXOrdThreads];
+  uint32_t wsum[kXOrdWaves];
+  uint32_t pos[kXOrdWin];
+  uint32_t act[kXOrdWin];
+  uint32_t meth[kXOrdWin];
+  int64_t a0[kXOrdWin], a1[kXOrdWin], a2[kXOrdWin];
+};
+
+template <int S>
+__global__ __launch_bounds__(kXOrdThreads) void sx_drain_ord_kernel(const uint32_t* __restrict__ recv,
+                                                                    int64_t req_stride, int64_t tab_off, int64_t C,
+                                                                    PackedLayout L, int R,
+                                                                    uint32_t* __restrict__ reply, int64_t rep_stride,
+                                                                    int64_t* __restrict__ state, uint32_t n_state,
+                                                                    uint64_t delay_ticks,
+                                                                    unsigned long long* __restrict__ stats) {
+  if (!sx_need_order(recv, req_stride, R, L)) return;
+  extern __shared__ __align__(16) unsigned char smem_sx[];
+  SxOrdLds& Ls = *reinterpret_cast<SxOrdLds*>(smem_sx);
+  int64_t* st_lds = reinterpret_cast<int64_t*>(smem_sx + sizeof(SxOrdLds));
+  const uint32_t s = blockIdx.x;
+  const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t n_loc = (state && s < n_state) ? (n_state - 1 - s) / kSxShards + 1 : 0;
+  const bool in_lds = state && n_loc <= kXOrdStateMax;
+  if (in_lds)
+    for (uint32_t j = threadIdx.x; j < n_loc; j += kXOrdThreads) st_lds[j] = state[s + (uint64_t)j * kSxShards];
+  __syncthreads();
+  const uint64_t null_mb = low_mask(L.w[1]);
+  unsigned long long failed = 0;
+  for (int p = 0; p < R; ++p) {  // source-rank order: every (sender, actor) pair stays FIFO
+    const uint32_t* rq = recv + (int64_t)p * req_stride;
+    const uint4 h = *reinterpret_cast<const uint4*>(rq);
+    if (!((h.w >> 16) & kFlagValid)) continue;
+    const int64_t count = (int64_t)(h.x < C ? h.x : C);
+    const uint32_t hm = h.w & 0xffffu;
+    const uint32_t lo = min((int64_t)rq[tab_off + s], count), hi = min((int64_t)rq[tab_off + s + 1], count);
+    uint32_t* rp = reply + (int64_t)p * rep_stride;
+    unsigned long long* okmap = reinterpret_cast<unsigned long long*>(rp + 4);
+    uint8_t* vals = reinterpret_cast<uint8_t*>(rp + 4 + packed_ok_words(count));
+    for (uint32_t w0 = lo; w0 < hi; w0 += kXOrdWin) {
+      for (uint32_t b = lane; b < kXOrdThreads; b += kWave) Ls.wcnt[w][b] = 0;
+      uint32_t q[kXOrdK], bin[kXOrdK], wr[kXOrdK], mbv[kXOrdK], mv[kXOrdK];
+      int64_t x0[kXOrdK], x1[kXOrdK], x2[kXOrdK];
+      bool valid[kXOrdK];
+#pragma unroll
+      for (int k = 0; k < kXOrdK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
+        q[k] = w0 + w * (kWave * kXOrdK) + k * kWave + lane;
+        valid[k] = q[k] < hi;
+        uint32_t rec[S];
+        if (valid[k]) {
+          load_words<S>(rq + 4 + (int64_t)q[k] * S, rec);
+          const uint64_t mbf = packed_field<S>(L, 1, rec);
+          valid[k] = mbf != null_mb;
+          mbv[k] = (uint32_t)mbf;
+          mv[k] = L.w[0] ? (uint32_t)packed_field<S>(L, 0, rec) : hm;
+          x0[k] = zz_dec(packed_field<S>(L, 2, rec));
+          x1[k] = zz_dec(packed_field<S>(L, 3, rec));
+          x2[k] = zz_dec(packed_field<S>(L, 4, rec));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kXOrdK; ++k) {
+        bin[k] = valid[k] ? (mbv[k] >> kSxShardBits) & (kXOrdThreads - 1) : 0u;
+        const uint64_t peers = match_bits(bin[k], 9, __ballot(valid[k]));
+        const unsigned below = mbcnt64(peers);
+        const int leader = peers ? __builtin_ctzll(peers) : 0;
+        unsigned old = 0;
+        if (valid[k] && below == 0) {
+          old = Ls.wcnt[w][bin[k]];
+          Ls.wcnt[w][bin[k]] = old + (unsigned)__popcll(peers);
+        }
+        wr[k] = (unsigned)__shfl((int)old, leader) + below;
+      }
+      __syncthreads();
+      {
+        const unsigned b = threadIdx.x;
+        unsigned r = 0;
+#pragma unroll
+        for (int ww = 0; ww < kXOrdWaves; ++ww) {
+          const unsigned c = Ls.wcnt[ww][b];
+          Ls.wcnt[ww][b] = r;
+          r += c;
+        }
+        Ls.bcount[b] = r;
+        const unsigned inc = wave_incl_scan(r);
+        if (lane == kWave - 1) Ls.wsum[w] = inc;
+        __syncthreads();
+        unsigned off = inc - r;
+        for (unsigned ww = 0; ww < w; ++ww) off += Ls.wsum[ww];
+        Ls.bstart[b] = off;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kXOrdK; ++k) {
+        if (!valid[k]) continue;
+        const unsigned d = Ls.bstart[bin[k]] + Ls.wcnt[w][bin[k]] + wr[k];
+        Ls.pos[d] = q[k];
+        Ls.act[d] = in_lds ? (mbv[k] >> kSxShardBits) : mbv[k];
+        Ls.meth[d] = mv[k];
+        Ls.a0[d] = x0[k];
+        Ls.a1[d] = x1[k];
+        Ls.a2[d] = x2[k];
+      }
+      __syncthreads();
+      {
+        const unsigned b = threadIdx.x, e = Ls.bstart[b] + Ls.bcount[b];
+        int64_t* st = in_lds ? st_lds : state;
+        const uint32_t nst = in_lds ? n_loc : n_state;
+        for (unsigned d = Ls.bstart[b]; d < e; ++d) {
+          MsgRecord m;
+          m.actor = Ls.act[d];
+          m.method = (uint16_t)Ls.meth[d];
+          m.flags = kFlagValid | kFlagRouted;
+          m.a0 = Ls.a0[d], m.a1 = Ls.a1[d], m.a2 = Ls.a2[d];
+          const ReplyRecord rr = run_handler(m, st, nst, delay_ticks, OutboxView(), true);
+          bool ok = rr.status == kStatusOk;
+          uint64_t code = ok ? (L.vb == 8 ? (uint64_t)rr.value : zz_enc(rr.value)) : (uint64_t)rr.status;
+          if (ok && L.vb < 8 && (code >> (8 * L.vb))) {
+            ok = false;
+            code = kStatusFailed;
+          }
+          failed += !ok;
+          const uint32_t qq = Ls.pos[d];
+          switch (L.vb) {
+            case 1: vals[qq] = (uint8_t)code; break;
+            case 2: reinterpret_cast<uint16_t*>(vals)[qq] = (uint16_t)code; break;
+            case 4: reinterpret_cast<uint32_t*>(vals)[qq] = (uint32_t)code; break;
+            default: reinterpret_cast<uint64_t*>(vals)[qq] = code;
+          }
+          if (ok) atomicOr(&okmap[qq / kWave], 1ull << (qq % kWave));
+          if (!in_lds) vm_drain();
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (in_lds)
+    for (uint32_t j = threadIdx.x; j < n_loc; j += kXOrdThreads) state[s + (uint64_t)j * kSxShards] = st_lds[j];
+  for (int off = 32; off > 0; off >>= 1) failed += __shfl_xor(failed, off);
+  if (lane_id() == 0 && failed) atomicAdd(&stats[0], failed);
+}
+
+// ---------------------------------------------------------------- host
+SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int64_t max_chunk, int chunks,
+                               int64_t C_alloc, int64_t C0, std::shared_ptr<FakeComm> fake)
+    : device_(device), comm_((void*)comm), fake_(std::move(fake)), R_(R), rank_(rank), chunks_(chunks),
+      max_chunk_(max_chunk), C_alloc_(C_alloc) {
+  if (R < 1 || R > kSxMaxRanks) throw std::invalid_argument("SortedExchange: 1 <= ranks <= 16");
+  if (chunks < 1 || chunks > kSxMaxChunks) throw std::invalid_argument("SortedExchange: 1 <= chunks <= 4");
+  if (max_chunk < 1 || C_alloc < 64 || C0 < 1 || C0 > C_alloc) throw std::invalid_argument("SortedExchange: geometry");
+  if (C_alloc > 0x7fffffff / R) throw std::invalid_argument("SortedExchange: R * C must fit an int32 position");
+  if (fake_ && (comm_ || fake_->size() != R || rank < 0 || rank >= R))
+    throw std::invalid_argument("SortedExchange: fake communicator must match R and replace comm");
+  if (!fake_ && !comm_) throw std::invalid_argument("SortedExchange: needs a communicator (RCCL or FakeComm)");
+  if (comm_ && (!rccl().alltoall || !rccl().allreduce))
+    throw std::runtime_error("SortedExchange: RCCL entry points not found in the process");
+  PT_HIP_CHECK(hipSetDevice(device_));
+  int lo = 0, hi = 0;
+  PT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  PT_HIP_CHECK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));
+  const int64_t rq = packed_req_words(C_alloc, 8) + kSxTableWords, rp = packed_rep_words(C_alloc, 8);
+  for (int i = 0; i < chunks_; ++i) {
+    Bufs& b = bufs_[i];
+    PT_HIP_CHECK(hipMalloc(&b.send, (size_t)R * rq * 4));
+    PT_HIP_CHECK(hipMalloc(&b.recv, (size_t)R * rq * 4));
+    PT_HIP_CHECK(hipMalloc(&b.reply, (size_t)R * rp * 4));
+    PT_HIP_CHECK(hipMalloc(&b.back, (size_t)R * rp * 4));
+    PT_HIP_CHECK(hipMalloc(&b.perm, (size_t)max_chunk * 4));
+    for (hipEvent_t* e : {&ev_routed_[i], &ev_req_in_[i], &ev_served_[i], &ev_rep_in_[i]})
+      PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  PT_HIP_CHECK(hipMalloc(&hist_, (size_t)kMboxSortHistWords * 4));
+  PT_HIP_CHECK(hipMalloc(&boff_, (size_t)kXMaxBuckets * 4));
+  PT_HIP_CHECK(hipMalloc(&meta_dev_, 2 * kMetaWords * sizeof(uint64_t)));
+  PT_HIP_CHECK(hipMemset(meta_dev_, 0, 2 * kMetaWords * sizeof(uint64_t)));
+  PT_HIP_CHECK(hipMalloc(&stats_, 2 * sizeof(unsigned long long)));
+  PT_HIP_CHECK(hipMemset(stats_, 0, 2 * sizeof(unsigned long long)));
+  PT_HIP_CHECK(hipHostMalloc(&meta_host_, 2 * kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
+  memset(meta_host_, 0, 2 * kMetaWords * sizeof(uint64_t));
+  for (auto& e : ev_meta_) PT_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // start-up layout: every column at full width (8-dword records, 8-byte replies)
+  uint64_t wide[kMetaWords] = {};
+  wide[kMetaMbox] = kMaxMbox - 2;
+  for (int j = 0; j < 3; ++j) wide[kMetaArg0 + j] = ~0ull;
+  wide[kMetaMethod] = 0xffff;
+  wide[kMetaMcol] = 1;
+  for (int m = 0; m < 8; ++m) wide[kMetaFlags + m] = 1;
+  L_ = sx_layout(wide);
+  C_ = C0;
+}
+
+SortedExchange::~SortedExchange() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
+  (void)hipSetDevice(device_);
+  for (int i = 0; i < chunks_; ++i) {
+    Bufs& b = bufs_[i];
+    for (void* p : {(void*)b.send, (void*)b.recv, (void*)b.reply, (void*)b.back, (void*)b.perm}) (void)hipFree(p);
+    for (hipEvent_t e : {ev_routed_[i], ev_req_in_[i], ev_served_[i], ev_rep_in_[i]}) (void)hipEventDestroy(e);
+  }
+  for (hipEvent_t e : ev_meta_) (void)hipEventDestroy(e);
+  (void)hipFree(hist_);
+  (void)hipFree(boff_);
+  (void)hipFree(meta_dev_);
+  (void)hipFree(stats_);
+  (void)hipHostFree(meta_host_);
+  (void)hipStreamDestroy(comm_stream_);
+}
+
+std::vector<uint64_t> SortedExchange::stats() const {
+  unsigned long long h[2] = {0, 0};
+  PT_HIP_CHECK(hipMemcpy(h, stats_, sizeof h, hipMemcpyDeviceToHost));
+  return {h[0], h[1]};
+}
+
+void SortedExchange::adopt(const uint64_t* meta, int64_t from) {
+  L_ = sx_layout(meta);
+  const double need = (double)meta[kMetaCap];
+  // the busiest bucket two Sends ago plus 1 % and 8 sigma: uniform traffic then
+  // overflows with probability ~1e-15 per bucket, and skewed traffic that is
+  // stable over a few Sends fits as well
+  int64_t c = (int64_t)(need * 1.01 + 8.0 * sqrt(need) + 64.0);
+  c = ((c + 63) / 64) * 64;
+  C_ = std::max<int64_t>(64, std::min<int64_t>(c, C_alloc_));
+  agreed_ = true;
+  spec_from_ = from;
+  std::copy(meta, meta + kMetaWords, spec_meta_);
+}
+
+void SortedExchange::pick_spec(hipStream_t cs) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(cs, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) return;
+  // Send k uses the agreement of Send k - 2 (a fixed lag: every rank derives
+  // the same geometry); it has normally completed long ago
+  const int64_t want = sends_ - 2;
+  if (want < 0) return;
+  const int j = (int)(want & 1);
+  if (meta_send_[j] != want) return;  // recorded under a graph capture: keep the layout in force
+  PT_HIP_CHECK(hipEventSynchronize(ev_meta_[j]));
+  adopt(meta_host_ + j * kMetaWords, want);
+}
+
+void SortedExchange::a2a(const void* src, void* dst, size_t bytes_per_peer) {
+  if (fake_) {
+    fake_->alltoall(rank_, src, dst, bytes_per_peer, comm_stream_);
+    return;
+  }
+  const int rc = rccl().alltoall(src, dst, bytes_per_peer, kNcclInt8, comm_, comm_stream_);
+  if (rc != 0)
+    throw std::runtime_error(std::string("ncclAllToAll failed: ") + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+}
+
+void SortedExchange::allreduce_meta(uint64_t* dev, hipStream_t s) {
+  if (fake_) {
+    fake_->allreduce_max(rank_, dev, kMetaWords, s);
+    return;
+  }
+  const int rc = rccl().allreduce(dev, dev, kMetaWords, kNcclUint64, kNcclMax, comm_, s);
+  if (rc != 0)
+    throw std::runtime_error(std::string("ncclAllReduce failed: ") + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+}
+
+void SortedExchange::send(const SxSend& a) {
+  if (a.M < 0 || a.M > max_chunk_ * chunks_) throw std::invalid_argument("SortedExchange: batch exceeds max_batch");
+  if (a.M > 0 && (!a.actor || !a.a0)) throw std::invalid_argument("SortedExchange: actor and a0 columns required");
+  if (a.cap == 0 || (a.cap & (a.cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
+  PT_HIP_CHECK(hipSetDevice(device_));
+  const hipStream_t cs = as_stream(a.stream);
+  pick_spec(cs);
+  hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(cs, &capst) == hipSuccess && capst != hipStreamCaptureStatusNone;
+  const PackedLayout L = L_;
+  const int S = sx_round_S(L.S);
+  const int64_t C = C_;
+  const int64_t tab_off = packed_req_words(C, S);
+  const int64_t rq = tab_off + kSxTableWords, rp = packed_rep_words(C, L.vb);
+  wire_ = SxWire();
+  wire_.L = L;
+  wire_.S = S;
+  wire_.C = C;
+  wire_.req_words = rq;
+  wire_.rep_words = rp;
+  wire_.agreed = agreed_;
+  wire_.spec_from = spec_from_;
+  std::copy(spec_meta_, spec_meta_ + kMetaWords, wire_.meta);
+  const int cur = (int)(sends_ & 1);
+  uint64_t* meta = meta_dev_ + cur * kMetaWords;
+  PT_HIP_CHECK(hipMemsetAsync(meta, 0, kMetaWords * sizeof(uint64_t), cs));
+  const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
+  const uint32_t B = (uint32_t)R_ * kSxShards;
+  const bool may_order = a.ordered;
+  auto chunk_in = [&](int i, int64_t& lo, int64_t& m) {
+    lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
+    m = std::min<int64_t>(a.M, lo + max_chunk_) - lo;
+    SortIn in{};
+    auto off = [](uintptr_t p, int64_t e, int64_t sz) { return p ? p + (uintptr_t)(e * sz) : (uintptr_t)0; };
+    in.actor = (const uint32_t*)off(a.actor, lo, 4);
+    in.a0 = (const int64_t*)off(a.a0, lo, 8);
+    in.a1 = (const int64_t*)off(a.a1, lo, 8);
+    in.a2 = (const int64_t*)off(a.a2, lo, 8);
+    in.mcol = (const uint16_t*)off(a.method_col, lo, 2);
+    in.method_uniform = (uint32_t)a.method_uniform;
+    in.M = m;
+    in.table = (const TableEntry*)a.table;
+    in.mask = a.cap - 1;
+    in.dir = (const uint32_t*)a.dir;
+    in.n_dir = a.n_dir;
+    in.aw = a.affine_w;
+    in.aw_shift = (a.affine_w && (a.affine_w & (a.affine_w - 1)) == 0) ? __builtin_ctz(a.affine_w) : -1;
+    in.rank_self = rank_;
+    const int64_t tiles = (m + kSTile - 1) / kSTile;
+    int64_t G = std::min<int64_t>({std::max<int64_t>(tiles, 1), (int64_t)(kMboxSortHistWords / B), 1024});
+    if (G >= 8) G -= G % 8;
+    in.G = (uint32_t)std::max<int64_t>(G, 1);
+    in.tiles = (uint32_t)tiles;
+    in.tpb = (uint32_t)((tiles + in.G - 1) / in.G);
+    return in;
+  };
+  auto serve = [&](int i) {
+    Bufs& b = bufs_[i];
+    PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_req_in_[i], 0));
+    if (may_order) {
+      hipLaunchKernelGGL(sx_reply_init_kernel, dim3(R_), dim3(256), 0, cs, (const uint32_t*)b.recv, rq, C, L, R_,
+                         b.reply, rp);
+      const size_t lds = sizeof(SxOrdLds) + (size_t)kXOrdStateMax * sizeof(int64_t);
+#define PT_SX_ORD(SV)                                                                                            \
+  do {                                                                                                           \
+    static bool attr = false;                                                                                    \
+    if (!attr) {                                                                                                 \
+      PT_HIP_CHECK(hipFuncSetAttribute((const void*)sx_drain_ord_kernel<SV>,                                     \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                   \
+      attr = true;                                                                                               \
+    }                                                                                                            \
+    hipLaunchKernelGGL((sx_drain_ord_kernel<SV>), dim3(kSxShards), dim3(kXOrdThreads), lds, cs,                 \
+                       (const uint32_t*)b.recv, rq, tab_off, C, L, R_, b.reply, rp, (int64_t*)a.state, a.n_state, \
+                       a.delay_ticks, stats_);                                                                   \
+  } while (0)
+      switch (S) {
+        case 1: PT_SX_ORD(1); break;
+        case 2: PT_SX_ORD(2); break;
+        case 3: PT_SX_ORD(3); break;
+        case 4: PT_SX_ORD(4); break;
+        case 6: PT_SX_ORD(6); break;
+        default: PT_SX_ORD(8); break;
+      }
+#undef PT_SX_ORD
+    }
+    // ~2048 blocks over the R regions (at least one per region)
+    const int64_t per = std::max<int64_t>(1, max_chunk_ / R_);
+    const unsigned X = (unsigned)std::max<int64_t>(1, std::min<int64_t>((per + 1023) / 1024, std::max(1, 2048 / R_)));
+#define PT_SX_PAR(SV)                                                                                         \
+  hipLaunchKernelGGL((sx_drain_par_kernel<SV>), dim3(X, R_), dim3(256), 0, cs, (const uint32_t*)b.recv, rq, C, L, \
+                     R_, may_order, b.reply, rp, (int64_t*)a.state, a.n_state, a.delay_ticks, stats_)
+    switch (S) {
+      case 1: PT_SX_PAR(1); break;
+      case 2: PT_SX_PAR(2); break;
+      case 3: PT_SX_PAR(3); break;
+      case 4: PT_SX_PAR(4); break;
+      case 6: PT_SX_PAR(6); break;
+      default: PT_SX_PAR(8); break;
+    }
+#undef PT_SX_PAR
+    PT_HIP_CHECK(hipGetLastError());
+    PT_HIP_CHECK(hipEventRecord(ev_served_[i], cs));
+    PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_served_[i], 0));
+    a2a(b.reply, b.back, (size_t)rp * 4);
+    PT_HIP_CHECK(hipEventRecord(ev_rep_in_[i], comm_stream_));
+  };
+  for (int i = 0; i < chunks_; ++i) {
+    Bufs& b = bufs_[i];
+    int64_t lo, m;
+    const SortIn in = chunk_in(i, lo, m);
+#define PT_SX_MODE(KERNEL, ...)                                      \
+  do {                                                               \
+    if (mode == 2) hipLaunchKernelGGL((KERNEL<2>), __VA_ARGS__);     \
+    else if (mode == 1) hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<0>), __VA_ARGS__);               \
+  } while (0)
+    PT_SX_MODE(sx_count_kernel, dim3(in.G), dim3(kST), 0, cs, in, R_, hist_, (unsigned long long*)meta);
+    hipLaunchKernelGGL(sx_scan_kernel, dim3(R_), dim3(1024), 0, cs, hist_, in.G, R_, b.send, rq, tab_off, (uint32_t)C,
+                       (uint32_t)a.method_uniform, (uint32_t)kFlagValid, rank_, (unsigned long long*)meta, boff_);
+#undef PT_SX_MODE
+#define PT_SX_SCAT(MO, SV)                                                                                       \
+  hipLaunchKernelGGL((sx_scatter_kernel<MO, SV>), dim3(in.G), dim3(kST), 0, cs, in, R_, (const uint32_t*)hist_, \
+                     (const uint32_t*)boff_, b.send, rq, (uint32_t)C, L, b.perm, (unsigned long long*)meta)
+#define PT_SX_SCAT_S(MO)            \
+  switch (S) {                      \
+    case 1: PT_SX_SCAT(MO, 1); break; \
+    case 2: PT_SX_SCAT(MO, 2); break; \
+    case 3: PT_SX_SCAT(MO, 3); break; \
+    case 4: PT_SX_SCAT(MO, 4); break; \
+    case 6: PT_SX_SCAT(MO, 6); break; \
+    default: PT_SX_SCAT(MO, 8); break; \
+  }
+    if (mode == 2) {
+      PT_SX_SCAT_S(2)
+    } else if (mode == 1) {
+      PT_SX_SCAT_S(1)
+    } else {
+      PT_SX_SCAT_S(0)
+    }
+#undef PT_SX_SCAT_S
+#undef PT_SX_SCAT
+    PT_HIP_CHECK(hipGetLastError());
+    PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
+    PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_routed_[i], 0));
+    a2a(b.send, b.recv, (size_t)rq * 4);
+    PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], comm_stream_));
+    if (i > 0) serve(i - 1);
+  }
+  serve(chunks_ - 1);
+  // this Send's agreement, for Send + 2 (the comm stream is past every chunk's scatter)
+  allreduce_meta(meta, comm_stream_);
+  PT_HIP_CHECK(hipMemcpyAsync(meta_host_ + cur * kMetaWords, meta, kMetaWords * sizeof(uint64_t),
+                              hipMemcpyDeviceToHost, comm_stream_));
+  PT_HIP_CHECK(hipEventRecord(ev_meta_[cur], comm_stream_));
+  meta_send_[cur] = capturing ? -1 : sends_;
+  for (int i = 0; i < chunks_; ++i) {
+    int64_t lo, m;
+    (void)chunk_in(i, lo, m);
+    PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_rep_in_[i], 0));
+    if (m > 0)
+      launch_complete_packed((uintptr_t)bufs_[i].back, C, R_, L.vb, (uintptr_t)bufs_[i].perm, m,
+                             a.out_val + (uintptr_t)(lo * 8), a.out_st + (uintptr_t)(lo * 4), 0, false,
+                             (uintptr_t)cs);
+  }
+  ++sends_;
+}
+
+}  // namespace ptype

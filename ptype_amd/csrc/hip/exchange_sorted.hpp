@@ -1,0 +1,135 @@
+// Sorted exchange: the multi-GPU Send with mailbox delivery, where the sender's
+// counting sort does the receiver's enqueue.
+//
+// Every rank sorts its batch stably by (destination rank, destination actor
+// shard) straight into the per-peer request regions of the all-to-all (count /
+// scan / scatter, the building blocks of sort_common.hpp).  A region therefore
+// arrives as the SENDER'S part of the receiver's actor mailboxes: 64 shard runs
+// (an actor's messages in message order within its run) and a shard table.  The
+// receiver runs no enqueue pass at all -- its drain reads the received regions
+// as its mailboxes:
+//   * parallel drain (batches without ordered methods): every record of every
+//     region runs independently, replies land at the record's position of the
+//     reply region (coalesced);
+//   * ordered drain: one block per shard takes that shard's runs of every source
+//     region in source-rank order, actors' state in LDS, each actor's records
+//     one at a time in ring order (LDS bins), so every (sender, actor) pair is
+//     FIFO.
+// The sender's completion gathers each message's reply through the position
+// the scatter recorded (perm).  Per message on the wire: the wire-v3 packed
+// record (packed.hpp) and a packed reply.
+//
+// No host wait per Send.  Region geometry (record layout L, per-peer capacity
+// C) cannot be agreed within a Send without a host round trip (RCCL's sizes
+// are host arguments), so Send k uses the agreement of Send k - 2: every Send
+// folds its own column maxima and busiest bucket into a 16-word vector on the
+// device, all-reduces it (MAX) on the comm stream and copies it to pinned host
+// memory; two Sends later every rank derives the same L and C from it (the lag
+// is fixed, so ranks never disagree on a geometry).  Sends 0 and 1 use the
+// widest layout.  A message that does not fit the layout in force (a field
+// wider than agreed, or its bucket past C) is answered STATUS_OVERFLOW --
+// send_all re-sends it -- and its slot carries a null record (mailbox field all
+// ones, which no real mailbox uses: the agreed width leaves room for it).
+// Padded all-to-alls (ncclAllToAll, equal split) keep the step free of host
+// sizes, so it also captures into a hipGraph.
+//
+// Reference: the batched fan-out this replaces is the optimus coordinator's
+// goroutine-per-range Calls (example/optimus/coordinator/coordinator.go:67-98)
+// over cluster/rpc.go:69-105; the per-request server goroutine of net/rpc
+// (example/calculator/server/server.go:16-20) is the mailbox drain.
+#pragma once
+#include <memory>
+#include <vector>
+
+#include "engine.hpp"
+#include "packed.hpp"
+
+namespace ptype {
+
+constexpr int kSxShardBits = 6;  // actor shards per rank on the wire: mailbox & 63
+constexpr int kSxShards = 1 << kSxShardBits;
+constexpr int kSxMaxRanks = 16;
+constexpr int kSxMaxChunks = 4;
+constexpr int kSxTableWords = (kSxShards + 1 + 3) & ~3;  // shard table at the end of a request region
+
+struct SxSend {
+  uintptr_t actor = 0, a0 = 0, a1 = 0, a2 = 0, method_col = 0;
+  int method_uniform = 0;
+  int64_t M = 0;
+  uintptr_t table = 0;
+  uint64_t cap = 0;
+  uintptr_t dir = 0;
+  uint32_t n_dir = 0, affine_w = 0;
+  uintptr_t out_val = 0, out_st = 0, state = 0;
+  uint32_t n_state = 0;
+  uint64_t delay_ticks = 0;
+  bool ordered = false;  // receivers run each actor's records one at a time in ring order
+  uintptr_t stream = 0;
+};
+
+struct SxWire {
+  PackedLayout L{};
+  int S = 0;                // dwords per request record as moved (L.S rounded to a kernel variant)
+  int64_t C = 0;            // per-peer capacity (records) of this Send
+  int64_t req_words = 0;    // per peer, per chunk, as moved
+  int64_t rep_words = 0;
+  bool agreed = false;      // L and C came from an agreement (else the start-up wide layout)
+  int64_t spec_from = -1;   // the Send whose agreement they came from
+  uint64_t meta[kMetaWords] = {};
+};
+
+class SortedExchange {
+ public:
+  // R ranks (comm: the process group's ncclComm_t, or fake), batches of up to
+  // chunks * max_chunk messages; C_alloc: per-peer capacity the buffers hold;
+  // C0: the start-up capacity (until the first agreement applies).
+  SortedExchange(int device, uintptr_t comm, int R, int rank, int64_t max_chunk, int chunks, int64_t C_alloc,
+                 int64_t C0, std::shared_ptr<FakeComm> fake = nullptr);
+  ~SortedExchange();
+  void send(const SxSend& a);
+  const SxWire& last_wire() const { return wire_; }
+  int64_t sends() const { return sends_; }
+  std::vector<uint64_t> stats() const;  // receiver counters: handler failures, replies wider than agreed
+
+ private:
+  struct Bufs {
+    uint32_t *send = nullptr, *recv = nullptr, *reply = nullptr, *back = nullptr;
+    int32_t* perm = nullptr;
+  };
+  void pick_spec(hipStream_t cs);
+  void adopt(const uint64_t* meta, int64_t from);
+  void a2a(const void* src, void* dst, size_t bytes_per_peer);
+  void allreduce_meta(uint64_t* dev, hipStream_t s);
+  bool collectives() const { return comm_ != nullptr || fake_ != nullptr; }
+
+  int device_;
+  void* comm_;
+  std::shared_ptr<FakeComm> fake_;
+  int R_, rank_, chunks_;
+  int64_t max_chunk_, C_alloc_;
+  hipStream_t comm_stream_ = nullptr;
+  Bufs bufs_[kSxMaxChunks];
+  uint32_t* hist_ = nullptr;  // [G][R * 64] per-block bucket counts -> prefixes
+  uint32_t* boff_ = nullptr;  // [R * 64] bucket offsets within their region
+  uint64_t* meta_dev_ = nullptr;   // [2][kMetaWords] agreement vectors (device)
+  uint64_t* meta_host_ = nullptr;  // [2][kMetaWords] pinned copies
+  unsigned long long* stats_ = nullptr;  // [2] receiver counters
+  hipEvent_t ev_meta_[2]{};
+  int64_t meta_send_[2] = {-1, -1};  // the Send whose agreement each buffer holds
+  hipEvent_t ev_routed_[kSxMaxChunks]{}, ev_req_in_[kSxMaxChunks]{}, ev_served_[kSxMaxChunks]{},
+      ev_rep_in_[kSxMaxChunks]{};
+  // the layout and capacity in force
+  PackedLayout L_{};
+  int64_t C_ = 0;
+  bool agreed_ = false;
+  int64_t spec_from_ = -1;
+  uint64_t spec_meta_[kMetaWords] = {};
+  int64_t sends_ = 0;
+  SxWire wire_;
+};
+
+// The layout of an agreement: packed_layout with a mailbox field one bit wider
+// than the largest mailbox, so the all-ones value is free for null records.
+PackedLayout sx_layout(const uint64_t* meta);
+
+}  // namespace ptype

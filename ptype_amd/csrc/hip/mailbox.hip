@@ -772,8 +772,11 @@ Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) 
   PT_HIP_CHECK(hipMalloc((void**)&mv_.ctr, ctr_bytes));
   PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, ctr_bytes, stream_));
   PT_HIP_CHECK(hipMalloc((void**)&sort_hist_, (size_t)kMboxSortHistWords * sizeof(uint32_t)));
-  PT_HIP_CHECK(hipMalloc((void**)&sort_tot_, (size_t)shards * sizeof(uint32_t)));
-  bytes_ += (size_t)kMboxSortHistWords * sizeof(uint32_t) + (size_t)shards * sizeof(uint32_t);
+  PT_HIP_CHECK(hipMalloc((void**)&sort_gsum_, (size_t)kMboxSortGroups * shards * sizeof(uint32_t)));
+  PT_HIP_CHECK(hipMemsetAsync(sort_gsum_, 0, (size_t)kMboxSortGroups * shards * sizeof(uint32_t), stream_));
+  PT_HIP_CHECK(hipMalloc((void**)&sort_ticket_, kTicketWords * sizeof(unsigned)));
+  PT_HIP_CHECK(hipMemsetAsync(sort_ticket_, 0, kTicketWords * sizeof(unsigned), stream_));
+  bytes_ += (size_t)kMboxSortHistWords * sizeof(uint32_t) + (size_t)kMboxSortGroups * shards * sizeof(uint32_t);
   PT_HIP_CHECK(hipMalloc((void**)&mv_.stats, kMbStripes * kMbStatWords * 8));
   PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStripes * kMbStatWords * 8, stream_));
   bytes_ += ctr_bytes + kMbStripes * kMbStatWords * 8;
@@ -796,8 +799,9 @@ Mailboxes::~Mailboxes() {
   if (mv_.a2) (void)hipFree(mv_.a2);
   (void)hipFree(mv_.ctr);
   (void)hipFree(mv_.stats);
-  if (sort_hist_) (void)hipFree(sort_hist_);
-  if (sort_tot_) (void)hipFree(sort_tot_);
+  for (void* p : {(void*)sort_hist_, (void*)sort_gsum_, (void*)sort_ticket_, (void*)sort_rw_, (void*)sort_sidx_,
+                  (void*)stage_val_, (void*)stage_st_})
+    if (p) (void)hipFree(p);
   if (ctrl_) (void)hipHostFree(ctrl_);
 }
 
@@ -865,6 +869,8 @@ void Mailboxes::reset(uintptr_t stream) {
   PT_HIP_CHECK(hipMemsetAsync(mv_.rec, 0, rec_bytes_, s));
   PT_HIP_CHECK(hipMemsetAsync(mv_.ctr, 0, (size_t)shards() * kMboxCtrStride * 8, s));
   PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStripes * kMbStatWords * 8, s));
+  PT_HIP_CHECK(hipMemsetAsync(sort_gsum_, 0, (size_t)kMboxSortGroups * shards() * sizeof(uint32_t), s));
+  PT_HIP_CHECK(hipMemsetAsync(sort_ticket_, 0, kTicketWords * sizeof(unsigned), s));
 }
 
 std::vector<uint64_t> Mailboxes::stats() const {

@@ -58,6 +58,7 @@ constexpr int kMboxMaxShards = 4096;
 // shard) histogram's size -- it bounds the count / scatter grid (G <= words / S)
 constexpr int kMboxSortMaxShards = 1024;
 constexpr uint32_t kMboxSortHistWords = 1u << 18;
+constexpr uint32_t kMboxSortGroups = 32;  // group sums of 32 blocks each (G <= 1024)
 enum MboxStat : int {
   kMbEnqueued = 0,   // records written into rings
   kMbOverflow = 1,   // messages answered kStatusOverflow (ring full)
@@ -197,8 +198,14 @@ class Mailboxes {
   hipStream_t stream_ = nullptr;
   bool started_ = false;
   uint64_t launches_ = 0;
-  uint32_t* sort_hist_ = nullptr;  // [G][S] per-block shard counts -> prefixes (send_sorted)
-  uint32_t* sort_tot_ = nullptr;   // [S] the epoch's total per shard
+  uint32_t* sort_hist_ = nullptr;   // [G][S] per-block shard counts (send_sorted)
+  uint32_t* sort_gsum_ = nullptr;   // [kMboxSortGroups][S] group sums (zero between Sends: the drains clear them)
+  unsigned* sort_ticket_ = nullptr; // last-block ticket of the parallel drain (self-resetting)
+  uint32_t* sort_rw_ = nullptr;     // [M] each message's mailbox (route word), count -> scatter
+  uint32_t* sort_sidx_ = nullptr;   // [M] each message's ring slot, scatter -> drain / completion
+  uint64_t sort_cap_ = 0;           // messages the two arrays hold
+  int64_t* stage_val_ = nullptr;    // ordered drain: replies staged at ring slots [S * Q]
+  int32_t* stage_st_ = nullptr;
 };
 
 }  // namespace ptype

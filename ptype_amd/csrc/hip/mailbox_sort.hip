@@ -4,18 +4,25 @@
 // The epoch form of a Send (mailbox.hpp has the ring layout) runs
 //
 //   count    each block resolves its contiguous range of the batch against the
-//            registry mirror (route directory / hash probe) and counts its
-//            messages per shard: hist[block][shard];
-//   scan     exclusive prefix of hist over blocks, per shard; column totals;
-//   scatter  each block re-resolves its range and writes every message into its
-//            shard's ring at (tail + prefix + rank), the rank computed in message
-//            order (wave match on the shard bits + per-wave counts), so each
-//            ring holds its messages in MESSAGE ORDER: every actor's mailbox is
-//            FIFO by construction, with no atomic per message or per tile;
-//   drain    parallel (batches without ordered methods): every record runs
-//            independently; ordered: one block owns one shard -- its actors'
-//            state staged in LDS -- and runs each actor's records one at a time
-//            in ring order, distinct actors side by side (LDS bins).
+//            registry mirror (route directory / hash probe), keeps each
+//            message's mailbox (route word) and counts its messages per shard:
+//            hist[block][shard], plus group sums over 32 blocks (atomics);
+//   scatter  each block's prefix per shard is the group sums before its group
+//            plus the rows before it inside its group (at most 31 + 31 L2-hot
+//            rows: no scan pass); it writes every message into its shard's ring
+//            at (tail + prefix + rank), the rank computed in message order (wave
+//            match on the shard bits + per-wave counts), so each ring holds its
+//            messages in MESSAGE ORDER: every actor's mailbox is FIFO by
+//            construction, with no atomic per message; it records each
+//            message's ring slot;
+//   drain    parallel (batches without ordered methods): each record is taken
+//            from its ring slot in message order -- the replies are written
+//            coalesced (draining in ring order scattered every reply: 273 us of
+//            random stores per 8 Mi); ordered: one block owns one shard -- its
+//            actors' state staged in LDS -- and runs each actor's records one at
+//            a time in ring order, distinct actors side by side (LDS bins),
+//            replies staged at their ring slots; a completion pass gathers them
+//            into message order.
 //
 // Records are 16 B in the common case (compact form, plane A only):
 //   w0 = origin | kCompactMark    (bit 31 marks an epoch record; a live ring's
@@ -31,9 +38,7 @@
 // count / scatter block b takes the range of virtual block (b % 8) * G/8 + b / 8,
 // so each XCD owns one contiguous eighth of the batch -- and therefore one
 // contiguous part of every shard's run, whose partially written lines meet in
-// ONE L2.  The parallel drain gives XCD x the same part x of every shard: the
-// origins of that part are (the rings being message-ordered) one eighth of the
-// batch, so the scattered reply stores of one output line come from one XCD.
+// ONE L2.
 //
 // Reference: the server's per-request goroutine of stdlib net/rpc
 // (example/calculator/server/server.go:16-20, :38; handler
@@ -44,14 +49,11 @@
 #include "mailbox.hpp"
 #include "mailbox_dev.hpp"
 #include "route_common.hpp"
+#include "sort_common.hpp"
 
 namespace ptype {
 
 namespace {
-constexpr int kST = 256;             // count / scatter threads per block
-constexpr int kSK = 8;               // messages per thread per tile
-constexpr int kSTile = kST * kSK;    // 2048 messages
-constexpr int kSWave = kSK * kWave;  // a wave's contiguous run of a tile (512)
 constexpr uint32_t kCompactMark = 0x80000000u;
 constexpr uint32_t kCompactLong = 0x80000000u;
 constexpr int kOrdThreads = 512;  // ordered drain: one block per shard, one bin per thread
@@ -63,92 +65,13 @@ constexpr int kDrainThreads = 256;
 constexpr int kDrainK = 4;
 }  // namespace
 
-// ---------------------------------------------------------------- inputs
-struct SortIn {  // by value
-  const uint32_t* actor;
-  const int64_t* a0;
-  const int64_t* a1;
-  const int64_t* a2;
-  const uint16_t* mcol;
-  uint32_t method_uniform;
-  int64_t M;
-  const TableEntry* table;
-  uint64_t mask;
-  const uint32_t* dir;
-  uint32_t n_dir;
-  uint32_t aw;
-  int aw_shift;
-  int rank_self;
-  uint32_t origin_base;
-  uint32_t G;      // blocks
-  uint32_t tiles;  // ceil(M / kSTile)
-  uint32_t tpb;    // tiles per block
-};
-
-// Block b's range: XCD (b % 8) owns virtual blocks [x * G/8, (x+1) * G/8).
-__device__ __forceinline__ uint32_t virt_block(uint32_t b, uint32_t G) {
-  return (G >= 8 && (G & 7) == 0) ? (b & 7) * (G >> 3) + (b >> 3) : b;
-}
-
-template <int MODE>
-__device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[kSK], int (&r)[kSK],
-                                          uint32_t (&mb)[kSK]) {
-  if constexpr (MODE == 1) {
-    uint32_t w[kSK];
-#pragma unroll
-    for (int k = 0; k < kSK; ++k) w[k] = a[k] < in.n_dir ? in.dir[a[k]] : kDirFallback;
-#pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
-      mb[k] = w[k] >> 8;
-      if (w[k] == kDirFallback) {
-        if (a[k] != 0xffffffffu) lookup_entry(in.table, in.mask, actor_key(a[k]), r[k], mb[k]);
-        else r[k] = -1;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      if (MODE == 2 && a[k] < in.n_dir) {
-        r[k] = in.aw_shift >= 0 ? (int)(a[k] & (in.aw - 1)) : (int)(a[k] % in.aw);
-        mb[k] = in.aw_shift >= 0 ? a[k] >> in.aw_shift : a[k] / in.aw;
-      } else if (a[k] == 0xffffffffu) {
-        r[k] = -1;
-        mb[k] = 0;
-      } else {
-        lookup_entry(in.table, in.mask, actor_key(a[k]), r[k], mb[k]);
-      }
-    }
-  }
-}
-
-// Message i of tile t for (item k, lane) of wave w: a wave owns a contiguous run
-// of the tile, so message order within a tile is (wave, item, lane).
-__device__ __forceinline__ int64_t tile_index(uint32_t t, int k) {
-  return (int64_t)t * kSTile + (threadIdx.x / kWave) * kSWave + k * kWave + lane_id();
-}
-
-__device__ __forceinline__ void load_actors(const SortIn& in, uint32_t t, uint32_t (&a)[kSK]) {
-#pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const int64_t i = tile_index(t, k);
-    a[k] = i < in.M ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
-  }
-}
-
-// Lanes of this wave whose `key` (log_bits bits) equals this lane's, among `act`.
-__device__ __forceinline__ uint64_t match_bits(uint32_t key, uint32_t log_bits, uint64_t act) {
-  uint64_t m = act;
-  for (uint32_t b = 0; b < log_bits; ++b) {
-    const uint64_t bb = __ballot((key >> b) & 1u);
-    m &= ((key >> b) & 1u) ? bb : ~bb;
-  }
-  return m;
-}
-
 // ---------------------------------------------------------------- K2s pass 1: count
+constexpr uint32_t kGroupBlocks = 32;  // the scatter's prefix: group sums + rows inside the group
+constexpr uint32_t kNoSlot = 0xffffffffu;
+
 template <int MODE, bool ARRIVAL>
-__global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_s, uint32_t* __restrict__ hist) {
+__global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_s, uint32_t* __restrict__ hist,
+                                                        uint32_t* __restrict__ gsum, uint32_t* __restrict__ rw) {
   __shared__ uint32_t cnt[kMboxSortMaxShards];
   const uint32_t S = 1u << log_s;
   const uint32_t v = virt_block(blockIdx.x, in.G);
@@ -162,81 +85,54 @@ __global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_
     uint32_t mb[kSK];
     resolve_k<MODE>(in, a, r, mb);
     if (t + 1 < t1) load_actors(in, t + 1, a);  // next tile's loads in flight while this one counts
-    if constexpr (ARRIVAL) {
-      unsigned c = 0;
+    unsigned c = 0;
 #pragma unroll
-      for (int k = 0; k < kSK; ++k) c += (r[k] == in.rank_self && mb[k] < kMaxMbox) ? 1u : 0u;
+    for (int k = 0; k < kSK; ++k) {
+      const int64_t i = tile_index(t, k);
+      const bool ok = r[k] == in.rank_self && mb[k] < kMaxMbox;
+      if (i < in.M) rw[i] = ok ? mb[k] : kNoSlot;
+      if constexpr (ARRIVAL) {
+        c += ok ? 1u : 0u;
+      } else if (ok) {
+        atomicAdd(&cnt[mb[k] & (S - 1)], 1u);
+      }
+    }
+    if constexpr (ARRIVAL) {
       c = (unsigned)__builtin_amdgcn_readlane((int)wave_incl_scan(c), 63);
       if (lane_id() == 0 && c) atomicAdd(&cnt[t & (S - 1)], c);
-    } else {
-#pragma unroll
-      for (int k = 0; k < kSK; ++k)
-        if (r[k] == in.rank_self && mb[k] < kMaxMbox) atomicAdd(&cnt[mb[k] & (S - 1)], 1u);
     }
   }
   __syncthreads();
-  for (uint32_t s = threadIdx.x; s < S; s += kST) hist[(size_t)v * S + s] = cnt[s];
-}
-
-// ---------------------------------------------------------------- K2s pass 2: scan
-// hist [G][S] -> exclusive prefix over blocks per shard, in place; etot[s] = the
-// shard's total.  Block: 64 shards x 16 row groups (coalesced 256-B row reads).
-__global__ __launch_bounds__(1024) void mbx_scan_kernel(uint32_t* __restrict__ hist, uint32_t G, uint32_t log_s,
-                                                        uint32_t* __restrict__ etot) {
-  __shared__ uint32_t part[16][64];
-  const uint32_t S = 1u << log_s;
-  const uint32_t lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const uint32_t c = blockIdx.x * 64 + lane;
-  const uint32_t rows = (G + 15) / 16, r0 = min(G, g * rows), r1 = min(G, r0 + rows);
-  uint32_t sum = 0;
-  if (c < S) {
-    uint32_t r = r0;
-    for (; r + 8 <= r1; r += 8) {
-      uint32_t x[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = hist[(size_t)(r + j) * S + c];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sum += x[j];
-    }
-    for (; r < r1; ++r) sum += hist[(size_t)r * S + c];
-  }
-  part[g][lane] = sum;
-  __syncthreads();
-  uint32_t run = 0;
-  for (uint32_t j = 0; j < g; ++j) run += part[j][lane];
-  if (c < S) {
-    if (g == 15) etot[c] = run + sum;
-    for (uint32_t r = r0; r < r1; ++r) {
-      const uint32_t x = hist[(size_t)r * S + c];
-      hist[(size_t)r * S + c] = run;
-      run += x;
-    }
+  uint32_t* g = gsum + (size_t)(v / kGroupBlocks) * S;
+  for (uint32_t s = threadIdx.x; s < S; s += kST) {
+    const uint32_t c = cnt[s];
+    hist[(size_t)v * S + s] = c;
+    if (c) atomicAdd(&g[s], c);
   }
 }
 
-// ---------------------------------------------------------------- K2s pass 3: scatter
-struct SortTileIn {
-  uint32_t a[kSK];
-  int64_t x0[kSK], x1[kSK], x2[kSK];
-};
-
-__device__ __forceinline__ void load_args(const SortIn& in, uint32_t t, SortTileIn& x) {
+// ---------------------------------------------------------------- K2s pass 2: scatter
+template <bool A2, bool MC>
+__device__ __forceinline__ void load_routed(const SortIn& in, const uint32_t* __restrict__ rw, uint32_t t,
+                                            uint32_t (&m)[kSK], int64_t (&x0)[kSK], int64_t (&x1)[kSK],
+                                            int64_t (&x2)[kSK], uint32_t (&meth)[kSK]) {
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     const int64_t i = tile_index(t, k);
     const bool ok = i < in.M;
-    x.a[k] = ok ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
-    x.x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
-    x.x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
-    x.x2[k] = ok && in.a2 ? __builtin_nontemporal_load(in.a2 + i) : 0;
+    m[k] = ok ? __builtin_nontemporal_load(rw + i) : kNoSlot;
+    x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
+    x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    if constexpr (A2) x2[k] = ok ? __builtin_nontemporal_load(in.a2 + i) : 0;
+    if constexpr (MC) meth[k] = ok ? (uint32_t)in.mcol[i] : 0u;
   }
 }
 
-__device__ __forceinline__ bool fits_i32(int64_t v) { return v == (int64_t)(int32_t)v; }
-
-template <int MODE, bool ARRIVAL>
+template <bool ARRIVAL, bool A2, bool MC>
 __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv, const uint32_t* __restrict__ hist,
-                                                          ReplyView rv) {
+                                                          const uint32_t* __restrict__ gsum,
+                                                          const uint32_t* __restrict__ rw,
+                                                          uint32_t* __restrict__ sidx, ReplyView rv) {
   __shared__ uint32_t run[kMboxSortMaxShards];   // this block's next offset per shard
   __shared__ uint32_t room[kMboxSortMaxShards];  // offset limit per shard (free ring slots)
   __shared__ unsigned long long base[kMboxSortMaxShards];  // ring position of offset 0 (the tail)
@@ -245,8 +141,13 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
   const uint64_t Q = 1ull << mv.log_q;
   const uint32_t v = virt_block(blockIdx.x, in.G);
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t g0 = v / kGroupBlocks, v0 = g0 * kGroupBlocks;
   for (uint32_t s = threadIdx.x; s < S; s += kST) {
-    run[s] = hist[(size_t)v * S + s];
+    // this block's prefix: whole groups before it, then the rows before it in its group
+    uint32_t p = 0;
+    for (uint32_t g = 0; g < g0; ++g) p += gsum[(size_t)g * S + s];
+    for (uint32_t u = v0; u < v; ++u) p += hist[(size_t)u * S + s];
+    run[s] = p;
     const uint64_t tl = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
     base[s] = tl;
     const uint64_t free = hd + Q > tl ? hd + Q - tl : 0;
@@ -254,40 +155,36 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
   }
   unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0;
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
-  SortTileIn x;
-  if (t0 < t1) load_args(in, t0, x);
+  uint32_t nm[kSK], nmeth[kSK];
+  int64_t n0[kSK], n1[kSK], n2[kSK];
+  if (t0 < t1) load_routed<A2, MC>(in, rw, t0, nm, n0, n1, n2, nmeth);
   for (uint32_t t = t0; t < t1; ++t) {
     for (uint32_t s = lane; s < S; s += kWave) wcnt[w][s] = 0;  // this wave's row only
-    int r[kSK];
-    uint32_t mb[kSK];
-    resolve_k<MODE>(in, x.a, r, mb);
+    uint32_t mb[kSK], meth[kSK];
     int64_t v0[kSK], v1[kSK], v2[kSK];
-    uint32_t meth[kSK];
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
-      v0[k] = x.x0[k], v1[k] = x.x1[k], v2[k] = x.x2[k];
-      const int64_t i = tile_index(t, k);
-      meth[k] = in.mcol && i < in.M ? (uint32_t)in.mcol[i] : in.method_uniform;
+      mb[k] = nm[k], v0[k] = n0[k], v1[k] = n1[k];
+      v2[k] = A2 ? n2[k] : 0;
+      meth[k] = MC ? nmeth[k] : in.method_uniform;
     }
-    if (t + 1 < t1) load_args(in, t + 1, x);  // next tile's loads in flight across this tile's barriers
+    if (t + 1 < t1) load_routed<A2, MC>(in, rw, t + 1, nm, n0, n1, n2, nmeth);  // in flight across the barriers
     // rank of each message among this wave's earlier messages of its shard
     uint32_t wr[kSK], sh[kSK];
-    bool ok[kSK];
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
-      ok[k] = r[k] == in.rank_self && mb[k] < kMaxMbox;
+      const bool ok = mb[k] != kNoSlot;
       sh[k] = ARRIVAL ? (t & (S - 1)) : (mb[k] & (S - 1));
-      const uint64_t act = __ballot(ok[k]);
+      const uint64_t act = __ballot(ok);
       const uint64_t peers = ARRIVAL ? act : match_bits(sh[k], mv.log_s, act);
       const unsigned below = mbcnt64(peers);
       const int leader = peers ? __builtin_ctzll(peers) : 0;
       unsigned old = 0;
-      if (ok[k] && below == 0) {  // group leader: one plain LDS read-add per distinct shard of the wave
+      if (ok && below == 0) {  // group leader: one plain LDS read-add per distinct shard of the wave
         old = wcnt[w][sh[k]];
         wcnt[w][sh[k]] = old + (unsigned)__popcll(peers);
       }
-      old = (unsigned)__shfl((int)old, leader);
-      wr[k] = old + below;
+      wr[k] = (unsigned)__shfl((int)old, leader) + below;
     }
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < S; s += kST) {  // wave offsets in message order, then the block's run
@@ -306,18 +203,21 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
       const int64_t i = tile_index(t, k);
       if (i >= in.M) continue;
       const uint32_t origin = in.origin_base + (uint32_t)i;
-      if (!ok[k]) {
+      if (mb[k] == kNoSlot) {
         ++n_miss;
+        sidx[i] = kNoSlot;
         write_status(rv, origin, kStatusNoActor);
         continue;
       }
       const uint32_t off = wcnt[w][sh[k]] + wr[k];
       if (off >= room[sh[k]]) {  // the ring is full: answered now, re-sent by send_all
         ++n_ovf;
+        sidx[i] = kNoSlot;
         write_status(rv, origin, kStatusOverflow);
         continue;
       }
       const uint64_t slot = slot_at(mv, sh[k], base[sh[k]] + off);
+      sidx[i] = (uint32_t)slot;
       const bool compact = meth[k] < 128u && fits_i32(v0[k]) && fits_i32(v1[k]) && v2[k] == 0;
       if (compact) {
         *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
@@ -368,69 +268,76 @@ __device__ __forceinline__ SortRec decode_sorted(const u32x4& ha, const u32x4& h
   return x;
 }
 
-// Range of shard s this epoch: [tail, tail + min(total, free slots)).
-__device__ __forceinline__ void epoch_range(const MboxView& mv, const uint32_t* etot, uint32_t s, uint64_t& lo,
-                                            uint64_t& n, uint32_t& tot) {
-  const uint64_t Q = 1ull << mv.log_q;
-  lo = *ctr_tail(mv, s);
-  const uint64_t hd = *ctr_head(mv, s);
-  const uint64_t free = hd + Q > lo ? hd + Q - lo : 0;
-  tot = etot[s];
-  n = tot < free ? tot : free;
+__device__ __forceinline__ SortRec load_sorted(const MboxView& mv, uint64_t slot) {
+  const u32x4 ha = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
+  u32x4 hb = {0u, 0u, 0u, 0u};
+  int64_t a2v = 0;
+  if (rec_is_long(ha)) {
+    hb = *reinterpret_cast<const u32x4*>(rec_b(mv, slot));
+    if (((ha.z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[slot];
+  }
+  return decode_sorted(ha, hb, a2v);
+}
+
+// The epoch's total of shard s (group sums) -- and the group words zeroed for
+// the next Send once read (`clear`: the caller is the shard's last reader).
+__device__ __forceinline__ uint32_t epoch_total(uint32_t* gsum, uint32_t ngroups, uint32_t S, uint32_t s, bool clear) {
+  uint32_t t = 0;
+  for (uint32_t g = 0; g < ngroups; ++g) {
+    t += gsum[(size_t)g * S + s];
+    if (clear) gsum[(size_t)g * S + s] = 0u;
+  }
+  return t;
 }
 
 // The epoch's positions of shard s are consumed: head = tail = tail + total
 // (overflowed positions were never written and are skipped with them).
-__device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uint64_t lo, uint32_t tot) {
-  *ctr_tail(mv, s) = lo + tot;
-  *ctr_done(mv, s) = lo + tot;
-  *ctr_head(mv, s) = lo + tot;
+__device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uint32_t tot) {
+  const uint64_t t = *ctr_tail(mv, s) + tot;
+  *ctr_tail(mv, s) = t;
+  *ctr_done(mv, s) = t;
+  *ctr_head(mv, s) = t;
 }
 
 // ---------------------------------------------------------------- K3s parallel drain
-// Grid X * S blocks: shard s, part p of X.  XCD x (= block % 8) takes parts
-// [x * X/8, (x+1) * X/8) of every shard.  The last block of a shard commits it.
+// Batches without ordered methods: every record runs on its own, so the drain
+// takes each message's record from its ring slot in MESSAGE order (the slot the
+// scatter recorded) -- the record reads are gathers, the replies land
+// coalesced.  The last block commits every shard (and clears the group sums).
 template <int FIXED>
-__global__ __launch_bounds__(kDrainThreads) void mbx_drain_par_kernel(MboxView mv, const uint32_t* __restrict__ etot,
-                                                                      uint32_t X, int64_t* __restrict__ state,
-                                                                      uint32_t n_state, uint64_t delay_ticks,
-                                                                      OutboxView ob, ReplyView rv) {
-  const uint32_t L = blockIdx.x;
-  uint32_t s, p;
-  if ((X & 7) == 0) {
-    const uint32_t px = X >> 3, j = L >> 3, x = L & 7;
-    s = j / px;
-    p = x * px + j % px;
-  } else {
-    s = L / X;
-    p = L % X;
-  }
-  uint64_t lo, n;
-  uint32_t tot;
-  epoch_range(mv, etot, s, lo, n, tot);
-  const uint64_t b0 = lo + n * p / X, b1 = lo + n * (p + 1) / X;
+__global__ __launch_bounds__(kDrainThreads) void mbx_drain_msg_kernel(MboxView mv, const uint32_t* __restrict__ sidx,
+                                                                      int64_t M, uint32_t origin_base,
+                                                                      int64_t* __restrict__ state, uint32_t n_state,
+                                                                      uint64_t delay_ticks, OutboxView ob, ReplyView rv,
+                                                                      uint32_t* __restrict__ gsum, uint32_t ngroups,
+                                                                      unsigned* __restrict__ ticket) {
   unsigned long long done = 0, failed = 0, holes = 0;
-  for (uint64_t p0 = b0; p0 < b1; p0 += (uint64_t)kDrainK * kDrainThreads) {
+  const int64_t stride = (int64_t)gridDim.x * kDrainThreads;
+  for (int64_t i0 = blockIdx.x * (int64_t)kDrainThreads + threadIdx.x; i0 < M; i0 += stride * kDrainK) {
+    uint32_t sl[kDrainK];
+#pragma unroll
+    for (int u = 0; u < kDrainK; ++u) {
+      const int64_t i = i0 + u * stride;
+      sl[u] = i < M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
+    }
     u32x4 ha[kDrainK];
 #pragma unroll
-    for (int k = 0; k < kDrainK; ++k) {
-      const uint64_t q = p0 + (uint64_t)k * kDrainThreads + threadIdx.x;
-      ha[k] = q < b1 ? *reinterpret_cast<const u32x4*>(rec_a(mv, slot_at(mv, s, q))) : u32x4{0u, 0u, 0u, 0u};
-    }
+    for (int u = 0; u < kDrainK; ++u)
+      ha[u] = sl[u] != kNoSlot ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[u])) : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int k = 0; k < kDrainK; ++k) {
-      const uint64_t q = p0 + (uint64_t)k * kDrainThreads + threadIdx.x;
-      if (q >= b1) continue;
+    for (int u = 0; u < kDrainK; ++u) {
+      if (sl[u] == kNoSlot) continue;  // answered by the scatter (no actor / ring full)
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
-      const uint64_t slot = slot_at(mv, s, q);
-      if (rec_is_long(ha[k])) {
-        hb = *reinterpret_cast<const u32x4*>(rec_b(mv, slot));
-        if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[slot];
+      if (rec_is_long(ha[u])) {
+        hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[u]));
+        if (((ha[u].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[u]];
       }
-      const SortRec x = decode_sorted(ha[k], hb, a2v);
+      const SortRec x = decode_sorted(ha[u], hb, a2v);
+      const int64_t i = i0 + u * stride;
       if (!x.valid) {
         ++holes;
+        write_status(rv, origin_base + (uint32_t)i, kStatusNotDelivered);
         continue;
       }
       MsgRecord m;
@@ -440,20 +347,17 @@ __global__ __launch_bounds__(kDrainThreads) void mbx_drain_par_kernel(MboxView m
       m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
       const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
       failed += rr.status != kStatusOk;
-      write_reply(rv, x.origin, rr);
+      write_reply(rv, origin_base + (uint32_t)i, rr);
       ++done;
     }
   }
   block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
-  // the last block of this shard commits it (every block of the shard has read
-  // the counters by the time it takes its ticket)
-  __shared__ int last;
-  unsigned long long* tk = mv.ctr + (uint64_t)s * kMboxCtrStride + kMboxCtrTicket;
-  if (threadIdx.x == 0) last = atomicAdd(tk, 1ull) == X - 1;
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = last_block_ticket(ticket);
   __syncthreads();
-  if (last && threadIdx.x == 0) {
-    epoch_commit(mv, s, lo, tot);
-    *tk = 0;
+  if (last) {  // every block's records are read: the rings are consumed
+    const uint32_t S = 1u << mv.log_s;
+    for (uint32_t s = threadIdx.x; s < S; s += kDrainThreads) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
   }
 }
 
@@ -464,59 +368,61 @@ __global__ __launch_bounds__(kDrainThreads) void mbx_drain_par_kernel(MboxView m
 // mod bins), then thread b runs bin b's records one at a time in ring order: an
 // actor's messages run serially and in FIFO order, distinct bins in parallel.
 // Every method of the shard runs here (so a batch mixing ordered and other
-// methods keeps per-actor FIFO across all of them).
+// methods keeps per-actor FIFO across all of them).  Replies are staged at the
+// records' ring slots (a window's slots are contiguous: whole lines), and
+// mbx_complete_kernel gathers them into message order.
 struct OrdLds {
   uint32_t wcnt[kOrdWaves][kOrdThreads];  // per-wave bin counts -> offsets
   uint32_t bstart[kOrdThreads];
   uint32_t bcount[kOrdThreads];
   uint32_t wsum[kOrdWaves];
-  uint32_t org[kOrdWin];
+  uint32_t slot[kOrdWin];
   uint32_t act[kOrdWin];  // actor index for the handler (LDS-local or global mailbox)
   uint32_t meth[kOrdWin];  // method | flags << 16
   int64_t a0[kOrdWin], a1[kOrdWin], a2[kOrdWin];
 };
 
-__global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView mv, const uint32_t* __restrict__ etot,
-                                                                        int64_t* __restrict__ state, uint32_t n_state,
-                                                                        uint64_t delay_ticks, OutboxView ob,
-                                                                        ReplyView rv) {
+__global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView mv, uint32_t* __restrict__ gsum,
+                                                                        uint32_t ngroups, int64_t* __restrict__ state,
+                                                                        uint32_t n_state, uint64_t delay_ticks,
+                                                                        OutboxView ob, int64_t* __restrict__ sval,
+                                                                        int32_t* __restrict__ sst) {
   extern __shared__ __align__(16) unsigned char smem_ord[];
   OrdLds& L = *reinterpret_cast<OrdLds*>(smem_ord);
   int64_t* st_lds = reinterpret_cast<int64_t*>(smem_ord + sizeof(OrdLds));
   const uint32_t s = blockIdx.x;
   const uint32_t S = 1u << mv.log_s;
+  const uint64_t Q = 1ull << mv.log_q;
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
-  uint64_t lo, n;
-  uint32_t tot;
-  epoch_range(mv, etot, s, lo, n, tot);
+  __shared__ uint32_t tot_s;
+  if (threadIdx.x == 0) tot_s = epoch_total(gsum, ngroups, S, s, true);
+  const uint64_t lo = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
+  const uint64_t free = hd + Q > lo ? hd + Q - lo : 0;
   // this shard's actors are mailboxes s, s + S, s + 2S, ...: local index j = mb >> log_s
   const uint32_t n_loc = (state && s < n_state) ? (n_state - 1 - s) / S + 1 : 0;
   const bool in_lds = state && n_loc <= kOrdStateMax;
   if (in_lds)
     for (uint32_t j = threadIdx.x; j < n_loc; j += kOrdThreads) st_lds[j] = state[s + (uint64_t)j * S];
   __syncthreads();
+  const uint32_t tot = tot_s;
+  const uint64_t n = tot < free ? tot : free;
   unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
   for (uint64_t w0 = lo; w0 < lo + n; w0 += kOrdWin) {
     const uint64_t w1 = lo + n < w0 + kOrdWin ? lo + n : w0 + kOrdWin;
     for (uint32_t b = lane; b < kOrdThreads; b += kWave) L.wcnt[w][b] = 0;
     SortRec x[kOrdK];
     uint32_t bin[kOrdK], wr[kOrdK];
+    uint64_t slot[kOrdK];
 #pragma unroll
     for (int k = 0; k < kOrdK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
       const uint64_t q = w0 + (uint64_t)w * (kWave * kOrdK) + (uint64_t)k * kWave + lane;
-      u32x4 ha = {0u, 0u, 0u, 0u}, hb = {0u, 0u, 0u, 0u};
-      int64_t a2v = 0;
+      slot[k] = slot_at(mv, s, q);
       if (q < w1) {
-        const uint64_t slot = slot_at(mv, s, q);
-        ha = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
-        if (rec_is_long(ha)) {
-          hb = *reinterpret_cast<const u32x4*>(rec_b(mv, slot));
-          if (((ha.z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[slot];
-        }
+        x[k] = load_sorted(mv, slot[k]);
+        if (!x[k].valid) ++holes;
+      } else {
+        x[k].valid = false;
       }
-      x[k] = decode_sorted(ha, hb, a2v);
-      if (q < w1 && !x[k].valid) ++holes;
-      x[k].valid = x[k].valid && q < w1;
     }
 #pragma unroll
     for (int k = 0; k < kOrdK; ++k) {
@@ -554,7 +460,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
     for (int k = 0; k < kOrdK; ++k) {
       if (!x[k].valid) continue;
       const unsigned d = L.bstart[bin[k]] + L.wcnt[w][bin[k]] + wr[k];
-      L.org[d] = x[k].origin;
+      L.slot[d] = (uint32_t)slot[k];
       L.act[d] = in_lds ? (x[k].mb >> mv.log_s) : x[k].mb;
       L.meth[d] = x[k].method | (x[k].flags << 16);
       L.a0[d] = x[k].a0;
@@ -575,7 +481,8 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
         m.a0 = L.a0[d], m.a1 = L.a1[d], m.a2 = L.a2[d];
         const ReplyRecord rr = run_handler(m, st, nst, delay_ticks, ob, true);
         failed += rr.status != kStatusOk;
-        write_reply(rv, L.org[d], rr);
+        sval[L.slot[d]] = rr.value;
+        sst[L.slot[d]] = rr.status;
         ++done;
         if (!in_lds) vm_drain();  // global state: this store lands before the bin's next load
       }
@@ -587,13 +494,34 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
   __syncthreads();  // block_add_stats' LDS partials are reused
   block_add_stats(mv.stats, serial, kMbSerial, 0, -1, 0, -1);
-  if (threadIdx.x == 0) epoch_commit(mv, s, lo, tot);
+  if (threadIdx.x == 0) epoch_commit(mv, s, tot);
+}
+
+// Ordered drain's replies, staged at ring slots, gathered into message order.
+__global__ __launch_bounds__(256) void mbx_complete_kernel(const uint32_t* __restrict__ sidx, int64_t M,
+                                                           uint32_t origin_base, const int64_t* __restrict__ sval,
+                                                           const int32_t* __restrict__ sst, ReplyView rv) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < M; i0 += stride * 4) {
+    uint32_t sl[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sl[u] = i0 + u * stride < M ? __builtin_nontemporal_load(sidx + i0 + u * stride) : kNoSlot;
+    int64_t v[4];
+    int32_t st[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (sl[u] != kNoSlot) v[u] = sval[sl[u]], st[u] = sst[sl[u]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (sl[u] != kNoSlot) put_reply(rv, origin_base + (uint32_t)(i0 + u * stride), v[u], st[u]);
+  }
 }
 
 // ---------------------------------------------------------------- host
 void Mailboxes::send_sorted(const MboxSend& a) {
   const uint32_t S = shards();
   if (S > (uint32_t)kMboxSortMaxShards) throw std::invalid_argument("sorted mailboxes: at most 1024 shards");
+  if ((uint64_t)S * slots() > 0xfffffffeull) throw std::invalid_argument("sorted mailboxes: shards * slots < 2^32");
   if (started_ && running()) throw std::runtime_error("mailbox send: a persistent consumer owns the rings");
   if (a.M <= 0) return;
   if (!a.actor || !a.a0) throw std::invalid_argument("mailbox send: missing column");
@@ -605,6 +533,27 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   if (a.arrival && a.ordered) throw std::invalid_argument("mailbox send: arrival sharding cannot serve ordered methods");
   PT_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = as_stream(a.stream);
+  // per-message workspace (route words, ring slots): grown outside graph capture
+  if ((uint64_t)a.M > sort_cap_) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("mailbox send: a larger batch than before inside a graph capture (warm up first)");
+    PT_HIP_CHECK(hipStreamSynchronize(st));
+    if (sort_rw_) PT_HIP_CHECK(hipFree(sort_rw_));
+    if (sort_sidx_) PT_HIP_CHECK(hipFree(sort_sidx_));
+    PT_HIP_CHECK(hipMalloc((void**)&sort_rw_, (size_t)a.M * 4));
+    PT_HIP_CHECK(hipMalloc((void**)&sort_sidx_, (size_t)a.M * 4));
+    sort_cap_ = (uint64_t)a.M;
+  }
+  if (a.ordered && !stage_val_) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("mailbox send: first ordered Send inside a graph capture (warm up first)");
+    const uint64_t n = (uint64_t)S * slots();
+    PT_HIP_CHECK(hipMalloc((void**)&stage_val_, n * 8));
+    PT_HIP_CHECK(hipMalloc((void**)&stage_st_, n * 4));
+    bytes_ += n * 12;
+  }
   SortIn in{};
   in.actor = (const uint32_t*)a.actor;
   in.a0 = (const int64_t*)a.a0;
@@ -624,37 +573,42 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   const int64_t tiles = (a.M + kSTile - 1) / kSTile;
   if (tiles > 0xffffffffll) throw std::invalid_argument("mailbox send: batch too large");
   in.tiles = (uint32_t)tiles;
-  // blocks: as many as the histogram holds (it stays L2-resident for the scan),
+  // blocks: as many as the histogram holds (it stays L2-resident for the prefixes),
   // a multiple of 8 (one contiguous eighth of the batch per XCD)
   static const int64_t g_env = getenv("PTYPE_SORT_BLOCKS") ? atoll(getenv("PTYPE_SORT_BLOCKS")) : 0;
-  int64_t G = std::min<int64_t>({tiles, (int64_t)(kMboxSortHistWords / S), g_env > 0 ? g_env : (int64_t)1024});
+  int64_t G = std::min<int64_t>({tiles, (int64_t)(kMboxSortHistWords / S), g_env > 0 ? g_env : (int64_t)1024,
+                                 (int64_t)kMboxSortGroups * kGroupBlocks});
   if (G >= 8) G -= G % 8;
   G = std::max<int64_t>(G, 1);
   in.G = (uint32_t)G;
   in.tpb = (uint32_t)((tiles + G - 1) / G);
+  const uint32_t ngroups = (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks);
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
   const ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
-#define PT_SORT_K(KERNEL, MO, AR, ...) hipLaunchKernelGGL((KERNEL<MO, AR>), __VA_ARGS__)
-#define PT_SORT(KERNEL, ...)                                             \
-  do {                                                                   \
-    if (a.arrival) {                                                     \
-      if (mode == 2) PT_SORT_K(KERNEL, 2, true, __VA_ARGS__);            \
-      else if (mode == 1) PT_SORT_K(KERNEL, 1, true, __VA_ARGS__);       \
-      else PT_SORT_K(KERNEL, 0, true, __VA_ARGS__);                      \
-    } else {                                                             \
-      if (mode == 2) PT_SORT_K(KERNEL, 2, false, __VA_ARGS__);           \
-      else if (mode == 1) PT_SORT_K(KERNEL, 1, false, __VA_ARGS__);      \
-      else PT_SORT_K(KERNEL, 0, false, __VA_ARGS__);                     \
-    }                                                                    \
+#define PT_COUNT(MO, AR) \
+  hipLaunchKernelGGL((mbx_count_kernel<MO, AR>), dim3(in.G), dim3(kST), 0, st, in, mv_.log_s, sort_hist_, sort_gsum_, sort_rw_)
+  if (a.arrival) {
+    if (mode == 2) PT_COUNT(2, true); else if (mode == 1) PT_COUNT(1, true); else PT_COUNT(0, true);
+  } else {
+    if (mode == 2) PT_COUNT(2, false); else if (mode == 1) PT_COUNT(1, false); else PT_COUNT(0, false);
+  }
+#undef PT_COUNT
+  PT_HIP_CHECK(hipGetLastError());
+#define PT_SCAT(AR, A2, MC)                                                                                      \
+  hipLaunchKernelGGL((mbx_scatter_kernel<AR, A2, MC>), dim3(in.G), dim3(kST), 0, st, in, mv_,                   \
+                     (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_, sort_sidx_, rv)
+#define PT_SCAT_AR(AR)                                  \
+  do {                                                  \
+    if (a.a2 && a.method_col) PT_SCAT(AR, true, true);   \
+    else if (a.a2) PT_SCAT(AR, true, false);            \
+    else if (a.method_col) PT_SCAT(AR, false, true);    \
+    else PT_SCAT(AR, false, false);                     \
   } while (0)
-  PT_SORT(mbx_count_kernel, dim3(in.G), dim3(kST), 0, st, in, mv_.log_s, sort_hist_);
+  if (a.arrival) PT_SCAT_AR(true);
+  else PT_SCAT_AR(false);
+#undef PT_SCAT_AR
+#undef PT_SCAT
   PT_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(mbx_scan_kernel, dim3((S + 63) / 64), dim3(1024), 0, st, sort_hist_, in.G, mv_.log_s, sort_tot_);
-  PT_HIP_CHECK(hipGetLastError());
-  PT_SORT(mbx_scatter_kernel, dim3(in.G), dim3(kST), 0, st, in, mv_, (const uint32_t*)sort_hist_, rv);
-  PT_HIP_CHECK(hipGetLastError());
-#undef PT_SORT
-#undef PT_SORT_K
   OutboxView ob;
   if (a.outbox_cap) {
     if (a.outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
@@ -674,17 +628,23 @@ void Mailboxes::send_sorted(const MboxSend& a) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       attr = true;
     }
-    hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(S), dim3(kOrdThreads), lds, st, mv_, (const uint32_t*)sort_tot_,
-                       (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv);
+    hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(S), dim3(kOrdThreads), lds, st, mv_, sort_gsum_, ngroups,
+                       (int64_t*)a.state, a.n_state, a.delay_ticks, ob, stage_val_, stage_st_);
+    PT_HIP_CHECK(hipGetLastError());
+    const unsigned gc = (unsigned)std::min<int64_t>(std::max<int64_t>((a.M + 1023) / 1024, 1), 2048);
+    hipLaunchKernelGGL(mbx_complete_kernel, dim3(gc), dim3(256), 0, st, (const uint32_t*)sort_sidx_, a.M,
+                       a.origin_base, (const int64_t*)stage_val_, (const int32_t*)stage_st_, rv);
   } else {
-    // X parts per shard, a multiple of 8 (XCD-aware), ~2048 blocks in all
-    const uint32_t X = 8u * std::max<uint32_t>(1u, 256u / S);
+    const unsigned gd = (unsigned)std::min<int64_t>(std::max<int64_t>((a.M + kDrainThreads * kDrainK - 1) /
+                                                                          (kDrainThreads * kDrainK), 1), 4096);
     if (a.fixed_method == kCalculatorMultiply)
-      hipLaunchKernelGGL((mbx_drain_par_kernel<kCalculatorMultiply>), dim3(X * S), dim3(kDrainThreads), 0, st, mv_,
-                         (const uint32_t*)sort_tot_, X, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv);
+      hipLaunchKernelGGL((mbx_drain_msg_kernel<kCalculatorMultiply>), dim3(gd), dim3(kDrainThreads), 0, st, mv_,
+                         (const uint32_t*)sort_sidx_, a.M, a.origin_base, (int64_t*)a.state, a.n_state,
+                         a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_);
     else
-      hipLaunchKernelGGL((mbx_drain_par_kernel<0>), dim3(X * S), dim3(kDrainThreads), 0, st, mv_,
-                         (const uint32_t*)sort_tot_, X, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv);
+      hipLaunchKernelGGL((mbx_drain_msg_kernel<0>), dim3(gd), dim3(kDrainThreads), 0, st, mv_,
+                         (const uint32_t*)sort_sidx_, a.M, a.origin_base, (int64_t*)a.state, a.n_state,
+                         a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_);
   }
   PT_HIP_CHECK(hipGetLastError());
 }

@@ -1,0 +1,122 @@
+// Counting-sort building blocks shared by the sorted epoch mailboxes
+// (mailbox_sort.hip) and the sorted exchange (exchange_sorted.hip): a batch is
+// cut into tiles of kSTile messages, each block owns a contiguous range of tiles
+// (XCD-grouped, see virt_block), messages are resolved against the registry
+// mirror, and a message's rank within its (tile, bucket) is computed in MESSAGE
+// order by a wave match on the bucket bits plus per-wave counts -- a stable sort
+// with no atomic per message.
+#pragma once
+#include "common.hpp"
+#include "route_common.hpp"
+
+namespace ptype {
+
+constexpr int kST = 256;             // count / scatter threads per block
+constexpr int kSK = 8;               // messages per thread per tile
+constexpr int kSTile = kST * kSK;    // 2048 messages
+constexpr int kSWave = kSK * kWave;  // a wave's contiguous run of a tile (512)
+
+
+struct SortIn {  // by value
+  const uint32_t* actor;
+  const int64_t* a0;
+  const int64_t* a1;
+  const int64_t* a2;
+  const uint16_t* mcol;
+  uint32_t method_uniform;
+  int64_t M;
+  const TableEntry* table;
+  uint64_t mask;
+  const uint32_t* dir;
+  uint32_t n_dir;
+  uint32_t aw;
+  int aw_shift;
+  int rank_self;
+  uint32_t origin_base;
+  uint32_t G;      // blocks
+  uint32_t tiles;  // ceil(M / kSTile)
+  uint32_t tpb;    // tiles per block
+};
+
+// Block b's range: XCD (b % 8) owns virtual blocks [x * G/8, (x+1) * G/8).
+__device__ __forceinline__ uint32_t virt_block(uint32_t b, uint32_t G) {
+  return (G >= 8 && (G & 7) == 0) ? (b & 7) * (G >> 3) + (b >> 3) : b;
+}
+
+template <int MODE>
+__device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[kSK], int (&r)[kSK],
+                                          uint32_t (&mb)[kSK]) {
+  if constexpr (MODE == 1) {
+    uint32_t w[kSK];
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) w[k] = a[k] < in.n_dir ? in.dir[a[k]] : kDirFallback;
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
+      mb[k] = w[k] >> 8;
+      if (w[k] == kDirFallback) {
+        if (a[k] != 0xffffffffu) lookup_entry(in.table, in.mask, actor_key(a[k]), r[k], mb[k]);
+        else r[k] = -1;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      if (MODE == 2 && a[k] < in.n_dir) {
+        r[k] = in.aw_shift >= 0 ? (int)(a[k] & (in.aw - 1)) : (int)(a[k] % in.aw);
+        mb[k] = in.aw_shift >= 0 ? a[k] >> in.aw_shift : a[k] / in.aw;
+      } else if (a[k] == 0xffffffffu) {
+        r[k] = -1;
+        mb[k] = 0;
+      } else {
+        lookup_entry(in.table, in.mask, actor_key(a[k]), r[k], mb[k]);
+      }
+    }
+  }
+}
+
+// Message i of tile t for (item k, lane) of wave w: a wave owns a contiguous run
+// of the tile, so message order within a tile is (wave, item, lane).
+__device__ __forceinline__ int64_t tile_index(uint32_t t, int k) {
+  return (int64_t)t * kSTile + (threadIdx.x / kWave) * kSWave + k * kWave + lane_id();
+}
+
+__device__ __forceinline__ void load_actors(const SortIn& in, uint32_t t, uint32_t (&a)[kSK]) {
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    const int64_t i = tile_index(t, k);
+    a[k] = i < in.M ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
+  }
+}
+
+// Lanes of this wave whose `key` (log_bits bits) equals this lane's, among `act`.
+__device__ __forceinline__ uint64_t match_bits(uint32_t key, uint32_t log_bits, uint64_t act) {
+  uint64_t m = act;
+  for (uint32_t b = 0; b < log_bits; ++b) {
+    const uint64_t bb = __ballot((key >> b) & 1u);
+    m &= ((key >> b) & 1u) ? bb : ~bb;
+  }
+  return m;
+}
+
+// A tile's raw inputs, loaded one tile ahead of their use.
+struct SortTileIn {
+  uint32_t a[kSK];
+  int64_t x0[kSK], x1[kSK], x2[kSK];
+};
+
+__device__ __forceinline__ void load_args(const SortIn& in, uint32_t t, SortTileIn& x) {
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    const int64_t i = tile_index(t, k);
+    const bool ok = i < in.M;
+    x.a[k] = ok ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
+    x.x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
+    x.x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    x.x2[k] = ok && in.a2 ? __builtin_nontemporal_load(in.a2 + i) : 0;
+  }
+}
+
+__device__ __forceinline__ bool fits_i32(int64_t v) { return v == (int64_t)(int32_t)v; }
+
+}  // namespace ptype

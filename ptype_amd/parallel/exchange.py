@@ -188,6 +188,7 @@ class ActorExchange:
         self._last_mailbox = True  # whether the last send went through the mailboxes (until known: assume so)
         self._pump_graph = None  # (key, hipGraph of a group of device-pump epochs, its buffers)
         self.last_wire = None  # engine.last_wire() of the latest native send
+        self._sorted = None  # _hip.SortedExchange: N > 1 mailbox delivery (csrc/hip/exchange_sorted.hpp)
 
     def _comm_ptr(self) -> int:
         """Raw ncclComm_t of the group's RCCL backend (0 without collectives)."""
@@ -248,6 +249,53 @@ class ActorExchange:
             w = self._engine.last_wire()
             self.last_wire = w
             self.counters.wire_bytes += self.chunks * 4 * (w["req_words"] + w["rep_words"])
+        return out_val, out_status
+
+    def _use_sorted(self) -> bool:
+        """Mailbox delivery across ranks through the sorted exchange: the sender's
+        counting sort by (destination rank, actor shard) fills the receivers'
+        mailboxes directly, with no host wait per Send (csrc/hip/exchange_sorted.hpp).
+        PTYPE_SORTED_EXCHANGE=0 keeps the epoch engine's delivery on receipt."""
+        if self.delivery != "mailbox" or not self.use_engine or self.device.type != "cuda":
+            return False
+        if self.outbox is not None or self.checksum is not None or self.chunks > 4:
+            return False
+        if not (1 < self.world <= 16 or self.force_collectives):
+            return False
+        return os.environ.get("PTYPE_SORTED_EXCHANGE", "1") != "0"
+
+    def _get_sorted(self):
+        if self._sorted is None:
+            h = B.hip()
+            dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            # the buffers hold 2.5x the uniform share per peer (skewed traffic fits); the
+            # start-up capacity is the static mean + 8 sigma
+            room = float(os.environ.get("PTYPE_SORTED_ROOM", "2.5"))
+            c_alloc = max(64, self.C, min(self.max_chunk, int(math.ceil(room * self.max_chunk / self.world))))
+            fake = self.fake[0] if self.fake is not None else None
+            self._sorted = h.SortedExchange(dev, 0 if fake is not None else self._comm_ptr(), self.world, self.rank,
+                                            self.max_chunk, self.chunks, c_alloc, min(self.C, c_alloc), fake=fake)
+            self._sorted_c_alloc = c_alloc
+        return self._sorted
+
+    def _send_sorted(self, req: B.MsgBatch, out_val, out_status):
+        if req.actor.dtype != torch.int32 or req.a0.dtype != torch.int64:
+            raise TypeError("MsgBatch: actor must be int32 and a0..a2 int64")
+        uniform = isinstance(req.method, int)
+        mcol = None if uniform else req.method.to(torch.int16).contiguous()
+        d, n_dir, affine = self.table.directory()
+        state = self.state
+        eng = self._get_sorted()
+        eng.send(B._ptr(req.actor), B._ptr(req.a0), B._ptr(req.a1), B._ptr(req.a2), B._ptr(mcol),
+                 int(req.method) if uniform else 0, req.M, B._ptr(self.table.table), self.table.cap, B._ptr(d), n_dir,
+                 affine, B._ptr(out_val), B._ptr(out_status), B._ptr(state), 0 if state is None else state.numel(),
+                 int(self.delay_us) * 100, self.mailbox_ordered, torch.cuda.current_stream(self.device).cuda_stream)
+        w = eng.last_wire()
+        w["req_words"] *= self.world  # all peers, per chunk (as the epoch engine reports it)
+        w["rep_words"] *= self.world
+        w.update(engine="sorted", exact=False, adapted=bool(w["agreed"]), C_alloc=self._sorted_c_alloc)
+        self.last_wire = w
+        self.counters.wire_bytes += self.chunks * 4 * (w["req_words"] + w["rep_words"])
         return out_val, out_status
 
     def _mailbox_on_receipt(self) -> bool:
@@ -322,6 +370,9 @@ class ActorExchange:
         if self._last_mailbox:
             with trace.range("ptype.send.mailbox"):
                 return self._send_mailbox(req, out_val, out_status)
+        if self.use_engine and self._use_sorted():
+            with trace.range("ptype.send.sorted"):
+                return self._send_sorted(req, out_val, out_status)
         if self.use_engine and self._engine is None:
             try:
                 self._get_engine()
@@ -596,6 +647,10 @@ class ActorExchange:
             s.toowide += int(b.ws[B.STAT_TOOWIDE])
             if w[B.STAT_ROUTE_ERROR]:
                 raise RuntimeError("route look-back stalled: epoch results are invalid")
+        if self._sorted is not None:
+            f = self._sorted.stats()
+            s.failed += int(f[0])
+            s.toowide += int(f[1])
         if self.mailboxes is not None:
             m = self.mailboxes.stats()
             s.nomatch += m["no_actor"]

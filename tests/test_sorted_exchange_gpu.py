@@ -1,0 +1,157 @@
+"""Sorted exchange (csrc/hip/exchange_sorted.hpp) on MI355X: the multi-GPU Send
+with mailbox delivery, run on one GPU as R in-process ranks (FakeComm: one host
+thread + stream per rank, the all-to-alls as device copies between them).
+
+* calculator replies exact across Sends 0-1 (start-up wide layout) and 2+
+  (layout and capacity agreed two Sends earlier -- no host wait per Send);
+* ordered SeqFold traffic from every rank to every rank's actors: every actor's
+  replies chain exactly once (audit_fold) and each (sender, actor) pair ran in
+  message order;
+* a message wider than the layout in force is answered STATUS_OVERFLOW (its slot
+  carries a null record) and send_all re-sends it until the agreed layout grows.
+"""
+import threading
+
+import pytest
+import torch
+
+from ptype_amd.ops import batch as B
+from ptype_amd.ops import hip
+from ptype_amd.ops.mailbox import audit_fold
+from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_SEQ_FOLD, STATUS_OK, STATUS_OVERFLOW
+from ptype_amd.ops.table import RegistryTable, actor_keys
+from ptype_amd.parallel.exchange import ActorExchange
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_ranks(R, body, timeout=240):
+    fc = hip().FakeComm(R)
+    res, errors = [None] * R, []
+    start = threading.Barrier(R)
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                res[r] = body(r, fc, start, s)
+        except BaseException as e:  # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    ths = [threading.Thread(target=run, args=(r,)) for r in range(R)]
+    [t.start() for t in ths]
+    [t.join(timeout=timeout) for t in ths]
+    assert not errors, errors
+    return res
+
+
+def _table(n, R):
+    tab = RegistryTable(2 * n, device="cuda")
+    ids = torch.arange(n)
+    g = torch.Generator().manual_seed(99)
+    slot = torch.randperm(n, generator=g)  # random placement: routes read the mirror
+    tab.upsert(actor_keys(ids), (slot % R).to(torch.int32), (slot // R).to(torch.int32))
+    tab.enable_directory(n)
+    return tab, slot
+
+
+@pytest.mark.parametrize("R,chunks", [(2, 1), (3, 2), (4, 2)])
+def test_sorted_exchange_calculator_exact_across_layouts(R, chunks):
+    n, M = 8192, 100_000
+
+    def body(r, fc, start, s):
+        tab, _ = _table(n, R)
+        st = torch.zeros(n // R + 1, dtype=torch.int64, device="cuda")
+        ex = ActorExchange(tab, M, chunks=chunks, state=st, fake=(fc, r), delivery="mailbox", mailbox_ordered=False)
+        start.wait()
+        wires = []
+        for k in range(5):
+            req = B.gen_requests(M - 777 * r, n, METHOD_CALC_MULTIPLY, seed=40 + 7 * r + k, device="cuda")
+            v, sts = ex.send(req)
+            s.synchronize()
+            assert bool((sts == STATUS_OK).all()), (k, int((sts != STATUS_OK).sum()))
+            assert torch.equal(v, req.a0 * req.a1)
+            wires.append(dict(ex.last_wire))
+        return wires
+
+    res = _run_ranks(R, body)
+    for wires in res:
+        assert wires[0]["engine"] == "sorted" and not wires[0]["agreed"] and wires[0]["S"] == 8
+        assert wires[2]["agreed"] and wires[2]["spec_from"] == 0 and wires[4]["spec_from"] == 2
+        assert wires[2]["S"] <= 2 and wires[2]["vb"] == 4  # 16-bit args, 17-bit mailboxes: 8-B records
+    assert len({w[3]["C"] for w in res}) == 1  # every rank derived the same geometry
+
+
+@pytest.mark.parametrize("R", [2, 4])
+def test_sorted_exchange_ordered_seqfold_fifo_per_sender(R):
+    n, M = 4096, 60_000
+
+    def fold(M, seed):
+        g = torch.Generator().manual_seed(seed)
+        return B.MsgBatch(torch.randint(0, n, (M,), generator=g, dtype=torch.int32).cuda(),
+                          torch.randint(-(1 << 20), 1 << 20, (M,), generator=g, dtype=torch.int64).cuda(),
+                          None, None, METHOD_SEQ_FOLD)
+
+    states0 = [torch.randint(0, 1 << 30, (n // R + 1,), dtype=torch.int64,
+                             generator=torch.Generator().manual_seed(r)) for r in range(R)]
+
+    def body(r, fc, start, s):
+        tab, slot = _table(n, R)
+        st = states0[r].cuda()
+        ex = ActorExchange(tab, M, chunks=2, state=st, fake=(fc, r), delivery="mailbox")
+        start.wait()
+        out = []
+        for k in range(3):  # Sends 0-1 wide, Send 2 agreed
+            req = fold(M, 500 + 10 * r + k)
+            v, sts = ex.send(req)
+            s.synchronize()
+            out.append((req.actor.cpu().long(), req.a0.cpu(), v.cpu(), sts.cpu()))
+        return out, st.cpu(), slot
+
+    res = _run_ranks(R, body)
+    slot = res[0][2]
+    P = n // R + 1
+    # global mailbox key of an actor: owner rank * P + local mailbox
+    key_of = lambda a: (slot[a] % R) * P + slot[a] // R  # noqa: E731
+    before = torch.cat(states0)
+    after = torch.cat([x[1] for x in res])
+    actor = torch.cat([torch.cat([o[k][0] for k in range(3)]) for o, _, _ in res])
+    a0 = torch.cat([torch.cat([o[k][1] for k in range(3)]) for o, _, _ in res])
+    v = torch.cat([torch.cat([o[k][2] for k in range(3)]) for o, _, _ in res])
+    sts = torch.cat([torch.cat([o[k][3] for k in range(3)]) for o, _, _ in res])
+    ok, order = audit_fold(key_of(actor), a0, v, sts, before, after)
+    assert ok, order
+    # per (sender, actor): message order (senders' messages are concatenated rank-major, Send-major)
+    sizes = [sum(len(o[k][0]) for k in range(3)) for o, _, _ in res]
+    bounds = torch.cumsum(torch.tensor([0] + sizes), 0)
+    for x, seq in list(order.items())[:256]:
+        for r in range(R):
+            mine = [i for i in seq if bounds[r] <= i < bounds[r + 1]]
+            assert mine == sorted(mine), f"actor {x}: sender {r}'s messages out of order"
+
+
+def test_sorted_exchange_too_wide_is_overflow_then_resent():
+    R, n, M = 2, 4096, 20_000
+
+    def body(r, fc, start, s):
+        tab, _ = _table(n, R)
+        st = torch.zeros(n // R + 1, dtype=torch.int64, device="cuda")
+        ex = ActorExchange(tab, M, chunks=1, state=st, fake=(fc, r), delivery="mailbox", mailbox_ordered=False)
+        start.wait()
+        for k in range(3):  # settle a narrow layout (16-bit arguments)
+            req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=3 + k + 10 * r, device="cuda")
+            ex.send(req)
+        s.synchronize()
+        wide = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=77 + r, device="cuda")
+        wide.a0[::100] = 1 << 40  # 1 % of the messages need 42-bit arguments
+        v, sts = ex.send(wide)
+        s.synchronize()
+        first = sts.clone()
+        v, sts = ex.send_all(wide)  # re-sends until the agreed layout holds them
+        s.synchronize()
+        return first.cpu(), v.cpu(), sts.cpu(), (wide.a0 * wide.a1).cpu(), ex.counters.resends
+
+    for first, v, sts, ref, resends in _run_ranks(R, body):
+        assert int((first == STATUS_OVERFLOW).sum()) == len(first[::100])
+        assert bool((sts == STATUS_OK).all()) and torch.equal(v, ref) and resends >= 1
