@@ -41,6 +41,7 @@ enum RecordFlags : uint16_t {
   kFlagRouted = 2,  // `actor` holds the destination's local mailbox index
   kFlagIdentity = 4,  // slot header: slot position == message index (R = 1, no gaps)
   kFlagA2 = 8,        // mailbox record: the third argument is in the ring's a2 side array
+  kFlagSharded = 16,  // sorted-exchange region header: records sorted by actor shard (shard table at its end)
 };
 
 enum ReplyStatus : int32_t {

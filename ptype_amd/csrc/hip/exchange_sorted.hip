@@ -41,14 +41,15 @@ __device__ __forceinline__ bool sx_fits(const PackedLayout& L, uint32_t meth, ui
   return fits(2, z0) && fits(3, z1) && fits(4, z2);
 }
 
-// Whether the received regions of a chunk may hold ordered methods: a method
-// column on the wire, or a sender whose uniform method is ordered.
-__device__ __forceinline__ bool sx_need_order(const uint32_t* recv, int64_t req_stride, int R, const PackedLayout& L) {
-  if (L.w[0]) return true;
-  for (int p = 0; p < R; ++p) {
-    const uint32_t hw = recv[(int64_t)p * req_stride + 3];
-    if (((hw >> 16) & kFlagValid) && recv[(int64_t)p * req_stride] && method_ordered(hw & 0xffffu)) return true;
-  }
+// A received region sorted by actor shard (its sender's batch may carry ordered
+// methods): served by the ordered drain; every other region by the parallel one.
+__device__ __forceinline__ bool sx_sharded(const uint32_t* region) {
+  const uint32_t hw = region[3];
+  return ((hw >> 16) & kFlagValid) && ((hw >> 16) & kFlagSharded) && region[0];
+}
+__device__ __forceinline__ bool sx_any_sharded(const uint32_t* recv, int64_t req_stride, int R) {
+  for (int p = 0; p < R; ++p)
+    if (sx_sharded(recv + (int64_t)p * req_stride)) return true;
   return false;
 }
 
@@ -62,11 +63,11 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // ---------------------------------------------------------------- sender: count
 template <int MODE>
-__global__ __launch_bounds__(kST) void sx_count_kernel(SortIn in, int R, uint32_t* __restrict__ hist,
+__global__ __launch_bounds__(kST) void sx_count_kernel(SortIn in, int R, uint32_t K, uint32_t* __restrict__ hist,
                                                        unsigned long long* __restrict__ meta) {
   __shared__ uint32_t cnt[kXMaxBuckets];
   __shared__ uint32_t mbmax_s;
-  const uint32_t B = (uint32_t)R * kSxShards;
+  const uint32_t B = (uint32_t)R * K;
   const uint32_t v = virt_block(blockIdx.x, in.G);
   for (uint32_t b = threadIdx.x; b < B; b += kST) cnt[b] = 0;
   if (threadIdx.x == 0) mbmax_s = 0;
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(kST) void sx_count_kernel(SortIn in, int R, uint32_
 #pragma unroll
     for (int k = 0; k < kSK; ++k)
       if (r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox) {
-        atomicAdd(&cnt[(uint32_t)r[k] * kSxShards + (mb[k] & (kSxShards - 1))], 1u);
+        atomicAdd(&cnt[(uint32_t)r[k] * K + (mb[k] & (K - 1))], 1u);
         mbmax = mb[k] > mbmax ? mb[k] : mbmax;
       }
   }
@@ -95,19 +96,43 @@ __global__ __launch_bounds__(kST) void sx_count_kernel(SortIn in, int R, uint32_
 }
 
 // ---------------------------------------------------------------- sender: scan + region tables
-// Block d owns region d's 64 shard columns of hist [G][R * 64]: exclusive prefix
-// over blocks (in place), then the shard offsets within the region, its shard
-// table (clamped to C) and header, and the region total into meta[kMetaCap].
-__global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hist, uint32_t G, int R,
+// Block d owns region d's K bucket columns of hist [G][R * K] (K = 64 actor
+// shards when the sender's batch may carry ordered methods, else 1): exclusive
+// prefix over blocks (in place), the buckets' offsets within the region, its
+// shard table (clamped to C) and header, and the region total into meta[kMetaCap].
+__global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hist, uint32_t G, int R, uint32_t K,
                                                        uint32_t* __restrict__ sendbuf, int64_t req_stride,
                                                        int64_t tab_off, uint32_t C, uint32_t method_uniform,
                                                        uint32_t hdr_flags, int rank_self,
                                                        unsigned long long* __restrict__ meta,
                                                        uint32_t* __restrict__ boff) {
   __shared__ uint32_t part[16][64];
-  const uint32_t B = (uint32_t)R * kSxShards;
+  __shared__ uint32_t wsum[16];
+  const uint32_t B = (uint32_t)R * K;
+  const uint32_t d = blockIdx.x;
+  uint32_t* region = sendbuf + (int64_t)d * req_stride;
+  if (K == 1) {  // one column: every thread a row (G <= 1024), a block-wide scan
+    const uint32_t r = threadIdx.x, w = r / kWave, lane = lane_id();
+    const uint32_t x = r < G ? hist[(size_t)r * B + d] : 0u;
+    const uint32_t inc = wave_incl_scan(x);
+    if (lane == kWave - 1) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = inc - x;
+    for (uint32_t j = 0; j < w; ++j) off += wsum[j];
+    if (r < G) hist[(size_t)r * B + d] = off;
+    if (r == blockDim.x - 1) {
+      const uint32_t all = off + x;
+      const uint32_t n = all < C ? all : C;
+      boff[d] = 0;
+      region[tab_off] = 0;
+      for (int s = 1; s <= kSxShards; ++s) region[tab_off + s] = n;
+      *reinterpret_cast<uint4*>(region) = make_uint4(n, all, (uint32_t)rank_self, (hdr_flags << 16) | method_uniform);
+      if (all) meta_max(meta + kMetaCap, all);
+    }
+    return;
+  }
   const uint32_t lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const uint32_t d = blockIdx.x, c = d * kSxShards + lane;
+  const uint32_t c = d * K + lane;
   const uint32_t rows = (G + 15) / 16, r0 = min(G, g * rows), r1 = min(G, r0 + rows);
   uint32_t sum = 0;
   {
@@ -138,7 +163,6 @@ __global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hi
     const uint32_t off = inc - total;
     const uint32_t all = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     boff[c] = off;
-    uint32_t* region = sendbuf + (int64_t)d * req_stride;
     region[tab_off + lane] = off < C ? off : C;
     if (lane == 0) {
       const uint32_t n = all < C ? all : C;
@@ -151,7 +175,7 @@ __global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hi
 
 // ---------------------------------------------------------------- sender: scatter
 template <int MODE, int S>
-__global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, const uint32_t* __restrict__ hist,
+__global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint32_t K, const uint32_t* __restrict__ hist,
                                                          const uint32_t* __restrict__ boff,
                                                          uint32_t* __restrict__ sendbuf, int64_t req_stride,
                                                          uint32_t C, PackedLayout L, int32_t* __restrict__ perm,
@@ -159,8 +183,8 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, const
   __shared__ uint32_t run[kXMaxBuckets];
   __shared__ uint32_t bo[kXMaxBuckets];
   __shared__ uint32_t wcnt[kST / kWave][kXMaxBuckets];
-  const uint32_t B = (uint32_t)R * kSxShards;
-  const uint32_t bbits = 32 - __builtin_clz(B - 1);  // bucket index bits (B >= 64)
+  const uint32_t B = (uint32_t)R * K;
+  const uint32_t bbits = B > 1 ? 32 - __builtin_clz(B - 1) : 0;  // bucket index bits
   const uint32_t v = virt_block(blockIdx.x, in.G);
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
   for (uint32_t b = threadIdx.x; b < B; b += kST) {
@@ -190,7 +214,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, const
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       ok[k] = r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
-      bk[k] = ok[k] ? (uint32_t)r[k] * kSxShards + (mb[k] & (kSxShards - 1)) : 0u;
+      bk[k] = ok[k] ? (uint32_t)r[k] * K + (mb[k] & (K - 1)) : 0u;
       if (ok[k]) {
         const uint64_t z0 = zz_enc(v0[k]), z1 = zz_enc(v1[k]), z2 = zz_enc(v2[k]);
         acc.z0 = z0 > acc.z0 ? z0 : acc.z0;
@@ -330,9 +354,9 @@ __global__ __launch_bounds__(256) void sx_drain_par_kernel(const uint32_t* __res
                                                            uint32_t* __restrict__ reply, int64_t rep_stride,
                                                            int64_t* __restrict__ state, uint32_t n_state,
                                                            uint64_t delay_ticks, unsigned long long* __restrict__ stats) {
-  if (may_order && sx_need_order(recv, req_stride, R, L)) return;  // the ordered drain serves this chunk
   const int p = blockIdx.y;
   const uint32_t* rq = recv + (int64_t)p * req_stride;
+  if (may_order && sx_sharded(rq)) return;  // the ordered drain serves this region
   const uint4 h = *reinterpret_cast<const uint4*>(rq);
   const int64_t count = ((h.w >> 16) & kFlagValid) ? (int64_t)(h.x < C ? h.x : C) : 0;
   const uint32_t hm = h.w & 0xffffu;
@@ -359,8 +383,8 @@ __global__ __launch_bounds__(256) void sx_drain_par_kernel(const uint32_t* __res
 __global__ __launch_bounds__(256) void sx_reply_init_kernel(const uint32_t* __restrict__ recv, int64_t req_stride,
                                                             int64_t C, PackedLayout L, int R,
                                                             uint32_t* __restrict__ reply, int64_t rep_stride) {
-  if (!sx_need_order(recv, req_stride, R, L)) return;
   const int p = blockIdx.x;
+  if (!sx_sharded(recv + (int64_t)p * req_stride)) return;
   const uint4 h = *reinterpret_cast<const uint4*>(recv + (int64_t)p * req_stride);
   const int64_t count = ((h.w >> 16) & kFlagValid) ? (int64_t)(h.x < C ? h.x : C) : 0;
   uint32_t* rp = reply + (int64_t)p * rep_stride;
@@ -387,7 +411,7 @@ __global__ __launch_bounds__(kXOrdThreads) void sx_drain_ord_kernel(const uint32
                                                                     int64_t* __restrict__ state, uint32_t n_state,
                                                                     uint64_t delay_ticks,
                                                                     unsigned long long* __restrict__ stats) {
-  if (!sx_need_order(recv, req_stride, R, L)) return;
+  if (!sx_any_sharded(recv, req_stride, R)) return;
   extern __shared__ __align__(16) unsigned char smem_sx[];
   SxOrdLds& Ls = *reinterpret_cast<SxOrdLds*>(smem_sx);
   int64_t* st_lds = reinterpret_cast<int64_t*>(smem_sx + sizeof(SxOrdLds));
@@ -402,8 +426,8 @@ __global__ __launch_bounds__(kXOrdThreads) void sx_drain_ord_kernel(const uint32
   unsigned long long failed = 0;
   for (int p = 0; p < R; ++p) {  // source-rank order: every (sender, actor) pair stays FIFO
     const uint32_t* rq = recv + (int64_t)p * req_stride;
+    if (!sx_sharded(rq)) continue;  // (a region of a batch without ordered methods: the parallel drain's)
     const uint4 h = *reinterpret_cast<const uint4*>(rq);
-    if (!((h.w >> 16) & kFlagValid)) continue;
     const int64_t count = (int64_t)(h.x < C ? h.x : C);
     const uint32_t hm = h.w & 0xffffu;
     const uint32_t lo = min((int64_t)rq[tab_off + s], count), hi = min((int64_t)rq[tab_off + s + 1], count);
@@ -658,8 +682,12 @@ void SortedExchange::send(const SxSend& a) {
   uint64_t* meta = meta_dev_ + cur * kMetaWords;
   PT_HIP_CHECK(hipMemsetAsync(meta, 0, kMetaWords * sizeof(uint64_t), cs));
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
-  const uint32_t B = (uint32_t)R_ * kSxShards;
   const bool may_order = a.ordered;
+  // sort by actor shard only when this rank's batch may carry ordered methods;
+  // otherwise by rank alone (a region is then one FIFO queue of this sender)
+  const bool sharded = may_order && (a.method_col != 0 || method_ordered((uint32_t)a.method_uniform));
+  const uint32_t K = sharded ? (uint32_t)kSxShards : 1u;
+  const uint32_t B = (uint32_t)R_ * K;
   auto chunk_in = [&](int i, int64_t& lo, int64_t& m) {
     lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
     m = std::min<int64_t>(a.M, lo + max_chunk_) - lo;
@@ -747,12 +775,13 @@ void SortedExchange::send(const SxSend& a) {
     else if (mode == 1) hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__); \
     else hipLaunchKernelGGL((KERNEL<0>), __VA_ARGS__);               \
   } while (0)
-    PT_SX_MODE(sx_count_kernel, dim3(in.G), dim3(kST), 0, cs, in, R_, hist_, (unsigned long long*)meta);
-    hipLaunchKernelGGL(sx_scan_kernel, dim3(R_), dim3(1024), 0, cs, hist_, in.G, R_, b.send, rq, tab_off, (uint32_t)C,
-                       (uint32_t)a.method_uniform, (uint32_t)kFlagValid, rank_, (unsigned long long*)meta, boff_);
+    PT_SX_MODE(sx_count_kernel, dim3(in.G), dim3(kST), 0, cs, in, R_, K, hist_, (unsigned long long*)meta);
+    hipLaunchKernelGGL(sx_scan_kernel, dim3(R_), dim3(1024), 0, cs, hist_, in.G, R_, K, b.send, rq, tab_off,
+                       (uint32_t)C, (uint32_t)a.method_uniform,
+                       (uint32_t)(kFlagValid | (sharded ? kFlagSharded : 0)), rank_, (unsigned long long*)meta, boff_);
 #undef PT_SX_MODE
 #define PT_SX_SCAT(MO, SV)                                                                                       \
-  hipLaunchKernelGGL((sx_scatter_kernel<MO, SV>), dim3(in.G), dim3(kST), 0, cs, in, R_, (const uint32_t*)hist_, \
+  hipLaunchKernelGGL((sx_scatter_kernel<MO, SV>), dim3(in.G), dim3(kST), 0, cs, in, R_, K, (const uint32_t*)hist_, \
                      (const uint32_t*)boff_, b.send, rq, (uint32_t)C, L, b.perm, (unsigned long long*)meta)
 #define PT_SX_SCAT_S(MO)            \
   switch (S) {                      \

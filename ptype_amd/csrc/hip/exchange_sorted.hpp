@@ -1,20 +1,21 @@
 // Sorted exchange: the multi-GPU Send with mailbox delivery, where the sender's
 // counting sort does the receiver's enqueue.
 //
-// Every rank sorts its batch stably by (destination rank, destination actor
-// shard) straight into the per-peer request regions of the all-to-all (count /
-// scan / scatter, the building blocks of sort_common.hpp).  A region therefore
-// arrives as the SENDER'S part of the receiver's actor mailboxes: 64 shard runs
-// (an actor's messages in message order within its run) and a shard table.  The
-// receiver runs no enqueue pass at all -- its drain reads the received regions
-// as its mailboxes:
-//   * parallel drain (batches without ordered methods): every record of every
-//     region runs independently, replies land at the record's position of the
-//     reply region (coalesced);
-//   * ordered drain: one block per shard takes that shard's runs of every source
-//     region in source-rank order, actors' state in LDS, each actor's records
-//     one at a time in ring order (LDS bins), so every (sender, actor) pair is
-//     FIFO.
+// Every rank sorts its batch stably straight into the per-peer request regions
+// of the all-to-all (count / scan / scatter, the building blocks of
+// sort_common.hpp): by destination rank alone when its batch carries no ordered
+// method, by (destination rank, destination actor shard) when it may.  A region
+// therefore arrives as the SENDER'S part of the receiver's actor mailboxes --
+// one message-ordered queue, or 64 shard runs (an actor's messages in message
+// order within its run) plus a shard table (header flag kFlagSharded).  The
+// receiver runs no enqueue pass at all -- its drains read the received regions
+// as its mailboxes, chosen per region:
+//   * parallel drain (unsharded regions): every record runs independently,
+//     replies land at the record's position of the reply region (coalesced);
+//   * ordered drain (sharded regions): one block per shard takes that shard's
+//     runs of every sharded region in source-rank order, actors' state in LDS,
+//     each actor's records one at a time in ring order (LDS bins), so every
+//     (sender, actor) pair is FIFO.
 // The sender's completion gathers each message's reply through the position
 // the scatter recorded (perm).  Per message on the wire: the wire-v3 packed
 // record (packed.hpp) and a packed reply.
@@ -109,8 +110,8 @@ class SortedExchange {
   int64_t max_chunk_, C_alloc_;
   hipStream_t comm_stream_ = nullptr;
   Bufs bufs_[kSxMaxChunks];
-  uint32_t* hist_ = nullptr;  // [G][R * 64] per-block bucket counts -> prefixes
-  uint32_t* boff_ = nullptr;  // [R * 64] bucket offsets within their region
+  uint32_t* hist_ = nullptr;  // [G][R * K] per-block bucket counts -> prefixes (K = 64 or 1)
+  uint32_t* boff_ = nullptr;  // [R * K] bucket offsets within their region
   uint64_t* meta_dev_ = nullptr;   // [2][kMetaWords] agreement vectors (device)
   uint64_t* meta_host_ = nullptr;  // [2][kMetaWords] pinned copies
   unsigned long long* stats_ = nullptr;  // [2] receiver counters

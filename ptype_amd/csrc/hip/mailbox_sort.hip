@@ -61,8 +61,6 @@ constexpr int kOrdK = 4;
 constexpr int kOrdWin = kOrdThreads * kOrdK;  // records per window (2048)
 constexpr int kOrdWaves = kOrdThreads / kWave;
 constexpr uint32_t kOrdStateMax = 4096;  // a shard's actors whose state is staged in LDS (32 KB)
-constexpr int kDrainThreads = 256;
-constexpr int kDrainK = 4;
 }  // namespace
 
 // ---------------------------------------------------------------- K2s pass 1: count
@@ -155,20 +153,17 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
   }
   unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0;
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
-  uint32_t nm[kSK], nmeth[kSK];
-  int64_t n0[kSK], n1[kSK], n2[kSK];
-  if (t0 < t1) load_routed<A2, MC>(in, rw, t0, nm, n0, n1, n2, nmeth);
   for (uint32_t t = t0; t < t1; ++t) {
     for (uint32_t s = lane; s < S; s += kWave) wcnt[w][s] = 0;  // this wave's row only
+    // (no next-tile prefetch: the double buffer cost the occupancy that hides these loads better)
     uint32_t mb[kSK], meth[kSK];
     int64_t v0[kSK], v1[kSK], v2[kSK];
+    load_routed<A2, MC>(in, rw, t, mb, v0, v1, v2, meth);
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
-      mb[k] = nm[k], v0[k] = n0[k], v1[k] = n1[k];
-      v2[k] = A2 ? n2[k] : 0;
-      meth[k] = MC ? nmeth[k] : in.method_uniform;
+      if (!A2) v2[k] = 0;
+      if (!MC) meth[k] = in.method_uniform;
     }
-    if (t + 1 < t1) load_routed<A2, MC>(in, rw, t + 1, nm, n0, n1, n2, nmeth);  // in flight across the barriers
     // rank of each message among this wave's earlier messages of its shard
     uint32_t wr[kSK], sh[kSK];
 #pragma unroll
@@ -305,39 +300,41 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 // scatter recorded) -- the record reads are gathers, the replies land
 // coalesced.  The last block commits every shard (and clears the group sums).
 template <int FIXED>
-__global__ __launch_bounds__(kDrainThreads) void mbx_drain_msg_kernel(MboxView mv, const uint32_t* __restrict__ sidx,
-                                                                      int64_t M, uint32_t origin_base,
-                                                                      int64_t* __restrict__ state, uint32_t n_state,
-                                                                      uint64_t delay_ticks, OutboxView ob, ReplyView rv,
-                                                                      uint32_t* __restrict__ gsum, uint32_t ngroups,
-                                                                      unsigned* __restrict__ ticket) {
+__global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ sidx,
+                                                            int64_t* __restrict__ state, uint32_t n_state,
+                                                            uint64_t delay_ticks, OutboxView ob, ReplyView rv,
+                                                            uint32_t* __restrict__ gsum, uint32_t ngroups,
+                                                            unsigned* __restrict__ ticket) {
+  // the scatter's block -> tile ranges: a tile's records sit in ~S short runs that
+  // this block's waves read whole (line reuse in L1 / L2), not one record per block
   unsigned long long done = 0, failed = 0, holes = 0;
-  const int64_t stride = (int64_t)gridDim.x * kDrainThreads;
-  for (int64_t i0 = blockIdx.x * (int64_t)kDrainThreads + threadIdx.x; i0 < M; i0 += stride * kDrainK) {
-    uint32_t sl[kDrainK];
+  const uint32_t v = virt_block(blockIdx.x, in.G);
+  const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
+  for (uint32_t t = t0; t < t1; ++t) {
+    uint32_t sl[kSK];
 #pragma unroll
-    for (int u = 0; u < kDrainK; ++u) {
-      const int64_t i = i0 + u * stride;
-      sl[u] = i < M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
+    for (int k = 0; k < kSK; ++k) {
+      const int64_t i = tile_index(t, k);
+      sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
     }
-    u32x4 ha[kDrainK];
+    u32x4 ha[kSK];
 #pragma unroll
-    for (int u = 0; u < kDrainK; ++u)
-      ha[u] = sl[u] != kNoSlot ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[u])) : u32x4{0u, 0u, 0u, 0u};
+    for (int k = 0; k < kSK; ++k)
+      ha[k] = sl[k] != kNoSlot ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k])) : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int u = 0; u < kDrainK; ++u) {
-      if (sl[u] == kNoSlot) continue;  // answered by the scatter (no actor / ring full)
+    for (int k = 0; k < kSK; ++k) {
+      if (sl[k] == kNoSlot) continue;  // answered by the scatter (no actor / ring full)
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
-      if (rec_is_long(ha[u])) {
-        hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[u]));
-        if (((ha[u].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[u]];
+      if (rec_is_long(ha[k])) {
+        hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
+        if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
       }
-      const SortRec x = decode_sorted(ha[u], hb, a2v);
-      const int64_t i = i0 + u * stride;
+      const SortRec x = decode_sorted(ha[k], hb, a2v);
+      const uint32_t origin = in.origin_base + (uint32_t)tile_index(t, k);
       if (!x.valid) {
         ++holes;
-        write_status(rv, origin_base + (uint32_t)i, kStatusNotDelivered);
+        write_status(rv, origin, kStatusNotDelivered);
         continue;
       }
       MsgRecord m;
@@ -347,7 +344,7 @@ __global__ __launch_bounds__(kDrainThreads) void mbx_drain_msg_kernel(MboxView m
       m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
       const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
       failed += rr.status != kStatusOk;
-      write_reply(rv, origin_base + (uint32_t)i, rr);
+      write_reply(rv, origin, rr);
       ++done;
     }
   }
@@ -357,7 +354,7 @@ __global__ __launch_bounds__(kDrainThreads) void mbx_drain_msg_kernel(MboxView m
   __syncthreads();
   if (last) {  // every block's records are read: the rings are consumed
     const uint32_t S = 1u << mv.log_s;
-    for (uint32_t s = threadIdx.x; s < S; s += kDrainThreads) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
+    for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
   }
 }
 
@@ -635,16 +632,14 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     hipLaunchKernelGGL(mbx_complete_kernel, dim3(gc), dim3(256), 0, st, (const uint32_t*)sort_sidx_, a.M,
                        a.origin_base, (const int64_t*)stage_val_, (const int32_t*)stage_st_, rv);
   } else {
-    const unsigned gd = (unsigned)std::min<int64_t>(std::max<int64_t>((a.M + kDrainThreads * kDrainK - 1) /
-                                                                          (kDrainThreads * kDrainK), 1), 4096);
     if (a.fixed_method == kCalculatorMultiply)
-      hipLaunchKernelGGL((mbx_drain_msg_kernel<kCalculatorMultiply>), dim3(gd), dim3(kDrainThreads), 0, st, mv_,
-                         (const uint32_t*)sort_sidx_, a.M, a.origin_base, (int64_t*)a.state, a.n_state,
-                         a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_);
+      hipLaunchKernelGGL((mbx_drain_msg_kernel<kCalculatorMultiply>), dim3(in.G), dim3(kST), 0, st, mv_, in,
+                         (const uint32_t*)sort_sidx_, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_,
+                         ngroups, sort_ticket_);
     else
-      hipLaunchKernelGGL((mbx_drain_msg_kernel<0>), dim3(gd), dim3(kDrainThreads), 0, st, mv_,
-                         (const uint32_t*)sort_sidx_, a.M, a.origin_base, (int64_t*)a.state, a.n_state,
-                         a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_);
+      hipLaunchKernelGGL((mbx_drain_msg_kernel<0>), dim3(in.G), dim3(kST), 0, st, mv_, in,
+                         (const uint32_t*)sort_sidx_, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_,
+                         ngroups, sort_ticket_);
   }
   PT_HIP_CHECK(hipGetLastError());
 }

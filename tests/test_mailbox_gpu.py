@@ -185,7 +185,7 @@ def test_mailbox_send_graph_replay():
 
 
 @pytest.mark.parametrize("R,ordered,packed", [(4, True, True), (3, False, True), (4, True, False), (3, False, False)])
-def test_mailbox_delivery_on_receipt_multirank(R, ordered, packed):
+def test_mailbox_delivery_on_receipt_multirank(R, ordered, packed, monkeypatch):
     """N > 1: every rank's received records go through its HBM mailboxes (K2 on
     receipt from the request regions, K3 into the reply regions), on the engine's
     real multi-rank pipeline (FakeComm ranks, one GPU).  Ordered: SeqFold traffic
@@ -197,6 +197,8 @@ def test_mailbox_delivery_on_receipt_multirank(R, ordered, packed):
 
     from ptype_amd.ops import hip
 
+    # the epoch engine's delivery on receipt (the sorted exchange is tested in test_sorted_exchange_gpu.py)
+    monkeypatch.setenv("PTYPE_SORTED_EXCHANGE", "0")
     n, M = 4096, 60_000
     fc = hip().FakeComm(R)
     res, errors = [None] * R, []

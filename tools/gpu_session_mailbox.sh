@@ -4,8 +4,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 420 python -u -m pytest tests/test_mailbox_gpu.py tests/test_sorted_exchange_gpu.py -v --timeout 150 --timeout-method thread > gpurun_out/r3_mb_tests.log 2>&1
-echo "tests rc=$?"
+rc=$?; echo "tests rc=$rc"
 grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/r3_mb_tests.log | tail -40
+[ $rc -le 1 ] || exit $rc  # a crash / time limit: nothing more on the GPU
 timeout -k 10 240 python bench.py --steps 20 --warmup 8 > gpurun_out/r3_bench.json 2> gpurun_out/r3_bench.err
 rc=$?; echo "bench rc=$rc"; head -c 4000 gpurun_out/r3_bench.json
 [ $rc -eq 0 ] || exit $rc
