@@ -193,41 +193,25 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
   }
   MetaAcc acc;
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
-  SortTileIn x;
-  if (t0 < t1) load_args(in, t0, x);
   for (uint32_t t = t0; t < t1; ++t) {
     for (uint32_t b = lane; b < B; b += kWave) wcnt[w][b] = 0;
+    // phase 1: routes and ranks only (a small register file: occupancy hides the loads)
+    uint32_t a[kSK];
+    load_actors(in, t, a);
     int r[kSK];
     uint32_t mb[kSK];
-    resolve_k<MODE>(in, x.a, r, mb);
-    int64_t v0[kSK], v1[kSK], v2[kSK];
-    uint32_t meth[kSK];
-#pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      v0[k] = x.x0[k], v1[k] = x.x1[k], v2[k] = x.x2[k];
-      const int64_t i = tile_index(t, k);
-      meth[k] = in.mcol && i < in.M ? (uint32_t)in.mcol[i] : in.method_uniform;
-    }
-    if (t + 1 < t1) load_args(in, t + 1, x);
+    resolve_k<MODE>(in, a, r, mb);
     uint32_t wr[kSK], bk[kSK];
-    bool ok[kSK];
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
-      ok[k] = r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
-      bk[k] = ok[k] ? (uint32_t)r[k] * K + (mb[k] & (K - 1)) : 0u;
-      if (ok[k]) {
-        const uint64_t z0 = zz_enc(v0[k]), z1 = zz_enc(v1[k]), z2 = zz_enc(v2[k]);
-        acc.z0 = z0 > acc.z0 ? z0 : acc.z0;
-        acc.z1 = z1 > acc.z1 ? z1 : acc.z1;
-        acc.z2 = z2 > acc.z2 ? z2 : acc.z2;
-        acc.mm = meth[k] > acc.mm ? meth[k] : acc.mm;
-        acc.flags |= 1u << (meth[k] < 7 ? meth[k] : 7);
-      }
-      const uint64_t peers = match_bits(bk[k], bbits, __ballot(ok[k]));
+      const bool ok = r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
+      if (!ok) r[k] = -1;
+      bk[k] = ok ? (uint32_t)r[k] * K + (mb[k] & (K - 1)) : 0u;
+      const uint64_t peers = match_bits(bk[k], bbits, __ballot(ok));
       const unsigned below = mbcnt64(peers);
       const int leader = peers ? __builtin_ctzll(peers) : 0;
       unsigned old = 0;
-      if (ok[k] && below == 0) {
+      if (ok && below == 0) {
         old = wcnt[w][bk[k]];
         wcnt[w][bk[k]] = old + (unsigned)__popcll(peers);
       }
@@ -245,11 +229,12 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
       run[b] = rr;
     }
     __syncthreads();
+    // phase 2: each message's arguments, packed at its position
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       const int64_t i = tile_index(t, k);
       if (i >= in.M) continue;
-      if (!ok[k]) {
+      if (r[k] < 0) {
         perm[i] = -2;  // no such actor: the completion answers kStatusNoActor
         continue;
       }
@@ -258,11 +243,20 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
         perm[i] = -1;
         continue;
       }
-      const uint64_t z0 = zz_enc(v0[k]), z1 = zz_enc(v1[k]), z2 = zz_enc(v2[k]);
+      const int64_t x0 = __builtin_nontemporal_load(in.a0 + i);
+      const int64_t x1 = in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+      const int64_t x2 = in.a2 ? __builtin_nontemporal_load(in.a2 + i) : 0;
+      const uint32_t meth = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
+      const uint64_t z0 = zz_enc(x0), z1 = zz_enc(x1), z2 = zz_enc(x2);
+      acc.z0 = z0 > acc.z0 ? z0 : acc.z0;
+      acc.z1 = z1 > acc.z1 ? z1 : acc.z1;
+      acc.z2 = z2 > acc.z2 ? z2 : acc.z2;
+      acc.mm = meth > acc.mm ? meth : acc.mm;
+      acc.flags |= 1u << (meth < 7 ? meth : 7);
       uint64_t f[5];
-      const bool fit = sx_fits(L, meth[k], in.method_uniform, mb[k], z0, z1, z2);
+      const bool fit = sx_fits(L, meth, in.method_uniform, mb[k], z0, z1, z2);
       if (fit) {
-        f[0] = meth[k], f[1] = mb[k], f[2] = z0, f[3] = z1, f[4] = z2;
+        f[0] = meth, f[1] = mb[k], f[2] = z0, f[3] = z1, f[4] = z2;
         perm[i] = (int32_t)((uint32_t)r[k] * C + pos);
       } else {  // wider than the layout in force: a null record holds the slot
         f[0] = 0, f[1] = low_mask(L.w[1]), f[2] = 0, f[3] = 0, f[4] = 0;

@@ -110,6 +110,9 @@ __global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_
 }
 
 // ---------------------------------------------------------------- K2s pass 2: scatter
+// The tile's arguments are loaded with its route words, before the ranking (in
+// flight across it).  Loading them only once the ranks are known (a smaller
+// register file, occupancy 4 -> 5) measured slower: 124 -> 164 us per 8 Mi.
 template <bool A2, bool MC>
 __device__ __forceinline__ void load_routed(const SortIn& in, const uint32_t* __restrict__ rw, uint32_t t,
                                             uint32_t (&m)[kSK], int64_t (&x0)[kSK], int64_t (&x1)[kSK],
@@ -121,7 +124,9 @@ __device__ __forceinline__ void load_routed(const SortIn& in, const uint32_t* __
     m[k] = ok ? __builtin_nontemporal_load(rw + i) : kNoSlot;
     x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
     x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    x2[k] = 0;
     if constexpr (A2) x2[k] = ok ? __builtin_nontemporal_load(in.a2 + i) : 0;
+    meth[k] = in.method_uniform;
     if constexpr (MC) meth[k] = ok ? (uint32_t)in.mcol[i] : 0u;
   }
 }
@@ -131,11 +136,14 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
                                                           const uint32_t* __restrict__ gsum,
                                                           const uint32_t* __restrict__ rw,
                                                           uint32_t* __restrict__ sidx, ReplyView rv) {
-  __shared__ uint32_t run[kMboxSortMaxShards];   // this block's next offset per shard
-  __shared__ uint32_t room[kMboxSortMaxShards];  // offset limit per shard (free ring slots)
-  __shared__ unsigned long long base[kMboxSortMaxShards];  // ring position of offset 0 (the tail)
-  __shared__ uint32_t wcnt[kST / kWave][kMboxSortMaxShards];  // per-wave counts -> wave offsets
+  // LDS sized by the shard count (32 B per shard): occupancy is not capped by the 1024-shard maximum
+  extern __shared__ __align__(16) unsigned char smem_sc[];
   const uint32_t S = 1u << mv.log_s;
+  unsigned long long* base = reinterpret_cast<unsigned long long*>(smem_sc);  // ring position of offset 0 (tail)
+  uint32_t* run = reinterpret_cast<uint32_t*>(base + S);                       // this block's next offset per shard
+  uint32_t* room = run + S;                                                    // offset limit (free ring slots)
+  uint32_t* wcnt_all = room + S;  // [kST / kWave][S] per-wave counts -> wave offsets
+  auto wcnt = [&](unsigned ww, uint32_t sh) -> uint32_t& { return wcnt_all[ww * S + sh]; };
   const uint64_t Q = 1ull << mv.log_q;
   const uint32_t v = virt_block(blockIdx.x, in.G);
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
@@ -154,16 +162,10 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
   unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0;
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
   for (uint32_t t = t0; t < t1; ++t) {
-    for (uint32_t s = lane; s < S; s += kWave) wcnt[w][s] = 0;  // this wave's row only
-    // (no next-tile prefetch: the double buffer cost the occupancy that hides these loads better)
+    for (uint32_t s = lane; s < S; s += kWave) wcnt(w, s) = 0;  // this wave's row only
     uint32_t mb[kSK], meth[kSK];
     int64_t v0[kSK], v1[kSK], v2[kSK];
     load_routed<A2, MC>(in, rw, t, mb, v0, v1, v2, meth);
-#pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      if (!A2) v2[k] = 0;
-      if (!MC) meth[k] = in.method_uniform;
-    }
     // rank of each message among this wave's earlier messages of its shard
     uint32_t wr[kSK], sh[kSK];
 #pragma unroll
@@ -176,8 +178,8 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
       const int leader = peers ? __builtin_ctzll(peers) : 0;
       unsigned old = 0;
       if (ok && below == 0) {  // group leader: one plain LDS read-add per distinct shard of the wave
-        old = wcnt[w][sh[k]];
-        wcnt[w][sh[k]] = old + (unsigned)__popcll(peers);
+        old = wcnt(w, sh[k]);
+        wcnt(w, sh[k]) = old + (unsigned)__popcll(peers);
       }
       wr[k] = (unsigned)__shfl((int)old, leader) + below;
     }
@@ -186,8 +188,8 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
       uint32_t rr = run[s];
 #pragma unroll
       for (int ww = 0; ww < kST / kWave; ++ww) {
-        const uint32_t c = wcnt[ww][s];
-        wcnt[ww][s] = rr;
+        const uint32_t c = wcnt(ww, s);
+        wcnt(ww, s) = rr;
         rr += c;
       }
       run[s] = rr;
@@ -204,26 +206,28 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
         write_status(rv, origin, kStatusNoActor);
         continue;
       }
-      const uint32_t off = wcnt[w][sh[k]] + wr[k];
+      const uint32_t off = wcnt(w, sh[k]) + wr[k];
       if (off >= room[sh[k]]) {  // the ring is full: answered now, re-sent by send_all
         ++n_ovf;
         sidx[i] = kNoSlot;
         write_status(rv, origin, kStatusOverflow);
         continue;
       }
+      const int64_t x0 = v0[k], x1 = v1[k], x2 = v2[k];
+      const uint32_t mt = meth[k];
       const uint64_t slot = slot_at(mv, sh[k], base[sh[k]] + off);
       sidx[i] = (uint32_t)slot;
-      const bool compact = meth[k] < 128u && fits_i32(v0[k]) && fits_i32(v1[k]) && v2[k] == 0;
+      const bool compact = mt < 128u && fits_i32(x0) && fits_i32(x1) && x2 == 0;
       if (compact) {
         *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
-            u32x4{origin | kCompactMark, mb[k] | (meth[k] << 24), (uint32_t)v0[k], (uint32_t)v1[k]};
+            u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)x0, (uint32_t)x1};
       } else {
-        const uint32_t fl = v2[k] != 0 ? (uint32_t)kFlagA2 : 0u;
+        const uint32_t fl = x2 != 0 ? (uint32_t)kFlagA2 : 0u;
         *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
-            u32x4{origin | kCompactMark, mb[k] | kCompactLong, (meth[k] & 0xffffu) | (fl << 16), 0u};
+            u32x4{origin | kCompactMark, mb[k] | kCompactLong, (mt & 0xffffu) | (fl << 16), 0u};
         *reinterpret_cast<u32x4*>(rec_b(mv, slot)) =
-            u32x4{(uint32_t)v0[k], (uint32_t)((uint64_t)v0[k] >> 32), (uint32_t)v1[k], (uint32_t)((uint64_t)v1[k] >> 32)};
-        if (fl) mv.a2[slot] = v2[k];
+            u32x4{(uint32_t)x0, (uint32_t)((uint64_t)x0 >> 32), (uint32_t)x1, (uint32_t)((uint64_t)x1 >> 32)};
+        if (fl) mv.a2[slot] = x2;
       }
       ++n_enq;
     }
@@ -592,7 +596,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_COUNT
   PT_HIP_CHECK(hipGetLastError());
 #define PT_SCAT(AR, A2, MC)                                                                                      \
-  hipLaunchKernelGGL((mbx_scatter_kernel<AR, A2, MC>), dim3(in.G), dim3(kST), 0, st, in, mv_,                   \
+  hipLaunchKernelGGL((mbx_scatter_kernel<AR, A2, MC>), dim3(in.G), dim3(kST), (size_t)32 * S, st, in, mv_,                   \
                      (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_, sort_sidx_, rv)
 #define PT_SCAT_AR(AR)                                  \
   do {                                                  \
