@@ -326,6 +326,12 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("cpu", &GpuConfig::cpu)
       .def_readwrite("mailbox_shards", &GpuConfig::mailbox_shards)
       .def_readwrite("mailbox_slots", &GpuConfig::mailbox_slots)
+      .def_readwrite("elastic", &GpuConfig::elastic)
+      .def_readwrite("form_group", &GpuConfig::form_group)
+      .def_readwrite("group_timeout_s", &GpuConfig::group_timeout_s)
+      .def_readwrite("grace_s", &GpuConfig::grace_s)
+      .def_readwrite("send_timeout_s", &GpuConfig::send_timeout_s)
+      .def_readwrite("replicate_every", &GpuConfig::replicate_every)
       .def_readwrite("watch", &GpuConfig::watch);
   py::class_<MemberConfig, std::shared_ptr<MemberConfig>>(m, "MemberConfig")
       .def(py::init<>())

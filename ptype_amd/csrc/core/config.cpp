@@ -129,6 +129,12 @@ void decode_ptype(const YNode& root, Config& c) {
         else if (g.first == "mailbox_shards") c.gpu.mailbox_shards = (uint32_t)want_int(G, g.first, g.second);
         else if (g.first == "mailbox_slots") c.gpu.mailbox_slots = (uint32_t)want_int(G, g.first, g.second);
         else if (g.first == "watch") c.gpu.watch = want_bool(G, g.first, g.second);
+        else if (g.first == "elastic") c.gpu.elastic = want_bool(G, g.first, g.second);
+        else if (g.first == "form_group") c.gpu.form_group = want_bool(G, g.first, g.second);
+        else if (g.first == "group_timeout_s") c.gpu.group_timeout_s = want_float(G, g.first, g.second);
+        else if (g.first == "grace_s") c.gpu.grace_s = want_float(G, g.first, g.second);
+        else if (g.first == "send_timeout_s") c.gpu.send_timeout_s = want_float(G, g.first, g.second);
+        else if (g.first == "replicate_every") c.gpu.replicate_every = (uint32_t)want_int(G, g.first, g.second);
       }
       if (c.gpu.mailbox_shards == 0 || (c.gpu.mailbox_shards & (c.gpu.mailbox_shards - 1)))
         fail(Errc::kConfig, "gpu.mailbox_shards must be a power of two");

@@ -58,6 +58,13 @@ struct GpuConfig {
   uint32_t mailbox_shards = 256;
   uint32_t mailbox_slots = 0;  // 0: sized from max_batch
   bool watch = true;          // follow the store (shard records, leases) into the GPU registry mirror
+  // rank failures (runtime.py recover): Join's group re-forms through the store
+  bool elastic = true;          // recover a failed Send (abort, re-form, re-home, re-send)
+  bool form_group = false;      // form the group through the store even at world <= 1 (collectives forced)
+  double group_timeout_s = 10;  // collective timeout of the group (gloo; RCCL's is the send watchdog's)
+  double grace_s = 8;           // how long a recovery waits for the dead node's lease to lapse
+  double send_timeout_s = 30;   // GPU: a Send's device work overdue this long aborts the communicator
+  uint32_t replicate_every = 0; // buddy replicas of the actor state every N Sends (0: only on request)
 };
 
 struct Config {

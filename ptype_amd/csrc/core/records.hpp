@@ -51,6 +51,7 @@ enum ReplyStatus : int32_t {
   kStatusNoActor = 3,       // registry lookup miss
   kStatusOverflow = 4,      // epoch bucket full; message deferred to the next epoch
   kStatusNotDelivered = 5,  // reply slot never written
+  kStatusRankLost = 6,      // the actor's rank died with the message in flight (re-homed since: re-send)
 };
 
 struct alignas(16) MsgRecord {

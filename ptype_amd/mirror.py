@@ -23,6 +23,20 @@ read, the way the reference's clients follow ``WatchService``
 
 So a node that joins after this one becomes routable at the next Send, and one
 whose lease lapses disappears within TTL + the re-list period.
+
+After a rank failure (runtime.py ``recover``) the survivors form data-plane
+generation g + 1 and re-home the dead rank's actors (parallel/elastic.py
+``ring_placement``): a record then carries ``"gen"`` and ``"blocks"`` -- the
+original ranks whose actors the node hosts, block j in mailboxes
+``[j * count, (j + 1) * count)`` (actor ``b + world * k`` of original rank b in
+mailbox ``j * count + k``, ``world`` the original world).  The mirror drops the
+records of older generations without touching the table (the recovering
+runtime rebuilt it for the new placement), so a dead node's late DELETE can not
+unroute actors that were adopted meanwhile.
+
+``apply()`` is constant-time when nothing changed: the watch thread bumps a
+version on every event / re-list, and apply returns at once while the version
+is the one it applied and no shard deadline has passed.
 """
 from __future__ import annotations
 
@@ -49,6 +63,18 @@ def _now_ms() -> int:
     return int(time.monotonic() * 1000)
 
 
+def record_ids(rec: dict) -> tuple[torch.Tensor, torch.Tensor]:
+    """(actor ids, mailboxes) of a shard record: actor ``b + world * k`` of every
+    hosted original rank b (``blocks``, default ``[rank]``) in mailbox
+    ``j * count + k`` (j = the block's index)."""
+    P, W = int(rec["count"]), int(rec["world"])
+    blocks = rec.get("blocks") or [int(rec["rank"])]
+    k = torch.arange(P, dtype=torch.int64)
+    ids = torch.cat([int(b) + W * k for b in blocks])
+    mbox = torch.cat([j * P + k for j in range(len(blocks))])
+    return ids, mbox
+
+
 class ShardLease:
     """This node's shard record, attached to a lease kept alive until ``close()``
     (graceful close revokes it: the shard disappears at once)."""
@@ -69,6 +95,12 @@ class ShardLease:
     def _drain(self):
         while self._ka.recv(1.0) is not None or not self._ka.closed:
             pass
+
+    def update(self, **fields) -> None:
+        """Re-publish the record (same lease) with ``fields`` changed -- a new
+        data-plane generation's rank and hosted blocks."""
+        self.record = dict(self.record, **fields)
+        self.kv.put(self.key, json.dumps(self.record).encode(), self.lease)
 
     def stop_keepalive(self) -> None:
         """Stop refreshing without revoking: the record expires with the lease (a crash, for tests)."""
@@ -94,6 +126,10 @@ class RegistryMirror:
         self.ttl_ms, self.grace_ms, self.relist_s = int(ttl_ms), int(grace_ms), float(relist_s)
         self.shards: dict[str, dict] = {}  # applied: key -> {record, deadline}
         self.applies = 0
+        self.min_gen = 0  # records of older data-plane generations are ignored
+        self._version = 0  # bumped by the watch thread on every change it queues
+        self._applied = -1
+        self._next_expiry = 0
         self._lock = threading.Lock()
         self._pending: list[tuple[str, str, dict | None]] = []
         self._seen: dict[str, int] = {}  # key -> monotonic ms it was last listed (lease alive)
@@ -104,6 +140,7 @@ class RegistryMirror:
         for kv_ in res.kvs:
             self._pending.append(("PUT", kv_.key, json.loads(kv_.value)))
             self._seen[kv_.key] = now
+        self._version += 1
         self._stop = threading.Event()
         self._ctx = Context.with_cancel()
         self._watch = kv.watch(self._ctx, self.prefix, self._opts.end, res.rev + 1) if watch else None
@@ -125,6 +162,7 @@ class RegistryMirror:
                             else:
                                 self._pending.append(("DELETE", ev.kv.key, None))
                                 self._seen.pop(ev.kv.key, None)
+                        self._version += 1
             else:
                 self._stop.wait(min(0.1, self.relist_s))
             if time.monotonic() >= next_list:
@@ -147,13 +185,26 @@ class RegistryMirror:
                 if k not in listed and not any(p[1] == k for p in self._pending):
                     self._pending.append(("DELETE", k, None))  # a missed DELETE
                     self._seen.pop(k, None)
+            self._version += 1
 
     # ------------------------------------------------------------------ applied on the runtime's stream
-    def _ids(self, rec: dict) -> tuple[torch.Tensor, torch.Tensor]:
-        mbox = torch.arange(int(rec["count"]), dtype=torch.int64)
-        return int(rec["rank"]) + int(rec["world"]) * mbox, mbox
+    @staticmethod
+    def _ids(rec: dict) -> tuple[torch.Tensor, torch.Tensor]:
+        return record_ids(rec)
+
+    def set_generation(self, gen: int) -> None:
+        """Data-plane generation ``gen`` formed: forget the records of older ones
+        (without deleting their actors: the runtime re-homed them)."""
+        with self._lock:
+            self.min_gen = int(gen)
+            self._pending = [p for p in self._pending if p[0] == "DELETE" or int(p[2].get("gen", 0)) >= gen]
+            self._version += 1
+        for k in [k for k, sh in self.shards.items() if int(sh["record"].get("gen", 0)) < gen]:
+            self.shards.pop(k)
 
     def _put(self, key: str, rec: dict, deadline: int) -> None:
+        if int(rec.get("gen", 0)) < self.min_gen:
+            return
         old = self.shards.get(key)
         if old is not None and old["record"] != rec:
             self._delete(key)
@@ -172,10 +223,13 @@ class RegistryMirror:
     def apply(self) -> int:
         """Apply pending registry changes and expiries to the table; returns the
         number of shards added, changed or removed."""
+        now = _now_ms()
+        if self._version == self._applied and now < self._next_expiry:
+            return 0  # nothing new since the last apply (a plain int compare: no lock)
         with self._lock:
             ops, self._pending = self._pending, []
             seen = dict(self._seen)
-        now = _now_ms()
+            version = self._version
         changed = 0
         for op, key, rec in ops:
             if op == "PUT":
@@ -197,6 +251,8 @@ class RegistryMirror:
             changed += live_before - len(self.shards)
         if changed:
             self.applies += 1
+        self._applied = version
+        self._next_expiry = min((sh["deadline"] for sh in self.shards.values()), default=now + self.ttl_ms)
         return changed
 
     def wait_shards(self, n: int, timeout_s: float = 60.0) -> None:
@@ -212,7 +268,8 @@ class RegistryMirror:
 
     @property
     def actors(self) -> int:
-        return sum(int(sh["record"]["count"]) for sh in self.shards.values())
+        return sum(int(sh["record"]["count"]) * len(sh["record"].get("blocks") or [0])
+                   for sh in self.shards.values())
 
     def close(self) -> None:
         self._stop.set()

@@ -30,6 +30,7 @@ STATUS_FAILED = 2
 STATUS_NO_ACTOR = 3
 STATUS_OVERFLOW = 4
 STATUS_NOT_DELIVERED = 5
+STATUS_RANK_LOST = 6  # the actor's rank died with the message in flight (re-homed since: re-send)
 
 MSG_WORDS = 4    # int64 words per 32-B message record
 REPLY_WORDS = 2  # int64 words per 16-B reply record

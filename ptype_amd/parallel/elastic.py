@@ -24,6 +24,13 @@ never repaired in place -- it is aborted and a new *generation* is formed:
 5. the caller's batch is re-sent (``send_resilient``): delivery is
    at-least-once, as with the reference's client retries (rpc.go:107-116).
 
+The same recovery runs underneath ``Join -> NewClient -> Send``: the
+``DeviceRuntime`` of a group Join formed is elastic (runtime.py ``send`` /
+``recover`` / ``replicate``, built from the helpers below: ``abort_group``,
+``settle_membership``, ``ring_placement``, ``buddy``, ``lost_blocks`` and the
+``SendWatchdog`` that bounds an RCCL Send's device work).  ``ElasticDataPlane``
+is the standalone form (its own table and exchange, no registry mirror).
+
 Actor state survives a rank loss through **buddy replicas** kept in HBM:
 ``replicate()`` (collective; also run every ``replicate_every`` sends) ships
 every block a node hosts to its *buddy* -- the next surviving node after it in
@@ -85,6 +92,98 @@ def buddy(nodes0: list[str], members: list[str], node: str) -> str:
         if n in alive:
             return n
     return node
+
+
+def abort_group() -> None:
+    """Abort the default process group (a failed generation): RCCL's
+    communicator is aborted (kernels spinning on a dead peer return), gloo's
+    pairs are closed.  Never raises."""
+    if dist.is_initialized():
+        try:
+            dist.distributed_c10d._abort_process_group()
+        except Exception:
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+
+
+def settle_membership(alive, members: list[str], me: str, grace_s: float) -> list[str]:
+    """The next generation's proposal after a collective failed: wait (at most
+    ``grace_s``) until the lease-based membership ``alive()`` has dropped
+    somebody of ``members`` (the dead node's 2 s registry lease lapsing), then
+    keep the survivors in their old order (so ranks stay dense and ordered)."""
+    old = set(members)
+    deadline = time.monotonic() + grace_s
+    live = alive()
+    while set(live) >= old and time.monotonic() < deadline:  # nobody's lease has expired yet
+        time.sleep(0.1)
+        live = alive()
+    proposal = [n for n in members if n in set(live)]
+    if me not in proposal:
+        proposal = sorted(set(proposal) | {me})
+    return proposal
+
+
+def lost_blocks(nodes0: list[str], before: list[str], after: list[str]) -> list[int]:
+    """Original ranks whose host in generation ``before`` is not in ``after``."""
+    own = ring_placement(nodes0, before)
+    gone = set(before) - set(after)
+    return sorted(r for n in gone for r in own.get(n, []))
+
+
+class SendWatchdog:
+    """Bounds how long a Send's device work may stay incomplete (RCCL over xGMI
+    has no timeout of its own for the engine's collectives, which are issued on
+    the group's communicator outside torch's watchdog).  ``arm(event)`` after a
+    Send; a daemon thread polls the armed events and, when one is overdue,
+    aborts the communicator -- the RCCL kernels waiting on a dead peer return --
+    and marks the generation failed, so the next Send raises and recovers."""
+
+    def __init__(self, timeout_s: float, poll_s: float = 0.05):
+        import threading
+
+        self.timeout_s, self.poll_s = float(timeout_s), float(poll_s)
+        self.failed: str | None = None
+        self._q: list[tuple[object, float]] = []
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, daemon=True, name="ptype-send-watchdog")
+        self._th.start()
+
+    def arm(self, event) -> None:
+        with self._lock:
+            self._q.append((event, time.monotonic() + self.timeout_s))
+            if len(self._q) > 64:  # completed events are dropped by the thread; bound the backlog anyway
+                self._q = [x for x in self._q if not x[0].query()]
+
+    def reset(self) -> None:
+        with self._lock:
+            self._q = []
+        self.failed = None
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.poll_s):
+            with self._lock:
+                q = self._q
+            now = time.monotonic()
+            keep = []
+            for ev, dl in q:
+                if ev.query():
+                    continue
+                if now > dl and self.failed is None:
+                    self.failed = f"a Send's device work did not complete within {self.timeout_s:.1f} s"
+                    abort_group()
+                keep.append((ev, dl))
+            with self._lock:
+                if self._q is q:
+                    self._q = keep
+                else:  # armed meanwhile
+                    self._q = keep + self._q[len(q):]
+
+    def close(self) -> None:
+        self._stop.set()
+        self._th.join(1.0)
 
 
 class ElasticDataPlane:
@@ -247,27 +346,12 @@ class ElasticDataPlane:
         """Abort the failed generation, wait for the lease-driven membership to
         settle, form the next generation from the survivors, re-home actors."""
         self._abort()
-        old = set(self.members)
-        deadline = time.monotonic() + self.grace_s
-        alive = self.alive()
-        while set(alive) >= old and time.monotonic() < deadline:  # nobody's lease has expired yet
-            time.sleep(0.1)
-            alive = self.alive()
-        proposal = [n for n in self.members if n in set(alive)]
-        if self.me not in proposal:
-            proposal = sorted(set(proposal) | {self.me})
+        proposal = settle_membership(self.alive, self.members, self.me, self.grace_s)
         self.recoveries += 1
         self._form(self.gen + 1, proposal)
 
     def _abort(self) -> None:
-        if dist.is_initialized():
-            try:
-                dist.distributed_c10d._abort_process_group()
-            except Exception:
-                try:
-                    dist.destroy_process_group()
-                except Exception:
-                    pass
+        abort_group()
         self.exchange = None
 
     def close(self) -> None:

@@ -20,12 +20,27 @@ actors = 2M slots = 32 MB of HBM).  ``mirror.RegistryMirror`` follows those
 records (watch + lease expiry) into the table; with ``gpu.world > 1`` Join
 forms the data-plane group through the store first (parallel/bootstrap.py).
 
+Rank failures.  A runtime whose group Join formed is elastic:
+when a Send's collective fails (gloo: reset / timeout; RCCL: the send watchdog
+aborts a communicator whose work is overdue), the runtime aborts the group,
+waits for the registry's lease-based membership to drop the dead node, forms
+generation g + 1 of the group through the store (bootstrap.form_group), re-homes
+the dead rank's actors onto its ring successor (state from the buddy replica
+``replicate()`` keeps, else zero), republishes its shard record and re-sends:
+``send_all`` re-sends the whole batch (at-least-once, like the reference
+client's retries, cluster/rpc.go:107-116); ``send(..., resend_overflow=False)``
+answers the messages whose actor lived on the lost rank with
+``STATUS_RANK_LOST`` and delivers the rest.  The reference's client survives a
+dead node the same way: lease lapse (cluster/registry.go:51-86), watch re-list
+(:119-150), balancer re-selection (cluster/rpc.go:197-244).
+
 Reference: the reference has no device side; this realises SURVEY C9/C10/C14
 under the API of cluster/cluster.go and cluster/rpc.go.
 """
 from __future__ import annotations
 
 import json
+import logging
 import os
 import time
 
@@ -33,11 +48,12 @@ import torch
 
 from .ops import batch as B
 from .ops import hip
-from .ops.records import STATUS_OK
+from .ops.records import STATUS_OK, STATUS_RANK_LOST
 from .ops.table import RegistryTable, actor_keys
 from .utils import trace
 
 ACTORS_PREFIX = "_ptype/actors"
+_log = logging.getLogger("ptype.runtime")
 
 
 def _dist():
@@ -81,11 +97,24 @@ class DeviceRuntime:
             self.server = hip().DeviceServer(self.device.index or 0, int(ring), self.state.data_ptr(), self.actors,
                                              self.delay_us, float(idle_ms), 60.0,
                                              f"ptype-{os.getpid()}-{self.device.index or 0}" if shm else "")
+        self._ring, self._idle_ms = int(ring), float(idle_ms)
         self.table = RegistryTable(2 * self.actors * self.world, device=self.device)
         # dense actor ids [0, actors*world): route through the compiled directory (K5b)
         self.table.enable_directory(self.actors * self.world, affine_world=self.world)
         self.max_batch = int(max_batch)
-        self.chunks = chunks or (1 if self.world == 1 else 4)
+        # 2 pipeline chunks at N > 1: the measured optimum at R = 2, 4 and 8 (profiles/r2_chunk_model)
+        self.chunks = chunks or (1 if self.world == 1 else 2)
+        # elasticity (set by for_cluster when Join formed the group)
+        self.world0 = self.world    # the original world: actor a belongs to original rank a % world0
+        self.blocks = [self.rank]   # original ranks whose actors this process hosts (mailbox-block order)
+        self.membership = None      # {"me", "nodes0", "members", "gen"} of the group Join formed
+        self._elastic_cfg = None
+        self.replicas: dict[int, torch.Tensor] = {}  # original rank -> its block as of the last replicate()
+        self.restored: list[int] = []
+        self.recoveries = 0
+        self.replicate_every = 0
+        self._sends = 0
+        self._watchdog = None
         self.mailbox_shards, self.mailbox_slots = int(mailbox_shards), int(mailbox_slots)
         self._exchange = None
         self.shards: dict[str, list[dict]] = {}
@@ -119,15 +148,19 @@ class DeviceRuntime:
             lr = os.environ.get("LOCAL_RANK")
             return torch.device("cuda", int(lr) if lr is not None else r % max(ndev, 1))
 
-        if g.world > 1 and not (dist.is_available() and dist.is_initialized()):
+        members = None
+        if (g.world > 1 or g.form_group) and not (dist.is_available() and dist.is_initialized()):
             from .parallel.bootstrap import form_group, node_id, wait_nodes
 
             me = node_id(core_cluster.local_addr, cfg.port)
             registry = Registry(core_cluster.registry)
-            nodes = wait_nodes(registry, cfg.service_name, g.world)
+            nodes = wait_nodes(registry, cfg.service_name, max(g.world, 1))
             backend = g.backend or ("gloo" if g.cpu else "nccl")
-            members, tcp = form_group(KVStore(core_cluster.store), core_cluster.local_addr, me, cfg.service_name, 0,
-                                      nodes, backend, device_for_rank)
+            store = KVStore(core_cluster.store)
+            if backend == "nccl":  # a failed collective aborts the communicator instead of the process
+                os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+            members, tcp = form_group(store, core_cluster.local_addr, me, cfg.service_name, 0, nodes, backend,
+                                      device_for_rank, timeout_s=g.group_timeout_s)
             owns = True
         d = _dist()
         rank = d.get_rank() if d else 0
@@ -135,6 +168,16 @@ class DeviceRuntime:
                  max_batch=g.max_batch, service=cfg.service_name, mailbox_shards=g.mailbox_shards,
                  mailbox_slots=g.mailbox_slots)
         rt._tcp_store, rt._owns_group = tcp, owns
+        if members is not None and g.elastic:
+            rt.membership = {"me": me, "nodes0": list(members), "members": list(members), "gen": 0}
+            rt._elastic_cfg = {"store": store, "registry": registry, "local_addr": core_cluster.local_addr,
+                               "backend": backend, "timeout_s": g.group_timeout_s, "grace_s": g.grace_s,
+                               "max_recoveries": 3}
+            rt.replicate_every = int(g.replicate_every)
+            if g.send_timeout_s > 0:  # (arms device events on a GPU; on the host it only carries a failure flag)
+                from .parallel.elastic import SendWatchdog
+
+                rt._watchdog = SendWatchdog(g.send_timeout_s)
         rt.attach(core_cluster.registry.kv, cfg.service_name, cfg.node_name, watch=g.watch)
         # Send needs every rank's routes: wait until all shards of the group are mirrored
         rt.mirror.wait_shards(rt.world)
@@ -151,6 +194,7 @@ class DeviceRuntime:
         self.table.clear()
         self.mirror = RegistryMirror(self.table, kv, service, watch=watch)
         self.mirror.apply()
+        self._kv, self._node = kv, node
 
     def sync(self) -> int:
         """Apply pending registry changes (joins, leaves, lease expiries) now."""
@@ -198,7 +242,12 @@ class DeviceRuntime:
 
     @property
     def total_actors(self) -> int:
-        return self.actors * self.world
+        return self.actors * self.world0
+
+    @property
+    def mailboxes(self) -> int:
+        """Mailboxes this process hosts (``actors`` per hosted block)."""
+        return self.state.numel()
 
     @property
     def exchange(self):
@@ -225,13 +274,147 @@ class DeviceRuntime:
     def send(self, service: str | None, batch: B.MsgBatch, resend_overflow: bool = True):
         """Batched Send: every message to its actor anywhere in the node and the
         replies back in message order.  Collective across the process group.
-        Registry changes seen since the last Send are applied first."""
+        Registry changes seen since the last Send are applied first.  With an
+        elastic group a rank failure is recovered here (module docstring)."""
         self._check_service(service)
         self.sync()
-        ex = self.exchange
-        if resend_overflow:
-            return ex.send_all(batch)
-        return ex.send(batch)
+        if self.membership is None:
+            ex = self.exchange
+            return ex.send_all(batch) if resend_overflow else ex.send(batch)
+        lost_before: list[int] = []
+        todo = None  # after a recovery without re-sends: the indices still to deliver
+        for attempt in range(self._elastic_cfg["max_recoveries"] + 1):
+            try:
+                if self._watchdog is not None and self._watchdog.failed:
+                    raise RuntimeError(self._watchdog.failed)
+                sub = batch if todo is None else batch.index_select(todo)
+                out = self.exchange.send_all(sub) if resend_overflow else self.exchange.send(sub)
+            except RuntimeError as e:  # gloo / RCCL errors (DistBackendError is a RuntimeError)
+                if attempt == self._elastic_cfg["max_recoveries"]:
+                    raise
+                _log.warning("data-plane generation %d failed: %s", self.membership["gen"], str(e)[:300])
+                trace.mark("ptype.rank_failure")
+                lost_before += self.recover()
+                if not resend_overflow and lost_before:
+                    # messages whose actor lived on a lost rank: STATUS_RANK_LOST, not re-run
+                    a = batch.actor.to(torch.int64)
+                    lost = torch.zeros(a.numel(), dtype=torch.bool, device=a.device)
+                    for r in lost_before:
+                        lost |= (a % self.world0) == r
+                    todo = torch.nonzero(~lost).flatten()
+                continue
+            self._sends += 1
+            if self._watchdog is not None and self.on_gpu:
+                ev = torch.cuda.Event()
+                ev.record()
+                self._watchdog.arm(ev)
+            if self.replicate_every and self._sends % self.replicate_every == 0:
+                try:
+                    self.replicate()
+                except RuntimeError:
+                    self.recover()  # the batch WAS delivered: recover, never re-send it
+            if todo is None:
+                return out
+            val = torch.zeros(batch.M, dtype=out[0].dtype, device=out[0].device)
+            st = torch.full((batch.M,), STATUS_RANK_LOST, dtype=out[1].dtype, device=out[1].device)
+            val[todo] = out[0]
+            st[todo] = out[1]
+            return (val, st) + tuple(out[2:])
+        raise AssertionError("unreachable")
+
+    # ------------------------------------------------------------------ rank failures (SURVEY 5.3)
+    def replicate(self) -> None:
+        """Collective over the current generation: every rank ships the blocks it
+        hosts to its buddy (the node that would adopt them, elastic.buddy) and
+        keeps the blocks it is buddy of, resident in HBM.  Point-to-point only."""
+        import torch.distributed as dist
+
+        from .parallel.elastic import buddy, ring_placement
+
+        m = self.membership
+        if m is None:
+            return
+        own = ring_placement(m["nodes0"], m["members"])
+        dst = buddy(m["nodes0"], m["members"], m["me"])
+        if dst == m["me"]:
+            return
+        src = next(n for n in m["members"] if buddy(m["nodes0"], m["members"], n) == m["me"])
+        P = self.actors
+        recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=self.device)
+        ops = [dist.P2POp(dist.isend, self.state, m["members"].index(dst)),
+               dist.P2POp(dist.irecv, recv, m["members"].index(src))]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(own[src])}
+
+    def recover(self) -> list[int]:
+        """Abort the failed generation, let the lease-based membership settle,
+        form the next generation through the store and re-home the lost ranks'
+        actors.  Returns the original ranks that were lost."""
+        from .parallel.bootstrap import alive_nodes, form_group
+        from .parallel.elastic import abort_group, lost_blocks, settle_membership
+
+        m, c = self.membership, self._elastic_cfg
+        if m is None:
+            raise RuntimeError("recover(): this runtime's group was not formed by Join")
+        abort_group()
+        self._exchange = None
+        if self._watchdog is not None:
+            self._watchdog.reset()
+        proposal = settle_membership(lambda: alive_nodes(c["registry"], self.service), m["members"], m["me"],
+                                     c["grace_s"])
+        members, tcp = form_group(c["store"], c["local_addr"], m["me"], self.service, m["gen"] + 1, proposal,
+                                  c["backend"], lambda r: self.device if c["backend"] == "nccl" else None,
+                                  timeout_s=c["timeout_s"])
+        lost = lost_blocks(m["nodes0"], m["members"], members)
+        self._tcp_store = tcp
+        m["members"], m["gen"] = list(members), m["gen"] + 1
+        self.rank, self.world = members.index(m["me"]), len(members)
+        self._rehome()
+        self.recoveries += 1
+        _log.warning("data-plane generation %d formed: world %d, lost original ranks %s, hosting %s", m["gen"],
+                     self.world, lost, self.blocks)
+        trace.mark("ptype.regenerated")
+        return lost
+
+    def _rehome(self) -> None:
+        """Placement of the current generation (elastic.ring_placement): keep the
+        state of blocks that stay, adopt lost blocks from their replicas, rebuild
+        the registry table and the dispatcher, republish this rank's record."""
+        from .parallel.elastic import ring_placement
+
+        m = self.membership
+        own = ring_placement(m["nodes0"], m["members"])
+        P, W0 = self.actors, self.world0
+        new_blocks = own[m["me"]]
+        state = torch.zeros(P * len(new_blocks), dtype=torch.int64, device=self.device)
+        self.restored = []
+        for j, r in enumerate(new_blocks):
+            if r in self.blocks:
+                i = self.blocks.index(r)
+                state[j * P:(j + 1) * P] = self.state[i * P:(i + 1) * P]
+            elif r in self.replicas:
+                state[j * P:(j + 1) * P] = self.replicas[r]
+                self.restored.append(r)
+        self.blocks, self.state, self.replicas = new_blocks, state, {}
+        self.table.clear()
+        k = torch.arange(P, dtype=torch.int64)
+        for node, rs in own.items():
+            rank = m["members"].index(node)
+            for j, r in enumerate(rs):
+                self.table.upsert(actor_keys(r + W0 * k), torch.full((P,), rank, dtype=torch.int32),
+                                  (j * P + k).to(torch.int32))
+        self.table.enable_directory(W0 * P, affine_world=W0)
+        self._ltable = None
+        if self.server is not None:  # the dispatcher serves the new state tensor
+            name = self.server.shm_name
+            self.server.close()
+            self.server = hip().DeviceServer(self.device.index or 0, self._ring, self.state.data_ptr(),
+                                             self.mailboxes, self.delay_us, self._idle_ms, 60.0, name)
+        if self.mirror is not None:
+            self.mirror.set_generation(m["gen"])
+        if self.shard_lease is not None:
+            self.shard_lease.update(rank=self.rank, world=W0, count=P, gen=m["gen"], blocks=list(new_blocks))
 
     def tell(self, batch: B.MsgBatch, outbox_capacity: int | None = None):
         """Fire-and-forget delivery that lets GPU handlers send on: ``batch`` is
@@ -364,6 +547,8 @@ class DeviceRuntime:
         if self._closed:
             return
         self._closed = True
+        if self._watchdog is not None:
+            self._watchdog.close()
         if self.mirror is not None:
             self.mirror.close()
         if self.shard_lease is not None:

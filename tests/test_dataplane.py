@@ -97,6 +97,97 @@ def test_join_forms_data_plane_and_send(tmp_path):
         assert world == 3 and ok_mul and ok_add and counted and shards == 3 and ping == "x", res
 
 
+def _survivor(i, pp, pc, sp, tmp, crash, q):
+    """Join (world 3, elastic) -> NewClient -> Send; node ``crash`` dies without any
+    cleanup after the first round; the survivors keep calling client.Send."""
+    os.environ["PTYPE_ADVERTISE_ADDR"] = "127.0.0.1"
+    from ptype_amd import cluster as C
+    from ptype_amd.ops.batch import MsgBatch
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD, STATUS_OK, STATUS_RANK_LOST
+
+    c = None
+    try:
+        ic = ",".join(f"e{j}=http://127.0.0.1:{pp[j]}" for j in range(3))
+        cfg = C.Config()
+        cfg.service_name, cfg.node_name, cfg.port = "calc", f"n{i}", sp[i]
+        cfg.member = _member(C, i, pp, pc, ic, tmp)
+        cfg.has_gpu = True
+        cfg.gpu.cpu, cfg.gpu.world, cfg.gpu.actors, cfg.gpu.max_batch = True, 3, 32, 4096
+        cfg.gpu.group_timeout_s, cfg.gpu.grace_s = 5.0, 10.0
+        srv = C.Serve(sp[i], Host(), host="127.0.0.1")
+        c = C.Join(C.background(), cfg)
+        rt = c.runtime
+        client = c.NewClient("calc", C.ConnConfig(retries=0, allow_local=False))
+        n = rt.total_actors
+        ids = torch.arange(n, dtype=torch.int32)
+        add = MsgBatch(ids, torch.ones(n, dtype=torch.int64), None, None, METHOD_COUNTER_ADD)
+        _, st = client.Send(add)
+        ok1 = bool((st == STATUS_OK).all())
+        rt.replicate()  # every block has a copy on its buddy (the node that adopts it)
+        me = rt.membership["me"]
+        dead = rt.membership["nodes0"][crash]
+        if me == dead:
+            os._exit(0)  # crash: no group teardown, no lease revoke, its Raft member gone
+        # the survivors' next Send fails inside the collective and recovers underneath;
+        # without re-sends, the messages of the lost rank's actors say so explicitly
+        a = ids.to(torch.int64) + 100 * i
+        mul = MsgBatch(ids, a, torch.full((n,), 7, dtype=torch.int64), None, METHOD_CALC_MULTIPLY)
+        val, st = client.Send(mul, resend_overflow=False)
+        lost = (ids % 3) == crash
+        ok_lost = bool((st[lost] == STATUS_RANK_LOST).all()) and bool((st[~lost] == STATUS_OK).all()) \
+            and torch.equal(val[~lost], a[~lost] * 7)
+        val, st = client.Send(mul)  # re-sent: the adopter answers now
+        ok2 = ok_lost and bool((st == STATUS_OK).all()) and torch.equal(val, a * 7)
+        _, st = client.Send(add)
+        ok3 = bool((st == STATUS_OK).all())
+        import torch.distributed as dist
+
+        dist.barrier()
+        P = rt.actors
+        own = sorted(int(x) for x in rt.state[:P].unique().tolist())
+        adopted = sorted(int(x) for x in rt.state[P:].unique().tolist())
+        q.put((me, dead, ok1, ok2, ok3, own, adopted, rt.restored, rt.world, rt.recoveries, rt.blocks,
+               rt.membership["gen"], len(rt.mirror.shards)))
+        dist.barrier()
+        client.Close()
+        srv.Close()
+        c.Close()
+    except Exception as e:
+        import traceback
+
+        q.put(("error", i, repr(e), traceback.format_exc()[-2500:]))
+        if c is not None:
+            c.Close()
+
+
+@pytest.mark.timeout(240)
+def test_join_send_survives_a_dead_rank(tmp_path):
+    """a rank dies mid-run; the survivors' ``client.Send`` (Join ->
+    NewClient -> Send, no elastic object in the test) recovers underneath:
+    abort, lease-driven membership, generation 1 through the store, the dead
+    rank's actors re-homed on its ring successor from the buddy replica."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pp, pc, sp = ([free_port() for _ in range(3)] for _ in range(3))
+    crash = 1
+    procs = [ctx.Process(target=_survivor, args=(i, pp, pc, sp, str(tmp_path), crash, q)) for i in range(3)]
+    [p.start() for p in procs]
+    res = [q.get(timeout=200) for _ in range(2)]
+    [p.join(30) for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    errors = [r for r in res if r[0] == "error"]
+    assert not errors, "\n".join("\n".join(map(str, r)) for r in errors)
+    for me, dead, ok1, ok2, ok3, own, adopted, restored, world, recov, blocks, gen, shards in res:
+        assert ok1 and ok2 and ok3, (me, ok1, ok2, ok3)
+        assert world == 2 and recov == 1 and gen == 1, (world, recov, gen)
+        assert own == [5], own  # 3 adds before the crash (one per rank), 2 after (two survivors)
+        if len(blocks) > 1:  # the adopter: the dead rank's actors resumed from the replica (3) + 2
+            assert blocks[1] == crash and restored == [crash] and adopted == [5], (blocks, restored, adopted)
+    assert sorted(len(r[10]) for r in res) == [1, 2]  # exactly one survivor adopted the dead rank
+
+
 def test_mirror_follows_joins_and_lease_expiry(tmp_path, ports, monkeypatch):
     monkeypatch.setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
     from ptype_amd import cluster as C
@@ -214,3 +305,42 @@ def test_send_names_a_hosted_service():
     v, _ = rt.send("Prime", b)
     assert torch.equal(v, b.a0 * b.a1)
     rt.close()
+
+
+def test_join_world1_reforms_after_a_flagged_failure(tmp_path, ports, monkeypatch):
+    """The CPU twin of test_elastic_gpu's Join case: gloo group formed by Join at
+    world 1 (``form_group``), a generation flagged failed, the next Send
+    re-forms generation 1 through the store and re-sends."""
+    monkeypatch.setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    from ptype_amd import cluster as C
+    from ptype_amd.ops.batch import MsgBatch
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD, STATUS_OK
+
+    pp, pc = ports(), ports()
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "w1", "n0", ports()
+    cfg.member = _member(C, 0, [pp], [pc], f"e0=http://127.0.0.1:{pp}", str(tmp_path))
+    cfg.has_gpu = True
+    cfg.gpu.cpu, cfg.gpu.world, cfg.gpu.form_group, cfg.gpu.actors, cfg.gpu.grace_s = True, 1, True, 64, 0.3
+    srv = C.Serve(cfg.port, Host(), host="127.0.0.1")
+    c = C.Join(C.background(), cfg)
+    try:
+        rt = c.runtime
+        client = c.NewClient("w1", C.ConnConfig(retries=0))
+        ids = torch.arange(rt.total_actors, dtype=torch.int32)
+        add = MsgBatch(ids, torch.ones(ids.numel(), dtype=torch.int64), None, None, METHOD_COUNTER_ADD)
+        assert bool((client.Send(add)[1] == STATUS_OK).all())
+        rt._watchdog.failed = "injected"
+        mul = MsgBatch(ids, ids.to(torch.int64), torch.full((ids.numel(),), 3, dtype=torch.int64), None,
+                       METHOD_CALC_MULTIPLY)
+        val, st = client.Send(mul)
+        assert bool((st == STATUS_OK).all()) and torch.equal(val, ids.to(torch.int64) * 3)
+        assert bool((client.Send(add)[1] == STATUS_OK).all())
+        assert rt.membership["gen"] == 1 and rt.recoveries == 1
+        assert rt.state.unique().tolist() == [2] and rt.shard_lease.record["gen"] == 1
+        rt.sync()
+        assert len(rt.mirror.shards) == 1 and rt.table.live == rt.total_actors
+        client.Close()
+    finally:
+        c.Close()
+        srv.Close()

@@ -74,3 +74,73 @@ def test_elastic_rccl_abort_and_reform_world1():
     assert out["gen0"] == 0 and out["gen1"] == 1 and out["recoveries"] == 1, out
     assert out["ok1"] and out["ok2"] and out["ok3"], out
     assert out["state"] == [2], out  # both CounterAdd rounds landed on state kept across the re-formation
+
+
+_JOIN_SCRIPT = textwrap.dedent("""
+    import json, os, sys, tempfile, torch
+    sys.path.insert(0, os.environ["PTYPE_ROOT"])
+    os.environ["PTYPE_ADVERTISE_ADDR"] = "127.0.0.1"
+    from ptype_amd import cluster as C
+    from ptype_amd.ops.batch import MsgBatch
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD, STATUS_OK
+    pp, pc, sp = (int(x) for x in os.environ["PORTS"].split(","))
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "jg", "j0", sp
+    cfg.member = C.member_config(name="j0", dir=tempfile.mkdtemp(prefix="elj_"),
+                                 lpurls=[f"http://127.0.0.1:{pp}"], apurls=[f"http://127.0.0.1:{pp}"],
+                                 lcurls=[f"http://127.0.0.1:{pc}"], acurls=[f"http://127.0.0.1:{pc}"],
+                                 initial_cluster=f"j0=http://127.0.0.1:{pp}", unsafe_no_fsync=True)
+    cfg.has_gpu = True
+    cfg.gpu.device, cfg.gpu.world, cfg.gpu.form_group, cfg.gpu.actors = 0, 1, True, 4096
+    cfg.gpu.grace_s, cfg.gpu.send_timeout_s = 0.5, 20.0
+    class Host:
+        def Ping(self, x):
+            return x
+    srv = C.Serve(sp, Host(), host="127.0.0.1")
+    c = C.Join(C.background(), cfg)
+    rt = c.runtime
+    client = c.NewClient("jg", C.ConnConfig(retries=0))
+    n = rt.total_actors
+    ids = torch.arange(n, dtype=torch.int32, device="cuda")
+    add = MsgBatch(ids, torch.ones(n, dtype=torch.int64, device="cuda"), None, None, METHOD_COUNTER_ADD)
+    _, st = client.Send(add)
+    torch.cuda.synchronize()
+    out = {"gen0": rt.membership["gen"], "forced": bool(rt.exchange.force_collectives),
+           "ok1": bool((st == STATUS_OK).all())}
+    # a failed generation as the send watchdog reports it: the next Send aborts the RCCL
+    # communicator, re-forms the group through the store and re-sends
+    rt._watchdog.failed = "injected: device work overdue"
+    mul = MsgBatch(ids, ids.to(torch.int64), torch.full((n,), 7, dtype=torch.int64, device="cuda"), None,
+                   METHOD_CALC_MULTIPLY)
+    val, st = client.Send(mul)
+    _, st2 = client.Send(add)
+    torch.cuda.synchronize()
+    out["gen1"] = rt.membership["gen"]
+    out["recoveries"] = rt.recoveries
+    out["ok2"] = bool((st == STATUS_OK).all()) and torch.equal(val, ids.to(torch.int64) * 7)
+    out["ok3"] = bool((st2 == STATUS_OK).all())
+    out["state"] = sorted(int(x) for x in rt.state.unique().tolist())
+    out["record_gen"] = rt.shard_lease.record.get("gen")
+    print("RESULT " + json.dumps(out))
+    client.Close()
+    c.Close()
+    srv.Close()
+""")
+
+
+@pytest.mark.gpu
+def test_join_runtime_aborts_and_reforms_world1():
+    """VERDICT r2 #3, GPU half: the abort / re-form runs through Join's runtime
+    (no ElasticDataPlane): a failed generation (as the send watchdog flags it)
+    makes the next client.Send abort the RCCL communicator, form generation 1
+    through the store and re-send; state survives, replies are right."""
+    env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1",
+               PORTS=",".join(str(free_port()) for _ in range(3)))
+    r = subprocess.run([sys.executable, "-c", _JOIN_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads(line[0][7:])
+    assert out["gen0"] == 0 and out["gen1"] == 1 and out["recoveries"] == 1 and out["forced"], out
+    assert out["ok1"] and out["ok2"] and out["ok3"], out
+    assert out["state"] == [2] and out["record_gen"] == 1, out
