@@ -179,10 +179,21 @@ class Client:
     batched device-native path (see ``ptype_amd.runtime``).
     """
 
-    def __init__(self, core: _core.RpcClient, runtime=None, service: str = ""):
+    def __init__(self, core: _core.RpcClient, runtime=None, service: str = "", local_addr: str = "",
+                 max_connections: int = 3):
         self._c = core
         self._rt = runtime
         self.service = service
+        self._local_addr, self._max_connections = local_addr, int(max_connections)
+        self._router = None  # replica routing of Send (parallel/replicas.py), when the service is replicated
+        self._router_checked = False
+
+    def _replica_router(self):
+        if not self._router_checked:
+            self._router_checked = True
+            if self._rt.has_replicas(self.service):
+                self._router = self._rt.replica_router(self.service, self._max_connections, self._local_addr)
+        return self._router
 
     def Call(self, serviceMethod: str, args: Any) -> Any:
         return self._c.call(serviceMethod, args)
@@ -195,7 +206,7 @@ class Client:
         RCCL epoch exchange across ranks, device dispatch, replies in order."""
         if self._rt is None:
             raise RuntimeError("Client.Send needs the cluster's device runtime (Join with a gpu: section)")
-        return self._rt.send(self.service, batch, **kw)
+        return self._rt.send(self.service, batch, router=self._replica_router(), **kw)
 
     def Tell(self, batch, **kw):
         """Batched fire-and-forget to GPU actors of this service; handlers may send
@@ -205,6 +216,8 @@ class Client:
         return self._rt.tell(batch, **kw)
 
     def Close(self) -> None:
+        if self._router is not None:
+            self._router.close()
         self._c.close()
 
     def ConnectionErrs(self) -> ErrChannel:
@@ -327,7 +340,8 @@ class Cluster:
         return self._c.member_list(_ctx(ctx))
 
     def NewClient(self, serviceName: str, cfg: ConnConfig | None = None) -> Client:
-        c = Client(self._c.new_client(serviceName, cfg), self.runtime, serviceName)
+        mc = cfg.max_connections if cfg is not None else _core.default_conn_config().max_connections
+        c = Client(self._c.new_client(serviceName, cfg), self.runtime, serviceName, self.local_addr, mc)
         self._clients.append(c)
         return c
 

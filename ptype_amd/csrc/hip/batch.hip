@@ -75,6 +75,32 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
   }
 }
 
+// Replica routing (SURVEY 2.4 "service replication"): a replicated stateless
+// service is hosted on several ranks, each holding the same logical actors
+// [0, n) at its mailboxes [0, n) -- global actor id a * W + rank in the strided
+// id space of the group (so the route directory's affine rule applies).  The
+// client picks the replica per message with the reference client's rules: the
+// selected replicas (all of them in mesh mode, else FNV-1a picks -- host side,
+// ConnectionBalancer::select_nodes) taken round robin, the first call to index 1
+// (cluster/rpc.go:176-183, 246-270): message i of a Send whose counter starts at
+// seq0 goes to sel[(seq0 + 1 + i) % n_sel].  Ids >= n map to -1 (no actor).
+constexpr int kMaxReplicaSel = 64;
+struct ReplicaSel {
+  uint8_t rank[kMaxReplicaSel];
+  uint32_t n;
+};
+
+__global__ __launch_bounds__(256) void replica_route_kernel(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                            int64_t M, ReplicaSel sel, uint64_t first, uint32_t W,
+                                                            uint32_t n_logical) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += step) {
+    const uint32_t a = (uint32_t)in[i];
+    const uint32_t j = (uint32_t)((first + (uint64_t)i) % sel.n);
+    out[i] = a < n_logical ? (int32_t)(a * W + sel.rank[j]) : -1;
+  }
+}
+
 // Pass 1: lookup + histogram.  Block b owns messages [b*P, min(M,(b+1)*P)).
 // Each thread resolves K messages per tile (coalesced, item-major), with their
 // lookups overlapped.  With a route directory (DIR) an actor id below n_dir costs
@@ -651,6 +677,25 @@ static inline unsigned grid_cap(int64_t work, int per, unsigned cap) {
   if (g > cap) g = cap;
   return (unsigned)g;
 }
+
+void launch_replica_route(uintptr_t in, uintptr_t out, int64_t M, const std::vector<int>& ranks, uint64_t seq0,
+                          uint32_t W, uint32_t n_logical, uintptr_t stream) {
+  if (M <= 0) return;
+  if (ranks.empty() || ranks.size() > (size_t)kMaxReplicaSel)
+    throw std::invalid_argument("replica_route: 1.." + std::to_string(kMaxReplicaSel) + " selected replicas");
+  if ((uint64_t)n_logical * W > 0x7fffffffull) throw std::invalid_argument("replica_route: ids exceed int32");
+  ReplicaSel sel{};
+  for (size_t k = 0; k < ranks.size(); ++k) {
+    if (ranks[k] < 0 || (uint32_t)ranks[k] >= W) throw std::invalid_argument("replica_route: rank out of range");
+    sel.rank[k] = (uint8_t)ranks[k];
+  }
+  sel.n = (uint32_t)ranks.size();
+  hipLaunchKernelGGL(replica_route_kernel, dim3(grid_cap(M, 256, 2048)), dim3(256), 0, as_stream(stream),
+                     (const int32_t*)in, (int32_t*)out, M, sel, (seq0 + 1) % sel.n, W, n_logical);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+int replica_sel_max() { return kMaxReplicaSel; }
 
 void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M, uint32_t n_actors, uint64_t seed,
                          uintptr_t seed_ptr, uintptr_t stream) {

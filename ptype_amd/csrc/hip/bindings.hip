@@ -52,6 +52,9 @@ void launch_table_lookup(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uin
 void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uintptr_t);
 void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t, uintptr_t);
+void launch_replica_route(uintptr_t, uintptr_t, int64_t, const std::vector<int>&, uint64_t, uint32_t, uint32_t,
+                          uintptr_t);
+int replica_sel_max();
 int64_t route_grid(int64_t, int64_t*);
 int64_t gob_max_bytes(int64_t, int, uint32_t);
 int64_t gob_ws_words(int64_t);
@@ -156,6 +159,9 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("cols"), py::arg("status"), py::arg("stream"));
   m.def("gen_requests", &launch_gen_requests, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("M"),
         py::arg("n_actors"), py::arg("seed"), py::arg("seed_ptr"), py::arg("stream"));
+  m.def("replica_route", &launch_replica_route, py::arg("actor_in"), py::arg("actor_out"), py::arg("M"),
+        py::arg("ranks"), py::arg("seq0"), py::arg("world"), py::arg("n_logical"), py::arg("stream"));
+  m.def("max_replica_sel", &replica_sel_max);
   m.def("route_grid", [](int64_t M) {
     int64_t P;
     int64_t G = route_grid(M, &P);

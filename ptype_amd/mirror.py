@@ -79,12 +79,13 @@ class ShardLease:
     """This node's shard record, attached to a lease kept alive until ``close()``
     (graceful close revokes it: the shard disappears at once)."""
 
-    def __init__(self, kv, service: str, node: str, rank: int, world: int, count: int, ttl_s: int = LEASE_TTL_S):
+    def __init__(self, kv, service: str, node: str, rank: int, world: int, count: int, ttl_s: int = LEASE_TTL_S,
+                 **extra):
         from ._core import Context
 
         self.kv = kv
         self.key = f"{STORE_PREFIX}{ACTORS_PREFIX}/{service}/{node}"
-        self.record = {"rank": int(rank), "world": int(world), "count": int(count), "node": node}
+        self.record = {"rank": int(rank), "world": int(world), "count": int(count), "node": node, **extra}
         self.lease, _ = kv.grant(int(ttl_s))
         kv.put(self.key, json.dumps(self.record).encode(), self.lease)
         self._ctx = Context.with_cancel()
@@ -208,6 +209,9 @@ class RegistryMirror:
         old = self.shards.get(key)
         if old is not None and old["record"] != rec:
             self._delete(key)
+        if self.table is None:  # records only (a replica set: parallel/replicas.py)
+            self.shards[key] = {"record": rec, "deadline": deadline}
+            return
         ids, mbox = self._ids(rec)
         n = ids.numel()
         self.table.upsert(actor_keys(ids), torch.full((n,), int(rec["rank"]), dtype=torch.int32),
@@ -216,7 +220,7 @@ class RegistryMirror:
 
     def _delete(self, key: str) -> None:
         sh = self.shards.pop(key, None)
-        if sh is not None:
+        if sh is not None and self.table is not None:
             ids, _ = self._ids(sh["record"])
             self.table.delete(actor_keys(ids))
 
@@ -245,7 +249,8 @@ class RegistryMirror:
         live_before = len(self.shards)
         expired = [k for k, sh in self.shards.items() if sh["deadline"] < now]
         if expired:
-            self.table.sweep(now)
+            if self.table is not None:
+                self.table.sweep(now)
             for k in expired:
                 self.shards.pop(k, None)
             changed += live_before - len(self.shards)

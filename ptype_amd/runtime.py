@@ -168,6 +168,7 @@ class DeviceRuntime:
                  max_batch=g.max_batch, service=cfg.service_name, mailbox_shards=g.mailbox_shards,
                  mailbox_slots=g.mailbox_slots)
         rt._tcp_store, rt._owns_group = tcp, owns
+        rt._addr = (core_cluster.local_addr, int(cfg.port))
         if members is not None and g.elastic:
             rt.membership = {"me": me, "nodes0": list(members), "members": list(members), "gen": 0}
             rt._elastic_cfg = {"store": store, "registry": registry, "local_addr": core_cluster.local_addr,
@@ -271,12 +272,54 @@ class DeviceRuntime:
             raise ValueError(f"Send to {service!r}: this process's data plane hosts {sorted(self.hosted)} "
                              "(co-host more services with DeviceRuntime.host)")
 
-    def send(self, service: str | None, batch: B.MsgBatch, resend_overflow: bool = True):
+    # ------------------------------------------------------------------ replicated services (parallel/replicas.py)
+    def serve_replica(self, service: str, address: str | None = None, port: int | None = None) -> None:
+        """Serve ``service`` as one replica of a replicated stateless service:
+        its logical actors [0, actors) are this rank's mailboxes (lease-attached
+        record ``_ptype/actors/<service>/<node>`` with ``"replica": true``)."""
+        from .mirror import ShardLease
+
+        if getattr(self, "_kv", None) is None:
+            raise RuntimeError("serve_replica needs a control plane (Join, or attach())")
+        addr, p = self._addr if getattr(self, "_addr", None) else ("", 0)
+        self.host(service)
+        lease = ShardLease(self._kv, service, self._node, self.blocks[0], self.world0, self.actors, replica=True,
+                           address=address if address is not None else addr, port=int(port if port is not None else p))
+        self._replica_leases = getattr(self, "_replica_leases", {})
+        self._replica_leases[service] = lease
+
+    def has_replicas(self, service: str) -> bool:
+        """Whether ``service`` has replica records in the store."""
+        from .mirror import ACTORS_PREFIX, STORE_PREFIX, _prefix_end
+
+        kv = getattr(self, "_kv", None)
+        if kv is None:
+            return False
+        from ._core import RangeOpts
+
+        o = RangeOpts()
+        pfx = f"{STORE_PREFIX}{ACTORS_PREFIX}/{service}/"
+        o.end = _prefix_end(pfx)
+        return any(json.loads(x.value).get("replica") for x in kv.get(pfx, o).kvs)
+
+    def replica_router(self, service: str, max_connections: int = 3, local_addr: str | None = None):
+        """A client's replica selection for ``service`` (follows its records)."""
+        from .parallel.replicas import ReplicaRouter
+
+        la = local_addr if local_addr is not None else (self._addr[0] if getattr(self, "_addr", None) else "")
+        return ReplicaRouter(service, self.world0, la, max_connections, kv=self._kv)
+
+    def send(self, service: str | None, batch: B.MsgBatch, resend_overflow: bool = True, router=None):
         """Batched Send: every message to its actor anywhere in the node and the
         replies back in message order.  Collective across the process group.
         Registry changes seen since the last Send are applied first.  With an
-        elastic group a rank failure is recovered here (module docstring)."""
-        self._check_service(service)
+        elastic group a rank failure is recovered here (module docstring).
+        ``router``: a replicated service's ReplicaRouter -- the batch's logical
+        actor ids are routed to the selected replicas, round robin."""
+        if router is not None:
+            batch = B.MsgBatch(router.route(batch.actor), batch.a0, batch.a1, batch.a2, batch.method)
+        else:
+            self._check_service(service)
         self.sync()
         if self.membership is None:
             ex = self.exchange
@@ -549,6 +592,8 @@ class DeviceRuntime:
         self._closed = True
         if self._watchdog is not None:
             self._watchdog.close()
+        for lease in getattr(self, "_replica_leases", {}).values():
+            lease.close()
         if self.mirror is not None:
             self.mirror.close()
         if self.shard_lease is not None:

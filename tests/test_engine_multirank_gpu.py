@@ -242,3 +242,78 @@ def test_gpu_multirank_tells(packed):
     for r in range(R):
         assert torch.equal(states[r], exp[r::R]), r  # actor a -> rank a % R, mailbox a // R
     assert all(e == hops for e in epochs), epochs
+
+
+@pytest.mark.gpu
+def test_gpu_replicated_prime_over_fakecomm_r4():
+    """Prime served by 2 replica ranks (1, 3) of an R = 4 FakeComm
+    pipeline; every rank's calls split over them exactly as its balancer's
+    round robin picks (the replica_route kernel), Prime.Check answers right;
+    after replica 1 is lost every call lands on rank 3."""
+    from ptype_amd.parallel.exchange import ActorExchange
+    from ptype_amd.parallel.replicas import ReplicaRouter
+    from ptype_amd.ops.records import METHOD_PRIME_CHECK
+
+    R, P = 4, 512
+    n = P * R
+    fc = hip().FakeComm(R)
+    recs = [{"rank": r, "world": R, "count": P, "node": f"p{r}", "replica": True, "address": f"10.0.0.{r}",
+             "port": 7000} for r in (1, 3)]
+    sizes = [20_000 + 999 * r for r in range(R)]
+    states, results, errors = [None] * R, [None] * R, []
+    start = threading.Barrier(R)
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                tab = RegistryTable(2 * n, device="cuda")
+                ids = torch.arange(n)
+                tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
+                tab.enable_directory(n, affine_world=R)
+                st = torch.zeros(P, dtype=torch.int64, device="cuda")
+                ex = ActorExchange(tab, max(sizes), chunks=2, state=st, fake=(fc, r))
+                router = ReplicaRouter("Prime", R, f"10.1.0.{r}", 3, records=recs)
+                M = sizes[r]
+                a = (torch.arange(M, device="cuda") % P).to(torch.int32)
+                start.wait()
+                _, s1 = ex.send(B.MsgBatch(router.route(a), torch.ones(M, dtype=torch.int64, device="cuda"), None,
+                                           None, METHOD_COUNTER_ADD))
+                t = torch.tensor([97, 91, 62, 273, 7919], dtype=torch.int64, device="cuda")
+                pv, ps = ex.send(B.MsgBatch(router.route(torch.arange(5, dtype=torch.int32, device="cuda")),
+                                            torch.full_like(t, 2), t, t, METHOD_PRIME_CHECK))
+                s.synchronize()
+                start.wait()
+                c1 = st.clone()
+                router.set_records(recs[1:])  # replica 1 lost
+                _, s2 = ex.send(B.MsgBatch(router.route(a), torch.ones(M, dtype=torch.int64, device="cuda"), None,
+                                           None, METHOD_COUNTER_ADD))
+                s.synchronize()
+                results[r] = (s1.cpu(), ps.cpu(), pv.cpu(), s2.cpu())
+                states[r] = (c1.cpu(), (st - c1).cpu())
+        except BaseException as e:  # noqa: BLE001
+            errors.append((r, repr(e)))
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(R)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in threads), "a rank hung"
+    assert not errors, errors
+    want1 = {q: torch.zeros(P, dtype=torch.int64) for q in (1, 3)}
+    for r in range(R):
+        s1, ps, pv, s2 = results[r]
+        assert bool((s1 == STATUS_OK).all()) and bool((s2 == STATUS_OK).all()) and bool((ps == STATUS_OK).all())
+        assert pv.tolist() == [97, 7, 2, 3, 7919]
+        for i in range(sizes[r]):
+            want1[(1, 3)[(1 + i) % 2]][i % P] += 1
+    total = sum(torch.bincount(torch.arange(sizes[r]) % P, minlength=P) for r in range(R))
+    for r in range(R):
+        c1, c2 = states[r]
+        if r in (1, 3):
+            assert torch.equal(c1, want1[r]), r
+            assert torch.equal(c2, total if r == 3 else torch.zeros(P, dtype=torch.int64)), r
+        else:
+            assert int(c1.sum()) == 0 and int(c2.sum()) == 0
