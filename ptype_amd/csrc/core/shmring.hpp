@@ -37,8 +37,37 @@
 
 namespace ptype {
 
-constexpr uint64_t kShmMagic = 0x33736d6570797470ull;  // "ptypems3" (taker entries)
+constexpr uint64_t kShmMagic = 0x34736d6570797470ull;  // "ptypems4" (GPU peer lanes)
 constexpr int kShmMaxMethods = 32;
+
+// GPU peer lanes: a GPU in ANOTHER process calls this
+// server's actors without any host on the path.  The server keeps kXLanes
+// single-producer lanes in fine-grained HBM (XLane, exported by IPC handle in
+// the header); a calling process registers one (XLaneReg: its process token and
+// the IPC handle of a 16-B reply slot in ITS OWN HBM), the server imports that
+// slot, and from then on the caller's kernel writes a request into the lane over
+// xGMI and spins on its local reply slot, which the persistent dispatcher fills
+// with one 16-B store.  A lane carries one call at a time (the caller waits for
+// each reply), so it needs no sequence taking, owners or rescue: seq + 1 in
+// req_tag publishes, `served` acknowledges.
+constexpr int kXLanes = 64;
+enum XLaneState : uint32_t { kXLaneFree = 0, kXLaneRequested = 1, kXLaneReady = 2, kXLaneFailed = 3 };
+struct XLaneReg {
+  std::atomic<uint64_t> token;  // the caller's process token (ring_self_token); 0: free
+  std::atomic<uint32_t> state;
+  int32_t device;               // the caller's HIP device ordinal (diagnostics)
+  uint8_t reply_ipc[64];        // hipIpcMemHandle_t of the caller's reply slot allocation
+  uint64_t pad[2];
+};
+struct alignas(128) XLane {  // server HBM; one per wave lane of the dispatcher
+  uint64_t req_tag;  // caller: seq + 1 once the request below is out (release)
+  uint64_t served;   // dispatcher: req_tag of the last request answered
+  uint64_t w0;       // actor | method << 32 | flags << 48 (MsgRecord word 0)
+  int64_t a0, a1, a2;
+  uint64_t rep_ptr;  // server-side address of the caller's reply slot {value, reply_tag}
+  uint64_t pad[9];
+};
+static_assert(sizeof(XLane) == 128, "XLane layout");
 
 struct ShmMethod {
   char name[96];  // "Service.Method"
@@ -63,6 +92,10 @@ struct alignas(64) ShmHeader {
   char req_sock[64];      // abstract unix socket handing out the dma-buf fd
   uint8_t ipc_handle[64]; // hipIpcMemHandle_t of the ring (GPU peers)
   uint32_t ipc_valid, pad2;
+  // GPU peer lanes
+  uint8_t xl_ipc[64];     // hipIpcMemHandle_t of the XLane array
+  uint32_t xl_valid, xl_lanes;
+  XLaneReg xregs[kXLanes];
 };
 static_assert(sizeof(ShmHeader) <= 16384, "ShmHeader too large");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "process-shared atomics must be lock-free");

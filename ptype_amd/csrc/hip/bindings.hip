@@ -13,6 +13,7 @@
 #include "exchange_sorted.hpp"
 #include "mailbox.hpp"
 #include "server.hpp"
+#include "xcall.hpp"
 
 namespace py = pybind11;
 
@@ -428,6 +429,17 @@ PYBIND11_MODULE(_hip, m) {
                              "address of the C++ object (the epoch engine delivers into these mailboxes)");
   m.def("rccl_available", [] { return rccl().alltoall != nullptr; });
 
+  py::class_<PeerLane, std::shared_ptr<PeerLane>>(m, "PeerLane")
+      .def(py::init([](const std::string& shm, int device, double timeout_s) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<PeerLane>(shm, device, timeout_s);
+           }),
+           py::arg("shm_name"), py::arg("device"), py::arg("timeout_s") = 10.0)
+      .def("call", &PeerLane::call, py::arg("actor"), py::arg("method"), py::arg("method_uniform"), py::arg("a0"),
+           py::arg("a1"), py::arg("a2"), py::arg("n"), py::arg("out_val"), py::arg("out_st"), py::arg("ticks"),
+           py::arg("timeout_s"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("lane", &PeerLane::lane)
+      .def_property_readonly("calls", &PeerLane::calls);
   py::class_<DeviceServer>(m, "DeviceServer")
       .def(py::init<int, uint32_t, uintptr_t, uint32_t, uint64_t, double, double, const std::string&>(),
            py::arg("device"), py::arg("ring") = 4096, py::arg("state") = 0, py::arg("n_state") = 0,
@@ -435,6 +447,7 @@ PYBIND11_MODULE(_hip, m) {
       .def("export_method", &DeviceServer::export_method, py::arg("name"), py::arg("method"), py::arg("actor") = 0,
            py::arg("fields") = std::vector<std::string>{}, py::arg("actor_field") = "")
       .def_property_readonly("shm_name", &DeviceServer::shm_name)
+      .def_property_readonly("xlanes", [](DeviceServer& s) { return s.xlanes_exported(); })
       .def(
           "call",
           [](DeviceServer& s, int method, uint32_t actor, int64_t a0, int64_t a1, int64_t a2, double timeout) {

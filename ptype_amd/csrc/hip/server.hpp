@@ -126,12 +126,47 @@ struct PollConfig {
   uint32_t sleep = 1;
 };
 
+// GPU peer lanes (shmring.hpp XLane): lane l of the wave serves XLane l.  A
+// request is pending when req_tag == served + 1; the reply goes straight into
+// the caller's HBM (rep_ptr, imported by the server) as one 16-B store, then
+// `served` acknowledges.  Returns the number of lanes served (wave-uniform).
+__device__ __forceinline__ unsigned serve_xlanes(XLane* __restrict__ xl, uint32_t nx, int64_t* __restrict__ state,
+                                                 uint32_t n_state, uint64_t delay_ticks) {
+  const unsigned lane = lane_id();
+  bool ready = false;
+  uint64_t t = 0;
+  if (xl && lane < nx) {
+    t = sys_ld(&xl[lane].req_tag);
+    ready = t != 0 && t == sys_ld(&xl[lane].served) + 1;
+  }
+  const uint64_t m = __ballot(ready);
+  if (!m) return 0;
+  if (ready) {  // payload loads ordered after the tag load (the branch waits for it)
+    XLane* L = &xl[lane];
+    const uint64_t w0 = sys_ld(&L->w0);
+    MsgRecord msg;
+    msg.actor = (uint32_t)w0;
+    msg.method = (uint16_t)(w0 >> 32);
+    msg.flags = (uint16_t)(w0 >> 48);
+    msg.a0 = (int64_t)sys_ld(reinterpret_cast<const uint64_t*>(&L->a0));
+    msg.a1 = (int64_t)sys_ld(reinterpret_cast<const uint64_t*>(&L->a1));
+    msg.a2 = (int64_t)sys_ld(reinterpret_cast<const uint64_t*>(&L->a2));
+    const ReplyRecord r = run_handler(msg, state, n_state, delay_ticks);
+    uint64_t* out = reinterpret_cast<uint64_t*>(sys_ld(&L->rep_ptr));
+    if (out) sys_st16(out, (uint64_t)r.value, reply_tag(t - 1, (uint32_t)r.status));
+    __threadfence_system();
+    sys_st(&L->served, t);
+  }
+  return (unsigned)__popcll(m);
+}
+
 __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __restrict__ req,
                                                                  ReplySlot* __restrict__ rep, uint64_t ring_mask,
                                                                  ServerCtrl* __restrict__ ctrl, uint64_t head,
                                                                  int64_t* __restrict__ state, uint32_t n_state,
                                                                  uint64_t delay_ticks, uint64_t idle_ticks,
-                                                                 uint64_t max_ticks, PollConfig poll) {
+                                                                 uint64_t max_ticks, PollConfig poll,
+                                                                 XLane* __restrict__ xl, uint32_t nx) {
   const unsigned lane = lane_id();
   const uint64_t t_start = realtime_ticks();
   uint64_t last_work = t_start;
@@ -158,6 +193,14 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
     const bool ready = tag == seq + 1 && (!spec || cs == ring_csum(seq, w0, w1, w2, w3));
     const uint64_t m = __ballot(ready);
     const unsigned n = (m == ~0ull) ? 64u : (unsigned)__builtin_ctzll(~m);
+    if (nx) {  // GPU peer lanes: local HBM loads, no PCIe trip
+      const unsigned nxs = serve_xlanes(xl, nx, state, n_state, delay_ticks);
+      if (nxs) {
+        processed += nxs;
+        last_work = realtime_ticks();
+        if (n == 0) continue;
+      }
+    }
     if (n == 0) {
       if ((++idle_polls & 3) == 0) {
         if ((idle_polls & 63) == 0) {
@@ -180,7 +223,12 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
           __threadfence_system();
           sys_st(&ctrl->state, kStopped);
           __threadfence_system();
-          if (!lifetime_exit && sys_ld(&req[head & ring_mask].tag) == head + 1) {
+          bool pending = sys_ld(&req[head & ring_mask].tag) == head + 1;
+          for (uint32_t k = 0; k < nx && !pending; ++k) {
+            const uint64_t t = sys_ld(&xl[k].req_tag);
+            pending = t != 0 && t == sys_ld(&xl[k].served) + 1;
+          }
+          if (!lifetime_exit && pending) {
             uint64_t expected = kStopped;
             resume = __hip_atomic_compare_exchange_strong(&ctrl->state, &expected, (uint64_t)kRunning,
                                                           __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
@@ -325,6 +373,7 @@ class DeviceServer {
       drep_ = reinterpret_cast<ReplySlot*>(dbase + (reinterpret_cast<const char*>(rep_) - hbase));
       dctrl_ = reinterpret_cast<ServerCtrl*>(dbase + (reinterpret_cast<const char*>(ctrl_) - hbase));
       if (xproc_device_ring_enabled()) export_device_ring();
+      export_xlanes();
     }
     for (uint32_t i = 0; i < ring_; ++i) owner_[i].store(i, std::memory_order_relaxed);
     stream_ = dedicated_stream(device_);  // the persistent dispatcher runs here
@@ -360,6 +409,11 @@ class DeviceServer {
     (void)hipSetDevice(device_);
     (void)hipStreamSynchronize(stream_);
     (void)hipStreamDestroy(stream_);
+    for (auto& p : xl_imports_)
+      if (p) (void)hipIpcCloseMemHandle(p);
+    xl_imports_.clear();
+    if (xl_) (void)hipFree(xl_);
+    xl_ = nullptr;
     if (seg_) {
       handoff_.reset();  // no new client maps the ring (mapped ones keep the buffer alive)
       if (dmabuf_fd_ >= 0) (void)hsa_amd_portable_close_dmabuf(dmabuf_fd_);
@@ -394,6 +448,7 @@ class DeviceServer {
   }
 
   std::string shm_name() const { return seg_ ? seg_->name() : std::string(); }
+  bool xlanes_exported() const { return xl_ != nullptr; }
   uint64_t ring_fds_handed() const { return handoff_ ? handoff_->handed() : 0; }  // client processes that mapped the ring
 
   // Publish n requests and wait for all replies (any thread).
@@ -574,14 +629,105 @@ class DeviceServer {
     hdr_->req_dev = 1;  // published with the magic (release) at the end of construction
   }
 
-  // Same-node clients poke the futex when they find the wave parked.
+  // Same-node clients poke the futex when they find the wave parked.  With GPU
+  // peer lanes registered the loop also wakes every millisecond: it admits new
+  // lane registrations and relaunches a parked wave for a pending lane request
+  // (a GPU caller cannot poke a futex).
   void waker_loop() {
     while (!closed_) {
-      shm_futex_wait(&hdr_->wake, 0, 2000);
+      shm_futex_wait(&hdr_->wake, 0, xl_live_ ? 1000 : 2000);
       const uint32_t w = hdr_->wake.exchange(0);
       if (closed_ || w == 2) break;
-      if (w) ensure_running();
+      if (xl_) admit_xlanes();
+      if (w || (xl_live_ && xlane_pending())) ensure_running();
     }
+  }
+
+  // ---- GPU peer lanes (shmring.hpp)
+  void export_xlanes() {
+    if (getenv("PTYPE_XLANES") && std::string(getenv("PTYPE_XLANES")) == "0") return;
+    const size_t bytes = sizeof(XLane) * kXLanes;
+    if (hipExtMallocWithFlags((void**)&xl_, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+      (void)hipGetLastError();
+      xl_ = nullptr;
+      return;
+    }
+    hipIpcMemHandle_t h;
+    if (!open_to_cpu(xl_) || hipIpcGetMemHandle(&h, xl_) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(xl_);
+      xl_ = nullptr;
+      return;
+    }
+    PT_HIP_CHECK(hipMemset(xl_, 0, bytes));
+    PT_HIP_CHECK(hipDeviceSynchronize());
+    static_assert(sizeof(h) <= sizeof(hdr_->xl_ipc), "IPC handle size");
+    memcpy(hdr_->xl_ipc, &h, sizeof h);
+    hdr_->xl_lanes = kXLanes;
+    hdr_->xl_valid = 1;
+    xl_imports_.assign(kXLanes, nullptr);
+  }
+
+  // Requested lanes: import the caller's reply slot, reset the lane, mark it
+  // ready.  Lanes of dead callers are reclaimed.
+  void admit_xlanes() {
+    uint32_t live = 0;
+    for (int i = 0; i < kXLanes; ++i) {
+      XLaneReg& g = hdr_->xregs[i];
+      const uint32_t st = g.state.load(std::memory_order_acquire);
+      const uint64_t tok = g.token.load(std::memory_order_acquire);
+      if (st == kXLaneFree || !tok || !ring_token_alive(tok)) {  // released, or its caller is gone
+        if (xl_imports_[i]) {  // let go of the caller's reply slot
+          xlane_write(i, 0, 0);
+          (void)hipIpcCloseMemHandle(xl_imports_[i]);
+          xl_imports_[i] = nullptr;
+        }
+        if (st != kXLaneFree) {
+          g.state.store(kXLaneFree, std::memory_order_release);
+          uint64_t t = tok;
+          g.token.compare_exchange_strong(t, 0);
+        }
+        continue;
+      }
+      ++live;
+      if (st != kXLaneRequested) continue;
+      void* p = nullptr;
+      hipIpcMemHandle_t h;
+      memcpy(&h, g.reply_ipc, sizeof h);
+      (void)hipSetDevice(device_);
+      if (xl_imports_[i]) {
+        (void)hipIpcCloseMemHandle(xl_imports_[i]);
+        xl_imports_[i] = nullptr;
+      }
+      if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        (void)hipGetLastError();
+        g.state.store(kXLaneFailed, std::memory_order_release);
+        continue;
+      }
+      xl_imports_[i] = p;
+      xlane_write(i, (uint64_t)(uintptr_t)p, 0);
+      g.state.store(kXLaneReady, std::memory_order_release);
+    }
+    xl_live_ = live;
+  }
+
+  // Reset lane i (through the BAR mapping): sequence restarts at 0.
+  void xlane_write(int i, uint64_t rep_ptr, uint64_t seq) {
+    volatile XLane* L = &xl_[i];
+    L->rep_ptr = rep_ptr;
+    L->served = seq;
+    L->req_tag = seq;
+    _mm_sfence();
+    (void)L->req_tag;  // non-posted read: the writes have landed
+  }
+
+  bool xlane_pending() const {
+    for (int i = 0; i < kXLanes; ++i) {
+      const volatile XLane* L = &xl_[i];
+      const uint64_t t = L->req_tag;
+      if (t && t == L->served + 1) return true;
+    }
+    return false;
   }
 
   void ensure_running() {
@@ -599,7 +745,7 @@ class DeviceServer {
           (void)hipSetDevice(device_);
           hipLaunchKernelGGL(persistent_dispatch_kernel, dim3(1), dim3(64), 0, stream_, dreq_, drep_,
                              (uint64_t)(ring_ - 1), dctrl_, head, state_, n_state_, delay_ticks_, idle_ticks_,
-                             max_ticks_, poll_);
+                             max_ticks_, poll_, xl_, xl_ ? (uint32_t)kXLanes : 0u);
           PT_HIP_CHECK(hipGetLastError());
           launches_.fetch_add(1);
           return;
@@ -655,6 +801,9 @@ class DeviceServer {
   TraceRec* trace_ = nullptr;
   TraceRec* dtrace_ = nullptr;
   uint32_t trace_cap_ = 0;
+  XLane* xl_ = nullptr;               // GPU peer lanes (fine-grained HBM, IPC-exported)
+  std::vector<void*> xl_imports_;     // per lane: the caller's imported reply slot
+  std::atomic<uint32_t> xl_live_{0};  // registered lanes (the waker polls while any)
 };
 
 }  // namespace ptype
