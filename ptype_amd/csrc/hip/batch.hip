@@ -1037,6 +1037,25 @@ __global__ void outbox_advance_kernel(unsigned long long* __restrict__ count, ui
   count[0] = 0;
 }
 
+// Multi-rank device-counted epochs route a bank's FULL capacity (the route and
+// all-to-all passes take host sizes); the slots past the bank's device count
+// become no-actor messages (answered locally, never on the wire).
+__global__ __launch_bounds__(256) void outbox_seal_kernel(uint32_t* __restrict__ actor, uint64_t cap,
+                                                          const unsigned long long* __restrict__ count) {
+  const unsigned long long n0 = count[0];
+  const uint64_t n = n0 < cap ? n0 : cap;
+  for (uint64_t i = n + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x)
+    actor[i] = 0xffffffffu;
+}
+
+void launch_outbox_seal(uintptr_t actor, uint64_t cap, uintptr_t count, uintptr_t stream) {
+  if (!actor || !count) throw std::invalid_argument("outbox_seal: null buffer");
+  if (cap == 0) return;
+  hipLaunchKernelGGL(outbox_seal_kernel, dim3(grid_cap((int64_t)cap, 256, 1024)), dim3(256), 0, as_stream(stream),
+                     (uint32_t*)actor, cap, (const unsigned long long*)count);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
 void launch_outbox_advance(uintptr_t count, uint64_t cap, uintptr_t epoch_m, int64_t j, uintptr_t stream) {
   if (!count || !epoch_m || j < 0) throw std::invalid_argument("outbox_advance: null buffer or negative index");
   hipLaunchKernelGGL(outbox_advance_kernel, dim3(1), dim3(1), 0, as_stream(stream), (unsigned long long*)count, cap,

@@ -204,6 +204,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("stats"), py::arg("checksum"), py::arg("stream"), py::arg("m_dev") = 0,
         "world-1 Send: registry resolution + handler dispatch in one pass into the caller's outputs "
         "(m_dev: a device u64 holding the batch's real length <= M, read by the kernel)");
+  m.def("outbox_seal", &launch_outbox_seal, py::arg("actor"), py::arg("cap"), py::arg("count"), py::arg("stream"),
+        "before a device-counted multi-rank epoch: actor[i] = no-actor for min(count[0], cap) <= i < cap");
   m.def("outbox_advance", &launch_outbox_advance, py::arg("count"), py::arg("cap"), py::arg("epoch_m"), py::arg("j"),
         py::arg("stream"),
         "after a device-counted epoch: epoch_m[j] = min(count[0], cap), count[0] = 0 (the consumed bank)");
@@ -273,7 +275,14 @@ PYBIND11_MODULE(_hip, m) {
                                                   "(one host thread + stream per rank on one GPU)")
       .def(py::init<int, bool, double>(), py::arg("R"), py::arg("loopback") = false, py::arg("link_gbps") = 0.0)
       .def_property_readonly("size", &FakeComm::size)
-      .def_property_readonly("loopback", &FakeComm::loopback);
+      .def_property_readonly("loopback", &FakeComm::loopback)
+      .def(
+          "allreduce_max",
+          [](FakeComm& c, int rank, uintptr_t dev, int n, uintptr_t stream) {
+            c.allreduce_max(rank, reinterpret_cast<uint64_t*>(dev), n, reinterpret_cast<hipStream_t>(stream));
+          },
+          py::arg("rank"), py::arg("dev"), py::arg("n"), py::arg("stream"), py::call_guard<py::gil_scoped_release>(),
+          "element-wise max of n u64 over the in-process ranks (collective over them)");
 
   py::class_<EpochEngine>(m, "EpochEngine",
                           "chunk-pipelined Send (route -> ncclAllToAll -> dispatch -> ncclAllToAll -> complete) "

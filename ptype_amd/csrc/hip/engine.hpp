@@ -45,6 +45,7 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
                        const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, uintptr_t out_val, uintptr_t out_st,
                        uintptr_t stats, uintptr_t checksum, uintptr_t stream, uintptr_t m_dev = 0);
 void launch_outbox_advance(uintptr_t count, uint64_t cap, uintptr_t epoch_m, int64_t j, uintptr_t stream);
+void launch_outbox_seal(uintptr_t actor, uint64_t cap, uintptr_t count, uintptr_t stream);
 void launch_pack_replies(uintptr_t v2, int R, int64_t C, uintptr_t reply, int vb, uintptr_t stats,
                          int64_t expected_per_rank, uintptr_t stream);
 void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,

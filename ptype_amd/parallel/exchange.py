@@ -75,6 +75,7 @@ class EpochStats:
     nomatch: int = 0
     failed: int = 0
     toowide: int = 0  # wire v3 replies that did not fit the agreed value plane (must stay 0)
+    pump_sealed: int = 0  # idle slots of device-pump epochs (routed as no-actor; not counted in nomatch)
     mailbox: dict | None = None  # HBM mailbox counters (mailbox delivery)
 
 
@@ -478,6 +479,9 @@ class ActorExchange:
             if self._device_pump_ok(outbox):
                 e, d = self._pump_device(outbox, max_epochs, check_every)
                 return epochs + e, delivered + d
+            if self._device_pump_multi_ok(outbox):
+                e, d = self._pump_device_multi(outbox, max_epochs, check_every)
+                return epochs + e, delivered + d
             while epochs < max_epochs:
                 n = outbox.pending()
                 mx = self._agree_max(n) if self.world > 1 else n
@@ -498,6 +502,92 @@ class ActorExchange:
         return bool(self.use_engine and self.world == 1 and not self.force_collectives and self.direct
                     and self.delivery != "mailbox" and outbox.cap <= self.max_chunk * self.chunks
                     and os.environ.get("PTYPE_DEVICE_PUMP", "1") != "0" and os.environ.get("PTYPE_LOCAL", "1") != "0")
+
+    def _device_pump_multi_ok(self, outbox) -> bool:
+        """Several ranks (RCCL, or FakeComm in-process ranks) on the native engine
+        with an outbox whose bank fits one Send."""
+        # (a destination slot holds a whole bank, so no tell can overflow: nothing to re-send)
+        return bool(self.use_engine and self.device.type == "cuda" and (self.world > 1 or self.force_collectives)
+                    and (self.fake is None or not self.fake[0].loopback)
+                    and outbox.cap <= self.max_chunk * self.chunks and self.C >= outbox.cap
+                    and os.environ.get("PTYPE_DEVICE_PUMP", "1") != "0")
+
+    def _pump_device_multi(self, outbox, max_epochs: int, check_every: int):
+        """Multi-rank pump without a host round trip per epoch.
+        Epoch j routes the active bank's FULL capacity -- the slots past its device
+        count are sealed as no-actor messages, so no host size is needed -- over
+        the padded all-to-all (wire v2: no agreement wait), the handlers emit into
+        the other bank, and a tiny kernel records the count.  After a group of
+        ``check_every`` epochs the group's counts and what is left pending are
+        max-reduced over the ranks ON THE DEVICE (RCCL all-reduce / FakeComm) and
+        copied to pinned memory; the host reads them while the next group already
+        runs.  Every rank reads the same agreed vector, so all stop after the same
+        group: when nothing is left anywhere."""
+        from ..ops import hip
+
+        k = max(2, check_every + (check_every & 1))
+        cap = outbox.cap
+        dev = self.device
+        p0 = outbox.active
+        val = torch.empty(cap, dtype=torch.int64, device=dev)  # replies of tells: discarded
+        st = torch.empty(cap, dtype=torch.int32, device=dev)
+        own = torch.zeros(2, k + 1, dtype=torch.int64, device=dev)  # per group: epoch counts + what is left
+        agreed = torch.zeros(2, k + 1, dtype=torch.int64, device=dev)
+        host = torch.zeros(2, 2, k + 1, dtype=torch.int64, pin_memory=True)  # [group buffer][own, agreed]
+        ev = [torch.cuda.Event(), torch.cuda.Event()]
+        start_count = outbox.banks[p0]["count"]  # active again after every (even) group
+        # wire v2 (no agreement wait inside a Send), direct dispatch (no ring to overflow)
+        prev = (self._capturing, self.delivery)
+        self._capturing, self.delivery = True, "direct"
+
+        def launch(h):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            for j in range(k):
+                b = outbox.bank
+                outbox.active ^= 1  # the handlers emit into the other bank (emptied when it was consumed)
+                hip().outbox_seal(B._ptr(b["actor"]), cap, B._ptr(b["count"]), stream)
+                self.send(B.MsgBatch(b["actor"], b["a0"], b["a1"], b["a2"], b["method"]), val, st)
+                hip().outbox_advance(B._ptr(b["count"]), cap, B._ptr(own[h]), j, stream)
+            own[h, k:].copy_(start_count[:1])  # pending after the group
+            agreed[h].copy_(own[h])
+            if self.fake is not None:  # max over the ranks, on the device side of the comm
+                self.fake[0].allreduce_max(self.rank, agreed[h].data_ptr(), k + 1, stream)
+            else:
+                dist.all_reduce(agreed[h], op=dist.ReduceOp.MAX, group=self.group)
+            host[h, 0].copy_(own[h], non_blocking=True)
+            host[h, 1].copy_(agreed[h], non_blocking=True)
+            ev[h].record()
+
+        def account(h):
+            mine = host[h, 0, :k].tolist()
+            self.counters.pump_sealed += k * cap - sum(mine)  # sealed slots route as no-actor: kept out of stats()
+            return sum(mine)
+
+        epochs = delivered = 0
+        try:
+            launch(0)
+            launched, h = k, 1
+            while True:
+                more = launched < max_epochs
+                if more:  # the next group runs while this one's agreed counts are read
+                    launch(h)
+                    launched += k
+                ev[h ^ 1].synchronize()
+                counts = host[h ^ 1, 1, :k].tolist()  # agreed: the same on every rank
+                left = int(host[h ^ 1, 1, k])
+                n_ep = sum(1 for m in counts if m)
+                epochs += n_ep
+                self.counters.epochs += n_ep
+                delivered += account(h ^ 1)
+                if not more or left == 0:
+                    if more:  # the group in flight (no-op: nothing was left) completes on every rank alike
+                        ev[h].synchronize()
+                        delivered += account(h)
+                    break
+                h ^= 1
+        finally:
+            self._capturing, self.delivery = prev
+        return epochs, delivered
 
     def _pump_device(self, outbox, max_epochs: int, check_every: int):
         """World-1 pump without a host round trip per epoch.  Epoch j sends the
@@ -638,7 +728,9 @@ class ActorExchange:
 
     def stats(self) -> EpochStats:
         c = self.counters
-        s = EpochStats(sent=c.sent, epochs=c.epochs, wire_bytes=c.wire_bytes, resends=c.resends)
+        s = EpochStats(sent=c.sent, epochs=c.epochs, wire_bytes=c.wire_bytes, resends=c.resends,
+                       pump_sealed=c.pump_sealed)
+        s.nomatch -= c.pump_sealed
         for b in self.bufs:
             w = B.ws_stats(b.ws).tolist()
             s.nomatch += w[B.STAT_NOMATCH]

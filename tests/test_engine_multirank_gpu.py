@@ -317,3 +317,75 @@ def test_gpu_replicated_prime_over_fakecomm_r4():
             assert torch.equal(c2, total if r == 3 else torch.zeros(P, dtype=torch.int64)), r
         else:
             assert int(c1.sum()) == 0 and int(c2.sum()) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_multirank_device_pump_no_host_round_trip_per_epoch(monkeypatch):
+    """the FakeComm R = 4 token ring on the device-counted
+    multi-rank pump -- each epoch routes its outbox bank by the bank's DEVICE
+    count (idle slots sealed), and the ranks agree on what is left with a device
+    all-reduce once per group of epochs: no host agreement per epoch (counted),
+    and every actor's visits match a plain simulation."""
+    from ptype_amd.ops.outbox import DeviceOutbox
+    from ptype_amd.ops.records import METHOD_FORWARD
+    from ptype_amd.parallel.exchange import ActorExchange
+
+    R, n_per, T, hops, stride = 4, 3000, 1500, 11, 5
+    n = n_per * R
+    cap = 3 * T
+    fc = hip().FakeComm(R)
+    starts = [[(r * 701 + 17 * t) % n for t in range(T)] for r in range(R)]
+    states, errors, epochs, agrees, sealed = [None] * R, [], [None] * R, [0] * R, [0] * R
+    orig = ActorExchange._agree_max
+
+    def counting(self, v):
+        agrees[self.rank] += 1
+        return orig(self, v)
+
+    monkeypatch.setattr(ActorExchange, "_agree_max", counting)
+    start = threading.Barrier(R)
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                tab = RegistryTable(4 * n, device="cuda")
+                ids = torch.arange(n)
+                tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
+                st = torch.zeros(n_per, dtype=torch.int64, device="cuda")
+                ex = ActorExchange(tab, cap, chunks=1, state=st, slack=3.0, fake=(fc, r))
+                ob = DeviceOutbox(cap, device="cuda")
+                assert ex._device_pump_multi_ok(ob)
+                s0 = torch.tensor(starts[r], dtype=torch.int64)
+                init = B.MsgBatch(s0.to(torch.int32).cuda(), ((s0 + stride) % n).cuda(),
+                                  torch.full((T,), hops, dtype=torch.int64, device="cuda"),
+                                  torch.full((T,), stride | (n << 32), dtype=torch.int64, device="cuda"),
+                                  METHOD_FORWARD)
+                start.wait()
+                epochs[r], _ = ex.pump(ob, initial=init, check_every=4)
+                s.synchronize()
+                states[r] = st.cpu()
+                sealed[r] = ex.stats().pump_sealed
+                assert ob.dropped == 0
+        except BaseException as e:  # noqa: BLE001 - surfaced below
+            errors.append((r, repr(e)))
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(R)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in threads), "a rank hung"
+    assert not errors, errors
+    exp = torch.zeros(n, dtype=torch.int64)
+    for ss in starts:
+        for a in ss:
+            for _ in range(hops + 1):
+                exp[a] += 1
+                a = (a + stride) % n
+    for r in range(R):
+        assert torch.equal(states[r], exp[r::R]), r
+    assert all(e == hops for e in epochs), epochs
+    assert agrees == [1] * R, agrees  # the initial batch's size only: none per epoch
+    assert all(x > 0 for x in sealed), sealed  # the device-counted path ran
