@@ -72,6 +72,8 @@ def _parse():
                         "2: K2 enqueue + K3 drain; at N > 1 on receipt), or one fused resolve-and-run pass")
     p.add_argument("--sharding", choices=["actor", "arrival"], default="actor",
                    help="mailbox rings: per actor (every actor's messages FIFO in one ring) or per arrival tile")
+    p.add_argument("--mailbox-shards", type=int, default=256, help="HBM mailbox shard rings per GPU")
+    p.add_argument("--mailbox-slots", type=int, default=0, help="slots per mailbox ring (0: 2x the uniform load)")
     p.add_argument("--zipf", type=float, default=0.0, metavar="S",
                    help="skewed load: actor popularity Zipf(S) (hot actors scattered over the GPUs); batches "
                         "pre-generated outside the timed loop, so compare against --zipf 0 --pregen")
@@ -270,7 +272,8 @@ def main():
         # mailbox delivery: actor-sharded rings (each actor's messages in message
         # order in one ring) unless --sharding arrival (tile-sharded queues)
         ex = ActorExchange(table, Mq, chunks=chunks, state=state, fake=fake, delivery=delivery,
-                           mailbox_ordered=sharding == "actor")
+                           mailbox_ordered=sharding == "actor", mailbox_shards=args.mailbox_shards,
+                           mailbox_slots=args.mailbox_slots)
         _LIVE_EXCHANGES.append(weakref.ref(ex))  # (weak: a finished measurement's buffers stay freeable)
         if Mq == M and method == METHOD_CALC_MULTIPLY:
             rq, v, t = req, val, st

@@ -57,6 +57,7 @@ struct GpuConfig {
   bool cpu = false;           // actor runtime on the host reference path (tests, GPU-less hosts)
   uint32_t mailbox_shards = 256;
   uint32_t mailbox_slots = 0;  // 0: sized from max_batch
+  std::string delivery = "auto";  // "mailbox": every Send through the HBM mailboxes; "direct"; "auto"
   bool watch = true;          // follow the store (shard records, leases) into the GPU registry mirror
   // rank failures (runtime.py recover): Join's group re-forms through the store
   bool elastic = true;          // recover a failed Send (abort, re-form, re-home, re-send)

@@ -67,6 +67,7 @@ enum MboxStat : int {
   kMbFailed = 4,     // handler status != ok
   kMbHoles = 5,      // positions skipped as holes
   kMbSerial = 6,     // records run serialised (same actor twice in a window)
+  kMbSpilled = 7,    // stateless messages whose ring was full, run from the batch by the drain
   kMbTicket = 8,     // reserved (the epoch drain's tickets are per shard: kMboxCtrTicket)
   kMbStatWords = 16,
 };

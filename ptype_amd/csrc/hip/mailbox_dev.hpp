@@ -48,8 +48,15 @@ __device__ __forceinline__ unsigned long long* ctr_head(const MboxView& mv, uint
 // every other 16 B of 64 records: the enqueue's DRAM writes were 419 MB for 268 MB
 // of records (PMC WRITE_SIZE).  Bench mailbox step: 0.247 ms (32-B records) ->
 // 0.215 ms (planes, de-aliased; see the pad in the Mailboxes constructor).
+// Ring position -> slot.  Each shard's ring is ROTATED by a hashed offset: the
+// shards' tails advance in step under uniform traffic, and with power-of-two
+// ring strides their active lines would sit at the same offset of every ring --
+// the same HBM channels (S = 256: drain 114 us vs 66 us at S = 64, the rings
+// 2 MB apart).  The rotation spreads them over the channels; a slot stays a
+// bijection of (shard, position mod Q).
 __device__ __forceinline__ uint64_t slot_at(const MboxView& mv, uint32_t s, uint64_t pos) {
-  return ((uint64_t)s << mv.log_q) | (pos & ((1ull << mv.log_q) - 1));
+  const uint64_t rot = mv.log_q ? (uint64_t)((s * 0x9E3779B1u) >> (32 - mv.log_q)) : 0ull;
+  return ((uint64_t)s << mv.log_q) | ((pos + rot) & ((1ull << mv.log_q) - 1));
 }
 __device__ __forceinline__ uint32_t* rec_a(const MboxView& mv, uint64_t slot) {
   return mv.rec + slot * (mv.planar ? 4 : 8);

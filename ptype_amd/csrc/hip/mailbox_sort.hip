@@ -66,6 +66,12 @@ constexpr uint32_t kOrdStateMax = 4096;  // a shard's actors whose state is stag
 // ---------------------------------------------------------------- K2s pass 1: count
 constexpr uint32_t kGroupBlocks = 32;  // the scatter's prefix: group sums + rows inside the group
 constexpr uint32_t kNoSlot = 0xffffffffu;
+// A stateless batch's message whose shard ring is full SPILLS: the parallel drain
+// runs it straight from the batch (its route word + argument columns) in message
+// order, like any other -- no STATUS_OVERFLOW, so no re-send round and no host
+// read of an overflow count.  Ordered batches keep the ring's
+// FIFO and answer kStatusOverflow (send_all re-sends the tail).
+constexpr uint32_t kSpillSlot = 0xfffffffeu;
 
 template <int MODE, bool ARRIVAL>
 __global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_s, uint32_t* __restrict__ hist,
@@ -135,8 +141,8 @@ template <bool ARRIVAL, bool A2, bool MC>
 __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv, const uint32_t* __restrict__ hist,
                                                           const uint32_t* __restrict__ gsum,
                                                           const uint32_t* __restrict__ rw,
-                                                          uint32_t* __restrict__ sidx, ReplyView rv) {
-  // LDS sized by the shard count (32 B per shard): occupancy is not capped by the 1024-shard maximum
+                                                          uint32_t* __restrict__ sidx, ReplyView rv, bool spill) {
+  // LDS sized by the shard count (16 + 4 * waves B per shard): occupancy is not capped by the 1024-shard maximum
   extern __shared__ __align__(16) unsigned char smem_sc[];
   const uint32_t S = 1u << mv.log_s;
   unsigned long long* base = reinterpret_cast<unsigned long long*>(smem_sc);  // ring position of offset 0 (tail)
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
     const uint64_t free = hd + Q > tl ? hd + Q - tl : 0;
     room[s] = (uint32_t)(free < 0xffffffffull ? free : 0xffffffffull);
   }
-  unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0;
+  unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0, n_spill = 0;
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
   for (uint32_t t = t0; t < t1; ++t) {
     for (uint32_t s = lane; s < S; s += kWave) wcnt(w, s) = 0;  // this wave's row only
@@ -207,8 +213,13 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
         continue;
       }
       const uint32_t off = wcnt(w, sh[k]) + wr[k];
-      if (off >= room[sh[k]]) {  // the ring is full: answered now, re-sent by send_all
-        ++n_ovf;
+      if (off >= room[sh[k]]) {  // the ring is full
+        if (spill) {  // stateless batch: the drain runs it from the batch
+          ++n_spill;
+          sidx[i] = kSpillSlot;
+          continue;
+        }
+        ++n_ovf;  // answered now, re-sent by send_all
         sidx[i] = kNoSlot;
         write_status(rv, origin, kStatusOverflow);
         continue;
@@ -234,6 +245,10 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
     __syncthreads();  // wcnt rows are reused by the next tile
   }
   block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
+  if (spill) {
+    __syncthreads();  // block_add_stats' LDS partials are reused
+    block_add_stats(mv.stats, n_spill, kMbSpilled, 0, -1, 0, -1);
+  }
 }
 
 // ---------------------------------------------------------------- compact record decode
@@ -305,6 +320,7 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 // coalesced.  The last block commits every shard (and clears the group sums).
 template <int FIXED>
 __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ sidx,
+                                                            const uint32_t* __restrict__ rw,
                                                             int64_t* __restrict__ state, uint32_t n_state,
                                                             uint64_t delay_ticks, OutboxView ob, ReplyView rv,
                                                             uint32_t* __restrict__ gsum, uint32_t ngroups,
@@ -324,17 +340,29 @@ __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn 
     u32x4 ha[kSK];
 #pragma unroll
     for (int k = 0; k < kSK; ++k)
-      ha[k] = sl[k] != kNoSlot ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k])) : u32x4{0u, 0u, 0u, 0u};
+      ha[k] = sl[k] < kSpillSlot ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k])) : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       if (sl[k] == kNoSlot) continue;  // answered by the scatter (no actor / ring full)
-      u32x4 hb = {0u, 0u, 0u, 0u};
-      int64_t a2v = 0;
-      if (rec_is_long(ha[k])) {
-        hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
-        if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
+      SortRec x;
+      if (sl[k] == kSpillSlot) {  // its ring was full: the message runs straight from the batch
+        const int64_t i = tile_index(t, k);
+        x.valid = true;
+        x.mb = rw[i];
+        x.method = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
+        x.flags = 0;
+        x.a0 = in.a0[i];
+        x.a1 = in.a1 ? in.a1[i] : 0;
+        x.a2 = in.a2 ? in.a2[i] : 0;
+      } else {
+        u32x4 hb = {0u, 0u, 0u, 0u};
+        int64_t a2v = 0;
+        if (rec_is_long(ha[k])) {
+          hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
+          if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
+        }
+        x = decode_sorted(ha[k], hb, a2v);
       }
-      const SortRec x = decode_sorted(ha[k], hb, a2v);
       const uint32_t origin = in.origin_base + (uint32_t)tile_index(t, k);
       if (!x.valid) {
         ++holes;
@@ -408,22 +436,34 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   const uint32_t tot = tot_s;
   const uint64_t n = tot < free ? tot : free;
   unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
+  // window records are loaded one window AHEAD: the next window's loads are in
+  // flight while this one's bins run serially (the block is one per shard, so
+  // nothing else on the CU would hide their latency)
+  SortRec x[kOrdK];
+  uint64_t slot[kOrdK];
+  const auto load_window = [&](uint64_t base) {
+    const uint64_t end = lo + n < base + kOrdWin ? lo + n : base + kOrdWin;
+#pragma unroll
+    for (int k = 0; k < kOrdK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
+      const uint64_t q = base + (uint64_t)w * (kWave * kOrdK) + (uint64_t)k * kWave + lane;
+      slot[k] = slot_at(mv, s, q);
+      if (q < end) {
+        x[k] = load_sorted(mv, slot[k]);
+      } else {
+        x[k].valid = false;
+        x[k].mb = 0;
+      }
+    }
+  };
+  if (n) load_window(lo);
   for (uint64_t w0 = lo; w0 < lo + n; w0 += kOrdWin) {
     const uint64_t w1 = lo + n < w0 + kOrdWin ? lo + n : w0 + kOrdWin;
     for (uint32_t b = lane; b < kOrdThreads; b += kWave) L.wcnt[w][b] = 0;
-    SortRec x[kOrdK];
     uint32_t bin[kOrdK], wr[kOrdK];
-    uint64_t slot[kOrdK];
 #pragma unroll
-    for (int k = 0; k < kOrdK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
+    for (int k = 0; k < kOrdK; ++k) {
       const uint64_t q = w0 + (uint64_t)w * (kWave * kOrdK) + (uint64_t)k * kWave + lane;
-      slot[k] = slot_at(mv, s, q);
-      if (q < w1) {
-        x[k] = load_sorted(mv, slot[k]);
-        if (!x[k].valid) ++holes;
-      } else {
-        x[k].valid = false;
-      }
+      if (q < w1 && !x[k].valid) ++holes;
     }
 #pragma unroll
     for (int k = 0; k < kOrdK; ++k) {
@@ -469,6 +509,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
       L.a2[d] = x[k].a2;
     }
     __syncthreads();
+    if (w0 + kOrdWin < lo + n) load_window(w0 + kOrdWin);  // the next window's records, in flight meanwhile
     {  // this thread's bin, serially in ring order
       const unsigned b = threadIdx.x, e = L.bstart[b] + L.bcount[b];
       if (L.bcount[b] > 1) serial += L.bcount[b] - 1;  // records that waited behind their bin's earlier ones
@@ -499,22 +540,29 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
 }
 
 // Ordered drain's replies, staged at ring slots, gathered into message order.
-__global__ __launch_bounds__(256) void mbx_complete_kernel(const uint32_t* __restrict__ sidx, int64_t M,
-                                                           uint32_t origin_base, const int64_t* __restrict__ sval,
+// Tile-granular like the parallel drain: block b gathers the tiles whose
+// records scatter block b wrote, so its reads hit ~S short runs of contiguous
+// slots (lines shared by the block's waves) instead of one line per message.
+__global__ __launch_bounds__(kST) void mbx_complete_kernel(SortIn in, const uint32_t* __restrict__ sidx,
+                                                           const int64_t* __restrict__ sval,
                                                            const int32_t* __restrict__ sst, ReplyView rv) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < M; i0 += stride * 4) {
-    uint32_t sl[4];
+  const uint32_t v = virt_block(blockIdx.x, in.G);
+  const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
+  for (uint32_t t = t0; t < t1; ++t) {
+    uint32_t sl[kSK];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) sl[u] = i0 + u * stride < M ? __builtin_nontemporal_load(sidx + i0 + u * stride) : kNoSlot;
-    int64_t v[4];
-    int32_t st[4];
+    for (int k = 0; k < kSK; ++k) {
+      const int64_t i = tile_index(t, k);
+      sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
+    }
+    int64_t val[kSK];
+    int32_t st[kSK];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (sl[u] != kNoSlot) v[u] = sval[sl[u]], st[u] = sst[sl[u]];
+    for (int k = 0; k < kSK; ++k)
+      if (sl[k] < kSpillSlot) val[k] = sval[sl[k]], st[k] = sst[sl[k]];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (sl[u] != kNoSlot) put_reply(rv, origin_base + (uint32_t)(i0 + u * stride), v[u], st[u]);
+    for (int k = 0; k < kSK; ++k)
+      if (sl[k] < kSpillSlot) put_reply(rv, in.origin_base + (uint32_t)tile_index(t, k), val[k], st[k]);
   }
 }
 
@@ -596,8 +644,9 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_COUNT
   PT_HIP_CHECK(hipGetLastError());
 #define PT_SCAT(AR, A2, MC)                                                                                      \
-  hipLaunchKernelGGL((mbx_scatter_kernel<AR, A2, MC>), dim3(in.G), dim3(kST), (size_t)32 * S, st, in, mv_,                   \
-                     (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_, sort_sidx_, rv)
+  hipLaunchKernelGGL((mbx_scatter_kernel<AR, A2, MC>), dim3(in.G), dim3(kST), (size_t)(16 + 4 * (kST / kWave)) * S, st, in, mv_,                   \
+                     (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_, sort_sidx_, rv, \
+                     !a.ordered)
 #define PT_SCAT_AR(AR)                                  \
   do {                                                  \
     if (a.a2 && a.method_col) PT_SCAT(AR, true, true);   \
@@ -632,17 +681,18 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(S), dim3(kOrdThreads), lds, st, mv_, sort_gsum_, ngroups,
                        (int64_t*)a.state, a.n_state, a.delay_ticks, ob, stage_val_, stage_st_);
     PT_HIP_CHECK(hipGetLastError());
-    const unsigned gc = (unsigned)std::min<int64_t>(std::max<int64_t>((a.M + 1023) / 1024, 1), 2048);
-    hipLaunchKernelGGL(mbx_complete_kernel, dim3(gc), dim3(256), 0, st, (const uint32_t*)sort_sidx_, a.M,
-                       a.origin_base, (const int64_t*)stage_val_, (const int32_t*)stage_st_, rv);
+    hipLaunchKernelGGL(mbx_complete_kernel, dim3(in.G), dim3(kST), 0, st, in, (const uint32_t*)sort_sidx_,
+                       (const int64_t*)stage_val_, (const int32_t*)stage_st_, rv);
   } else {
     if (a.fixed_method == kCalculatorMultiply)
       hipLaunchKernelGGL((mbx_drain_msg_kernel<kCalculatorMultiply>), dim3(in.G), dim3(kST), 0, st, mv_, in,
-                         (const uint32_t*)sort_sidx_, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_,
+                         (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_, (int64_t*)a.state, a.n_state,
+                         a.delay_ticks, ob, rv, sort_gsum_,
                          ngroups, sort_ticket_);
     else
       hipLaunchKernelGGL((mbx_drain_msg_kernel<0>), dim3(in.G), dim3(kST), 0, st, mv_, in,
-                         (const uint32_t*)sort_sidx_, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_,
+                         (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_, (int64_t*)a.state, a.n_state,
+                         a.delay_ticks, ob, rv, sort_gsum_,
                          ngroups, sort_ticket_);
   }
   PT_HIP_CHECK(hipGetLastError());

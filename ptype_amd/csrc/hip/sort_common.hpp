@@ -11,9 +11,16 @@
 
 namespace ptype {
 
-constexpr int kST = 256;             // count / scatter threads per block
-constexpr int kSK = 8;               // messages per thread per tile
-constexpr int kSTile = kST * kSK;    // 2048 messages
+// 512 threads (8 waves) per block, 4096-message tiles: with 256 shards a tile
+// gives each shard a run of ~16 records (256 B, two whole lines) instead of ~8
+// -- half-written lines evicted from L2 before their other half arrived made
+// the 2048-message tiles write 1.9x the record bytes (PMC, r3).
+#ifndef PTYPE_SORT_THREADS
+#define PTYPE_SORT_THREADS 512
+#endif
+constexpr int kST = PTYPE_SORT_THREADS;  // count / scatter threads per block
+constexpr int kSK = 8;                   // messages per thread per tile
+constexpr int kSTile = kST * kSK;        // 4096 messages
 constexpr int kSWave = kSK * kWave;  // a wave's contiguous run of a tile (512)
 
 

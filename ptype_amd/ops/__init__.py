@@ -54,8 +54,22 @@ def hip():
     return _HIP
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def raw_stream(device) -> int:
+    """The current HIP stream of ``device`` as an integer handle.  The raw
+    accessor skips building a torch Stream object (~1.5 us on every Send)."""
+    idx = device.index if isinstance(device, torch.device) else device
+    if idx is None:
+        idx = torch.cuda.current_device()
+    if _raw_stream is not None:
+        return _raw_stream(idx)
+    return torch.cuda.current_stream(idx).cuda_stream
+
+
 def _stream(t: torch.Tensor) -> int:
-    return torch.cuda.current_stream(t.device).cuda_stream
+    return raw_stream(t.device)
 
 
 def _ptr(t: torch.Tensor | None) -> int:

@@ -27,11 +27,11 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _ptr, hip
+from . import _ptr, hip, raw_stream
 from .batch import MsgBatch, _handler_ref, fold_step
 from .records import STATUS_NO_ACTOR, STATUS_OK, method_ordered
 
-STAT_NAMES = ("enqueued", "overflow", "no_actor", "processed", "failed", "holes", "serialised")
+STAT_NAMES = ("enqueued", "overflow", "no_actor", "processed", "failed", "holes", "serialised", "spilled")
 SORT_MAX_SHARDS = 1024  # csrc/hip/mailbox.hpp kMboxSortMaxShards
 
 
@@ -61,7 +61,7 @@ class Mailboxes:
         return int(self._m.handle)
 
     def _stream(self) -> int:
-        return torch.cuda.current_stream(self.device).cuda_stream
+        return raw_stream(self.device)
 
     def enqueue(self, batch: MsgBatch, table, out_val: torch.Tensor, out_status: torch.Tensor, rank_self: int = 0,
                 origin_base: int = 0, live: bool = False, arrival: bool = False) -> None:
@@ -115,6 +115,9 @@ class Mailboxes:
         fixed = int(batch.method) if isinstance(batch.method, int) else 0
         if sort is None:
             sort = self.shards <= SORT_MAX_SHARDS
+        # a stateless batch on the sorted kernels never answers STATUS_OVERFLOW: a
+        # message whose ring is full spills to the drain, which runs it from the batch
+        self.last_spills = bool(sort and not ordered)
         if not sort:
             self.enqueue(batch, table, out_val, out_status, rank_self=rank_self, arrival=arrival)
             self.drain(state, out_val, out_status, ordered=ordered, delay_us=delay_us, outbox=outbox,

@@ -51,6 +51,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import batch as B
+from ..ops import raw_stream
 from ..ops.packed import META_CAP
 from ..ops.records import STATUS_OVERFLOW, method_ordered
 from ..ops.table import RegistryTable
@@ -244,7 +245,7 @@ class ActorExchange:
             int(req.method) if uniform else 0, req.M, B._ptr(self.table.table), self.table.cap, B._ptr(d), n_dir,
             affine, fmt.nargs, fmt.method_col, B._ptr(out_val), B._ptr(out_status), B._ptr(state),
             0 if state is None else state.numel(), int(self.delay_us) * 100, ob, ob_cap, self.direct and not mb,
-            B._ptr(self.checksum), torch.cuda.current_stream(self.device).cuda_stream, self.packed_active(),
+            B._ptr(self.checksum), raw_stream(self.device), self.packed_active(),
             mb, self.mailbox_ordered)
         if self.world > 1 or self.force_collectives:
             w = self._engine.last_wire()
@@ -290,7 +291,7 @@ class ActorExchange:
         eng.send(B._ptr(req.actor), B._ptr(req.a0), B._ptr(req.a1), B._ptr(req.a2), B._ptr(mcol),
                  int(req.method) if uniform else 0, req.M, B._ptr(self.table.table), self.table.cap, B._ptr(d), n_dir,
                  affine, B._ptr(out_val), B._ptr(out_status), B._ptr(state), 0 if state is None else state.numel(),
-                 int(self.delay_us) * 100, self.mailbox_ordered, torch.cuda.current_stream(self.device).cuda_stream)
+                 int(self.delay_us) * 100, self.mailbox_ordered, raw_stream(self.device))
         w = eng.last_wire()
         w["req_words"] *= self.world  # all peers, per chunk (as the epoch engine reports it)
         w["rep_words"] *= self.world
@@ -358,6 +359,12 @@ class ActorExchange:
         dev = self.device
         out_val = torch.empty(M, dtype=torch.int64, device=dev) if out_val is None else out_val
         out_status = torch.empty(M, dtype=torch.int32, device=dev) if out_status is None else out_status
+        self._last_mailbox = self._use_mailbox(req)
+        if self._last_mailbox:  # world 1: one sorted mailbox pass over the whole batch (no wire, no chunks)
+            self.counters.sent += M
+            self.counters.epochs += 1
+            with trace.range("ptype.send.mailbox"):
+                return self._send_mailbox(req, out_val, out_status)
         n = self.chunks
         bounds = [min(M, i * self.max_chunk) for i in range(n + 1)]
         R, C = self.world, self.C
@@ -367,10 +374,6 @@ class ActorExchange:
         wq, wr = R * fmt.req_words(C), R * B.WireFormat.rep_words(C)
         self.counters.sent += M
         self.counters.epochs += n
-        self._last_mailbox = self._use_mailbox(req)
-        if self._last_mailbox:
-            with trace.range("ptype.send.mailbox"):
-                return self._send_mailbox(req, out_val, out_status)
         if self.use_engine and self._use_sorted():
             with trace.range("ptype.send.sorted"):
                 return self._send_sorted(req, out_val, out_status)
@@ -704,6 +707,9 @@ class ActorExchange:
         take this exit together -- no count, no host round trip, no agreement."""
         if self.world == 1 and not self.force_collectives and not self._last_mailbox and self.C >= self.max_chunk:
             return True  # one destination whose slot holds a whole chunk: nothing can overflow
+        if (self.world == 1 and not self.force_collectives and self._last_mailbox and self.mailboxes is not None
+                and getattr(self.mailboxes, "last_spills", False)):
+            return True  # stateless mailbox Send: full rings spill to the drain (no STATUS_OVERFLOW)
         if self._mailbox_on_receipt():
             # the slots fit, but K2 on receipt can still answer STATUS_OVERFLOW when a
             # receiver's rings fill (skewed traffic to one shard): count them (ADVICE r2)

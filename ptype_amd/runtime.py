@@ -66,7 +66,7 @@ class DeviceRuntime:
     def __init__(self, device=None, actors: int = 1024, ring: int = 4096, idle_ms: float = 200.0,
                  delay_us: int = 0, max_batch: int = 1 << 20, chunks: int = 0, random_state: bool = False,
                  group=None, shm: bool = True, service: str = "", mailbox_shards: int = 256,
-                 mailbox_slots: int = 0):
+                 mailbox_slots: int = 0, delivery: str = "auto"):
         if device is None:
             device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         self.device = torch.device(device)
@@ -116,6 +116,7 @@ class DeviceRuntime:
         self._sends = 0
         self._watchdog = None
         self.mailbox_shards, self.mailbox_slots = int(mailbox_shards), int(mailbox_slots)
+        self.delivery = delivery or "auto"  # "mailbox": every Send through the HBM mailboxes (ActorExchange)
         self._exchange = None
         self.shards: dict[str, list[dict]] = {}
         self.mirror = None  # RegistryMirror (watch-driven) once attached to a control plane
@@ -166,7 +167,7 @@ class DeviceRuntime:
         rank = d.get_rank() if d else 0
         rt = cls(device_for_rank(rank), actors=g.actors, ring=g.ring, idle_ms=g.idle_ms, delay_us=g.delay_us,
                  max_batch=g.max_batch, service=cfg.service_name, mailbox_shards=g.mailbox_shards,
-                 mailbox_slots=g.mailbox_slots)
+                 mailbox_slots=g.mailbox_slots, delivery=g.delivery)
         rt._tcp_store, rt._owns_group = tcp, owns
         rt._addr = (core_cluster.local_addr, int(cfg.port))
         if members is not None and g.elastic:
@@ -256,7 +257,7 @@ class DeviceRuntime:
             from .parallel.exchange import ActorExchange
 
             self._exchange = ActorExchange(self.table, self.max_batch, chunks=self.chunks, group=self.group,
-                                           state=self.state, delay_us=self.delay_us,
+                                           state=self.state, delay_us=self.delay_us, delivery=self.delivery,
                                            mailbox_shards=self.mailbox_shards, mailbox_slots=self.mailbox_slots)
         return self._exchange
 

@@ -44,16 +44,33 @@ def available() -> bool:
     return bool(h and h.roctx_available())
 
 
-@contextlib.contextmanager
+class _Range:
+    __slots__ = ("h", "name")
+
+    def __init__(self, h, name):
+        self.h, self.name = h, name
+
+    def __enter__(self):
+        self.h.roctx_push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        self.h.roctx_pop()
+        return False
+
+
+_NULL = contextlib.nullcontext()
+_ROCTX = None  # the module when the roctx library is loaded, else False (decided once)
+
+
 def range(name: str):  # noqa: A001 - mirrors roctxRange naming
-    h = _h()
-    if h is not None:
-        h.roctx_push(name)
-    try:
-        yield
-    finally:
-        if h is not None:
-            h.roctx_pop()
+    """roctx range around a block; a shared no-op context (no allocation, no
+    generator frame) when no roctx library is loaded -- it sits on every Send."""
+    global _ROCTX
+    if _ROCTX is None:
+        h = _h()
+        _ROCTX = h if (h is not None and h.roctx_available()) else False
+    return _Range(_ROCTX, name) if _ROCTX else _NULL
 
 
 def mark(name: str) -> None:

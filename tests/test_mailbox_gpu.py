@@ -354,6 +354,34 @@ def test_sorted_mailbox_overflow_keeps_fifo_prefix():
         assert bool(ok_s[:1024].all()) and not bool(ok_s[1024:].any())  # the first 1024 in message order ran
 
 
+def test_sorted_mailbox_stateless_spills_instead_of_overflow():
+    """a stateless batch whose rings are far too small (all traffic
+    on 4 x 1024 slots) spills: every message is answered by the drain straight
+    from the batch -- no STATUS_OVERFLOW, so ``send_all`` needs no re-send round
+    and no host read of an overflow count."""
+    n, M = 64, 50_000
+    t, _ = placed_table(n)
+    mb = Mailboxes(DEV, shards=4, slots=1024)
+    req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=5, device=DEV)
+    v, st = mb.send(req, t, None)
+    torch.cuda.synchronize()
+    assert bool((st == STATUS_OK).all()) and torch.equal(v, req.a0 * req.a1)
+    s = mb.stats()
+    assert s["overflow"] == 0 and s["spilled"] == M - 4 * 1024 and s["processed"] == M, s
+    # through the exchange: send_all takes the no-overflow exit (no re-send, no count read)
+    ex = ActorExchange(t, M, chunks=1, delivery="mailbox", mailbox_shards=4, mailbox_slots=1024)
+    calls = []
+    orig = torch.Tensor.sum
+    try:
+        torch.Tensor.sum = lambda self, *a, **k: calls.append(1) or orig(self, *a, **k)
+        v2, st2 = ex.send_all(req)
+    finally:
+        torch.Tensor.sum = orig
+    torch.cuda.synchronize()
+    assert torch.equal(v2, req.a0 * req.a1) and bool((st2 == STATUS_OK).all())
+    assert ex.counters.resends == 0 and not calls
+
+
 def test_live_mailbox_sustained_overload_keeps_consumer_rate():
     """two producer streams keep a persistent consumer ~3x over
     capacity for more than a second.  A full ring reserves nothing (no holes),
