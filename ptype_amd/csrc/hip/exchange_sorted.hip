@@ -803,12 +803,18 @@ void SortedExchange::send(const SxSend& a) {
     if (i > 0) serve(i - 1);
   }
   serve(chunks_ - 1);
-  // this Send's agreement, for Send + 2 (the comm stream is past every chunk's scatter)
-  allreduce_meta(meta, comm_stream_);
-  PT_HIP_CHECK(hipMemcpyAsync(meta_host_ + cur * kMetaWords, meta, kMetaWords * sizeof(uint64_t),
-                              hipMemcpyDeviceToHost, comm_stream_));
-  PT_HIP_CHECK(hipEventRecord(ev_meta_[cur], comm_stream_));
-  meta_send_[cur] = capturing ? -1 : sends_;
+  // this Send's agreement, for Send + 2 (the comm stream is past every chunk's
+  // scatter).  A captured Send keeps the layout in force (a replay runs no host
+  // code to adopt a new one), so it records no agreement.
+  if (!capturing) {
+    allreduce_meta(meta, comm_stream_);
+    PT_HIP_CHECK(hipMemcpyAsync(meta_host_ + cur * kMetaWords, meta, kMetaWords * sizeof(uint64_t),
+                                hipMemcpyDeviceToHost, comm_stream_));
+    PT_HIP_CHECK(hipEventRecord(ev_meta_[cur], comm_stream_));
+    meta_send_[cur] = sends_;
+  } else {
+    meta_send_[cur] = -1;
+  }
   for (int i = 0; i < chunks_; ++i) {
     int64_t lo, m;
     (void)chunk_in(i, lo, m);

@@ -10,6 +10,11 @@ thread + stream per rank, the all-to-alls as device copies between them).
 * a message wider than the layout in force is answered STATUS_OVERFLOW (its slot
   carries a null record) and send_all re-sends it until the agreed layout grows.
 """
+import json
+import os
+import subprocess
+import sys
+import textwrap
 import threading
 
 import pytest
@@ -21,6 +26,8 @@ from ptype_amd.ops.mailbox import audit_fold
 from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_SEQ_FOLD, STATUS_OK, STATUS_OVERFLOW
 from ptype_amd.ops.table import RegistryTable, actor_keys
 from ptype_amd.parallel.exchange import ActorExchange
+
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -155,3 +162,67 @@ def test_sorted_exchange_too_wide_is_overflow_then_resent():
     for first, v, sts, ref, resends in _run_ranks(R, body):
         assert int((first == STATUS_OVERFLOW).sum()) == len(first[::100])
         assert bool((sts == STATUS_OK).all()) and torch.equal(v, ref) and resends >= 1
+
+
+_GRAPH_SCRIPT = textwrap.dedent("""
+    import json, os, sys, torch, torch.distributed as dist
+    sys.path.insert(0, os.environ["PTYPE_ROOT"])
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
+    from ptype_amd.ops.table import RegistryTable, actor_keys
+    from ptype_amd.parallel.exchange import ActorExchange
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    n, M = 1 << 15, 1 << 20
+    t = RegistryTable(2 * n, device=dev)
+    ids = torch.arange(n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(3))
+    t.upsert(actor_keys(ids), torch.zeros(n, dtype=torch.int32), perm.to(torch.int32))
+    t.enable_directory(n, affine_world=1)
+    ex = ActorExchange(t, M, chunks=2, delivery="mailbox", mailbox_ordered=False)
+    assert ex.force_collectives and ex._use_sorted()
+    req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=1, device=dev)
+    val = torch.empty(M, dtype=torch.int64, device=dev)
+    st = torch.empty(M, dtype=torch.int32, device=dev)
+    for _ in range(3):  # past the start-up layout: Send 2 runs on an agreed one
+        ex.send(req, val, st)
+    torch.cuda.synchronize()
+    print("warm", flush=True, file=sys.stderr)
+    seed = torch.tensor([11], dtype=torch.int64, device=dev)
+    def prologue():
+        B.gen_requests(M, n, METHOD_CALC_MULTIPLY, device=dev, out=req, seed_tensor=seed)
+        seed.add_(1)
+    g = ex.capture(req, val, st, prologue=prologue, allow_collectives=True)
+    print("captured", flush=True, file=sys.stderr)
+    oks = []
+    for k in range(4):  # every replay: new requests, a whole sorted-exchange Send with RCCL all-to-alls
+        g.replay()
+        torch.cuda.synchronize()
+        print("replay", k, flush=True, file=sys.stderr)
+        oks.append(bool((st == STATUS_OK).all()) and bool(torch.equal(val, req.a0 * req.a1)))
+    w = ex.last_wire
+    print("RESULT " + json.dumps({"ok": oks, "engine": w["engine"], "agreed": bool(w["agreed"]), "S": int(w["S"])}))
+    dist.destroy_process_group()
+""")
+
+
+@pytest.mark.gpu
+def test_sorted_exchange_step_captures_into_a_hipgraph():
+    """the N > 1 Send path (the sorted exchange: packed wire-v3
+    records, RCCL all-to-alls, the lag-2 agreed layout -- no host wait) captured
+    into a hipGraph with real RCCL collectives (world 1, forced on) and replayed
+    on fresh batches: every reply right."""
+    from conftest import free_port
+
+    env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    try:
+        r = subprocess.run([sys.executable, "-X", "faulthandler", "-c", _GRAPH_SCRIPT], env=env, capture_output=True, text=True,
+                           timeout=120)
+    except subprocess.TimeoutExpired as e:
+        raise AssertionError("graph capture / replay hung; stderr: " + str(e.stderr)[-2000:]) from e
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    out = json.loads(line[0][7:])
+    assert all(out["ok"]) and out["engine"] == "sorted" and out["agreed"], out
