@@ -54,9 +54,11 @@ __device__ __forceinline__ unsigned long long* ctr_head(const MboxView& mv, uint
 // the same HBM channels (S = 256: drain 114 us vs 66 us at S = 64, the rings
 // 2 MB apart).  The rotation spreads them over the channels; a slot stays a
 // bijection of (shard, position mod Q).
+__device__ __forceinline__ uint32_t shard_rot(const MboxView& mv, uint32_t s) {
+  return mv.log_q ? (s * 0x9E3779B1u) >> (32 - mv.log_q) : 0u;
+}
 __device__ __forceinline__ uint64_t slot_at(const MboxView& mv, uint32_t s, uint64_t pos) {
-  const uint64_t rot = mv.log_q ? (uint64_t)((s * 0x9E3779B1u) >> (32 - mv.log_q)) : 0ull;
-  return ((uint64_t)s << mv.log_q) | ((pos + rot) & ((1ull << mv.log_q) - 1));
+  return ((uint64_t)s << mv.log_q) | ((pos + shard_rot(mv, s)) & ((1ull << mv.log_q) - 1));
 }
 __device__ __forceinline__ uint32_t* rec_a(const MboxView& mv, uint64_t slot) {
   return mv.rec + slot * (mv.planar ? 4 : 8);

@@ -435,35 +435,26 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   __syncthreads();
   const uint32_t tot = tot_s;
   const uint64_t n = tot < free ? tot : free;
+  const uint64_t sbase = (uint64_t)s << mv.log_q, qmask = Q - 1, rot = shard_rot(mv, s);  // slot_at, hoisted
   unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
-  // window records are loaded one window AHEAD: the next window's loads are in
-  // flight while this one's bins run serially (the block is one per shard, so
-  // nothing else on the CU would hide their latency)
-  SortRec x[kOrdK];
-  uint64_t slot[kOrdK];
-  const auto load_window = [&](uint64_t base) {
-    const uint64_t end = lo + n < base + kOrdWin ? lo + n : base + kOrdWin;
-#pragma unroll
-    for (int k = 0; k < kOrdK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
-      const uint64_t q = base + (uint64_t)w * (kWave * kOrdK) + (uint64_t)k * kWave + lane;
-      slot[k] = slot_at(mv, s, q);
-      if (q < end) {
-        x[k] = load_sorted(mv, slot[k]);
-      } else {
-        x[k].valid = false;
-        x[k].mb = 0;
-      }
-    }
-  };
-  if (n) load_window(lo);
+  // (loading the next window ahead, during this one's serial bins, measured no
+  // faster -- 188 -> 200 us -- and spilled registers to scratch)
   for (uint64_t w0 = lo; w0 < lo + n; w0 += kOrdWin) {
     const uint64_t w1 = lo + n < w0 + kOrdWin ? lo + n : w0 + kOrdWin;
     for (uint32_t b = lane; b < kOrdThreads; b += kWave) L.wcnt[w][b] = 0;
+    SortRec x[kOrdK];
     uint32_t bin[kOrdK], wr[kOrdK];
+    uint64_t slot[kOrdK];
 #pragma unroll
-    for (int k = 0; k < kOrdK; ++k) {
+    for (int k = 0; k < kOrdK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
       const uint64_t q = w0 + (uint64_t)w * (kWave * kOrdK) + (uint64_t)k * kWave + lane;
-      if (q < w1 && !x[k].valid) ++holes;
+      slot[k] = sbase | ((q + rot) & qmask);
+      if (q < w1) {
+        x[k] = load_sorted(mv, slot[k]);
+        if (!x[k].valid) ++holes;
+      } else {
+        x[k].valid = false;
+      }
     }
 #pragma unroll
     for (int k = 0; k < kOrdK; ++k) {
@@ -509,7 +500,6 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
       L.a2[d] = x[k].a2;
     }
     __syncthreads();
-    if (w0 + kOrdWin < lo + n) load_window(w0 + kOrdWin);  // the next window's records, in flight meanwhile
     {  // this thread's bin, serially in ring order
       const unsigned b = threadIdx.x, e = L.bstart[b] + L.bcount[b];
       if (L.bcount[b] > 1) serial += L.bcount[b] - 1;  // records that waited behind their bin's earlier ones
