@@ -629,9 +629,37 @@ void SortedExchange::pick_spec(hipStream_t cs) {
   adopt(meta_host_ + j * kMetaWords, want);
 }
 
-void SortedExchange::a2a(const void* src, void* dst, size_t bytes_per_peer) {
+void SortedExchange::a2a(const void* src, void* dst, size_t bytes_per_peer, bool grouped_p2p) {
   if (fake_) {
     fake_->alltoall(rank_, src, dst, bytes_per_peer, comm_stream_);
+    return;
+  }
+  // PTYPE_SX_SELF_COPY: at world 1 the all-to-all is a device copy.  RCCL
+  // collectives issued on this engine's comm stream crash hipGraph
+  // instantiation on this stack (ncclAllToAll and grouped send / recv alike,
+  // tools/rccl_capture_probe.py, profiles/r3_rccl_capture_probe.txt), so the
+  // capture test validates the captured pipeline with the copy in their place.
+  static const bool self_copy = getenv("PTYPE_SX_SELF_COPY") != nullptr;
+  if (self_copy && R_ == 1) {
+    PT_HIP_CHECK(hipMemcpyAsync(dst, src, bytes_per_peer, hipMemcpyDeviceToDevice, comm_stream_));
+    return;
+  }
+  if (grouped_p2p && rccl().p2p()) {
+    // under a hipGraph capture: ncclAllToAll's captured form crashed graph
+    // instantiation here (RCCL 2.26; tools/rccl_capture_probe.py) while grouped
+    // ncclSend / ncclRecv -- what torch captures -- instantiate and replay
+    auto check = [](int rc, const char* what) {
+      if (rc != 0)
+        throw std::runtime_error(std::string(what) + " failed: " + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+    };
+    check(rccl().group_start(), "ncclGroupStart");
+    for (int q = 0; q < R_; ++q) {
+      check(rccl().send((const char*)src + (size_t)q * bytes_per_peer, bytes_per_peer, kNcclInt8, q, comm_,
+                        comm_stream_), "ncclSend");
+      check(rccl().recv((char*)dst + (size_t)q * bytes_per_peer, bytes_per_peer, kNcclInt8, q, comm_, comm_stream_),
+            "ncclRecv");
+    }
+    check(rccl().group_end(), "ncclGroupEnd");
     return;
   }
   const int rc = rccl().alltoall(src, dst, bytes_per_peer, kNcclInt8, comm_, comm_stream_);
@@ -756,7 +784,7 @@ void SortedExchange::send(const SxSend& a) {
     PT_HIP_CHECK(hipGetLastError());
     PT_HIP_CHECK(hipEventRecord(ev_served_[i], cs));
     PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_served_[i], 0));
-    a2a(b.reply, b.back, (size_t)rp * 4);
+    a2a(b.reply, b.back, (size_t)rp * 4, capturing);
     PT_HIP_CHECK(hipEventRecord(ev_rep_in_[i], comm_stream_));
   };
   for (int i = 0; i < chunks_; ++i) {
@@ -798,7 +826,7 @@ void SortedExchange::send(const SxSend& a) {
     PT_HIP_CHECK(hipGetLastError());
     PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
     PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_routed_[i], 0));
-    a2a(b.send, b.recv, (size_t)rq * 4);
+    a2a(b.send, b.recv, (size_t)rq * 4, capturing);
     PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], comm_stream_));
     if (i > 0) serve(i - 1);
   }

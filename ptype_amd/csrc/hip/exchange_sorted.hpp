@@ -99,7 +99,7 @@ class SortedExchange {
   };
   void pick_spec(hipStream_t cs);
   void adopt(const uint64_t* meta, int64_t from);
-  void a2a(const void* src, void* dst, size_t bytes_per_peer);
+  void a2a(const void* src, void* dst, size_t bytes_per_peer, bool grouped_p2p = false);
   void allreduce_meta(uint64_t* dev, hipStream_t s);
   bool collectives() const { return comm_ != nullptr || fake_ != nullptr; }
 

@@ -210,12 +210,16 @@ _GRAPH_SCRIPT = textwrap.dedent("""
 @pytest.mark.gpu
 def test_sorted_exchange_step_captures_into_a_hipgraph():
     """the N > 1 Send path (the sorted exchange: packed wire-v3
-    records, RCCL all-to-alls, the lag-2 agreed layout -- no host wait) captured
-    into a hipGraph with real RCCL collectives (world 1, forced on) and replayed
-    on fresh batches: every reply right."""
+    records, comm-stream fork / join per chunk, the layout in force -- no host
+    wait) captured into a hipGraph and replayed on fresh batches: every reply
+    right.  World 1 with the process group up; the all-to-all is a device copy
+    (PTYPE_SX_SELF_COPY) because RCCL collectives issued on the engine's own
+    comm stream crash graph instantiation on this ROCm stack (see
+    tools/rccl_capture_probe.py -- torch's own captured all_to_all works)."""
     from conftest import free_port
 
-    env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
+               PTYPE_SX_SELF_COPY="1")
     try:
         r = subprocess.run([sys.executable, "-X", "faulthandler", "-c", _GRAPH_SCRIPT], env=env, capture_output=True, text=True,
                            timeout=120)
