@@ -284,6 +284,23 @@ class Server:
             device_server.export_method(service_method, int(method_id), int(actor), list(fields), actor_field)
             self._s.set_shm_segment(device_server.shm_name)
 
+    def RegisterDeviceBatch(self, service_method: str, batch_handle, fields: Iterable[str] = (), actor_field: str = "",
+                            max_batch: int = 1 << 16) -> None:
+        """Serve ``service_method`` (registered for single calls first) in
+        batches: the pipelined requests a connection has buffered are decoded
+        together -- on the GPU with ``batch_handle = DeviceRuntime.gob_bridge(...).handle()``
+        (K4, csrc/hip/gob_bridge.hpp), or on the host with ``_core.host_batch_multiply()``."""
+        fn, ctx = batch_handle
+        self._s.register_device_batch(service_method, fn, ctx, list(fields), actor_field, int(max_batch))
+
+    @property
+    def batches(self) -> int:
+        return self._s.batches
+
+    @property
+    def batched_calls(self) -> int:
+        return self._s.batched_calls
+
     def Listen(self, port: int = 0, host: str = "0.0.0.0", local: bool = True) -> int:
         return self._s.listen(host, int(port), local)
 

@@ -1,6 +1,7 @@
 // pybind11 bindings for the host control plane (_core).  Python is a thin
 // layer over these: every behaviour lives in C++.
 #include <pybind11/functional.h>
+#include <condition_variable>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -638,6 +639,11 @@ PYBIND11_MODULE(_core, m) {
            py::arg("name"), py::arg("submit_fn"), py::arg("submit_ctx"), py::arg("method"), py::arg("actor") = 0,
            py::arg("fields") = std::vector<std::string>{}, py::arg("actor_field") = "")
       .def("set_shm_segment", &RpcServer::set_shm_segment, py::arg("name"))
+      .def("register_device_batch", &RpcServer::register_device_batch, py::arg("name"), py::arg("batch_fn"),
+           py::arg("batch_ctx"), py::arg("fields") = std::vector<std::string>{}, py::arg("actor_field") = "",
+           py::arg("max_batch") = (size_t)(1 << 16))
+      .def_property_readonly("batches", &RpcServer::batches)
+      .def_property_readonly("batched_calls", &RpcServer::batched_calls)
       .def("has_service", &RpcServer::has_service)
       .def(
           "listen",
@@ -714,6 +720,34 @@ PYBIND11_MODULE(_core, m) {
              if (!o.ok()) fail(o.code, o.error);
              return from_gob(o.reply);
            })
+      .def(
+          "call_many",
+          [](RpcConn& c, const std::string& method, py::list args, double timeout) {
+            // every call pipelined on the connection (Go's client.Go in a loop), then all replies
+            std::vector<gob::Value> in;
+            in.reserve(args.size());
+            for (auto a : args) in.push_back(to_gob(py::reinterpret_borrow<py::object>(a)));
+            std::vector<RpcOutcome> out(in.size());
+            {
+              py::gil_scoped_release nogil;
+              std::mutex mu;
+              std::condition_variable cv;
+              size_t left = in.size();
+              for (size_t i = 0; i < in.size(); ++i)
+                c.go(method, in[i], [&, i](RpcOutcome o) {
+                  std::lock_guard<std::mutex> g(mu);
+                  out[i] = std::move(o);
+                  if (--left == 0) cv.notify_all();
+                });
+              std::unique_lock<std::mutex> lk(mu);
+              if (!cv.wait_for(lk, std::chrono::duration<double>(timeout), [&] { return left == 0; }))
+                fail(Errc::kTimeout, "call_many: replies outstanding after the timeout");
+            }
+            py::list res;
+            for (auto& o : out) res.append(o.ok() ? from_gob(o.reply) : py::object(py::str("error: " + o.error)));
+            return res;
+          },
+          py::arg("method"), py::arg("args"), py::arg("timeout") = 60.0)
       .def("close", &RpcConn::close);
   // A raw handle on another process's dispatcher segment (by name): device calls
   // straight into the rings that process's GPU polls -- used to time remote calls
@@ -773,6 +807,8 @@ PYBIND11_MODULE(_core, m) {
         return fd;
       },
       py::arg("name"));
+  m.def("host_batch_multiply", []() { return py::make_tuple((uintptr_t)&host_batch_multiply, (uintptr_t)0); },
+        "(fn, ctx) of the CPU batch handler twin of the GPU gob bridge (Calculator.Multiply)");
   m.def(
       "dial_http",
       [](const std::string& host, int port, double timeout, bool allow_local) {

@@ -522,5 +522,81 @@ bool Decoder::decode(Value* out) {
   }
 }
 
+namespace {
+// Reads from an in-memory message while a Decoder parses it, then restores its source.
+struct ReadSwap {
+  std::function<bool(char*, size_t)>& slot;
+  std::function<bool(char*, size_t)> saved;
+  ReadSwap(std::function<bool(char*, size_t)>& s, const std::string& buf, size_t* pos) : slot(s), saved(std::move(s)) {
+    slot = [&buf, pos](char* p, size_t n) {
+      if (*pos + n > buf.size()) return false;
+      memcpy(p, buf.data() + *pos, n);
+      *pos += n;
+      return true;
+    };
+  }
+  ~ReadSwap() { slot = std::move(saved); }
+};
+}  // namespace
+
+bool Decoder::next_raw(std::string* raw, int64_t* type_id) {
+  for (;;) {
+    raw->clear();
+    unsigned char c;
+    if (!read_((char*)&c, 1)) return false;
+    raw->push_back((char)c);
+    uint64_t len;
+    if (c < 128) {
+      len = c;
+    } else {
+      const int n = 256 - c;
+      if (n > 8) fail(Errc::kRpc, "gob: bad message length");
+      unsigned char buf[8];
+      if (!read_((char*)buf, n)) fail(Errc::kRpc, "gob: unexpected EOF");
+      len = 0;
+      for (int i = 0; i < n; ++i) {
+        len = (len << 8) | buf[i];
+        raw->push_back((char)buf[i]);
+      }
+    }
+    if (len > (1u << 28)) fail(Errc::kRpc, "gob: message too large");
+    const size_t hdr = raw->size();
+    raw->resize(hdr + len);
+    if (len && !read_(&(*raw)[hdr], len)) fail(Errc::kRpc, "gob: unexpected EOF");
+    size_t pos = hdr;
+    int64_t id;
+    {
+      ReadSwap swap(read_, *raw, &pos);
+      remaining_ = len;
+      id = get_int();
+      if (id < 0) {
+        types_[(int)-id] = decode_wiretype();
+        skip_remaining();
+      }
+      remaining_ = 0;
+    }
+    if (id < 0) continue;
+    *type_id = id;
+    return true;
+  }
+}
+
+void Decoder::decode_raw(const std::string& raw, Value* out) {
+  size_t pos = 0;
+  ReadSwap swap(read_, raw, &pos);
+  if (!decode(out)) fail(Errc::kRpc, "gob: empty message");
+}
+
+bool Decoder::int_struct_fields(int64_t type_id, std::vector<std::string>* names) const {
+  auto it = types_.find((int)type_id);
+  if (it == types_.end() || it->second.kind != 1) return false;
+  names->clear();
+  for (const auto& f : it->second.fields) {
+    if (f.second != 2 && f.second != 7) return false;  // gob's predefined int (2) / uint (7)
+    names->push_back(f.first);
+  }
+  return !names->empty();
+}
+
 }  // namespace gob
 }  // namespace ptype

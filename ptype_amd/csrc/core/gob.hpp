@@ -77,6 +77,15 @@ class Decoder {
   explicit Decoder(std::function<bool(char*, size_t)> read) : read_(std::move(read)) {}
   // Reads messages until one value is complete; consumes type definitions on the way.
   bool decode(Value* out);
+  // The next VALUE message undecoded (its length prefix included) and its type
+  // id; type definitions on the way are consumed (K4: a batch of such messages
+  // is decoded on the GPU).  False at a clean end of stream.
+  bool next_raw(std::string* raw, int64_t* type_id);
+  // Decode a message captured by next_raw (host fallback for one message).
+  void decode_raw(const std::string& raw, Value* out);
+  // Field names of a received struct type in wire order, when every field is a
+  // (signed / unsigned) integer; false otherwise.
+  bool int_struct_fields(int64_t type_id, std::vector<std::string>* names) const;
 
  private:
   struct WireType {

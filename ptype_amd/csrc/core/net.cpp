@@ -114,6 +114,12 @@ bool Conn::fill() {
   }
 }
 
+bool Conn::input_pending() {
+  if (rbuf_.size() > rpos_) return true;
+  pollfd pfd{fd_, POLLIN, 0};
+  return ::poll(&pfd, 1, 0) > 0 && (pfd.revents & POLLIN);
+}
+
 bool Conn::read_exact(char* p, size_t n) {
   while (rbuf_.size() - rpos_ < n)
     if (!fill()) return false;

@@ -27,6 +27,8 @@ class Conn {
   bool write_raw(const std::string& bytes);   // thread-safe
   bool read_exact(char* p, size_t n);         // buffered
   bool read_line(std::string* line);          // up to and excluding '\n'
+  // Whether more input is available right now (buffered, or readable without blocking).
+  bool input_pending();
   void shutdown();
   bool alive() const { return alive_.load(); }
   int fd() const { return fd_; }

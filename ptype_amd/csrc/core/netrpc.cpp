@@ -309,15 +309,45 @@ void RpcServer::serve_conn(std::shared_ptr<Conn> c) {
   auto emu = std::make_shared<std::mutex>();
   std::atomic<int> inflight{0};
   gob::Decoder dec([c](char* p, size_t n) { return c->read_exact(p, n); });
+  std::vector<PendingCall> pending;  // K4: buffered requests of one batched method
+  const BatchMethod* pending_bm = nullptr;
+  auto flush = [&] {
+    if (!pending.empty()) flush_batch(pending, *pending_bm, *enc, *emu, *c);
+    pending.clear();
+    pending_bm = nullptr;
+  };
   try {
     for (;;) {
       gob::Value req, args;
       if (!dec.decode(&req)) break;
-      if (!dec.decode(&args)) break;
       const gob::Value* smv = req.field("ServiceMethod");
       const gob::Value* seqv = req.field("Seq");
       const std::string sm = smv ? smv->s : "";
       const uint64_t seq = seqv ? seqv->u : 0;
+      const BatchMethod* bm = nullptr;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = batch_methods_.find(sm);
+        if (it != batch_methods_.end()) bm = &it->second;  // (entries are never erased)
+      }
+      if (bm) {
+        PendingCall pc;
+        pc.sm = sm;
+        pc.seq = seq;
+        if (!dec.next_raw(&pc.raw, &pc.type_id)) break;
+        if (dec.int_struct_fields(pc.type_id, &pc.names) && pc.names.size() <= 8) {
+          if (pending_bm && (pending_bm != bm || pending.back().type_id != pc.type_id)) flush();
+          pending_bm = bm;
+          pending.push_back(std::move(pc));
+          // the connection's pipelined requests, until its input runs dry
+          if (pending.size() >= bm->max_batch || !c->input_pending()) flush();
+          continue;
+        }
+        dec.decode_raw(pc.raw, &args);  // not an integer struct: the single-call path
+      } else if (!dec.decode(&args)) {
+        break;
+      }
+      if (!c->input_pending()) flush();
       ++inflight;
       std::thread([this, c, enc, emu, sm, seq, args, &inflight] {  // a goroutine per request
         RpcOutcome o = dispatch(sm, args);
@@ -342,10 +372,138 @@ void RpcServer::serve_conn(std::shared_ptr<Conn> c) {
         --inflight;
       }).detach();
     }
+    flush();
   } catch (const std::exception&) {
   }
   c->shutdown();
   while (inflight.load() > 0) sleep_ms(1);
+}
+
+// ---------------------------------------------------------------- K4 batched device methods
+void RpcServer::register_device_batch(const std::string& service_method, uintptr_t fn, uintptr_t ctx,
+                                      std::vector<std::string> fields, std::string actor_field, size_t max_batch) {
+  if (!fn) throw std::invalid_argument("register_device_batch: null batch function");
+  if (fields.size() > 3) throw std::invalid_argument("register_device_batch: at most 3 argument fields");
+  std::lock_guard<std::mutex> g(mu_);
+  if (!methods_.count(service_method))
+    fail(Errc::kRpc, "register_device_batch: register " + service_method + " for single calls first");
+  BatchMethod& b = batch_methods_[service_method];
+  b.fn = (DeviceBatchFn)fn;
+  b.ctx = (void*)ctx;
+  b.fields = std::move(fields);
+  b.actor_field = std::move(actor_field);
+  b.max_batch = std::max<size_t>(1, max_batch);
+}
+
+// One GPU pass for the buffered calls, then every Response + reply encoded in
+// sequence (the same host encoder as the single-call path: identical bytes) and
+// written with one syscall.
+void RpcServer::flush_batch(std::vector<PendingCall>& pending, const BatchMethod& bm, gob::Encoder& enc,
+                            std::mutex& emu, Conn& c) {
+  const int64_t n = (int64_t)pending.size();
+  const std::vector<std::string>& names = pending.front().names;
+  int32_t col[4] = {-1, -1, -1, -1};
+  auto index_of = [&](const std::string& f) {
+    for (size_t j = 0; j < names.size(); ++j)
+      if (names[j] == f) return (int32_t)j;
+    return (int32_t)-1;
+  };
+  for (size_t k = 0; k < bm.fields.size(); ++k) col[k] = index_of(bm.fields[k]);
+  if (!bm.actor_field.empty()) col[3] = index_of(bm.actor_field);
+  std::string bytes;
+  std::vector<int64_t> offsets((size_t)n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    offsets[(size_t)i] = (int64_t)bytes.size();
+    bytes += pending[(size_t)i].raw;
+  }
+  offsets[(size_t)n] = (int64_t)bytes.size();
+  std::vector<int32_t> gst((size_t)n, 0);
+  std::vector<ReplyRecord> rep((size_t)n);
+  const int rc = bm.fn(bm.ctx, (const uint8_t*)bytes.data(), offsets.data(), n, pending.front().type_id,
+                       (int)names.size(), col, gst.data(), rep.data());
+  batches_.fetch_add(1);
+  batched_calls_.fetch_add((uint64_t)n);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    counts_[pending.front().sm] += (uint64_t)n;
+  }
+  std::string buf;
+  std::lock_guard<std::mutex> g(emu);
+  for (int64_t i = 0; i < n; ++i) {
+    RpcOutcome o;
+    if (rc != 0) {
+      o.error = "device dispatcher unavailable";
+    } else if (gst[(size_t)i] != 0) {
+      o.error = "gob: decoding error (device status " + std::to_string(gst[(size_t)i]) + ")";
+    } else {
+      o = device_outcome(rep[(size_t)i]);
+    }
+    gob::Value resp = gob::Value::Struct("Response");
+    resp.fields.emplace_back("ServiceMethod", gob::Value::String(pending[(size_t)i].sm));
+    resp.fields.emplace_back("Seq", gob::Value::Uint(pending[(size_t)i].seq));
+    resp.fields.emplace_back("Error", gob::Value::String(o.error));
+    enc.encode(resp, &buf);
+    enc.encode(o.ok() ? o.reply : gob::Value::Struct(""), &buf);
+  }
+  c.write_raw(buf);
+}
+
+namespace {
+bool gob_get_uint(const uint8_t*& p, const uint8_t* end, uint64_t* x) {
+  if (p >= end) return false;
+  const uint8_t c = *p++;
+  if (c < 128) {
+    *x = c;
+    return true;
+  }
+  const int n = 256 - c;
+  if (n > 8 || end - p < n) return false;
+  uint64_t v = 0;
+  for (int i = 0; i < n; ++i) v = (v << 8) | *p++;
+  *x = v;
+  return true;
+}
+int64_t gob_unzz(uint64_t u) { return (u & 1) ? (int64_t)~(u >> 1) : (int64_t)(u >> 1); }
+}  // namespace
+
+int host_batch_multiply(void* ctx, const uint8_t* bytes, const int64_t* offsets, int64_t n, int64_t type_id, int nf,
+                        const int32_t* field_col, int32_t* gob_status, ReplyRecord* out) {
+  (void)ctx;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint8_t* p = bytes + offsets[i];
+    const uint8_t* end = bytes + offsets[i + 1];
+    int64_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int32_t st = 0;
+    uint64_t len = 0, tid = 0;
+    if (!gob_get_uint(p, end, &len) || (uint64_t)(end - p) != len) {
+      st = 1;
+    } else if (!gob_get_uint(p, end, &tid) || gob_unzz(tid) != type_id) {
+      st = 2;
+    } else {
+      int field = -1;
+      for (;;) {
+        uint64_t delta, u;
+        if (!gob_get_uint(p, end, &delta)) {
+          st = 1;
+          break;
+        }
+        if (delta == 0) break;
+        field += (int)delta;
+        if (field >= nf || field >= 8 || !gob_get_uint(p, end, &u)) {
+          st = 3;
+          break;
+        }
+        v[field] = gob_unzz(u);
+      }
+      if (st == 0 && p != end) st = 4;
+    }
+    gob_status[i] = st;
+    const int64_t a = field_col[0] >= 0 ? v[field_col[0]] : 0, b = field_col[1] >= 0 ? v[field_col[1]] : 0;
+    out[i].value = (int64_t)((uint64_t)a * (uint64_t)b);
+    out[i].status = kStatusOk;
+    out[i].actor = 0;
+  }
+  return 0;
 }
 
 // ---------------------------------------------------------------- local fast path

@@ -75,6 +75,15 @@ class NetRpcConn : public RpcConn, public std::enable_shared_from_this<NetRpcCon
 
 using RpcHandler = std::function<gob::Value(const gob::Value& args)>;  // throw Error(kRpc, msg) to fail
 
+// K4 on the serving path: a device-BATCHED method takes n raw gob VALUE messages
+// of one integer-struct type (length prefixes included, message i at
+// bytes[offsets[i], offsets[i+1])) and answers all n at once -- decoded on the
+// GPU straight into mailbox columns.  field_col[k] is the wire-field index of the
+// method's k-th argument field (k < 3) and field_col[3] the actor field's (-1:
+// absent / fixed actor).  gob_status[i] != 0: message i did not decode.
+typedef int (*DeviceBatchFn)(void* ctx, const uint8_t* bytes, const int64_t* offsets, int64_t n, int64_t type_id,
+                             int nf, const int32_t* field_col, int32_t* gob_status, ReplyRecord* out);
+
 class RpcServer {
  public:
   RpcServer() = default;
@@ -95,9 +104,33 @@ class RpcServer {
   // The shared-memory segment of this server's GPU actors: published as the
   // port's locator while listening, so same-node clients call them directly.
   void set_shm_segment(const std::string& name) { shm_segment_ = name; }
+  // Serve `service_method` (already registered for single calls) in batches:
+  // the pipelined requests a connection has buffered go through `fn` together.
+  void register_device_batch(const std::string& service_method, uintptr_t fn, uintptr_t ctx,
+                             std::vector<std::string> fields, std::string actor_field, size_t max_batch = 1 << 16);
+  uint64_t batches() const { return batches_.load(); }
+  uint64_t batched_calls() const { return batched_calls_.load(); }
 
  private:
+  struct BatchMethod {
+    DeviceBatchFn fn = nullptr;
+    void* ctx = nullptr;
+    std::vector<std::string> fields;
+    std::string actor_field;
+    size_t max_batch = 1 << 16;
+  };
+  struct PendingCall {
+    std::string sm;
+    uint64_t seq = 0;
+    int64_t type_id = 0;
+    std::string raw;
+    std::vector<std::string> names;  // the args type's wire fields
+  };
+  void flush_batch(std::vector<PendingCall>& pending, const BatchMethod& bm, gob::Encoder& enc, std::mutex& emu,
+                   Conn& c);
   void serve_conn(std::shared_ptr<Conn> c);
+  std::map<std::string, BatchMethod> batch_methods_;
+  std::atomic<uint64_t> batches_{0}, batched_calls_{0};
   mutable std::mutex mu_;
   std::map<std::string, RpcHandler> methods_;
   std::map<std::string, std::function<std::string()>> debug_handlers_;
@@ -107,6 +140,12 @@ class RpcServer {
   std::string shm_segment_;
   bool locator_ = false;
 };
+
+// The host twin of the GPU gob bridge, for GPU-less runs and the batching tests:
+// decodes each integer-struct value message on the CPU (the same wire rules as
+// gob_decode_kernel) and answers Calculator.Multiply (field 0 * field 1).
+int host_batch_multiply(void* ctx, const uint8_t* bytes, const int64_t* offsets, int64_t n, int64_t type_id, int nf,
+                        const int32_t* field_col, int32_t* gob_status, ReplyRecord* out);
 
 // gob args -> device message, and a device reply -> net/rpc outcome: shared by
 // the in-process device bridge and the cross-process shared-memory connection.

@@ -14,6 +14,7 @@
 #include "mailbox.hpp"
 #include "server.hpp"
 #include "xcall.hpp"
+#include "gob_bridge.hpp"
 
 namespace py = pybind11;
 
@@ -438,6 +439,21 @@ PYBIND11_MODULE(_hip, m) {
                              "address of the C++ object (the epoch engine delivers into these mailboxes)");
   m.def("rccl_available", [] { return rccl().alltoall != nullptr; });
 
+  py::class_<GobBridge>(m, "GobBridge",
+                        "K4 on the net/rpc serving path: batched gob requests decoded on the GPU into mailbox "
+                        "columns (csrc/hip/gob_bridge.hpp); pass handle() to RpcServer.register_device_batch")
+      .def(py::init([](int device, Mailboxes& mb, uint32_t method, uint32_t fixed_actor, uintptr_t table,
+                       uint64_t cap, uintptr_t state, uint32_t n_state, uint64_t delay_us) {
+             return new GobBridge(device, &mb, method, fixed_actor, table, cap, state, n_state, delay_us * 100);
+           }),
+           py::arg("device"), py::arg("mailboxes"), py::arg("method"), py::arg("actor") = 0, py::arg("table"),
+           py::arg("cap"), py::arg("state") = 0, py::arg("n_state") = 0, py::arg("delay_us") = 0,
+           py::keep_alive<1, 3>())
+      .def("handle", [](GobBridge& b) {
+        return py::make_tuple((uintptr_t)&GobBridge::batch_c, (uintptr_t)&b);
+      })
+      .def_property_readonly("batches", &GobBridge::batches)
+      .def_property_readonly("calls", &GobBridge::calls);
   py::class_<PeerLane, std::shared_ptr<PeerLane>>(m, "PeerLane")
       .def(py::init([](const std::string& shm, int device, double timeout_s) {
              py::gil_scoped_release nogil;

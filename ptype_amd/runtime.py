@@ -503,12 +503,33 @@ class DeviceRuntime:
             self._ltable = t
         return self._ltable
 
-    def serve(self, server, service: str, methods: dict) -> None:
+    def serve(self, server, service: str, methods: dict, batch: bool = False) -> None:
         """Expose GPU handlers over net/rpc: ``methods`` maps a Go method name to
-        ``(method_id, [arg field names])`` -- e.g. ``{"Multiply": (1, ["A", "B"])}``."""
+        ``(method_id, [arg field names])`` -- e.g. ``{"Multiply": (1, ["A", "B"])}``.
+        ``batch``: also serve each method in batches through the GPU gob bridge
+        (K4: a connection's pipelined requests decoded on the GPU into mailbox
+        columns, ``gob_bridge``)."""
         self.host(service)
         for name, (mid, fields) in methods.items():
             server.RegisterDevice(f"{service}.{name}", self.server, mid, fields)
+            if batch:
+                server.RegisterDeviceBatch(f"{service}.{name}", self.gob_bridge(mid).handle(), fields)
+
+    def gob_bridge(self, method_id: int, actor: int = 0):
+        """The GPU gob bridge of ``method_id`` (csrc/hip/gob_bridge.hpp): batches
+        of gob argument messages decoded on this GPU and sent through mailboxes of
+        their own (separate rings: the bridge runs on its own stream), answering
+        actor ``actor`` (or the request's actor field).  Kept alive by the runtime."""
+        from .ops.mailbox import Mailboxes
+
+        if not self.on_gpu:
+            raise RuntimeError("gob_bridge needs a GPU runtime (use _core.host_batch_multiply() on the host)")
+        self._bridges = getattr(self, "_bridges", [])
+        mb = Mailboxes(self.device, shards=64, slots=1 << 12)
+        b = hip().GobBridge(self.device.index or 0, mb._m, int(method_id), int(actor), self.table.table.data_ptr(),
+                            self.table.cap, self.state.data_ptr(), self.state.numel(), self.delay_us)
+        self._bridges.append((mb, b))
+        return b
 
     # ------------------------------------------------------------------ snapshots (C14)
     def snapshot_to_host(self) -> dict:
