@@ -148,7 +148,8 @@ struct alignas(64) ServerCtrl {
   uint64_t trace_ring;   // device address of the TraceRec ring
   uint64_t calib_req;    // host sets 1; the kernel answers with calib_ticks and clears it
   uint64_t calib_ticks;
-  uint64_t pad[6];
+  uint64_t xl_n;         // GPU peer lanes to poll (0 while none is registered: no cost on the ring's path)
+  uint64_t pad[5];
 };
 static_assert(sizeof(ServerCtrl) == 128, "ServerCtrl layout");
 

@@ -176,6 +176,8 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
   uint64_t trace_mask = sys_ld(&ctrl->trace_mask);
   TraceRec* trace = reinterpret_cast<TraceRec*>(sys_ld(&ctrl->trace_ring));
   unsigned idle_polls = 0, iters = 0;
+  // GPU peer lanes are polled only while some are registered (re-read on the idle path)
+  uint32_t nxl = xl ? (uint32_t)min<uint64_t>(sys_ld(&ctrl->xl_n), (uint64_t)nx) : 0u;
   for (;;) {
     // every poll is a PCIe round trip to host memory: the stop flag is read on
     // one poll in 16, not before every ring poll (that made a poll two trips)
@@ -193,8 +195,8 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
     const bool ready = tag == seq + 1 && (!spec || cs == ring_csum(seq, w0, w1, w2, w3));
     const uint64_t m = __ballot(ready);
     const unsigned n = (m == ~0ull) ? 64u : (unsigned)__builtin_ctzll(~m);
-    if (nx) {  // GPU peer lanes: local HBM loads, no PCIe trip
-      const unsigned nxs = serve_xlanes(xl, nx, state, n_state, delay_ticks);
+    if (nxl) {  // GPU peer lanes: local HBM loads, no PCIe trip
+      const unsigned nxs = serve_xlanes(xl, nxl, state, n_state, delay_ticks);
       if (nxs) {
         processed += nxs;
         last_work = realtime_ticks();
@@ -206,6 +208,7 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
         if ((idle_polls & 63) == 0) {
           trace_mask = sys_ld(&ctrl->trace_mask);
           trace = reinterpret_cast<TraceRec*>(sys_ld(&ctrl->trace_ring));
+          if (xl) nxl = (uint32_t)min<uint64_t>(sys_ld(&ctrl->xl_n), (uint64_t)nx);
         }
         if (lane == 0 && sys_ld(&ctrl->calib_req)) {  // clock calibration handshake
           sys_st(&ctrl->calib_ticks, realtime_ticks());
@@ -224,7 +227,8 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
           sys_st(&ctrl->state, kStopped);
           __threadfence_system();
           bool pending = sys_ld(&req[head & ring_mask].tag) == head + 1;
-          for (uint32_t k = 0; k < nx && !pending; ++k) {
+          const uint32_t nxp = xl ? (uint32_t)min<uint64_t>(sys_ld(&ctrl->xl_n), (uint64_t)nx) : 0u;
+          for (uint32_t k = 0; k < nxp && !pending; ++k) {
             const uint64_t t = sys_ld(&xl[k].req_tag);
             pending = t != 0 && t == sys_ld(&xl[k].served) + 1;
           }
@@ -709,6 +713,10 @@ class DeviceServer {
       g.state.store(kXLaneReady, std::memory_order_release);
     }
     xl_live_ = live;
+    uint64_t top = 0;  // lanes the wave polls: up to the highest registered one
+    for (int i = 0; i < kXLanes; ++i)
+      if (xl_imports_[i]) top = (uint64_t)i + 1;
+    __atomic_store_n(&ctrl_->xl_n, top, __ATOMIC_SEQ_CST);
   }
 
   // Reset lane i (through the BAR mapping): sequence restarts at 0.
