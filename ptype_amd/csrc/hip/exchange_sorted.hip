@@ -62,9 +62,15 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 }
 
 // ---------------------------------------------------------------- sender: count
+// Registry modes 0/1 (hash probe / directory gather) also leave each message's
+// resolved route word ((mailbox << 8) | rank, kDirMissing when unroutable) in
+// rw[] -- the chunk's perm column, overwritten by the scatter -- so the scatter
+// reads it coalesced instead of repeating the random gather (affine mode 2
+// computes its routes and passes rw = null).
 template <int MODE>
 __global__ __launch_bounds__(kST) void sx_count_kernel(SortIn in, int R, uint32_t K, uint32_t* __restrict__ hist,
-                                                       unsigned long long* __restrict__ meta) {
+                                                       unsigned long long* __restrict__ meta,
+                                                       uint32_t* __restrict__ rw) {
   __shared__ uint32_t cnt[kXMaxBuckets];
   __shared__ uint32_t mbmax_s;
   const uint32_t B = (uint32_t)R * K;
@@ -82,11 +88,17 @@ __global__ __launch_bounds__(kST) void sx_count_kernel(SortIn in, int R, uint32_
     resolve_k<MODE>(in, a, r, mb);
     if (t + 1 < t1) load_actors(in, t + 1, a);
 #pragma unroll
-    for (int k = 0; k < kSK; ++k)
-      if (r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox) {
+    for (int k = 0; k < kSK; ++k) {
+      const bool ok = r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
+      if constexpr (MODE != 2) {
+        const int64_t i = tile_index(t, k);
+        if (i < in.M) rw[i] = ok ? (mb[k] << 8) | (uint32_t)r[k] : kDirMissing;
+      }
+      if (ok) {
         atomicAdd(&cnt[(uint32_t)r[k] * K + (mb[k] & (K - 1))], 1u);
         mbmax = mb[k] > mbmax ? mb[k] : mbmax;
       }
+    }
   }
   mbmax = wave_max(mbmax);
   if (lane_id() == 0 && mbmax) atomicMax(&mbmax_s, mbmax);
@@ -196,26 +208,41 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
   for (uint32_t t = t0; t < t1; ++t) {
     for (uint32_t b = lane; b < B; b += kWave) wcnt[w][b] = 0;
     // phase 1: routes and ranks only (a small register file: occupancy hides the loads)
-    uint32_t a[kSK];
-    load_actors(in, t, a);
     int r[kSK];
     uint32_t mb[kSK];
-    resolve_k<MODE>(in, a, r, mb);
-    uint32_t wr[kSK], bk[kSK];
+    if constexpr (MODE == 2) {
+      uint32_t a[kSK];
+      load_actors(in, t, a);
+      resolve_k<MODE>(in, a, r, mb);
+    } else {  // the count pass's route words (see sx_count_kernel)
+      uint32_t rw[kSK];
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {
+        const int64_t i = tile_index(t, k);
+        rw[k] = i < in.M ? (uint32_t)perm[i] : kDirMissing;
+      }
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {
+        r[k] = rw[k] == kDirMissing ? -1 : (int)(rw[k] & 0xffu);
+        mb[k] = rw[k] >> 8;
+      }
+    }
+    // one register per item into phase 2: (rank within the wave's run << 8) | rank
+    // (0xff: no such actor) -- the bucket is recomputed from (rank, mailbox)
+    uint32_t pr[kSK];
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       const bool ok = r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
-      if (!ok) r[k] = -1;
-      bk[k] = ok ? (uint32_t)r[k] * K + (mb[k] & (K - 1)) : 0u;
-      const uint64_t peers = match_bits(bk[k], bbits, __ballot(ok));
+      const uint32_t bk = ok ? (uint32_t)r[k] * K + (mb[k] & (K - 1)) : 0u;
+      const uint64_t peers = match_bits(bk, bbits, __ballot(ok));
       const unsigned below = mbcnt64(peers);
       const int leader = peers ? __builtin_ctzll(peers) : 0;
       unsigned old = 0;
       if (ok && below == 0) {
-        old = wcnt[w][bk[k]];
-        wcnt[w][bk[k]] = old + (unsigned)__popcll(peers);
+        old = wcnt[w][bk];
+        wcnt[w][bk] = old + (unsigned)__popcll(peers);
       }
-      wr[k] = (unsigned)__shfl((int)old, leader) + below;
+      pr[k] = ok ? (((unsigned)__shfl((int)old, leader) + below) << 8) | (uint32_t)r[k] : 0xffu;
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < B; b += kST) {
@@ -234,11 +261,13 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
     for (int k = 0; k < kSK; ++k) {
       const int64_t i = tile_index(t, k);
       if (i >= in.M) continue;
-      if (r[k] < 0) {
+      const uint32_t rk = pr[k] & 0xffu;
+      if (rk == 0xffu) {
         perm[i] = -2;  // no such actor: the completion answers kStatusNoActor
         continue;
       }
-      const uint32_t pos = bo[bk[k]] + wcnt[w][bk[k]] + wr[k];
+      const uint32_t bk = rk * K + (mb[k] & (K - 1));
+      const uint32_t pos = bo[bk] + wcnt[w][bk] + (pr[k] >> 8);
       if (pos >= C) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
         perm[i] = -1;
         continue;
@@ -247,24 +276,26 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
       const int64_t x1 = in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
       const int64_t x2 = in.a2 ? __builtin_nontemporal_load(in.a2 + i) : 0;
       const uint32_t meth = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
-      const uint64_t z0 = zz_enc(x0), z1 = zz_enc(x1), z2 = zz_enc(x2);
+      const uint64_t z0 = zz_enc(x0), z1 = zz_enc(x1), z2 = in.a2 ? zz_enc(x2) : 0ull;
       acc.z0 = z0 > acc.z0 ? z0 : acc.z0;
       acc.z1 = z1 > acc.z1 ? z1 : acc.z1;
-      acc.z2 = z2 > acc.z2 ? z2 : acc.z2;
-      acc.mm = meth > acc.mm ? meth : acc.mm;
-      acc.flags |= 1u << (meth < 7 ? meth : 7);
+      if (in.a2) acc.z2 = z2 > acc.z2 ? z2 : acc.z2;
+      if (in.mcol) {  // a uniform method is flagged once per batch (meta_publish)
+        acc.mm = meth > acc.mm ? meth : acc.mm;
+        acc.flags |= 1u << (meth < 7 ? meth : 7);
+      }
       uint64_t f[5];
       const bool fit = sx_fits(L, meth, in.method_uniform, mb[k], z0, z1, z2);
       if (fit) {
         f[0] = meth, f[1] = mb[k], f[2] = z0, f[3] = z1, f[4] = z2;
-        perm[i] = (int32_t)((uint32_t)r[k] * C + pos);
+        perm[i] = (int32_t)(rk * C + pos);
       } else {  // wider than the layout in force: a null record holds the slot
         f[0] = 0, f[1] = low_mask(L.w[1]), f[2] = 0, f[3] = 0, f[4] = 0;
         perm[i] = -1;
       }
       uint32_t rec[S];
       packed_pack<S>(L, f, rec);
-      store_words<S>(sendbuf + (int64_t)r[k] * req_stride + 4 + (int64_t)pos * S, rec);
+      store_words<S>(sendbuf + (int64_t)rk * req_stride + 4 + (int64_t)pos * S, rec);
     }
     __syncthreads();
   }
@@ -729,6 +760,8 @@ void SortedExchange::send(const SxSend& a) {
     in.aw = a.affine_w;
     in.aw_shift = (a.affine_w && (a.affine_w & (a.affine_w - 1)) == 0) ? __builtin_ctz(a.affine_w) : -1;
     in.rank_self = rank_;
+    static const bool dir_nt = getenv("PTYPE_DIR_NT") && atoi(getenv("PTYPE_DIR_NT")) != 0;
+    in.dir_nt = dir_nt;
     const int64_t tiles = (m + kSTile - 1) / kSTile;
     int64_t G = std::min<int64_t>({std::max<int64_t>(tiles, 1), (int64_t)(kMboxSortHistWords / B), 1024});
     if (G >= 8) G -= G % 8;
@@ -797,7 +830,8 @@ void SortedExchange::send(const SxSend& a) {
     else if (mode == 1) hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__); \
     else hipLaunchKernelGGL((KERNEL<0>), __VA_ARGS__);               \
   } while (0)
-    PT_SX_MODE(sx_count_kernel, dim3(in.G), dim3(kST), 0, cs, in, R_, K, hist_, (unsigned long long*)meta);
+    PT_SX_MODE(sx_count_kernel, dim3(in.G), dim3(kST), 0, cs, in, R_, K, hist_, (unsigned long long*)meta,
+               mode == 2 ? nullptr : (uint32_t*)b.perm);
     hipLaunchKernelGGL(sx_scan_kernel, dim3(R_), dim3(1024), 0, cs, hist_, in.G, R_, K, b.send, rq, tab_off,
                        (uint32_t)C, (uint32_t)a.method_uniform,
                        (uint32_t)(kFlagValid | (sharded ? kFlagSharded : 0)), rank_, (unsigned long long*)meta, boff_);

@@ -205,8 +205,9 @@ class Mailboxes {
   uint32_t* sort_rw_ = nullptr;     // [M] each message's mailbox (route word), count -> scatter
   uint32_t* sort_sidx_ = nullptr;   // [M] each message's ring slot, scatter -> drain / completion
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
-  int64_t* stage_val_ = nullptr;    // ordered drain: replies staged at ring slots [S * Q]
-  int32_t* stage_st_ = nullptr;
+  // ordered drain: replies staged at ring slots [S * Q], one 16-B word each
+  // (value lo, value hi, status, 0) -- one gather per message in the completion
+  void* stage_rep_ = nullptr;
 };
 
 }  // namespace ptype

@@ -472,8 +472,7 @@ struct OrdLds {
 __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView mv, uint32_t* __restrict__ gsum,
                                                                         uint32_t ngroups, int64_t* __restrict__ state,
                                                                         uint32_t n_state, uint64_t delay_ticks,
-                                                                        OutboxView ob, int64_t* __restrict__ sval,
-                                                                        int32_t* __restrict__ sst) {
+                                                                        OutboxView ob, u32x4* __restrict__ srep) {
   extern __shared__ __align__(16) unsigned char smem_ord[];
   OrdLds& L = *reinterpret_cast<OrdLds*>(smem_ord);
   int64_t* st_lds = reinterpret_cast<int64_t*>(smem_ord + sizeof(OrdLds));
@@ -571,8 +570,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
         m.a0 = L.a0[d], m.a1 = L.a1[d], m.a2 = L.a2[d];
         const ReplyRecord rr = run_handler(m, st, nst, delay_ticks, ob, true);
         failed += rr.status != kStatusOk;
-        sval[L.slot[d]] = rr.value;
-        sst[L.slot[d]] = rr.status;
+        srep[L.slot[d]] = u32x4{(uint32_t)rr.value, (uint32_t)((uint64_t)rr.value >> 32), (uint32_t)rr.status, 0u};
         ++done;
         if (!in_lds) vm_drain();  // global state: this store lands before the bin's next load
       }
@@ -592,8 +590,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
 // records scatter block b wrote, so its reads hit ~S short runs of contiguous
 // slots (lines shared by the block's waves) instead of one line per message.
 __global__ __launch_bounds__(kST) void mbx_complete_kernel(SortIn in, const uint32_t* __restrict__ sidx,
-                                                           const int64_t* __restrict__ sval,
-                                                           const int32_t* __restrict__ sst, ReplyView rv) {
+                                                           const u32x4* __restrict__ srep, ReplyView rv) {
   const uint32_t v = virt_block(blockIdx.x, in.G);
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
   for (uint32_t t = t0; t < t1; ++t) {
@@ -603,14 +600,15 @@ __global__ __launch_bounds__(kST) void mbx_complete_kernel(SortIn in, const uint
       const int64_t i = tile_index(t, k);
       sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
     }
-    int64_t val[kSK];
-    int32_t st[kSK];
+    u32x4 r[kSK];
 #pragma unroll
     for (int k = 0; k < kSK; ++k)
-      if (sl[k] < kSpillSlot) val[k] = sval[sl[k]], st[k] = sst[sl[k]];
+      if (sl[k] < kSpillSlot) r[k] = srep[sl[k]];  // one 16-B gather per message
 #pragma unroll
     for (int k = 0; k < kSK; ++k)
-      if (sl[k] < kSpillSlot) put_reply(rv, in.origin_base + (uint32_t)tile_index(t, k), val[k], st[k]);
+      if (sl[k] < kSpillSlot)
+        put_reply(rv, in.origin_base + (uint32_t)tile_index(t, k), (int64_t)(((uint64_t)r[k].y << 32) | r[k].x),
+                  (int32_t)r[k].z);
   }
 }
 
@@ -642,14 +640,13 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     PT_HIP_CHECK(hipMalloc((void**)&sort_sidx_, (size_t)a.M * 4));
     sort_cap_ = (uint64_t)a.M;
   }
-  if (a.ordered && !stage_val_) {
+  if (a.ordered && !stage_rep_) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       throw std::runtime_error("mailbox send: first ordered Send inside a graph capture (warm up first)");
     const uint64_t n = (uint64_t)S * slots();
-    PT_HIP_CHECK(hipMalloc((void**)&stage_val_, n * 8));
-    PT_HIP_CHECK(hipMalloc((void**)&stage_st_, n * 4));
-    bytes_ += n * 12;
+    PT_HIP_CHECK(hipMalloc(&stage_rep_, n * 16));
+    bytes_ += n * 16;
   }
   SortIn in{};
   in.actor = (const uint32_t*)a.actor;
@@ -667,6 +664,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.aw_shift = (a.affine_w && (a.affine_w & (a.affine_w - 1)) == 0) ? __builtin_ctz(a.affine_w) : -1;
   in.rank_self = a.rank_self;
   in.origin_base = a.origin_base;
+  static const bool dir_nt = getenv("PTYPE_DIR_NT") && atoi(getenv("PTYPE_DIR_NT")) != 0;
+  in.dir_nt = dir_nt;
   const int64_t tiles = (a.M + kSTile - 1) / kSTile;
   if (tiles > 0xffffffffll) throw std::invalid_argument("mailbox send: batch too large");
   in.tiles = (uint32_t)tiles;
@@ -748,10 +747,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       attr = true;
     }
     hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(S), dim3(kOrdThreads), lds, st, mv_, sort_gsum_, ngroups,
-                       (int64_t*)a.state, a.n_state, a.delay_ticks, ob, stage_val_, stage_st_);
+                       (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);
     PT_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(mbx_complete_kernel, dim3(in.G), dim3(kST), 0, st, in, (const uint32_t*)sort_sidx_,
-                       (const int64_t*)stage_val_, (const int32_t*)stage_st_, rv);
+                       (const u32x4*)stage_rep_, rv);
   } else {
     if (a.fixed_method == kCalculatorMultiply)
       hipLaunchKernelGGL((mbx_drain_msg_kernel<kCalculatorMultiply>), dim3(in.G), dim3(kST), 0, st, mv_, in,

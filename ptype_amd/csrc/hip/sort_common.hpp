@@ -24,6 +24,13 @@ constexpr int kSTile = kST * kSK;        // 4096 messages
 constexpr int kSWave = kSK * kWave;  // a wave's contiguous run of a tile (512)
 
 
+// The route directory gather: one 4-B word per message from a table that lives
+// in L2 / MALL, at random -- each lane a different line.  `nt` (PTYPE_DIR_NT=1)
+// loads it non-temporal (experiment: the TA stalls on TCP for these gathers).
+__device__ __forceinline__ uint32_t dir_load(const uint32_t* p, bool nt) {
+  return nt ? __builtin_nontemporal_load(p) : *p;
+}
+
 struct SortIn {  // by value
   const uint32_t* actor;
   const int64_t* a0;
@@ -43,6 +50,7 @@ struct SortIn {  // by value
   uint32_t G;      // blocks
   uint32_t tiles;  // ceil(M / kSTile)
   uint32_t tpb;    // tiles per block
+  bool dir_nt;       // non-temporal directory gathers (experiment)
 };
 
 // Block b's range: XCD (b % 8) owns virtual blocks [x * G/8, (x+1) * G/8).
@@ -56,7 +64,7 @@ __device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[
   if constexpr (MODE == 1) {
     uint32_t w[kSK];
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) w[k] = a[k] < in.n_dir ? in.dir[a[k]] : kDirFallback;
+    for (int k = 0; k < kSK; ++k) w[k] = a[k] < in.n_dir ? dir_load(in.dir + a[k], in.dir_nt) : kDirFallback;
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
