@@ -800,7 +800,7 @@ Mailboxes::~Mailboxes() {
   (void)hipFree(mv_.ctr);
   (void)hipFree(mv_.stats);
   for (void* p : {(void*)sort_hist_, (void*)sort_gsum_, (void*)sort_ticket_, (void*)sort_rw_, (void*)sort_sidx_,
-                  stage_rep_})
+                  (void*)sort_tinfo_, stage_rep_})
     if (p) (void)hipFree(p);
   if (ctrl_) (void)hipHostFree(ctrl_);
 }

@@ -203,7 +203,8 @@ class Mailboxes {
   uint32_t* sort_gsum_ = nullptr;   // [kMboxSortGroups][S] group sums (zero between Sends: the drains clear them)
   unsigned* sort_ticket_ = nullptr; // last-block ticket of the parallel drain (self-resetting)
   uint32_t* sort_rw_ = nullptr;     // [M] each message's mailbox (route word), count -> scatter
-  uint32_t* sort_sidx_ = nullptr;   // [M] each message's ring slot, scatter -> drain / completion
+  uint32_t* sort_sidx_ = nullptr;   // [M] each message's ring slot (message-order drain; spilled tiles)
+  uint32_t* sort_tinfo_ = nullptr;  // [tiles][2][S] each tile's runs: slot bias, count (ring-order drain / completion)
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
   // ordered drain: replies staged at ring slots [S * Q], one 16-B word each
   // (value lo, value hi, status, 0) -- one gather per message in the completion

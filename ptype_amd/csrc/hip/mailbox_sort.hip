@@ -72,8 +72,9 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // read of an overflow count.  Ordered batches keep the ring's
 // FIFO and answer kStatusOverflow (send_all re-sends the tail).
 constexpr uint32_t kSpillSlot = 0xfffffffeu;
+constexpr uint32_t kRunSpilled = 0x80000000u;  // tinfo count word: the run did not fit the ring's room
 
-template <int MODE, bool ARRIVAL>
+template <int MODE>
 __global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_s, uint32_t* __restrict__ hist,
                                                         uint32_t* __restrict__ gsum, uint32_t* __restrict__ rw) {
   __shared__ uint32_t cnt[kMboxSortMaxShards];
@@ -89,21 +90,12 @@ __global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_
     uint32_t mb[kSK];
     resolve_k<MODE>(in, a, r, mb);
     if (t + 1 < t1) load_actors(in, t + 1, a);  // next tile's loads in flight while this one counts
-    unsigned c = 0;
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       const int64_t i = tile_index(t, k);
       const bool ok = r[k] == in.rank_self && mb[k] < kMaxMbox;
       if (i < in.M) rw[i] = ok ? mb[k] : kNoSlot;
-      if constexpr (ARRIVAL) {
-        c += ok ? 1u : 0u;
-      } else if (ok) {
-        atomicAdd(&cnt[mb[k] & (S - 1)], 1u);
-      }
-    }
-    if constexpr (ARRIVAL) {
-      c = (unsigned)__builtin_amdgcn_readlane((int)wave_incl_scan(c), 63);
-      if (lane_id() == 0 && c) atomicAdd(&cnt[t & (S - 1)], c);
+      if (ok) atomicAdd(&cnt[mb[k] & (S - 1)], 1u);
     }
   }
   __syncthreads();
@@ -137,37 +129,33 @@ __device__ __forceinline__ void load_routed(const SortIn& in, const uint32_t* __
   }
 }
 
-// STAGED (per-actor rings, opt-in: PTYPE_SCATTER_STAGED=1): a tile's records
-// are first placed in LDS in ring order -- grouped by shard, message order
-// within a shard -- and then written out by consecutive threads, so a wave's
-// stores cover a few whole runs instead of 64 scattered 16-B records.
-// Measured SLOWER on MI355X (8 Mi msgs, 256 shards: 117 -> 161 us): the 80 KB
-// stage halves the resident blocks and adds three barriers and a binary search
-// per record, which costs more than the scattered stores (L2 merges them).
-constexpr size_t kStageBytes = (size_t)kSTile * 16;
-__host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t S, bool staged) {
-  return (size_t)S * (16 + 4 * (kST / kWave)) + (staged ? (size_t)S * 12 + kStageBytes : 0);
-}
+// Per-tile runs (`tinfo`, [tiles][2][S] u32): tile t's records of shard s sit at
+// ring slots s | ((bias + j) & (Q - 1)), j < count (bias = epoch-start tail +
+// the run's offset + the shard's rotation; count clamped to the free room, its
+// top bit set when the run spilled / overflowed the room) -- what the ring-order
+// drain and completion read instead of a per-message slot index.  The slot
+// index `sidx` is written only where a consumer needs it: every message with
+// `all_sidx` (the message-order drain, PTYPE_MBOX_DRAIN=msg), and the whole
+// tile when some message of it spilled (the drain runs that tile in message
+// order).  (An opt-in LDS-staged write-out in ring order measured slower,
+// 117 -> 161 us per 8 Mi msgs: the 80 KB stage halved the resident blocks;
+// removed, see git history 4c4ea76.)
+__host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t S) { return (size_t)S * (16 + 4 * (kST / kWave)); }
 
-template <bool ARRIVAL, bool A2, bool MC, bool STAGED>
+template <bool A2, bool MC>
 __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv, const uint32_t* __restrict__ hist,
                                                           const uint32_t* __restrict__ gsum,
                                                           const uint32_t* __restrict__ rw,
-                                                          uint32_t* __restrict__ sidx, ReplyView rv, bool spill) {
-  // LDS sized by the shard count (16 + 4 * waves B per shard, + 12 B and the stage
-  // when STAGED): occupancy is not capped by the 1024-shard maximum
+                                                          uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
+                                                          ReplyView rv, bool spill, bool all_sidx) {
+  // LDS sized by the shard count (16 + 4 * waves B per shard): occupancy is not
+  // capped by the 1024-shard maximum
   extern __shared__ __align__(16) unsigned char smem_sc[];
   const uint32_t S = 1u << mv.log_s;
-  u32x4* stage = reinterpret_cast<u32x4*>(smem_sc);  // STAGED: the tile's records in ring order
-  unsigned long long* base =
-      reinterpret_cast<unsigned long long*>(smem_sc + (STAGED ? kStageBytes : 0));  // ring position of offset 0 (tail)
+  unsigned long long* base = reinterpret_cast<unsigned long long*>(smem_sc);  // ring position of offset 0 (tail)
   uint32_t* run = reinterpret_cast<uint32_t*>(base + S);  // this block's next offset per shard
   uint32_t* room = run + S;                               // offset limit (free ring slots)
   uint32_t* wcnt_all = room + S;                          // [kST / kWave][S] per-wave counts -> wave offsets
-  uint32_t* rb = wcnt_all + (kST / kWave) * S;            // STAGED: run[] before this tile
-  uint32_t* tc = rb + S;                                  // STAGED: this tile's count per shard
-  uint32_t* tpre = tc + S;                                // STAGED: exclusive prefix of tc (stage offsets)
-  __shared__ uint32_t scan_w[kST / kWave];
   auto wcnt = [&](unsigned ww, uint32_t sh) -> uint32_t& { return wcnt_all[ww * S + sh]; };
   const uint64_t Q = 1ull << mv.log_q;
   const uint32_t v = virt_block(blockIdx.x, in.G);
@@ -196,9 +184,8 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       const bool ok = mb[k] != kNoSlot;
-      sh[k] = ARRIVAL ? (t & (S - 1)) : (mb[k] & (S - 1));
-      const uint64_t act = __ballot(ok);
-      const uint64_t peers = ARRIVAL ? act : match_bits(sh[k], mv.log_s, act);
+      sh[k] = mb[k] & (S - 1);
+      const uint64_t peers = match_bits(sh[k], mv.log_s, __ballot(ok));
       const unsigned below = mbcnt64(peers);
       const int leader = peers ? __builtin_ctzll(peers) : 0;
       unsigned old = 0;
@@ -209,34 +196,22 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
       wr[k] = (unsigned)__shfl((int)old, leader) + below;
     }
     __syncthreads();
+    int sp = 0;
     for (uint32_t s = threadIdx.x; s < S; s += kST) {  // wave offsets in message order, then the block's run
       uint32_t rr = run[s];
-      if constexpr (STAGED) rb[s] = rr;
 #pragma unroll
       for (int ww = 0; ww < kST / kWave; ++ww) {
         const uint32_t c = wcnt(ww, s);
         wcnt(ww, s) = rr;
         rr += c;
       }
-      if constexpr (STAGED) tc[s] = rr - run[s];
       run[s] = rr;
+      sp |= rr > room[s];
     }
-    if constexpr (STAGED) {  // stage offsets: exclusive prefix of the tile's shard counts
-      __syncthreads();
-      const uint32_t per = (S + kST - 1) / kST, s0 = threadIdx.x * per, s1 = min(S, s0 + per);
-      uint32_t mine = 0;
-      for (uint32_t s = s0; s < s1; ++s) mine += tc[s];
-      const uint32_t incl = wave_incl_scan(mine);
-      if (lane == kWave - 1) scan_w[w] = incl;
-      __syncthreads();
-      uint32_t acc = incl - mine;
-      for (unsigned ww = 0; ww < w; ++ww) acc += scan_w[ww];
-      for (uint32_t s = s0; s < s1; ++s) {
-        tpre[s] = acc;
-        acc += tc[s];
-      }
-    }
-    __syncthreads();
+    bool tile_spill = false;  // (either barrier publishes the wave offsets too)
+    if (spill) tile_spill = __syncthreads_or(sp) != 0;
+    else __syncthreads();
+    const bool wsidx = all_sidx || tile_spill;
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       const int64_t i = tile_index(t, k);
@@ -244,7 +219,7 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
       const uint32_t origin = in.origin_base + (uint32_t)i;
       if (mb[k] == kNoSlot) {
         ++n_miss;
-        sidx[i] = kNoSlot;
+        if (wsidx) sidx[i] = kNoSlot;
         write_status(rv, origin, kStatusNoActor);
         continue;
       }
@@ -256,22 +231,15 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
           continue;
         }
         ++n_ovf;  // answered now, re-sent by send_all
-        sidx[i] = kNoSlot;
+        if (wsidx) sidx[i] = kNoSlot;
         write_status(rv, origin, kStatusOverflow);
         continue;
       }
       const int64_t x0 = v0[k], x1 = v1[k], x2 = v2[k];
       const uint32_t mt = meth[k];
       const uint64_t slot = slot_at(mv, sh[k], base[sh[k]] + off);
-      sidx[i] = (uint32_t)slot;
-      const bool compact = mt < 128u && fits_i32(x0) && fits_i32(x1) && x2 == 0;
-      if (STAGED) {  // the write-out below stores it (a wide record goes out now; its stage entry says so)
-        const uint32_t lpos = tpre[sh[k]] + (off - rb[sh[k]]);
-        stage[lpos] = compact ? u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)x0, (uint32_t)x1}
-                              : u32x4{0u, 0u, 0u, 0u};
-      }
-      if (STAGED && compact) {
-      } else if (compact) {
+      if (wsidx) sidx[i] = (uint32_t)slot;
+      if (mt < 128u && fits_i32(x0) && fits_i32(x1) && x2 == 0) {
         *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
             u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)x0, (uint32_t)x1};
       } else {
@@ -284,23 +252,16 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
       }
       ++n_enq;
     }
-    if constexpr (STAGED) {  // write-out in ring order: thread j stores stage position j
-      __syncthreads();
-      const uint32_t total = tpre[S - 1] + tc[S - 1];
-      for (uint32_t j = threadIdx.x; j < total; j += kST) {
-        uint32_t lo = 0, hi = S - 1;  // the last shard whose stage offset is <= j (a non-empty one)
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi + 1) >> 1;
-          if (tpre[mid] <= j) lo = mid;
-          else hi = mid - 1;
-        }
-        const uint32_t off = rb[lo] + (j - tpre[lo]);
-        if (off >= room[lo]) continue;  // spilled / overflowed: never staged
-        const u32x4 r = stage[j];
-        if (r.x) *reinterpret_cast<u32x4*>(rec_a(mv, slot_at(mv, lo, base[lo] + off))) = r;
+    if (tinfo) {  // the tile's runs (after the stores: the messages' registers are dead by now -- +25 VGPRs above)
+      // slot bias from the epoch-start tail (a drain may commit before the completion reads it)
+      for (uint32_t s = threadIdx.x; s < S; s += kST) {
+        const uint32_t r0 = wcnt(0, s), rr = run[s];  // wave 0's offset = the run before this tile
+        const uint32_t cc = r0 >= room[s] ? 0u : min(rr - r0, room[s] - r0);
+        tinfo[(size_t)t * 2 * S + s] = (uint32_t)(base[s] + r0) + shard_rot(mv, s);
+        tinfo[(size_t)t * 2 * S + S + s] = cc | (rr > room[s] ? kRunSpilled : 0u);
       }
     }
-    __syncthreads();  // wcnt rows (and the stage) are reused by the next tile
+    __syncthreads();  // wcnt rows are reused by the next tile
   }
   block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
   if (spill) {
@@ -372,10 +333,77 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 }
 
 // ---------------------------------------------------------------- K3s parallel drain
-// Batches without ordered methods: every record runs on its own, so the drain
-// takes each message's record from its ring slot in MESSAGE order (the slot the
-// scatter recorded) -- the record reads are gathers, the replies land
-// coalesced.  The last block commits every shard (and clears the group sums).
+// Batches without ordered methods: every record runs on its own.
+//
+// Ring-order form (default): one block per tile.  The tile's records sit in S
+// runs (the scatter's tinfo); the block reads them in RING order -- consecutive
+// lanes take consecutive ring slots, so the loads are whole-line runs -- runs
+// each handler, stages the reply in LDS at the message's place in the tile
+// (origin), and writes the tile's replies out coalesced.  Replaces the
+// message-order form's slot-index read (4 B per message) and its 16-B gather per
+// message (one line per lane).
+//
+// Message-order form (PTYPE_MBOX_DRAIN=msg, and any tile with a spilled
+// message): each message's record is taken from the ring slot the scatter
+// recorded, replies coalesced; a spilled message runs straight from the batch.
+//
+// The last block commits every shard (and clears the group sums).
+template <int FIXED>
+__device__ __forceinline__ void drain_tile_msg(const MboxView& mv, const SortIn& in, uint32_t t,
+                                               const uint32_t* __restrict__ sidx, const uint32_t* __restrict__ rw,
+                                               int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks,
+                                               const OutboxView& ob, const ReplyView& rv, unsigned long long& done,
+                                               unsigned long long& failed, unsigned long long& holes) {
+  uint32_t sl[kSK];
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    const int64_t i = tile_index(t, k);
+    sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
+  }
+  u32x4 ha[kSK];
+#pragma unroll
+  for (int k = 0; k < kSK; ++k)
+    ha[k] = sl[k] < kSpillSlot ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k])) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    if (sl[k] == kNoSlot) continue;  // answered by the scatter (no actor / ring full)
+    SortRec x;
+    if (sl[k] == kSpillSlot) {  // its ring was full: the message runs straight from the batch
+      const int64_t i = tile_index(t, k);
+      x.valid = true;
+      x.mb = rw[i];
+      x.method = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
+      x.flags = 0;
+      x.a0 = in.a0[i];
+      x.a1 = in.a1 ? in.a1[i] : 0;
+      x.a2 = in.a2 ? in.a2[i] : 0;
+    } else {
+      u32x4 hb = {0u, 0u, 0u, 0u};
+      int64_t a2v = 0;
+      if (rec_is_long(ha[k])) {
+        hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
+        if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
+      }
+      x = decode_sorted(ha[k], hb, a2v);
+    }
+    const uint32_t origin = in.origin_base + (uint32_t)tile_index(t, k);
+    if (!x.valid) {
+      ++holes;
+      write_status(rv, origin, kStatusNotDelivered);
+      continue;
+    }
+    MsgRecord m;
+    m.actor = x.mb;
+    m.method = (uint16_t)(FIXED ? FIXED : x.method);
+    m.flags = (uint16_t)x.flags;
+    m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
+    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
+    failed += rr.status != kStatusOk;
+    write_reply(rv, origin, rr);
+    ++done;
+  }
+}
+
 template <int FIXED>
 __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ sidx,
                                                             const uint32_t* __restrict__ rw,
@@ -388,56 +416,8 @@ __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn 
   unsigned long long done = 0, failed = 0, holes = 0;
   const uint32_t v = virt_block(blockIdx.x, in.G);
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
-  for (uint32_t t = t0; t < t1; ++t) {
-    uint32_t sl[kSK];
-#pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      const int64_t i = tile_index(t, k);
-      sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
-    }
-    u32x4 ha[kSK];
-#pragma unroll
-    for (int k = 0; k < kSK; ++k)
-      ha[k] = sl[k] < kSpillSlot ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k])) : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      if (sl[k] == kNoSlot) continue;  // answered by the scatter (no actor / ring full)
-      SortRec x;
-      if (sl[k] == kSpillSlot) {  // its ring was full: the message runs straight from the batch
-        const int64_t i = tile_index(t, k);
-        x.valid = true;
-        x.mb = rw[i];
-        x.method = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
-        x.flags = 0;
-        x.a0 = in.a0[i];
-        x.a1 = in.a1 ? in.a1[i] : 0;
-        x.a2 = in.a2 ? in.a2[i] : 0;
-      } else {
-        u32x4 hb = {0u, 0u, 0u, 0u};
-        int64_t a2v = 0;
-        if (rec_is_long(ha[k])) {
-          hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
-          if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
-        }
-        x = decode_sorted(ha[k], hb, a2v);
-      }
-      const uint32_t origin = in.origin_base + (uint32_t)tile_index(t, k);
-      if (!x.valid) {
-        ++holes;
-        write_status(rv, origin, kStatusNotDelivered);
-        continue;
-      }
-      MsgRecord m;
-      m.actor = x.mb;
-      m.method = (uint16_t)(FIXED ? FIXED : x.method);
-      m.flags = (uint16_t)x.flags;
-      m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
-      const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
-      failed += rr.status != kStatusOk;
-      write_reply(rv, origin, rr);
-      ++done;
-    }
-  }
+  for (uint32_t t = t0; t < t1; ++t)
+    drain_tile_msg<FIXED>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
   block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
   __shared__ bool last;
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
@@ -445,6 +425,305 @@ __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn 
   if (last) {  // every block's records are read: the rings are consumed
     const uint32_t S = 1u << mv.log_s;
     for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
+  }
+}
+
+// Tile t's runs in LDS: per shard the slot bias (ring slot of run entry j =
+// shard base | ((bias + j) & (Q - 1))) and an owner table (run entry j of the
+// tile -> its shard), j in [0, total).  Entries past a shard's free room (an
+// ordered batch's overflow: never written) are left out (the scatter clamped the
+// counts).  Returns the total; `spill` is set when a run overflowed the room (a
+// stateless tile's spill).
+struct RunLds {
+  uint32_t* bias;   // [S]
+  uint32_t* excl;   // [S] exclusive prefix of the (clamped) counts
+  uint16_t* owner;  // [kSTile]
+};
+
+__device__ __forceinline__ uint32_t load_tile_runs(const MboxView& mv, const uint32_t* __restrict__ tinfo, uint32_t t,
+                                                   const RunLds& L, int& spill) {
+  __shared__ uint32_t wsum[kST / kWave];
+  __shared__ uint32_t total_s;
+  const uint32_t S = 1u << mv.log_s;
+  const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  // thread j owns the shards [j * per, (j + 1) * per): a contiguous scan
+  const uint32_t per = (S + kST - 1) / kST, s0 = threadIdx.x * per, s1 = min(S, s0 + per);
+  uint32_t cnt[2] = {0u, 0u};  // per <= 2 (S <= 1024)
+  uint32_t mine = 0;
+  int sp = 0;
+  for (uint32_t s = s0, q = 0; s < s1; ++s, ++q) {
+    const uint32_t cw = tinfo[(size_t)t * 2 * S + S + s];
+    sp |= (cw & kRunSpilled) != 0;
+    cnt[q] = cw & ~kRunSpilled;
+    mine += cnt[q];
+    L.bias[s] = tinfo[(size_t)t * 2 * S + s];
+  }
+  const uint32_t incl = wave_incl_scan(mine);
+  if (lane == kWave - 1) wsum[w] = incl;
+  spill = __syncthreads_or(sp);
+  uint32_t acc = incl - mine;
+  for (unsigned ww = 0; ww < w; ++ww) acc += wsum[ww];
+  if (threadIdx.x == kST - 1) total_s = acc + mine;
+  for (uint32_t s = s0, q = 0; s < s1; ++s, ++q) {
+    L.excl[s] = acc;
+    L.bias[s] -= acc;
+    for (uint32_t j = acc; j < acc + cnt[q]; ++j) L.owner[j] = (uint16_t)s;
+    acc += cnt[q];
+  }
+  __syncthreads();
+  return total_s;
+}
+
+constexpr uint8_t kAbsent = 0xff;  // staged status: no record of this message in the tile's runs
+__host__ __device__ constexpr size_t ring_drain_lds_bytes(uint32_t S) {
+  return (size_t)kSTile * (8 + 2 + 1) + (size_t)S * 8;
+}
+
+template <int FIXED>
+__global__ __launch_bounds__(kST) void mbx_drain_ring_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ tinfo,
+                                                             const uint32_t* __restrict__ sidx,
+                                                             const uint32_t* __restrict__ rw,
+                                                             int64_t* __restrict__ state, uint32_t n_state,
+                                                             uint64_t delay_ticks, OutboxView ob, ReplyView rv,
+                                                             uint32_t* __restrict__ gsum, uint32_t ngroups,
+                                                             unsigned* __restrict__ ticket) {
+  extern __shared__ __align__(16) unsigned char smem_rd[];
+  const uint32_t S = 1u << mv.log_s;
+  int64_t* sval = reinterpret_cast<int64_t*>(smem_rd);  // [kSTile] reply values by place in the tile
+  RunLds L;
+  L.bias = reinterpret_cast<uint32_t*>(sval + kSTile);
+  L.excl = L.bias + S;
+  L.owner = reinterpret_cast<uint16_t*>(L.excl + S);
+  uint8_t* sst = reinterpret_cast<uint8_t*>(L.owner + kSTile);  // [kSTile] statuses, kAbsent = none
+  unsigned long long done = 0, failed = 0, holes = 0;
+  // tiles dealt XCD by XCD like the scatter's blocks (whose writes the XCD's L2 may still hold)
+  const uint32_t t = virt_block(blockIdx.x, gridDim.x);
+  if (t < in.tiles) {
+    const uint64_t i0 = (uint64_t)t * kSTile;
+    const uint32_t n_t = (uint32_t)min((uint64_t)kSTile, (uint64_t)in.M - i0);
+    for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
+    int spill = 0;
+    const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
+    if (spill) {  // some message of the tile spilled: the scatter left the tile's slot indices
+      drain_tile_msg<FIXED>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
+    } else {
+      const uint64_t sbase_mask = (1ull << mv.log_q) - 1;
+      u32x4 ha[kSK];
+      uint32_t sl[kSK];
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {  // ring order: lane-consecutive entries of the runs
+        const uint32_t j = (uint32_t)k * kST + threadIdx.x;
+        sl[k] = kNoSlot;
+        if (j < T) {
+          const uint32_t s = L.owner[j];
+          sl[k] = (uint32_t)(((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & sbase_mask));
+          ha[k] = *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k]));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {
+        if (sl[k] == kNoSlot) continue;
+        u32x4 hb = {0u, 0u, 0u, 0u};
+        int64_t a2v = 0;
+        if (rec_is_long(ha[k])) {
+          hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
+          if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
+        }
+        const SortRec x = decode_sorted(ha[k], hb, a2v);
+        const uint32_t local = x.origin - in.origin_base - (uint32_t)i0;
+        if (!x.valid || local >= n_t) {  // never written this epoch (cannot happen on a spill-free tile)
+          ++holes;
+          continue;
+        }
+        MsgRecord m;
+        m.actor = x.mb;
+        m.method = (uint16_t)(FIXED ? FIXED : x.method);
+        m.flags = (uint16_t)x.flags;
+        m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
+        const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
+        failed += rr.status != kStatusOk;
+        sval[local] = rr.value;
+        sst[local] = (uint8_t)rr.status;
+        ++done;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {  // the tile's replies, coalesced (misses were answered by the scatter)
+        const uint32_t j = (uint32_t)k * kST + threadIdx.x;
+        if (j < n_t && sst[j] != kAbsent) put_reply(rv, in.origin_base + (uint32_t)(i0 + j), sval[j], sst[j]);
+      }
+    }
+  }
+  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = last_block_ticket(ticket);
+  __syncthreads();
+  if (last)  // every block's records are read: the rings are consumed
+    for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
+}
+
+// ---------------------------------------------------------------- arrival rings (fixed positions)
+// Arrival sharding (batches without ordered methods): tile t's messages go to
+// shard t & (S - 1), at ring offsets (t >> log S) * kSTile + (place in the
+// tile) past the epoch's tail -- FIXED positions, so there is no count pass and
+// no slot index: one enqueue pass resolves each message and writes its record
+// (a tile is one contiguous 64 KB run of its ring: whole-line stores), and the
+// drain reads the same positions in message order (whole-line loads, replies
+// coalesced).  A message with no actor here leaves a zero record (its status is
+// written by the enqueue); a tile whose run does not fit the ring's free room
+// spills whole -- the drain runs it straight from the batch, re-resolving each
+// message -- and tiles spill only as a suffix of a shard's sequence.
+__device__ __forceinline__ bool arrival_fits(const MboxView& mv, const SortIn& in, uint32_t t, uint64_t& pos0) {
+  const uint32_t s = t & ((1u << mv.log_s) - 1);
+  const uint64_t Q = 1ull << mv.log_q;
+  const uint64_t tl = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
+  const uint64_t room = hd + Q > tl ? hd + Q - tl : 0;
+  const uint64_t off = (uint64_t)(t >> mv.log_s) * kSTile;
+  const uint64_t n_t = min((uint64_t)kSTile, (uint64_t)in.M - (uint64_t)t * kSTile);
+  pos0 = tl + off;
+  return off + n_t <= room;
+}
+
+template <int MODE, bool A2, bool MC>
+__global__ __launch_bounds__(kST) void mbx_arrival_enqueue_kernel(SortIn in, MboxView mv, ReplyView rv) {
+  unsigned long long n_enq = 0, n_miss = 0, n_spill = 0;
+  const uint32_t t = virt_block(blockIdx.x, gridDim.x);
+  if (t < in.tiles) {
+    uint64_t pos0 = 0;
+    const bool fits = arrival_fits(mv, in, t, pos0);
+    const uint32_t s = t & ((1u << mv.log_s) - 1);
+    uint32_t a[kSK], mb[kSK], meth[kSK];
+    int64_t x0[kSK], x1[kSK], x2[kSK];
+    int r[kSK];
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      const int64_t i = tile_index(t, k);
+      const bool ok = i < in.M;
+      a[k] = ok ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
+      x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
+      x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+      x2[k] = 0;
+      if constexpr (A2) x2[k] = ok ? __builtin_nontemporal_load(in.a2 + i) : 0;
+      meth[k] = in.method_uniform;
+      if constexpr (MC) meth[k] = ok ? (uint32_t)in.mcol[i] : 0u;
+    }
+    resolve_k<MODE>(in, a, r, mb);
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      const int64_t i = tile_index(t, k);
+      if (i >= in.M) continue;
+      const uint32_t origin = in.origin_base + (uint32_t)i;
+      const bool ok = r[k] == in.rank_self && mb[k] < kMaxMbox;
+      const uint64_t slot = slot_at(mv, s, pos0 + (uint64_t)(i - (int64_t)t * kSTile));
+      if (!ok) {
+        ++n_miss;
+        write_status(rv, origin, kStatusNoActor);
+        if (fits) *reinterpret_cast<u32x4*>(rec_a(mv, slot)) = u32x4{0u, 0u, 0u, 0u};
+        continue;
+      }
+      if (!fits) {
+        ++n_spill;
+        continue;
+      }
+      const uint32_t mt = meth[k];
+      if (mt < 128u && fits_i32(x0[k]) && fits_i32(x1[k]) && x2[k] == 0) {
+        *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
+            u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)x0[k], (uint32_t)x1[k]};
+      } else {
+        const uint32_t fl = x2[k] != 0 ? (uint32_t)kFlagA2 : 0u;
+        *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
+            u32x4{origin | kCompactMark, mb[k] | kCompactLong, (mt & 0xffffu) | (fl << 16), 0u};
+        *reinterpret_cast<u32x4*>(rec_b(mv, slot)) = u32x4{(uint32_t)x0[k], (uint32_t)((uint64_t)x0[k] >> 32),
+                                                           (uint32_t)x1[k], (uint32_t)((uint64_t)x1[k] >> 32)};
+        if (fl) mv.a2[slot] = x2[k];
+      }
+      ++n_enq;
+    }
+  }
+  block_add_stats(mv.stats, n_enq, kMbEnqueued, n_miss, kMbNoActor, n_spill, kMbSpilled);
+}
+
+template <int FIXED, int MODE>
+__global__ __launch_bounds__(kST) void mbx_arrival_drain_kernel(MboxView mv, SortIn in, int64_t* __restrict__ state,
+                                                                uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
+                                                                ReplyView rv, unsigned* __restrict__ ticket) {
+  unsigned long long done = 0, failed = 0;
+  const uint32_t S = 1u << mv.log_s;
+  const uint32_t t = virt_block(blockIdx.x, gridDim.x);
+  if (t < in.tiles) {
+    uint64_t pos0 = 0;
+    const bool fits = arrival_fits(mv, in, t, pos0);
+    const uint32_t s = t & (S - 1);
+    SortRec x[kSK];
+    if (fits) {
+      u32x4 ha[kSK];
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {
+        const int64_t i = tile_index(t, k);
+        ha[k] = i < in.M ? *reinterpret_cast<const u32x4*>(rec_a(mv, slot_at(mv, s, pos0 + (uint64_t)(i - (int64_t)t * kSTile))))
+                         : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {
+        u32x4 hb = {0u, 0u, 0u, 0u};
+        int64_t a2v = 0;
+        if ((ha[k].x & kCompactMark) && rec_is_long(ha[k])) {
+          const uint64_t slot = slot_at(mv, s, pos0 + (uint64_t)(tile_index(t, k) - (int64_t)t * kSTile));
+          hb = *reinterpret_cast<const u32x4*>(rec_b(mv, slot));
+          if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[slot];
+        }
+        x[k] = decode_sorted(ha[k], hb, a2v);  // a zero record (no actor): not valid
+      }
+    } else {  // the tile spilled: run it from the batch
+      uint32_t a[kSK], mb[kSK];
+      int r[kSK];
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {
+        const int64_t i = tile_index(t, k);
+        a[k] = i < in.M ? in.actor[i] : 0xffffffffu;
+      }
+      resolve_k<MODE>(in, a, r, mb);
+#pragma unroll
+      for (int k = 0; k < kSK; ++k) {
+        const int64_t i = tile_index(t, k);
+        x[k].valid = i < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
+        if (!x[k].valid) continue;
+        x[k].mb = mb[k];
+        x[k].method = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
+        x[k].flags = 0;
+        x[k].a0 = in.a0[i];
+        x[k].a1 = in.a1 ? in.a1[i] : 0;
+        x[k].a2 = in.a2 ? in.a2[i] : 0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      if (!x[k].valid) continue;  // no actor: answered by the enqueue
+      MsgRecord m;
+      m.actor = x[k].mb;
+      m.method = (uint16_t)(FIXED ? FIXED : x[k].method);
+      m.flags = (uint16_t)x[k].flags;
+      m.a0 = x[k].a0, m.a1 = x[k].a1, m.a2 = x[k].a2;
+      const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
+      failed += rr.status != kStatusOk;
+      write_reply(rv, in.origin_base + (uint32_t)tile_index(t, k), rr);
+      ++done;
+    }
+  }
+  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, 0, -1);
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = last_block_ticket(ticket);
+  __syncthreads();
+  if (last) {  // every tile is read: each shard consumed the positions of its tiles that fit
+    for (uint32_t s = threadIdx.x; s < S; s += kST) {
+      uint64_t used = 0;
+      for (uint32_t tt = s; tt < in.tiles; tt += S) {
+        uint64_t pos0 = 0;
+        if (!arrival_fits(mv, in, tt, pos0)) break;  // the spilled suffix
+        used += min((uint64_t)kSTile, (uint64_t)in.M - (uint64_t)tt * kSTile);
+      }
+      epoch_commit(mv, s, (uint32_t)used);
+    }
   }
 }
 
@@ -466,6 +745,7 @@ struct OrdLds {
   uint32_t slot[kOrdWin];
   uint32_t act[kOrdWin];  // actor index for the handler (LDS-local or global mailbox)
   uint32_t meth[kOrdWin];  // method | flags << 16
+  uint32_t orig[kOrdWin];  // origin: the completion's place for the reply
   int64_t a0[kOrdWin], a1[kOrdWin], a2[kOrdWin];
 };
 
@@ -552,6 +832,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
       L.slot[d] = (uint32_t)slot[k];
       L.act[d] = in_lds ? (x[k].mb >> mv.log_s) : x[k].mb;
       L.meth[d] = x[k].method | (x[k].flags << 16);
+      L.orig[d] = x[k].origin;
       L.a0[d] = x[k].a0;
       L.a1[d] = x[k].a1;
       L.a2[d] = x[k].a2;
@@ -570,7 +851,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
         m.a0 = L.a0[d], m.a1 = L.a1[d], m.a2 = L.a2[d];
         const ReplyRecord rr = run_handler(m, st, nst, delay_ticks, ob, true);
         failed += rr.status != kStatusOk;
-        srep[L.slot[d]] = u32x4{(uint32_t)rr.value, (uint32_t)((uint64_t)rr.value >> 32), (uint32_t)rr.status, 0u};
+        srep[L.slot[d]] = u32x4{(uint32_t)rr.value, (uint32_t)((uint64_t)rr.value >> 32), (uint32_t)rr.status, L.orig[d]};
         ++done;
         if (!in_lds) vm_drain();  // global state: this store lands before the bin's next load
       }
@@ -585,30 +866,56 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   if (threadIdx.x == 0) epoch_commit(mv, s, tot);
 }
 
-// Ordered drain's replies, staged at ring slots, gathered into message order.
-// Tile-granular like the parallel drain: block b gathers the tiles whose
-// records scatter block b wrote, so its reads hit ~S short runs of contiguous
-// slots (lines shared by the block's waves) instead of one line per message.
-__global__ __launch_bounds__(kST) void mbx_complete_kernel(SortIn in, const uint32_t* __restrict__ sidx,
-                                                           const u32x4* __restrict__ srep, ReplyView rv) {
-  const uint32_t v = virt_block(blockIdx.x, in.G);
-  const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
-  for (uint32_t t = t0; t < t1; ++t) {
-    uint32_t sl[kSK];
+// Ordered drain's replies, staged at ring slots as {value, status, origin}, put
+// back into message order -- in RING order like the parallel drain: one block
+// per tile reads the tile's runs (whole lines), stages each reply at its place
+// in the tile (the origin word) in LDS, and writes the tile's replies out
+// coalesced.  (The message-order form gathered one 16-B word per message by the
+// scatter's slot index: 109 us per 8 Mi SeqFold messages.)  Overflowed
+// messages were answered by the scatter and have no run entry.
+__global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxView mv,
+                                                                const uint32_t* __restrict__ tinfo,
+                                                                const u32x4* __restrict__ srep, ReplyView rv) {
+  extern __shared__ __align__(16) unsigned char smem_cr[];
+  const uint32_t S = 1u << mv.log_s;
+  int64_t* sval = reinterpret_cast<int64_t*>(smem_cr);
+  RunLds L;
+  L.bias = reinterpret_cast<uint32_t*>(sval + kSTile);
+  L.excl = L.bias + S;
+  L.owner = reinterpret_cast<uint16_t*>(L.excl + S);
+  uint8_t* sst = reinterpret_cast<uint8_t*>(L.owner + kSTile);
+  const uint32_t t = virt_block(blockIdx.x, gridDim.x);
+  if (t >= in.tiles) return;
+  const uint64_t i0 = (uint64_t)t * kSTile;
+  const uint32_t n_t = (uint32_t)min((uint64_t)kSTile, (uint64_t)in.M - i0);
+  for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
+  int spill = 0;
+  const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
+  const uint64_t qmask = (1ull << mv.log_q) - 1;
+  u32x4 r[kSK];
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      const int64_t i = tile_index(t, k);
-      sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
+  for (int k = 0; k < kSK; ++k) {
+    const uint32_t j = (uint32_t)k * kST + threadIdx.x;
+    if (j < T) {
+      const uint32_t s = L.owner[j];
+      r[k] = srep[((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & qmask)];
+    } else {
+      r[k] = u32x4{0u, 0u, 0u, 0xffffffffu};
     }
-    u32x4 r[kSK];
+  }
 #pragma unroll
-    for (int k = 0; k < kSK; ++k)
-      if (sl[k] < kSpillSlot) r[k] = srep[sl[k]];  // one 16-B gather per message
+  for (int k = 0; k < kSK; ++k) {
+    const uint32_t local = r[k].w - in.origin_base - (uint32_t)i0;
+    if (local < n_t) {
+      sval[local] = (int64_t)(((uint64_t)r[k].y << 32) | r[k].x);
+      sst[local] = (uint8_t)r[k].z;
+    }
+  }
+  __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kSK; ++k)
-      if (sl[k] < kSpillSlot)
-        put_reply(rv, in.origin_base + (uint32_t)tile_index(t, k), (int64_t)(((uint64_t)r[k].y << 32) | r[k].x),
-                  (int32_t)r[k].z);
+  for (int k = 0; k < kSK; ++k) {
+    const uint32_t j = (uint32_t)k * kST + threadIdx.x;
+    if (j < n_t && sst[j] != kAbsent) put_reply(rv, in.origin_base + (uint32_t)(i0 + j), sval[j], sst[j]);
   }
 }
 
@@ -628,16 +935,22 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   if (a.arrival && a.ordered) throw std::invalid_argument("mailbox send: arrival sharding cannot serve ordered methods");
   PT_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = as_stream(a.stream);
-  // per-message workspace (route words, ring slots): grown outside graph capture
-  if ((uint64_t)a.M > sort_cap_) {
+  const int64_t tiles = (a.M + kSTile - 1) / kSTile;
+  if (tiles > 0xffffffffll) throw std::invalid_argument("mailbox send: batch too large");
+  // per-message workspace (route words, ring slots) and per-tile runs: grown outside graph capture
+  if (!a.arrival && (uint64_t)a.M > sort_cap_) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       throw std::runtime_error("mailbox send: a larger batch than before inside a graph capture (warm up first)");
     PT_HIP_CHECK(hipStreamSynchronize(st));
-    if (sort_rw_) PT_HIP_CHECK(hipFree(sort_rw_));
-    if (sort_sidx_) PT_HIP_CHECK(hipFree(sort_sidx_));
+    for (uint32_t** p : {&sort_rw_, &sort_sidx_, &sort_tinfo_})
+      if (*p) {
+        PT_HIP_CHECK(hipFree(*p));
+        *p = nullptr;
+      }
     PT_HIP_CHECK(hipMalloc((void**)&sort_rw_, (size_t)a.M * 4));
     PT_HIP_CHECK(hipMalloc((void**)&sort_sidx_, (size_t)a.M * 4));
+    PT_HIP_CHECK(hipMalloc((void**)&sort_tinfo_, (size_t)tiles * 2 * S * 4));
     sort_cap_ = (uint64_t)a.M;
   }
   if (a.ordered && !stage_rep_) {
@@ -666,8 +979,6 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.origin_base = a.origin_base;
   static const bool dir_nt = getenv("PTYPE_DIR_NT") && atoi(getenv("PTYPE_DIR_NT")) != 0;
   in.dir_nt = dir_nt;
-  const int64_t tiles = (a.M + kSTile - 1) / kSTile;
-  if (tiles > 0xffffffffll) throw std::invalid_argument("mailbox send: batch too large");
   in.tiles = (uint32_t)tiles;
   // blocks: as many as the histogram holds (it stays L2-resident for the prefixes),
   // a multiple of 8 (one contiguous eighth of the batch per XCD)
@@ -678,55 +989,11 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   G = std::max<int64_t>(G, 1);
   in.G = (uint32_t)G;
   in.tpb = (uint32_t)((tiles + G - 1) / G);
+  // one block per tile (tile-granular kernels), dealt XCD by XCD: a multiple of 8
+  const uint32_t tile_grid = (uint32_t)(tiles >= 8 ? (tiles + 7) / 8 * 8 : tiles);
   const uint32_t ngroups = (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks);
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
   const ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
-#define PT_COUNT(MO, AR) \
-  hipLaunchKernelGGL((mbx_count_kernel<MO, AR>), dim3(in.G), dim3(kST), 0, st, in, mv_.log_s, sort_hist_, sort_gsum_, sort_rw_)
-  if (a.arrival) {
-    if (mode == 2) PT_COUNT(2, true); else if (mode == 1) PT_COUNT(1, true); else PT_COUNT(0, true);
-  } else {
-    if (mode == 2) PT_COUNT(2, false); else if (mode == 1) PT_COUNT(1, false); else PT_COUNT(0, false);
-  }
-#undef PT_COUNT
-  PT_HIP_CHECK(hipGetLastError());
-  // per-actor rings, records staged in LDS and written out in ring order: opt-in (measured slower)
-  static const bool staged_ok = getenv("PTYPE_SCATTER_STAGED") && atoi(getenv("PTYPE_SCATTER_STAGED")) != 0;
-  const bool staged = staged_ok && !a.arrival && !a.a2;
-#define PT_SCAT1(AR, A2, MC, ST)                                                                                  \
-  do {                                                                                                            \
-    const size_t lds_ = scatter_lds_bytes(S, ST);                                                                 \
-    if (ST) {                                                                                                     \
-      static bool attr_ = false;                                                                                  \
-      if (!attr_) { /* above the 64 KB default dynamic LDS */                                                     \
-        PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_scatter_kernel<AR, A2, MC, ST>,                         \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,                              \
-                                         (int)scatter_lds_bytes(kMboxSortMaxShards, true)));                      \
-        attr_ = true;                                                                                             \
-      }                                                                                                           \
-    }                                                                                                             \
-    hipLaunchKernelGGL((mbx_scatter_kernel<AR, A2, MC, ST>), dim3(in.G), dim3(kST), lds_, st, in, mv_,           \
-                       (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_,       \
-                       sort_sidx_, rv, !a.ordered);                                                               \
-  } while (0)
-#define PT_SCAT(AR, A2, MC)                                  \
-  do {                                                       \
-    if (!(AR) && !(A2) && staged) PT_SCAT1(AR, A2, MC, true); \
-    else PT_SCAT1(AR, A2, MC, false);                         \
-  } while (0)
-#define PT_SCAT_AR(AR)                                  \
-  do {                                                  \
-    if (a.a2 && a.method_col) PT_SCAT(AR, true, true);   \
-    else if (a.a2) PT_SCAT(AR, true, false);            \
-    else if (a.method_col) PT_SCAT(AR, false, true);    \
-    else PT_SCAT(AR, false, false);                     \
-  } while (0)
-  if (a.arrival) PT_SCAT_AR(true);
-  else PT_SCAT_AR(false);
-#undef PT_SCAT_AR
-#undef PT_SCAT
-#undef PT_SCAT1
-  PT_HIP_CHECK(hipGetLastError());
   OutboxView ob;
   if (a.outbox_cap) {
     if (a.outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
@@ -738,6 +1005,56 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     ob.count = (unsigned long long*)a.outbox[5];
     ob.cap = a.outbox_cap;
   }
+  const bool fixed_mul = a.fixed_method == kCalculatorMultiply;
+
+  if (a.arrival) {  // fixed positions: enqueue + drain, no count pass
+#define PT_AENQ(MO)                                                                                        \
+  do {                                                                                                     \
+    if (a.a2 && a.method_col)                                                                              \
+      hipLaunchKernelGGL((mbx_arrival_enqueue_kernel<MO, true, true>), dim3(tile_grid), dim3(kST), 0, st, in, mv_, rv);  \
+    else if (a.a2)                                                                                         \
+      hipLaunchKernelGGL((mbx_arrival_enqueue_kernel<MO, true, false>), dim3(tile_grid), dim3(kST), 0, st, in, mv_, rv); \
+    else if (a.method_col)                                                                                 \
+      hipLaunchKernelGGL((mbx_arrival_enqueue_kernel<MO, false, true>), dim3(tile_grid), dim3(kST), 0, st, in, mv_, rv); \
+    else                                                                                                   \
+      hipLaunchKernelGGL((mbx_arrival_enqueue_kernel<MO, false, false>), dim3(tile_grid), dim3(kST), 0, st, in, mv_, rv); \
+  } while (0)
+#define PT_ADRAIN(FX, MO)                                                                                   \
+  hipLaunchKernelGGL((mbx_arrival_drain_kernel<FX, MO>), dim3(tile_grid), dim3(kST), 0, st, mv_, in, (int64_t*)a.state, \
+                     a.n_state, a.delay_ticks, ob, rv, sort_ticket_)
+    if (mode == 2) PT_AENQ(2); else if (mode == 1) PT_AENQ(1); else PT_AENQ(0);
+    PT_HIP_CHECK(hipGetLastError());
+    if (fixed_mul) {
+      if (mode == 2) PT_ADRAIN(kCalculatorMultiply, 2); else if (mode == 1) PT_ADRAIN(kCalculatorMultiply, 1);
+      else PT_ADRAIN(kCalculatorMultiply, 0);
+    } else {
+      if (mode == 2) PT_ADRAIN(0, 2); else if (mode == 1) PT_ADRAIN(0, 1); else PT_ADRAIN(0, 0);
+    }
+#undef PT_AENQ
+#undef PT_ADRAIN
+    PT_HIP_CHECK(hipGetLastError());
+    return;
+  }
+
+#define PT_COUNT(MO) \
+  hipLaunchKernelGGL((mbx_count_kernel<MO>), dim3(in.G), dim3(kST), 0, st, in, mv_.log_s, sort_hist_, sort_gsum_, sort_rw_)
+  if (mode == 2) PT_COUNT(2); else if (mode == 1) PT_COUNT(1); else PT_COUNT(0);
+#undef PT_COUNT
+  PT_HIP_CHECK(hipGetLastError());
+  // the stateless drain: ring order (default) or message order (PTYPE_MBOX_DRAIN=msg: every slot index written)
+  static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
+  const bool all_sidx = msg_drain && !a.ordered;
+#define PT_SCAT(A2, MC)                                                                                           \
+  hipLaunchKernelGGL((mbx_scatter_kernel<A2, MC>), dim3(in.G), dim3(kST), scatter_lds_bytes(S), st, in, mv_,     \
+                     (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_, sort_sidx_, \
+                     all_sidx ? nullptr : sort_tinfo_, rv, !a.ordered, all_sidx)
+  if (a.a2 && a.method_col) PT_SCAT(true, true);
+  else if (a.a2) PT_SCAT(true, false);
+  else if (a.method_col) PT_SCAT(false, true);
+  else PT_SCAT(false, false);
+#undef PT_SCAT
+  PT_HIP_CHECK(hipGetLastError());
+  const size_t ring_lds = ring_drain_lds_bytes(S);
   if (a.ordered) {
     const size_t lds = sizeof(OrdLds) + (size_t)kOrdStateMax * sizeof(int64_t);
     static bool attr = false;
@@ -749,19 +1066,24 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(S), dim3(kOrdThreads), lds, st, mv_, sort_gsum_, ngroups,
                        (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);
     PT_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(mbx_complete_kernel, dim3(in.G), dim3(kST), 0, st, in, (const uint32_t*)sort_sidx_,
-                       (const u32x4*)stage_rep_, rv);
+    hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST), ring_lds, st, in, mv_,
+                       (const uint32_t*)sort_tinfo_, (const u32x4*)stage_rep_, rv);
+  } else if (msg_drain) {
+#define PT_DMSG(FX)                                                                                              \
+  hipLaunchKernelGGL((mbx_drain_msg_kernel<FX>), dim3(in.G), dim3(kST), 0, st, mv_, in, (const uint32_t*)sort_sidx_, \
+                     (const uint32_t*)sort_rw_, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_,  \
+                     ngroups, sort_ticket_)
+    if (fixed_mul) PT_DMSG(kCalculatorMultiply);
+    else PT_DMSG(0);
+#undef PT_DMSG
   } else {
-    if (a.fixed_method == kCalculatorMultiply)
-      hipLaunchKernelGGL((mbx_drain_msg_kernel<kCalculatorMultiply>), dim3(in.G), dim3(kST), 0, st, mv_, in,
-                         (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_, (int64_t*)a.state, a.n_state,
-                         a.delay_ticks, ob, rv, sort_gsum_,
-                         ngroups, sort_ticket_);
-    else
-      hipLaunchKernelGGL((mbx_drain_msg_kernel<0>), dim3(in.G), dim3(kST), 0, st, mv_, in,
-                         (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_, (int64_t*)a.state, a.n_state,
-                         a.delay_ticks, ob, rv, sort_gsum_,
-                         ngroups, sort_ticket_);
+#define PT_DRING(FX)                                                                                            \
+  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX>), dim3(tile_grid), dim3(kST), ring_lds, st, mv_, in,            \
+                     (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_,       \
+                     (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_)
+    if (fixed_mul) PT_DRING(kCalculatorMultiply);
+    else PT_DRING(0);
+#undef PT_DRING
   }
   PT_HIP_CHECK(hipGetLastError());
 }

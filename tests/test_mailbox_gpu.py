@@ -54,7 +54,8 @@ def test_mailbox_send_calculator_matches_reference(directory):
     assert (ctr[:, 0] == ctr[:, 2]).all() and int(ctr[:, 0].sum()) == M  # every ring drained
 
 
-def test_mailbox_unknown_actor_and_three_args():
+@pytest.mark.parametrize("sharding", ["actor", "arrival"])
+def test_mailbox_unknown_actor_and_three_args(sharding):
     n, M = 4096, 50_000
     t, _ = placed_table(n)
     mb = Mailboxes(DEV, shards=64, slots=4096)
@@ -63,7 +64,7 @@ def test_mailbox_unknown_actor_and_three_args():
     lo = torch.randint(0, 50, (M,), generator=g)
     req = B.MsgBatch(actor.to(DEV), lo.to(DEV), (lo + 10).to(DEV), torch.randint(2, 5000, (M,), generator=g).to(DEV),
                      METHOD_PRIME_CHECK)
-    val, st = mb.send(req, t, None)
+    val, st = mb.send(req, t, None, sharding=sharding)
     torch.cuda.synchronize()
     ref_v, ref_s = B._handler_ref(torch.full((M,), METHOD_PRIME_CHECK), actor.long(), lo, lo + 10,
                                   req.a2.cpu(), None)
@@ -272,6 +273,34 @@ def test_sorted_mailbox_calculator_exact(sharding, M):
     assert s["enqueued"] == 2 * M and s["processed"] == 2 * M and s["overflow"] == 0 and s["holes"] == 0
     ctr = mb.shard_counters()
     assert (ctr[:, 0] == ctr[:, 2]).all() and int(ctr[:, 0].sum()) == 2 * M
+
+
+@pytest.mark.parametrize("sharding", ["actor", "arrival"])
+def test_sorted_mailbox_partial_spill_then_clean_send(sharding):
+    """Rings that hold only part of a Send: the early tiles / runs go through the
+    rings, the rest spill (run from the batch by the drain: the ring-order drain
+    takes a spilled tile in message order).  Every message is answered exactly,
+    misses included, and the next Send finds every ring consumed."""
+    n, M = 4096, 300_000
+    t, _ = placed_table(n)
+    mb = Mailboxes(DEV, shards=16, slots=8192)
+    g = torch.Generator().manual_seed(11)
+    for rep in range(2):
+        actor = torch.randint(0, n + 300, (M,), generator=g, dtype=torch.int32)  # ids >= n: no actor
+        a0 = torch.randint(-(1 << 31), 1 << 31, (M,), generator=g, dtype=torch.int64)
+        a1 = torch.randint(-(1 << 20), 1 << 20, (M,), generator=g, dtype=torch.int64)
+        req = B.MsgBatch(actor.to(DEV), a0.to(DEV), a1.to(DEV), None, METHOD_CALC_MULTIPLY)
+        val, st = mb.send(req, t, None, sharding=sharding)
+        torch.cuda.synchronize()
+        known = actor < n
+        st, val = st.cpu(), val.cpu()
+        assert bool((st[known] == STATUS_OK).all()) and bool((st[~known] == STATUS_NO_ACTOR).all())
+        assert torch.equal(val[known], (a0 * a1)[known])
+        ctr = mb.shard_counters()
+        assert (ctr[:, 0] == ctr[:, 2]).all()  # consumed: tail == head on every shard
+    s = mb.stats()
+    assert s["spilled"] > 0 and s["overflow"] == 0 and s["holes"] == 0
+    assert s["processed"] == s["enqueued"] + s["spilled"], s
 
 
 def test_sorted_vs_tagged_kernels_same_replies():
