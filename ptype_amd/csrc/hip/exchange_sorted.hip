@@ -303,6 +303,150 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
   meta_publish(acc, in.mcol != nullptr, in.method_uniform, in.M, meta);
 }
 
+// ---------------------------------------------------------------- sender: one pass (rank-only batches)
+// count + scan + scatter as ONE kernel when the sender sorts by rank alone
+// (K = 1: a region is one message-ordered run, so a message's position is its
+// tile's prefix within the region plus its rank in the tile -- no region-wide
+// totals are needed before writing).  Each block claims the next tile in launch
+// order, resolves its messages (the directory gather, once), ranks them per
+// destination, publishes the tile's per-destination counts and looks back over
+// earlier tiles' descriptors for its prefix (decoupled look-back, as in the
+// mailbox sort: mailbox_sort.hip mbx_onesweep_kernel; u64 descriptors {tag 24 |
+// status 2 | value 38} through memory-side atomics), then packs and stores its
+// records.  The last tile writes the region headers and shard tables, the
+// last block to finish advances the epoch tag (every block has read it by then).
+
+template <int MODE, int S>
+__global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsigned long long* __restrict__ desc,
+                                                          unsigned* __restrict__ tctr, unsigned* __restrict__ ticket,
+                                                          uint32_t* __restrict__ sendbuf, int64_t req_stride,
+                                                          int64_t tab_off, uint32_t C, uint32_t hdr_word3,
+                                                          int rank_self, PackedLayout L, int32_t* __restrict__ perm,
+                                                          unsigned long long* __restrict__ meta,
+                                                          unsigned long long* __restrict__ stats) {
+  __shared__ uint32_t wcnt[kST / kWave][kSxMaxRanks];
+  __shared__ uint32_t pre[kSxMaxRanks];
+  __shared__ uint32_t tile_s, tag_s, mbmax_s;
+  const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  if (threadIdx.x == 0) {
+    tag_s = (tctr[1] & 0xffffffu) + 1u;
+    const uint32_t t = atomicAdd(&tctr[0], 1u);
+    if (t == in.tiles - 1) atomicExch(&tctr[0], 0u);  // every block has claimed
+    tile_s = t;
+    mbmax_s = 0;
+  }
+  if (lane < kSxMaxRanks) wcnt[w][lane] = 0;
+  __syncthreads();
+  const uint32_t t = tile_s, tag = tag_s;
+  const uint32_t rbits = R > 1 ? 32 - __builtin_clz((uint32_t)R - 1) : 0;
+  // phase 1: routes and ranks (a small register file: occupancy hides the gathers)
+  uint32_t pr[kSK], mb[kSK];
+  uint32_t mbmax = 0;
+  {
+    uint32_t a[kSK];
+    int r[kSK];
+    load_actors(in, t, a);
+    resolve_k<MODE>(in, a, r, mb);
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      const bool ok = tile_index(t, k) < in.M && r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
+      if (ok) mbmax = mb[k] > mbmax ? mb[k] : mbmax;
+      const uint32_t bk = ok ? (uint32_t)r[k] : 0u;
+      const uint64_t peers = match_bits(bk, rbits, __ballot(ok));
+      const unsigned below = mbcnt64(peers);
+      const int leader = peers ? __builtin_ctzll(peers) : 0;
+      unsigned old = 0;
+      if (ok && below == 0) {
+        old = wcnt[w][bk];
+        wcnt[w][bk] = old + (unsigned)__popcll(peers);
+      }
+      pr[k] = ok ? (((unsigned)__shfl((int)old, leader) + below) << 8) | bk : 0xffu;
+    }
+  }
+  mbmax = wave_max(mbmax);
+  if (lane == 0 && mbmax) atomicMax(&mbmax_s, mbmax);
+  __syncthreads();
+  if (threadIdx.x < (unsigned)R) {  // destination d: wave offsets, publish, look back
+    const uint32_t d = threadIdx.x;
+    uint32_t c = 0;
+#pragma unroll
+    for (int ww = 0; ww < kST / kWave; ++ww) {
+      const uint32_t x = wcnt[ww][d];
+      wcnt[ww][d] = c;
+      c += x;
+    }
+    unsigned long long* dp = desc + (size_t)t * R + d;
+    uint64_t excl = 0;
+    unsigned long long timeouts = 0;
+    if (t == 0) {
+      __hip_atomic_exchange(dp, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_exchange(dp, desc_word(tag, kDescA, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      excl = lookback(desc + d, (uint32_t)R, (int64_t)t - 1, tag, timeouts);
+      __hip_atomic_exchange(dp, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+      if (timeouts) atomicAdd(&stats[2], timeouts);
+    }
+    pre[d] = (uint32_t)excl;
+    if (t == in.tiles - 1) {  // region d's header and (single-run) shard table
+      const uint32_t all = (uint32_t)(excl + c), n = all < C ? all : C;
+      uint32_t* region = sendbuf + (int64_t)d * req_stride;
+      region[tab_off] = 0;
+      for (int s2 = 1; s2 <= kSxShards; ++s2) region[tab_off + s2] = n;
+      *reinterpret_cast<uint4*>(region) = make_uint4(n, all, (uint32_t)rank_self, hdr_word3);
+      if (all) meta_max(meta + kMetaCap, all);
+    }
+  }
+  __syncthreads();
+  // phase 2: each message's arguments, packed at its position
+  MetaAcc acc;
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    const int64_t i = tile_index(t, k);
+    if (i >= in.M) continue;
+    const uint32_t rk = pr[k] & 0xffu;
+    if (rk == 0xffu) {
+      perm[i] = -2;  // no such actor: the completion answers kStatusNoActor
+      continue;
+    }
+    const uint32_t pos = pre[rk] + wcnt[w][rk] + (pr[k] >> 8);
+    if (pos >= C) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
+      perm[i] = -1;
+      continue;
+    }
+    const int64_t x0 = __builtin_nontemporal_load(in.a0 + i);
+    const int64_t x1 = in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    const int64_t x2 = in.a2 ? __builtin_nontemporal_load(in.a2 + i) : 0;
+    const uint32_t meth = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
+    const uint64_t z0 = zz_enc(x0), z1 = zz_enc(x1), z2 = in.a2 ? zz_enc(x2) : 0ull;
+    acc.z0 = z0 > acc.z0 ? z0 : acc.z0;
+    acc.z1 = z1 > acc.z1 ? z1 : acc.z1;
+    if (in.a2) acc.z2 = z2 > acc.z2 ? z2 : acc.z2;
+    if (in.mcol) {
+      acc.mm = meth > acc.mm ? meth : acc.mm;
+      acc.flags |= 1u << (meth < 7 ? meth : 7);
+    }
+    uint64_t f[5];
+    const bool fit = sx_fits(L, meth, in.method_uniform, mb[k], z0, z1, z2);
+    if (fit) {
+      f[0] = meth, f[1] = mb[k], f[2] = z0, f[3] = z1, f[4] = z2;
+      perm[i] = (int32_t)(rk * C + pos);
+    } else {  // wider than the layout in force: a null record holds the slot
+      f[0] = 0, f[1] = low_mask(L.w[1]), f[2] = 0, f[3] = 0, f[4] = 0;
+      perm[i] = -1;
+    }
+    uint32_t rec[S];
+    packed_pack<S>(L, f, rec);
+    store_words<S>(sendbuf + (int64_t)rk * req_stride + 4 + (int64_t)pos * S, rec);
+  }
+  acc.mb = mbmax_s;  // (the mailbox maximum of this tile: every lane sees the block's)
+  meta_publish(acc, in.mcol != nullptr, in.method_uniform, in.M, meta);
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = last_block_ticket(ticket);
+  __syncthreads();
+  if (last && threadIdx.x == 0) tctr[1] += 1u;  // every block has read this launch's tag: the next one's
+}
+
 // ---------------------------------------------------------------- receiver: parallel drain
 // grid (X, R): block (x, p) strides over source p's region in 64-record groups
 // per wave; a reply lands at its request's position (one ok-bitmap word per group).
@@ -593,10 +737,17 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   }
   PT_HIP_CHECK(hipMalloc(&hist_, (size_t)kMboxSortHistWords * 4));
   PT_HIP_CHECK(hipMalloc(&boff_, (size_t)kXMaxBuckets * 4));
+  const int64_t max_tiles = (max_chunk + kSTile - 1) / kSTile;
+  PT_HIP_CHECK(hipMalloc(&desc_, (size_t)std::max<int64_t>(max_tiles, 1) * R * 8));
+  PT_HIP_CHECK(hipMemset(desc_, 0, (size_t)std::max<int64_t>(max_tiles, 1) * R * 8));  // tag 0: never a live tag
+  PT_HIP_CHECK(hipMalloc(&tctr_, 2 * sizeof(unsigned)));
+  PT_HIP_CHECK(hipMemset(tctr_, 0, 2 * sizeof(unsigned)));
+  PT_HIP_CHECK(hipMalloc(&ticket_, kTicketWords * sizeof(unsigned)));
+  PT_HIP_CHECK(hipMemset(ticket_, 0, kTicketWords * sizeof(unsigned)));
   PT_HIP_CHECK(hipMalloc(&meta_dev_, 2 * kMetaWords * sizeof(uint64_t)));
   PT_HIP_CHECK(hipMemset(meta_dev_, 0, 2 * kMetaWords * sizeof(uint64_t)));
-  PT_HIP_CHECK(hipMalloc(&stats_, 2 * sizeof(unsigned long long)));
-  PT_HIP_CHECK(hipMemset(stats_, 0, 2 * sizeof(unsigned long long)));
+  PT_HIP_CHECK(hipMalloc(&stats_, 3 * sizeof(unsigned long long)));
+  PT_HIP_CHECK(hipMemset(stats_, 0, 3 * sizeof(unsigned long long)));
   PT_HIP_CHECK(hipHostMalloc(&meta_host_, 2 * kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
   memset(meta_host_, 0, 2 * kMetaWords * sizeof(uint64_t));
   for (auto& e : ev_meta_) PT_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -621,6 +772,9 @@ SortedExchange::~SortedExchange() {  // no synchronisation: a collective stuck o
   for (hipEvent_t e : ev_meta_) (void)hipEventDestroy(e);
   (void)hipFree(hist_);
   (void)hipFree(boff_);
+  (void)hipFree(desc_);
+  (void)hipFree(tctr_);
+  (void)hipFree(ticket_);
   (void)hipFree(meta_dev_);
   (void)hipFree(stats_);
   (void)hipHostFree(meta_host_);
@@ -628,9 +782,9 @@ SortedExchange::~SortedExchange() {  // no synchronisation: a collective stuck o
 }
 
 std::vector<uint64_t> SortedExchange::stats() const {
-  unsigned long long h[2] = {0, 0};
+  unsigned long long h[3] = {0, 0, 0};
   PT_HIP_CHECK(hipMemcpy(h, stats_, sizeof h, hipMemcpyDeviceToHost));
-  return {h[0], h[1]};
+  return {h[0], h[1], h[2]};
 }
 
 void SortedExchange::adopt(const uint64_t* meta, int64_t from) {
@@ -830,6 +984,41 @@ void SortedExchange::send(const SxSend& a) {
     else if (mode == 1) hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__); \
     else hipLaunchKernelGGL((KERNEL<0>), __VA_ARGS__);               \
   } while (0)
+    // rank-only batches: count + scan + scatter, or one pass with look-back (PTYPE_SX_SORT=onepass; measured
+    // slower at R = 8, 4 Mi msgs per chunk: 90 us vs 34 + 6.5 + 44 -- the look-back's memory-side atomic
+    // round trips cost more than the count pass's second read of the batch)
+    static const bool one_pass = getenv("PTYPE_SX_SORT") && std::string(getenv("PTYPE_SX_SORT")) == "onepass";
+    if (!sharded && in.tiles > 0 && one_pass) {
+      const uint32_t hdr3 = ((uint32_t)kFlagValid << 16) | (uint32_t)a.method_uniform;
+#define PT_SX_OS(MO, SV)                                                                                         \
+  hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_, ticket_, \
+                     b.send, rq, tab_off, (uint32_t)C, hdr3, rank_, L, b.perm, (unsigned long long*)meta, stats_)
+#define PT_SX_OS_S(MO)              \
+  switch (S) {                      \
+    case 1: PT_SX_OS(MO, 1); break; \
+    case 2: PT_SX_OS(MO, 2); break; \
+    case 3: PT_SX_OS(MO, 3); break; \
+    case 4: PT_SX_OS(MO, 4); break; \
+    case 6: PT_SX_OS(MO, 6); break; \
+    default: PT_SX_OS(MO, 8); break; \
+  }
+      if (mode == 2) {
+        PT_SX_OS_S(2)
+      } else if (mode == 1) {
+        PT_SX_OS_S(1)
+      } else {
+        PT_SX_OS_S(0)
+      }
+#undef PT_SX_OS_S
+#undef PT_SX_OS
+      PT_HIP_CHECK(hipGetLastError());
+      PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
+      PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_routed_[i], 0));
+      a2a(b.send, b.recv, (size_t)rq * 4, capturing);
+      PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], comm_stream_));
+      if (i > 0) serve(i - 1);
+      continue;
+    }
     PT_SX_MODE(sx_count_kernel, dim3(in.G), dim3(kST), 0, cs, in, R_, K, hist_, (unsigned long long*)meta,
                mode == 2 ? nullptr : (uint32_t*)b.perm);
     hipLaunchKernelGGL(sx_scan_kernel, dim3(R_), dim3(1024), 0, cs, hist_, in.G, R_, K, b.send, rq, tab_off,

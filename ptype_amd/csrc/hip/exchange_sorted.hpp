@@ -90,7 +90,8 @@ class SortedExchange {
   void send(const SxSend& a);
   const SxWire& last_wire() const { return wire_; }
   int64_t sends() const { return sends_; }
-  std::vector<uint64_t> stats() const;  // receiver counters: handler failures, replies wider than agreed
+  // receiver counters: handler failures, replies wider than agreed; sender: one-pass look-backs that gave up (0)
+  std::vector<uint64_t> stats() const;
 
  private:
   struct Bufs {
@@ -112,6 +113,9 @@ class SortedExchange {
   Bufs bufs_[kSxMaxChunks];
   uint32_t* hist_ = nullptr;  // [G][R * K] per-block bucket counts -> prefixes (K = 64 or 1)
   uint32_t* boff_ = nullptr;  // [R * K] bucket offsets within their region
+  unsigned long long* desc_ = nullptr;  // [tiles][R] one-pass look-back descriptors (rank-only batches)
+  unsigned* tctr_ = nullptr;    // [0] one-pass tile counter (self-resetting), [1] its epoch tag
+  unsigned* ticket_ = nullptr;  // last-block ticket of the one-pass kernel (self-resetting)
   uint64_t* meta_dev_ = nullptr;   // [2][kMetaWords] agreement vectors (device)
   uint64_t* meta_host_ = nullptr;  // [2][kMetaWords] pinned copies
   unsigned long long* stats_ = nullptr;  // [2] receiver counters

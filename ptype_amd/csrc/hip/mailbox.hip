@@ -776,6 +776,8 @@ Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) 
   PT_HIP_CHECK(hipMemsetAsync(sort_gsum_, 0, (size_t)kMboxSortGroups * shards * sizeof(uint32_t), stream_));
   PT_HIP_CHECK(hipMalloc((void**)&sort_ticket_, kTicketWords * sizeof(unsigned)));
   PT_HIP_CHECK(hipMemsetAsync(sort_ticket_, 0, kTicketWords * sizeof(unsigned), stream_));
+  PT_HIP_CHECK(hipMalloc((void**)&sort_tctr_, 2 * sizeof(unsigned)));
+  PT_HIP_CHECK(hipMemsetAsync(sort_tctr_, 0, 2 * sizeof(unsigned), stream_));
   bytes_ += (size_t)kMboxSortHistWords * sizeof(uint32_t) + (size_t)kMboxSortGroups * shards * sizeof(uint32_t);
   PT_HIP_CHECK(hipMalloc((void**)&mv_.stats, kMbStripes * kMbStatWords * 8));
   PT_HIP_CHECK(hipMemsetAsync(mv_.stats, 0, kMbStripes * kMbStatWords * 8, stream_));
@@ -800,7 +802,7 @@ Mailboxes::~Mailboxes() {
   (void)hipFree(mv_.ctr);
   (void)hipFree(mv_.stats);
   for (void* p : {(void*)sort_hist_, (void*)sort_gsum_, (void*)sort_ticket_, (void*)sort_rw_, (void*)sort_sidx_,
-                  (void*)sort_tinfo_, stage_rep_})
+                  (void*)sort_tinfo_, (void*)sort_desc_, (void*)sort_tctr_, stage_rep_})
     if (p) (void)hipFree(p);
   if (ctrl_) (void)hipHostFree(ctrl_);
 }

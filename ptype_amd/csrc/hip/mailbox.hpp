@@ -69,6 +69,7 @@ enum MboxStat : int {
   kMbSerial = 6,     // records run serialised (same actor twice in a window)
   kMbSpilled = 7,    // stateless messages whose ring was full, run from the batch by the drain
   kMbTicket = 8,     // reserved (the epoch drain's tickets are per shard: kMboxCtrTicket)
+  kMbLookback = 9,   // one-pass sort: look-backs that gave up waiting (a bug guard; must stay 0)
   kMbStatWords = 16,
 };
 constexpr int kMbStripes = 32;  // stats copies (block-striped atomics; stats() sums them)
@@ -205,6 +206,8 @@ class Mailboxes {
   uint32_t* sort_rw_ = nullptr;     // [M] each message's mailbox (route word), count -> scatter
   uint32_t* sort_sidx_ = nullptr;   // [M] each message's ring slot (message-order drain; spilled tiles)
   uint32_t* sort_tinfo_ = nullptr;  // [tiles][2][S] each tile's runs: slot bias, count (ring-order drain / completion)
+  unsigned long long* sort_desc_ = nullptr;  // [tiles][S] one-pass sort: per-tile shard counts / prefixes (look-back)
+  unsigned* sort_tctr_ = nullptr;   // [0] one-pass sort's tile counter (self-resetting), [1] its epoch tag
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
   // ordered drain: replies staged at ring slots [S * Q], one 16-B word each
   // (value lo, value hi, status, 0) -- one gather per message in the completion

@@ -270,6 +270,168 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
   }
 }
 
+// ---------------------------------------------------------------- K2s one pass: resolve + look-back + scatter
+// The count and scatter passes as ONE kernel (a single-pass counting sort with
+// decoupled look-back): each block claims the next tile in launch order (a tile
+// counter, so every earlier tile's block is already running), resolves its
+// messages through the route directory ONCE (the gather is the expensive part:
+// 8 Mi random 4-B lookups cost ~27 us of L2 request rate on MI355X,
+// tools/gather_probe.hip), ranks them per shard in message order (wave match),
+// publishes its per-shard counts, and finds its offset in each shard's epoch run
+// by looking back over earlier tiles' descriptors until one carries an
+// inclusive prefix.  Descriptors are u64 {epoch tag 24 | status 2 | value 38},
+// published and read with memory-side atomics (the per-XCD L2s are not coherent
+// within a kernel); the tag (from a device word the drain advances) makes a
+// previous Send's descriptors invalid without clearing them, graph replays
+// included.  The last tile leaves each shard's epoch total in gsum[0][s] for the
+// drains' commit.  The batch's inputs are read once and the route words never
+// leave registers (the two-pass form wrote and re-read 4 B per message).
+__host__ __device__ constexpr size_t onesweep_lds_bytes(uint32_t S) { return (size_t)S * (8 + 4 + 4 + 4 * (kST / kWave)); }
+
+template <int MODE, bool A2, bool MC>
+__global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
+                                                           unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
+                                                           uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
+                                                           uint32_t* __restrict__ rw, ReplyView rv, bool spill,
+                                                           bool all_sidx) {
+  extern __shared__ __align__(16) unsigned char smem_os[];
+  const uint32_t S = 1u << mv.log_s;
+  unsigned long long* base = reinterpret_cast<unsigned long long*>(smem_os);  // ring position of this tile's run (tail + prefix)
+  uint32_t* room = reinterpret_cast<uint32_t*>(base + S);                     // offset limit past the tail
+  uint32_t* pre = room + S;                                                   // the tile's prefix per shard
+  uint32_t* wcnt_all = pre + S;                                               // [kST / kWave][S]
+  auto wcnt = [&](unsigned ww, uint32_t sh) -> uint32_t& { return wcnt_all[ww * S + sh]; };
+  __shared__ uint32_t tile_s;
+  const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  const uint32_t tag = (tctr[1] & 0xffffffu) + 1u;  // this Send's epoch tag (the drain advances tctr[1])
+  if (threadIdx.x == 0) {
+    const uint32_t t = atomicAdd(&tctr[0], 1u);
+    if (t == in.tiles - 1) atomicExch(&tctr[0], 0u);  // every block has claimed: ready for the next Send
+    tile_s = t;
+  }
+  for (uint32_t s = lane; s < S; s += kWave) wcnt(w, s) = 0;
+  __syncthreads();
+  const uint32_t t = tile_s;
+  // the tile's columns: actors, then the arguments in flight across the gathers and the ranking
+  uint32_t a[kSK], mb[kSK], meth[kSK];
+  int64_t v0[kSK], v1[kSK], v2[kSK];
+  int r[kSK];
+  load_actors(in, t, a);
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    const int64_t i = tile_index(t, k);
+    const bool ok = i < in.M;
+    v0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
+    v1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    v2[k] = 0;
+    if constexpr (A2) v2[k] = ok ? __builtin_nontemporal_load(in.a2 + i) : 0;
+    meth[k] = in.method_uniform;
+    if constexpr (MC) meth[k] = ok ? (uint32_t)in.mcol[i] : 0u;
+  }
+  resolve_k<MODE>(in, a, r, mb);
+  uint32_t wr[kSK];
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    const bool ok = tile_index(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
+    if (!ok) mb[k] = kNoSlot;
+    const uint32_t sh = mb[k] & (S - 1);
+    const uint64_t peers = match_bits(sh, mv.log_s, __ballot(ok));
+    const unsigned below = mbcnt64(peers);
+    const int leader = peers ? __builtin_ctzll(peers) : 0;
+    unsigned old = 0;
+    if (ok && below == 0) {
+      old = wcnt(w, sh);
+      wcnt(w, sh) = old + (unsigned)__popcll(peers);
+    }
+    wr[k] = (unsigned)__shfl((int)old, leader) + below;
+  }
+  __syncthreads();
+  // per shard: wave offsets within the tile, publish the tile's count, look back for its prefix
+  const uint64_t Q = 1ull << mv.log_q;
+  unsigned long long timeouts = 0;
+  int sp = 0;
+  for (uint32_t s = threadIdx.x; s < S; s += kST) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int ww = 0; ww < kST / kWave; ++ww) {
+      const uint32_t x = wcnt(ww, s);
+      wcnt(ww, s) = c;
+      c += x;
+    }
+    unsigned long long* d = desc + (size_t)t * S + s;
+    uint64_t excl = 0;
+    if (t == 0) {
+      __hip_atomic_exchange(d, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_exchange(d, desc_word(tag, kDescA, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      excl = lookback(desc + s, S, (int64_t)t - 1, tag, timeouts);
+      __hip_atomic_exchange(d, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t == in.tiles - 1) gsum[s] = (uint32_t)(excl + c);  // the epoch's total of shard s
+    const uint64_t tl = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
+    const uint64_t free = hd + Q > tl ? hd + Q - tl : 0;
+    const uint32_t rm = (uint32_t)(free < 0xffffffffull ? free : 0xffffffffull);
+    base[s] = tl;
+    room[s] = rm;
+    pre[s] = (uint32_t)excl;
+    sp |= excl + c > rm;
+    if (tinfo) {
+      const uint32_t cc = excl >= rm ? 0u : (uint32_t)min((uint64_t)c, rm - excl);
+      tinfo[(size_t)t * 2 * S + s] = (uint32_t)(tl + excl) + shard_rot(mv, s);
+      tinfo[(size_t)t * 2 * S + S + s] = cc | (excl + c > rm ? kRunSpilled : 0u);
+    }
+  }
+  bool tile_spill = false;
+  if (spill) tile_spill = __syncthreads_or(sp) != 0;
+  else __syncthreads();
+  const bool wsidx = all_sidx || tile_spill;
+  unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0, n_spill = 0;
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    const int64_t i = tile_index(t, k);
+    if (i >= in.M) continue;
+    const uint32_t origin = in.origin_base + (uint32_t)i;
+    if (mb[k] == kNoSlot) {
+      ++n_miss;
+      if (wsidx) sidx[i] = kNoSlot;
+      write_status(rv, origin, kStatusNoActor);
+      continue;
+    }
+    const uint32_t sh = mb[k] & (S - 1);
+    const uint32_t off = pre[sh] + wcnt(w, sh) + wr[k];
+    if (off >= room[sh]) {  // the ring is full
+      if (spill) {  // the drain runs it from the batch: its route word is all it needs from here
+        ++n_spill;
+        sidx[i] = kSpillSlot;
+        rw[i] = mb[k];
+        continue;
+      }
+      ++n_ovf;
+      if (wsidx) sidx[i] = kNoSlot;
+      write_status(rv, origin, kStatusOverflow);
+      continue;
+    }
+    const uint64_t slot = slot_at(mv, sh, base[sh] + off);
+    if (wsidx) sidx[i] = (uint32_t)slot;
+    const uint32_t mt = meth[k];
+    if (mt < 128u && fits_i32(v0[k]) && fits_i32(v1[k]) && v2[k] == 0) {
+      *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
+          u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)v0[k], (uint32_t)v1[k]};
+    } else {
+      const uint32_t fl = v2[k] != 0 ? (uint32_t)kFlagA2 : 0u;
+      *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
+          u32x4{origin | kCompactMark, mb[k] | kCompactLong, (mt & 0xffffu) | (fl << 16), 0u};
+      *reinterpret_cast<u32x4*>(rec_b(mv, slot)) =
+          u32x4{(uint32_t)v0[k], (uint32_t)((uint64_t)v0[k] >> 32), (uint32_t)v1[k], (uint32_t)((uint64_t)v1[k] >> 32)};
+      if (fl) mv.a2[slot] = v2[k];
+    }
+    ++n_enq;
+  }
+  block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
+  __syncthreads();  // block_add_stats' LDS partials are reused
+  block_add_stats(mv.stats, n_spill, kMbSpilled, timeouts, kMbLookback, 0, -1);
+}
+
 // ---------------------------------------------------------------- compact record decode
 struct SortRec {
   uint32_t origin, mb, method, flags;
@@ -410,7 +572,7 @@ __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn 
                                                             int64_t* __restrict__ state, uint32_t n_state,
                                                             uint64_t delay_ticks, OutboxView ob, ReplyView rv,
                                                             uint32_t* __restrict__ gsum, uint32_t ngroups,
-                                                            unsigned* __restrict__ ticket) {
+                                                            unsigned* __restrict__ ticket, unsigned* __restrict__ tctr) {
   // the scatter's block -> tile ranges: a tile's records sit in ~S short runs that
   // this block's waves read whole (line reuse in L1 / L2), not one record per block
   unsigned long long done = 0, failed = 0, holes = 0;
@@ -425,6 +587,7 @@ __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn 
   if (last) {  // every block's records are read: the rings are consumed
     const uint32_t S = 1u << mv.log_s;
     for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
+    if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
   }
 }
 
@@ -486,7 +649,7 @@ __global__ __launch_bounds__(kST) void mbx_drain_ring_kernel(MboxView mv, SortIn
                                                              int64_t* __restrict__ state, uint32_t n_state,
                                                              uint64_t delay_ticks, OutboxView ob, ReplyView rv,
                                                              uint32_t* __restrict__ gsum, uint32_t ngroups,
-                                                             unsigned* __restrict__ ticket) {
+                                                             unsigned* __restrict__ ticket, unsigned* __restrict__ tctr) {
   extern __shared__ __align__(16) unsigned char smem_rd[];
   const uint32_t S = 1u << mv.log_s;
   int64_t* sval = reinterpret_cast<int64_t*>(smem_rd);  // [kSTile] reply values by place in the tile
@@ -558,8 +721,10 @@ __global__ __launch_bounds__(kST) void mbx_drain_ring_kernel(MboxView mv, SortIn
   __shared__ bool last;
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
   __syncthreads();
-  if (last)  // every block's records are read: the rings are consumed
+  if (last) {  // every block's records are read: the rings are consumed
     for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
+    if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
+  }
 }
 
 // ---------------------------------------------------------------- arrival rings (fixed positions)
@@ -875,8 +1040,10 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
 // messages were answered by the scatter and have no run entry.
 __global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxView mv,
                                                                 const uint32_t* __restrict__ tinfo,
-                                                                const u32x4* __restrict__ srep, ReplyView rv) {
+                                                                const u32x4* __restrict__ srep, ReplyView rv,
+                                                                unsigned* __restrict__ tctr) {
   extern __shared__ __align__(16) unsigned char smem_cr[];
+  if (blockIdx.x == 0 && threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag (the sort is done)
   const uint32_t S = 1u << mv.log_s;
   int64_t* sval = reinterpret_cast<int64_t*>(smem_cr);
   RunLds L;
@@ -943,7 +1110,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       throw std::runtime_error("mailbox send: a larger batch than before inside a graph capture (warm up first)");
     PT_HIP_CHECK(hipStreamSynchronize(st));
-    for (uint32_t** p : {&sort_rw_, &sort_sidx_, &sort_tinfo_})
+    for (void** p : {(void**)&sort_rw_, (void**)&sort_sidx_, (void**)&sort_tinfo_, (void**)&sort_desc_})
       if (*p) {
         PT_HIP_CHECK(hipFree(*p));
         *p = nullptr;
@@ -951,6 +1118,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     PT_HIP_CHECK(hipMalloc((void**)&sort_rw_, (size_t)a.M * 4));
     PT_HIP_CHECK(hipMalloc((void**)&sort_sidx_, (size_t)a.M * 4));
     PT_HIP_CHECK(hipMalloc((void**)&sort_tinfo_, (size_t)tiles * 2 * S * 4));
+    // look-back descriptors: zero = no tag (every Send's tag is >= 1)
+    PT_HIP_CHECK(hipMalloc((void**)&sort_desc_, (size_t)tiles * S * 8));
+    PT_HIP_CHECK(hipMemsetAsync(sort_desc_, 0, (size_t)tiles * S * 8, st));
+    PT_HIP_CHECK(hipStreamSynchronize(st));
     sort_cap_ = (uint64_t)a.M;
   }
   if (a.ordered && !stage_rep_) {
@@ -991,7 +1162,9 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.tpb = (uint32_t)((tiles + G - 1) / G);
   // one block per tile (tile-granular kernels), dealt XCD by XCD: a multiple of 8
   const uint32_t tile_grid = (uint32_t)(tiles >= 8 ? (tiles + 7) / 8 * 8 : tiles);
-  const uint32_t ngroups = (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks);
+  // the sort: one pass with look-back (default), or count + scatter (PTYPE_MBOX_SORT=twopass)
+  static const bool two_pass = getenv("PTYPE_MBOX_SORT") && std::string(getenv("PTYPE_MBOX_SORT")) == "twopass";
+  const uint32_t ngroups = two_pass ? (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks) : 1u;
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
   const ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
   OutboxView ob;
@@ -1036,23 +1209,41 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     return;
   }
 
-#define PT_COUNT(MO) \
-  hipLaunchKernelGGL((mbx_count_kernel<MO>), dim3(in.G), dim3(kST), 0, st, in, mv_.log_s, sort_hist_, sort_gsum_, sort_rw_)
-  if (mode == 2) PT_COUNT(2); else if (mode == 1) PT_COUNT(1); else PT_COUNT(0);
-#undef PT_COUNT
-  PT_HIP_CHECK(hipGetLastError());
   // the stateless drain: ring order (default) or message order (PTYPE_MBOX_DRAIN=msg: every slot index written)
   static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
   const bool all_sidx = msg_drain && !a.ordered;
+  uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
+  if (two_pass) {
+#define PT_COUNT(MO) \
+  hipLaunchKernelGGL((mbx_count_kernel<MO>), dim3(in.G), dim3(kST), 0, st, in, mv_.log_s, sort_hist_, sort_gsum_, sort_rw_)
+    if (mode == 2) PT_COUNT(2); else if (mode == 1) PT_COUNT(1); else PT_COUNT(0);
+#undef PT_COUNT
+    PT_HIP_CHECK(hipGetLastError());
 #define PT_SCAT(A2, MC)                                                                                           \
   hipLaunchKernelGGL((mbx_scatter_kernel<A2, MC>), dim3(in.G), dim3(kST), scatter_lds_bytes(S), st, in, mv_,     \
                      (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_, sort_sidx_, \
-                     all_sidx ? nullptr : sort_tinfo_, rv, !a.ordered, all_sidx)
-  if (a.a2 && a.method_col) PT_SCAT(true, true);
-  else if (a.a2) PT_SCAT(true, false);
-  else if (a.method_col) PT_SCAT(false, true);
-  else PT_SCAT(false, false);
+                     tinfo, rv, !a.ordered, all_sidx)
+    if (a.a2 && a.method_col) PT_SCAT(true, true);
+    else if (a.a2) PT_SCAT(true, false);
+    else if (a.method_col) PT_SCAT(false, true);
+    else PT_SCAT(false, false);
 #undef PT_SCAT
+  } else {
+    // one block per tile, claimed in launch order (the grid is exactly the tile count)
+#define PT_OS1(MO, A2, MC)                                                                                         \
+  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(S), st, in, \
+                     mv_, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx)
+#define PT_OS(MO)                                   \
+  do {                                              \
+    if (a.a2 && a.method_col) PT_OS1(MO, true, true); \
+    else if (a.a2) PT_OS1(MO, true, false);         \
+    else if (a.method_col) PT_OS1(MO, false, true); \
+    else PT_OS1(MO, false, false);                  \
+  } while (0)
+    if (mode == 2) PT_OS(2); else if (mode == 1) PT_OS(1); else PT_OS(0);
+#undef PT_OS
+#undef PT_OS1
+  }
   PT_HIP_CHECK(hipGetLastError());
   const size_t ring_lds = ring_drain_lds_bytes(S);
   if (a.ordered) {
@@ -1067,12 +1258,12 @@ void Mailboxes::send_sorted(const MboxSend& a) {
                        (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);
     PT_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST), ring_lds, st, in, mv_,
-                       (const uint32_t*)sort_tinfo_, (const u32x4*)stage_rep_, rv);
+                       (const uint32_t*)sort_tinfo_, (const u32x4*)stage_rep_, rv, sort_tctr_);
   } else if (msg_drain) {
 #define PT_DMSG(FX)                                                                                              \
   hipLaunchKernelGGL((mbx_drain_msg_kernel<FX>), dim3(in.G), dim3(kST), 0, st, mv_, in, (const uint32_t*)sort_sidx_, \
                      (const uint32_t*)sort_rw_, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_,  \
-                     ngroups, sort_ticket_)
+                     ngroups, sort_ticket_, sort_tctr_)
     if (fixed_mul) PT_DMSG(kCalculatorMultiply);
     else PT_DMSG(0);
 #undef PT_DMSG
@@ -1080,7 +1271,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #define PT_DRING(FX)                                                                                            \
   hipLaunchKernelGGL((mbx_drain_ring_kernel<FX>), dim3(tile_grid), dim3(kST), ring_lds, st, mv_, in,            \
                      (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_,       \
-                     (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_)
+                     (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_, \
+                     sort_tctr_)
     if (fixed_mul) PT_DRING(kCalculatorMultiply);
     else PT_DRING(0);
 #undef PT_DRING

@@ -203,7 +203,7 @@ constexpr unsigned kCapCopies = 16;  // block b adds into copy b % 16 (same-addr
 constexpr size_t kCapFoldWords = kCapCopies * kMaxCapCols + kTicketWords;
 
 // Block-wide reduction of every thread's accumulator into meta[] (atomic max).
-// Every thread of the (256-thread) block must call it.  A block only issues the
+// Every thread of the block (up to 1024 threads) must call it.  A block only issues the
 // atomic when its value beats what meta[] already holds (a relaxed read, at worst
 // stale-low, i.e. one unneeded atomic): thousands of blocks hitting the same 16
 // words with atomics serialise at L2, and on random data the maxima settle after
@@ -226,8 +226,8 @@ __device__ __forceinline__ void meta_publish(MetaAcc acc, bool has_mcol, uint32_
     t = __shfl_xor(acc.mm, off), acc.mm = t > acc.mm ? t : acc.mm;
     acc.flags |= __shfl_xor(acc.flags, off);
   }
-  __shared__ uint64_t part[256 / 64][6];
-  const int w = threadIdx.x / 64;
+  __shared__ uint64_t part[1024 / 64][6];  // (sized for 256 threads once: 512-thread blocks overran it)
+  const int w = threadIdx.x / 64, nw = (int)(blockDim.x / 64);
   if ((threadIdx.x & 63) == 0) {
     part[w][0] = acc.mb, part[w][1] = acc.z0, part[w][2] = acc.z1, part[w][3] = acc.z2, part[w][4] = acc.mm,
     part[w][5] = acc.flags;
@@ -235,11 +235,11 @@ __device__ __forceinline__ void meta_publish(MetaAcc acc, bool has_mcol, uint32_
   __syncthreads();
   if (threadIdx.x < 5) {  // words 0..3 = mailbox, a0..a2; thread 4 -> kMetaMethod
     uint64_t v = 0;
-    for (int k = 0; k < 256 / 64; ++k) v = part[k][threadIdx.x] > v ? part[k][threadIdx.x] : v;
+    for (int k = 0; k < nw; ++k) v = part[k][threadIdx.x] > v ? part[k][threadIdx.x] : v;
     if (v) meta_max(meta + (threadIdx.x == 4 ? (int)kMetaMethod : (int)threadIdx.x), v);
   } else if (threadIdx.x == 5) {
     uint32_t f = 0;
-    for (int k = 0; k < 256 / 64; ++k) f |= (uint32_t)part[k][5];
+    for (int k = 0; k < nw; ++k) f |= (uint32_t)part[k][5];
     if (M > 0 && blockIdx.x == 0) {
       if (has_mcol) {
         meta_max(meta + kMetaMcol, 1);

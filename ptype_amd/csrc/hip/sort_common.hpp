@@ -134,4 +134,58 @@ __device__ __forceinline__ void load_args(const SortIn& in, uint32_t t, SortTile
 
 __device__ __forceinline__ bool fits_i32(int64_t v) { return v == (int64_t)(int32_t)v; }
 
+// ---------------------------------------------------------------- one-pass sorts: decoupled look-back
+// Per (tile, bucket) descriptors, u64 {epoch tag 24 | status 2 | value 38}, published
+// with memory-side atomic exchanges and read with memory-side no-op atomics: the
+// per-XCD L2s are not coherent within a kernel, so a plain or sc1 poll could keep
+// reading a stale line (mailbox_dev.hpp ld_fresh).  The tag comes from a device
+// word advanced once per Send, so earlier Sends' descriptors (and graph replays')
+// read as unpublished without any clearing.  Users: mailbox_sort.hip
+// mbx_onesweep_kernel, exchange_sorted.hip sx_onesweep_kernel.
+constexpr uint64_t kDescA = 1ull << 38, kDescP = 2ull << 38, kDescVal = (1ull << 38) - 1;
+__device__ __forceinline__ uint64_t desc_word(uint32_t tag, uint64_t status, uint64_t v) {
+  return ((uint64_t)tag << 40) | status | v;
+}
+constexpr uint32_t kLookbackSpins = 1u << 20;  // a bug guard (a lost descriptor must not hang the GPU)
+
+// Sum of the descriptors of tiles q, q-1, ... (stride `stride` words apart, this
+// column's) back to the first inclusive prefix: a window of kLbWin predecessors
+// is read at once (memory-side atomics in flight together -- one round trip per
+// window instead of one per tile); an unpublished entry is re-polled.
+constexpr int kLbWin = 8;
+__device__ __forceinline__ uint64_t lookback(unsigned long long* col, uint32_t stride, int64_t q, uint32_t tag,
+                                             unsigned long long& timeouts) {
+  uint64_t excl = 0;
+  uint32_t spins = 0;
+  while (q >= 0) {
+    uint64_t x[kLbWin];
+#pragma unroll
+    for (int j = 0; j < kLbWin; ++j)
+      x[j] = q - j >= 0 ? __hip_atomic_fetch_add(col + (size_t)(q - j) * stride, 0ull, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                        : desc_word(tag, kDescP, 0);  // before tile 0: 0
+    int j = 0;
+    bool done = false;
+    for (; j < kLbWin; ++j) {
+      if ((uint32_t)(x[j] >> 40) != tag) break;  // not published yet: poll it again
+      excl += x[j] & kDescVal;
+      if (x[j] & kDescP) {
+        done = true;
+        break;
+      }
+    }
+    if (done) break;
+    q -= j;
+    if (j < kLbWin) {
+      if (++spins > kLookbackSpins) {
+        ++timeouts;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return excl;
+}
+
+
 }  // namespace ptype

@@ -31,7 +31,8 @@ from . import _ptr, hip, raw_stream
 from .batch import MsgBatch, _handler_ref, fold_step
 from .records import STATUS_NO_ACTOR, STATUS_OK, method_ordered
 
-STAT_NAMES = ("enqueued", "overflow", "no_actor", "processed", "failed", "holes", "serialised", "spilled")
+STAT_NAMES = ("enqueued", "overflow", "no_actor", "processed", "failed", "holes", "serialised", "spilled", "reserved",
+              "lookback_timeouts")
 SORT_MAX_SHARDS = 1024  # csrc/hip/mailbox.hpp kMboxSortMaxShards
 
 

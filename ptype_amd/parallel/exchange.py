@@ -749,8 +749,12 @@ class ActorExchange:
             f = self._sorted.stats()
             s.failed += int(f[0])
             s.toowide += int(f[1])
+            if len(f) > 2 and f[2]:
+                raise RuntimeError("sorted exchange: one-pass look-back stalled: results are invalid")
         if self.mailboxes is not None:
             m = self.mailboxes.stats()
+            if m.get("lookback_timeouts"):
+                raise RuntimeError("mailbox sort: one-pass look-back stalled: results are invalid")
             s.nomatch += m["no_actor"]
             s.overflow += m["overflow"]
             s.failed += m["failed"]

@@ -230,3 +230,47 @@ def test_sorted_exchange_step_captures_into_a_hipgraph():
     assert line, r.stdout[-2000:] + r.stderr[-2000:]
     out = json.loads(line[0][7:])
     assert all(out["ok"]) and out["engine"] == "sorted" and out["agreed"], out
+
+
+def test_alternate_sort_kernels_exact_in_a_subprocess():
+    """The non-default sort kernels, switched by environment (read once per
+    process): the sorted exchange's one-pass look-back sort (PTYPE_SX_SORT=onepass)
+    at R = 4, and the mailbox's two-pass count + scatter (PTYPE_MBOX_SORT=twopass)
+    with the message-order drain (PTYPE_MBOX_DRAIN=msg) -- replies exact."""
+    code = textwrap.dedent("""
+        import sys, threading, torch
+        sys.path.insert(0, sys.argv[1])
+        sys.path.insert(0, sys.argv[1] + "/tests")
+        from test_sorted_exchange_gpu import _run_ranks, _table
+        from ptype_amd.ops import batch as B
+        from ptype_amd.ops.mailbox import Mailboxes
+        from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
+        from ptype_amd.parallel.exchange import ActorExchange
+        R, n, M = 4, 8192, 120_000
+        def body(r, fc, start, s):
+            tab, _ = _table(n, R)
+            st = torch.zeros(n // R + 1, dtype=torch.int64, device="cuda")
+            ex = ActorExchange(tab, M, chunks=2, state=st, fake=(fc, r), delivery="mailbox", mailbox_ordered=False)
+            start.wait()
+            for k in range(4):
+                req = B.gen_requests(M - 911 * r, n, METHOD_CALC_MULTIPLY, seed=70 + 5 * r + k, device="cuda")
+                v, sts = ex.send(req)
+                s.synchronize()
+                assert bool((sts == STATUS_OK).all()) and torch.equal(v, req.a0 * req.a1), (r, k)
+            assert ex.stats().failed == 0
+            return True
+        assert all(_run_ranks(R, body))
+        tab, _ = _table(n, 1)
+        mb = Mailboxes("cuda", shards=64, slots=1 << 12)
+        for k in range(3):  # rings smaller than the traffic (~4.7 K messages per shard): the tail spills
+            req = B.gen_requests(300_000, n, METHOD_CALC_MULTIPLY, seed=9 + k, device="cuda")
+            v, sts = mb.send(req, tab, None)
+            torch.cuda.synchronize()
+            assert bool((sts == STATUS_OK).all()) and torch.equal(v, req.a0 * req.a1), k
+        s = mb.stats()
+        assert s["spilled"] > 0 and s["lookback_timeouts"] == 0
+        print("SUBPROCESS-OK")
+    """)
+    env = dict(os.environ, PTYPE_SX_SORT="onepass", PTYPE_MBOX_SORT="twopass", PTYPE_MBOX_DRAIN="msg")
+    p = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0 and "SUBPROCESS-OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
