@@ -288,7 +288,26 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
 // leave registers (the two-pass form wrote and re-read 4 B per message).
 __host__ __device__ constexpr size_t onesweep_lds_bytes(uint32_t S) { return (size_t)S * (8 + 4 + 4 + 4 * (kST / kWave)); }
 
-template <int MODE, bool A2, bool MC>
+template <bool A2, bool MC>
+__device__ __forceinline__ void load_cols(const SortIn& in, uint32_t t, int64_t (&v0)[kSK], int64_t (&v1)[kSK],
+                                          int64_t (&v2)[kSK], uint32_t (&meth)[kSK]) {
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    const int64_t i = tile_index(t, k);
+    const bool ok = i < in.M;
+    v0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
+    v1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    v2[k] = 0;
+    if constexpr (A2) v2[k] = ok ? __builtin_nontemporal_load(in.a2 + i) : 0;
+    meth[k] = in.method_uniform;
+    if constexpr (MC) meth[k] = ok ? (uint32_t)in.mcol[i] : 0u;
+  }
+}
+
+// LATE: the arguments are loaded after the look-back (a smaller register file
+// across it, more resident blocks; measured slower), else with the actors (in
+// flight across the gathers, the ranking and the look-back).
+template <int MODE, bool A2, bool MC, bool LATE>
 __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
                                                            unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                            uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
@@ -317,17 +336,7 @@ __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView m
   int64_t v0[kSK], v1[kSK], v2[kSK];
   int r[kSK];
   load_actors(in, t, a);
-#pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const int64_t i = tile_index(t, k);
-    const bool ok = i < in.M;
-    v0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
-    v1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
-    v2[k] = 0;
-    if constexpr (A2) v2[k] = ok ? __builtin_nontemporal_load(in.a2 + i) : 0;
-    meth[k] = in.method_uniform;
-    if constexpr (MC) meth[k] = ok ? (uint32_t)in.mcol[i] : 0u;
-  }
+  if constexpr (!LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
   resolve_k<MODE>(in, a, r, mb);
   uint32_t wr[kSK];
 #pragma unroll
@@ -385,6 +394,7 @@ __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView m
   if (spill) tile_spill = __syncthreads_or(sp) != 0;
   else __syncthreads();
   const bool wsidx = all_sidx || tile_spill;
+  if constexpr (LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
   unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0, n_spill = 0;
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
@@ -1162,8 +1172,11 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.tpb = (uint32_t)((tiles + G - 1) / G);
   // one block per tile (tile-granular kernels), dealt XCD by XCD: a multiple of 8
   const uint32_t tile_grid = (uint32_t)(tiles >= 8 ? (tiles + 7) / 8 * 8 : tiles);
-  // the sort: one pass with look-back (default), or count + scatter (PTYPE_MBOX_SORT=twopass)
-  static const bool two_pass = getenv("PTYPE_MBOX_SORT") && std::string(getenv("PTYPE_MBOX_SORT")) == "twopass";
+  // the sort: one pass with look-back, or count + scatter -- for batches under 1024 tiles (4 Mi msgs) and
+  // with PTYPE_MBOX_SORT=twopass (measured: 8 Mi msgs 0.212-0.221 vs 0.228-0.230 ms per Send; 1 Mi msgs
+  // 0.047-0.049 vs 0.043: a small grid cannot hide the look-back's round trips); PTYPE_MBOX_SORT=onepass forces it
+  static const char* sort_env = getenv("PTYPE_MBOX_SORT");
+  const bool two_pass = sort_env ? std::string(sort_env) == "twopass" : tiles < 1024;
   const uint32_t ngroups = two_pass ? (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks) : 1u;
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
   const ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
@@ -1230,9 +1243,17 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_SCAT
   } else {
     // one block per tile, claimed in launch order (the grid is exactly the tile count)
-#define PT_OS1(MO, A2, MC)                                                                                         \
-  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(S), st, in, \
-                     mv_, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx)
+    // (PTYPE_OS_LATE=1: arguments loaded after the look-back, 87 instead of 115 VGPRs -- measured slower,
+    // 0.231 vs 0.223 ms per 8 Mi Send: the loads' latency is then exposed)
+    static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
+#define PT_OS2(MO, A2, MC, LT)                                                                                     \
+  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(S), st,  \
+                     in, mv_, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx)
+#define PT_OS1(MO, A2, MC)              \
+  do {                                  \
+    if (late) PT_OS2(MO, A2, MC, true); \
+    else PT_OS2(MO, A2, MC, false);     \
+  } while (0)
 #define PT_OS(MO)                                   \
   do {                                              \
     if (a.a2 && a.method_col) PT_OS1(MO, true, true); \
@@ -1243,6 +1264,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     if (mode == 2) PT_OS(2); else if (mode == 1) PT_OS(1); else PT_OS(0);
 #undef PT_OS
 #undef PT_OS1
+#undef PT_OS2
   }
   PT_HIP_CHECK(hipGetLastError());
   const size_t ring_lds = ring_drain_lds_bytes(S);
