@@ -1222,18 +1222,38 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     return;
   }
 
+  // Stateless batches run on a COARSER view of the same rings: S' shards of
+  // Q * S / S' slots (every ring is empty between epoch Sends, so any view keeps
+  // each actor's messages in one ring, in message order; ordered batches keep the
+  // full S for the ordered drain's one block per shard).  Longer runs per tile
+  // and shard (~256 records of a 4096-message tile: whole lines for the scatter's
+  // stores and the drain's loads).  8 Mi msgs, 256 shards -> 32 / 16 / 8:
+  // 0.222 -> 0.186 / 0.179 / 0.180 ms per Send (PTYPE_MBOX_STATELESS_SHARDS,
+  // 0 = the full geometry).
+  MboxView mv = mv_;
+  uint32_t Sv = S;
+  if (!a.ordered) {
+    static const int s_env =
+        getenv("PTYPE_MBOX_STATELESS_SHARDS") ? atoi(getenv("PTYPE_MBOX_STATELESS_SHARDS")) : 16;
+    if (s_env > 0 && (s_env & (s_env - 1)) == 0 && (uint32_t)s_env < S) {
+      const uint32_t k = mv.log_s - (uint32_t)__builtin_ctz((unsigned)s_env);
+      mv.log_s -= k;
+      mv.log_q += k;
+      Sv = (uint32_t)s_env;
+    }
+  }
   // the stateless drain: ring order (default) or message order (PTYPE_MBOX_DRAIN=msg: every slot index written)
   static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
   const bool all_sidx = msg_drain && !a.ordered;
   uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
   if (two_pass) {
 #define PT_COUNT(MO) \
-  hipLaunchKernelGGL((mbx_count_kernel<MO>), dim3(in.G), dim3(kST), 0, st, in, mv_.log_s, sort_hist_, sort_gsum_, sort_rw_)
+  hipLaunchKernelGGL((mbx_count_kernel<MO>), dim3(in.G), dim3(kST), 0, st, in, mv.log_s, sort_hist_, sort_gsum_, sort_rw_)
     if (mode == 2) PT_COUNT(2); else if (mode == 1) PT_COUNT(1); else PT_COUNT(0);
 #undef PT_COUNT
     PT_HIP_CHECK(hipGetLastError());
 #define PT_SCAT(A2, MC)                                                                                           \
-  hipLaunchKernelGGL((mbx_scatter_kernel<A2, MC>), dim3(in.G), dim3(kST), scatter_lds_bytes(S), st, in, mv_,     \
+  hipLaunchKernelGGL((mbx_scatter_kernel<A2, MC>), dim3(in.G), dim3(kST), scatter_lds_bytes(Sv), st, in, mv,     \
                      (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_, sort_sidx_, \
                      tinfo, rv, !a.ordered, all_sidx)
     if (a.a2 && a.method_col) PT_SCAT(true, true);
@@ -1247,8 +1267,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     // 0.231 vs 0.223 ms per 8 Mi Send: the loads' latency is then exposed)
     static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
 #define PT_OS2(MO, A2, MC, LT)                                                                                     \
-  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(S), st,  \
-                     in, mv_, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx)
+  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv), st, \
+                     in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx)
 #define PT_OS1(MO, A2, MC)              \
   do {                                  \
     if (late) PT_OS2(MO, A2, MC, true); \
@@ -1267,7 +1287,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_OS2
   }
   PT_HIP_CHECK(hipGetLastError());
-  const size_t ring_lds = ring_drain_lds_bytes(S);
+  const size_t ring_lds = ring_drain_lds_bytes(Sv);
   if (a.ordered) {
     const size_t lds = sizeof(OrdLds) + (size_t)kOrdStateMax * sizeof(int64_t);
     static bool attr = false;
@@ -1276,14 +1296,14 @@ void Mailboxes::send_sorted(const MboxSend& a) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       attr = true;
     }
-    hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(S), dim3(kOrdThreads), lds, st, mv_, sort_gsum_, ngroups,
+    hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(Sv), dim3(kOrdThreads), lds, st, mv, sort_gsum_, ngroups,
                        (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);
     PT_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST), ring_lds, st, in, mv_,
+    hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST), ring_lds, st, in, mv,
                        (const uint32_t*)sort_tinfo_, (const u32x4*)stage_rep_, rv, sort_tctr_);
   } else if (msg_drain) {
 #define PT_DMSG(FX)                                                                                              \
-  hipLaunchKernelGGL((mbx_drain_msg_kernel<FX>), dim3(in.G), dim3(kST), 0, st, mv_, in, (const uint32_t*)sort_sidx_, \
+  hipLaunchKernelGGL((mbx_drain_msg_kernel<FX>), dim3(in.G), dim3(kST), 0, st, mv, in, (const uint32_t*)sort_sidx_, \
                      (const uint32_t*)sort_rw_, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_,  \
                      ngroups, sort_ticket_, sort_tctr_)
     if (fixed_mul) PT_DMSG(kCalculatorMultiply);
@@ -1291,7 +1311,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_DMSG
   } else {
 #define PT_DRING(FX)                                                                                            \
-  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX>), dim3(tile_grid), dim3(kST), ring_lds, st, mv_, in,            \
+  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX>), dim3(tile_grid), dim3(kST), ring_lds, st, mv, in,            \
                      (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_,       \
                      (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_, \
                      sort_tctr_)

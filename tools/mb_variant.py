@@ -23,7 +23,8 @@ def main():
     S = int(os.environ.get("MB_SHARDS", 256))
     dev = torch.device("cuda", 0)
     t = RegistryTable(2 * n, device=dev)
-    perm = torch.randperm(n, generator=torch.Generator().manual_seed(1))
+    affine = os.environ.get("MB_AFFINE") == "1"  # identity placement: routes computed, no directory gather
+    perm = torch.arange(n) if affine else torch.randperm(n, generator=torch.Generator().manual_seed(1))
     t.upsert(actor_keys(torch.arange(n)), torch.zeros(n, dtype=torch.int32), perm.to(torch.int32))
     t.enable_directory(n, affine_world=1)
     state = torch.zeros(n, dtype=torch.int64, device=dev)
