@@ -208,6 +208,7 @@ class Mailboxes {
   uint32_t* sort_tinfo_ = nullptr;  // [tiles][2][S] each tile's runs: slot bias, count (ring-order drain / completion)
   unsigned long long* sort_desc_ = nullptr;  // [tiles][S] one-pass sort: per-tile shard counts / prefixes (look-back)
   unsigned* sort_tctr_ = nullptr;   // [0] one-pass sort's tile counter (self-resetting), [1] its epoch tag
+  uint8_t* sort_stab_ = nullptr;    // LDS-table count: one byte per actor (shard, or not-here / probe)
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
   // ordered drain: replies staged at ring slots [S * Q], one 16-B word each
   // (value lo, value hi, status, 0) -- one gather per message in the completion

@@ -107,19 +107,119 @@ __global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_
   }
 }
 
+// Count from an LDS shard table.  What the count needs of a message is its
+// shard (mailbox & (S - 1)) and whether it is this rank's -- one byte per actor
+// -- while a route directory gather costs an L2 request per message (8 Mi
+// lookups: 40 us against 14 us for the copy of the same column,
+// tools/gather_probe.hip; from a 1-B table staged in LDS: 15 us).  So a small
+// kernel condenses the directory into a byte table (0xff: not here, 0xfe: probe
+// the hash table) and the count stages it in LDS, one 1024-thread block per CU
+// covering `sub` scatter blocks' tiles (a hist row for each); the scatter then
+// resolves its messages itself (the one gather of the Send) instead of reading
+// route words the count wrote.  Directories of up to kStabMax actors.  Opt-in
+// (PTYPE_MBOX_SORT=ldscount): the count drops to 18 us (+ 5 us for the table)
+// from 50, but the scatter's own gather is not hidden behind its streams (80 ->
+// 112 us), so 8 Mi Sends take 0.190 ms against the one-pass sort's 0.178.
+constexpr uint32_t kStabMax = 144 * 1024;
+constexpr int kCT = 1024;  // LDS-table count threads per block
+constexpr uint8_t kStabMiss = 0xff, kStabProbe = 0xfe;
+
+__global__ __launch_bounds__(256) void mbx_stab_kernel(const uint32_t* __restrict__ dir, uint32_t n_dir, int rank_self,
+                                                       uint32_t log_s, uint8_t* __restrict__ stab) {
+  const uint32_t i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n_dir) return;
+  uint8_t b[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t w = i + k < n_dir ? dir[i + k] : kDirMissing;
+    const uint32_t mb = w >> 8;
+    b[k] = w == kDirFallback ? kStabProbe
+           : (w == kDirMissing || (int)(w & 0xff) != rank_self || mb >= kMaxMbox) ? kStabMiss
+                                                                                 : (uint8_t)(mb & ((1u << log_s) - 1));
+  }
+  if (i + 3 < n_dir) {
+    *reinterpret_cast<uint32_t*>(stab + i) = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) |
+                                             ((uint32_t)b[3] << 24);
+  } else {
+    for (int k = 0; k < 4 && i + k < n_dir; ++k) stab[i + k] = b[k];
+  }
+}
+
+__global__ __launch_bounds__(kCT) void mbx_count_lds_kernel(SortIn in, uint32_t log_s, const uint8_t* __restrict__ stab,
+                                                            uint32_t sub, uint32_t* __restrict__ hist,
+                                                            uint32_t* __restrict__ gsum) {
+  extern __shared__ __align__(16) unsigned char smem_cl[];
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem_cl);  // [S]
+  uint8_t* tab = smem_cl + (size_t)kMboxSortMaxShards * 4;
+  const uint32_t S = 1u << log_s, n = in.n_dir;
+  for (uint32_t j = threadIdx.x * 16; j < n; j += kCT * 16) {
+    if (j + 16 <= n) *reinterpret_cast<uint4*>(tab + j) = *reinterpret_cast<const uint4*>(stab + j);
+    else for (uint32_t k = j; k < n; ++k) tab[k] = stab[k];
+  }
+  constexpr int kIt = kSTile / kCT;  // messages per thread per tile (4)
+  for (uint32_t u = 0; u < sub; ++u) {
+    const uint32_t v = blockIdx.x * sub + u;  // the scatter block whose hist row this is
+    for (uint32_t s = threadIdx.x; s < S; s += kCT) cnt[s] = 0;
+    __syncthreads();
+    if (v < in.G) {
+      const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
+      for (uint32_t t = t0; t < t1; ++t) {
+        uint32_t a[kIt];
+#pragma unroll
+        for (int k = 0; k < kIt; ++k) {
+          const int64_t i = (int64_t)t * kSTile + k * kCT + threadIdx.x;
+          a[k] = i < in.M ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
+        }
+#pragma unroll
+        for (int k = 0; k < kIt; ++k) {
+          uint32_t sh = a[k] < n ? tab[a[k]] : (a[k] == 0xffffffffu ? kStabMiss : kStabProbe);
+          if (sh == kStabProbe) {  // not in the directory: the hash table decides
+            int r = -1;
+            uint32_t mb = 0;
+            lookup_entry(in.table, in.mask, actor_key(a[k]), r, mb);
+            sh = (r == in.rank_self && mb < kMaxMbox) ? (mb & (S - 1)) : kStabMiss;
+          }
+          if (sh != kStabMiss) atomicAdd(&cnt[sh], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    if (v < in.G) {
+      uint32_t* g = gsum + (size_t)(v / kGroupBlocks) * S;
+      for (uint32_t s = threadIdx.x; s < S; s += kCT) {
+        const uint32_t c = cnt[s];
+        hist[(size_t)v * S + s] = c;
+        if (c) atomicAdd(&g[s], c);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------- K2s pass 2: scatter
 // The tile's arguments are loaded with its route words, before the ranking (in
 // flight across it).  Loading them only once the ranks are known (a smaller
 // register file, occupancy 4 -> 5) measured slower: 124 -> 164 us per 8 Mi.
-template <bool A2, bool MC>
+// RMODE < 0: the count's route words; else the scatter resolves each message
+// itself (registry mode RMODE) -- after the LDS-table count, which writes none.
+template <bool A2, bool MC, int RMODE = -1>
 __device__ __forceinline__ void load_routed(const SortIn& in, const uint32_t* __restrict__ rw, uint32_t t,
                                             uint32_t (&m)[kSK], int64_t (&x0)[kSK], int64_t (&x1)[kSK],
                                             int64_t (&x2)[kSK], uint32_t (&meth)[kSK]) {
+  if constexpr (RMODE >= 0) {
+    uint32_t a[kSK];
+    int r[kSK];
+    load_actors(in, t, a);
+    resolve_k<RMODE>(in, a, r, m);
+#pragma unroll
+    for (int k = 0; k < kSK; ++k)
+      if (!(tile_index(t, k) < in.M && r[k] == in.rank_self && m[k] < kMaxMbox)) m[k] = kNoSlot;
+  }
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     const int64_t i = tile_index(t, k);
     const bool ok = i < in.M;
-    m[k] = ok ? __builtin_nontemporal_load(rw + i) : kNoSlot;
+    if constexpr (RMODE < 0) m[k] = ok ? __builtin_nontemporal_load(rw + i) : kNoSlot;
     x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
     x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
     x2[k] = 0;
@@ -142,10 +242,10 @@ __device__ __forceinline__ void load_routed(const SortIn& in, const uint32_t* __
 // removed, see git history 4c4ea76.)
 __host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t S) { return (size_t)S * (16 + 4 * (kST / kWave)); }
 
-template <bool A2, bool MC>
+template <bool A2, bool MC, int RMODE = -1>
 __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv, const uint32_t* __restrict__ hist,
                                                           const uint32_t* __restrict__ gsum,
-                                                          const uint32_t* __restrict__ rw,
+                                                          uint32_t* __restrict__ rw,
                                                           uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
                                                           ReplyView rv, bool spill, bool all_sidx) {
   // LDS sized by the shard count (16 + 4 * waves B per shard): occupancy is not
@@ -178,7 +278,7 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
     for (uint32_t s = lane; s < S; s += kWave) wcnt(w, s) = 0;  // this wave's row only
     uint32_t mb[kSK], meth[kSK];
     int64_t v0[kSK], v1[kSK], v2[kSK];
-    load_routed<A2, MC>(in, rw, t, mb, v0, v1, v2, meth);
+    load_routed<A2, MC, RMODE>(in, rw, t, mb, v0, v1, v2, meth);
     // rank of each message among this wave's earlier messages of its shard
     uint32_t wr[kSK], sh[kSK];
 #pragma unroll
@@ -228,6 +328,7 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
         if (spill) {  // stateless batch: the drain runs it from the batch
           ++n_spill;
           sidx[i] = kSpillSlot;
+          if constexpr (RMODE >= 0) rw[i] = mb[k];  // (else the count wrote it)
           continue;
         }
         ++n_ovf;  // answered now, re-sent by send_all
@@ -1176,7 +1277,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // with PTYPE_MBOX_SORT=twopass (measured: 8 Mi msgs 0.212-0.221 vs 0.228-0.230 ms per Send; 1 Mi msgs
   // 0.047-0.049 vs 0.043: a small grid cannot hide the look-back's round trips); PTYPE_MBOX_SORT=onepass forces it
   static const char* sort_env = getenv("PTYPE_MBOX_SORT");
-  const bool two_pass = sort_env ? std::string(sort_env) == "twopass" : tiles < 1024;
+  static const std::string sort_sel = sort_env ? sort_env : "";
+  bool two_pass = !sort_sel.empty() ? (sort_sel == "twopass" || sort_sel == "ldscount") : tiles < 1024;
   const uint32_t ngroups = two_pass ? (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks) : 1u;
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
   const ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
@@ -1246,7 +1348,39 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
   const bool all_sidx = msg_drain && !a.ordered;
   uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
-  if (two_pass) {
+  // the LDS-table count (PTYPE_MBOX_SORT=ldscount): directory registry, table <= kStabMax, shards <= 128
+  const bool lds_count = two_pass && sort_sel == "ldscount" && mode == 1 && a.n_dir <= kStabMax && Sv <= 128;
+  if (lds_count) {
+    if (!sort_stab_) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        throw std::runtime_error("mailbox send: first LDS-count Send inside a graph capture (warm up first)");
+      PT_HIP_CHECK(hipMalloc((void**)&sort_stab_, kStabMax + 16));
+    }
+    hipLaunchKernelGGL(mbx_stab_kernel, dim3((a.n_dir + 1023) / 1024), dim3(256), 0, st, (const uint32_t*)a.dir,
+                       a.n_dir, a.rank_self, mv.log_s, sort_stab_);
+    static bool attr = false;
+    const size_t lds = (size_t)kMboxSortMaxShards * 4 + kStabMax;
+    if (!attr) {
+      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_count_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+      attr = true;
+    }
+    const uint32_t sub = (in.G + 255) / 256;  // scatter blocks per count block (about one count block per CU)
+    hipLaunchKernelGGL(mbx_count_lds_kernel, dim3((in.G + sub - 1) / sub), dim3(kCT),
+                       (size_t)kMboxSortMaxShards * 4 + a.n_dir, st, in, mv.log_s, (const uint8_t*)sort_stab_, sub,
+                       sort_hist_, sort_gsum_);
+    PT_HIP_CHECK(hipGetLastError());
+#define PT_SCAT(A2, MC)                                                                                           \
+  hipLaunchKernelGGL((mbx_scatter_kernel<A2, MC, 1>), dim3(in.G), dim3(kST), scatter_lds_bytes(Sv), st, in, mv,  \
+                     (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, sort_rw_, sort_sidx_, tinfo, rv,      \
+                     !a.ordered, all_sidx)
+    if (a.a2 && a.method_col) PT_SCAT(true, true);
+    else if (a.a2) PT_SCAT(true, false);
+    else if (a.method_col) PT_SCAT(false, true);
+    else PT_SCAT(false, false);
+#undef PT_SCAT
+  } else if (two_pass) {
 #define PT_COUNT(MO) \
   hipLaunchKernelGGL((mbx_count_kernel<MO>), dim3(in.G), dim3(kST), 0, st, in, mv.log_s, sort_hist_, sort_gsum_, sort_rw_)
     if (mode == 2) PT_COUNT(2); else if (mode == 1) PT_COUNT(1); else PT_COUNT(0);
@@ -1254,8 +1388,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     PT_HIP_CHECK(hipGetLastError());
 #define PT_SCAT(A2, MC)                                                                                           \
   hipLaunchKernelGGL((mbx_scatter_kernel<A2, MC>), dim3(in.G), dim3(kST), scatter_lds_bytes(Sv), st, in, mv,     \
-                     (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, (const uint32_t*)sort_rw_, sort_sidx_, \
-                     tinfo, rv, !a.ordered, all_sidx)
+                     (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, sort_rw_, sort_sidx_, tinfo, rv,      \
+                     !a.ordered, all_sidx)
     if (a.a2 && a.method_col) PT_SCAT(true, true);
     else if (a.a2) PT_SCAT(true, false);
     else if (a.method_col) PT_SCAT(false, true);

@@ -164,19 +164,22 @@ __device__ __forceinline__ uint64_t lookback(unsigned long long* col, uint32_t s
       x[j] = q - j >= 0 ? __hip_atomic_fetch_add(col + (size_t)(q - j) * stride, 0ull, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT)
                         : desc_word(tag, kDescP, 0);  // before tile 0: 0
-    int j = 0;
-    bool done = false;
-    for (; j < kLbWin; ++j) {
-      if ((uint32_t)(x[j] >> 40) != tag) break;  // not published yet: poll it again
-      excl += x[j] & kDescVal;
-      if (x[j] & kDescP) {
-        done = true;
-        break;
+    int j = 0;  // entries consumed (unrolled with flags: a register array indexed at run time spills to scratch)
+    bool done = false, stall = false;
+#pragma unroll
+    for (int k = 0; k < kLbWin; ++k) {
+      if (done || stall) continue;
+      if ((uint32_t)(x[k] >> 40) != tag) {  // not published yet: poll it again
+        stall = true;
+        continue;
       }
+      excl += x[k] & kDescVal;
+      ++j;
+      if (x[k] & kDescP) done = true;
     }
     if (done) break;
     q -= j;
-    if (j < kLbWin) {
+    if (stall) {
       if (++spins > kLookbackSpins) {
         ++timeouts;
         break;

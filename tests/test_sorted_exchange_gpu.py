@@ -232,11 +232,14 @@ def test_sorted_exchange_step_captures_into_a_hipgraph():
     assert all(out["ok"]) and out["engine"] == "sorted" and out["agreed"], out
 
 
-def test_alternate_sort_kernels_exact_in_a_subprocess():
+@pytest.mark.parametrize("mbox_sort", ["twopass", "ldscount"])
+def test_alternate_sort_kernels_exact_in_a_subprocess(mbox_sort):
     """The non-default sort kernels, switched by environment (read once per
     process): the sorted exchange's one-pass look-back sort (PTYPE_SX_SORT=onepass)
-    at R = 4, and the mailbox's two-pass count + scatter (PTYPE_MBOX_SORT=twopass)
-    with the message-order drain (PTYPE_MBOX_DRAIN=msg) -- replies exact."""
+    at R = 4, and the mailbox's two-pass count + scatter (PTYPE_MBOX_SORT=twopass;
+    ldscount: the count from an LDS shard table, the scatter resolving) with the
+    message-order drain (PTYPE_MBOX_DRAIN=msg) -- replies exact, unknown actors
+    answered STATUS_NO_ACTOR."""
     code = textwrap.dedent("""
         import sys, threading, torch
         sys.path.insert(0, sys.argv[1])
@@ -262,15 +265,18 @@ def test_alternate_sort_kernels_exact_in_a_subprocess():
         assert all(_run_ranks(R, body))
         tab, _ = _table(n, 1)
         mb = Mailboxes("cuda", shards=64, slots=1 << 12)
+        from ptype_amd.ops.records import STATUS_NO_ACTOR
         for k in range(3):  # rings smaller than the traffic (~4.7 K messages per shard): the tail spills
-            req = B.gen_requests(300_000, n, METHOD_CALC_MULTIPLY, seed=9 + k, device="cuda")
+            req = B.gen_requests(300_000, n + 64, METHOD_CALC_MULTIPLY, seed=9 + k, device="cuda")  # ids >= n: none
             v, sts = mb.send(req, tab, None)
             torch.cuda.synchronize()
-            assert bool((sts == STATUS_OK).all()) and torch.equal(v, req.a0 * req.a1), k
+            known = req.actor < n
+            assert bool((sts[known] == STATUS_OK).all()) and torch.equal(v[known], (req.a0 * req.a1)[known]), k
+            assert bool((sts[~known] == STATUS_NO_ACTOR).all()), k
         s = mb.stats()
         assert s["spilled"] > 0 and s["lookback_timeouts"] == 0
         print("SUBPROCESS-OK")
     """)
-    env = dict(os.environ, PTYPE_SX_SORT="onepass", PTYPE_MBOX_SORT="twopass", PTYPE_MBOX_DRAIN="msg")
+    env = dict(os.environ, PTYPE_SX_SORT="onepass", PTYPE_MBOX_SORT=mbox_sort, PTYPE_MBOX_DRAIN="msg")
     p = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0 and "SUBPROCESS-OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
