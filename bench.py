@@ -243,11 +243,13 @@ def main():
     pregen = args.zipf > 0 or args.pregen
     use_graph = use_gpu and not pregen and (args.graph == "on" or (args.graph == "auto" and not dist_on and fake is None))
     if args.steps_per_graph == 0:  # auto (measured at 8 Mi msgs: 1 -> 89-90, 2 -> 93.8, 4 -> 94.8 G msg/s)
-        args.steps_per_graph = next((u for u in (4, 2) if use_graph and args.steps % u == 0
-                                     and args.warmup % u == 0), 1)
+        # the timed steps replay a graph of U whole steps (U divides --steps); warm-up
+        # steps that do not fill a U-step replay run on a 1-step graph of the same
+        # step, so exactly --warmup steps warm up and exactly --steps are timed
+        args.steps_per_graph = next((u for u in (4, 2) if use_graph and args.steps % u == 0), 1)
     if args.steps_per_graph < 1 or (args.steps_per_graph > 1 and (
-            not use_graph or args.steps % args.steps_per_graph or args.warmup % args.steps_per_graph)):
-        raise SystemExit("--steps-per-graph: needs the graph path, and steps / warmup multiples of it")
+            not use_graph or args.steps % args.steps_per_graph)):
+        raise SystemExit("--steps-per-graph: needs the graph path, and --steps a multiple of it")
     pre = []
     if pregen:  # 4 distinct batches per rank, generated before any timing
         for k in range(4):
@@ -283,25 +285,33 @@ def main():
                             torch.empty(Mq, dtype=torch.int64, device=device), None, method)
             v = torch.empty(Mq, dtype=torch.int64, device=device)
             t = torch.empty(Mq, dtype=torch.int32, device=device)
-        graph = None
+        graph = graph1 = None
+        U = args.steps_per_graph
         if use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
             # seed from device memory and the graph advances it, so every replay is a new batch
-            U = args.steps_per_graph
-            seed_t = torch.tensor([rank * 0x9E3779B9 + 7 + j * 0x1000193 for j in range(U)], dtype=torch.int64,
+            seed_t = torch.tensor([rank * 0x9E3779B9 + 7 + j * 0x1000193 for j in range(U + 1)], dtype=torch.int64,
                                   device=device)
 
             def prologue(j=0):  # step j of a replay draws from seed j; the last one advances them all
                 B.gen_requests(Mq, n_actors, method, device=device, out=rq, seed_tensor=seed_t[j:j + 1])
                 if j == U - 1:
-                    seed_t.add_(U * 0x1000193)
+                    seed_t[:U].add_(U * 0x1000193)
 
-            graph = ex.capture(rq, v, t, prologue=prologue, allow_collectives=args.graph == "on",
-                               repeat=args.steps_per_graph)
+            graph = ex.capture(rq, v, t, prologue=prologue, allow_collectives=args.graph == "on", repeat=U)
+            if U > 1 and warmup % U:  # the warm-up steps a U-step replay cannot cover
+
+                def prologue1(j=0):
+                    B.gen_requests(Mq, n_actors, method, device=device, out=rq, seed_tensor=seed_t[U:U + 1])
+                    seed_t[U:U + 1].add_(0x1000193)
+
+                graph1 = ex.capture(rq, v, t, prologue=prologue1, allow_collectives=args.graph == "on", repeat=1)
 
         def step(s_):
             if graph is not None:
-                if s_ % args.steps_per_graph == 0:  # one replay runs steps_per_graph whole steps
+                if s_ < warmup and graph1 is not None:  # warm-up: one step per replay
+                    graph1.replay()
+                elif (s_ - warmup) % U == 0:  # timed: one replay runs U whole steps
                     graph.replay()
                 return
             if pre and Mq == M and method == METHOD_CALC_MULTIPLY:
