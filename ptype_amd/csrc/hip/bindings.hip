@@ -406,14 +406,14 @@ PYBIND11_MODULE(_hip, m) {
              uint32_t affine_w, int rank_self, uint32_t origin_base, uintptr_t out_val, uintptr_t out_st,
              uint64_t out_n, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
              const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, bool arrival, bool ordered,
-             int fixed_method, uintptr_t stream) {
+             int fixed_method, uintptr_t stream, int sort_mode) {
             MboxSend a;
             a.actor = actor, a.a0 = a0, a.a1 = a1, a.a2 = a2, a.method_col = method_col;
             a.method_uniform = method_uniform, a.M = M, a.table = table, a.cap = cap, a.dir = dir;
             a.n_dir = n_dir, a.affine_w = affine_w, a.rank_self = rank_self, a.origin_base = origin_base;
             a.out_val = out_val, a.out_st = out_st, a.out_n = out_n, a.state = state, a.n_state = n_state;
             a.delay_ticks = delay_ticks, a.outbox = outbox, a.outbox_cap = outbox_cap, a.arrival = arrival;
-            a.ordered = ordered, a.fixed_method = fixed_method, a.stream = stream;
+            a.ordered = ordered, a.fixed_method = fixed_method, a.stream = stream, a.sort_mode = sort_mode;
             mb.send_sorted(a);
           },
           "epoch Send through the sorted mailboxes: stable counting-sort enqueue + ordered / parallel drain",
@@ -421,7 +421,8 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"),
           py::arg("affine_w"), py::arg("rank_self"), py::arg("origin_base"), py::arg("out_val"), py::arg("out_st"),
           py::arg("out_n"), py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"),
-          py::arg("outbox_cap"), py::arg("arrival"), py::arg("ordered"), py::arg("fixed_method"), py::arg("stream"))
+          py::arg("outbox_cap"), py::arg("arrival"), py::arg("ordered"), py::arg("fixed_method"), py::arg("stream"),
+          py::arg("sort_mode") = 0)
       .def("start", &Mailboxes::start, py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"),
            py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("blocks") = 16, py::arg("idle_ms") = 0.0,
            py::arg("max_s") = 60.0)

@@ -147,6 +147,9 @@ struct MboxSend {
   bool arrival = false;  // shard by arrival tile (batches without ordered methods)
   bool ordered = true;   // ordered drain: per-actor serial, FIFO; else the parallel drain
   int fixed_method = 0;  // every message carries this method (constant-folded handler)
+  // sort kernels: 0 auto (PTYPE_MBOX_SORT, else one-pass from 1024 tiles on), 1 one-pass look-back,
+  // 2 count + scatter, 3 LDS-table count + resolving scatter
+  int sort_mode = 0;
   uintptr_t stream = 0;
 };
 

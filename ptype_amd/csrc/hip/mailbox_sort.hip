@@ -1277,8 +1277,13 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // with PTYPE_MBOX_SORT=twopass (measured: 8 Mi msgs 0.212-0.221 vs 0.228-0.230 ms per Send; 1 Mi msgs
   // 0.047-0.049 vs 0.043: a small grid cannot hide the look-back's round trips); PTYPE_MBOX_SORT=onepass forces it
   static const char* sort_env = getenv("PTYPE_MBOX_SORT");
-  static const std::string sort_sel = sort_env ? sort_env : "";
-  bool two_pass = !sort_sel.empty() ? (sort_sel == "twopass" || sort_sel == "ldscount") : tiles < 1024;
+  static const int env_mode = !sort_env ? 0
+                              : std::string(sort_env) == "onepass" ? 1
+                              : std::string(sort_env) == "twopass" ? 2
+                              : std::string(sort_env) == "ldscount" ? 3 : 0;
+  const int sort_mode = a.sort_mode ? a.sort_mode : env_mode ? env_mode : (tiles < 1024 ? 2 : 1);
+  if (sort_mode < 1 || sort_mode > 3) throw std::invalid_argument("mailbox send: sort_mode 0..3");
+  const bool two_pass = sort_mode != 1;
   const uint32_t ngroups = two_pass ? (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks) : 1u;
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
   const ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
@@ -1349,7 +1354,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   const bool all_sidx = msg_drain && !a.ordered;
   uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
   // the LDS-table count (PTYPE_MBOX_SORT=ldscount): directory registry, table <= kStabMax, shards <= 128
-  const bool lds_count = two_pass && sort_sel == "ldscount" && mode == 1 && a.n_dir <= kStabMax && Sv <= 128;
+  const bool lds_count = sort_mode == 3 && mode == 1 && a.n_dir <= kStabMax && Sv <= 128;
   if (lds_count) {
     if (!sort_stab_) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;

@@ -36,6 +36,9 @@ STAT_NAMES = ("enqueued", "overflow", "no_actor", "processed", "failed", "holes"
 SORT_MAX_SHARDS = 1024  # csrc/hip/mailbox.hpp kMboxSortMaxShards
 
 
+SORT_MODES = {"auto": 0, "onepass": 1, "twopass": 2, "ldscount": 3}
+
+
 def batch_ordered(batch: MsgBatch) -> bool:
     """Whether a batch may carry an ordered method (a method column: assume so)."""
     return method_ordered(batch.method) if isinstance(batch.method, int) else True
@@ -91,7 +94,8 @@ class Mailboxes:
 
     def send(self, batch: MsgBatch, table, state: torch.Tensor | None, out_val: torch.Tensor | None = None,
              out_status: torch.Tensor | None = None, rank_self: int = 0, delay_us: int = 0,
-             ordered: bool | None = None, outbox=None, sharding: str = "actor", sort: bool | None = None):
+             ordered: bool | None = None, outbox=None, sharding: str = "actor", sort: bool | None = None,
+             sort_mode: str = "auto"):
         """World-1 Send through the mailboxes: K2 + K3, replies in message order.
 
         ``sharding``: ``"actor"`` (every actor's messages in one ring, FIFO in
@@ -100,7 +104,9 @@ class Mailboxes:
         may carry an ordered method): drain each actor's records one at a time in
         ring order; otherwise every record runs in parallel.  ``sort`` (default on):
         the sorted epoch kernels (csrc/hip/mailbox_sort.hip: counting-sort enqueue,
-        16-B records); off: the tagged reservation kernels of mailbox.hip."""
+        16-B records); off: the tagged reservation kernels of mailbox.hip.
+        ``sort_mode`` (actor sharding): ``"auto"``, ``"onepass"`` (look-back sort),
+        ``"twopass"`` (count + scatter) or ``"ldscount"`` (LDS-table count)."""
         M = batch.M
         out_val = torch.empty(M, dtype=torch.int64, device=self.device) if out_val is None else out_val
         out_status = torch.empty(M, dtype=torch.int32, device=self.device) if out_status is None else out_status
@@ -134,7 +140,7 @@ class Mailboxes:
                             int(batch.method) if uniform else 0, M, _ptr(table.table), table.cap, _ptr(d), n_dir,
                             affine, int(rank_self), 0, _ptr(out_val), _ptr(out_status), out_val.numel(), _ptr(state),
                             0 if state is None else state.numel(), int(delay_us) * 100, ob, ob_cap, arrival, ordered,
-                            fixed, self._stream())
+                            fixed, self._stream(), SORT_MODES[sort_mode])
         return out_val, out_status
 
     # ---- persistent consumer ("tell" sessions)

@@ -486,3 +486,82 @@ def test_live_mailbox_sustained_overload_keeps_consumer_rate():
     start = torch.cumsum(k_per, 0) - k_per
     expect = torch.arange(mo.numel(), device=DEV) - start[mo[order]] + 1
     assert torch.equal(vo[order], expect)
+
+
+# ---------------------------------------------------------------- sort kernels (mailbox_sort.hip)
+@pytest.mark.parametrize("sort_mode", ["onepass", "twopass", "ldscount"])
+@pytest.mark.parametrize("M", [5000, (1 << 20) + 333])
+def test_sorted_mailbox_sort_modes_exact(sort_mode, M):
+    """Every sort kernel (one-pass look-back, count + scatter, LDS-table count)
+    fills the same per-actor rings: exact replies, misses answered, rings
+    consumed, no look-back timeout -- over Sends that reuse the rings."""
+    n = 1 << 15
+    t, _ = placed_table(n)
+    mb = Mailboxes(DEV, shards=256, slots=1 << 14)
+    g = torch.Generator().manual_seed(21)
+    for rep in range(3):
+        actor = torch.randint(0, n + 100, (M,), generator=g, dtype=torch.int32)
+        a0 = torch.randint(-(1 << 31), 1 << 31, (M,), generator=g, dtype=torch.int64)
+        a1 = torch.randint(-(1 << 20), 1 << 20, (M,), generator=g, dtype=torch.int64)
+        req = B.MsgBatch(actor.to(DEV), a0.to(DEV), a1.to(DEV), None, METHOD_CALC_MULTIPLY)
+        val, st = mb.send(req, t, None, sort_mode=sort_mode)
+        torch.cuda.synchronize()
+        known = actor < n
+        st, val = st.cpu(), val.cpu()
+        assert bool((st[known] == STATUS_OK).all()) and bool((st[~known] == STATUS_NO_ACTOR).all()), rep
+        assert torch.equal(val[known], (a0 * a1)[known]), rep
+        ctr = mb.shard_counters()
+        assert (ctr[:, 0] == ctr[:, 2]).all()
+    s = mb.stats()
+    assert s["lookback_timeouts"] == 0 and s["holes"] == 0 and s["overflow"] == 0
+
+
+def test_sorted_mailbox_onepass_ordered_fifo_and_spill():
+    """The one-pass sort on the ordered path (full shard geometry, SeqFold chains
+    audited exactly once and in message order per actor) and on a stateless
+    batch whose rings overflow (spilled tiles drained in message order)."""
+    n, M = 4096, 1 << 18
+    t, perm = placed_table(n)
+    state = torch.randint(0, 1 << 30, (n,), dtype=torch.int64, device=DEV)
+    s0 = state.cpu().clone()
+    mb = Mailboxes(DEV, shards=64, slots=1 << 14)
+    req = fold_batch(M, n, 43)
+    v, st = mb.send(req, t, state, sort_mode="onepass")
+    torch.cuda.synchronize()
+    ok, order = audit_fold(perm[req.actor.cpu().long()], req.a0.cpu(), v.cpu(), st.cpu(), s0, state.cpu())
+    assert ok, order
+    assert all(seq == sorted(seq) for seq in order.values())
+    small = Mailboxes(DEV, shards=16, slots=4096)
+    req2 = B.gen_requests(300_000, n, METHOD_CALC_MULTIPLY, seed=17, device=DEV)
+    v2, st2 = small.send(req2, t, None, sort_mode="onepass")
+    torch.cuda.synchronize()
+    assert bool((st2 == STATUS_OK).all()) and torch.equal(v2, req2.a0 * req2.a1)
+    s = small.stats()
+    assert s["spilled"] > 0 and s["lookback_timeouts"] == 0 and s["processed"] == 300_000
+
+
+def test_sorted_mailbox_onepass_graph_replays():
+    """A captured one-pass Send replayed with new batches: its look-back tag comes
+    from a device word the drain advances, so a replay never reads the previous
+    replay's descriptors as its own."""
+    n, M = 1 << 15, 1 << 19
+    t, _ = placed_table(n)
+    mb = Mailboxes(DEV, shards=256, slots=1 << 14)
+    req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=1, device=DEV)
+    val = torch.empty(M, dtype=torch.int64, device=DEV)
+    st = torch.empty(M, dtype=torch.int32, device=DEV)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        mb.send(req, t, None, val, st, sort_mode="onepass")  # warm-up: workspaces grown outside the capture
+    s.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        mb.send(req, t, None, val, st, sort_mode="onepass")
+    for k in range(4):
+        fresh = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=100 + k, device=DEV)
+        req.actor.copy_(fresh.actor), req.a0.copy_(fresh.a0), req.a1.copy_(fresh.a1)
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1), k
+    assert mb.stats()["lookback_timeouts"] == 0
