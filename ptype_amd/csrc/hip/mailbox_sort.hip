@@ -44,6 +44,7 @@
 // (example/calculator/server/server.go:16-20, :38; handler
 // example/calculator/calculator.go:9-12) -- here an explicit FIFO queue in HBM.
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "mailbox.hpp"
@@ -708,14 +709,16 @@ __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn 
 // ordered batch's overflow: never written) are left out (the scatter clamped the
 // counts).  Returns the total; `spill` is set when a run overflowed the room (a
 // stateless tile's spill).
+template <typename OwnT>
 struct RunLds {
-  uint32_t* bias;   // [S]
-  uint32_t* excl;   // [S] exclusive prefix of the (clamped) counts
-  uint16_t* owner;  // [kSTile]
+  uint32_t* bias;  // [S]
+  uint32_t* excl;  // [S] exclusive prefix of the (clamped) counts
+  OwnT* owner;     // [kSTile]: u8 for up to 256 shards, else u16
 };
 
+template <typename OwnT>
 __device__ __forceinline__ uint32_t load_tile_runs(const MboxView& mv, const uint32_t* __restrict__ tinfo, uint32_t t,
-                                                   const RunLds& L, int& spill) {
+                                                   const RunLds<OwnT>& L, int& spill) {
   __shared__ uint32_t wsum[kST / kWave];
   __shared__ uint32_t total_s;
   const uint32_t S = 1u << mv.log_s;
@@ -741,7 +744,7 @@ __device__ __forceinline__ uint32_t load_tile_runs(const MboxView& mv, const uin
   for (uint32_t s = s0, q = 0; s < s1; ++s, ++q) {
     L.excl[s] = acc;
     L.bias[s] -= acc;
-    for (uint32_t j = acc; j < acc + cnt[q]; ++j) L.owner[j] = (uint16_t)s;
+    for (uint32_t j = acc; j < acc + cnt[q]; ++j) L.owner[j] = (OwnT)s;
     acc += cnt[q];
   }
   __syncthreads();
@@ -749,12 +752,15 @@ __device__ __forceinline__ uint32_t load_tile_runs(const MboxView& mv, const uin
 }
 
 constexpr uint8_t kAbsent = 0xff;  // staged status: no record of this message in the tile's runs
+// NARROW (S <= 256): a 1-B owner table whose bytes are reused for the staged
+// statuses once the records are loaded -- 36 KB of LDS instead of 46 KB, four
+// blocks per CU (with at most 64 VGPRs: launch bounds 8 waves per SIMD)
 __host__ __device__ constexpr size_t ring_drain_lds_bytes(uint32_t S) {
-  return (size_t)kSTile * (8 + 2 + 1) + (size_t)S * 8;
+  return S <= 256 ? (size_t)kSTile * (8 + 1) + (size_t)S * 8 : (size_t)kSTile * (8 + 2 + 1) + (size_t)S * 8;
 }
 
-template <int FIXED>
-__global__ __launch_bounds__(kST) void mbx_drain_ring_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ tinfo,
+template <int FIXED, bool NARROW>
+__global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ tinfo,
                                                              const uint32_t* __restrict__ sidx,
                                                              const uint32_t* __restrict__ rw,
                                                              int64_t* __restrict__ state, uint32_t n_state,
@@ -762,20 +768,23 @@ __global__ __launch_bounds__(kST) void mbx_drain_ring_kernel(MboxView mv, SortIn
                                                              uint32_t* __restrict__ gsum, uint32_t ngroups,
                                                              unsigned* __restrict__ ticket, unsigned* __restrict__ tctr) {
   extern __shared__ __align__(16) unsigned char smem_rd[];
+  using OwnT = typename std::conditional<NARROW, uint8_t, uint16_t>::type;
   const uint32_t S = 1u << mv.log_s;
   int64_t* sval = reinterpret_cast<int64_t*>(smem_rd);  // [kSTile] reply values by place in the tile
-  RunLds L;
+  RunLds<OwnT> L;
   L.bias = reinterpret_cast<uint32_t*>(sval + kSTile);
   L.excl = L.bias + S;
-  L.owner = reinterpret_cast<uint16_t*>(L.excl + S);
-  uint8_t* sst = reinterpret_cast<uint8_t*>(L.owner + kSTile);  // [kSTile] statuses, kAbsent = none
+  L.owner = reinterpret_cast<OwnT*>(L.excl + S);
+  // [kSTile] statuses, kAbsent = none (NARROW: the owner table's bytes, once the records are loaded)
+  uint8_t* sst = NARROW ? reinterpret_cast<uint8_t*>(L.owner) : reinterpret_cast<uint8_t*>(L.owner + kSTile);
   unsigned long long done = 0, failed = 0, holes = 0;
   // tiles dealt XCD by XCD like the scatter's blocks (whose writes the XCD's L2 may still hold)
   const uint32_t t = virt_block(blockIdx.x, gridDim.x);
   if (t < in.tiles) {
     const uint64_t i0 = (uint64_t)t * kSTile;
     const uint32_t n_t = (uint32_t)min((uint64_t)kSTile, (uint64_t)in.M - i0);
-    for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
+    if constexpr (!NARROW)
+      for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
     int spill = 0;
     const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
     if (spill) {  // some message of the tile spilled: the scatter left the tile's slot indices
@@ -793,6 +802,11 @@ __global__ __launch_bounds__(kST) void mbx_drain_ring_kernel(MboxView mv, SortIn
           sl[k] = (uint32_t)(((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & sbase_mask));
           ha[k] = *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k]));
         }
+      }
+      if constexpr (NARROW) {  // every owner entry is read: its bytes become the status stage
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
+        __syncthreads();
       }
 #pragma unroll
       for (int k = 0; k < kSK; ++k) {
@@ -1157,7 +1171,7 @@ __global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxV
   if (blockIdx.x == 0 && threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag (the sort is done)
   const uint32_t S = 1u << mv.log_s;
   int64_t* sval = reinterpret_cast<int64_t*>(smem_cr);
-  RunLds L;
+  RunLds<uint16_t> L;
   L.bias = reinterpret_cast<uint32_t*>(sval + kSTile);
   L.excl = L.bias + S;
   L.owner = reinterpret_cast<uint16_t*>(L.excl + S);
@@ -1438,7 +1452,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(Sv), dim3(kOrdThreads), lds, st, mv, sort_gsum_, ngroups,
                        (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);
     PT_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST), ring_lds, st, in, mv,
+    hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST),
+                       (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, in, mv,
                        (const uint32_t*)sort_tinfo_, (const u32x4*)stage_rep_, rv, sort_tctr_);
   } else if (msg_drain) {
 #define PT_DMSG(FX)                                                                                              \
@@ -1449,14 +1464,22 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else PT_DMSG(0);
 #undef PT_DMSG
   } else {
-#define PT_DRING(FX)                                                                                            \
-  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX>), dim3(tile_grid), dim3(kST), ring_lds, st, mv, in,            \
+    static const bool narrow_ok = !(getenv("PTYPE_DRAIN_NARROW") && std::string(getenv("PTYPE_DRAIN_NARROW")) == "0");
+#define PT_DRING1(FX, NW)                                                                                       \
+  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, NW>), dim3(tile_grid), dim3(kST),                               \
+                     NW ? ring_lds : (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, mv, in,                 \
                      (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_,       \
                      (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_, \
                      sort_tctr_)
+#define PT_DRING(FX)                                   \
+  do {                                                 \
+    if (narrow_ok && Sv <= 256) PT_DRING1(FX, true);   \
+    else PT_DRING1(FX, false);                         \
+  } while (0)
     if (fixed_mul) PT_DRING(kCalculatorMultiply);
     else PT_DRING(0);
 #undef PT_DRING
+#undef PT_DRING1
   }
   PT_HIP_CHECK(hipGetLastError());
 }
