@@ -1,28 +1,35 @@
 // Sorted epoch mailboxes: K2 as a stable counting sort into the shard rings,
-// K3 as an XCD-aware parallel drain or an LDS-binned ordered drain.
+// K3 as a ring-order parallel drain or an LDS-binned ordered drain.
 //
 // The epoch form of a Send (mailbox.hpp has the ring layout) runs
 //
-//   count    each block resolves its contiguous range of the batch against the
-//            registry mirror (route directory / hash probe), keeps each
-//            message's mailbox (route word) and counts its messages per shard:
-//            hist[block][shard], plus group sums over 32 blocks (atomics);
-//   scatter  each block's prefix per shard is the group sums before its group
-//            plus the rows before it inside its group (at most 31 + 31 L2-hot
-//            rows: no scan pass); it writes every message into its shard's ring
-//            at (tail + prefix + rank), the rank computed in message order (wave
-//            match on the shard bits + per-wave counts), so each ring holds its
-//            messages in MESSAGE ORDER: every actor's mailbox is FIFO by
-//            construction, with no atomic per message; it records each
-//            message's ring slot;
-//   drain    parallel (batches without ordered methods): each record is taken
-//            from its ring slot in message order -- the replies are written
-//            coalesced (draining in ring order scattered every reply: 273 us of
-//            random stores per 8 Mi); ordered: one block owns one shard -- its
-//            actors' state staged in LDS -- and runs each actor's records one at
-//            a time in ring order, distinct actors side by side (LDS bins),
-//            replies staged at their ring slots; a completion pass gathers them
-//            into message order.
+//   sort     every message goes into its shard's ring at (tail + prefix + rank),
+//            the rank computed in message order (wave match on the shard bits +
+//            per-wave counts), so each ring holds its messages in MESSAGE ORDER:
+//            every actor's mailbox is FIFO by construction, with no atomic per
+//            message.  Two forms:
+//              one pass (batches of >= 1024 tiles): a block claims the next tile,
+//              resolves it (one route-directory gather per message), ranks it,
+//              and finds its prefix by a decoupled look-back over earlier tiles'
+//              descriptors (mbx_onesweep_kernel);
+//              count + scatter: the count resolves and histograms per block
+//              (+ group sums over 32 blocks); each scatter block's prefix is the
+//              group sums before its group plus at most 31 rows inside it (no
+//              scan pass);
+//            either records each tile's runs (slot bias + count per shard) for
+//            the drains;
+//   drain    parallel (batches without ordered methods): one block per tile reads
+//            the tile's runs in ring order (whole lines), stages the replies in
+//            LDS at their place in the tile and writes them out coalesced;
+//            ordered: one block owns one shard -- its actors' state staged in
+//            LDS -- and runs each actor's records one at a time in ring order,
+//            distinct actors side by side (LDS bins), replies staged at their
+//            ring slots; a ring-order completion puts them in message order.
+//
+// Stateless batches use a 16-shard view of the rings (every ring is empty
+// between epoch Sends): longer runs per tile and shard.  Arrival sharding
+// (stateless only) skips the sort: tile t's messages sit at fixed positions of
+// ring t mod S.
 //
 // Records are 16 B in the common case (compact form, plane A only):
 //   w0 = origin | kCompactMark    (bit 31 marks an epoch record; a live ring's
