@@ -592,7 +592,9 @@ bool Decoder::int_struct_fields(int64_t type_id, std::vector<std::string>* names
   if (it == types_.end() || it->second.kind != 1) return false;
   names->clear();
   for (const auto& f : it->second.fields) {
-    if (f.second != 2 && f.second != 7) return false;  // gob's predefined int (2) / uint (7)
+    // only gob's predefined int (kTInt = 2): the device decoders zigzag every
+    // field, which is wrong for uint (3); 7 is complex (two uints), not uint
+    if (f.second != kTInt) return false;
     names->push_back(f.first);
   }
   return !names->empty();

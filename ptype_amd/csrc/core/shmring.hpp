@@ -51,7 +51,19 @@ constexpr int kShmMaxMethods = 32;
 // each reply), so it needs no sequence taking, owners or rescue: seq + 1 in
 // req_tag publishes, `served` acknowledges.
 constexpr int kXLanes = 64;
-enum XLaneState : uint32_t { kXLaneFree = 0, kXLaneRequested = 1, kXLaneReady = 2, kXLaneFailed = 3 };
+// Lane life cycle: Free -> (caller) Requested -> (server: reply slot imported) Ready
+// -> (caller) Releasing -> (server: no request in flight, import closed) Free.
+// The caller frees its reply slot only once it reads Free again, and the server
+// closes its import only once the lane is quiet (served == req_tag: the
+// dispatcher wave has stored its last reply), so neither side unmaps memory the
+// other may still write.  A dead caller's lane takes the same server-side path.
+enum XLaneState : uint32_t {
+  kXLaneFree = 0,
+  kXLaneRequested = 1,
+  kXLaneReady = 2,
+  kXLaneFailed = 3,
+  kXLaneReleasing = 4,
+};
 struct XLaneReg {
   std::atomic<uint64_t> token;  // the caller's process token (ring_self_token); 0: free
   std::atomic<uint32_t> state;

@@ -385,6 +385,7 @@ PYBIND11_MODULE(_hip, m) {
            },
            "geometry of the last send (per peer and chunk); agreed: from the agreement of Send spec_from")
       .def("stats", &SortedExchange::stats)
+      .def_property("epoch_counter", &SortedExchange::epoch_counter, &SortedExchange::set_epoch_counter)
       .def_property_readonly("sends", &SortedExchange::sends);
   py::class_<Mailboxes>(m, "Mailboxes",
                         "HBM actor mailboxes: S shard rings of Q 32-B tagged records (K2 enqueue, K3 epoch drain, "
@@ -430,6 +431,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("running", &Mailboxes::running)
       .def("reset", &Mailboxes::reset, py::arg("stream"))
       .def("stats", &Mailboxes::stats)
+      .def_property("epoch_counter", &Mailboxes::epoch_counter, &Mailboxes::set_epoch_counter)
       .def("shard_counters", &Mailboxes::shard_counters)
       .def_property_readonly("shards", &Mailboxes::shards)
       .def_property_readonly("slots", &Mailboxes::slots)
@@ -444,12 +446,15 @@ PYBIND11_MODULE(_hip, m) {
                         "K4 on the net/rpc serving path: batched gob requests decoded on the GPU into mailbox "
                         "columns (csrc/hip/gob_bridge.hpp); pass handle() to RpcServer.register_device_batch")
       .def(py::init([](int device, Mailboxes& mb, uint32_t method, uint32_t fixed_actor, uintptr_t table,
-                       uint64_t cap, uintptr_t state, uint32_t n_state, uint64_t delay_us) {
-             return new GobBridge(device, &mb, method, fixed_actor, table, cap, state, n_state, delay_us * 100);
+                       uint64_t cap, uintptr_t state, uint32_t n_state, uint64_t delay_us, uintptr_t order_stream) {
+             return new GobBridge(device, &mb, method, fixed_actor, table, cap, state, n_state, delay_us * 100,
+                                  order_stream);
            }),
            py::arg("device"), py::arg("mailboxes"), py::arg("method"), py::arg("actor") = 0, py::arg("table"),
            py::arg("cap"), py::arg("state") = 0, py::arg("n_state") = 0, py::arg("delay_us") = 0,
-           py::keep_alive<1, 3>())
+           py::arg("order_stream") = 0, py::keep_alive<1, 3>())
+      .def("retarget", &GobBridge::retarget, py::arg("table"), py::arg("cap"), py::arg("state"), py::arg("n_state"),
+           py::call_guard<py::gil_scoped_release>())
       .def("handle", [](GobBridge& b) {
         return py::make_tuple((uintptr_t)&GobBridge::batch_c, (uintptr_t)&b);
       })

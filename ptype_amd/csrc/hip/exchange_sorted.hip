@@ -329,7 +329,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
   __shared__ uint32_t tile_s, tag_s, mbmax_s;
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
   if (threadIdx.x == 0) {
-    tag_s = (tctr[1] & 0xffffffu) + 1u;
+    tag_s = epoch_tag(tctr[1]);  // 1..0xffffff across the counter's wrap
     const uint32_t t = atomicAdd(&tctr[0], 1u);
     if (t == in.tiles - 1) atomicExch(&tctr[0], 0u);  // every block has claimed
     tile_s = t;
@@ -785,6 +785,19 @@ std::vector<uint64_t> SortedExchange::stats() const {
   unsigned long long h[3] = {0, 0, 0};
   PT_HIP_CHECK(hipMemcpy(h, stats_, sizeof h, hipMemcpyDeviceToHost));
   return {h[0], h[1], h[2]};
+}
+
+void SortedExchange::set_epoch_counter(uint32_t v) {
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipDeviceSynchronize());
+  PT_HIP_CHECK(hipMemcpy(tctr_ + 1, &v, sizeof v, hipMemcpyHostToDevice));
+}
+
+uint32_t SortedExchange::epoch_counter() const {
+  uint32_t v = 0;
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipMemcpy(&v, tctr_ + 1, sizeof v, hipMemcpyDeviceToHost));
+  return v;
 }
 
 void SortedExchange::adopt(const uint64_t* meta, int64_t from) {

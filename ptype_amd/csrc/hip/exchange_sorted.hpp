@@ -92,6 +92,9 @@ class SortedExchange {
   int64_t sends() const { return sends_; }
   // receiver counters: handler failures, replies wider than agreed; sender: one-pass look-backs that gave up (0)
   std::vector<uint64_t> stats() const;
+  // the one-pass sort's epoch counter (tests: preset near the 2^24 tag wrap); synchronous
+  void set_epoch_counter(uint32_t v);
+  uint32_t epoch_counter() const;
 
  private:
   struct Bufs {

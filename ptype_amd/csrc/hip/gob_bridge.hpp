@@ -29,11 +29,15 @@ namespace ptype {
 void launch_gob_decode(uintptr_t buf, uintptr_t offsets, int64_t M, uint32_t type_id, const std::vector<uintptr_t>& cols,
                        uintptr_t status, uintptr_t stream);
 
-// actor[i] = the actor field's column (or the fixed actor)
+// actor[i] = the actor field's column (or the fixed actor); a message that failed
+// to decode (gob status != 0) gets no actor (0xffffffff): it is answered
+// no-actor by the enqueue and never runs a handler -- the client is told
+// "decoding error", so a stateful method must not have changed state for it
 __global__ __launch_bounds__(256) void gob_bridge_actor_kernel(const int64_t* __restrict__ col, uint32_t fixed,
-                                                               int64_t n, uint32_t* __restrict__ actor) {
+                                                               const int32_t* __restrict__ gst, int64_t n,
+                                                               uint32_t* __restrict__ actor) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    actor[i] = col ? (uint32_t)col[i] : fixed;
+    actor[i] = gst[i] != 0 ? 0xffffffffu : col ? (uint32_t)col[i] : fixed;
 }
 
 class GobBridge {
@@ -42,18 +46,34 @@ class GobBridge {
 
   // mb: this process's HBM mailboxes; table: the registry mirror used for ids
   // past the directory (mailbox index = actor id below n_state: computed routes)
+  // order_stream: the runtime's stream (0: the null stream).  Each batch starts
+  // after the work queued there and that stream's later work waits for the
+  // batch, so a bridge batch and the runtime's Sends never update actor state
+  // concurrently.
   GobBridge(int device, Mailboxes* mb, uint32_t method, uint32_t fixed_actor, uintptr_t table, uint64_t cap,
-            uintptr_t state, uint32_t n_state, uint64_t delay_ticks)
+            uintptr_t state, uint32_t n_state, uint64_t delay_ticks, uintptr_t order_stream = 0)
       : device_(device), mb_(mb), method_(method), fixed_actor_(fixed_actor), table_(table), cap_(cap),
-        state_(state), n_state_(n_state), delay_ticks_(delay_ticks) {
+        state_(state), n_state_(n_state), delay_ticks_(delay_ticks), order_(as_stream(order_stream)) {
     if (!mb_) throw std::invalid_argument("GobBridge: mailboxes required");
     PT_HIP_CHECK(hipSetDevice(device_));
     PT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    PT_HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
+    PT_HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+  }
+  // After a data-plane recovery re-homed the actors (runtime._rehome): the new
+  // registry mirror and state tensor, taken at the next batch.  The handle the
+  // net/rpc server holds stays valid.
+  void retarget(uintptr_t table, uint64_t cap, uintptr_t state, uint32_t n_state) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (stream_) PT_HIP_CHECK(hipStreamSynchronize(stream_));
+    table_ = table, cap_ = cap, state_ = state, n_state_ = n_state;
   }
   ~GobBridge() {
     (void)hipSetDevice(device_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     release();
+    (void)hipEventDestroy(ev_in_);
+    (void)hipEventDestroy(ev_out_);
     if (stream_) (void)hipStreamDestroy(stream_);
   }
   GobBridge(const GobBridge&) = delete;
@@ -83,6 +103,8 @@ class GobBridge {
     PT_HIP_CHECK(hipSetDevice(device_));
     const size_t nbytes = (size_t)offsets[n];
     grow(n, nbytes);
+    PT_HIP_CHECK(hipEventRecord(ev_in_, order_));  // after the runtime's queued Sends
+    PT_HIP_CHECK(hipStreamWaitEvent(stream_, ev_in_, 0));
     memcpy(h_bytes_, bytes, nbytes);
     memcpy(h_off_, offsets, (size_t)(n + 1) * sizeof(int64_t));
     PT_HIP_CHECK(hipMemcpyAsync(d_bytes_, h_bytes_, nbytes, hipMemcpyHostToDevice, stream_));
@@ -94,7 +116,7 @@ class GobBridge {
     auto column = [&](int k) -> uintptr_t { return col[k] >= 0 && col[k] < nf ? cols[(size_t)col[k]] : 0; };
     const unsigned gx = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(gob_bridge_actor_kernel, dim3(gx), dim3(256), 0, stream_, (const int64_t*)column(3),
-                       fixed_actor_, n, d_actor_);
+                       fixed_actor_, (const int32_t*)d_gst_, n, d_actor_);
     PT_HIP_CHECK(hipGetLastError());
     MboxSend a;
     a.actor = (uintptr_t)d_actor_;
@@ -122,6 +144,8 @@ class GobBridge {
     PT_HIP_CHECK(hipMemcpyAsync(h_val_, d_val_, (size_t)n * 8, hipMemcpyDeviceToHost, stream_));
     PT_HIP_CHECK(hipMemcpyAsync(h_st_, d_st_, (size_t)n * 4, hipMemcpyDeviceToHost, stream_));
     PT_HIP_CHECK(hipMemcpyAsync(h_gst_, d_gst_, (size_t)n * 4, hipMemcpyDeviceToHost, stream_));
+    PT_HIP_CHECK(hipEventRecord(ev_out_, stream_));
+    PT_HIP_CHECK(hipStreamWaitEvent(order_, ev_out_, 0));  // the runtime's later Sends run after this batch
     PT_HIP_CHECK(hipStreamSynchronize(stream_));
     for (int64_t i = 0; i < n; ++i) {
       out[i].value = h_val_[i];
@@ -192,7 +216,9 @@ class GobBridge {
   uintptr_t state_;
   uint32_t n_state_;
   uint64_t delay_ticks_;
+  hipStream_t order_ = nullptr;
   hipStream_t stream_ = nullptr;
+  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
   std::mutex mu_;
   uint64_t cap_n_ = 0;
   size_t cap_bytes_ = 0;

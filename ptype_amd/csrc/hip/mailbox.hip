@@ -875,6 +875,19 @@ void Mailboxes::reset(uintptr_t stream) {
   PT_HIP_CHECK(hipMemsetAsync(sort_ticket_, 0, kTicketWords * sizeof(unsigned), s));
 }
 
+void Mailboxes::set_epoch_counter(uint32_t v) {
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipDeviceSynchronize());
+  PT_HIP_CHECK(hipMemcpy(sort_tctr_ + 1, &v, sizeof v, hipMemcpyHostToDevice));
+}
+
+uint32_t Mailboxes::epoch_counter() const {
+  uint32_t v = 0;
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipMemcpy(&v, sort_tctr_ + 1, sizeof v, hipMemcpyDeviceToHost));
+  return v;
+}
+
 std::vector<uint64_t> Mailboxes::stats() const {
   std::vector<uint64_t> raw((size_t)kMbStripes * kMbStatWords), v(kMbStatWords, 0);
   PT_HIP_CHECK(hipSetDevice(device_));

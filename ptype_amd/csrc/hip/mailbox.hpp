@@ -185,6 +185,9 @@ class Mailboxes {
   void reset(uintptr_t stream);  // counters and rings to empty (no consumer may be running)
 
   std::vector<uint64_t> stats() const;            // kMbStatWords device counters
+  // the one-pass sort's epoch counter (tests: preset near the 2^24 tag wrap); synchronous
+  void set_epoch_counter(uint32_t v);
+  uint32_t epoch_counter() const;
   std::vector<uint64_t> shard_counters() const;   // [tail, done, head] per shard
   uint32_t shards() const { return 1u << mv_.log_s; }
   uint32_t slots() const { return 1u << mv_.log_q; }

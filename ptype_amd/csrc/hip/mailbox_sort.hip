@@ -431,7 +431,9 @@ __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView m
   auto wcnt = [&](unsigned ww, uint32_t sh) -> uint32_t& { return wcnt_all[ww * S + sh]; };
   __shared__ uint32_t tile_s;
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
-  const uint32_t tag = (tctr[1] & 0xffffffu) + 1u;  // this Send's epoch tag (the drain advances tctr[1])
+  // this Send's epoch tag, 1..0xffffff (the drain advances tctr[1]; the modulus keeps the tag inside the
+  // descriptor's 24-bit field across the counter's wrap -- tag 0 is reserved for never-published words)
+  const uint32_t tag = epoch_tag(tctr[1]);
   if (threadIdx.x == 0) {
     const uint32_t t = atomicAdd(&tctr[0], 1u);
     if (t == in.tiles - 1) atomicExch(&tctr[0], 0u);  // every block has claimed: ready for the next Send

@@ -673,33 +673,46 @@ class DeviceServer {
   }
 
   // Requested lanes: import the caller's reply slot, reset the lane, mark it
-  // ready.  Lanes of dead callers are reclaimed.
+  // ready.  Released lanes and lanes of dead callers are reclaimed -- but an
+  // import is closed only once the lane is quiet: the dispatcher wave
+  // may have loaded rep_ptr for a request it is still running (a handler delay),
+  // and its 16-B reply store into an unmapped slot would fault this process.  A
+  // lane with a request in flight is retried at the next waker pass (the wave
+  // finishes every request it took; `served` then equals `req_tag`).
   void admit_xlanes() {
     uint32_t live = 0;
     for (int i = 0; i < kXLanes; ++i) {
       XLaneReg& g = hdr_->xregs[i];
       const uint32_t st = g.state.load(std::memory_order_acquire);
       const uint64_t tok = g.token.load(std::memory_order_acquire);
-      if (st == kXLaneFree || !tok || !ring_token_alive(tok)) {  // released, or its caller is gone
-        if (xl_imports_[i]) {  // let go of the caller's reply slot
+      const bool gone = st == kXLaneFree || st == kXLaneReleasing || !tok || !ring_token_alive(tok);
+      if (gone) {
+        if (xl_imports_[i]) {  // let go of the caller's reply slot once nothing can write it
+          if (!xlane_quiet(i)) {
+            ++live;  // keep polling: the wave must finish (and the waker relaunch it for) the request
+            continue;
+          }
           xlane_write(i, 0, 0);
+          (void)hipSetDevice(device_);
           (void)hipIpcCloseMemHandle(xl_imports_[i]);
           xl_imports_[i] = nullptr;
         }
-        if (st != kXLaneFree) {
-          g.state.store(kXLaneFree, std::memory_order_release);
+        if (st != kXLaneFree) {  // the slot is reusable only now (the caller frees its reply slot on Free)
           uint64_t t = tok;
           g.token.compare_exchange_strong(t, 0);
+          g.state.store(kXLaneFree, std::memory_order_release);
         }
         continue;
       }
       ++live;
       if (st != kXLaneRequested) continue;
+      if (xl_imports_[i] && !xlane_quiet(i)) continue;  // the previous holder's request is still running
       void* p = nullptr;
       hipIpcMemHandle_t h;
       memcpy(&h, g.reply_ipc, sizeof h);
       (void)hipSetDevice(device_);
       if (xl_imports_[i]) {
+        xlane_write(i, 0, 0);
         (void)hipIpcCloseMemHandle(xl_imports_[i]);
         xl_imports_[i] = nullptr;
       }
@@ -717,6 +730,13 @@ class DeviceServer {
     for (int i = 0; i < kXLanes; ++i)
       if (xl_imports_[i]) top = (uint64_t)i + 1;
     __atomic_store_n(&ctrl_->xl_n, top, __ATOMIC_SEQ_CST);
+  }
+
+  // No request of lane i in flight: the wave answered everything published there.
+  bool xlane_quiet(int i) const {
+    const volatile XLane* L = &xl_[i];
+    const uint64_t t = L->req_tag;
+    return t == 0 || L->served == t;
   }
 
   // Reset lane i (through the BAR mapping): sequence restarts at 0.

@@ -146,6 +146,10 @@ constexpr uint64_t kDescA = 1ull << 38, kDescP = 2ull << 38, kDescVal = (1ull <<
 __device__ __forceinline__ uint64_t desc_word(uint32_t tag, uint64_t status, uint64_t v) {
   return ((uint64_t)tag << 40) | status | v;
 }
+// A Send's descriptor tag from its device counter: 1..0xffffff for every counter
+// value (2^24 - 1 distinct tags; a plain `(ctr & 0xffffff) + 1` reaches 0x1000000,
+// whose shift out of the 24-bit field would publish tag 0 and stall every look-back).
+__host__ __device__ __forceinline__ uint32_t epoch_tag(uint32_t ctr) { return ctr % 0xffffffu + 1u; }
 constexpr uint32_t kLookbackSpins = 1u << 20;  // a bug guard (a lost descriptor must not hang the GPU)
 
 // Sum of the descriptors of tiles q, q-1, ... (stride `stride` words apart, this

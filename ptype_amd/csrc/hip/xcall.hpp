@@ -180,28 +180,47 @@ class PeerLane {
     return st == kStatusNotDelivered;
   }
   void retire() { release(); }
+  // Two-phase release: the lane goes Releasing, the server's waker
+  // closes its import of our reply slot once no request is in flight and marks
+  // the lane Free -- only then is the slot freed here.  If the server does not
+  // answer within the bound (it died, or a handler is stuck), the 4 KB slot is
+  // leaked rather than freed under a possible late reply store.
   void release() {
+    bool acked = true;
     if (lane_ >= 0) {
       XLaneReg& g = hdr_->xregs[lane_];
-      g.state.store(kXLaneFree, std::memory_order_release);
-      g.token.store(0, std::memory_order_release);
-      hdr_->wake.store(1, std::memory_order_release);
-      shm_futex_wake(&hdr_->wake);
+      g.state.store(kXLaneReleasing, std::memory_order_release);
+      const auto t0 = std::chrono::steady_clock::now();
+      acked = false;
+      for (;;) {
+        hdr_->wake.store(1, std::memory_order_release);
+        shm_futex_wake(&hdr_->wake);
+        if (g.state.load(std::memory_order_acquire) == kXLaneFree) {
+          acked = true;
+          break;
+        }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > release_wait_s_) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      }
       lane_ = -1;
     }
     if (peer_) (void)hipIpcCloseMemHandle(peer_);
     peer_ = nullptr;
-    // the reply slot stays allocated until the server has let go of its import
-    // (it frees a lane whose state is Free at its next waker pass)
     if (reply_) {
-      std::this_thread::sleep_for(std::chrono::milliseconds(5));
-      (void)hipFree(reply_);
+      if (acked) (void)hipFree(reply_);
+      else ++leaked_slots_;
       reply_ = nullptr;
     }
     if (done_) (void)hipFree(done_);
     done_ = nullptr;
   }
 
+ public:
+  static uint64_t leaked_slots() { return leaked_slots_; }
+
+ private:
+  double release_wait_s_ = 2.0;
+  static inline uint64_t leaked_slots_ = 0;
   int device_;
   std::shared_ptr<ShmSegment> seg_;
   ShmHeader* hdr_ = nullptr;

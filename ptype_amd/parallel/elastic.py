@@ -64,6 +64,32 @@ class Excluded(RuntimeError):
     """This node is not a member of the newest generation."""
 
 
+# What a collective raises when a PEER failed, as opposed to a local error (CUDA
+# OOM, a launch failure, a stalled look-back), which must propagate unchanged
+# instead of aborting the whole group (ADVICE r3): gloo's transport errors carry
+# their source path, RCCL's entry points are named in the engines' messages
+# (csrc/hip/engine.hpp, exchange_sorted.hip, ipc_comm.hpp), and torch raises its
+# Dist* errors for both backends.
+_PEER_FAILURE_MARKS = ("gloo/transport", "Connection closed by peer", "Connection reset by peer", "Broken pipe",
+                       "ncclAllToAll failed", "ncclAllReduce failed", "ncclSend failed", "ncclRecv failed",
+                       "ncclGroupEnd failed", "ncclGroupStart failed", "ncclRemoteError", "ncclSystemError",
+                       "IpcComm: peer", "FakeComm: a rank did not reach")
+
+
+def is_rank_failure(e: BaseException) -> bool:
+    """Whether ``e`` (raised by a data-plane collective) means a peer rank failed."""
+    import torch.distributed as dist
+
+    if isinstance(e, RankFailure):
+        return True
+    for name in ("DistBackendError", "DistNetworkError", "DistStoreError"):
+        t = getattr(dist, name, None)
+        if t is not None and isinstance(e, t):
+            return True
+    msg = str(e)
+    return any(m in msg for m in _PEER_FAILURE_MARKS)
+
+
 def ring_placement(nodes0: list[str], members: list[str]) -> dict[str, list[int]]:
     """Original rank -> owner: every surviving node owns its own original rank
     first, then adopts each dead original rank whose next surviving successor

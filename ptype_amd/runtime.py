@@ -325,16 +325,21 @@ class DeviceRuntime:
         if self.membership is None:
             ex = self.exchange
             return ex.send_all(batch) if resend_overflow else ex.send(batch)
+        from .parallel.elastic import RankFailure, is_rank_failure
+
         lost_before: list[int] = []
         todo = None  # after a recovery without re-sends: the indices still to deliver
         for attempt in range(self._elastic_cfg["max_recoveries"] + 1):
             try:
                 if self._watchdog is not None and self._watchdog.failed:
-                    raise RuntimeError(self._watchdog.failed)
+                    raise RankFailure(self._watchdog.failed)
                 sub = batch if todo is None else batch.index_select(todo)
                 out = self.exchange.send_all(sub) if resend_overflow else self.exchange.send(sub)
-            except RuntimeError as e:  # gloo / RCCL errors (DistBackendError is a RuntimeError)
-                if attempt == self._elastic_cfg["max_recoveries"]:
+            except RuntimeError as e:
+                # only a peer's failure re-forms the group; a local error (OOM, a launch
+                # failure, a stalled look-back) propagates unchanged -- recovering from it
+                # would abort every rank and re-run delivered, non-commutative messages
+                if not is_rank_failure(e) or attempt == self._elastic_cfg["max_recoveries"]:
                     raise
                 _log.warning("data-plane generation %d failed: %s", self.membership["gen"], str(e)[:300])
                 trace.mark("ptype.rank_failure")
@@ -355,7 +360,9 @@ class DeviceRuntime:
             if self.replicate_every and self._sends % self.replicate_every == 0:
                 try:
                     self.replicate()
-                except RuntimeError:
+                except RuntimeError as e:
+                    if not is_rank_failure(e):
+                        raise
                     self.recover()  # the batch WAS delivered: recover, never re-send it
             if todo is None:
                 return out
@@ -455,6 +462,8 @@ class DeviceRuntime:
             self.server.close()
             self.server = hip().DeviceServer(self.device.index or 0, self._ring, self.state.data_ptr(),
                                              self.mailboxes, self.delay_us, self._idle_ms, 60.0, name)
+        for _, b in getattr(self, "_bridges", []):  # the net/rpc server keeps their handles: retarget in place
+            b.retarget(self.table.table.data_ptr(), self.table.cap, self.state.data_ptr(), self.state.numel())
         if self.mirror is not None:
             self.mirror.set_generation(m["gen"])
         if self.shard_lease is not None:
@@ -510,6 +519,10 @@ class DeviceRuntime:
         (K4: a connection's pipelined requests decoded on the GPU into mailbox
         columns, ``gob_bridge``)."""
         self.host(service)
+        if batch and self.world0 > 1:
+            # the bridge routes with mailbox = actor id on this GPU: right only when
+            # this rank hosts every actor (ADVICE r3)
+            raise ValueError("serve(batch=True): the GPU gob bridge serves single-rank runtimes only")
         for name, (mid, fields) in methods.items():
             server.RegisterDevice(f"{service}.{name}", self.server, mid, fields)
             if batch:
@@ -526,8 +539,11 @@ class DeviceRuntime:
             raise RuntimeError("gob_bridge needs a GPU runtime (use _core.host_batch_multiply() on the host)")
         self._bridges = getattr(self, "_bridges", [])
         mb = Mailboxes(self.device, shards=64, slots=1 << 12)
+        # ordered after the runtime's stream both ways: a bridge batch and a Send never
+        # update actor state concurrently
         b = hip().GobBridge(self.device.index or 0, mb._m, int(method_id), int(actor), self.table.table.data_ptr(),
-                            self.table.cap, self.state.data_ptr(), self.state.numel(), self.delay_us)
+                            self.table.cap, self.state.data_ptr(), self.state.numel(), self.delay_us,
+                            torch.cuda.current_stream(self.device).cuda_stream)
         self._bridges.append((mb, b))
         return b
 

@@ -52,3 +52,22 @@ def test_register_batch_needs_the_single_call_method():
     srv = C.Server()
     with pytest.raises(Exception, match="single calls first"):
         srv.RegisterDeviceBatch("Calculator.Multiply", _core.host_batch_multiply(), ["A", "B"])
+
+
+@pytest.mark.timeout(60)
+def test_uint_struct_fields_fall_back_to_the_single_call_path():
+    """the batch path's decoders zigzag every field, which is
+    right only for gob ``int`` (type 2).  A struct with a ``uint`` field (gob type
+    3) is not captured for the batch path: the host single-call path answers it,
+    with the right value."""
+    from ptype_amd.gobtypes import GoStruct, GoUint
+
+    srv, port = _serve(_core.host_batch_multiply())
+    try:
+        cli = _core.dial_http("127.0.0.1", port, allow_local=False)
+        calls = [GoStruct("Args", [("A", 6 + i), ("B", GoUint(7 + i))]) for i in range(50)]
+        got = cli.call_many("Calculator.Multiply", calls)
+        assert got == [(6 + i) * (7 + i) for i in range(50)]
+        assert srv.batched_calls == 0 and srv.call_counts()["Calculator.Multiply"] == 50
+    finally:
+        srv.Close()

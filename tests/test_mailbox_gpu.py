@@ -565,3 +565,21 @@ def test_sorted_mailbox_onepass_graph_replays():
         torch.cuda.synchronize()
         assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1), k
     assert mb.stats()["lookback_timeouts"] == 0
+
+
+def test_sorted_mailbox_onepass_epoch_tag_wraps():
+    """the one-pass look-back tag stays in the descriptor's
+    24-bit field when its device counter passes 0xffffff -- every Send across
+    the wrap sorts exactly and no look-back gives up."""
+    n, M = 1 << 15, (1 << 20) + 333
+    t, _ = placed_table(n)
+    mb = Mailboxes(DEV, shards=256, slots=1 << 14)
+    start = 0xFFFFFD
+    mb._m.epoch_counter = start
+    for k in range(4):  # tags 0xfffffe, 0xffffff, 1 (the counter's 0x1000000), 2
+        req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=300 + k, device=DEV)
+        val, st = mb.send(req, t, None, sort_mode="onepass")
+        torch.cuda.synchronize()
+        assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1), k
+    assert mb._m.epoch_counter == start + 4
+    assert mb.stats()["lookback_timeouts"] == 0

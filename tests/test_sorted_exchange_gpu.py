@@ -164,6 +164,43 @@ def test_sorted_exchange_too_wide_is_overflow_then_resent():
         assert bool((sts == STATUS_OK).all()) and torch.equal(v, ref) and resends >= 1
 
 
+def test_sorted_exchange_onepass_epoch_tag_wraps_in_a_subprocess():
+    """the sorted exchange's one-pass sort (PTYPE_SX_SORT=onepass)
+    across its epoch counter's 24-bit tag wrap: exact replies, no stalled look-back."""
+    code = textwrap.dedent("""
+        import sys, torch
+        sys.path.insert(0, sys.argv[1])
+        sys.path.insert(0, sys.argv[1] + "/tests")
+        from test_sorted_exchange_gpu import _run_ranks, _table
+        from ptype_amd.ops import batch as B
+        from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
+        from ptype_amd.parallel.exchange import ActorExchange
+        R, n, M = 2, 8192, 100_000
+        def body(r, fc, start, s):
+            tab, _ = _table(n, R)
+            st = torch.zeros(n // R + 1, dtype=torch.int64, device="cuda")
+            ex = ActorExchange(tab, M, chunks=1, state=st, fake=(fc, r), delivery="mailbox", mailbox_ordered=False)
+            req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=5 + r, device="cuda")
+            ex.send(req)  # builds the engine
+            s.synchronize()
+            ex._sorted.epoch_counter = 0xFFFFFD
+            start.wait()
+            for k in range(4):
+                req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=60 + 5 * r + k, device="cuda")
+                v, sts = ex.send(req)
+                s.synchronize()
+                assert bool((sts == STATUS_OK).all()) and torch.equal(v, req.a0 * req.a1), (r, k)
+            assert ex._sorted.epoch_counter == 0xFFFFFD + 4
+            assert ex.stats().failed == 0  # (raises on a stalled look-back)
+            return True
+        assert all(_run_ranks(R, body))
+        print("SUBPROCESS-OK")
+    """)
+    env = dict(os.environ, PTYPE_SX_SORT="onepass")
+    p = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0 and "SUBPROCESS-OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
+
+
 _GRAPH_SCRIPT = textwrap.dedent("""
     import json, os, sys, torch, torch.distributed as dist
     sys.path.insert(0, os.environ["PTYPE_ROOT"])
