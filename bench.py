@@ -80,6 +80,10 @@ def _parse():
     p.add_argument("--pregen", action="store_true", help="uniform load, pre-generated like --zipf (A/B baseline)")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary (affine placement) measurement after the headline")
+    p.add_argument("--comm", choices=["rccl", "ipc"], default="rccl",
+                   help="N > 1 data-plane collectives: RCCL over the process group (one GPU per rank), or IpcComm "
+                        "(csrc/hip/ipc_comm.hpp: peers' HBM segments by IPC handle, a gloo group for the host side) "
+                        "-- ipc lets every rank share one GPU: a multi-process rehearsal, not a scaling figure")
     return p.parse_args()
 
 
@@ -163,6 +167,7 @@ def wire_info(ex, req) -> dict:
         # padded: every peer region at the agreed capacity
         return {"wire": "v3-packed", "record_bytes": 4 * w["S"], "reply_bytes": w["vb"] + 0.125,
                 "field_bits": w["w"], "exchange": "exact" if w.get("exact") else "padded",
+                "engine": w.get("engine", "epoch"),
                 "wire_bytes_per_msg": 4 * (w["req_words"] + w["rep_words"]) * ex.chunks / max(req.M, 1)}
     return {"wire": "v2", "record_bytes": 4 * (ex.fmt or B.WireFormat.for_batch(req)).stride, "reply_bytes": 9}
 
@@ -186,22 +191,26 @@ def main():
         print(f"--gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     use_gpu = not args.cpu
+    ipc = use_gpu and args.comm == "ipc" and world > 1
     if use_gpu:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        dev_idx = local % max(1, torch.cuda.device_count()) if ipc else local  # ipc: ranks may share a GPU
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     dist_on = world > 1 or args.force_dist
+    nccl = dist_on and use_gpu and not ipc
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
-                                device_id=device if use_gpu else None)
+        dist.init_process_group("nccl" if nccl else "gloo", rank=rank, world_size=world,
+                                device_id=device if nccl else None)
+    red_dev = device if nccl else torch.device("cpu")  # where host-level reductions' tensors live
 
     def barrier():
         if dist_on:
-            if use_gpu:
-                dist.barrier(device_ids=[local])
+            if nccl:
+                dist.barrier(device_ids=[dev_idx])
             else:
                 dist.barrier()
 
@@ -275,7 +284,7 @@ def main():
         # order in one ring) unless --sharding arrival (tile-sharded queues)
         ex = ActorExchange(table, Mq, chunks=chunks, state=state, fake=fake, delivery=delivery,
                            mailbox_ordered=sharding == "actor", mailbox_shards=args.mailbox_shards,
-                           mailbox_slots=args.mailbox_slots)
+                           mailbox_slots=args.mailbox_slots, comm="ipc" if ipc else "rccl")
         _LIVE_EXCHANGES.append(weakref.ref(ex))  # (weak: a finished measurement's buffers stay freeable)
         if Mq == M and method == METHOD_CALC_MULTIPLY:
             rq, v, t = req, val, st
@@ -328,6 +337,9 @@ def main():
         sync()
         if warmup:
             verify("warmup", last(warmup), v, t, method)
+        # re-send rounds are counted over the timed steps only: the first Sends of the
+        # sorted exchange run at the static start-up capacity, before any agreement
+        ex.warmup_resends, ex.counters.resends = ex.counters.resends, 0
         barrier()
         sync()
         t0 = time.perf_counter()
@@ -337,7 +349,7 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         if dist_on:
-            tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = float(tt.item())
         if steps:
@@ -404,7 +416,7 @@ def main():
     # by RCCL alone (same chunking, same per-peer sizes), so a multi-GPU line says
     # whether the step is bound by xGMI or by the kernels around it
     diag = None
-    if dist_on and use_gpu and ex.last_wire is not None and args.steps:
+    if nccl and ex.last_wire is not None and args.steps:
         w = ex.last_wire
         # bytes per chunk, all peers (rounded to a multiple of the world: equal splits)
         sizes = [(4 * int(w[k]) + world - 1) // world * world for k in ("req_words", "rep_words")]
@@ -494,7 +506,7 @@ def main():
             host_barrier("ptype/bench/rtt/done")  # keep serving until every rank is done calling
         srv.close()
         if dist_on:
-            t = torch.tensor([p50, p50_remote, float(len(rtt_errors))], dtype=torch.float64, device=device)
+            t = torch.tensor([p50, p50_remote, float(len(rtt_errors))], dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             p50, p50_remote, n_err = (float(x) for x in t.tolist())
             if n_err and not rtt_errors:
@@ -533,9 +545,12 @@ def main():
                 "model": "calculator actor (Calculator.Multiply)",
                 "global_batch": M * world,
                 "seq_len": None,
-                "parallelism": f"actors sharded over {world} GPU(s)" + ((", RCCL all-to-all epochs" if use_gpu
-                                                                           else ", gloo all-to-all epochs (CPU)")
-                                                                          if dist_on else ""),
+                "parallelism": (f"{world} ranks sharing {torch.cuda.device_count()} GPU(s), IpcComm all-to-alls "
+                                "(multi-process rehearsal, not a scaling figure)" if ipc else
+                                f"actors sharded over {world} GPU(s)" + ((", RCCL all-to-all epochs" if use_gpu
+                                                                          else ", gloo all-to-all epochs (CPU)")
+                                                                         if dist_on else "")),
+                "comm": ("ipc" if ipc else "rccl") if dist_on and use_gpu else None,
                 "msgs_per_gpu_per_step": M,
                 "actors": n_actors,
                 "chunks": chunks,
@@ -544,7 +559,8 @@ def main():
                 "hip_graph": graphed,
                 "steps_per_graph": args.steps_per_graph if graphed else None,
                 **({"load": f"zipf({args.zipf})" if args.zipf > 0 else "uniform", "pregenerated": True,
-                    "resend_rounds": ex.counters.resends} if pregen else {}),
+                    "resend_rounds": ex.counters.resends, "resend_rounds_warmup": ex.warmup_resends}
+                   if pregen else {}),
                 **({"slot_capacity": ex.last_wire.get("C"), "slot_capacity_alloc": ex.last_wire.get("C_alloc"),
                     "slot_capacity_static": ex.C} if ex.last_wire is not None else {}),
                 "placement": args.placement,

@@ -11,6 +11,7 @@
 #include "common.hpp"
 #include "engine.hpp"
 #include "exchange_sorted.hpp"
+#include "ipc_comm.hpp"
 #include "mailbox.hpp"
 #include "server.hpp"
 #include "xcall.hpp"
@@ -271,12 +272,16 @@ PYBIND11_MODULE(_hip, m) {
   m.def("memcpy_h2d_async", &memcpy_h2d_async);
   m.def("stream_sync", &stream_sync, py::call_guard<py::gil_scoped_release>());
 
-  py::class_<FakeComm, std::shared_ptr<FakeComm>>(m, "FakeComm",
-                                                  "in-process R-rank all-to-all for multi-rank engine tests "
-                                                  "(one host thread + stream per rank on one GPU)")
+  py::class_<HostComm, std::shared_ptr<HostComm>>(m, "HostComm",
+                                                  "a non-RCCL communicator the engines drive (FakeComm, IpcComm)")
+      .def_property_readonly("size", &HostComm::size)
+      .def_property_readonly("loopback", &HostComm::loopback)
+      .def_property_readonly("device_side", &HostComm::device_side)
+      .def("check", &HostComm::check, "raise if an earlier collective failed (a peer missed it)");
+  py::class_<FakeComm, HostComm, std::shared_ptr<FakeComm>>(m, "FakeComm",
+                                                            "in-process R-rank all-to-all for multi-rank engine tests "
+                                                            "(one host thread + stream per rank on one GPU)")
       .def(py::init<int, bool, double>(), py::arg("R"), py::arg("loopback") = false, py::arg("link_gbps") = 0.0)
-      .def_property_readonly("size", &FakeComm::size)
-      .def_property_readonly("loopback", &FakeComm::loopback)
       .def(
           "allreduce_max",
           [](FakeComm& c, int rank, uintptr_t dev, int n, uintptr_t stream) {
@@ -285,10 +290,42 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("rank"), py::arg("dev"), py::arg("n"), py::arg("stream"), py::call_guard<py::gil_scoped_release>(),
           "element-wise max of n u64 over the in-process ranks (collective over them)");
 
+  py::class_<IpcComm, HostComm, std::shared_ptr<IpcComm>>(
+      m, "IpcComm",
+      "one rank per PROCESS: collectives through peers' HBM segments imported by IPC handle, stream-ordered on "
+      "the device (csrc/hip/ipc_comm.hpp)")
+      .def(py::init<int, int, int, size_t, double>(), py::arg("device"), py::arg("R"), py::arg("rank"),
+           py::arg("cap_bytes"), py::arg("timeout_s") = 30.0)
+      .def("handle", [](const IpcComm& c) { return py::bytes(c.handle()); })
+      .def(
+          "connect",
+          [](IpcComm& c, const std::vector<py::bytes>& hs) {
+            std::vector<std::string> v;
+            for (const auto& h : hs) v.push_back(std::string(h));
+            c.connect(v);
+          },
+          py::arg("handles"))
+      .def_property_readonly("failed", &IpcComm::failed)
+      .def_property_readonly("ops", &IpcComm::ops)
+      .def_property_readonly("rank", &IpcComm::rank)
+      .def_property_readonly("cap", &IpcComm::cap)
+      .def(
+          "alltoall",
+          [](IpcComm& c, uintptr_t src, uintptr_t dst, size_t bytes, uintptr_t stream) {
+            c.alltoall(c.rank(), (const void*)src, (void*)dst, bytes, reinterpret_cast<hipStream_t>(stream));
+          },
+          py::arg("src"), py::arg("dst"), py::arg("bytes"), py::arg("stream"))
+      .def(
+          "allreduce_max",
+          [](IpcComm& c, uintptr_t dev, int n, uintptr_t stream) {
+            c.allreduce_max(c.rank(), reinterpret_cast<uint64_t*>(dev), n, reinterpret_cast<hipStream_t>(stream));
+          },
+          py::arg("dev"), py::arg("n"), py::arg("stream"));
+
   py::class_<EpochEngine>(m, "EpochEngine",
                           "chunk-pipelined Send (route -> ncclAllToAll -> dispatch -> ncclAllToAll -> complete) "
                           "enqueued from one host call; comm = raw ncclComm_t or 0 for no collectives")
-      .def(py::init<int, uintptr_t, int, int, int64_t, int64_t, int, std::shared_ptr<FakeComm>, bool, int64_t>(),
+      .def(py::init<int, uintptr_t, int, int, int64_t, int64_t, int, std::shared_ptr<HostComm>, bool, int64_t>(),
            py::arg("device"), py::arg("comm"), py::arg("R"), py::arg("rank"), py::arg("C"), py::arg("max_chunk"),
            py::arg("chunks"), py::arg("fake") = nullptr, py::arg("adaptive") = false, py::arg("c_fixed") = 0)
       .def(
@@ -350,7 +387,7 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<SortedExchange>(m, "SortedExchange",
                              "multi-GPU Send with mailbox delivery: the sender's counting sort by (rank, actor shard) "
                              "fills the peers' mailboxes directly; see csrc/hip/exchange_sorted.hpp")
-      .def(py::init<int, uintptr_t, int, int, int64_t, int, int64_t, int64_t, std::shared_ptr<FakeComm>>(),
+      .def(py::init<int, uintptr_t, int, int, int64_t, int, int64_t, int64_t, std::shared_ptr<HostComm>>(),
            py::arg("device"), py::arg("comm"), py::arg("R"), py::arg("rank"), py::arg("max_chunk"), py::arg("chunks"),
            py::arg("C_alloc"), py::arg("C0"), py::arg("fake") = nullptr)
       .def(
@@ -386,6 +423,8 @@ PYBIND11_MODULE(_hip, m) {
            "geometry of the last send (per peer and chunk); agreed: from the agreement of Send spec_from")
       .def("stats", &SortedExchange::stats)
       .def_property("epoch_counter", &SortedExchange::epoch_counter, &SortedExchange::set_epoch_counter)
+      .def("last_overflow", &SortedExchange::last_overflow, py::call_guard<py::gil_scoped_release>(),
+           "messages the last Send answered STATUS_OVERFLOW, max over ranks (waits for its agreement copy)")
       .def_property_readonly("sends", &SortedExchange::sends);
   py::class_<Mailboxes>(m, "Mailboxes",
                         "HBM actor mailboxes: S shard rings of Q 32-B tagged records (K2 enqueue, K3 epoch drain, "

@@ -18,6 +18,7 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <cstring>
 #include <deque>
 #include <memory>
 #include <mutex>
@@ -156,7 +157,32 @@ static __global__ __launch_bounds__(256) void fake_copy_regions_kernel(const uin
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) d[i] = s[i];
 }
 
-class FakeComm {
+// The data plane's collectives when they are not RCCL's: the engines drive a
+// HostComm through these calls, one rank's view at a time (`r`).  Two
+// implementations: FakeComm (R ranks of ONE process, host threads) and IpcComm
+// (ipc_comm.hpp: one rank per PROCESS, peers' HBM imported by IPC handle, every
+// collective stream-ordered on the device).
+class HostComm {
+ public:
+  virtual ~HostComm() = default;
+  virtual int size() const = 0;
+  // loopback: one driving rank stands for a symmetric node (recv = send, identity all-reduce)
+  virtual bool loopback() const { return false; }
+  // whether allreduce_max is stream-ordered on the device (no host wait inside it)
+  virtual bool device_side() const { return false; }
+  // recv_r[q] = send_q[r], `bytes` per peer region
+  virtual void alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) = 0;
+  // regions `stride` bytes apart; send_bytes[q] of region q go to peer q, which
+  // lands recv_bytes[.] in its region r (nullptr: whole regions)
+  virtual void alltoallv(int r, const void* src, void* dst, size_t stride, const size_t* send_bytes,
+                         const size_t* recv_bytes, hipStream_t s) = 0;
+  // element-wise max of n u64 over the ranks, in place
+  virtual void allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) = 0;
+  // throws when an earlier collective failed (a peer missed it); called at every Send
+  virtual void check() const {}
+};
+
+class FakeComm : public HostComm {
  public:
   explicit FakeComm(int R, bool loopback = false, double link_gbps = 0.0)
       : R_(R), loopback_(loopback), link_gbps_(link_gbps), slots_(R) {
@@ -172,16 +198,17 @@ class FakeComm {
       (void)hipEventDestroy(sl.done);
     }
   }
-  int size() const { return R_; }
-  bool loopback() const { return loopback_; }
+  int size() const override { return R_; }
+  bool loopback() const override { return loopback_; }
 
-  // recv_r[q] = send_q[r], `bytes` per peer region
-  void alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) {
-    alltoallv(r, src, dst, bytes, nullptr, s);
+  void alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) override {
+    alltoallv(r, src, dst, bytes, nullptr, nullptr, s);
   }
-  // Regions `stride` bytes apart; only the first `recv_bytes[q]` of region q move
-  // (nullptr: whole regions).  Loopback: this rank stands for all, recv = send.
-  void alltoallv(int r, const void* src, void* dst, size_t stride, const size_t* recv_bytes, hipStream_t s) {
+  // Only the first `recv_bytes[q]` of region q move (in-process copies: the
+  // receiver's sizes are all it needs).  Loopback: this rank stands for all, recv = send.
+  void alltoallv(int r, const void* src, void* dst, size_t stride, const size_t* send_bytes, const size_t* recv_bytes,
+                 hipStream_t s) override {
+    (void)send_bytes;
     if (loopback_) {
       size_t off_rank = 0;
       if (!recv_bytes) {
@@ -228,7 +255,7 @@ class FakeComm {
   }
 
   // element-wise max of n u64 on every rank (host-synchronous, like the engine's use)
-  void allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) {
+  void allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) override {
     if (loopback_) return;  // every rank holds the same maxima
     slots_[r].host.assign(n, 0);
     PT_HIP_CHECK(hipMemcpyAsync(slots_[r].host.data(), dev, n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -306,7 +333,7 @@ class EpochEngine {
   // agreed in the same all-reduce as the layout (never above `C`).
   // `c_fixed` (0: C): the capacity of Sends that do not adapt (wire v2).
   EpochEngine(int device, uintptr_t comm, int R, int rank, int64_t C, int64_t max_chunk, int chunks,
-              std::shared_ptr<FakeComm> fake = nullptr, bool adaptive = false, int64_t c_fixed = 0)
+              std::shared_ptr<HostComm> fake = nullptr, bool adaptive = false, int64_t c_fixed = 0)
       : device_(device), comm_((void*)comm), fake_(std::move(fake)), R_(R), rank_(rank), C_(C), C_alloc_(C),
         C_fixed_(c_fixed > 0 && c_fixed <= C ? c_fixed : C), max_chunk_(max_chunk), chunks_(chunks),
         adaptive_(adaptive) {
@@ -419,6 +446,7 @@ class EpochEngine {
   void reset_host_profile() { prof_ = HostProfile(); }
 
   void send(const EngineSend& a) {
+    if (fake_) fake_->check();  // an earlier collective's failure surfaces here (IpcComm: a peer missed one)
     const uint64_t t0 = now();
     send_impl(a);
     prof_.total_ns += now() - t0;
@@ -557,7 +585,7 @@ class EpochEngine {
     // there already (its completions waited for them), and no cross-stream hop
     // sits on this, the one host wait of the Send
     const int64_t n_agree = exact_ ? agree_words_ : kMetaWords;
-    if (fake_ && !fake_->loopback()) {
+    if (fake_ && !fake_->loopback() && !fake_->device_side()) {  // in-process ranks: a host-synchronous MAX
       fake_->allreduce_max(rank_, meta_dev_, (int)n_agree, cs);
       PT_HIP_CHECK(hipMemcpy(meta_host_, meta_dev_, n_agree * sizeof(uint64_t), hipMemcpyDeviceToHost));
       for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
@@ -567,6 +595,7 @@ class EpochEngine {
       prof_.meta_ns += now() - t0;
       return;
     }
+    if (fake_ && !fake_->loopback()) fake_->allreduce_max(rank_, meta_dev_, (int)n_agree, cs);  // device-side (IpcComm)
     const int rc = fake_ ? 0 : rccl().allreduce(meta_dev_, meta_dev_, n_agree, kNcclUint64, kNcclMax, comm_, cs);
     if (rc != 0)
       throw std::runtime_error(std::string("ncclAllReduce failed: ") +
@@ -850,7 +879,7 @@ class EpochEngine {
     Timed t(prof_.a2a_ns);
     const size_t stride = (size_t)stride_words * 4;
     if (fake_) {
-      fake_->alltoallv(rank_, (const void*)src, (void*)dst, stride, xr_, comm_stream_);
+      fake_->alltoallv(rank_, (const void*)src, (void*)dst, stride, xs_, xr_, comm_stream_);
       return;
     }
     auto check = [](int rc, const char* what) {
@@ -870,7 +899,7 @@ class EpochEngine {
   bool collectives() const { return comm_ != nullptr || fake_ != nullptr; }
 
   void* comm_;
-  std::shared_ptr<FakeComm> fake_;
+  std::shared_ptr<HostComm> fake_;
   int R_, rank_;
   int64_t C_, C_alloc_, C_fixed_, max_chunk_;
   int chunks_;

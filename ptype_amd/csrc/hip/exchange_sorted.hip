@@ -185,6 +185,14 @@ __global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hi
   }
 }
 
+// This block's overflow answers into meta[kMetaOverflow] (a count per rank; the
+// agreement's MAX then says whether ANY rank must re-send -- send_all reads it
+// from the agreement's pinned copy, no count pass and no extra collective).
+__device__ __forceinline__ void fold_overflow(uint32_t n, unsigned long long* meta) {
+  for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off);
+  if (lane_id() == 0 && n) atomicAdd(meta + kMetaOverflow, (unsigned long long)n);
+}
+
 // ---------------------------------------------------------------- sender: scatter
 template <int MODE, int S>
 __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint32_t K, const uint32_t* __restrict__ hist,
@@ -204,6 +212,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
     bo[b] = boff[b];
   }
   MetaAcc acc;
+  uint32_t n_ovf = 0;  // messages answered kStatusOverflow (folded into the agreement: send_all's re-send test)
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
   for (uint32_t t = t0; t < t1; ++t) {
     for (uint32_t b = lane; b < B; b += kWave) wcnt[w][b] = 0;
@@ -270,6 +279,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
       const uint32_t pos = bo[bk] + wcnt[w][bk] + (pr[k] >> 8);
       if (pos >= C) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
         perm[i] = -1;
+        ++n_ovf;
         continue;
       }
       const int64_t x0 = __builtin_nontemporal_load(in.a0 + i);
@@ -292,6 +302,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
       } else {  // wider than the layout in force: a null record holds the slot
         f[0] = 0, f[1] = low_mask(L.w[1]), f[2] = 0, f[3] = 0, f[4] = 0;
         perm[i] = -1;
+        ++n_ovf;
       }
       uint32_t rec[S];
       packed_pack<S>(L, f, rec);
@@ -301,6 +312,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
   }
   acc.mb = 0;  // the count pass folds the mailboxes
   meta_publish(acc, in.mcol != nullptr, in.method_uniform, in.M, meta);
+  fold_overflow(n_ovf, meta);
 }
 
 // ---------------------------------------------------------------- sender: one pass (rank-only batches)
@@ -400,6 +412,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
   __syncthreads();
   // phase 2: each message's arguments, packed at its position
   MetaAcc acc;
+  uint32_t n_ovf = 0;
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     const int64_t i = tile_index(t, k);
@@ -412,6 +425,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
     const uint32_t pos = pre[rk] + wcnt[w][rk] + (pr[k] >> 8);
     if (pos >= C) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
       perm[i] = -1;
+      ++n_ovf;
       continue;
     }
     const int64_t x0 = __builtin_nontemporal_load(in.a0 + i);
@@ -434,6 +448,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
     } else {  // wider than the layout in force: a null record holds the slot
       f[0] = 0, f[1] = low_mask(L.w[1]), f[2] = 0, f[3] = 0, f[4] = 0;
       perm[i] = -1;
+      ++n_ovf;
     }
     uint32_t rec[S];
     packed_pack<S>(L, f, rec);
@@ -441,6 +456,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
   }
   acc.mb = mbmax_s;  // (the mailbox maximum of this tile: every lane sees the block's)
   meta_publish(acc, in.mcol != nullptr, in.method_uniform, in.M, meta);
+  fold_overflow(n_ovf, meta);
   __shared__ bool last;
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
   __syncthreads();
@@ -708,7 +724,7 @@ __global__ __launch_bounds__(kXOrdThreads) void sx_drain_ord_kernel(const uint32
 
 // ---------------------------------------------------------------- host
 SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int64_t max_chunk, int chunks,
-                               int64_t C_alloc, int64_t C0, std::shared_ptr<FakeComm> fake)
+                               int64_t C_alloc, int64_t C0, std::shared_ptr<HostComm> fake)
     : device_(device), comm_((void*)comm), fake_(std::move(fake)), R_(R), rank_(rank), chunks_(chunks),
       max_chunk_(max_chunk), C_alloc_(C_alloc) {
   if (R < 1 || R > kSxMaxRanks) throw std::invalid_argument("SortedExchange: 1 <= ranks <= 16");
@@ -800,9 +816,24 @@ uint32_t SortedExchange::epoch_counter() const {
   return v;
 }
 
+uint64_t SortedExchange::last_overflow() const {
+  const int64_t k = sends_ - 1;
+  if (k < 0) return 0;
+  const int j = (int)(k & 1);
+  if (meta_send_[j] != k) throw std::runtime_error("SortedExchange: the last Send recorded no agreement (captured)");
+  PT_HIP_CHECK(hipEventSynchronize(ev_meta_[j]));
+  return meta_host_[j * kMetaWords + kMetaOverflow];
+}
+
 void SortedExchange::adopt(const uint64_t* meta, int64_t from) {
   L_ = sx_layout(meta);
-  const double need = (double)meta[kMetaCap];
+  // the busiest bucket of the last kNeedWindow agreements: a small Send (send_all's
+  // re-send of a few overflowed messages) must not shrink the capacity of the full
+  // Sends after it.  Every rank sees the same agreements, so all derive the same C.
+  need_hist_[need_n_++ % kNeedWindow] = meta[kMetaCap];
+  uint64_t busiest = 0;
+  for (int j = 0; j < kNeedWindow && j < need_n_; ++j) busiest = std::max(busiest, need_hist_[j]);
+  const double need = (double)busiest;
   // the busiest bucket two Sends ago plus 1 % and 8 sigma: uniform traffic then
   // overflows with probability ~1e-15 per bucket, and skewed traffic that is
   // stable over a few Sends fits as well
@@ -880,6 +911,7 @@ void SortedExchange::send(const SxSend& a) {
   if (a.M > 0 && (!a.actor || !a.a0)) throw std::invalid_argument("SortedExchange: actor and a0 columns required");
   if (a.cap == 0 || (a.cap & (a.cap - 1))) throw std::invalid_argument("table capacity must be a power of two");
   PT_HIP_CHECK(hipSetDevice(device_));
+  if (fake_) fake_->check();  // an earlier collective's failure surfaces here (IpcComm: a peer missed one)
   const hipStream_t cs = as_stream(a.stream);
   pick_spec(cs);
   hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;

@@ -85,13 +85,17 @@ class SortedExchange {
   // chunks * max_chunk messages; C_alloc: per-peer capacity the buffers hold;
   // C0: the start-up capacity (until the first agreement applies).
   SortedExchange(int device, uintptr_t comm, int R, int rank, int64_t max_chunk, int chunks, int64_t C_alloc,
-                 int64_t C0, std::shared_ptr<FakeComm> fake = nullptr);
+                 int64_t C0, std::shared_ptr<HostComm> fake = nullptr);
   ~SortedExchange();
   void send(const SxSend& a);
   const SxWire& last_wire() const { return wire_; }
   int64_t sends() const { return sends_; }
   // receiver counters: handler failures, replies wider than agreed; sender: one-pass look-backs that gave up (0)
   std::vector<uint64_t> stats() const;
+  // Messages answered STATUS_OVERFLOW by the last Send, max over the ranks (0: no
+  // rank must re-send).  Waits for that Send's agreement copy -- one host wait on
+  // an event already queued, no collective of its own.
+  uint64_t last_overflow() const;
   // the one-pass sort's epoch counter (tests: preset near the 2^24 tag wrap); synchronous
   void set_epoch_counter(uint32_t v);
   uint32_t epoch_counter() const;
@@ -109,7 +113,7 @@ class SortedExchange {
 
   int device_;
   void* comm_;
-  std::shared_ptr<FakeComm> fake_;
+  std::shared_ptr<HostComm> fake_;
   int R_, rank_, chunks_;
   int64_t max_chunk_, C_alloc_;
   hipStream_t comm_stream_ = nullptr;
@@ -132,6 +136,9 @@ class SortedExchange {
   bool agreed_ = false;
   int64_t spec_from_ = -1;
   uint64_t spec_meta_[kMetaWords] = {};
+  static constexpr int kNeedWindow = 4;      // capacity: the busiest bucket of the last 4 agreements
+  uint64_t need_hist_[kNeedWindow] = {};
+  int need_n_ = 0;
   int64_t sends_ = 0;
   SxWire wire_;
 };

@@ -1,0 +1,246 @@
+// IpcComm (ipc_comm.hpp): process-to-process collectives through IPC-imported
+// HBM segments, stream-ordered on the device.
+#include "ipc_comm.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+namespace ptype {
+
+namespace {
+
+__device__ __forceinline__ uint64_t ipc_ld(const uint64_t* p) {  // memory-side read: no stale L2 line
+  return __hip_atomic_fetch_add(const_cast<uint64_t*>(p), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void ipc_st(uint64_t* p, uint64_t v) {
+  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t* word_at(uint64_t base, size_t off) {
+  return reinterpret_cast<uint64_t*>(base + off);
+}
+
+// One wave: lane q waits for rank q's word >= want.  which 0: rank q's `consumed`
+// (its inbox is free for this op -- this rank's own too: ops issued on two
+// streams, e.g. the epoch engine's agreement and its all-to-alls, are serialised
+// here); 1: this rank's posted[q] (rank q's data is in).
+// A timeout marks this rank failed (sticky) and the host flag; a rank already
+// failed returns at once.
+__global__ __launch_bounds__(64) void ipc_wait_kernel(const uint64_t* __restrict__ segs, int R, int rank, int which,
+                                                      uint64_t want, uint64_t timeout_ticks,
+                                                      uint64_t* __restrict__ host_failed) {
+  const int q = (int)threadIdx.x;
+  uint64_t* mine_failed = word_at(segs[rank], kIpcFailedOff);
+  bool timed_out = false;
+  if (q < R && ipc_ld(mine_failed) == 0) {
+    const uint64_t* w = which == 0 ? word_at(segs[q], kIpcConsumedOff) : word_at(segs[rank], kIpcPostedOff) + q;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t n = 0;
+    while (ipc_ld(w) < want) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+        timed_out = true;
+        break;
+      }
+      if ((++n & 63) == 0 && ipc_ld(mine_failed)) break;  // another wave of this rank gave up already
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  if (__ballot(timed_out) && q == 0) {
+    ipc_st(mine_failed, 1);
+    __hip_atomic_store(host_failed, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// `bytes` (a multiple of 4) from s to d by the blocks of one grid row.
+__device__ __forceinline__ void row_copy(const uint8_t* __restrict__ s, uint8_t* __restrict__ d, uint64_t bytes) {
+  const uint64_t n16 = bytes / 16, stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint4* s16 = reinterpret_cast<const uint4*>(s);
+  uint4* d16 = reinterpret_cast<uint4*>(d);
+  for (uint64_t i = i0; i < n16; i += stride) d16[i] = s16[i];
+  for (uint64_t i = n16 * 4 + i0; i < bytes / 4; i += stride)
+    reinterpret_cast<uint32_t*>(d)[i] = reinterpret_cast<const uint32_t*>(s)[i];
+}
+
+__device__ __forceinline__ bool rank_failed(const uint64_t* segs, int rank) {
+  __shared__ bool f;
+  if (threadIdx.x == 0) f = ipc_ld(word_at(segs[rank], kIpcFailedOff)) != 0;
+  __syncthreads();
+  return f;
+}
+
+// K1: region q of src -> slot `rank` of peer q's inbox; the last block of row q
+// publishes posted[rank] = seq in peer q's segment.
+__global__ __launch_bounds__(256) void ipc_push_kernel(const uint8_t* __restrict__ src, uint64_t src_stride,
+                                                       IpcSizes send, const uint64_t* __restrict__ segs, int rank,
+                                                       uint64_t cap, uint64_t seq, unsigned* __restrict__ ctr) {
+  if (rank_failed(segs, rank)) return;  // this comm is dead: nobody waits for this op any more
+  const int q = (int)blockIdx.y;
+  row_copy(src + (uint64_t)q * src_stride, reinterpret_cast<uint8_t*>(segs[q]) + kIpcCtrlBytes + (uint64_t)rank * cap,
+           send.n[q]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();  // release this block's stores (the reader is another process)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (atomicAdd(&ctr[q], 1u) == gridDim.x - 1) {  // every block of the row has released its part
+      atomicExch(&ctr[q], 0u);
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ipc_st(word_at(segs[q], kIpcPostedOff) + rank, seq);
+    }
+  }
+}
+
+// K3: inbox slot q -> region q of dst (or, reduce_n > 0, the element-wise max of
+// the R slots into reduce_dst); the last block marks the inbox consumed.
+__global__ __launch_bounds__(256) void ipc_out_kernel(uint8_t* __restrict__ dst, uint64_t dst_stride, IpcSizes recv,
+                                                      const uint64_t* __restrict__ segs, int rank, int R, uint64_t cap,
+                                                      uint64_t seq, unsigned* __restrict__ ctr,
+                                                      uint64_t* __restrict__ reduce_dst, int reduce_n) {
+  if (rank_failed(segs, rank)) return;
+  if (threadIdx.x == 0) {  // acquire: the posted flags were read by the wait kernel
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const uint8_t* inbox = reinterpret_cast<const uint8_t*>(segs[rank]) + kIpcCtrlBytes;
+  if (reduce_n > 0) {
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+      for (int k = (int)threadIdx.x; k < reduce_n; k += (int)blockDim.x) {
+        uint64_t m = 0;
+        for (int q = 0; q < R; ++q) m = max(m, reinterpret_cast<const uint64_t*>(inbox + (uint64_t)q * cap)[k]);
+        reduce_dst[k] = m;
+      }
+  } else {
+    const int q = (int)blockIdx.y;
+    row_copy(inbox + (uint64_t)q * cap, dst + (uint64_t)q * dst_stride, recv.n[q]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every inbox load has returned (its data is stored)
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(ctr, 1u) == gridDim.x * gridDim.y - 1) {
+    atomicExch(ctr, 0u);
+    ipc_st(word_at(segs[rank], kIpcConsumedOff), seq);
+  }
+}
+
+}  // namespace
+
+IpcComm::IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s)
+    : device_(device), R_(R), rank_(rank), cap_((cap_bytes + 15) / 16 * 16), timeout_s_(timeout_s) {
+  if (R < 1 || R > kIpcMaxRanks || rank < 0 || rank >= R) throw std::invalid_argument("IpcComm: 0 <= rank < R <= 64");
+  if (cap_ < 16) throw std::invalid_argument("IpcComm: capacity");
+  timeout_ticks_ = (uint64_t)(std::max(0.01, timeout_s) * 1e8);  // s_memrealtime: 100 MHz
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipMalloc((void**)&seg_, kIpcCtrlBytes + (size_t)R * cap_));
+  PT_HIP_CHECK(hipMemset(seg_, 0, kIpcCtrlBytes));
+  PT_HIP_CHECK(hipMalloc((void**)&segs_dev_, kIpcMaxRanks * sizeof(uint64_t)));
+  PT_HIP_CHECK(hipMalloc((void**)&ctr_, (kIpcMaxRanks + 1) * sizeof(unsigned)));
+  PT_HIP_CHECK(hipMemset(ctr_, 0, (kIpcMaxRanks + 1) * sizeof(unsigned)));
+  PT_HIP_CHECK(hipHostMalloc((void**)&host_failed_, 64, hipHostMallocMapped));
+  *host_failed_ = 0;
+  PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dev_failed_, host_failed_, 0));
+  PT_HIP_CHECK(hipDeviceSynchronize());
+  imports_.assign((size_t)R, nullptr);
+}
+
+IpcComm::~IpcComm() {  // no synchronisation: a wait on a dead peer ends at its timeout, not here
+  (void)hipSetDevice(device_);
+  for (void* p : imports_)
+    if (p) (void)hipIpcCloseMemHandle(p);
+  (void)hipFree(seg_);
+  (void)hipFree(segs_dev_);
+  (void)hipFree(ctr_);
+  (void)hipHostFree(host_failed_);
+}
+
+std::string IpcComm::handle() const {
+  hipIpcMemHandle_t h;
+  PT_HIP_CHECK(hipSetDevice(device_));
+  PT_HIP_CHECK(hipIpcGetMemHandle(&h, seg_));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof h);
+}
+
+void IpcComm::connect(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != R_) throw std::invalid_argument("IpcComm.connect: one handle per rank");
+  if (connected_) throw std::runtime_error("IpcComm.connect: already connected");
+  PT_HIP_CHECK(hipSetDevice(device_));
+  uint64_t segs[kIpcMaxRanks] = {};
+  for (int q = 0; q < R_; ++q) {
+    if (q == rank_) {
+      segs[q] = (uint64_t)(uintptr_t)seg_;
+      continue;
+    }
+    if (handles[(size_t)q].size() != sizeof(hipIpcMemHandle_t))
+      throw std::invalid_argument("IpcComm.connect: bad handle for rank " + std::to_string(q));
+    hipIpcMemHandle_t h;
+    memcpy(&h, handles[(size_t)q].data(), sizeof h);
+    void* p = nullptr;
+    PT_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    imports_[(size_t)q] = p;
+    segs[q] = (uint64_t)(uintptr_t)p;
+  }
+  PT_HIP_CHECK(hipMemcpy(segs_dev_, segs, sizeof segs, hipMemcpyHostToDevice));
+  connected_ = true;
+}
+
+bool IpcComm::failed() const { return __atomic_load_n(host_failed_, __ATOMIC_ACQUIRE) != 0; }
+
+void IpcComm::check() const {
+  if (failed())
+    throw std::runtime_error("IpcComm: peer did not reach a collective within " + std::to_string(timeout_s_) +
+                             " s (rank " + std::to_string(rank_) + " of " + std::to_string(R_) + ", op " +
+                             std::to_string(seq_) + ")");
+}
+
+void IpcComm::op(const void* src, size_t src_stride, void* dst, size_t dst_stride, const IpcSizes& send,
+                 const IpcSizes& recv, hipStream_t s, uint64_t* reduce_dst, int reduce_n) {
+  if (!connected_) throw std::runtime_error("IpcComm: connect() first");
+  uint64_t smax = 0, rmax = 0;
+  for (int q = 0; q < R_; ++q) {
+    if (send.n[q] > cap_ || recv.n[q] > cap_ || send.n[q] % 4 || recv.n[q] % 4)
+      throw std::invalid_argument("IpcComm: a region exceeds the capacity or is not a 4-B multiple");
+    smax = std::max(smax, send.n[q]);
+    rmax = std::max(rmax, recv.n[q]);
+  }
+  PT_HIP_CHECK(hipSetDevice(device_));
+  const uint64_t seq = ++seq_;
+  auto blocks = [](uint64_t bytes) {  // ~16 KB per block, at most 64 per peer
+    return (unsigned)std::min<uint64_t>(64, std::max<uint64_t>(1, (bytes + 16383) / 16384));
+  };
+  hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, s, segs_dev_, R_, rank_, 0, seq - 1, timeout_ticks_,
+                     dev_failed_);
+  hipLaunchKernelGGL(ipc_push_kernel, dim3(blocks(smax), R_), dim3(256), 0, s, (const uint8_t*)src,
+                     (uint64_t)src_stride, send, segs_dev_, rank_, (uint64_t)cap_, seq, ctr_);
+  hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, s, segs_dev_, R_, rank_, 1, seq, timeout_ticks_,
+                     dev_failed_);
+  hipLaunchKernelGGL(ipc_out_kernel, dim3(reduce_n > 0 ? 1 : blocks(rmax), reduce_n > 0 ? 1 : R_), dim3(256), 0, s,
+                     (uint8_t*)dst, (uint64_t)dst_stride, recv, segs_dev_, rank_, R_, (uint64_t)cap_, seq,
+                     ctr_ + kIpcMaxRanks, reduce_dst, reduce_n);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+void IpcComm::alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) {
+  alltoallv(r, src, dst, bytes, nullptr, nullptr, s);
+}
+
+void IpcComm::alltoallv(int r, const void* src, void* dst, size_t stride, const size_t* send_bytes,
+                        const size_t* recv_bytes, hipStream_t s) {
+  if (r != rank_) throw std::invalid_argument("IpcComm: one rank per process");
+  IpcSizes sn{}, rn{};
+  for (int q = 0; q < R_; ++q) {
+    sn.n[q] = send_bytes ? send_bytes[q] : stride;
+    rn.n[q] = recv_bytes ? recv_bytes[q] : stride;
+  }
+  op(src, stride, dst, stride, sn, rn, s, nullptr, 0);
+}
+
+void IpcComm::allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) {
+  if (r != rank_) throw std::invalid_argument("IpcComm: one rank per process");
+  if (n < 1 || (size_t)n * 8 > cap_) throw std::invalid_argument("IpcComm: all-reduce larger than the capacity");
+  IpcSizes sn{}, rn{};
+  for (int q = 0; q < R_; ++q) sn.n[q] = (uint64_t)n * 8;
+  op(dev, 0, nullptr, 0, sn, rn, s, dev, n);
+}
+
+}  // namespace ptype

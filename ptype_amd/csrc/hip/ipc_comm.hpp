@@ -1,0 +1,98 @@
+// IpcComm: the data plane's collectives between PROCESSES on one node without
+// RCCL -- one rank per process, each rank's receive segment in its own HBM,
+// exported with hipIpcGetMemHandle and imported by every peer.  It exists so the
+// engines' multi-rank pipelines (EpochEngine, SortedExchange) run across real
+// process boundaries on a one-GPU box: RCCL refuses two ranks on one device
+// ("Duplicate GPU detected"), and FakeComm's ranks share one process.  On a
+// multi-GPU node the same code imports the peers' segments over xGMI.
+//
+// Segment of rank r (hipMalloc, exported once):
+//   [0, 512)      posted[64]: peer q stores posted[q] = s once its op-s data sits
+//                 in this inbox (remote, system-scope atomic store)
+//   [512]         consumed: r stores s once it has copied op s out of its inbox
+//   [640]         failed: r's sticky error word (a wait that timed out)
+//   [4096, ...)   inbox[R][cap]: peer q's region of the op in flight at q * cap
+//
+// Op s (every rank issues the same ops in the same order; s is a host counter),
+// all on the caller's stream, no host wait:
+//   K0 wait   one wave: every rank's consumed >= s - 1 (its inbox is free again;
+//             this rank's own too, so ops issued on two streams stay serialised)
+//   K1 push   (X, R) blocks: region q of src -> peer q's inbox slot r; the last
+//             block of each peer releases (system fence) and stores posted[r] = s
+//             into that peer's segment
+//   K2 wait   one wave: every posted[q] of this rank's segment >= s
+//   K3 out    (X, R) blocks: agent acquire, inbox slot q -> region q of dst (or
+//             the element-wise max of the R slots, for all-reduce); the last
+//             block stores consumed = s
+// Waits are bounded (timeout_s): a peer that never arrives (killed) makes the
+// wave set `failed` (and a pinned host flag) and exit, every later kernel of
+// this comm skips its work, and the next Send's check() throws
+// "IpcComm: peer ...", which the elastic path reads as a rank failure.  Every
+// wave reaches an exit, so the grid drains even when a peer is gone.
+//
+// The hand-off follows MI355X_MICROARCH.md "inter-workgroup visibility":
+// producer plain stores -> s_waitcnt vmcnt(0) -> barrier -> one lane's release
+// fence (system scope: the consumer is another process) -> vmcnt(0) -> flag
+// store; consumer poll -> acquire fence -> vmcnt(0) -> barrier -> plain loads.
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+
+namespace ptype {
+
+constexpr int kIpcMaxRanks = 64;
+constexpr size_t kIpcCtrlBytes = 4096;
+constexpr size_t kIpcPostedOff = 0, kIpcConsumedOff = 512, kIpcFailedOff = 640;
+
+struct IpcSizes {  // by value: bytes per peer region (<= cap)
+  uint64_t n[kIpcMaxRanks];
+};
+
+class IpcComm : public HostComm {
+ public:
+  // cap_bytes: the largest region one op moves per peer (16-B multiple).
+  IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s = 30.0);
+  ~IpcComm() override;
+  IpcComm(const IpcComm&) = delete;
+  IpcComm& operator=(const IpcComm&) = delete;
+
+  // this rank's segment handle (hipIpcMemHandle_t bytes), for the other ranks
+  std::string handle() const;
+  // every rank's handle, in rank order (this rank's own is skipped); imports the peers
+  void connect(const std::vector<std::string>& handles);
+
+  int size() const override { return R_; }
+  bool device_side() const override { return true; }
+  void alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) override;
+  void alltoallv(int r, const void* src, void* dst, size_t stride, const size_t* send_bytes, const size_t* recv_bytes,
+                 hipStream_t s) override;
+  void allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) override;
+  void check() const override;
+
+  bool failed() const;           // a wait of this rank timed out (pinned host flag; no sync)
+  uint64_t ops() const { return seq_; }
+  int rank() const { return rank_; }
+  size_t cap() const { return cap_; }
+
+ private:
+  void op(const void* src, size_t src_stride, void* dst, size_t dst_stride, const IpcSizes& send,
+          const IpcSizes& recv, hipStream_t s, uint64_t* reduce_dst, int reduce_n);
+
+  int device_, R_, rank_;
+  size_t cap_;
+  uint64_t timeout_ticks_;
+  double timeout_s_;
+  uint8_t* seg_ = nullptr;                 // this rank's segment
+  std::vector<void*> imports_;             // peers' segments (nullptr for self)
+  uint64_t* segs_dev_ = nullptr;           // [R] segment base of every rank, as mapped here
+  unsigned* ctr_ = nullptr;                // [2] last-block tickets (push, out), self-resetting
+  uint64_t* host_failed_ = nullptr;        // pinned: set by a timed-out wait
+  uint64_t* dev_failed_ = nullptr;         // its device address
+  uint64_t seq_ = 0;                       // ops issued
+  bool connected_ = false;
+};
+
+}  // namespace ptype

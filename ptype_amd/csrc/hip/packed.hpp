@@ -50,6 +50,7 @@ enum PackedMeta : int {
   kMetaMethod = 4,  // largest method id sent
   kMetaMcol = 5,    // 1 if any rank sends a per-record method column (then every record carries one)
   kMetaCap = 6,     // largest per-destination bucket of any chunk on any rank (adaptive slot capacity)
+  kMetaOverflow = 7,  // sorted exchange: messages a rank answered STATUS_OVERFLOW this Send (MAX: any rank's)
   kMetaFlags = 8,   // words 8..15: 1 if method id (word - 8) occurs; word 15: ids >= 7
   kMetaWords = 16,
 };

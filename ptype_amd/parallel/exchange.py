@@ -52,7 +52,7 @@ import torch.distributed as dist
 
 from ..ops import batch as B
 from ..ops import raw_stream
-from ..ops.packed import META_CAP
+from ..ops.packed import META_CAP, META_WORDS
 from ..ops.records import STATUS_OVERFLOW, method_ordered
 from ..ops.table import RegistryTable
 from ..utils import trace
@@ -105,9 +105,12 @@ class ActorExchange:
     def __init__(self, table: RegistryTable, max_batch: int, chunks: int = 1, group=None, state=None,
                  delay_us: int = 0, slack: float = 0.01, fmt: B.WireFormat | None = None,
                  packed: bool | None = None, fake=None, delivery: str = "auto", mailbox_shards: int = 256,
-                 mailbox_slots: int = 0, mailbox_ordered: bool | None = None):
+                 mailbox_slots: int = 0, mailbox_ordered: bool | None = None, comm: str = "rccl",
+                 comm_timeout_s: float = 30.0):
         if delivery not in ("auto", "direct", "mailbox"):
             raise ValueError("delivery: 'auto', 'direct' or 'mailbox'")
+        if comm not in ("rccl", "ipc"):
+            raise ValueError("comm: 'rccl' (the process group's communicator) or 'ipc'")
         # How a message reaches its actor on the GPU that hosts it (world 1):
         #   direct  -- resolved and run in one streaming pass (no queue): stateless and
         #              commutative methods, and ordered ones as linearizable CAS updates
@@ -138,6 +141,13 @@ class ActorExchange:
             self.world = dist.get_world_size(group)
         else:
             self.rank, self.world = 0, 1
+        # comm="ipc": the native engines' collectives go through an IpcComm
+        # (csrc/hip/ipc_comm.hpp) -- one rank per process, peers' HBM imported by IPC
+        # handle -- over a group of any backend (gloo is enough: it only carries the
+        # handles and the host agreements).  It runs the multi-process pipeline where
+        # RCCL cannot: several ranks on one GPU.  Built below, once the geometry is agreed.
+        self.ipc = None
+        self.comm_kind = comm if fake is None and self.world > 1 else "rccl"
         # run the RCCL all-to-alls even on a single rank (validates the collective
         # path on a 1-GPU box; a 1-rank all-to-all is a device-local copy)
         self.force_collectives = bool(fake is None and dist.is_available() and dist.is_initialized()
@@ -147,7 +157,7 @@ class ActorExchange:
         # every rank must use the same slot geometry (equal-split all-to-all):
         # agree on the largest chunk and the chunk count once, collectively
         if self.world > 1 and fake is None:
-            t = torch.tensor([self.max_chunk, self.chunks], dtype=torch.int64, device=self.device)
+            t = torch.tensor([self.max_chunk, self.chunks], dtype=torch.int64, device=self._agree_device())
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             self.max_chunk, self.chunks = int(t[0]), int(t[1])
         self.C = capacity_for(self.max_chunk, self.world, slack)
@@ -173,6 +183,10 @@ class ActorExchange:
                         if self.adaptive else self.C)
         self.bufs = [_ChunkBufs(self.world, self.C_alloc, self.max_chunk, self.device, self.force_collectives,
                                 fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 8))]
+        if self.comm_kind == "ipc":
+            if not self.use_engine:
+                raise RuntimeError("comm='ipc' drives the native engines: it needs a GPU")
+            self.ipc = ipc_group_comm(self.group, self.device, self.ipc_cap_bytes(), comm_timeout_s)
         self.checksum = None  # optional int64[1] reply-value checksum (block-reduced)
         self.outbox = None  # DeviceOutbox that dispatched handlers send into (set by pump)
         # direct completion of self-directed messages (no reply staging, no
@@ -191,10 +205,40 @@ class ActorExchange:
         self._pump_graph = None  # (key, hipGraph of a group of device-pump epochs, its buffers)
         self.last_wire = None  # engine.last_wire() of the latest native send
         self._sorted = None  # _hip.SortedExchange: N > 1 mailbox delivery (csrc/hip/exchange_sorted.hpp)
+        self._last_sorted = False  # whether the last send() ran on it
+
+    def _agree_device(self) -> torch.device:
+        """Where host-level agreements' tensors live: CPU for a gloo group (its
+        CUDA collectives are not universally available), else the exchange's device."""
+        if self.device.type == "cuda" and dist.is_available() and dist.is_initialized():
+            if dist.get_backend(self.group) == "gloo":
+                return torch.device("cpu")
+        return self.device
+
+    def _sorted_c_alloc(self) -> int:
+        # the sorted exchange's buffers hold 2.5x the uniform share per peer (skewed
+        # traffic fits); the start-up capacity is the static mean + 8 sigma
+        room = float(os.environ.get("PTYPE_SORTED_ROOM", "2.5"))
+        return max(64, self.C, min(self.max_chunk, int(math.ceil(room * self.max_chunk / self.world))))
+
+    def ipc_cap_bytes(self) -> int:
+        """The largest region one collective moves per peer, over both native
+        engines: the sorted exchange's request regions (widest layout, 8 dwords per
+        record + the shard table: csrc/hip/packed.hpp packed_req_words,
+        exchange_sorted.hpp kSxTableWords), the epoch engine's v2 slots (3
+        arguments + a method column) and its agreement vector."""
+        c = self._sorted_c_alloc()
+        sorted_req = 4 * (((4 + c * 8 + 3) & ~3) + 68)
+        epoch_req = 4 * int(B.hip().wire_req_words(self.C_alloc, 3, True))
+        epoch_rep = 4 * int(B.hip().wire_rep_words(self.C_alloc))
+        agree = 8 * (META_WORDS + self.world * self.world * self.chunks)
+        return max(sorted_req, epoch_req, epoch_rep, agree)
 
     def _comm_ptr(self) -> int:
         """Raw ncclComm_t of the group's RCCL backend (0 without collectives)."""
         if self.world == 1 and not self.force_collectives:
+            return 0
+        if self.ipc is not None:
             return 0
         pg = self.group if self.group is not None else dist.group.WORLD
         try:
@@ -217,9 +261,10 @@ class ActorExchange:
         if self._engine is None:
             h = B.hip()
             dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-            if self.fake is not None:
+            if self.fake is not None or self.ipc is not None:
                 eng = h.EpochEngine(dev, 0, self.world, self.rank, self.C_alloc, self.max_chunk, self.chunks,
-                                    fake=self.fake[0], adaptive=self.adaptive, c_fixed=self.C)
+                                    fake=self.fake[0] if self.fake is not None else self.ipc,
+                                    adaptive=self.adaptive, c_fixed=self.C)
             else:
                 eng = h.EpochEngine(dev, self._comm_ptr(), self.world, self.rank, self.C_alloc, self.max_chunk,
                                     self.chunks, adaptive=self.adaptive, c_fixed=self.C)
@@ -257,8 +302,13 @@ class ActorExchange:
         """Mailbox delivery across ranks through the sorted exchange: the sender's
         counting sort by (destination rank, actor shard) fills the receivers'
         mailboxes directly, with no host wait per Send (csrc/hip/exchange_sorted.hpp).
-        PTYPE_SORTED_EXCHANGE=0 keeps the epoch engine's delivery on receipt."""
-        if self.delivery != "mailbox" or not self.use_engine or self.device.type != "cuda":
+        It is the N > 1 path of delivery "mailbox" and of "auto" (Join's default:
+        ordered methods keep per-(sender, actor) FIFO through its ordered drain,
+        stateless ones run in parallel) -- "direct" keeps the epoch engine's fused
+        dispatch.  PTYPE_SORTED_EXCHANGE=0 keeps the epoch engine everywhere."""
+        if self.delivery == "direct" or not self.use_engine or self.device.type != "cuda":
+            return False
+        if self.delivery == "auto" and self.world == 1:  # world 1: the fused local pass / world-1 mailboxes
             return False
         if self.outbox is not None or self.checksum is not None or self.chunks > 4:
             return False
@@ -270,11 +320,8 @@ class ActorExchange:
         if self._sorted is None:
             h = B.hip()
             dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-            # the buffers hold 2.5x the uniform share per peer (skewed traffic fits); the
-            # start-up capacity is the static mean + 8 sigma
-            room = float(os.environ.get("PTYPE_SORTED_ROOM", "2.5"))
-            c_alloc = max(64, self.C, min(self.max_chunk, int(math.ceil(room * self.max_chunk / self.world))))
-            fake = self.fake[0] if self.fake is not None else None
+            c_alloc = self._sorted_c_alloc()
+            fake = self.fake[0] if self.fake is not None else self.ipc
             self._sorted = h.SortedExchange(dev, 0 if fake is not None else self._comm_ptr(), self.world, self.rank,
                                             self.max_chunk, self.chunks, c_alloc, min(self.C, c_alloc), fake=fake)
             self._sorted_c_alloc = c_alloc
@@ -374,7 +421,8 @@ class ActorExchange:
         wq, wr = R * fmt.req_words(C), R * B.WireFormat.rep_words(C)
         self.counters.sent += M
         self.counters.epochs += n
-        if self.use_engine and self._use_sorted():
+        self._last_sorted = bool(self.use_engine and self._use_sorted())
+        if self._last_sorted:
             with trace.range("ptype.send.sorted"):
                 return self._send_sorted(req, out_val, out_status)
         if self.use_engine and self._engine is None:
@@ -555,6 +603,8 @@ class ActorExchange:
             agreed[h].copy_(own[h])
             if self.fake is not None:  # max over the ranks, on the device side of the comm
                 self.fake[0].allreduce_max(self.rank, agreed[h].data_ptr(), k + 1, stream)
+            elif self.ipc is not None:
+                self.ipc.allreduce_max(agreed[h].data_ptr(), k + 1, stream)
             else:
                 dist.all_reduce(agreed[h], op=dist.ReduceOp.MAX, group=self.group)
             host[h, 0].copy_(own[h], non_blocking=True)
@@ -688,9 +738,14 @@ class ActorExchange:
             return val, st
         for _ in range(max_epochs):
             over = st == STATUS_OVERFLOW
-            n_over = int(over.sum())
-            if self.world > 1:
-                n_over = self._agree_max(n_over)
+            if self._last_sorted:
+                # the sorted exchange folds every rank's overflow count into its own
+                # agreement all-reduce: one wait on that copy, no count pass, no collective
+                n_over = int(self._sorted.last_overflow())
+            else:
+                n_over = int(over.sum())
+                if self.world > 1:
+                    n_over = self._agree_max(n_over)
             if n_over == 0:
                 break
             idx = torch.nonzero(over).flatten()
@@ -710,6 +765,8 @@ class ActorExchange:
         if (self.world == 1 and not self.force_collectives and self._last_mailbox and self.mailboxes is not None
                 and getattr(self.mailboxes, "last_spills", False)):
             return True  # stateless mailbox Send: full rings spill to the drain (no STATUS_OVERFLOW)
+        if getattr(self, "_last_sorted", False):
+            return False  # the agreement that sized it is two Sends old: read this Send's count (send_all)
         if self._mailbox_on_receipt():
             # the slots fit, but K2 on receipt can still answer STATUS_OVERFLOW when a
             # receiver's rings fill (skewed traffic to one shard): count them
@@ -724,7 +781,7 @@ class ActorExchange:
         re-send rounds).  In-process FakeComm ranks agree through a barrier; the
         loopback stand-in is one rank that speaks for a symmetric node."""
         if self.fake is None:
-            t = torch.tensor([v], dtype=torch.int64, device=self.device)
+            t = torch.tensor([v], dtype=torch.int64, device=self._agree_device())
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             return int(t.item())
         fc = self.fake[0]
@@ -760,6 +817,19 @@ class ActorExchange:
             s.failed += m["failed"]
             s.mailbox = m
         return s
+
+
+def ipc_group_comm(group, device: torch.device, cap_bytes: int, timeout_s: float = 30.0):
+    """An ``_hip.IpcComm`` over the ranks of ``group`` (collective): every rank
+    allocates its receive segment, the IPC handles travel through the group
+    (``all_gather_object``; gloo is enough) and every rank imports the others'."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    c = B.hip().IpcComm(idx, world, rank, int(cap_bytes), float(timeout_s))
+    handles = [None] * world
+    dist.all_gather_object(handles, c.handle(), group=group)
+    c.connect(handles)
+    return c
 
 
 class _FakeAgree:

@@ -68,13 +68,39 @@ def test_bench_multi_gpu(nproc):
         pytest.skip(f"needs {nproc} GPUs (RCCL refuses two ranks on one device)")
     out = _run(nproc, ["--steps", "3", "--warmup", "2", "--rtt-calls", "200"], timeout=900)
     assert out["n_gpus"] == nproc and out["value"] > 0  # (the bench verifies every reply itself)
-    assert out["config"]["wire"] == "v3-packed" and out["config"]["exchange"] == "exact"
+    # the N > 1 mailbox path is the sorted exchange (csrc/hip/exchange_sorted.hpp): wire-v3
+    # records through padded RCCL all-to-alls at the capacity agreed two Sends earlier
+    c = out["config"]
+    assert c["wire"] == "v3-packed" and c["engine"] == "sorted" and c["exchange"] == "padded", c
+    assert c["comm"] == "rccl" and c["record_bytes"] <= 8
     assert out["p50_rtt_remote_us"] is not None and out["diag"]["a2a_only_ms_per_step"] > 0
     assert out["rtt_error"] is None and out["rtt_remote_request_ring"] == "device"
-    # skewed traffic through the exact-size exchange: no re-send rounds
-    z = _run(nproc, ["--steps", "3", "--warmup", "1", "--rtt-calls", "0", "--zipf", "1.1", "--no-secondary"],
+    # skewed traffic: once the agreement of Send k - 2 sizes the regions (from Send 2 on),
+    # no re-send rounds -- the warm-up's start-up Sends may re-send, the timed ones must not
+    z = _run(nproc, ["--steps", "3", "--warmup", "3", "--rtt-calls", "0", "--zipf", "1.1", "--no-secondary"],
              timeout=900)
-    assert z["config"]["resend_rounds"] == 0 and z["value"] > 0
+    assert z["config"]["resend_rounds"] == 0 and z["value"] > 0, z["config"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_multi_process_on_one_gpu_ipc(nproc):
+    """The bench's N > 1 path across real processes on ONE GPU:
+    torchrun ranks, a gloo group for the host side, the sorted exchange's
+    all-to-alls and agreement through IpcComm (peers' HBM by IPC handle) --
+    every reply verified by the bench itself, the cross-process RTT through the
+    next rank's dispatcher ring, and skewed (Zipf) traffic without re-sends once
+    the agreement applies."""
+    small = ["--msgs-per-gpu", str(1 << 18), "--actors-per-gpu", "8192", "--comm", "ipc"]
+    out = _run(nproc, ["--steps", "4", "--warmup", "3", "--rtt-calls", "200", "--no-secondary"] + small,
+               timeout=600, launcher="self")
+    c = out["config"]
+    assert out["n_gpus"] == nproc and out["value"] > 0
+    assert c["comm"] == "ipc" and c["engine"] == "sorted" and c["wire"] == "v3-packed" and c["record_bytes"] <= 8
+    assert out["rtt_error"] is None and out["p50_rtt_remote_us"] > 0
+    z = _run(nproc, ["--steps", "4", "--warmup", "3", "--rtt-calls", "0", "--zipf", "1.1", "--no-secondary"] + small,
+             timeout=600, launcher="self")
+    assert z["config"]["resend_rounds"] == 0 and z["value"] > 0, z["config"]
 
 
 @pytest.mark.gpu
