@@ -470,22 +470,50 @@ __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView m
   const uint64_t Q = 1ull << mv.log_q;
   unsigned long long timeouts = 0;
   int sp = 0;
-  for (uint32_t s = threadIdx.x; s < S; s += kST) {
-    uint32_t c = 0;
+  // Up to 64 shards (the stateless 16-shard view): W = kST / S lanes per shard, the
+  // whole block looking back W tiles per round trip (lookback_group); more shards:
+  // one lane per shard, kLbWin tiles per round trip.
+  const uint32_t W = S <= kST / 8 ? min(64u, kST / S) : 1u;
+  uint32_t* tcnt = pre;  // (W > 1) the tile's count per shard, until pre[] takes the prefix
+  if (W > 1) {
+    for (uint32_t s = threadIdx.x; s < S; s += kST) {
+      uint32_t c = 0;
 #pragma unroll
-    for (int ww = 0; ww < kST / kWave; ++ww) {
-      const uint32_t x = wcnt(ww, s);
-      wcnt(ww, s) = c;
-      c += x;
+      for (int ww = 0; ww < kST / kWave; ++ww) {
+        const uint32_t x = wcnt(ww, s);
+        wcnt(ww, s) = c;
+        c += x;
+      }
+      tcnt[s] = c;
+      __hip_atomic_exchange(desc + (size_t)t * S + s, desc_word(tag, t == 0 ? kDescP : kDescA, c), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
     }
-    unsigned long long* d = desc + (size_t)t * S + s;
+    __syncthreads();
+  }
+  for (uint32_t s = W > 1 ? threadIdx.x / W : threadIdx.x; s < S; s += W > 1 ? S : kST) {
+    uint32_t c = 0;
     uint64_t excl = 0;
-    if (t == 0) {
-      __hip_atomic_exchange(d, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long* d = desc + (size_t)t * S + s;
+    if (W > 1) {
+      c = tcnt[s];
+      if (t > 0) excl = lookback_group(desc + s, S, (int64_t)t - 1, tag, W, timeouts);
+      if ((threadIdx.x & (W - 1)) != 0) continue;  // one lane per shard from here
+      if (t > 0)
+        __hip_atomic_exchange(d, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      __hip_atomic_exchange(d, desc_word(tag, kDescA, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      excl = lookback(desc + s, S, (int64_t)t - 1, tag, timeouts);
-      __hip_atomic_exchange(d, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int ww = 0; ww < kST / kWave; ++ww) {
+        const uint32_t x = wcnt(ww, s);
+        wcnt(ww, s) = c;
+        c += x;
+      }
+      if (t == 0) {
+        __hip_atomic_exchange(d, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_exchange(d, desc_word(tag, kDescA, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        excl = lookback(desc + s, S, (int64_t)t - 1, tag, timeouts);
+        __hip_atomic_exchange(d, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     if (t == in.tiles - 1) gsum[s] = (uint32_t)(excl + c);  // the epoch's total of shard s
     const uint64_t tl = *ctr_tail(mv, s), hd = *ctr_head(mv, s);

@@ -193,6 +193,44 @@ __device__ __forceinline__ uint64_t lookback(unsigned long long* col, uint32_t s
   }
   return excl;
 }
-
+// The same sum with W lanes per column (W = 8, 16, 32 or 64; lane groups aligned
+// inside a wave, all lanes of a group call it together): lane j of the group
+// reads tile q - j, so one round trip covers W predecessors instead of kLbWin.
+// The one-pass mailbox sort runs 16 columns (the stateless view) on its 512
+// threads: 32 lanes each.  Every lane of the group returns the group's sum.
+__device__ __forceinline__ uint64_t lookback_group(unsigned long long* col, uint32_t stride, int64_t q, uint32_t tag,
+                                                   uint32_t W, unsigned long long& timeouts) {
+  const uint32_t lane = lane_id(), j = lane & (W - 1), gbase = lane & ~(W - 1);
+  const uint64_t full = W >= 64 ? ~0ull : (1ull << W) - 1;
+  uint64_t excl = 0;
+  uint32_t spins = 0;
+  for (;;) {
+    const int64_t qq = q - (int64_t)j;
+    const uint64_t x = qq >= 0 ? __hip_atomic_fetch_add(col + (size_t)qq * stride, 0ull, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                               : desc_word(tag, kDescP, 0);  // before tile 0: 0
+    const bool pub = (uint32_t)(x >> 40) == tag;
+    const uint64_t pubm = (__ballot(pub) >> gbase) & full;
+    const uint64_t pm = (__ballot(pub && (x & kDescP)) >> gbase) & full;
+    const uint64_t unpub = ~pubm & full;
+    const uint32_t first_unpub = unpub ? (uint32_t)__builtin_ctzll(unpub) : W;
+    const uint32_t first_p = pm ? (uint32_t)__builtin_ctzll(pm) : W;
+    const bool fin = first_p < first_unpub;
+    const uint32_t n = fin ? first_p + 1 : first_unpub;  // entries summed this round
+    uint64_t v = j < n ? (x & kDescVal) : 0ull;
+    for (uint32_t off = W >> 1; off > 0; off >>= 1) v += __shfl_xor(v, (int)off);
+    excl += v;
+    if (fin) break;
+    q -= (int64_t)n;
+    if (n < W) {  // an unpublished predecessor: poll it again
+      if (++spins > kLookbackSpins) {
+        if (j == 0) ++timeouts;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  return excl;
+}
 
 }  // namespace ptype
