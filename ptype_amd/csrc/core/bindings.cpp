@@ -329,6 +329,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("mailbox_slots", &GpuConfig::mailbox_slots)
       .def_readwrite("elastic", &GpuConfig::elastic)
       .def_readwrite("delivery", &GpuConfig::delivery)
+      .def_readwrite("comm", &GpuConfig::comm)
       .def_readwrite("form_group", &GpuConfig::form_group)
       .def_readwrite("group_timeout_s", &GpuConfig::group_timeout_s)
       .def_readwrite("grace_s", &GpuConfig::grace_s)

@@ -131,6 +131,7 @@ void decode_ptype(const YNode& root, Config& c) {
         else if (g.first == "watch") c.gpu.watch = want_bool(G, g.first, g.second);
         else if (g.first == "elastic") c.gpu.elastic = want_bool(G, g.first, g.second);
         else if (g.first == "delivery") c.gpu.delivery = want_string(G, g.first, g.second);
+        else if (g.first == "comm") c.gpu.comm = want_string(G, g.first, g.second);
         else if (g.first == "form_group") c.gpu.form_group = want_bool(G, g.first, g.second);
         else if (g.first == "group_timeout_s") c.gpu.group_timeout_s = want_float(G, g.first, g.second);
         else if (g.first == "grace_s") c.gpu.grace_s = want_float(G, g.first, g.second);
@@ -142,6 +143,7 @@ void decode_ptype(const YNode& root, Config& c) {
       if (c.gpu.world < 0) fail(Errc::kConfig, "gpu.world must be >= 0");
       if (c.gpu.delivery != "auto" && c.gpu.delivery != "mailbox" && c.gpu.delivery != "direct")
         fail(Errc::kConfig, "gpu.delivery must be auto, mailbox or direct");
+      if (c.gpu.comm != "rccl" && c.gpu.comm != "ipc") fail(Errc::kConfig, "gpu.comm must be rccl or ipc");
       if (c.gpu.ring == 0 || (c.gpu.ring & (c.gpu.ring - 1)))
         fail(Errc::kConfig, "gpu.ring must be a power of two");
     }

@@ -66,7 +66,7 @@ class DeviceRuntime:
     def __init__(self, device=None, actors: int = 1024, ring: int = 4096, idle_ms: float = 200.0,
                  delay_us: int = 0, max_batch: int = 1 << 20, chunks: int = 0, random_state: bool = False,
                  group=None, shm: bool = True, service: str = "", mailbox_shards: int = 256,
-                 mailbox_slots: int = 0, delivery: str = "auto"):
+                 mailbox_slots: int = 0, delivery: str = "auto", comm: str = "rccl", comm_timeout_s: float = 30.0):
         if device is None:
             device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         self.device = torch.device(device)
@@ -117,6 +117,9 @@ class DeviceRuntime:
         self._watchdog = None
         self.mailbox_shards, self.mailbox_slots = int(mailbox_shards), int(mailbox_slots)
         self.delivery = delivery or "auto"  # "mailbox": every Send through the HBM mailboxes (ActorExchange)
+        # N > 1 collectives: the group's RCCL communicator, or IpcComm ("ipc": peers' HBM by
+        # IPC handle over a gloo group -- several ranks may share one GPU)
+        self.comm, self.comm_timeout_s = comm or "rccl", float(comm_timeout_s)
         self._exchange = None
         self.shards: dict[str, list[dict]] = {}
         self.mirror = None  # RegistryMirror (watch-driven) once attached to a control plane
@@ -156,7 +159,7 @@ class DeviceRuntime:
             me = node_id(core_cluster.local_addr, cfg.port)
             registry = Registry(core_cluster.registry)
             nodes = wait_nodes(registry, cfg.service_name, max(g.world, 1))
-            backend = g.backend or ("gloo" if g.cpu else "nccl")
+            backend = g.backend or ("gloo" if g.cpu or g.comm == "ipc" else "nccl")
             store = KVStore(core_cluster.store)
             if backend == "nccl":  # a failed collective aborts the communicator instead of the process
                 os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
@@ -167,7 +170,8 @@ class DeviceRuntime:
         rank = d.get_rank() if d else 0
         rt = cls(device_for_rank(rank), actors=g.actors, ring=g.ring, idle_ms=g.idle_ms, delay_us=g.delay_us,
                  max_batch=g.max_batch, service=cfg.service_name, mailbox_shards=g.mailbox_shards,
-                 mailbox_slots=g.mailbox_slots, delivery=g.delivery)
+                 mailbox_slots=g.mailbox_slots, delivery=g.delivery, comm=g.comm,
+                 comm_timeout_s=g.group_timeout_s)
         rt._tcp_store, rt._owns_group = tcp, owns
         rt._addr = (core_cluster.local_addr, int(cfg.port))
         if members is not None and g.elastic:
@@ -258,7 +262,9 @@ class DeviceRuntime:
 
             self._exchange = ActorExchange(self.table, self.max_batch, chunks=self.chunks, group=self.group,
                                            state=self.state, delay_us=self.delay_us, delivery=self.delivery,
-                                           mailbox_shards=self.mailbox_shards, mailbox_slots=self.mailbox_slots)
+                                           mailbox_shards=self.mailbox_shards, mailbox_slots=self.mailbox_slots,
+                                           comm=self.comm if self.on_gpu else "rccl",
+                                           comm_timeout_s=self.comm_timeout_s)
         return self._exchange
 
     # ------------------------------------------------------------------ data plane
@@ -335,6 +341,10 @@ class DeviceRuntime:
                     raise RankFailure(self._watchdog.failed)
                 sub = batch if todo is None else batch.index_select(todo)
                 out = self.exchange.send_all(sub) if resend_overflow else self.exchange.send(sub)
+                ipc = self.exchange.ipc
+                if ipc is not None:  # IpcComm: a peer that missed a collective is seen once the Send's waits end
+                    torch.cuda.current_stream(self.device).synchronize()
+                    ipc.check()
             except RuntimeError as e:
                 # only a peer's failure re-forms the group; a local error (OOM, a launch
                 # failure, a stalled look-back) propagates unchanged -- recovering from it
@@ -391,11 +401,15 @@ class DeviceRuntime:
             return
         src = next(n for n in m["members"] if buddy(m["nodes0"], m["members"], n) == m["me"])
         P = self.actors
-        recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=self.device)
-        ops = [dist.P2POp(dist.isend, self.state, m["members"].index(dst)),
+        # a gloo group (CPU runtimes, comm="ipc") moves host tensors
+        host = self.on_gpu and dist.get_backend(self.group) == "gloo"
+        io_dev = torch.device("cpu") if host else self.device
+        recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=io_dev)
+        ops = [dist.P2POp(dist.isend, self.state.to(io_dev), m["members"].index(dst)),
                dist.P2POp(dist.irecv, recv, m["members"].index(src))]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
+        recv = recv.to(self.device)
         self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(own[src])}
 
     def recover(self) -> list[int]:
