@@ -412,6 +412,27 @@ def main():
                     else "Calculator.Multiply"
             del ex3
 
+    # BASELINE configs 4 and 5 and the public API path, under the same clock (utils/benchmarks.py)
+    if not args.no_secondary and args.steps and use_gpu and fake is None:
+        from ptype_amd.utils import benchmarks as BM
+
+        def max_over_ranks(x):
+            if not dist_on:
+                return x
+            tt = torch.tensor([x], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            return float(tt.item())
+
+        secondaries["optimus_fanout"] = BM.optimus_fanout(table, n_actors, device, args.steps, max(1, args.warmup),
+                                                          rank=rank, world=world, chunks=chunks,
+                                                          comm="ipc" if ipc else "rccl",
+                                                          barrier=barrier if dist_on else None,
+                                                          max_over_ranks=max_over_ranks)
+        if world == 1 and not dist_on:
+            secondaries["registry_1m"] = BM.registry_1m(device)
+            secondaries["api_send"] = BM.api_send(device, sorted({M, min(M, 1 << 20)}, reverse=True),
+                                                  args.actors_per_gpu, args.steps, max(1, args.warmup))
+
     # diagnostics, outside the timed region: the step's all-to-all byte volume moved
     # by RCCL alone (same chunking, same per-peer sizes), so a multi-GPU line says
     # whether the step is bound by xGMI or by the kernels around it

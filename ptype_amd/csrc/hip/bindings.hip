@@ -68,6 +68,8 @@ int64_t route_fused_grid(int64_t, int64_t*);
 void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uint32_t, uintptr_t, uintptr_t);
 void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 int64_t wire_req_words(int64_t, int, bool);
+void launch_prime_gather(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t,
+                         uintptr_t);
 int64_t wire_rep_words(int64_t);
 void launch_packed_meta(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int, int64_t, uint32_t, uint32_t,
                         uintptr_t, uintptr_t);
@@ -182,6 +184,9 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("wire_req_words", &wire_req_words, py::arg("C"), py::arg("nargs"), py::arg("mc"));
   m.def("wire_rep_words", &wire_rep_words, py::arg("C"));
+  m.def("prime_gather", &launch_prime_gather, py::arg("val"), py::arg("st"), py::arg("first"), py::arg("n"),
+        py::arg("target"), py::arg("T"), py::arg("out"), py::arg("out_st"), py::arg("scanned"), py::arg("stream"),
+        "optimus watchReplies on the device: per target, the first non-target reply of its ranges (early exit)");
   m.def("roctx_available", [] { return roctx().push != nullptr; });
   m.def("roctx_push", [](const std::string& s) { return roctx().push ? roctx().push(s.c_str()) : -1; });
   m.def("roctx_pop", [] { return roctx().pop ? roctx().pop() : -1; });

@@ -96,16 +96,68 @@ def make_batch(target: int, n_actors: int, device) -> MsgBatch:
                                                                              device=device), METHOD_PRIME_CHECK)
 
 
+class FanOut:
+    """The coordinator for many targets at once (BASELINE config 4): every
+    target's 10-wide ranges (splitWork, coordinator.go:67-73) in ONE batch,
+    range r of the batch to actor r % n_actors, and the gather (watchReplies,
+    :91-98) on the device -- ``csrc/hip/optimus.hip``: one wave per target scans
+    its ranges in order and stops at the first non-target reply."""
+
+    def __init__(self, targets: torch.Tensor, n_actors: int, device):
+        device = torch.device(device)
+        tg = targets.to(device=device, dtype=torch.int64)
+        self.targets, self.T, self.device = tg, int(tg.numel()), device
+        self.n = (tg + 9) // 10  # ranges per target: i = 10, 20, ... < target + 10
+        self.M = int(self.n.sum()) if self.T else 0
+        tid = torch.repeat_interleave(torch.arange(self.T, device=device), self.n)
+        self.first = torch.cumsum(self.n, 0) - self.n
+        k = torch.arange(self.M, device=device) - self.first[tid]
+        lo = torch.where(k == 0, torch.full_like(k, 2), k * 10)
+        actors = (torch.arange(self.M, device=device) % max(1, n_actors)).to(torch.int32)
+        self.batch = MsgBatch(actors, lo, (k + 1) * 10, tg[tid], METHOD_PRIME_CHECK)
+        self.answer = torch.empty(self.T, dtype=torch.int64, device=device)
+        self.status = torch.empty(self.T, dtype=torch.int32, device=device)
+
+    def gather(self, val: torch.Tensor, st: torch.Tensor):
+        """Per target: its smallest divisor (the first non-target reply in range
+        order) or the target itself; a failed range's status in ``status``."""
+        if self.device.type == "cuda":
+            from ..ops import hip, raw_stream
+
+            hip().prime_gather(val.data_ptr(), st.data_ptr(), self.first.data_ptr(), self.n.data_ptr(),
+                               self.targets.data_ptr(), self.T, self.answer.data_ptr(), self.status.data_ptr(), 0,
+                               raw_stream(self.device))
+            return self.answer, self.status
+        return gather_ref(val, st, self.first, self.n, self.targets)
+
+
+def gather_ref(val, st, first, n, targets):
+    """Host reference of the device gather (same decision per target)."""
+    ans = targets.clone()
+    status = torch.zeros(targets.numel(), dtype=torch.int32)
+    for j in range(targets.numel()):
+        f, c, t = int(first[j]), int(n[j]), int(targets[j])
+        for i in range(f, f + c):
+            if int(st[i]) != STATUS_OK:
+                status[j] = int(st[i])
+                break
+            if int(val[i]) != t:
+                ans[j] = int(val[i])
+                break
+    return ans, status
+
+
 def check_device(runtime, target: int) -> int:
-    """One batched Send + a device-side gather (smallest divisor found).  The
-    prime workers are co-hosted on the runtime's GPU actors."""
+    """One batched Send + the device-side gather (the first non-target reply in
+    range order: the smallest divisor).  The prime workers are co-hosted on the
+    runtime's GPU actors."""
     runtime.host(SERVICE)
-    batch = make_batch(target, runtime.total_actors, runtime.device)
-    val, st = runtime.send(SERVICE, batch)
-    if not bool((st == STATUS_OK).all()):
+    f = FanOut(torch.tensor([target], dtype=torch.int64), runtime.total_actors, runtime.device)
+    val, st = runtime.send(SERVICE, f.batch)
+    ans, status = f.gather(val, st)
+    if int(status[0]) != STATUS_OK:
         raise RuntimeError("prime check failed on device")
-    divisors = torch.where(val != target, val, torch.full_like(val, target))
-    return int(divisors.min().item()) if divisors.numel() else target
+    return int(ans[0])
 
 
 class Coordinator:

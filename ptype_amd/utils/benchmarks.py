@@ -1,0 +1,203 @@
+"""Secondary measurements of ``bench.py`` (BASELINE.json configs 4 and 5, and the
+public API path), each a dict that bench.py puts under ``secondaries``.
+
+* ``registry_1m``: the 1M-actor GPU registry mirror (K5 inserts / updates /
+  lookups, K5b directory build, K6 sweep scan) and its snapshot into pinned host
+  DRAM (K7) and restore -- BASELINE config 5 (reference: the etcd keyspace of
+  cluster/registry.go:51-86, here mirrored in HBM).
+* ``optimus_fanout``: the optimus coordinator for many targets per step -- one
+  Send of every target's 10-wide ranges (coordinator.go:67-73) through the
+  node's data plane (the sorted exchange at N > 1) and the device gather
+  (coordinator.go:91-98, csrc/hip/optimus.hip) -- BASELINE config 4, with the
+  reference's 250 ms per-candidate delay set to 0 as BASELINE.md prescribes.
+* ``api_send``: ``Join -> NewClient -> Client.Send`` eager, the whole public
+  API path (control-plane member, registry mirror apply, send_all) around the
+  same mailbox Send as the headline.
+
+Every timing brackets its steps with device synchronisation (and, with a
+process group, barriers) and verifies the replies outside the timed loop."""
+from __future__ import annotations
+
+import os
+import socket
+import tempfile
+import time
+
+import torch
+
+
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def timed(step, steps: int, warmup: int, device, barrier=None) -> float:
+    """Seconds for ``steps`` calls of ``step`` after ``warmup`` untimed ones."""
+    for _ in range(warmup):
+        step()
+    _sync(device)
+    if barrier:
+        barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    _sync(device)
+    if barrier:
+        barrier()
+    return time.perf_counter() - t0
+
+
+# ---------------------------------------------------------------------------- config 5
+def registry_1m(device, n: int = 1 << 20, reps: int = 5) -> dict:
+    from ..ops.table import RegistryTable, actor_keys
+
+    out = {"config": "1M-actor GPU registry mirror + snapshot to pinned host DRAM", "actors": n}
+    keys = actor_keys(torch.arange(n, dtype=torch.int64)).to(device)
+    ranks = (torch.arange(n, device=device) % 8).to(torch.int32)
+    mbox = (torch.arange(n, device=device) // 8).to(torch.int32)
+    exp = torch.full((n,), 1 << 40, dtype=torch.int64, device=device)
+    ins = []
+    t = None
+    for _ in range(reps):  # inserts into an empty table (allocation outside the timed region)
+        t = RegistryTable(2 * n, device=device)
+        _sync(device)
+        t0 = time.perf_counter()
+        t.upsert(keys, ranks, mbox, exp)
+        _sync(device)
+        ins.append(time.perf_counter() - t0)
+    out["insert_ops_per_s"] = n / min(ins)
+    out["update_ops_per_s"] = n / (timed(lambda: t.upsert(keys, ranks, mbox, exp), reps, 1, device) / reps)
+    q = keys[torch.randperm(n, device=device)]
+    out["lookup_ops_per_s"] = n / (timed(lambda: t.lookup(q), reps, 1, device) / reps)
+    t.enable_directory(n)
+
+    def build_dir():
+        t._dir_dirty = True
+        t.directory()
+
+    out["directory_build_ms"] = timed(build_dir, reps, 1, device) / reps * 1e3
+    out["sweep_scan_ms"] = timed(lambda: t.sweep(1), reps, 1, device) / reps * 1e3
+    side = torch.cuda.Stream(device)
+    h_ent, h_exp = t.snapshot_to_host(side)  # pinned buffers allocated once, reused
+    els = []
+    for _ in range(reps):
+        _sync(device)
+        t0 = time.perf_counter()
+        h_ent, h_exp = t.snapshot_to_host(side)
+        els.append(time.perf_counter() - t0)
+    nbytes = h_ent.numel() * 8 + h_exp.numel() * 8
+    out["snapshot_bytes"] = nbytes
+    out["snapshot_to_pinned_ms"] = min(els) * 1e3
+    out["snapshot_gb_per_s"] = nbytes / min(els) / 1e9
+    rest = []
+    for _ in range(3):
+        t2 = RegistryTable(2 * n, device=device)
+        _sync(device)
+        t0 = time.perf_counter()
+        t2.load_packed(h_ent, h_exp)
+        _sync(device)
+        rest.append(time.perf_counter() - t0)
+        if t2.live != n:
+            raise RuntimeError(f"registry restore: {t2.live} of {n} entries")
+    out["restore_ms"] = min(rest) * 1e3
+    if not all(torch.equal(a, b) for a, b in zip(t.lookup(q), t2.lookup(q))):
+        raise RuntimeError("registry restore: lookups differ from the snapshotted table")
+    return out
+
+
+# ---------------------------------------------------------------------------- config 4
+def optimus_fanout(table, n_actors: int, device, steps: int, warmup: int, rank: int = 0, world: int = 1,
+                   targets: int = 1024, base: int = 80_001, chunks: int = 1, comm: str = "rccl", barrier=None,
+                   max_over_ranks=None) -> dict:
+    """``targets`` odd numbers per rank from ``base`` (distinct per rank), every
+    one split into 10-wide ranges and answered by the Prime.Check actors of the
+    whole node; the answers are checked against trial division on a sample."""
+    from ..models.optimus import FanOut
+    from ..ops.records import STATUS_OK
+    from ..parallel.exchange import ActorExchange
+
+    tg = torch.arange(targets, dtype=torch.int64) * 2 + base + rank * 2 * targets
+    f = FanOut(tg, n_actors, device)
+    ex = ActorExchange(table, f.M, chunks=chunks, delivery="mailbox", mailbox_ordered=False, comm=comm)
+    val = torch.empty(f.M, dtype=torch.int64, device=device)
+    st = torch.empty(f.M, dtype=torch.int32, device=device)
+
+    def step():
+        ex.send(f.batch, val, st)
+        f.gather(val, st)
+
+    step()
+    _sync(device)
+    if not bool((f.status == STATUS_OK).all()):
+        raise RuntimeError("optimus fan-out: a range failed")
+    for j in range(0, targets, max(1, targets // 32)):
+        t = int(tg[j])
+        want = next((d for d in range(2, int(t ** 0.5) + 2) if t % d == 0 and d < t), t)
+        if int(f.answer[j]) != want:
+            raise RuntimeError(f"optimus fan-out: target {t} answered {int(f.answer[j])}, expected {want}")
+    el = timed(step, steps, warmup, device, barrier)
+    if max_over_ranks is not None:
+        el = max_over_ranks(el)
+    return {"config": "example/optimus fan-out + device gather (delay 0)", "targets_per_gpu_per_step": targets,
+            "ranges_per_gpu_per_step": f.M, "value": f.M * world * steps / el,
+            "unit": "ranges/s (Prime.Check messages, whole node)", "targets_per_s": targets * world * steps / el,
+            "ms_per_step": el / steps * 1e3, "delivery": "mailbox" + (" (sorted exchange)" if world > 1 else ""),
+            "gather": "device (first non-target reply per target, early exit)"}
+
+
+# ---------------------------------------------------------------------------- public API
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def api_send(device, sizes, actors: int, steps: int, warmup: int) -> dict:
+    """Join (one control-plane member, GPU runtime, lease-attached shard, registry
+    mirror) -> NewClient -> Client.Send of pre-generated batches, eager, through
+    the HBM mailboxes (gpu.delivery: mailbox)."""
+    from .. import cluster as C
+    from ..ops import batch as B
+    from ..ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
+
+    os.environ.setdefault("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    pp, pc = _port(), _port()
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "calculator", "bench", _port()
+    cfg.member = C.member_config(name="b0", dir=tempfile.mkdtemp(prefix="ptype_bench_"),
+                                 lpurls=[f"http://127.0.0.1:{pp}"], apurls=[f"http://127.0.0.1:{pp}"],
+                                 lcurls=[f"http://127.0.0.1:{pc}"], acurls=[f"http://127.0.0.1:{pc}"],
+                                 initial_cluster=f"b0=http://127.0.0.1:{pp}", unsafe_no_fsync=True)
+    cfg.has_gpu = True
+    g = cfg.gpu
+    g.device, g.actors, g.max_batch, g.delivery = device.index or 0, actors, max(sizes), "mailbox"
+    t0 = time.perf_counter()
+    c = C.Join(C.background(), cfg)
+    out = {"path": "Join -> NewClient -> Client.Send (eager, mailbox delivery, pre-generated batches)",
+           "join_s": time.perf_counter() - t0}
+    try:
+        client = c.NewClient("calculator", C.ConnConfig(retries=0, allow_local=False))
+        for M in sizes:
+            batches = [B.gen_requests(M, actors, METHOD_CALC_MULTIPLY, seed=11 + k, device=device) for k in range(2)]
+            res = {}
+            k = [0]
+
+            def step():
+                b = batches[k[0] & 1]
+                k[0] += 1
+                th = time.perf_counter()
+                res["out"] = client.Send(b)
+                res["host"] = res.get("host", 0.0) + time.perf_counter() - th
+                res["b"] = b
+
+            el = timed(step, steps, warmup, device)
+            host_us = res["host"] / (steps + warmup) * 1e6
+            v, s = res["out"]
+            if not (bool((s == STATUS_OK).all()) and torch.equal(v, res["b"].a0 * res["b"].a1)):
+                raise RuntimeError("api_send: verification failed")
+            out[f"{M}"] = {"msgs_per_step": M, "value": M * steps / el, "ms_per_step": el / steps * 1e3,
+                           "host_us_per_send": host_us}
+        client.Close()
+    finally:
+        c.Close()
+    return out

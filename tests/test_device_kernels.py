@@ -615,3 +615,28 @@ def test_gpu_records_to_soa(mfma):
     torch.cuda.synchronize()
     assert torch.equal(out.actor.cpu(), ref.actor) and torch.equal(out.method.cpu(), ref.method)
     assert torch.equal(out.a0.cpu(), ref.a0) and torch.equal(out.a1.cpu(), ref.a1) and torch.equal(out.a2.cpu(), ref.a2)
+
+
+@pytest.mark.gpu
+def test_prime_gather_kernel_matches_reference():
+    """csrc/hip/optimus.hip: the device gather (one wave per target, early exit at
+    the first deciding reply) equals the host reference, failed statuses included."""
+    import torch
+
+    from ptype_amd.models.optimus import FanOut, gather_ref
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.records import METHOD_PRIME_CHECK
+
+    g = torch.Generator().manual_seed(4)
+    targets = torch.randint(2, 200_000, (3000,), generator=g)
+    f = FanOut(targets, 4096, "cuda")
+    b = f.batch
+    val, st = B._handler_ref(torch.full((f.M,), METHOD_PRIME_CHECK), b.actor.long().cpu(), b.a0.cpu(), b.a1.cpu(),
+                             b.a2.cpu(), None)
+    st = st.to(torch.int32)
+    st[torch.randint(0, f.M, (50,), generator=g)] = 3  # a few failed ranges
+    ans, status = f.gather(val.cuda(), st.cuda())
+    ref_a, ref_s = gather_ref(val, st, f.first.cpu(), f.n.cpu(), f.targets.cpu())
+    torch.cuda.synchronize()
+    ok = ref_s == 0
+    assert torch.equal(status.cpu(), ref_s) and torch.equal(ans.cpu()[ok], ref_a[ok])

@@ -119,3 +119,20 @@ def test_optimus_fan_out_over_workers(tmp_path, ports):
             c.Close()
         for s in servers:
             s.Close()
+
+
+def test_optimus_fanout_gather_reference():
+    """FanOut: every target's splitWork ranges in one batch; the gather returns the
+    first non-target reply in range order (the smallest divisor) or the target."""
+    import torch
+
+    from ptype_amd.models.optimus import FanOut
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.records import METHOD_PRIME_CHECK
+
+    f = FanOut(torch.tensor([221, 97, 100, 1009 * 1013, 2]), 64, "cpu")
+    b = f.batch
+    assert f.M == sum((t + 9) // 10 for t in (221, 97, 100, 1009 * 1013, 2))
+    val, st = B._handler_ref(torch.full((f.M,), METHOD_PRIME_CHECK), b.actor.long(), b.a0, b.a1, b.a2, None)
+    ans, status = f.gather(val, st.to(torch.int32))
+    assert ans.tolist() == [13, 97, 2, 1009, 2] and status.tolist() == [0] * 5
