@@ -81,6 +81,11 @@ std::shared_ptr<ShmSegment> ShmSegment::attach(const std::string& name) {
   return s;
 }
 
+void ShmSegment::unlink_now() {
+  shm_unlink(name_.c_str());
+  unlink_ = false;
+}
+
 ShmSegment::~ShmSegment() {
   if (base_) munmap(base_, size_);
   if (unlink_) shm_unlink(name_.c_str());

@@ -155,6 +155,9 @@ class ShmSegment {
   size_t size() const { return size_; }
   const std::string& name() const { return name_; }
   void unlink_on_close() { unlink_ = true; }
+  // Remove the name now (every peer has attached): the mappings stay valid, and a
+  // process killed later leaves nothing behind in /dev/shm.
+  void unlink_now();
 
  private:
   std::string name_;

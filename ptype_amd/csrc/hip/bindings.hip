@@ -297,19 +297,13 @@ PYBIND11_MODULE(_hip, m) {
 
   py::class_<IpcComm, HostComm, std::shared_ptr<IpcComm>>(
       m, "IpcComm",
-      "one rank per PROCESS: collectives through peers' HBM segments imported by IPC handle, stream-ordered on "
-      "the device (csrc/hip/ipc_comm.hpp)")
-      .def(py::init<int, int, int, size_t, double>(), py::arg("device"), py::arg("R"), py::arg("rank"),
-           py::arg("cap_bytes"), py::arg("timeout_s") = 30.0)
-      .def("handle", [](const IpcComm& c) { return py::bytes(c.handle()); })
-      .def(
-          "connect",
-          [](IpcComm& c, const std::vector<py::bytes>& hs) {
-            std::vector<std::string> v;
-            for (const auto& h : hs) v.push_back(std::string(h));
-            c.connect(v);
-          },
-          py::arg("handles"))
+      "one rank per PROCESS: collectives through shared-memory segments every rank maps and registers, "
+      "stream-ordered on the device (csrc/hip/ipc_comm.hpp)")
+      .def(py::init<int, int, int, size_t, double, const std::string&>(), py::arg("device"), py::arg("R"),
+           py::arg("rank"), py::arg("cap_bytes"), py::arg("timeout_s"), py::arg("name"))
+      .def("handle", &IpcComm::handle, "this rank's segment name")
+      .def("connect", &IpcComm::connect, py::arg("names"))
+      .def("seal", &IpcComm::seal, "remove this rank's segment name (after every rank connected)")
       .def_property_readonly("failed", &IpcComm::failed)
       .def_property_readonly("ops", &IpcComm::ops)
       .def_property_readonly("rank", &IpcComm::rank)

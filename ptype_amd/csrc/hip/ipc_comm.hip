@@ -1,5 +1,5 @@
-// IpcComm (ipc_comm.hpp): process-to-process collectives through IPC-imported
-// HBM segments, stream-ordered on the device.
+// IpcComm (ipc_comm.hpp): process-to-process collectives through shared-memory
+// segments every rank maps and registers, stream-ordered on the device.
 #include "ipc_comm.hpp"
 
 #include <algorithm>
@@ -10,11 +10,14 @@ namespace ptype {
 
 namespace {
 
-__device__ __forceinline__ uint64_t ipc_ld(const uint64_t* p) {  // memory-side read: no stale L2 line
-  return __hip_atomic_fetch_add(const_cast<uint64_t*>(p), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// Flag words live in host memory mapped into every process: system-scope loads
+// and stores (the dispatcher's polling idiom, server.hpp sys_ld / sys_st) -- no
+// read-modify-write, which would need PCIe atomics.
+__device__ __forceinline__ uint64_t ipc_ld(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void ipc_st(uint64_t* p, uint64_t v) {
-  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint64_t* word_at(uint64_t base, size_t off) {
   return reinterpret_cast<uint64_t*>(base + off);
@@ -126,14 +129,16 @@ __global__ __launch_bounds__(256) void ipc_out_kernel(uint8_t* __restrict__ dst,
 
 }  // namespace
 
-IpcComm::IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s)
+IpcComm::IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s, const std::string& name)
     : device_(device), R_(R), rank_(rank), cap_((cap_bytes + 15) / 16 * 16), timeout_s_(timeout_s) {
   if (R < 1 || R > kIpcMaxRanks || rank < 0 || rank >= R) throw std::invalid_argument("IpcComm: 0 <= rank < R <= 64");
   if (cap_ < 16) throw std::invalid_argument("IpcComm: capacity");
   timeout_ticks_ = (uint64_t)(std::max(0.01, timeout_s) * 1e8);  // s_memrealtime: 100 MHz
   PT_HIP_CHECK(hipSetDevice(device_));
-  PT_HIP_CHECK(hipMalloc((void**)&seg_, kIpcCtrlBytes + (size_t)R * cap_));
-  PT_HIP_CHECK(hipMemset(seg_, 0, kIpcCtrlBytes));
+  segs_.assign((size_t)R, nullptr);
+  registered_.assign((size_t)R, false);
+  segs_[(size_t)rank] = ShmSegment::create(name, kIpcCtrlBytes + (size_t)R * cap_);  // zero-filled
+  map_segment(rank);
   PT_HIP_CHECK(hipMalloc((void**)&segs_dev_, kIpcMaxRanks * sizeof(uint64_t)));
   PT_HIP_CHECK(hipMalloc((void**)&ctr_, (kIpcMaxRanks + 1) * sizeof(unsigned)));
   PT_HIP_CHECK(hipMemset(ctr_, 0, (kIpcMaxRanks + 1) * sizeof(unsigned)));
@@ -141,48 +146,45 @@ IpcComm::IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s
   *host_failed_ = 0;
   PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dev_failed_, host_failed_, 0));
   PT_HIP_CHECK(hipDeviceSynchronize());
-  imports_.assign((size_t)R, nullptr);
 }
 
 IpcComm::~IpcComm() {  // no synchronisation: a wait on a dead peer ends at its timeout, not here
   (void)hipSetDevice(device_);
-  for (void* p : imports_)
-    if (p) (void)hipIpcCloseMemHandle(p);
-  (void)hipFree(seg_);
+  for (size_t q = 0; q < segs_.size(); ++q)
+    if (registered_[q]) (void)hipHostUnregister(segs_[q]->base());
   (void)hipFree(segs_dev_);
   (void)hipFree(ctr_);
   (void)hipHostFree(host_failed_);
 }
 
-std::string IpcComm::handle() const {
-  hipIpcMemHandle_t h;
-  PT_HIP_CHECK(hipSetDevice(device_));
-  PT_HIP_CHECK(hipIpcGetMemHandle(&h, seg_));
-  return std::string(reinterpret_cast<const char*>(&h), sizeof h);
+void IpcComm::map_segment(int q) {
+  PT_HIP_CHECK(hipHostRegister(segs_[(size_t)q]->base(), segs_[(size_t)q]->size(),
+                               hipHostRegisterMapped | hipHostRegisterPortable));
+  registered_[(size_t)q] = true;
 }
 
-void IpcComm::connect(const std::vector<std::string>& handles) {
-  if ((int)handles.size() != R_) throw std::invalid_argument("IpcComm.connect: one handle per rank");
+void IpcComm::connect(const std::vector<std::string>& names) {
+  if ((int)names.size() != R_) throw std::invalid_argument("IpcComm.connect: one segment name per rank");
   if (connected_) throw std::runtime_error("IpcComm.connect: already connected");
   PT_HIP_CHECK(hipSetDevice(device_));
   uint64_t segs[kIpcMaxRanks] = {};
+  const size_t want = kIpcCtrlBytes + (size_t)R_ * cap_;
   for (int q = 0; q < R_; ++q) {
-    if (q == rank_) {
-      segs[q] = (uint64_t)(uintptr_t)seg_;
-      continue;
+    if (q != rank_) {
+      segs_[(size_t)q] = ShmSegment::attach(names[(size_t)q]);
+      if (!segs_[(size_t)q] || segs_[(size_t)q]->size() < want)
+        throw std::runtime_error("IpcComm.connect: no segment " + names[(size_t)q] + " of rank " + std::to_string(q));
+      map_segment(q);
     }
-    if (handles[(size_t)q].size() != sizeof(hipIpcMemHandle_t))
-      throw std::invalid_argument("IpcComm.connect: bad handle for rank " + std::to_string(q));
-    hipIpcMemHandle_t h;
-    memcpy(&h, handles[(size_t)q].data(), sizeof h);
-    void* p = nullptr;
-    PT_HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-    imports_[(size_t)q] = p;
-    segs[q] = (uint64_t)(uintptr_t)p;
+    void* d = nullptr;
+    PT_HIP_CHECK(hipHostGetDevicePointer(&d, segs_[(size_t)q]->base(), 0));
+    segs[q] = (uint64_t)(uintptr_t)d;
   }
   PT_HIP_CHECK(hipMemcpy(segs_dev_, segs, sizeof segs, hipMemcpyHostToDevice));
   connected_ = true;
 }
+
+void IpcComm::seal() { segs_[(size_t)rank_]->unlink_now(); }
 
 bool IpcComm::failed() const { return __atomic_load_n(host_failed_, __ATOMIC_ACQUIRE) != 0; }
 

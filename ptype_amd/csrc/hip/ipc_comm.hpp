@@ -1,27 +1,35 @@
 // IpcComm: the data plane's collectives between PROCESSES on one node without
-// RCCL -- one rank per process, each rank's receive segment in its own HBM,
-// exported with hipIpcGetMemHandle and imported by every peer.  It exists so the
-// engines' multi-rank pipelines (EpochEngine, SortedExchange) run across real
-// process boundaries on a one-GPU box: RCCL refuses two ranks on one device
-// ("Duplicate GPU detected"), and FakeComm's ranks share one process.  On a
-// multi-GPU node the same code imports the peers' segments over xGMI.
+// RCCL -- one rank per process, stream-ordered on the device, no host wait.  It
+// exists so the engines' multi-rank pipelines (EpochEngine, SortedExchange) run
+// across real process boundaries on a one-GPU box: RCCL refuses two ranks on
+// one device ("Duplicate GPU detected"), and FakeComm's ranks share one process.
 //
-// Segment of rank r (hipMalloc, exported once):
-//   [0, 512)      posted[64]: peer q stores posted[q] = s once its op-s data sits
-//                 in this inbox (remote, system-scope atomic store)
+// Transport: every rank's receive segment is a POSIX shared-memory file that
+// EVERY rank maps and registers with HIP (hipHostRegister, mapped) in its own
+// process, so the GPU reaches it through that process's own mapping.  The first
+// design imported the peers' HBM by IPC handle; a peer killed mid-run then took
+// its HBM with it and the survivors' next collective faulted on the unmapped
+// import (measured on the MI355X box, r4).  Host pages stay mapped for as long
+// as any survivor maps them, so a dead peer costs a timeout, never a fault.
+// (Bandwidth is PCIe's, not HBM's: this is the test / rehearsal transport; a
+// multi-GPU node runs RCCL over xGMI.)
+//
+// Segment of rank r (host shared memory, registered by every rank):
+//   [0, 512)      posted[64]: rank q stores posted[q] = s once its op-s data sits
+//                 in this inbox (system-scope store)
 //   [512]         consumed: r stores s once it has copied op s out of its inbox
 //   [640]         failed: r's sticky error word (a wait that timed out)
-//   [4096, ...)   inbox[R][cap]: peer q's region of the op in flight at q * cap
+//   [4096, ...)   inbox[R][cap]: rank q's region of the op in flight at q * cap
 //
 // Op s (every rank issues the same ops in the same order; s is a host counter),
-// all on the caller's stream, no host wait:
+// all on the caller's stream:
 //   K0 wait   one wave: every rank's consumed >= s - 1 (its inbox is free again;
 //             this rank's own too, so ops issued on two streams stay serialised)
-//   K1 push   (X, R) blocks: region q of src -> peer q's inbox slot r; the last
-//             block of each peer releases (system fence) and stores posted[r] = s
-//             into that peer's segment
+//   K1 push   (X, R) blocks: region q of src -> rank q's inbox slot r; the last
+//             block of each row releases (system fence) and stores posted[r] = s
+//             into rank q's segment
 //   K2 wait   one wave: every posted[q] of this rank's segment >= s
-//   K3 out    (X, R) blocks: agent acquire, inbox slot q -> region q of dst (or
+//   K3 out    (X, R) blocks: system acquire, inbox slot q -> region q of dst (or
 //             the element-wise max of the R slots, for all-reduce); the last
 //             block stores consumed = s
 // Waits are bounded (timeout_s): a peer that never arrives (killed) makes the
@@ -40,6 +48,7 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "shmring.hpp"
 
 namespace ptype {
 
@@ -54,15 +63,18 @@ struct IpcSizes {  // by value: bytes per peer region (<= cap)
 class IpcComm : public HostComm {
  public:
   // cap_bytes: the largest region one op moves per peer (16-B multiple).
-  IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s = 30.0);
+  // name: this rank's segment name (unique per group and rank).
+  IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s, const std::string& name);
   ~IpcComm() override;
   IpcComm(const IpcComm&) = delete;
   IpcComm& operator=(const IpcComm&) = delete;
 
-  // this rank's segment handle (hipIpcMemHandle_t bytes), for the other ranks
-  std::string handle() const;
-  // every rank's handle, in rank order (this rank's own is skipped); imports the peers
-  void connect(const std::vector<std::string>& handles);
+  // this rank's segment name, for the other ranks
+  std::string handle() const { return segs_[(size_t)rank_]->name(); }
+  // every rank's segment name, in rank order (this rank's own is skipped); maps and registers the peers'
+  void connect(const std::vector<std::string>& names);
+  // once EVERY rank has connected: remove this rank's name (the mappings stay)
+  void seal();
 
   int size() const override { return R_; }
   bool device_side() const override { return true; }
@@ -80,15 +92,16 @@ class IpcComm : public HostComm {
  private:
   void op(const void* src, size_t src_stride, void* dst, size_t dst_stride, const IpcSizes& send,
           const IpcSizes& recv, hipStream_t s, uint64_t* reduce_dst, int reduce_n);
+  void map_segment(int q);
 
   int device_, R_, rank_;
   size_t cap_;
   uint64_t timeout_ticks_;
   double timeout_s_;
-  uint8_t* seg_ = nullptr;                 // this rank's segment
-  std::vector<void*> imports_;             // peers' segments (nullptr for self)
-  uint64_t* segs_dev_ = nullptr;           // [R] segment base of every rank, as mapped here
-  unsigned* ctr_ = nullptr;                // [2] last-block tickets (push, out), self-resetting
+  std::vector<std::shared_ptr<ShmSegment>> segs_;  // every rank's segment, mapped in this process
+  std::vector<bool> registered_;
+  uint64_t* segs_dev_ = nullptr;           // [R] device address of every rank's segment, as mapped here
+  unsigned* ctr_ = nullptr;                // last-block tickets: [R] push rows, [1] out (self-resetting)
   uint64_t* host_failed_ = nullptr;        // pinned: set by a timed-out wait
   uint64_t* dev_failed_ = nullptr;         // its device address
   uint64_t seq_ = 0;                       // ops issued

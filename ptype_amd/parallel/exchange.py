@@ -821,14 +821,22 @@ class ActorExchange:
 
 def ipc_group_comm(group, device: torch.device, cap_bytes: int, timeout_s: float = 30.0):
     """An ``_hip.IpcComm`` over the ranks of ``group`` (collective): every rank
-    allocates its receive segment, the IPC handles travel through the group
-    (``all_gather_object``; gloo is enough) and every rank imports the others'."""
+    creates its receive segment (shared memory), the names travel through the
+    group (``all_gather_object``; gloo is enough), every rank maps and registers
+    the others', and once all have, the names are removed (nothing is left in
+    /dev/shm when a rank is killed later)."""
+    import uuid
+
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    c = B.hip().IpcComm(idx, world, rank, int(cap_bytes), float(timeout_s))
-    handles = [None] * world
-    dist.all_gather_object(handles, c.handle(), group=group)
-    c.connect(handles)
+    token = [uuid.uuid4().hex[:12] if rank == 0 else None]
+    dist.broadcast_object_list(token, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    c = B.hip().IpcComm(idx, world, rank, int(cap_bytes), float(timeout_s), f"ptype-ipc-{token[0]}-{rank}")
+    names = [None] * world
+    dist.all_gather_object(names, c.handle(), group=group)
+    c.connect(names)
+    dist.barrier(group=group)
+    c.seal()
     return c
 
 

@@ -1,10 +1,10 @@
 """One rank of a multi-PROCESS data-plane test on one GPU (tests/test_ipc_comm_gpu.py).
 
 Usage: python _ipc_worker.py <scenario> <rank> <world> <port>.  Every rank joins a
-gloo group (the host side: IPC handles, host agreements, result gathering) and
-drives the native engines' collectives through an IpcComm on cuda:0
-(csrc/hip/ipc_comm.hpp).  Rank 0 prints one ``RESULT {json}`` line; a failed
-check raises (non-zero exit)."""
+gloo group (the host side: segment names, host agreements, result gathering)
+and drives the native engines' collectives through an IpcComm on cuda:0
+(csrc/hip/ipc_comm.hpp: shared-memory segments every rank maps).  Rank 0
+prints one ``RESULT {json}`` line; a failed check raises (non-zero exit)."""
 import json
 import os
 import signal

@@ -2,11 +2,11 @@
 
 RCCL refuses two ranks on one device, so a one-GPU box could only run the
 multi-rank pipelines as in-process FakeComm ranks.  IpcComm
-(csrc/hip/ipc_comm.hpp) moves their collectives through the peers' HBM
-segments, imported by IPC handle, stream-ordered on the device: each rank here
-is its own Python process (torch.distributed gloo group for the host side),
-exactly the one-process-per-GPU shape of a node -- only the transport differs
-from RCCL over xGMI.
+(csrc/hip/ipc_comm.hpp) moves their collectives through shared-memory segments
+that every rank maps and registers with HIP, stream-ordered on the device:
+each rank here is its own Python process (torch.distributed gloo group for the
+host side), exactly the one-process-per-rank shape of a node -- only the
+transport differs from RCCL over xGMI.
 
 Numerics: calculator replies compared exactly with A * B; ordered SeqFold
 traffic audited exactly-once with per-(sender, actor) FIFO (ops.mailbox.audit_fold)
