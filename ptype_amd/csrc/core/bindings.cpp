@@ -3,11 +3,13 @@
 #include <pybind11/functional.h>
 #include <condition_variable>
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include <unordered_map>
 
 #include "api.hpp"
+#include "follower.hpp"
 #include "gob.hpp"
 #include "json.hpp"
 #include "records.hpp"
@@ -517,6 +519,61 @@ PYBIND11_MODULE(_core, m) {
       .def("status", &KvClient::status, py::arg("timeout_ms") = 5000, py::call_guard<py::gil_scoped_release>())
       .def("watch", &KvClient::watch, py::arg("ctx"), py::arg("key"), py::arg("end") = "", py::arg("start_rev") = 0,
            py::call_guard<py::gil_scoped_release>());
+
+  // the GPU registry mirror's compiled control side (follower.hpp)
+  py::class_<RegistryFollower, std::shared_ptr<RegistryFollower>>(m, "RegistryFollower")
+      .def(py::init([](std::shared_ptr<KvClient> kv, const std::string& prefix, int64_t ttl_ms, int64_t grace_ms,
+                       double relist_s, bool watch) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<RegistryFollower>(std::move(kv), prefix, ttl_ms, grace_ms, relist_s, watch);
+           }),
+           py::arg("kv"), py::arg("prefix"), py::arg("ttl_ms"), py::arg("grace_ms"), py::arg("relist_s"),
+           py::arg("watch") = true)
+      .def("quiet", &RegistryFollower::quiet, py::arg("now_ms"))
+      .def(
+          "take",
+          [](RegistryFollower& f, int64_t now_ms) {
+            bool sweep = false;
+            int64_t changed = 0;
+            std::vector<MirrorOp> ops;
+            {
+              py::gil_scoped_release nogil;
+              ops = f.take(now_ms, &sweep, &changed);
+            }
+            py::list out;
+            for (auto& op : ops) {  // (kind, key, rank, deadline, ids int64[n], mbox int32[n] or None)
+              py::array_t<int64_t> ids((py::ssize_t)op.ids.size());
+              std::copy(op.ids.begin(), op.ids.end(), ids.mutable_data());
+              py::object mb = py::none();
+              if (op.kind == MirrorOp::kUpsert) {
+                py::array_t<int32_t> a((py::ssize_t)op.mbox.size());
+                std::copy(op.mbox.begin(), op.mbox.end(), a.mutable_data());
+                mb = a;
+              }
+              out.append(py::make_tuple((int)op.kind, op.key, op.rank, op.deadline_ms, ids, mb));
+            }
+            return py::make_tuple(out, sweep, changed);
+          },
+          py::arg("now_ms"), "apply what is queued: ([(kind, key, rank, deadline, ids, mbox)], sweep, changed)")
+      .def("set_generation", &RegistryFollower::set_generation, py::arg("gen"))
+      .def("shards", &RegistryFollower::shards, "applied shards: [(key, record JSON, deadline ms)]")
+      .def_property_readonly("actors", &RegistryFollower::actors)
+      .def_property_readonly("version", &RegistryFollower::version)
+      .def_property_readonly("applies", &RegistryFollower::applies)
+      .def_property_readonly("relists", &RegistryFollower::relists)
+      .def_property_readonly("events", &RegistryFollower::events)
+      .def("close", &RegistryFollower::close, py::call_guard<py::gil_scoped_release>());
+  py::class_<ShardLease, std::shared_ptr<ShardLease>>(m, "ShardLease")
+      .def(py::init([](std::shared_ptr<KvClient> kv, const std::string& key, const std::string& record, int64_t ttl_s) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<ShardLease>(std::move(kv), key, record, ttl_s);
+           }),
+           py::arg("kv"), py::arg("key"), py::arg("record"), py::arg("ttl_s"))
+      .def("update", &ShardLease::update, py::arg("record"), py::call_guard<py::gil_scoped_release>())
+      .def("stop_keepalive", &ShardLease::stop_keepalive)
+      .def("close", &ShardLease::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("record", &ShardLease::record)
+      .def_property_readonly("lease", &ShardLease::lease);
 
   // ---------------------------------------------------------------- registry / store
   py::class_<Registry, std::shared_ptr<Registry>>(m, "Registry");
