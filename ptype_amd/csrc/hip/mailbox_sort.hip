@@ -416,13 +416,13 @@ __device__ __forceinline__ void load_cols(const SortIn& in, uint32_t t, int64_t 
 // LATE: the arguments are loaded after the look-back (a smaller register file
 // across it, more resident blocks; measured slower), else with the actors (in
 // flight across the gathers, the ranking and the look-back).
+// One tile of the one-pass sort (the block claims it); returns its index.
 template <int MODE, bool A2, bool MC, bool LATE>
-__global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
-                                                           unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
-                                                           uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
-                                                           uint32_t* __restrict__ rw, ReplyView rv, bool spill,
-                                                           bool all_sidx) {
-  extern __shared__ __align__(16) unsigned char smem_os[];
+__device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxView& mv, unsigned long long* __restrict__ desc,
+                                                  unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
+                                                  uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
+                                                  uint32_t* __restrict__ rw, const ReplyView& rv, bool spill,
+                                                  bool all_sidx, unsigned char* smem_os) {
   const uint32_t S = 1u << mv.log_s;
   unsigned long long* base = reinterpret_cast<unsigned long long*>(smem_os);  // ring position of this tile's run (tail + prefix)
   uint32_t* room = reinterpret_cast<uint32_t*>(base + S);                     // offset limit past the tail
@@ -579,6 +579,17 @@ __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView m
   block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
   __syncthreads();  // block_add_stats' LDS partials are reused
   block_add_stats(mv.stats, n_spill, kMbSpilled, timeouts, kMbLookback, 0, -1);
+  return t;
+}
+
+template <int MODE, bool A2, bool MC, bool LATE>
+__global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
+                                                           unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
+                                                           uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
+                                                           uint32_t* __restrict__ rw, ReplyView rv, bool spill,
+                                                           bool all_sidx) {
+  extern __shared__ __align__(16) unsigned char smem_os[];
+  (void)onesweep_tile<MODE, A2, MC, LATE>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill, all_sidx, smem_os);
 }
 
 // ---------------------------------------------------------------- compact record decode
@@ -659,7 +670,7 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 // recorded, replies coalesced; a spilled message runs straight from the batch.
 //
 // The last block commits every shard (and clears the group sums).
-template <int FIXED>
+template <int FIXED, bool FRESH = false>
 __device__ __forceinline__ void drain_tile_msg(const MboxView& mv, const SortIn& in, uint32_t t,
                                                const uint32_t* __restrict__ sidx, const uint32_t* __restrict__ rw,
                                                int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks,
@@ -673,8 +684,10 @@ __device__ __forceinline__ void drain_tile_msg(const MboxView& mv, const SortIn&
   }
   u32x4 ha[kSK];
 #pragma unroll
-  for (int k = 0; k < kSK; ++k)
-    ha[k] = sl[k] < kSpillSlot ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k])) : u32x4{0u, 0u, 0u, 0u};
+  for (int k = 0; k < kSK; ++k) {
+    const u32x4* rp = reinterpret_cast<const u32x4*>(rec_a(mv, sl[k] < kSpillSlot ? sl[k] : 0));
+    ha[k] = sl[k] < kSpillSlot ? (FRESH ? __builtin_nontemporal_load(rp) : *rp) : u32x4{0u, 0u, 0u, 0u};
+  }
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     if (sl[k] == kNoSlot) continue;  // answered by the scatter (no actor / ring full)
@@ -692,8 +705,9 @@ __device__ __forceinline__ void drain_tile_msg(const MboxView& mv, const SortIn&
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
       if (rec_is_long(ha[k])) {
-        hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
-        if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
+        const u32x4* bp = reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
+        hb = FRESH ? __builtin_nontemporal_load(bp) : *bp;
+        if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = FRESH ? __builtin_nontemporal_load(mv.a2 + sl[k]) : mv.a2[sl[k]];
       }
       x = decode_sorted(ha[k], hb, a2v);
     }
@@ -796,15 +810,19 @@ __host__ __device__ constexpr size_t ring_drain_lds_bytes(uint32_t S) {
   return S <= 256 ? (size_t)kSTile * (8 + 1) + (size_t)S * 8 : (size_t)kSTile * (8 + 2 + 1) + (size_t)S * 8;
 }
 
-template <int FIXED, bool NARROW>
-__global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ tinfo,
-                                                             const uint32_t* __restrict__ sidx,
-                                                             const uint32_t* __restrict__ rw,
-                                                             int64_t* __restrict__ state, uint32_t n_state,
-                                                             uint64_t delay_ticks, OutboxView ob, ReplyView rv,
-                                                             uint32_t* __restrict__ gsum, uint32_t ngroups,
-                                                             unsigned* __restrict__ ticket, unsigned* __restrict__ tctr) {
-  extern __shared__ __align__(16) unsigned char smem_rd[];
+// Tile t's records, read in RING order from its runs (tinfo), each through the
+// handler table; replies staged in LDS at their place in the tile and written
+// out coalesced.  FRESH: the records were written by other waves of THIS block
+// in this kernel (the fused sort + drain) -- loaded non-temporal (L1 bypassed:
+// served by the XCD's L2, which holds the stores; a line another block of the
+// CU cached earlier would be stale in L1).
+template <int FIXED, bool NARROW, bool FRESH>
+__device__ __forceinline__ void drain_ring_tile(const MboxView& mv, const SortIn& in, uint32_t t,
+                                                const uint32_t* __restrict__ tinfo, const uint32_t* __restrict__ sidx,
+                                                const uint32_t* __restrict__ rw, int64_t* __restrict__ state,
+                                                uint32_t n_state, uint64_t delay_ticks, const OutboxView& ob,
+                                                const ReplyView& rv, unsigned char* smem_rd, unsigned long long& done,
+                                                unsigned long long& failed, unsigned long long& holes) {
   using OwnT = typename std::conditional<NARROW, uint8_t, uint16_t>::type;
   const uint32_t S = 1u << mv.log_s;
   int64_t* sval = reinterpret_cast<int64_t*>(smem_rd);  // [kSTile] reply values by place in the tile
@@ -814,77 +832,136 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
   L.owner = reinterpret_cast<OwnT*>(L.excl + S);
   // [kSTile] statuses, kAbsent = none (NARROW: the owner table's bytes, once the records are loaded)
   uint8_t* sst = NARROW ? reinterpret_cast<uint8_t*>(L.owner) : reinterpret_cast<uint8_t*>(L.owner + kSTile);
+  const uint64_t i0 = (uint64_t)t * kSTile;
+  const uint32_t n_t = (uint32_t)min((uint64_t)kSTile, (uint64_t)in.M - i0);
+  if constexpr (!NARROW)
+    for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
+  int spill = 0;
+  const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
+  if (spill) {  // some message of the tile spilled: the scatter left the tile's slot indices
+    drain_tile_msg<FIXED, FRESH>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
+    return;
+  }
+  const uint64_t sbase_mask = (1ull << mv.log_q) - 1;
+  u32x4 ha[kSK];
+  uint32_t sl[kSK];
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {  // ring order: lane-consecutive entries of the runs
+    const uint32_t j = (uint32_t)k * kST + threadIdx.x;
+    sl[k] = kNoSlot;
+    if (j < T) {
+      const uint32_t s = L.owner[j];
+      sl[k] = (uint32_t)(((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & sbase_mask));
+      const u32x4* rp = reinterpret_cast<const u32x4*>(rec_a(mv, sl[k]));
+      ha[k] = FRESH ? __builtin_nontemporal_load(rp) : *rp;
+    }
+  }
+  if constexpr (NARROW) {  // every owner entry is read: its bytes become the status stage
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {
+    if (sl[k] == kNoSlot) continue;
+    u32x4 hb = {0u, 0u, 0u, 0u};
+    int64_t a2v = 0;
+    if (rec_is_long(ha[k])) {
+      const u32x4* bp = reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
+      hb = FRESH ? __builtin_nontemporal_load(bp) : *bp;
+      if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = FRESH ? __builtin_nontemporal_load(mv.a2 + sl[k]) : mv.a2[sl[k]];
+    }
+    const SortRec x = decode_sorted(ha[k], hb, a2v);
+    const uint32_t local = x.origin - in.origin_base - (uint32_t)i0;
+    if (!x.valid || local >= n_t) {  // never written this epoch (cannot happen on a spill-free tile)
+      ++holes;
+      continue;
+    }
+    MsgRecord m;
+    m.actor = x.mb;
+    m.method = (uint16_t)(FIXED ? FIXED : x.method);
+    m.flags = (uint16_t)x.flags;
+    m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
+    const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
+    failed += rr.status != kStatusOk;
+    sval[local] = rr.value;
+    sst[local] = (uint8_t)rr.status;
+    ++done;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kSK; ++k) {  // the tile's replies, coalesced (misses were answered by the scatter)
+    const uint32_t j = (uint32_t)k * kST + threadIdx.x;
+    if (j < n_t && sst[j] != kAbsent) put_reply(rv, in.origin_base + (uint32_t)(i0 + j), sval[j], sst[j]);
+  }
+}
+
+template <int FIXED, bool NARROW>
+__global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ tinfo,
+                                                             const uint32_t* __restrict__ sidx,
+                                                             const uint32_t* __restrict__ rw,
+                                                             int64_t* __restrict__ state, uint32_t n_state,
+                                                             uint64_t delay_ticks, OutboxView ob, ReplyView rv,
+                                                             uint32_t* __restrict__ gsum, uint32_t ngroups,
+                                                             unsigned* __restrict__ ticket, unsigned* __restrict__ tctr) {
+  extern __shared__ __align__(16) unsigned char smem_rd[];
+  const uint32_t S = 1u << mv.log_s;
   unsigned long long done = 0, failed = 0, holes = 0;
   // tiles dealt XCD by XCD like the scatter's blocks (whose writes the XCD's L2 may still hold)
   const uint32_t t = virt_block(blockIdx.x, gridDim.x);
-  if (t < in.tiles) {
-    const uint64_t i0 = (uint64_t)t * kSTile;
-    const uint32_t n_t = (uint32_t)min((uint64_t)kSTile, (uint64_t)in.M - i0);
-    if constexpr (!NARROW)
-      for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
-    int spill = 0;
-    const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
-    if (spill) {  // some message of the tile spilled: the scatter left the tile's slot indices
-      drain_tile_msg<FIXED>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
-    } else {
-      const uint64_t sbase_mask = (1ull << mv.log_q) - 1;
-      u32x4 ha[kSK];
-      uint32_t sl[kSK];
-#pragma unroll
-      for (int k = 0; k < kSK; ++k) {  // ring order: lane-consecutive entries of the runs
-        const uint32_t j = (uint32_t)k * kST + threadIdx.x;
-        sl[k] = kNoSlot;
-        if (j < T) {
-          const uint32_t s = L.owner[j];
-          sl[k] = (uint32_t)(((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & sbase_mask));
-          ha[k] = *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k]));
-        }
-      }
-      if constexpr (NARROW) {  // every owner entry is read: its bytes become the status stage
-        __syncthreads();
-        for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
-        __syncthreads();
-      }
-#pragma unroll
-      for (int k = 0; k < kSK; ++k) {
-        if (sl[k] == kNoSlot) continue;
-        u32x4 hb = {0u, 0u, 0u, 0u};
-        int64_t a2v = 0;
-        if (rec_is_long(ha[k])) {
-          hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
-          if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
-        }
-        const SortRec x = decode_sorted(ha[k], hb, a2v);
-        const uint32_t local = x.origin - in.origin_base - (uint32_t)i0;
-        if (!x.valid || local >= n_t) {  // never written this epoch (cannot happen on a spill-free tile)
-          ++holes;
-          continue;
-        }
-        MsgRecord m;
-        m.actor = x.mb;
-        m.method = (uint16_t)(FIXED ? FIXED : x.method);
-        m.flags = (uint16_t)x.flags;
-        m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
-        const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
-        failed += rr.status != kStatusOk;
-        sval[local] = rr.value;
-        sst[local] = (uint8_t)rr.status;
-        ++done;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < kSK; ++k) {  // the tile's replies, coalesced (misses were answered by the scatter)
-        const uint32_t j = (uint32_t)k * kST + threadIdx.x;
-        if (j < n_t && sst[j] != kAbsent) put_reply(rv, in.origin_base + (uint32_t)(i0 + j), sval[j], sst[j]);
-      }
-    }
-  }
+  if (t < in.tiles)
+    drain_ring_tile<FIXED, NARROW, false>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob, rv, smem_rd,
+                                          done, failed, holes);
   block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
   __shared__ bool last;
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
   __syncthreads();
   if (last) {  // every block's records are read: the rings are consumed
     for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
+    if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
+  }
+}
+
+// ---------------------------------------------------------------- fused one-pass sort + ring-order drain
+// Batches of stateless methods (the parallel drain): the block that sorts tile t
+// into the rings drains tile t's runs right after -- the runs of a tile are
+// exactly the records it wrote, so no other block's progress is needed, only a
+// barrier between the block's stores and its ring-order reads (FRESH loads).
+// The records still go through the rings (written, then read back in ring
+// order by other lanes than wrote them), but the Send is one launch instead of
+// two, the drain's reads are L2 hits of lines the sort just wrote, and no block
+// waits at a kernel boundary for the slowest tile.  The last block to finish
+// commits every shard's epoch (tail = head = tail + total) and advances the
+// look-back tag.  PTYPE_MBOX_FUSED=0: the separate kernels.
+template <int MODE, bool A2, bool MC, int FIXED>
+__global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
+                                                            unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
+                                                            uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
+                                                            uint32_t* __restrict__ rw, ReplyView rv,
+                                                            int64_t* __restrict__ state, uint32_t n_state,
+                                                            uint64_t delay_ticks, OutboxView ob,
+                                                            unsigned* __restrict__ ticket) {
+  extern __shared__ __align__(16) unsigned char smem_sd[];
+  const uint32_t S = 1u << mv.log_s;
+  const uint32_t t = onesweep_tile<MODE, A2, MC, false>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, true, false,
+                                                        smem_sd);
+  // every wave's ring stores are out before any wave reads the tile's runs
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned long long done = 0, failed = 0, holes = 0;
+  drain_ring_tile<FIXED, true, true>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob, rv, smem_sd, done,
+                                     failed, holes);
+  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
+  __shared__ bool last;
+  if (threadIdx.x == 0) {
+    // the last tile's block wrote the epoch totals (gsum): release them before its ticket
+    if (t == in.tiles - 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = last_block_ticket(ticket);
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (last) {  // every block's records are read: the rings are consumed
+    for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, 1, S, s, true));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
   }
 }
@@ -1249,6 +1326,12 @@ __global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxV
 }
 
 // ---------------------------------------------------------------- host
+// The fused sort + drain for stateless one-pass Sends (PTYPE_MBOX_FUSED=0: two launches).
+static bool fused_ok() {
+  static const bool on = !(getenv("PTYPE_MBOX_FUSED") && std::string(getenv("PTYPE_MBOX_FUSED")) == "0");
+  return on;
+}
+
 void Mailboxes::send_sorted(const MboxSend& a) {
   const uint32_t S = shards();
   if (S > (uint32_t)kMboxSortMaxShards) throw std::invalid_argument("sorted mailboxes: at most 1024 shards");
@@ -1332,7 +1415,11 @@ void Mailboxes::send_sorted(const MboxSend& a) {
                               : std::string(sort_env) == "onepass" ? 1
                               : std::string(sort_env) == "twopass" ? 2
                               : std::string(sort_env) == "ldscount" ? 3 : 0;
-  const int sort_mode = a.sort_mode ? a.sort_mode : env_mode ? env_mode : (tiles < 1024 ? 2 : 1);
+  // (stateless batches of any size take the one-pass sort when the fused sort + drain is on: one launch per Send)
+  const int sort_mode = a.sort_mode ? a.sort_mode
+                        : env_mode  ? env_mode
+                        : (tiles >= 1024 || (!a.ordered && !a.arrival && fused_ok())) ? 1
+                                                                                       : 2;
   if (sort_mode < 1 || sort_mode > 3) throw std::invalid_argument("mailbox send: sort_mode 0..3");
   const bool two_pass = sort_mode != 1;
   const uint32_t ngroups = two_pass ? (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks) : 1u;
@@ -1451,6 +1538,30 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else if (a.method_col) PT_SCAT(false, true);
     else PT_SCAT(false, false);
 #undef PT_SCAT
+  } else if (!a.ordered && !all_sidx && Sv <= 256 && fused_ok()) {
+    // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel)
+    const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv));
+#define PT_SD2(MO, A2, MC, FX)                                                                                      \
+  hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX>), dim3(in.tiles), dim3(kST), lds, st, in, mv, sort_desc_, \
+                     sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv, (int64_t*)a.state, a.n_state,    \
+                     a.delay_ticks, ob, sort_ticket_)
+#define PT_SD(MO)                                                            \
+  do {                                                                       \
+    if (a.a2 && a.method_col) PT_SD2(MO, true, true, 0);                     \
+    else if (a.method_col) PT_SD2(MO, false, true, 0);                       \
+    else if (a.a2) {                                                         \
+      if (fixed_mul) PT_SD2(MO, true, false, kCalculatorMultiply);           \
+      else PT_SD2(MO, true, false, 0);                                       \
+    } else {                                                                 \
+      if (fixed_mul) PT_SD2(MO, false, false, kCalculatorMultiply);          \
+      else PT_SD2(MO, false, false, 0);                                      \
+    }                                                                        \
+  } while (0)
+    if (mode == 2) PT_SD(2); else if (mode == 1) PT_SD(1); else PT_SD(0);
+#undef PT_SD
+#undef PT_SD2
+    PT_HIP_CHECK(hipGetLastError());
+    return;
   } else {
     // one block per tile, claimed in launch order (the grid is exactly the tile count)
     // (PTYPE_OS_LATE=1: arguments loaded after the look-back, 87 instead of 115 VGPRs -- measured slower,
