@@ -671,10 +671,10 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 //
 // The last block commits every shard (and clears the group sums).
 template <int FIXED, bool FRESH = false>
-__device__ __forceinline__ void drain_tile_msg(const MboxView& mv, const SortIn& in, uint32_t t,
+__device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t t,
                                                const uint32_t* __restrict__ sidx, const uint32_t* __restrict__ rw,
                                                int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks,
-                                               const OutboxView& ob, const ReplyView& rv, unsigned long long& done,
+                                               OutboxView ob, ReplyView rv, unsigned long long& done,
                                                unsigned long long& failed, unsigned long long& holes) {
   uint32_t sl[kSK];
 #pragma unroll
@@ -816,13 +816,20 @@ __host__ __device__ constexpr size_t ring_drain_lds_bytes(uint32_t S) {
 // in this kernel (the fused sort + drain) -- loaded non-temporal (L1 bypassed:
 // served by the XCD's L2, which holds the stores; a line another block of the
 // CU cached earlier would be stale in L1).
+struct DrainCounts {
+  unsigned long long done = 0, failed = 0, holes = 0;
+};
+
+// (views and counts by value: references to a kernel's locals or arguments put
+// them in scratch)
 template <int FIXED, bool NARROW, bool FRESH>
-__device__ __forceinline__ void drain_ring_tile(const MboxView& mv, const SortIn& in, uint32_t t,
-                                                const uint32_t* __restrict__ tinfo, const uint32_t* __restrict__ sidx,
-                                                const uint32_t* __restrict__ rw, int64_t* __restrict__ state,
-                                                uint32_t n_state, uint64_t delay_ticks, const OutboxView& ob,
-                                                const ReplyView& rv, unsigned char* smem_rd, unsigned long long& done,
-                                                unsigned long long& failed, unsigned long long& holes) {
+__device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, uint32_t t,
+                                                       const uint32_t* __restrict__ tinfo,
+                                                       const uint32_t* __restrict__ sidx,
+                                                       const uint32_t* __restrict__ rw, int64_t* __restrict__ state,
+                                                       uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
+                                                       ReplyView rv, unsigned char* smem_rd) {
+  unsigned long long done = 0, failed = 0, holes = 0;
   using OwnT = typename std::conditional<NARROW, uint8_t, uint16_t>::type;
   const uint32_t S = 1u << mv.log_s;
   int64_t* sval = reinterpret_cast<int64_t*>(smem_rd);  // [kSTile] reply values by place in the tile
@@ -840,7 +847,7 @@ __device__ __forceinline__ void drain_ring_tile(const MboxView& mv, const SortIn
   const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
   if (spill) {  // some message of the tile spilled: the scatter left the tile's slot indices
     drain_tile_msg<FIXED, FRESH>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
-    return;
+    return DrainCounts{done, failed, holes};
   }
   const uint64_t sbase_mask = (1ull << mv.log_q) - 1;
   u32x4 ha[kSK];
@@ -894,6 +901,7 @@ __device__ __forceinline__ void drain_ring_tile(const MboxView& mv, const SortIn
     const uint32_t j = (uint32_t)k * kST + threadIdx.x;
     if (j < n_t && sst[j] != kAbsent) put_reply(rv, in.origin_base + (uint32_t)(i0 + j), sval[j], sst[j]);
   }
+  return DrainCounts{done, failed, holes};
 }
 
 template <int FIXED, bool NARROW>
@@ -906,13 +914,13 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
                                                              unsigned* __restrict__ ticket, unsigned* __restrict__ tctr) {
   extern __shared__ __align__(16) unsigned char smem_rd[];
   const uint32_t S = 1u << mv.log_s;
-  unsigned long long done = 0, failed = 0, holes = 0;
+  DrainCounts dc;
   // tiles dealt XCD by XCD like the scatter's blocks (whose writes the XCD's L2 may still hold)
   const uint32_t t = virt_block(blockIdx.x, gridDim.x);
   if (t < in.tiles)
-    drain_ring_tile<FIXED, NARROW, false>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob, rv, smem_rd,
-                                          done, failed, holes);
-  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
+    dc = drain_ring_tile<FIXED, NARROW, false>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob, rv,
+                                               smem_rd);
+  block_add_stats(mv.stats, dc.done, kMbProcessed, dc.failed, kMbFailed, dc.holes, kMbHoles);
   __shared__ bool last;
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
   __syncthreads();
@@ -948,10 +956,9 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
   // every wave's ring stores are out before any wave reads the tile's runs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  unsigned long long done = 0, failed = 0, holes = 0;
-  drain_ring_tile<FIXED, true, true>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob, rv, smem_sd, done,
-                                     failed, holes);
-  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
+  const DrainCounts dc = drain_ring_tile<FIXED, true, true>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks,
+                                                            ob, rv, smem_sd);
+  block_add_stats(mv.stats, dc.done, kMbProcessed, dc.failed, kMbFailed, dc.holes, kMbHoles);
   __shared__ bool last;
   if (threadIdx.x == 0) {
     // the last tile's block wrote the epoch totals (gsum): release them before its ticket
