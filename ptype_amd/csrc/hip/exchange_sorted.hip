@@ -541,7 +541,16 @@ __global__ __launch_bounds__(256) void sx_drain_par_kernel(const uint32_t* __res
                                                            uint64_t delay_ticks, unsigned long long* __restrict__ stats) {
   const int p = blockIdx.y;
   const uint32_t* rq = recv + (int64_t)p * req_stride;
-  if (may_order && sx_sharded(rq)) return;  // the ordered drain serves this region
+  if (may_order && sx_sharded(rq)) {  // the ordered drain (launched next) serves this region:
+    if (blockIdx.x == 0) {            // its reply header and zeroed ok bitmap first (it sets bits one record at a time)
+      const uint4 h = *reinterpret_cast<const uint4*>(rq);
+      const int64_t count = ((h.w >> 16) & kFlagValid) ? (int64_t)(h.x < C ? h.x : C) : 0;
+      uint32_t* rp = reply + (int64_t)p * rep_stride;
+      if (threadIdx.x == 0) *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
+      for (int64_t j = threadIdx.x; j < packed_ok_words(count); j += blockDim.x) rp[4 + j] = 0u;
+    }
+    return;
+  }
   const uint4 h = *reinterpret_cast<const uint4*>(rq);
   const int64_t count = ((h.w >> 16) & kFlagValid) ? (int64_t)(h.x < C ? h.x : C) : 0;
   const uint32_t hm = h.w & 0xffffu;
@@ -563,20 +572,9 @@ __global__ __launch_bounds__(256) void sx_drain_par_kernel(const uint32_t* __res
 }
 
 // ---------------------------------------------------------------- receiver: ordered drain
-// Reply headers and zeroed ok bitmaps first (the ordered drain sets ok bits one
-// record at a time).  grid R.
-__global__ __launch_bounds__(256) void sx_reply_init_kernel(const uint32_t* __restrict__ recv, int64_t req_stride,
-                                                            int64_t C, PackedLayout L, int R,
-                                                            uint32_t* __restrict__ reply, int64_t rep_stride) {
-  const int p = blockIdx.x;
-  if (!sx_sharded(recv + (int64_t)p * req_stride)) return;
-  const uint4 h = *reinterpret_cast<const uint4*>(recv + (int64_t)p * req_stride);
-  const int64_t count = ((h.w >> 16) & kFlagValid) ? (int64_t)(h.x < C ? h.x : C) : 0;
-  uint32_t* rp = reply + (int64_t)p * rep_stride;
-  if (threadIdx.x == 0) *reinterpret_cast<uint4*>(rp) = make_uint4((uint32_t)count, 0u, 0u, 0u);
-  for (int64_t j = threadIdx.x; j < packed_ok_words(count); j += blockDim.x) rp[4 + j] = 0u;
-}
-
+// Launched after the parallel drain, which wrote the sharded regions' reply
+// headers and zeroed their ok bitmaps (one launch less per chunk than a
+// separate init kernel).  grid: one block per actor shard.
 struct SxOrdLds {
   uint32_t wcnt[kXOrdWaves][kXOrdThreads];
   uint32_t bstart[kXOrdThreads];
@@ -972,9 +970,22 @@ void SortedExchange::send(const SxSend& a) {
   auto serve = [&](int i) {
     Bufs& b = bufs_[i];
     PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_req_in_[i], 0));
-    if (may_order) {
-      hipLaunchKernelGGL(sx_reply_init_kernel, dim3(R_), dim3(256), 0, cs, (const uint32_t*)b.recv, rq, C, L, R_,
-                         b.reply, rp);
+    // ~2048 blocks over the R regions (at least one per region)
+    const int64_t per = std::max<int64_t>(1, max_chunk_ / R_);
+    const unsigned X = (unsigned)std::max<int64_t>(1, std::min<int64_t>((per + 1023) / 1024, std::max(1, 2048 / R_)));
+#define PT_SX_PAR(SV)                                                                                         \
+  hipLaunchKernelGGL((sx_drain_par_kernel<SV>), dim3(X, R_), dim3(256), 0, cs, (const uint32_t*)b.recv, rq, C, L, \
+                     R_, may_order, b.reply, rp, (int64_t*)a.state, a.n_state, a.delay_ticks, stats_)
+    switch (S) {
+      case 1: PT_SX_PAR(1); break;
+      case 2: PT_SX_PAR(2); break;
+      case 3: PT_SX_PAR(3); break;
+      case 4: PT_SX_PAR(4); break;
+      case 6: PT_SX_PAR(6); break;
+      default: PT_SX_PAR(8); break;
+    }
+#undef PT_SX_PAR
+    if (may_order) {  // after the parallel drain (it initialised the sharded regions' replies)
       const size_t lds = sizeof(SxOrdLds) + (size_t)kXOrdStateMax * sizeof(int64_t);
 #define PT_SX_ORD(SV)                                                                                            \
   do {                                                                                                           \
@@ -998,21 +1009,6 @@ void SortedExchange::send(const SxSend& a) {
       }
 #undef PT_SX_ORD
     }
-    // ~2048 blocks over the R regions (at least one per region)
-    const int64_t per = std::max<int64_t>(1, max_chunk_ / R_);
-    const unsigned X = (unsigned)std::max<int64_t>(1, std::min<int64_t>((per + 1023) / 1024, std::max(1, 2048 / R_)));
-#define PT_SX_PAR(SV)                                                                                         \
-  hipLaunchKernelGGL((sx_drain_par_kernel<SV>), dim3(X, R_), dim3(256), 0, cs, (const uint32_t*)b.recv, rq, C, L, \
-                     R_, may_order, b.reply, rp, (int64_t*)a.state, a.n_state, a.delay_ticks, stats_)
-    switch (S) {
-      case 1: PT_SX_PAR(1); break;
-      case 2: PT_SX_PAR(2); break;
-      case 3: PT_SX_PAR(3); break;
-      case 4: PT_SX_PAR(4); break;
-      case 6: PT_SX_PAR(6); break;
-      default: PT_SX_PAR(8); break;
-    }
-#undef PT_SX_PAR
     PT_HIP_CHECK(hipGetLastError());
     PT_HIP_CHECK(hipEventRecord(ev_served_[i], cs));
     PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_served_[i], 0));
