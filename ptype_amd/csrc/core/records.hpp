@@ -29,6 +29,14 @@ enum MethodId : uint16_t {
   kMethodCount = 8,
 };
 
+// Served only by a persistent dispatcher that holds a relay table (xcall.hpp
+// PeerRelay): the request (actor = remote actor, a0 = remote method, a1, a2 =
+// its arguments) is forwarded from the dispatcher wave through a GPU peer lane
+// to ANOTHER process's dispatcher, and that actor's reply is this call's reply
+// -- a call a handler makes to a remote actor, with no host on its path.
+// Outside a dispatcher with a relay table: kStatusNoMethod.
+constexpr uint16_t kMethodRelay = 0x7e;
+
 // Multiplier of kSeqFold (odd, so the fold is a bijection of the prior state).
 constexpr uint64_t kFoldMul = 0x100000001b3ull;
 
@@ -149,7 +157,8 @@ struct alignas(64) ServerCtrl {
   uint64_t calib_req;    // host sets 1; the kernel answers with calib_ticks and clears it
   uint64_t calib_ticks;
   uint64_t xl_n;         // GPU peer lanes to poll (0 while none is registered: no cost on the ring's path)
-  uint64_t pad[5];
+  uint64_t relay;        // device address of a RelayTable (server.hpp): kMethodRelay calls go through it
+  uint64_t pad[4];
 };
 static_assert(sizeof(ServerCtrl) == 128, "ServerCtrl layout");
 

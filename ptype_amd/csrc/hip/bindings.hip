@@ -509,6 +509,16 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("timeout_s"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("lane", &PeerLane::lane)
       .def_property_readonly("calls", &PeerLane::calls);
+  py::class_<PeerRelay, std::shared_ptr<PeerRelay>>(m, "PeerRelay",
+                                                    "handler-initiated remote calls: peer lanes on another "
+                                                    "dispatcher as a relay table for this process's dispatcher")
+      .def(py::init([](const std::string& shm, int device, int n_lanes, double timeout_s) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<PeerRelay>(shm, device, n_lanes, timeout_s);
+           }),
+           py::arg("shm_name"), py::arg("device"), py::arg("n_lanes") = 8, py::arg("timeout_s") = 1.0)
+      .def_property_readonly("table", &PeerRelay::table)
+      .def_property_readonly("lanes", &PeerRelay::lanes);
   py::class_<DeviceServer>(m, "DeviceServer")
       .def(py::init<int, uint32_t, uintptr_t, uint32_t, uint64_t, double, double, const std::string&>(),
            py::arg("device"), py::arg("ring") = 4096, py::arg("state") = 0, py::arg("n_state") = 0,
@@ -517,6 +527,8 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("fields") = std::vector<std::string>{}, py::arg("actor_field") = "")
       .def_property_readonly("shm_name", &DeviceServer::shm_name)
       .def_property_readonly("xlanes", [](DeviceServer& s) { return s.xlanes_exported(); })
+      .def("set_relay", &DeviceServer::set_relay, py::arg("table"),
+           "route kMethodRelay calls through a PeerRelay's table (0: off)")
       .def(
           "call",
           [](DeviceServer& s, int method, uint32_t actor, int64_t a0, int64_t a1, int64_t a2, double timeout) {

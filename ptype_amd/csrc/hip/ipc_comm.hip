@@ -65,6 +65,13 @@ __device__ __forceinline__ void row_copy(const uint8_t* __restrict__ s, uint8_t*
     reinterpret_cast<uint32_t*>(d)[i] = reinterpret_cast<const uint32_t*>(s)[i];
 }
 
+// `bytes` (a multiple of 4) of zeros at d by the blocks of one grid row.
+__device__ __forceinline__ void row_zero(uint8_t* __restrict__ d, uint64_t bytes) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < bytes / 4; i += stride)
+    reinterpret_cast<uint32_t*>(d)[i] = 0u;
+}
+
 __device__ __forceinline__ bool rank_failed(const uint64_t* segs, int rank) {
   __shared__ bool f;
   if (threadIdx.x == 0) f = ipc_ld(word_at(segs[rank], kIpcFailedOff)) != 0;
@@ -101,7 +108,13 @@ __global__ __launch_bounds__(256) void ipc_out_kernel(uint8_t* __restrict__ dst,
                                                       const uint64_t* __restrict__ segs, int rank, int R, uint64_t cap,
                                                       uint64_t seq, unsigned* __restrict__ ctr,
                                                       uint64_t* __restrict__ reduce_dst, int reduce_n) {
-  if (rank_failed(segs, rank)) return;
+  if (rank_failed(segs, rank)) {
+    // the op never completed: its destination is zeroed rather than left as the
+    // buffer's old (or never written) contents -- a zero region header is an
+    // empty region to every consumer; an all-reduce keeps this rank's own input
+    if (reduce_n == 0) row_zero(dst + (uint64_t)blockIdx.y * dst_stride, recv.n[blockIdx.y]);
+    return;
+  }
   if (threadIdx.x == 0) {  // acquire: the posted flags were read by the wait kernel
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -279,7 +279,10 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
   // each source region's value plane starts past its count-sized ok bitmap: the
   // offsets once per block in LDS, not a dependent header load per message
   __shared__ uint32_t voff[kMaxRanks];
-  for (int d = threadIdx.x; d < R; d += blockDim.x) voff[d] = 4 + (uint32_t)packed_ok_words(rep[(int64_t)d * rep_words]);
+  // (the count clamped to the region: a region no peer wrote this time -- a failed
+  // collective -- holds whatever the buffer held, and must not move the plane out)
+  for (int d = threadIdx.x; d < R; d += blockDim.x)
+    voff[d] = 4 + (uint32_t)packed_ok_words(std::min<int64_t>(rep[(int64_t)d * rep_words], (int64_t)C));
   __syncthreads();
   unsigned long long sum = 0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;

@@ -160,6 +160,79 @@ __device__ __forceinline__ unsigned serve_xlanes(XLane* __restrict__ xl, uint32_
   return (unsigned)__popcll(m);
 }
 
+// Relay table (kMethodRelay): one GPU peer lane per relay slot -- the peer
+// server's lane (imported), this process's reply slot (fine-grained HBM) and the
+// lane's next sequence, kept here on the device (the dispatcher wave owns it).
+// Built by PeerRelay (xcall.hpp); a slot whose call timed out is retired
+// (lane = null: later relays on it answer kStatusNotDelivered).
+struct RelayLane {
+  XLane* lane;
+  uint64_t* reply;
+  uint64_t seq;
+  uint64_t pad;
+};
+constexpr int kRelayMax = 64;
+struct RelayTable {
+  RelayLane lanes[kRelayMax];
+  uint32_t n;  // slots in use
+  uint32_t pad;
+  uint64_t timeout_ticks;
+};
+
+// The dispatcher lanes holding kMethodRelay requests (`mine`) forward them: lane
+// l uses relay slot l % n, one round per group of n lanes (a slot carries one
+// call at a time); each call is a peer-lane publish into the other server's
+// HBM and a spin on the local reply slot (bounded by the table's timeout).
+__device__ __forceinline__ void relay_calls(RelayTable* __restrict__ rt, bool mine, const MsgRecord& msg,
+                                            ReplyRecord& r) {
+  const unsigned lane = lane_id();
+  const uint32_t n = rt->n;
+  if (n == 0) {
+    if (mine) r.status = kStatusNoMethod;
+    return;
+  }
+  for (uint32_t round = 0; round * n < (uint32_t)kWave; ++round) {
+    if (!mine || lane / n != round) continue;
+    RelayLane* L = &rt->lanes[lane % n];
+    // the slot's words through memory-side atomics: the wave may be relaunched on
+    // another XCD, whose L2 could hold a line of the table from an earlier run
+    auto slot_ld = [](uint64_t* p) { return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto slot_st = [](uint64_t* p, uint64_t v) {
+      (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    uint64_t* lane_word = reinterpret_cast<uint64_t*>(&L->lane);
+    XLane* x = reinterpret_cast<XLane*>(slot_ld(lane_word));
+    r.value = 0;
+    r.status = kStatusNotDelivered;
+    if (!x) continue;
+    const uint64_t seq = slot_ld(&L->seq);
+    const uint64_t w0 = (uint64_t)msg.actor | ((uint64_t)(uint16_t)msg.a0 << 32) | ((uint64_t)kFlagValid << 48);
+    sys_st(&x->w0, w0);
+    sys_st(reinterpret_cast<uint64_t*>(&x->a0), (uint64_t)msg.a1);
+    sys_st(reinterpret_cast<uint64_t*>(&x->a1), (uint64_t)msg.a2);
+    sys_st(reinterpret_cast<uint64_t*>(&x->a2), 0ull);
+    __threadfence_system();
+    sys_st(&x->req_tag, seq + 1);
+    const uint64_t t0 = realtime_ticks();
+    for (;;) {
+      const uint64_t tag = sys_ld(L->reply + 1);
+      if (reply_tag_is(tag, seq)) {
+        const int64_t v = (int64_t)sys_ld(L->reply);
+        if (sys_ld(L->reply + 1) != tag) continue;  // the value belongs to this tag only if it still carries it
+        r.value = v;
+        r.status = (int32_t)(tag & 0xff);
+        slot_st(&L->seq, seq + 1);
+        break;
+      }
+      if (realtime_ticks() - t0 > rt->timeout_ticks) {
+        slot_st(lane_word, 0ull);  // out of step with the peer: retired
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __restrict__ req,
                                                                  ReplySlot* __restrict__ rep, uint64_t ring_mask,
                                                                  ServerCtrl* __restrict__ ctrl, uint64_t head,
@@ -178,6 +251,7 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
   unsigned idle_polls = 0, iters = 0;
   // GPU peer lanes are polled only while some are registered (re-read on the idle path)
   uint32_t nxl = xl ? (uint32_t)min<uint64_t>(sys_ld(&ctrl->xl_n), (uint64_t)nx) : 0u;
+  RelayTable* relay = reinterpret_cast<RelayTable*>(sys_ld(&ctrl->relay));  // (re-read on the idle path)
   for (;;) {
     // every poll is a PCIe round trip to host memory: the stop flag is read on
     // one poll in 16, not before every ring poll (that made a poll two trips)
@@ -209,6 +283,7 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
           trace_mask = sys_ld(&ctrl->trace_mask);
           trace = reinterpret_cast<TraceRec*>(sys_ld(&ctrl->trace_ring));
           if (xl) nxl = (uint32_t)min<uint64_t>(sys_ld(&ctrl->xl_n), (uint64_t)nx);
+          relay = reinterpret_cast<RelayTable*>(sys_ld(&ctrl->relay));
         }
         if (lane == 0 && sys_ld(&ctrl->calib_req)) {  // clock calibration handshake
           sys_st(&ctrl->calib_ticks, realtime_ticks());
@@ -268,7 +343,10 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
       msg.a0 = (int64_t)w1;
       msg.a1 = (int64_t)w2;
       msg.a2 = (int64_t)w3;
-      const ReplyRecord r = run_handler(msg, state, n_state, delay_ticks);
+      ReplyRecord r;
+      const bool relayed = msg.method == kMethodRelay && relay != nullptr;
+      if (!relayed) r = run_handler(msg, state, n_state, delay_ticks);
+      if (__ballot(relayed)) relay_calls(relay, relayed, msg, r);
       // value + tag in ONE 16-B store (one PCIe write that lands whole): the
       // host that sees the tag sees the value, so no fence and no second write
       ReplySlot* o = &rep[seq & ring_mask];
@@ -453,6 +531,10 @@ class DeviceServer {
 
   std::string shm_name() const { return seg_ ? seg_->name() : std::string(); }
   bool xlanes_exported() const { return xl_ != nullptr; }
+  // kMethodRelay calls of this dispatcher go through `table` (a device RelayTable,
+  // xcall.hpp PeerRelay; 0 turns relaying off).  Takes effect at the wave's next
+  // launch or idle poll.
+  void set_relay(uintptr_t table) { __atomic_store_n(&ctrl_->relay, (uint64_t)table, __ATOMIC_SEQ_CST); }
   uint64_t ring_fds_handed() const { return handoff_ ? handoff_->handed() : 0; }  // client processes that mapped the ring
 
   // Publish n requests and wait for all replies (any thread).

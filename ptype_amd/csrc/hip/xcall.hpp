@@ -171,6 +171,10 @@ class PeerLane {
 
   int lane() const { return lane_; }
   uint64_t calls() const { return seq_; }
+  // the lane as a relay slot: the peer's lane (imported) and this process's reply
+  // slot; the caller must not also call() through it (PeerRelay owns the sequence)
+  XLane* peer_lane() const { return lane_ >= 0 ? peer_ + lane_ : nullptr; }
+  uint64_t* reply_slot() const { return reply_; }
 
  private:
   bool last_status_failed(uintptr_t out_st, uint64_t done, hipStream_t s) {
@@ -229,6 +233,41 @@ class PeerLane {
   uint64_t* done_ = nullptr;
   int lane_ = -1;
   uint64_t seq_ = 0;
+};
+
+// Handler-initiated remote calls: n peer lanes on another process's dispatcher,
+// handed to THIS process's dispatcher as a relay table.  A kMethodRelay request
+// it serves (server.hpp relay_calls) is forwarded from the dispatcher wave
+// through a lane -- publish into the peer's HBM, spin on the local reply slot --
+// and the remote actor's reply returned as the call's own.  Reference: a server
+// handler that itself dials and Calls another node (cluster/rpc.go:59-67).
+class PeerRelay {
+ public:
+  PeerRelay(const std::string& shm_name, int device, int n_lanes, double timeout_s) : device_(device) {
+    if (n_lanes < 1 || n_lanes > kRelayMax) throw std::invalid_argument("PeerRelay: 1..64 lanes");
+    for (int i = 0; i < n_lanes; ++i) lanes_.push_back(std::make_shared<PeerLane>(shm_name, device, 10.0));
+    RelayTable t{};
+    for (int i = 0; i < n_lanes; ++i) t.lanes[i] = RelayLane{lanes_[(size_t)i]->peer_lane(), lanes_[(size_t)i]->reply_slot(), 0, 0};
+    t.n = (uint32_t)n_lanes;
+    t.timeout_ticks = (uint64_t)(timeout_s * 1e8);
+    PT_HIP_CHECK(hipSetDevice(device_));
+    PT_HIP_CHECK(hipMalloc((void**)&table_, sizeof(RelayTable)));
+    PT_HIP_CHECK(hipMemcpy(table_, &t, sizeof t, hipMemcpyHostToDevice));
+  }
+  ~PeerRelay() {
+    (void)hipSetDevice(device_);
+    lanes_.clear();  // lanes first: their release waits for the peer to let go of the reply slots
+    (void)hipFree(table_);
+  }
+  PeerRelay(const PeerRelay&) = delete;
+  PeerRelay& operator=(const PeerRelay&) = delete;
+  uintptr_t table() const { return (uintptr_t)table_; }
+  int lanes() const { return (int)lanes_.size(); }
+
+ private:
+  int device_;
+  std::vector<std::shared_ptr<PeerLane>> lanes_;
+  RelayTable* table_ = nullptr;
 };
 
 }  // namespace ptype

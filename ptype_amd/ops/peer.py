@@ -57,3 +57,34 @@ class PeerCaller:
         done = self._lane.call(p(actor), p(mcol), mu, p(c0), p(c1), p(c2), n, p(val), p(st), p(ticks),
                                float(timeout_s), stream)
         return val, st, ticks.to(torch.float64) * TICK_NS, int(done)
+
+
+class PeerRelay:
+    """Handler-initiated remote calls: ``n_lanes``
+    GPU peer lanes on another process's dispatcher, handed to ``server`` (this
+    process's ``DeviceServer``) as its relay table.  A request to ``server``
+    with method ``METHOD_RELAY`` -- actor = the REMOTE actor, a0 = the remote
+    method, a1/a2 = its arguments -- is forwarded by the dispatcher wave itself
+    (publish into the peer's HBM lane, spin on a reply slot in this GPU's HBM)
+    and the remote reply returned as the call's own: a handler that calls
+    another server, with no host between the hops (reference: a handler
+    dialling another node, cluster/rpc.go:59-67).
+
+    Close ``server`` (or ``detach()`` and let it go idle) before dropping the
+    relay: the wave reads the table until its next idle refresh."""
+
+    def __init__(self, server, shm_name: str, device=None, n_lanes: int = 8, timeout_s: float = 1.0):
+        dev = torch.device(device if device is not None else "cuda")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self._relay = hip().PeerRelay(shm_name, dev.index, int(n_lanes), float(timeout_s))
+        self._server = server
+        server.set_relay(self._relay.table)
+
+    @property
+    def lanes(self) -> int:
+        return self._relay.lanes
+
+    def detach(self):
+        self._server.set_relay(0)

@@ -11,6 +11,9 @@ METHOD_RETRY_TEST = 4
 METHOD_COUNTER_ADD = 5
 METHOD_FORWARD = 6  # actor-to-actor tell: count the visit, emit Forward to a0 while a1 > 0
 METHOD_SEQ_FOLD = 7  # ORDERED: reply = state; state = state * FOLD_MUL + a0 (mod 2**64)
+# dispatcher-only: forwarded to another process's actor through a GPU peer lane (csrc/hip/xcall.hpp PeerRelay);
+# actor = remote actor, a0 = remote method, a1 / a2 = its arguments
+METHOD_RELAY = 0x7E
 
 FOLD_MUL = 0x100000001B3
 ORDERED_METHODS = frozenset({METHOD_SEQ_FOLD})  # one at a time per actor, in mailbox order

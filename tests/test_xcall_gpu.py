@@ -74,3 +74,75 @@ def test_gpu_initiated_call_between_processes():
     assert out["ok_mul"] and out["ok_add"], out
     assert tail[0] == "STATE" and int(tail[1]) == 200, tail  # the server's actor state saw every add
     assert out["p50_us"] < 50.0, out  # a GPU->GPU round trip, no host: single-digit microseconds expected
+
+
+_RELAYER = textwrap.dedent("""
+    import json, os, sys, time, torch, numpy as np
+    sys.path.insert(0, os.environ["PTYPE_ROOT"])
+    from ptype_amd.ops import hip
+    from ptype_amd.ops.peer import PeerRelay
+    from ptype_amd.ops.records import METHOD_RELAY, METHOD_CALC_MULTIPLY, METHOD_COUNTER_ADD, STATUS_OK
+    state = torch.zeros(1024, dtype=torch.int64, device="cuda")
+    srv = hip().DeviceServer(0, 1024, state.data_ptr(), 1024, 0, 2000.0, 60.0, f"ptype-relay-{os.getpid()}")
+    relay = PeerRelay(srv, sys.argv[1], "cuda:0", n_lanes=8)
+    # stateful through the relay: 100 CounterAdd(+2) on the REMOTE actor 7, in order
+    adds, lat = [], []
+    for _ in range(100):
+        t = time.perf_counter()
+        v, st, _ = srv.call(METHOD_RELAY, 7, METHOD_COUNTER_ADD, 2)
+        lat.append(time.perf_counter() - t)
+        adds.append((v, st))
+    ok_add = [v for v, _ in adds] == list(range(2, 202, 2)) and all(st == STATUS_OK for _, st in adds)
+    # a batch: 64 relayed Multiply calls served by one dispatcher pass (8 slots, 8 rounds)
+    n = 256
+    req = np.zeros((n, 4), dtype=np.int64)
+    a = np.arange(n, dtype=np.int64) - 100
+    b = np.arange(n, dtype=np.int64) % 13 + 2
+    req[:, 0] = (np.arange(n) % 1024) | (METHOD_RELAY << 32) | (1 << 48)
+    req[:, 1] = METHOD_CALC_MULTIPLY
+    req[:, 2] = a
+    req[:, 3] = b
+    rep = np.zeros((n, 2), dtype=np.int64)
+    t = time.perf_counter()
+    srv.call_many(req.ctypes.data, rep.ctypes.data, n)
+    batch_s = time.perf_counter() - t
+    ok_mul = bool((rep[:, 0] == a * b).all()) and bool(((rep[:, 1] & 0xff) == STATUS_OK).all())
+    # a local (non-relayed) call on the same dispatcher still runs its own handler
+    v, st, _ = srv.call(METHOD_COUNTER_ADD, 7, 5)
+    ok_local = v == 5 and st == STATUS_OK
+    srv.close()
+    del relay
+    lat = sorted(lat[10:])
+    print("RESULT " + json.dumps({"ok_add": ok_add, "ok_mul": ok_mul, "ok_local": ok_local,
+                                  "p50_us": lat[len(lat) // 2] * 1e6, "batch_us": batch_s * 1e6}), flush=True)
+""")
+
+
+@pytest.mark.gpu
+def test_handler_initiated_remote_call_relays_through_the_dispatcher():
+    """A's dispatcher forwards METHOD_RELAY requests to B's actors over GPU peer
+    lanes: B's state sees every relayed add, replies are exact,
+    and A's own handlers keep working alongside."""
+    env = dict(os.environ, PTYPE_ROOT=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    srv = subprocess.Popen([sys.executable, "-c", _SERVER], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, text=True)
+    try:
+        line = srv.stdout.readline().split()
+        assert line and line[0] == "SHM", (line, srv.stderr.read()[-2000:] if srv.poll() is not None else "")
+        assert line[2] == "1", "the server exported no GPU peer lanes"
+        c = subprocess.run([sys.executable, "-c", _RELAYER, line[1]], env=env, capture_output=True, text=True,
+                           timeout=180)
+        assert c.returncode == 0, c.stderr[-3000:]
+        res = [x for x in c.stdout.splitlines() if x.startswith("RESULT ")]
+        assert res, c.stdout[-2000:] + c.stderr[-2000:]
+        out = json.loads(res[0][7:])
+        srv.stdin.write("done\n")
+        srv.stdin.flush()
+        tail = srv.stdout.readline().split()
+        assert srv.wait(60) == 0
+    finally:
+        if srv.poll() is None:
+            srv.kill()
+    print("relay", out, tail)
+    assert out["ok_add"] and out["ok_mul"] and out["ok_local"], out
+    assert tail[0] == "STATE" and int(tail[1]) == 200, tail  # B's actor 7 saw the relayed adds only
