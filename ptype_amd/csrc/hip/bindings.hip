@@ -413,13 +413,19 @@ PYBIND11_MODULE(_hip, m) {
              d["S"] = w.S;  // as moved (the layout's dwords rounded to a kernel variant)
              d["req_words"] = w.req_words;
              d["rep_words"] = w.rep_words;
+             d["req_moved"] = w.req_moved;
+             d["rep_moved"] = w.rep_moved;
+             d["pairs"] = w.pairs;
+             d["cap_out"] = std::vector<uint32_t>(w.cap_out, w.cap_out + e.ranks());
+             d["cap_in"] = std::vector<uint32_t>(w.cap_in, w.cap_in + e.ranks());
              d["C"] = w.C;
              d["agreed"] = w.agreed;
              d["spec_from"] = w.spec_from;
              d["meta"] = std::vector<uint64_t>(w.meta, w.meta + kMetaWords);
              return d;
            },
-           "geometry of the last send (per peer and chunk); agreed: from the agreement of Send spec_from")
+           "geometry of the last send (region strides per peer and chunk; *_moved: words this rank sent per "
+           "chunk, all peers; pairs: per-pair capacities in force); agreed: from the agreement of Send spec_from")
       .def("stats", &SortedExchange::stats)
       .def_property("epoch_counter", &SortedExchange::epoch_counter, &SortedExchange::set_epoch_counter)
       .def("last_overflow", &SortedExchange::last_overflow, py::call_guard<py::gil_scoped_release>(),

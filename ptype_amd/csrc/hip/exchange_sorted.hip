@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kST) void sx_count_kernel(SortIn in, int R, uint32_
 // shard table (clamped to C) and header, and the region total into meta[kMetaCap].
 __global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hist, uint32_t G, int R, uint32_t K,
                                                        uint32_t* __restrict__ sendbuf, int64_t req_stride,
-                                                       int64_t tab_off, uint32_t C, uint32_t method_uniform,
+                                                       SxCaps caps, uint32_t method_uniform,
                                                        uint32_t hdr_flags, int rank_self,
                                                        unsigned long long* __restrict__ meta,
                                                        uint32_t* __restrict__ boff) {
@@ -122,7 +122,10 @@ __global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hi
   __shared__ uint32_t wsum[16];
   const uint32_t B = (uint32_t)R * K;
   const uint32_t d = blockIdx.x;
+  const uint32_t C = caps.c[d];  // this destination's capacity
+  constexpr int64_t tab_off = 4;
   uint32_t* region = sendbuf + (int64_t)d * req_stride;
+  unsigned long long* pair = meta + kSxMetaPair + rank_self * R + d;
   if (K == 1) {  // one column: every thread a row (G <= 1024), a block-wide scan
     const uint32_t r = threadIdx.x, w = r / kWave, lane = lane_id();
     const uint32_t x = r < G ? hist[(size_t)r * B + d] : 0u;
@@ -139,7 +142,10 @@ __global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hi
       region[tab_off] = 0;
       for (int s = 1; s <= kSxShards; ++s) region[tab_off + s] = n;
       *reinterpret_cast<uint4*>(region) = make_uint4(n, all, (uint32_t)rank_self, (hdr_flags << 16) | method_uniform);
-      if (all) meta_max(meta + kMetaCap, all);
+      if (all) {
+        meta_max(meta + kMetaCap, all);
+        meta_max(pair, all);
+      }
     }
     return;
   }
@@ -180,7 +186,10 @@ __global__ __launch_bounds__(1024) void sx_scan_kernel(uint32_t* __restrict__ hi
       const uint32_t n = all < C ? all : C;
       region[tab_off + kSxShards] = n;
       *reinterpret_cast<uint4*>(region) = make_uint4(n, all, (uint32_t)rank_self, (hdr_flags << 16) | method_uniform);
-      if (all) meta_max(meta + kMetaCap, all);
+      if (all) {
+        meta_max(meta + kMetaCap, all);
+        meta_max(pair, all);
+      }
     }
   }
 }
@@ -198,8 +207,12 @@ template <int MODE, int S>
 __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint32_t K, const uint32_t* __restrict__ hist,
                                                          const uint32_t* __restrict__ boff,
                                                          uint32_t* __restrict__ sendbuf, int64_t req_stride,
-                                                         uint32_t C, PackedLayout L, int32_t* __restrict__ perm,
+                                                         uint32_t C, SxCaps caps, PackedLayout L,
+                                                         int32_t* __restrict__ perm,
                                                          unsigned long long* __restrict__ meta) {
+  // C: the region stride in records (positions are encoded rk * C + pos);
+  // caps: each destination's capacity (<= C) -- a message past it overflows
+  __shared__ uint32_t cap_s[kSxMaxRanks];
   __shared__ uint32_t run[kXMaxBuckets];
   __shared__ uint32_t bo[kXMaxBuckets];
   __shared__ uint32_t wcnt[kST / kWave][kXMaxBuckets];
@@ -211,6 +224,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
     run[b] = hist[(size_t)v * B + b];
     bo[b] = boff[b];
   }
+  if (threadIdx.x < (unsigned)kSxMaxRanks) cap_s[threadIdx.x] = caps.c[threadIdx.x];
   MetaAcc acc;
   uint32_t n_ovf = 0;  // messages answered kStatusOverflow (folded into the agreement: send_all's re-send test)
   const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
@@ -277,7 +291,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
       }
       const uint32_t bk = rk * K + (mb[k] & (K - 1));
       const uint32_t pos = bo[bk] + wcnt[w][bk] + (pr[k] >> 8);
-      if (pos >= C) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
+      if (pos >= cap_s[rk]) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
         perm[i] = -1;
         ++n_ovf;
         continue;
@@ -306,7 +320,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
       }
       uint32_t rec[S];
       packed_pack<S>(L, f, rec);
-      store_words<S>(sendbuf + (int64_t)rk * req_stride + 4 + (int64_t)pos * S, rec);
+      store_words<S>(sendbuf + (int64_t)rk * req_stride + kSxRecOff + (int64_t)pos * S, rec);
     }
     __syncthreads();
   }
@@ -332,13 +346,16 @@ template <int MODE, int S>
 __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsigned long long* __restrict__ desc,
                                                           unsigned* __restrict__ tctr, unsigned* __restrict__ ticket,
                                                           uint32_t* __restrict__ sendbuf, int64_t req_stride,
-                                                          int64_t tab_off, uint32_t C, uint32_t hdr_word3,
+                                                          uint32_t C, SxCaps caps, uint32_t hdr_word3,
                                                           int rank_self, PackedLayout L, int32_t* __restrict__ perm,
                                                           unsigned long long* __restrict__ meta,
                                                           unsigned long long* __restrict__ stats) {
   __shared__ uint32_t wcnt[kST / kWave][kSxMaxRanks];
   __shared__ uint32_t pre[kSxMaxRanks];
+  __shared__ uint32_t cap_s[kSxMaxRanks];  // per-destination capacities (C: the region stride in records)
   __shared__ uint32_t tile_s, tag_s, mbmax_s;
+  constexpr int64_t tab_off = 4;
+  if (threadIdx.x < (unsigned)kSxMaxRanks) cap_s[threadIdx.x] = caps.c[threadIdx.x];
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
   if (threadIdx.x == 0) {
     tag_s = epoch_tag(tctr[1]);  // 1..0xffffff across the counter's wrap
@@ -401,12 +418,15 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
     }
     pre[d] = (uint32_t)excl;
     if (t == in.tiles - 1) {  // region d's header and (single-run) shard table
-      const uint32_t all = (uint32_t)(excl + c), n = all < C ? all : C;
+      const uint32_t all = (uint32_t)(excl + c), n = all < cap_s[d] ? all : cap_s[d];
       uint32_t* region = sendbuf + (int64_t)d * req_stride;
       region[tab_off] = 0;
       for (int s2 = 1; s2 <= kSxShards; ++s2) region[tab_off + s2] = n;
       *reinterpret_cast<uint4*>(region) = make_uint4(n, all, (uint32_t)rank_self, hdr_word3);
-      if (all) meta_max(meta + kMetaCap, all);
+      if (all) {
+        meta_max(meta + kMetaCap, all);
+        meta_max(meta + kSxMetaPair + rank_self * R + d, all);
+      }
     }
   }
   __syncthreads();
@@ -423,7 +443,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
       continue;
     }
     const uint32_t pos = pre[rk] + wcnt[w][rk] + (pr[k] >> 8);
-    if (pos >= C) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
+    if (pos >= cap_s[rk]) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
       perm[i] = -1;
       ++n_ovf;
       continue;
@@ -452,7 +472,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
     }
     uint32_t rec[S];
     packed_pack<S>(L, f, rec);
-    store_words<S>(sendbuf + (int64_t)rk * req_stride + 4 + (int64_t)pos * S, rec);
+    store_words<S>(sendbuf + (int64_t)rk * req_stride + kSxRecOff + (int64_t)pos * S, rec);
   }
   acc.mb = mbmax_s;  // (the mailbox maximum of this tile: every lane sees the block's)
   meta_publish(acc, in.mcol != nullptr, in.method_uniform, in.M, meta);
@@ -482,7 +502,7 @@ __device__ __forceinline__ unsigned long long sx_drain_range(const uint32_t* rq,
 #pragma unroll
     for (int u = 0; u < kXDispU; ++u) {
       const int64_t s = base + u * step + lane;
-      if (s < count) load_words<S>(rq + 4 + s * S, wv[u]);
+      if (s < count) load_words<S>(rq + kSxRecOff + s * S, wv[u]);
     }
 #pragma unroll
     for (int u = 0; u < kXDispU; ++u) {
@@ -628,7 +648,7 @@ __global__ __launch_bounds__(kXOrdThreads) void sx_drain_ord_kernel(const uint32
         valid[k] = q[k] < hi;
         uint32_t rec[S];
         if (valid[k]) {
-          load_words<S>(rq + 4 + (int64_t)q[k] * S, rec);
+          load_words<S>(rq + kSxRecOff + (int64_t)q[k] * S, rec);
           const uint64_t mbf = packed_field<S>(L, 1, rec);
           valid[k] = mbf != null_mb;
           mbv[k] = (uint32_t)mbf;
@@ -738,7 +758,7 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   int lo = 0, hi = 0;
   PT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   PT_HIP_CHECK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));
-  const int64_t rq = packed_req_words(C_alloc, 8) + kSxTableWords, rp = packed_rep_words(C_alloc, 8);
+  const int64_t rq = sx_req_words(C_alloc, 8), rp = packed_rep_words(C_alloc, 8);
   for (int i = 0; i < chunks_; ++i) {
     Bufs& b = bufs_[i];
     PT_HIP_CHECK(hipMalloc(&b.send, (size_t)R * rq * 4));
@@ -758,12 +778,12 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   PT_HIP_CHECK(hipMemset(tctr_, 0, 2 * sizeof(unsigned)));
   PT_HIP_CHECK(hipMalloc(&ticket_, kTicketWords * sizeof(unsigned)));
   PT_HIP_CHECK(hipMemset(ticket_, 0, kTicketWords * sizeof(unsigned)));
-  PT_HIP_CHECK(hipMalloc(&meta_dev_, 2 * kMetaWords * sizeof(uint64_t)));
-  PT_HIP_CHECK(hipMemset(meta_dev_, 0, 2 * kMetaWords * sizeof(uint64_t)));
+  PT_HIP_CHECK(hipMalloc(&meta_dev_, 2 * kSxMetaWords * sizeof(uint64_t)));
+  PT_HIP_CHECK(hipMemset(meta_dev_, 0, 2 * kSxMetaWords * sizeof(uint64_t)));
   PT_HIP_CHECK(hipMalloc(&stats_, 3 * sizeof(unsigned long long)));
   PT_HIP_CHECK(hipMemset(stats_, 0, 3 * sizeof(unsigned long long)));
-  PT_HIP_CHECK(hipHostMalloc(&meta_host_, 2 * kMetaWords * sizeof(uint64_t), hipHostMallocDefault));
-  memset(meta_host_, 0, 2 * kMetaWords * sizeof(uint64_t));
+  PT_HIP_CHECK(hipHostMalloc(&meta_host_, 2 * kSxMetaWords * sizeof(uint64_t), hipHostMallocDefault));
+  memset(meta_host_, 0, 2 * kSxMetaWords * sizeof(uint64_t));
   for (auto& e : ev_meta_) PT_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // start-up layout: every column at full width (8-dword records, 8-byte replies)
   uint64_t wide[kMetaWords] = {};
@@ -774,6 +794,7 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   for (int m = 0; m < 8; ++m) wide[kMetaFlags + m] = 1;
   L_ = sx_layout(wide);
   C_ = C0;
+  for (auto& c : cap_) c = (uint32_t)C0;
 }
 
 SortedExchange::~SortedExchange() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
@@ -820,7 +841,7 @@ uint64_t SortedExchange::last_overflow() const {
   const int j = (int)(k & 1);
   if (meta_send_[j] != k) throw std::runtime_error("SortedExchange: the last Send recorded no agreement (captured)");
   PT_HIP_CHECK(hipEventSynchronize(ev_meta_[j]));
-  return meta_host_[j * kMetaWords + kMetaOverflow];
+  return meta_host_[j * kSxMetaWords + kMetaOverflow];
 }
 
 void SortedExchange::adopt(const uint64_t* meta, int64_t from) {
@@ -828,16 +849,37 @@ void SortedExchange::adopt(const uint64_t* meta, int64_t from) {
   // the busiest bucket of the last kNeedWindow agreements: a small Send (send_all's
   // re-send of a few overflowed messages) must not shrink the capacity of the full
   // Sends after it.  Every rank sees the same agreements, so all derive the same C.
-  need_hist_[need_n_++ % kNeedWindow] = meta[kMetaCap];
-  uint64_t busiest = 0;
-  for (int j = 0; j < kNeedWindow && j < need_n_; ++j) busiest = std::max(busiest, need_hist_[j]);
-  const double need = (double)busiest;
+  const int h = need_n_++ % kNeedWindow;
+  need_hist_[h] = meta[kMetaCap];
+  const int RR = R_ * R_;
+  std::copy(meta + kSxMetaPair, meta + kSxMetaPair + RR, pair_hist_[h]);
   // the busiest bucket two Sends ago plus 1 % and 8 sigma: uniform traffic then
   // overflows with probability ~1e-15 per bucket, and skewed traffic that is
   // stable over a few Sends fits as well
-  int64_t c = (int64_t)(need * 1.01 + 8.0 * sqrt(need) + 64.0);
-  c = ((c + 63) / 64) * 64;
-  C_ = std::max<int64_t>(64, std::min<int64_t>(c, C_alloc_));
+  auto capacity = [&](uint64_t need) {
+    int64_t c = (int64_t)((double)need * 1.01 + 8.0 * sqrt((double)need) + 64.0);
+    c = ((c + 63) / 64) * 64;
+    return std::max<int64_t>(64, std::min<int64_t>(c, C_alloc_));
+  };
+  uint64_t busiest = 0;
+  for (int j = 0; j < kNeedWindow && j < need_n_; ++j) busiest = std::max(busiest, need_hist_[j]);
+  C_ = capacity(busiest);
+  // per pair (sender p -> destination q): the same rule over that pair's totals.
+  // Under skew (one hot destination) the uniform C moves every pair at the hot
+  // pair's size; prefixes of per-pair capacities move what the traffic needs.
+  // Worth it only when the bytes saved are real: every rank evaluates the same
+  // matrix, so all take the same decision.
+  int64_t sum_pairs = 0;
+  for (int k = 0; k < RR; ++k) {
+    uint64_t need = 0;
+    for (int j = 0; j < kNeedWindow && j < need_n_; ++j) need = std::max(need, pair_hist_[j][k]);
+    cap_[k] = (uint32_t)std::min<int64_t>(capacity(need), C_);
+    sum_pairs += cap_[k];
+  }
+  static const bool pairs_off = getenv("PTYPE_SX_PAIRS") && atoi(getenv("PTYPE_SX_PAIRS")) == 0;
+  pairs_ = !pairs_off && R_ > 1 && (double)sum_pairs < 0.85 * (double)C_ * RR;
+  if (!pairs_)
+    for (int k = 0; k < RR; ++k) cap_[k] = (uint32_t)C_;
   agreed_ = true;
   spec_from_ = from;
   std::copy(meta, meta + kMetaWords, spec_meta_);
@@ -853,12 +895,14 @@ void SortedExchange::pick_spec(hipStream_t cs) {
   const int j = (int)(want & 1);
   if (meta_send_[j] != want) return;  // recorded under a graph capture: keep the layout in force
   PT_HIP_CHECK(hipEventSynchronize(ev_meta_[j]));
-  adopt(meta_host_ + j * kMetaWords, want);
+  adopt(meta_host_ + j * kSxMetaWords, want);
 }
 
-void SortedExchange::a2a(const void* src, void* dst, size_t bytes_per_peer, bool grouped_p2p) {
+void SortedExchange::a2a(const void* src, void* dst, size_t stride, const size_t* send, const size_t* recv,
+                         bool grouped_p2p) {
   if (fake_) {
-    fake_->alltoall(rank_, src, dst, bytes_per_peer, comm_stream_);
+    if (send) fake_->alltoallv(rank_, src, dst, stride, send, recv, comm_stream_);
+    else fake_->alltoall(rank_, src, dst, stride, comm_stream_);
     return;
   }
   // PTYPE_SX_SELF_COPY: at world 1 the all-to-all is a device copy.  RCCL
@@ -868,38 +912,38 @@ void SortedExchange::a2a(const void* src, void* dst, size_t bytes_per_peer, bool
   // capture test validates the captured pipeline with the copy in their place.
   static const bool self_copy = getenv("PTYPE_SX_SELF_COPY") != nullptr;
   if (self_copy && R_ == 1) {
-    PT_HIP_CHECK(hipMemcpyAsync(dst, src, bytes_per_peer, hipMemcpyDeviceToDevice, comm_stream_));
+    PT_HIP_CHECK(hipMemcpyAsync(dst, src, recv ? recv[0] : stride, hipMemcpyDeviceToDevice, comm_stream_));
     return;
   }
-  if (grouped_p2p && rccl().p2p()) {
-    // under a hipGraph capture: ncclAllToAll's captured form crashed graph
-    // instantiation here (RCCL 2.26; tools/rccl_capture_probe.py) while grouped
-    // ncclSend / ncclRecv -- what torch captures -- instantiate and replay
-    auto check = [](int rc, const char* what) {
-      if (rc != 0)
-        throw std::runtime_error(std::string(what) + " failed: " + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
-    };
+  auto check = [](int rc, const char* what) {
+    if (rc != 0)
+      throw std::runtime_error(std::string(what) + " failed: " + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+  };
+  if ((grouped_p2p || send) && rccl().p2p()) {
+    // per-pair prefixes (send / recv sizes), or under a hipGraph capture:
+    // ncclAllToAll's captured form crashed graph instantiation here (RCCL 2.26;
+    // tools/rccl_capture_probe.py) while grouped ncclSend / ncclRecv -- what
+    // torch captures -- instantiate and replay
     check(rccl().group_start(), "ncclGroupStart");
     for (int q = 0; q < R_; ++q) {
-      check(rccl().send((const char*)src + (size_t)q * bytes_per_peer, bytes_per_peer, kNcclInt8, q, comm_,
+      check(rccl().send((const char*)src + (size_t)q * stride, send ? send[q] : stride, kNcclInt8, q, comm_,
                         comm_stream_), "ncclSend");
-      check(rccl().recv((char*)dst + (size_t)q * bytes_per_peer, bytes_per_peer, kNcclInt8, q, comm_, comm_stream_),
+      check(rccl().recv((char*)dst + (size_t)q * stride, recv ? recv[q] : stride, kNcclInt8, q, comm_, comm_stream_),
             "ncclRecv");
     }
     check(rccl().group_end(), "ncclGroupEnd");
     return;
   }
-  const int rc = rccl().alltoall(src, dst, bytes_per_peer, kNcclInt8, comm_, comm_stream_);
-  if (rc != 0)
-    throw std::runtime_error(std::string("ncclAllToAll failed: ") + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
+  if (send) throw std::runtime_error("SortedExchange: per-pair sizes need RCCL's grouped send / recv");
+  check(rccl().alltoall(src, dst, stride, kNcclInt8, comm_, comm_stream_), "ncclAllToAll");
 }
 
 void SortedExchange::allreduce_meta(uint64_t* dev, hipStream_t s) {
   if (fake_) {
-    fake_->allreduce_max(rank_, dev, kMetaWords, s);
+    fake_->allreduce_max(rank_, dev, kSxMetaPair + R_ * R_, s);
     return;
   }
-  const int rc = rccl().allreduce(dev, dev, kMetaWords, kNcclUint64, kNcclMax, comm_, s);
+  const int rc = rccl().allreduce(dev, dev, kSxMetaPair + R_ * R_, kNcclUint64, kNcclMax, comm_, s);
   if (rc != 0)
     throw std::runtime_error(std::string("ncclAllReduce failed: ") + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
 }
@@ -917,8 +961,27 @@ void SortedExchange::send(const SxSend& a) {
   const PackedLayout L = L_;
   const int S = sx_round_S(L.S);
   const int64_t C = C_;
-  const int64_t tab_off = packed_req_words(C, S);
-  const int64_t rq = tab_off + kSxTableWords, rp = packed_rep_words(C, L.vb);
+  constexpr int64_t tab_off = 4;  // the shard table follows the header
+  const int64_t rq = sx_req_words(C, S), rp = packed_rep_words(C, L.vb);
+  // per-pair capacities: this rank's requests to q fit cap_out[q], p's to this
+  // rank cap_in[p]; with pairs_ only those prefixes move (grouped send / recv).
+  // Loopback (one rank standing for all): what "arrives" from q is what this
+  // rank sent to q, so the inbound capacities are the outbound ones.
+  const bool loop = fake_ && fake_->loopback();
+  SxCaps caps_out{}, caps_in{};
+  size_t rq_send[kSxMaxRanks], rq_recv[kSxMaxRanks], rp_send[kSxMaxRanks], rp_recv[kSxMaxRanks];
+  int64_t req_moved = 0, rep_moved = 0;
+  for (int q = 0; q < R_; ++q) {
+    caps_out.c[q] = pairs_ ? cap_[rank_ * R_ + q] : (uint32_t)C;
+    caps_in.c[q] = pairs_ ? (loop ? caps_out.c[q] : cap_[q * R_ + rank_]) : (uint32_t)C;
+    rq_send[q] = 4 * (size_t)sx_req_words(caps_out.c[q], S);
+    rq_recv[q] = 4 * (size_t)sx_req_words(caps_in.c[q], S);
+    rp_send[q] = 4 * (size_t)packed_rep_words(caps_in.c[q], L.vb);   // replies to q answer q's requests
+    rp_recv[q] = 4 * (size_t)packed_rep_words(caps_out.c[q], L.vb);
+    req_moved += (int64_t)rq_send[q] / 4;
+    rep_moved += (int64_t)rp_send[q] / 4;
+  }
+  const bool pairs = pairs_;
   wire_ = SxWire();
   wire_.L = L;
   wire_.S = S;
@@ -928,9 +991,14 @@ void SortedExchange::send(const SxSend& a) {
   wire_.agreed = agreed_;
   wire_.spec_from = spec_from_;
   std::copy(spec_meta_, spec_meta_ + kMetaWords, wire_.meta);
+  wire_.req_moved = req_moved;
+  wire_.rep_moved = rep_moved;
+  wire_.pairs = pairs;
+  std::copy(caps_out.c, caps_out.c + kSxMaxRanks, wire_.cap_out);
+  std::copy(caps_in.c, caps_in.c + kSxMaxRanks, wire_.cap_in);
   const int cur = (int)(sends_ & 1);
-  uint64_t* meta = meta_dev_ + cur * kMetaWords;
-  PT_HIP_CHECK(hipMemsetAsync(meta, 0, kMetaWords * sizeof(uint64_t), cs));
+  uint64_t* meta = meta_dev_ + cur * kSxMetaWords;
+  PT_HIP_CHECK(hipMemsetAsync(meta, 0, kSxMetaWords * sizeof(uint64_t), cs));
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
   const bool may_order = a.ordered;
   // sort by actor shard only when this rank's batch may carry ordered methods;
@@ -1012,7 +1080,7 @@ void SortedExchange::send(const SxSend& a) {
     PT_HIP_CHECK(hipGetLastError());
     PT_HIP_CHECK(hipEventRecord(ev_served_[i], cs));
     PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_served_[i], 0));
-    a2a(b.reply, b.back, (size_t)rp * 4, capturing);
+    a2a(b.reply, b.back, (size_t)rp * 4, pairs ? rp_send : nullptr, pairs ? rp_recv : nullptr, capturing);
     PT_HIP_CHECK(hipEventRecord(ev_rep_in_[i], comm_stream_));
   };
   for (int i = 0; i < chunks_; ++i) {
@@ -1033,7 +1101,7 @@ void SortedExchange::send(const SxSend& a) {
       const uint32_t hdr3 = ((uint32_t)kFlagValid << 16) | (uint32_t)a.method_uniform;
 #define PT_SX_OS(MO, SV)                                                                                         \
   hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_, ticket_, \
-                     b.send, rq, tab_off, (uint32_t)C, hdr3, rank_, L, b.perm, (unsigned long long*)meta, stats_)
+                     b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm, (unsigned long long*)meta, stats_)
 #define PT_SX_OS_S(MO)              \
   switch (S) {                      \
     case 1: PT_SX_OS(MO, 1); break; \
@@ -1055,20 +1123,20 @@ void SortedExchange::send(const SxSend& a) {
       PT_HIP_CHECK(hipGetLastError());
       PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
       PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_routed_[i], 0));
-      a2a(b.send, b.recv, (size_t)rq * 4, capturing);
+      a2a(b.send, b.recv, (size_t)rq * 4, pairs ? rq_send : nullptr, pairs ? rq_recv : nullptr, capturing);
       PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], comm_stream_));
       if (i > 0) serve(i - 1);
       continue;
     }
     PT_SX_MODE(sx_count_kernel, dim3(in.G), dim3(kST), 0, cs, in, R_, K, hist_, (unsigned long long*)meta,
                mode == 2 ? nullptr : (uint32_t*)b.perm);
-    hipLaunchKernelGGL(sx_scan_kernel, dim3(R_), dim3(1024), 0, cs, hist_, in.G, R_, K, b.send, rq, tab_off,
-                       (uint32_t)C, (uint32_t)a.method_uniform,
+    hipLaunchKernelGGL(sx_scan_kernel, dim3(R_), dim3(1024), 0, cs, hist_, in.G, R_, K, b.send, rq, caps_out,
+                       (uint32_t)a.method_uniform,
                        (uint32_t)(kFlagValid | (sharded ? kFlagSharded : 0)), rank_, (unsigned long long*)meta, boff_);
 #undef PT_SX_MODE
 #define PT_SX_SCAT(MO, SV)                                                                                       \
   hipLaunchKernelGGL((sx_scatter_kernel<MO, SV>), dim3(in.G), dim3(kST), 0, cs, in, R_, K, (const uint32_t*)hist_, \
-                     (const uint32_t*)boff_, b.send, rq, (uint32_t)C, L, b.perm, (unsigned long long*)meta)
+                     (const uint32_t*)boff_, b.send, rq, (uint32_t)C, caps_out, L, b.perm, (unsigned long long*)meta)
 #define PT_SX_SCAT_S(MO)            \
   switch (S) {                      \
     case 1: PT_SX_SCAT(MO, 1); break; \
@@ -1090,7 +1158,7 @@ void SortedExchange::send(const SxSend& a) {
     PT_HIP_CHECK(hipGetLastError());
     PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
     PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_routed_[i], 0));
-    a2a(b.send, b.recv, (size_t)rq * 4, capturing);
+    a2a(b.send, b.recv, (size_t)rq * 4, pairs ? rq_send : nullptr, pairs ? rq_recv : nullptr, capturing);
     PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], comm_stream_));
     if (i > 0) serve(i - 1);
   }
@@ -1100,7 +1168,7 @@ void SortedExchange::send(const SxSend& a) {
   // code to adopt a new one), so it records no agreement.
   if (!capturing) {
     allreduce_meta(meta, comm_stream_);
-    PT_HIP_CHECK(hipMemcpyAsync(meta_host_ + cur * kMetaWords, meta, kMetaWords * sizeof(uint64_t),
+    PT_HIP_CHECK(hipMemcpyAsync(meta_host_ + cur * kSxMetaWords, meta, (kSxMetaPair + R_ * R_) * sizeof(uint64_t),
                                 hipMemcpyDeviceToHost, comm_stream_));
     PT_HIP_CHECK(hipEventRecord(ev_meta_[cur], comm_stream_));
     meta_send_[cur] = sends_;

@@ -31,8 +31,12 @@
 // wider than agreed, or its bucket past C) is answered STATUS_OVERFLOW --
 // send_all re-sends it -- and its slot carries a null record (mailbox field all
 // ones, which no real mailbox uses: the agreed width leaves room for it).
-// Padded all-to-alls (ncclAllToAll, equal split) keep the step free of host
-// sizes, so it also captures into a hipGraph.
+// The all-to-alls need no host sizes of their own either: padded regions
+// (ncclAllToAll, equal split) while traffic is even, and under skew the agreed
+// per-(sender, destination) capacities -- the same lag-2 agreement carries the
+// R x R matrix of region totals -- whose region prefixes move by grouped
+// ncclSend / ncclRecv (each region is [header][shard table][records], so its
+// used part is a prefix).  Either way the step captures into a hipGraph.
 //
 // Reference: the batched fan-out this replaces is the optimus coordinator's
 // goroutine-per-range Calls (example/optimus/coordinator/coordinator.go:67-98)
@@ -51,7 +55,18 @@ constexpr int kSxShardBits = 6;  // actor shards per rank on the wire: mailbox &
 constexpr int kSxShards = 1 << kSxShardBits;
 constexpr int kSxMaxRanks = 16;
 constexpr int kSxMaxChunks = 4;
-constexpr int kSxTableWords = (kSxShards + 1 + 3) & ~3;  // shard table at the end of a request region
+constexpr int kSxTableWords = (kSxShards + 1 + 3) & ~3;  // shard table, right after a request region's header
+constexpr int kSxRecOff = 4 + kSxTableWords;             // records start here: a region's used part is a prefix
+// request region words for n records of S dwords: [header 4][shard table][n * S], 16-B padded
+__host__ __device__ inline int64_t sx_req_words(int64_t n, int S) { return (kSxRecOff + n * S + 3) & ~3ll; }
+// The agreement vector: the packed meta words, then the R x R matrix of
+// per-(sender, destination) region totals (row = sender; the MAX all-reduce
+// fills every row) -- the per-pair capacities of Send + 2.
+constexpr int kSxMetaPair = kMetaWords;
+constexpr int kSxMetaWords = kMetaWords + kSxMaxRanks * kSxMaxRanks;
+struct SxCaps {  // per-destination capacities (records), by value into the sender's kernels
+  uint32_t c[kSxMaxRanks];
+};
 
 struct SxSend {
   uintptr_t actor = 0, a0 = 0, a1 = 0, a2 = 0, method_col = 0;
@@ -72,8 +87,13 @@ struct SxWire {
   PackedLayout L{};
   int S = 0;                // dwords per request record as moved (L.S rounded to a kernel variant)
   int64_t C = 0;            // per-peer capacity (records) of this Send
-  int64_t req_words = 0;    // per peer, per chunk, as moved
+  int64_t req_words = 0;    // region stride (per peer, per chunk; the moved prefix may be shorter)
   int64_t rep_words = 0;
+  int64_t req_moved = 0;    // words this rank sends per chunk, all peers (requests / replies)
+  int64_t rep_moved = 0;
+  bool pairs = false;       // per-pair capacities in force (prefixes moved by grouped send / recv)
+  uint32_t cap_out[kSxMaxRanks] = {};  // this rank's capacity per destination
+  uint32_t cap_in[kSxMaxRanks] = {};   // per source
   bool agreed = false;      // L and C came from an agreement (else the start-up wide layout)
   int64_t spec_from = -1;   // the Send whose agreement they came from
   uint64_t meta[kMetaWords] = {};
@@ -90,6 +110,7 @@ class SortedExchange {
   void send(const SxSend& a);
   const SxWire& last_wire() const { return wire_; }
   int64_t sends() const { return sends_; }
+  int ranks() const { return R_; }
   // receiver counters: handler failures, replies wider than agreed; sender: one-pass look-backs that gave up (0)
   std::vector<uint64_t> stats() const;
   // Messages answered STATUS_OVERFLOW by the last Send, max over the ranks (0: no
@@ -107,7 +128,8 @@ class SortedExchange {
   };
   void pick_spec(hipStream_t cs);
   void adopt(const uint64_t* meta, int64_t from);
-  void a2a(const void* src, void* dst, size_t bytes_per_peer, bool grouped_p2p = false);
+  // regions `stride` bytes apart; send[q] / recv[q] bytes of each (nullptr: whole regions)
+  void a2a(const void* src, void* dst, size_t stride, const size_t* send, const size_t* recv, bool grouped_p2p);
   void allreduce_meta(uint64_t* dev, hipStream_t s);
   bool collectives() const { return comm_ != nullptr || fake_ != nullptr; }
 
@@ -123,8 +145,8 @@ class SortedExchange {
   unsigned long long* desc_ = nullptr;  // [tiles][R] one-pass look-back descriptors (rank-only batches)
   unsigned* tctr_ = nullptr;    // [0] one-pass tile counter (self-resetting), [1] its epoch tag
   unsigned* ticket_ = nullptr;  // last-block ticket of the one-pass kernel (self-resetting)
-  uint64_t* meta_dev_ = nullptr;   // [2][kMetaWords] agreement vectors (device)
-  uint64_t* meta_host_ = nullptr;  // [2][kMetaWords] pinned copies
+  uint64_t* meta_dev_ = nullptr;   // [2][kSxMetaWords] agreement vectors (device)
+  uint64_t* meta_host_ = nullptr;  // [2][kSxMetaWords] pinned copies
   unsigned long long* stats_ = nullptr;  // [2] receiver counters
   hipEvent_t ev_meta_[2]{};
   int64_t meta_send_[2] = {-1, -1};  // the Send whose agreement each buffer holds
@@ -138,7 +160,12 @@ class SortedExchange {
   uint64_t spec_meta_[kMetaWords] = {};
   static constexpr int kNeedWindow = 4;      // capacity: the busiest bucket of the last 4 agreements
   uint64_t need_hist_[kNeedWindow] = {};
+  uint64_t pair_hist_[kNeedWindow][kSxMaxRanks * kSxMaxRanks] = {};  // per-pair totals of the same agreements
   int need_n_ = 0;
+  // per-pair capacities in force (row = sender); pairs_: they differ enough from
+  // the uniform C that moving prefixes pays (the same decision on every rank)
+  uint32_t cap_[kSxMaxRanks * kSxMaxRanks] = {};
+  bool pairs_ = false;
   int64_t sends_ = 0;
   SxWire wire_;
 };

@@ -340,8 +340,10 @@ class ActorExchange:
                  affine, B._ptr(out_val), B._ptr(out_status), B._ptr(state), 0 if state is None else state.numel(),
                  int(self.delay_us) * 100, self.mailbox_ordered, raw_stream(self.device))
         w = eng.last_wire()
-        w["req_words"] *= self.world  # all peers, per chunk (as the epoch engine reports it)
-        w["rep_words"] *= self.world
+        # words moved per chunk, all peers (as the epoch engine reports it): padded
+        # regions, or the per-pair prefixes when the agreed capacities differ
+        w["req_words"] = w["req_moved"]
+        w["rep_words"] = w["rep_moved"]
         w.update(engine="sorted", exact=False, adapted=bool(w["agreed"]), C_alloc=self._sorted_c_alloc)
         self.last_wire = w
         self.counters.wire_bytes += self.chunks * 4 * (w["req_words"] + w["rep_words"])

@@ -138,6 +138,45 @@ def test_sorted_exchange_ordered_seqfold_fifo_per_sender(R):
             assert mine == sorted(mine), f"actor {x}: sender {r}'s messages out of order"
 
 
+def test_sorted_exchange_zipf_skew_moves_per_pair_prefixes():
+    """under Zipf(1.1) load one destination is hot; the agreed
+    per-(sender, destination) capacities move each region's used prefix
+    (grouped send / recv) instead of every pair at the hot pair's size.  Replies
+    exact, no re-send once the agreement applies, fewer words than padding."""
+    R, n, M = 4, 8192, 120_000
+
+    def body(r, fc, start, s):
+        tab, _ = _table(n, R)
+        st = torch.zeros(n // R + 1, dtype=torch.int64, device="cuda")
+        ex = ActorExchange(tab, M, chunks=1, state=st, fake=(fc, r), delivery="mailbox", mailbox_ordered=False)
+        start.wait()
+        wires, resends = [], []
+        for k in range(7):
+            req = B.gen_zipf_requests(M, n, 1.1, seed=900 + 13 * r + k, device="cuda")
+            before = ex.counters.resends
+            v, sts = ex.send_all(req)
+            s.synchronize()
+            assert bool((sts == STATUS_OK).all()), (k, int((sts != STATUS_OK).sum()))
+            assert torch.equal(v, req.a0 * req.a1), k
+            wires.append(dict(ex.last_wire))
+            resends.append(ex.counters.resends - before)
+        return wires, resends
+
+    res = _run_ranks(R, body)
+    for wires, resends in res:
+        w = wires[-1]
+        assert w["pairs"], w
+        assert max(w["cap_in"]) > 1.2 * min(w["cap_in"]) or max(w["cap_out"]) > 1.2 * min(w["cap_out"]), w
+        padded = R * (w["C"] * w["S"])
+        assert w["req_words"] < 0.9 * padded, (w["req_words"], padded)
+        assert sum(resends[4:]) == 0, resends
+    caps = [tuple(x[0][-1]["cap_out"]) for x in res]
+    ins = [tuple(x[0][-1]["cap_in"]) for x in res]
+    for p in range(R):  # sender p's capacity toward q is what q expects from p
+        for q in range(R):
+            assert caps[p][q] == ins[q][p]
+
+
 def test_sorted_exchange_too_wide_is_overflow_then_resent():
     R, n, M = 2, 4096, 20_000
 
