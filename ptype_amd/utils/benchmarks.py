@@ -171,7 +171,9 @@ def api_send(device, sizes, actors: int, steps: int, warmup: int) -> dict:
     cfg.has_gpu = True
     g = cfg.gpu
     g.device, g.actors, g.max_batch, g.delivery = device.index or 0, actors, max(sizes), "mailbox"
+    g.cpu = device.type == "cpu"  # (the CPU twin of the path, for tests)
     t0 = time.perf_counter()
+    srv = C.Serve(cfg.port, _Host(), host="127.0.0.1")  # the node's net/rpc server (what NewClient dials)
     c = C.Join(C.background(), cfg)
     out = {"path": "Join -> NewClient -> Client.Send (eager, mailbox delivery, pre-generated batches)",
            "join_s": time.perf_counter() - t0}
@@ -200,4 +202,12 @@ def api_send(device, sizes, actors: int, steps: int, warmup: int) -> dict:
         client.Close()
     finally:
         c.Close()
+        srv.Close()
     return out
+
+
+class _Host:
+    """A host-side net/rpc receiver for the node's address (the balancer dials it)."""
+
+    def Ping(self, x):
+        return x

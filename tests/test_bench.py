@@ -120,3 +120,13 @@ def test_bench_zipf_cpu():
     out = _run(2, ["--cpu", "--zipf", "1.1", "--no-secondary"] + SMALL, launcher="self")
     assert out["config"]["load"] == "zipf(1.1)" and out["config"]["pregenerated"] is True
     assert out["value"] > 0
+
+
+def test_api_send_secondary_runs_join_newclient_send_on_cpu():
+    """bench.py's api_send secondary (Join -> NewClient -> Client.Send), CPU twin."""
+    import torch
+
+    from ptype_amd.utils import benchmarks as BM
+
+    out = BM.api_send(torch.device("cpu"), [2048], 512, 2, 1)
+    assert out["2048"]["msgs_per_step"] == 2048 and out["2048"]["value"] > 0
