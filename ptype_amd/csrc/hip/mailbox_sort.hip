@@ -473,7 +473,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   // Up to 64 shards (the stateless 16-shard view): W = kST / S lanes per shard, the
   // whole block looking back W tiles per round trip (lookback_group); more shards:
   // one lane per shard, kLbWin tiles per round trip.
-  const uint32_t W = S <= kST / 8 ? min(64u, kST / S) : 1u;
+  const uint32_t W = (in.lb_group && S <= kST / 8) ? min(64u, kST / S) : 1u;
   uint32_t* tcnt = pre;  // (W > 1) the tile's count per shard, until pre[] takes the prefix
   if (W > 1) {
     for (uint32_t s = threadIdx.x; s < S; s += kST) {
@@ -1402,6 +1402,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.origin_base = a.origin_base;
   static const bool dir_nt = getenv("PTYPE_DIR_NT") && atoi(getenv("PTYPE_DIR_NT")) != 0;
   in.dir_nt = dir_nt;
+  static const bool lb_group = !(getenv("PTYPE_LB_GROUP") && atoi(getenv("PTYPE_LB_GROUP")) == 0);
+  in.lb_group = lb_group;
   in.tiles = (uint32_t)tiles;
   // blocks: as many as the histogram holds (it stays L2-resident for the prefixes),
   // a multiple of 8 (one contiguous eighth of the batch per XCD)

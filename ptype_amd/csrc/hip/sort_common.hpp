@@ -51,6 +51,7 @@ struct SortIn {  // by value
   uint32_t tiles;  // ceil(M / kSTile)
   uint32_t tpb;    // tiles per block
   bool dir_nt;       // non-temporal directory gathers (experiment)
+  bool lb_group;     // one-pass sorts: group look-back (W lanes per shard) where the shard count allows
 };
 
 // Block b's range: XCD (b % 8) owns virtual blocks [x * G/8, (x+1) * G/8).
