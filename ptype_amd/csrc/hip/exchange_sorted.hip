@@ -1027,7 +1027,7 @@ void SortedExchange::send(const SxSend& a) {
     in.rank_self = rank_;
     static const bool dir_nt = getenv("PTYPE_DIR_NT") && atoi(getenv("PTYPE_DIR_NT")) != 0;
     in.dir_nt = dir_nt;
-    static const bool lb_group = !(getenv("PTYPE_LB_GROUP") && atoi(getenv("PTYPE_LB_GROUP")) == 0);
+    static const bool lb_group = getenv("PTYPE_LB_GROUP") && atoi(getenv("PTYPE_LB_GROUP")) == 1;  // measured slower
     in.lb_group = lb_group;
     const int64_t tiles = (m + kSTile - 1) / kSTile;
     int64_t G = std::min<int64_t>({std::max<int64_t>(tiles, 1), (int64_t)(kMboxSortHistWords / B), 1024});

@@ -417,12 +417,21 @@ __device__ __forceinline__ void load_cols(const SortIn& in, uint32_t t, int64_t 
 // across it, more resident blocks; measured slower), else with the actors (in
 // flight across the gathers, the ranking and the look-back).
 // One tile of the one-pass sort (the block claims it); returns its index.
+//
+// reserve (stateless batches): no look-back.  A stateless record runs on its
+// own, so a ring need not hold its messages in message order -- only each
+// tile's run in message order (the drains read a tile's runs through tinfo).
+// The tile is the block's index and each shard's run is reserved with ONE
+// atomicAdd on the shard's epoch counter (gsum row 0, which then holds the
+// epoch's total): 16 device-scope atomics per tile, ~2048 per counter at 8 Mi
+// messages -- against a look-back whose walk grows with the tiles in flight
+// (each hop a memory-side round trip).
 template <int MODE, bool A2, bool MC, bool LATE>
 __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxView& mv, unsigned long long* __restrict__ desc,
                                                   unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                   uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
                                                   uint32_t* __restrict__ rw, const ReplyView& rv, bool spill,
-                                                  bool all_sidx, unsigned char* smem_os) {
+                                                  bool all_sidx, unsigned char* smem_os, bool reserve = false) {
   const uint32_t S = 1u << mv.log_s;
   unsigned long long* base = reinterpret_cast<unsigned long long*>(smem_os);  // ring position of this tile's run (tail + prefix)
   uint32_t* room = reinterpret_cast<uint32_t*>(base + S);                     // offset limit past the tail
@@ -434,14 +443,14 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   // this Send's epoch tag, 1..0xffffff (the drain advances tctr[1]; the modulus keeps the tag inside the
   // descriptor's 24-bit field across the counter's wrap -- tag 0 is reserved for never-published words)
   const uint32_t tag = epoch_tag(tctr[1]);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && !reserve) {
     const uint32_t t = atomicAdd(&tctr[0], 1u);
     if (t == in.tiles - 1) atomicExch(&tctr[0], 0u);  // every block has claimed: ready for the next Send
     tile_s = t;
   }
   for (uint32_t s = lane; s < S; s += kWave) wcnt(w, s) = 0;
   __syncthreads();
-  const uint32_t t = tile_s;
+  const uint32_t t = reserve ? blockIdx.x : tile_s;
   // the tile's columns: actors, then the arguments in flight across the gathers and the ranking
   uint32_t a[kSK], mb[kSK], meth[kSK];
   int64_t v0[kSK], v1[kSK], v2[kSK];
@@ -473,7 +482,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   // Up to 64 shards (the stateless 16-shard view): W = kST / S lanes per shard, the
   // whole block looking back W tiles per round trip (lookback_group); more shards:
   // one lane per shard, kLbWin tiles per round trip.
-  const uint32_t W = (in.lb_group && S <= kST / 8) ? min(64u, kST / S) : 1u;
+  const uint32_t W = (!reserve && in.lb_group && S <= kST / 8) ? min(64u, kST / S) : 1u;
   uint32_t* tcnt = pre;  // (W > 1) the tile's count per shard, until pre[] takes the prefix
   if (W > 1) {
     for (uint32_t s = threadIdx.x; s < S; s += kST) {
@@ -507,7 +516,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
         wcnt(ww, s) = c;
         c += x;
       }
-      if (t == 0) {
+      if (reserve) {
+        excl = c ? atomicAdd(&gsum[s], c) : 0u;  // this tile's run of shard s (gsum row 0: the epoch total)
+      } else if (t == 0) {
         __hip_atomic_exchange(d, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         __hip_atomic_exchange(d, desc_word(tag, kDescA, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -515,7 +526,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
         __hip_atomic_exchange(d, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    if (t == in.tiles - 1) gsum[s] = (uint32_t)(excl + c);  // the epoch's total of shard s
+    if (!reserve && t == in.tiles - 1) gsum[s] = (uint32_t)(excl + c);  // the epoch's total of shard s
     const uint64_t tl = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
     const uint64_t free = hd + Q > tl ? hd + Q - tl : 0;
     const uint32_t rm = (uint32_t)(free < 0xffffffffull ? free : 0xffffffffull);
@@ -587,9 +598,10 @@ __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView m
                                                            unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                            uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
                                                            uint32_t* __restrict__ rw, ReplyView rv, bool spill,
-                                                           bool all_sidx) {
+                                                           bool all_sidx, bool reserve) {
   extern __shared__ __align__(16) unsigned char smem_os[];
-  (void)onesweep_tile<MODE, A2, MC, LATE>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill, all_sidx, smem_os);
+  (void)onesweep_tile<MODE, A2, MC, LATE>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill, all_sidx, smem_os,
+                                          reserve);
 }
 
 // ---------------------------------------------------------------- compact record decode
@@ -948,11 +960,11 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
                                                             uint32_t* __restrict__ rw, ReplyView rv,
                                                             int64_t* __restrict__ state, uint32_t n_state,
                                                             uint64_t delay_ticks, OutboxView ob,
-                                                            unsigned* __restrict__ ticket) {
+                                                            unsigned* __restrict__ ticket, bool reserve) {
   extern __shared__ __align__(16) unsigned char smem_sd[];
   const uint32_t S = 1u << mv.log_s;
   const uint32_t t = onesweep_tile<MODE, A2, MC, false>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, true, false,
-                                                        smem_sd);
+                                                        smem_sd, reserve);
   // every wave's ring stores are out before any wave reads the tile's runs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -968,7 +980,10 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
   }
   __syncthreads();
   if (last) {  // every block's records are read: the rings are consumed
-    for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, 1, S, s, true));
+    // (reserve: the totals were built by memory-side atomics in this launch -- read and
+    // cleared the same way, not through this XCD's L2)
+    for (uint32_t s = threadIdx.x; s < S; s += kST)
+      epoch_commit(mv, s, reserve ? atomicExch(&gsum[s], 0u) : epoch_total(gsum, 1, S, s, true));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
   }
 }
@@ -1338,6 +1353,12 @@ static bool fused_ok() {
   static const bool on = !(getenv("PTYPE_MBOX_FUSED") && std::string(getenv("PTYPE_MBOX_FUSED")) == "0");
   return on;
 }
+// one-pass sorts of stateless batches reserve each tile's runs with atomics
+// instead of looking back (onesweep_tile); PTYPE_MBOX_RESERVE=0: look-back
+static bool reserve_ok() {
+  static const bool on = !(getenv("PTYPE_MBOX_RESERVE") && std::string(getenv("PTYPE_MBOX_RESERVE")) == "0");
+  return on;
+}
 
 void Mailboxes::send_sorted(const MboxSend& a) {
   const uint32_t S = shards();
@@ -1402,7 +1423,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.origin_base = a.origin_base;
   static const bool dir_nt = getenv("PTYPE_DIR_NT") && atoi(getenv("PTYPE_DIR_NT")) != 0;
   in.dir_nt = dir_nt;
-  static const bool lb_group = !(getenv("PTYPE_LB_GROUP") && atoi(getenv("PTYPE_LB_GROUP")) == 0);
+  static const bool lb_group = getenv("PTYPE_LB_GROUP") && atoi(getenv("PTYPE_LB_GROUP")) == 1;  // measured slower
   in.lb_group = lb_group;
   in.tiles = (uint32_t)tiles;
   // blocks: as many as the histogram holds (it stays L2-resident for the prefixes),
@@ -1499,6 +1520,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // the stateless drain: ring order (default) or message order (PTYPE_MBOX_DRAIN=msg: every slot index written)
   static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
   const bool all_sidx = msg_drain && !a.ordered;
+  const bool reserve = !a.ordered && reserve_ok();  // (one-pass only: tiles reserve runs, no look-back)
   uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
   // the LDS-table count (PTYPE_MBOX_SORT=ldscount): directory registry, table <= kStabMax, shards <= 128
   const bool lds_count = sort_mode == 3 && mode == 1 && a.n_dir <= kStabMax && Sv <= 128;
@@ -1553,7 +1575,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #define PT_SD2(MO, A2, MC, FX)                                                                                      \
   hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX>), dim3(in.tiles), dim3(kST), lds, st, in, mv, sort_desc_, \
                      sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv, (int64_t*)a.state, a.n_state,    \
-                     a.delay_ticks, ob, sort_ticket_)
+                     a.delay_ticks, ob, sort_ticket_, reserve)
 #define PT_SD(MO)                                                            \
   do {                                                                       \
     if (a.a2 && a.method_col) PT_SD2(MO, true, true, 0);                     \
@@ -1578,7 +1600,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
 #define PT_OS2(MO, A2, MC, LT)                                                                                     \
   hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv), st, \
-                     in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx)
+                     in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx, \
+                     reserve)
 #define PT_OS1(MO, A2, MC)              \
   do {                                  \
     if (late) PT_OS2(MO, A2, MC, true); \
