@@ -36,6 +36,12 @@
 //                                  lap tags never have it)
 //   w1 = mailbox (24 bits) | method << 24 (7 bits)
 //   w2, w3 = a0, a1 as int32
+// 8 B for stateless batches of one method with two arguments (in.rec8, set by
+// the host: one u64 per slot of plane A viewed as 8-B cells):
+//   bits [0, 12) place in the tile (the drains know the tile) | mailbox (wm bits)
+//   | zigzag a0 (w0 bits) | zigzag a1 (w1 bits),   12 + wm + w0 + w1 = 64
+// where a message whose mailbox or arguments do not fit the fields SPILLS (its
+// tile is drained in message order, the message run straight from the batch);
 // and 32 B (+ the a2 side array) when an argument needs 64 bits or a third
 // argument is present (long form: w1 bit 31, w2 = method | flags << 16, plane B
 // {a0, a1}).  The tagged 32-B records of mailbox.hip stay the format of live
@@ -450,7 +456,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   }
   for (uint32_t s = lane; s < S; s += kWave) wcnt(w, s) = 0;
   __syncthreads();
-  const uint32_t t = reserve ? blockIdx.x : tile_s;
+  // (reserve: tiles dealt XCD by XCD, as the ring drain deals them -- its reads of a tile's runs then
+  // meet the lines in the L2 that took the sort's stores)
+  const uint32_t t = reserve ? virt_block(blockIdx.x, gridDim.x) : tile_s;
   // the tile's columns: actors, then the arguments in flight across the gathers and the ranking
   uint32_t a[kSK], mb[kSK], meth[kSK];
   int64_t v0[kSK], v1[kSK], v2[kSK];
@@ -459,10 +467,17 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   if constexpr (!LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
   resolve_k<MODE>(in, a, r, mb);
   uint32_t wr[kSK];
+  uint32_t escm = 0;  // (in.rec8) messages whose fields do not fit an 8-B record: they spill
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     const bool ok = tile_index(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
     if (!ok) mb[k] = kNoSlot;
+    if (in.rec8 && ok && !LATE) {
+      const uint32_t wm = in.rec8 & 0xffu, w0 = (in.rec8 >> 8) & 0xffu, w1 = (in.rec8 >> 16) & 0xffu;
+      const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
+      const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
+      if ((mb[k] >> wm) != 0 || (z0 >> w0) != 0 || (z1 >> w1) != 0) escm |= 1u << k;
+    }
     const uint32_t sh = mb[k] & (S - 1);
     const uint64_t peers = match_bits(sh, mv.log_s, __ballot(ok));
     const unsigned below = mbcnt64(peers);
@@ -540,6 +555,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
       tinfo[(size_t)t * 2 * S + S + s] = cc | (excl + c > rm ? kRunSpilled : 0u);
     }
   }
+  sp |= escm != 0;
   bool tile_spill = false;
   if (spill) tile_spill = __syncthreads_or(sp) != 0;
   else __syncthreads();
@@ -559,7 +575,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     }
     const uint32_t sh = mb[k] & (S - 1);
     const uint32_t off = pre[sh] + wcnt(w, sh) + wr[k];
-    if (off >= room[sh]) {  // the ring is full
+    if (off >= room[sh] || ((escm >> k) & 1u)) {  // the ring is full (or the record would not fit 8 B)
       if (spill) {  // the drain runs it from the batch: its route word is all it needs from here
         ++n_spill;
         sidx[i] = kSpillSlot;
@@ -574,7 +590,13 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     const uint64_t slot = slot_at(mv, sh, base[sh] + off);
     if (wsidx) sidx[i] = (uint32_t)slot;
     const uint32_t mt = meth[k];
-    if (mt < 128u && fits_i32(v0[k]) && fits_i32(v1[k]) && v2[k] == 0) {
+    if (in.rec8) {  // 8-B record (stateless, uniform method, two arguments; wider ones spilled above)
+      const uint32_t wm = in.rec8 & 0xffu, w0 = (in.rec8 >> 8) & 0xffu;
+      const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
+      const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
+      reinterpret_cast<uint64_t*>(mv.rec)[slot] =
+          (uint64_t)(i & (kSTile - 1)) | ((uint64_t)mb[k] << 12) | (z0 << (12 + wm)) | (z1 << (12 + wm + w0));
+    } else if (mt < 128u && fits_i32(v0[k]) && fits_i32(v1[k]) && v2[k] == 0) {
       *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
           u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)v0[k], (uint32_t)v1[k]};
     } else {
@@ -635,6 +657,25 @@ __device__ __forceinline__ SortRec decode_sorted(const u32x4& ha, const u32x4& h
   return x;
 }
 
+// An 8-B record (in.rec8) of the tile whose first message is `tile_origin`.
+template <bool FRESH>
+__device__ __forceinline__ SortRec decode_rec8(uint64_t r, const SortIn& in, const MboxView&, uint64_t,
+                                               uint32_t tile_origin) {
+  const uint32_t wm = in.rec8 & 0xffu, w0 = (in.rec8 >> 8) & 0xffu, w1 = (in.rec8 >> 16) & 0xffu;
+  const uint64_t m0 = (1ull << w0) - 1;
+  SortRec x;
+  x.valid = true;
+  x.origin = tile_origin + (uint32_t)(r & (kSTile - 1));
+  x.mb = (uint32_t)((r >> 12) & ((1ull << wm) - 1));
+  x.method = in.method_uniform;
+  x.flags = 0;
+  x.a2 = 0;
+  const uint64_t z0 = (r >> (12 + wm)) & m0, z1 = (r >> (12 + wm + w0)) & ((1ull << w1) - 1);
+  x.a0 = (int64_t)(z0 >> 1) ^ -(int64_t)(z0 & 1);
+  x.a1 = (int64_t)(z1 >> 1) ^ -(int64_t)(z1 & 1);
+  return x;
+}
+
 __device__ __forceinline__ SortRec load_sorted(const MboxView& mv, uint64_t slot) {
   const u32x4 ha = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
   u32x4 hb = {0u, 0u, 0u, 0u};
@@ -682,7 +723,7 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 // recorded, replies coalesced; a spilled message runs straight from the batch.
 //
 // The last block commits every shard (and clears the group sums).
-template <int FIXED, bool FRESH = false>
+template <int FIXED, bool FRESH = false, bool R8 = false>
 __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t t,
                                                const uint32_t* __restrict__ sidx, const uint32_t* __restrict__ rw,
                                                int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks,
@@ -694,11 +735,17 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
     const int64_t i = tile_index(t, k);
     sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
   }
-  u32x4 ha[kSK];
+  using RecT = typename std::conditional<R8, uint64_t, u32x4>::type;  // the ring record as loaded
+  RecT ha[kSK];
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
-    const u32x4* rp = reinterpret_cast<const u32x4*>(rec_a(mv, sl[k] < kSpillSlot ? sl[k] : 0));
-    ha[k] = sl[k] < kSpillSlot ? (FRESH ? __builtin_nontemporal_load(rp) : *rp) : u32x4{0u, 0u, 0u, 0u};
+    if constexpr (R8) {
+      const uint64_t* rp = reinterpret_cast<const uint64_t*>(mv.rec) + (sl[k] < kSpillSlot ? sl[k] : 0);
+      ha[k] = sl[k] < kSpillSlot ? (FRESH ? __builtin_nontemporal_load(rp) : *rp) : 0ull;
+    } else {
+      const u32x4* rp = reinterpret_cast<const u32x4*>(rec_a(mv, sl[k] < kSpillSlot ? sl[k] : 0));
+      ha[k] = sl[k] < kSpillSlot ? (FRESH ? __builtin_nontemporal_load(rp) : *rp) : u32x4{0u, 0u, 0u, 0u};
+    }
   }
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
@@ -713,6 +760,8 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
       x.a0 = in.a0[i];
       x.a1 = in.a1 ? in.a1[i] : 0;
       x.a2 = in.a2 ? in.a2[i] : 0;
+    } else if constexpr (R8) {
+      x = decode_rec8<FRESH>(ha[k], in, mv, sl[k], in.origin_base + t * kSTile);
     } else {
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
@@ -834,7 +883,7 @@ struct DrainCounts {
 
 // (views and counts by value: references to a kernel's locals or arguments put
 // them in scratch)
-template <int FIXED, bool NARROW, bool FRESH>
+template <int FIXED, bool NARROW, bool FRESH, bool R8 = false>
 __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, uint32_t t,
                                                        const uint32_t* __restrict__ tinfo,
                                                        const uint32_t* __restrict__ sidx,
@@ -858,11 +907,12 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   int spill = 0;
   const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
   if (spill) {  // some message of the tile spilled: the scatter left the tile's slot indices
-    drain_tile_msg<FIXED, FRESH>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
+    drain_tile_msg<FIXED, FRESH, R8>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
     return DrainCounts{done, failed, holes};
   }
   const uint64_t sbase_mask = (1ull << mv.log_q) - 1;
-  u32x4 ha[kSK];
+  using RecT = typename std::conditional<R8, uint64_t, u32x4>::type;  // the ring record as loaded
+  RecT ha[kSK];
   uint32_t sl[kSK];
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {  // ring order: lane-consecutive entries of the runs
@@ -871,8 +921,13 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
     if (j < T) {
       const uint32_t s = L.owner[j];
       sl[k] = (uint32_t)(((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & sbase_mask));
-      const u32x4* rp = reinterpret_cast<const u32x4*>(rec_a(mv, sl[k]));
-      ha[k] = FRESH ? __builtin_nontemporal_load(rp) : *rp;
+      if constexpr (R8) {
+        const uint64_t* rp = reinterpret_cast<const uint64_t*>(mv.rec) + sl[k];
+        ha[k] = FRESH ? __builtin_nontemporal_load(rp) : *rp;
+      } else {
+        const u32x4* rp = reinterpret_cast<const u32x4*>(rec_a(mv, sl[k]));
+        ha[k] = FRESH ? __builtin_nontemporal_load(rp) : *rp;
+      }
     }
   }
   if constexpr (NARROW) {  // every owner entry is read: its bytes become the status stage
@@ -883,14 +938,19 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     if (sl[k] == kNoSlot) continue;
-    u32x4 hb = {0u, 0u, 0u, 0u};
-    int64_t a2v = 0;
-    if (rec_is_long(ha[k])) {
-      const u32x4* bp = reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
-      hb = FRESH ? __builtin_nontemporal_load(bp) : *bp;
-      if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = FRESH ? __builtin_nontemporal_load(mv.a2 + sl[k]) : mv.a2[sl[k]];
+    SortRec x;
+    if constexpr (R8) {
+      x = decode_rec8<FRESH>(ha[k], in, mv, sl[k], in.origin_base + (uint32_t)i0);
+    } else {
+      u32x4 hb = {0u, 0u, 0u, 0u};
+      int64_t a2v = 0;
+      if (rec_is_long(ha[k])) {
+        const u32x4* bp = reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
+        hb = FRESH ? __builtin_nontemporal_load(bp) : *bp;
+        if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = FRESH ? __builtin_nontemporal_load(mv.a2 + sl[k]) : mv.a2[sl[k]];
+      }
+      x = decode_sorted(ha[k], hb, a2v);
     }
-    const SortRec x = decode_sorted(ha[k], hb, a2v);
     const uint32_t local = x.origin - in.origin_base - (uint32_t)i0;
     if (!x.valid || local >= n_t) {  // never written this epoch (cannot happen on a spill-free tile)
       ++holes;
@@ -916,7 +976,7 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   return DrainCounts{done, failed, holes};
 }
 
-template <int FIXED, bool NARROW>
+template <int FIXED, bool NARROW, bool R8>
 __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ tinfo,
                                                              const uint32_t* __restrict__ sidx,
                                                              const uint32_t* __restrict__ rw,
@@ -930,8 +990,8 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
   // tiles dealt XCD by XCD like the scatter's blocks (whose writes the XCD's L2 may still hold)
   const uint32_t t = virt_block(blockIdx.x, gridDim.x);
   if (t < in.tiles)
-    dc = drain_ring_tile<FIXED, NARROW, false>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob, rv,
-                                               smem_rd);
+    dc = drain_ring_tile<FIXED, NARROW, false, R8>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob, rv,
+                                                   smem_rd);
   block_add_stats(mv.stats, dc.done, kMbProcessed, dc.failed, kMbFailed, dc.holes, kMbHoles);
   __shared__ bool last;
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
@@ -953,7 +1013,7 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
 // waits at a kernel boundary for the slowest tile.  The last block to finish
 // commits every shard's epoch (tail = head = tail + total) and advances the
 // look-back tag.  PTYPE_MBOX_FUSED=0: the separate kernels.
-template <int MODE, bool A2, bool MC, int FIXED>
+template <int MODE, bool A2, bool MC, int FIXED, bool R8>
 __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
                                                             unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                             uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
@@ -968,8 +1028,8 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
   // every wave's ring stores are out before any wave reads the tile's runs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const DrainCounts dc = drain_ring_tile<FIXED, true, true>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks,
-                                                            ob, rv, smem_sd);
+  const DrainCounts dc = drain_ring_tile<FIXED, true, true, R8>(mv, in, t, tinfo, sidx, rw, state, n_state,
+                                                                delay_ticks, ob, rv, smem_sd);
   block_add_stats(mv.stats, dc.done, kMbProcessed, dc.failed, kMbFailed, dc.holes, kMbHoles);
   __shared__ bool last;
   if (threadIdx.x == 0) {
@@ -1448,8 +1508,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // (stateless batches of any size take the one-pass sort when the fused sort + drain is on: one launch per Send)
   const int sort_mode = a.sort_mode ? a.sort_mode
                         : env_mode  ? env_mode
-                        : (tiles >= 1024 || (!a.ordered && !a.arrival && fused_ok())) ? 1
-                                                                                       : 2;
+                        : (tiles >= 1024 || (!a.ordered && !a.arrival && (fused_ok() || reserve_ok()))) ? 1
+                                                                                                         : 2;
   if (sort_mode < 1 || sort_mode > 3) throw std::invalid_argument("mailbox send: sort_mode 0..3");
   const bool two_pass = sort_mode != 1;
   const uint32_t ngroups = two_pass ? (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks) : 1u;
@@ -1521,6 +1581,20 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
   const bool all_sidx = msg_drain && !a.ordered;
   const bool reserve = !a.ordered && reserve_ok();  // (one-pass only: tiles reserve runs, no look-back)
+  // 8-B ring records: one-pass sort of a stateless batch of one two-argument method, ring-order drain
+  // (PTYPE_MBOX_REC8=0: 16-B records).  Field widths: the mailbox from the state size (a wider
+  // mailbox spills), the rest split between the zigzag arguments.
+  static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
+  static const bool rec8_ok = !(getenv("PTYPE_MBOX_REC8") && std::string(getenv("PTYPE_MBOX_REC8")) == "0");
+  const bool r8 = rec8_ok && sort_mode == 1 && !a.ordered && !a.arrival && !a.a2 && !a.method_col && mv.planar &&
+                  !all_sidx && !late;
+  if (r8) {
+    uint32_t wm = 20;
+    if (a.n_state > 1) wm = 32u - (uint32_t)__builtin_clz(a.n_state - 1);
+    wm = std::max(1u, std::min(wm, 24u));
+    const uint32_t w0 = (52u - wm) / 2, w1 = 52u - wm - w0;
+    in.rec8 = wm | (w0 << 8) | (w1 << 16);
+  }
   uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
   // the LDS-table count (PTYPE_MBOX_SORT=ldscount): directory registry, table <= kStabMax, shards <= 128
   const bool lds_count = sort_mode == 3 && mode == 1 && a.n_dir <= kStabMax && Sv <= 128;
@@ -1572,10 +1646,16 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   } else if (!a.ordered && !all_sidx && Sv <= 256 && fused_ok()) {
     // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel)
     const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv));
-#define PT_SD2(MO, A2, MC, FX)                                                                                      \
-  hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX>), dim3(in.tiles), dim3(kST), lds, st, in, mv, sort_desc_, \
+#define PT_SD3(MO, A2, MC, FX, R8)                                                                                  \
+  hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, R8>), dim3(in.tiles), dim3(kST), lds, st, in, mv,          \
+                     sort_desc_,                                                                                     \
                      sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv, (int64_t*)a.state, a.n_state,    \
                      a.delay_ticks, ob, sort_ticket_, reserve)
+#define PT_SD2(MO, A2, MC, FX)                               \
+  do {                                                       \
+    if (!(A2) && !(MC) && r8) PT_SD3(MO, false, false, FX, true); \
+    else PT_SD3(MO, A2, MC, FX, false);                      \
+  } while (0)
 #define PT_SD(MO)                                                            \
   do {                                                                       \
     if (a.a2 && a.method_col) PT_SD2(MO, true, true, 0);                     \
@@ -1591,13 +1671,13 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     if (mode == 2) PT_SD(2); else if (mode == 1) PT_SD(1); else PT_SD(0);
 #undef PT_SD
 #undef PT_SD2
+#undef PT_SD3
     PT_HIP_CHECK(hipGetLastError());
     return;
   } else {
     // one block per tile, claimed in launch order (the grid is exactly the tile count)
     // (PTYPE_OS_LATE=1: arguments loaded after the look-back, 87 instead of 115 VGPRs -- measured slower,
     // 0.231 vs 0.223 ms per 8 Mi Send: the loads' latency is then exposed)
-    static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
 #define PT_OS2(MO, A2, MC, LT)                                                                                     \
   hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv), st, \
                      in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx, \
@@ -1645,12 +1725,17 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_DMSG
   } else {
     static const bool narrow_ok = !(getenv("PTYPE_DRAIN_NARROW") && std::string(getenv("PTYPE_DRAIN_NARROW")) == "0");
-#define PT_DRING1(FX, NW)                                                                                       \
-  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, NW>), dim3(tile_grid), dim3(kST),                               \
+#define PT_DRING2(FX, NW, R8)                                                                                   \
+  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, NW, R8>), dim3(tile_grid), dim3(kST),                           \
                      NW ? ring_lds : (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, mv, in,                 \
                      (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_,       \
                      (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_, \
                      sort_tctr_)
+#define PT_DRING1(FX, NW)                     \
+  do {                                        \
+    if (r8) PT_DRING2(FX, NW, true);          \
+    else PT_DRING2(FX, NW, false);            \
+  } while (0)
 #define PT_DRING(FX)                                   \
   do {                                                 \
     if (narrow_ok && Sv <= 256) PT_DRING1(FX, true);   \
@@ -1660,6 +1745,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else PT_DRING(0);
 #undef PT_DRING
 #undef PT_DRING1
+#undef PT_DRING2
   }
   PT_HIP_CHECK(hipGetLastError());
 }

@@ -52,6 +52,9 @@ struct SortIn {  // by value
   uint32_t tpb;    // tiles per block
   bool dir_nt;       // non-temporal directory gathers (experiment)
   bool lb_group;     // one-pass sorts: group look-back (W lanes per shard) where the shard count allows
+  // 8-B ring records (stateless mailbox Sends, mailbox_sort.hip): mailbox bits | a0 bits << 8 |
+  // a1 bits << 16 (zigzag); 0: 16-B records
+  uint32_t rec8;
 };
 
 // Block b's range: XCD (b % 8) owns virtual blocks [x * G/8, (x+1) * G/8).

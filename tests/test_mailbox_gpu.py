@@ -6,6 +6,11 @@ reference; ordered (SeqFold) traffic is audited by chain reconstruction
 before to after the Send through every message exactly once, which also
 exposes the order each actor ran its messages in (FIFO checks).
 """
+import os
+import subprocess
+import sys
+import textwrap
+
 import pytest
 import torch
 
@@ -15,6 +20,8 @@ from ptype_amd.ops.records import (METHOD_CALC_MULTIPLY, METHOD_PRIME_CHECK, MET
                                    STATUS_OK, STATUS_OVERFLOW)
 from ptype_amd.ops.table import RegistryTable, actor_keys
 from ptype_amd.parallel.exchange import ActorExchange
+
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -409,6 +416,42 @@ def test_sorted_mailbox_stateless_spills_instead_of_overflow():
     torch.cuda.synchronize()
     assert torch.equal(v2, req.a0 * req.a1) and bool((st2 == STATUS_OK).all())
     assert ex.counters.resends == 0 and not calls
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_sorted_mailbox_8b_records_spill_what_does_not_fit(fused):
+    """8-B ring records (stateless one-method batches): the mailbox field is
+    sized from the state (1000 entries: 10 bits) and the arguments share the
+    rest, so actors past mailbox 1023 and arguments of 40 bits cannot be
+    encoded -- those messages spill (run straight from the batch) and every
+    reply is still exact; the rest ride 8-B records.  Fused and separate
+    kernels, in a subprocess (the switches are read once per process)."""
+    code = textwrap.dedent('''
+        import torch
+        from ptype_amd.ops import batch as B
+        from ptype_amd.ops.mailbox import Mailboxes
+        from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
+        from test_mailbox_gpu import placed_table
+        n, M = 5000, 300_000
+        t, _ = placed_table(n)
+        state = torch.zeros(1000, dtype=torch.int64, device="cuda")
+        mb = Mailboxes("cuda", shards=256, slots=16384)
+        for k in range(3):
+            req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=11 + k, device="cuda")
+            if k == 1:
+                req.a0[::97] = (1 << 40) + 3
+                req.a1[::89] = -(1 << 38)
+            v, st = mb.send(req, t, state, ordered=False)
+            torch.cuda.synchronize()
+            assert bool((st == STATUS_OK).all()), int((st != STATUS_OK).sum())
+            assert torch.equal(v, req.a0 * req.a1), k
+        s = mb.stats()
+        assert s["overflow"] == 0 and s["spilled"] > 0 and s["processed"] == 3 * M, s
+        print("OK", s["spilled"])
+    ''')
+    env = dict(os.environ, PTYPE_MBOX_FUSED=fused, PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "tests")]))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
 
 def test_live_mailbox_sustained_overload_keeps_consumer_rate():
