@@ -558,6 +558,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   sp |= escm != 0;
   bool tile_spill = false;
   if (spill) tile_spill = __syncthreads_or(sp) != 0;
+  // a tile spilled by its records' widths (no run overran its ring): flag one of its
+  // runs, so the drains take the tile in message order through the slot indices
+  // (the thread that wrote shard 0's count word: program order)
+  if (tile_spill && tinfo && threadIdx.x == 0) tinfo[(size_t)t * 2 * S + S] |= kRunSpilled;
   else __syncthreads();
   const bool wsidx = all_sidx || tile_spill;
   if constexpr (LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
@@ -1582,15 +1586,17 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   const bool all_sidx = msg_drain && !a.ordered;
   const bool reserve = !a.ordered && reserve_ok();  // (one-pass only: tiles reserve runs, no look-back)
   // 8-B ring records: one-pass sort of a stateless batch of one two-argument method, ring-order drain
-  // (PTYPE_MBOX_REC8=0: 16-B records).  Field widths: the mailbox from the state size (a wider
-  // mailbox spills), the rest split between the zigzag arguments.
+  // (PTYPE_MBOX_REC8=0: 16-B records).  Field widths: the mailbox from the state size or the
+  // directory (a wider mailbox spills), the rest split between the zigzag arguments.
   static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
   static const bool rec8_ok = !(getenv("PTYPE_MBOX_REC8") && std::string(getenv("PTYPE_MBOX_REC8")) == "0");
   const bool r8 = rec8_ok && sort_mode == 1 && !a.ordered && !a.arrival && !a.a2 && !a.method_col && mv.planar &&
                   !all_sidx && !late;
   if (r8) {
+    // (the largest mailbox the routes can name: below the state size, or the directory's actor count)
+    const uint32_t nmb = std::max(a.n_state, a.n_dir);
     uint32_t wm = 20;
-    if (a.n_state > 1) wm = 32u - (uint32_t)__builtin_clz(a.n_state - 1);
+    if (nmb > 1) wm = 32u - (uint32_t)__builtin_clz(nmb - 1);
     wm = std::max(1u, std::min(wm, 24u));
     const uint32_t w0 = (52u - wm) / 2, w1 = 52u - wm - w0;
     in.rec8 = wm | (w0 << 8) | (w1 << 16);
