@@ -216,6 +216,13 @@ class Mailboxes {
   unsigned* sort_tctr_ = nullptr;   // [0] one-pass sort's tile counter (self-resetting), [1] its epoch tag
   uint8_t* sort_stab_ = nullptr;    // LDS-table count: one byte per actor (shard, or not-here / probe)
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
+  // 8-B ring records: [0] the field widths in force (device; updated by each Send's
+  // last block), per-tile field bit lengths, and a pinned mirror of [0] (bit 31: the
+  // fields no longer fit 64 bits -- the host then keeps 16-B records)
+  uint32_t* r8w_ = nullptr;
+  uint32_t* r8max_ = nullptr;
+  uint32_t* r8host_ = nullptr;
+  uint64_t r8_tiles_ = 0;
   // ordered drain: replies staged at ring slots [S * Q], one 16-B word each
   // (value lo, value hi, status, 0) -- one gather per message in the completion
   void* stage_rep_ = nullptr;

@@ -41,7 +41,10 @@
 //   bits [0, 12) place in the tile (the drains know the tile) | mailbox (wm bits)
 //   | zigzag a0 (w0 bits) | zigzag a1 (w1 bits),   12 + wm + w0 + w1 = 64
 // where a message whose mailbox or arguments do not fit the fields SPILLS (its
-// tile is drained in message order, the message run straight from the batch);
+// tile is drained in message order, the message run straight from the batch).
+// The widths are a device word the previous Send's last block sets from that
+// Send's per-tile field maxima (no host read): a batch whose values grow spills
+// for one Send, then fits;
 // and 32 B (+ the a2 side array) when an argument needs 64 bits or a third
 // argument is present (long form: w1 bit 31, w2 = method | flags << 16, plane B
 // {a0, a1}).  The tagged 32-B records of mailbox.hip stay the format of live
@@ -419,6 +422,47 @@ __device__ __forceinline__ void load_cols(const SortIn& in, uint32_t t, int64_t 
   }
 }
 
+__device__ __forceinline__ uint32_t bitlen64(uint64_t x) { return x ? 64u - (uint32_t)__clzll(x) : 0u; }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+  return v;
+}
+
+// The next Send's 8-B field widths from this Send's per-tile bit lengths (the last
+// block, after every tile's maxima are out): each field as wide as its largest
+// value, the slack of the 52 bits split between the arguments.  Fields that no
+// longer fit set bit 31 (the host then keeps 16-B records).
+__device__ __forceinline__ void rec8_next(const SortIn& in, uint32_t* r8w, uint32_t* host, uint32_t tiles) {
+  __shared__ uint32_t mx[3];
+  if (threadIdx.x < 3) mx[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t bm = 0, b0 = 0, b1 = 0;
+  for (uint32_t t = threadIdx.x; t < tiles; t += blockDim.x) {
+    const uint32_t x = __hip_atomic_fetch_add(in.r8max + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bm = max(bm, x & 0xffu), b0 = max(b0, (x >> 8) & 0xffu), b1 = max(b1, (x >> 16) & 0xffu);
+  }
+  bm = wave_max_u32(bm), b0 = wave_max_u32(b0), b1 = wave_max_u32(b1);
+  if (lane_id() == 0) {
+    atomicMax(&mx[0], bm);
+    atomicMax(&mx[1], b0);
+    atomicMax(&mx[2], b1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t wm = max(mx[0], 1u), n0 = max(mx[1], 1u), n1 = max(mx[2], 1u);
+    uint32_t w = 0;
+    if (wm <= 24 && wm + n0 + n1 <= 52) {
+      const uint32_t w0 = n0 + (52 - wm - n0 - n1) / 2;
+      w = wm | (w0 << 8) | ((52 - wm - w0) << 16);
+    } else {
+      const uint32_t wmc = min(wm, 24u), w0 = (52 - wmc) / 2;
+      w = wmc | (w0 << 8) | ((52 - wmc - w0) << 16) | 0x80000000u;
+    }
+    *r8w = w;
+    if (host) __hip_atomic_store(host, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // LATE: the arguments are loaded after the look-back (a smaller register file
 // across it, more resident blocks; measured slower), else with the actors (in
 // flight across the gathers, the ranking and the look-back).
@@ -468,14 +512,17 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   resolve_k<MODE>(in, a, r, mb);
   uint32_t wr[kSK];
   uint32_t escm = 0;  // (in.rec8) messages whose fields do not fit an 8-B record: they spill
+  const uint32_t w8 = in.rec8 ? *in.r8w : 0u;  // this Send's 8-B field widths
+  uint64_t or_m = 0, or_0 = 0, or_1 = 0;       // (in.rec8) the tile's fields, OR-ed: their bit lengths
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     const bool ok = tile_index(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
     if (!ok) mb[k] = kNoSlot;
     if (in.rec8 && ok && !LATE) {
-      const uint32_t wm = in.rec8 & 0xffu, w0 = (in.rec8 >> 8) & 0xffu, w1 = (in.rec8 >> 16) & 0xffu;
+      const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
       const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
       const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
+      or_m |= mb[k], or_0 |= z0, or_1 |= z1;
       if ((mb[k] >> wm) != 0 || (z0 >> w0) != 0 || (z1 >> w1) != 0) escm |= 1u << k;
     }
     const uint32_t sh = mb[k] & (S - 1);
@@ -562,6 +609,24 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   // runs, so the drains take the tile in message order through the slot indices
   // (the thread that wrote shard 0's count word: program order)
   if (tile_spill && tinfo && threadIdx.x == 0) tinfo[(size_t)t * 2 * S + S] |= kRunSpilled;
+  if (in.rec8) {  // the tile's field bit lengths, for the next Send's widths (rec8_next)
+    const uint32_t bm = wave_max_u32(bitlen64(or_m)), b0 = wave_max_u32(bitlen64(or_0)),
+                   b1 = wave_max_u32(bitlen64(or_1));
+    __shared__ uint32_t tmax[3];
+    if (threadIdx.x < 3) tmax[threadIdx.x] = 0;
+    __syncthreads();
+    if (lane == 0) {
+      atomicMax(&tmax[0], bm);
+      atomicMax(&tmax[1], b0);
+      atomicMax(&tmax[2], b1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // a memory-side write, complete before this thread's later ticket (the fused
+                             // kernel's last block reads it within the launch)
+      (void)atomicExch(&in.r8max[t], tmax[0] | (tmax[1] << 8) | (tmax[2] << 16));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
   else __syncthreads();
   const bool wsidx = all_sidx || tile_spill;
   if constexpr (LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
@@ -595,7 +660,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     if (wsidx) sidx[i] = (uint32_t)slot;
     const uint32_t mt = meth[k];
     if (in.rec8) {  // 8-B record (stateless, uniform method, two arguments; wider ones spilled above)
-      const uint32_t wm = in.rec8 & 0xffu, w0 = (in.rec8 >> 8) & 0xffu;
+      const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu;
       const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
       const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
       reinterpret_cast<uint64_t*>(mv.rec)[slot] =
@@ -663,9 +728,8 @@ __device__ __forceinline__ SortRec decode_sorted(const u32x4& ha, const u32x4& h
 
 // An 8-B record (in.rec8) of the tile whose first message is `tile_origin`.
 template <bool FRESH>
-__device__ __forceinline__ SortRec decode_rec8(uint64_t r, const SortIn& in, const MboxView&, uint64_t,
-                                               uint32_t tile_origin) {
-  const uint32_t wm = in.rec8 & 0xffu, w0 = (in.rec8 >> 8) & 0xffu, w1 = (in.rec8 >> 16) & 0xffu;
+__device__ __forceinline__ SortRec decode_rec8(uint64_t r, const SortIn& in, uint32_t w8, uint32_t tile_origin) {
+  const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
   const uint64_t m0 = (1ull << w0) - 1;
   SortRec x;
   x.valid = true;
@@ -740,6 +804,7 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
     sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
   }
   using RecT = typename std::conditional<R8, uint64_t, u32x4>::type;  // the ring record as loaded
+  const uint32_t w8 = R8 ? *in.r8w : 0u;  // the 8-B field widths this Send's sort used
   RecT ha[kSK];
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
@@ -765,7 +830,7 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
       x.a1 = in.a1 ? in.a1[i] : 0;
       x.a2 = in.a2 ? in.a2[i] : 0;
     } else if constexpr (R8) {
-      x = decode_rec8<FRESH>(ha[k], in, mv, sl[k], in.origin_base + t * kSTile);
+      x = decode_rec8<FRESH>(ha[k], in, w8, in.origin_base + t * kSTile);
     } else {
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
@@ -916,6 +981,7 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   }
   const uint64_t sbase_mask = (1ull << mv.log_q) - 1;
   using RecT = typename std::conditional<R8, uint64_t, u32x4>::type;  // the ring record as loaded
+  const uint32_t w8 = R8 ? *in.r8w : 0u;  // the 8-B field widths this Send's sort used
   RecT ha[kSK];
   uint32_t sl[kSK];
 #pragma unroll
@@ -944,7 +1010,7 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
     if (sl[k] == kNoSlot) continue;
     SortRec x;
     if constexpr (R8) {
-      x = decode_rec8<FRESH>(ha[k], in, mv, sl[k], in.origin_base + (uint32_t)i0);
+      x = decode_rec8<FRESH>(ha[k], in, w8, in.origin_base + (uint32_t)i0);
     } else {
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
@@ -987,7 +1053,8 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
                                                              int64_t* __restrict__ state, uint32_t n_state,
                                                              uint64_t delay_ticks, OutboxView ob, ReplyView rv,
                                                              uint32_t* __restrict__ gsum, uint32_t ngroups,
-                                                             unsigned* __restrict__ ticket, unsigned* __restrict__ tctr) {
+                                                             unsigned* __restrict__ ticket, unsigned* __restrict__ tctr,
+                                                             uint32_t* __restrict__ r8host) {
   extern __shared__ __align__(16) unsigned char smem_rd[];
   const uint32_t S = 1u << mv.log_s;
   DrainCounts dc;
@@ -1003,6 +1070,7 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
   if (last) {  // every block's records are read: the rings are consumed
     for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
+    if constexpr (R8) rec8_next(in, const_cast<uint32_t*>(in.r8w), r8host, in.tiles);
   }
 }
 
@@ -1024,7 +1092,8 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
                                                             uint32_t* __restrict__ rw, ReplyView rv,
                                                             int64_t* __restrict__ state, uint32_t n_state,
                                                             uint64_t delay_ticks, OutboxView ob,
-                                                            unsigned* __restrict__ ticket, bool reserve) {
+                                                            unsigned* __restrict__ ticket, bool reserve,
+                                                            uint32_t* __restrict__ r8host) {
   extern __shared__ __align__(16) unsigned char smem_sd[];
   const uint32_t S = 1u << mv.log_s;
   const uint32_t t = onesweep_tile<MODE, A2, MC, false>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, true, false,
@@ -1049,6 +1118,7 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
     for (uint32_t s = threadIdx.x; s < S; s += kST)
       epoch_commit(mv, s, reserve ? atomicExch(&gsum[s], 0u) : epoch_total(gsum, 1, S, s, true));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
+    if constexpr (R8) rec8_next(in, const_cast<uint32_t*>(in.r8w), r8host, in.tiles);
   }
 }
 
@@ -1592,14 +1662,33 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   static const bool rec8_ok = !(getenv("PTYPE_MBOX_REC8") && std::string(getenv("PTYPE_MBOX_REC8")) == "0");
   const bool r8 = rec8_ok && sort_mode == 1 && !a.ordered && !a.arrival && !a.a2 && !a.method_col && mv.planar &&
                   !all_sidx && !late;
-  if (r8) {
-    // (the largest mailbox the routes can name: below the state size, or the directory's actor count)
-    const uint32_t nmb = std::max(a.n_state, a.n_dir);
-    uint32_t wm = 20;
-    if (nmb > 1) wm = 32u - (uint32_t)__builtin_clz(nmb - 1);
-    wm = std::max(1u, std::min(wm, 24u));
-    const uint32_t w0 = (52u - wm) / 2, w1 = 52u - wm - w0;
-    in.rec8 = wm | (w0 << 8) | (w1 << 16);
+  if (r8 && (!r8w_ || r8_tiles_ < (uint64_t)tiles)) {  // (outside a capture: grown with the sort workspace)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("mailbox send: first 8-B-record Send of this size inside a graph capture (warm up first)");
+    PT_HIP_CHECK(hipStreamSynchronize(st));
+    if (!r8w_) {
+      // the first Send's widths: the mailbox from the state size or the directory, the rest split
+      const uint32_t nmb = std::max(a.n_state, a.n_dir);
+      uint32_t wm = 20;
+      if (nmb > 1) wm = 32u - (uint32_t)__builtin_clz(nmb - 1);
+      wm = std::max(1u, std::min(wm, 24u));
+      const uint32_t w0 = (52u - wm) / 2, w = wm | (w0 << 8) | ((52u - wm - w0) << 16);
+      PT_HIP_CHECK(hipMalloc((void**)&r8w_, 16));
+      PT_HIP_CHECK(hipMemcpy(r8w_, &w, 4, hipMemcpyHostToDevice));
+      PT_HIP_CHECK(hipHostMalloc((void**)&r8host_, 64, hipHostMallocMapped));
+      *r8host_ = w;
+    }
+    if (r8max_) PT_HIP_CHECK(hipFree(r8max_));
+    PT_HIP_CHECK(hipMalloc((void**)&r8max_, (size_t)tiles * 4));
+    r8_tiles_ = (uint64_t)tiles;
+  }
+  // fields that outgrew 64 bits (the last Send's widths, bit 31): 16-B records from here on
+  const bool r8_on = r8 && !(__atomic_load_n(r8host_, __ATOMIC_RELAXED) & 0x80000000u);
+  if (r8_on) {
+    in.rec8 = 1;
+    in.r8w = r8w_;
+    in.r8max = r8max_;
   }
   uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
   // the LDS-table count (PTYPE_MBOX_SORT=ldscount): directory registry, table <= kStabMax, shards <= 128
@@ -1656,10 +1745,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, R8>), dim3(in.tiles), dim3(kST), lds, st, in, mv,          \
                      sort_desc_,                                                                                     \
                      sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv, (int64_t*)a.state, a.n_state,    \
-                     a.delay_ticks, ob, sort_ticket_, reserve)
+                     a.delay_ticks, ob, sort_ticket_, reserve, r8host_)
 #define PT_SD2(MO, A2, MC, FX)                               \
   do {                                                       \
-    if (!(A2) && !(MC) && r8) PT_SD3(MO, false, false, FX, true); \
+    if (!(A2) && !(MC) && r8_on) PT_SD3(MO, false, false, FX, true); \
     else PT_SD3(MO, A2, MC, FX, false);                      \
   } while (0)
 #define PT_SD(MO)                                                            \
@@ -1736,10 +1825,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
                      NW ? ring_lds : (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, mv, in,                 \
                      (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_,       \
                      (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_, \
-                     sort_tctr_)
+                     sort_tctr_, r8host_)
 #define PT_DRING1(FX, NW)                     \
   do {                                        \
-    if (r8) PT_DRING2(FX, NW, true);          \
+    if (r8_on) PT_DRING2(FX, NW, true);       \
     else PT_DRING2(FX, NW, false);            \
   } while (0)
 #define PT_DRING(FX)                                   \

@@ -52,9 +52,12 @@ struct SortIn {  // by value
   uint32_t tpb;    // tiles per block
   bool dir_nt;       // non-temporal directory gathers (experiment)
   bool lb_group;     // one-pass sorts: group look-back (W lanes per shard) where the shard count allows
-  // 8-B ring records (stateless mailbox Sends, mailbox_sort.hip): mailbox bits | a0 bits << 8 |
-  // a1 bits << 16 (zigzag); 0: 16-B records
+  // 8-B ring records (stateless mailbox Sends, mailbox_sort.hip): nonzero = on; the field widths
+  // (mailbox bits | a0 bits << 8 | a1 bits << 16, zigzag arguments) are the device word *r8w,
+  // set by the previous Send's last block from its per-tile field maxima (r8max)
   uint32_t rec8;
+  const uint32_t* r8w;
+  uint32_t* r8max;
 };
 
 // Block b's range: XCD (b % 8) owns virtual blocks [x * G/8, (x+1) * G/8).

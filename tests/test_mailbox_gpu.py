@@ -56,7 +56,8 @@ def test_mailbox_send_calculator_matches_reference(directory):
     assert bool((st == STATUS_OK).all())
     assert torch.equal(val, req.a0 * req.a1)
     s = mb.stats()
-    assert s["enqueued"] == M and s["processed"] == M and s["overflow"] == 0 and s["holes"] == 0
+    # (a message whose fields outgrow the first Send's 8-B record widths spills: run from the batch)
+    assert s["enqueued"] + s["spilled"] == M and s["processed"] == M and s["overflow"] == 0 and s["holes"] == 0
     ctr = mb.shard_counters()
     assert (ctr[:, 0] == ctr[:, 2]).all() and int(ctr[:, 0].sum()) == M  # every ring drained
 
