@@ -166,7 +166,7 @@ def wire_info(ex, req) -> dict:
         # exact: the regions' used prefixes move (counts all-to-all + grouped send/recv);
         # padded: every peer region at the agreed capacity
         return {"wire": "v3-packed", "record_bytes": 4 * w["S"], "reply_bytes": w["vb"] + 0.125,
-                "field_bits": w["w"], "exchange": "exact" if w.get("exact") else "padded",
+                "field_bits": w["w"], "exchange": "exact" if w.get("exact") else ("per-pair prefixes" if w.get("pairs") else "padded"),
                 "engine": w.get("engine", "epoch"),
                 "wire_bytes_per_msg": 4 * (w["req_words"] + w["rep_words"]) * ex.chunks / max(req.M, 1)}
     return {"wire": "v2", "record_bytes": 4 * (ex.fmt or B.WireFormat.for_batch(req)).stride, "reply_bytes": 9}
