@@ -38,6 +38,7 @@
 //   i.e. 9 B per reply instead of a 16-B record.  The reverse all-to-all brings
 //   every reply back to the slot its request left from; `perm[i]` remembers it
 //   as d * C + pos (-1 overflow, -2 no actor).
+#include <algorithm>
 #include <vector>
 
 #include "common.hpp"
@@ -69,6 +70,40 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
   if (seed_ptr) seed = *seed_ptr;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = mix64(seed ^ (uint64_t)i * 0x9e3779b97f4a7c15ull);
+    actor[i] = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
+    a0[i] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
+    a1[i] = (int64_t)((h >> 40) & 0xffff);
+  }
+}
+
+// The same batch, four consecutive messages per thread: one 16-B store of actor
+// ids and two of each argument column per thread (the same values per index).
+__global__ __launch_bounds__(256) void gen_requests_vec4_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
+                                                                int64_t* __restrict__ a1, int64_t M,
+                                                                uint32_t n_actors, uint64_t seed,
+                                                                const uint64_t* __restrict__ seed_ptr, uint64_t magic) {
+  if (seed_ptr) seed = *seed_ptr;
+  const int64_t M4 = M / 4;
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < M4; q += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t ac[4];
+    int64_t x0[4], x1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = (uint64_t)q * 4 + j;
+      const uint64_t h = mix64(seed ^ i * 0x9e3779b97f4a7c15ull);
+      ac[j] = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
+      x0[j] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
+      x1[j] = (int64_t)((h >> 40) & 0xffff);
+    }
+    reinterpret_cast<uint4*>(actor)[q] = make_uint4(ac[0], ac[1], ac[2], ac[3]);
+    reinterpret_cast<longlong2*>(a0)[2 * q] = make_longlong2(x0[0], x0[1]);
+    reinterpret_cast<longlong2*>(a0)[2 * q + 1] = make_longlong2(x0[2], x0[3]);
+    reinterpret_cast<longlong2*>(a1)[2 * q] = make_longlong2(x1[0], x1[1]);
+    reinterpret_cast<longlong2*>(a1)[2 * q + 1] = make_longlong2(x1[2], x1[3]);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(M - M4 * 4)) {  // the tail
+    const uint64_t i = (uint64_t)M4 * 4 + threadIdx.x;
+    const uint64_t h = mix64(seed ^ i * 0x9e3779b97f4a7c15ull);
     actor[i] = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
     a0[i] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
     a1[i] = (int64_t)((h >> 40) & 0xffff);
@@ -709,9 +744,18 @@ void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M,
     const char* e = getenv("PTYPE_GEN_BLOCKS");
     return e ? (unsigned)atoi(e) : 8192u;
   }();
+  static const bool vec4 = !(getenv("PTYPE_GEN_VEC") && atoi(getenv("PTYPE_GEN_VEC")) == 0);
   const uint64_t magic = variant == 1 ? 0ull : ~0ull / n_actors;
-  hipLaunchKernelGGL(gen_requests_kernel, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
-                     (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr, magic);
+  // (vec4: 16-B stores need 16-B aligned columns -- torch's allocations are; slices may not be)
+  const bool aligned = ((actor | a0 | a1) & 15u) == 0;
+  if (vec4 && aligned)
+    hipLaunchKernelGGL(gen_requests_vec4_kernel, dim3(grid_cap(std::max<int64_t>(M / 4, 1), 256, cap_blocks)),
+                       dim3(256), 0, as_stream(stream), (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors,
+                       seed, (const uint64_t*)seed_ptr, magic);
+  else
+    hipLaunchKernelGGL(gen_requests_kernel, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
+                       (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr,
+                       magic);
   PT_HIP_CHECK(hipGetLastError());
 }
 
