@@ -274,6 +274,8 @@ def main():
             bad = int((t != STATUS_OK).sum())
             raise SystemExit(f"[rank {rank}] {tag}: verification failed ({bad} non-OK replies)")
 
+    host_us_per_step = [None]
+
     def measure(table, steps, warmup, delivery=args.delivery, sharding=args.sharding, Mq=M,
                 method=METHOD_CALC_MULTIPLY):
         """Warm up, then time `steps` Sends of `Mq` messages (barrier + synchronize
@@ -343,11 +345,15 @@ def main():
         barrier()
         sync()
         t0 = time.perf_counter()
+        host = 0.0
         for s_ in range(steps):
+            h0 = time.perf_counter()
             step(warmup + s_)
+            host += time.perf_counter() - h0
         sync()
         barrier()
         elapsed = time.perf_counter() - t0
+        host_us_per_step[0] = host / max(steps, 1) * 1e6  # the host's time inside the step calls (no waits)
         if dist_on:
             tt = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -369,6 +375,7 @@ def main():
     if hang_s and float(hang_s) > 0:
         _hang_watchdog(float(hang_s), rank)
     elapsed, ex, graphed = measure(table, args.steps, args.warmup)
+    head_host_us = host_us_per_step[0]
     def lookup_mode(t):
         if t.dir is None:
             return "hash-table probe"
@@ -485,7 +492,7 @@ def main():
 
         tag = os.environ.get("MASTER_PORT", "0")
         shm = f"/ptype-bench-{tag}-{rank}" if dist_on else ""
-        srv = hip().DeviceServer(local, 4096, state.data_ptr(), state.numel(), 0, 200.0, 60.0, shm)
+        srv = hip().DeviceServer(device.index, 4096, state.data_ptr(), state.numel(), 0, 200.0, 60.0, shm)
 
         def timed_calls(call):
             lat = []
@@ -584,6 +591,8 @@ def main():
                 "client_batch": "SoA (actor u32, A i64, B i64)",
                 "hip_graph": graphed,
                 "steps_per_graph": args.steps_per_graph if graphed else None,
+                # host time inside the timed step calls (this rank; a graph replay launches U steps)
+                "host_us_per_step": round(head_host_us, 2) if head_host_us is not None else None,
                 **({"load": f"zipf({args.zipf})" if args.zipf > 0 else "uniform", "pregenerated": True,
                     "resend_rounds": ex.counters.resends, "resend_rounds_warmup": ex.warmup_resends}
                    if pregen else {}),
