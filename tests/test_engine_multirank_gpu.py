@@ -60,7 +60,8 @@ def test_gpu_engine_multirank(R, packed, chunks, mixed, big):
                 tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
                 tab.enable_directory(n, affine_world=R)
                 st = torch.zeros(n // R + 1, dtype=torch.int64, device="cuda")
-                ex = ActorExchange(tab, Mmax, chunks=chunks, state=st, packed=packed, fake=(fc, r))
+                # (delivery "direct": the epoch engine; "auto" at N > 1 is the sorted exchange now)
+                ex = ActorExchange(tab, Mmax, chunks=chunks, state=st, packed=packed, fake=(fc, r), delivery="direct")
                 actor, a0, a1, m = batches[r]
                 req = B.MsgBatch(actor.cuda(), a0.cuda(), a1.cuda(), None,
                                  m.to(torch.int16).cuda() if mixed else METHOD_CALC_MULTIPLY)
@@ -121,7 +122,7 @@ def test_gpu_engine_loopback(R, chunks, sync, link, monkeypatch):
     tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
     tab.enable_directory(n, affine_world=R)
     ex = ActorExchange(tab, M, chunks=chunks, state=torch.zeros(n // R, dtype=torch.int64, device="cuda"),
-                       fake=(hip().FakeComm(R, loopback=True, link_gbps=link), 0))
+                       fake=(hip().FakeComm(R, loopback=True, link_gbps=link), 0), delivery="direct")
     for seed in (3, 4):
         req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=seed, device="cuda")
         val, st = ex.send(req)
@@ -156,7 +157,7 @@ def test_gpu_engine_zipf_skew_no_resend(adaptive, monkeypatch):
                 tab.upsert(actor_keys(ids), (ids % R).to(torch.int32), (ids // R).to(torch.int32))
                 tab.enable_directory(n, affine_world=R)
                 st = torch.zeros(n // R, dtype=torch.int64, device="cuda")
-                ex = ActorExchange(tab, M, chunks=2, state=st, fake=(fc, r))
+                ex = ActorExchange(tab, M, chunks=2, state=st, fake=(fc, r), delivery="direct")
                 req = B.gen_zipf_requests(M, n, 1.1, seed=10 + r, device="cuda")
                 start.wait()
                 v, sts = ex.send(req)  # one pass, no host re-send loop
