@@ -279,17 +279,19 @@ def test_gpu_replicated_prime_over_fakecomm_r4():
                 M = sizes[r]
                 a = (torch.arange(M, device="cuda") % P).to(torch.int32)
                 start.wait()
-                _, s1 = ex.send(B.MsgBatch(router.route(a), torch.ones(M, dtype=torch.int64, device="cuda"), None,
-                                           None, METHOD_COUNTER_ADD))
+                # (send_all, as Client.Send: the sorted exchange's first Sends run at the start-up
+                # capacity, and all of this traffic lands on the two replicas -- overflow, re-sent)
+                _, s1 = ex.send_all(B.MsgBatch(router.route(a), torch.ones(M, dtype=torch.int64, device="cuda"), None,
+                                               None, METHOD_COUNTER_ADD))
                 t = torch.tensor([97, 91, 62, 273, 7919], dtype=torch.int64, device="cuda")
-                pv, ps = ex.send(B.MsgBatch(router.route(torch.arange(5, dtype=torch.int32, device="cuda")),
-                                            torch.full_like(t, 2), t, t, METHOD_PRIME_CHECK))
+                pv, ps = ex.send_all(B.MsgBatch(router.route(torch.arange(5, dtype=torch.int32, device="cuda")),
+                                                torch.full_like(t, 2), t, t, METHOD_PRIME_CHECK))
                 s.synchronize()
                 start.wait()
                 c1 = st.clone()
                 router.set_records(recs[1:])  # replica 1 lost
-                _, s2 = ex.send(B.MsgBatch(router.route(a), torch.ones(M, dtype=torch.int64, device="cuda"), None,
-                                           None, METHOD_COUNTER_ADD))
+                _, s2 = ex.send_all(B.MsgBatch(router.route(a), torch.ones(M, dtype=torch.int64, device="cuda"), None,
+                                               None, METHOD_COUNTER_ADD))
                 s.synchronize()
                 results[r] = (s1.cpu(), ps.cpu(), pv.cpu(), s2.cpu())
                 states[r] = (c1.cpu(), (st - c1).cpu())
