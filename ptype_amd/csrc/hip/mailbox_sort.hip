@@ -511,20 +511,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   if constexpr (!LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
   resolve_k<MODE>(in, a, r, mb);
   uint32_t wr[kSK];
-  uint32_t escm = 0;  // (in.rec8) messages whose fields do not fit an 8-B record: they spill
-  const uint32_t w8 = in.rec8 ? *in.r8w : 0u;  // this Send's 8-B field widths
-  uint64_t or_m = 0, or_0 = 0, or_1 = 0;       // (in.rec8) the tile's fields, OR-ed: their bit lengths
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     const bool ok = tile_index(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
     if (!ok) mb[k] = kNoSlot;
-    if (in.rec8 && ok && !LATE) {
-      const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
-      const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
-      const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
-      or_m |= mb[k], or_0 |= z0, or_1 |= z1;
-      if ((mb[k] >> wm) != 0 || (z0 >> w0) != 0 || (z1 >> w1) != 0) escm |= 1u << k;
-    }
     const uint32_t sh = mb[k] & (S - 1);
     const uint64_t peers = match_bits(sh, mv.log_s, __ballot(ok));
     const unsigned below = mbcnt64(peers);
@@ -602,6 +592,23 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
       tinfo[(size_t)t * 2 * S + S + s] = cc | (excl + c > rm ? kRunSpilled : 0u);
     }
   }
+  if constexpr (LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
+  // (in.rec8) the messages whose fields do not fit an 8-B record -- they spill -- and
+  // the tile's fields OR-ed (their bit lengths size the next Send's records)
+  uint32_t escm = 0;
+  const uint32_t w8 = in.rec8 ? *in.r8w : 0u;  // this Send's 8-B field widths
+  uint64_t or_m = 0, or_0 = 0, or_1 = 0;
+  if (in.rec8) {
+    const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      if (mb[k] == kNoSlot) continue;
+      const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
+      const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
+      or_m |= mb[k], or_0 |= z0, or_1 |= z1;
+      if ((mb[k] >> wm) != 0 || (z0 >> w0) != 0 || (z1 >> w1) != 0) escm |= 1u << k;
+    }
+  }
   sp |= escm != 0;
   bool tile_spill = false;
   if (spill) tile_spill = __syncthreads_or(sp) != 0;
@@ -629,7 +636,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   }
   else __syncthreads();
   const bool wsidx = all_sidx || tile_spill;
-  if constexpr (LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
   unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0, n_spill = 0;
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
@@ -1663,7 +1669,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
   static const bool rec8_ok = !(getenv("PTYPE_MBOX_REC8") && std::string(getenv("PTYPE_MBOX_REC8")) == "0");
   const bool r8 = rec8_ok && sort_mode == 1 && !a.ordered && !a.arrival && !a.a2 && !a.method_col && mv.planar &&
-                  !all_sidx && !late;
+                  !all_sidx;
   if (r8 && (!r8w_ || r8_tiles_ < (uint64_t)tiles)) {  // (outside a capture: grown with the sort workspace)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
