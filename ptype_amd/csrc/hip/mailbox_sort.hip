@@ -489,7 +489,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   uint32_t* wcnt_all = pre + S;                                               // [kST / kWave][S]
   auto wcnt = [&](unsigned ww, uint32_t sh) -> uint32_t& { return wcnt_all[ww * S + sh]; };
   __shared__ uint32_t tile_s;
+  __shared__ uint32_t tmax[3];  // (in.rec8) the tile's field bit lengths
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  if (threadIdx.x < 3) tmax[threadIdx.x] = 0;  // (ordered before use by the tile's first barrier)
   // this Send's epoch tag, 1..0xffffff (the drain advances tctr[1]; the modulus keeps the tag inside the
   // descriptor's 24-bit field across the counter's wrap -- tag 0 is reserved for never-published words)
   const uint32_t tag = epoch_tag(tctr[1]);
@@ -610,31 +612,22 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     }
   }
   sp |= escm != 0;
-  bool tile_spill = false;
-  if (spill) tile_spill = __syncthreads_or(sp) != 0;
-  // a tile spilled by its records' widths (no run overran its ring): flag one of its
-  // runs, so the drains take the tile in message order through the slot indices
-  // (the thread that wrote shard 0's count word: program order)
-  if (tile_spill && tinfo && threadIdx.x == 0) tinfo[(size_t)t * 2 * S + S] |= kRunSpilled;
-  if (in.rec8) {  // the tile's field bit lengths, for the next Send's widths (rec8_next)
+  if (in.rec8) {  // the tile's field bit lengths (read by thread 0 past the spill barrier)
     const uint32_t bm = wave_max_u32(bitlen64(or_m)), b0 = wave_max_u32(bitlen64(or_0)),
                    b1 = wave_max_u32(bitlen64(or_1));
-    __shared__ uint32_t tmax[3];
-    if (threadIdx.x < 3) tmax[threadIdx.x] = 0;
-    __syncthreads();
     if (lane == 0) {
       atomicMax(&tmax[0], bm);
       atomicMax(&tmax[1], b0);
       atomicMax(&tmax[2], b1);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // a memory-side write, complete before this thread's later ticket (the fused
-                             // kernel's last block reads it within the launch)
-      (void)atomicExch(&in.r8max[t], tmax[0] | (tmax[1] << 8) | (tmax[2] << 16));
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
+  bool tile_spill = false;
+  if (spill) tile_spill = __syncthreads_or(sp) != 0;
   else __syncthreads();
+  // a tile spilled by its records' widths (no run overran its ring): flag one of its
+  // runs, so the drains take the tile in message order through the slot indices
+  // (the thread that wrote shard 0's count word: program order)
+  if (tile_spill && tinfo && threadIdx.x == 0) tinfo[(size_t)t * 2 * S + S] |= kRunSpilled;
   const bool wsidx = all_sidx || tile_spill;
   unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0, n_spill = 0;
 #pragma unroll
@@ -684,6 +677,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     }
     ++n_enq;
   }
+  // the tile's field bit lengths, for the next Send's widths (rec8_next): a memory-side write
+  // (the fused kernel's last block reads it within the launch: its ticket follows a vmcnt(0) wait)
+  if (in.rec8 && threadIdx.x == 0) (void)atomicExch(&in.r8max[t], tmax[0] | (tmax[1] << 8) | (tmax[2] << 16));
   block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
   __syncthreads();  // block_add_stats' LDS partials are reused
   block_add_stats(mv.stats, n_spill, kMbSpilled, timeouts, kMbLookback, 0, -1);
