@@ -341,6 +341,13 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
 // status 2 | value 38} through memory-side atomics), then packs and stores its
 // records.  The last tile writes the region headers and shard tables, the
 // last block to finish advances the epoch tag (every block has read it by then).
+//
+// reserve (the default for rank-only batches): no look-back.  A rank-only
+// region is a queue of stateless records that the receiver runs in parallel,
+// so a region need not hold this sender's messages in message order: each
+// tile reserves its run in every destination's region with ONE atomicAdd on
+// that region's counter (rcnt), and the last block to finish writes the
+// headers from the totals (and clears the counters for the next chunk).
 
 template <int MODE, int S>
 __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsigned long long* __restrict__ desc,
@@ -349,7 +356,8 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
                                                           uint32_t C, SxCaps caps, uint32_t hdr_word3,
                                                           int rank_self, PackedLayout L, int32_t* __restrict__ perm,
                                                           unsigned long long* __restrict__ meta,
-                                                          unsigned long long* __restrict__ stats) {
+                                                          unsigned long long* __restrict__ stats,
+                                                          uint32_t* __restrict__ rcnt, bool reserve) {
   __shared__ uint32_t wcnt[kST / kWave][kSxMaxRanks];
   __shared__ uint32_t pre[kSxMaxRanks];
   __shared__ uint32_t cap_s[kSxMaxRanks];  // per-destination capacities (C: the region stride in records)
@@ -359,9 +367,13 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
   if (threadIdx.x == 0) {
     tag_s = epoch_tag(tctr[1]);  // 1..0xffffff across the counter's wrap
-    const uint32_t t = atomicAdd(&tctr[0], 1u);
-    if (t == in.tiles - 1) atomicExch(&tctr[0], 0u);  // every block has claimed
-    tile_s = t;
+    if (!reserve) {
+      const uint32_t t = atomicAdd(&tctr[0], 1u);
+      if (t == in.tiles - 1) atomicExch(&tctr[0], 0u);  // every block has claimed
+      tile_s = t;
+    } else {
+      tile_s = virt_block(blockIdx.x, gridDim.x);  // (tiles dealt XCD by XCD)
+    }
     mbmax_s = 0;
   }
   if (lane < kSxMaxRanks) wcnt[w][lane] = 0;
@@ -407,7 +419,9 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
     unsigned long long* dp = desc + (size_t)t * R + d;
     uint64_t excl = 0;
     unsigned long long timeouts = 0;
-    if (t == 0) {
+    if (reserve) {
+      excl = c ? atomicAdd(&rcnt[d], c) : 0u;  // this tile's run of region d (headers: the last block)
+    } else if (t == 0) {
       __hip_atomic_exchange(dp, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       __hip_atomic_exchange(dp, desc_word(tag, kDescA, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -417,7 +431,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
       if (timeouts) atomicAdd(&stats[2], timeouts);
     }
     pre[d] = (uint32_t)excl;
-    if (t == in.tiles - 1) {  // region d's header and (single-run) shard table
+    if (!reserve && t == in.tiles - 1) {  // region d's header and (single-run) shard table
       const uint32_t all = (uint32_t)(excl + c), n = all < cap_s[d] ? all : cap_s[d];
       uint32_t* region = sendbuf + (int64_t)d * req_stride;
       region[tab_off] = 0;
@@ -481,6 +495,18 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
   __syncthreads();
   if (last && threadIdx.x == 0) tctr[1] += 1u;  // every block has read this launch's tag: the next one's
+  if (last && reserve && threadIdx.x < (unsigned)R) {  // every tile has reserved: the regions' headers
+    const uint32_t d = threadIdx.x;
+    const uint32_t all = atomicExch(&rcnt[d], 0u), n = all < cap_s[d] ? all : cap_s[d];  // (memory-side)
+    uint32_t* region = sendbuf + (int64_t)d * req_stride;
+    region[tab_off] = 0;
+    for (int s2 = 1; s2 <= kSxShards; ++s2) region[tab_off + s2] = n;
+    *reinterpret_cast<uint4*>(region) = make_uint4(n, all, (uint32_t)rank_self, hdr_word3);
+    if (all) {
+      meta_max(meta + kMetaCap, all);
+      meta_max(meta + kSxMetaPair + rank_self * R + d, all);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- receiver: parallel drain
@@ -778,6 +804,8 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   PT_HIP_CHECK(hipMemset(tctr_, 0, 2 * sizeof(unsigned)));
   PT_HIP_CHECK(hipMalloc(&ticket_, kTicketWords * sizeof(unsigned)));
   PT_HIP_CHECK(hipMemset(ticket_, 0, kTicketWords * sizeof(unsigned)));
+  PT_HIP_CHECK(hipMalloc(&rcnt_, kSxMaxChunks * kSxMaxRanks * sizeof(uint32_t)));
+  PT_HIP_CHECK(hipMemset(rcnt_, 0, kSxMaxChunks * kSxMaxRanks * sizeof(uint32_t)));
   PT_HIP_CHECK(hipMalloc(&meta_dev_, 2 * kSxMetaWords * sizeof(uint64_t)));
   PT_HIP_CHECK(hipMemset(meta_dev_, 0, 2 * kSxMetaWords * sizeof(uint64_t)));
   PT_HIP_CHECK(hipMalloc(&stats_, 3 * sizeof(unsigned long long)));
@@ -810,6 +838,7 @@ SortedExchange::~SortedExchange() {  // no synchronisation: a collective stuck o
   (void)hipFree(desc_);
   (void)hipFree(tctr_);
   (void)hipFree(ticket_);
+  (void)hipFree(rcnt_);
   (void)hipFree(meta_dev_);
   (void)hipFree(stats_);
   (void)hipHostFree(meta_host_);
@@ -1098,12 +1127,17 @@ void SortedExchange::send(const SxSend& a) {
     // rank-only batches: count + scan + scatter, or one pass with look-back (PTYPE_SX_SORT=onepass; measured
     // slower at R = 8, 4 Mi msgs per chunk: 90 us vs 34 + 6.5 + 44 -- the look-back's memory-side atomic
     // round trips cost more than the count pass's second read of the batch)
-    static const bool one_pass = getenv("PTYPE_SX_SORT") && std::string(getenv("PTYPE_SX_SORT")) == "onepass";
-    if (!sharded && in.tiles > 0 && one_pass) {
+    // rank-only batches: one pass with per-tile run reservation (the default; no look-back),
+    // PTYPE_SX_SORT=onepass: the look-back form, =twopass: count + scan + scatter
+    static const char* sx_sort = getenv("PTYPE_SX_SORT");
+    static const int sx_mode = !sx_sort ? 0 : std::string(sx_sort) == "onepass" ? 1 : std::string(sx_sort) == "twopass" ? 2 : 0;
+    const bool reserve = sx_mode == 0;
+    if (!sharded && in.tiles > 0 && sx_mode != 2) {
       const uint32_t hdr3 = ((uint32_t)kFlagValid << 16) | (uint32_t)a.method_uniform;
 #define PT_SX_OS(MO, SV)                                                                                         \
   hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_, ticket_, \
-                     b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm, (unsigned long long*)meta, stats_)
+                     b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm, (unsigned long long*)meta, stats_, \
+                     rcnt_ + i * kSxMaxRanks, reserve)
 #define PT_SX_OS_S(MO)              \
   switch (S) {                      \
     case 1: PT_SX_OS(MO, 1); break; \

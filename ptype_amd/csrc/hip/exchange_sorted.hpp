@@ -145,6 +145,7 @@ class SortedExchange {
   unsigned long long* desc_ = nullptr;  // [tiles][R] one-pass look-back descriptors (rank-only batches)
   unsigned* tctr_ = nullptr;    // [0] one-pass tile counter (self-resetting), [1] its epoch tag
   unsigned* ticket_ = nullptr;  // last-block ticket of the one-pass kernel (self-resetting)
+  uint32_t* rcnt_ = nullptr;    // [chunks][kSxMaxRanks] one-pass run reservations per region (self-resetting)
   uint64_t* meta_dev_ = nullptr;   // [2][kSxMetaWords] agreement vectors (device)
   uint64_t* meta_host_ = nullptr;  // [2][kSxMetaWords] pinned copies
   unsigned long long* stats_ = nullptr;  // [2] receiver counters
