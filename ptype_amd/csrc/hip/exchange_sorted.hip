@@ -930,8 +930,8 @@ void SortedExchange::pick_spec(hipStream_t cs) {
 void SortedExchange::a2a(const void* src, void* dst, size_t stride, const size_t* send, const size_t* recv,
                          bool grouped_p2p) {
   if (fake_) {
-    if (send) fake_->alltoallv(rank_, src, dst, stride, send, recv, comm_stream_);
-    else fake_->alltoall(rank_, src, dst, stride, comm_stream_);
+    if (send) fake_->alltoallv(rank_, src, dst, stride, send, recv, cur_comm_);
+    else fake_->alltoall(rank_, src, dst, stride, cur_comm_);
     return;
   }
   // PTYPE_SX_SELF_COPY: at world 1 the all-to-all is a device copy.  RCCL
@@ -941,7 +941,7 @@ void SortedExchange::a2a(const void* src, void* dst, size_t stride, const size_t
   // capture test validates the captured pipeline with the copy in their place.
   static const bool self_copy = getenv("PTYPE_SX_SELF_COPY") != nullptr;
   if (self_copy && R_ == 1) {
-    PT_HIP_CHECK(hipMemcpyAsync(dst, src, recv ? recv[0] : stride, hipMemcpyDeviceToDevice, comm_stream_));
+    PT_HIP_CHECK(hipMemcpyAsync(dst, src, recv ? recv[0] : stride, hipMemcpyDeviceToDevice, cur_comm_));
     return;
   }
   auto check = [](int rc, const char* what) {
@@ -956,15 +956,15 @@ void SortedExchange::a2a(const void* src, void* dst, size_t stride, const size_t
     check(rccl().group_start(), "ncclGroupStart");
     for (int q = 0; q < R_; ++q) {
       check(rccl().send((const char*)src + (size_t)q * stride, send ? send[q] : stride, kNcclInt8, q, comm_,
-                        comm_stream_), "ncclSend");
-      check(rccl().recv((char*)dst + (size_t)q * stride, recv ? recv[q] : stride, kNcclInt8, q, comm_, comm_stream_),
+                        cur_comm_), "ncclSend");
+      check(rccl().recv((char*)dst + (size_t)q * stride, recv ? recv[q] : stride, kNcclInt8, q, comm_, cur_comm_),
             "ncclRecv");
     }
     check(rccl().group_end(), "ncclGroupEnd");
     return;
   }
   if (send) throw std::runtime_error("SortedExchange: per-pair sizes need RCCL's grouped send / recv");
-  check(rccl().alltoall(src, dst, stride, kNcclInt8, comm_, comm_stream_), "ncclAllToAll");
+  check(rccl().alltoall(src, dst, stride, kNcclInt8, comm_, cur_comm_), "ncclAllToAll");
 }
 
 void SortedExchange::allreduce_meta(uint64_t* dev, hipStream_t s) {
@@ -984,6 +984,10 @@ void SortedExchange::send(const SxSend& a) {
   PT_HIP_CHECK(hipSetDevice(device_));
   if (fake_) fake_->check();  // an earlier collective's failure surfaces here (IpcComm: a peer missed one)
   const hipStream_t cs = as_stream(a.stream);
+  // PTYPE_SX_COMM_CS=1: the collectives on the caller's stream itself (a graph-capture probe:
+  // tools/rccl_capture_probe.py sx1cs) instead of the engine's comm stream
+  static const bool comm_on_cs = getenv("PTYPE_SX_COMM_CS") && atoi(getenv("PTYPE_SX_COMM_CS")) == 1;
+  cur_comm_ = comm_on_cs ? cs : comm_stream_;
   pick_spec(cs);
   hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;
   const bool capturing = hipStreamIsCapturing(cs, &capst) == hipSuccess && capst != hipStreamCaptureStatusNone;
@@ -1110,9 +1114,9 @@ void SortedExchange::send(const SxSend& a) {
     }
     PT_HIP_CHECK(hipGetLastError());
     PT_HIP_CHECK(hipEventRecord(ev_served_[i], cs));
-    PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_served_[i], 0));
+    PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_served_[i], 0));
     a2a(b.reply, b.back, (size_t)rp * 4, pairs ? rp_send : nullptr, pairs ? rp_recv : nullptr, capturing);
-    PT_HIP_CHECK(hipEventRecord(ev_rep_in_[i], comm_stream_));
+    PT_HIP_CHECK(hipEventRecord(ev_rep_in_[i], cur_comm_));
   };
   for (int i = 0; i < chunks_; ++i) {
     Bufs& b = bufs_[i];
@@ -1158,9 +1162,9 @@ void SortedExchange::send(const SxSend& a) {
 #undef PT_SX_OS
       PT_HIP_CHECK(hipGetLastError());
       PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
-      PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_routed_[i], 0));
+      PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
       a2a(b.send, b.recv, (size_t)rq * 4, pairs ? rq_send : nullptr, pairs ? rq_recv : nullptr, capturing);
-      PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], comm_stream_));
+      PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], cur_comm_));
       if (i > 0) serve(i - 1);
       continue;
     }
@@ -1193,9 +1197,9 @@ void SortedExchange::send(const SxSend& a) {
 #undef PT_SX_SCAT
     PT_HIP_CHECK(hipGetLastError());
     PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
-    PT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_routed_[i], 0));
+    PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
     a2a(b.send, b.recv, (size_t)rq * 4, pairs ? rq_send : nullptr, pairs ? rq_recv : nullptr, capturing);
-    PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], comm_stream_));
+    PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], cur_comm_));
     if (i > 0) serve(i - 1);
   }
   serve(chunks_ - 1);
@@ -1203,10 +1207,10 @@ void SortedExchange::send(const SxSend& a) {
   // scatter).  A captured Send keeps the layout in force (a replay runs no host
   // code to adopt a new one), so it records no agreement.
   if (!capturing) {
-    allreduce_meta(meta, comm_stream_);
+    allreduce_meta(meta, cur_comm_);
     PT_HIP_CHECK(hipMemcpyAsync(meta_host_ + cur * kSxMetaWords, meta, (kSxMetaPair + R_ * R_) * sizeof(uint64_t),
-                                hipMemcpyDeviceToHost, comm_stream_));
-    PT_HIP_CHECK(hipEventRecord(ev_meta_[cur], comm_stream_));
+                                hipMemcpyDeviceToHost, cur_comm_));
+    PT_HIP_CHECK(hipEventRecord(ev_meta_[cur], cur_comm_));
     meta_send_[cur] = sends_;
   } else {
     meta_send_[cur] = -1;

@@ -139,6 +139,7 @@ class SortedExchange {
   int R_, rank_, chunks_;
   int64_t max_chunk_, C_alloc_;
   hipStream_t comm_stream_ = nullptr;
+  hipStream_t cur_comm_ = nullptr;  // the stream this Send's collectives go on (comm_stream_, or the caller's)
   Bufs bufs_[kSxMaxChunks];
   uint32_t* hist_ = nullptr;  // [G][R * K] per-block bucket counts -> prefixes (K = 64 or 1)
   uint32_t* boff_ = nullptr;  // [R * K] bucket offsets within their region
