@@ -986,11 +986,16 @@ void SortedExchange::send(const SxSend& a) {
   const hipStream_t cs = as_stream(a.stream);
   // PTYPE_SX_COMM_CS=1: the collectives on the caller's stream itself (a graph-capture probe:
   // tools/rccl_capture_probe.py sx1cs) instead of the engine's comm stream
+  // Under a hipGraph capture the collectives go on the capturing stream itself: RCCL calls on a
+  // stream forked into the capture crash graph instantiation on this stack, issued on the
+  // capture stream they instantiate and replay correctly (tools/rccl_capture_probe.py sx1cs,
+  // profiles/r3_rccl_capture_probe.txt) -- the captured Send then runs its chunks' collectives in
+  // order with their compute instead of beside it.
   static const bool comm_on_cs = getenv("PTYPE_SX_COMM_CS") && atoi(getenv("PTYPE_SX_COMM_CS")) == 1;
-  cur_comm_ = comm_on_cs ? cs : comm_stream_;
-  pick_spec(cs);
   hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;
   const bool capturing = hipStreamIsCapturing(cs, &capst) == hipSuccess && capst != hipStreamCaptureStatusNone;
+  cur_comm_ = (comm_on_cs || (capturing && comm_)) ? cs : comm_stream_;
+  pick_spec(cs);
   const PackedLayout L = L_;
   const int S = sx_round_S(L.S);
   const int64_t C = C_;

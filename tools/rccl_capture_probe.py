@@ -63,7 +63,8 @@ def main():
         v.zero_()
         g.replay()
         torch.cuda.synchronize()
-        print(json.dumps({"mode": mode, "ok": bool(torch.equal(v, req.a0 * req.a1))}))
+        print(json.dumps({"mode": mode, "ok": bool(torch.equal(v, req.a0 * req.a1))}), flush=True)
+        os._exit(0)  # (the teardown after a captured RCCL graph hung here once: skip it)
     dist.destroy_process_group()
 
 
