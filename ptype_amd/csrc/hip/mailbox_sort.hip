@@ -1485,11 +1485,14 @@ __global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxV
 
 // ---------------------------------------------------------------- host
 // The fused sort + drain for stateless one-pass Sends (PTYPE_MBOX_FUSED=0: two launches).
-// the fused sort + drain kernel (PTYPE_MBOX_FUSED=1): measured slower than the two kernels once the
-// sort reserves its runs (8 Mi: 149 vs 95 + 39 us; its register file halves the drain's occupancy)
-static bool fused_ok() {
-  static const bool on = getenv("PTYPE_MBOX_FUSED") && std::string(getenv("PTYPE_MBOX_FUSED")) == "1";
-  return on;
+// the fused sort + drain kernel: slower than the two kernels for large batches once the sort
+// reserves its runs (8 Mi: 149 vs 95 + 39 us; its register file halves the drain's occupancy),
+// faster for small ones, where a launch and a kernel boundary weigh more (1 Mi bench step: 5-7 %
+// in three sessions).  Default: fused up to 512 tiles (2 Mi messages); PTYPE_MBOX_FUSED=1 / 0
+// forces it on / off.
+static bool fused_ok(int64_t tiles) {
+  static const int env = getenv("PTYPE_MBOX_FUSED") ? atoi(getenv("PTYPE_MBOX_FUSED")) : -1;
+  return env == 1 || (env < 0 && tiles <= 512);
 }
 // one-pass sorts of stateless batches reserve each tile's runs with atomics
 // instead of looking back (onesweep_tile); PTYPE_MBOX_RESERVE=0: look-back
@@ -1586,7 +1589,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // (stateless batches of any size take the one-pass sort when the fused sort + drain is on: one launch per Send)
   const int sort_mode = a.sort_mode ? a.sort_mode
                         : env_mode  ? env_mode
-                        : (tiles >= 1024 || (!a.ordered && !a.arrival && (fused_ok() || reserve_ok()))) ? 1
+                        : (tiles >= 1024 || (!a.ordered && !a.arrival && (fused_ok(tiles) || reserve_ok()))) ? 1
                                                                                                          : 2;
   if (sort_mode < 1 || sort_mode > 3) throw std::invalid_argument("mailbox send: sort_mode 0..3");
   const bool two_pass = sort_mode != 1;
@@ -1742,7 +1745,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else if (a.method_col) PT_SCAT(false, true);
     else PT_SCAT(false, false);
 #undef PT_SCAT
-  } else if (!a.ordered && !all_sidx && Sv <= 256 && fused_ok()) {
+  } else if (!a.ordered && !all_sidx && Sv <= 256 && fused_ok(tiles)) {
     // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel)
     const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv));
 #define PT_SD3(MO, A2, MC, FX, R8)                                                                                  \
