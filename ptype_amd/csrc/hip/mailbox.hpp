@@ -84,7 +84,11 @@ struct MboxView {
   uint32_t log_s = 0, log_q = 0;
   uint32_t planar = 0;
   uint64_t b_off = 0;  // planar: word offset of plane B (past plane A + a de-aliasing pad)
+  // one-pass sorts of stateless batches: per-shard run reservations, one counter per
+  // 128-B line (kResvStride words; null: the epoch totals are in the group sums)
+  uint32_t* resv = nullptr;
 };
+constexpr int kResvStride = 32;
 
 // Host-visible control block of the persistent consumer.
 struct alignas(64) MboxCtrl {
@@ -216,6 +220,7 @@ class Mailboxes {
   unsigned* sort_tctr_ = nullptr;   // [0] one-pass sort's tile counter (self-resetting), [1] its epoch tag
   uint8_t* sort_stab_ = nullptr;    // LDS-table count: one byte per actor (shard, or not-here / probe)
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
+  uint32_t* sort_resv_ = nullptr;   // [S][kResvStride] one-pass run reservations (zero between Sends)
   // 8-B ring records: [0] the field widths in force (device; updated by each Send's
   // last block), per-tile field bit lengths, and a pinned mirror of [0] (bit 31: the
   // fields no longer fit 64 bits -- the host then keeps 16-B records)

@@ -571,7 +571,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
         c += x;
       }
       if (reserve) {
-        excl = c ? atomicAdd(&gsum[s], c) : 0u;  // this tile's run of shard s (gsum row 0: the epoch total)
+        excl = c ? atomicAdd(&mv.resv[s * kResvStride], c) : 0u;  // this tile's run of shard s
       } else if (t == 0) {
         __hip_atomic_exchange(d, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
@@ -768,6 +768,13 @@ __device__ __forceinline__ uint32_t epoch_total(uint32_t* gsum, uint32_t ngroups
   return t;
 }
 
+// The epoch's total of shard s, cleared for the next Send: the reservation counter of
+// a one-pass stateless Send (memory-side, as its tiles added to it), else the group sums.
+__device__ __forceinline__ uint32_t epoch_sum(const MboxView& mv, uint32_t* gsum, uint32_t ngroups, uint32_t S,
+                                              uint32_t s) {
+  return mv.resv ? atomicExch(&mv.resv[s * kResvStride], 0u) : epoch_total(gsum, ngroups, S, s, true);
+}
+
 // The epoch's positions of shard s are consumed: head = tail = tail + total
 // (overflowed positions were never written and are skipped with them).
 __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uint32_t tot) {
@@ -881,7 +888,7 @@ __global__ __launch_bounds__(kST) void mbx_drain_msg_kernel(MboxView mv, SortIn 
   __syncthreads();
   if (last) {  // every block's records are read: the rings are consumed
     const uint32_t S = 1u << mv.log_s;
-    for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
+    for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_sum(mv, gsum, ngroups, S, s));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
   }
 }
@@ -1070,7 +1077,7 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
   __syncthreads();
   if (last) {  // every block's records are read: the rings are consumed
-    for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_total(gsum, ngroups, S, s, true));
+    for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_sum(mv, gsum, ngroups, S, s));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
     if constexpr (R8) rec8_next(in, const_cast<uint32_t*>(in.r8w), r8host, in.tiles);
   }
@@ -1118,7 +1125,7 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
     // (reserve: the totals were built by memory-side atomics in this launch -- read and
     // cleared the same way, not through this XCD's L2)
     for (uint32_t s = threadIdx.x; s < S; s += kST)
-      epoch_commit(mv, s, reserve ? atomicExch(&gsum[s], 0u) : epoch_total(gsum, 1, S, s, true));
+      epoch_commit(mv, s, epoch_sum(mv, gsum, 1, S, s));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
     if constexpr (R8) rec8_next(in, const_cast<uint32_t*>(in.r8w), r8host, in.tiles);
   }
@@ -1661,7 +1668,17 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // the stateless drain: ring order (default) or message order (PTYPE_MBOX_DRAIN=msg: every slot index written)
   static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
   const bool all_sidx = msg_drain && !a.ordered;
-  const bool reserve = !a.ordered && reserve_ok();  // (one-pass only: tiles reserve runs, no look-back)
+  const bool reserve = !a.ordered && reserve_ok() && sort_mode == 1;  // (one-pass: tiles reserve runs)
+  if (reserve) {
+    if (!sort_resv_) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        throw std::runtime_error("mailbox send: first reserving Send inside a graph capture (warm up first)");
+      PT_HIP_CHECK(hipMalloc((void**)&sort_resv_, (size_t)kMboxSortMaxShards * kResvStride * 4));
+      PT_HIP_CHECK(hipMemset(sort_resv_, 0, (size_t)kMboxSortMaxShards * kResvStride * 4));
+    }
+    mv.resv = sort_resv_;
+  }
   // 8-B ring records: one-pass sort of a stateless batch of one two-argument method, ring-order drain
   // (PTYPE_MBOX_REC8=0: 16-B records).  Field widths: the mailbox from the state size or the
   // directory (a wider mailbox spills), the rest split between the zigzag arguments.
