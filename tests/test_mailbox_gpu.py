@@ -450,7 +450,9 @@ def test_sorted_mailbox_8b_records_spill_what_does_not_fit(fused):
         assert s["overflow"] == 0 and s["spilled"] > 0 and s["processed"] == 3 * M, s
         print("OK", s["spilled"])
     ''')
-    env = dict(os.environ, PTYPE_MBOX_FUSED=fused, PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "tests")]))
+    # (PTYPE_MBOX_REC8=1: this batch size would take 16-B records by default)
+    env = dict(os.environ, PTYPE_MBOX_FUSED=fused, PTYPE_MBOX_REC8="1",
+               PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "tests")]))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
