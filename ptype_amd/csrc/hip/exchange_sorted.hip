@@ -905,6 +905,12 @@ void SortedExchange::adopt(const uint64_t* meta, int64_t from) {
     cap_[k] = (uint32_t)std::min<int64_t>(capacity(need), C_);
     sum_pairs += cap_[k];
   }
+  // (loopback: one rank stands for a symmetric node and only its own row is filled -- the
+  // decision is taken on that row)
+  if (fake_ && fake_->loopback()) {
+    sum_pairs = 0;
+    for (int q = 0; q < R_; ++q) sum_pairs += (int64_t)R_ * cap_[rank_ * R_ + q];
+  }
   static const bool pairs_off = getenv("PTYPE_SX_PAIRS") && atoi(getenv("PTYPE_SX_PAIRS")) == 0;
   pairs_ = !pairs_off && R_ > 1 && (double)sum_pairs < 0.85 * (double)C_ * RR;
   if (!pairs_)
