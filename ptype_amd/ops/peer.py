@@ -16,6 +16,7 @@ from . import hip
 from .records import METHOD_CALC_MULTIPLY
 
 TICK_NS = 10.0  # s_memrealtime runs at 100 MHz
+_ATTACHED: list = []  # relays handed to a dispatcher (kept until process exit; see PeerRelay)
 
 
 class PeerCaller:
@@ -70,8 +71,10 @@ class PeerRelay:
     another server, with no host between the hops (reference: a handler
     dialling another node, cluster/rpc.go:59-67).
 
-    Close ``server`` (or ``detach()`` and let it go idle) before dropping the
-    relay: the wave reads the table until its next idle refresh."""
+    The native relay (its lanes and device table) is kept for the life of the
+    process once attached: the dispatcher wave reads the table until its next
+    idle refresh, so freeing it earlier could pull memory out from under a
+    running wave."""
 
     def __init__(self, server, shm_name: str, device=None, n_lanes: int = 8, timeout_s: float = 1.0):
         dev = torch.device(device if device is not None else "cuda")
@@ -81,6 +84,7 @@ class PeerRelay:
         self._relay = hip().PeerRelay(shm_name, dev.index, int(n_lanes), float(timeout_s))
         self._server = server
         server.set_relay(self._relay.table)
+        _ATTACHED.append(self._relay)
 
     @property
     def lanes(self) -> int:
