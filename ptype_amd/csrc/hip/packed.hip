@@ -267,9 +267,10 @@ __global__ __launch_bounds__(256) void pack_replies_kernel(const uint32_t* __res
 
 // ---- K8 for v3 replies: a gather per message (coalesced outputs); kCompU
 // messages per thread per trip, all perm reads, then all reply reads, in flight
-constexpr int kCompU = 4;
+// (messages per thread per trip: a kernel template argument, PTYPE_COMP_U in {2, 4, 8}; default 4)
 constexpr int32_t kPastBatch = INT32_MIN;  // (perm codes: >= 0 slot position, -1 overflow, -2 no actor, -3 direct)
 
+template <int kCompU>
 __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
                                                               uint32_t C, int R, int vb,
                                                               const int32_t* __restrict__ perm, int64_t M,
@@ -478,10 +479,16 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t p
   if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
   if (R < 1 || R > kMaxRanks) throw std::invalid_argument("complete: 1 <= R <= 64");
   if (vb != 1 && vb != 2 && vb != 4 && vb != 8) throw std::invalid_argument("complete: vb in {1,2,4,8}");
-  hipLaunchKernelGGL(complete_packed_kernel, dim3(grid_for(M, 256 * kCompU, checksum ? 1024 : 8192)), dim3(256), 0,
-                     as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R, vb,
-                     (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum,
-                     direct);
+  static const int comp_u = getenv("PTYPE_COMP_U") ? atoi(getenv("PTYPE_COMP_U")) : 4;
+#define PT_COMP(U)                                                                                                 \
+  hipLaunchKernelGGL(complete_packed_kernel<U>, dim3(grid_for(M, 256 * (U), checksum ? 1024 : 8192)), dim3(256), 0, \
+                     as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R, vb,          \
+                     (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum,   \
+                     direct)
+  if (comp_u == 8) PT_COMP(8);
+  else if (comp_u == 2) PT_COMP(2);
+  else PT_COMP(4);
+#undef PT_COMP
   PT_HIP_CHECK(hipGetLastError());
 }
 void launch_pack_replies(uintptr_t v2, int R, int64_t C, uintptr_t reply, int vb, uintptr_t stats,
