@@ -1086,7 +1086,10 @@ void SortedExchange::send(const SxSend& a) {
     PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_req_in_[i], 0));
     // ~2048 blocks over the R regions (at least one per region)
     const int64_t per = std::max<int64_t>(1, max_chunk_ / R_);
-    const unsigned X = (unsigned)std::max<int64_t>(1, std::min<int64_t>((per + 1023) / 1024, std::max(1, 2048 / R_)));
+    static const int drain_blocks = getenv("PTYPE_SX_DRAIN_BLOCKS") ? atoi(getenv("PTYPE_SX_DRAIN_BLOCKS")) : 2048;
+    static const int drain_per = getenv("PTYPE_SX_DRAIN_PER") ? atoi(getenv("PTYPE_SX_DRAIN_PER")) : 1024;
+    const unsigned X = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>((per + drain_per - 1) / drain_per, std::max(1, drain_blocks / R_)));
 #define PT_SX_PAR(SV)                                                                                         \
   hipLaunchKernelGGL((sx_drain_par_kernel<SV>), dim3(X, R_), dim3(256), 0, cs, (const uint32_t*)b.recv, rq, C, L, \
                      R_, may_order, b.reply, rp, (int64_t*)a.state, a.n_state, a.delay_ticks, stats_)
