@@ -405,11 +405,6 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
 // drains' commit.  The batch's inputs are read once and the route words never
 // leave registers (the two-pass form wrote and re-read 4 B per message).
 __host__ __device__ constexpr size_t onesweep_lds_bytes(uint32_t S) { return (size_t)S * (8 + 4 + 4 + 4 * (kST / kWave)); }
-// with the 8-B records' staging: the tile's per-shard run starts (S words) and the tile's records
-// in ring order (kSTile x 8 B, 8-B aligned)
-__host__ __device__ constexpr size_t onesweep_lds_bytes(uint32_t S, bool r8) {
-  return onesweep_lds_bytes(S) + (r8 ? ((size_t)(S + 1) * 4 + 8 + (size_t)kSTile * 8) : 0);
-}
 
 template <bool A2, bool MC>
 __device__ __forceinline__ void load_cols(const SortIn& in, uint32_t t, int64_t (&v0)[kSK], int64_t (&v1)[kSK],
@@ -493,12 +488,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   uint32_t* pre = room + S;                                                   // the tile's prefix per shard
   uint32_t* wcnt_all = pre + S;                                               // [kST / kWave][S]
   auto wcnt = [&](unsigned ww, uint32_t sh) -> uint32_t& { return wcnt_all[ww * S + sh]; };
-  // (in.rec8) the tile's records staged in ring order -- shard by shard, each shard's run in
-  // message order -- then written out with lane-consecutive 8-B stores (whole lines), not
-  // 16 partial runs per store instruction; texcl: each shard's run start in the stage
-  uint32_t* texcl = wcnt_all + (kST / kWave) * S;
-  uint64_t* stage = reinterpret_cast<uint64_t*>(
-      (reinterpret_cast<uintptr_t>(texcl + S + 1) + 7) & ~static_cast<uintptr_t>(7));
   __shared__ uint32_t tile_s;
   __shared__ uint32_t tmax[3];  // (in.rec8) the tile's field bit lengths
   const unsigned w = threadIdx.x / kWave, lane = lane_id();
@@ -564,7 +553,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     }
     __syncthreads();
   }
-  uint32_t c_mine = 0;  // (in.rec8: S <= 64, one shard per lane of wave 0) this lane's shard's tile count
   for (uint32_t s = W > 1 ? threadIdx.x / W : threadIdx.x; s < S; s += W > 1 ? S : kST) {
     uint32_t c = 0;
     uint64_t excl = 0;
@@ -582,7 +570,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
         wcnt(ww, s) = c;
         c += x;
       }
-      c_mine = c;
       if (reserve) {
         excl = c ? atomicAdd(&mv.resv[s * kResvStride], c) : 0u;  // this tile's run of shard s
       } else if (t == 0) {
@@ -625,11 +612,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     }
   }
   sp |= escm != 0;
-  if (in.rec8 && w == 0) {  // the shards' run starts in the stage (ordered before use by the spill barrier)
-    const uint32_t incl = wave_incl_scan(c_mine);
-    if (lane < S) texcl[lane] = incl - c_mine;
-    if (lane == S - 1) texcl[S] = incl;  // (one word past: the tile's total -- the stage's length)
-  }
   if (in.rec8) {  // the tile's field bit lengths (read by thread 0 past the spill barrier)
     const uint32_t bm = wave_max_u32(bitlen64(or_m)), b0 = wave_max_u32(bitlen64(or_0)),
                    b1 = wave_max_u32(bitlen64(or_1));
@@ -676,12 +658,11 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     const uint64_t slot = slot_at(mv, sh, base[sh] + off);
     if (wsidx) sidx[i] = (uint32_t)slot;
     const uint32_t mt = meth[k];
-    if (in.rec8) {  // 8-B record (stateless, uniform method, two arguments; wider ones spilled above):
-                    // staged at its place in the tile's ring order, written out below
+    if (in.rec8) {  // 8-B record (stateless, uniform method, two arguments; wider ones spilled above)
       const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu;
       const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
       const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
-      stage[texcl[sh] + off - pre[sh]] =
+      reinterpret_cast<uint64_t*>(mv.rec)[slot] =
           (uint64_t)(i & (kSTile - 1)) | ((uint64_t)mb[k] << 12) | (z0 << (12 + wm)) | (z1 << (12 + wm + w0));
     } else if (mt < 128u && fits_i32(v0[k]) && fits_i32(v1[k]) && v2[k] == 0) {
       *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
@@ -695,20 +676,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
       if (fl) mv.a2[slot] = v2[k];
     }
     ++n_enq;
-  }
-  if (in.rec8) {  // the staged records, lane-consecutive into each shard's run (whole-line stores)
-    __syncthreads();
-    const uint32_t T = texcl[S];
-    uint64_t* ring64 = reinterpret_cast<uint64_t*>(mv.rec);
-    for (uint32_t j = threadIdx.x; j < T; j += kST) {
-      uint32_t s = 0;  // the shard whose run holds stage entry j: the last with texcl[s] <= j (S <= 64)
-      for (uint32_t b = 32; b; b >>= 1)
-        if (s + b < S && texcl[s + b] <= j) s += b;
-      const uint32_t off = pre[s] + (j - texcl[s]);
-      // (past the ring's room: never written -- answered overflow / spilled above; an escaped
-      // message's entry holds no record and its slot is never read: its tile drains by slot index)
-      if (off < room[s]) ring64[slot_at(mv, s, base[s] + off)] = stage[j];
-    }
   }
   // the tile's field bit lengths, for the next Send's widths (rec8_next): a memory-side write
   // (the fused kernel's last block reads it within the launch: its ticket follows a vmcnt(0) wait)
@@ -1720,7 +1687,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // there -- 1 Mi bench step 24.1 vs 21.9 G msg/s in three sessions -- while 8 Mi gains with 8 B)
   static const int rec8_env = getenv("PTYPE_MBOX_REC8") ? atoi(getenv("PTYPE_MBOX_REC8")) : -1;
   const bool r8 = (rec8_env == 1 || (rec8_env < 0 && tiles > 512)) && sort_mode == 1 && !a.ordered && !a.arrival &&
-                  !a.a2 && !a.method_col && mv.planar && !all_sidx && Sv <= 64;  // (the stage's shard search)
+                  !a.a2 && !a.method_col && mv.planar && !all_sidx;
   if (r8 && (!r8w_ || r8_tiles_ < (uint64_t)tiles)) {  // (outside a capture: grown with the sort workspace)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
@@ -1799,7 +1766,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_SCAT
   } else if (!a.ordered && !all_sidx && Sv <= 256 && fused_ok(tiles)) {
     // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel)
-    const size_t lds = std::max(onesweep_lds_bytes(Sv, r8_on), ring_drain_lds_bytes(Sv));
+    const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv));
 #define PT_SD3(MO, A2, MC, FX, R8)                                                                                  \
   hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, R8>), dim3(in.tiles), dim3(kST), lds, st, in, mv,          \
                      sort_desc_,                                                                                     \
@@ -1833,7 +1800,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     // (PTYPE_OS_LATE=1: arguments loaded after the look-back, 87 instead of 115 VGPRs -- measured slower,
     // 0.231 vs 0.223 ms per 8 Mi Send: the loads' latency is then exposed)
 #define PT_OS2(MO, A2, MC, LT)                                                                                     \
-  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv, r8_on), st, \
+  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv), st, \
                      in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx, \
                      reserve)
 #define PT_OS1(MO, A2, MC)              \
