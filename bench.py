@@ -366,7 +366,8 @@ def main():
         mb = ex_.mailboxes
         if mb is None:
             return {}
-        return {"mailbox_shards": mb.shards, "mailbox_slots": mb.slots, "mailbox_ring_bytes": mb.bytes}
+        return {"mailbox_shards": mb.shards, "mailbox_slots": mb.slots, "mailbox_ring_bytes": mb.bytes,
+                "mailbox_record_bytes": mb.last_record_bytes}
 
     table = build_table(args.placement)
     hang_s = os.environ.get("PTYPE_HANG_DIAG")

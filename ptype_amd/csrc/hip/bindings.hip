@@ -480,6 +480,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("shards", &Mailboxes::shards)
       .def_property_readonly("slots", &Mailboxes::slots)
       .def_property_readonly("bytes", &Mailboxes::bytes)
+      .def_property_readonly("last_record_bytes", &Mailboxes::last_record_bytes)
       .def_property_readonly("consumer_processed", &Mailboxes::consumer_processed)
       .def_property_readonly("launches", &Mailboxes::launches)
       .def_property_readonly("handle", [](Mailboxes& m) { return (uintptr_t)&m; },

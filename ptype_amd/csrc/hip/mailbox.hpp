@@ -196,6 +196,8 @@ class Mailboxes {
   uint32_t shards() const { return 1u << mv_.log_s; }
   uint32_t slots() const { return 1u << mv_.log_q; }
   uint64_t bytes() const { return bytes_; }
+  // ring record bytes of the last sorted Send (8: 8-B records, 16: compact, 32: long records in use)
+  int last_record_bytes() const { return last_rec_bytes_; }
   uint64_t consumer_processed() const;
   uint64_t launches() const { return launches_; }
   const MboxView& view() const { return mv_; }
@@ -220,6 +222,7 @@ class Mailboxes {
   unsigned* sort_tctr_ = nullptr;   // [0] one-pass sort's tile counter (self-resetting), [1] its epoch tag
   uint8_t* sort_stab_ = nullptr;    // LDS-table count: one byte per actor (shard, or not-here / probe)
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
+  int last_rec_bytes_ = 0;
   uint32_t* sort_resv_ = nullptr;   // [S][kResvStride] one-pass run reservations (zero between Sends)
   // 8-B ring records: [0] the field widths in force (device; updated by each Send's
   // last block), per-tile field bit lengths, and a pinned mirror of [0] (bit 31: the

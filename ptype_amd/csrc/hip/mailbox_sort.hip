@@ -1617,6 +1617,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   const bool fixed_mul = a.fixed_method == kCalculatorMultiply;
 
   if (a.arrival) {  // fixed positions: enqueue + drain, no count pass
+    last_rec_bytes_ = (a.a2 || a.method_col) ? 32 : 16;
 #define PT_AENQ(MO)                                                                                        \
   do {                                                                                                     \
     if (a.a2 && a.method_col)                                                                              \
@@ -1711,6 +1712,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   }
   // fields that outgrew 64 bits (the last Send's widths, bit 31): 16-B records from here on
   const bool r8_on = r8 && !(__atomic_load_n(r8host_, __ATOMIC_RELAXED) & 0x80000000u);
+  last_rec_bytes_ = r8_on ? 8 : ((a.a2 || a.method_col) ? 32 : 16);  // (16: compact unless a value is wide)
   if (r8_on) {
     in.rec8 = 1;
     in.r8w = r8w_;

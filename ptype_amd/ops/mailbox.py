@@ -60,6 +60,11 @@ class Mailboxes:
         return int(self._m.bytes)
 
     @property
+    def last_record_bytes(self) -> int:
+        """Ring record size of the last sorted Send: 8 (8-B records), 16 (compact) or 32."""
+        return int(self._m.last_record_bytes)
+
+    @property
     def handle(self) -> int:
         """Address of the native object: the epoch engine delivers received records into it."""
         return int(self._m.handle)
