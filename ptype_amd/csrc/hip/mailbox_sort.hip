@@ -26,7 +26,7 @@
 //            distinct actors side by side (LDS bins), replies staged at their
 //            ring slots; a ring-order completion puts them in message order.
 //
-// Stateless batches use a 16-shard view of the rings (every ring is empty
+// Stateless batches use an 8-shard view of the rings (every ring is empty
 // between epoch Sends): longer runs per tile and shard.  Arrival sharding
 // (stateless only) skips the sort: tile t's messages sit at fixed positions of
 // ring t mod S.
@@ -533,7 +533,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   const uint64_t Q = 1ull << mv.log_q;
   unsigned long long timeouts = 0;
   int sp = 0;
-  // Up to 64 shards (the stateless 16-shard view): W = kST / S lanes per shard, the
+  // Up to 64 shards (the stateless 8-shard view): W = kST / S lanes per shard, the
   // whole block looking back W tiles per round trip (lookback_group); more shards:
   // one lane per shard, kLbWin tiles per round trip.
   const uint32_t W = (!reserve && in.lb_group && S <= kST / 8) ? min(64u, kST / S) : 1u;
@@ -1653,12 +1653,13 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // and shard (~256 records of a 4096-message tile: whole lines for the scatter's
   // stores and the drain's loads).  8 Mi msgs, 256 shards -> 32 / 16 / 8:
   // 0.222 -> 0.186 / 0.179 / 0.180 ms per Send (PTYPE_MBOX_STATELESS_SHARDS,
-  // 0 = the full geometry).
+  // 0 = the full geometry).  Round 4, with run reservations and 8-B records: 8
+  // shards, 2-3 % faster per bench step than 16 (profiles/r4_mailbox_ab.md).
   MboxView mv = mv_;
   uint32_t Sv = S;
   if (!a.ordered) {
     static const int s_env =
-        getenv("PTYPE_MBOX_STATELESS_SHARDS") ? atoi(getenv("PTYPE_MBOX_STATELESS_SHARDS")) : 16;
+        getenv("PTYPE_MBOX_STATELESS_SHARDS") ? atoi(getenv("PTYPE_MBOX_STATELESS_SHARDS")) : 8;
     if (s_env > 0 && (s_env & (s_env - 1)) == 0 && (uint32_t)s_env < S) {
       const uint32_t k = mv.log_s - (uint32_t)__builtin_ctz((unsigned)s_env);
       mv.log_s -= k;
