@@ -251,11 +251,12 @@ def main():
     st = torch.empty(M, dtype=torch.int32, device=device)
     pregen = args.zipf > 0 or args.pregen
     use_graph = use_gpu and not pregen and (args.graph == "on" or (args.graph == "auto" and not dist_on and fake is None))
-    if args.steps_per_graph == 0:  # auto (measured at 8 Mi msgs: 1 -> 89-90, 2 -> 93.8, 4 -> 94.8 G msg/s)
+    if args.steps_per_graph == 0:  # auto (measured at 8 Mi msgs: 1 -> 89-90, 2 -> 93.8, 4 -> 94.8 G msg/s, round 2)
         # the timed steps replay a graph of U whole steps (U divides --steps); warm-up
         # steps that do not fill a U-step replay run on a 1-step graph of the same
         # step, so exactly --warmup steps warm up and exactly --steps are timed
-        args.steps_per_graph = next((u for u in (4, 2) if use_graph and args.steps % u == 0), 1)
+        # (round 4: 20 steps per replay measured 1-3 % above 4 at 8 Mi and 1 Mi, profiles/r4_mailbox_ab.md)
+        args.steps_per_graph = next((u for u in (20, 10, 5, 4, 2) if use_graph and args.steps % u == 0), 1)
     if args.steps_per_graph < 1 or (args.steps_per_graph > 1 and (
             not use_graph or args.steps % args.steps_per_graph)):
         raise SystemExit("--steps-per-graph: needs the graph path, and --steps a multiple of it")
