@@ -59,7 +59,7 @@ struct GpuConfig {
   uint32_t mailbox_slots = 0;  // 0: sized from max_batch
   std::string delivery = "auto";  // "mailbox": every Send through the HBM mailboxes; "direct"; "auto"
   // data-plane collectives at world > 1: "rccl" (the group's communicator, one GPU per rank) or
-  // "ipc" (IpcComm: peers' HBM segments by IPC handle over a gloo group; ranks may share a GPU)
+  // "ipc" (IpcComm: shared-memory segments every rank maps, over a gloo group; ranks may share a GPU)
   std::string comm = "rccl";
   bool watch = true;          // follow the store (shard records, leases) into the GPU registry mirror
   // rank failures (runtime.py recover): Join's group re-forms through the store

@@ -44,12 +44,21 @@ constexpr uint64_t kFoldMul = 0x100000001b3ull;
 // they must run one at a time per actor, in mailbox order (HBM mailboxes, K2/K3).
 inline constexpr bool method_ordered(uint32_t m) { return m == kSeqFold; }
 
+// Methods whose handler reads no actor state at all (the reply is a function of
+// the arguments): a message only has to reach its actor's GPU, so a sender may
+// resolve just the destination rank (the route directory's rank byte table) and
+// carry the actor id instead of the destination mailbox.
+inline constexpr bool method_stateless(uint32_t m) {
+  return m == kCalculatorMultiply || m == kPrimeCheck || m == kEcho;
+}
+
 enum RecordFlags : uint16_t {
   kFlagValid = 1,
   kFlagRouted = 2,  // `actor` holds the destination's local mailbox index
   kFlagIdentity = 4,  // slot header: slot position == message index (R = 1, no gaps)
   kFlagA2 = 8,        // mailbox record: the third argument is in the ring's a2 side array
   kFlagSharded = 16,  // sorted-exchange region header: records sorted by actor shard (shard table at its end)
+  kFlagActorIds = 32,  // sorted-exchange region header: the mailbox field carries actor ids (stateless method)
 };
 
 enum ReplyStatus : int32_t {

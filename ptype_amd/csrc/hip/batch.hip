@@ -675,10 +675,18 @@ __global__ __launch_bounds__(256) void local_send_kernel(
 __global__ __launch_bounds__(256) void complete_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
                                                        uint32_t C, const int32_t* __restrict__ perm, int64_t M,
                                                        int64_t* __restrict__ out_val, int32_t* __restrict__ out_st,
-                                                       unsigned long long* __restrict__ checksum, bool direct) {
+                                                       unsigned long long* __restrict__ checksum, bool direct,
+                                                       const uint64_t* __restrict__ failed) {
   unsigned long long sum = 0;
+  // a failed collective wrote no reply slots (see complete_packed_kernel)
+  const bool lost = failed && __hip_atomic_load(failed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t p = perm[i];
+    if (lost && (p >= 0 || p == -3)) {
+      out_val[i] = 0;
+      out_st[i] = kStatusNotDelivered;
+      continue;
+    }
     if (direct && p < 0) {
       if (checksum) sum += (unsigned long long)out_val[i];
       continue;
@@ -989,12 +997,13 @@ void launch_dispatch(uintptr_t recv, int R, int64_t C, int nargs, bool mc, uintp
 }
 
 void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
-                     uintptr_t checksum, bool direct, uintptr_t stream) {
+                     uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed) {
   if (M <= 0) return;
   if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
   hipLaunchKernelGGL(complete_kernel, dim3(grid_cap(M, 256, checksum ? 1024 : 8192)), dim3(256), 0,
                      as_stream(stream), (const uint32_t*)rep, wire_rep_words(C), (uint32_t)C, (const int32_t*)perm, M,
-                     (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum, direct);
+                     (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum, direct,
+                     (const uint64_t*)failed);
   PT_HIP_CHECK(hipGetLastError());
 }
 

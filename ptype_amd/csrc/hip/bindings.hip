@@ -65,8 +65,8 @@ void launch_gob_encode(const std::vector<uintptr_t>&, int64_t, uint32_t, uintptr
 void launch_gob_decode(uintptr_t, uintptr_t, int64_t, uint32_t, const std::vector<uintptr_t>&, uintptr_t, uintptr_t);
 void set_route_tuning(int, int, int);
 int64_t route_fused_grid(int64_t, int64_t*);
-void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uint32_t, uintptr_t, uintptr_t);
-void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
+void launch_table_build_dir(uintptr_t, uint64_t, uintptr_t, uint64_t, uint32_t, uintptr_t, uintptr_t, uintptr_t);
+void launch_complete(uintptr_t, int64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t, uintptr_t);
 int64_t wire_req_words(int64_t, int, bool);
 void launch_prime_gather(uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t,
                          uintptr_t);
@@ -77,7 +77,7 @@ void launch_dispatch_packed(uintptr_t, int, int64_t, const PackedLayout&, uintpt
                             uintptr_t, int64_t, const std::vector<uintptr_t>&, uint64_t, const std::vector<uintptr_t>&,
                             int, uintptr_t);
 void launch_complete_packed(uintptr_t, int64_t, int, int, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool,
-                            uintptr_t);
+                            uintptr_t, uintptr_t);
 void launch_records_to_soa(uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 void launch_snapshot_copy(uintptr_t, uintptr_t, int64_t, uintptr_t);
 }  // namespace ptype
@@ -199,7 +199,8 @@ PYBIND11_MODULE(_hip, m) {
         "(default), 1 = single-pass look-back route; prep_pipe: 0 = default (directory path: next tile's ids "
         "loaded before this tile's gathers), -1 = off -- knobs for experiments");
   m.def("table_build_dir", &launch_table_build_dir, py::arg("table"), py::arg("cap"), py::arg("dir"),
-        py::arg("n_dir"), py::arg("affine_w"), py::arg("affine_stats"), py::arg("stream"));
+        py::arg("n_dir"), py::arg("affine_w"), py::arg("affine_stats"), py::arg("stream"), py::arg("dir_rank") = 0,
+        "K5b/K5c: the dense route directory (4-B route word per id) and, with dir_rank, its rank byte table");
   m.def("dispatch", &launch_dispatch, py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("nargs"), py::arg("mc"),
         py::arg("reply"), py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"),
         py::arg("expected_per_rank"), py::arg("outbox"), py::arg("outbox_cap"), py::arg("direct"), py::arg("self"),
@@ -217,7 +218,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("stream"),
         "after a device-counted epoch: epoch_m[j] = min(count[0], cap), count[0] = 0 (the consumed bank)");
   m.def("complete", &launch_complete, py::arg("rep"), py::arg("C"), py::arg("perm"), py::arg("M"),
-        py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"), py::arg("stream"));
+        py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"), py::arg("stream"),
+        py::arg("failed") = 0);
   m.def("records_to_soa", &launch_records_to_soa, py::arg("rec"), py::arg("M"), py::arg("actor"), py::arg("method"),
         py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("mfma"), py::arg("stream"),
         "32-B AoS request records -> SoA columns (dwordx4 copy, or MFMA byte transposition)");
@@ -269,7 +271,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("outbox_cap"), py::arg("direct"), py::arg("self"), py::arg("stream"));
   m.def("complete_packed", &launch_complete_packed, py::arg("rep"), py::arg("C"), py::arg("R"), py::arg("vb"), py::arg("perm"),
         py::arg("M"), py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"),
-        py::arg("stream"));
+        py::arg("stream"), py::arg("failed") = 0);
 
   m.def("pinned_alloc", &pinned_alloc);
   m.def("pinned_free", &pinned_free);
@@ -394,18 +396,19 @@ PYBIND11_MODULE(_hip, m) {
           [](SortedExchange& e, uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2, uintptr_t method_col,
              int method_uniform, int64_t M, uintptr_t table, uint64_t cap, uintptr_t dir, uint32_t n_dir,
              uint32_t affine_w, uintptr_t out_val, uintptr_t out_st, uintptr_t state, uint32_t n_state,
-             uint64_t delay_ticks, bool ordered, uintptr_t stream) {
+             uint64_t delay_ticks, bool ordered, uintptr_t stream, uintptr_t dir_rank) {
             SxSend a;
             a.actor = actor, a.a0 = a0, a.a1 = a1, a.a2 = a2, a.method_col = method_col;
             a.method_uniform = method_uniform, a.M = M, a.table = table, a.cap = cap, a.dir = dir, a.n_dir = n_dir;
             a.affine_w = affine_w, a.out_val = out_val, a.out_st = out_st, a.state = state, a.n_state = n_state;
-            a.delay_ticks = delay_ticks, a.ordered = ordered, a.stream = stream;
+            a.delay_ticks = delay_ticks, a.ordered = ordered, a.stream = stream, a.dir_rank = dir_rank;
             e.send(a);
           },
           py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("a2"), py::arg("method_col"),
           py::arg("method_uniform"), py::arg("M"), py::arg("table"), py::arg("cap"), py::arg("dir"), py::arg("n_dir"),
           py::arg("affine_w"), py::arg("out_val"), py::arg("out_st"), py::arg("state"), py::arg("n_state"),
-          py::arg("delay_ticks"), py::arg("ordered"), py::arg("stream"), py::call_guard<py::gil_scoped_release>())
+          py::arg("delay_ticks"), py::arg("ordered"), py::arg("stream"), py::arg("dir_rank") = 0,
+          py::call_guard<py::gil_scoped_release>())
       .def("last_wire",
            [](const SortedExchange& e) {
              const auto& w = e.last_wire();
@@ -421,6 +424,8 @@ PYBIND11_MODULE(_hip, m) {
              d["C"] = w.C;
              d["agreed"] = w.agreed;
              d["spec_from"] = w.spec_from;
+             d["shard_ok"] = w.shard_ok;
+             d["route_mode"] = w.route_mode;
              d["meta"] = std::vector<uint64_t>(w.meta, w.meta + kMetaWords);
              return d;
            },

@@ -59,6 +59,10 @@ __host__ __device__ __forceinline__ uint64_t actor_key(uint32_t actor) { return 
 // 0xFFFFFFFF = not registered; kDirFallback = probe the hash table instead.
 constexpr uint32_t kDirMissing = 0xffffffffu;
 constexpr uint32_t kDirFallback = 0xfffffffeu;
+// The directory's rank byte table (K5c, one byte per actor id, built with the
+// directory): 0xFF = not registered; kRankFallback = probe the hash table.
+constexpr uint8_t kRankMissing = 0xffu;
+constexpr uint8_t kRankFallback = 0xfeu;
 
 __device__ __forceinline__ unsigned lane_id() { return __lane_id(); }
 

@@ -50,7 +50,7 @@ void launch_outbox_seal(uintptr_t actor, uint64_t cap, uintptr_t count, uintptr_
 void launch_pack_replies(uintptr_t v2, int R, int64_t C, uintptr_t reply, int vb, uintptr_t stats,
                          int64_t expected_per_rank, uintptr_t stream);
 void launch_complete(uintptr_t rep, int64_t C, uintptr_t perm, int64_t M, uintptr_t out_val, uintptr_t out_st,
-                     uintptr_t checksum, bool direct, uintptr_t stream);
+                     uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed = 0);
 int64_t wire_req_words(int64_t C, int nargs, bool mc);
 int64_t wire_rep_words(int64_t C);
 // wire format v3 (packed.hpp / packed.hip)
@@ -70,7 +70,7 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
                             const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
                             const std::vector<uintptr_t>& direct, int self, uintptr_t stream);
 void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
-                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream);
+                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed = 0);
 
 // ---- RCCL entry points (from the library torch loaded)
 namespace engine_detail {
@@ -160,7 +160,7 @@ static __global__ __launch_bounds__(256) void fake_copy_regions_kernel(const uin
 // The data plane's collectives when they are not RCCL's: the engines drive a
 // HostComm through these calls, one rank's view at a time (`r`).  Two
 // implementations: FakeComm (R ranks of ONE process, host threads) and IpcComm
-// (ipc_comm.hpp: one rank per PROCESS, peers' HBM imported by IPC handle, every
+// (ipc_comm.hpp: one rank per PROCESS, shared-memory segments every rank maps, every
 // collective stream-ordered on the device).
 class HostComm {
  public:
@@ -180,6 +180,11 @@ class HostComm {
   virtual void allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) = 0;
   // throws when an earlier collective failed (a peer missed it); called at every Send
   virtual void check() const {}
+  // device address of a word that is nonzero once a collective of this comm has
+  // failed (nullptr: collectives cannot fail softly).  The completion kernels read
+  // it in stream order: the replies of a failed op answer kStatusNotDelivered
+  // instead of whatever the unwritten regions decode to.
+  virtual const uint64_t* device_failed() const { return nullptr; }
 };
 
 class FakeComm : public HostComm {
@@ -791,12 +796,13 @@ class EpochEngine {
     Timed t(prof_.kernels_ns);
     const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M), m = m_of(a, i);
     const EngineBufs& b = bufs_[bi];
+    const uintptr_t failed = fake_ ? (uintptr_t)fake_->device_failed() : 0;
     if (packed_)
       launch_complete_packed(b.back, C_, R_, L_.vb, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4), a.checksum,
-                             a.direct, (uintptr_t)cs);
+                             a.direct, (uintptr_t)cs, failed);
     else
       launch_complete(collectives() ? b.back : b.reply, C_, b.perm, m, off(a.out_val, lo, 8), off(a.out_st, lo, 4),
-                      a.checksum, a.direct, (uintptr_t)cs);
+                      a.checksum, a.direct, (uintptr_t)cs, failed);
   }
 
   void record(hipEvent_t e, hipStream_t s) {

@@ -33,9 +33,13 @@ PackedLayout sx_layout(const uint64_t* meta) {
 static int sx_round_S(int S) { return S <= 4 ? S : S <= 6 ? 6 : 8; }
 
 // A field fits the layout in force (the mailbox all-ones value is reserved).
+// reject_ordered: the agreement in force saw no ordered method, so no rank
+// sorts by actor shard this Send and the receivers skip their ordered drain --
+// an ordered message overflows (re-sent once the agreement carries its method).
 __device__ __forceinline__ bool sx_fits(const PackedLayout& L, uint32_t meth, uint32_t hdr_method, uint32_t mb,
-                                        uint64_t z0, uint64_t z1, uint64_t z2) {
+                                        uint64_t z0, uint64_t z1, uint64_t z2, bool reject_ordered) {
   auto fits = [&](int q, uint64_t v) { return L.w[q] >= 64 || (v >> L.w[q]) == 0; };
+  if (reject_ordered && method_ordered(meth)) return false;
   if (L.w[0] ? !fits(0, meth) : meth != hdr_method) return false;
   if (L.w[1] == 0 || (uint64_t)mb >= low_mask(L.w[1])) return false;
   return fits(2, z0) && fits(3, z1) && fits(4, z2);
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
                                                          uint32_t* __restrict__ sendbuf, int64_t req_stride,
                                                          uint32_t C, SxCaps caps, PackedLayout L,
                                                          int32_t* __restrict__ perm,
-                                                         unsigned long long* __restrict__ meta) {
+                                                         unsigned long long* __restrict__ meta, bool reject_ordered) {
   // C: the region stride in records (positions are encoded rk * C + pos);
   // caps: each destination's capacity (<= C) -- a message past it overflows
   __shared__ uint32_t cap_s[kSxMaxRanks];
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
         acc.flags |= 1u << (meth < 7 ? meth : 7);
       }
       uint64_t f[5];
-      const bool fit = sx_fits(L, meth, in.method_uniform, mb[k], z0, z1, z2);
+      const bool fit = sx_fits(L, meth, in.method_uniform, mb[k], z0, z1, z2, reject_ordered);
       if (fit) {
         f[0] = meth, f[1] = mb[k], f[2] = z0, f[3] = z1, f[4] = z2;
         perm[i] = (int32_t)(rk * C + pos);
@@ -357,7 +361,8 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
                                                           int rank_self, PackedLayout L, int32_t* __restrict__ perm,
                                                           unsigned long long* __restrict__ meta,
                                                           unsigned long long* __restrict__ stats,
-                                                          uint32_t* __restrict__ rcnt, bool reserve) {
+                                                          uint32_t* __restrict__ rcnt, bool reserve,
+                                                          bool reject_ordered) {
   __shared__ uint32_t wcnt[kST / kWave][kSxMaxRanks];
   __shared__ uint32_t pre[kSxMaxRanks];
   __shared__ uint32_t cap_s[kSxMaxRanks];  // per-destination capacities (C: the region stride in records)
@@ -475,7 +480,7 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
       acc.flags |= 1u << (meth < 7 ? meth : 7);
     }
     uint64_t f[5];
-    const bool fit = sx_fits(L, meth, in.method_uniform, mb[k], z0, z1, z2);
+    const bool fit = sx_fits(L, meth, in.method_uniform, mb[k], z0, z1, z2, reject_ordered);
     if (fit) {
       f[0] = meth, f[1] = mb[k], f[2] = z0, f[3] = z1, f[4] = z2;
       perm[i] = (int32_t)(rk * C + pos);
@@ -813,6 +818,7 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   PT_HIP_CHECK(hipHostMalloc(&meta_host_, 2 * kSxMetaWords * sizeof(uint64_t), hipHostMallocDefault));
   memset(meta_host_, 0, 2 * kSxMetaWords * sizeof(uint64_t));
   for (auto& e : ev_meta_) PT_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  PT_HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   // start-up layout: every column at full width (8-dword records, 8-byte replies)
   uint64_t wide[kMetaWords] = {};
   wide[kMetaMbox] = kMaxMbox - 2;
@@ -825,14 +831,19 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   for (auto& c : cap_) c = (uint32_t)C0;
 }
 
-SortedExchange::~SortedExchange() {  // no synchronisation: a collective stuck on a dead peer must not hang the owner
+SortedExchange::~SortedExchange() {
   (void)hipSetDevice(device_);
+  // RCCL: no synchronisation (a collective stuck on a dead peer must not hang the
+  // owner).  A device-side comm's waits end at its timeout: drain them, so no
+  // kernel of this engine still reads buffers freed below.
+  if (fake_ && fake_->device_side()) (void)hipStreamSynchronize(comm_stream_);
   for (int i = 0; i < chunks_; ++i) {
     Bufs& b = bufs_[i];
     for (void* p : {(void*)b.send, (void*)b.recv, (void*)b.reply, (void*)b.back, (void*)b.perm}) (void)hipFree(p);
     for (hipEvent_t e : {ev_routed_[i], ev_req_in_[i], ev_served_[i], ev_rep_in_[i]}) (void)hipEventDestroy(e);
   }
   for (hipEvent_t e : ev_meta_) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(ev_join_);
   (void)hipFree(hist_);
   (void)hipFree(boff_);
   (void)hipFree(desc_);
@@ -1043,11 +1054,33 @@ void SortedExchange::send(const SxSend& a) {
   const int cur = (int)(sends_ & 1);
   uint64_t* meta = meta_dev_ + cur * kSxMetaWords;
   PT_HIP_CHECK(hipMemsetAsync(meta, 0, kSxMetaWords * sizeof(uint64_t), cs));
-  const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
-  const bool may_order = a.ordered;
+  // Sharded (ordered) regions only while the agreement in force saw an ordered
+  // method on some rank (or before the first agreement): every rank derives the
+  // same answer, so when it is no, no region is sharded anywhere and the
+  // receivers launch no ordered drain at all.  A rank whose batch carries ordered
+  // methods meanwhile answers them OVERFLOW (send_all re-sends them) and folds
+  // their method flags into this Send's agreement, which permits them two Sends on.
+  bool shard_ok = !agreed_;
+  for (int m = 0; m < 7 && !shard_ok; ++m)
+    if (method_ordered((uint32_t)m) && spec_meta_[kMetaFlags + m]) shard_ok = true;
+  if (spec_meta_[kMetaFlags + 7]) shard_ok = true;  // method ids >= 7: may be ordered
+  static const bool shard_always = getenv("PTYPE_SX_SHARD_GATE") && atoi(getenv("PTYPE_SX_SHARD_GATE")) == 0;
+  if (shard_always) shard_ok = true;
+  const bool may_order = a.ordered && shard_ok;
+  const bool wants_order = a.ordered && (a.method_col != 0 || method_ordered((uint32_t)a.method_uniform));
+  const bool reject_ordered = wants_order && !shard_ok;
   // sort by actor shard only when this rank's batch may carry ordered methods;
   // otherwise by rank alone (a region is then one FIFO queue of this sender)
-  const bool sharded = may_order && (a.method_col != 0 || method_ordered((uint32_t)a.method_uniform));
+  const bool sharded = may_order && wants_order;
+  // rank byte gathers (MODE 3) for a rank-only sort of a stateless uniform method:
+  // a message needs only its destination rank (1 B per id: a 1 M-actor table is
+  // 1 MB, L2-resident, against the 4 MB directory), and carries its actor id
+  static const bool rank_table = !(getenv("PTYPE_SX_RANK_TABLE") && atoi(getenv("PTYPE_SX_RANK_TABLE")) == 0);
+  const bool stateless = a.method_col == 0 && method_stateless((uint32_t)a.method_uniform);
+  int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
+  if (mode == 1 && rank_table && a.dir_rank && stateless && !sharded && a.n_dir <= kMaxMbox) mode = 3;
+  wire_.shard_ok = shard_ok;
+  wire_.route_mode = mode;
   const uint32_t K = sharded ? (uint32_t)kSxShards : 1u;
   const uint32_t B = (uint32_t)R_ * K;
   auto chunk_in = [&](int i, int64_t& lo, int64_t& m) {
@@ -1065,6 +1098,7 @@ void SortedExchange::send(const SxSend& a) {
     in.table = (const TableEntry*)a.table;
     in.mask = a.cap - 1;
     in.dir = (const uint32_t*)a.dir;
+    in.dirr = (const uint8_t*)a.dir_rank;
     in.n_dir = a.n_dir;
     in.aw = a.affine_w;
     in.aw_shift = (a.affine_w && (a.affine_w & (a.affine_w - 1)) == 0) ? __builtin_ctz(a.affine_w) : -1;
@@ -1150,12 +1184,13 @@ void SortedExchange::send(const SxSend& a) {
     static const char* sx_sort = getenv("PTYPE_SX_SORT");
     static const int sx_mode = !sx_sort ? 0 : std::string(sx_sort) == "onepass" ? 1 : std::string(sx_sort) == "twopass" ? 2 : 0;
     const bool reserve = sx_mode == 0;
-    if (!sharded && in.tiles > 0 && sx_mode != 2) {
-      const uint32_t hdr3 = ((uint32_t)kFlagValid << 16) | (uint32_t)a.method_uniform;
+    if (!sharded && in.tiles > 0 && (sx_mode != 2 || mode == 3)) {
+      const uint32_t hdr3 =
+          ((uint32_t)(kFlagValid | (mode == 3 ? kFlagActorIds : 0)) << 16) | (uint32_t)a.method_uniform;
 #define PT_SX_OS(MO, SV)                                                                                         \
   hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_, ticket_, \
                      b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm, (unsigned long long*)meta, stats_, \
-                     rcnt_ + i * kSxMaxRanks, reserve)
+                     rcnt_ + i * kSxMaxRanks, reserve, reject_ordered)
 #define PT_SX_OS_S(MO)              \
   switch (S) {                      \
     case 1: PT_SX_OS(MO, 1); break; \
@@ -1165,7 +1200,9 @@ void SortedExchange::send(const SxSend& a) {
     case 6: PT_SX_OS(MO, 6); break; \
     default: PT_SX_OS(MO, 8); break; \
   }
-      if (mode == 2) {
+      if (mode == 3) {
+        PT_SX_OS_S(3)
+      } else if (mode == 2) {
         PT_SX_OS_S(2)
       } else if (mode == 1) {
         PT_SX_OS_S(1)
@@ -1190,7 +1227,8 @@ void SortedExchange::send(const SxSend& a) {
 #undef PT_SX_MODE
 #define PT_SX_SCAT(MO, SV)                                                                                       \
   hipLaunchKernelGGL((sx_scatter_kernel<MO, SV>), dim3(in.G), dim3(kST), 0, cs, in, R_, K, (const uint32_t*)hist_, \
-                     (const uint32_t*)boff_, b.send, rq, (uint32_t)C, caps_out, L, b.perm, (unsigned long long*)meta)
+                     (const uint32_t*)boff_, b.send, rq, (uint32_t)C, caps_out, L, b.perm, (unsigned long long*)meta, \
+                     reject_ordered)
 #define PT_SX_SCAT_S(MO)            \
   switch (S) {                      \
     case 1: PT_SX_SCAT(MO, 1); break; \
@@ -1226,6 +1264,13 @@ void SortedExchange::send(const SxSend& a) {
                                 hipMemcpyDeviceToHost, cur_comm_));
     PT_HIP_CHECK(hipEventRecord(ev_meta_[cur], cur_comm_));
     meta_send_[cur] = sends_;
+    // a device-side comm (IpcComm) can fail inside the agreement too: joined back
+    // into the caller's stream, every op of this Send (and its failure word) is
+    // behind the caller's next sync, and no wait kernel of it outlives the engine
+    if (fake_ && fake_->device_side() && cur_comm_ != cs) {
+      PT_HIP_CHECK(hipEventRecord(ev_join_, cur_comm_));
+      PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_join_, 0));
+    }
   } else {
     meta_send_[cur] = -1;
   }
@@ -1236,7 +1281,7 @@ void SortedExchange::send(const SxSend& a) {
     if (m > 0)
       launch_complete_packed((uintptr_t)bufs_[i].back, C, R_, L.vb, (uintptr_t)bufs_[i].perm, m,
                              a.out_val + (uintptr_t)(lo * 8), a.out_st + (uintptr_t)(lo * 4), 0, false,
-                             (uintptr_t)cs);
+                             (uintptr_t)cs, fake_ ? (uintptr_t)fake_->device_failed() : 0);
   }
   ++sends_;
 }

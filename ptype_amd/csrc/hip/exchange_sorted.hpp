@@ -75,6 +75,7 @@ struct SxSend {
   uintptr_t table = 0;
   uint64_t cap = 0;
   uintptr_t dir = 0;
+  uintptr_t dir_rank = 0;  // the directory's rank byte table (stateless batches: rank-only gathers)
   uint32_t n_dir = 0, affine_w = 0;
   uintptr_t out_val = 0, out_st = 0, state = 0;
   uint32_t n_state = 0;
@@ -95,6 +96,8 @@ struct SxWire {
   uint32_t cap_out[kSxMaxRanks] = {};  // this rank's capacity per destination
   uint32_t cap_in[kSxMaxRanks] = {};   // per source
   bool agreed = false;      // L and C came from an agreement (else the start-up wide layout)
+  bool shard_ok = true;     // sharded (ordered) regions may be sent this Send (else ordered messages overflow)
+  int route_mode = 0;       // sender resolution: 0 hash, 1 directory, 2 affine, 3 rank byte table
   int64_t spec_from = -1;   // the Send whose agreement they came from
   uint64_t meta[kMetaWords] = {};
 };
@@ -151,6 +154,7 @@ class SortedExchange {
   uint64_t* meta_host_ = nullptr;  // [2][kSxMetaWords] pinned copies
   unsigned long long* stats_ = nullptr;  // [2] receiver counters
   hipEvent_t ev_meta_[2]{};
+  hipEvent_t ev_join_{};  // device-side comms: the comm stream joined back into the caller's
   int64_t meta_send_[2] = {-1, -1};  // the Send whose agreement each buffer holds
   hipEvent_t ev_routed_[kSxMaxChunks]{}, ev_req_in_[kSxMaxChunks]{}, ev_served_[kSxMaxChunks]{},
       ev_rep_in_[kSxMaxChunks]{};

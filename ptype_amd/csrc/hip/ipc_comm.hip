@@ -161,8 +161,14 @@ IpcComm::IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s
   PT_HIP_CHECK(hipDeviceSynchronize());
 }
 
-IpcComm::~IpcComm() {  // no synchronisation: a wait on a dead peer ends at its timeout, not here
+IpcComm::~IpcComm() {
   (void)hipSetDevice(device_);
+  // the last op on every stream this comm used: its kernels read the segments
+  // unregistered below.  Bounded -- a wait on a dead peer ends at the timeout.
+  for (auto& se : last_op_) {
+    (void)hipEventSynchronize(se.second);
+    (void)hipEventDestroy(se.second);
+  }
   for (size_t q = 0; q < segs_.size(); ++q)
     if (registered_[q]) (void)hipHostUnregister(segs_[q]->base());
   (void)hipFree(segs_dev_);
@@ -233,6 +239,15 @@ void IpcComm::op(const void* src, size_t src_stride, void* dst, size_t dst_strid
                      (uint8_t*)dst, (uint64_t)dst_stride, recv, segs_dev_, rank_, R_, (uint64_t)cap_, seq,
                      ctr_ + kIpcMaxRanks, reduce_dst, reduce_n);
   PT_HIP_CHECK(hipGetLastError());
+  hipEvent_t* ev = nullptr;
+  for (auto& se : last_op_)
+    if (se.first == s) ev = &se.second;
+  if (!ev) {
+    last_op_.emplace_back(s, nullptr);
+    ev = &last_op_.back().second;
+    PT_HIP_CHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  }
+  PT_HIP_CHECK(hipEventRecord(*ev, s));
 }
 
 void IpcComm::alltoall(int r, const void* src, void* dst, size_t bytes, hipStream_t s) {

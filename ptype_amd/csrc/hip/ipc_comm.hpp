@@ -83,6 +83,7 @@ class IpcComm : public HostComm {
                  hipStream_t s) override;
   void allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) override;
   void check() const override;
+  const uint64_t* device_failed() const override { return dev_failed_; }
 
   bool failed() const;           // a wait of this rank timed out (pinned host flag; no sync)
   uint64_t ops() const { return seq_; }
@@ -105,6 +106,7 @@ class IpcComm : public HostComm {
   uint64_t* host_failed_ = nullptr;        // pinned: set by a timed-out wait
   uint64_t* dev_failed_ = nullptr;         // its device address
   uint64_t seq_ = 0;                       // ops issued
+  std::vector<std::pair<hipStream_t, hipEvent_t>> last_op_;  // per stream used: an event after its last op
   bool connected_ = false;
 };
 

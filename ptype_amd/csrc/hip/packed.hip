@@ -276,10 +276,15 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
                                                               const int32_t* __restrict__ perm, int64_t M,
                                                               int64_t* __restrict__ out_val,
                                                               int32_t* __restrict__ out_st,
-                                                              unsigned long long* __restrict__ checksum, bool direct) {
+                                                              unsigned long long* __restrict__ checksum, bool direct,
+                                                              const uint64_t* __restrict__ failed) {
   // each source region's value plane starts past its count-sized ok bitmap: the
   // offsets once per block in LDS, not a dependent header load per message
   __shared__ uint32_t voff[kMaxRanks];
+  // a failed collective (IpcComm: a peer missed it) wrote no reply regions: every
+  // message that went through one answers kStatusNotDelivered (direct completion
+  // included -- its own-slot dispatch saw an empty region)
+  const bool lost = failed && __hip_atomic_load(failed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
   // (the count clamped to the region: a region no peer wrote this time -- a failed
   // collective -- holds whatever the buffer held, and must not move the plane out)
   for (int d = threadIdx.x; d < R; d += blockDim.x)
@@ -318,6 +323,11 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
     for (int u = 0; u < kCompU; ++u) {
       const int64_t i = i0 + u * stride;
       if (p[u] == kPastBatch) continue;
+      if (lost && (p[u] >= 0 || p[u] == -3)) {
+        out_val[i] = 0;
+        out_st[i] = kStatusNotDelivered;
+        continue;
+      }
       if (direct && p[u] < 0) {
         if (checksum) sum += (unsigned long long)out_val[i];
         continue;
@@ -474,7 +484,7 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
 }
 
 void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
-                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream) {
+                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed) {
   if (M <= 0) return;
   if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
   if (R < 1 || R > kMaxRanks) throw std::invalid_argument("complete: 1 <= R <= 64");
@@ -484,7 +494,7 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t p
   hipLaunchKernelGGL(complete_packed_kernel<U>, dim3(grid_for(M, 256 * (U), checksum ? 1024 : 8192)), dim3(256), 0, \
                      as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R, vb,          \
                      (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum,   \
-                     direct)
+                     direct, (const uint64_t*)failed)
   if (comp_u == 8) PT_COMP(8);
   else if (comp_u == 2) PT_COMP(2);
   else PT_COMP(4);

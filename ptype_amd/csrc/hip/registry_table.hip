@@ -250,8 +250,8 @@ __global__ __launch_bounds__(256) void table_pack_kernel(const TableEntry* __res
 // every id present and no violation, the data path can compute route words
 // arithmetically -- no directory gathers at all (`astats` = {present, violations}).
 __global__ __launch_bounds__(256) void table_build_dir_kernel(const TableEntry* __restrict__ t, uint64_t cap,
-                                                              uint32_t* __restrict__ dir, uint64_t n_dir,
-                                                              uint32_t affine_w,
+                                                              uint32_t* __restrict__ dir, uint8_t* __restrict__ dirr,
+                                                              uint64_t n_dir, uint32_t affine_w,
                                                               unsigned long long* __restrict__ astats) {
   unsigned long long present = 0, bad = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -259,6 +259,7 @@ __global__ __launch_bounds__(256) void table_build_dir_kernel(const TableEntry* 
     const uint64_t key = ((uint64_t)v.y << 32) | v.x;
     if (key == kKeyEmpty || key == kKeyTomb || key > n_dir) continue;  // actor_key(id) = id + 1
     dir[key - 1] = (v.z < 0xfeu && v.w < (1u << 24)) ? (v.z | (v.w << 8)) : kDirFallback;
+    if (dirr) dirr[key - 1] = v.z < kRankFallback ? (uint8_t)v.z : kRankFallback;
     if (affine_w) {
       const uint64_t id = key - 1;
       ++present;
@@ -340,12 +341,13 @@ void launch_table_sweep(uintptr_t table, uint64_t cap, uintptr_t exp_tbl, uint64
 }
 
 void launch_table_build_dir(uintptr_t table, uint64_t cap, uintptr_t dir, uint64_t n_dir, uint32_t affine_w,
-                            uintptr_t astats, uintptr_t stream) {
+                            uintptr_t astats, uintptr_t stream, uintptr_t dir_rank) {
   hipStream_t s = as_stream(stream);
   PT_HIP_CHECK(hipMemsetAsync((void*)dir, 0xff, n_dir * sizeof(uint32_t), s));
+  if (dir_rank) PT_HIP_CHECK(hipMemsetAsync((void*)dir_rank, kRankMissing, n_dir, s));
   if (affine_w) PT_HIP_CHECK(hipMemsetAsync((void*)astats, 0, 2 * sizeof(unsigned long long), s));
   hipLaunchKernelGGL(table_build_dir_kernel, dim3(grid_for((int64_t)cap)), dim3(256), 0, s, (const TableEntry*)table,
-                     cap, (uint32_t*)dir, n_dir, affine_w, (unsigned long long*)astats);
+                     cap, (uint32_t*)dir, (uint8_t*)dir_rank, n_dir, affine_w, (unsigned long long*)astats);
   PT_HIP_CHECK(hipGetLastError());
 }
 

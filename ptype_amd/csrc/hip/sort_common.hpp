@@ -42,6 +42,7 @@ struct SortIn {  // by value
   const TableEntry* table;
   uint64_t mask;
   const uint32_t* dir;
+  const uint8_t* dirr;  // MODE 3: the directory's rank byte table (one byte per id: 4x fewer lines than dir)
   uint32_t n_dir;
   uint32_t aw;
   int aw_shift;
@@ -65,10 +66,27 @@ __device__ __forceinline__ uint32_t virt_block(uint32_t b, uint32_t G) {
   return (G >= 8 && (G & 7) == 0) ? (b & 7) * (G >> 3) + (b >> 3) : b;
 }
 
+// Route modes: 0 hash probe, 1 directory gather (rank, mailbox), 2 affine rule
+// (computed), 3 rank byte gather -- stateless batches only: `mb` is then the
+// actor id itself (the receiver's stateless handler needs no mailbox), except for
+// ids the byte table sends to the hash table, which keep the probed mailbox.
 template <int MODE>
 __device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[kSK], int (&r)[kSK],
                                           uint32_t (&mb)[kSK]) {
-  if constexpr (MODE == 1) {
+  if constexpr (MODE == 3) {
+    uint32_t w[kSK];
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) w[k] = a[k] < in.n_dir ? (uint32_t)in.dirr[a[k]] : (uint32_t)kRankFallback;
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      r[k] = w[k] == kRankMissing ? -1 : (int)w[k];
+      mb[k] = a[k];
+      if (w[k] == kRankFallback) {
+        if (a[k] != 0xffffffffu) lookup_entry(in.table, in.mask, actor_key(a[k]), r[k], mb[k]);
+        else r[k] = -1;
+      }
+    }
+  } else if constexpr (MODE == 1) {
     uint32_t w[kSK];
 #pragma unroll
     for (int k = 0; k < kSK; ++k) w[k] = a[k] < in.n_dir ? dir_load(in.dir + a[k], in.dir_nt) : kDirFallback;

@@ -77,6 +77,7 @@ class RegistryTable:
         self.expiry = torch.zeros(self.cap, dtype=torch.int64, device=self.device)
         self.stats = torch.zeros(8, dtype=torch.int64, device=self.device)
         self.dir = None  # route directory (K5b), GPU only; see enable_directory
+        self.dir_rank = None  # its rank byte table (K5c): one byte per id, built with it
         self.dir_n = 0
         self.affine_world = 0  # strided-rule candidate W (0: no check)
         self.affine = 0  # W when the last build verified the rule for every id of the range
@@ -101,6 +102,9 @@ class RegistryTable:
             raise ValueError("directory range too large")
         self.dir_n = int(n_ids)
         self.dir = torch.empty(self.dir_n, dtype=torch.int32, device=self.device)
+        # the rank byte of every id (0xff: not registered, 0xfe: probe the table):
+        # what a stateless batch's sender needs, at a quarter of the directory's lines
+        self.dir_rank = torch.empty(self.dir_n, dtype=torch.uint8, device=self.device)
         self.affine_world = int(affine_world)
         self._astats = torch.zeros(2, dtype=torch.int64, device=self.device) if affine_world else None
         self._dir_dirty = True
@@ -111,7 +115,7 @@ class RegistryTable:
             return None, 0, 0
         if self._dir_dirty:
             hip().table_build_dir(_ptr(self.table), self.cap, _ptr(self.dir), self.dir_n, self.affine_world,
-                                  _ptr(self._astats), _stream(self.table))
+                                  _ptr(self._astats), _stream(self.table), _ptr(self.dir_rank))
             self.affine = 0
             if self.affine_world:
                 present, bad = (int(x) for x in self._astats.tolist())  # one sync per rebuild

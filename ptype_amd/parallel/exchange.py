@@ -142,9 +142,10 @@ class ActorExchange:
         else:
             self.rank, self.world = 0, 1
         # comm="ipc": the native engines' collectives go through an IpcComm
-        # (csrc/hip/ipc_comm.hpp) -- one rank per process, peers' HBM imported by IPC
-        # handle -- over a group of any backend (gloo is enough: it only carries the
-        # handles and the host agreements).  It runs the multi-process pipeline where
+        # (csrc/hip/ipc_comm.hpp) -- one rank per process, every rank's receive segment
+        # a POSIX shared-memory file that all ranks map and register with HIP -- over a
+        # group of any backend (gloo is enough: it only carries the segment names and
+        # the host agreements).  It runs the multi-process pipeline where
         # RCCL cannot: several ranks on one GPU.  Built below, once the geometry is agreed.
         self.ipc = None
         self.comm_kind = comm if fake is None and self.world > 1 else "rccl"
@@ -324,7 +325,7 @@ class ActorExchange:
             fake = self.fake[0] if self.fake is not None else self.ipc
             self._sorted = h.SortedExchange(dev, 0 if fake is not None else self._comm_ptr(), self.world, self.rank,
                                             self.max_chunk, self.chunks, c_alloc, min(self.C, c_alloc), fake=fake)
-            self._sorted_c_alloc = c_alloc
+            self._sorted_c_alloc_val = c_alloc
         return self._sorted
 
     def _send_sorted(self, req: B.MsgBatch, out_val, out_status):
@@ -338,13 +339,14 @@ class ActorExchange:
         eng.send(B._ptr(req.actor), B._ptr(req.a0), B._ptr(req.a1), B._ptr(req.a2), B._ptr(mcol),
                  int(req.method) if uniform else 0, req.M, B._ptr(self.table.table), self.table.cap, B._ptr(d), n_dir,
                  affine, B._ptr(out_val), B._ptr(out_status), B._ptr(state), 0 if state is None else state.numel(),
-                 int(self.delay_us) * 100, self.mailbox_ordered, raw_stream(self.device))
+                 int(self.delay_us) * 100, self.mailbox_ordered, raw_stream(self.device),
+                 B._ptr(self.table.dir_rank) if d is not None else 0)
         w = eng.last_wire()
         # words moved per chunk, all peers (as the epoch engine reports it): padded
         # regions, or the per-pair prefixes when the agreed capacities differ
         w["req_words"] = w["req_moved"]
         w["rep_words"] = w["rep_moved"]
-        w.update(engine="sorted", exact=False, adapted=bool(w["agreed"]), C_alloc=self._sorted_c_alloc)
+        w.update(engine="sorted", exact=False, adapted=bool(w["agreed"]), C_alloc=self._sorted_c_alloc_val)
         self.last_wire = w
         self.counters.wire_bytes += self.chunks * 4 * (w["req_words"] + w["rep_words"])
         return out_val, out_status

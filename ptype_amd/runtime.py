@@ -117,8 +117,8 @@ class DeviceRuntime:
         self._watchdog = None
         self.mailbox_shards, self.mailbox_slots = int(mailbox_shards), int(mailbox_slots)
         self.delivery = delivery or "auto"  # "mailbox": every Send through the HBM mailboxes (ActorExchange)
-        # N > 1 collectives: the group's RCCL communicator, or IpcComm ("ipc": peers' HBM by
-        # IPC handle over a gloo group -- several ranks may share one GPU)
+        # N > 1 collectives: the group's RCCL communicator, or IpcComm ("ipc": shared-memory
+        # segments every rank maps, over a gloo group -- several ranks may share one GPU)
         self.comm, self.comm_timeout_s = comm or "rccl", float(comm_timeout_s)
         self._exchange = None
         self.shards: dict[str, list[dict]] = {}

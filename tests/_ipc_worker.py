@@ -19,7 +19,8 @@ import torch.distributed as dist  # noqa: E402
 
 from ptype_amd.ops import batch as B  # noqa: E402
 from ptype_amd.ops import hip  # noqa: E402
-from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, METHOD_SEQ_FOLD, STATUS_OK  # noqa: E402
+from ptype_amd.ops.records import (METHOD_CALC_MULTIPLY, METHOD_SEQ_FOLD, STATUS_NOT_DELIVERED,  # noqa: E402
+                                   STATUS_OK)
 from ptype_amd.ops.table import RegistryTable, actor_keys  # noqa: E402
 from ptype_amd.parallel.exchange import ActorExchange, ipc_group_comm  # noqa: E402
 
@@ -178,15 +179,19 @@ def kill(rank, R):
         os.kill(os.getpid(), signal.SIGKILL)
     t0 = time.time()
     req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=99, device=DEV)
-    ex.send(req)  # enqueues; its waits end at the timeout on the device
+    v, sts = ex.send(req)  # enqueues; its waits end at the timeout on the device
     torch.cuda.synchronize()
     waited = time.time() - t0
     assert ex.ipc.failed, "the dead peer's collective was not detected"
+    # no false successes: every message of the failed Send answers NotDelivered
+    # (the completion reads the comm's failure word in stream order)
+    counts = {int(k): int(c) for k, c in zip(*torch.unique(sts.cpu(), return_counts=True))}
+    assert STATUS_OK not in counts and counts.get(STATUS_NOT_DELIVERED, 0) >= M * 0.99, counts
     try:
         ex.send(req)
     except RuntimeError as e:
         assert "IpcComm: peer" in str(e) and is_rank_failure(e), str(e)
-        return {"raised": str(e)[:120], "waited_s": round(waited, 2)}
+        return {"raised": str(e)[:120], "waited_s": round(waited, 2), "statuses": counts}
     raise AssertionError("the Send after a peer's death did not raise")
 
 

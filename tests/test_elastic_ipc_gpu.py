@@ -2,8 +2,8 @@
 
 Three processes on one GPU, each ``Join`` with a ``gpu:`` section (``world: 3``,
 ``comm: ipc``): Join forms the group through the replicated store (gloo for the
-host side), the sorted exchange's collectives run through IpcComm (peers' HBM by
-IPC handle).  One node dies without cleanup after the first round; the
+host side), the sorted exchange's collectives run through IpcComm (shared-memory
+segments that every rank maps and registers with HIP, csrc/hip/ipc_comm.hpp).  One node dies without cleanup after the first round; the
 survivors' ``Client.Send`` sees the dead peer at the comm's timeout, aborts the
 generation, waits for the lease-driven membership, forms generation 1 through
 the store and re-homes the dead rank's actors from the buddy replica --
