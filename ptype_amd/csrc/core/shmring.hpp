@@ -14,6 +14,7 @@
 //
 // Layout: [ShmHeader, 16 KB][ServerCtrl, 4 KB][RingSlot x ring][ReplySlot x ring][u64 owner x ring]
 //         [RingTaker x kRingTakers] (ringproto.hpp: who holds which sequence numbers)
+//         [XLane x kXLanes][XReply x kXLanes] (GPU peer lanes and their reply slots)
 //
 // Request ring placement: by default the ring the dispatcher
 // polls is NOT the segment's RingSlot area but fine-grained memory on the
@@ -22,8 +23,7 @@
 // maps it with plain mmap -- no HIP in the client -- and writes requests through
 // the BAR, so the polling wave's tag and payload reads stay in HBM instead of
 // crossing PCIe twice per call.  Replies, the owner words and the control block
-// stay in host memory (the client polls them).  GPU peers can import the same
-// ring with the hipIpcMemHandle in the header.  PTYPE_XPROC_RING=host keeps the
+// stay in host memory (the client polls them).  PTYPE_XPROC_RING=host keeps the
 // ring in the segment (either side).
 #pragma once
 #include <atomic>
@@ -37,26 +37,32 @@
 
 namespace ptype {
 
-constexpr uint64_t kShmMagic = 0x34736d6570797470ull;  // "ptypems4" (GPU peer lanes)
+constexpr uint64_t kShmMagic = 0x35736d6570797470ull;  // "ptypems5" (GPU peer lanes in the segment)
 constexpr int kShmMaxMethods = 32;
 
 // GPU peer lanes: a GPU in ANOTHER process calls this
 // server's actors without any host on the path.  The server keeps kXLanes
-// single-producer lanes in fine-grained HBM (XLane, exported by IPC handle in
-// the header); a calling process registers one (XLaneReg: its process token and
-// the IPC handle of a 16-B reply slot in ITS OWN HBM), the server imports that
-// slot, and from then on the caller's kernel writes a request into the lane over
-// xGMI and spins on its local reply slot, which the persistent dispatcher fills
-// with one 16-B store.  A lane carries one call at a time (the caller waits for
-// each reply), so it needs no sequence taking, owners or rescue: seq + 1 in
-// req_tag publishes, `served` acknowledges.
+// single-producer lanes (XLane) and their 16-B reply slots (XReply) in THIS
+// segment -- host shared memory that the server and every calling process map
+// and register with HIP, so each GPU reaches them through its own process's
+// mapping.  A calling process registers one lane (XLaneReg: its process token);
+// from then on the caller's kernel writes a request into the lane and spins on
+// the lane's reply slot, which the persistent dispatcher fills with one 16-B
+// store.  A lane carries one call at a time (the caller waits for each reply),
+// so it needs no sequence taking, owners or rescue: seq + 1 in req_tag
+// publishes, `served` acknowledges.
+//
+// Crash safety: no process ever touches memory another process
+// owns.  Round 4's lanes lived in the server's HBM and the reply slots in the
+// caller's (both imported by IPC handle), and an import of a killed process's
+// HBM faults the GPU of the survivor (profiles/r4_ipc_kill_faults.md).  Pages
+// of a shared segment stay mapped for as long as any survivor maps them, so a
+// dead server costs its callers a timeout (kStatusNotDelivered) and a dead
+// caller costs the server nothing: its lane is reclaimed once quiet.
 constexpr int kXLanes = 64;
-// Lane life cycle: Free -> (caller) Requested -> (server: reply slot imported) Ready
-// -> (caller) Releasing -> (server: no request in flight, import closed) Free.
-// The caller frees its reply slot only once it reads Free again, and the server
-// closes its import only once the lane is quiet (served == req_tag: the
-// dispatcher wave has stored its last reply), so neither side unmaps memory the
-// other may still write.  A dead caller's lane takes the same server-side path.
+// Lane life cycle: Free -> (caller) Requested -> (server: lane reset) Ready ->
+// (caller) Releasing -> (server: no request in flight, lane reset) Free.  A dead
+// caller's lane takes the same server-side path; the caller may register again.
 enum XLaneState : uint32_t {
   kXLaneFree = 0,
   kXLaneRequested = 1,
@@ -68,18 +74,22 @@ struct XLaneReg {
   std::atomic<uint64_t> token;  // the caller's process token (ring_self_token); 0: free
   std::atomic<uint32_t> state;
   int32_t device;               // the caller's HIP device ordinal (diagnostics)
-  uint8_t reply_ipc[64];        // hipIpcMemHandle_t of the caller's reply slot allocation
   uint64_t pad[2];
 };
-struct alignas(128) XLane {  // server HBM; one per wave lane of the dispatcher
+struct alignas(128) XLane {  // in the segment; one per wave lane of the dispatcher
   uint64_t req_tag;  // caller: seq + 1 once the request below is out (release)
   uint64_t served;   // dispatcher: req_tag of the last request answered
   uint64_t w0;       // actor | method << 32 | flags << 48 (MsgRecord word 0)
   int64_t a0, a1, a2;
-  uint64_t rep_ptr;  // server-side address of the caller's reply slot {value, reply_tag}
-  uint64_t pad[9];
+  uint64_t pad[10];
 };
 static_assert(sizeof(XLane) == 128, "XLane layout");
+struct alignas(64) XReply {  // in the segment: lane i's reply {value, reply_tag(seq, status)}
+  uint64_t value;
+  uint64_t tag;
+  uint64_t pad[6];
+};
+static_assert(sizeof(XReply) == 64, "XReply layout");
 
 struct ShmMethod {
   char name[96];  // "Service.Method"
@@ -102,10 +112,7 @@ struct alignas(64) ShmHeader {
   uint64_t req_dev_off;   // offset of the ring in the dma-buf
   uint64_t req_dev_bytes;
   char req_sock[64];      // abstract unix socket handing out the dma-buf fd
-  uint8_t ipc_handle[64]; // hipIpcMemHandle_t of the ring (GPU peers)
-  uint32_t ipc_valid, pad2;
-  // GPU peer lanes
-  uint8_t xl_ipc[64];     // hipIpcMemHandle_t of the XLane array
+  // GPU peer lanes (the XLane / XReply areas of the segment)
   uint32_t xl_valid, xl_lanes;
   XLaneReg xregs[kXLanes];
 };
@@ -114,9 +121,13 @@ static_assert(std::atomic<uint64_t>::is_always_lock_free, "process-shared atomic
 
 constexpr size_t kShmHeaderBytes = 16384, kShmCtrlBytes = 4096;
 
+inline size_t shm_lanes_offset(uint32_t ring) {  // 128-B aligned
+  const size_t o = kShmHeaderBytes + kShmCtrlBytes + (size_t)ring * (sizeof(RingSlot) + sizeof(ReplySlot) + sizeof(uint64_t)) +
+                   (size_t)kRingTakers * sizeof(RingTaker);
+  return (o + 127) & ~(size_t)127;
+}
 inline size_t shm_bytes(uint32_t ring) {
-  return kShmHeaderBytes + kShmCtrlBytes + (size_t)ring * (sizeof(RingSlot) + sizeof(ReplySlot) + sizeof(uint64_t)) +
-         (size_t)kRingTakers * sizeof(RingTaker);
+  return shm_lanes_offset(ring) + (size_t)kXLanes * (sizeof(XLane) + sizeof(XReply));
 }
 
 struct ShmView {
@@ -126,6 +137,8 @@ struct ShmView {
   ReplySlot* rep = nullptr;
   std::atomic<uint64_t>* owner = nullptr;
   RingTaker* takers = nullptr;
+  XLane* xl = nullptr;     // GPU peer lanes
+  XReply* xrep = nullptr;  // their reply slots
   bool bar = false;  // `req` is device memory written through a BAR mapping
 };
 
@@ -138,6 +151,8 @@ inline ShmView shm_view(void* base, uint32_t ring) {
   v.rep = reinterpret_cast<ReplySlot*>(reinterpret_cast<char*>(v.req) + (size_t)ring * sizeof(RingSlot));
   v.owner = reinterpret_cast<std::atomic<uint64_t>*>(reinterpret_cast<char*>(v.rep) + (size_t)ring * sizeof(ReplySlot));
   v.takers = reinterpret_cast<RingTaker*>(reinterpret_cast<char*>(v.owner) + (size_t)ring * sizeof(uint64_t));
+  v.xl = reinterpret_cast<XLane*>(p + shm_lanes_offset(ring));
+  v.xrep = reinterpret_cast<XReply*>(reinterpret_cast<char*>(v.xl) + (size_t)kXLanes * sizeof(XLane));
   return v;
 }
 

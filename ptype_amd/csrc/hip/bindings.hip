@@ -530,7 +530,8 @@ PYBIND11_MODULE(_hip, m) {
            }),
            py::arg("shm_name"), py::arg("device"), py::arg("n_lanes") = 8, py::arg("timeout_s") = 1.0)
       .def_property_readonly("table", &PeerRelay::table)
-      .def_property_readonly("lanes", &PeerRelay::lanes);
+      .def_property_readonly("lanes", &PeerRelay::lanes)
+      .def("slots", &PeerRelay::slots, "per lane [seq, suspect] as the device table holds them");
   py::class_<DeviceServer>(m, "DeviceServer")
       .def(py::init<int, uint32_t, uintptr_t, uint32_t, uint64_t, double, double, const std::string&>(),
            py::arg("device"), py::arg("ring") = 4096, py::arg("state") = 0, py::arg("n_state") = 0,

@@ -126,12 +126,13 @@ struct PollConfig {
   uint32_t sleep = 1;
 };
 
-// GPU peer lanes (shmring.hpp XLane): lane l of the wave serves XLane l.  A
-// request is pending when req_tag == served + 1; the reply goes straight into
-// the caller's HBM (rep_ptr, imported by the server) as one 16-B store, then
+// GPU peer lanes (shmring.hpp XLane, in the segment): lane l of the wave serves
+// XLane l.  A request is pending when req_tag == served + 1; the reply goes into
+// the lane's reply slot (XReply l, also in the segment) as one 16-B store, then
 // `served` acknowledges.  Returns the number of lanes served (wave-uniform).
-__device__ __forceinline__ unsigned serve_xlanes(XLane* __restrict__ xl, uint32_t nx, int64_t* __restrict__ state,
-                                                 uint32_t n_state, uint64_t delay_ticks) {
+__device__ __forceinline__ unsigned serve_xlanes(XLane* __restrict__ xl, XReply* __restrict__ xrep, uint32_t nx,
+                                                 int64_t* __restrict__ state, uint32_t n_state,
+                                                 uint64_t delay_ticks) {
   const unsigned lane = lane_id();
   bool ready = false;
   uint64_t t = 0;
@@ -152,24 +153,24 @@ __device__ __forceinline__ unsigned serve_xlanes(XLane* __restrict__ xl, uint32_
     msg.a1 = (int64_t)sys_ld(reinterpret_cast<const uint64_t*>(&L->a1));
     msg.a2 = (int64_t)sys_ld(reinterpret_cast<const uint64_t*>(&L->a2));
     const ReplyRecord r = run_handler(msg, state, n_state, delay_ticks);
-    uint64_t* out = reinterpret_cast<uint64_t*>(sys_ld(&L->rep_ptr));
-    if (out) sys_st16(out, (uint64_t)r.value, reply_tag(t - 1, (uint32_t)r.status));
+    sys_st16(reinterpret_cast<uint64_t*>(&xrep[lane]), (uint64_t)r.value, reply_tag(t - 1, (uint32_t)r.status));
     __threadfence_system();
     sys_st(&L->served, t);
   }
   return (unsigned)__popcll(m);
 }
 
-// Relay table (kMethodRelay): one GPU peer lane per relay slot -- the peer
-// server's lane (imported), this process's reply slot (fine-grained HBM) and the
-// lane's next sequence, kept here on the device (the dispatcher wave owns it).
-// Built by PeerRelay (xcall.hpp); a slot whose call timed out is retired
-// (lane = null: later relays on it answer kStatusNotDelivered).
+// Relay table (kMethodRelay): one GPU peer lane of ANOTHER server per relay slot
+// -- its lane and reply slot in that server's segment (mapped and registered by
+// this process), the lane's next sequence and whether a timed-out call on it is
+// still unanswered.  Built by PeerRelay (xcall.hpp).  While the dispatcher wave
+// runs, slot l's words live in lane l's registers (RelayRegs); they are written
+// back when the wave parks or the table is replaced.
 struct RelayLane {
   XLane* lane;
-  uint64_t* reply;
-  uint64_t seq;
-  uint64_t pad;
+  XReply* reply;
+  uint64_t seq;      // the sequence of the lane's next call
+  uint64_t suspect;  // 1: call `seq` timed out -- the slot is reused once its late reply lands
 };
 constexpr int kRelayMax = 64;
 struct RelayTable {
@@ -179,58 +180,146 @@ struct RelayTable {
   uint64_t timeout_ticks;
 };
 
-// The dispatcher lanes holding kMethodRelay requests (`mine`) forward them: lane
-// l uses relay slot l % n, one round per group of n lanes (a slot carries one
-// call at a time); each call is a peer-lane publish into the other server's
-// HBM and a spin on the local reply slot (bounded by the table's timeout).
-__device__ __forceinline__ void relay_calls(RelayTable* __restrict__ rt, bool mine, const MsgRecord& msg,
-                                            ReplyRecord& r) {
+// Asynchronous relays: the wave never waits on a peer.  A relayed
+// request takes a free slot, is published into the peer's lane, and parks there
+// (pend = its ring sequence + 1) while the wave goes on serving its ring, its own
+// peer lanes and other relays; every trip polls the parked slots' reply words,
+// and a reply (or the slot's deadline) completes the ring request it belongs to.
+// A timed-out call fails that call only: the slot is suspect until the late reply
+// lands (then free again), never retired.  A peer that died leaves its slots
+// suspect -- their memory is this process's mapping of the peer's segment, so
+// nothing faults.
+struct RelayRegs {
+  uint64_t seq = 0, pend = 0, deadline = 0;
+  XLane* x = nullptr;
+  XReply* rp = nullptr;
+  bool suspect = false;
+};
+// slot words through memory-side atomics: the wave may be relaunched on another
+// XCD, whose L2 could hold a line of the table from an earlier run
+__device__ __forceinline__ uint64_t relay_ld(uint64_t* p) {
+  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void relay_st(uint64_t* p, uint64_t v) {
+  (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ RelayRegs relay_load(RelayTable* rt) {
+  RelayRegs g;
   const unsigned lane = lane_id();
-  const uint32_t n = rt->n;
-  if (n == 0) {
-    if (mine) r.status = kStatusNoMethod;
-    return;
-  }
-  for (uint32_t round = 0; round * n < (uint32_t)kWave; ++round) {
-    if (!mine || lane / n != round) continue;
-    RelayLane* L = &rt->lanes[lane % n];
-    // the slot's words through memory-side atomics: the wave may be relaunched on
-    // another XCD, whose L2 could hold a line of the table from an earlier run
-    auto slot_ld = [](uint64_t* p) { return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto slot_st = [](uint64_t* p, uint64_t v) {
-      (void)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    uint64_t* lane_word = reinterpret_cast<uint64_t*>(&L->lane);
-    XLane* x = reinterpret_cast<XLane*>(slot_ld(lane_word));
-    r.value = 0;
-    r.status = kStatusNotDelivered;
-    if (!x) continue;
-    const uint64_t seq = slot_ld(&L->seq);
-    const uint64_t w0 = (uint64_t)msg.actor | ((uint64_t)(uint16_t)msg.a0 << 32) | ((uint64_t)kFlagValid << 48);
-    sys_st(&x->w0, w0);
-    sys_st(reinterpret_cast<uint64_t*>(&x->a0), (uint64_t)msg.a1);
-    sys_st(reinterpret_cast<uint64_t*>(&x->a1), (uint64_t)msg.a2);
-    sys_st(reinterpret_cast<uint64_t*>(&x->a2), 0ull);
-    __threadfence_system();
-    sys_st(&x->req_tag, seq + 1);
-    const uint64_t t0 = realtime_ticks();
-    for (;;) {
-      const uint64_t tag = sys_ld(L->reply + 1);
-      if (reply_tag_is(tag, seq)) {
-        const int64_t v = (int64_t)sys_ld(L->reply);
-        if (sys_ld(L->reply + 1) != tag) continue;  // the value belongs to this tag only if it still carries it
-        r.value = v;
-        r.status = (int32_t)(tag & 0xff);
-        slot_st(&L->seq, seq + 1);
-        break;
+  if (!rt || lane >= (unsigned)relay_ld(reinterpret_cast<uint64_t*>(&rt->n)) % 0x100000000ull) return g;
+  RelayLane* L = &rt->lanes[lane];
+  g.x = reinterpret_cast<XLane*>(relay_ld(reinterpret_cast<uint64_t*>(&L->lane)));
+  g.rp = reinterpret_cast<XReply*>(relay_ld(reinterpret_cast<uint64_t*>(&L->reply)));
+  g.seq = relay_ld(&L->seq);
+  g.suspect = relay_ld(&L->suspect) != 0;
+  return g;
+}
+__device__ __forceinline__ void relay_store(RelayTable* rt, const RelayRegs& g) {
+  if (!rt || !g.x) return;
+  RelayLane* L = &rt->lanes[lane_id()];
+  relay_st(&L->seq, g.seq);
+  relay_st(&L->suspect, g.suspect ? 1ull : 0ull);
+}
+
+// Complete parked relays whose reply landed or whose deadline passed (their ring
+// replies written here); clear suspect slots whose late reply landed.  Returns
+// the number of ring requests completed (wave-uniform).
+__device__ __forceinline__ unsigned relay_poll(RelayRegs& g, ReplySlot* __restrict__ rep, uint64_t ring_mask,
+                                               uint64_t now) {
+  bool fin = false;
+  if (g.pend || g.suspect) {
+    const uint64_t tag = sys_ld(&g.rp->tag);
+    bool got = reply_tag_is(tag, g.seq);
+    int64_t v = 0;
+    if (got) {
+      v = (int64_t)sys_ld(&g.rp->value);
+      got = sys_ld(&g.rp->tag) == tag;  // the value belongs to this tag only if it still carries it
+    }
+    if (g.pend) {
+      const uint64_t seq = g.pend - 1;
+      if (got) {
+        sys_st16(reinterpret_cast<uint64_t*>(&rep[seq & ring_mask]), (uint64_t)v,
+                 reply_tag(seq, (uint32_t)(tag & 0xff)));
+        g.seq += 1;
+        g.pend = 0;
+        fin = true;
+      } else if (now > g.deadline) {
+        sys_st16(reinterpret_cast<uint64_t*>(&rep[seq & ring_mask]), 0ull, reply_tag(seq, kStatusNotDelivered));
+        g.suspect = true;  // the peer may still answer call g.seq
+        g.pend = 0;
+        fin = true;
       }
-      if (realtime_ticks() - t0 > rt->timeout_ticks) {
-        slot_st(lane_word, 0ull);  // out of step with the peer: retired
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+    } else if (got) {  // a suspect slot's late reply: the lane is in step again
+      g.seq += 1;
+      g.suspect = false;
     }
   }
+  return (unsigned)__popcll(__ballot(fin));
+}
+
+// Relayed ring requests wait for a slot in a FIFO in device memory (one entry of
+// 5 words per ring slot: every entry is a ring request not yet answered, so the
+// ring's size bounds it), so the ring head never stops behind a relay: requests
+// after it are served at once (other callers unaffected).  The
+// queue is empty whenever the wave parks (a queued relay is work in flight).
+struct RelayQueue {
+  uint64_t* q = nullptr;  // [ring][5]: ring seq, w0..w3
+  uint64_t mask = 0;      // ring - 1
+  uint64_t head = 0, tail = 0;  // wave-uniform
+};
+__device__ __forceinline__ uint64_t q_ld(const uint64_t* p) {  // another lane's store: past the L1
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Queue this trip's relayed requests (lanes < n flagged in `relayed_mask`, ring
+// sequence head + lane), then let every free slot take the next queued request
+// in order and publish it into its peer lane.  With no slot parked and requests
+// still queued, no slot can free (every one is suspect: the peer stopped
+// answering), so the queued requests fail at once (kStatusNotDelivered) -- a dead
+// peer never holds them until their callers' timeouts.  Returns the ring
+// requests failed here (wave-uniform).
+__device__ __forceinline__ unsigned relay_dispatch(RelayRegs& g, RelayQueue& rq, uint64_t relayed_mask,
+                                                   uint64_t head, uint64_t w0, uint64_t w1, uint64_t w2,
+                                                   uint64_t w3, uint64_t timeout_ticks, uint64_t now,
+                                                   ReplySlot* __restrict__ rep, uint64_t ring_mask) {
+  const unsigned lane = lane_id();
+  const uint64_t below = (1ull << lane) - 1;
+  if (relayed_mask) {
+    if ((relayed_mask >> lane) & 1) {
+      uint64_t* e = rq.q + ((rq.tail + (uint64_t)__popcll(relayed_mask & below)) & rq.mask) * 5;
+      e[0] = head + lane, e[1] = w0, e[2] = w1, e[3] = w2, e[4] = w3;
+    }
+    rq.tail += (uint64_t)__popcll(relayed_mask);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the entries before any lane reads them
+  }
+  const uint64_t avail = rq.tail - rq.head;
+  if (!avail) return 0;
+  const uint64_t free_mask = __ballot(g.x != nullptr && !g.pend && !g.suspect);
+  const uint64_t q = (uint64_t)__popcll(free_mask & below);
+  if (((free_mask >> lane) & 1) && q < avail) {
+    const uint64_t* e = rq.q + ((rq.head + q) & rq.mask) * 5;
+    const uint64_t seq = q_ld(e), s0 = q_ld(e + 1), s1 = q_ld(e + 2), s2 = q_ld(e + 3), s3 = q_ld(e + 4);
+    // request: actor = the remote actor, a0 = the remote method, a1 / a2 = its arguments
+    const uint64_t rw0 = (s0 & 0xffffffffull) | ((uint64_t)(uint16_t)s1 << 32) | ((uint64_t)kFlagValid << 48);
+    sys_st(&g.x->w0, rw0);
+    sys_st(reinterpret_cast<uint64_t*>(&g.x->a0), s2);
+    sys_st(reinterpret_cast<uint64_t*>(&g.x->a1), s3);
+    sys_st(reinterpret_cast<uint64_t*>(&g.x->a2), 0ull);
+    __threadfence_system();
+    sys_st(&g.x->req_tag, g.seq + 1);
+    g.pend = seq + 1;
+    g.deadline = now + timeout_ticks;
+  }
+  const uint64_t took = min((uint64_t)__popcll(free_mask), avail);
+  rq.head += took;
+  if (rq.tail == rq.head || __ballot(g.pend != 0)) return 0;
+  const uint64_t left = rq.tail - rq.head;  // nothing parked, nothing can free: fail the rest
+  for (uint64_t i = lane; i < left; i += kWave) {
+    const uint64_t seq = q_ld(rq.q + ((rq.head + i) & rq.mask) * 5);
+    sys_st16(reinterpret_cast<uint64_t*>(&rep[seq & ring_mask]), 0ull, reply_tag(seq, kStatusNotDelivered));
+  }
+  rq.head = rq.tail;
+  return (unsigned)left;
 }
 
 __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __restrict__ req,
@@ -239,7 +328,8 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
                                                                  int64_t* __restrict__ state, uint32_t n_state,
                                                                  uint64_t delay_ticks, uint64_t idle_ticks,
                                                                  uint64_t max_ticks, PollConfig poll,
-                                                                 XLane* __restrict__ xl, uint32_t nx) {
+                                                                 XLane* __restrict__ xl, XReply* __restrict__ xrep,
+                                                                 uint32_t nx, uint64_t* __restrict__ relay_q) {
   const unsigned lane = lane_id();
   const uint64_t t_start = realtime_ticks();
   uint64_t last_work = t_start;
@@ -251,11 +341,26 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
   unsigned idle_polls = 0, iters = 0;
   // GPU peer lanes are polled only while some are registered (re-read on the idle path)
   uint32_t nxl = xl ? (uint32_t)min<uint64_t>(sys_ld(&ctrl->xl_n), (uint64_t)nx) : 0u;
-  RelayTable* relay = reinterpret_cast<RelayTable*>(sys_ld(&ctrl->relay));  // (re-read on the idle path)
+  // relay slots: lane l holds slot l (re-read on the idle path while none is parked)
+  RelayTable* relay = reinterpret_cast<RelayTable*>(sys_ld(&ctrl->relay));
+  RelayRegs rg = relay_load(relay);
+  uint64_t relay_timeout = relay ? relay_ld(&relay->timeout_ticks) : 0;
+  bool parked_any = __ballot(rg.suspect) != 0;  // wave-uniform: a relay is parked or a slot is suspect
+  RelayQueue rq;
+  rq.q = relay_q;
+  rq.mask = ring_mask;
   for (;;) {
     // every poll is a PCIe round trip to host memory: the stop flag is read on
     // one poll in 16, not before every ring poll (that made a poll two trips)
-    if ((++iters & 15) == 0 && sys_ld(&ctrl->stop)) break;
+    if ((++iters & 15) == 0 && sys_ld(&ctrl->stop) && !__ballot(rg.pend != 0) && rq.tail == rq.head) break;
+    if (parked_any) {  // parked relays first: their replies may be waiting, and their slots the queue
+      const uint64_t now = realtime_ticks();
+      unsigned done = relay_poll(rg, rep, ring_mask, now);
+      if (rq.tail != rq.head) done += relay_dispatch(rg, rq, 0, 0, 0, 0, 0, 0, relay_timeout, now, rep, ring_mask);
+      processed += done;
+      if (done) last_work = realtime_ticks();
+      parked_any = __ballot(rg.pend != 0 || rg.suspect) != 0 || rq.tail != rq.head;
+    }
     const uint64_t seq = head + lane;
     RingSlot* s = &req[seq & ring_mask];
     // Every poll is PCIe reads of host memory.  With `poll.full` the head slot is
@@ -268,9 +373,9 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
     if (spec) w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3), cs = sys_ld(&s->csum);
     const bool ready = tag == seq + 1 && (!spec || cs == ring_csum(seq, w0, w1, w2, w3));
     const uint64_t m = __ballot(ready);
-    const unsigned n = (m == ~0ull) ? 64u : (unsigned)__builtin_ctzll(~m);
-    if (nxl) {  // GPU peer lanes: local HBM loads, no PCIe trip
-      const unsigned nxs = serve_xlanes(xl, nxl, state, n_state, delay_ticks);
+    unsigned n = (m == ~0ull) ? 64u : (unsigned)__builtin_ctzll(~m);
+    if (nxl) {  // GPU peer lanes (the segment's host memory)
+      const unsigned nxs = serve_xlanes(xl, xrep, nxl, state, n_state, delay_ticks);
       if (nxs) {
         processed += nxs;
         last_work = realtime_ticks();
@@ -283,7 +388,14 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
           trace_mask = sys_ld(&ctrl->trace_mask);
           trace = reinterpret_cast<TraceRec*>(sys_ld(&ctrl->trace_ring));
           if (xl) nxl = (uint32_t)min<uint64_t>(sys_ld(&ctrl->xl_n), (uint64_t)nx);
-          relay = reinterpret_cast<RelayTable*>(sys_ld(&ctrl->relay));
+          RelayTable* r2 = reinterpret_cast<RelayTable*>(sys_ld(&ctrl->relay));
+          if (r2 != relay && !__ballot(rg.pend != 0) && rq.tail == rq.head) {  // a new table: the old one keeps its slots' words
+            relay_store(relay, rg);
+            relay = r2;
+            rg = relay_load(relay);
+            relay_timeout = relay ? relay_ld(&relay->timeout_ticks) : 0;
+            parked_any = __ballot(rg.suspect) != 0;
+          }
         }
         if (lane == 0 && sys_ld(&ctrl->calib_req)) {  // clock calibration handshake
           sys_st(&ctrl->calib_ticks, realtime_ticks());
@@ -292,9 +404,16 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
         }
       }
       const uint64_t now = realtime_ticks();
-      const bool idle = idle_ticks && now - last_work > idle_ticks;
+      const bool parked = __ballot(rg.pend != 0) != 0 || rq.tail != rq.head;  // relays in flight: no exit
+      const bool idle = idle_ticks && now - last_work > idle_ticks && !parked;
       lifetime_exit = now - t_start > max_ticks;
       if (idle || lifetime_exit) {
+        for (uint64_t i = rq.head + lane; i < rq.tail; i += kWave) {  // (lifetime exit) queued relays fail now
+          const uint64_t qs = q_ld(rq.q + (i & rq.mask) * 5);
+          sys_st16(reinterpret_cast<uint64_t*>(&rep[qs & ring_mask]), 0ull, reply_tag(qs, kStatusNotDelivered));
+        }
+        rq.head = rq.tail;
+        relay_store(relay, rg);  // (a lifetime exit with parked relays: their callers time out)
         int resume = 0;
         if (lane == 0) {
           sys_st(&ctrl->resume_head, head);
@@ -332,10 +451,16 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
       continue;
     }
     const uint64_t t_seen = realtime_ticks();
-    if (lane < n) {
-      if (!spec) {  // ordered after this lane's tag read (it returned; the branch depends on it)
-        w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3);
-      }
+    if (lane < n && !spec) {  // ordered after this lane's tag read (it returned; the branch depends on it)
+      w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3);
+    }
+    const bool relayed = lane < n && (uint16_t)(w0 >> 32) == kMethodRelay && relay != nullptr;
+    const uint64_t rmask = __ballot(relayed);
+    if (rmask) {  // queued for a relay slot (the free ones publish now); the ring moves on
+      processed += relay_dispatch(rg, rq, rmask, head, w0, w1, w2, w3, relay_timeout, t_seen, rep, ring_mask);
+      parked_any = true;
+    }
+    if (lane < n && !relayed) {
       MsgRecord msg;
       msg.actor = (uint32_t)w0;
       msg.method = (uint16_t)(w0 >> 32);
@@ -343,10 +468,7 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
       msg.a0 = (int64_t)w1;
       msg.a1 = (int64_t)w2;
       msg.a2 = (int64_t)w3;
-      ReplyRecord r;
-      const bool relayed = msg.method == kMethodRelay && relay != nullptr;
-      if (!relayed) r = run_handler(msg, state, n_state, delay_ticks);
-      if (__ballot(relayed)) relay_calls(relay, relayed, msg, r);
+      const ReplyRecord r = run_handler(msg, state, n_state, delay_ticks);
       // value + tag in ONE 16-B store (one PCIe write that lands whole): the
       // host that sees the tag sees the value, so no fence and no second write
       ReplySlot* o = &rep[seq & ring_mask];
@@ -361,9 +483,10 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
       }
     }
     head += n;
-    processed += n;
+    processed += (uint64_t)__popcll(__ballot(lane < n && !relayed));
     last_work = realtime_ticks();
   }
+  relay_store(relay, rg);
   if (lane == 0) {
     sys_st(&ctrl->resume_head, head);
     __threadfence_system();
@@ -459,6 +582,7 @@ class DeviceServer {
     }
     for (uint32_t i = 0; i < ring_; ++i) owner_[i].store(i, std::memory_order_relaxed);
     stream_ = dedicated_stream(device_);  // the persistent dispatcher runs here
+    PT_HIP_CHECK(hipMalloc((void**)&relay_q_, (size_t)ring_ * 5 * sizeof(uint64_t)));  // relay FIFO (relay_dispatch)
     if (hdr_) {  // publish the segment only once fully initialised
       hdr_->ring = ring_;
       hdr_->owner_pid = (int32_t)getpid();
@@ -491,10 +615,8 @@ class DeviceServer {
     (void)hipSetDevice(device_);
     (void)hipStreamSynchronize(stream_);
     (void)hipStreamDestroy(stream_);
-    for (auto& p : xl_imports_)
-      if (p) (void)hipIpcCloseMemHandle(p);
-    xl_imports_.clear();
-    if (xl_) (void)hipFree(xl_);
+    (void)hipFree(relay_q_);
+    relay_q_ = nullptr;
     xl_ = nullptr;
     if (seg_) {
       handoff_.reset();  // no new client maps the ring (mapped ones keep the buffer alive)
@@ -663,8 +785,9 @@ class DeviceServer {
 
   // Cross-process request ring in device memory (shmring.hpp):
   // fine-grained HBM that this process writes through its BAR mapping, client
-  // processes through an mmap of its dma-buf (fd handed over a unix socket), and
-  // GPU peers through its IPC handle.  Any failure leaves the segment's ring.
+  // processes through an mmap of its dma-buf (fd handed over a unix socket).  (No
+  // IPC handle: an import of this process's HBM would fault its importer's GPU
+  // once this process died.)  Any failure leaves the segment's ring.
   void export_device_ring() {
     const size_t bytes = sizeof(RingSlot) * ring_;
     RingSlot* d = nullptr;
@@ -695,14 +818,6 @@ class DeviceServer {
     }
     PT_HIP_CHECK(hipMemset(d, 0, bytes));
     PT_HIP_CHECK(hipDeviceSynchronize());
-    hipIpcMemHandle_t ipc;
-    if (hipIpcGetMemHandle(&ipc, d) == hipSuccess) {
-      static_assert(sizeof(ipc) <= sizeof(hdr_->ipc_handle), "IPC handle size");
-      memcpy(hdr_->ipc_handle, &ipc, sizeof ipc);
-      hdr_->ipc_valid = 1;
-    } else {
-      (void)hipGetLastError();
-    }
     dmabuf_fd_ = fd;
     req_ = d;
     dreq_ = d;
@@ -729,38 +844,27 @@ class DeviceServer {
     }
   }
 
-  // ---- GPU peer lanes (shmring.hpp)
+  // ---- GPU peer lanes (shmring.hpp): the segment's XLane / XReply areas, which
+  // this process registered with HIP along with the rest of the segment
   void export_xlanes() {
     if (getenv("PTYPE_XLANES") && std::string(getenv("PTYPE_XLANES")) == "0") return;
-    const size_t bytes = sizeof(XLane) * kXLanes;
-    if (hipExtMallocWithFlags((void**)&xl_, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
-      (void)hipGetLastError();
-      xl_ = nullptr;
-      return;
-    }
-    hipIpcMemHandle_t h;
-    if (!open_to_cpu(xl_) || hipIpcGetMemHandle(&h, xl_) != hipSuccess) {
-      (void)hipGetLastError();
-      (void)hipFree(xl_);
-      xl_ = nullptr;
-      return;
-    }
-    PT_HIP_CHECK(hipMemset(xl_, 0, bytes));
-    PT_HIP_CHECK(hipDeviceSynchronize());
-    static_assert(sizeof(h) <= sizeof(hdr_->xl_ipc), "IPC handle size");
-    memcpy(hdr_->xl_ipc, &h, sizeof h);
+    const ShmView v = shm_view(seg_->base(), ring_);
+    hxl_ = v.xl;
+    hxrep_ = v.xrep;
+    const char* hbase = static_cast<const char*>(seg_->base());
+    char* dbase = nullptr;
+    PT_HIP_CHECK(hipHostGetDevicePointer((void**)&dbase, seg_->base(), 0));
+    xl_ = reinterpret_cast<XLane*>(dbase + (reinterpret_cast<const char*>(hxl_) - hbase));
+    xrep_ = reinterpret_cast<XReply*>(dbase + (reinterpret_cast<const char*>(hxrep_) - hbase));
     hdr_->xl_lanes = kXLanes;
     hdr_->xl_valid = 1;
-    xl_imports_.assign(kXLanes, nullptr);
   }
 
-  // Requested lanes: import the caller's reply slot, reset the lane, mark it
-  // ready.  Released lanes and lanes of dead callers are reclaimed -- but an
-  // import is closed only once the lane is quiet: the dispatcher wave
-  // may have loaded rep_ptr for a request it is still running (a handler delay),
-  // and its 16-B reply store into an unmapped slot would fault this process.  A
-  // lane with a request in flight is retried at the next waker pass (the wave
-  // finishes every request it took; `served` then equals `req_tag`).
+  // Requested lanes are reset and marked ready; released lanes and lanes of dead
+  // callers are reset and freed once quiet (served == req_tag: the wave has
+  // answered every request it took -- a reset under a request still running
+  // would let its late `served` store confuse the next holder).  A lane with a
+  // request in flight is retried at the next waker pass.
   void admit_xlanes() {
     uint32_t live = 0;
     for (int i = 0; i < kXLanes; ++i) {
@@ -769,73 +873,50 @@ class DeviceServer {
       const uint64_t tok = g.token.load(std::memory_order_acquire);
       const bool gone = st == kXLaneFree || st == kXLaneReleasing || !tok || !ring_token_alive(tok);
       if (gone) {
-        if (xl_imports_[i]) {  // let go of the caller's reply slot once nothing can write it
-          if (!xlane_quiet(i)) {
-            ++live;  // keep polling: the wave must finish (and the waker relaunch it for) the request
-            continue;
-          }
-          xlane_write(i, 0, 0);
-          (void)hipSetDevice(device_);
-          (void)hipIpcCloseMemHandle(xl_imports_[i]);
-          xl_imports_[i] = nullptr;
+        if (st == kXLaneFree) continue;
+        if (!xlane_quiet(i)) {
+          ++live;  // keep polling: the wave must finish (and the waker relaunch it for) the request
+          continue;
         }
-        if (st != kXLaneFree) {  // the slot is reusable only now (the caller frees its reply slot on Free)
-          uint64_t t = tok;
-          g.token.compare_exchange_strong(t, 0);
-          g.state.store(kXLaneFree, std::memory_order_release);
-        }
+        xlane_reset(i);
+        uint64_t t = tok;
+        g.token.compare_exchange_strong(t, 0);
+        g.state.store(kXLaneFree, std::memory_order_release);
         continue;
       }
       ++live;
       if (st != kXLaneRequested) continue;
-      if (xl_imports_[i] && !xlane_quiet(i)) continue;  // the previous holder's request is still running
-      void* p = nullptr;
-      hipIpcMemHandle_t h;
-      memcpy(&h, g.reply_ipc, sizeof h);
-      (void)hipSetDevice(device_);
-      if (xl_imports_[i]) {
-        xlane_write(i, 0, 0);
-        (void)hipIpcCloseMemHandle(xl_imports_[i]);
-        xl_imports_[i] = nullptr;
-      }
-      if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-        (void)hipGetLastError();
-        g.state.store(kXLaneFailed, std::memory_order_release);
-        continue;
-      }
-      xl_imports_[i] = p;
-      xlane_write(i, (uint64_t)(uintptr_t)p, 0);
+      if (!xlane_quiet(i)) continue;  // a previous holder's request is still running
+      xlane_reset(i);
       g.state.store(kXLaneReady, std::memory_order_release);
     }
     xl_live_ = live;
     uint64_t top = 0;  // lanes the wave polls: up to the highest registered one
-    for (int i = 0; i < kXLanes; ++i)
-      if (xl_imports_[i]) top = (uint64_t)i + 1;
+    for (int i = 0; i < kXLanes; ++i) {
+      const uint32_t st = hdr_->xregs[i].state.load(std::memory_order_acquire);
+      if (st == kXLaneReady || st == kXLaneReleasing || !xlane_quiet(i)) top = (uint64_t)i + 1;
+    }
     __atomic_store_n(&ctrl_->xl_n, top, __ATOMIC_SEQ_CST);
   }
 
   // No request of lane i in flight: the wave answered everything published there.
   bool xlane_quiet(int i) const {
-    const volatile XLane* L = &xl_[i];
-    const uint64_t t = L->req_tag;
-    return t == 0 || L->served == t;
+    const uint64_t t = __atomic_load_n(&hxl_[i].req_tag, __ATOMIC_ACQUIRE);
+    return t == 0 || __atomic_load_n(&hxl_[i].served, __ATOMIC_ACQUIRE) == t;
   }
 
-  // Reset lane i (through the BAR mapping): sequence restarts at 0.
-  void xlane_write(int i, uint64_t rep_ptr, uint64_t seq) {
-    volatile XLane* L = &xl_[i];
-    L->rep_ptr = rep_ptr;
-    L->served = seq;
-    L->req_tag = seq;
-    _mm_sfence();
-    (void)L->req_tag;  // non-posted read: the writes have landed
+  // Reset lane i and its reply slot (host memory): sequence restarts at 0.
+  void xlane_reset(int i) {
+    __atomic_store_n(&hxl_[i].served, 0ull, __ATOMIC_RELAXED);
+    __atomic_store_n(&hxl_[i].req_tag, 0ull, __ATOMIC_RELAXED);
+    __atomic_store_n(&hxrep_[i].value, 0ull, __ATOMIC_RELAXED);
+    __atomic_store_n(&hxrep_[i].tag, 0ull, __ATOMIC_RELEASE);
   }
 
   bool xlane_pending() const {
     for (int i = 0; i < kXLanes; ++i) {
-      const volatile XLane* L = &xl_[i];
-      const uint64_t t = L->req_tag;
-      if (t && t == L->served + 1) return true;
+      const uint64_t t = __atomic_load_n(&hxl_[i].req_tag, __ATOMIC_ACQUIRE);
+      if (t && t == __atomic_load_n(&hxl_[i].served, __ATOMIC_ACQUIRE) + 1) return true;
     }
     return false;
   }
@@ -855,7 +936,7 @@ class DeviceServer {
           (void)hipSetDevice(device_);
           hipLaunchKernelGGL(persistent_dispatch_kernel, dim3(1), dim3(64), 0, stream_, dreq_, drep_,
                              (uint64_t)(ring_ - 1), dctrl_, head, state_, n_state_, delay_ticks_, idle_ticks_,
-                             max_ticks_, poll_, xl_, xl_ ? (uint32_t)kXLanes : 0u);
+                             max_ticks_, poll_, xl_, xrep_, xl_ ? (uint32_t)kXLanes : 0u, relay_q_);
           PT_HIP_CHECK(hipGetLastError());
           launches_.fetch_add(1);
           return;
@@ -911,8 +992,11 @@ class DeviceServer {
   TraceRec* trace_ = nullptr;
   TraceRec* dtrace_ = nullptr;
   uint32_t trace_cap_ = 0;
-  XLane* xl_ = nullptr;               // GPU peer lanes (fine-grained HBM, IPC-exported)
-  std::vector<void*> xl_imports_;     // per lane: the caller's imported reply slot
+  uint64_t* relay_q_ = nullptr;       // relayed requests waiting for a relay slot (device FIFO)
+  XLane* xl_ = nullptr;               // GPU peer lanes (the segment's, device address)
+  XReply* xrep_ = nullptr;            // their reply slots (device address)
+  XLane* hxl_ = nullptr;              // the same two areas, host addresses
+  XReply* hxrep_ = nullptr;
   std::atomic<uint32_t> xl_live_{0};  // registered lanes (the waker polls while any)
 };
 

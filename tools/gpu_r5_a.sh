@@ -16,7 +16,8 @@ echo l8; tail -1 gpurun_out/${TAG}_l8.log
 timeout -k 10 200 python3 bench.py --loopback 8 --steps 20 --warmup 5 --rtt-calls 0 --no-secondary > gpurun_out/${TAG}_l8b.json 2>gpurun_out/${TAG}_l8b.err || exit 4
 echo l8b; cat gpurun_out/${TAG}_l8b.json
 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
-  tests/test_sorted_exchange_gpu.py tests/test_ipc_comm_gpu.py > gpurun_out/${TAG}_tests.log 2>&1 || exit 5
+  tests/test_sorted_exchange_gpu.py tests/test_ipc_comm_gpu.py tests/test_xcall_gpu.py tests/test_shm_rpc_gpu.py \
+  > gpurun_out/${TAG}_tests.log 2>&1 || exit 5
 tail -3 gpurun_out/${TAG}_tests.log
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_1m -o prof -- \
   python3 bench.py --msgs-per-gpu 1048576 --steps 8 --warmup 4 --rtt-calls 0 --no-secondary > gpurun_out/${TAG}_1m.log 2>&1 || exit 6
