@@ -51,6 +51,9 @@ def _parse():
     p.add_argument("--cpu", action="store_true", help="gloo/CPU dry run of the same pipeline (tests)")
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the step as a captured hipGraph (auto: single rank)")
+    p.add_argument("--pipeline", choices=["on", "off"], default="off",
+                   help="graph path: generate step j+1's batch on a forked stream while step j's Send runs "
+                        "(client-side double buffering, PipelinedSendGraph)")
     p.add_argument("--steps-per-graph", type=int, default=0,
                    help="whole steps per graph replay (the graph launch and the seed advance show per replay); "
                         "steps and warmup must be multiples.  0 = auto: the largest of 4, 2, 1 dividing both")
@@ -256,10 +259,13 @@ def main():
         # steps that do not fill a U-step replay run on a 1-step graph of the same
         # step, so exactly --warmup steps warm up and exactly --steps are timed
         # (round 4: 20 steps per replay measured 1-3 % above 4 at 8 Mi and 1 Mi, profiles/r4_mailbox_ab.md)
-        args.steps_per_graph = next((u for u in (20, 10, 5, 4, 2) if use_graph and args.steps % u == 0), 1)
+        even = args.pipeline == "on"
+        args.steps_per_graph = next((u for u in (20, 10, 5, 4, 2) if use_graph and args.steps % u == 0
+                                     and (u % 2 == 0 or not even)), 1)
     if args.steps_per_graph < 1 or (args.steps_per_graph > 1 and (
             not use_graph or args.steps % args.steps_per_graph)):
         raise SystemExit("--steps-per-graph: needs the graph path, and --steps a multiple of it")
+    pipelined = use_graph and args.pipeline == "on" and args.steps_per_graph % 2 == 0
     pre = []
     if pregen:  # 4 distinct batches per rank, generated before any timing
         for k in range(4):
@@ -278,7 +284,7 @@ def main():
     host_us_per_step = [None]
 
     def measure(table, steps, warmup, delivery=args.delivery, sharding=args.sharding, Mq=M,
-                method=METHOD_CALC_MULTIPLY):
+                method=METHOD_CALC_MULTIPLY, wide=False):
         """Warm up, then time `steps` Sends of `Mq` messages (barrier + synchronize
         on both sides, max over ranks); returns (seconds, exchange, graph used).
         Replies are verified after the warm-up and after the timed steps: every
@@ -289,7 +295,7 @@ def main():
                            mailbox_ordered=sharding == "actor", mailbox_shards=args.mailbox_shards,
                            mailbox_slots=args.mailbox_slots, comm="ipc" if ipc else "rccl")
         _LIVE_EXCHANGES.append(weakref.ref(ex))  # (weak: a finished measurement's buffers stay freeable)
-        if Mq == M and method == METHOD_CALC_MULTIPLY:
+        if Mq == M and method == METHOD_CALC_MULTIPLY and not wide:
             rq, v, t = req, val, st
         else:
             rq = B.MsgBatch(torch.empty(Mq, dtype=torch.int32, device=device),
@@ -299,14 +305,33 @@ def main():
             t = torch.empty(Mq, dtype=torch.int32, device=device)
         graph = graph1 = None
         U = args.steps_per_graph
-        if use_graph:
+        vt = [rq, v, t]  # the batch and replies the verification reads
+        if pipelined:
+            # two batches and two reply sets, alternately: step j + 1's batch is generated on a
+            # forked stream while step j's Send runs (PipelinedSendGraph)
+            from ptype_amd.parallel.exchange import PipelinedSendGraph
+
+            rq2 = B.MsgBatch(torch.empty_like(rq.actor), torch.empty_like(rq.a0), torch.empty_like(rq.a1), None, method)
+            v2, t2 = torch.empty_like(v), torch.empty_like(t)
+            seed_p = torch.tensor([rank * 0x9E3779B9 + 7 + j * 0x1000193 for j in range(U)], dtype=torch.int64,
+                                  device=device)
+
+            def gen(r_, j):  # step j of a replay draws from seed j; j == U: the next replay's step 0
+                if j == U:
+                    seed_p.add_(U * 0x1000193)
+                    j = 0
+                B.gen_requests(Mq, n_actors, method, wide=wide, device=device, out=r_, seed_tensor=seed_p[j:j + 1])
+
+            graph = PipelinedSendGraph(ex, [rq, rq2], [(v, t), (v2, t2)], gen, U)
+            vt = [rq2, v2, t2]
+        elif use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
             # seed from device memory and the graph advances it, so every replay is a new batch
             seed_t = torch.tensor([rank * 0x9E3779B9 + 7 + j * 0x1000193 for j in range(U + 1)], dtype=torch.int64,
                                   device=device)
 
             def prologue(j=0):  # step j of a replay draws from seed j; the last one advances them all
-                B.gen_requests(Mq, n_actors, method, device=device, out=rq, seed_tensor=seed_t[j:j + 1])
+                B.gen_requests(Mq, n_actors, method, wide=wide, device=device, out=rq, seed_tensor=seed_t[j:j + 1])
                 if j == U - 1:
                     seed_t[:U].add_(U * 0x1000193)
 
@@ -314,12 +339,28 @@ def main():
             if U > 1 and warmup % U:  # the warm-up steps a U-step replay cannot cover
 
                 def prologue1(j=0):
-                    B.gen_requests(Mq, n_actors, method, device=device, out=rq, seed_tensor=seed_t[U:U + 1])
+                    B.gen_requests(Mq, n_actors, method, wide=wide, device=device, out=rq, seed_tensor=seed_t[U:U + 1])
                     seed_t[U:U + 1].add_(0x1000193)
 
                 graph1 = ex.capture(rq, v, t, prologue=prologue1, allow_collectives=args.graph == "on", repeat=1)
 
         def step(s_):
+            if pipelined:
+                if s_ < warmup - warmup % U:  # warm-up: whole replays, then eager steps
+                    if s_ % U == 0:
+                        graph.prime()
+                        graph.replay()
+                elif s_ < warmup:
+                    B.gen_requests(Mq, n_actors, method, wide=wide, seed=(s_ * world + rank) * 0x1000193 + 7, device=device,
+                                   out=rq2)
+                    ex.send(rq2, v2, t2)
+                    if s_ == warmup - 1:
+                        graph.prime()  # the first timed step's batch (the pipeline's steady state)
+                elif (s_ - warmup) % U == 0:
+                    if warmup == 0 and s_ == 0:
+                        graph.prime()
+                    graph.replay()
+                return
             if graph is not None:
                 if s_ < warmup and graph1 is not None:  # warm-up: one step per replay
                     graph1.replay()
@@ -329,17 +370,17 @@ def main():
             if pre and Mq == M and method == METHOD_CALC_MULTIPLY:
                 ex.send_all(pre[s_ % len(pre)], out=(v, t))
                 return
-            B.gen_requests(Mq, n_actors, method, seed=(s_ * world + rank) * 0x1000193 + 7, device=device, out=rq)
+            B.gen_requests(Mq, n_actors, method, wide=wide, seed=(s_ * world + rank) * 0x1000193 + 7, device=device, out=rq)
             ex.send(rq, v, t)
 
         def last(k):
-            return pre[(k - 1) % len(pre)] if pre and Mq == M and method == METHOD_CALC_MULTIPLY else rq
+            return pre[(k - 1) % len(pre)] if pre and Mq == M and method == METHOD_CALC_MULTIPLY else vt[0]
 
         for s_ in range(warmup):
             step(s_)
         sync()
         if warmup:
-            verify("warmup", last(warmup), v, t, method)
+            verify("warmup", last(warmup), vt[1], vt[2], method)
         # re-send rounds are counted over the timed steps only: the first Sends of the
         # sorted exchange run at the static start-up capacity, before any agreement
         ex.warmup_resends, ex.counters.resends = ex.counters.resends, 0
@@ -360,15 +401,17 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = float(tt.item())
         if steps:
-            verify("timed", last(warmup + steps), v, t, method)
+            verify("timed", last(warmup + steps), vt[1], vt[2], method)
         return elapsed, ex, graph is not None
 
     def mailbox_info(ex_):
         mb = ex_.mailboxes
         if mb is None:
             return {}
-        return {"mailbox_shards": mb.shards, "mailbox_slots": mb.slots, "mailbox_ring_bytes": mb.bytes,
-                "mailbox_record_bytes": mb.last_record_bytes}
+        # mailbox_shards: the rings allocated; ring_view_shards: how the timed Sends used them (stateless
+        # batches: a coarser view of the same rings, every actor's messages still in one ring)
+        return {"mailbox_shards": mb.shards, "ring_view_shards": mb.last_view_shards, "mailbox_slots": mb.slots,
+                "mailbox_ring_bytes": mb.bytes, "mailbox_record_bytes": mb.last_record_bytes}
 
     table = build_table(args.placement)
     hang_s = os.environ.get("PTYPE_HANG_DIAG")
@@ -405,6 +448,8 @@ def main():
             # an ORDERED stateful method (SeqFold: state = state * K + a0, non-commutative):
             # every actor runs its messages one at a time in ring (= message) order
             runs.append(("ordered_seqfold", dict(delivery="mailbox", sharding="actor", method=METHOD_SEQ_FOLD)))
+            # full-range int64 arguments: no 8-B ring record holds them (16-B records)
+            runs.append(("wide_args", dict(delivery="mailbox", sharding="actor", wide=True)))
         if args.delivery != "direct":
             runs.append(("direct", dict(delivery="direct")))
         else:
@@ -419,6 +464,7 @@ def main():
                 secondaries[name]["sharding"] = kw.get("sharding", "actor")
                 secondaries[name]["method"] = "SeqFold (ordered)" if kw.get("method") == METHOD_SEQ_FOLD \
                     else "Calculator.Multiply"
+                secondaries[name]["args"] = "full-range int64" if kw.get("wide") else "A: 16-bit signed, B: 16-bit"
             del ex3
 
     # BASELINE configs 4 and 5 and the public API path, under the same clock (utils/benchmarks.py)
@@ -591,8 +637,11 @@ def main():
                 "chunks": chunks,
                 **wire_info(ex, req),
                 "client_batch": "SoA (actor u32, A i64, B i64)",
+                "args": "A: 16-bit signed, B: 16-bit (int64 columns; see secondaries.wide_args for full-range)",
                 "hip_graph": graphed,
                 "steps_per_graph": args.steps_per_graph if graphed else None,
+                # the next step's batch generated on a forked stream during this step's Send
+                "pipelined_generator": bool(pipelined),
                 # host time inside the timed step calls (this rank; a graph replay launches U steps)
                 "host_us_per_step": round(head_host_us, 2) if head_host_us is not None else None,
                 **({"load": f"zipf({args.zipf})" if args.zipf > 0 else "uniform", "pregenerated": True,

@@ -203,10 +203,22 @@ class Client:
 
     def Send(self, batch, **kw):
         """Batched submit of a ``MsgBatch`` to GPU actors of this service:
-        RCCL epoch exchange across ranks, device dispatch, replies in order."""
+        RCCL epoch exchange across ranks, device dispatch, replies in order.
+
+        Asynchronous like ``Go`` (cluster/rpc.go:69-105): it returns device tensors
+        ``(value, status)`` as soon as the Send is enqueued, with no host wait on
+        it.  With more than one rank, a message that overflowed its region (skewed
+        traffic beyond the agreed capacity) reads STATUS_OVERFLOW until its re-send
+        -- at most two Sends later, or at ``Flush()`` -- writes its reply into the
+        same tensors; keep ``batch`` unchanged until then."""
         if self._rt is None:
             raise RuntimeError("Client.Send needs the cluster's device runtime (Join with a gpu: section)")
         return self._rt.send(self.service, batch, router=self._replica_router(), **kw)
+
+    def Flush(self) -> None:
+        """Every earlier ``Send``'s replies final (pending re-sends run now)."""
+        if self._rt is not None:
+            self._rt.flush()
 
     def Tell(self, batch, **kw):
         """Batched fire-and-forget to GPU actors of this service; handlers may send
@@ -223,7 +235,7 @@ class Client:
     def ConnectionErrs(self) -> ErrChannel:
         return self._c.connection_errs()
 
-    call, go, send, tell, close = Call, Go, Send, Tell, Close
+    call, go, send, tell, close, flush = Call, Go, Send, Tell, Close, Flush
 
     @property
     def conns_updated(self) -> IntChannel:

@@ -63,6 +63,9 @@ __device__ __forceinline__ uint32_t mod_u64_u32(uint64_t h, uint32_t n, uint64_t
   return (uint32_t)r;
 }
 
+// WIDE: full-range int64 arguments (two more hashes per message) -- values no
+// narrow record holds, for the wide-argument figures (16-B ring records).
+template <bool WIDE>
 __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
                                                            int64_t* __restrict__ a1, int64_t M, uint32_t n_actors,
                                                            uint64_t seed, const uint64_t* __restrict__ seed_ptr,
@@ -71,8 +74,13 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = mix64(seed ^ (uint64_t)i * 0x9e3779b97f4a7c15ull);
     actor[i] = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
-    a0[i] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
-    a1[i] = (int64_t)((h >> 40) & 0xffff);
+    if constexpr (WIDE) {
+      a0[i] = (int64_t)mix64(h ^ 0xa0761d6478bd642full);
+      a1[i] = (int64_t)mix64(h ^ 0xe7037ed1a0b428dbull);
+    } else {
+      a0[i] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
+      a1[i] = (int64_t)((h >> 40) & 0xffff);
+    }
   }
 }
 
@@ -741,7 +749,7 @@ void launch_replica_route(uintptr_t in, uintptr_t out, int64_t M, const std::vec
 int replica_sel_max() { return kMaxReplicaSel; }
 
 void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M, uint32_t n_actors, uint64_t seed,
-                         uintptr_t seed_ptr, uintptr_t stream) {
+                         uintptr_t seed_ptr, uintptr_t stream, bool wide) {
   if (M <= 0) return;
   if (n_actors == 0) throw std::invalid_argument("n_actors must be > 0");
   static const int variant = [] {  // tuning knobs: PTYPE_GEN_DIV=1 plain `%`; PTYPE_GEN_BLOCKS grid cap
@@ -758,12 +766,16 @@ void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M,
   const uint64_t magic = variant == 1 ? 0ull : ~0ull / n_actors;
   // (vec4: 16-B stores need 16-B aligned columns -- torch's allocations are; slices may not be)
   const bool aligned = ((actor | a0 | a1) & 15u) == 0;
-  if (vec4 && aligned)
+  if (wide)
+    hipLaunchKernelGGL(gen_requests_kernel<true>, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
+                       (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr,
+                       magic);
+  else if (vec4 && aligned)
     hipLaunchKernelGGL(gen_requests_vec4_kernel, dim3(grid_cap(std::max<int64_t>(M / 4, 1), 256, cap_blocks)),
                        dim3(256), 0, as_stream(stream), (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors,
                        seed, (const uint64_t*)seed_ptr, magic);
   else
-    hipLaunchKernelGGL(gen_requests_kernel, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(gen_requests_kernel<false>, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
                        (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr,
                        magic);
   PT_HIP_CHECK(hipGetLastError());

@@ -54,7 +54,7 @@ void launch_table_upsert_packed(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintp
 void launch_table_lookup(uintptr_t, uint64_t, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t);
 void launch_table_sweep(uintptr_t, uint64_t, uintptr_t, uint64_t, uintptr_t, uintptr_t);
 void launch_table_pack(uintptr_t, uint64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t);
-void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t, uintptr_t);
+void launch_gen_requests(uintptr_t, uintptr_t, uintptr_t, int64_t, uint32_t, uint64_t, uintptr_t, uintptr_t, bool);
 void launch_replica_route(uintptr_t, uintptr_t, int64_t, const std::vector<int>&, uint64_t, uint32_t, uint32_t,
                           uintptr_t);
 int replica_sel_max();
@@ -163,7 +163,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gob_decode", &launch_gob_decode, py::arg("buf"), py::arg("offsets"), py::arg("M"), py::arg("type_id"),
         py::arg("cols"), py::arg("status"), py::arg("stream"));
   m.def("gen_requests", &launch_gen_requests, py::arg("actor"), py::arg("a0"), py::arg("a1"), py::arg("M"),
-        py::arg("n_actors"), py::arg("seed"), py::arg("seed_ptr"), py::arg("stream"));
+        py::arg("n_actors"), py::arg("seed"), py::arg("seed_ptr"), py::arg("stream"), py::arg("wide") = false);
   m.def("replica_route", &launch_replica_route, py::arg("actor_in"), py::arg("actor_out"), py::arg("M"),
         py::arg("ranks"), py::arg("seq0"), py::arg("world"), py::arg("n_logical"), py::arg("stream"));
   m.def("max_replica_sel", &replica_sel_max);
@@ -435,6 +435,21 @@ PYBIND11_MODULE(_hip, m) {
       .def_property("epoch_counter", &SortedExchange::epoch_counter, &SortedExchange::set_epoch_counter)
       .def("last_overflow", &SortedExchange::last_overflow, py::call_guard<py::gil_scoped_release>(),
            "messages the last Send answered STATUS_OVERFLOW, max over ranks (waits for its agreement copy)")
+      .def("overflow_of", &SortedExchange::overflow_of, py::arg("send"), py::call_guard<py::gil_scoped_release>(),
+           "the same count for Send `send` (valid until Send send + 2 is issued)")
+      .def("host_profile",
+           [](const SortedExchange& e) {
+             const auto p = e.host_profile();
+             py::dict d;
+             d["sends"] = p.sends;
+             d["total_ns"] = p.total_ns;
+             d["spec_wait_ns"] = p.spec_wait_ns;
+             d["overflow_waits"] = p.overflow_waits;
+             d["overflow_wait_ns"] = p.overflow_wait_ns;
+             return d;
+           },
+           "host time of send() calls; spec_wait_ns: waits for Send k - 2's agreement (backpressure); "
+           "overflow_waits: reads of a Send's overflow count (last_overflow / overflow_of)")
       .def_property_readonly("sends", &SortedExchange::sends);
   py::class_<Mailboxes>(m, "Mailboxes",
                         "HBM actor mailboxes: S shard rings of Q 32-B tagged records (K2 enqueue, K3 epoch drain, "
@@ -486,6 +501,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("slots", &Mailboxes::slots)
       .def_property_readonly("bytes", &Mailboxes::bytes)
       .def_property_readonly("last_record_bytes", &Mailboxes::last_record_bytes)
+      .def_property_readonly("last_view_shards", &Mailboxes::last_view_shards)
       .def_property_readonly("consumer_processed", &Mailboxes::consumer_processed)
       .def_property_readonly("launches", &Mailboxes::launches)
       .def_property_readonly("handle", [](Mailboxes& m) { return (uintptr_t)&m; },

@@ -3,6 +3,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 
 #include "exchange_sorted.hpp"
@@ -875,12 +876,22 @@ uint32_t SortedExchange::epoch_counter() const {
   return v;
 }
 
-uint64_t SortedExchange::last_overflow() const {
-  const int64_t k = sends_ - 1;
-  if (k < 0) return 0;
+static uint64_t sx_now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+uint64_t SortedExchange::last_overflow() const { return sends_ > 0 ? overflow_of(sends_ - 1) : 0; }
+
+uint64_t SortedExchange::overflow_of(int64_t k) const {
+  if (k < 0 || k >= sends_) return 0;
   const int j = (int)(k & 1);
-  if (meta_send_[j] != k) throw std::runtime_error("SortedExchange: the last Send recorded no agreement (captured)");
+  if (meta_send_[j] != k) throw std::runtime_error("SortedExchange: no agreement of that Send (captured, or reused)");
+  const uint64_t t0 = sx_now_ns();
   PT_HIP_CHECK(hipEventSynchronize(ev_meta_[j]));
+  prof_.overflow_waits += 1;
+  prof_.overflow_wait_ns += sx_now_ns() - t0;
   return meta_host_[j * kSxMetaWords + kMetaOverflow];
 }
 
@@ -940,7 +951,9 @@ void SortedExchange::pick_spec(hipStream_t cs) {
   if (want < 0) return;
   const int j = (int)(want & 1);
   if (meta_send_[j] != want) return;  // recorded under a graph capture: keep the layout in force
+  const uint64_t t0 = sx_now_ns();
   PT_HIP_CHECK(hipEventSynchronize(ev_meta_[j]));
+  prof_.spec_wait_ns += sx_now_ns() - t0;
   adopt(meta_host_ + j * kSxMetaWords, want);
 }
 
@@ -995,6 +1008,15 @@ void SortedExchange::allreduce_meta(uint64_t* dev, hipStream_t s) {
 }
 
 void SortedExchange::send(const SxSend& a) {
+  const uint64_t t_enter = sx_now_ns();
+  struct Tally {  // every return path counts the call
+    HostProfile& p;
+    uint64_t t0;
+    ~Tally() {
+      p.sends += 1;
+      p.total_ns += sx_now_ns() - t0;
+    }
+  } tally{prof_, t_enter};
   if (a.M < 0 || a.M > max_chunk_ * chunks_) throw std::invalid_argument("SortedExchange: batch exceeds max_batch");
   if (a.M > 0 && (!a.actor || !a.a0)) throw std::invalid_argument("SortedExchange: actor and a0 columns required");
   if (a.cap == 0 || (a.cap & (a.cap - 1))) throw std::invalid_argument("table capacity must be a power of two");

@@ -120,6 +120,17 @@ class SortedExchange {
   // rank must re-send).  Waits for that Send's agreement copy -- one host wait on
   // an event already queued, no collective of its own.
   uint64_t last_overflow() const;
+  // The same count for Send k (its agreement buffer is reused by Send k + 2: valid
+  // until then).  Send k's copy completes before Send k + 2 can even pick its
+  // layout, so a caller that resolves Send k just before Send k + 2 waits on
+  // nothing the pipeline would not wait on anyway.
+  uint64_t overflow_of(int64_t k) const;
+  // host time: every send() call, and the part of it spent waiting for an
+  // agreement (pick_spec: Send k - 2's; last_overflow / overflow_of: counted apart)
+  struct HostProfile {
+    uint64_t sends = 0, total_ns = 0, spec_wait_ns = 0, overflow_waits = 0, overflow_wait_ns = 0;
+  };
+  HostProfile host_profile() const { return prof_; }
   // the one-pass sort's epoch counter (tests: preset near the 2^24 tag wrap); synchronous
   void set_epoch_counter(uint32_t v);
   uint32_t epoch_counter() const;
@@ -174,6 +185,7 @@ class SortedExchange {
   bool pairs_ = false;
   int64_t sends_ = 0;
   SxWire wire_;
+  mutable HostProfile prof_;
 };
 
 // The layout of an agreement: packed_layout with a mailbox field one bit wider

@@ -198,6 +198,8 @@ class Mailboxes {
   uint64_t bytes() const { return bytes_; }
   // ring record bytes of the last sorted Send (8: 8-B records, 16: compact, 32: long records in use)
   int last_record_bytes() const { return last_rec_bytes_; }
+  // shards the last sorted Send's rings were viewed as (stateless batches: a coarser view, 8 by default)
+  uint32_t last_view_shards() const { return last_view_shards_; }
   uint64_t consumer_processed() const;
   uint64_t launches() const { return launches_; }
   const MboxView& view() const { return mv_; }
@@ -223,6 +225,7 @@ class Mailboxes {
   uint8_t* sort_stab_ = nullptr;    // LDS-table count: one byte per actor (shard, or not-here / probe)
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
   int last_rec_bytes_ = 0;
+  uint32_t last_view_shards_ = 0;
   uint32_t* sort_resv_ = nullptr;   // [S][kResvStride] one-pass run reservations (zero between Sends)
   // 8-B ring records: [0] the field widths in force (device; updated by each Send's
   // last block), per-tile field bit lengths, and a pinned mirror of [0] (bit 31: the

@@ -1618,6 +1618,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 
   if (a.arrival) {  // fixed positions: enqueue + drain, no count pass
     last_rec_bytes_ = (a.a2 || a.method_col) ? 32 : 16;
+    last_view_shards_ = S;
 #define PT_AENQ(MO)                                                                                        \
   do {                                                                                                     \
     if (a.a2 && a.method_col)                                                                              \
@@ -1667,6 +1668,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       Sv = (uint32_t)s_env;
     }
   }
+  last_view_shards_ = Sv;
   // the stateless drain: ring order (default) or message order (PTYPE_MBOX_DRAIN=msg: every slot index written)
   static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
   const bool all_sidx = msg_drain && !a.ordered;

@@ -99,17 +99,19 @@ class MsgBatch:
 
 
 def gen_requests(M: int, n_actors: int, method: int = METHOD_CALC_MULTIPLY, seed: int = 0, device="cuda",
-                 out: MsgBatch | None = None, seed_tensor: torch.Tensor | None = None) -> MsgBatch:
+                 out: MsgBatch | None = None, seed_tensor: torch.Tensor | None = None, wide: bool = False) -> MsgBatch:
     """Synthetic client load: M calls (A, B) to uniformly hashed actors in [0, n_actors).
-    ``seed_tensor`` (GPU int64[1]) is read by the kernel instead of ``seed``, so a
-    captured graph produces a fresh batch on every replay."""
+    A is a 16-bit signed and B a 16-bit unsigned value; ``wide``: both full-range
+    int64 (products wrap, as the handler's do).  ``seed_tensor`` (GPU int64[1]) is
+    read by the kernel instead of ``seed``, so a captured graph produces a fresh
+    batch on every replay."""
     device = torch.device(device)
     if out is None:
         out = MsgBatch(torch.empty(M, dtype=torch.int32, device=device), torch.empty(M, dtype=torch.int64, device=device),
                        torch.empty(M, dtype=torch.int64, device=device), None, method)
     if device.type == "cuda":
         hip().gen_requests(_ptr(out.actor), _ptr(out.a0), _ptr(out.a1), M, int(n_actors), int(seed) & (2**64 - 1),
-                           _ptr(seed_tensor), _stream(out.actor))
+                           _ptr(seed_tensor), _stream(out.actor), bool(wide))
         return out
     if seed_tensor is not None:
         seed = int(seed_tensor.reshape(-1)[0])
@@ -117,6 +119,11 @@ def gen_requests(M: int, n_actors: int, method: int = METHOD_CALC_MULTIPLY, seed
     with np.errstate(over="ignore"):
         h = mix64(np.uint64(seed & (2**64 - 1)) ^ (i * np.uint64(0x9E3779B97F4A7C15)))
     out.actor.copy_(torch.from_numpy((h % np.uint64(n_actors)).astype(np.int64)).to(torch.int32))
+    if wide:
+        with np.errstate(over="ignore"):
+            out.a0.copy_(torch.from_numpy(mix64(h ^ np.uint64(0xA0761D6478BD642F)).view(np.int64)))
+            out.a1.copy_(torch.from_numpy(mix64(h ^ np.uint64(0xE7037ED1A0B428DB)).view(np.int64)))
+        return out
     out.a0.copy_(torch.from_numpy(((h >> np.uint64(20)) & np.uint64(0xFFFF)).astype(np.int64) - 0x8000))
     out.a1.copy_(torch.from_numpy(((h >> np.uint64(40)) & np.uint64(0xFFFF)).astype(np.int64)))
     return out

@@ -65,6 +65,12 @@ class Mailboxes:
         return int(self._m.last_record_bytes)
 
     @property
+    def last_view_shards(self) -> int:
+        """Shards the last sorted Send viewed the rings as: the full count for ordered
+        batches, a coarser view (8 by default) for stateless ones."""
+        return int(self._m.last_view_shards)
+
+    @property
     def handle(self) -> int:
         """Address of the native object: the epoch engine delivers received records into it."""
         return int(self._m.handle)

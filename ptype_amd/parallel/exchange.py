@@ -42,6 +42,7 @@ schedule over ``torch.distributed`` and serves CPU/gloo groups, and
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 import threading
@@ -206,6 +207,7 @@ class ActorExchange:
         self._pump_graph = None  # (key, hipGraph of a group of device-pump epochs, its buffers)
         self.last_wire = None  # engine.last_wire() of the latest native send
         self._sorted = None  # _hip.SortedExchange: N > 1 mailbox delivery (csrc/hip/exchange_sorted.hpp)
+        self._deferred = collections.deque()  # send_all(defer=True): (Send index, batch, val, st, rounds)
         self._last_sorted = False  # whether the last send() ran on it
 
     def _agree_device(self) -> torch.device:
@@ -404,6 +406,8 @@ class ActorExchange:
         ``(value int64[M], status int32[M])`` in message order.  Collective:
         every rank of the group must call it (with its own, possibly empty, batch)
         the same number of times."""
+        if self._deferred:  # a deferred Send two Sends old: its agreement buffer is reused by this one
+            self._resolve_deferred(final=False)
         M = req.M
         if M > self.max_chunk * self.chunks:
             raise ValueError(f"batch of {M} exceeds max_batch {self.max_chunk * self.chunks}")
@@ -732,17 +736,54 @@ class ActorExchange:
         return epochs, delivered
 
     # ------------------------------------------------------------------
-    def send_all(self, req: B.MsgBatch, max_epochs: int = 16, out: tuple | None = None):
+    def send_all(self, req: B.MsgBatch, max_epochs: int = 16, out: tuple | None = None, defer: bool = False):
         """`send` + re-send of overflowed messages until every one is delivered.
         Reads the overflow count once per epoch (a host round trip); with adaptive
         slot capacity (native engine, wire v3) skewed traffic fits in the first
-        epoch and no re-send round runs."""
+        epoch and no re-send round runs.
+
+        ``defer`` (sorted exchange, N > 1): return without waiting
+        for this Send's overflow count.  The count arrives with the Send's own
+        agreement, which Send k + 2 waits for anyway to pick its layout, so Send k
+        is resolved right before Send k + 2 is issued (or by ``flush()``): when any
+        rank overflowed, every rank runs the re-send rounds then -- the same point
+        on every rank -- and writes the replies into Send k's output tensors.  Until
+        then a message that overflowed reads STATUS_OVERFLOW ("pending re-send"),
+        and the batch ``req`` must stay unchanged.  No host wait on the current
+        Send."""
         val, st = self.send(req, *(out or ()))
         if self._fits_for_sure():
             return val, st
+        if defer and self._last_sorted and out is None:
+            self._deferred.append((self._sorted.sends - 1, req, val, st, max_epochs))
+            return val, st
+        return self._resend_rounds(req, val, st, max_epochs, None)
+
+    def flush(self) -> None:
+        """Resolve every deferred Send (``send_all(defer=True)``): afterwards all
+        their outputs are final.  Collective (re-send rounds may run)."""
+        self._resolve_deferred(final=True)
+
+    def _resolve_deferred(self, final: bool) -> None:
+        # Send k is resolved just before Send k + 2 (its agreement buffer is reused
+        # then); `final`: all of them.  The order and the points are the same on every
+        # rank (every rank issues the same Sends), so the re-send rounds stay collective.
+        while self._deferred:
+            k, req, val, st, max_epochs = self._deferred[0]
+            if not final and k > self._sorted.sends - 2:
+                break
+            self._deferred.popleft()
+            n_over = int(self._sorted.overflow_of(k))
+            if n_over:
+                self._resend_rounds(req, val, st, max_epochs, n_over)
+
+    def _resend_rounds(self, req, val, st, max_epochs: int, n_first):
+        n_over = n_first
         for _ in range(max_epochs):
             over = st == STATUS_OVERFLOW
-            if self._last_sorted:
+            if n_over is not None:
+                pass  # (a deferred Send's count, already read)
+            elif self._last_sorted:
                 # the sorted exchange folds every rank's overflow count into its own
                 # agreement all-reduce: one wait on that copy, no count pass, no collective
                 n_over = int(self._sorted.last_overflow())
@@ -752,6 +793,7 @@ class ActorExchange:
                     n_over = self._agree_max(n_over)
             if n_over == 0:
                 break
+            n_over = None
             idx = torch.nonzero(over).flatten()
             self.counters.resends += 1
             v2, s2 = self.send(req.index_select(idx))
@@ -911,6 +953,72 @@ class SendGraph:
         finally:
             ex._capturing = prev
         self.replays = 0
+
+    def replay(self) -> None:
+        """One graph launch: ``repeat`` steps."""
+        self.graph.replay()
+        self.replays += 1
+        self.ex.counters.sent += self.M * self.repeat
+        self.ex.counters.epochs += self.ex.chunks * self.repeat
+
+
+class PipelinedSendGraph:
+    """``repeat`` steps per hipGraph replay with client-side double buffering: the
+    generation of step j + 1's batch runs on a forked stream while step j's Send
+    runs, so the client producing messages overlaps the system delivering them (a
+    producer that fills the next batch while the current one is in flight).
+
+    ``reqs`` / ``outs``: two request batches and two (value, status) output pairs,
+    used alternately (``repeat`` must be even, so every replay starts on
+    ``reqs[0]``).  ``gen(req, j)`` enqueues the generation of step j's batch into
+    ``req`` on the current stream; j runs 1 .. repeat, where j == repeat is the
+    NEXT replay's first batch -- so call ``prime()`` (the first batch, j = 0) once
+    before the first replay.  Step j's Send waits for its batch (event join) and
+    the generation into a buffer waits for the Send that last read it.  After a
+    replay, ``reqs[1]`` / ``outs[1]`` hold the last step's batch and replies."""
+
+    def __init__(self, ex: ActorExchange, reqs, outs, gen, repeat: int = 2):
+        if repeat < 2 or repeat % 2:
+            raise ValueError("PipelinedSendGraph: repeat must be even (>= 2)")
+        self.ex, self.reqs, self.outs, self.gen, self.repeat = ex, list(reqs), list(outs), gen, int(repeat)
+        self.M = self.reqs[0].M
+        dev = ex.device
+        self.side = torch.cuda.Stream(dev)
+
+        def body():
+            main = torch.cuda.current_stream(dev)
+            for j in range(self.repeat):
+                cur, nxt = j % 2, (j + 1) % 2
+                freed = torch.cuda.Event()
+                freed.record(main)  # Send j - 1 (the last reader of reqs[nxt]) is done here
+                self.side.wait_event(freed)
+                with torch.cuda.stream(self.side):
+                    gen(self.reqs[nxt], j + 1)
+                ready = torch.cuda.Event()
+                ready.record(self.side)
+                ex.send(self.reqs[cur], *self.outs[cur])
+                main.wait_event(ready)  # the next Send's batch is complete
+
+        ex.table.directory()  # build outside the capture if dirty
+        prev, ex._capturing = ex._capturing, True
+        try:
+            warm = torch.cuda.Stream(dev)
+            warm.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(warm):  # warm allocations / lazy state outside the graph
+                for k in range(2):
+                    gen(self.reqs[k], 0)
+                    ex.send(self.reqs[k], *self.outs[k])
+            torch.cuda.current_stream(dev).wait_stream(warm)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                body()
+        finally:
+            ex._capturing = prev
+        self.replays = 0
+
+    def prime(self) -> None:
+        """The first replay's first batch (eager, on the current stream)."""
+        self.gen(self.reqs[0], 0)
 
     def replay(self) -> None:
         """One graph launch: ``repeat`` steps."""

@@ -330,7 +330,9 @@ class DeviceRuntime:
         self.sync()
         if self.membership is None:
             ex = self.exchange
-            return ex.send_all(batch) if resend_overflow else ex.send(batch)
+            # more than one rank: no host wait on this Send (its overflow, if any, is
+            # re-sent just before Send + 2 or at flush(): ActorExchange.send_all)
+            return ex.send_all(batch, defer=self.world > 1) if resend_overflow else ex.send(batch)
         from .parallel.elastic import RankFailure, is_rank_failure
 
         lost_before: list[int] = []
@@ -382,6 +384,11 @@ class DeviceRuntime:
             st[todo] = out[1]
             return (val, st) + tuple(out[2:])
         raise AssertionError("unreachable")
+
+    def flush(self) -> None:
+        """Every earlier Send's replies final (deferred re-sends run now).  Collective."""
+        if getattr(self, "_exchange", None) is not None:
+            self._exchange.flush()
 
     # ------------------------------------------------------------------ rank failures (SURVEY 5.3)
     def replicate(self) -> None:

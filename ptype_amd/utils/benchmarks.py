@@ -108,41 +108,54 @@ def registry_1m(device, n: int = 1 << 20, reps: int = 5) -> dict:
 # ---------------------------------------------------------------------------- config 4
 def optimus_fanout(table, n_actors: int, device, steps: int, warmup: int, rank: int = 0, world: int = 1,
                    targets: int = 1024, base: int = 80_001, chunks: int = 1, comm: str = "rccl", barrier=None,
-                   max_over_ranks=None) -> dict:
-    """``targets`` odd numbers per rank from ``base`` (distinct per rank), every
+                   max_over_ranks=None, sets: int = 3) -> dict:
+    """``targets`` odd numbers per rank and set (distinct per rank and set), every
     one split into 10-wide ranges and answered by the Prime.Check actors of the
-    whole node; the answers are checked against trial division on a sample."""
+    whole node; the answers are checked against trial division on a sample.
+    Steps cycle over ``sets`` distinct batches (~230 MB each at the defaults):
+    more than the 256 MB MALL, so no step reads a batch the cache still holds."""
     from ..models.optimus import FanOut
     from ..ops.records import STATUS_OK
     from ..parallel.exchange import ActorExchange
 
-    tg = torch.arange(targets, dtype=torch.int64) * 2 + base + rank * 2 * targets
-    f = FanOut(tg, n_actors, device)
-    ex = ActorExchange(table, f.M, chunks=chunks, delivery="mailbox", mailbox_ordered=False, comm=comm)
-    val = torch.empty(f.M, dtype=torch.int64, device=device)
-    st = torch.empty(f.M, dtype=torch.int32, device=device)
+    fs = []
+    for j in range(sets):
+        tg = torch.arange(targets, dtype=torch.int64) * 2 + base + (rank + j * world) * 2 * targets
+        fs.append((tg, FanOut(tg, n_actors, device)))
+    Mx = max(f.M for _, f in fs)
+    ex = ActorExchange(table, Mx, chunks=chunks, delivery="mailbox", mailbox_ordered=False, comm=comm)
+    val = torch.empty(Mx, dtype=torch.int64, device=device)
+    st = torch.empty(Mx, dtype=torch.int32, device=device)
+    k = [0]
 
     def step():
-        ex.send(f.batch, val, st)
-        f.gather(val, st)
+        f = fs[k[0] % sets][1]
+        k[0] += 1
+        ex.send(f.batch, val[:f.M], st[:f.M])
+        f.gather(val[:f.M], st[:f.M])
 
-    step()
-    _sync(device)
-    if not bool((f.status == STATUS_OK).all()):
-        raise RuntimeError("optimus fan-out: a range failed")
-    for j in range(0, targets, max(1, targets // 32)):
-        t = int(tg[j])
-        want = next((d for d in range(2, int(t ** 0.5) + 2) if t % d == 0 and d < t), t)
-        if int(f.answer[j]) != want:
-            raise RuntimeError(f"optimus fan-out: target {t} answered {int(f.answer[j])}, expected {want}")
+    for tg, f in fs:  # every set once, checked
+        step()
+        _sync(device)
+        if not bool((f.status == STATUS_OK).all()):
+            raise RuntimeError("optimus fan-out: a range failed")
+        for j in range(0, targets, max(1, targets // 32)):
+            t = int(tg[j])
+            want = next((d for d in range(2, int(t ** 0.5) + 2) if t % d == 0 and d < t), t)
+            if int(f.answer[j]) != want:
+                raise RuntimeError(f"optimus fan-out: target {t} answered {int(f.answer[j])}, expected {want}")
+    k0 = k[0] + warmup  # the first timed step's set
     el = timed(step, steps, warmup, device, barrier)
     if max_over_ranks is not None:
         el = max_over_ranks(el)
+    M = sum(fs[(k0 + i) % sets][1].M for i in range(steps))  # the timed steps' ranges
+    bbytes = sum(f.M * 28 for _, f in fs)  # actor 4 + three int64 columns per range
     return {"config": "example/optimus fan-out + device gather (delay 0)", "targets_per_gpu_per_step": targets,
-            "ranges_per_gpu_per_step": f.M, "value": f.M * world * steps / el,
+            "ranges_per_gpu_per_step": M // max(steps, 1), "value": M * world / el,
             "unit": "ranges/s (Prime.Check messages, whole node)", "targets_per_s": targets * world * steps / el,
             "ms_per_step": el / steps * 1e3, "delivery": "mailbox" + (" (sorted exchange)" if world > 1 else ""),
-            "gather": "device (first non-target reply per target, early exit)"}
+            "gather": "device (first non-target reply per target, early exit)",
+            "distinct_batches": sets, "batch_bytes_total": bbytes}
 
 
 # ---------------------------------------------------------------------------- public API
@@ -180,12 +193,14 @@ def api_send(device, sizes, actors: int, steps: int, warmup: int) -> dict:
     try:
         client = c.NewClient("calculator", C.ConnConfig(retries=0, allow_local=False))
         for M in sizes:
-            batches = [B.gen_requests(M, actors, METHOD_CALC_MULTIPLY, seed=11 + k, device=device) for k in range(2)]
+            # at least 3 distinct batches, together more than the 256 MB MALL (20 B per message)
+            nb = max(3, -(-300_000_000 // (20 * M)))
+            batches = [B.gen_requests(M, actors, METHOD_CALC_MULTIPLY, seed=11 + k, device=device) for k in range(nb)]
             res = {}
             k = [0]
 
             def step():
-                b = batches[k[0] & 1]
+                b = batches[k[0] % nb]
                 k[0] += 1
                 th = time.perf_counter()
                 res["out"] = client.Send(b)
@@ -202,7 +217,8 @@ def api_send(device, sizes, actors: int, steps: int, warmup: int) -> dict:
             if not (bool((s == STATUS_OK).all()) and torch.equal(v, res["b"].a0 * res["b"].a1)):
                 raise RuntimeError("api_send: verification failed")
             out[f"{M}"] = {"msgs_per_step": M, "value": M * steps / el, "ms_per_step": el / steps * 1e3,
-                           "host_us_per_send": host_us}
+                           "host_us_per_send": host_us, "distinct_batches": nb, "batch_bytes_total": nb * 20 * M}
+            del batches
         client.Close()
     finally:
         c.Close()

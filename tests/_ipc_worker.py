@@ -141,6 +141,58 @@ def sorted_fold(rank, R):
     return {"messages": int(bounds[-1]), "actors": len(order)}
 
 
+def sorted_defer(rank, R):
+    """send_all(defer=True) across processes: no host wait on the
+    current Send -- Send k's overflow count is read just before Send k + 2 (its
+    agreement, which Send k + 2 waits for anyway) -- then flush(); every reply
+    exact, skewed start-up Sends included (their overflow re-sent late, into the
+    same output tensors).  Host time per Send reported without the backpressure
+    wait for Send k - 2's agreement."""
+    n, M = 16384, 120_000
+    tab, _ = table(n, R)
+    st = torch.zeros(n // R + 1, dtype=torch.int64, device=DEV)
+    ex = ActorExchange(tab, M, chunks=2, state=st, delivery="mailbox", mailbox_ordered=False, comm="ipc",
+                       comm_timeout_s=30.0)
+    outs, host = [], []
+    K = 12
+    for k in range(K):
+        # Zipf-skewed early Sends overflow the start-up capacity; uniform later ones fit
+        req = (B.gen_zipf_requests(M, n, 1.1, seed=300 + 17 * rank + k, device=DEV) if k < 3 else
+               B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=700 + 7 * rank + k, device=DEV))
+        t = time.perf_counter()
+        v, sts = ex.send_all(req, defer=True)
+        host.append(time.perf_counter() - t)
+        outs.append((req, v, sts))
+        # deferred: only Sends at least two old were resolved (their agreement adopted already)
+        assert all(d[0] <= ex._sorted.sends - 2 for d in ex._deferred) or len(ex._deferred) <= 2
+    prof = ex._sorted.host_profile()
+    waits_before_flush = int(prof["overflow_waits"])
+    ex.flush()
+    torch.cuda.synchronize()
+    for k, (req, v, sts) in enumerate(outs):
+        assert bool((sts == STATUS_OK).all()), (k, int((sts != STATUS_OK).sum()))
+        assert torch.equal(v, req.a0 * req.a1), k
+    rounds_skewed = int(ex.counters.resends)
+    # steady state (uniform traffic, agreed capacity): the only overflow reads are of
+    # Sends two Sends old -- none of the current Send -- and no re-send round runs
+    w0, r0, outs = int(ex._sorted.host_profile()["overflow_waits"]), int(ex.counters.resends), []
+    for k in range(K):
+        req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=900 + 7 * rank + k, device=DEV)
+        outs.append((req,) + tuple(ex.send_all(req, defer=True)))
+    steady_waits = int(ex._sorted.host_profile()["overflow_waits"]) - w0
+    ex.flush()
+    torch.cuda.synchronize()
+    for k, (req, v, sts) in enumerate(outs):
+        assert bool((sts == STATUS_OK).all()) and torch.equal(v, req.a0 * req.a1), k
+    prof = ex._sorted.host_profile()
+    sends = int(prof["sends"])
+    return {"resend_rounds": rounds_skewed, "steady_resend_rounds": int(ex.counters.resends) - r0,
+            "steady_overflow_waits": steady_waits, "overflow_waits_before_flush": waits_before_flush,
+            "deferred_sends": K, "host_us_per_send_all": sorted(host)[len(host) // 2] * 1e6,
+            "host_us_per_native_send": (prof["total_ns"] - prof["spec_wait_ns"]) / max(sends, 1) / 1e3,
+            "backpressure_us_per_send": prof["spec_wait_ns"] / max(sends, 1) / 1e3}
+
+
 def epoch_direct(rank, R):
     """The epoch engine (delivery "direct": route -> all-to-all -> dispatch ->
     all-to-all -> complete, wire v3 with the exact-size exchange) across processes."""

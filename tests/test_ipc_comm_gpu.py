@@ -67,6 +67,15 @@ def test_sorted_exchange_across_processes_seqfold_exactly_once_fifo(R):
     assert out["messages"] == R * 3 * 50_000 and out["actors"] > 0
 
 
+def test_deferred_resend_has_no_host_wait_on_the_current_send():
+    out = _launch("sorted_defer", 2)
+    print("defer", out)
+    assert out["resend_rounds"] >= 1  # the skewed start-up Sends overflowed and were re-sent late
+    # steady state: every overflow read before flush() was of a Send two Sends old (K - 2 of them)
+    assert out["steady_resend_rounds"] == 0 and out["steady_overflow_waits"] == out["deferred_sends"] - 2, out
+    assert out["host_us_per_native_send"] < 200.0, out
+
+
 def test_epoch_engine_across_processes_exact_size_exchange():
     out = _launch("epoch_direct", 2)
     assert out["exact"] and out["S"] > 0

@@ -24,3 +24,7 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_1m -o pr
 echo 1m; tail -1 gpurun_out/${TAG}_1m.log
 timeout -k 10 400 python3 bench.py > gpurun_out/${TAG}_b1.json 2> gpurun_out/${TAG}_b1.err || exit 7
 cat gpurun_out/${TAG}_b1.json
+timeout -k 10 200 python3 bench.py --pipeline on --no-secondary > gpurun_out/${TAG}_pipe8m.json 2> gpurun_out/${TAG}_pipe8m.err || exit 8
+cat gpurun_out/${TAG}_pipe8m.json
+timeout -k 10 200 python3 bench.py --pipeline on --no-secondary --msgs-per-gpu 1048576 > gpurun_out/${TAG}_pipe1m.json 2> gpurun_out/${TAG}_pipe1m.err || exit 9
+cat gpurun_out/${TAG}_pipe1m.json
