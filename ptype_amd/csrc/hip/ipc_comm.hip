@@ -5,6 +5,8 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
+#include <atomic>
 
 namespace ptype {
 
@@ -21,37 +23,6 @@ __device__ __forceinline__ void ipc_st(uint64_t* p, uint64_t v) {
 }
 __device__ __forceinline__ uint64_t* word_at(uint64_t base, size_t off) {
   return reinterpret_cast<uint64_t*>(base + off);
-}
-
-// One wave: lane q waits for rank q's word >= want.  which 0: rank q's `consumed`
-// (its inbox is free for this op -- this rank's own too: ops issued on two
-// streams, e.g. the epoch engine's agreement and its all-to-alls, are serialised
-// here); 1: this rank's posted[q] (rank q's data is in).
-// A timeout marks this rank failed (sticky) and the host flag; a rank already
-// failed returns at once.
-__global__ __launch_bounds__(64) void ipc_wait_kernel(const uint64_t* __restrict__ segs, int R, int rank, int which,
-                                                      uint64_t want, uint64_t timeout_ticks,
-                                                      uint64_t* __restrict__ host_failed) {
-  const int q = (int)threadIdx.x;
-  uint64_t* mine_failed = word_at(segs[rank], kIpcFailedOff);
-  bool timed_out = false;
-  if (q < R && ipc_ld(mine_failed) == 0) {
-    const uint64_t* w = which == 0 ? word_at(segs[q], kIpcConsumedOff) : word_at(segs[rank], kIpcPostedOff) + q;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t n = 0;
-    while (ipc_ld(w) < want) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-        timed_out = true;
-        break;
-      }
-      if ((++n & 63) == 0 && ipc_ld(mine_failed)) break;  // another wave of this rank gave up already
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  if (__ballot(timed_out) && q == 0) {
-    ipc_st(mine_failed, 1);
-    __hip_atomic_store(host_failed, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
 }
 
 // `bytes` (a multiple of 4) from s to d by the blocks of one grid row.
@@ -79,15 +50,42 @@ __device__ __forceinline__ bool rank_failed(const uint64_t* segs, int rank) {
   return f;
 }
 
-// K1: region q of src -> slot `rank` of peer q's inbox; the last block of row q
-// publishes posted[rank] = seq in peer q's segment.
+// Bounded wait of one lane for *w >= want (another process's store, system
+// scope); a timeout marks this rank failed (sticky, and the pinned host flag).
+// Returns false when this rank's comm is (or just became) failed.
+__device__ __forceinline__ bool wait_word(const uint64_t* w, uint64_t want, uint64_t* mine_failed,
+                                          uint64_t timeout_ticks, uint64_t* host_failed) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t n = 0;
+  while (ipc_ld(w) < want) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+      ipc_st(mine_failed, 1);
+      __hip_atomic_store(host_failed, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    if ((++n & 63) == 0 && ipc_ld(mine_failed)) return false;  // another wave of this rank gave up already
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return ipc_ld(mine_failed) == 0;
+}
+
+// K1: every block of row q waits until peer q's inbox is free for this op
+// (consumed >= seq - 1; this rank's own too, so ops issued on two streams stay
+// serialised), then copies region q of src into slot `rank` of peer q's inbox;
+// the last block of row q publishes posted[rank] = seq in peer q's segment.
 __global__ __launch_bounds__(256) void ipc_push_kernel(const uint8_t* __restrict__ src, uint64_t src_stride,
-                                                       IpcSizes send, const uint64_t* __restrict__ segs, int rank,
-                                                       uint64_t cap, uint64_t seq, unsigned* __restrict__ ctr) {
-  if (rank_failed(segs, rank)) return;  // this comm is dead: nobody waits for this op any more
+                                                       const IpcSizes* __restrict__ send, const uint64_t* __restrict__ segs,
+                                                       int rank, uint64_t cap, uint64_t seq, unsigned* __restrict__ ctr,
+                                                       uint64_t timeout_ticks, uint64_t* __restrict__ host_failed) {
   const int q = (int)blockIdx.y;
+  uint64_t* mine_failed = word_at(segs[rank], kIpcFailedOff);
+  __shared__ bool go;
+  if (threadIdx.x == 0)
+    go = wait_word(word_at(segs[q], kIpcConsumedOff), seq - 1, mine_failed, timeout_ticks, host_failed);
+  __syncthreads();
+  if (!go) return;  // this comm is dead: nobody waits for this op any more
   row_copy(src + (uint64_t)q * src_stride, reinterpret_cast<uint8_t*>(segs[q]) + kIpcCtrlBytes + (uint64_t)rank * cap,
-           send.n[q]);
+           send->n[q]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -102,41 +100,59 @@ __global__ __launch_bounds__(256) void ipc_push_kernel(const uint8_t* __restrict
   }
 }
 
-// K3: inbox slot q -> region q of dst (or, reduce_n > 0, the element-wise max of
-// the R slots into reduce_dst); the last block marks the inbox consumed.
-__global__ __launch_bounds__(256) void ipc_out_kernel(uint8_t* __restrict__ dst, uint64_t dst_stride, IpcSizes recv,
+// K2: every block of row q waits for posted[q] >= seq (rank q's data is in this
+// rank's inbox), then copies inbox slot q to region q of dst (or, reduce_n > 0,
+// one block waits for every rank and takes the element-wise max of the R slots
+// into reduce_dst); the last block marks the inbox consumed.
+__global__ __launch_bounds__(256) void ipc_out_kernel(uint8_t* __restrict__ dst, uint64_t dst_stride,
+                                                      const IpcSizes* __restrict__ recv,
                                                       const uint64_t* __restrict__ segs, int rank, int R, uint64_t cap,
                                                       uint64_t seq, unsigned* __restrict__ ctr,
-                                                      uint64_t* __restrict__ reduce_dst, int reduce_n) {
-  if (rank_failed(segs, rank)) {
+                                                      uint64_t* __restrict__ reduce_dst, int reduce_n,
+                                                      uint64_t timeout_ticks, uint64_t* __restrict__ host_failed,
+                                                      uint64_t* __restrict__ slot_done) {
+  uint64_t* mine_failed = word_at(segs[rank], kIpcFailedOff);
+  const uint64_t* posted = word_at(segs[rank], kIpcPostedOff);
+  __shared__ bool go;
+  if (reduce_n > 0) {  // one block: lane q waits for rank q
+    const int q = (int)threadIdx.x;
+    bool ok = true;
+    if (q < R) ok = wait_word(posted + q, seq, mine_failed, timeout_ticks, host_failed);
+    go = __syncthreads_and(ok) != 0;
+  } else {
+    if (threadIdx.x == 0) go = wait_word(posted + blockIdx.y, seq, mine_failed, timeout_ticks, host_failed);
+    __syncthreads();
+  }
+  if (!go) {
     // the op never completed: its destination is zeroed rather than left as the
     // buffer's old (or never written) contents -- a zero region header is an
-    // empty region to every consumer; an all-reduce keeps this rank's own input
-    if (reduce_n == 0) row_zero(dst + (uint64_t)blockIdx.y * dst_stride, recv.n[blockIdx.y]);
+    // empty region to every consumer; the completion kernels read the failure
+    // word and answer kStatusNotDelivered; an all-reduce keeps this rank's input
+    if (reduce_n == 0) row_zero(dst + (uint64_t)blockIdx.y * dst_stride, recv->n[blockIdx.y]);
     return;
   }
-  if (threadIdx.x == 0) {  // acquire: the posted flags were read by the wait kernel
+  if (threadIdx.x == 0) {  // acquire: the posted flag was read above
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
   const uint8_t* inbox = reinterpret_cast<const uint8_t*>(segs[rank]) + kIpcCtrlBytes;
   if (reduce_n > 0) {
-    if (blockIdx.x == 0 && blockIdx.y == 0)
-      for (int k = (int)threadIdx.x; k < reduce_n; k += (int)blockDim.x) {
-        uint64_t m = 0;
-        for (int q = 0; q < R; ++q) m = max(m, reinterpret_cast<const uint64_t*>(inbox + (uint64_t)q * cap)[k]);
-        reduce_dst[k] = m;
-      }
+    for (int k = (int)threadIdx.x; k < reduce_n; k += (int)blockDim.x) {
+      uint64_t m = 0;
+      for (int q = 0; q < R; ++q) m = max(m, reinterpret_cast<const uint64_t*>(inbox + (uint64_t)q * cap)[k]);
+      reduce_dst[k] = m;
+    }
   } else {
     const int q = (int)blockIdx.y;
-    row_copy(inbox + (uint64_t)q * cap, dst + (uint64_t)q * dst_stride, recv.n[q]);
+    row_copy(inbox + (uint64_t)q * cap, dst + (uint64_t)q * dst_stride, recv->n[q]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every inbox load has returned (its data is stored)
   __syncthreads();
   if (threadIdx.x == 0 && atomicAdd(ctr, 1u) == gridDim.x * gridDim.y - 1) {
     atomicExch(ctr, 0u);
     ipc_st(word_at(segs[rank], kIpcConsumedOff), seq);
+    ipc_st(slot_done, seq);  // every block has read this op's sizes: the host may reuse the slot
   }
 }
 
@@ -154,6 +170,9 @@ IpcComm::IpcComm(int device, int R, int rank, size_t cap_bytes, double timeout_s
   map_segment(rank);
   PT_HIP_CHECK(hipMalloc((void**)&segs_dev_, kIpcMaxRanks * sizeof(uint64_t)));
   PT_HIP_CHECK(hipMalloc((void**)&ctr_, (kIpcMaxRanks + 1) * sizeof(unsigned)));
+  PT_HIP_CHECK(hipHostMalloc((void**)&sizes_host_, kIpcSizeSlots * sizeof(IpcSizeSlot), hipHostMallocMapped));
+  memset((void*)sizes_host_, 0, kIpcSizeSlots * sizeof(IpcSizeSlot));
+  PT_HIP_CHECK(hipHostGetDevicePointer((void**)&sizes_dev_, sizes_host_, 0));
   PT_HIP_CHECK(hipMemset(ctr_, 0, (kIpcMaxRanks + 1) * sizeof(unsigned)));
   PT_HIP_CHECK(hipHostMalloc((void**)&host_failed_, 64, hipHostMallocMapped));
   *host_failed_ = 0;
@@ -173,6 +192,7 @@ IpcComm::~IpcComm() {
     if (registered_[q]) (void)hipHostUnregister(segs_[q]->base());
   (void)hipFree(segs_dev_);
   (void)hipFree(ctr_);
+  (void)hipHostFree(sizes_host_);
   (void)hipHostFree(host_failed_);
 }
 
@@ -229,15 +249,27 @@ void IpcComm::op(const void* src, size_t src_stride, void* dst, size_t dst_strid
   auto blocks = [](uint64_t bytes) {  // ~16 KB per block, at most 64 per peer
     return (unsigned)std::min<uint64_t>(64, std::max<uint64_t>(1, (bytes + 16383) / 16384));
   };
-  hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, s, segs_dev_, R_, rank_, 0, seq - 1, timeout_ticks_,
-                     dev_failed_);
+  // the per-peer sizes go through a small device ring of IpcSizes (kernel
+  // arguments of 512 B each made every launch slower); slot reuse is safe once
+  // the ring has wrapped, because ops on a comm complete in order
+  const int k = (int)(seq % kIpcSizeSlots);
+  IpcSizeSlot* hs = sizes_host_ + k;
+  const uint64_t prev = seq > (uint64_t)kIpcSizeSlots ? seq - kIpcSizeSlots : 0;
+  while (__atomic_load_n(&hs->done, __ATOMIC_ACQUIRE) < prev) {  // (the host is kIpcSizeSlots ops ahead: rare)
+    if (failed()) break;  // a failed comm's kernels return early and mark nothing: the slot is free
+    std::this_thread::yield();
+  }
+  hs->send = send;
+  hs->recv = recv;
+  std::atomic_thread_fence(std::memory_order_release);
+  IpcSizeSlot* ds = sizes_dev_ + k;
   hipLaunchKernelGGL(ipc_push_kernel, dim3(blocks(smax), R_), dim3(256), 0, s, (const uint8_t*)src,
-                     (uint64_t)src_stride, send, segs_dev_, rank_, (uint64_t)cap_, seq, ctr_);
-  hipLaunchKernelGGL(ipc_wait_kernel, dim3(1), dim3(64), 0, s, segs_dev_, R_, rank_, 1, seq, timeout_ticks_,
-                     dev_failed_);
+                     (uint64_t)src_stride, (const IpcSizes*)&ds->send, segs_dev_, rank_, (uint64_t)cap_, seq, ctr_,
+                     timeout_ticks_, dev_failed_);
   hipLaunchKernelGGL(ipc_out_kernel, dim3(reduce_n > 0 ? 1 : blocks(rmax), reduce_n > 0 ? 1 : R_), dim3(256), 0, s,
-                     (uint8_t*)dst, (uint64_t)dst_stride, recv, segs_dev_, rank_, R_, (uint64_t)cap_, seq,
-                     ctr_ + kIpcMaxRanks, reduce_dst, reduce_n);
+                     (uint8_t*)dst, (uint64_t)dst_stride, (const IpcSizes*)&ds->recv, segs_dev_, rank_, R_,
+                     (uint64_t)cap_, seq, ctr_ + kIpcMaxRanks, reduce_dst, reduce_n, timeout_ticks_, dev_failed_,
+                     &ds->done);
   PT_HIP_CHECK(hipGetLastError());
   hipEvent_t* ev = nullptr;
   for (auto& se : last_op_)

@@ -22,16 +22,15 @@
 //   [4096, ...)   inbox[R][cap]: rank q's region of the op in flight at q * cap
 //
 // Op s (every rank issues the same ops in the same order; s is a host counter),
-// all on the caller's stream:
-//   K0 wait   one wave: every rank's consumed >= s - 1 (its inbox is free again;
-//             this rank's own too, so ops issued on two streams stay serialised)
-//   K1 push   (X, R) blocks: region q of src -> rank q's inbox slot r; the last
-//             block of each row releases (system fence) and stores posted[r] = s
-//             into rank q's segment
-//   K2 wait   one wave: every posted[q] of this rank's segment >= s
-//   K3 out    (X, R) blocks: system acquire, inbox slot q -> region q of dst (or
-//             the element-wise max of the R slots, for all-reduce); the last
-//             block stores consumed = s
+// all on the caller's stream -- two kernels:
+//   K1 push   (X, R) blocks: row q waits for rank q's consumed >= s - 1 (its
+//             inbox is free again; this rank's own too, so ops issued on two
+//             streams stay serialised), copies region q of src -> rank q's inbox
+//             slot r; the last block of each row releases (system fence) and
+//             stores posted[r] = s into rank q's segment
+//   K2 out    (X, R) blocks: row q waits for posted[q] >= s, system acquire,
+//             inbox slot q -> region q of dst (or the element-wise max of the R
+//             slots, for all-reduce); the last block stores consumed = s
 // Waits are bounded (timeout_s): a peer that never arrives (killed) makes the
 // wave set `failed` (and a pinned host flag) and exit, every later kernel of
 // this comm skips its work, and the next Send's check() throws
@@ -56,8 +55,18 @@ constexpr int kIpcMaxRanks = 64;
 constexpr size_t kIpcCtrlBytes = 4096;
 constexpr size_t kIpcPostedOff = 0, kIpcConsumedOff = 512, kIpcFailedOff = 640;
 
-struct IpcSizes {  // by value: bytes per peer region (<= cap)
+struct IpcSizes {  // bytes per peer region (<= cap)
   uint64_t n[kIpcMaxRanks];
+};
+// Per-peer sizes of the ops in flight: a ring of slots in pinned host memory
+// (512-B kernel arguments made every launch slower), read by the kernels over
+// the bus; the out kernel's last block marks the slot done, and the host reuses
+// a slot only once its previous op is done (or the comm has failed).
+constexpr int kIpcSizeSlots = 64;
+struct IpcSizeSlot {
+  IpcSizes send, recv;
+  uint64_t done;  // the seq of the last op that finished with this slot
+  uint64_t pad[7];
 };
 
 class IpcComm : public HostComm {
@@ -103,6 +112,8 @@ class IpcComm : public HostComm {
   std::vector<bool> registered_;
   uint64_t* segs_dev_ = nullptr;           // [R] device address of every rank's segment, as mapped here
   unsigned* ctr_ = nullptr;                // last-block tickets: [R] push rows, [1] out (self-resetting)
+  IpcSizeSlot* sizes_host_ = nullptr;     // [kIpcSizeSlots] pinned (the host writes, the kernels read)
+  IpcSizeSlot* sizes_dev_ = nullptr;      // the same, device address
   uint64_t* host_failed_ = nullptr;        // pinned: set by a timed-out wait
   uint64_t* dev_failed_ = nullptr;         // its device address
   uint64_t seq_ = 0;                       // ops issued

@@ -73,7 +73,8 @@ def test_deferred_resend_has_no_host_wait_on_the_current_send():
     assert out["resend_rounds"] >= 1  # the skewed start-up Sends overflowed and were re-sent late
     # steady state: every overflow read before flush() was of a Send two Sends old (K - 2 of them)
     assert out["steady_resend_rounds"] == 0 and out["steady_overflow_waits"] == out["deferred_sends"] - 2, out
-    assert out["host_us_per_native_send"] < 200.0, out
+    # host time of the native Send with IpcComm: ~2 kernels per collective op, 5 ops per Send
+    assert out["host_us_per_native_send"] < 1000.0, out
 
 
 def test_epoch_engine_across_processes_exact_size_exchange():
