@@ -355,15 +355,15 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
 // headers from the totals (and clears the counters for the next chunk).
 
 template <int MODE, int S>
-__global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsigned long long* __restrict__ desc,
-                                                          unsigned* __restrict__ tctr, unsigned* __restrict__ ticket,
-                                                          uint32_t* __restrict__ sendbuf, int64_t req_stride,
-                                                          uint32_t C, SxCaps caps, uint32_t hdr_word3,
-                                                          int rank_self, PackedLayout L, int32_t* __restrict__ perm,
-                                                          unsigned long long* __restrict__ meta,
-                                                          unsigned long long* __restrict__ stats,
-                                                          uint32_t* __restrict__ rcnt, bool reserve,
-                                                          bool reject_ordered) {
+__device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long long* __restrict__ desc,
+                                                 unsigned* __restrict__ tctr, unsigned* __restrict__ ticket,
+                                                 uint32_t* __restrict__ sendbuf, int64_t req_stride,
+                                                 uint32_t C, SxCaps caps, uint32_t hdr_word3,
+                                                 int rank_self, PackedLayout L, int32_t* __restrict__ perm,
+                                                 unsigned long long* __restrict__ meta,
+                                                 unsigned long long* __restrict__ stats,
+                                                 uint32_t* __restrict__ rcnt, bool reserve,
+                                                 bool reject_ordered) {
   __shared__ uint32_t wcnt[kST / kWave][kSxMaxRanks];
   __shared__ uint32_t pre[kSxMaxRanks];
   __shared__ uint32_t cap_s[kSxMaxRanks];  // per-destination capacities (C: the region stride in records)
@@ -514,6 +514,28 @@ __global__ __launch_bounds__(kST) void sx_onesweep_kernel(SortIn in, int R, unsi
     }
   }
 }
+
+#define PT_SX_OS_PARAMS                                                                                        \
+  SortIn in, int R, unsigned long long *__restrict__ desc, unsigned *__restrict__ tctr,                          \
+      unsigned *__restrict__ ticket, uint32_t *__restrict__ sendbuf, int64_t req_stride, uint32_t C, SxCaps caps, \
+      uint32_t hdr_word3, int rank_self, PackedLayout L, int32_t *__restrict__ perm,                             \
+      unsigned long long *__restrict__ meta, unsigned long long *__restrict__ stats, uint32_t *__restrict__ rcnt, \
+      bool reserve, bool reject_ordered
+#define PT_SX_OS_ARGS \
+  in, R, desc, tctr, ticket, sendbuf, req_stride, C, caps, hdr_word3, rank_self, L, perm, meta, stats, rcnt, reserve, reject_ordered
+template <int MODE, int S>
+__global__ __launch_bounds__(kST) void sx_onesweep_kernel(PT_SX_OS_PARAMS) {
+  sx_onesweep_body<MODE, S>(PT_SX_OS_ARGS);
+}
+// The same pass held to 64 VGPRs (8 waves per SIMD: 4 blocks per CU, so a 4 Mi chunk's
+// 1024 tiles are resident at once instead of in 1.33 rounds); PTYPE_SX_OCC8=1 (experiment)
+template <int MODE, int S>
+__global__ __launch_bounds__(kST) __attribute__((amdgpu_waves_per_eu(8, 8))) void sx_onesweep_occ8_kernel(
+    PT_SX_OS_PARAMS) {
+  sx_onesweep_body<MODE, S>(PT_SX_OS_ARGS);
+}
+#undef PT_SX_OS_PARAMS
+#undef PT_SX_OS_ARGS
 
 // ---------------------------------------------------------------- receiver: parallel drain
 // grid (X, R): block (x, p) strides over source p's region in 64-record groups
@@ -1209,10 +1231,18 @@ void SortedExchange::send(const SxSend& a) {
     if (!sharded && in.tiles > 0 && (sx_mode != 2 || mode == 3)) {
       const uint32_t hdr3 =
           ((uint32_t)(kFlagValid | (mode == 3 ? kFlagActorIds : 0)) << 16) | (uint32_t)a.method_uniform;
-#define PT_SX_OS(MO, SV)                                                                                         \
-  hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_, ticket_, \
-                     b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm, (unsigned long long*)meta, stats_, \
-                     rcnt_ + i * kSxMaxRanks, reserve, reject_ordered)
+  static const bool occ8 = getenv("PTYPE_SX_OCC8") && atoi(getenv("PTYPE_SX_OCC8")) == 1;
+#define PT_SX_OS(MO, SV)                                                                                           \
+  do {                                                                                                             \
+    if (occ8 && SV == 2 && (MO == 3 || MO == 1))                                                                   \
+      hipLaunchKernelGGL((sx_onesweep_occ8_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_, \
+                         ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm, (unsigned long long*)meta, \
+                         stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered);                                 \
+    else                                                                                                           \
+      hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_,      \
+                         ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm,                        \
+                         (unsigned long long*)meta, stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered);      \
+  } while (0)
 #define PT_SX_OS_S(MO)              \
   switch (S) {                      \
     case 1: PT_SX_OS(MO, 1); break; \

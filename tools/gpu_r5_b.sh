@@ -13,7 +13,7 @@ rc=$?; echo "tests rc=$rc"; grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_o
 [ $rc -le 1 ] || exit $rc
 L8="python3 bench.py --loopback 8 --steps 20 --warmup 5 --rtt-calls 0 --no-secondary"
 i=0
-for K in "" "PTYPE_COMP_U=2" "PTYPE_SX_DRAIN_BLOCKS=4096" "PTYPE_SX_DRAIN_PER=512" "CHUNKS1"; do
+for K in "" "PTYPE_SX_OCC8=1" "PTYPE_COMP_U=2" "PTYPE_SX_DRAIN_BLOCKS=4096" "PTYPE_SX_DRAIN_PER=512" "CHUNKS1"; do
   i=$((i+1))
   if [ "$K" = "CHUNKS1" ]; then
     timeout -k 10 200 $L8 --chunks 1 > gpurun_out/${TAG}_l8_$i.json 2>gpurun_out/${TAG}_l8_$i.err || exit 3
