@@ -51,9 +51,6 @@ def _parse():
     p.add_argument("--cpu", action="store_true", help="gloo/CPU dry run of the same pipeline (tests)")
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the step as a captured hipGraph (auto: single rank)")
-    p.add_argument("--pipeline", choices=["on", "off"], default="off",
-                   help="graph path: generate step j+1's batch on a forked stream while step j's Send runs "
-                        "(client-side double buffering, PipelinedSendGraph)")
     p.add_argument("--steps-per-graph", type=int, default=0,
                    help="whole steps per graph replay (the graph launch and the seed advance show per replay); "
                         "steps and warmup must be multiples.  0 = auto: the largest of 4, 2, 1 dividing both")
@@ -81,6 +78,9 @@ def _parse():
                    help="skewed load: actor popularity Zipf(S) (hot actors scattered over the GPUs); batches "
                         "pre-generated outside the timed loop, so compare against --zipf 0 --pregen")
     p.add_argument("--pregen", action="store_true", help="uniform load, pre-generated like --zipf (A/B baseline)")
+    p.add_argument("--method", choices=["multiply", "seqfold"], default="multiply",
+                   help="the timed step's method (seqfold: the ordered stateful method -- experiments; "
+                        "the headline is Calculator.Multiply)")
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary (affine placement) measurement after the headline")
     p.add_argument("--comm", choices=["rccl", "ipc"], default="rccl",
@@ -259,13 +259,10 @@ def main():
         # steps that do not fill a U-step replay run on a 1-step graph of the same
         # step, so exactly --warmup steps warm up and exactly --steps are timed
         # (round 4: 20 steps per replay measured 1-3 % above 4 at 8 Mi and 1 Mi, profiles/r4_mailbox_ab.md)
-        even = args.pipeline == "on"
-        args.steps_per_graph = next((u for u in (20, 10, 5, 4, 2) if use_graph and args.steps % u == 0
-                                     and (u % 2 == 0 or not even)), 1)
+        args.steps_per_graph = next((u for u in (20, 10, 5, 4, 2) if use_graph and args.steps % u == 0), 1)
     if args.steps_per_graph < 1 or (args.steps_per_graph > 1 and (
             not use_graph or args.steps % args.steps_per_graph)):
         raise SystemExit("--steps-per-graph: needs the graph path, and --steps a multiple of it")
-    pipelined = use_graph and args.pipeline == "on" and args.steps_per_graph % 2 == 0
     pre = []
     if pregen:  # 4 distinct batches per rank, generated before any timing
         for k in range(4):
@@ -306,25 +303,7 @@ def main():
         graph = graph1 = None
         U = args.steps_per_graph
         vt = [rq, v, t]  # the batch and replies the verification reads
-        if pipelined:
-            # two batches and two reply sets, alternately: step j + 1's batch is generated on a
-            # forked stream while step j's Send runs (PipelinedSendGraph)
-            from ptype_amd.parallel.exchange import PipelinedSendGraph
-
-            rq2 = B.MsgBatch(torch.empty_like(rq.actor), torch.empty_like(rq.a0), torch.empty_like(rq.a1), None, method)
-            v2, t2 = torch.empty_like(v), torch.empty_like(t)
-            seed_p = torch.tensor([rank * 0x9E3779B9 + 7 + j * 0x1000193 for j in range(U)], dtype=torch.int64,
-                                  device=device)
-
-            def gen(r_, j):  # step j of a replay draws from seed j; j == U: the next replay's step 0
-                if j == U:
-                    seed_p.add_(U * 0x1000193)
-                    j = 0
-                B.gen_requests(Mq, n_actors, method, wide=wide, device=device, out=r_, seed_tensor=seed_p[j:j + 1])
-
-            graph = PipelinedSendGraph(ex, [rq, rq2], [(v, t), (v2, t2)], gen, U)
-            vt = [rq2, v2, t2]
-        elif use_graph:
+        if use_graph:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
             # seed from device memory and the graph advances it, so every replay is a new batch
             seed_t = torch.tensor([rank * 0x9E3779B9 + 7 + j * 0x1000193 for j in range(U + 1)], dtype=torch.int64,
@@ -345,22 +324,6 @@ def main():
                 graph1 = ex.capture(rq, v, t, prologue=prologue1, allow_collectives=args.graph == "on", repeat=1)
 
         def step(s_):
-            if pipelined:
-                if s_ < warmup - warmup % U:  # warm-up: whole replays, then eager steps
-                    if s_ % U == 0:
-                        graph.prime()
-                        graph.replay()
-                elif s_ < warmup:
-                    B.gen_requests(Mq, n_actors, method, wide=wide, seed=(s_ * world + rank) * 0x1000193 + 7, device=device,
-                                   out=rq2)
-                    ex.send(rq2, v2, t2)
-                    if s_ == warmup - 1:
-                        graph.prime()  # the first timed step's batch (the pipeline's steady state)
-                elif (s_ - warmup) % U == 0:
-                    if warmup == 0 and s_ == 0:
-                        graph.prime()
-                    graph.replay()
-                return
             if graph is not None:
                 if s_ < warmup and graph1 is not None:  # warm-up: one step per replay
                     graph1.replay()
@@ -419,7 +382,8 @@ def main():
         hang_s = str(300 + 0.2 * (args.steps + args.warmup) * (3 if not args.no_secondary else 1))
     if hang_s and float(hang_s) > 0:
         _hang_watchdog(float(hang_s), rank)
-    elapsed, ex, graphed = measure(table, args.steps, args.warmup)
+    head_method = METHOD_SEQ_FOLD if args.method == "seqfold" else METHOD_CALC_MULTIPLY
+    elapsed, ex, graphed = measure(table, args.steps, args.warmup, method=head_method)
     head_host_us = host_us_per_step[0]
     def lookup_mode(t):
         if t.dir is None:
@@ -623,7 +587,8 @@ def main():
             "rtt_remote_request_ring": remote_ring,
             "rtt_error": "; ".join(rtt_errors) if rtt_errors else None,
             "config": {
-                "model": "calculator actor (Calculator.Multiply)",
+                "model": "calculator actor (Calculator.Multiply)" if args.method == "multiply" else
+                         "SeqFold actor (ordered stateful method; experiment, not the headline)",
                 "global_batch": M * world,
                 "seq_len": None,
                 "parallelism": (f"{world} ranks sharing {torch.cuda.device_count()} GPU(s), IpcComm all-to-alls "
@@ -640,8 +605,6 @@ def main():
                 "args": "A: 16-bit signed, B: 16-bit (int64 columns; see secondaries.wide_args for full-range)",
                 "hip_graph": graphed,
                 "steps_per_graph": args.steps_per_graph if graphed else None,
-                # the next step's batch generated on a forked stream during this step's Send
-                "pipelined_generator": bool(pipelined),
                 # host time inside the timed step calls (this rank; a graph replay launches U steps)
                 "host_us_per_step": round(head_host_us, 2) if head_host_us is not None else None,
                 **({"load": f"zipf({args.zipf})" if args.zipf > 0 else "uniform", "pregenerated": True,

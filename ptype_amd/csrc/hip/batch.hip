@@ -65,7 +65,8 @@ __device__ __forceinline__ uint32_t mod_u64_u32(uint64_t h, uint32_t n, uint64_t
 
 // WIDE: full-range int64 arguments (two more hashes per message) -- values no
 // narrow record holds, for the wide-argument figures (16-B ring records).
-template <bool WIDE>
+// NT: non-temporal stores (PTYPE_GEN_NT=1, experiment: the columns are read once, by the Send)
+template <bool WIDE, bool NT = false>
 __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
                                                            int64_t* __restrict__ a1, int64_t M, uint32_t n_actors,
                                                            uint64_t seed, const uint64_t* __restrict__ seed_ptr,
@@ -73,13 +74,23 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
   if (seed_ptr) seed = *seed_ptr;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < M; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = mix64(seed ^ (uint64_t)i * 0x9e3779b97f4a7c15ull);
-    actor[i] = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
+    const uint32_t ac = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
+    int64_t x0, x1;
     if constexpr (WIDE) {
-      a0[i] = (int64_t)mix64(h ^ 0xa0761d6478bd642full);
-      a1[i] = (int64_t)mix64(h ^ 0xe7037ed1a0b428dbull);
+      x0 = (int64_t)mix64(h ^ 0xa0761d6478bd642full);
+      x1 = (int64_t)mix64(h ^ 0xe7037ed1a0b428dbull);
     } else {
-      a0[i] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
-      a1[i] = (int64_t)((h >> 40) & 0xffff);
+      x0 = (int64_t)((h >> 20) & 0xffff) - 0x8000;
+      x1 = (int64_t)((h >> 40) & 0xffff);
+    }
+    if constexpr (NT) {
+      __builtin_nontemporal_store(ac, actor + i);
+      __builtin_nontemporal_store(x0, a0 + i);
+      __builtin_nontemporal_store(x1, a1 + i);
+    } else {
+      actor[i] = ac;
+      a0[i] = x0;
+      a1[i] = x1;
     }
   }
 }
@@ -774,6 +785,10 @@ void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M,
     hipLaunchKernelGGL(gen_requests_vec4_kernel, dim3(grid_cap(std::max<int64_t>(M / 4, 1), 256, cap_blocks)),
                        dim3(256), 0, as_stream(stream), (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors,
                        seed, (const uint64_t*)seed_ptr, magic);
+  else if (getenv("PTYPE_GEN_NT") && atoi(getenv("PTYPE_GEN_NT")) == 1)
+    hipLaunchKernelGGL((gen_requests_kernel<false, true>), dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0,
+                       as_stream(stream), (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed,
+                       (const uint64_t*)seed_ptr, magic);
   else
     hipLaunchKernelGGL(gen_requests_kernel<false>, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
                        (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr,

@@ -1306,6 +1306,10 @@ __global__ __launch_bounds__(kST) void mbx_arrival_drain_kernel(MboxView mv, Sor
 // methods keeps per-actor FIFO across all of them).  Replies are staged at the
 // records' ring slots (a window's slots are contiguous: whole lines), and
 // mbx_complete_kernel gathers them into message order.
+// A12: the batch carries a second / third argument column.  Without them (a
+// one-argument ordered method, e.g. SeqFold) the window's a1 / a2 arrays are not
+// allocated: 68 instead of 100 KB of LDS, so two drain blocks fit a CU.
+template <bool A12>
 struct OrdLds {
   uint32_t wcnt[kOrdWaves][kOrdThreads];  // per-wave bin counts -> offsets
   uint32_t bstart[kOrdThreads];
@@ -1315,16 +1319,17 @@ struct OrdLds {
   uint32_t act[kOrdWin];  // actor index for the handler (LDS-local or global mailbox)
   uint32_t meth[kOrdWin];  // method | flags << 16
   uint32_t orig[kOrdWin];  // origin: the completion's place for the reply
-  int64_t a0[kOrdWin], a1[kOrdWin], a2[kOrdWin];
+  int64_t a0[kOrdWin], a1[A12 ? kOrdWin : 2], a2[A12 ? kOrdWin : 2];
 };
 
+template <bool A12>
 __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView mv, uint32_t* __restrict__ gsum,
                                                                         uint32_t ngroups, int64_t* __restrict__ state,
                                                                         uint32_t n_state, uint64_t delay_ticks,
                                                                         OutboxView ob, u32x4* __restrict__ srep) {
   extern __shared__ __align__(16) unsigned char smem_ord[];
-  OrdLds& L = *reinterpret_cast<OrdLds*>(smem_ord);
-  int64_t* st_lds = reinterpret_cast<int64_t*>(smem_ord + sizeof(OrdLds));
+  OrdLds<A12>& L = *reinterpret_cast<OrdLds<A12>*>(smem_ord);
+  int64_t* st_lds = reinterpret_cast<int64_t*>(smem_ord + sizeof(OrdLds<A12>));
   const uint32_t s = blockIdx.x;
   const uint32_t S = 1u << mv.log_s;
   const uint64_t Q = 1ull << mv.log_q;
@@ -1403,8 +1408,10 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
       L.meth[d] = x[k].method | (x[k].flags << 16);
       L.orig[d] = x[k].origin;
       L.a0[d] = x[k].a0;
-      L.a1[d] = x[k].a1;
-      L.a2[d] = x[k].a2;
+      if constexpr (A12) {
+        L.a1[d] = x[k].a1;
+        L.a2[d] = x[k].a2;
+      }
     }
     __syncthreads();
     {  // this thread's bin, serially in ring order
@@ -1417,7 +1424,9 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
         m.actor = L.act[d];
         m.method = (uint16_t)(L.meth[d] & 0xffffu);
         m.flags = (uint16_t)(L.meth[d] >> 16);
-        m.a0 = L.a0[d], m.a1 = L.a1[d], m.a2 = L.a2[d];
+        m.a0 = L.a0[d];
+        m.a1 = A12 ? L.a1[d] : 0;
+        m.a2 = A12 ? L.a2[d] : 0;
         const ReplyRecord rr = run_handler(m, st, nst, delay_ticks, ob, true);
         failed += rr.status != kStatusOk;
         srep[L.slot[d]] = u32x4{(uint32_t)rr.value, (uint32_t)((uint64_t)rr.value >> 32), (uint32_t)rr.status, L.orig[d]};
@@ -1828,15 +1837,26 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   PT_HIP_CHECK(hipGetLastError());
   const size_t ring_lds = ring_drain_lds_bytes(Sv);
   if (a.ordered) {
-    const size_t lds = sizeof(OrdLds) + (size_t)kOrdStateMax * sizeof(int64_t);
-    static bool attr = false;
-    if (!attr) {  // above the 64 KB default dynamic LDS
-      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      attr = true;
-    }
-    hipLaunchKernelGGL(mbx_drain_ordered_kernel, dim3(Sv), dim3(kOrdThreads), lds, st, mv, sort_gsum_, ngroups,
-                       (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);
+    // state staged per shard: what its actors need (mailboxes s, s + S, ...), not the cap
+    const uint32_t n_loc = a.state && a.n_state ? std::min<uint32_t>((a.n_state + Sv - 1) / Sv, kOrdStateMax) : 0;
+    const size_t st_lds = (size_t)n_loc * sizeof(int64_t);  // (covers every shard the kernel stages: n_loc <= cap)
+    const bool a12 = a.a1 || a.a2;  // (a column given: staged; none: the handlers see zeros)
+#define PT_ORD(A12)                                                                                           \
+  do {                                                                                                        \
+    const size_t lds = sizeof(OrdLds<A12>) + std::max<size_t>(st_lds, 16);                                   \
+    static bool attr = false;                                                                                 \
+    if (!attr) { /* above the 64 KB default dynamic LDS */                                                    \
+      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12>,                            \
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,                            \
+                                       (int)(sizeof(OrdLds<A12>) + (size_t)kOrdStateMax * sizeof(int64_t)))); \
+      attr = true;                                                                                            \
+    }                                                                                                         \
+    hipLaunchKernelGGL(mbx_drain_ordered_kernel<A12>, dim3(Sv), dim3(kOrdThreads), lds, st, mv, sort_gsum_,  \
+                       ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);         \
+  } while (0)
+    if (a12) PT_ORD(true);
+    else PT_ORD(false);
+#undef PT_ORD
     PT_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST),
                        (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, in, mv,

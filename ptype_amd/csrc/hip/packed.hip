@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void pack_replies_kernel(const uint32_t* __res
 // (messages per thread per trip: a kernel template argument, PTYPE_COMP_U in {2, 4, 8}; default 4)
 constexpr int32_t kPastBatch = INT32_MIN;  // (perm codes: >= 0 slot position, -1 overflow, -2 no actor, -3 direct)
 
-template <int kCompU>
+template <int kCompU, bool NT = false>
 __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
                                                               uint32_t C, int R, int vb,
                                                               const int32_t* __restrict__ perm, int64_t M,
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
 #pragma unroll
     for (int u = 0; u < kCompU; ++u) {
       const int64_t i = i0 + u * stride;
-      p[u] = i < M ? perm[i] : kPastBatch;
+      p[u] = i < M ? (NT ? __builtin_nontemporal_load(perm + i) : perm[i]) : kPastBatch;
     }
     uint64_t code[kCompU];
     unsigned long long okw[kCompU];
@@ -344,8 +344,13 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
       } else {
         st = p[u] == -1 ? kStatusOverflow : kStatusNoActor;
       }
-      out_val[i] = v;
-      out_st[i] = st;
+      if constexpr (NT) {  // (the caller reads them; nothing here re-reads them)
+        __builtin_nontemporal_store(v, out_val + i);
+        __builtin_nontemporal_store(st, out_st + i);
+      } else {
+        out_val[i] = v;
+        out_st[i] = st;
+      }
       sum += (unsigned long long)v;
     }
   }
@@ -490,6 +495,15 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t p
   if (R < 1 || R > kMaxRanks) throw std::invalid_argument("complete: 1 <= R <= 64");
   if (vb != 1 && vb != 2 && vb != 4 && vb != 8) throw std::invalid_argument("complete: vb in {1,2,4,8}");
   static const int comp_u = getenv("PTYPE_COMP_U") ? atoi(getenv("PTYPE_COMP_U")) : 4;
+  static const bool comp_nt = getenv("PTYPE_COMP_NT") && atoi(getenv("PTYPE_COMP_NT")) == 1;  // (experiment)
+  if (comp_nt && comp_u == 4) {
+    hipLaunchKernelGGL((complete_packed_kernel<4, true>), dim3(grid_for(M, 256 * 4, checksum ? 1024 : 8192)),
+                       dim3(256), 0, as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R,
+                       vb, (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st,
+                       (unsigned long long*)checksum, direct, (const uint64_t*)failed);
+    PT_HIP_CHECK(hipGetLastError());
+    return;
+  }
 #define PT_COMP(U)                                                                                                 \
   hipLaunchKernelGGL(complete_packed_kernel<U>, dim3(grid_for(M, 256 * (U), checksum ? 1024 : 8192)), dim3(256), 0, \
                      as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R, vb,          \

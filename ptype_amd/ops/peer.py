@@ -2,8 +2,10 @@
 
 ``PeerCaller(shm_name, device)`` registers a lane on another process's
 persistent dispatcher (same node: this GPU or a peer over xGMI) and runs calls
-from a KERNEL on this process's GPU: the request goes into the server's HBM
-lane, the reply lands in this GPU's HBM, no host on the path.  Every call's
+from a KERNEL on this process's GPU: the request goes into a lane of the
+server's shared-memory segment and the reply comes back in the lane's reply
+slot -- memory this process maps itself, so a dead server costs a timeout, not
+a fault -- with no host on the path.  Every call's
 round trip is stamped with the device clock (s_memrealtime, 100 MHz).
 
 Reference: one remote request/reply, cluster/rpc.go:59-67.
@@ -65,11 +67,12 @@ class PeerRelay:
     GPU peer lanes on another process's dispatcher, handed to ``server`` (this
     process's ``DeviceServer``) as its relay table.  A request to ``server``
     with method ``METHOD_RELAY`` -- actor = the REMOTE actor, a0 = the remote
-    method, a1/a2 = its arguments -- is forwarded by the dispatcher wave itself
-    (publish into the peer's HBM lane, spin on a reply slot in this GPU's HBM)
-    and the remote reply returned as the call's own: a handler that calls
-    another server, with no host between the hops (reference: a handler
-    dialling another node, cluster/rpc.go:59-67).
+    method, a1/a2 = its arguments -- is forwarded by the dispatcher wave itself:
+    published into a free lane of the peer's segment and parked there while the
+    wave keeps serving; the remote reply, when it lands, completes the call (a
+    timed-out relay answers kStatusNotDelivered and fails that call only).  A
+    handler that calls another server, with no host between the hops
+    (reference: a handler dialling another node, cluster/rpc.go:59-67).
 
     The native relay (its lanes and device table) is kept for the life of the
     process once attached: the dispatcher wave reads the table until its next
@@ -89,6 +92,11 @@ class PeerRelay:
     @property
     def lanes(self) -> int:
         return self._relay.lanes
+
+    def slots(self) -> list[int]:
+        """Per lane ``[seq, suspect]`` as the device table holds them (the dispatcher
+        wave writes its slot words back when it parks or the table is replaced)."""
+        return [int(x) for x in self._relay.slots()]
 
     def detach(self):
         self._server.set_relay(0)

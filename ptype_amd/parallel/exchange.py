@@ -961,68 +961,3 @@ class SendGraph:
         self.ex.counters.sent += self.M * self.repeat
         self.ex.counters.epochs += self.ex.chunks * self.repeat
 
-
-class PipelinedSendGraph:
-    """``repeat`` steps per hipGraph replay with client-side double buffering: the
-    generation of step j + 1's batch runs on a forked stream while step j's Send
-    runs, so the client producing messages overlaps the system delivering them (a
-    producer that fills the next batch while the current one is in flight).
-
-    ``reqs`` / ``outs``: two request batches and two (value, status) output pairs,
-    used alternately (``repeat`` must be even, so every replay starts on
-    ``reqs[0]``).  ``gen(req, j)`` enqueues the generation of step j's batch into
-    ``req`` on the current stream; j runs 1 .. repeat, where j == repeat is the
-    NEXT replay's first batch -- so call ``prime()`` (the first batch, j = 0) once
-    before the first replay.  Step j's Send waits for its batch (event join) and
-    the generation into a buffer waits for the Send that last read it.  After a
-    replay, ``reqs[1]`` / ``outs[1]`` hold the last step's batch and replies."""
-
-    def __init__(self, ex: ActorExchange, reqs, outs, gen, repeat: int = 2):
-        if repeat < 2 or repeat % 2:
-            raise ValueError("PipelinedSendGraph: repeat must be even (>= 2)")
-        self.ex, self.reqs, self.outs, self.gen, self.repeat = ex, list(reqs), list(outs), gen, int(repeat)
-        self.M = self.reqs[0].M
-        dev = ex.device
-        self.side = torch.cuda.Stream(dev)
-
-        def body():
-            main = torch.cuda.current_stream(dev)
-            for j in range(self.repeat):
-                cur, nxt = j % 2, (j + 1) % 2
-                freed = torch.cuda.Event()
-                freed.record(main)  # Send j - 1 (the last reader of reqs[nxt]) is done here
-                self.side.wait_event(freed)
-                with torch.cuda.stream(self.side):
-                    gen(self.reqs[nxt], j + 1)
-                ready = torch.cuda.Event()
-                ready.record(self.side)
-                ex.send(self.reqs[cur], *self.outs[cur])
-                main.wait_event(ready)  # the next Send's batch is complete
-
-        ex.table.directory()  # build outside the capture if dirty
-        prev, ex._capturing = ex._capturing, True
-        try:
-            warm = torch.cuda.Stream(dev)
-            warm.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(warm):  # warm allocations / lazy state outside the graph
-                for k in range(2):
-                    gen(self.reqs[k], 0)
-                    ex.send(self.reqs[k], *self.outs[k])
-            torch.cuda.current_stream(dev).wait_stream(warm)
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                body()
-        finally:
-            ex._capturing = prev
-        self.replays = 0
-
-    def prime(self) -> None:
-        """The first replay's first batch (eager, on the current stream)."""
-        self.gen(self.reqs[0], 0)
-
-    def replay(self) -> None:
-        """One graph launch: ``repeat`` steps."""
-        self.graph.replay()
-        self.replays += 1
-        self.ex.counters.sent += self.M * self.repeat
-        self.ex.counters.epochs += self.ex.chunks * self.repeat

@@ -171,7 +171,11 @@ def _expect(p, word, timeout=120):
                 break
             if line.startswith(word):
                 return line.split()
-    raise AssertionError(f"no {word!r} from the child (rc {p.poll()}): " + (p.stderr.read()[-3000:] if p.poll() is not None else ""))
+    if p.poll() is None:  # still running: stop it to read what it said
+        p.kill()
+        p.wait(30)
+    raise AssertionError(f"no {word!r} from the child (rc {p.returncode}): stdout tail "
+                         + p.stdout.read()[-1500:] + " stderr " + p.stderr.read()[-3000:])
 
 
 def _unlink_shm(name):
@@ -404,10 +408,13 @@ _RELAY_TO_DYING = textwrap.dedent("""
     t = time.time()
     v1, s1, _ = srv.call(METHOD_RELAY, 7, METHOD_CALC_MULTIPLY, 6, 7, 30.0)  # parked: the target is busy, then killed
     w1 = time.time() - t
+    print("CALL1", s1, round(w1, 3), flush=True)
     t = time.time()
     v2, s2, _ = srv.call(METHOD_RELAY, 7, METHOD_CALC_MULTIPLY, 6, 7, 30.0)  # the only slot is suspect: fails at once
     w2 = time.time() - t
+    print("CALL2", s2, round(w2, 3), flush=True)
     v3, s3, _ = srv.call(METHOD_ECHO, 3, 99)  # local calls unaffected
+    print("CALL3", v3, s3, flush=True)
     x = (torch.arange(1 << 20, device="cuda") * 2).sum().item()
     time.sleep(2.5)  # the wave parks after 2 s idle and writes its slot words back to the table
     out = {"s1": s1, "w1": w1, "s2": s2, "w2": w2, "local": [v3, s3], "slots": [int(q) for q in relay.slots()],
