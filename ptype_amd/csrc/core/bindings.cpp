@@ -9,6 +9,7 @@
 #include <unordered_map>
 
 #include "api.hpp"
+#include "dataplane.hpp"
 #include "follower.hpp"
 #include "gob.hpp"
 #include "json.hpp"
@@ -965,6 +966,37 @@ PYBIND11_MODULE(_core, m) {
       .def_property_readonly("local_addr", &Cluster::local_addr)
       .def_property_readonly("member_id", [](Cluster& c) { return c.member().id(); })
       .def("member_status", [](Cluster& c) { return c.member().status(); });
+
+  // ---------------------------------------------------------------- data-plane lifecycle (dataplane.hpp)
+  py::class_<DataPlane, std::shared_ptr<DataPlane>>(m, "DataPlane",
+                                                    "RCCL communicator lifecycle of a service's GPU data plane: "
+                                                    "rendezvous through the replicated store, init, abort, "
+                                                    "lease-driven membership, next generation")
+      .def(py::init([](std::shared_ptr<Cluster> c, const std::string& service, const std::string& me, int device,
+                       double timeout_s) {
+             return std::make_shared<DataPlane>(c->registry, c->registry->kv_ptr(), service, me, device, timeout_s);
+           }),
+           py::arg("cluster"), py::arg("service"), py::arg("me"), py::arg("device"), py::arg("timeout_s") = 30.0)
+      .def("form", &DataPlane::form, py::arg("gen"), py::arg("members"), py::call_guard<py::gil_scoped_release>())
+      .def("alive_nodes", &DataPlane::alive_nodes, py::call_guard<py::gil_scoped_release>())
+      .def("wait_nodes", &DataPlane::wait_nodes, py::arg("world"), py::call_guard<py::gil_scoped_release>())
+      .def("settle", &DataPlane::settle, py::arg("current"), py::arg("grace_s"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("recover", &DataPlane::recover, py::arg("grace_s"), py::call_guard<py::gil_scoped_release>())
+      .def("async_error", &DataPlane::async_error)
+      .def("abort", &DataPlane::abort, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("aborted", &DataPlane::aborted)
+      .def("allreduce_max", &DataPlane::allreduce_max, py::arg("values"), py::call_guard<py::gil_scoped_release>())
+      .def("sendrecv", &DataPlane::sendrecv, py::arg("send"), py::arg("send_bytes"), py::arg("dst"), py::arg("recv"),
+           py::arg("recv_bytes"), py::arg("src"), py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &DataPlane::barrier, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("comm", &DataPlane::comm)
+      .def_property_readonly("rank", &DataPlane::rank)
+      .def_property_readonly("size", &DataPlane::size)
+      .def_property_readonly("gen", &DataPlane::gen)
+      .def_property_readonly("members", &DataPlane::members)
+      .def_property_readonly("me", &DataPlane::me)
+      .def_static("available", &DataPlane::available);
 
   // ---------------------------------------------------------------- gob (golden tests)
   m.def("gob_encode", [](py::list values) {
