@@ -334,6 +334,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("delivery", &GpuConfig::delivery)
       .def_readwrite("comm", &GpuConfig::comm)
       .def_readwrite("form_group", &GpuConfig::form_group)
+      .def_readwrite("native_group", &GpuConfig::native_group)
       .def_readwrite("group_timeout_s", &GpuConfig::group_timeout_s)
       .def_readwrite("grace_s", &GpuConfig::grace_s)
       .def_readwrite("send_timeout_s", &GpuConfig::send_timeout_s)
@@ -978,6 +979,8 @@ PYBIND11_MODULE(_core, m) {
            }),
            py::arg("cluster"), py::arg("service"), py::arg("me"), py::arg("device"), py::arg("timeout_s") = 30.0)
       .def("form", &DataPlane::form, py::arg("gen"), py::arg("members"), py::call_guard<py::gil_scoped_release>())
+      .def("set_device", &DataPlane::set_device, py::arg("device"))
+      .def_property_readonly("device", &DataPlane::device)
       .def("alive_nodes", &DataPlane::alive_nodes, py::call_guard<py::gil_scoped_release>())
       .def("wait_nodes", &DataPlane::wait_nodes, py::arg("world"), py::call_guard<py::gil_scoped_release>())
       .def("settle", &DataPlane::settle, py::arg("current"), py::arg("grace_s"),
@@ -987,6 +990,8 @@ PYBIND11_MODULE(_core, m) {
       .def("abort", &DataPlane::abort, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("aborted", &DataPlane::aborted)
       .def("allreduce_max", &DataPlane::allreduce_max, py::arg("values"), py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_max_dev", &DataPlane::allreduce_max_dev, py::arg("dev"), py::arg("n"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
       .def("sendrecv", &DataPlane::sendrecv, py::arg("send"), py::arg("send_bytes"), py::arg("dst"), py::arg("recv"),
            py::arg("recv_bytes"), py::arg("src"), py::call_guard<py::gil_scoped_release>())
       .def("barrier", &DataPlane::barrier, py::call_guard<py::gil_scoped_release>())

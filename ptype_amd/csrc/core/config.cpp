@@ -133,6 +133,7 @@ void decode_ptype(const YNode& root, Config& c) {
         else if (g.first == "delivery") c.gpu.delivery = want_string(G, g.first, g.second);
         else if (g.first == "comm") c.gpu.comm = want_string(G, g.first, g.second);
         else if (g.first == "form_group") c.gpu.form_group = want_bool(G, g.first, g.second);
+        else if (g.first == "native_group") c.gpu.native_group = want_bool(G, g.first, g.second);
         else if (g.first == "group_timeout_s") c.gpu.group_timeout_s = want_float(G, g.first, g.second);
         else if (g.first == "grace_s") c.gpu.grace_s = want_float(G, g.first, g.second);
         else if (g.first == "send_timeout_s") c.gpu.send_timeout_s = want_float(G, g.first, g.second);

@@ -69,6 +69,9 @@ struct GpuConfig {
   double grace_s = 8;           // how long a recovery waits for the dead node's lease to lapse
   double send_timeout_s = 30;   // GPU: a Send's device work overdue this long aborts the communicator
   uint32_t replicate_every = 0; // buddy replicas of the actor state every N Sends (0: only on request)
+  // RCCL groups: the communicator's lifecycle in the control plane (dataplane.hpp: store
+  // rendezvous, ncclCommInitRank, ncclCommAbort, next generation) instead of a torch process group
+  bool native_group = true;
 };
 
 struct Config {

@@ -527,13 +527,6 @@ template <int MODE, int S>
 __global__ __launch_bounds__(kST) void sx_onesweep_kernel(PT_SX_OS_PARAMS) {
   sx_onesweep_body<MODE, S>(PT_SX_OS_ARGS);
 }
-// The same pass held to 64 VGPRs (8 waves per SIMD: 4 blocks per CU, so a 4 Mi chunk's
-// 1024 tiles are resident at once instead of in 1.33 rounds); PTYPE_SX_OCC8=1 (experiment)
-template <int MODE, int S>
-__global__ __launch_bounds__(kST) __attribute__((amdgpu_waves_per_eu(8, 8))) void sx_onesweep_occ8_kernel(
-    PT_SX_OS_PARAMS) {
-  sx_onesweep_body<MODE, S>(PT_SX_OS_ARGS);
-}
 #undef PT_SX_OS_PARAMS
 #undef PT_SX_OS_ARGS
 
@@ -1231,14 +1224,8 @@ void SortedExchange::send(const SxSend& a) {
     if (!sharded && in.tiles > 0 && (sx_mode != 2 || mode == 3)) {
       const uint32_t hdr3 =
           ((uint32_t)(kFlagValid | (mode == 3 ? kFlagActorIds : 0)) << 16) | (uint32_t)a.method_uniform;
-  static const bool occ8 = getenv("PTYPE_SX_OCC8") && atoi(getenv("PTYPE_SX_OCC8")) == 1;
 #define PT_SX_OS(MO, SV)                                                                                           \
   do {                                                                                                             \
-    if (occ8 && SV == 2 && (MO == 3 || MO == 1))                                                                   \
-      hipLaunchKernelGGL((sx_onesweep_occ8_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_, \
-                         ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm, (unsigned long long*)meta, \
-                         stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered);                                 \
-    else                                                                                                           \
       hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_,      \
                          ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm,                        \
                          (unsigned long long*)meta, stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered);      \

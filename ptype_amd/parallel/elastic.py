@@ -9,7 +9,9 @@ RCCL: the watchdog aborts the communicator with
 ``TORCH_NCCL_ASYNC_ERROR_HANDLING=2``).  RCCL is not fault tolerant, so a group is
 never repaired in place -- it is aborted and a new *generation* is formed:
 
-1. ``send`` fails -> the survivor aborts its group (``_abort_process_group``),
+1. ``send`` fails -> the survivor aborts its group (a compiled ``NativeGroup``:
+   ``ncclCommAbort`` in csrc/core/dataplane.cpp; a torch group:
+   ``_abort_process_group``),
 2. waits until the control plane's lease-based membership (the service's
    registry nodes) drops the dead node (bounded by ``grace_s``),
 3. re-rendezvouses through the replicated KV store (``bootstrap.form_group``,
@@ -159,23 +161,35 @@ def lost_blocks(nodes0: list[str], before: list[str], after: list[str]) -> list[
 
 
 class SendWatchdog:
-    """Bounds how long a Send's device work may stay incomplete (RCCL over xGMI
-    has no timeout of its own for the engine's collectives, which are issued on
-    the group's communicator outside torch's watchdog).  ``arm(event)`` after a
-    Send; a daemon thread polls the armed events and, when one is overdue,
-    aborts the communicator -- the RCCL kernels waiting on a dead peer return --
-    and marks the generation failed, so the next Send raises and recovers."""
+    """Bounds how long a Send may stay incomplete (RCCL over xGMI has no timeout
+    of its own for the engine's collectives, which are issued on the group's
+    communicator outside torch's watchdog).  ``begin()`` / ``end()`` bracket the
+    host part of a Send (a host wait on a collective whose peer died would never
+    return), ``arm(event)`` after it covers its device work; a daemon thread
+    polls both and, when one is overdue, calls ``abort`` -- the communicator is
+    aborted, so RCCL kernels and host waits on a dead peer return -- and marks the
+    generation failed: the Send (or the next one) raises and recovers.  ``abort``
+    is the default process group's (``abort_group``) or a compiled
+    ``NativeGroup``'s ``ncclCommAbort``."""
 
-    def __init__(self, timeout_s: float, poll_s: float = 0.05):
+    def __init__(self, timeout_s: float, poll_s: float = 0.05, abort=None):
         import threading
 
         self.timeout_s, self.poll_s = float(timeout_s), float(poll_s)
+        self.abort = abort if abort is not None else abort_group
         self.failed: str | None = None
         self._q: list[tuple[object, float]] = []
+        self._host_deadline: float | None = None
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._th = threading.Thread(target=self._run, daemon=True, name="ptype-send-watchdog")
         self._th.start()
+
+    def begin(self) -> None:
+        self._host_deadline = time.monotonic() + self.timeout_s
+
+    def end(self) -> None:
+        self._host_deadline = None
 
     def arm(self, event) -> None:
         with self._lock:
@@ -186,20 +200,31 @@ class SendWatchdog:
     def reset(self) -> None:
         with self._lock:
             self._q = []
+        self._host_deadline = None
         self.failed = None
+
+    def _fail(self, why: str) -> None:
+        if self.failed is None:
+            self.failed = why
+            try:
+                self.abort()
+            except Exception:
+                pass
 
     def _run(self) -> None:
         while not self._stop.wait(self.poll_s):
             with self._lock:
                 q = self._q
             now = time.monotonic()
+            hd = self._host_deadline
+            if hd is not None and now > hd:
+                self._fail(f"a Send did not return within {self.timeout_s:.1f} s")
             keep = []
             for ev, dl in q:
                 if ev.query():
                     continue
-                if now > dl and self.failed is None:
-                    self.failed = f"a Send's device work did not complete within {self.timeout_s:.1f} s"
-                    abort_group()
+                if now > dl:
+                    self._fail(f"a Send's device work did not complete within {self.timeout_s:.1f} s")
                 keep.append((ev, dl))
             with self._lock:
                 if self._q is q:

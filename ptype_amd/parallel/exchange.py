@@ -135,8 +135,13 @@ class ActorExchange:
         # ``fake = (_hip.FakeComm(R), rank)``: one of R in-process ranks on one GPU
         # (tests drive each from its own thread and stream; geometry must match)
         self.fake = fake
+        # a NativeGroup (parallel/native_group.py): the compiled DataPlane's communicator --
+        # no torch process group behind it
+        self.native = group is not None and hasattr(group, "comm_ptr") and hasattr(group, "dp")
         if fake is not None:
             self.rank, self.world = int(fake[1]), int(fake[0].size)
+        elif self.native:
+            self.rank, self.world = group.rank, group.size
         elif dist.is_available() and dist.is_initialized():
             self.rank = dist.get_rank(group)
             self.world = dist.get_world_size(group)
@@ -152,16 +157,19 @@ class ActorExchange:
         self.comm_kind = comm if fake is None and self.world > 1 else "rccl"
         # run the RCCL all-to-alls even on a single rank (validates the collective
         # path on a 1-GPU box; a 1-rank all-to-all is a device-local copy)
-        self.force_collectives = bool(fake is None and dist.is_available() and dist.is_initialized()
-                                      and self.world == 1)
+        self.force_collectives = bool(fake is None and self.world == 1
+                                      and (self.native or (dist.is_available() and dist.is_initialized())))
         self.chunks = max(1, int(chunks))
         self.max_chunk = int(math.ceil(max_batch / self.chunks))
         # every rank must use the same slot geometry (equal-split all-to-all):
         # agree on the largest chunk and the chunk count once, collectively
         if self.world > 1 and fake is None:
-            t = torch.tensor([self.max_chunk, self.chunks], dtype=torch.int64, device=self._agree_device())
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            self.max_chunk, self.chunks = int(t[0]), int(t[1])
+            if self.native:
+                self.max_chunk, self.chunks = group.allreduce_max([self.max_chunk, self.chunks])
+            else:
+                t = torch.tensor([self.max_chunk, self.chunks], dtype=torch.int64, device=self._agree_device())
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+                self.max_chunk, self.chunks = int(t[0]), int(t[1])
         self.C = capacity_for(self.max_chunk, self.world, slack)
         self.state = state
         self.delay_us = delay_us
@@ -186,6 +194,8 @@ class ActorExchange:
         self.bufs = [_ChunkBufs(self.world, self.C_alloc, self.max_chunk, self.device, self.force_collectives,
                                 fmt or B.FULL_FORMAT) for _ in range(min(self.chunks, 8))]
         if self.comm_kind == "ipc":
+            if self.native:
+                raise RuntimeError("comm='ipc' forms its own transport over a gloo group, not a native RCCL group")
             if not self.use_engine:
                 raise RuntimeError("comm='ipc' drives the native engines: it needs a GPU")
             self.ipc = ipc_group_comm(self.group, self.device, self.ipc_cap_bytes(), comm_timeout_s)
@@ -213,6 +223,8 @@ class ActorExchange:
     def _agree_device(self) -> torch.device:
         """Where host-level agreements' tensors live: CPU for a gloo group (its
         CUDA collectives are not universally available), else the exchange's device."""
+        if getattr(self, "native", False):
+            return self.device
         if self.device.type == "cuda" and dist.is_available() and dist.is_initialized():
             if dist.get_backend(self.group) == "gloo":
                 return torch.device("cpu")
@@ -243,6 +255,8 @@ class ActorExchange:
             return 0
         if self.ipc is not None:
             return 0
+        if self.native:
+            return self.group.comm_ptr()
         pg = self.group if self.group is not None else dist.group.WORLD
         try:
             backend = pg._get_backend(self.device)
@@ -613,6 +627,8 @@ class ActorExchange:
                 self.fake[0].allreduce_max(self.rank, agreed[h].data_ptr(), k + 1, stream)
             elif self.ipc is not None:
                 self.ipc.allreduce_max(agreed[h].data_ptr(), k + 1, stream)
+            elif self.native:
+                self.group.allreduce_max_dev(agreed[h], stream)
             else:
                 dist.all_reduce(agreed[h], op=dist.ReduceOp.MAX, group=self.group)
             host[h, 0].copy_(own[h], non_blocking=True)
@@ -826,6 +842,8 @@ class ActorExchange:
         """Max of ``v`` over the group (every rank must take the same number of
         re-send rounds).  In-process FakeComm ranks agree through a barrier; the
         loopback stand-in is one rank that speaks for a symmetric node."""
+        if self.fake is None and self.native:
+            return int(self.group.allreduce_max([v])[0])
         if self.fake is None:
             t = torch.tensor([v], dtype=torch.int64, device=self._agree_device())
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)

@@ -77,8 +77,11 @@ class DeviceRuntime:
             torch.cuda.set_device(self.device)
         d = _dist()
         self.group = group
-        self.rank = d.get_rank(group) if d else 0
-        self.world = d.get_world_size(group) if d else 1
+        if group is not None and hasattr(group, "comm_ptr"):  # NativeGroup: the compiled DataPlane
+            self.rank, self.world = group.rank, group.size
+        else:
+            self.rank = d.get_rank(group) if d else 0
+            self.world = d.get_world_size(group) if d else 1
         self.service = service
         # services whose actors are this runtime's actors: the one it joined as, plus
         # any co-hosted through host()/serve() (one actor id space per runtime)
@@ -153,25 +156,35 @@ class DeviceRuntime:
             return torch.device("cuda", int(lr) if lr is not None else r % max(ndev, 1))
 
         members = None
+        native = None
         if (g.world > 1 or g.form_group) and not (dist.is_available() and dist.is_initialized()):
             from .parallel.bootstrap import form_group, node_id, wait_nodes
 
             me = node_id(core_cluster.local_addr, cfg.port)
             registry = Registry(core_cluster.registry)
-            nodes = wait_nodes(registry, cfg.service_name, max(g.world, 1))
             backend = g.backend or ("gloo" if g.cpu or g.comm == "ipc" else "nccl")
             store = KVStore(core_cluster.store)
-            if backend == "nccl":  # a failed collective aborts the communicator instead of the process
-                os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
-            members, tcp = form_group(store, core_cluster.local_addr, me, cfg.service_name, 0, nodes, backend,
-                                      device_for_rank, timeout_s=g.group_timeout_s)
+            from .parallel.native_group import NativeGroup
+
+            if backend == "nccl" and g.native_group and NativeGroup.available():
+                # the RCCL communicator's whole lifecycle in the control plane (csrc/core/dataplane.hpp):
+                # unique id through the replicated store, ncclCommInitRank -- no torch process group
+                native = NativeGroup.join(core_cluster, cfg.service_name, me, device_for_rank, max(g.world, 1),
+                                          timeout_s=max(30.0, g.group_timeout_s))
+                members = native.members
+            else:
+                nodes = wait_nodes(registry, cfg.service_name, max(g.world, 1))
+                if backend == "nccl":  # a failed collective aborts the communicator instead of the process
+                    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+                members, tcp = form_group(store, core_cluster.local_addr, me, cfg.service_name, 0, nodes, backend,
+                                          device_for_rank, timeout_s=g.group_timeout_s)
             owns = True
         d = _dist()
-        rank = d.get_rank() if d else 0
+        rank = native.rank if native is not None else (d.get_rank() if d else 0)
         rt = cls(device_for_rank(rank), actors=g.actors, ring=g.ring, idle_ms=g.idle_ms, delay_us=g.delay_us,
                  max_batch=g.max_batch, service=cfg.service_name, mailbox_shards=g.mailbox_shards,
                  mailbox_slots=g.mailbox_slots, delivery=g.delivery, comm=g.comm,
-                 comm_timeout_s=g.group_timeout_s)
+                 comm_timeout_s=g.group_timeout_s, group=native)
         rt._tcp_store, rt._owns_group = tcp, owns
         rt._addr = (core_cluster.local_addr, int(cfg.port))
         if members is not None and g.elastic:
@@ -183,7 +196,7 @@ class DeviceRuntime:
             if g.send_timeout_s > 0:  # (arms device events on a GPU; on the host it only carries a failure flag)
                 from .parallel.elastic import SendWatchdog
 
-                rt._watchdog = SendWatchdog(g.send_timeout_s)
+                rt._watchdog = SendWatchdog(g.send_timeout_s, abort=rt._abort_generation)
         rt.attach(core_cluster.registry.kv, cfg.service_name, cfg.node_name, watch=g.watch)
         # Send needs every rank's routes: wait until all shards of the group are mirrored
         rt.mirror.wait_shards(rt.world)
@@ -342,7 +355,15 @@ class DeviceRuntime:
                 if self._watchdog is not None and self._watchdog.failed:
                     raise RankFailure(self._watchdog.failed)
                 sub = batch if todo is None else batch.index_select(todo)
-                out = self.exchange.send_all(sub) if resend_overflow else self.exchange.send(sub)
+                if self._watchdog is not None:
+                    self._watchdog.begin()  # the host part of the Send is bounded too
+                try:
+                    out = self.exchange.send_all(sub) if resend_overflow else self.exchange.send(sub)
+                finally:
+                    if self._watchdog is not None:
+                        self._watchdog.end()
+                if self._watchdog is not None and self._watchdog.failed:  # aborted mid-Send: its replies are void
+                    raise RankFailure(self._watchdog.failed)
                 ipc = self.exchange.ipc
                 if ipc is not None:  # IpcComm: a peer that missed a collective is seen once the Send's waits end
                     torch.cuda.current_stream(self.device).synchronize()
@@ -408,6 +429,11 @@ class DeviceRuntime:
             return
         src = next(n for n in m["members"] if buddy(m["nodes0"], m["members"], n) == m["me"])
         P = self.actors
+        if self._native:  # the compiled group's ncclSend / ncclRecv pair (csrc/core/dataplane.cpp)
+            recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=self.device)
+            self.group.sendrecv(self.state.contiguous(), m["members"].index(dst), recv, m["members"].index(src))
+            self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(own[src])}
+            return
         # a gloo group (CPU runtimes, comm="ipc") moves host tensors
         host = self.on_gpu and dist.get_backend(self.group) == "gloo"
         io_dev = torch.device("cpu") if host else self.device
@@ -424,22 +450,36 @@ class DeviceRuntime:
         form the next generation through the store and re-home the lost ranks'
         actors.  Returns the original ranks that were lost."""
         from .parallel.bootstrap import alive_nodes, form_group
-        from .parallel.elastic import abort_group, lost_blocks, settle_membership
+        from .parallel.elastic import lost_blocks, settle_membership
+
+        from .parallel.elastic import Excluded
 
         m, c = self.membership, self._elastic_cfg
         if m is None:
             raise RuntimeError("recover(): this runtime's group was not formed by Join")
-        abort_group()
+        self._abort_generation()
         self._exchange = None
         if self._watchdog is not None:
             self._watchdog.reset()
-        proposal = settle_membership(lambda: alive_nodes(c["registry"], self.service), m["members"], m["me"],
-                                     c["grace_s"])
-        members, tcp = form_group(c["store"], c["local_addr"], m["me"], self.service, m["gen"] + 1, proposal,
-                                  c["backend"], lambda r: self.device if c["backend"] == "nccl" else None,
-                                  timeout_s=c["timeout_s"])
+        if self._native:
+            # the compiled lifecycle: lease-driven proposal, the first current record
+            # in the store wins, ncclCommInitRank of the next generation
+            proposal = self.group.dp.settle(m["members"], float(c["grace_s"]))
+            try:
+                self.group.form(m["gen"] + 1, proposal)
+            except RuntimeError as e:
+                if "excluded" in str(e):
+                    raise Excluded(str(e)) from e
+                raise
+            members = self.group.members
+        else:
+            proposal = settle_membership(lambda: alive_nodes(c["registry"], self.service), m["members"], m["me"],
+                                         c["grace_s"])
+            members, tcp = form_group(c["store"], c["local_addr"], m["me"], self.service, m["gen"] + 1, proposal,
+                                      c["backend"], lambda r: self.device if c["backend"] == "nccl" else None,
+                                      timeout_s=c["timeout_s"])
+            self._tcp_store = tcp
         lost = lost_blocks(m["nodes0"], m["members"], members)
-        self._tcp_store = tcp
         m["members"], m["gen"] = list(members), m["gen"] + 1
         self.rank, self.world = members.index(m["me"]), len(members)
         self._rehome()
@@ -448,6 +488,23 @@ class DeviceRuntime:
                      self.world, lost, self.blocks)
         trace.mark("ptype.regenerated")
         return lost
+
+    @property
+    def _native(self) -> bool:
+        """Whether the group is the compiled DataPlane (parallel/native_group.py)."""
+        return self.group is not None and hasattr(self.group, "comm_ptr")
+
+    def _abort_generation(self) -> None:
+        """Abort the current data-plane generation (any thread; never raises)."""
+        if self._native:
+            try:
+                self.group.abort()
+            except Exception:
+                pass
+        else:
+            from .parallel.elastic import abort_group
+
+            abort_group()
 
     def _rehome(self) -> None:
         """Placement of the current generation (elastic.ring_placement): keep the
@@ -659,7 +716,9 @@ class DeviceRuntime:
             self.shard_lease.close()
         if self.server is not None:
             self.server.close()
-        if self._owns_group:
+        if self._owns_group and self._native:
+            self.group.abort()  # ncclCommAbort: never waits on a member that may be gone
+        elif self._owns_group:
             import torch.distributed as dist
 
             if dist.is_initialized():
