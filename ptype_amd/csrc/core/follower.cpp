@@ -76,6 +76,7 @@ RegistryFollower::RegistryFollower(std::shared_ptr<KvClient> kv, const std::stri
   }
   version_.fetch_add(1, std::memory_order_release);
   ctx_ = Context::with_cancel(Context::background());
+  watching_ = watch;
   if (watch) watch_ = kv_->watch(ctx_, prefix_, end_, res.rev + 1);
   th_ = std::thread([this] { run(); });
 }
@@ -124,7 +125,9 @@ void RegistryFollower::run() {
 }
 
 // A full re-list (the reference re-lists on every event, cluster/registry.go:131):
-// refreshes every listed shard's liveness and queues what the watch missed.
+// refreshes every listed shard's liveness and queues what the watch missed -- a
+// key never applied, a record that changed since it was applied (or queued), a
+// key gone -- and re-opens a watch that closed, from just past the listing.
 void RegistryFollower::relist() {
   RangeResult res;
   try {
@@ -135,28 +138,43 @@ void RegistryFollower::relist() {
     return;  // control plane electing: keep the last view; the K6 deadlines keep running
   }
   const int64_t now = mono_ms();
+  if (watching_ && watch_ && watch_->closed() && !stop_.load()) {
+    try {
+      watch_ = kv_->watch(ctx_, prefix_, end_, res.rev + 1);
+      ++watch_reopens_;
+    } catch (const std::exception&) {
+    }
+  }
   std::map<std::string, const KeyValue*> listed;
   for (const auto& x : res.kvs) listed[x.key] = &x;
   std::lock_guard<std::mutex> g(mu_);
-  auto queued = [&](const std::string& k, bool put_only) {
-    return std::any_of(pending_.begin(), pending_.end(),
-                       [&](const Pending& p) { return p.key == k && (!put_only || p.put); });
+  // the newest queued operation on k (nullptr: none) -- what take() will leave applied
+  auto last_queued = [&](const std::string& k) -> const Pending* {
+    for (auto it = pending_.rbegin(); it != pending_.rend(); ++it)
+      if (it->key == k) return &*it;
+    return nullptr;
   };
   for (const auto& [k, x] : listed) {
     seen_[k] = now;
     // shards_ belongs to take(); a missed PUT is detected against what was queued or applied
-    if (std::find(applied_keys_.begin(), applied_keys_.end(), k) == applied_keys_.end() && !queued(k, true)) {
+    const Pending* q = last_queued(k);
+    const auto a = applied_json_.find(k);
+    const std::string* have = q ? (q->put ? &q->rec.json : nullptr) : (a != applied_json_.end() ? &a->second : nullptr);
+    if (!have || *have != x->value) {
       try {
         pending_.push_back({true, k, ShardRecord::parse(x->value)});
       } catch (const std::exception&) {
       }
     }
   }
-  for (const std::string& k : applied_keys_)
-    if (!listed.count(k) && !queued(k, false)) {
+  for (const auto& [k, json] : applied_json_) {
+    (void)json;
+    const Pending* q = last_queued(k);
+    if (!listed.count(k) && (!q || q->put)) {
       pending_.push_back({false, k, {}});  // a missed DELETE
       seen_.erase(k);
     }
+  }
   relists_.fetch_add(1);
   version_.fetch_add(1, std::memory_order_release);
 }
@@ -245,8 +263,8 @@ std::vector<MirrorOp> RegistryFollower::take(int64_t now_ms, bool* sweep, int64_
   next_expiry_ = nx;
   {
     std::lock_guard<std::mutex> g(mu_);
-    applied_keys_.clear();
-    for (const auto& kv : shards_) applied_keys_.push_back(kv.first);
+    applied_json_.clear();
+    for (const auto& kv : shards_) applied_json_[kv.first] = kv.second.rec.json;
   }
   return ops;
 }
@@ -265,8 +283,8 @@ void RegistryFollower::set_generation(int64_t gen) {
   }
   {
     std::lock_guard<std::mutex> g(mu_);
-    applied_keys_.clear();
-    for (const auto& kv : shards_) applied_keys_.push_back(kv.first);
+    applied_json_.clear();
+    for (const auto& kv : shards_) applied_json_[kv.first] = kv.second.rec.json;
   }
   version_.fetch_add(1, std::memory_order_release);
 }

@@ -117,7 +117,9 @@ class RegistryFollower {
   std::vector<Pending> pending_;
   std::map<std::string, int64_t> seen_;  // key -> monotonic ms last listed / put (lease alive)
   int64_t min_gen_ = 0;
-  std::vector<std::string> applied_keys_;  // keys of shards_ as of the last take (for the re-list)
+  std::map<std::string, std::string> applied_json_;  // shards_' records as of the last take (for the re-list)
+  bool watching_ = false;                             // a watch was asked for (re-opened when it closes)
+  uint64_t watch_reopens_ = 0;
   std::atomic<uint64_t> version_{0};
   std::atomic<uint64_t> relists_{0}, events_{0};
 

@@ -285,6 +285,39 @@ def test_mirror_k6_sweeps_shards_not_seen(tmp_path, ports, monkeypatch):
         c.Close()
 
 
+def test_mirror_relist_catches_a_changed_record(tmp_path, ports, monkeypatch):
+    """with no watch event for it, a record that CHANGED after it
+    was applied (a ShardLease.update: a new generation's geometry) is caught by
+    the re-list -- not only a key never applied -- and the mirror follows it."""
+    monkeypatch.setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    from ptype_amd import cluster as C
+    from ptype_amd.mirror import RegistryMirror, ShardLease
+    from ptype_amd.ops.table import RegistryTable
+
+    pp, pc = ports(), ports()
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "svc", "n0", ports()
+    cfg.member = _member(C, 0, [pp], [pc], f"e0=http://127.0.0.1:{pp}", str(tmp_path))
+    c = C.Join(C.background(), cfg, runtime=False)
+    try:
+        kv = c._c.registry.kv
+        lease = ShardLease(kv, "svc", "x", 0, 1, 8)
+        t = RegistryTable(256, device="cpu")
+        m = RegistryMirror(t, kv, "svc", relist_s=0.2, watch=False)  # the re-list is the only follower
+        m.wait_shards(1, 5)
+        assert t.live == 8
+        lease.update(count=24)  # same key, new record
+        t0 = time.time()
+        while t.live != 24 and time.time() - t0 < 5:
+            m.apply()
+            time.sleep(0.05)
+        assert t.live == 24 and time.time() - t0 < 2.0, t.live
+        m.close()
+        lease.close()
+    finally:
+        c.Close()
+
+
 def test_send_names_a_hosted_service():
     """A Send names its service: the runtime's own, or one co-hosted on its actors
     (host() / serve()); anything else is refused instead of silently routed."""
