@@ -27,7 +27,15 @@ constexpr int kXMaxBuckets = kSxMaxRanks * kSxShards;
 PackedLayout sx_layout(const uint64_t* meta) {
   uint64_t m[kMetaWords];
   std::copy(meta, meta + kMetaWords, m);
-  m[kMetaMbox] = meta[kMetaMbox] + 1;  // one more value: all-ones is the null record
+  // every value of the widest mailbox (or actor id) seen fits, plus one: all-ones is
+  // the null record.  Sized by the bit length, not the value: under skewed load the
+  // largest id a batch happens to carry changes from Send to Send, and a batch
+  // whose max is 2^b - 1 after an agreement that saw 2^b - 2 must not overflow.
+  {
+    const uint64_t v = meta[kMetaMbox];
+    const int b = v ? 64 - __builtin_clzll(v) : 0;
+    m[kMetaMbox] = (b >= 63 ? ~0ull >> 1 : (1ull << b) - 1) + 1;
+  }
   return packed_layout(m);
 }
 
@@ -837,7 +845,7 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   PT_HIP_CHECK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
   // start-up layout: every column at full width (8-dword records, 8-byte replies)
   uint64_t wide[kMetaWords] = {};
-  wide[kMetaMbox] = kMaxMbox - 2;
+  wide[kMetaMbox] = (kMaxMbox >> 1) - 1;  // (sx_layout: 24-bit field, every mailbox below kMaxMbox - 1)
   for (int j = 0; j < 3; ++j) wide[kMetaArg0 + j] = ~0ull;
   wide[kMetaMethod] = 0xffff;
   wide[kMetaMcol] = 1;
