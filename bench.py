@@ -279,6 +279,7 @@ def main():
             raise SystemExit(f"[rank {rank}] {tag}: verification failed ({bad} non-OK replies)")
 
     host_us_per_step = [None]
+    host_split = [None]  # the sorted engine's host time split (timed steps, this rank)
 
     def measure(table, steps, warmup, delivery=args.delivery, sharding=args.sharding, Mq=M,
                 method=METHOD_CALC_MULTIPLY, wide=False):
@@ -349,6 +350,8 @@ def main():
         ex.warmup_resends, ex.counters.resends = ex.counters.resends, 0
         barrier()
         sync()
+        sx = getattr(ex, "_sorted", None)
+        prof0 = sx.host_profile() if sx is not None and hasattr(sx, "host_profile") else None
         t0 = time.perf_counter()
         host = 0.0
         for s_ in range(steps):
@@ -359,6 +362,17 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         host_us_per_step[0] = host / max(steps, 1) * 1e6  # the host's time inside the step calls (no waits)
+        if prof0 is not None:
+            # where the host's step time goes: enqueueing the Send's work vs waiting for the
+            # agreement of Send k - 2 (pick_spec: backpressure -- the host is 2 Sends ahead
+            # of a busy GPU) vs resolving an overflow count
+            p1 = sx.host_profile()
+            d = {k: p1[k] - prof0[k] for k in p1}
+            n = max(int(d.get("sends", 0)), 1)
+            host_split[0] = {"sends": int(d.get("sends", 0)),
+                             "enqueue_us_per_send": round((d["total_ns"] - d["spec_wait_ns"]) / n / 1e3, 2),
+                             "agreement_wait_us_per_send": round(d["spec_wait_ns"] / n / 1e3, 2),
+                             "overflow_wait_us_per_send": round(d["overflow_wait_ns"] / n / 1e3, 2)}
         if dist_on:
             tt = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -385,6 +399,7 @@ def main():
     head_method = METHOD_SEQ_FOLD if args.method == "seqfold" else METHOD_CALC_MULTIPLY
     elapsed, ex, graphed = measure(table, args.steps, args.warmup, method=head_method)
     head_host_us = host_us_per_step[0]
+    head_host_split = host_split[0]
     def lookup_mode(t):
         if t.dir is None:
             return "hash-table probe"
@@ -607,6 +622,7 @@ def main():
                 "steps_per_graph": args.steps_per_graph if graphed else None,
                 # host time inside the timed step calls (this rank; a graph replay launches U steps)
                 "host_us_per_step": round(head_host_us, 2) if head_host_us is not None else None,
+                **({"host_split": head_host_split} if head_host_split is not None else {}),
                 **({"load": f"zipf({args.zipf})" if args.zipf > 0 else "uniform", "pregenerated": True,
                     "resend_rounds": ex.counters.resends, "resend_rounds_warmup": ex.warmup_resends}
                    if pregen else {}),

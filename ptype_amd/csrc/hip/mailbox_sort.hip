@@ -1444,6 +1444,195 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   if (threadIdx.x == 0) epoch_commit(mv, s, tot);
 }
 
+// ---------------------------------------------------------------- K3s ordered drain, binned
+// The same per-actor FIFO drain, with the shard's records binned before any runs
+// (the windowed form above is 16 dependent load -> sort -> serial
+// rounds per 8 Mi SeqFold shard, 175 us).  A super-window of up to nr * 4096
+// records is binned first: each round reads only the records' first 8 B (valid
+// mark + mailbox) -- the next round's are loaded while this one is binned -- and
+// places each record's window offset (2 B) in LDS, stably by bin (a round's bin
+// runs in ring order, rounds in ring order).  Then thread b walks bin b's
+// entries round by round, loading 8 records at a time ahead of running them
+// one after another: an actor's messages run serially in FIFO order, distinct
+// bins in parallel, with the record loads in flight together instead of one
+// window's load per round trip.  The replies are staged at the records' ring
+// slots as before (mbx_complete_ring_kernel).  PTYPE_ORD_DRAIN=win: the windowed form.
+constexpr int kOrdBinK = 8;                            // records per thread per binning round
+constexpr int kOrdRound = kOrdThreads * kOrdBinK;      // 4096
+constexpr int kOrdBinRoundsMax = 12;                   // rounds per super-window (LDS-bound)
+constexpr int kOrdBinBatch = 8;                        // records a bin walk loads ahead
+
+__host__ __device__ constexpr size_t ord_bin_lds_bytes(uint32_t nr, uint32_t n_loc) {
+  return (size_t)kOrdWaves * kOrdThreads * 4                     // wcnt
+         + (((size_t)nr * (kOrdThreads + 1) * 2 + 15) & ~(size_t)15)  // bs: bin starts per round (u16)
+         + (size_t)nr * kOrdRound * 2                              // pos: window offsets (u16)
+         + (size_t)n_loc * 8;                                      // staged state
+}
+
+__global__ __launch_bounds__(kOrdThreads) void mbx_drain_ord_bin_kernel(MboxView mv, uint32_t* __restrict__ gsum,
+                                                                        uint32_t ngroups, int64_t* __restrict__ state,
+                                                                        uint32_t n_state, uint64_t delay_ticks,
+                                                                        OutboxView ob, u32x4* __restrict__ srep,
+                                                                        uint32_t nr) {
+  extern __shared__ __align__(16) unsigned char smem_ob[];
+  uint32_t(*wcnt)[kOrdThreads] = reinterpret_cast<uint32_t(*)[kOrdThreads]>(smem_ob);
+  uint16_t* bs = reinterpret_cast<uint16_t*>(smem_ob + (size_t)kOrdWaves * kOrdThreads * 4);
+  uint16_t* pos = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(bs) +
+                                              (((size_t)nr * (kOrdThreads + 1) * 2 + 15) & ~(size_t)15));
+  int64_t* st_lds = reinterpret_cast<int64_t*>(pos + (size_t)nr * kOrdRound);
+  __shared__ uint32_t tot_s;
+  __shared__ uint32_t wsum[kOrdWaves];
+  const uint32_t s = blockIdx.x;
+  const uint32_t S = 1u << mv.log_s;
+  const uint64_t Q = 1ull << mv.log_q;
+  const unsigned w = threadIdx.x / kWave, lane = lane_id();
+  if (threadIdx.x == 0) tot_s = epoch_total(gsum, ngroups, S, s, true);
+  const uint64_t lo = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
+  const uint64_t free = hd + Q > lo ? hd + Q - lo : 0;
+  const uint32_t n_loc = (state && s < n_state) ? (n_state - 1 - s) / S + 1 : 0;
+  const bool in_lds = state && n_loc <= kOrdStateMax;
+  if (in_lds)
+    for (uint32_t j = threadIdx.x; j < n_loc; j += kOrdThreads) st_lds[j] = state[s + (uint64_t)j * S];
+  __syncthreads();
+  const uint32_t tot = tot_s;
+  const uint64_t n = tot < free ? tot : free;
+  const uint64_t sbase = (uint64_t)s << mv.log_q, qmask = Q - 1, rot = shard_rot(mv, s);
+  const uint64_t SW = (uint64_t)nr * kOrdRound;  // records per super-window
+  unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
+  int64_t* st = in_lds ? st_lds : state;
+  const uint32_t nst = in_lds ? n_loc : n_state;
+  for (uint64_t w0 = lo; w0 < lo + n; w0 += SW) {
+    const uint64_t w1 = lo + n < w0 + SW ? lo + n : w0 + SW;
+    const uint32_t rounds = (uint32_t)((w1 - w0 + kOrdRound - 1) / kOrdRound);
+    // ---- bin: round r's records' headers (loaded one round ahead)
+    uint2 h[kOrdBinK];
+    auto load_hdr = [&](uint32_t r, uint2(&x)[kOrdBinK]) {
+#pragma unroll
+      for (int k = 0; k < kOrdBinK; ++k) {
+        const uint64_t q = w0 + (uint64_t)r * kOrdRound + (uint64_t)w * (kWave * kOrdBinK) + (uint64_t)k * kWave + lane;
+        x[k] = q < w1 ? *reinterpret_cast<const uint2*>(rec_a(mv, sbase | ((q + rot) & qmask))) : uint2{0u, 0u};
+      }
+    };
+    load_hdr(0, h);
+    for (uint32_t r = 0; r < rounds; ++r) {
+      uint2 nx[kOrdBinK];
+      if (r + 1 < rounds) load_hdr(r + 1, nx);
+      for (uint32_t b = lane; b < kOrdThreads; b += kWave) wcnt[w][b] = 0;
+      uint32_t bin[kOrdBinK], wr[kOrdBinK];
+      bool ok[kOrdBinK];
+#pragma unroll
+      for (int k = 0; k < kOrdBinK; ++k) {
+        ok[k] = (h[k].x & kCompactMark) != 0;
+        const uint64_t q = w0 + (uint64_t)r * kOrdRound + (uint64_t)w * (kWave * kOrdBinK) + (uint64_t)k * kWave + lane;
+        if (!ok[k] && q < w1) ++holes;
+        bin[k] = ((h[k].y & 0xffffffu) >> mv.log_s) & (kOrdThreads - 1);
+        const uint64_t peers = match_bits(bin[k], 9, __ballot(ok[k]));
+        const unsigned below = mbcnt64(peers);
+        const int leader = peers ? __builtin_ctzll(peers) : 0;
+        unsigned old = 0;
+        if (ok[k] && below == 0) {
+          old = wcnt[w][bin[k]];
+          wcnt[w][bin[k]] = old + (unsigned)__popcll(peers);
+        }
+        wr[k] = (unsigned)__shfl((int)old, leader) + below;
+      }
+      __syncthreads();
+      uint16_t* bsr = bs + (size_t)r * (kOrdThreads + 1);
+      {  // bin totals and wave offsets (thread b owns bin b), then an exclusive scan over bins
+        const unsigned b = threadIdx.x;
+        unsigned c = 0;
+#pragma unroll
+        for (int ww = 0; ww < kOrdWaves; ++ww) {
+          const unsigned x = wcnt[ww][b];
+          wcnt[ww][b] = c;
+          c += x;
+        }
+        const unsigned inc = wave_incl_scan(c);
+        if (lane == kWave - 1) wsum[w] = inc;
+        __syncthreads();
+        unsigned off = inc - c;
+        for (unsigned ww = 0; ww < w; ++ww) off += wsum[ww];
+        bsr[b] = (uint16_t)off;
+        if (b == kOrdThreads - 1) bsr[kOrdThreads] = (uint16_t)(off + c);
+      }
+      __syncthreads();
+      uint16_t* pr = pos + (size_t)r * kOrdRound;
+#pragma unroll
+      for (int k = 0; k < kOrdBinK; ++k) {
+        if (!ok[k]) continue;
+        const uint32_t q = (uint32_t)r * kOrdRound + w * (kWave * kOrdBinK) + (uint32_t)k * kWave + lane;
+        pr[bsr[bin[k]] + wcnt[w][bin[k]] + wr[k]] = (uint16_t)q;  // (bsr[kOrdRound]: 4096 fits u16)
+      }
+#pragma unroll
+      for (int k = 0; k < kOrdBinK; ++k) h[k] = nx[k];
+    }
+    __syncthreads();
+    // ---- run: this thread's bin, round by round, kOrdBinBatch records loaded ahead
+    {
+      const unsigned b = threadIdx.x;
+      uint32_t r = 0, d = 0, e = 0;
+      if (rounds) {
+        d = bs[b];
+        e = bs[b + 1];
+      }
+      uint32_t mine = 0;
+      for (;;) {
+        uint64_t sl[kOrdBinBatch];
+        bool have[kOrdBinBatch];
+#pragma unroll
+        for (int k = 0; k < kOrdBinBatch; ++k) {
+          while (d >= e && r < rounds) {
+            if (++r >= rounds) break;
+            d = bs[(size_t)r * (kOrdThreads + 1) + b];
+            e = bs[(size_t)r * (kOrdThreads + 1) + b + 1];
+          }
+          have[k] = r < rounds && d < e;
+          sl[k] = 0;
+          if (have[k]) {
+            sl[k] = sbase | ((w0 + pos[(size_t)r * kOrdRound + d] + rot) & qmask);
+            ++d;
+          }
+        }
+        if (!have[0]) break;
+        u32x4 ha[kOrdBinBatch];
+#pragma unroll
+        for (int k = 0; k < kOrdBinBatch; ++k)
+          ha[k] = have[k] ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k])) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < kOrdBinBatch; ++k) {
+          if (!have[k]) continue;
+          u32x4 hb = {0u, 0u, 0u, 0u};
+          int64_t a2v = 0;
+          if (rec_is_long(ha[k])) {
+            hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
+            if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
+          }
+          const SortRec x = decode_sorted(ha[k], hb, a2v);
+          MsgRecord m;
+          m.actor = in_lds ? (x.mb >> mv.log_s) : x.mb;
+          m.method = (uint16_t)x.method;
+          m.flags = (uint16_t)x.flags;
+          m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
+          const ReplyRecord rr = run_handler(m, st, nst, delay_ticks, ob, true);
+          failed += rr.status != kStatusOk;
+          srep[sl[k]] = u32x4{(uint32_t)rr.value, (uint32_t)((uint64_t)rr.value >> 32), (uint32_t)rr.status, x.origin};
+          ++done;
+          ++mine;
+          if (!in_lds) vm_drain();  // global state: this store lands before the bin's next load
+        }
+      }
+      if (mine > 1) serial += mine - 1;
+    }
+    __syncthreads();  // the super-window's LDS is reused
+  }
+  if (in_lds)
+    for (uint32_t j = threadIdx.x; j < n_loc; j += kOrdThreads) state[s + (uint64_t)j * S] = st_lds[j];
+  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
+  __syncthreads();
+  block_add_stats(mv.stats, serial, kMbSerial, 0, -1, 0, -1);
+  if (threadIdx.x == 0) epoch_commit(mv, s, tot);
+}
+
 // Ordered drain's replies, staged at ring slots as {value, status, origin}, put
 // back into message order -- in RING order like the parallel drain: one block
 // per tile reads the tile's runs (whole lines), stages each reply at its place
@@ -1854,8 +2043,25 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     hipLaunchKernelGGL(mbx_drain_ordered_kernel<A12>, dim3(Sv), dim3(kOrdThreads), lds, st, mv, sort_gsum_,  \
                        ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);         \
   } while (0)
-    if (a12) PT_ORD(true);
-    else PT_ORD(false);
+    static const bool ord_win = getenv("PTYPE_ORD_DRAIN") && std::string(getenv("PTYPE_ORD_DRAIN")) == "win";
+    if (!ord_win) {
+      // the binned form: as many rounds per super-window as the LDS left by the state allows
+      const size_t cap = 160 * 1024 - 256;  // (the static words share the 160 KB)
+      uint32_t nr = kOrdBinRoundsMax;
+      while (nr > 1 && ord_bin_lds_bytes(nr, n_loc) > cap) --nr;
+      static bool attr = false;
+      if (!attr) {
+        PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ord_bin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)cap));
+        attr = true;
+      }
+      hipLaunchKernelGGL(mbx_drain_ord_bin_kernel, dim3(Sv), dim3(kOrdThreads), ord_bin_lds_bytes(nr, n_loc), st, mv,
+                         sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_, nr);
+    } else if (a12) {
+      PT_ORD(true);
+    } else {
+      PT_ORD(false);
+    }
 #undef PT_ORD
     PT_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST),
