@@ -78,6 +78,7 @@ constexpr int kOrdK = 4;
 constexpr int kOrdWin = kOrdThreads * kOrdK;  // records per window (2048)
 constexpr int kOrdWaves = kOrdThreads / kWave;
 constexpr uint32_t kOrdStateMax = 4096;  // a shard's actors whose state is staged in LDS (32 KB)
+constexpr int kSKSmall = 2;  // messages per thread of a small fused Send's tiles (1024-message tiles)
 }  // namespace
 
 // ---------------------------------------------------------------- K2s pass 1: count
@@ -406,12 +407,12 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
 // leave registers (the two-pass form wrote and re-read 4 B per message).
 __host__ __device__ constexpr size_t onesweep_lds_bytes(uint32_t S) { return (size_t)S * (8 + 4 + 4 + 4 * (kST / kWave)); }
 
-template <bool A2, bool MC>
-__device__ __forceinline__ void load_cols(const SortIn& in, uint32_t t, int64_t (&v0)[kSK], int64_t (&v1)[kSK],
-                                          int64_t (&v2)[kSK], uint32_t (&meth)[kSK]) {
+template <bool A2, bool MC, int SK = kSK>
+__device__ __forceinline__ void load_cols(const SortIn& in, uint32_t t, int64_t (&v0)[SK], int64_t (&v1)[SK],
+                                          int64_t (&v2)[SK], uint32_t (&meth)[SK]) {
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const int64_t i = tile_index(t, k);
+  for (int k = 0; k < SK; ++k) {
+    const int64_t i = tile_index<SK>(t, k);
     const bool ok = i < in.M;
     v0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
     v1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
@@ -476,7 +477,7 @@ __device__ __forceinline__ void rec8_next(const SortIn& in, uint32_t* r8w, uint3
 // epoch's total): 16 device-scope atomics per tile, ~2048 per counter at 8 Mi
 // messages -- against a look-back whose walk grows with the tiles in flight
 // (each hop a memory-side round trip).
-template <int MODE, bool A2, bool MC, bool LATE>
+template <int MODE, bool A2, bool MC, bool LATE, int SK = kSK>
 __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxView& mv, unsigned long long* __restrict__ desc,
                                                   unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                   uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
@@ -506,16 +507,16 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   // meet the lines in the L2 that took the sort's stores)
   const uint32_t t = reserve ? virt_block(blockIdx.x, gridDim.x) : tile_s;
   // the tile's columns: actors, then the arguments in flight across the gathers and the ranking
-  uint32_t a[kSK], mb[kSK], meth[kSK];
-  int64_t v0[kSK], v1[kSK], v2[kSK];
-  int r[kSK];
-  load_actors(in, t, a);
-  if constexpr (!LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
-  resolve_k<MODE>(in, a, r, mb);
-  uint32_t wr[kSK];
+  uint32_t a[SK], mb[SK], meth[SK];
+  int64_t v0[SK], v1[SK], v2[SK];
+  int r[SK];
+  load_actors<SK>(in, t, a);
+  if constexpr (!LATE) load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
+  resolve_k<MODE, SK>(in, a, r, mb);
+  uint32_t wr[SK];
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const bool ok = tile_index(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
+  for (int k = 0; k < SK; ++k) {
+    const bool ok = tile_index<SK>(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
     if (!ok) mb[k] = kNoSlot;
     const uint32_t sh = mb[k] & (S - 1);
     const uint64_t peers = match_bits(sh, mv.log_s, __ballot(ok));
@@ -594,7 +595,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
       tinfo[(size_t)t * 2 * S + S + s] = cc | (excl + c > rm ? kRunSpilled : 0u);
     }
   }
-  if constexpr (LATE) load_cols<A2, MC>(in, t, v0, v1, v2, meth);
+  if constexpr (LATE) load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
   // (in.rec8) the messages whose fields do not fit an 8-B record -- they spill -- and
   // the tile's fields OR-ed (their bit lengths size the next Send's records)
   uint32_t escm = 0;
@@ -603,7 +604,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   if (in.rec8) {
     const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
+    for (int k = 0; k < SK; ++k) {
       if (mb[k] == kNoSlot) continue;
       const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
       const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
@@ -631,8 +632,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   const bool wsidx = all_sidx || tile_spill;
   unsigned long long n_enq = 0, n_ovf = 0, n_miss = 0, n_spill = 0;
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const int64_t i = tile_index(t, k);
+  for (int k = 0; k < SK; ++k) {
+    const int64_t i = tile_index<SK>(t, k);
     if (i >= in.M) continue;
     const uint32_t origin = in.origin_base + (uint32_t)i;
     if (mb[k] == kNoSlot) {
@@ -663,7 +664,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
       const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
       const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
       reinterpret_cast<uint64_t*>(mv.rec)[slot] =
-          (uint64_t)(i & (kSTile - 1)) | ((uint64_t)mb[k] << 12) | (z0 << (12 + wm)) | (z1 << (12 + wm + w0));
+          (uint64_t)(i & ((kST * SK) - 1)) | ((uint64_t)mb[k] << 12) | (z0 << (12 + wm)) | (z1 << (12 + wm + w0));
     } else if (mt < 128u && fits_i32(v0[k]) && fits_i32(v1[k]) && v2[k] == 0) {
       *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
           u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)v0[k], (uint32_t)v1[k]};
@@ -729,13 +730,13 @@ __device__ __forceinline__ SortRec decode_sorted(const u32x4& ha, const u32x4& h
 }
 
 // An 8-B record (in.rec8) of the tile whose first message is `tile_origin`.
-template <bool FRESH>
+template <bool FRESH, int SK = kSK>
 __device__ __forceinline__ SortRec decode_rec8(uint64_t r, const SortIn& in, uint32_t w8, uint32_t tile_origin) {
   const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
   const uint64_t m0 = (1ull << w0) - 1;
   SortRec x;
   x.valid = true;
-  x.origin = tile_origin + (uint32_t)(r & (kSTile - 1));
+  x.origin = tile_origin + (uint32_t)(r & ((kST * SK) - 1));
   x.mb = (uint32_t)((r >> 12) & ((1ull << wm) - 1));
   x.method = in.method_uniform;
   x.flags = 0;
@@ -800,23 +801,23 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 // recorded, replies coalesced; a spilled message runs straight from the batch.
 //
 // The last block commits every shard (and clears the group sums).
-template <int FIXED, bool FRESH = false, bool R8 = false>
+template <int FIXED, bool FRESH = false, bool R8 = false, int SK = kSK>
 __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t t,
                                                const uint32_t* __restrict__ sidx, const uint32_t* __restrict__ rw,
                                                int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks,
                                                OutboxView ob, ReplyView rv, unsigned long long& done,
                                                unsigned long long& failed, unsigned long long& holes) {
-  uint32_t sl[kSK];
+  uint32_t sl[SK];
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const int64_t i = tile_index(t, k);
+  for (int k = 0; k < SK; ++k) {
+    const int64_t i = tile_index<SK>(t, k);
     sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
   }
   using RecT = typename std::conditional<R8, uint64_t, u32x4>::type;  // the ring record as loaded
   const uint32_t w8 = R8 ? *in.r8w : 0u;  // the 8-B field widths this Send's sort used
-  RecT ha[kSK];
+  RecT ha[SK];
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
+  for (int k = 0; k < SK; ++k) {
     if constexpr (R8) {
       const uint64_t* rp = reinterpret_cast<const uint64_t*>(mv.rec) + (sl[k] < kSpillSlot ? sl[k] : 0);
       ha[k] = sl[k] < kSpillSlot ? (FRESH ? __builtin_nontemporal_load(rp) : *rp) : 0ull;
@@ -826,11 +827,11 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
     }
   }
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
+  for (int k = 0; k < SK; ++k) {
     if (sl[k] == kNoSlot) continue;  // answered by the scatter (no actor / ring full)
     SortRec x;
     if (sl[k] == kSpillSlot) {  // its ring was full: the message runs straight from the batch
-      const int64_t i = tile_index(t, k);
+      const int64_t i = tile_index<SK>(t, k);
       x.valid = true;
       x.mb = rw[i];
       x.method = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
@@ -839,7 +840,7 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
       x.a1 = in.a1 ? in.a1[i] : 0;
       x.a2 = in.a2 ? in.a2[i] : 0;
     } else if constexpr (R8) {
-      x = decode_rec8<FRESH>(ha[k], in, w8, in.origin_base + t * kSTile);
+      x = decode_rec8<FRESH, SK>(ha[k], in, w8, in.origin_base + t * (kST * SK));
     } else {
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
@@ -850,7 +851,7 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
       }
       x = decode_sorted(ha[k], hb, a2v);
     }
-    const uint32_t origin = in.origin_base + (uint32_t)tile_index(t, k);
+    const uint32_t origin = in.origin_base + (uint32_t)tile_index<SK>(t, k);
     if (!x.valid) {
       ++holes;
       write_status(rv, origin, kStatusNotDelivered);
@@ -945,8 +946,8 @@ constexpr uint8_t kAbsent = 0xff;  // staged status: no record of this message i
 // NARROW (S <= 256): a 1-B owner table whose bytes are reused for the staged
 // statuses once the records are loaded -- 36 KB of LDS instead of 46 KB, four
 // blocks per CU (with at most 64 VGPRs: launch bounds 8 waves per SIMD)
-__host__ __device__ constexpr size_t ring_drain_lds_bytes(uint32_t S) {
-  return S <= 256 ? (size_t)kSTile * (8 + 1) + (size_t)S * 8 : (size_t)kSTile * (8 + 2 + 1) + (size_t)S * 8;
+__host__ __device__ constexpr size_t ring_drain_lds_bytes(uint32_t S, size_t tile = kSTile) {
+  return S <= 256 ? tile * (8 + 1) + (size_t)S * 8 : tile * (8 + 2 + 1) + (size_t)S * 8;
 }
 
 // Tile t's records, read in RING order from its runs (tinfo), each through the
@@ -961,7 +962,7 @@ struct DrainCounts {
 
 // (views and counts by value: references to a kernel's locals or arguments put
 // them in scratch)
-template <int FIXED, bool NARROW, bool FRESH, bool R8 = false>
+template <int FIXED, bool NARROW, bool FRESH, bool R8 = false, int SK = kSK>
 __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, uint32_t t,
                                                        const uint32_t* __restrict__ tinfo,
                                                        const uint32_t* __restrict__ sidx,
@@ -971,30 +972,30 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   unsigned long long done = 0, failed = 0, holes = 0;
   using OwnT = typename std::conditional<NARROW, uint8_t, uint16_t>::type;
   const uint32_t S = 1u << mv.log_s;
-  int64_t* sval = reinterpret_cast<int64_t*>(smem_rd);  // [kSTile] reply values by place in the tile
+  int64_t* sval = reinterpret_cast<int64_t*>(smem_rd);  // [(kST * SK)] reply values by place in the tile
   RunLds<OwnT> L;
-  L.bias = reinterpret_cast<uint32_t*>(sval + kSTile);
+  L.bias = reinterpret_cast<uint32_t*>(sval + (kST * SK));
   L.excl = L.bias + S;
   L.owner = reinterpret_cast<OwnT*>(L.excl + S);
-  // [kSTile] statuses, kAbsent = none (NARROW: the owner table's bytes, once the records are loaded)
-  uint8_t* sst = NARROW ? reinterpret_cast<uint8_t*>(L.owner) : reinterpret_cast<uint8_t*>(L.owner + kSTile);
-  const uint64_t i0 = (uint64_t)t * kSTile;
-  const uint32_t n_t = (uint32_t)min((uint64_t)kSTile, (uint64_t)in.M - i0);
+  // [(kST * SK)] statuses, kAbsent = none (NARROW: the owner table's bytes, once the records are loaded)
+  uint8_t* sst = NARROW ? reinterpret_cast<uint8_t*>(L.owner) : reinterpret_cast<uint8_t*>(L.owner + (kST * SK));
+  const uint64_t i0 = (uint64_t)t * (kST * SK);
+  const uint32_t n_t = (uint32_t)min((uint64_t)(kST * SK), (uint64_t)in.M - i0);
   if constexpr (!NARROW)
-    for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
+    for (uint32_t j = threadIdx.x; j < (kST * SK); j += kST) sst[j] = kAbsent;
   int spill = 0;
   const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
   if (spill) {  // some message of the tile spilled: the scatter left the tile's slot indices
-    drain_tile_msg<FIXED, FRESH, R8>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
+    drain_tile_msg<FIXED, FRESH, R8, SK>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
     return DrainCounts{done, failed, holes};
   }
   const uint64_t sbase_mask = (1ull << mv.log_q) - 1;
   using RecT = typename std::conditional<R8, uint64_t, u32x4>::type;  // the ring record as loaded
   const uint32_t w8 = R8 ? *in.r8w : 0u;  // the 8-B field widths this Send's sort used
-  RecT ha[kSK];
-  uint32_t sl[kSK];
+  RecT ha[SK];
+  uint32_t sl[SK];
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {  // ring order: lane-consecutive entries of the runs
+  for (int k = 0; k < SK; ++k) {  // ring order: lane-consecutive entries of the runs
     const uint32_t j = (uint32_t)k * kST + threadIdx.x;
     sl[k] = kNoSlot;
     if (j < T) {
@@ -1011,15 +1012,15 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   }
   if constexpr (NARROW) {  // every owner entry is read: its bytes become the status stage
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < kSTile; j += kST) sst[j] = kAbsent;
+    for (uint32_t j = threadIdx.x; j < (kST * SK); j += kST) sst[j] = kAbsent;
     __syncthreads();
   }
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
+  for (int k = 0; k < SK; ++k) {
     if (sl[k] == kNoSlot) continue;
     SortRec x;
     if constexpr (R8) {
-      x = decode_rec8<FRESH>(ha[k], in, w8, in.origin_base + (uint32_t)i0);
+      x = decode_rec8<FRESH, SK>(ha[k], in, w8, in.origin_base + (uint32_t)i0);
     } else {
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
@@ -1048,7 +1049,7 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {  // the tile's replies, coalesced (misses were answered by the scatter)
+  for (int k = 0; k < SK; ++k) {  // the tile's replies, coalesced (misses were answered by the scatter)
     const uint32_t j = (uint32_t)k * kST + threadIdx.x;
     if (j < n_t && sst[j] != kAbsent) put_reply(rv, in.origin_base + (uint32_t)(i0 + j), sval[j], sst[j]);
   }
@@ -1094,7 +1095,7 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
 // waits at a kernel boundary for the slowest tile.  The last block to finish
 // commits every shard's epoch (tail = head = tail + total) and advances the
 // look-back tag.  PTYPE_MBOX_FUSED=0: the separate kernels.
-template <int MODE, bool A2, bool MC, int FIXED, bool R8>
+template <int MODE, bool A2, bool MC, int FIXED, bool R8, int SK = kSK>
 __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
                                                             unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                             uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
@@ -1105,13 +1106,13 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
                                                             uint32_t* __restrict__ r8host) {
   extern __shared__ __align__(16) unsigned char smem_sd[];
   const uint32_t S = 1u << mv.log_s;
-  const uint32_t t = onesweep_tile<MODE, A2, MC, false>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, true, false,
-                                                        smem_sd, reserve);
+  const uint32_t t = onesweep_tile<MODE, A2, MC, false, SK>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, true, false,
+                                                            smem_sd, reserve);
   // every wave's ring stores are out before any wave reads the tile's runs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const DrainCounts dc = drain_ring_tile<FIXED, true, true, R8>(mv, in, t, tinfo, sidx, rw, state, n_state,
-                                                                delay_ticks, ob, rv, smem_sd);
+  const DrainCounts dc = drain_ring_tile<FIXED, true, true, R8, SK>(mv, in, t, tinfo, sidx, rw, state, n_state,
+                                                                    delay_ticks, ob, rv, smem_sd);
   block_add_stats(mv.stats, dc.done, kMbProcessed, dc.failed, kMbFailed, dc.holes, kMbHoles);
   __shared__ bool last;
   if (threadIdx.x == 0) {
@@ -1723,6 +1724,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   hipStream_t st = as_stream(a.stream);
   const int64_t tiles = (a.M + kSTile - 1) / kSTile;
   if (tiles > 0xffffffffll) throw std::invalid_argument("mailbox send: batch too large");
+  // per-tile workspace sized for the small tiles a fused Send may take (kSKSmall)
+  const int64_t tiles_ws = (a.M + kST * kSKSmall - 1) / (kST * kSKSmall);
   // per-message workspace (route words, ring slots) and per-tile runs: grown outside graph capture
   if (!a.arrival && (uint64_t)a.M > sort_cap_) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1736,10 +1739,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       }
     PT_HIP_CHECK(hipMalloc((void**)&sort_rw_, (size_t)a.M * 4));
     PT_HIP_CHECK(hipMalloc((void**)&sort_sidx_, (size_t)a.M * 4));
-    PT_HIP_CHECK(hipMalloc((void**)&sort_tinfo_, (size_t)tiles * 2 * S * 4));
+    PT_HIP_CHECK(hipMalloc((void**)&sort_tinfo_, (size_t)tiles_ws * 2 * S * 4));
     // look-back descriptors: zero = no tag (every Send's tag is >= 1)
-    PT_HIP_CHECK(hipMalloc((void**)&sort_desc_, (size_t)tiles * S * 8));
-    PT_HIP_CHECK(hipMemsetAsync(sort_desc_, 0, (size_t)tiles * S * 8, st));
+    PT_HIP_CHECK(hipMalloc((void**)&sort_desc_, (size_t)tiles_ws * S * 8));
+    PT_HIP_CHECK(hipMemsetAsync(sort_desc_, 0, (size_t)tiles_ws * S * 8, st));
     PT_HIP_CHECK(hipStreamSynchronize(st));
     sort_cap_ = (uint64_t)a.M;
   }
@@ -1890,7 +1893,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   static const int rec8_env = getenv("PTYPE_MBOX_REC8") ? atoi(getenv("PTYPE_MBOX_REC8")) : -1;
   const bool r8 = (rec8_env == 1 || (rec8_env < 0 && tiles > 512)) && sort_mode == 1 && !a.ordered && !a.arrival &&
                   !a.a2 && !a.method_col && mv.planar && !all_sidx;
-  if (r8 && (!r8w_ || r8_tiles_ < (uint64_t)tiles)) {  // (outside a capture: grown with the sort workspace)
+  if (r8 && (!r8w_ || r8_tiles_ < (uint64_t)tiles_ws)) {  // (outside a capture: grown with the sort workspace)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
       throw std::runtime_error("mailbox send: first 8-B-record Send of this size inside a graph capture (warm up first)");
@@ -1908,8 +1911,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       *r8host_ = w;
     }
     if (r8max_) PT_HIP_CHECK(hipFree(r8max_));
-    PT_HIP_CHECK(hipMalloc((void**)&r8max_, (size_t)tiles * 4));
-    r8_tiles_ = (uint64_t)tiles;
+    PT_HIP_CHECK(hipMalloc((void**)&r8max_, (size_t)tiles_ws * 4));
+    r8_tiles_ = (uint64_t)tiles_ws;
   }
   // fields that outgrew 64 bits (the last Send's widths, bit 31): 16-B records from here on
   const bool r8_on = r8 && !(__atomic_load_n(r8host_, __ATOMIC_RELAXED) & 0x80000000u);
@@ -1968,13 +1971,24 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else PT_SCAT(false, false);
 #undef PT_SCAT
   } else if (!a.ordered && !all_sidx && Sv <= 256 && fused_ok(tiles)) {
-    // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel)
-    const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv));
-#define PT_SD3(MO, A2, MC, FX, R8)                                                                                  \
-  hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, R8>), dim3(in.tiles), dim3(kST), lds, st, in, mv,          \
+    // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel).  Small batches
+    // take 1024-message tiles (SK = 2: 4x the blocks, ~1/4 of the registers per wave), so a
+    // 1 Mi Send has 1024 blocks -- 4 per CU -- instead of one;
+    // PTYPE_MBOX_SK=2 / 8 forces the tile.
+    static const int sk_env = getenv("PTYPE_MBOX_SK") ? atoi(getenv("PTYPE_MBOX_SK")) : 0;
+    const bool small = sk_env == kSKSmall || (sk_env != kSK && tiles < 1024);
+    if (small) in.tiles = (uint32_t)((a.M + kST * kSKSmall - 1) / (kST * kSKSmall));
+    const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv, small ? kST * kSKSmall : kSTile));
+#define PT_SD4(MO, A2, MC, FX, R8, SKV)                                                                             \
+  hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, R8, SKV>), dim3(in.tiles), dim3(kST), lds, st, in, mv,     \
                      sort_desc_,                                                                                     \
                      sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv, (int64_t*)a.state, a.n_state,    \
                      a.delay_ticks, ob, sort_ticket_, reserve, r8host_)
+#define PT_SD3(MO, A2, MC, FX, R8)                 \
+  do {                                             \
+    if (small) PT_SD4(MO, A2, MC, FX, R8, kSKSmall); \
+    else PT_SD4(MO, A2, MC, FX, R8, kSK);          \
+  } while (0)
 #define PT_SD2(MO, A2, MC, FX)                               \
   do {                                                       \
     if (!(A2) && !(MC) && r8_on) PT_SD3(MO, false, false, FX, true); \
@@ -1996,6 +2010,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_SD
 #undef PT_SD2
 #undef PT_SD3
+#undef PT_SD4
     PT_HIP_CHECK(hipGetLastError());
     return;
   } else {
@@ -2046,15 +2061,21 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     static const bool ord_win = getenv("PTYPE_ORD_DRAIN") && std::string(getenv("PTYPE_ORD_DRAIN")) == "win";
     if (!ord_win) {
       // the binned form: as many rounds per super-window as the LDS left by the state allows
-      const size_t cap = 160 * 1024 - 256;  // (the static words share the 160 KB)
+      // (the largest dynamic LDS the runtime grants this kernel: its static words and the stats
+      // partials share the CU's 160 KB; found once, stepping down from 156 KB)
+      static size_t cap = 0;
+      if (!cap) {
+        for (size_t c = 156 * 1024; c >= 64 * 1024; c -= 4 * 1024)
+          if (hipFuncSetAttribute((const void*)mbx_drain_ord_bin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)c) == hipSuccess) {
+            cap = c;
+            break;
+          }
+        (void)hipGetLastError();
+        if (!cap) throw std::runtime_error("mailbox send: no LDS for the binned ordered drain");
+      }
       uint32_t nr = kOrdBinRoundsMax;
       while (nr > 1 && ord_bin_lds_bytes(nr, n_loc) > cap) --nr;
-      static bool attr = false;
-      if (!attr) {
-        PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ord_bin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)cap));
-        attr = true;
-      }
       hipLaunchKernelGGL(mbx_drain_ord_bin_kernel, dim3(Sv), dim3(kOrdThreads), ord_bin_lds_bytes(nr, n_loc), st, mv,
                          sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_, nr);
     } else if (a12) {

@@ -70,15 +70,15 @@ __device__ __forceinline__ uint32_t virt_block(uint32_t b, uint32_t G) {
 // (computed), 3 rank byte gather -- stateless batches only: `mb` is then the
 // actor id itself (the receiver's stateless handler needs no mailbox), except for
 // ids the byte table sends to the hash table, which keep the probed mailbox.
-template <int MODE>
-__device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[kSK], int (&r)[kSK],
-                                          uint32_t (&mb)[kSK]) {
+template <int MODE, int SK = kSK>
+__device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[SK], int (&r)[SK],
+                                          uint32_t (&mb)[SK]) {
   if constexpr (MODE == 3) {
-    uint32_t w[kSK];
+    uint32_t w[SK];
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) w[k] = a[k] < in.n_dir ? (uint32_t)in.dirr[a[k]] : (uint32_t)kRankFallback;
+    for (int k = 0; k < SK; ++k) w[k] = a[k] < in.n_dir ? (uint32_t)in.dirr[a[k]] : (uint32_t)kRankFallback;
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
+    for (int k = 0; k < SK; ++k) {
       r[k] = w[k] == kRankMissing ? -1 : (int)w[k];
       mb[k] = a[k];
       if (w[k] == kRankFallback) {
@@ -87,11 +87,11 @@ __device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[
       }
     }
   } else if constexpr (MODE == 1) {
-    uint32_t w[kSK];
+    uint32_t w[SK];
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) w[k] = a[k] < in.n_dir ? dir_load(in.dir + a[k], in.dir_nt) : kDirFallback;
+    for (int k = 0; k < SK; ++k) w[k] = a[k] < in.n_dir ? dir_load(in.dir + a[k], in.dir_nt) : kDirFallback;
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
+    for (int k = 0; k < SK; ++k) {
       r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
       mb[k] = w[k] >> 8;
       if (w[k] == kDirFallback) {
@@ -101,7 +101,7 @@ __device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
+    for (int k = 0; k < SK; ++k) {
       if (MODE == 2 && a[k] < in.n_dir) {
         r[k] = in.aw_shift >= 0 ? (int)(a[k] & (in.aw - 1)) : (int)(a[k] % in.aw);
         mb[k] = in.aw_shift >= 0 ? a[k] >> in.aw_shift : a[k] / in.aw;
@@ -117,14 +117,18 @@ __device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[
 
 // Message i of tile t for (item k, lane) of wave w: a wave owns a contiguous run
 // of the tile, so message order within a tile is (wave, item, lane).
+// SK: messages per thread of the tile (kSK by default; the fused mailbox Send of a
+// small batch takes smaller tiles, mailbox_sort.hip).
+template <int SK = kSK>
 __device__ __forceinline__ int64_t tile_index(uint32_t t, int k) {
-  return (int64_t)t * kSTile + (threadIdx.x / kWave) * kSWave + k * kWave + lane_id();
+  return (int64_t)t * (kST * SK) + (threadIdx.x / kWave) * (SK * kWave) + k * kWave + lane_id();
 }
 
-__device__ __forceinline__ void load_actors(const SortIn& in, uint32_t t, uint32_t (&a)[kSK]) {
+template <int SK = kSK>
+__device__ __forceinline__ void load_actors(const SortIn& in, uint32_t t, uint32_t (&a)[SK]) {
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const int64_t i = tile_index(t, k);
+  for (int k = 0; k < SK; ++k) {
+    const int64_t i = tile_index<SK>(t, k);
     a[k] = i < in.M ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
   }
 }

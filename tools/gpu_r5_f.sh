@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 session F: the binned ordered drain -- mailbox / ordered GPU tests, then
-# the SeqFold line binned vs windowed (PTYPE_ORD_DRAIN=win) and its kernel stats.
+# the SeqFold line binned vs windowed (PTYPE_ORD_DRAIN=win) and its kernel stats, the
+# 1 Mi step with 1024- vs 4096-message fused tiles (PTYPE_MBOX_SK=8) and its kernel stats.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}" && mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -18,3 +19,10 @@ done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_seqp -o prof -- \
   python3 bench.py --method seqfold --steps 8 --warmup 4 --rtt-calls 0 --no-secondary > gpurun_out/${TAG}_seqp.log 2>&1 || exit 4
 python3 tools/kstats.py gpurun_out/${TAG}_seqp/prof_kernel_stats.csv | head -8
+for K in "X=0" "PTYPE_MBOX_SK=8"; do
+  env $K timeout -k 10 200 python3 bench.py --no-secondary --rtt-calls 0 --msgs-per-gpu 1048576 > gpurun_out/${TAG}_1m_$K.json 2>gpurun_out/${TAG}_1m_$K.err || exit 5
+  echo "1m [$K] $(val gpurun_out/${TAG}_1m_$K.json)"
+done
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_1mp -o prof -- \
+  python3 bench.py --msgs-per-gpu 1048576 --steps 8 --warmup 4 --rtt-calls 0 --no-secondary > gpurun_out/${TAG}_1mp.log 2>&1 || exit 6
+python3 tools/kstats.py gpurun_out/${TAG}_1mp/prof_kernel_stats.csv | head -6
