@@ -362,7 +362,10 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
 // that region's counter (rcnt), and the last block to finish writes the
 // headers from the totals (and clears the counters for the next chunk).
 
-template <int MODE, int S>
+// SK: messages per thread of a tile (tile = 512 * SK); EARLY: the argument columns are
+// loaded with the actors (in flight across the gather, the ranking and the reservation)
+// instead of after it -- more registers, less exposed latency.
+template <int MODE, int S, int SK = kSK, bool EARLY = false>
 __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long long* __restrict__ desc,
                                                  unsigned* __restrict__ tctr, unsigned* __restrict__ ticket,
                                                  uint32_t* __restrict__ sendbuf, int64_t req_stride,
@@ -395,16 +398,25 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
   const uint32_t t = tile_s, tag = tag_s;
   const uint32_t rbits = R > 1 ? 32 - __builtin_clz((uint32_t)R - 1) : 0;
   // phase 1: routes and ranks (a small register file: occupancy hides the gathers)
-  uint32_t pr[kSK], mb[kSK];
+  uint32_t pr[SK], mb[SK];
+  int64_t e0[EARLY ? SK : 1], e1[EARLY ? SK : 1];
   uint32_t mbmax = 0;
   {
-    uint32_t a[kSK];
-    int r[kSK];
-    load_actors(in, t, a);
-    resolve_k<MODE>(in, a, r, mb);
+    uint32_t a[SK];
+    int r[SK];
+    load_actors<SK>(in, t, a);
+    if constexpr (EARLY) {
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      const bool ok = tile_index(t, k) < in.M && r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
+      for (int k = 0; k < SK; ++k) {
+        const int64_t i = tile_index<SK>(t, k);
+        e0[k] = i < in.M ? __builtin_nontemporal_load(in.a0 + i) : 0;
+        e1[k] = i < in.M && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+      }
+    }
+    resolve_k<MODE, SK>(in, a, r, mb);
+#pragma unroll
+    for (int k = 0; k < SK; ++k) {
+      const bool ok = tile_index<SK>(t, k) < in.M && r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
       if (ok) mbmax = mb[k] > mbmax ? mb[k] : mbmax;
       const uint32_t bk = ok ? (uint32_t)r[k] : 0u;
       const uint64_t peers = match_bits(bk, rbits, __ballot(ok));
@@ -462,8 +474,8 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
   MetaAcc acc;
   uint32_t n_ovf = 0;
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const int64_t i = tile_index(t, k);
+  for (int k = 0; k < SK; ++k) {
+    const int64_t i = tile_index<SK>(t, k);
     if (i >= in.M) continue;
     const uint32_t rk = pr[k] & 0xffu;
     if (rk == 0xffu) {
@@ -476,8 +488,14 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
       ++n_ovf;
       continue;
     }
-    const int64_t x0 = __builtin_nontemporal_load(in.a0 + i);
-    const int64_t x1 = in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    int64_t x0, x1;
+    if constexpr (EARLY) {
+      x0 = e0[k];
+      x1 = e1[k];
+    } else {
+      x0 = __builtin_nontemporal_load(in.a0 + i);
+      x1 = in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    }
     const int64_t x2 = in.a2 ? __builtin_nontemporal_load(in.a2 + i) : 0;
     const uint32_t meth = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
     const uint64_t z0 = zz_enc(x0), z1 = zz_enc(x1), z2 = in.a2 ? zz_enc(x2) : 0ull;
@@ -531,9 +549,9 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
       bool reserve, bool reject_ordered
 #define PT_SX_OS_ARGS \
   in, R, desc, tctr, ticket, sendbuf, req_stride, C, caps, hdr_word3, rank_self, L, perm, meta, stats, rcnt, reserve, reject_ordered
-template <int MODE, int S>
+template <int MODE, int S, int SK = kSK, bool EARLY = false>
 __global__ __launch_bounds__(kST) void sx_onesweep_kernel(PT_SX_OS_PARAMS) {
-  sx_onesweep_body<MODE, S>(PT_SX_OS_ARGS);
+  sx_onesweep_body<MODE, S, SK, EARLY>(PT_SX_OS_ARGS);
 }
 #undef PT_SX_OS_PARAMS
 #undef PT_SX_OS_ARGS
@@ -826,7 +844,7 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
   }
   PT_HIP_CHECK(hipMalloc(&hist_, (size_t)kMboxSortHistWords * 4));
   PT_HIP_CHECK(hipMalloc(&boff_, (size_t)kXMaxBuckets * 4));
-  const int64_t max_tiles = (max_chunk + kSTile - 1) / kSTile;
+  const int64_t max_tiles = (max_chunk + kSTile / 2 - 1) / (kSTile / 2);  // (2048-message tiles: PTYPE_SX_TILE=4)
   PT_HIP_CHECK(hipMalloc(&desc_, (size_t)std::max<int64_t>(max_tiles, 1) * R * 8));
   PT_HIP_CHECK(hipMemset(desc_, 0, (size_t)std::max<int64_t>(max_tiles, 1) * R * 8));  // tag 0: never a live tag
   PT_HIP_CHECK(hipMalloc(&tctr_, 2 * sizeof(unsigned)));
@@ -1232,11 +1250,27 @@ void SortedExchange::send(const SxSend& a) {
     if (!sharded && in.tiles > 0 && (sx_mode != 2 || mode == 3)) {
       const uint32_t hdr3 =
           ((uint32_t)(kFlagValid | (mode == 3 ? kFlagActorIds : 0)) << 16) | (uint32_t)a.method_uniform;
+      // PTYPE_SX_TILE=4 / 4e / 8e (experiments, 8-B records of modes 1 and 3): 2048-message tiles
+      // (SK = 4), and/or the argument columns loaded with the actors (e = early)
+      static const char* sx_tile = getenv("PTYPE_SX_TILE");
+      static const int tile_sk = sx_tile && sx_tile[0] == '4' ? 4 : kSK;
+      static const bool tile_early = sx_tile && sx_tile[0] && sx_tile[1] == 'e';
+      SortIn in_t = in;
+      in_t.tiles = (uint32_t)((m + kST * tile_sk - 1) / (kST * tile_sk));
+#define PT_SX_OS1(MO, SV, SKV, EV)                                                                                 \
+  hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV, SKV, EV>), dim3(in_t.tiles), dim3(kST), 0, cs, in_t, R_, desc_,  \
+                     tctr_, ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm,                     \
+                     (unsigned long long*)meta, stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered)
 #define PT_SX_OS(MO, SV)                                                                                           \
   do {                                                                                                             \
-      hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_,      \
-                         ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm,                        \
-                         (unsigned long long*)meta, stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered);      \
+    if ((MO == 1 || MO == 3) && SV == 2 && (tile_sk != kSK || tile_early)) {                                       \
+      if (tile_sk == 4 && tile_early) PT_SX_OS1(MO, SV, 4, true);                                                  \
+      else if (tile_sk == 4) PT_SX_OS1(MO, SV, 4, false);                                                          \
+      else PT_SX_OS1(MO, SV, kSK, true);                                                                           \
+    } else {                                                                                                       \
+      in_t.tiles = in.tiles;                                                                                       \
+      PT_SX_OS1(MO, SV, kSK, false);                                                                               \
+    }                                                                                                              \
   } while (0)
 #define PT_SX_OS_S(MO)              \
   switch (S) {                      \
@@ -1258,6 +1292,7 @@ void SortedExchange::send(const SxSend& a) {
       }
 #undef PT_SX_OS_S
 #undef PT_SX_OS
+#undef PT_SX_OS1
       PT_HIP_CHECK(hipGetLastError());
       PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
       PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
