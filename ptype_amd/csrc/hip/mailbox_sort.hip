@@ -687,15 +687,15 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   return t;
 }
 
-template <int MODE, bool A2, bool MC, bool LATE>
+template <int MODE, bool A2, bool MC, bool LATE, int SK = kSK>
 __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
                                                            unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                            uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
                                                            uint32_t* __restrict__ rw, ReplyView rv, bool spill,
                                                            bool all_sidx, bool reserve) {
   extern __shared__ __align__(16) unsigned char smem_os[];
-  (void)onesweep_tile<MODE, A2, MC, LATE>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill, all_sidx, smem_os,
-                                          reserve);
+  (void)onesweep_tile<MODE, A2, MC, LATE, SK>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill, all_sidx, smem_os,
+                                              reserve);
 }
 
 // ---------------------------------------------------------------- compact record decode
@@ -1056,7 +1056,7 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   return DrainCounts{done, failed, holes};
 }
 
-template <int FIXED, bool NARROW, bool R8>
+template <int FIXED, bool NARROW, bool R8, int SK = kSK>
 __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ tinfo,
                                                              const uint32_t* __restrict__ sidx,
                                                              const uint32_t* __restrict__ rw,
@@ -1071,8 +1071,8 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
   // tiles dealt XCD by XCD like the scatter's blocks (whose writes the XCD's L2 may still hold)
   const uint32_t t = virt_block(blockIdx.x, gridDim.x);
   if (t < in.tiles)
-    dc = drain_ring_tile<FIXED, NARROW, false, R8>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob, rv,
-                                                   smem_rd);
+    dc = drain_ring_tile<FIXED, NARROW, false, R8, SK>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob,
+                                                       rv, smem_rd);
   block_add_stats(mv.stats, dc.done, kMbProcessed, dc.failed, kMbFailed, dc.holes, kMbHoles);
   __shared__ bool last;
   if (threadIdx.x == 0) last = last_block_ticket(ticket);
@@ -1785,7 +1785,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.G = (uint32_t)G;
   in.tpb = (uint32_t)((tiles + G - 1) / G);
   // one block per tile (tile-granular kernels), dealt XCD by XCD: a multiple of 8
-  const uint32_t tile_grid = (uint32_t)(tiles >= 8 ? (tiles + 7) / 8 * 8 : tiles);
+  uint32_t tile_grid = (uint32_t)(tiles >= 8 ? (tiles + 7) / 8 * 8 : tiles);
   // the sort: one pass with look-back, or count + scatter -- for batches under 1024 tiles (4 Mi msgs) and
   // with PTYPE_MBOX_SORT=twopass (measured: 8 Mi msgs 0.212-0.221 vs 0.228-0.230 ms per Send; 1 Mi msgs
   // 0.047-0.049 vs 0.043: a small grid cannot hide the look-back's round trips); PTYPE_MBOX_SORT=onepass forces it
@@ -1874,6 +1874,11 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
   const bool all_sidx = msg_drain && !a.ordered;
   const bool reserve = !a.ordered && reserve_ok() && sort_mode == 1;  // (one-pass: tiles reserve runs)
+  static const int sk_mid_env = getenv("PTYPE_MBOX_SK") ? atoi(getenv("PTYPE_MBOX_SK")) : 0;
+  // (the unfused one-pass Send with 2048-message tiles: set below when it is the path taken)
+  const bool mid_ok = sk_mid_env == 4 && !a.ordered && !a.arrival && !all_sidx && sort_mode == 1 && !a.a2 &&
+                      !a.method_col && !(!a.ordered && !all_sidx && Sv <= 256 && fused_ok(tiles));
+  bool mid = false;
   if (reserve) {
     if (!sort_resv_) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -2014,13 +2019,25 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     PT_HIP_CHECK(hipGetLastError());
     return;
   } else {
-    // one block per tile, claimed in launch order (the grid is exactly the tile count)
+    // one block per tile, claimed in launch order (the grid is exactly the tile count).
+    // PTYPE_MBOX_SK=4 (experiment; stateless two-column batches, ring-order drain): 2048-message
+    // tiles for the sort and the drain -- fewer registers per wave, more blocks per CU
+    mid = mid_ok && !late;
+    if (mid) {
+      in.tiles = (uint32_t)((a.M + kST * 4 - 1) / (kST * 4));
+      tile_grid = in.tiles >= 8 ? (in.tiles + 7) / 8 * 8 : in.tiles;
+    }
     // (PTYPE_OS_LATE=1: arguments loaded after the look-back, 87 instead of 115 VGPRs -- measured slower,
     // 0.231 vs 0.223 ms per 8 Mi Send: the loads' latency is then exposed)
-#define PT_OS2(MO, A2, MC, LT)                                                                                     \
-  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv), st, \
-                     in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx, \
-                     reserve)
+#define PT_OS3(MO, A2, MC, LT, SKV)                                                                                \
+  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT, SKV>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv),  \
+                     st, in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered,      \
+                     all_sidx, reserve)
+#define PT_OS2(MO, A2, MC, LT)                                     \
+  do {                                                             \
+    if (mid && !(A2) && !(MC) && !(LT)) PT_OS3(MO, false, false, false, 4); \
+    else PT_OS3(MO, A2, MC, LT, kSK);                              \
+  } while (0)
 #define PT_OS1(MO, A2, MC)              \
   do {                                  \
     if (late) PT_OS2(MO, A2, MC, true); \
@@ -2037,6 +2054,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_OS
 #undef PT_OS1
 #undef PT_OS2
+#undef PT_OS3
   }
   PT_HIP_CHECK(hipGetLastError());
   const size_t ring_lds = ring_drain_lds_bytes(Sv);
@@ -2098,12 +2116,17 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_DMSG
   } else {
     static const bool narrow_ok = !(getenv("PTYPE_DRAIN_NARROW") && std::string(getenv("PTYPE_DRAIN_NARROW")) == "0");
-#define PT_DRING2(FX, NW, R8)                                                                                   \
-  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, NW, R8>), dim3(tile_grid), dim3(kST),                           \
-                     NW ? ring_lds : (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, mv, in,                 \
-                     (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_,       \
-                     (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_, \
+#define PT_DRING3(FX, NW, R8, SKV)                                                                               \
+  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, NW, R8, SKV>), dim3(tile_grid), dim3(kST),                         \
+                     NW ? ring_drain_lds_bytes(Sv, (size_t)kST * SKV) : (size_t)kST * SKV * (8 + 2 + 1) + (size_t)Sv * 8, \
+                     st, mv, in, (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_, \
+                     (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_,        \
                      sort_tctr_, r8host_)
+#define PT_DRING2(FX, NW, R8)                      \
+  do {                                             \
+    if (mid && (NW)) PT_DRING3(FX, true, R8, 4);   \
+    else PT_DRING3(FX, NW, R8, kSK);               \
+  } while (0)
 #define PT_DRING1(FX, NW)                     \
   do {                                        \
     if (r8_on) PT_DRING2(FX, NW, true);       \
@@ -2119,6 +2142,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_DRING
 #undef PT_DRING1
 #undef PT_DRING2
+#undef PT_DRING3
   }
   PT_HIP_CHECK(hipGetLastError());
 }

@@ -13,3 +13,13 @@ for K in "X=0" "PTYPE_SX_TILE=4" "PTYPE_SX_TILE=4e" "PTYPE_SX_TILE=8e" "X=1"; do
   env $K timeout -k 10 200 $L8 > gpurun_out/${TAG}_l8_$K.json 2>gpurun_out/${TAG}_l8_$K.err || exit 3
   echo "l8 [$K] $(val gpurun_out/${TAG}_l8_$K.json)"
 done
+# the ordered (SeqFold) Send's sort: one pass with look-back (default) vs count + scan + scatter
+for K in "X=0" "PTYPE_MBOX_SORT=twopass" "PTYPE_MBOX_SORT=ldscount"; do
+  env $K timeout -k 10 200 python3 bench.py --no-secondary --rtt-calls 0 --method seqfold > gpurun_out/${TAG}_seq_$K.json 2>gpurun_out/${TAG}_seq_$K.err || exit 4
+  echo "seqfold [$K] $(val gpurun_out/${TAG}_seq_$K.json)"
+done
+# the headline 8 Mi step: 4096- vs 2048-message tiles for the unfused sort + ring drain
+for K in "X=0" "PTYPE_MBOX_SK=4"; do
+  env $K timeout -k 10 200 python3 bench.py --no-secondary --rtt-calls 0 > gpurun_out/${TAG}_8m_$K.json 2>gpurun_out/${TAG}_8m_$K.err || exit 5
+  echo "8m [$K] $(val gpurun_out/${TAG}_8m_$K.json)"
+done
