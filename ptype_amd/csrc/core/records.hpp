@@ -37,6 +37,16 @@ enum MethodId : uint16_t {
 // Outside a dispatcher with a relay table: kStatusNoMethod.
 constexpr uint16_t kMethodRelay = 0x7e;
 
+// An actor handler that decides to call another actor and continues on its reply
+// (the optimus coordinator: coordinator.go:75-89 fans candidates out to Prime
+// workers and counts the primes).  Local actor A, a0 = candidate n, a1 = worker
+// count W, a2 = first worker id B (remote actors B .. B + W - 1 of the relay
+// peer).  The handler picks the worker itself (B + hash(n) % W), asks it
+// PrimeCheck(2, isqrt(n) + 1, n) through the relay, and on the reply adds 1 to
+// A's state if n is prime; this call's reply is A's tally after it.  Served like
+// kMethodRelay (a dispatcher with a relay table); elsewhere kStatusNoMethod.
+constexpr uint16_t kMethodCoordPrime = 0x7d;
+
 // Multiplier of kSeqFold (odd, so the fold is a bijection of the prior state).
 constexpr uint64_t kFoldMul = 0x100000001b3ull;
 

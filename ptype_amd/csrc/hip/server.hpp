@@ -194,6 +194,8 @@ struct RelayRegs {
   XLane* x = nullptr;
   XReply* rp = nullptr;
   bool suspect = false;
+  uint32_t cont = 0;  // kMethodCoordPrime: the local actor + 1 whose continuation runs on the reply
+  int64_t cont_n = 0;  // ... and its candidate
 };
 // slot words through memory-side atomics: the wave may be relaunched on another
 // XCD, whose L2 could hold a line of the table from an earlier run
@@ -225,7 +227,7 @@ __device__ __forceinline__ void relay_store(RelayTable* rt, const RelayRegs& g) 
 // replies written here); clear suspect slots whose late reply landed.  Returns
 // the number of ring requests completed (wave-uniform).
 __device__ __forceinline__ unsigned relay_poll(RelayRegs& g, ReplySlot* __restrict__ rep, uint64_t ring_mask,
-                                               uint64_t now) {
+                                               uint64_t now, int64_t* __restrict__ state, uint32_t n_state) {
   bool fin = false;
   if (g.pend || g.suspect) {
     const uint64_t tag = sys_ld(&g.rp->tag);
@@ -238,8 +240,20 @@ __device__ __forceinline__ unsigned relay_poll(RelayRegs& g, ReplySlot* __restri
     if (g.pend) {
       const uint64_t seq = g.pend - 1;
       if (got) {
-        sys_st16(reinterpret_cast<uint64_t*>(&rep[seq & ring_mask]), (uint64_t)v,
-                 reply_tag(seq, (uint32_t)(tag & 0xff)));
+        uint32_t st = (uint32_t)(tag & 0xff);
+        if (g.cont) {  // the coordinator's continuation: tally a prime into its own state
+          const uint32_t a = g.cont - 1;
+          if (!state || a >= n_state) {
+            v = 0, st = kStatusNoActor;
+          } else if (st == kStatusOk) {
+            const bool prime = g.cont_n >= 2 && v == g.cont_n;  // no divisor in [2, isqrt(n)]
+            unsigned long long* sp = reinterpret_cast<unsigned long long*>(state + a);
+            v = prime ? (int64_t)atomicAdd(sp, 1ull) + 1
+                      : (int64_t)__hip_atomic_load(sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          g.cont = 0;
+        }
+        sys_st16(reinterpret_cast<uint64_t*>(&rep[seq & ring_mask]), (uint64_t)v, reply_tag(seq, st));
         g.seq += 1;
         g.pend = 0;
         fin = true;
@@ -247,6 +261,7 @@ __device__ __forceinline__ unsigned relay_poll(RelayRegs& g, ReplySlot* __restri
         sys_st16(reinterpret_cast<uint64_t*>(&rep[seq & ring_mask]), 0ull, reply_tag(seq, kStatusNotDelivered));
         g.suspect = true;  // the peer may still answer call g.seq
         g.pend = 0;
+        g.cont = 0;
         fin = true;
       }
     } else if (got) {  // a suspect slot's late reply: the lane is in step again
@@ -299,12 +314,30 @@ __device__ __forceinline__ unsigned relay_dispatch(RelayRegs& g, RelayQueue& rq,
   if (((free_mask >> lane) & 1) && q < avail) {
     const uint64_t* e = rq.q + ((rq.head + q) & rq.mask) * 5;
     const uint64_t seq = q_ld(e), s0 = q_ld(e + 1), s1 = q_ld(e + 2), s2 = q_ld(e + 3), s3 = q_ld(e + 4);
-    // request: actor = the remote actor, a0 = the remote method, a1 / a2 = its arguments
-    const uint64_t rw0 = (s0 & 0xffffffffull) | ((uint64_t)(uint16_t)s1 << 32) | ((uint64_t)kFlagValid << 48);
+    uint64_t rw0, r0, r1, r2;
+    if ((uint16_t)(s0 >> 32) == kMethodCoordPrime) {
+      // the coordinator's handler: it picks the worker and builds the PrimeCheck itself
+      const int64_t n = (int64_t)s1;
+      const uint64_t W = (uint64_t)((int64_t)s2 > 0 ? s2 : 1);
+      uint64_t h = (uint64_t)n * 0x9e3779b97f4a7c15ull;
+      h ^= h >> 29;
+      const uint64_t worker = (uint64_t)s3 + h % W;
+      int64_t lim = n > 3 ? (int64_t)sqrt((double)n) + 1 : n;
+      while (lim > 2 && (lim - 1) * (lim - 1) > n) --lim;  // (double rounding) isqrt(n) + 1
+      rw0 = (worker & 0xffffffffull) | ((uint64_t)kPrimeCheck << 32) | ((uint64_t)kFlagValid << 48);
+      r0 = 2, r1 = (uint64_t)lim, r2 = (uint64_t)n;
+      g.cont = (uint32_t)s0 + 1;
+      g.cont_n = n;
+    } else {
+      // kMethodRelay: actor = the remote actor, a0 = the remote method, a1 / a2 = its arguments
+      rw0 = (s0 & 0xffffffffull) | ((uint64_t)(uint16_t)s1 << 32) | ((uint64_t)kFlagValid << 48);
+      r0 = s2, r1 = s3, r2 = 0;
+      g.cont = 0;
+    }
     sys_st(&g.x->w0, rw0);
-    sys_st(reinterpret_cast<uint64_t*>(&g.x->a0), s2);
-    sys_st(reinterpret_cast<uint64_t*>(&g.x->a1), s3);
-    sys_st(reinterpret_cast<uint64_t*>(&g.x->a2), 0ull);
+    sys_st(reinterpret_cast<uint64_t*>(&g.x->a0), r0);
+    sys_st(reinterpret_cast<uint64_t*>(&g.x->a1), r1);
+    sys_st(reinterpret_cast<uint64_t*>(&g.x->a2), r2);
     __threadfence_system();
     sys_st(&g.x->req_tag, g.seq + 1);
     g.pend = seq + 1;
@@ -355,7 +388,7 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
     if ((++iters & 15) == 0 && sys_ld(&ctrl->stop) && !__ballot(rg.pend != 0) && rq.tail == rq.head) break;
     if (parked_any) {  // parked relays first: their replies may be waiting, and their slots the queue
       const uint64_t now = realtime_ticks();
-      unsigned done = relay_poll(rg, rep, ring_mask, now);
+      unsigned done = relay_poll(rg, rep, ring_mask, now, state, n_state);
       if (rq.tail != rq.head) done += relay_dispatch(rg, rq, 0, 0, 0, 0, 0, 0, relay_timeout, now, rep, ring_mask);
       processed += done;
       if (done) last_work = realtime_ticks();
@@ -454,7 +487,8 @@ __global__ __launch_bounds__(64) void persistent_dispatch_kernel(RingSlot* __res
     if (lane < n && !spec) {  // ordered after this lane's tag read (it returned; the branch depends on it)
       w0 = sys_ld(w), w1 = sys_ld(w + 1), w2 = sys_ld(w + 2), w3 = sys_ld(w + 3);
     }
-    const bool relayed = lane < n && (uint16_t)(w0 >> 32) == kMethodRelay && relay != nullptr;
+    const bool relayed = lane < n && relay != nullptr &&
+                         ((uint16_t)(w0 >> 32) == kMethodRelay || (uint16_t)(w0 >> 32) == kMethodCoordPrime);
     const uint64_t rmask = __ballot(relayed);
     if (rmask) {  // queued for a relay slot (the free ones publish now); the ring moves on
       processed += relay_dispatch(rg, rq, rmask, head, w0, w1, w2, w3, relay_timeout, t_seen, rep, ring_mask);

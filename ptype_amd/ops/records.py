@@ -14,6 +14,9 @@ METHOD_SEQ_FOLD = 7  # ORDERED: reply = state; state = state * FOLD_MUL + a0 (mo
 # dispatcher-only: forwarded to another process's actor through a GPU peer lane (csrc/hip/xcall.hpp PeerRelay);
 # actor = remote actor, a0 = remote method, a1 / a2 = its arguments
 METHOD_RELAY = 0x7E
+# handler-initiated: local actor A (a0 = n, a1 = workers W, a2 = first worker B) picks a worker,
+# asks it PrimeCheck over the relay and tallies primes into its own state (csrc/core/records.hpp)
+METHOD_COORD_PRIME = 0x7D
 
 FOLD_MUL = 0x100000001B3
 ORDERED_METHODS = frozenset({METHOD_SEQ_FOLD})  # one at a time per actor, in mailbox order

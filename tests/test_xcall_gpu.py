@@ -152,6 +152,73 @@ def test_handler_initiated_remote_call_relays_through_the_dispatcher():
     assert tail[0] == "STATE" and int(tail[1]) == 200, tail  # B's actor 7 saw the relayed adds only
 
 
+_COORD = textwrap.dedent("""
+    import json, os, sys, time, torch, numpy as np
+    sys.path.insert(0, os.environ["PTYPE_ROOT"])
+    from ptype_amd.ops import hip
+    from ptype_amd.ops.peer import PeerRelay
+    from ptype_amd.ops.records import METHOD_COORD_PRIME, STATUS_OK
+    state = torch.zeros(1024, dtype=torch.int64, device="cuda")
+    srv = hip().DeviceServer(0, 1024, state.data_ptr(), 1024, 0, 2000.0, 60.0, f"ptype-coord-{os.getpid()}")
+    relay = PeerRelay(srv, sys.argv[1], "cuda:0", n_lanes=8)
+    N, W, B, A = 3000, 16, 100, 5
+    req = np.zeros((N, 4), dtype=np.int64)
+    req[:, 0] = A | (METHOD_COORD_PRIME << 32) | (1 << 48)
+    req[:, 1] = np.arange(N)
+    req[:, 2] = W
+    req[:, 3] = B
+    rep = np.zeros((N, 2), dtype=np.int64)
+    t = time.perf_counter()
+    srv.call_many(req.ctypes.data, rep.ctypes.data, N)
+    dt = time.perf_counter() - t
+    torch.cuda.synchronize()
+    v, st, _ = srv.call(METHOD_COORD_PRIME, A, 7919, W, B)  # one more prime, one call
+    srv.close()
+    del relay
+    sieve = np.ones(N, dtype=bool); sieve[:2] = False
+    for p in range(2, int(N ** 0.5) + 1):
+        if sieve[p]:
+            sieve[p * p::p] = False
+    n_primes = int(sieve.sum())
+    prime_replies = sorted(int(x) for x in rep[sieve, 0])
+    print("RESULT " + json.dumps({"all_ok": bool(((rep[:, 1] & 0xff) == STATUS_OK).all()),
+                                  "tally": int(state[A].item()), "n_primes": n_primes,
+                                  "prime_replies_exact": prime_replies == list(range(1, n_primes + 1)),
+                                  "last": [int(v), int(st)], "us_per_call": dt / N * 1e6}), flush=True)
+""")
+
+
+@pytest.mark.gpu
+def test_actor_handler_decides_its_remote_call_and_continues_on_the_reply():
+    """not a host-chosen forward -- the coordinator actor's
+    handler picks the worker (hash of the candidate), builds the PrimeCheck, and
+    its continuation tallies primes into its own state when the reply lands
+    (optimus coordinator.go:75-89).  3000 candidates over 16 remote workers: the
+    tally is the prime count, every prime's reply is a distinct tally value."""
+    env = dict(os.environ, PTYPE_ROOT=ROOT, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    srv = subprocess.Popen([sys.executable, "-c", _SERVER], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, text=True)
+    try:
+        line = srv.stdout.readline().split()
+        assert line and line[0] == "SHM", (line, srv.stderr.read()[-2000:] if srv.poll() is not None else "")
+        c = subprocess.run([sys.executable, "-c", _COORD, line[1]], env=env, capture_output=True, text=True,
+                           timeout=180)
+        assert c.returncode == 0, c.stderr[-3000:]
+        res = [x for x in c.stdout.splitlines() if x.startswith("RESULT ")]
+        assert res, c.stdout[-2000:] + c.stderr[-2000:]
+        out = json.loads(res[0][7:])
+        srv.stdin.write("done\n")
+        srv.stdin.flush()
+        tail = srv.stdout.readline().split()
+        assert srv.wait(60) == 0
+    finally:
+        if srv.poll() is None:
+            srv.kill()
+    print("coord", out, tail)
+    assert out["all_ok"] and out["tally"] == out["n_primes"] + 1 == 431, out  # pi(2999) = 430, + 7919
+    assert out["prime_replies_exact"] and out["last"] == [431, 0], out
+
+
 # ---------------------------------------------------------------- r5: duplex relays, SIGKILLs
 def _spawn(src, *args, env=None):
     return subprocess.Popen([sys.executable, "-c", src, *args], env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,

@@ -9,6 +9,7 @@ TAG=${1:-r5f}
 val() { python3 -c "import json; d=json.load(open('$1')); print(round(d['value']/1e9,3), round(d['ms_per_step'],4))"; }
 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_mailbox_gpu.py \
   tests/test_sorted_exchange_gpu.py "tests/test_ipc_comm_gpu.py::test_sorted_exchange_across_processes_seqfold_exactly_once_fifo" \
+  "tests/test_xcall_gpu.py::test_actor_handler_decides_its_remote_call_and_continues_on_the_reply" \
   > gpurun_out/${TAG}_tests.log 2>&1; rc=$?
 echo "tests rc=$rc"; grep -E "passed|failed|FAILED" gpurun_out/${TAG}_tests.log | tail -5
 [ $rc -eq 0 ] || exit 2
