@@ -1457,7 +1457,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
 // one after another: an actor's messages run serially in FIFO order, distinct
 // bins in parallel, with the record loads in flight together instead of one
 // window's load per round trip.  The replies are staged at the records' ring
-// slots as before (mbx_complete_ring_kernel).  PTYPE_ORD_DRAIN=win: the windowed form.
+// slots as before (mbx_complete_ring_kernel).  PTYPE_ORD_DRAIN=bin (the windowed form is the default).
 constexpr int kOrdBinK = 8;                            // records per thread per binning round
 constexpr int kOrdRound = kOrdThreads * kOrdBinK;      // 4096
 constexpr int kOrdBinRoundsMax = 12;                   // rounds per super-window (LDS-bound)
@@ -1976,12 +1976,12 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else PT_SCAT(false, false);
 #undef PT_SCAT
   } else if (!a.ordered && !all_sidx && Sv <= 256 && fused_ok(tiles)) {
-    // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel).  Small batches
-    // take 1024-message tiles (SK = 2: 4x the blocks, ~1/4 of the registers per wave), so a
-    // 1 Mi Send has 1024 blocks -- 4 per CU -- instead of one;
-    // PTYPE_MBOX_SK=2 / 8 forces the tile.
+    // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel).  PTYPE_MBOX_SK=2:
+    // 1024-message tiles (4x the blocks, 72-78 instead of 121 VGPRs).  Measured slower at 1 Mi
+    // (round 5: fused kernel 40.2 vs 31.4 us, bench 19.8 vs 22.9 G msg/s): four times the
+    // run reservations on the 8-shard view's counters, so 4096-message tiles stay the default.
     static const int sk_env = getenv("PTYPE_MBOX_SK") ? atoi(getenv("PTYPE_MBOX_SK")) : 0;
-    const bool small = sk_env == kSKSmall || (sk_env != kSK && tiles < 1024);
+    const bool small = sk_env == kSKSmall;
     if (small) in.tiles = (uint32_t)((a.M + kST * kSKSmall - 1) / (kST * kSKSmall));
     const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv, small ? kST * kSKSmall : kSTile));
 #define PT_SD4(MO, A2, MC, FX, R8, SKV)                                                                             \
@@ -2076,8 +2076,11 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     hipLaunchKernelGGL(mbx_drain_ordered_kernel<A12>, dim3(Sv), dim3(kOrdThreads), lds, st, mv, sort_gsum_,  \
                        ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);         \
   } while (0)
-    static const bool ord_win = getenv("PTYPE_ORD_DRAIN") && std::string(getenv("PTYPE_ORD_DRAIN")) == "win";
-    if (!ord_win) {
+    // the binned form (PTYPE_ORD_DRAIN=bin) measured slower than the windowed one with whole-shard
+    // super-windows (round 5: 233 vs 175 us per 8 Mi SeqFold Send -- its reply stores land all over
+    // the shard's ring); PTYPE_ORD_BIN_ROUNDS sizes its super-window
+    static const bool ord_bin = getenv("PTYPE_ORD_DRAIN") && std::string(getenv("PTYPE_ORD_DRAIN")) == "bin";
+    if (ord_bin) {
       // the binned form: as many rounds per super-window as the LDS left by the state allows
       // (the largest dynamic LDS the runtime grants this kernel: its static words and the stats
       // partials share the CU's 160 KB; found once, stepping down from 156 KB)
@@ -2092,7 +2095,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
         (void)hipGetLastError();
         if (!cap) throw std::runtime_error("mailbox send: no LDS for the binned ordered drain");
       }
-      uint32_t nr = kOrdBinRoundsMax;
+      static const int nr_env = getenv("PTYPE_ORD_BIN_ROUNDS") ? atoi(getenv("PTYPE_ORD_BIN_ROUNDS")) : 0;
+      uint32_t nr = nr_env > 0 ? std::min<uint32_t>((uint32_t)nr_env, kOrdBinRoundsMax) : kOrdBinRoundsMax;
       while (nr > 1 && ord_bin_lds_bytes(nr, n_loc) > cap) --nr;
       hipLaunchKernelGGL(mbx_drain_ord_bin_kernel, dim3(Sv), dim3(kOrdThreads), ord_bin_lds_bytes(nr, n_loc), st, mv,
                          sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_, nr);

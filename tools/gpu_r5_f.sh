@@ -19,11 +19,11 @@ for K in "X=0" "PTYPE_ORD_DRAIN=win"; do
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_seqp -o prof -- \
   python3 bench.py --method seqfold --steps 8 --warmup 4 --rtt-calls 0 --no-secondary > gpurun_out/${TAG}_seqp.log 2>&1 || exit 4
-python3 tools/kstats.py gpurun_out/${TAG}_seqp/prof_kernel_stats.csv | head -8
+python3 tools/kstats.py gpurun_out/${TAG}_seqp/prof_kernel_stats.csv > gpurun_out/${TAG}_seqp.txt && sed -n 1,8p gpurun_out/${TAG}_seqp.txt
 for K in "X=0" "PTYPE_MBOX_SK=8"; do
   env $K timeout -k 10 200 python3 bench.py --no-secondary --rtt-calls 0 --msgs-per-gpu 1048576 > gpurun_out/${TAG}_1m_$K.json 2>gpurun_out/${TAG}_1m_$K.err || exit 5
   echo "1m [$K] $(val gpurun_out/${TAG}_1m_$K.json)"
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_1mp -o prof -- \
   python3 bench.py --msgs-per-gpu 1048576 --steps 8 --warmup 4 --rtt-calls 0 --no-secondary > gpurun_out/${TAG}_1mp.log 2>&1 || exit 6
-python3 tools/kstats.py gpurun_out/${TAG}_1mp/prof_kernel_stats.csv | head -6
+python3 tools/kstats.py gpurun_out/${TAG}_1mp/prof_kernel_stats.csv > gpurun_out/${TAG}_1mp.txt && sed -n 1,6p gpurun_out/${TAG}_1mp.txt

@@ -23,3 +23,8 @@ for K in "X=0" "PTYPE_MBOX_SK=4"; do
   env $K timeout -k 10 200 python3 bench.py --no-secondary --rtt-calls 0 > gpurun_out/${TAG}_8m_$K.json 2>gpurun_out/${TAG}_8m_$K.err || exit 5
   echo "8m [$K] $(val gpurun_out/${TAG}_8m_$K.json)"
 done
+# the N > 1 path at world 1 with the RCCL collectives forced on: eager vs one hipGraph per step
+for K in "--graph off" "--graph on"; do
+  timeout -k 10 200 python3 bench.py --force-dist --no-secondary --rtt-calls 0 $K > "gpurun_out/${TAG}_fd_${K#--graph }.json" 2>"gpurun_out/${TAG}_fd_${K#--graph }.err" || exit 6
+  echo "force-dist [$K] $(val "gpurun_out/${TAG}_fd_${K#--graph }.json")"
+done
