@@ -296,9 +296,11 @@ def main():
         if Mq == M and method == METHOD_CALC_MULTIPLY and not wide:
             rq, v, t = req, val, st
         else:
+            # (SeqFold takes one argument: its batch carries no second column)
             rq = B.MsgBatch(torch.empty(Mq, dtype=torch.int32, device=device),
                             torch.empty(Mq, dtype=torch.int64, device=device),
-                            torch.empty(Mq, dtype=torch.int64, device=device), None, method)
+                            None if method == METHOD_SEQ_FOLD else torch.empty(Mq, dtype=torch.int64, device=device),
+                            None, method)
             v = torch.empty(Mq, dtype=torch.int64, device=device)
             t = torch.empty(Mq, dtype=torch.int32, device=device)
         graph = graph1 = None

@@ -86,11 +86,11 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
     if constexpr (NT) {
       __builtin_nontemporal_store(ac, actor + i);
       __builtin_nontemporal_store(x0, a0 + i);
-      __builtin_nontemporal_store(x1, a1 + i);
+      if (a1) __builtin_nontemporal_store(x1, a1 + i);
     } else {
       actor[i] = ac;
       a0[i] = x0;
-      a1[i] = x1;
+      if (a1) a1[i] = x1;  // (null: a one-argument batch)
     }
   }
 }
@@ -776,7 +776,7 @@ void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M,
   static const bool vec4 = getenv("PTYPE_GEN_VEC") && atoi(getenv("PTYPE_GEN_VEC")) == 1;
   const uint64_t magic = variant == 1 ? 0ull : ~0ull / n_actors;
   // (vec4: 16-B stores need 16-B aligned columns -- torch's allocations are; slices may not be)
-  const bool aligned = ((actor | a0 | a1) & 15u) == 0;
+  const bool aligned = ((actor | a0 | a1) & 15u) == 0 && a1;
   if (wide)
     hipLaunchKernelGGL(gen_requests_kernel<true>, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
                        (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr,

@@ -1310,27 +1310,29 @@ __global__ __launch_bounds__(kST) void mbx_arrival_drain_kernel(MboxView mv, Sor
 // A12: the batch carries a second / third argument column.  Without them (a
 // one-argument ordered method, e.g. SeqFold) the window's a1 / a2 arrays are not
 // allocated: 68 instead of 100 KB of LDS, so two drain blocks fit a CU.
-template <bool A12>
+template <bool A12, int OK = kOrdK>
 struct OrdLds {
+  static constexpr int kWin = kOrdThreads * OK;
   uint32_t wcnt[kOrdWaves][kOrdThreads];  // per-wave bin counts -> offsets
   uint32_t bstart[kOrdThreads];
   uint32_t bcount[kOrdThreads];
   uint32_t wsum[kOrdWaves];
-  uint32_t slot[kOrdWin];
-  uint32_t act[kOrdWin];  // actor index for the handler (LDS-local or global mailbox)
-  uint32_t meth[kOrdWin];  // method | flags << 16
-  uint32_t orig[kOrdWin];  // origin: the completion's place for the reply
-  int64_t a0[kOrdWin], a1[A12 ? kOrdWin : 2], a2[A12 ? kOrdWin : 2];
+  uint32_t slot[kWin];
+  uint32_t act[kWin];  // actor index for the handler (LDS-local or global mailbox)
+  uint32_t meth[kWin];  // method | flags << 16
+  uint32_t orig[kWin];  // origin: the completion's place for the reply
+  int64_t a0[kWin], a1[A12 ? kWin : 2], a2[A12 ? kWin : 2];
 };
 
-template <bool A12>
+// OK: records per thread per window (window = 512 * OK records; PTYPE_ORD_WIN=4096: OK = 8)
+template <bool A12, int OK = kOrdK>
 __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView mv, uint32_t* __restrict__ gsum,
                                                                         uint32_t ngroups, int64_t* __restrict__ state,
                                                                         uint32_t n_state, uint64_t delay_ticks,
                                                                         OutboxView ob, u32x4* __restrict__ srep) {
   extern __shared__ __align__(16) unsigned char smem_ord[];
-  OrdLds<A12>& L = *reinterpret_cast<OrdLds<A12>*>(smem_ord);
-  int64_t* st_lds = reinterpret_cast<int64_t*>(smem_ord + sizeof(OrdLds<A12>));
+  OrdLds<A12, OK>& L = *reinterpret_cast<OrdLds<A12, OK>*>(smem_ord);
+  int64_t* st_lds = reinterpret_cast<int64_t*>(smem_ord + sizeof(OrdLds<A12, OK>));
   const uint32_t s = blockIdx.x;
   const uint32_t S = 1u << mv.log_s;
   const uint64_t Q = 1ull << mv.log_q;
@@ -1351,15 +1353,15 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
   // (loading the next window ahead, during this one's serial bins, measured no
   // faster -- 188 -> 200 us -- and spilled registers to scratch)
-  for (uint64_t w0 = lo; w0 < lo + n; w0 += kOrdWin) {
-    const uint64_t w1 = lo + n < w0 + kOrdWin ? lo + n : w0 + kOrdWin;
+  for (uint64_t w0 = lo; w0 < lo + n; w0 += (kOrdThreads * OK)) {
+    const uint64_t w1 = lo + n < w0 + (kOrdThreads * OK) ? lo + n : w0 + (kOrdThreads * OK);
     for (uint32_t b = lane; b < kOrdThreads; b += kWave) L.wcnt[w][b] = 0;
-    SortRec x[kOrdK];
-    uint32_t bin[kOrdK], wr[kOrdK];
-    uint64_t slot[kOrdK];
+    SortRec x[OK];
+    uint32_t bin[OK], wr[OK];
+    uint64_t slot[OK];
 #pragma unroll
-    for (int k = 0; k < kOrdK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
-      const uint64_t q = w0 + (uint64_t)w * (kWave * kOrdK) + (uint64_t)k * kWave + lane;
+    for (int k = 0; k < OK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
+      const uint64_t q = w0 + (uint64_t)w * (kWave * OK) + (uint64_t)k * kWave + lane;
       slot[k] = sbase | ((q + rot) & qmask);
       if (q < w1) {
         x[k] = load_sorted(mv, slot[k]);
@@ -1369,7 +1371,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
       }
     }
 #pragma unroll
-    for (int k = 0; k < kOrdK; ++k) {
+    for (int k = 0; k < OK; ++k) {
       bin[k] = (x[k].mb >> mv.log_s) & (kOrdThreads - 1);
       const uint64_t peers = match_bits(bin[k], 9, __ballot(x[k].valid));
       const unsigned below = mbcnt64(peers);
@@ -1401,7 +1403,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kOrdK; ++k) {
+    for (int k = 0; k < OK; ++k) {
       if (!x[k].valid) continue;
       const unsigned d = L.bstart[bin[k]] + L.wcnt[w][bin[k]] + wr[k];
       L.slot[d] = (uint32_t)slot[k];
@@ -2063,18 +2065,26 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     const uint32_t n_loc = a.state && a.n_state ? std::min<uint32_t>((a.n_state + Sv - 1) / Sv, kOrdStateMax) : 0;
     const size_t st_lds = (size_t)n_loc * sizeof(int64_t);  // (covers every shard the kernel stages: n_loc <= cap)
     const bool a12 = a.a1 || a.a2;  // (a column given: staged; none: the handlers see zeros)
-#define PT_ORD(A12)                                                                                           \
+#define PT_ORD2(A12, OKV)                                                                                     \
   do {                                                                                                        \
-    const size_t lds = sizeof(OrdLds<A12>) + std::max<size_t>(st_lds, 16);                                   \
+    const size_t lds = sizeof(OrdLds<A12, OKV>) + std::max<size_t>(st_lds, 16);                              \
     static bool attr = false;                                                                                 \
     if (!attr) { /* above the 64 KB default dynamic LDS */                                                    \
-      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12>,                            \
+      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12, OKV>,                       \
                                        hipFuncAttributeMaxDynamicSharedMemorySize,                            \
-                                       (int)(sizeof(OrdLds<A12>) + (size_t)kOrdStateMax * sizeof(int64_t)))); \
+                                       (int)(sizeof(OrdLds<A12, OKV>) + (size_t)kOrdStateMax * sizeof(int64_t)))); \
       attr = true;                                                                                            \
     }                                                                                                         \
-    hipLaunchKernelGGL(mbx_drain_ordered_kernel<A12>, dim3(Sv), dim3(kOrdThreads), lds, st, mv, sort_gsum_,  \
-                       ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_);         \
+    hipLaunchKernelGGL((mbx_drain_ordered_kernel<A12, OKV>), dim3(Sv), dim3(kOrdThreads), lds, st, mv,         \
+                       sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_); \
+  } while (0)
+    // PTYPE_ORD_WIN=4096: 4096-record windows (one-argument batches only: the LDS of a window
+    // with a1 / a2 columns would not fit)
+    static const bool win8 = getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 4096;
+#define PT_ORD(A12)                                \
+  do {                                             \
+    if (win8 && !(A12)) PT_ORD2(false, 8);         \
+    else PT_ORD2(A12, kOrdK);                      \
   } while (0)
     // the binned form (PTYPE_ORD_DRAIN=bin) measured slower than the windowed one with whole-shard
     // super-windows (round 5: 233 vs 175 us per 8 Mi SeqFold Send -- its reply stores land all over
@@ -2106,6 +2116,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       PT_ORD(false);
     }
 #undef PT_ORD
+#undef PT_ORD2
     PT_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST),
                        (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, in, mv,

@@ -125,7 +125,8 @@ def gen_requests(M: int, n_actors: int, method: int = METHOD_CALC_MULTIPLY, seed
             out.a1.copy_(torch.from_numpy(mix64(h ^ np.uint64(0xE7037ED1A0B428DB)).view(np.int64)))
         return out
     out.a0.copy_(torch.from_numpy(((h >> np.uint64(20)) & np.uint64(0xFFFF)).astype(np.int64) - 0x8000))
-    out.a1.copy_(torch.from_numpy(((h >> np.uint64(40)) & np.uint64(0xFFFF)).astype(np.int64)))
+    if out.a1 is not None:  # (a one-argument batch: no second column)
+        out.a1.copy_(torch.from_numpy(((h >> np.uint64(40)) & np.uint64(0xFFFF)).astype(np.int64)))
     return out
 
 
