@@ -108,6 +108,7 @@ def _spawn_ranks(args) -> int:
 
 
 _LIVE_EXCHANGES: list = []  # for the hang watchdog
+_EMIT_ON_HANG: list = [None]  # rank 0's JSON line, printed by the watchdog if a last secondary hangs
 
 
 def _hang_watchdog(after_s: float, rank: int) -> None:
@@ -123,6 +124,11 @@ def _hang_watchdog(after_s: float, rank: int) -> None:
 
     def dump():
         print(f"[rank {rank}] HANG after {after_s:.0f} s", file=sys.stderr, flush=True)
+        if _EMIT_ON_HANG[0] is not None:  # only the last secondary is left: report the line, end cleanly
+            try:
+                _EMIT_ON_HANG[0]()
+            finally:
+                os._exit(0)
         names = ["routed", "req_in", "served", "rep_in"]
         for ref in _LIVE_EXCHANGES:
             ex = ref()
@@ -578,7 +584,12 @@ def main():
 
     total_msgs = M * world * args.steps
     value = total_msgs / elapsed if elapsed > 0 else 0.0
-    if rank == 0:
+    printed = [False]
+
+    def emit():  # rank 0's one JSON line (also from the hang watchdog, once, after a late secondary hangs)
+        if rank != 0 or printed[0]:
+            return
+        printed[0] = True
         out = {
             "metric": "messages/sec",
             "value": value,
@@ -644,6 +655,28 @@ def main():
         if secondaries:
             out["secondaries"] = secondaries
         print(json.dumps(out), flush=True)
+
+    if dist_on and use_gpu and fake is None and not args.no_secondary and args.steps:
+        # the public API path at N > 1 (Join -> NewClient -> Client.Send on every rank), last: if it
+        # hangs, the hang watchdog prints the line measured so far (emit) instead of nothing
+        from ptype_amd.utils import benchmarks as BM
+
+        secondaries["api_send"] = {"error": "did not finish (hang watchdog)"}
+        _EMIT_ON_HANG[0] = emit
+        try:
+            def max_over_ranks(x):
+                tt = torch.tensor([x], dtype=torch.float64, device=red_dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                return float(tt.item())
+
+            secondaries["api_send"] = BM.api_send(device, [min(M, 1 << 22)], args.actors_per_gpu, args.steps,
+                                                  max(1, args.warmup), rank=rank, world=world,
+                                                  comm="ipc" if ipc else "rccl", barrier=barrier,
+                                                  max_over_ranks=max_over_ranks)
+        except Exception as e:  # noqa: BLE001
+            secondaries["api_send"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+            print(f"[rank {rank}] secondary api_send failed: {e!r}", file=sys.stderr, flush=True)
+    emit()
     if dist_on:
         dist.destroy_process_group()
 

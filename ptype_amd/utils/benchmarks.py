@@ -165,37 +165,54 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def api_send(device, sizes, actors: int, steps: int, warmup: int) -> dict:
-    """Join (one control-plane member, GPU runtime, lease-attached shard, registry
+def api_send(device, sizes, actors: int, steps: int, warmup: int, rank: int = 0, world: int = 1,
+             comm: str = "rccl", barrier=None, max_over_ranks=None) -> dict:
+    """Join (a control-plane member, GPU runtime, lease-attached shard, registry
     mirror) -> NewClient -> Client.Send of pre-generated batches, eager, through
-    the HBM mailboxes (gpu.delivery: mailbox)."""
+    the HBM mailboxes (gpu.delivery: mailbox).  With ``world`` > 1 (inside the
+    bench's process group): one member per rank in a static cluster on
+    127.0.0.1 (ports from MASTER_PORT), every rank's runtime on the existing
+    group, and every rank Sends its own batches to actors all over the node (the
+    sorted exchange, deferred re-sends: no host wait per Send); the timed loop
+    ends with ``Client.Flush``, and the slowest rank's time counts."""
     from .. import cluster as C
     from ..ops import batch as B
     from ..ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
 
     os.environ.setdefault("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
-    pp, pc = _port(), _port()
     cfg = C.Config()
-    cfg.service_name, cfg.node_name, cfg.port = "calculator", "bench", _port()
-    cfg.member = C.member_config(name="b0", dir=tempfile.mkdtemp(prefix="ptype_bench_"),
+    if world > 1:  # every rank derives the same static cluster from the rendezvous port
+        base = int(os.environ.get("MASTER_PORT", "29500")) + 1237
+        if base + 3 * world >= 65536:
+            base = 20000 + base % 20000
+        pp, pc, port = base + 2 * rank, base + 2 * rank + 1, base + 2 * world + rank
+        initial = ",".join(f"b{r}=http://127.0.0.1:{base + 2 * r}" for r in range(world))
+    else:
+        pp, pc, port = _port(), _port(), _port()
+        initial = f"b0=http://127.0.0.1:{pp}"
+    cfg.service_name, cfg.node_name, cfg.port = "calculator", f"bench{rank}", port
+    cfg.member = C.member_config(name=f"b{rank}", dir=tempfile.mkdtemp(prefix="ptype_bench_"),
                                  lpurls=[f"http://127.0.0.1:{pp}"], apurls=[f"http://127.0.0.1:{pp}"],
                                  lcurls=[f"http://127.0.0.1:{pc}"], acurls=[f"http://127.0.0.1:{pc}"],
-                                 initial_cluster=f"b0=http://127.0.0.1:{pp}", unsafe_no_fsync=True)
+                                 initial_cluster=initial, unsafe_no_fsync=True)
     cfg.has_gpu = True
     g = cfg.gpu
     g.device, g.actors, g.max_batch, g.delivery = device.index or 0, actors, max(sizes), "mailbox"
+    g.world, g.comm = world, comm
     g.cpu = device.type == "cpu"  # (the CPU twin of the path, for tests)
     t0 = time.perf_counter()
     srv = C.Serve(cfg.port, _Host(), host="127.0.0.1")  # the node's net/rpc server (what NewClient dials)
     c = C.Join(C.background(), cfg)
     out = {"path": "Join -> NewClient -> Client.Send (eager, mailbox delivery, pre-generated batches)",
-           "join_s": time.perf_counter() - t0}
+           "join_s": time.perf_counter() - t0, "ranks": world}
     try:
         client = c.NewClient("calculator", C.ConnConfig(retries=0, allow_local=False))
+        n_ids = c.runtime.total_actors  # every rank's actors
         for M in sizes:
             # at least 3 distinct batches, together more than the 256 MB MALL (20 B per message)
             nb = max(3, -(-300_000_000 // (20 * M)))
-            batches = [B.gen_requests(M, actors, METHOD_CALC_MULTIPLY, seed=11 + k, device=device) for k in range(nb)]
+            batches = [B.gen_requests(M, n_ids, METHOD_CALC_MULTIPLY, seed=11 + k + 1000 * rank, device=device)
+                       for k in range(nb)]
             res = {}
             k = [0]
 
@@ -209,14 +226,26 @@ def api_send(device, sizes, actors: int, steps: int, warmup: int) -> dict:
 
             for _ in range(warmup):  # (first Sends of a size grow workspaces: not in the host figure)
                 step()
+            client.Flush()
             _sync(device)
+            if barrier:
+                barrier()
             res["host"] = 0.0
-            el = timed(step, steps, 0, device)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            client.Flush()  # the last Sends' deferred re-sends (none in a steady state) are timed too
+            _sync(device)
+            if barrier:
+                barrier()
+            el = time.perf_counter() - t0
+            if max_over_ranks is not None:
+                el = max_over_ranks(el)
             host_us = res["host"] / steps * 1e6
             v, s = res["out"]
             if not (bool((s == STATUS_OK).all()) and torch.equal(v, res["b"].a0 * res["b"].a1)):
                 raise RuntimeError("api_send: verification failed")
-            out[f"{M}"] = {"msgs_per_step": M, "value": M * steps / el, "ms_per_step": el / steps * 1e3,
+            out[f"{M}"] = {"msgs_per_step": M, "value": M * world * steps / el, "ms_per_step": el / steps * 1e3,
                            "host_us_per_send": host_us, "distinct_batches": nb, "batch_bytes_total": nb * 20 * M}
             del batches
         client.Close()

@@ -133,3 +133,58 @@ def test_api_send_secondary_runs_join_newclient_send_on_cpu():
 
     out = BM.api_send(torch.device("cpu"), [2048], 512, 2, 1)
     assert out["2048"]["msgs_per_step"] == 2048 and out["2048"]["value"] > 0
+
+
+_API_RANK = r"""
+import json, os, sys, torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["PTYPE_ROOT"])
+from ptype_amd.utils import benchmarks as BM
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+
+def mx(x):
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+out = BM.api_send(torch.device("cpu"), [4096], 512, 3, 1, rank=rank, world=world, barrier=dist.barrier,
+                  max_over_ranks=mx)
+print("RESULT " + json.dumps(out), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def test_api_send_secondary_across_ranks_on_cpu():
+    """the api_send secondary at N > 1 -- one control-plane member
+    per rank (static cluster from MASTER_PORT), every rank's runtime on the
+    existing process group, Client.Send from every rank (deferred re-sends, the
+    timed loop ends with Flush), the replies verified on every rank."""
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE="2", LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-c", _API_RANK], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        assert p.returncode == 0, e[-3000:]
+        line = [x for x in o.splitlines() if x.startswith("RESULT ")]
+        assert line, o[-2000:] + e[-2000:]
+        outs.append(json.loads(line[0][7:]))
+    for out in outs:
+        assert out["ranks"] == 2 and out["4096"]["msgs_per_step"] == 4096 and out["4096"]["value"] > 0, out
+
+
+@pytest.mark.gpu
+def test_bench_api_send_secondary_at_n2_over_ipc():
+    """The api_send secondary in the N > 1 bench line: two torchrun
+    ranks on one GPU (IpcComm), Join -> NewClient -> Client.Send on both, replies
+    verified, no host wait per Send beyond the deferred re-send resolution."""
+    small = ["--msgs-per-gpu", str(1 << 18), "--actors-per-gpu", "8192", "--comm", "ipc"]
+    out = _run(2, ["--steps", "3", "--warmup", "2", "--rtt-calls", "0"] + small, timeout=600, launcher="self")
+    api = out["secondaries"]["api_send"]
+    assert "error" not in api, api
+    assert api["ranks"] == 2 and api[str(1 << 18)]["value"] > 0, api
