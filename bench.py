@@ -431,6 +431,9 @@ def main():
         if args.delivery == "mailbox" and args.sharding == "actor":
             # BASELINE config 2 at its own size: 1 Mi messages per step
             runs.append(("config2_1m", dict(delivery="mailbox", sharding="actor", Mq=min(M, 1 << 20))))
+            # the same 1 Mi step through arrival-sharded rings (stateless batches: a tile's messages in
+            # one ring at fixed positions -- no sort, an enqueue and a drain kernel)
+            runs.append(("config2_1m_arrival", dict(delivery="mailbox", sharding="arrival", Mq=min(M, 1 << 20))))
             runs.append(("arrival_sharded", dict(delivery="mailbox", sharding="arrival")))
             # an ORDERED stateful method (SeqFold: state = state * K + a0, non-commutative):
             # every actor runs its messages one at a time in ring (= message) order
