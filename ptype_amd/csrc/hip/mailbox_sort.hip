@@ -1324,8 +1324,13 @@ struct OrdLds {
   int64_t a0[kWin], a1[A12 ? kWin : 2], a2[A12 ? kWin : 2];
 };
 
-// OK: records per thread per window (window = 512 * OK records; PTYPE_ORD_WIN=4096: OK = 8)
-template <bool A12, int OK = kOrdK>
+// OK: records per thread per window (window = 512 * OK records; PTYPE_ORD_WIN=4096: OK = 8).
+// FIXED = kSeqFold: a uniform SeqFold batch.  With every actor of the shard in its
+// own bin (at most kOrdThreads of them, state staged), thread b IS actor b's
+// consumer for the whole Send: its state stays in a register and each record is
+// one fold (reply = the state before, state = state * kFoldMul + a0) -- no handler
+// switch, no LDS state round trip per message.
+template <bool A12, int OK = kOrdK, int FIXED = 0>
 __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView mv, uint32_t* __restrict__ gsum,
                                                                         uint32_t ngroups, int64_t* __restrict__ state,
                                                                         uint32_t n_state, uint64_t delay_ticks,
@@ -1347,6 +1352,8 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   if (in_lds)
     for (uint32_t j = threadIdx.x; j < n_loc; j += kOrdThreads) st_lds[j] = state[s + (uint64_t)j * S];
   __syncthreads();
+  const bool reg = FIXED == kSeqFold && in_lds && n_loc <= (uint32_t)kOrdThreads;  // actor b's state in thread b
+  uint64_t sreg = reg && threadIdx.x < n_loc ? (uint64_t)st_lds[threadIdx.x] : 0ull;
   const uint32_t tot = tot_s;
   const uint64_t n = tot < free ? tot : free;
   const uint64_t sbase = (uint64_t)s << mv.log_q, qmask = Q - 1, rot = shard_rot(mv, s);  // slot_at, hoisted
@@ -1408,7 +1415,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
       const unsigned d = L.bstart[bin[k]] + L.wcnt[w][bin[k]] + wr[k];
       L.slot[d] = (uint32_t)slot[k];
       L.act[d] = in_lds ? (x[k].mb >> mv.log_s) : x[k].mb;
-      L.meth[d] = x[k].method | (x[k].flags << 16);
+      if (!reg) L.meth[d] = x[k].method | (x[k].flags << 16);
       L.orig[d] = x[k].origin;
       L.a0[d] = x[k].a0;
       if constexpr (A12) {
@@ -1417,7 +1424,23 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
       }
     }
     __syncthreads();
-    {  // this thread's bin, serially in ring order
+    if (reg) {  // uniform SeqFold, one actor per bin: the folds in a register
+      const unsigned b = threadIdx.x, e = L.bstart[b] + L.bcount[b];
+      if (L.bcount[b] > 1) serial += L.bcount[b] - 1;
+      for (unsigned d = L.bstart[b]; d < e; ++d) {
+        const uint64_t prev = sreg;
+        uint32_t st = kStatusOk;
+        if (L.act[d] == b && b < n_loc) {
+          sreg = prev * kFoldMul + (uint64_t)L.a0[d];
+        } else {  // a mailbox past the state (routed here by a stale registry entry)
+          st = kStatusNoActor;
+          ++failed;
+        }
+        const uint64_t v = st == kStatusOk ? prev : 0ull;
+        srep[L.slot[d]] = u32x4{(uint32_t)v, (uint32_t)(v >> 32), st, L.orig[d]};
+        ++done;
+      }
+    } else {  // this thread's bin, serially in ring order
       const unsigned b = threadIdx.x, e = L.bstart[b] + L.bcount[b];
       if (L.bcount[b] > 1) serial += L.bcount[b] - 1;  // records that waited behind their bin's earlier ones
       int64_t* st = in_lds ? st_lds : state;
@@ -1439,6 +1462,8 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
     }
     __syncthreads();  // the window's LDS is reused
   }
+  if (reg && threadIdx.x < n_loc) st_lds[threadIdx.x] = (int64_t)sreg;
+  if (reg) __syncthreads();
   if (in_lds)
     for (uint32_t j = threadIdx.x; j < n_loc; j += kOrdThreads) state[s + (uint64_t)j * S] = st_lds[j];
   block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
@@ -2065,26 +2090,35 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     const uint32_t n_loc = a.state && a.n_state ? std::min<uint32_t>((a.n_state + Sv - 1) / Sv, kOrdStateMax) : 0;
     const size_t st_lds = (size_t)n_loc * sizeof(int64_t);  // (covers every shard the kernel stages: n_loc <= cap)
     const bool a12 = a.a1 || a.a2;  // (a column given: staged; none: the handlers see zeros)
-#define PT_ORD2(A12, OKV)                                                                                     \
+#define PT_ORD3(A12, OKV, FXV)                                                                                \
   do {                                                                                                        \
     const size_t lds = sizeof(OrdLds<A12, OKV>) + std::max<size_t>(st_lds, 16);                              \
     static bool attr = false;                                                                                 \
     if (!attr) { /* above the 64 KB default dynamic LDS */                                                    \
-      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12, OKV>,                       \
+      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12, OKV, FXV>,                  \
                                        hipFuncAttributeMaxDynamicSharedMemorySize,                            \
                                        (int)(sizeof(OrdLds<A12, OKV>) + (size_t)kOrdStateMax * sizeof(int64_t)))); \
       attr = true;                                                                                            \
     }                                                                                                         \
-    hipLaunchKernelGGL((mbx_drain_ordered_kernel<A12, OKV>), dim3(Sv), dim3(kOrdThreads), lds, st, mv,         \
+    hipLaunchKernelGGL((mbx_drain_ordered_kernel<A12, OKV, FXV>), dim3(Sv), dim3(kOrdThreads), lds, st, mv,    \
                        sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_); \
   } while (0)
-    // PTYPE_ORD_WIN=4096: 4096-record windows (one-argument batches only: the LDS of a window
-    // with a1 / a2 columns would not fit)
-    static const bool win8 = getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 4096;
-#define PT_ORD(A12)                                \
-  do {                                             \
-    if (win8 && !(A12)) PT_ORD2(false, 8);         \
-    else PT_ORD2(A12, kOrdK);                      \
+    // one-argument batches: 4096-record windows (PTYPE_ORD_WIN=2048: the 2048-record form;
+    // round 5: 0.375 vs 0.383 ms per 8 Mi SeqFold step), and a uniform SeqFold batch folds
+    // in registers (PTYPE_ORD_FIXED=0: the handler switch)
+    static const bool win8 = !(getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 2048);
+    static const bool fixed_ok = !(getenv("PTYPE_ORD_FIXED") && atoi(getenv("PTYPE_ORD_FIXED")) == 0);
+    const bool fold = fixed_ok && a.fixed_method == kSeqFold && !a.method_col;
+#define PT_ORD(A12)                                            \
+  do {                                                         \
+    if (win8 && !(A12)) {                                      \
+      if (fold) PT_ORD3(false, 8, kSeqFold);                   \
+      else PT_ORD3(false, 8, 0);                               \
+    } else if (!(A12) && fold) {                               \
+      PT_ORD3(false, kOrdK, kSeqFold);                         \
+    } else {                                                   \
+      PT_ORD3(A12, kOrdK, 0);                                  \
+    }                                                          \
   } while (0)
     // the binned form (PTYPE_ORD_DRAIN=bin) measured slower than the windowed one with whole-shard
     // super-windows (round 5: 233 vs 175 us per 8 Mi SeqFold Send -- its reply stores land all over
@@ -2116,7 +2150,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       PT_ORD(false);
     }
 #undef PT_ORD
-#undef PT_ORD2
+#undef PT_ORD3
     PT_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST),
                        (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, in, mv,
