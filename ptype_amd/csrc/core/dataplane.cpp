@@ -300,6 +300,14 @@ int DataPlane::form(uint64_t gen, const std::vector<std::string>& proposal) {
   rank_ = rank;
   gen_ = gen;
   members_ = members;
+  if (rank == 0 && gen >= 2) {  // generation gen - 2's records are nobody's any more (best effort)
+    try {
+      const std::string old = std::string(kStorePrefix) + "/_ptype/nccl/" + service_ + "/" + std::to_string(gen - 2) + "/";
+      int64_t deleted = 0;
+      (void)kv_->del(old, prefix_range_end(old), &deleted, 2000);
+    } catch (const std::exception&) {
+    }
+  }
   return rank;
 }
 
