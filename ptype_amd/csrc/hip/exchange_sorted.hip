@@ -775,7 +775,33 @@ __global__ __launch_bounds__(kXOrdThreads) void sx_drain_ord_kernel(const uint32
         Ls.a2[d] = x2[k];
       }
       __syncthreads();
-      {
+      if (in_lds && n_loc <= (uint32_t)kXOrdThreads && !L.w[0] && hm == kSeqFold) {
+        // a uniform SeqFold region with one actor per bin: thread b folds actor b's
+        // messages with the state in a register (mailbox_sort.hip, the same fold)
+        const unsigned b = threadIdx.x, e = Ls.bstart[b] + Ls.bcount[b];
+        uint64_t sreg = b < n_loc ? (uint64_t)st_lds[b] : 0ull;
+        for (unsigned d = Ls.bstart[b]; d < e; ++d) {
+          const bool mine = Ls.act[d] == b && b < n_loc;
+          const uint64_t prev = sreg;
+          if (mine) sreg = prev * kFoldMul + (uint64_t)Ls.a0[d];
+          bool ok = mine;
+          uint64_t code = ok ? (L.vb == 8 ? prev : zz_enc((int64_t)prev)) : (uint64_t)kStatusNoActor;
+          if (ok && L.vb < 8 && (code >> (8 * L.vb))) {
+            ok = false;
+            code = kStatusFailed;
+          }
+          failed += !ok;
+          const uint32_t qq = Ls.pos[d];
+          switch (L.vb) {
+            case 1: vals[qq] = (uint8_t)code; break;
+            case 2: reinterpret_cast<uint16_t*>(vals)[qq] = (uint16_t)code; break;
+            case 4: reinterpret_cast<uint32_t*>(vals)[qq] = (uint32_t)code; break;
+            default: reinterpret_cast<uint64_t*>(vals)[qq] = code;
+          }
+          if (ok) atomicOr(&okmap[qq / kWave], 1ull << (qq % kWave));
+        }
+        if (b < n_loc) st_lds[b] = (int64_t)sreg;
+      } else {
         const unsigned b = threadIdx.x, e = Ls.bstart[b] + Ls.bcount[b];
         int64_t* st = in_lds ? st_lds : state;
         const uint32_t nst = in_lds ? n_loc : n_state;
