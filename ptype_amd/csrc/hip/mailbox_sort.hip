@@ -1330,7 +1330,7 @@ struct OrdLds {
 // consumer for the whole Send: its state stays in a register and each record is
 // one fold (reply = the state before, state = state * kFoldMul + a0) -- no handler
 // switch, no LDS state round trip per message.
-template <bool A12, int OK = kOrdK, int FIXED = 0>
+template <bool A12, int OK = kOrdK, int FIXED = 0, bool PF = false>
 __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView mv, uint32_t* __restrict__ gsum,
                                                                         uint32_t ngroups, int64_t* __restrict__ state,
                                                                         uint32_t n_state, uint64_t delay_ticks,
@@ -1358,24 +1358,57 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   const uint64_t n = tot < free ? tot : free;
   const uint64_t sbase = (uint64_t)s << mv.log_q, qmask = Q - 1, rot = shard_rot(mv, s);  // slot_at, hoisted
   unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
-  // (loading the next window ahead, during this one's serial bins, measured no
-  // faster -- 188 -> 200 us -- and spilled registers to scratch)
+  // PF (PTYPE_ORD_PREFETCH=1): the next window's records (their first 16 B) are loaded
+  // while this one is binned and run -- one block per CU (the LDS), so the registers are
+  // there.  (Round 3, with the handler switch's register file: measured no faster, 188 ->
+  // 200 us, and spilled to scratch.)
+  const uint64_t n_end = lo + n;
+  auto load_win = [&](uint64_t wa, u32x4(&h)[OK]) {
+#pragma unroll
+    for (int k = 0; k < OK; ++k) {
+      const uint64_t q = wa + (uint64_t)w * (kWave * OK) + (uint64_t)k * kWave + lane;
+      h[k] = q < n_end && q < wa + (kOrdThreads * OK) ? *reinterpret_cast<const u32x4*>(rec_a(mv, sbase | ((q + rot) & qmask)))
+                                                      : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  u32x4 cur[PF ? OK : 1];
+  if constexpr (PF) {
+    if (lo < n_end) load_win(lo, cur);
+  }
   for (uint64_t w0 = lo; w0 < lo + n; w0 += (kOrdThreads * OK)) {
     const uint64_t w1 = lo + n < w0 + (kOrdThreads * OK) ? lo + n : w0 + (kOrdThreads * OK);
     for (uint32_t b = lane; b < kOrdThreads; b += kWave) L.wcnt[w][b] = 0;
     SortRec x[OK];
     uint32_t bin[OK], wr[OK];
     uint64_t slot[OK];
+    u32x4 nxt[PF ? OK : 1];
+    if constexpr (PF) {
+      if (w0 + (kOrdThreads * OK) < n_end) load_win(w0 + (kOrdThreads * OK), nxt);
+    }
 #pragma unroll
     for (int k = 0; k < OK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
       const uint64_t q = w0 + (uint64_t)w * (kWave * OK) + (uint64_t)k * kWave + lane;
       slot[k] = sbase | ((q + rot) & qmask);
       if (q < w1) {
-        x[k] = load_sorted(mv, slot[k]);
+        if constexpr (PF) {
+          u32x4 hb = {0u, 0u, 0u, 0u};
+          int64_t a2v = 0;
+          if (rec_is_long(cur[k])) {
+            hb = *reinterpret_cast<const u32x4*>(rec_b(mv, slot[k]));
+            if (((cur[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[slot[k]];
+          }
+          x[k] = decode_sorted(cur[k], hb, a2v);
+        } else {
+          x[k] = load_sorted(mv, slot[k]);
+        }
         if (!x[k].valid) ++holes;
       } else {
         x[k].valid = false;
       }
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int k = 0; k < OK; ++k) cur[k] = nxt[k];
     }
 #pragma unroll
     for (int k = 0; k < OK; ++k) {
@@ -2090,29 +2123,33 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     const uint32_t n_loc = a.state && a.n_state ? std::min<uint32_t>((a.n_state + Sv - 1) / Sv, kOrdStateMax) : 0;
     const size_t st_lds = (size_t)n_loc * sizeof(int64_t);  // (covers every shard the kernel stages: n_loc <= cap)
     const bool a12 = a.a1 || a.a2;  // (a column given: staged; none: the handlers see zeros)
-#define PT_ORD3(A12, OKV, FXV)                                                                                \
+#define PT_ORD4(A12, OKV, FXV, PFV)                                                                           \
   do {                                                                                                        \
     const size_t lds = sizeof(OrdLds<A12, OKV>) + std::max<size_t>(st_lds, 16);                              \
     static bool attr = false;                                                                                 \
     if (!attr) { /* above the 64 KB default dynamic LDS */                                                    \
-      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12, OKV, FXV>,                  \
+      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12, OKV, FXV, PFV>,             \
                                        hipFuncAttributeMaxDynamicSharedMemorySize,                            \
                                        (int)(sizeof(OrdLds<A12, OKV>) + (size_t)kOrdStateMax * sizeof(int64_t)))); \
       attr = true;                                                                                            \
     }                                                                                                         \
-    hipLaunchKernelGGL((mbx_drain_ordered_kernel<A12, OKV, FXV>), dim3(Sv), dim3(kOrdThreads), lds, st, mv,    \
-                       sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_); \
+    hipLaunchKernelGGL((mbx_drain_ordered_kernel<A12, OKV, FXV, PFV>), dim3(Sv), dim3(kOrdThreads), lds, st,  \
+                       mv, sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob,              \
+                       (u32x4*)stage_rep_);                                                                   \
   } while (0)
+#define PT_ORD3(A12, OKV, FXV) PT_ORD4(A12, OKV, FXV, false)
     // one-argument batches: 4096-record windows (PTYPE_ORD_WIN=2048: the 2048-record form;
     // round 5: 0.375 vs 0.383 ms per 8 Mi SeqFold step), and a uniform SeqFold batch folds
     // in registers (PTYPE_ORD_FIXED=0: the handler switch)
     static const bool win8 = !(getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 2048);
     static const bool fixed_ok = !(getenv("PTYPE_ORD_FIXED") && atoi(getenv("PTYPE_ORD_FIXED")) == 0);
     const bool fold = fixed_ok && a.fixed_method == kSeqFold && !a.method_col;
+    static const bool pf = getenv("PTYPE_ORD_PREFETCH") && atoi(getenv("PTYPE_ORD_PREFETCH")) == 1;
 #define PT_ORD(A12)                                            \
   do {                                                         \
     if (win8 && !(A12)) {                                      \
-      if (fold) PT_ORD3(false, 8, kSeqFold);                   \
+      if (fold && pf) PT_ORD4(false, 8, kSeqFold, true);       \
+      else if (fold) PT_ORD3(false, 8, kSeqFold);              \
       else PT_ORD3(false, 8, 0);                               \
     } else if (!(A12) && fold) {                               \
       PT_ORD3(false, kOrdK, kSeqFold);                         \
@@ -2151,6 +2188,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     }
 #undef PT_ORD
 #undef PT_ORD3
+#undef PT_ORD4
     PT_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST),
                        (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, in, mv,
