@@ -288,11 +288,18 @@ def main():
     host_split = [None]  # the sorted engine's host time split (timed steps, this rank)
 
     def measure(table, steps, warmup, delivery=args.delivery, sharding=args.sharding, Mq=M,
-                method=METHOD_CALC_MULTIPLY, wide=False):
+                method=METHOD_CALC_MULTIPLY, wide=False, pregen=False):
         """Warm up, then time `steps` Sends of `Mq` messages (barrier + synchronize
         on both sides, max over ranks); returns (seconds, exchange, graph used).
         Replies are verified after the warm-up and after the timed steps: every
-        status OK and, for Calculator.Multiply, every value == A * B."""
+        status OK and, for Calculator.Multiply, every value == A * B.  `pregen`:
+        the batches are generated before the timing -- distinct ones, together
+        more than the 256 MB MALL, cycled -- and each step is an eager Send."""
+        pq = None
+        if pregen:
+            nb = max(3, -(-300_000_000 // (20 * Mq)))
+            pq = [B.gen_requests(Mq, n_actors, METHOD_CALC_MULTIPLY, seed=(k * world + rank) * 104729 + 31,
+                                 device=device) for k in range(nb)]
         # mailbox delivery: actor-sharded rings (each actor's messages in message
         # order in one ring) unless --sharding arrival (tile-sharded queues)
         ex = ActorExchange(table, Mq, chunks=chunks, state=state, fake=fake, delivery=delivery,
@@ -312,7 +319,7 @@ def main():
         graph = graph1 = None
         U = args.steps_per_graph
         vt = [rq, v, t]  # the batch and replies the verification reads
-        if use_graph:
+        if use_graph and pq is None:
             # the whole step (new requests + Send) as one hipGraph; the generator reads its
             # seed from device memory and the graph advances it, so every replay is a new batch
             seed_t = torch.tensor([rank * 0x9E3779B9 + 7 + j * 0x1000193 for j in range(U + 1)], dtype=torch.int64,
@@ -339,6 +346,9 @@ def main():
                 elif (s_ - warmup) % U == 0:  # timed: one replay runs U whole steps
                     graph.replay()
                 return
+            if pq is not None:
+                ex.send_all(pq[s_ % len(pq)], out=(v, t))
+                return
             if pre and Mq == M and method == METHOD_CALC_MULTIPLY:
                 ex.send_all(pre[s_ % len(pre)], out=(v, t))
                 return
@@ -346,6 +356,8 @@ def main():
             ex.send(rq, v, t)
 
         def last(k):
+            if pq is not None:
+                return pq[(k - 1) % len(pq)]
             return pre[(k - 1) % len(pre)] if pre and Mq == M and method == METHOD_CALC_MULTIPLY else vt[0]
 
         for s_ in range(warmup):
@@ -434,6 +446,10 @@ def main():
             # the same 1 Mi step through arrival-sharded rings (stateless batches: a tile's messages in
             # one ring at fixed positions -- no sort, an enqueue and a drain kernel)
             runs.append(("config2_1m_arrival", dict(delivery="mailbox", sharding="arrival", Mq=min(M, 1 << 20))))
+            # config 2 with the client's batches made before the timing (15 distinct 1 Mi batches,
+            # 315 MB: more than the MALL), every step an eager Send through the actor-sharded rings
+            runs.append(("config2_1m_pregen", dict(delivery="mailbox", sharding="actor", Mq=min(M, 1 << 20),
+                                                   pregen=True)))
             runs.append(("arrival_sharded", dict(delivery="mailbox", sharding="arrival")))
             # an ORDERED stateful method (SeqFold: state = state * K + a0, non-commutative):
             # every actor runs its messages one at a time in ring (= message) order
@@ -455,6 +471,10 @@ def main():
                 secondaries[name]["method"] = "SeqFold (ordered)" if kw.get("method") == METHOD_SEQ_FOLD \
                     else "Calculator.Multiply"
                 secondaries[name]["args"] = "full-range int64" if kw.get("wide") else "A: 16-bit signed, B: 16-bit"
+                if kw.get("pregen"):
+                    nb = max(3, -(-300_000_000 // (20 * Mq)))
+                    secondaries[name]["batches"] = (f"{nb} distinct pre-generated batches ({nb * 20 * Mq >> 20} MB), "
+                                                    "cycled; eager Sends, generator not in the timed steps")
             del ex3
 
     # BASELINE configs 4 and 5 and the public API path, under the same clock (utils/benchmarks.py)
