@@ -1358,7 +1358,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   const uint64_t n = tot < free ? tot : free;
   const uint64_t sbase = (uint64_t)s << mv.log_q, qmask = Q - 1, rot = shard_rot(mv, s);  // slot_at, hoisted
   unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
-  // PF (PTYPE_ORD_PREFETCH=1): the next window's records (their first 16 B) are loaded
+  // PF (the fold's default; PTYPE_ORD_PREFETCH=0: off): the next window's records (their first 16 B) are loaded
   // while this one is binned and run -- one block per CU (the LDS), so the registers are
   // there.  (Round 3, with the handler switch's register file: measured no faster, 188 ->
   // 200 us, and spilled to scratch.)
@@ -2144,7 +2144,9 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     static const bool win8 = !(getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 2048);
     static const bool fixed_ok = !(getenv("PTYPE_ORD_FIXED") && atoi(getenv("PTYPE_ORD_FIXED")) == 0);
     const bool fold = fixed_ok && a.fixed_method == kSeqFold && !a.method_col;
-    static const bool pf = getenv("PTYPE_ORD_PREFETCH") && atoi(getenv("PTYPE_ORD_PREFETCH")) == 1;
+    // (the fold with the next window prefetched: 0.341 vs 0.357 ms per 8 Mi SeqFold step, round 5;
+    // PTYPE_ORD_PREFETCH=0 turns it off)
+    static const bool pf = !(getenv("PTYPE_ORD_PREFETCH") && atoi(getenv("PTYPE_ORD_PREFETCH")) == 0);
 #define PT_ORD(A12)                                            \
   do {                                                         \
     if (win8 && !(A12)) {                                      \
