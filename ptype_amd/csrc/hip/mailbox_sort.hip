@@ -433,13 +433,18 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // block, after every tile's maxima are out): each field as wide as its largest
 // value, the slack of the 52 bits split between the arguments.  Fields that no
 // longer fit set bit 31 (the host then keeps 16-B records).
+__device__ __forceinline__ void rec8_next_from(const uint32_t* r8max, uint32_t* r8w, uint32_t* host, uint32_t tiles);
 __device__ __forceinline__ void rec8_next(const SortIn& in, uint32_t* r8w, uint32_t* host, uint32_t tiles) {
+  rec8_next_from(in.r8max, r8w, host, tiles);
+}
+__device__ __forceinline__ void rec8_next_from(const uint32_t* r8max, uint32_t* r8w, uint32_t* host, uint32_t tiles) {
   __shared__ uint32_t mx[3];
   if (threadIdx.x < 3) mx[threadIdx.x] = 0;
   __syncthreads();
   uint32_t bm = 0, b0 = 0, b1 = 0;
   for (uint32_t t = threadIdx.x; t < tiles; t += blockDim.x) {
-    const uint32_t x = __hip_atomic_fetch_add(in.r8max + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t x = __hip_atomic_fetch_add(const_cast<uint32_t*>(r8max) + t, 0u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
     bm = max(bm, x & 0xffu), b0 = max(b0, (x >> 8) & 0xffu), b1 = max(b1, (x >> 16) & 0xffu);
   }
   bm = wave_max_u32(bm), b0 = wave_max_u32(b0), b1 = wave_max_u32(b1);
@@ -514,10 +519,24 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   if constexpr (!LATE) load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
   resolve_k<MODE, SK>(in, a, r, mb);
   uint32_t wr[SK];
+  // an ordered batch in 8-B records (!spill): a message whose fields do not fit takes no
+  // ring position at all -- it must not leave a hole the drain would read -- and answers
+  // kStatusOverflow (re-sent with the next widths)
+  uint32_t esc_pre = 0;
+  if (!LATE && in.rec8 && !spill) {
+    const uint32_t w8p = *in.r8w, wm = w8p & 0xffu, w0 = (w8p >> 8) & 0xffu, w1 = (w8p >> 16) & 0xffu;
+#pragma unroll
+    for (int k = 0; k < SK; ++k) {
+      const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
+      const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
+      if ((mb[k] >> wm) != 0 || (z0 >> w0) != 0 || (z1 >> w1) != 0) esc_pre |= 1u << k;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < SK; ++k) {
-    const bool ok = tile_index<SK>(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
-    if (!ok) mb[k] = kNoSlot;
+    const bool ok = tile_index<SK>(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox &&
+                    !((esc_pre >> k) & 1u);
+    if (!ok && !((esc_pre >> k) & 1u)) mb[k] = kNoSlot;
     const uint32_t sh = mb[k] & (S - 1);
     const uint64_t peers = match_bits(sh, mv.log_s, __ballot(ok));
     const unsigned below = mbcnt64(peers);
@@ -1330,11 +1349,51 @@ struct OrdLds {
 // consumer for the whole Send: its state stays in a register and each record is
 // one fold (reply = the state before, state = state * kFoldMul + a0) -- no handler
 // switch, no LDS state round trip per message.
-template <bool A12, int OK = kOrdK, int FIXED = 0, bool PF = false>
-__global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView mv, uint32_t* __restrict__ gsum,
+// R8: the sort wrote 8-B records (a uniform one-argument batch): each carries its
+// place in its tile (12 bits), the mailbox and the zigzag argument at the widths
+// *r8w; mbx_rec8_next_kernel derives the next Send's widths after the drain.
+struct R8Args {
+  const uint32_t* r8w = nullptr;  // this Send's widths (the sort's)
+  uint32_t method = 0;            // the batch's uniform method
+};
+__device__ __forceinline__ SortRec decode_rec8_ord(uint64_t r, uint32_t w8, uint32_t method) {
+  const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
+  SortRec x;
+  x.valid = true;
+  x.origin = (uint32_t)(r & (kSTile - 1));  // the place in the tile
+  x.mb = (uint32_t)((r >> 12) & ((1ull << wm) - 1));
+  x.method = method;
+  x.flags = 0;
+  x.a2 = 0;
+  const uint64_t z0 = (r >> (12 + wm)) & ((1ull << w0) - 1), z1 = (r >> (12 + wm + w0)) & ((1ull << w1) - 1);
+  x.a0 = (int64_t)(z0 >> 1) ^ -(int64_t)(z0 & 1);
+  x.a1 = (int64_t)(z1 >> 1) ^ -(int64_t)(z1 & 1);
+  return x;
+}
+
+// A window's records (their first 16 B; R8: the 8-B record), wave w's positions.
+template <bool R8, int OK>
+__device__ __forceinline__ void ord_load_win(const MboxView& mv, uint64_t wa, uint64_t n_end, uint64_t sbase,
+                                             uint64_t rot, uint64_t qmask, unsigned w, unsigned lane,
+                                             typename std::conditional<R8, uint64_t, u32x4>::type (&h)[OK]) {
+#pragma unroll
+  for (int k = 0; k < OK; ++k) {
+    const uint64_t q = wa + (uint64_t)w * (kWave * OK) + (uint64_t)k * kWave + lane;
+    const uint64_t sl = sbase | ((q + rot) & qmask);
+    const bool in = q < n_end && q < wa + (kOrdThreads * OK);
+    if constexpr (R8) h[k] = in ? reinterpret_cast<const uint64_t*>(mv.rec)[sl] : 0ull;
+    else h[k] = in ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl)) : u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
+// (one block per CU whatever its registers -- the window's LDS -- so the register
+// budget is that of 2 waves per SIMD: no spill for the prefetched window)
+template <bool A12, int OK = kOrdK, int FIXED = 0, bool PF = false, bool R8 = false>
+__global__ __launch_bounds__(kOrdThreads) __attribute__((amdgpu_waves_per_eu(1, 2))) void mbx_drain_ordered_kernel(MboxView mv, uint32_t* __restrict__ gsum,
                                                                         uint32_t ngroups, int64_t* __restrict__ state,
                                                                         uint32_t n_state, uint64_t delay_ticks,
-                                                                        OutboxView ob, u32x4* __restrict__ srep) {
+                                                                        OutboxView ob, u32x4* __restrict__ srep,
+                                                                        uint32_t origin_base, R8Args r8) {
   extern __shared__ __align__(16) unsigned char smem_ord[];
   OrdLds<A12, OK>& L = *reinterpret_cast<OrdLds<A12, OK>*>(smem_ord);
   int64_t* st_lds = reinterpret_cast<int64_t*>(smem_ord + sizeof(OrdLds<A12, OK>));
@@ -1363,17 +1422,11 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   // there.  (Round 3, with the handler switch's register file: measured no faster, 188 ->
   // 200 us, and spilled to scratch.)
   const uint64_t n_end = lo + n;
-  auto load_win = [&](uint64_t wa, u32x4(&h)[OK]) {
-#pragma unroll
-    for (int k = 0; k < OK; ++k) {
-      const uint64_t q = wa + (uint64_t)w * (kWave * OK) + (uint64_t)k * kWave + lane;
-      h[k] = q < n_end && q < wa + (kOrdThreads * OK) ? *reinterpret_cast<const u32x4*>(rec_a(mv, sbase | ((q + rot) & qmask)))
-                                                      : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-  u32x4 cur[PF ? OK : 1];
+  using RawT = typename std::conditional<R8, uint64_t, u32x4>::type;  // a record's first (R8: only) word
+  const uint32_t w8 = R8 ? *r8.r8w : 0u;
+  RawT cur[PF ? OK : 1];
   if constexpr (PF) {
-    if (lo < n_end) load_win(lo, cur);
+    if (lo < n_end) ord_load_win<R8, OK>(mv, lo, n_end, sbase, rot, qmask, w, lane, cur);
   }
   for (uint64_t w0 = lo; w0 < lo + n; w0 += (kOrdThreads * OK)) {
     const uint64_t w1 = lo + n < w0 + (kOrdThreads * OK) ? lo + n : w0 + (kOrdThreads * OK);
@@ -1381,16 +1434,20 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
     SortRec x[OK];
     uint32_t bin[OK], wr[OK];
     uint64_t slot[OK];
-    u32x4 nxt[PF ? OK : 1];
+    RawT nxt[PF ? OK : 1];
     if constexpr (PF) {
-      if (w0 + (kOrdThreads * OK) < n_end) load_win(w0 + (kOrdThreads * OK), nxt);
+      if (w0 + (kOrdThreads * OK) < n_end)
+        ord_load_win<R8, OK>(mv, w0 + (kOrdThreads * OK), n_end, sbase, rot, qmask, w, lane, nxt);
     }
 #pragma unroll
     for (int k = 0; k < OK; ++k) {  // wave w owns window positions [w * 64K, (w+1) * 64K)
       const uint64_t q = w0 + (uint64_t)w * (kWave * OK) + (uint64_t)k * kWave + lane;
       slot[k] = sbase | ((q + rot) & qmask);
       if (q < w1) {
-        if constexpr (PF) {
+        if constexpr (R8) {
+          x[k] = decode_rec8_ord(PF ? (uint64_t)cur[k] : reinterpret_cast<const uint64_t*>(mv.rec)[slot[k]], w8,
+                                 r8.method);
+        } else if constexpr (PF) {
           u32x4 hb = {0u, 0u, 0u, 0u};
           int64_t a2v = 0;
           if (rec_is_long(cur[k])) {
@@ -1449,7 +1506,8 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
       L.slot[d] = (uint32_t)slot[k];
       L.act[d] = in_lds ? (x[k].mb >> mv.log_s) : x[k].mb;
       if (!reg) L.meth[d] = x[k].method | (x[k].flags << 16);
-      L.orig[d] = x[k].origin;
+      // the message's place in its tile (the completion reads the tile's runs)
+      L.orig[d] = R8 ? x[k].origin : ((x[k].origin - origin_base) & (uint32_t)(kSTile - 1));
       L.a0[d] = x[k].a0;
       if constexpr (A12) {
         L.a1[d] = x[k].a1;
@@ -1505,6 +1563,14 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ordered_kernel(MboxView
   if (threadIdx.x == 0) epoch_commit(mv, s, tot);
 }
 
+// The next Send's 8-B field widths after an ordered 8-B-record Send (one block, launched
+// after the ordered drain: every block of it has decoded with this Send's widths).
+__global__ __launch_bounds__(256) void mbx_rec8_next_kernel(const uint32_t* __restrict__ r8max,
+                                                            uint32_t* __restrict__ r8w, uint32_t* __restrict__ host,
+                                                            uint32_t tiles) {
+  rec8_next_from(r8max, r8w, host, tiles);
+}
+
 // ---------------------------------------------------------------- K3s ordered drain, binned
 // The same per-actor FIFO drain, with the shard's records binned before any runs
 // (the windowed form above is 16 dependent load -> sort -> serial
@@ -1534,7 +1600,7 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ord_bin_kernel(MboxView
                                                                         uint32_t ngroups, int64_t* __restrict__ state,
                                                                         uint32_t n_state, uint64_t delay_ticks,
                                                                         OutboxView ob, u32x4* __restrict__ srep,
-                                                                        uint32_t nr) {
+                                                                        uint32_t nr, uint32_t origin_base) {
   extern __shared__ __align__(16) unsigned char smem_ob[];
   uint32_t(*wcnt)[kOrdThreads] = reinterpret_cast<uint32_t(*)[kOrdThreads]>(smem_ob);
   uint16_t* bs = reinterpret_cast<uint16_t*>(smem_ob + (size_t)kOrdWaves * kOrdThreads * 4);
@@ -1676,7 +1742,8 @@ __global__ __launch_bounds__(kOrdThreads) void mbx_drain_ord_bin_kernel(MboxView
           m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
           const ReplyRecord rr = run_handler(m, st, nst, delay_ticks, ob, true);
           failed += rr.status != kStatusOk;
-          srep[sl[k]] = u32x4{(uint32_t)rr.value, (uint32_t)((uint64_t)rr.value >> 32), (uint32_t)rr.status, x.origin};
+          srep[sl[k]] = u32x4{(uint32_t)rr.value, (uint32_t)((uint64_t)rr.value >> 32), (uint32_t)rr.status,
+                              (x.origin - origin_base) & (uint32_t)(kSTile - 1)};
           ++done;
           ++mine;
           if (!in_lds) vm_drain();  // global state: this store lands before the bin's next load
@@ -1735,7 +1802,7 @@ __global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxV
   }
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
-    const uint32_t local = r[k].w - in.origin_base - (uint32_t)i0;
+    const uint32_t local = r[k].w;  // the place in the tile (the drains write it; 0xffffffff: none)
     if (local < n_t) {
       sval[local] = (int64_t)(((uint64_t)r[k].y << 32) | r[k].x);
       sst[local] = (uint8_t)r[k].z;
@@ -1956,8 +2023,14 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // (batches up to 512 tiles, which take the fused kernel, keep 16-B records: measured faster
   // there -- 1 Mi bench step 24.1 vs 21.9 G msg/s in three sessions -- while 8 Mi gains with 8 B)
   static const int rec8_env = getenv("PTYPE_MBOX_REC8") ? atoi(getenv("PTYPE_MBOX_REC8")) : -1;
-  const bool r8 = (rec8_env == 1 || (rec8_env < 0 && tiles > 512)) && sort_mode == 1 && !a.ordered && !a.arrival &&
-                  !a.a2 && !a.method_col && mv.planar && !all_sidx;
+  // ordered batches (PTYPE_ORD_REC8=1): a uniform one-argument batch on the windowed drain's
+  // 4096-record form takes 8-B records too -- a record that does not fit overflows (re-sent)
+  static const bool ord_rec8_env = getenv("PTYPE_ORD_REC8") && atoi(getenv("PTYPE_ORD_REC8")) == 1;
+  static const bool ord_win2048 = getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 2048;
+  static const bool ord_bin_env = getenv("PTYPE_ORD_DRAIN") && std::string(getenv("PTYPE_ORD_DRAIN")) == "bin";
+  const bool ord_r8 = a.ordered && ord_rec8_env && !a.a1 && !ord_win2048 && !ord_bin_env;
+  const bool r8 = (rec8_env == 1 || (rec8_env < 0 && tiles > 512)) && sort_mode == 1 && (!a.ordered || ord_r8) &&
+                  !a.arrival && !a.a2 && !a.method_col && mv.planar && !all_sidx;
   if (r8 && (!r8w_ || r8_tiles_ < (uint64_t)tiles_ws)) {  // (outside a capture: grown with the sort workspace)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
@@ -2123,20 +2196,26 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     const uint32_t n_loc = a.state && a.n_state ? std::min<uint32_t>((a.n_state + Sv - 1) / Sv, kOrdStateMax) : 0;
     const size_t st_lds = (size_t)n_loc * sizeof(int64_t);  // (covers every shard the kernel stages: n_loc <= cap)
     const bool a12 = a.a1 || a.a2;  // (a column given: staged; none: the handlers see zeros)
-#define PT_ORD4(A12, OKV, FXV, PFV)                                                                           \
+    R8Args r8a;
+    if (r8_on) {
+      r8a.r8w = r8w_;
+      r8a.method = (uint32_t)a.method_uniform;
+    }
+#define PT_ORD5(A12, OKV, FXV, PFV, R8V)                                                                      \
   do {                                                                                                        \
     const size_t lds = sizeof(OrdLds<A12, OKV>) + std::max<size_t>(st_lds, 16);                              \
     static bool attr = false;                                                                                 \
     if (!attr) { /* above the 64 KB default dynamic LDS */                                                    \
-      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12, OKV, FXV, PFV>,             \
+      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_drain_ordered_kernel<A12, OKV, FXV, PFV, R8V>,        \
                                        hipFuncAttributeMaxDynamicSharedMemorySize,                            \
                                        (int)(sizeof(OrdLds<A12, OKV>) + (size_t)kOrdStateMax * sizeof(int64_t)))); \
       attr = true;                                                                                            \
     }                                                                                                         \
-    hipLaunchKernelGGL((mbx_drain_ordered_kernel<A12, OKV, FXV, PFV>), dim3(Sv), dim3(kOrdThreads), lds, st,  \
-                       mv, sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob,              \
-                       (u32x4*)stage_rep_);                                                                   \
+    hipLaunchKernelGGL((mbx_drain_ordered_kernel<A12, OKV, FXV, PFV, R8V>), dim3(Sv), dim3(kOrdThreads), lds,  \
+                       st, mv, sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob,          \
+                       (u32x4*)stage_rep_, a.origin_base, r8a);                                               \
   } while (0)
+#define PT_ORD4(A12, OKV, FXV, PFV) PT_ORD5(A12, OKV, FXV, PFV, false)
 #define PT_ORD3(A12, OKV, FXV) PT_ORD4(A12, OKV, FXV, false)
     // one-argument batches: 4096-record windows (PTYPE_ORD_WIN=2048: the 2048-record form;
     // round 5: 0.375 vs 0.383 ms per 8 Mi SeqFold step), and a uniform SeqFold batch folds
@@ -2149,7 +2228,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     static const bool pf = !(getenv("PTYPE_ORD_PREFETCH") && atoi(getenv("PTYPE_ORD_PREFETCH")) == 0);
 #define PT_ORD(A12)                                            \
   do {                                                         \
-    if (win8 && !(A12)) {                                      \
+    if (r8_on) { /* (ord_r8: one-argument, 4096-record form) */ \
+      if (fold && pf) PT_ORD5(false, 8, kSeqFold, true, true); \
+      else PT_ORD5(false, 8, 0, false, true);                  \
+    } else if (win8 && !(A12)) {                               \
       if (fold && pf) PT_ORD4(false, 8, kSeqFold, true);       \
       else if (fold) PT_ORD3(false, 8, kSeqFold);              \
       else PT_ORD3(false, 8, 0);                               \
@@ -2182,7 +2264,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       uint32_t nr = nr_env > 0 ? std::min<uint32_t>((uint32_t)nr_env, kOrdBinRoundsMax) : kOrdBinRoundsMax;
       while (nr > 1 && ord_bin_lds_bytes(nr, n_loc) > cap) --nr;
       hipLaunchKernelGGL(mbx_drain_ord_bin_kernel, dim3(Sv), dim3(kOrdThreads), ord_bin_lds_bytes(nr, n_loc), st, mv,
-                         sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_, nr);
+                         sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_, nr,
+                         a.origin_base);
     } else if (a12) {
       PT_ORD(true);
     } else {
@@ -2191,6 +2274,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_ORD
 #undef PT_ORD3
 #undef PT_ORD4
+#undef PT_ORD5
+    if (r8_on)
+      hipLaunchKernelGGL(mbx_rec8_next_kernel, dim3(1), dim3(256), 0, st, (const uint32_t*)r8max_, r8w_, r8host_,
+                         in.tiles);
     PT_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(mbx_complete_ring_kernel, dim3(tile_grid), dim3(kST),
                        (size_t)kSTile * (8 + 2 + 1) + (size_t)Sv * 8, st, in, mv,
