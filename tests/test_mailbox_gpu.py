@@ -629,3 +629,61 @@ def test_sorted_mailbox_onepass_epoch_tag_wraps():
         assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1), k
     assert mb._m.epoch_counter == start + 4
     assert mb.stats()["lookback_timeouts"] == 0
+
+
+_ORD_REC8 = textwrap.dedent("""
+    import json, os, sys, torch
+    sys.path.insert(0, os.environ["PTYPE_ROOT"])
+    sys.path.insert(0, os.path.join(os.environ["PTYPE_ROOT"], "tests"))
+    from ptype_amd.ops import batch as B
+    from ptype_amd.ops.mailbox import audit_fold
+    from ptype_amd.ops.records import METHOD_SEQ_FOLD, STATUS_OK
+    from ptype_amd.ops.table import RegistryTable, actor_keys
+    from ptype_amd.parallel.exchange import ActorExchange
+    dev = torch.device("cuda", 0)
+    n, M = 65536, 2_300_000  # 562 tiles: past the 512 that keep 16-B records
+    t = RegistryTable(2 * n, device=dev)
+    ids = torch.arange(n)
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(5))
+    t.upsert(actor_keys(ids), torch.zeros(n, dtype=torch.int32), perm.to(torch.int32))
+    t.enable_directory(n)
+    state = torch.randint(0, 1 << 30, (n,), dtype=torch.int64, device=dev)
+    ex = ActorExchange(t, M, state=state)
+    out = {}
+    for rnd in range(3):
+        g = torch.Generator().manual_seed(100 + rnd)
+        actor = torch.randint(0, n, (M,), generator=g, dtype=torch.int32)
+        # 16-bit arguments (8-B records), then one argument wider than the widths in force:
+        # it overflows and send_all re-sends it (in whatever records the next Send takes)
+        a0 = torch.randint(-30000, 30000, (M,), generator=g, dtype=torch.int64)
+        if rnd == 2:
+            a0[12345] = 1 << 40
+        b = B.MsgBatch(actor.to(dev), a0.to(dev), None, None, METHOD_SEQ_FOLD)
+        s0 = state.cpu().clone()
+        v, st = ex.send_all(b)
+        torch.cuda.synchronize()
+        s1 = state.cpu().clone()
+        ok, info = audit_fold(perm[actor.long()], a0, v.cpu(), st.cpu(), s0, s1)
+        out[rnd] = {"ok": bool(ok), "all_ok": bool((st == STATUS_OK).all()),
+                    "rec_bytes": int(ex.mailboxes.last_record_bytes), "info": "" if ok else str(info)[:300]}
+    print("RESULT " + json.dumps(out), flush=True)
+""")
+
+
+def test_mailbox_seqfold_in_8b_records_exactly_once_fifo():
+    """Ordered Sends in 8-B records (PTYPE_ORD_REC8=1): each message's place in its
+    tile rides through the ordered drain's reply stage, a message whose argument
+    outgrows the widths in force takes no ring position (no hole the drain could
+    read) and is re-sent -- every actor's replies still chain exactly once, in
+    FIFO order, over three Sends."""
+    env = dict(os.environ, PTYPE_ROOT=ROOT, PTYPE_ORD_REC8="1")
+    r = subprocess.run([sys.executable, "-c", _ORD_REC8], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    import json
+
+    out = json.loads(line[0][7:])
+    for rnd, o in out.items():
+        assert o["ok"] and o["all_ok"], (rnd, o)
+    assert out["0"]["rec_bytes"] == 8, out  # the ordered Send really took 8-B records
