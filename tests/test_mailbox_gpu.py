@@ -641,7 +641,7 @@ _ORD_REC8 = textwrap.dedent("""
     from ptype_amd.ops.table import RegistryTable, actor_keys
     from ptype_amd.parallel.exchange import ActorExchange
     dev = torch.device("cuda", 0)
-    n, M = 65536, 2_300_000  # 562 tiles: past the 512 that keep 16-B records
+    n, M = 65536, 4_300_000  # 1050 tiles: the one-pass sort (>= 1024 tiles), past the 512 that keep 16-B records
     t = RegistryTable(2 * n, device=dev)
     ids = torch.arange(n)
     perm = torch.randperm(n, generator=torch.Generator().manual_seed(5))

@@ -292,13 +292,23 @@ _DUPLEX = textwrap.dedent("""
     t = time.perf_counter()
     srv.call_many(req.ctypes.data, rep.ctypes.data, n, 120.0)
     relay_s = time.perf_counter() - t
+    # keep relays in flight (batches of 10 K, both ways) for at least half a second, so the
+    # local callers' p50 is measured while the dispatcher has parked relays
+    more, exact_more = 0, True
+    rep2 = np.zeros((n, 2), dtype=np.int64)
+    while time.perf_counter() - t < 0.5 or more < 3:
+        srv.call_many(req.ctypes.data, rep2.ctypes.data, n, 120.0)
+        exact_more = exact_more and bool((rep2[:, 0] == a * b).all()) and bool(((rep2[:, 1] & 0xff) == STATUS_OK).all())
+        more += 1
+    relay_total_s = time.perf_counter() - t
     stop.set()
     th.join()
     st = rep[:, 1] & 0xff
     base = sorted(base[200:])
     during = sorted(during[50:]) or [0.0]
-    out = {"exact": bool((rep[:, 0] == a * b).all()) and bool((st == STATUS_OK).all()),
-           "not_delivered": int((st == 5).sum()), "relay_s": relay_s, "relays_per_s": n / relay_s,
+    out = {"exact": bool((rep[:, 0] == a * b).all()) and bool((st == STATUS_OK).all()) and exact_more,
+           "not_delivered": int((st == 5).sum()), "relay_s": relay_s, "relays_per_s": n * (1 + more) / relay_total_s,
+           "relay_batches": 1 + more,
            "local_p50_us": base[len(base) // 2] * 1e6, "local_p50_during_us": during[len(during) // 2] * 1e6,
            "local_calls_during": len(during), "slots": [int(x) for x in relay.slots()]}
     print("RESULT " + json.dumps(out), flush=True)
@@ -342,8 +352,9 @@ def test_duplex_relays_do_not_block_the_dispatchers():
     assert rcs == [0, 0], [p.stderr.read()[-2000:] for p in ps]
     for o in outs:
         assert o["exact"] and o["not_delivered"] == 0, o
-        assert o["local_calls_during"] > 0, o  # the dispatcher served its own ring while relays were parked
-        assert o["local_p50_during_us"] < 200.0, o
+        assert o["local_calls_during"] > 100, o  # the dispatcher served its own ring while relays were parked
+        # other callers' p50 while relays are in flight: within a few microseconds of the quiet p50
+        assert o["local_p50_during_us"] < max(3 * o["local_p50_us"], o["local_p50_us"] + 30.0), o
 
 
 _SLOW_SERVER = textwrap.dedent("""
