@@ -2023,9 +2023,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // (batches up to 512 tiles, which take the fused kernel, keep 16-B records: measured faster
   // there -- 1 Mi bench step 24.1 vs 21.9 G msg/s in three sessions -- while 8 Mi gains with 8 B)
   static const int rec8_env = getenv("PTYPE_MBOX_REC8") ? atoi(getenv("PTYPE_MBOX_REC8")) : -1;
-  // ordered batches (PTYPE_ORD_REC8=1): a uniform one-argument batch on the windowed drain's
-  // 4096-record form takes 8-B records too -- a record that does not fit overflows (re-sent)
-  static const bool ord_rec8_env = getenv("PTYPE_ORD_REC8") && atoi(getenv("PTYPE_ORD_REC8")) == 1;
+  // ordered batches: a uniform one-argument batch on the windowed drain's 4096-record form
+  // takes 8-B records too -- a record that does not fit overflows (re-sent).  Round 5: 25.5
+  // vs 24.5 G msg/s per 8 Mi SeqFold step; PTYPE_ORD_REC8=0 keeps 16-B records
+  static const bool ord_rec8_env = !(getenv("PTYPE_ORD_REC8") && atoi(getenv("PTYPE_ORD_REC8")) == 0);
   static const bool ord_win2048 = getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 2048;
   static const bool ord_bin_env = getenv("PTYPE_ORD_DRAIN") && std::string(getenv("PTYPE_ORD_DRAIN")) == "bin";
   const bool ord_r8 = a.ordered && ord_rec8_env && !a.a1 && !ord_win2048 && !ord_bin_env;
