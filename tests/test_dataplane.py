@@ -377,3 +377,49 @@ def test_join_world1_reforms_after_a_flagged_failure(tmp_path, ports, monkeypatc
     finally:
         c.Close()
         srv.Close()
+
+
+def test_native_dataplane_membership_on_cpu(tmp_path, ports, monkeypatch):
+    """The compiled data plane's membership half (csrc/core/dataplane.cpp) without a
+    GPU: live nodes from the registry's leases, wait_nodes, and settle -- bounded by
+    its grace when nobody of the current members is gone, and the survivors in
+    their old order once a member's registration ends (the next generation's
+    proposal).  (form / ncclCommInitRank: tests/test_elastic_gpu.py.)"""
+    monkeypatch.setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    from ptype_amd import _core
+    from ptype_amd import cluster as C
+
+    if not _core.DataPlane.available():
+        pytest.skip("RCCL / HIP entry points not loaded in this process")
+    pp, pc, pa, pb = ports(), ports(), ports(), ports()
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "dp", "a", pa
+    cfg.member = _member(C, 0, [pp], [pc], f"e0=http://127.0.0.1:{pp}", str(tmp_path))
+    c = C.Join(C.background(), cfg, runtime=False)
+    other = None
+    try:
+        me, b = f"127.0.0.1:{pa}", f"127.0.0.1:{pb}"
+        other = C.new_etcd_registry([f"http://127.0.0.1:{pc}"])
+        other.Register(C.background(), "dp", "b", "127.0.0.1", pb)
+        dp = _core.DataPlane(c._c, "dp", me, -1, 10.0)
+        t0 = time.time()
+        while sorted(dp.alive_nodes()) != sorted([me, b]) and time.time() - t0 < 10:
+            time.sleep(0.05)
+        assert sorted(dp.alive_nodes()) == sorted([me, b])
+        assert dp.wait_nodes(2) == sorted([me, b])
+        # nobody of the current members is gone: the proposal after the grace, unchanged
+        t0 = time.time()
+        assert dp.settle([b, me], 0.4) == [b, me]
+        assert 0.35 < time.time() - t0 < 3.0
+        # b's registration ends: the survivors, without waiting out a long grace
+        other.close()
+        other = None
+        t0 = time.time()
+        assert dp.settle([b, me], 15.0) == [me]
+        assert time.time() - t0 < 8.0  # (the 2 s lease, or at once when the close revoked it)
+        # a proposal that lost this member too still carries it
+        assert dp.settle([b], 0.2) == [me]
+    finally:
+        if other is not None:
+            other.close()
+        c.Close()
