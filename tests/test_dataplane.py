@@ -423,3 +423,45 @@ def test_native_dataplane_membership_on_cpu(tmp_path, ports, monkeypatch):
         if other is not None:
             other.close()
         c.Close()
+
+
+def test_native_dataplane_rendezvous_converges_on_cpu(tmp_path, ports, monkeypatch):
+    """The compiled rendezvous without a GPU: the first current record of a
+    generation wins -- a member whose proposal differs adopts it, a member it
+    leaves out learns it is excluded -- and the communicator step (hipSetDevice,
+    ncclCommInitRank) is the only part left (it fails here for want of a device)."""
+    monkeypatch.setenv("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    from ptype_amd import _core
+    from ptype_amd import cluster as C
+
+    if not _core.DataPlane.available():
+        pytest.skip("RCCL / HIP entry points not loaded in this process")
+    pp, pc, pa, pb = ports(), ports(), ports(), ports()
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = "rv", "a", pa
+    cfg.member = _member(C, 0, [pp], [pc], f"e0=http://127.0.0.1:{pp}", str(tmp_path))
+    c = C.Join(C.background(), cfg, runtime=False)
+    other = C.new_etcd_registry([f"http://127.0.0.1:{pc}"])
+    try:
+        me, b = f"127.0.0.1:{pa}", f"127.0.0.1:{pb}"
+        other.Register(C.background(), "rv", "b", "127.0.0.1", pb)
+        da = _core.DataPlane(c._c, "rv", me, -1, 5.0)
+        db = _core.DataPlane(c._c, "rv", b, -1, 5.0)
+        da.wait_nodes(2)
+        # a proposes [a] alone (its view: b is gone) and publishes generation 3's record
+        with pytest.raises(RuntimeError, match="no device"):
+            da.form(3, [me])
+        # b, proposing [a, b], adopts the published record -- and is not in it
+        with pytest.raises(RuntimeError, match="excluded"):
+            db.form(3, [me, b])
+        # a record for a later generation with both: b is rank 1 of it (reaches the device step)
+        with pytest.raises(RuntimeError, match="no device"):
+            da.form(4, [me, b])
+        with pytest.raises(RuntimeError, match="no device"):
+            db.form(4, [me, b])
+        # a member outside its own proposal is refused at once
+        with pytest.raises(RuntimeError, match="not in the proposal"):
+            db.form(5, [me])
+    finally:
+        other.close()
+        c.Close()
