@@ -450,6 +450,9 @@ def main():
             # 315 MB: more than the MALL), every step an eager Send through the actor-sharded rings
             runs.append(("config2_1m_pregen", dict(delivery="mailbox", sharding="actor", Mq=min(M, 1 << 20),
                                                    pregen=True)))
+            # the headline step with the client's batches made before the timing (3 distinct 8 Mi
+            # batches, 503 MB): the Send alone, eager
+            runs.append(("mailbox_pregen", dict(delivery="mailbox", sharding="actor", pregen=True)))
             runs.append(("arrival_sharded", dict(delivery="mailbox", sharding="arrival")))
             # an ORDERED stateful method (SeqFold: state = state * K + a0, non-commutative):
             # every actor runs its messages one at a time in ring (= message) order
