@@ -14,9 +14,9 @@ echo "suite rc=$rc"; grep -E "passed|failed|FAILED" gpurun_out/${TAG}_suite.log 
 [ $rc -le 1 ] || exit 3
 timeout -k 10 600 python3 bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err; rc=$?
 echo "bench rc=$rc"
-python3 - <<'PY'
-import json, sys
-l = [x for x in open("gpurun_out/r5k_bench.json") if x.startswith("{")][-1]
+TAG=$TAG python3 - <<'PY'
+import json, os, sys
+l = [x for x in open(f"gpurun_out/{os.environ['TAG']}_bench.json") if x.startswith("{")][-1]
 d = json.loads(l)
 print("headline", round(d["value"] / 1e9, 2), "G", round(d["ms_per_step"], 4), "ms")
 for k, v in d.get("secondaries", {}).items():
