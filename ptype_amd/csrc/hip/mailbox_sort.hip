@@ -482,12 +482,29 @@ __device__ __forceinline__ void rec8_next_from(const uint32_t* r8max, uint32_t* 
 // epoch's total): 16 device-scope atomics per tile, ~2048 per counter at 8 Mi
 // messages -- against a look-back whose walk grows with the tiles in flight
 // (each hop a memory-side round trip).
-template <int MODE, bool A2, bool MC, bool LATE, int SK = kSK>
+// A tile's input columns in registers (the persistent sort loads tile t + 1's while
+// tile t ranks, reserves and scatters).
+template <int SK>
+struct TileRegs {
+  uint32_t a[SK], meth[SK];
+  int64_t v0[SK], v1[SK], v2[SK];
+};
+template <bool A2, bool MC, int SK>
+__device__ __forceinline__ void load_tile_regs(const SortIn& in, uint32_t t, TileRegs<SK>& r) {
+  load_actors<SK>(in, t, r.a);
+  load_cols<A2, MC, SK>(in, t, r.v0, r.v1, r.v2, r.meth);
+}
+
+// PRE: the tile (t_pre) and its inputs (*cur) come from the caller, and once its
+// messages are ranked the next tile's inputs (t_next) are loaded into *nxt.
+template <int MODE, bool A2, bool MC, bool LATE, int SK = kSK, bool PRE = false>
 __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxView& mv, unsigned long long* __restrict__ desc,
                                                   unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                   uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
                                                   uint32_t* __restrict__ rw, const ReplyView& rv, bool spill,
-                                                  bool all_sidx, unsigned char* smem_os, bool reserve = false) {
+                                                  bool all_sidx, unsigned char* smem_os, bool reserve = false,
+                                                  TileRegs<SK>* cur = nullptr, TileRegs<SK>* nxt = nullptr,
+                                                  uint32_t t_pre = 0, uint32_t t_next = 0xffffffffu) {
   const uint32_t S = 1u << mv.log_s;
   unsigned long long* base = reinterpret_cast<unsigned long long*>(smem_os);  // ring position of this tile's run (tail + prefix)
   uint32_t* room = reinterpret_cast<uint32_t*>(base + S);                     // offset limit past the tail
@@ -510,13 +527,21 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   __syncthreads();
   // (reserve: tiles dealt XCD by XCD, as the ring drain deals them -- its reads of a tile's runs then
   // meet the lines in the L2 that took the sort's stores)
-  const uint32_t t = reserve ? virt_block(blockIdx.x, gridDim.x) : tile_s;
+  const uint32_t t = PRE ? t_pre : reserve ? virt_block(blockIdx.x, gridDim.x) : tile_s;
   // the tile's columns: actors, then the arguments in flight across the gathers and the ranking
   uint32_t a[SK], mb[SK], meth[SK];
   int64_t v0[SK], v1[SK], v2[SK];
   int r[SK];
-  load_actors<SK>(in, t, a);
-  if constexpr (!LATE) load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
+  if constexpr (PRE) {
+#pragma unroll
+    for (int k = 0; k < SK; ++k) {
+      a[k] = cur->a[k], meth[k] = cur->meth[k];
+      v0[k] = cur->v0[k], v1[k] = cur->v1[k], v2[k] = cur->v2[k];
+    }
+  } else {
+    load_actors<SK>(in, t, a);
+    if constexpr (!LATE) load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
+  }
   resolve_k<MODE, SK>(in, a, r, mb);
   uint32_t wr[SK];
   // an ordered batch in 8-B records (!spill): a message whose fields do not fit takes no
@@ -549,6 +574,9 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     wr[k] = (unsigned)__shfl((int)old, leader) + below;
   }
   __syncthreads();
+  if constexpr (PRE) {  // the next tile's inputs, in flight across this one's reservation and scatter
+    if (t_next < in.tiles) load_tile_regs<A2, MC, SK>(in, t_next, *nxt);
+  }
   // per shard: wave offsets within the tile, publish the tile's count, look back for its prefix
   const uint64_t Q = 1ull << mv.log_q;
   unsigned long long timeouts = 0;
@@ -715,6 +743,36 @@ __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView m
   extern __shared__ __align__(16) unsigned char smem_os[];
   (void)onesweep_tile<MODE, A2, MC, LATE, SK>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill, all_sidx, smem_os,
                                               reserve);
+}
+
+// The reserving one-pass sort as a persistent grid (PTYPE_MBOX_PERSIST=1, experiment):
+// each block owns a contiguous range of tiles (its XCD's share, as the ring drain
+// deals them) and loads tile t + 1's inputs while tile t ranks, reserves and
+// scatters -- the input loads' latency off the per-tile chain.  Two register sets,
+// alternated by an unrolled pair of tiles (no indexed register arrays).
+template <int MODE, bool A2, bool MC, int SK = kSK>
+__global__ __launch_bounds__(kST) void mbx_onesweep_persist_kernel(SortIn in, MboxView mv,
+                                                                   unsigned long long* __restrict__ desc,
+                                                                   unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
+                                                                   uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
+                                                                   uint32_t* __restrict__ rw, ReplyView rv, bool spill,
+                                                                   bool all_sidx) {
+  extern __shared__ __align__(16) unsigned char smem_os[];
+  const uint32_t G = gridDim.x, vb = virt_block(blockIdx.x, G);
+  const uint32_t per = (in.tiles + G - 1) / G, t0 = vb * per, t1 = min(t0 + per, in.tiles);
+  TileRegs<SK> r0, r1;
+  if (t0 < t1) load_tile_regs<A2, MC, SK>(in, t0, r0);
+  for (uint32_t t = t0; t < t1; t += 2) {
+    (void)onesweep_tile<MODE, A2, MC, false, SK, true>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill,
+                                                       all_sidx, smem_os, true, &r0, &r1, t,
+                                                       t + 1 < t1 ? t + 1 : 0xffffffffu);
+    __syncthreads();  // the tile's LDS is reused
+    if (t + 1 >= t1) break;
+    (void)onesweep_tile<MODE, A2, MC, false, SK, true>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill,
+                                                       all_sidx, smem_os, true, &r1, &r0, t + 1,
+                                                       t + 2 < t1 ? t + 2 : 0xffffffffu);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- compact record decode
@@ -2157,6 +2215,11 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     // PTYPE_MBOX_SK=4 (experiment; stateless two-column batches, ring-order drain): 2048-message
     // tiles for the sort and the drain -- fewer registers per wave, more blocks per CU
     mid = mid_ok && !late;
+    static const int persist_env = getenv("PTYPE_MBOX_PERSIST") ? atoi(getenv("PTYPE_MBOX_PERSIST")) : 0;
+    const bool persist = persist_env > 0 && reserve && !mid && !late;
+    // blocks: PTYPE_MBOX_PERSIST per CU (256 CUs), a multiple of 8 (one contiguous range per XCD)
+    uint32_t pgrid = (uint32_t)std::min<int64_t>(tiles, (int64_t)256 * std::max(persist_env, 1));
+    if (pgrid >= 8) pgrid -= pgrid % 8;
     if (mid) {
       in.tiles = (uint32_t)((a.M + kST * 4 - 1) / (kST * 4));
       tile_grid = in.tiles >= 8 ? (in.tiles + 7) / 8 * 8 : in.tiles;
@@ -2170,6 +2233,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #define PT_OS2(MO, A2, MC, LT)                                     \
   do {                                                             \
     if (mid && !(A2) && !(MC) && !(LT)) PT_OS3(MO, false, false, false, 4); \
+    else if (persist && !(A2) && !(MC) && !(LT))                   \
+      hipLaunchKernelGGL((mbx_onesweep_persist_kernel<MO, false, false, kSK>), dim3(pgrid), dim3(kST),            \
+                         onesweep_lds_bytes(Sv), st, in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo,   \
+                         sort_rw_, rv, !a.ordered, all_sidx);                                                          \
     else PT_OS3(MO, A2, MC, LT, kSK);                              \
   } while (0)
 #define PT_OS1(MO, A2, MC)              \
