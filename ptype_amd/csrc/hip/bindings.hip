@@ -77,7 +77,7 @@ void launch_dispatch_packed(uintptr_t, int, int64_t, const PackedLayout&, uintpt
                             uintptr_t, int64_t, const std::vector<uintptr_t>&, uint64_t, const std::vector<uintptr_t>&,
                             int, uintptr_t);
 void launch_complete_packed(uintptr_t, int64_t, int, int, uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, bool,
-                            uintptr_t, uintptr_t);
+                            uintptr_t, uintptr_t, uintptr_t, int64_t);
 void launch_records_to_soa(uintptr_t, int64_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t, bool, uintptr_t);
 void launch_snapshot_copy(uintptr_t, uintptr_t, int64_t, uintptr_t);
 }  // namespace ptype
@@ -271,7 +271,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("outbox_cap"), py::arg("direct"), py::arg("self"), py::arg("stream"));
   m.def("complete_packed", &launch_complete_packed, py::arg("rep"), py::arg("C"), py::arg("R"), py::arg("vb"), py::arg("perm"),
         py::arg("M"), py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"),
-        py::arg("stream"), py::arg("failed") = 0);
+        py::arg("stream"), py::arg("failed") = 0, py::arg("zero") = 0, py::arg("zero_words") = 0);
 
   m.def("pinned_alloc", &pinned_alloc);
   m.def("pinned_free", &pinned_free);

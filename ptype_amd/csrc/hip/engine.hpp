@@ -70,7 +70,8 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
                             const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
                             const std::vector<uintptr_t>& direct, int self, uintptr_t stream);
 void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
-                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed = 0);
+                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed = 0,
+                            uintptr_t zero = 0, int64_t zero_words = 0);
 
 // ---- RCCL entry points (from the library torch loaded)
 namespace engine_detail {

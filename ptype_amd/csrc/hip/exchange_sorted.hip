@@ -865,8 +865,18 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
     PT_HIP_CHECK(hipMalloc(&b.reply, (size_t)R * rp * 4));
     PT_HIP_CHECK(hipMalloc(&b.back, (size_t)R * rp * 4));
     PT_HIP_CHECK(hipMalloc(&b.perm, (size_t)max_chunk * 4));
-    for (hipEvent_t* e : {&ev_routed_[i], &ev_req_in_[i], &ev_served_[i], &ev_rep_in_[i]})
-      PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    // The compute -> comm-stream hand-offs (routed, served) publish the request and
+    // reply regions to a reader on this device: RCCL's own send kernel here (it
+    // stages them through its FIFO; no peer reads a user buffer) or the loopback
+    // copy.  Their events drop the system-scope fence (-3.5 % of the loopback-8
+    // step, profiles/r5_mailbox_ab.md).  IpcComm's peers read the regions in place
+    // from their own processes, so a device-side comm keeps it, and
+    // PTYPE_SX_EVENT_FENCE=system restores it everywhere.
+    static const char* fence_env = getenv("PTYPE_SX_EVENT_FENCE");
+    const bool dev_fence = fence_env ? std::string(fence_env) == "device" : !(fake_ && fake_->device_side());
+    const unsigned local_flags = hipEventDisableTiming | (dev_fence ? hipEventDisableSystemFence : 0u);
+    for (hipEvent_t* e : {&ev_routed_[i], &ev_served_[i]}) PT_HIP_CHECK(hipEventCreateWithFlags(e, local_flags));
+    for (hipEvent_t* e : {&ev_req_in_[i], &ev_rep_in_[i]}) PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   PT_HIP_CHECK(hipMalloc(&hist_, (size_t)kMboxSortHistWords * 4));
   PT_HIP_CHECK(hipMalloc(&boff_, (size_t)kXMaxBuckets * 4));
@@ -1142,7 +1152,11 @@ void SortedExchange::send(const SxSend& a) {
   std::copy(caps_in.c, caps_in.c + kSxMaxRanks, wire_.cap_in);
   const int cur = (int)(sends_ & 1);
   uint64_t* meta = meta_dev_ + cur * kSxMetaWords;
-  PT_HIP_CHECK(hipMemsetAsync(meta, 0, kSxMetaWords * sizeof(uint64_t), cs));
+  // the previous Send's first completion cleared this buffer (it runs after that
+  // Send's reply all-to-all, so after the agreement copy of Send - 2 on the comm
+  // stream); a captured Send clears it itself
+  if (!meta_zeroed_[cur] || capturing) PT_HIP_CHECK(hipMemsetAsync(meta, 0, kSxMetaWords * sizeof(uint64_t), cs));
+  meta_zeroed_[cur] = false;
   // Sharded (ordered) regions only while the agreement in force saw an ordered
   // method on some rank (or before the first agreement): every rank derives the
   // same answer, so when it is no, no region is sharded anywhere and the
@@ -1382,14 +1396,21 @@ void SortedExchange::send(const SxSend& a) {
   } else {
     meta_send_[cur] = -1;
   }
+  static const bool zero_in_comp = !(getenv("PTYPE_SX_META_ZERO") && atoi(getenv("PTYPE_SX_META_ZERO")) == 0);
   for (int i = 0; i < chunks_; ++i) {
     int64_t lo, m;
     (void)chunk_in(i, lo, m);
     PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_rep_in_[i], 0));
-    if (m > 0)
+    if (m > 0) {
+      // the first completion also clears the agreement buffer of Send + 1 (that of
+      // Send - 1, whose copy to the host precedes this Send's reply all-to-alls)
+      const bool zero = zero_in_comp && !capturing && !meta_zeroed_[cur ^ 1];
       launch_complete_packed((uintptr_t)bufs_[i].back, C, R_, L.vb, (uintptr_t)bufs_[i].perm, m,
                              a.out_val + (uintptr_t)(lo * 8), a.out_st + (uintptr_t)(lo * 4), 0, false,
-                             (uintptr_t)cs, fake_ ? (uintptr_t)fake_->device_failed() : 0);
+                             (uintptr_t)cs, fake_ ? (uintptr_t)fake_->device_failed() : 0,
+                             zero ? (uintptr_t)(meta_dev_ + (cur ^ 1) * kSxMetaWords) : 0, zero ? kSxMetaWords : 0);
+      if (zero) meta_zeroed_[cur ^ 1] = true;
+    }
   }
   ++sends_;
 }

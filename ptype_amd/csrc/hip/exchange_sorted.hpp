@@ -167,6 +167,7 @@ class SortedExchange {
   hipEvent_t ev_meta_[2]{};
   hipEvent_t ev_join_{};  // device-side comms: the comm stream joined back into the caller's
   int64_t meta_send_[2] = {-1, -1};  // the Send whose agreement each buffer holds
+  bool meta_zeroed_[2] = {false, false};  // cleared by the previous Send's first completion launch
   hipEvent_t ev_routed_[kSxMaxChunks]{}, ev_req_in_[kSxMaxChunks]{}, ev_served_[kSxMaxChunks]{},
       ev_rep_in_[kSxMaxChunks]{};
   // the layout and capacity in force

@@ -277,7 +277,13 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
                                                               int64_t* __restrict__ out_val,
                                                               int32_t* __restrict__ out_st,
                                                               unsigned long long* __restrict__ checksum, bool direct,
-                                                              const uint64_t* __restrict__ failed) {
+                                                              const uint64_t* __restrict__ failed,
+                                                              uint64_t* __restrict__ zero, int64_t zero_words) {
+  // (an optional word range cleared on the way: the sorted exchange's next-Send
+  // agreement vector, instead of a separate fill launch on the critical path)
+  if (zero)
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < zero_words; w += (int64_t)gridDim.x * blockDim.x)
+      zero[w] = 0;
   // each source region's value plane starts past its count-sized ok bitmap: the
   // offsets once per block in LDS, not a dependent header load per message
   __shared__ uint32_t voff[kMaxRanks];
@@ -489,7 +495,8 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
 }
 
 void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
-                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed) {
+                            uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed,
+                            uintptr_t zero, int64_t zero_words) {
   if (M <= 0) return;
   if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
   if (R < 1 || R > kMaxRanks) throw std::invalid_argument("complete: 1 <= R <= 64");
@@ -500,7 +507,7 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t p
     hipLaunchKernelGGL((complete_packed_kernel<4, true>), dim3(grid_for(M, 256 * 4, checksum ? 1024 : 8192)),
                        dim3(256), 0, as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R,
                        vb, (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st,
-                       (unsigned long long*)checksum, direct, (const uint64_t*)failed);
+                       (unsigned long long*)checksum, direct, (const uint64_t*)failed, (uint64_t*)zero, zero_words);
     PT_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -508,7 +515,7 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t p
   hipLaunchKernelGGL(complete_packed_kernel<U>, dim3(grid_for(M, 256 * (U), checksum ? 1024 : 8192)), dim3(256), 0, \
                      as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R, vb,          \
                      (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum,   \
-                     direct, (const uint64_t*)failed)
+                     direct, (const uint64_t*)failed, (uint64_t*)zero, zero_words)
   if (comp_u == 8) PT_COMP(8);
   else if (comp_u == 2) PT_COMP(2);
   else PT_COMP(4);
