@@ -868,15 +868,19 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
     // The compute -> comm-stream hand-offs (routed, served) publish the request and
     // reply regions to a reader on this device: RCCL's own send kernel here (it
     // stages them through its FIFO; no peer reads a user buffer) or the loopback
-    // copy.  Their events drop the system-scope fence (-3.5 % of the loopback-8
-    // step, profiles/r5_mailbox_ab.md).  IpcComm's peers read the regions in place
-    // from their own processes, so a device-side comm keeps it, and
-    // PTYPE_SX_EVENT_FENCE=system restores it everywhere.
+    // copy.  The comm -> compute hand-offs (req_in, rep_in) publish what RCCL's
+    // receive kernel (or the loopback copy) wrote here.  Their events drop the
+    // system-scope fence (-3.5 % of the loopback-8 step for the first pair,
+    // profiles/r5_mailbox_ab.md).  IpcComm's peers read and write the regions in
+    // place from their own processes, so a device-side comm keeps it;
+    // PTYPE_SX_EVENT_FENCE=system restores it everywhere, =out only on the
+    // compute -> comm pair.
     static const char* fence_env = getenv("PTYPE_SX_EVENT_FENCE");
-    const bool dev_fence = fence_env ? std::string(fence_env) == "device" : !(fake_ && fake_->device_side());
-    const unsigned local_flags = hipEventDisableTiming | (dev_fence ? hipEventDisableSystemFence : 0u);
-    for (hipEvent_t* e : {&ev_routed_[i], &ev_served_[i]}) PT_HIP_CHECK(hipEventCreateWithFlags(e, local_flags));
-    for (hipEvent_t* e : {&ev_req_in_[i], &ev_rep_in_[i]}) PT_HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    const std::string fence = fence_env ? fence_env : (fake_ && fake_->device_side()) ? "system" : "device";
+    const unsigned out_flags = hipEventDisableTiming | (fence != "system" ? hipEventDisableSystemFence : 0u);
+    const unsigned in_flags = hipEventDisableTiming | (fence == "device" ? hipEventDisableSystemFence : 0u);
+    for (hipEvent_t* e : {&ev_routed_[i], &ev_served_[i]}) PT_HIP_CHECK(hipEventCreateWithFlags(e, out_flags));
+    for (hipEvent_t* e : {&ev_req_in_[i], &ev_rep_in_[i]}) PT_HIP_CHECK(hipEventCreateWithFlags(e, in_flags));
   }
   PT_HIP_CHECK(hipMalloc(&hist_, (size_t)kMboxSortHistWords * 4));
   PT_HIP_CHECK(hipMalloc(&boff_, (size_t)kXMaxBuckets * 4));
