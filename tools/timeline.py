@@ -5,7 +5,7 @@ import sys
 
 path = sys.argv[1]
 marker = sys.argv[2] if len(sys.argv) > 2 else "gen_requests"
-skip = ("fillBuffer",)
+skip = () if len(sys.argv) > 3 and sys.argv[3] == "all" else ("fillBuffer",)
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 gens = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 i0, i1 = gens[-3], gens[-2]
