@@ -2172,10 +2172,11 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     // 1024-message tiles (4x the blocks, 72-78 instead of 121 VGPRs).  Measured slower at 1 Mi
     // (round 5: fused kernel 40.2 vs 31.4 us, bench 19.8 vs 22.9 G msg/s): four times the
     // run reservations on the 8-shard view's counters, so 4096-message tiles stay the default.
+    // PTYPE_MBOX_SK=4: 2048-message tiles (2x the blocks and reservations)
     static const int sk_env = getenv("PTYPE_MBOX_SK") ? atoi(getenv("PTYPE_MBOX_SK")) : 0;
-    const bool small = sk_env == kSKSmall;
-    if (small) in.tiles = (uint32_t)((a.M + kST * kSKSmall - 1) / (kST * kSKSmall));
-    const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv, small ? kST * kSKSmall : kSTile));
+    const int fsk = sk_env == kSKSmall || sk_env == 4 ? sk_env : kSK;
+    if (fsk != kSK) in.tiles = (uint32_t)((a.M + kST * fsk - 1) / (kST * fsk));
+    const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv, kST * fsk));
 #define PT_SD4(MO, A2, MC, FX, R8, SKV)                                                                             \
   hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, R8, SKV>), dim3(in.tiles), dim3(kST), lds, st, in, mv,     \
                      sort_desc_,                                                                                     \
@@ -2183,7 +2184,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
                      a.delay_ticks, ob, sort_ticket_, reserve, r8host_)
 #define PT_SD3(MO, A2, MC, FX, R8)                 \
   do {                                             \
-    if (small) PT_SD4(MO, A2, MC, FX, R8, kSKSmall); \
+    if (fsk == kSKSmall) PT_SD4(MO, A2, MC, FX, R8, kSKSmall); \
+    else if (fsk == 4) PT_SD4(MO, A2, MC, FX, R8, 4); \
     else PT_SD4(MO, A2, MC, FX, R8, kSK);          \
   } while (0)
 #define PT_SD2(MO, A2, MC, FX)                               \

@@ -22,3 +22,6 @@ PTYPE_MBOX_SK=4 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-form
   $B > gpurun_out/${TAG}_prof.log 2>&1 || exit 3
 F=$(find gpurun_out/${TAG}_prof -name 'sk4_kernel_stats.csv' | head -1)
 cut -d, -f1-4 $F | sed -n 1,5p
+# device-scope atomic throughput on the hot reservation counters
+timeout -k 10 60 ./tools/atomic_contention_probe.bin > gpurun_out/${TAG}_atomics.jsonl || exit 3
+cat gpurun_out/${TAG}_atomics.jsonl
