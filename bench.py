@@ -408,7 +408,8 @@ def main():
         # mailbox_shards: the rings allocated; ring_view_shards: how the timed Sends used them (stateless
         # batches: a coarser view of the same rings, every actor's messages still in one ring)
         return {"mailbox_shards": mb.shards, "ring_view_shards": mb.last_view_shards, "mailbox_slots": mb.slots,
-                "mailbox_ring_bytes": mb.bytes, "mailbox_record_bytes": mb.last_record_bytes}
+                "mailbox_ring_bytes": mb.bytes, "mailbox_record_bytes": mb.last_record_bytes,
+                "mailbox_route": mb.last_route}
 
     table = build_table(args.placement)
     hang_s = os.environ.get("PTYPE_HANG_DIAG")
@@ -428,6 +429,8 @@ def main():
 
     route_mode = lookup_mode(table)
     head_mailbox = mailbox_info(ex)
+    if head_mailbox.get("mailbox_route") == 3:  # the stateless mailbox Send resolved ranks only
+        route_mode = "rank byte gather (1 B per id, from the route directory; stateless records carry the actor id)"
     secondaries = {}
     if args.placement != "affine" and not args.no_secondary and args.steps:
         # the same step with the strided placement, whose routes need no registry reads

@@ -471,7 +471,7 @@ PYBIND11_MODULE(_hip, m) {
              uint32_t affine_w, int rank_self, uint32_t origin_base, uintptr_t out_val, uintptr_t out_st,
              uint64_t out_n, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
              const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, bool arrival, bool ordered,
-             int fixed_method, uintptr_t stream, int sort_mode) {
+             int fixed_method, uintptr_t stream, int sort_mode, uintptr_t dir_rank) {
             MboxSend a;
             a.actor = actor, a.a0 = a0, a.a1 = a1, a.a2 = a2, a.method_col = method_col;
             a.method_uniform = method_uniform, a.M = M, a.table = table, a.cap = cap, a.dir = dir;
@@ -479,6 +479,7 @@ PYBIND11_MODULE(_hip, m) {
             a.out_val = out_val, a.out_st = out_st, a.out_n = out_n, a.state = state, a.n_state = n_state;
             a.delay_ticks = delay_ticks, a.outbox = outbox, a.outbox_cap = outbox_cap, a.arrival = arrival;
             a.ordered = ordered, a.fixed_method = fixed_method, a.stream = stream, a.sort_mode = sort_mode;
+            a.dir_rank = dir_rank;
             mb.send_sorted(a);
           },
           "epoch Send through the sorted mailboxes: stable counting-sort enqueue + ordered / parallel drain",
@@ -487,7 +488,7 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("affine_w"), py::arg("rank_self"), py::arg("origin_base"), py::arg("out_val"), py::arg("out_st"),
           py::arg("out_n"), py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"),
           py::arg("outbox_cap"), py::arg("arrival"), py::arg("ordered"), py::arg("fixed_method"), py::arg("stream"),
-          py::arg("sort_mode") = 0)
+          py::arg("sort_mode") = 0, py::arg("dir_rank") = 0)
       .def("start", &Mailboxes::start, py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"),
            py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("blocks") = 16, py::arg("idle_ms") = 0.0,
            py::arg("max_s") = 60.0)
@@ -502,6 +503,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("bytes", &Mailboxes::bytes)
       .def_property_readonly("last_record_bytes", &Mailboxes::last_record_bytes)
       .def_property_readonly("last_view_shards", &Mailboxes::last_view_shards)
+      .def_property_readonly("last_route", &Mailboxes::last_route)
       .def_property_readonly("consumer_processed", &Mailboxes::consumer_processed)
       .def_property_readonly("launches", &Mailboxes::launches)
       .def_property_readonly("handle", [](Mailboxes& m) { return (uintptr_t)&m; },

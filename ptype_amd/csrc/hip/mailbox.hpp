@@ -155,6 +155,10 @@ struct MboxSend {
   // 2 count + scatter, 3 LDS-table count + resolving scatter
   int sort_mode = 0;
   uintptr_t stream = 0;
+  // the directory's rank byte table (one byte per id): a stateless uniform batch
+  // resolves only its rank (1 MB at 1 M ids, L2-resident, against the 4 MB
+  // directory) and its records carry the actor id, which no stateless handler reads
+  uintptr_t dir_rank = 0;
 };
 
 class Mailboxes {
@@ -200,6 +204,8 @@ class Mailboxes {
   int last_record_bytes() const { return last_rec_bytes_; }
   // shards the last sorted Send's rings were viewed as (stateless batches: a coarser view, 8 by default)
   uint32_t last_view_shards() const { return last_view_shards_; }
+  // the last sorted Send's route: 0 hash probe, 1 directory, 2 affine rule, 3 rank byte table
+  int last_route() const { return last_route_; }
   uint64_t consumer_processed() const;
   uint64_t launches() const { return launches_; }
   const MboxView& view() const { return mv_; }
@@ -226,6 +232,7 @@ class Mailboxes {
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
   int last_rec_bytes_ = 0;
   uint32_t last_view_shards_ = 0;
+  int last_route_ = -1;
   uint32_t* sort_resv_ = nullptr;   // [S][kResvStride] one-pass run reservations (zero between Sends)
   // 8-B ring records: [0] the field widths in force (device; updated by each Send's
   // last block), per-tile field bit lengths, and a pinned mirror of [0] (bit 31: the

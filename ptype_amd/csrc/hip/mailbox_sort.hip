@@ -1950,6 +1950,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.table = (const TableEntry*)a.table;
   in.mask = a.cap - 1;
   in.dir = (const uint32_t*)a.dir;
+  in.dirr = (const uint8_t*)a.dir_rank;
   in.n_dir = a.n_dir;
   in.aw = a.affine_w;
   in.aw_shift = (a.affine_w && (a.affine_w & (a.affine_w - 1)) == 0) ? __builtin_ctz(a.affine_w) : -1;
@@ -2078,6 +2079,16 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   // (PTYPE_MBOX_REC8=0: 16-B records).  Field widths: the mailbox from the state size or the
   // directory (a wider mailbox spills), the rest split between the zigzag arguments.
   static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
+  // Rank byte gathers (route mode 3) for a stateless uniform one-pass Send on the
+  // directory: 1 B per id (L2-resident) instead of the 4-B route word, and the
+  // records carry the actor id -- every actor's messages still meet in one ring
+  // (the shard is a function of the id), and no stateless handler reads a mailbox.
+  // PTYPE_MBOX_RANK_TABLE=0: the directory gathers.
+  static const bool rank_env = !(getenv("PTYPE_MBOX_RANK_TABLE") && atoi(getenv("PTYPE_MBOX_RANK_TABLE")) == 0);
+  const bool rank_route = rank_env && mode == 1 && a.dir_rank && a.n_dir <= kMaxMbox && !a.ordered && !a.arrival &&
+                          !all_sidx && !a.a2 && !a.method_col && method_stateless((uint32_t)a.method_uniform) &&
+                          sort_mode == 1 && !late;
+  last_route_ = rank_route ? 3 : mode;
   // (batches up to 512 tiles, which take the fused kernel, keep 16-B records: measured faster
   // there -- 1 Mi bench step 24.1 vs 21.9 G msg/s in three sessions -- while 8 Mi gains with 8 B)
   static const int rec8_env = getenv("PTYPE_MBOX_REC8") ? atoi(getenv("PTYPE_MBOX_REC8")) : -1;
@@ -2205,7 +2216,10 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       else PT_SD2(MO, false, false, 0);                                      \
     }                                                                        \
   } while (0)
-    if (mode == 2) PT_SD(2); else if (mode == 1) PT_SD(1); else PT_SD(0);
+    if (rank_route) {
+      if (fixed_mul) PT_SD2(3, false, false, kCalculatorMultiply);
+      else PT_SD2(3, false, false, 0);
+    } else if (mode == 2) PT_SD(2); else if (mode == 1) PT_SD(1); else PT_SD(0);
 #undef PT_SD
 #undef PT_SD2
 #undef PT_SD3
@@ -2253,7 +2267,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else if (a.method_col) PT_OS1(MO, false, true); \
     else PT_OS1(MO, false, false);                  \
   } while (0)
-    if (mode == 2) PT_OS(2); else if (mode == 1) PT_OS(1); else PT_OS(0);
+    if (rank_route) PT_OS2(3, false, false, false);
+    else if (mode == 2) PT_OS(2); else if (mode == 1) PT_OS(1); else PT_OS(0);
 #undef PT_OS
 #undef PT_OS1
 #undef PT_OS2

@@ -71,6 +71,12 @@ class Mailboxes:
         return int(self._m.last_view_shards)
 
     @property
+    def last_route(self) -> int:
+        """Route of the last sorted Send: 0 hash probe, 1 route directory, 2 affine rule,
+        3 rank byte table (a stateless uniform batch; its records carry the actor id)."""
+        return int(self._m.last_route)
+
+    @property
     def handle(self) -> int:
         """Address of the native object: the epoch engine delivers received records into it."""
         return int(self._m.handle)
@@ -151,7 +157,8 @@ class Mailboxes:
                             int(batch.method) if uniform else 0, M, _ptr(table.table), table.cap, _ptr(d), n_dir,
                             affine, int(rank_self), 0, _ptr(out_val), _ptr(out_status), out_val.numel(), _ptr(state),
                             0 if state is None else state.numel(), int(delay_us) * 100, ob, ob_cap, arrival, ordered,
-                            fixed, self._stream(), SORT_MODES[sort_mode])
+                            fixed, self._stream(), SORT_MODES[sort_mode],
+                            _ptr(table.dir_rank) if d is not None else 0)
         return out_val, out_status
 
     # ---- persistent consumer ("tell" sessions)

@@ -62,6 +62,37 @@ def test_mailbox_send_calculator_matches_reference(directory):
     assert (ctr[:, 0] == ctr[:, 2]).all() and int(ctr[:, 0].sum()) == M  # every ring drained
 
 
+@pytest.mark.parametrize("M", [1 << 20, 5 << 20])
+def test_mailbox_stateless_rank_byte_route(M):
+    """A stateless uniform Send on the directory resolves ranks only (route mode 3,
+    the rank byte table) and its records carry actor ids: exact replies for
+    directory ids, ids past the directory (hash probe) and unregistered ids on both
+    sides of its end -- through the fused Send (1 Mi) and the two-kernel one with
+    8-B records (5 Mi)."""
+    n = 1 << 15
+    t = RegistryTable(4 * n, device=DEV)
+    ids = torch.cat([torch.arange(n), torch.arange(n + 100, n + 1100)])
+    perm = torch.randperm(ids.numel(), generator=torch.Generator().manual_seed(11))
+    t.upsert(actor_keys(ids), torch.zeros(ids.numel(), dtype=torch.int32), perm.to(torch.int32))
+    t.enable_directory(n + 50)  # ids n..n+49: in the directory, unregistered
+    g = torch.Generator().manual_seed(12)
+    actor = torch.randint(0, n + 3000, (M,), generator=g, dtype=torch.int32)
+    a0 = torch.randint(-(1 << 15), 1 << 15, (M,), generator=g, dtype=torch.int64)
+    a1 = torch.randint(-(1 << 15), 1 << 15, (M,), generator=g, dtype=torch.int64)
+    req = B.MsgBatch(actor.to(DEV), a0.to(DEV), a1.to(DEV), None, METHOD_CALC_MULTIPLY)
+    mb = Mailboxes(DEV, shards=256, slots=1 << 16)
+    for _ in range(2):  # (the second Send runs on the widths the first one measured)
+        val, st = mb.send(req, t, None, ordered=False)
+        torch.cuda.synchronize()
+        assert mb.last_route == 3
+        a = actor.to(DEV)
+        known = (a < n) | ((a >= n + 100) & (a < n + 1100))
+        assert torch.equal(st, torch.where(known, STATUS_OK, STATUS_NO_ACTOR).to(torch.int32))
+        assert torch.equal(val[known], (req.a0 * req.a1)[known])
+    ctr = mb.shard_counters()
+    assert (ctr[:, 0] == ctr[:, 2]).all()  # every ring drained
+
+
 @pytest.mark.parametrize("sharding", ["actor", "arrival"])
 def test_mailbox_unknown_actor_and_three_args(sharding):
     n, M = 4096, 50_000
