@@ -111,6 +111,7 @@ struct ReplyView {
   uint32_t* slots = nullptr;
   int64_t rep_words = 0;
   uint32_t C = 0;
+  uint32_t nt = 0;  // replies stored non-temporal (PTYPE_REPLY_NT=1, an experiment)
 };
 
 struct PackedLayout;

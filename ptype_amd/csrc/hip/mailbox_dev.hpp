@@ -127,6 +127,11 @@ __device__ __forceinline__ void put_reply(const ReplyView& rv, uint32_t origin, 
     reinterpret_cast<uint8_t*>(rb + 4 + 2 * (int64_t)rv.C)[pos] = (uint8_t)status;
     return;
   }
+  if (rv.nt) {
+    __builtin_nontemporal_store(value, rv.val + origin);
+    __builtin_nontemporal_store(status, rv.st + origin);
+    return;
+  }
   rv.val[origin] = value;
   rv.st[origin] = status;
 }

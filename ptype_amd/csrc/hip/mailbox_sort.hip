@@ -1989,7 +1989,9 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   const bool two_pass = sort_mode != 1;
   const uint32_t ngroups = two_pass ? (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks) : 1u;
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
-  const ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
+  ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
+  static const bool reply_nt = getenv("PTYPE_REPLY_NT") && atoi(getenv("PTYPE_REPLY_NT")) == 1;
+  rv.nt = reply_nt;
   OutboxView ob;
   if (a.outbox_cap) {
     if (a.outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
