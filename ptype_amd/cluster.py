@@ -431,6 +431,10 @@ def Join(ctx, cfg: Config, runtime: bool | None = None) -> Cluster:
         from .runtime import DeviceRuntime
 
         try:
+            if cfg.gpu.tune:  # the config's path switches (ops/tune.py, csrc/hip/tune.hpp)
+                from .ops import tune
+
+                tune.set(cfg.gpu.tune)
             rt = DeviceRuntime.for_cluster(core, cfg)
         except Exception:
             core.close()

@@ -335,6 +335,7 @@ PYBIND11_MODULE(_core, m) {
       .def_readwrite("comm", &GpuConfig::comm)
       .def_readwrite("form_group", &GpuConfig::form_group)
       .def_readwrite("native_group", &GpuConfig::native_group)
+      .def_readwrite("tune", &GpuConfig::tune)
       .def_readwrite("group_timeout_s", &GpuConfig::group_timeout_s)
       .def_readwrite("grace_s", &GpuConfig::grace_s)
       .def_readwrite("send_timeout_s", &GpuConfig::send_timeout_s)

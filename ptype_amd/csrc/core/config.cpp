@@ -138,6 +138,15 @@ void decode_ptype(const YNode& root, Config& c) {
         else if (g.first == "grace_s") c.gpu.grace_s = want_float(G, g.first, g.second);
         else if (g.first == "send_timeout_s") c.gpu.send_timeout_s = want_float(G, g.first, g.second);
         else if (g.first == "replicate_every") c.gpu.replicate_every = (uint32_t)want_int(G, g.first, g.second);
+        else if (g.first == "tune") {  // the data plane's path switches: {key: value} -> "key=value,..."
+          if (g.second.is_null()) continue;
+          if (g.second.kind != YNode::kMap) type_err(G, g.first, g.second, "map[string]string");
+          for (const auto& t : g.second.map)
+          {
+            if (t.second.kind != YNode::kScalar) type_err(G, t.first, t.second, "scalar");
+            c.gpu.tune += (c.gpu.tune.empty() ? "" : ",") + t.first + "=" + t.second.scalar;
+          }
+        }
       }
       if (c.gpu.mailbox_shards == 0 || (c.gpu.mailbox_shards & (c.gpu.mailbox_shards - 1)))
         fail(Errc::kConfig, "gpu.mailbox_shards must be a power of two");

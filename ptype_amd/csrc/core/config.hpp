@@ -72,6 +72,9 @@ struct GpuConfig {
   // RCCL groups: the communicator's lifecycle in the control plane (dataplane.hpp: store
   // rendezvous, ncclCommInitRank, ncclCommAbort, next generation) instead of a torch process group
   bool native_group = true;
+  // path switches of the data plane ("key=value,..."; csrc/hip/tune.hpp, ops/tune.py),
+  // from the `tune:` map -- applied by Join before the device runtime starts
+  std::string tune;
 };
 
 struct Config {

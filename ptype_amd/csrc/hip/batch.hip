@@ -65,8 +65,7 @@ __device__ __forceinline__ uint32_t mod_u64_u32(uint64_t h, uint32_t n, uint64_t
 
 // WIDE: full-range int64 arguments (two more hashes per message) -- values no
 // narrow record holds, for the wide-argument figures (16-B ring records).
-// NT: non-temporal stores (PTYPE_GEN_NT=1, experiment: the columns are read once, by the Send)
-template <bool WIDE, bool NT = false>
+template <bool WIDE>
 __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
                                                            int64_t* __restrict__ a1, int64_t M, uint32_t n_actors,
                                                            uint64_t seed, const uint64_t* __restrict__ seed_ptr,
@@ -83,49 +82,9 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
       x0 = (int64_t)((h >> 20) & 0xffff) - 0x8000;
       x1 = (int64_t)((h >> 40) & 0xffff);
     }
-    if constexpr (NT) {
-      __builtin_nontemporal_store(ac, actor + i);
-      __builtin_nontemporal_store(x0, a0 + i);
-      if (a1) __builtin_nontemporal_store(x1, a1 + i);
-    } else {
-      actor[i] = ac;
-      a0[i] = x0;
-      if (a1) a1[i] = x1;  // (null: a one-argument batch)
-    }
-  }
-}
-
-// The same batch, four consecutive messages per thread: one 16-B store of actor
-// ids and two of each argument column per thread (the same values per index).
-__global__ __launch_bounds__(256) void gen_requests_vec4_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
-                                                                int64_t* __restrict__ a1, int64_t M,
-                                                                uint32_t n_actors, uint64_t seed,
-                                                                const uint64_t* __restrict__ seed_ptr, uint64_t magic) {
-  if (seed_ptr) seed = *seed_ptr;
-  const int64_t M4 = M / 4;
-  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < M4; q += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t ac[4];
-    int64_t x0[4], x1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint64_t i = (uint64_t)q * 4 + j;
-      const uint64_t h = mix64(seed ^ i * 0x9e3779b97f4a7c15ull);
-      ac[j] = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
-      x0[j] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
-      x1[j] = (int64_t)((h >> 40) & 0xffff);
-    }
-    reinterpret_cast<uint4*>(actor)[q] = make_uint4(ac[0], ac[1], ac[2], ac[3]);
-    reinterpret_cast<longlong2*>(a0)[2 * q] = make_longlong2(x0[0], x0[1]);
-    reinterpret_cast<longlong2*>(a0)[2 * q + 1] = make_longlong2(x0[2], x0[3]);
-    reinterpret_cast<longlong2*>(a1)[2 * q] = make_longlong2(x1[0], x1[1]);
-    reinterpret_cast<longlong2*>(a1)[2 * q + 1] = make_longlong2(x1[2], x1[3]);
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(M - M4 * 4)) {  // the tail
-    const uint64_t i = (uint64_t)M4 * 4 + threadIdx.x;
-    const uint64_t h = mix64(seed ^ i * 0x9e3779b97f4a7c15ull);
-    actor[i] = magic ? mod_u64_u32(h, n_actors, magic) : (uint32_t)(h % n_actors);
-    a0[i] = (int64_t)((h >> 20) & 0xffff) - 0x8000;
-    a1[i] = (int64_t)((h >> 40) & 0xffff);
+    actor[i] = ac;
+    a0[i] = x0;
+    if (a1) a1[i] = x1;  // (null: a one-argument batch)
   }
 }
 
@@ -763,36 +722,16 @@ void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M,
                          uintptr_t seed_ptr, uintptr_t stream, bool wide) {
   if (M <= 0) return;
   if (n_actors == 0) throw std::invalid_argument("n_actors must be > 0");
-  static const int variant = [] {  // tuning knobs: PTYPE_GEN_DIV=1 plain `%`; PTYPE_GEN_BLOCKS grid cap
-    const char* e = getenv("PTYPE_GEN_DIV");
-    return e ? atoi(e) : 0;
-  }();
-  static const unsigned cap_blocks = [] {
-    const char* e = getenv("PTYPE_GEN_BLOCKS");
-    return e ? (unsigned)atoi(e) : 8192u;
-  }();
-  // PTYPE_GEN_VEC=1: four messages per thread (measured no faster: 13.6 vs 13.5 us at 1 Mi, 29.8 vs
-  // 26.7 at 8 Mi; the 1 Mi kernel costs ~12 us at any grid from 512 to 8192 blocks)
-  static const bool vec4 = getenv("PTYPE_GEN_VEC") && atoi(getenv("PTYPE_GEN_VEC")) == 1;
-  const uint64_t magic = variant == 1 ? 0ull : ~0ull / n_actors;
-  // (vec4: 16-B stores need 16-B aligned columns -- torch's allocations are; slices may not be)
-  const bool aligned = ((actor | a0 | a1) & 15u) == 0 && a1;
+  // (measured: four messages per thread with 16-B stores, non-temporal stores, plain `%`
+  // and grids from 512 to 8192 blocks were no faster -- removed, tools/gen_sweep.py)
+  const uint64_t magic = ~0ull / n_actors;
+  const dim3 g(grid_cap(M, 256, 8192u));
   if (wide)
-    hipLaunchKernelGGL(gen_requests_kernel<true>, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
-                       (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr,
-                       magic);
-  else if (vec4 && aligned)
-    hipLaunchKernelGGL(gen_requests_vec4_kernel, dim3(grid_cap(std::max<int64_t>(M / 4, 1), 256, cap_blocks)),
-                       dim3(256), 0, as_stream(stream), (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors,
-                       seed, (const uint64_t*)seed_ptr, magic);
-  else if (getenv("PTYPE_GEN_NT") && atoi(getenv("PTYPE_GEN_NT")) == 1)
-    hipLaunchKernelGGL((gen_requests_kernel<false, true>), dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0,
-                       as_stream(stream), (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed,
-                       (const uint64_t*)seed_ptr, magic);
+    hipLaunchKernelGGL(gen_requests_kernel<true>, g, dim3(256), 0, as_stream(stream), (uint32_t*)actor, (int64_t*)a0,
+                       (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr, magic);
   else
-    hipLaunchKernelGGL(gen_requests_kernel<false>, dim3(grid_cap(M, 256, cap_blocks)), dim3(256), 0, as_stream(stream),
-                       (uint32_t*)actor, (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr,
-                       magic);
+    hipLaunchKernelGGL(gen_requests_kernel<false>, g, dim3(256), 0, as_stream(stream), (uint32_t*)actor, (int64_t*)a0,
+                       (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr, magic);
   PT_HIP_CHECK(hipGetLastError());
 }
 
@@ -802,10 +741,7 @@ int64_t route_grid(int64_t M, int64_t* P_out) {
   // messages at P = 4096 was only 512 blocks, and the prep / scatter passes --
   // barrier-separated tiles, latency-bound -- ran at a quarter of the machine.
   // P is a whole number of scatter tiles (512 messages), at least one.
-  static const int64_t target = [] {
-    const char* e = getenv("PTYPE_ROUTE_BLOCKS");
-    return e ? (int64_t)atoll(e) : (int64_t)2048;
-  }();
+  constexpr int64_t target = 2048;
   int64_t P = (M + target - 1) / target;
   P = ((P + kScatterTile - 1) / kScatterTile) * kScatterTile;
   if (P < kScatterTile) P = kScatterTile;
@@ -1056,15 +992,7 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
   const int aw_shift = (affine_w && (affine_w & (affine_w - 1)) == 0) ? __builtin_ctz(affine_w) : -1;
   const int mode = (affine_w && n_dir) ? 2 : (dir && n_dir) ? 1 : 0;
   const bool fixed = !method_col && method_uniform == kCalculatorMultiply;
-  static const int items = [] {  // tuning knob: messages per thread per tile (PTYPE_LOCAL_ITEMS: 1, 2, 4; 0 auto)
-    const char* e = getenv("PTYPE_LOCAL_ITEMS");
-    const int k = e ? atoi(e) : 0;
-    return k == 1 || k == 2 || k == 4 ? k : 0;
-  }();
-  static const unsigned max_blocks = [] {
-    const char* e = getenv("PTYPE_LOCAL_BLOCKS");
-    return e ? (unsigned)atoi(e) : 16384u;
-  }();
+  constexpr unsigned max_blocks = 16384u;
   // The calculator on the directory path (the gather-bound hot path): one tile per
   // block, 8-16 K blocks -- measured (profiles/r2_local_items_sweep.txt) 2 Mi msgs:
   // 1 item x 8192 blocks 67.4 G msg/s vs 4 x 2048 59.1; 8 Mi: 2 x 16384 101.1 vs
@@ -1072,15 +1000,12 @@ void launch_local_send(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a2
   // 4 items x <= 8192 blocks (8 Mi affine: 122 vs 112; token-ring tells: 14.8 vs
   // 11.3 G msg/s -- smaller tiles mean more outbox reservations).
   const bool hot = fixed && mode == 1;
-  const int kk = items ? items : !hot ? 4 : M <= 256ll * 8192 ? 1 : M <= 2ll * 256 * 16384 ? 2 : 4;
+  const int kk = !hot ? 4 : M <= 256ll * 8192 ? 1 : M <= 2ll * 256 * 16384 ? 2 : 4;
   // outbox sends staged in LDS (the hot calculator method never sends), published
-  // with one reservation per `ot` tiles (PTYPE_OUTBOX_TILES): every reservation is
-  // a returning atomic on the outbox count, and same-address atomics serialise
-  static const unsigned ot = [] {
-    const char* e = getenv("PTYPE_OUTBOX_TILES");
-    const int v = e ? atoi(e) : 2;  // token-ring tells: 1 -> 14.6, 2 -> 15.5, 4 -> 15.2 G msg/s
-    return (unsigned)(v >= 1 && v <= 4 ? v : 2);
-  }();
+  // with one reservation per 2 tiles: every reservation is a returning atomic on the
+  // outbox count, and same-address atomics serialise (token-ring tells: 1 -> 14.6,
+  // 2 -> 15.5, 4 -> 15.2 G msg/s)
+  constexpr unsigned ot = 2;
   const bool sends = outbox_cap && !fixed;
   const dim3 g(grid_cap(M, 256 * kk * (sends ? ot : 1u), hot ? max_blocks : 8192u));
   const unsigned stage_cap = sends ? 256u * kk * ot : 0;

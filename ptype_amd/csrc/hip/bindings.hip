@@ -193,6 +193,18 @@ PYBIND11_MODULE(_hip, m) {
   m.def("roctx_mark", [](const std::string& s) {
     if (roctx().mark) roctx().mark(s.c_str());
   });
+  m.def("set_tune", &set_tune, py::arg("spec"),
+        "apply 'key=value,...' path switches (csrc/hip/tune.hpp) after PTYPE_TUNE; false on an unknown key");
+  m.def("tune", [] {
+    const Tune t = tune();
+    py::dict d;
+    d["mbox_fused"] = t.mbox_fused, d["mbox_rec8"] = t.mbox_rec8, d["mbox_sort"] = t.mbox_sort;
+    d["mbox_drain_msg"] = t.mbox_drain_msg, d["sx_sort"] = t.sx_sort, d["sx_self_copy"] = t.sx_self_copy;
+    d["sx_comm_cs"] = t.sx_comm_cs, d["sx_graph"] = t.sx_graph, d["stream_sync"] = t.stream_sync;
+    d["local"] = t.local, d["persistent_stream"] = t.persistent_stream, d["poll_lanes"] = t.poll_lanes;
+    d["poll_full"] = t.poll_full, d["poll_sleep"] = t.poll_sleep;
+    return d;
+  }, "the native path switches in force");
   m.def("set_route_tuning", &set_route_tuning, py::arg("prep_items") = 0, py::arg("mode") = 0,
         py::arg("prep_pipe") = 0,
         "3-pass route_prep items per thread (1, 2, 4, 8; 0 = default); mode 0 = 3-pass prep/scan/scatter "

@@ -7,6 +7,7 @@
 #include <string>
 
 #include "records.hpp"
+#include "tune.hpp"
 
 #define PT_HIP_CHECK(expr)                                                                 \
   do {                                                                                     \
@@ -127,7 +128,7 @@ __device__ __forceinline__ bool last_block_ticket(unsigned* words) {
 // on the same queue -- including the very enqueue it waits for (a live mailbox
 // session then stalls until the consumer's lifetime bound; a Send behind the
 // dispatcher waits for its idle exit: measured 2975 ms, tools/pstream_probe.py).
-// PTYPE_PERSISTENT_STREAM selects the placement:
+// tune persistent_stream selects the placement (tune.hpp):
 //   low    (default) a non-blocking stream at the lowest priority: its own queue
 //          pool, which only persistent kernels use
 //   cumask a CU-masked stream (a dedicated queue, never pooled) -- but HIP makes
@@ -136,8 +137,7 @@ __device__ __forceinline__ bool last_block_ticket(unsigned* words) {
 //   pooled an ordinary non-blocking stream (the hazard above)
 inline hipStream_t dedicated_stream(int device) {
   hipStream_t s = nullptr;
-  const char* env = getenv("PTYPE_PERSISTENT_STREAM");
-  const std::string mode = env ? env : "low";
+  const std::string mode = tune().persistent_stream;
   if (mode == "cumask") {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) {

@@ -28,6 +28,7 @@
 #include "common.hpp"
 #include "mailbox.hpp"
 #include "packed.hpp"
+#include "tune.hpp"
 
 namespace ptype {
 
@@ -351,20 +352,17 @@ class EpochEngine {
     int lo = 0, hi = 0;
     PT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     PT_HIP_CHECK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));  // comm first
-    // Hand-off events keep the default system-scope release unless
-    // PTYPE_EVENT_SCOPE=device: RCCL may move a buffer with peer reads / writes
-    // over xGMI, which must see (and not be hidden by) this GPU's L2 contents.
-    const char* scope = getenv("PTYPE_EVENT_SCOPE");
-    const unsigned ev_flags =
-        hipEventDisableTiming | ((scope && std::string(scope) == "device") ? hipEventReleaseToDevice : 0u);
+    // Hand-off events keep the default system-scope release: RCCL may move a buffer
+    // with peer reads / writes over xGMI, which must see (and not be hidden by) this
+    // GPU's L2 contents.
+    const unsigned ev_flags = hipEventDisableTiming;
     for (int i = 0; i < kMaxBufs; ++i)
       for (hipEvent_t* e : {&ev_route_[i], &ev_req_[i], &ev_disp_[i], &ev_rep_[i]})
         PT_HIP_CHECK(hipEventCreateWithFlags(e, ev_flags));
     PT_HIP_CHECK(hipEventCreateWithFlags(&ev_meta_out_, hipEventDisableTiming));
-    // Cross-stream hand-offs use events unless PTYPE_STREAM_SYNC=values (see handoff()).
+    // Cross-stream hand-offs use events unless tune stream_sync=1 (see handoff()).
     int wv = 0;
-    const char* sync = getenv("PTYPE_STREAM_SYNC");
-    if (sync && std::string(sync) == "values" &&
+    if (tune().stream_sync == 1 &&
         hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, device_) == hipSuccess && wv) {
       if (getenv("PTYPE_HANG_DIAG")) {
         // diagnosis: the words in pinned host memory, readable while a queue is stuck
@@ -415,7 +413,7 @@ class EpochEngine {
   };
   const WireInfo& last_wire() const { return wire_; }
   bool stream_values() const { return use_values_; }  // hand-offs via stream wait-value packets
-  // Hang diagnosis (PTYPE_HANG_DIAG with PTYPE_STREAM_SYNC=values): for every
+  // Hang diagnosis (PTYPE_HANG_DIAG with tune stream_sync=1): for every
   // (hand-off, buffer set) word its last signalled sequence and, when the words
   // live in pinned host memory, the value the GPU has written so far; plus
   // whether the compute / comm streams have drained (hipStreamQuery).
@@ -497,7 +495,7 @@ class EpochEngine {
     wire_.adapted = false;
     // exact-size exchange (SURVEY X1 + X2): needs every chunk's counts before the
     // agreement (adaptive mode preps all chunks) and RCCL's p2p calls
-    exact_ = packed_ && adaptive_ && nbufs_ >= chunks_ && exact_enabled_ && (fake_ || rccl().p2p());
+    exact_ = packed_ && adaptive_ && nbufs_ >= chunks_ && (fake_ || rccl().p2p());
     if (packed_) agree_layout(a, cs);
     wire_.C = C_;
     wire_.C_alloc = C_alloc_;
@@ -563,12 +561,9 @@ class EpochEngine {
   void agree_layout(const EngineSend& a, hipStream_t cs) {
     if (!fake_ && !rccl().allreduce) throw std::runtime_error("EpochEngine: ncclAllReduce not found in the process");
     const uint64_t t0 = now();
-    // With a buffer set per chunk, the width pass rides in route pass 1 of every
-    // chunk (route_prep_kernel<..., META>): the batch is read once before the
-    // agreement, and every chunk's pass 1 is done by the time it returns.
-    // Otherwise a separate width pass, and pass 1 of two chunks runs ahead.
+    // A separate width pass, and pass 1 of two chunks runs ahead (the width pass
+    // fused into route pass 1 measured 1-3 % slower: profiles/r1_multirank_ab.txt).
     prepped_ = 0;
-    const bool fused = nbufs_ >= chunks_ && meta_fused_;
     // adaptive capacity needs every chunk's histograms before the agreement (a
     // buffer set per chunk keeps them until its scatter)
     const bool adapt = adaptive_ && nbufs_ >= chunks_;
@@ -578,14 +573,9 @@ class EpochEngine {
       // meta[kMetaCap] -- CapFold -- so no separate histogram pass runs)
       if (exact_)  // other ranks' rows of the count matrix must be zero for the MAX
         PT_HIP_CHECK(hipMemsetAsync(meta_dev_ + kMetaWords, 0, (agree_words_ - kMetaWords) * sizeof(uint64_t), cs));
-      if (fused) {
-        PT_HIP_CHECK(hipMemsetAsync(meta_dev_, 0, kMetaWords * sizeof(uint64_t), cs));
-        prep_with_meta(a, cs, adapt);
-      } else {
-        launch_packed_meta(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.n_dir, a.affine_w,
-                           (uintptr_t)meta_dev_, (uintptr_t)cs);
-        if (adapt) prep_all(a, cs);
-      }
+      launch_packed_meta(a.actor, a.a0, a.a1, a.a2, a.method_col, a.method_uniform, a.M, a.n_dir, a.affine_w,
+                         (uintptr_t)meta_dev_, (uintptr_t)cs);
+      if (adapt) prep_all(a, cs);
     }
     // on the compute stream itself: the previous Send's collectives are complete
     // there already (its completions waited for them), and no cross-stream hop
@@ -597,7 +587,7 @@ class EpochEngine {
       for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
       L_ = packed_layout(meta_host_);
       if (adapt) adapt_capacity();
-      else if (!fused) prep_ahead(a, cs);
+      else prep_ahead(a, cs);
       prof_.meta_ns += now() - t0;
       return;
     }
@@ -608,7 +598,7 @@ class EpochEngine {
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
     PT_HIP_CHECK(hipMemcpyAsync(meta_host_, meta_dev_, n_agree * sizeof(uint64_t), hipMemcpyDeviceToHost, cs));
     PT_HIP_CHECK(hipEventRecord(ev_meta_out_, cs));
-    if (!fused && !adapt) prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
+    if (!adapt) prep_ahead(a, cs);  // the GPU routes while the host waits for the agreement
     PT_HIP_CHECK(hipEventSynchronize(ev_meta_out_));
     for (int k = 0; k < kMetaWords; ++k) wire_.meta[k] = meta_host_[k];
     L_ = packed_layout(meta_host_);
@@ -678,22 +668,6 @@ class EpochEngine {
                  a.affine_w, (uintptr_t)cs, &P);
     }
     prepped_ = n;
-  }
-
-  // Route pass 1 + the width pass, every chunk (one buffer set each).
-  void prep_with_meta(const EngineSend& a, hipStream_t cs, bool adapt) {
-    if (a.M > 0 && (!a.a0 || !a.actor)) throw std::invalid_argument("packed meta: actor and a0 columns required");
-    for (int i = 0; i < chunks_; ++i) {
-      const CapFold cf = cap_fold(i);
-      const int64_t lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
-      const MetaCols mc{(const int64_t*)off(a.a0, lo, 8), (const int64_t*)off(a.a1, lo, 8),
-                        (const int64_t*)off(a.a2, lo, 8), (const uint16_t*)off(a.method_col, lo, 2),
-                        (uint32_t)a.method_uniform, a.n_dir, a.affine_w, (unsigned long long*)meta_dev_};
-      int64_t P;
-      prep_G_[i] = route_prep(off(a.actor, lo, 4), m_of(a, i), a.table, a.cap, a.dir, a.n_dir, R_, bufs_[i].route,
-                              bufs_[i].hist, a.affine_w, (uintptr_t)cs, &P, &mc, adapt ? &cf : nullptr);
-    }
-    prepped_ = chunks_;
   }
 
   int64_t m_of(const EngineSend& a, int i) const {
@@ -820,7 +794,7 @@ class EpochEngine {
   // Default: hipEventRecord on the producer stream + hipStreamWaitEvent on the
   // consumer (barrier-AND packets on HSA completion signals).
   //
-  // Opt-in (PTYPE_STREAM_SYNC=values): a monotonic 64-bit sequence word per
+  // Opt-in (tune stream_sync=1): a monotonic 64-bit sequence word per
   // (hand-off, buffer set) written by the producer stream (hipStreamWriteValue64)
   // and waited on by the consumer stream (hipStreamWaitValue64, a CP wait-value
   // packet).  Measured on gfx950 (tools/event_gap_bench.hip,
@@ -941,17 +915,11 @@ class EpochEngine {
   int64_t agree_words_ = kMetaWords;  // meta + count matrix [R][R][chunks]
   size_t xs_[kMaxCapCols] = {}, xr_[kMaxCapCols] = {};  // bytes to / from each peer for the a2av in flight
   bool exact_ = false;  // this Send
-  bool exact_enabled_ = !(getenv("PTYPE_EXCHANGE") && std::string(getenv("PTYPE_EXCHANGE")) == "padded");
   bool packed_ = false;
   int prepped_ = 0;  // chunks whose route pass 1 ran ahead of the agreement wait (this Send)
   // world 1 without collectives: the fused local Send (batch.hip local_send_kernel);
-  // PTYPE_LOCAL=0 keeps the epoch-slot pipeline there (A/B and tests)
-  bool local_ = getenv("PTYPE_LOCAL") == nullptr || std::string(getenv("PTYPE_LOCAL")) != "0";
-  // v3: width pass fused into route pass 1 of every chunk (PTYPE_META_FUSED=1).
-  // Off by default: measured 1-3% slower than the separate pass + two preps run
-  // ahead (profiles/r1_multirank_ab.txt) -- the fused pass 1 holds 3 more int64
-  // columns per item, and every chunk's pass 1 lands before the first scatter.
-  bool meta_fused_ = getenv("PTYPE_META_FUSED") != nullptr && std::string(getenv("PTYPE_META_FUSED")) == "1";
+  // tune local=0 keeps the epoch-slot pipeline there (A/B and tests)
+  bool local_ = tune().local != 0;
   PackedLayout L_{};
   WireInfo wire_;
   HostProfile prof_;

@@ -10,6 +10,7 @@
 #include "mailbox.hpp"
 #include "mailbox_dev.hpp"
 #include "sort_common.hpp"
+#include "tune.hpp"
 
 namespace ptype {
 
@@ -222,9 +223,14 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
                                                          uint32_t* __restrict__ sendbuf, int64_t req_stride,
                                                          uint32_t C, SxCaps caps, PackedLayout L,
                                                          int32_t* __restrict__ perm,
-                                                         unsigned long long* __restrict__ meta, bool reject_ordered) {
+                                                         unsigned long long* __restrict__ meta, bool reject_ordered,
+                                                         uint32_t* __restrict__ first_ovf, uint32_t lo) {
   // C: the region stride in records (positions are encoded rk * C + pos);
-  // caps: each destination's capacity (<= C) -- a message past it overflows
+  // caps: each destination's capacity (<= C) -- a message past it overflows.
+  // first_ovf (sharded Sends): per bucket, the smallest Send-wide message index
+  // that overflowed (word kXMaxBuckets: zero once any did) -- sx_fifo_fixup_kernel
+  // then overflows every later message of that bucket, so each (sender, actor)
+  // pair runs a message-order PREFIX and send_all re-sends the suffix in order.
   __shared__ uint32_t cap_s[kSxMaxRanks];
   __shared__ uint32_t run[kXMaxBuckets];
   __shared__ uint32_t bo[kXMaxBuckets];
@@ -307,6 +313,10 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
       if (pos >= cap_s[rk]) {  // past the capacity in force: answered kStatusOverflow, re-sent by send_all
         perm[i] = -1;
         ++n_ovf;
+        if (first_ovf) {
+          atomicMin(first_ovf + bk, lo + (uint32_t)i);
+          atomicMin(first_ovf + kXMaxBuckets, 0u);
+        }
         continue;
       }
       const int64_t x0 = __builtin_nontemporal_load(in.a0 + i);
@@ -330,6 +340,10 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
         f[0] = 0, f[1] = low_mask(L.w[1]), f[2] = 0, f[3] = 0, f[4] = 0;
         perm[i] = -1;
         ++n_ovf;
+        if (first_ovf) {
+          atomicMin(first_ovf + bk, lo + (uint32_t)i);
+          atomicMin(first_ovf + kXMaxBuckets, 0u);
+        }
       }
       uint32_t rec[S];
       packed_pack<S>(L, f, rec);
@@ -339,6 +353,50 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
   }
   acc.mb = 0;  // the count pass folds the mailboxes
   meta_publish(acc, in.mcol != nullptr, in.method_uniform, in.M, meta);
+  fold_overflow(n_ovf, meta);
+}
+
+// ---------------------------------------------------------------- sender: FIFO fix-up (sharded Sends)
+// After a sharded chunk's scatter: when any message of this Send overflowed
+// (first_ovf[kXMaxBuckets] == 0), every PLACED message of this chunk whose
+// bucket (destination rank, actor shard) overflowed at an earlier message index
+// -- an earlier chunk's capacity, or a field wider than the layout in force --
+// becomes a null record and answers kStatusOverflow too.  A record's bucket is
+// read back from its region's shard table.  No overflow: one load, exit.
+template <int S>
+__global__ __launch_bounds__(256) void sx_fifo_fixup_kernel(uint32_t* __restrict__ sendbuf, int64_t req_stride, int R,
+                                                            uint32_t C, PackedLayout L, int32_t* __restrict__ perm,
+                                                            int64_t m, uint32_t lo,
+                                                            const uint32_t* __restrict__ first_ovf,
+                                                            unsigned long long* __restrict__ meta) {
+  if (__hip_atomic_load(first_ovf + kXMaxBuckets, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+  __shared__ uint32_t tab[kSxMaxRanks][kSxShards + 1];
+  __shared__ uint32_t fo[kXMaxBuckets];
+  for (uint32_t j = threadIdx.x; j < (uint32_t)R * (kSxShards + 1); j += blockDim.x) {
+    const uint32_t q = j / (kSxShards + 1), s = j % (kSxShards + 1);
+    tab[q][s] = sendbuf[(int64_t)q * req_stride + 4 + s];
+  }
+  for (uint32_t b = threadIdx.x; b < (uint32_t)R * kSxShards; b += blockDim.x)
+    fo[b] = __hip_atomic_load(first_ovf + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  uint32_t n_ovf = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t p = perm[i];
+    if (p < 0) continue;
+    const uint32_t rk = (uint32_t)p / C, pos = (uint32_t)p % C;
+    uint32_t s = 0;  // the shard whose run holds pos: the last s with tab[rk][s] <= pos
+#pragma unroll
+    for (uint32_t step = kSxShards / 2; step; step >>= 1)
+      if (tab[rk][s + step] <= pos) s += step;
+    if (fo[rk * kSxShards + s] < lo + (uint32_t)i) {
+      uint64_t f[5] = {0, low_mask(L.w[1]), 0, 0, 0};
+      uint32_t rec[S];
+      packed_pack<S>(L, f, rec);
+      store_words<S>(sendbuf + (int64_t)rk * req_stride + kSxRecOff + (int64_t)pos * S, rec);
+      perm[i] = -1;
+      ++n_ovf;
+    }
+  }
   fold_overflow(n_ovf, meta);
 }
 
@@ -362,10 +420,9 @@ __global__ __launch_bounds__(kST) void sx_scatter_kernel(SortIn in, int R, uint3
 // that region's counter (rcnt), and the last block to finish writes the
 // headers from the totals (and clears the counters for the next chunk).
 
-// SK: messages per thread of a tile (tile = 512 * SK); EARLY: the argument columns are
-// loaded with the actors (in flight across the gather, the ranking and the reservation)
-// instead of after it -- more registers, less exposed latency.
-template <int MODE, int S, int SK = kSK, bool EARLY = false>
+// (2048-message tiles and the argument columns loaded with the actors measured no
+// faster: removed, profiles/r5_mailbox_ab.md)
+template <int MODE, int S>
 __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long long* __restrict__ desc,
                                                  unsigned* __restrict__ tctr, unsigned* __restrict__ ticket,
                                                  uint32_t* __restrict__ sendbuf, int64_t req_stride,
@@ -398,25 +455,16 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
   const uint32_t t = tile_s, tag = tag_s;
   const uint32_t rbits = R > 1 ? 32 - __builtin_clz((uint32_t)R - 1) : 0;
   // phase 1: routes and ranks (a small register file: occupancy hides the gathers)
-  uint32_t pr[SK], mb[SK];
-  int64_t e0[EARLY ? SK : 1], e1[EARLY ? SK : 1];
+  uint32_t pr[kSK], mb[kSK];
   uint32_t mbmax = 0;
   {
-    uint32_t a[SK];
-    int r[SK];
-    load_actors<SK>(in, t, a);
-    if constexpr (EARLY) {
+    uint32_t a[kSK];
+    int r[kSK];
+    load_actors(in, t, a);
+    resolve_k<MODE>(in, a, r, mb);
 #pragma unroll
-      for (int k = 0; k < SK; ++k) {
-        const int64_t i = tile_index<SK>(t, k);
-        e0[k] = i < in.M ? __builtin_nontemporal_load(in.a0 + i) : 0;
-        e1[k] = i < in.M && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
-      }
-    }
-    resolve_k<MODE, SK>(in, a, r, mb);
-#pragma unroll
-    for (int k = 0; k < SK; ++k) {
-      const bool ok = tile_index<SK>(t, k) < in.M && r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
+    for (int k = 0; k < kSK; ++k) {
+      const bool ok = tile_index(t, k) < in.M && r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
       if (ok) mbmax = mb[k] > mbmax ? mb[k] : mbmax;
       const uint32_t bk = ok ? (uint32_t)r[k] : 0u;
       const uint64_t peers = match_bits(bk, rbits, __ballot(ok));
@@ -474,8 +522,8 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
   MetaAcc acc;
   uint32_t n_ovf = 0;
 #pragma unroll
-  for (int k = 0; k < SK; ++k) {
-    const int64_t i = tile_index<SK>(t, k);
+  for (int k = 0; k < kSK; ++k) {
+    const int64_t i = tile_index(t, k);
     if (i >= in.M) continue;
     const uint32_t rk = pr[k] & 0xffu;
     if (rk == 0xffu) {
@@ -488,14 +536,8 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
       ++n_ovf;
       continue;
     }
-    int64_t x0, x1;
-    if constexpr (EARLY) {
-      x0 = e0[k];
-      x1 = e1[k];
-    } else {
-      x0 = __builtin_nontemporal_load(in.a0 + i);
-      x1 = in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
-    }
+    const int64_t x0 = __builtin_nontemporal_load(in.a0 + i);
+    const int64_t x1 = in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
     const int64_t x2 = in.a2 ? __builtin_nontemporal_load(in.a2 + i) : 0;
     const uint32_t meth = in.mcol ? (uint32_t)in.mcol[i] : in.method_uniform;
     const uint64_t z0 = zz_enc(x0), z1 = zz_enc(x1), z2 = in.a2 ? zz_enc(x2) : 0ull;
@@ -549,9 +591,9 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
       bool reserve, bool reject_ordered
 #define PT_SX_OS_ARGS \
   in, R, desc, tctr, ticket, sendbuf, req_stride, C, caps, hdr_word3, rank_self, L, perm, meta, stats, rcnt, reserve, reject_ordered
-template <int MODE, int S, int SK = kSK, bool EARLY = false>
+template <int MODE, int S>
 __global__ __launch_bounds__(kST) void sx_onesweep_kernel(PT_SX_OS_PARAMS) {
-  sx_onesweep_body<MODE, S, SK, EARLY>(PT_SX_OS_ARGS);
+  sx_onesweep_body<MODE, S>(PT_SX_OS_ARGS);
 }
 #undef PT_SX_OS_PARAMS
 #undef PT_SX_OS_ARGS
@@ -872,25 +914,23 @@ SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int6
     // receive kernel (or the loopback copy) wrote here.  Their events drop the
     // system-scope fence (-3.5 % of the loopback-8 step for the first pair,
     // profiles/r5_mailbox_ab.md).  IpcComm's peers read and write the regions in
-    // place from their own processes, so a device-side comm keeps it;
-    // PTYPE_SX_EVENT_FENCE=system restores it everywhere, =out only on the
-    // compute -> comm pair.
-    static const char* fence_env = getenv("PTYPE_SX_EVENT_FENCE");
-    const std::string fence = fence_env ? fence_env : (fake_ && fake_->device_side()) ? "system" : "device";
-    const unsigned out_flags = hipEventDisableTiming | (fence != "system" ? hipEventDisableSystemFence : 0u);
-    const unsigned in_flags = hipEventDisableTiming | (fence == "device" ? hipEventDisableSystemFence : 0u);
+    // place from their own processes, so a device-side comm keeps it.
+    const bool sys_fence = fake_ && fake_->device_side();
+    const unsigned flags = hipEventDisableTiming | (sys_fence ? 0u : hipEventDisableSystemFence);
+    const unsigned out_flags = flags, in_flags = flags;
     for (hipEvent_t* e : {&ev_routed_[i], &ev_served_[i]}) PT_HIP_CHECK(hipEventCreateWithFlags(e, out_flags));
     for (hipEvent_t* e : {&ev_req_in_[i], &ev_rep_in_[i]}) PT_HIP_CHECK(hipEventCreateWithFlags(e, in_flags));
   }
   PT_HIP_CHECK(hipMalloc(&hist_, (size_t)kMboxSortHistWords * 4));
   PT_HIP_CHECK(hipMalloc(&boff_, (size_t)kXMaxBuckets * 4));
-  const int64_t max_tiles = (max_chunk + kSTile / 2 - 1) / (kSTile / 2);  // (2048-message tiles: PTYPE_SX_TILE=4)
+  const int64_t max_tiles = (max_chunk + kSTile - 1) / kSTile;
   PT_HIP_CHECK(hipMalloc(&desc_, (size_t)std::max<int64_t>(max_tiles, 1) * R * 8));
   PT_HIP_CHECK(hipMemset(desc_, 0, (size_t)std::max<int64_t>(max_tiles, 1) * R * 8));  // tag 0: never a live tag
   PT_HIP_CHECK(hipMalloc(&tctr_, 2 * sizeof(unsigned)));
   PT_HIP_CHECK(hipMemset(tctr_, 0, 2 * sizeof(unsigned)));
   PT_HIP_CHECK(hipMalloc(&ticket_, kTicketWords * sizeof(unsigned)));
   PT_HIP_CHECK(hipMemset(ticket_, 0, kTicketWords * sizeof(unsigned)));
+  PT_HIP_CHECK(hipMalloc(&first_ovf_, (kXMaxBuckets + 1) * sizeof(uint32_t)));
   PT_HIP_CHECK(hipMalloc(&rcnt_, kSxMaxChunks * kSxMaxRanks * sizeof(uint32_t)));
   PT_HIP_CHECK(hipMemset(rcnt_, 0, kSxMaxChunks * kSxMaxRanks * sizeof(uint32_t)));
   PT_HIP_CHECK(hipMalloc(&meta_dev_, 2 * kSxMetaWords * sizeof(uint64_t)));
@@ -932,6 +972,7 @@ SortedExchange::~SortedExchange() {
   (void)hipFree(tctr_);
   (void)hipFree(ticket_);
   (void)hipFree(rcnt_);
+  (void)hipFree(first_ovf_);
   (void)hipFree(meta_dev_);
   (void)hipFree(stats_);
   (void)hipHostFree(meta_host_);
@@ -1014,8 +1055,7 @@ void SortedExchange::adopt(const uint64_t* meta, int64_t from) {
     sum_pairs = 0;
     for (int q = 0; q < R_; ++q) sum_pairs += (int64_t)R_ * cap_[rank_ * R_ + q];
   }
-  static const bool pairs_off = getenv("PTYPE_SX_PAIRS") && atoi(getenv("PTYPE_SX_PAIRS")) == 0;
-  pairs_ = !pairs_off && R_ > 1 && (double)sum_pairs < 0.85 * (double)C_ * RR;
+  pairs_ = R_ > 1 && (double)sum_pairs < 0.85 * (double)C_ * RR;
   if (!pairs_)
     for (int k = 0; k < RR; ++k) cap_[k] = (uint32_t)C_;
   agreed_ = true;
@@ -1045,13 +1085,12 @@ void SortedExchange::a2a(const void* src, void* dst, size_t stride, const size_t
     else fake_->alltoall(rank_, src, dst, stride, cur_comm_);
     return;
   }
-  // PTYPE_SX_SELF_COPY: at world 1 the all-to-all is a device copy.  RCCL
+  // tune sx_self_copy: at world 1 the all-to-all is a device copy.  RCCL
   // collectives issued on this engine's comm stream crash hipGraph
   // instantiation on this stack (ncclAllToAll and grouped send / recv alike,
   // tools/rccl_capture_probe.py, profiles/r3_rccl_capture_probe.txt), so the
   // capture test validates the captured pipeline with the copy in their place.
-  static const bool self_copy = getenv("PTYPE_SX_SELF_COPY") != nullptr;
-  if (self_copy && R_ == 1) {
+  if (self_copy_ && R_ == 1) {
     PT_HIP_CHECK(hipMemcpyAsync(dst, src, recv ? recv[0] : stride, hipMemcpyDeviceToDevice, cur_comm_));
     return;
   }
@@ -1104,14 +1143,16 @@ void SortedExchange::send(const SxSend& a) {
   PT_HIP_CHECK(hipSetDevice(device_));
   if (fake_) fake_->check();  // an earlier collective's failure surfaces here (IpcComm: a peer missed one)
   const hipStream_t cs = as_stream(a.stream);
-  // PTYPE_SX_COMM_CS=1: the collectives on the caller's stream itself (a graph-capture probe:
+  // tune sx_comm_cs=1: the collectives on the caller's stream itself (a graph-capture probe:
   // tools/rccl_capture_probe.py sx1cs) instead of the engine's comm stream
   // Under a hipGraph capture the collectives go on the capturing stream itself: RCCL calls on a
   // stream forked into the capture crash graph instantiation on this stack, issued on the
   // capture stream they instantiate and replay correctly (tools/rccl_capture_probe.py sx1cs,
   // profiles/r3_rccl_capture_probe.txt) -- the captured Send then runs its chunks' collectives in
   // order with their compute instead of beside it.
-  static const bool comm_on_cs = getenv("PTYPE_SX_COMM_CS") && atoi(getenv("PTYPE_SX_COMM_CS")) == 1;
+  const Tune tn = tune();
+  const bool comm_on_cs = tn.sx_comm_cs != 0;
+  self_copy_ = tn.sx_self_copy != 0;
   hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;
   const bool capturing = hipStreamIsCapturing(cs, &capst) == hipSuccess && capst != hipStreamCaptureStatusNone;
   cur_comm_ = (comm_on_cs || (capturing && comm_)) ? cs : comm_stream_;
@@ -1171,8 +1212,6 @@ void SortedExchange::send(const SxSend& a) {
   for (int m = 0; m < 7 && !shard_ok; ++m)
     if (method_ordered((uint32_t)m) && spec_meta_[kMetaFlags + m]) shard_ok = true;
   if (spec_meta_[kMetaFlags + 7]) shard_ok = true;  // method ids >= 7: may be ordered
-  static const bool shard_always = getenv("PTYPE_SX_SHARD_GATE") && atoi(getenv("PTYPE_SX_SHARD_GATE")) == 0;
-  if (shard_always) shard_ok = true;
   const bool may_order = a.ordered && shard_ok;
   const bool wants_order = a.ordered && (a.method_col != 0 || method_ordered((uint32_t)a.method_uniform));
   const bool reject_ordered = wants_order && !shard_ok;
@@ -1182,13 +1221,14 @@ void SortedExchange::send(const SxSend& a) {
   // rank byte gathers (MODE 3) for a rank-only sort of a stateless uniform method:
   // a message needs only its destination rank (1 B per id: a 1 M-actor table is
   // 1 MB, L2-resident, against the 4 MB directory), and carries its actor id
-  static const bool rank_table = !(getenv("PTYPE_SX_RANK_TABLE") && atoi(getenv("PTYPE_SX_RANK_TABLE")) == 0);
   const bool stateless = a.method_col == 0 && method_stateless((uint32_t)a.method_uniform);
   int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
-  if (mode == 1 && rank_table && a.dir_rank && stateless && !sharded && a.n_dir <= kMaxMbox) mode = 3;
+  if (mode == 1 && a.dir_rank && stateless && !sharded && a.n_dir <= kMaxMbox) mode = 3;
   wire_.shard_ok = shard_ok;
   wire_.route_mode = mode;
   const uint32_t K = sharded ? (uint32_t)kSxShards : 1u;
+  // a sharded Send's per-bucket first overflow (sx_fifo_fixup_kernel): none yet
+  if (sharded) PT_HIP_CHECK(hipMemsetAsync(first_ovf_, 0xff, (kXMaxBuckets + 1) * sizeof(uint32_t), cs));
   const uint32_t B = (uint32_t)R_ * K;
   auto chunk_in = [&](int i, int64_t& lo, int64_t& m) {
     lo = std::min<int64_t>((int64_t)i * max_chunk_, a.M);
@@ -1210,10 +1250,6 @@ void SortedExchange::send(const SxSend& a) {
     in.aw = a.affine_w;
     in.aw_shift = (a.affine_w && (a.affine_w & (a.affine_w - 1)) == 0) ? __builtin_ctz(a.affine_w) : -1;
     in.rank_self = rank_;
-    static const bool dir_nt = getenv("PTYPE_DIR_NT") && atoi(getenv("PTYPE_DIR_NT")) != 0;
-    in.dir_nt = dir_nt;
-    static const bool lb_group = getenv("PTYPE_LB_GROUP") && atoi(getenv("PTYPE_LB_GROUP")) == 1;  // measured slower
-    in.lb_group = lb_group;
     const int64_t tiles = (m + kSTile - 1) / kSTile;
     int64_t G = std::min<int64_t>({std::max<int64_t>(tiles, 1), (int64_t)(kMboxSortHistWords / B), 1024});
     if (G >= 8) G -= G % 8;
@@ -1227,8 +1263,7 @@ void SortedExchange::send(const SxSend& a) {
     PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_req_in_[i], 0));
     // ~2048 blocks over the R regions (at least one per region)
     const int64_t per = std::max<int64_t>(1, max_chunk_ / R_);
-    static const int drain_blocks = getenv("PTYPE_SX_DRAIN_BLOCKS") ? atoi(getenv("PTYPE_SX_DRAIN_BLOCKS")) : 2048;
-    static const int drain_per = getenv("PTYPE_SX_DRAIN_PER") ? atoi(getenv("PTYPE_SX_DRAIN_PER")) : 1024;
+    constexpr int drain_blocks = 2048, drain_per = 1024;
     const unsigned X = (unsigned)std::max<int64_t>(
         1, std::min<int64_t>((per + drain_per - 1) / drain_per, std::max(1, drain_blocks / R_)));
 #define PT_SX_PAR(SV)                                                                                         \
@@ -1283,39 +1318,19 @@ void SortedExchange::send(const SxSend& a) {
     else if (mode == 1) hipLaunchKernelGGL((KERNEL<1>), __VA_ARGS__); \
     else hipLaunchKernelGGL((KERNEL<0>), __VA_ARGS__);               \
   } while (0)
-    // rank-only batches: count + scan + scatter, or one pass with look-back (PTYPE_SX_SORT=onepass; measured
-    // slower at R = 8, 4 Mi msgs per chunk: 90 us vs 34 + 6.5 + 44 -- the look-back's memory-side atomic
-    // round trips cost more than the count pass's second read of the batch)
     // rank-only batches: one pass with per-tile run reservation (the default; no look-back),
-    // PTYPE_SX_SORT=onepass: the look-back form, =twopass: count + scan + scatter
-    static const char* sx_sort = getenv("PTYPE_SX_SORT");
-    static const int sx_mode = !sx_sort ? 0 : std::string(sx_sort) == "onepass" ? 1 : std::string(sx_sort) == "twopass" ? 2 : 0;
+    // tune sx_sort=1: the look-back form (measured slower at R = 8, 4 Mi msgs per chunk: 90 us
+    // vs 34 + 6.5 + 44 for count + scan + scatter -- its memory-side atomic round trips),
+    // sx_sort=2: count + scan + scatter
+    const int sx_mode = tn.sx_sort;
     const bool reserve = sx_mode == 0;
     if (!sharded && in.tiles > 0 && (sx_mode != 2 || mode == 3)) {
       const uint32_t hdr3 =
           ((uint32_t)(kFlagValid | (mode == 3 ? kFlagActorIds : 0)) << 16) | (uint32_t)a.method_uniform;
-      // PTYPE_SX_TILE=4 / 4e / 8e (experiments, 8-B records of modes 1 and 3): 2048-message tiles
-      // (SK = 4), and/or the argument columns loaded with the actors (e = early)
-      static const char* sx_tile = getenv("PTYPE_SX_TILE");
-      static const int tile_sk = sx_tile && sx_tile[0] == '4' ? 4 : kSK;
-      static const bool tile_early = sx_tile && sx_tile[0] && sx_tile[1] == 'e';
-      SortIn in_t = in;
-      in_t.tiles = (uint32_t)((m + kST * tile_sk - 1) / (kST * tile_sk));
-#define PT_SX_OS1(MO, SV, SKV, EV)                                                                                 \
-  hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV, SKV, EV>), dim3(in_t.tiles), dim3(kST), 0, cs, in_t, R_, desc_,  \
-                     tctr_, ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm,                     \
-                     (unsigned long long*)meta, stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered)
-#define PT_SX_OS(MO, SV)                                                                                           \
-  do {                                                                                                             \
-    if ((MO == 1 || MO == 3) && SV == 2 && (tile_sk != kSK || tile_early)) {                                       \
-      if (tile_sk == 4 && tile_early) PT_SX_OS1(MO, SV, 4, true);                                                  \
-      else if (tile_sk == 4) PT_SX_OS1(MO, SV, 4, false);                                                          \
-      else PT_SX_OS1(MO, SV, kSK, true);                                                                           \
-    } else {                                                                                                       \
-      in_t.tiles = in.tiles;                                                                                       \
-      PT_SX_OS1(MO, SV, kSK, false);                                                                               \
-    }                                                                                                              \
-  } while (0)
+#define PT_SX_OS(MO, SV)                                                                                     \
+  hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV>), dim3(in.tiles), dim3(kST), 0, cs, in, R_, desc_, tctr_,  \
+                     ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm, (unsigned long long*)meta, \
+                     stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered)
 #define PT_SX_OS_S(MO)              \
   switch (S) {                      \
     case 1: PT_SX_OS(MO, 1); break; \
@@ -1336,7 +1351,6 @@ void SortedExchange::send(const SxSend& a) {
       }
 #undef PT_SX_OS_S
 #undef PT_SX_OS
-#undef PT_SX_OS1
       PT_HIP_CHECK(hipGetLastError());
       PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
       PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
@@ -1354,7 +1368,7 @@ void SortedExchange::send(const SxSend& a) {
 #define PT_SX_SCAT(MO, SV)                                                                                       \
   hipLaunchKernelGGL((sx_scatter_kernel<MO, SV>), dim3(in.G), dim3(kST), 0, cs, in, R_, K, (const uint32_t*)hist_, \
                      (const uint32_t*)boff_, b.send, rq, (uint32_t)C, caps_out, L, b.perm, (unsigned long long*)meta, \
-                     reject_ordered)
+                     reject_ordered, sharded ? first_ovf_ : nullptr, (uint32_t)lo)
 #define PT_SX_SCAT_S(MO)            \
   switch (S) {                      \
     case 1: PT_SX_SCAT(MO, 1); break; \
@@ -1373,6 +1387,21 @@ void SortedExchange::send(const SxSend& a) {
     }
 #undef PT_SX_SCAT_S
 #undef PT_SX_SCAT
+    if (sharded && m > 0) {
+      const unsigned fx = (unsigned)std::min<int64_t>((m + 2047) / 2048, 1024);
+#define PT_SX_FIX(SV)                                                                                         \
+  hipLaunchKernelGGL((sx_fifo_fixup_kernel<SV>), dim3(fx), dim3(256), 0, cs, b.send, rq, R_, (uint32_t)C, L, \
+                     b.perm, m, (uint32_t)lo, (const uint32_t*)first_ovf_, (unsigned long long*)meta)
+      switch (S) {
+        case 1: PT_SX_FIX(1); break;
+        case 2: PT_SX_FIX(2); break;
+        case 3: PT_SX_FIX(3); break;
+        case 4: PT_SX_FIX(4); break;
+        case 6: PT_SX_FIX(6); break;
+        default: PT_SX_FIX(8); break;
+      }
+#undef PT_SX_FIX
+    }
     PT_HIP_CHECK(hipGetLastError());
     PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
     PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
@@ -1400,7 +1429,6 @@ void SortedExchange::send(const SxSend& a) {
   } else {
     meta_send_[cur] = -1;
   }
-  static const bool zero_in_comp = !(getenv("PTYPE_SX_META_ZERO") && atoi(getenv("PTYPE_SX_META_ZERO")) == 0);
   for (int i = 0; i < chunks_; ++i) {
     int64_t lo, m;
     (void)chunk_in(i, lo, m);
@@ -1408,7 +1436,7 @@ void SortedExchange::send(const SxSend& a) {
     if (m > 0) {
       // the first completion also clears the agreement buffer of Send + 1 (that of
       // Send - 1, whose copy to the host precedes this Send's reply all-to-alls)
-      const bool zero = zero_in_comp && !capturing && !meta_zeroed_[cur ^ 1];
+      const bool zero = !capturing && !meta_zeroed_[cur ^ 1];
       launch_complete_packed((uintptr_t)bufs_[i].back, C, R_, L.vb, (uintptr_t)bufs_[i].perm, m,
                              a.out_val + (uintptr_t)(lo * 8), a.out_st + (uintptr_t)(lo * 4), 0, false,
                              (uintptr_t)cs, fake_ ? (uintptr_t)fake_->device_failed() : 0,

@@ -161,6 +161,7 @@ class SortedExchange {
   unsigned* tctr_ = nullptr;    // [0] one-pass tile counter (self-resetting), [1] its epoch tag
   unsigned* ticket_ = nullptr;  // last-block ticket of the one-pass kernel (self-resetting)
   uint32_t* rcnt_ = nullptr;    // [chunks][kSxMaxRanks] one-pass run reservations per region (self-resetting)
+  uint32_t* first_ovf_ = nullptr;  // sharded Sends: per-bucket first overflowed message index (+ an any-word)
   uint64_t* meta_dev_ = nullptr;   // [2][kSxMetaWords] agreement vectors (device)
   uint64_t* meta_host_ = nullptr;  // [2][kSxMetaWords] pinned copies
   unsigned long long* stats_ = nullptr;  // [2] receiver counters
@@ -184,6 +185,7 @@ class SortedExchange {
   // the uniform C that moving prefixes pays (the same decision on every rank)
   uint32_t cap_[kSxMaxRanks * kSxMaxRanks] = {};
   bool pairs_ = false;
+  bool self_copy_ = false;  // tune sx_self_copy (read per Send)
   int64_t sends_ = 0;
   SxWire wire_;
   mutable HostProfile prof_;

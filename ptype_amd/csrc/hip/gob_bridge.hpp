@@ -86,7 +86,7 @@ class GobBridge {
       static_cast<GobBridge*>(ctx)->run(bytes, offsets, n, type_id, nf, field_col, gob_status, out);
       return 0;
     } catch (const std::exception& e) {
-      if (getenv("PTYPE_GOB_BRIDGE_DEBUG")) fprintf(stderr, "ptype: gob bridge: %s\n", e.what());
+      if (getenv("PTYPE_DEBUG")) fprintf(stderr, "ptype: gob bridge: %s\n", e.what());
       return -1;
     }
   }

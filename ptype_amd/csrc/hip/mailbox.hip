@@ -599,14 +599,13 @@ void launch_mailbox_enqueue(const MboxView& mv, uintptr_t actor, uintptr_t a0, u
   constexpr int K = 8;   // actor sharding: a big tile amortises the (tile, shard) reservations
   // arrival sharding: 4 items per thread (one reservation per tile; 64 VGPRs, 8
   // waves/SIMD); 1 and 2 measured slower at 1 Mi and 8 Mi messages
-  // (profiles/r2_enq_items_sweep.txt).  PTYPE_ENQ_ITEMS overrides.
-  static const int ka_env = getenv("PTYPE_ENQ_ITEMS") ? atoi(getenv("PTYPE_ENQ_ITEMS")) : 0;
-  const int KA = ka_env == 1 || ka_env == 2 || ka_env == 4 ? ka_env : 4;
+  // (profiles/r2_enq_items_sweep.txt).
+  constexpr int KA = 4;
   const int aw_shift = (affine_w && (affine_w & (affine_w - 1)) == 0) ? __builtin_ctz(affine_w) : -1;
   const int mode = (affine_w && n_dir) ? 2 : (dir && n_dir) ? 1 : 0;
   const uint32_t S = 1u << mv.log_s;
   const size_t lds = (size_t)S * (8 + 8 + 4);
-  static const unsigned enq_blocks = getenv("PTYPE_ENQ_BLOCKS") ? (unsigned)atoi(getenv("PTYPE_ENQ_BLOCKS")) : 4096u;
+  constexpr unsigned enq_blocks = 4096u;
   const dim3 g(mb_grid(M, 256 * (arrival ? KA : K), enq_blocks));
 #define PT_ENQ(MO, LV)                                                                                                \
   hipLaunchKernelGGL((mailbox_enqueue_kernel<MO, LV, K>), g, dim3(256), lds, as_stream(stream), mv,                \
@@ -716,7 +715,7 @@ void launch_mailbox_drain(const MboxView& mv, uintptr_t state, uint32_t n_state,
     // ~1024 blocks over the shards (each block strides over its shard's queue).
     // Measured (8 Mi records, 256 shards): 1024 / 2048 / 4096 blocks 0.232 / 0.237 /
     // 0.240 ms per mailbox step; 4 records per thread instead of 2: no change.
-    static const unsigned target = getenv("PTYPE_DRAIN_BLOCKS") ? (unsigned)atoi(getenv("PTYPE_DRAIN_BLOCKS")) : 1024u;
+    constexpr unsigned target = 1024u;
     const unsigned X = S >= target ? 1u : target / S;
     // a Send that knows every queued record's method (uniform batch) drains with
     // that handler constant-folded
@@ -747,7 +746,7 @@ static uint32_t log2_exact(uint32_t v, const char* what) {
 Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) : device_(device) {
   mv_.log_s = log2_exact(shards, "mailbox shards");
   mv_.log_q = log2_exact(slots, "mailbox slots per shard");
-  mv_.planar = !(getenv("PTYPE_MBOX_PLANAR") && std::string(getenv("PTYPE_MBOX_PLANAR")) == "0");
+  mv_.planar = true;  // (the interleaved 32-B record form measured slower; the flag stays for the live rings)
   if (shards > (uint32_t)kMboxMaxShards) throw std::invalid_argument("mailbox shards <= 4096");
   if (slots < 64) throw std::invalid_argument("mailbox slots per shard >= 64");
   PT_HIP_CHECK(hipSetDevice(device_));
@@ -755,10 +754,9 @@ Mailboxes::Mailboxes(int device, uint32_t shards, uint32_t slots, bool with_a2) 
   const uint64_t n = (uint64_t)shards * slots;
   // plane B starts past plane A plus a pad: A[slot] and B[slot] are read together,
   // and a power-of-two distance between them aliases in the HBM address mapping.
-  // Measured (bench mailbox step, PTYPE_MBOX_BPAD sweep): pad 0 / 4.3 KB / 65 KB /
-  // 2 MB / 8 MB / 128 MB: 0.234-0.238 ms; 1 MB + 3.4 KB: 0.215-0.217; 33 MB: 0.219.
-  const uint64_t pad = mv_.planar ? (getenv("PTYPE_MBOX_BPAD") ? (uint64_t)atoll(getenv("PTYPE_MBOX_BPAD")) & ~15ull
-                                                               : 1052032ull) : 0ull;
+  // Measured (bench mailbox step, pad sweep): pad 0 / 4.3 KB / 65 KB / 2 MB / 8 MB /
+  // 128 MB: 0.234-0.238 ms; 1 MB + 3.4 KB: 0.215-0.217; 33 MB: 0.219.
+  const uint64_t pad = 1052032ull;
   mv_.b_off = (n * 16 + pad) / 4;
   rec_bytes_ = n * 32 + pad;
   PT_HIP_CHECK(hipMalloc((void**)&mv_.rec, rec_bytes_));
@@ -802,8 +800,8 @@ Mailboxes::~Mailboxes() {
   (void)hipFree(mv_.ctr);
   (void)hipFree(mv_.stats);
   for (void* p : {(void*)sort_hist_, (void*)sort_gsum_, (void*)sort_ticket_, (void*)sort_rw_, (void*)sort_sidx_,
-                  (void*)sort_tinfo_, (void*)sort_desc_, (void*)sort_tctr_, (void*)sort_stab_, stage_rep_,
-                  (void*)r8w_, (void*)r8max_, (void*)sort_resv_})
+                  (void*)sort_tinfo_, (void*)sort_desc_, (void*)sort_tctr_, stage_rep_,
+                  (void*)r8w_, (void*)r8max_, (void*)r8esc_, (void*)sort_resv_})
     if (p) (void)hipFree(p);
   if (ctrl_) (void)hipHostFree(ctrl_);
   if (r8host_) (void)hipHostFree(r8host_);

@@ -111,7 +111,6 @@ struct ReplyView {
   uint32_t* slots = nullptr;
   int64_t rep_words = 0;
   uint32_t C = 0;
-  uint32_t nt = 0;  // replies stored non-temporal (PTYPE_REPLY_NT=1, an experiment)
 };
 
 struct PackedLayout;
@@ -152,8 +151,8 @@ struct MboxSend {
   bool arrival = false;  // shard by arrival tile (batches without ordered methods)
   bool ordered = true;   // ordered drain: per-actor serial, FIFO; else the parallel drain
   int fixed_method = 0;  // every message carries this method (constant-folded handler)
-  // sort kernels: 0 auto (PTYPE_MBOX_SORT, else one-pass from 1024 tiles on), 1 one-pass look-back,
-  // 2 count + scatter, 3 LDS-table count + resolving scatter
+  // sort kernels: 0 auto (tune mbox_sort, else one-pass for stateless batches and from 1024
+  // tiles on), 1 one-pass (stateless: run reservations; ordered: look-back), 2 count + scatter
   int sort_mode = 0;
   uintptr_t stream = 0;
   // the directory's rank byte table (one byte per id): a stateless uniform batch
@@ -229,7 +228,6 @@ class Mailboxes {
   uint32_t* sort_tinfo_ = nullptr;  // [tiles][2][S] each tile's runs: slot bias, count (ring-order drain / completion)
   unsigned long long* sort_desc_ = nullptr;  // [tiles][S] one-pass sort: per-tile shard counts / prefixes (look-back)
   unsigned* sort_tctr_ = nullptr;   // [0] one-pass sort's tile counter (self-resetting), [1] its epoch tag
-  uint8_t* sort_stab_ = nullptr;    // LDS-table count: one byte per actor (shard, or not-here / probe)
   uint64_t sort_cap_ = 0;           // messages the two arrays hold
   int last_rec_bytes_ = 0;
   uint32_t last_view_shards_ = 0;
@@ -241,6 +239,7 @@ class Mailboxes {
   uint32_t* r8w_ = nullptr;
   uint32_t* r8max_ = nullptr;
   uint32_t* r8host_ = nullptr;
+  int64_t* r8esc_ = nullptr;  // ordered 8-B records: escape records' {a0, mailbox} by ring slot
   uint64_t r8_tiles_ = 0;
   // ordered drain: replies staged at ring slots [S * Q], one 16-B word each
   // (value lo, value hi, status, 0) -- one gather per message in the completion

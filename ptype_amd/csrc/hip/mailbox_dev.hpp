@@ -44,7 +44,7 @@ __device__ __forceinline__ unsigned long long* ctr_head(const MboxView& mv, uint
 // A record is two 16-B halves in two planes: plane A {tag, mailbox, origin,
 // method | flags} at rec[slot], plane B {a0, a1} at rec[b_off + slot], so a
 // wave's store of one half covers 64 consecutive 16-B cells -- whole lines.  As
-// one 32-B record per slot (PTYPE_MBOX_PLANAR=0) each store instruction wrote
+// one 32-B record per slot (the removed interleaved form) each store instruction wrote
 // every other 16 B of 64 records: the enqueue's DRAM writes were 419 MB for 268 MB
 // of records (PMC WRITE_SIZE).  Bench mailbox step: 0.247 ms (32-B records) ->
 // 0.215 ms (planes, de-aliased; see the pad in the Mailboxes constructor).
@@ -125,11 +125,6 @@ __device__ __forceinline__ void put_reply(const ReplyView& rv, uint32_t origin, 
     uint32_t* rb = rv.slots + (int64_t)d * rv.rep_words;
     reinterpret_cast<int64_t*>(rb + 4)[pos] = value;
     reinterpret_cast<uint8_t*>(rb + 4 + 2 * (int64_t)rv.C)[pos] = (uint8_t)status;
-    return;
-  }
-  if (rv.nt) {
-    __builtin_nontemporal_store(value, rv.val + origin);
-    __builtin_nontemporal_store(status, rv.st + origin);
     return;
   }
   rv.val[origin] = value;

@@ -67,6 +67,7 @@
 #include "mailbox_dev.hpp"
 #include "route_common.hpp"
 #include "sort_common.hpp"
+#include "tune.hpp"
 
 namespace ptype {
 
@@ -78,7 +79,6 @@ constexpr int kOrdK = 4;
 constexpr int kOrdWin = kOrdThreads * kOrdK;  // records per window (2048)
 constexpr int kOrdWaves = kOrdThreads / kWave;
 constexpr uint32_t kOrdStateMax = 4096;  // a shard's actors whose state is staged in LDS (32 KB)
-constexpr int kSKSmall = 2;  // messages per thread of a small fused Send's tiles (1024-message tiles)
 }  // namespace
 
 // ---------------------------------------------------------------- K2s pass 1: count
@@ -125,119 +125,19 @@ __global__ __launch_bounds__(kST) void mbx_count_kernel(SortIn in, uint32_t log_
   }
 }
 
-// Count from an LDS shard table.  What the count needs of a message is its
-// shard (mailbox & (S - 1)) and whether it is this rank's -- one byte per actor
-// -- while a route directory gather costs an L2 request per message (8 Mi
-// lookups: 40 us against 14 us for the copy of the same column,
-// tools/gather_probe.hip; from a 1-B table staged in LDS: 15 us).  So a small
-// kernel condenses the directory into a byte table (0xff: not here, 0xfe: probe
-// the hash table) and the count stages it in LDS, one 1024-thread block per CU
-// covering `sub` scatter blocks' tiles (a hist row for each); the scatter then
-// resolves its messages itself (the one gather of the Send) instead of reading
-// route words the count wrote.  Directories of up to kStabMax actors.  Opt-in
-// (PTYPE_MBOX_SORT=ldscount): the count drops to 18 us (+ 5 us for the table)
-// from 50, but the scatter's own gather is not hidden behind its streams (80 ->
-// 112 us), so 8 Mi Sends take 0.190 ms against the one-pass sort's 0.178.
-constexpr uint32_t kStabMax = 144 * 1024;
-constexpr int kCT = 1024;  // LDS-table count threads per block
-constexpr uint8_t kStabMiss = 0xff, kStabProbe = 0xfe;
-
-__global__ __launch_bounds__(256) void mbx_stab_kernel(const uint32_t* __restrict__ dir, uint32_t n_dir, int rank_self,
-                                                       uint32_t log_s, uint8_t* __restrict__ stab) {
-  const uint32_t i = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= n_dir) return;
-  uint8_t b[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint32_t w = i + k < n_dir ? dir[i + k] : kDirMissing;
-    const uint32_t mb = w >> 8;
-    b[k] = w == kDirFallback ? kStabProbe
-           : (w == kDirMissing || (int)(w & 0xff) != rank_self || mb >= kMaxMbox) ? kStabMiss
-                                                                                 : (uint8_t)(mb & ((1u << log_s) - 1));
-  }
-  if (i + 3 < n_dir) {
-    *reinterpret_cast<uint32_t*>(stab + i) = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) |
-                                             ((uint32_t)b[3] << 24);
-  } else {
-    for (int k = 0; k < 4 && i + k < n_dir; ++k) stab[i + k] = b[k];
-  }
-}
-
-__global__ __launch_bounds__(kCT) void mbx_count_lds_kernel(SortIn in, uint32_t log_s, const uint8_t* __restrict__ stab,
-                                                            uint32_t sub, uint32_t* __restrict__ hist,
-                                                            uint32_t* __restrict__ gsum) {
-  extern __shared__ __align__(16) unsigned char smem_cl[];
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem_cl);  // [S]
-  uint8_t* tab = smem_cl + (size_t)kMboxSortMaxShards * 4;
-  const uint32_t S = 1u << log_s, n = in.n_dir;
-  for (uint32_t j = threadIdx.x * 16; j < n; j += kCT * 16) {
-    if (j + 16 <= n) *reinterpret_cast<uint4*>(tab + j) = *reinterpret_cast<const uint4*>(stab + j);
-    else for (uint32_t k = j; k < n; ++k) tab[k] = stab[k];
-  }
-  constexpr int kIt = kSTile / kCT;  // messages per thread per tile (4)
-  for (uint32_t u = 0; u < sub; ++u) {
-    const uint32_t v = blockIdx.x * sub + u;  // the scatter block whose hist row this is
-    for (uint32_t s = threadIdx.x; s < S; s += kCT) cnt[s] = 0;
-    __syncthreads();
-    if (v < in.G) {
-      const uint32_t t0 = v * in.tpb, t1 = min(t0 + in.tpb, in.tiles);
-      for (uint32_t t = t0; t < t1; ++t) {
-        uint32_t a[kIt];
-#pragma unroll
-        for (int k = 0; k < kIt; ++k) {
-          const int64_t i = (int64_t)t * kSTile + k * kCT + threadIdx.x;
-          a[k] = i < in.M ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
-        }
-#pragma unroll
-        for (int k = 0; k < kIt; ++k) {
-          uint32_t sh = a[k] < n ? tab[a[k]] : (a[k] == 0xffffffffu ? kStabMiss : kStabProbe);
-          if (sh == kStabProbe) {  // not in the directory: the hash table decides
-            int r = -1;
-            uint32_t mb = 0;
-            lookup_entry(in.table, in.mask, actor_key(a[k]), r, mb);
-            sh = (r == in.rank_self && mb < kMaxMbox) ? (mb & (S - 1)) : kStabMiss;
-          }
-          if (sh != kStabMiss) atomicAdd(&cnt[sh], 1u);
-        }
-      }
-    }
-    __syncthreads();
-    if (v < in.G) {
-      uint32_t* g = gsum + (size_t)(v / kGroupBlocks) * S;
-      for (uint32_t s = threadIdx.x; s < S; s += kCT) {
-        const uint32_t c = cnt[s];
-        hist[(size_t)v * S + s] = c;
-        if (c) atomicAdd(&g[s], c);
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------- K2s pass 2: scatter
 // The tile's arguments are loaded with its route words, before the ranking (in
 // flight across it).  Loading them only once the ranks are known (a smaller
 // register file, occupancy 4 -> 5) measured slower: 124 -> 164 us per 8 Mi.
-// RMODE < 0: the count's route words; else the scatter resolves each message
-// itself (registry mode RMODE) -- after the LDS-table count, which writes none.
-template <bool A2, bool MC, int RMODE = -1>
+template <bool A2, bool MC>
 __device__ __forceinline__ void load_routed(const SortIn& in, const uint32_t* __restrict__ rw, uint32_t t,
                                             uint32_t (&m)[kSK], int64_t (&x0)[kSK], int64_t (&x1)[kSK],
                                             int64_t (&x2)[kSK], uint32_t (&meth)[kSK]) {
-  if constexpr (RMODE >= 0) {
-    uint32_t a[kSK];
-    int r[kSK];
-    load_actors(in, t, a);
-    resolve_k<RMODE>(in, a, r, m);
-#pragma unroll
-    for (int k = 0; k < kSK; ++k)
-      if (!(tile_index(t, k) < in.M && r[k] == in.rank_self && m[k] < kMaxMbox)) m[k] = kNoSlot;
-  }
 #pragma unroll
   for (int k = 0; k < kSK; ++k) {
     const int64_t i = tile_index(t, k);
     const bool ok = i < in.M;
-    if constexpr (RMODE < 0) m[k] = ok ? __builtin_nontemporal_load(rw + i) : kNoSlot;
+    m[k] = ok ? __builtin_nontemporal_load(rw + i) : kNoSlot;
     x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
     x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
     x2[k] = 0;
@@ -253,14 +153,14 @@ __device__ __forceinline__ void load_routed(const SortIn& in, const uint32_t* __
 // top bit set when the run spilled / overflowed the room) -- what the ring-order
 // drain and completion read instead of a per-message slot index.  The slot
 // index `sidx` is written only where a consumer needs it: every message with
-// `all_sidx` (the message-order drain, PTYPE_MBOX_DRAIN=msg), and the whole
+// `all_sidx` (the message-order drain, tune mbox_drain_msg=1), and the whole
 // tile when some message of it spilled (the drain runs that tile in message
 // order).  (An opt-in LDS-staged write-out in ring order measured slower,
 // 117 -> 161 us per 8 Mi msgs: the 80 KB stage halved the resident blocks;
 // removed, see git history 4c4ea76.)
 __host__ __device__ constexpr size_t scatter_lds_bytes(uint32_t S) { return (size_t)S * (16 + 4 * (kST / kWave)); }
 
-template <bool A2, bool MC, int RMODE = -1>
+template <bool A2, bool MC>
 __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv, const uint32_t* __restrict__ hist,
                                                           const uint32_t* __restrict__ gsum,
                                                           uint32_t* __restrict__ rw,
@@ -296,7 +196,7 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
     for (uint32_t s = lane; s < S; s += kWave) wcnt(w, s) = 0;  // this wave's row only
     uint32_t mb[kSK], meth[kSK];
     int64_t v0[kSK], v1[kSK], v2[kSK];
-    load_routed<A2, MC, RMODE>(in, rw, t, mb, v0, v1, v2, meth);
+    load_routed<A2, MC>(in, rw, t, mb, v0, v1, v2, meth);
     // rank of each message among this wave's earlier messages of its shard
     uint32_t wr[kSK], sh[kSK];
 #pragma unroll
@@ -346,7 +246,6 @@ __global__ __launch_bounds__(kST) void mbx_scatter_kernel(SortIn in, MboxView mv
         if (spill) {  // stateless batch: the drain runs it from the batch
           ++n_spill;
           sidx[i] = kSpillSlot;
-          if constexpr (RMODE >= 0) rw[i] = mb[k];  // (else the count wrote it)
           continue;
         }
         ++n_ovf;  // answered now, re-sent by send_all
@@ -469,9 +368,6 @@ __device__ __forceinline__ void rec8_next_from(const uint32_t* r8max, uint32_t* 
   }
 }
 
-// LATE: the arguments are loaded after the look-back (a smaller register file
-// across it, more resident blocks; measured slower), else with the actors (in
-// flight across the gathers, the ranking and the look-back).
 // One tile of the one-pass sort (the block claims it); returns its index.
 //
 // reserve (stateless batches): no look-back.  A stateless record runs on its
@@ -482,29 +378,12 @@ __device__ __forceinline__ void rec8_next_from(const uint32_t* r8max, uint32_t* 
 // epoch's total): 16 device-scope atomics per tile, ~2048 per counter at 8 Mi
 // messages -- against a look-back whose walk grows with the tiles in flight
 // (each hop a memory-side round trip).
-// A tile's input columns in registers (the persistent sort loads tile t + 1's while
-// tile t ranks, reserves and scatters).
-template <int SK>
-struct TileRegs {
-  uint32_t a[SK], meth[SK];
-  int64_t v0[SK], v1[SK], v2[SK];
-};
-template <bool A2, bool MC, int SK>
-__device__ __forceinline__ void load_tile_regs(const SortIn& in, uint32_t t, TileRegs<SK>& r) {
-  load_actors<SK>(in, t, r.a);
-  load_cols<A2, MC, SK>(in, t, r.v0, r.v1, r.v2, r.meth);
-}
-
-// PRE: the tile (t_pre) and its inputs (*cur) come from the caller, and once its
-// messages are ranked the next tile's inputs (t_next) are loaded into *nxt.
-template <int MODE, bool A2, bool MC, bool LATE, int SK = kSK, bool PRE = false>
+template <int MODE, bool A2, bool MC, int SK = kSK>
 __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxView& mv, unsigned long long* __restrict__ desc,
                                                   unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                   uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
                                                   uint32_t* __restrict__ rw, const ReplyView& rv, bool spill,
-                                                  bool all_sidx, unsigned char* smem_os, bool reserve = false,
-                                                  TileRegs<SK>* cur = nullptr, TileRegs<SK>* nxt = nullptr,
-                                                  uint32_t t_pre = 0, uint32_t t_next = 0xffffffffu) {
+                                                  bool all_sidx, unsigned char* smem_os, bool reserve = false) {
   const uint32_t S = 1u << mv.log_s;
   unsigned long long* base = reinterpret_cast<unsigned long long*>(smem_os);  // ring position of this tile's run (tail + prefix)
   uint32_t* room = reinterpret_cast<uint32_t*>(base + S);                     // offset limit past the tail
@@ -527,41 +406,21 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   __syncthreads();
   // (reserve: tiles dealt XCD by XCD, as the ring drain deals them -- its reads of a tile's runs then
   // meet the lines in the L2 that took the sort's stores)
-  const uint32_t t = PRE ? t_pre : reserve ? virt_block(blockIdx.x, gridDim.x) : tile_s;
+  const uint32_t t = reserve ? virt_block(blockIdx.x, gridDim.x) : tile_s;
   // the tile's columns: actors, then the arguments in flight across the gathers and the ranking
   uint32_t a[SK], mb[SK], meth[SK];
   int64_t v0[SK], v1[SK], v2[SK];
   int r[SK];
-  if constexpr (PRE) {
-#pragma unroll
-    for (int k = 0; k < SK; ++k) {
-      a[k] = cur->a[k], meth[k] = cur->meth[k];
-      v0[k] = cur->v0[k], v1[k] = cur->v1[k], v2[k] = cur->v2[k];
-    }
-  } else {
-    load_actors<SK>(in, t, a);
-    if constexpr (!LATE) load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
-  }
+  load_actors<SK>(in, t, a);
+  load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
   resolve_k<MODE, SK>(in, a, r, mb);
   uint32_t wr[SK];
-  // an ordered batch in 8-B records (!spill): a message whose fields do not fit takes no
-  // ring position at all -- it must not leave a hole the drain would read -- and answers
-  // kStatusOverflow (re-sent with the next widths)
-  uint32_t esc_pre = 0;
-  if (!LATE && in.rec8 && !spill) {
-    const uint32_t w8p = *in.r8w, wm = w8p & 0xffu, w0 = (w8p >> 8) & 0xffu, w1 = (w8p >> 16) & 0xffu;
-#pragma unroll
-    for (int k = 0; k < SK; ++k) {
-      const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
-      const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
-      if ((mb[k] >> wm) != 0 || (z0 >> w0) != 0 || (z1 >> w1) != 0) esc_pre |= 1u << k;
-    }
-  }
+  // (an ordered batch in 8-B records, !spill: a message whose fields do not fit takes its
+  // ring position like any other and is written as an escape record below -- FIFO kept)
 #pragma unroll
   for (int k = 0; k < SK; ++k) {
-    const bool ok = tile_index<SK>(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox &&
-                    !((esc_pre >> k) & 1u);
-    if (!ok && !((esc_pre >> k) & 1u)) mb[k] = kNoSlot;
+    const bool ok = tile_index<SK>(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
+    if (!ok) mb[k] = kNoSlot;
     const uint32_t sh = mb[k] & (S - 1);
     const uint64_t peers = match_bits(sh, mv.log_s, __ballot(ok));
     const unsigned below = mbcnt64(peers);
@@ -574,59 +433,28 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     wr[k] = (unsigned)__shfl((int)old, leader) + below;
   }
   __syncthreads();
-  if constexpr (PRE) {  // the next tile's inputs, in flight across this one's reservation and scatter
-    if (t_next < in.tiles) load_tile_regs<A2, MC, SK>(in, t_next, *nxt);
-  }
   // per shard: wave offsets within the tile, publish the tile's count, look back for its prefix
   const uint64_t Q = 1ull << mv.log_q;
   unsigned long long timeouts = 0;
   int sp = 0;
-  // Up to 64 shards (the stateless 8-shard view): W = kST / S lanes per shard, the
-  // whole block looking back W tiles per round trip (lookback_group); more shards:
-  // one lane per shard, kLbWin tiles per round trip.
-  const uint32_t W = (!reserve && in.lb_group && S <= kST / 8) ? min(64u, kST / S) : 1u;
-  uint32_t* tcnt = pre;  // (W > 1) the tile's count per shard, until pre[] takes the prefix
-  if (W > 1) {
-    for (uint32_t s = threadIdx.x; s < S; s += kST) {
-      uint32_t c = 0;
-#pragma unroll
-      for (int ww = 0; ww < kST / kWave; ++ww) {
-        const uint32_t x = wcnt(ww, s);
-        wcnt(ww, s) = c;
-        c += x;
-      }
-      tcnt[s] = c;
-      __hip_atomic_exchange(desc + (size_t)t * S + s, desc_word(tag, t == 0 ? kDescP : kDescA, c), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-  }
-  for (uint32_t s = W > 1 ? threadIdx.x / W : threadIdx.x; s < S; s += W > 1 ? S : kST) {
+  for (uint32_t s = threadIdx.x; s < S; s += kST) {
     uint32_t c = 0;
     uint64_t excl = 0;
     unsigned long long* d = desc + (size_t)t * S + s;
-    if (W > 1) {
-      c = tcnt[s];
-      if (t > 0) excl = lookback_group(desc + s, S, (int64_t)t - 1, tag, W, timeouts);
-      if ((threadIdx.x & (W - 1)) != 0) continue;  // one lane per shard from here
-      if (t > 0)
-        __hip_atomic_exchange(d, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
 #pragma unroll
-      for (int ww = 0; ww < kST / kWave; ++ww) {
-        const uint32_t x = wcnt(ww, s);
-        wcnt(ww, s) = c;
-        c += x;
-      }
-      if (reserve) {
-        excl = c ? atomicAdd(&mv.resv[s * kResvStride], c) : 0u;  // this tile's run of shard s
-      } else if (t == 0) {
-        __hip_atomic_exchange(d, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        __hip_atomic_exchange(d, desc_word(tag, kDescA, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        excl = lookback(desc + s, S, (int64_t)t - 1, tag, timeouts);
-        __hip_atomic_exchange(d, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    for (int ww = 0; ww < kST / kWave; ++ww) {
+      const uint32_t x = wcnt(ww, s);
+      wcnt(ww, s) = c;
+      c += x;
+    }
+    if (reserve) {
+      excl = c ? atomicAdd(&mv.resv[s * kResvStride], c) : 0u;  // this tile's run of shard s
+    } else if (t == 0) {
+      __hip_atomic_exchange(d, desc_word(tag, kDescP, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_exchange(d, desc_word(tag, kDescA, c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      excl = lookback(desc + s, S, (int64_t)t - 1, tag, timeouts);
+      __hip_atomic_exchange(d, desc_word(tag, kDescP, excl + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!reserve && t == in.tiles - 1) gsum[s] = (uint32_t)(excl + c);  // the epoch's total of shard s
     const uint64_t tl = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
@@ -642,7 +470,6 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
       tinfo[(size_t)t * 2 * S + S + s] = cc | (excl + c > rm ? kRunSpilled : 0u);
     }
   }
-  if constexpr (LATE) load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
   // (in.rec8) the messages whose fields do not fit an 8-B record -- they spill -- and
   // the tile's fields OR-ed (their bit lengths size the next Send's records)
   uint32_t escm = 0;
@@ -691,7 +518,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     }
     const uint32_t sh = mb[k] & (S - 1);
     const uint32_t off = pre[sh] + wcnt(w, sh) + wr[k];
-    if (off >= room[sh] || ((escm >> k) & 1u)) {  // the ring is full (or the record would not fit 8 B)
+    const bool esc = (escm >> k) & 1u;  // the record would not fit 8 B
+    if (off >= room[sh] || (esc && spill)) {  // the ring is full (or a stateless record spills)
       if (spill) {  // the drain runs it from the batch: its route word is all it needs from here
         ++n_spill;
         sidx[i] = kSpillSlot;
@@ -706,7 +534,11 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     const uint64_t slot = slot_at(mv, sh, base[sh] + off);
     if (wsidx) sidx[i] = (uint32_t)slot;
     const uint32_t mt = meth[k];
-    if (in.rec8) {  // 8-B record (stateless, uniform method, two arguments; wider ones spilled above)
+    if (in.rec8 && esc) {  // (ordered) escape: the place in the tile + bit 63, the fields aside
+      reinterpret_cast<uint64_t*>(mv.rec)[slot] = (uint64_t)(i & ((kST * SK) - 1)) | (1ull << 63);
+      *reinterpret_cast<u32x4*>(in.r8esc + 2 * slot) =
+          u32x4{(uint32_t)v0[k], (uint32_t)((uint64_t)v0[k] >> 32), mb[k], 0u};
+    } else if (in.rec8) {  // 8-B record (uniform method; stateless records that do not fit spilled above)
       const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu;
       const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
       const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
@@ -734,45 +566,14 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   return t;
 }
 
-template <int MODE, bool A2, bool MC, bool LATE, int SK = kSK>
+template <int MODE, bool A2, bool MC>
 __global__ __launch_bounds__(kST) void mbx_onesweep_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
                                                            unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                            uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
                                                            uint32_t* __restrict__ rw, ReplyView rv, bool spill,
                                                            bool all_sidx, bool reserve) {
   extern __shared__ __align__(16) unsigned char smem_os[];
-  (void)onesweep_tile<MODE, A2, MC, LATE, SK>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill, all_sidx, smem_os,
-                                              reserve);
-}
-
-// The reserving one-pass sort as a persistent grid (PTYPE_MBOX_PERSIST=1, experiment):
-// each block owns a contiguous range of tiles (its XCD's share, as the ring drain
-// deals them) and loads tile t + 1's inputs while tile t ranks, reserves and
-// scatters -- the input loads' latency off the per-tile chain.  Two register sets,
-// alternated by an unrolled pair of tiles (no indexed register arrays).
-template <int MODE, bool A2, bool MC, int SK = kSK>
-__global__ __launch_bounds__(kST) void mbx_onesweep_persist_kernel(SortIn in, MboxView mv,
-                                                                   unsigned long long* __restrict__ desc,
-                                                                   unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
-                                                                   uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
-                                                                   uint32_t* __restrict__ rw, ReplyView rv, bool spill,
-                                                                   bool all_sidx) {
-  extern __shared__ __align__(16) unsigned char smem_os[];
-  const uint32_t G = gridDim.x, vb = virt_block(blockIdx.x, G);
-  const uint32_t per = (in.tiles + G - 1) / G, t0 = vb * per, t1 = min(t0 + per, in.tiles);
-  TileRegs<SK> r0, r1;
-  if (t0 < t1) load_tile_regs<A2, MC, SK>(in, t0, r0);
-  for (uint32_t t = t0; t < t1; t += 2) {
-    (void)onesweep_tile<MODE, A2, MC, false, SK, true>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill,
-                                                       all_sidx, smem_os, true, &r0, &r1, t,
-                                                       t + 1 < t1 ? t + 1 : 0xffffffffu);
-    __syncthreads();  // the tile's LDS is reused
-    if (t + 1 >= t1) break;
-    (void)onesweep_tile<MODE, A2, MC, false, SK, true>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill,
-                                                       all_sidx, smem_os, true, &r1, &r0, t + 1,
-                                                       t + 2 < t1 ? t + 2 : 0xffffffffu);
-    __syncthreads();
-  }
+  (void)onesweep_tile<MODE, A2, MC>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, spill, all_sidx, smem_os, reserve);
 }
 
 // ---------------------------------------------------------------- compact record decode
@@ -873,7 +674,7 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 // message-order form's slot-index read (4 B per message) and its 16-B gather per
 // message (one line per lane).
 //
-// Message-order form (PTYPE_MBOX_DRAIN=msg, and any tile with a spilled
+// Message-order form (tune mbox_drain_msg=1, and any tile with a spilled
 // message): each message's record is taken from the ring slot the scatter
 // recorded, replies coalesced; a spilled message runs straight from the batch.
 //
@@ -1171,7 +972,7 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
 // two, the drain's reads are L2 hits of lines the sort just wrote, and no block
 // waits at a kernel boundary for the slowest tile.  The last block to finish
 // commits every shard's epoch (tail = head = tail + total) and advances the
-// look-back tag.  PTYPE_MBOX_FUSED=0: the separate kernels.
+// look-back tag.  Tune mbox_fused=0: the separate kernels.
 template <int MODE, bool A2, bool MC, int FIXED, bool R8, int SK = kSK>
 __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
                                                             unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
@@ -1183,8 +984,8 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
                                                             uint32_t* __restrict__ r8host) {
   extern __shared__ __align__(16) unsigned char smem_sd[];
   const uint32_t S = 1u << mv.log_s;
-  const uint32_t t = onesweep_tile<MODE, A2, MC, false, SK>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, true, false,
-                                                            smem_sd, reserve);
+  const uint32_t t = onesweep_tile<MODE, A2, MC, SK>(in, mv, desc, tctr, gsum, sidx, tinfo, rw, rv, true, false,
+                                                     smem_sd, reserve);
   // every wave's ring stores are out before any wave reads the tile's runs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1401,7 +1202,7 @@ struct OrdLds {
   int64_t a0[kWin], a1[A12 ? kWin : 2], a2[A12 ? kWin : 2];
 };
 
-// OK: records per thread per window (window = 512 * OK records; PTYPE_ORD_WIN=4096: OK = 8).
+// OK: records per thread per window (window = 512 * OK records: OK = 8 for one-argument batches).
 // FIXED = kSeqFold: a uniform SeqFold batch.  With every actor of the shard in its
 // own bin (at most kOrdThreads of them, state staged), thread b IS actor b's
 // consumer for the whole Send: its state stays in a register and each record is
@@ -1413,16 +1214,25 @@ struct OrdLds {
 struct R8Args {
   const uint32_t* r8w = nullptr;  // this Send's widths (the sort's)
   uint32_t method = 0;            // the batch's uniform method
+  const int64_t* esc = nullptr;   // escape records' {a0, mailbox}, by ring slot (SortIn::r8esc)
 };
-__device__ __forceinline__ SortRec decode_rec8_ord(uint64_t r, uint32_t w8, uint32_t method) {
+__device__ __forceinline__ SortRec decode_rec8_ord(uint64_t r, uint32_t w8, uint32_t method, const int64_t* esc,
+                                                   uint64_t slot) {
   const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
   SortRec x;
   x.valid = true;
   x.origin = (uint32_t)(r & (kSTile - 1));  // the place in the tile
-  x.mb = (uint32_t)((r >> 12) & ((1ull << wm) - 1));
   x.method = method;
   x.flags = 0;
   x.a2 = 0;
+  if (r >> 63) {  // escape record (one-argument batches leave the top bit of a record zero)
+    const u32x4 e = *reinterpret_cast<const u32x4*>(esc + 2 * slot);
+    x.a0 = (int64_t)(((uint64_t)e.y << 32) | e.x);
+    x.mb = e.z;
+    x.a1 = 0;
+    return x;
+  }
+  x.mb = (uint32_t)((r >> 12) & ((1ull << wm) - 1));
   const uint64_t z0 = (r >> (12 + wm)) & ((1ull << w0) - 1), z1 = (r >> (12 + wm + w0)) & ((1ull << w1) - 1);
   x.a0 = (int64_t)(z0 >> 1) ^ -(int64_t)(z0 & 1);
   x.a1 = (int64_t)(z1 >> 1) ^ -(int64_t)(z1 & 1);
@@ -1475,7 +1285,7 @@ __global__ __launch_bounds__(kOrdThreads) __attribute__((amdgpu_waves_per_eu(1, 
   const uint64_t n = tot < free ? tot : free;
   const uint64_t sbase = (uint64_t)s << mv.log_q, qmask = Q - 1, rot = shard_rot(mv, s);  // slot_at, hoisted
   unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
-  // PF (the fold's default; PTYPE_ORD_PREFETCH=0: off): the next window's records (their first 16 B) are loaded
+  // PF (the fold: the next window's records (their first 16 B) are loaded
   // while this one is binned and run -- one block per CU (the LDS), so the registers are
   // there.  (Round 3, with the handler switch's register file: measured no faster, 188 ->
   // 200 us, and spilled to scratch.)
@@ -1504,7 +1314,7 @@ __global__ __launch_bounds__(kOrdThreads) __attribute__((amdgpu_waves_per_eu(1, 
       if (q < w1) {
         if constexpr (R8) {
           x[k] = decode_rec8_ord(PF ? (uint64_t)cur[k] : reinterpret_cast<const uint64_t*>(mv.rec)[slot[k]], w8,
-                                 r8.method);
+                                 r8.method, r8.esc, slot[k]);
         } else if constexpr (PF) {
           u32x4 hb = {0u, 0u, 0u, 0u};
           int64_t a2v = 0;
@@ -1629,203 +1439,6 @@ __global__ __launch_bounds__(256) void mbx_rec8_next_kernel(const uint32_t* __re
   rec8_next_from(r8max, r8w, host, tiles);
 }
 
-// ---------------------------------------------------------------- K3s ordered drain, binned
-// The same per-actor FIFO drain, with the shard's records binned before any runs
-// (the windowed form above is 16 dependent load -> sort -> serial
-// rounds per 8 Mi SeqFold shard, 175 us).  A super-window of up to nr * 4096
-// records is binned first: each round reads only the records' first 8 B (valid
-// mark + mailbox) -- the next round's are loaded while this one is binned -- and
-// places each record's window offset (2 B) in LDS, stably by bin (a round's bin
-// runs in ring order, rounds in ring order).  Then thread b walks bin b's
-// entries round by round, loading 8 records at a time ahead of running them
-// one after another: an actor's messages run serially in FIFO order, distinct
-// bins in parallel, with the record loads in flight together instead of one
-// window's load per round trip.  The replies are staged at the records' ring
-// slots as before (mbx_complete_ring_kernel).  PTYPE_ORD_DRAIN=bin (the windowed form is the default).
-constexpr int kOrdBinK = 8;                            // records per thread per binning round
-constexpr int kOrdRound = kOrdThreads * kOrdBinK;      // 4096
-constexpr int kOrdBinRoundsMax = 12;                   // rounds per super-window (LDS-bound)
-constexpr int kOrdBinBatch = 8;                        // records a bin walk loads ahead
-
-__host__ __device__ constexpr size_t ord_bin_lds_bytes(uint32_t nr, uint32_t n_loc) {
-  return (size_t)kOrdWaves * kOrdThreads * 4                     // wcnt
-         + (((size_t)nr * (kOrdThreads + 1) * 2 + 15) & ~(size_t)15)  // bs: bin starts per round (u16)
-         + (size_t)nr * kOrdRound * 2                              // pos: window offsets (u16)
-         + (size_t)n_loc * 8;                                      // staged state
-}
-
-__global__ __launch_bounds__(kOrdThreads) void mbx_drain_ord_bin_kernel(MboxView mv, uint32_t* __restrict__ gsum,
-                                                                        uint32_t ngroups, int64_t* __restrict__ state,
-                                                                        uint32_t n_state, uint64_t delay_ticks,
-                                                                        OutboxView ob, u32x4* __restrict__ srep,
-                                                                        uint32_t nr, uint32_t origin_base) {
-  extern __shared__ __align__(16) unsigned char smem_ob[];
-  uint32_t(*wcnt)[kOrdThreads] = reinterpret_cast<uint32_t(*)[kOrdThreads]>(smem_ob);
-  uint16_t* bs = reinterpret_cast<uint16_t*>(smem_ob + (size_t)kOrdWaves * kOrdThreads * 4);
-  uint16_t* pos = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(bs) +
-                                              (((size_t)nr * (kOrdThreads + 1) * 2 + 15) & ~(size_t)15));
-  int64_t* st_lds = reinterpret_cast<int64_t*>(pos + (size_t)nr * kOrdRound);
-  __shared__ uint32_t tot_s;
-  __shared__ uint32_t wsum[kOrdWaves];
-  const uint32_t s = blockIdx.x;
-  const uint32_t S = 1u << mv.log_s;
-  const uint64_t Q = 1ull << mv.log_q;
-  const unsigned w = threadIdx.x / kWave, lane = lane_id();
-  if (threadIdx.x == 0) tot_s = epoch_total(gsum, ngroups, S, s, true);
-  const uint64_t lo = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
-  const uint64_t free = hd + Q > lo ? hd + Q - lo : 0;
-  const uint32_t n_loc = (state && s < n_state) ? (n_state - 1 - s) / S + 1 : 0;
-  const bool in_lds = state && n_loc <= kOrdStateMax;
-  if (in_lds)
-    for (uint32_t j = threadIdx.x; j < n_loc; j += kOrdThreads) st_lds[j] = state[s + (uint64_t)j * S];
-  __syncthreads();
-  const uint32_t tot = tot_s;
-  const uint64_t n = tot < free ? tot : free;
-  const uint64_t sbase = (uint64_t)s << mv.log_q, qmask = Q - 1, rot = shard_rot(mv, s);
-  const uint64_t SW = (uint64_t)nr * kOrdRound;  // records per super-window
-  unsigned long long done = 0, failed = 0, holes = 0, serial = 0;
-  int64_t* st = in_lds ? st_lds : state;
-  const uint32_t nst = in_lds ? n_loc : n_state;
-  for (uint64_t w0 = lo; w0 < lo + n; w0 += SW) {
-    const uint64_t w1 = lo + n < w0 + SW ? lo + n : w0 + SW;
-    const uint32_t rounds = (uint32_t)((w1 - w0 + kOrdRound - 1) / kOrdRound);
-    // ---- bin: round r's records' headers (loaded one round ahead)
-    uint2 h[kOrdBinK];
-    auto load_hdr = [&](uint32_t r, uint2(&x)[kOrdBinK]) {
-#pragma unroll
-      for (int k = 0; k < kOrdBinK; ++k) {
-        const uint64_t q = w0 + (uint64_t)r * kOrdRound + (uint64_t)w * (kWave * kOrdBinK) + (uint64_t)k * kWave + lane;
-        x[k] = q < w1 ? *reinterpret_cast<const uint2*>(rec_a(mv, sbase | ((q + rot) & qmask))) : uint2{0u, 0u};
-      }
-    };
-    load_hdr(0, h);
-    for (uint32_t r = 0; r < rounds; ++r) {
-      uint2 nx[kOrdBinK];
-      if (r + 1 < rounds) load_hdr(r + 1, nx);
-      for (uint32_t b = lane; b < kOrdThreads; b += kWave) wcnt[w][b] = 0;
-      uint32_t bin[kOrdBinK], wr[kOrdBinK];
-      bool ok[kOrdBinK];
-#pragma unroll
-      for (int k = 0; k < kOrdBinK; ++k) {
-        ok[k] = (h[k].x & kCompactMark) != 0;
-        const uint64_t q = w0 + (uint64_t)r * kOrdRound + (uint64_t)w * (kWave * kOrdBinK) + (uint64_t)k * kWave + lane;
-        if (!ok[k] && q < w1) ++holes;
-        bin[k] = ((h[k].y & 0xffffffu) >> mv.log_s) & (kOrdThreads - 1);
-        const uint64_t peers = match_bits(bin[k], 9, __ballot(ok[k]));
-        const unsigned below = mbcnt64(peers);
-        const int leader = peers ? __builtin_ctzll(peers) : 0;
-        unsigned old = 0;
-        if (ok[k] && below == 0) {
-          old = wcnt[w][bin[k]];
-          wcnt[w][bin[k]] = old + (unsigned)__popcll(peers);
-        }
-        wr[k] = (unsigned)__shfl((int)old, leader) + below;
-      }
-      __syncthreads();
-      uint16_t* bsr = bs + (size_t)r * (kOrdThreads + 1);
-      {  // bin totals and wave offsets (thread b owns bin b), then an exclusive scan over bins
-        const unsigned b = threadIdx.x;
-        unsigned c = 0;
-#pragma unroll
-        for (int ww = 0; ww < kOrdWaves; ++ww) {
-          const unsigned x = wcnt[ww][b];
-          wcnt[ww][b] = c;
-          c += x;
-        }
-        const unsigned inc = wave_incl_scan(c);
-        if (lane == kWave - 1) wsum[w] = inc;
-        __syncthreads();
-        unsigned off = inc - c;
-        for (unsigned ww = 0; ww < w; ++ww) off += wsum[ww];
-        bsr[b] = (uint16_t)off;
-        if (b == kOrdThreads - 1) bsr[kOrdThreads] = (uint16_t)(off + c);
-      }
-      __syncthreads();
-      uint16_t* pr = pos + (size_t)r * kOrdRound;
-#pragma unroll
-      for (int k = 0; k < kOrdBinK; ++k) {
-        if (!ok[k]) continue;
-        const uint32_t q = (uint32_t)r * kOrdRound + w * (kWave * kOrdBinK) + (uint32_t)k * kWave + lane;
-        pr[bsr[bin[k]] + wcnt[w][bin[k]] + wr[k]] = (uint16_t)q;  // (bsr[kOrdRound]: 4096 fits u16)
-      }
-#pragma unroll
-      for (int k = 0; k < kOrdBinK; ++k) h[k] = nx[k];
-    }
-    __syncthreads();
-    // ---- run: this thread's bin, round by round, kOrdBinBatch records loaded ahead
-    {
-      const unsigned b = threadIdx.x;
-      uint32_t r = 0, d = 0, e = 0;
-      if (rounds) {
-        d = bs[b];
-        e = bs[b + 1];
-      }
-      uint32_t mine = 0;
-      for (;;) {
-        uint64_t sl[kOrdBinBatch];
-        bool have[kOrdBinBatch];
-#pragma unroll
-        for (int k = 0; k < kOrdBinBatch; ++k) {
-          while (d >= e && r < rounds) {
-            if (++r >= rounds) break;
-            d = bs[(size_t)r * (kOrdThreads + 1) + b];
-            e = bs[(size_t)r * (kOrdThreads + 1) + b + 1];
-          }
-          have[k] = r < rounds && d < e;
-          sl[k] = 0;
-          if (have[k]) {
-            sl[k] = sbase | ((w0 + pos[(size_t)r * kOrdRound + d] + rot) & qmask);
-            ++d;
-          }
-        }
-        if (!have[0]) break;
-        u32x4 ha[kOrdBinBatch];
-#pragma unroll
-        for (int k = 0; k < kOrdBinBatch; ++k)
-          ha[k] = have[k] ? *reinterpret_cast<const u32x4*>(rec_a(mv, sl[k])) : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int k = 0; k < kOrdBinBatch; ++k) {
-          if (!have[k]) continue;
-          u32x4 hb = {0u, 0u, 0u, 0u};
-          int64_t a2v = 0;
-          if (rec_is_long(ha[k])) {
-            hb = *reinterpret_cast<const u32x4*>(rec_b(mv, sl[k]));
-            if (((ha[k].z >> 16) & kFlagA2) && mv.a2) a2v = mv.a2[sl[k]];
-          }
-          const SortRec x = decode_sorted(ha[k], hb, a2v);
-          MsgRecord m;
-          m.actor = in_lds ? (x.mb >> mv.log_s) : x.mb;
-          m.method = (uint16_t)x.method;
-          m.flags = (uint16_t)x.flags;
-          m.a0 = x.a0, m.a1 = x.a1, m.a2 = x.a2;
-          const ReplyRecord rr = run_handler(m, st, nst, delay_ticks, ob, true);
-          failed += rr.status != kStatusOk;
-          srep[sl[k]] = u32x4{(uint32_t)rr.value, (uint32_t)((uint64_t)rr.value >> 32), (uint32_t)rr.status,
-                              (x.origin - origin_base) & (uint32_t)(kSTile - 1)};
-          ++done;
-          ++mine;
-          if (!in_lds) vm_drain();  // global state: this store lands before the bin's next load
-        }
-      }
-      if (mine > 1) serial += mine - 1;
-    }
-    __syncthreads();  // the super-window's LDS is reused
-  }
-  if (in_lds)
-    for (uint32_t j = threadIdx.x; j < n_loc; j += kOrdThreads) state[s + (uint64_t)j * S] = st_lds[j];
-  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, holes, kMbHoles);
-  __syncthreads();
-  block_add_stats(mv.stats, serial, kMbSerial, 0, -1, 0, -1);
-  if (threadIdx.x == 0) epoch_commit(mv, s, tot);
-}
-
-// Ordered drain's replies, staged at ring slots as {value, status, origin}, put
-// back into message order -- in RING order like the parallel drain: one block
-// per tile reads the tile's runs (whole lines), stages each reply at its place
-// in the tile (the origin word) in LDS, and writes the tile's replies out
-// coalesced.  (The message-order form gathered one 16-B word per message by the
-// scatter's slot index: 109 us per 8 Mi SeqFold messages.)  Overflowed
-// messages were answered by the scatter and have no run entry.
 __global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxView mv,
                                                                 const uint32_t* __restrict__ tinfo,
                                                                 const u32x4* __restrict__ srep, ReplyView rv,
@@ -1875,23 +1488,23 @@ __global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxV
 }
 
 // ---------------------------------------------------------------- host
-// The fused sort + drain for stateless one-pass Sends (PTYPE_MBOX_FUSED=0: two launches).
-// the fused sort + drain kernel: slower than the two kernels for large batches once the sort
+// The fused sort + drain kernel: slower than the two kernels for large batches once the sort
 // reserves its runs (8 Mi: 149 vs 95 + 39 us; its register file halves the drain's occupancy),
 // faster for small ones, where a launch and a kernel boundary weigh more (1 Mi bench step: 5-7 %
-// in three sessions).  Default: fused up to 512 tiles (2 Mi messages); PTYPE_MBOX_FUSED=1 / 0
-// forces it on / off.
+// in three sessions).  Fused up to 512 tiles (2 Mi messages); tune mbox_fused=1 / 0 forces it.
 static bool fused_ok(int64_t tiles) {
-  static const int env = getenv("PTYPE_MBOX_FUSED") ? atoi(getenv("PTYPE_MBOX_FUSED")) : -1;
-  return env == 1 || (env < 0 && tiles <= 512);
-}
-// one-pass sorts of stateless batches reserve each tile's runs with atomics
-// instead of looking back (onesweep_tile); PTYPE_MBOX_RESERVE=0: look-back
-static bool reserve_ok() {
-  static const bool on = !(getenv("PTYPE_MBOX_RESERVE") && std::string(getenv("PTYPE_MBOX_RESERVE")) == "0");
-  return on;
+  const int f = tune().mbox_fused;
+  return f == 1 || (f < 0 && tiles <= 512);
 }
 
+// Removed variants (measured slower or flat; A/B rows in profiles/r4_mailbox_ab.md and
+// profiles/r5_mailbox_ab.md): the look-back sort for stateless batches (run reservations
+// won), the persistent reserving sort (42.8 vs 50.5 G msg/s), 1024- and 2048-message tiles
+// for the fused / separate sort, arguments loaded after the look-back, the LDS-table count,
+// the group look-back, non-temporal directory gathers and reply stores, the binned ordered
+// drain (233 vs 175 us), 2048-record ordered windows, the ordered drain without the
+// register fold or the prefetched window, 16-B ordered records at 8 Mi, the wide ring
+// drain and the 8 / 16 / 32-shard stateless views other than 8.
 void Mailboxes::send_sorted(const MboxSend& a) {
   const uint32_t S = shards();
   if (S > (uint32_t)kMboxSortMaxShards) throw std::invalid_argument("sorted mailboxes: at most 1024 shards");
@@ -1907,15 +1520,16 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   if (a.arrival && a.ordered) throw std::invalid_argument("mailbox send: arrival sharding cannot serve ordered methods");
   PT_HIP_CHECK(hipSetDevice(device_));
   hipStream_t st = as_stream(a.stream);
+  const Tune tn = tune();
+  auto capturing = [&] {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+  };
   const int64_t tiles = (a.M + kSTile - 1) / kSTile;
   if (tiles > 0xffffffffll) throw std::invalid_argument("mailbox send: batch too large");
-  // per-tile workspace sized for the small tiles a fused Send may take (kSKSmall)
-  const int64_t tiles_ws = (a.M + kST * kSKSmall - 1) / (kST * kSKSmall);
   // per-message workspace (route words, ring slots) and per-tile runs: grown outside graph capture
   if (!a.arrival && (uint64_t)a.M > sort_cap_) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-      throw std::runtime_error("mailbox send: a larger batch than before inside a graph capture (warm up first)");
+    if (capturing()) throw std::runtime_error("mailbox send: a larger batch than before inside a graph capture (warm up first)");
     PT_HIP_CHECK(hipStreamSynchronize(st));
     for (void** p : {(void**)&sort_rw_, (void**)&sort_sidx_, (void**)&sort_tinfo_, (void**)&sort_desc_})
       if (*p) {
@@ -1924,17 +1538,15 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       }
     PT_HIP_CHECK(hipMalloc((void**)&sort_rw_, (size_t)a.M * 4));
     PT_HIP_CHECK(hipMalloc((void**)&sort_sidx_, (size_t)a.M * 4));
-    PT_HIP_CHECK(hipMalloc((void**)&sort_tinfo_, (size_t)tiles_ws * 2 * S * 4));
+    PT_HIP_CHECK(hipMalloc((void**)&sort_tinfo_, (size_t)tiles * 2 * S * 4));
     // look-back descriptors: zero = no tag (every Send's tag is >= 1)
-    PT_HIP_CHECK(hipMalloc((void**)&sort_desc_, (size_t)tiles_ws * S * 8));
-    PT_HIP_CHECK(hipMemsetAsync(sort_desc_, 0, (size_t)tiles_ws * S * 8, st));
+    PT_HIP_CHECK(hipMalloc((void**)&sort_desc_, (size_t)tiles * S * 8));
+    PT_HIP_CHECK(hipMemsetAsync(sort_desc_, 0, (size_t)tiles * S * 8, st));
     PT_HIP_CHECK(hipStreamSynchronize(st));
     sort_cap_ = (uint64_t)a.M;
   }
   if (a.ordered && !stage_rep_) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-      throw std::runtime_error("mailbox send: first ordered Send inside a graph capture (warm up first)");
+    if (capturing()) throw std::runtime_error("mailbox send: first ordered Send inside a graph capture (warm up first)");
     const uint64_t n = (uint64_t)S * slots();
     PT_HIP_CHECK(hipMalloc(&stage_rep_, n * 16));
     bytes_ += n * 16;
@@ -1956,42 +1568,29 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   in.aw_shift = (a.affine_w && (a.affine_w & (a.affine_w - 1)) == 0) ? __builtin_ctz(a.affine_w) : -1;
   in.rank_self = a.rank_self;
   in.origin_base = a.origin_base;
-  static const bool dir_nt = getenv("PTYPE_DIR_NT") && atoi(getenv("PTYPE_DIR_NT")) != 0;
-  in.dir_nt = dir_nt;
-  static const bool lb_group = getenv("PTYPE_LB_GROUP") && atoi(getenv("PTYPE_LB_GROUP")) == 1;  // measured slower
-  in.lb_group = lb_group;
   in.tiles = (uint32_t)tiles;
   // blocks: as many as the histogram holds (it stays L2-resident for the prefixes),
   // a multiple of 8 (one contiguous eighth of the batch per XCD)
-  static const int64_t g_env = getenv("PTYPE_SORT_BLOCKS") ? atoll(getenv("PTYPE_SORT_BLOCKS")) : 0;
-  int64_t G = std::min<int64_t>({tiles, (int64_t)(kMboxSortHistWords / S), g_env > 0 ? g_env : (int64_t)1024,
+  int64_t G = std::min<int64_t>({tiles, (int64_t)(kMboxSortHistWords / S), (int64_t)1024,
                                  (int64_t)kMboxSortGroups * kGroupBlocks});
   if (G >= 8) G -= G % 8;
   G = std::max<int64_t>(G, 1);
   in.G = (uint32_t)G;
   in.tpb = (uint32_t)((tiles + G - 1) / G);
   // one block per tile (tile-granular kernels), dealt XCD by XCD: a multiple of 8
-  uint32_t tile_grid = (uint32_t)(tiles >= 8 ? (tiles + 7) / 8 * 8 : tiles);
-  // the sort: one pass with look-back, or count + scatter -- for batches under 1024 tiles (4 Mi msgs) and
-  // with PTYPE_MBOX_SORT=twopass (measured: 8 Mi msgs 0.212-0.221 vs 0.228-0.230 ms per Send; 1 Mi msgs
-  // 0.047-0.049 vs 0.043: a small grid cannot hide the look-back's round trips); PTYPE_MBOX_SORT=onepass forces it
-  static const char* sort_env = getenv("PTYPE_MBOX_SORT");
-  static const int env_mode = !sort_env ? 0
-                              : std::string(sort_env) == "onepass" ? 1
-                              : std::string(sort_env) == "twopass" ? 2
-                              : std::string(sort_env) == "ldscount" ? 3 : 0;
-  // (stateless batches of any size take the one-pass sort when the fused sort + drain is on: one launch per Send)
+  const uint32_t tile_grid = (uint32_t)(tiles >= 8 ? (tiles + 7) / 8 * 8 : tiles);
+  // the sort: one pass, or count + scatter.  Stateless batches always take the one pass (each
+  // tile reserves its runs: no look-back); ordered ones look back, which a grid under 1024
+  // tiles cannot hide (8 Mi msgs 0.212-0.221 vs 0.228-0.230 ms per Send; 1 Mi msgs 0.047-0.049
+  // vs 0.043 for count + scatter).  Tune mbox_sort=1 / 2 forces either.
   const int sort_mode = a.sort_mode ? a.sort_mode
-                        : env_mode  ? env_mode
-                        : (tiles >= 1024 || (!a.ordered && !a.arrival && (fused_ok(tiles) || reserve_ok()))) ? 1
-                                                                                                         : 2;
-  if (sort_mode < 1 || sort_mode > 3) throw std::invalid_argument("mailbox send: sort_mode 0..3");
-  const bool two_pass = sort_mode != 1;
+                        : tn.mbox_sort ? tn.mbox_sort
+                        : (tiles >= 1024 || (!a.ordered && !a.arrival)) ? 1 : 2;
+  if (sort_mode < 1 || sort_mode > 2) throw std::invalid_argument("mailbox send: sort_mode 0..2");
+  const bool two_pass = sort_mode == 2;
   const uint32_t ngroups = two_pass ? (uint32_t)((G + kGroupBlocks - 1) / kGroupBlocks) : 1u;
   const int mode = (a.affine_w && a.n_dir) ? 2 : (a.dir && a.n_dir) ? 1 : 0;
   ReplyView rv{(int64_t*)a.out_val, (int32_t*)a.out_st, a.out_n};
-  static const bool reply_nt = getenv("PTYPE_REPLY_NT") && atoi(getenv("PTYPE_REPLY_NT")) == 1;
-  rv.nt = reply_nt;
   OutboxView ob;
   if (a.outbox_cap) {
     if (a.outbox.size() != 6) throw std::invalid_argument("outbox: [actor, a0, a1, a2, method, count]");
@@ -2036,76 +1635,52 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     return;
   }
 
-  // Stateless batches run on a COARSER view of the same rings: S' shards of
-  // Q * S / S' slots (every ring is empty between epoch Sends, so any view keeps
-  // each actor's messages in one ring, in message order; ordered batches keep the
-  // full S for the ordered drain's one block per shard).  Longer runs per tile
-  // and shard (~256 records of a 4096-message tile: whole lines for the scatter's
-  // stores and the drain's loads).  8 Mi msgs, 256 shards -> 32 / 16 / 8:
-  // 0.222 -> 0.186 / 0.179 / 0.180 ms per Send (PTYPE_MBOX_STATELESS_SHARDS,
-  // 0 = the full geometry).  Round 4, with run reservations and 8-B records: 8
-  // shards, 2-3 % faster per bench step than 16 (profiles/r4_mailbox_ab.md).
+  // Stateless batches run on a COARSER view of the same rings: 8 shards of Q * S / 8
+  // slots (every ring is empty between epoch Sends, so any view keeps each actor's
+  // messages in one ring, in message order; ordered batches keep the full S for the
+  // ordered drain's one block per shard).  Longer runs per tile and shard: whole lines
+  // for the sort's stores and the drain's loads (8 Mi msgs, 256 shards -> 32 / 16 / 8:
+  // 0.222 -> 0.186 / 0.179 / 0.180 ms per Send; round 4 with run reservations and 8-B
+  // records: 8 shards 2-3 % faster per bench step than 16, profiles/r4_mailbox_ab.md).
   MboxView mv = mv_;
   uint32_t Sv = S;
-  if (!a.ordered) {
-    static const int s_env =
-        getenv("PTYPE_MBOX_STATELESS_SHARDS") ? atoi(getenv("PTYPE_MBOX_STATELESS_SHARDS")) : 8;
-    if (s_env > 0 && (s_env & (s_env - 1)) == 0 && (uint32_t)s_env < S) {
-      const uint32_t k = mv.log_s - (uint32_t)__builtin_ctz((unsigned)s_env);
-      mv.log_s -= k;
-      mv.log_q += k;
-      Sv = (uint32_t)s_env;
-    }
+  constexpr uint32_t kStatelessShards = 8;
+  if (!a.ordered && kStatelessShards < S) {
+    const uint32_t k = mv.log_s - (uint32_t)__builtin_ctz(kStatelessShards);
+    mv.log_s -= k;
+    mv.log_q += k;
+    Sv = kStatelessShards;
   }
   last_view_shards_ = Sv;
-  // the stateless drain: ring order (default) or message order (PTYPE_MBOX_DRAIN=msg: every slot index written)
-  static const bool msg_drain = getenv("PTYPE_MBOX_DRAIN") && std::string(getenv("PTYPE_MBOX_DRAIN")) == "msg";
+  // the stateless drain: ring order (default) or message order (tune mbox_drain_msg: every slot index written)
+  const bool msg_drain = tn.mbox_drain_msg != 0;
   const bool all_sidx = msg_drain && !a.ordered;
-  const bool reserve = !a.ordered && reserve_ok() && sort_mode == 1;  // (one-pass: tiles reserve runs)
-  static const int sk_mid_env = getenv("PTYPE_MBOX_SK") ? atoi(getenv("PTYPE_MBOX_SK")) : 0;
-  // (the unfused one-pass Send with 2048-message tiles: set below when it is the path taken)
-  const bool mid_ok = sk_mid_env == 4 && !a.ordered && !a.arrival && !all_sidx && sort_mode == 1 && !a.a2 &&
-                      !a.method_col && !(!a.ordered && !all_sidx && Sv <= 256 && fused_ok(tiles));
-  bool mid = false;
+  const bool reserve = !a.ordered && sort_mode == 1;  // (one-pass stateless: tiles reserve runs)
   if (reserve) {
     if (!sort_resv_) {
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-        throw std::runtime_error("mailbox send: first reserving Send inside a graph capture (warm up first)");
+      if (capturing()) throw std::runtime_error("mailbox send: first reserving Send inside a graph capture (warm up first)");
       PT_HIP_CHECK(hipMalloc((void**)&sort_resv_, (size_t)kMboxSortMaxShards * kResvStride * 4));
       PT_HIP_CHECK(hipMemset(sort_resv_, 0, (size_t)kMboxSortMaxShards * kResvStride * 4));
     }
     mv.resv = sort_resv_;
   }
-  // 8-B ring records: one-pass sort of a stateless batch of one two-argument method, ring-order drain
-  // (PTYPE_MBOX_REC8=0: 16-B records).  Field widths: the mailbox from the state size or the
-  // directory (a wider mailbox spills), the rest split between the zigzag arguments.
-  static const bool late = getenv("PTYPE_OS_LATE") && std::string(getenv("PTYPE_OS_LATE")) == "1";
   // Rank byte gathers (route mode 3) for a stateless uniform one-pass Send on the
   // directory: 1 B per id (L2-resident) instead of the 4-B route word, and the
   // records carry the actor id -- every actor's messages still meet in one ring
   // (the shard is a function of the id), and no stateless handler reads a mailbox.
-  // PTYPE_MBOX_RANK_TABLE=0: the directory gathers.
-  static const bool rank_env = !(getenv("PTYPE_MBOX_RANK_TABLE") && atoi(getenv("PTYPE_MBOX_RANK_TABLE")) == 0);
-  const bool rank_route = rank_env && mode == 1 && a.dir_rank && a.n_dir <= kMaxMbox && !a.ordered && !a.arrival &&
-                          !all_sidx && !a.a2 && !a.method_col && method_stateless((uint32_t)a.method_uniform) &&
-                          sort_mode == 1 && !late;
+  const bool rank_route = mode == 1 && a.dir_rank && a.n_dir <= kMaxMbox && !a.ordered && !all_sidx && !a.a2 &&
+                          !a.method_col && method_stateless((uint32_t)a.method_uniform) && sort_mode == 1;
   last_route_ = rank_route ? 3 : mode;
-  // (batches up to 512 tiles, which take the fused kernel, keep 16-B records: measured faster
-  // there -- 1 Mi bench step 24.1 vs 21.9 G msg/s in three sessions -- while 8 Mi gains with 8 B)
-  static const int rec8_env = getenv("PTYPE_MBOX_REC8") ? atoi(getenv("PTYPE_MBOX_REC8")) : -1;
-  // ordered batches: a uniform one-argument batch on the windowed drain's 4096-record form
-  // takes 8-B records too -- a record that does not fit overflows (re-sent).  Round 5: 25.5
-  // vs 24.5 G msg/s per 8 Mi SeqFold step; PTYPE_ORD_REC8=0 keeps 16-B records
-  static const bool ord_rec8_env = !(getenv("PTYPE_ORD_REC8") && atoi(getenv("PTYPE_ORD_REC8")) == 0);
-  static const bool ord_win2048 = getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 2048;
-  static const bool ord_bin_env = getenv("PTYPE_ORD_DRAIN") && std::string(getenv("PTYPE_ORD_DRAIN")) == "bin";
-  const bool ord_r8 = a.ordered && ord_rec8_env && !a.a1 && !ord_win2048 && !ord_bin_env;
-  const bool r8 = (rec8_env == 1 || (rec8_env < 0 && tiles > 512)) && sort_mode == 1 && (!a.ordered || ord_r8) &&
-                  !a.arrival && !a.a2 && !a.method_col && mv.planar && !all_sidx;
-  if (r8 && (!r8w_ || r8_tiles_ < (uint64_t)tiles_ws)) {  // (outside a capture: grown with the sort workspace)
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+  // 8-B ring records: one-pass sort of a batch of one method, at most two arguments for
+  // stateless batches (the ring-order drain) and one for ordered ones (the windowed drain:
+  // 25.5 vs 24.5 G msg/s per 8 Mi SeqFold step, round 5).  Batches up to 512 tiles, which
+  // take the fused kernel, keep 16-B records (1 Mi bench step 24.1 vs 21.9 G msg/s).  Field
+  // widths: the mailbox from the state size or the directory, the rest split between the
+  // zigzag arguments; a stateless record that does not fit spills, an ordered one escapes.
+  const bool r8 = (tn.mbox_rec8 == 1 || (tn.mbox_rec8 < 0 && tiles > 512)) && sort_mode == 1 &&
+                  (!a.ordered || !a.a1) && !a.a2 && !a.method_col && mv.planar && !all_sidx;
+  if (r8 && (!r8w_ || r8_tiles_ < (uint64_t)tiles)) {  // (outside a capture: grown with the sort workspace)
+    if (capturing())
       throw std::runtime_error("mailbox send: first 8-B-record Send of this size inside a graph capture (warm up first)");
     PT_HIP_CHECK(hipStreamSynchronize(st));
     if (!r8w_) {
@@ -2121,51 +1696,27 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       *r8host_ = w;
     }
     if (r8max_) PT_HIP_CHECK(hipFree(r8max_));
-    PT_HIP_CHECK(hipMalloc((void**)&r8max_, (size_t)tiles_ws * 4));
-    r8_tiles_ = (uint64_t)tiles_ws;
+    PT_HIP_CHECK(hipMalloc((void**)&r8max_, (size_t)tiles * 4));
+    r8_tiles_ = (uint64_t)tiles;
   }
   // fields that outgrew 64 bits (the last Send's widths, bit 31): 16-B records from here on
   const bool r8_on = r8 && !(__atomic_load_n(r8host_, __ATOMIC_RELAXED) & 0x80000000u);
   last_rec_bytes_ = r8_on ? 8 : ((a.a2 || a.method_col) ? 32 : 16);  // (16: compact unless a value is wide)
+  if (r8_on && a.ordered && !r8esc_) {  // escape side array: {a0, mailbox} per ring slot
+    if (capturing())
+      throw std::runtime_error("mailbox send: first ordered 8-B-record Send inside a graph capture (warm up first)");
+    const uint64_t n = (uint64_t)S * slots();
+    PT_HIP_CHECK(hipMalloc((void**)&r8esc_, n * 16));
+    bytes_ += n * 16;
+  }
   if (r8_on) {
     in.rec8 = 1;
     in.r8w = r8w_;
     in.r8max = r8max_;
+    in.r8esc = r8esc_;
   }
   uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
-  // the LDS-table count (PTYPE_MBOX_SORT=ldscount): directory registry, table <= kStabMax, shards <= 128
-  const bool lds_count = sort_mode == 3 && mode == 1 && a.n_dir <= kStabMax && Sv <= 128;
-  if (lds_count) {
-    if (!sort_stab_) {
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-        throw std::runtime_error("mailbox send: first LDS-count Send inside a graph capture (warm up first)");
-      PT_HIP_CHECK(hipMalloc((void**)&sort_stab_, kStabMax + 16));
-    }
-    hipLaunchKernelGGL(mbx_stab_kernel, dim3((a.n_dir + 1023) / 1024), dim3(256), 0, st, (const uint32_t*)a.dir,
-                       a.n_dir, a.rank_self, mv.log_s, sort_stab_);
-    static bool attr = false;
-    const size_t lds = (size_t)kMboxSortMaxShards * 4 + kStabMax;
-    if (!attr) {
-      PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_count_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds));
-      attr = true;
-    }
-    const uint32_t sub = (in.G + 255) / 256;  // scatter blocks per count block (about one count block per CU)
-    hipLaunchKernelGGL(mbx_count_lds_kernel, dim3((in.G + sub - 1) / sub), dim3(kCT),
-                       (size_t)kMboxSortMaxShards * 4 + a.n_dir, st, in, mv.log_s, (const uint8_t*)sort_stab_, sub,
-                       sort_hist_, sort_gsum_);
-    PT_HIP_CHECK(hipGetLastError());
-#define PT_SCAT(A2, MC)                                                                                           \
-  hipLaunchKernelGGL((mbx_scatter_kernel<A2, MC, 1>), dim3(in.G), dim3(kST), scatter_lds_bytes(Sv), st, in, mv,  \
-                     (const uint32_t*)sort_hist_, (const uint32_t*)sort_gsum_, sort_rw_, sort_sidx_, tinfo, rv,      \
-                     !a.ordered, all_sidx)
-    if (a.a2 && a.method_col) PT_SCAT(true, true);
-    else if (a.a2) PT_SCAT(true, false);
-    else if (a.method_col) PT_SCAT(false, true);
-    else PT_SCAT(false, false);
-#undef PT_SCAT
-  } else if (two_pass) {
+  if (two_pass) {
 #define PT_COUNT(MO) \
   hipLaunchKernelGGL((mbx_count_kernel<MO>), dim3(in.G), dim3(kST), 0, st, in, mv.log_s, sort_hist_, sort_gsum_, sort_rw_)
     if (mode == 2) PT_COUNT(2); else if (mode == 1) PT_COUNT(1); else PT_COUNT(0);
@@ -2180,31 +1731,19 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else if (a.method_col) PT_SCAT(false, true);
     else PT_SCAT(false, false);
 #undef PT_SCAT
-  } else if (!a.ordered && !all_sidx && Sv <= 256 && fused_ok(tiles)) {
-    // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel).  PTYPE_MBOX_SK=2:
-    // 1024-message tiles (4x the blocks, 72-78 instead of 121 VGPRs).  Measured slower at 1 Mi
-    // (round 5: fused kernel 40.2 vs 31.4 us, bench 19.8 vs 22.9 G msg/s): four times the
-    // run reservations on the 8-shard view's counters, so 4096-message tiles stay the default.
-    // PTYPE_MBOX_SK=4: 2048-message tiles (2x the blocks and reservations)
-    static const int sk_env = getenv("PTYPE_MBOX_SK") ? atoi(getenv("PTYPE_MBOX_SK")) : 0;
-    const int fsk = sk_env == kSKSmall || sk_env == 4 ? sk_env : kSK;
-    if (fsk != kSK) in.tiles = (uint32_t)((a.M + kST * fsk - 1) / (kST * fsk));
-    const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv, kST * fsk));
-#define PT_SD4(MO, A2, MC, FX, R8, SKV)                                                                             \
-  hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, R8, SKV>), dim3(in.tiles), dim3(kST), lds, st, in, mv,     \
-                     sort_desc_,                                                                                     \
-                     sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv, (int64_t*)a.state, a.n_state,    \
-                     a.delay_ticks, ob, sort_ticket_, reserve, r8host_)
-#define PT_SD3(MO, A2, MC, FX, R8)                 \
-  do {                                             \
-    if (fsk == kSKSmall) PT_SD4(MO, A2, MC, FX, R8, kSKSmall); \
-    else if (fsk == 4) PT_SD4(MO, A2, MC, FX, R8, 4); \
-    else PT_SD4(MO, A2, MC, FX, R8, kSK);          \
-  } while (0)
-#define PT_SD2(MO, A2, MC, FX)                               \
-  do {                                                       \
-    if (!(A2) && !(MC) && r8_on) PT_SD3(MO, false, false, FX, true); \
-    else PT_SD3(MO, A2, MC, FX, false);                      \
+  } else if (!a.ordered && !all_sidx && fused_ok(tiles)) {
+    // one-pass sort + ring-order drain in ONE launch (mbx_sortdrain_kernel)
+    const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv, kSTile));
+#define PT_SD2(MO, A2, MC, FX)                                                                                    \
+  do {                                                                                                            \
+    if (!(A2) && !(MC) && r8_on)                                                                                  \
+      hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, false, false, FX, true>), dim3(in.tiles), dim3(kST), lds, st, in, \
+                         mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv,              \
+                         (int64_t*)a.state, a.n_state, a.delay_ticks, ob, sort_ticket_, reserve, r8host_);          \
+    else                                                                                                          \
+      hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, false>), dim3(in.tiles), dim3(kST), lds, st, in, mv, \
+                         sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv,                  \
+                         (int64_t*)a.state, a.n_state, a.delay_ticks, ob, sort_ticket_, reserve, r8host_);          \
   } while (0)
 #define PT_SD(MO)                                                            \
   do {                                                                       \
@@ -2224,44 +1763,14 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     } else if (mode == 2) PT_SD(2); else if (mode == 1) PT_SD(1); else PT_SD(0);
 #undef PT_SD
 #undef PT_SD2
-#undef PT_SD3
-#undef PT_SD4
     PT_HIP_CHECK(hipGetLastError());
     return;
   } else {
-    // one block per tile, claimed in launch order (the grid is exactly the tile count).
-    // PTYPE_MBOX_SK=4 (experiment; stateless two-column batches, ring-order drain): 2048-message
-    // tiles for the sort and the drain -- fewer registers per wave, more blocks per CU
-    mid = mid_ok && !late;
-    static const int persist_env = getenv("PTYPE_MBOX_PERSIST") ? atoi(getenv("PTYPE_MBOX_PERSIST")) : 0;
-    const bool persist = persist_env > 0 && reserve && !mid && !late;
-    // blocks: PTYPE_MBOX_PERSIST per CU (256 CUs), a multiple of 8 (one contiguous range per XCD)
-    uint32_t pgrid = (uint32_t)std::min<int64_t>(tiles, (int64_t)256 * std::max(persist_env, 1));
-    if (pgrid >= 8) pgrid -= pgrid % 8;
-    if (mid) {
-      in.tiles = (uint32_t)((a.M + kST * 4 - 1) / (kST * 4));
-      tile_grid = in.tiles >= 8 ? (in.tiles + 7) / 8 * 8 : in.tiles;
-    }
-    // (PTYPE_OS_LATE=1: arguments loaded after the look-back, 87 instead of 115 VGPRs -- measured slower,
-    // 0.231 vs 0.223 ms per 8 Mi Send: the loads' latency is then exposed)
-#define PT_OS3(MO, A2, MC, LT, SKV)                                                                                \
-  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC, LT, SKV>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv),  \
-                     st, in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered,      \
-                     all_sidx, reserve)
-#define PT_OS2(MO, A2, MC, LT)                                     \
-  do {                                                             \
-    if (mid && !(A2) && !(MC) && !(LT)) PT_OS3(MO, false, false, false, 4); \
-    else if (persist && !(A2) && !(MC) && !(LT))                   \
-      hipLaunchKernelGGL((mbx_onesweep_persist_kernel<MO, false, false, kSK>), dim3(pgrid), dim3(kST),            \
-                         onesweep_lds_bytes(Sv), st, in, mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo,   \
-                         sort_rw_, rv, !a.ordered, all_sidx);                                                          \
-    else PT_OS3(MO, A2, MC, LT, kSK);                              \
-  } while (0)
-#define PT_OS1(MO, A2, MC)              \
-  do {                                  \
-    if (late) PT_OS2(MO, A2, MC, true); \
-    else PT_OS2(MO, A2, MC, false);     \
-  } while (0)
+    // one block per tile, claimed in launch order (the grid is exactly the tile count)
+#define PT_OS1(MO, A2, MC)                                                                                        \
+  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv), st, in, \
+                     mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx,  \
+                     reserve)
 #define PT_OS(MO)                                   \
   do {                                              \
     if (a.a2 && a.method_col) PT_OS1(MO, true, true); \
@@ -2269,15 +1778,12 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else if (a.method_col) PT_OS1(MO, false, true); \
     else PT_OS1(MO, false, false);                  \
   } while (0)
-    if (rank_route) PT_OS2(3, false, false, false);
+    if (rank_route) PT_OS1(3, false, false);
     else if (mode == 2) PT_OS(2); else if (mode == 1) PT_OS(1); else PT_OS(0);
 #undef PT_OS
 #undef PT_OS1
-#undef PT_OS2
-#undef PT_OS3
   }
   PT_HIP_CHECK(hipGetLastError());
-  const size_t ring_lds = ring_drain_lds_bytes(Sv);
   if (a.ordered) {
     // state staged per shard: what its actors need (mailboxes s, s + S, ...), not the cap
     const uint32_t n_loc = a.state && a.n_state ? std::min<uint32_t>((a.n_state + Sv - 1) / Sv, kOrdStateMax) : 0;
@@ -2287,6 +1793,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     if (r8_on) {
       r8a.r8w = r8w_;
       r8a.method = (uint32_t)a.method_uniform;
+      r8a.esc = r8esc_;
     }
 #define PT_ORD5(A12, OKV, FXV, PFV, R8V)                                                                      \
   do {                                                                                                        \
@@ -2302,65 +1809,19 @@ void Mailboxes::send_sorted(const MboxSend& a) {
                        st, mv, sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob,          \
                        (u32x4*)stage_rep_, a.origin_base, r8a);                                               \
   } while (0)
-#define PT_ORD4(A12, OKV, FXV, PFV) PT_ORD5(A12, OKV, FXV, PFV, false)
-#define PT_ORD3(A12, OKV, FXV) PT_ORD4(A12, OKV, FXV, false)
-    // one-argument batches: 4096-record windows (PTYPE_ORD_WIN=2048: the 2048-record form;
-    // round 5: 0.375 vs 0.383 ms per 8 Mi SeqFold step), and a uniform SeqFold batch folds
-    // in registers (PTYPE_ORD_FIXED=0: the handler switch)
-    static const bool win8 = !(getenv("PTYPE_ORD_WIN") && atoi(getenv("PTYPE_ORD_WIN")) == 2048);
-    static const bool fixed_ok = !(getenv("PTYPE_ORD_FIXED") && atoi(getenv("PTYPE_ORD_FIXED")) == 0);
-    const bool fold = fixed_ok && a.fixed_method == kSeqFold && !a.method_col;
-    // (the fold with the next window prefetched: 0.341 vs 0.357 ms per 8 Mi SeqFold step, round 5;
-    // PTYPE_ORD_PREFETCH=0 turns it off)
-    static const bool pf = !(getenv("PTYPE_ORD_PREFETCH") && atoi(getenv("PTYPE_ORD_PREFETCH")) == 0);
-#define PT_ORD(A12)                                            \
-  do {                                                         \
-    if (r8_on) { /* (ord_r8: one-argument, 4096-record form) */ \
-      if (fold && pf) PT_ORD5(false, 8, kSeqFold, true, true); \
-      else PT_ORD5(false, 8, 0, false, true);                  \
-    } else if (win8 && !(A12)) {                               \
-      if (fold && pf) PT_ORD4(false, 8, kSeqFold, true);       \
-      else if (fold) PT_ORD3(false, 8, kSeqFold);              \
-      else PT_ORD3(false, 8, 0);                               \
-    } else if (!(A12) && fold) {                               \
-      PT_ORD3(false, kOrdK, kSeqFold);                         \
-    } else {                                                   \
-      PT_ORD3(A12, kOrdK, 0);                                  \
-    }                                                          \
-  } while (0)
-    // the binned form (PTYPE_ORD_DRAIN=bin) measured slower than the windowed one with whole-shard
-    // super-windows (round 5: 233 vs 175 us per 8 Mi SeqFold Send -- its reply stores land all over
-    // the shard's ring); PTYPE_ORD_BIN_ROUNDS sizes its super-window
-    static const bool ord_bin = getenv("PTYPE_ORD_DRAIN") && std::string(getenv("PTYPE_ORD_DRAIN")) == "bin";
-    if (ord_bin) {
-      // the binned form: as many rounds per super-window as the LDS left by the state allows
-      // (the largest dynamic LDS the runtime grants this kernel: its static words and the stats
-      // partials share the CU's 160 KB; found once, stepping down from 156 KB)
-      static size_t cap = 0;
-      if (!cap) {
-        for (size_t c = 156 * 1024; c >= 64 * 1024; c -= 4 * 1024)
-          if (hipFuncSetAttribute((const void*)mbx_drain_ord_bin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)c) == hipSuccess) {
-            cap = c;
-            break;
-          }
-        (void)hipGetLastError();
-        if (!cap) throw std::runtime_error("mailbox send: no LDS for the binned ordered drain");
-      }
-      static const int nr_env = getenv("PTYPE_ORD_BIN_ROUNDS") ? atoi(getenv("PTYPE_ORD_BIN_ROUNDS")) : 0;
-      uint32_t nr = nr_env > 0 ? std::min<uint32_t>((uint32_t)nr_env, kOrdBinRoundsMax) : kOrdBinRoundsMax;
-      while (nr > 1 && ord_bin_lds_bytes(nr, n_loc) > cap) --nr;
-      hipLaunchKernelGGL(mbx_drain_ord_bin_kernel, dim3(Sv), dim3(kOrdThreads), ord_bin_lds_bytes(nr, n_loc), st, mv,
-                         sort_gsum_, ngroups, (int64_t*)a.state, a.n_state, a.delay_ticks, ob, (u32x4*)stage_rep_, nr,
-                         a.origin_base);
-    } else if (a12) {
-      PT_ORD(true);
+    // one-argument batches: 4096-record windows, and a uniform SeqFold batch folds in
+    // registers with the next window prefetched (0.341 vs 0.357 ms per 8 Mi SeqFold step,
+    // round 5); two- and three-argument batches: 2048-record windows, the handler switch
+    const bool fold = a.fixed_method == kSeqFold && !a.method_col;
+    if (r8_on) {  // (one-argument, 4096-record form)
+      if (fold) PT_ORD5(false, 8, kSeqFold, true, true);
+      else PT_ORD5(false, 8, 0, false, true);
+    } else if (!a12) {
+      if (fold) PT_ORD5(false, 8, kSeqFold, true, false);
+      else PT_ORD5(false, 8, 0, false, false);
     } else {
-      PT_ORD(false);
+      PT_ORD5(true, kOrdK, 0, false, false);
     }
-#undef PT_ORD
-#undef PT_ORD3
-#undef PT_ORD4
 #undef PT_ORD5
     if (r8_on)
       hipLaunchKernelGGL(mbx_rec8_next_kernel, dim3(1), dim3(256), 0, st, (const uint32_t*)r8max_, r8w_, r8host_,
@@ -2378,34 +1839,20 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else PT_DMSG(0);
 #undef PT_DMSG
   } else {
-    static const bool narrow_ok = !(getenv("PTYPE_DRAIN_NARROW") && std::string(getenv("PTYPE_DRAIN_NARROW")) == "0");
-#define PT_DRING3(FX, NW, R8, SKV)                                                                               \
-  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, NW, R8, SKV>), dim3(tile_grid), dim3(kST),                         \
-                     NW ? ring_drain_lds_bytes(Sv, (size_t)kST * SKV) : (size_t)kST * SKV * (8 + 2 + 1) + (size_t)Sv * 8, \
+    // the ring-order drain; its LDS stage is sized by the 8-shard view (narrow form)
+#define PT_DRING(FX, R8)                                                                                          \
+  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, true, R8>), dim3(tile_grid), dim3(kST), ring_drain_lds_bytes(Sv, kSTile), \
                      st, mv, in, (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_, \
                      (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_,        \
                      sort_tctr_, r8host_)
-#define PT_DRING2(FX, NW, R8)                      \
-  do {                                             \
-    if (mid && (NW)) PT_DRING3(FX, true, R8, 4);   \
-    else PT_DRING3(FX, NW, R8, kSK);               \
-  } while (0)
-#define PT_DRING1(FX, NW)                     \
-  do {                                        \
-    if (r8_on) PT_DRING2(FX, NW, true);       \
-    else PT_DRING2(FX, NW, false);            \
-  } while (0)
-#define PT_DRING(FX)                                   \
-  do {                                                 \
-    if (narrow_ok && Sv <= 256) PT_DRING1(FX, true);   \
-    else PT_DRING1(FX, false);                         \
-  } while (0)
-    if (fixed_mul) PT_DRING(kCalculatorMultiply);
-    else PT_DRING(0);
+    if (fixed_mul) {
+      if (r8_on) PT_DRING(kCalculatorMultiply, true);
+      else PT_DRING(kCalculatorMultiply, false);
+    } else {
+      if (r8_on) PT_DRING(0, true);
+      else PT_DRING(0, false);
+    }
 #undef PT_DRING
-#undef PT_DRING1
-#undef PT_DRING2
-#undef PT_DRING3
   }
   PT_HIP_CHECK(hipGetLastError());
 }

@@ -267,10 +267,10 @@ __global__ __launch_bounds__(256) void pack_replies_kernel(const uint32_t* __res
 
 // ---- K8 for v3 replies: a gather per message (coalesced outputs); kCompU
 // messages per thread per trip, all perm reads, then all reply reads, in flight
-// (messages per thread per trip: a kernel template argument, PTYPE_COMP_U in {2, 4, 8}; default 4)
+// (4 messages per thread per trip: 2 and 8 measured no faster, nor non-temporal stores)
 constexpr int32_t kPastBatch = INT32_MIN;  // (perm codes: >= 0 slot position, -1 overflow, -2 no actor, -3 direct)
 
-template <int kCompU, bool NT = false>
+template <int kCompU>
 __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
                                                               uint32_t C, int R, int vb,
                                                               const int32_t* __restrict__ perm, int64_t M,
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
 #pragma unroll
     for (int u = 0; u < kCompU; ++u) {
       const int64_t i = i0 + u * stride;
-      p[u] = i < M ? (NT ? __builtin_nontemporal_load(perm + i) : perm[i]) : kPastBatch;
+      p[u] = i < M ? perm[i] : kPastBatch;
     }
     uint64_t code[kCompU];
     unsigned long long okw[kCompU];
@@ -350,13 +350,8 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
       } else {
         st = p[u] == -1 ? kStatusOverflow : kStatusNoActor;
       }
-      if constexpr (NT) {  // (the caller reads them; nothing here re-reads them)
-        __builtin_nontemporal_store(v, out_val + i);
-        __builtin_nontemporal_store(st, out_st + i);
-      } else {
-        out_val[i] = v;
-        out_st[i] = st;
-      }
+      out_val[i] = v;
+      out_st[i] = st;
       sum += (unsigned long long)v;
     }
   }
@@ -406,10 +401,7 @@ void launch_packed_meta(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t a
   hipStream_t s = as_stream(stream);
   PT_HIP_CHECK(hipMemsetAsync((void*)meta, 0, kMetaWords * sizeof(uint64_t), s));
   if (M > 0 && (!a0 || !actor)) throw std::invalid_argument("packed meta: actor and a0 columns required");
-  static const unsigned cap = [] {  // blocks (tuning knob, PTYPE_META_BLOCKS; see tools/meta_bench.py)
-    const char* e = getenv("PTYPE_META_BLOCKS");
-    return e ? (unsigned)atoi(e) : 1024u;  // measured best on MI355X (profiles/r1_meta_sweep.jsonl)
-  }();
+  constexpr unsigned cap = 1024u;  // blocks: measured best on MI355X (profiles/r1_meta_sweep.jsonl)
   hipLaunchKernelGGL(packed_meta_kernel, dim3(grid_for(M, 256 * 8, cap)), dim3(256), 0, s, (const uint32_t*)actor,
                      (const int64_t*)a0, (const int64_t*)a1, (const int64_t*)a2, (const uint16_t*)method_col,
                      (uint32_t)method_uniform, M, n_dir, affine_w, (unsigned long long*)meta);
@@ -443,10 +435,7 @@ void launch_route_packed(uintptr_t actor, uintptr_t a0, uintptr_t a1, uintptr_t 
   const int64_t G = prepped ? route_grid(M, &P)
                             : route_prep(actor, M, table, cap, dir, n_dir, R, route, hist, affine_w, stream, &P);
   route_scan(G, R, C, req_words, sendbuf, hist, method_uniform, stats, rank_self, stream);
-  static const bool scatter_pipe = [] {  // PTYPE_SCATTER_PIPE=0: tiles load-then-place one at a time
-    const char* e = getenv("PTYPE_SCATTER_PIPE");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool scatter_pipe = true;  // (tiles loaded one ahead of their placement)
   if (M > 0) {
 #define PT_SCATTER_P(SV)                                                                                             \
   hipLaunchKernelGGL((route_scatter_packed_kernel<SV>), dim3((unsigned)G), dim3(kRouteThreads), 0, as_stream(stream), \
@@ -477,10 +466,7 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
     ob.cap = outbox_cap;
   }
   const int64_t per = expected_per_rank > 0 ? expected_per_rank : C;
-  static const unsigned target = [] {  // blocks over all sources (PTYPE_DISPATCH_BLOCKS: tuning knob)
-    const char* e = getenv("PTYPE_DISPATCH_BLOCKS");
-    return e ? (unsigned)atoi(e) : 4096u;
-  }();
+  constexpr unsigned target = 4096u;  // blocks over all sources
   const unsigned gx = grid_for(per, 256, (unsigned)(target / R > 0 ? target / R : 1));
   const int64_t req_words = packed_req_words(C, L.S), rep_words = packed_rep_words(C, L.vb);
   const unsigned stage_cap = outbox_cap ? kOutboxStage : 0;  // LDS stage only where handlers can send
@@ -501,25 +487,10 @@ void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t p
   if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
   if (R < 1 || R > kMaxRanks) throw std::invalid_argument("complete: 1 <= R <= 64");
   if (vb != 1 && vb != 2 && vb != 4 && vb != 8) throw std::invalid_argument("complete: vb in {1,2,4,8}");
-  static const int comp_u = getenv("PTYPE_COMP_U") ? atoi(getenv("PTYPE_COMP_U")) : 4;
-  static const bool comp_nt = getenv("PTYPE_COMP_NT") && atoi(getenv("PTYPE_COMP_NT")) == 1;  // (experiment)
-  if (comp_nt && comp_u == 4) {
-    hipLaunchKernelGGL((complete_packed_kernel<4, true>), dim3(grid_for(M, 256 * 4, checksum ? 1024 : 8192)),
-                       dim3(256), 0, as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R,
-                       vb, (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st,
-                       (unsigned long long*)checksum, direct, (const uint64_t*)failed, (uint64_t*)zero, zero_words);
-    PT_HIP_CHECK(hipGetLastError());
-    return;
-  }
-#define PT_COMP(U)                                                                                                 \
-  hipLaunchKernelGGL(complete_packed_kernel<U>, dim3(grid_for(M, 256 * (U), checksum ? 1024 : 8192)), dim3(256), 0, \
-                     as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R, vb,          \
-                     (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum,   \
-                     direct, (const uint64_t*)failed, (uint64_t*)zero, zero_words)
-  if (comp_u == 8) PT_COMP(8);
-  else if (comp_u == 2) PT_COMP(2);
-  else PT_COMP(4);
-#undef PT_COMP
+  hipLaunchKernelGGL(complete_packed_kernel<4>, dim3(grid_for(M, 256 * 4, checksum ? 1024 : 8192)), dim3(256), 0,
+                     as_stream(stream), (const uint32_t*)rep, packed_rep_words(C, vb), (uint32_t)C, R, vb,
+                     (const int32_t*)perm, M, (int64_t*)out_val, (int32_t*)out_st, (unsigned long long*)checksum,
+                     direct, (const uint64_t*)failed, (uint64_t*)zero, zero_words);
   PT_HIP_CHECK(hipGetLastError());
 }
 void launch_pack_replies(uintptr_t v2, int R, int64_t C, uintptr_t reply, int vb, uintptr_t stats,

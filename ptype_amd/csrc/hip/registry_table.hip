@@ -272,14 +272,13 @@ __global__ __launch_bounds__(256) void table_build_dir_kernel(const TableEntry* 
   }
 }
 
-// Blocks of the upsert / delete passes (PTYPE_TABLE_BLOCKS: tuning knob): each
+// Blocks of the upsert / delete passes: each
 // block publishes its counters with one same-address atomic, and those serialise
 // at L2.  1M-actor inserts: 4096 blocks 5.7-5.9 G/s, 1024 7.5, 512 8.5, 256 7.9
 // (profiles/r2_table_grid_sweep.txt).  (Skipping the max atomic behind an
 // agent-scope read made it worse: 3.0 G/s at 4096.)
 static unsigned table_blocks() {
-  static const unsigned b = getenv("PTYPE_TABLE_BLOCKS") ? (unsigned)atoi(getenv("PTYPE_TABLE_BLOCKS")) : 512u;
-  return b ? b : 512u;
+  return 512u;
 }
 
 static inline unsigned grid_for(int64_t n, int per_block = 256, unsigned cap = 4096) {

@@ -37,6 +37,7 @@
 #include <immintrin.h>
 
 #include "common.hpp"
+#include "tune.hpp"
 #include "handlers.hpp"
 #include "ringproto.hpp"
 #include "shmring.hpp"
@@ -65,7 +66,7 @@ inline bool open_to_cpu(const void* p) {
   if (!cpu.handle) return false;
   const hsa_status_t st = hsa_amd_agents_allow_access(1, &cpu, nullptr, p);
   if (st != HSA_STATUS_SUCCESS) {
-    if (getenv("PTYPE_RING_DEBUG")) fprintf(stderr, "ptype: hsa_amd_agents_allow_access -> %d\n", (int)st);
+    if (getenv("PTYPE_DEBUG")) fprintf(stderr, "ptype: hsa_amd_agents_allow_access -> %d\n", (int)st);
     return false;
   }
   // (the pointer's accessible-agent list does not name the CPU for device
@@ -75,7 +76,7 @@ inline bool open_to_cpu(const void* p) {
 }
 
 inline bool cpu_can_access(const void* p) {
-  const bool dbg = getenv("PTYPE_RING_DEBUG") != nullptr;
+  const bool dbg = getenv("PTYPE_DEBUG") != nullptr;
   hsa_amd_pointer_info_t info{};
   info.size = sizeof(info);
   uint32_t n = 0;
@@ -112,7 +113,7 @@ __device__ __forceinline__ void sys_st16(uint64_t* p, uint64_t lo, uint64_t hi) 
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
 }
 
-// How the wave polls the ring (tuning knobs, PTYPE_POLL_{LANES,FULL,SLEEP}):
+// How the wave polls the ring (tune poll_lanes / poll_full / poll_sleep, tune.hpp):
 // slots whose tag is read per trip (= most requests taken per batch), whether the
 // head slot's message is read in the same trip (checksum-validated), and how
 // many s_sleep(1) pauses separate empty polls.  Measured on MI355X
@@ -551,10 +552,8 @@ class DeviceServer {
       // instead of crossing PCIe (tools/ring_latency_probe.hip: ping-pong floor
       // 2.14 vs 2.38 us, and a call's payload read is a second round trip).
       // Replies and the control block (host-polled; CAS hand-off) stay in host
-      // memory.  PTYPE_RING_MEM=host, or a device the CPU cannot map, keeps the
-      // ring in pinned host memory.
-      const char* rm = getenv("PTYPE_RING_MEM");
-      if (!(rm && std::string(rm) == "host")) {
+      // memory.  A device the CPU cannot map keeps the ring in pinned host memory.
+      {
         if (hipExtMallocWithFlags((void**)&req_, sizeof(RingSlot) * ring_, hipDeviceMallocFinegrained) == hipSuccess) {
           if (open_to_cpu(req_)) {
             req_on_device_ = true;
@@ -563,7 +562,7 @@ class DeviceServer {
             req_ = nullptr;
           }
         } else {
-          if (getenv("PTYPE_RING_DEBUG")) fprintf(stderr, "ptype: fine-grained device ring allocation failed\n");
+          if (getenv("PTYPE_DEBUG")) fprintf(stderr, "ptype: fine-grained device ring allocation failed\n");
           (void)hipGetLastError();
           req_ = nullptr;
         }
@@ -826,7 +825,7 @@ class DeviceServer {
     const size_t bytes = sizeof(RingSlot) * ring_;
     RingSlot* d = nullptr;
     const auto dbg = [](const char* what, int st) {
-      if (getenv("PTYPE_RING_DEBUG")) fprintf(stderr, "ptype: device ring export: %s -> %d\n", what, st);
+      if (getenv("PTYPE_DEBUG")) fprintf(stderr, "ptype: device ring export: %s -> %d\n", what, st);
     };
     if (hipExtMallocWithFlags((void**)&d, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
       (void)hipGetLastError();
@@ -881,7 +880,6 @@ class DeviceServer {
   // ---- GPU peer lanes (shmring.hpp): the segment's XLane / XReply areas, which
   // this process registered with HIP along with the rest of the segment
   void export_xlanes() {
-    if (getenv("PTYPE_XLANES") && std::string(getenv("PTYPE_XLANES")) == "0") return;
     const ShmView v = shm_view(seg_->base(), ring_);
     hxl_ = v.xl;
     hxrep_ = v.xrep;
@@ -987,13 +985,11 @@ class DeviceServer {
   uint64_t delay_ticks_ = 0, idle_ticks_ = 0, max_ticks_ = 0;
   PollConfig poll_ = [] {
     PollConfig p;
-    auto env = [](const char* k, uint32_t d) {
-      const char* v = getenv(k);
-      return v ? (uint32_t)atoi(v) : d;
-    };
-    p.lanes = std::min<uint32_t>(64, std::max<uint32_t>(1, env("PTYPE_POLL_LANES", p.lanes)));
-    p.full = env("PTYPE_POLL_FULL", p.full);
-    p.sleep = env("PTYPE_POLL_SLEEP", p.sleep);
+    const Tune t = tune();
+    auto pick = [](int v, uint32_t d) { return v >= 0 ? (uint32_t)v : d; };
+    p.lanes = std::min<uint32_t>(64, std::max<uint32_t>(1, pick(t.poll_lanes, p.lanes)));
+    p.full = pick(t.poll_full, p.full);
+    p.sleep = pick(t.poll_sleep, p.sleep);
     return p;
   }();
   RingSlot* req_ = nullptr;

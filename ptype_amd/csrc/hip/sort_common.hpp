@@ -15,21 +15,12 @@ namespace ptype {
 // gives each shard a run of ~16 records (256 B, two whole lines) instead of ~8
 // -- half-written lines evicted from L2 before their other half arrived made
 // the 2048-message tiles write 1.9x the record bytes (PMC, r3).
-#ifndef PTYPE_SORT_THREADS
-#define PTYPE_SORT_THREADS 512
-#endif
-constexpr int kST = PTYPE_SORT_THREADS;  // count / scatter threads per block
+constexpr int kST = 512;                 // count / scatter threads per block
 constexpr int kSK = 8;                   // messages per thread per tile
 constexpr int kSTile = kST * kSK;        // 4096 messages
 constexpr int kSWave = kSK * kWave;  // a wave's contiguous run of a tile (512)
 
 
-// The route directory gather: one 4-B word per message from a table that lives
-// in L2 / MALL, at random -- each lane a different line.  `nt` (PTYPE_DIR_NT=1)
-// loads it non-temporal (experiment: the TA stalls on TCP for these gathers).
-__device__ __forceinline__ uint32_t dir_load(const uint32_t* p, bool nt) {
-  return nt ? __builtin_nontemporal_load(p) : *p;
-}
 
 struct SortIn {  // by value
   const uint32_t* actor;
@@ -51,14 +42,16 @@ struct SortIn {  // by value
   uint32_t G;      // blocks
   uint32_t tiles;  // ceil(M / kSTile)
   uint32_t tpb;    // tiles per block
-  bool dir_nt;       // non-temporal directory gathers (experiment)
-  bool lb_group;     // one-pass sorts: group look-back (W lanes per shard) where the shard count allows
   // 8-B ring records (stateless mailbox Sends, mailbox_sort.hip): nonzero = on; the field widths
   // (mailbox bits | a0 bits << 8 | a1 bits << 16, zigzag arguments) are the device word *r8w,
   // set by the previous Send's last block from its per-tile field maxima (r8max)
   uint32_t rec8;
   const uint32_t* r8w;
   uint32_t* r8max;
+  // ordered 8-B records: a message whose fields do not fit keeps its ring slot as an
+  // ESCAPE record (bit 63 set, place in the tile kept) and its {a0, mailbox} go here,
+  // indexed by ring slot -- so the ring stays each actor's FIFO (no overflow, no hole)
+  int64_t* r8esc;
 };
 
 // Block b's range: XCD (b % 8) owns virtual blocks [x * G/8, (x+1) * G/8).
@@ -89,7 +82,7 @@ __device__ __forceinline__ void resolve_k(const SortIn& in, const uint32_t (&a)[
   } else if constexpr (MODE == 1) {
     uint32_t w[SK];
 #pragma unroll
-    for (int k = 0; k < SK; ++k) w[k] = a[k] < in.n_dir ? dir_load(in.dir + a[k], in.dir_nt) : kDirFallback;
+    for (int k = 0; k < SK; ++k) w[k] = a[k] < in.n_dir ? in.dir[a[k]] : kDirFallback;
 #pragma unroll
     for (int k = 0; k < SK; ++k) {
       r[k] = w[k] == kDirMissing ? -1 : (int)(w[k] & 0xff);
@@ -215,45 +208,6 @@ __device__ __forceinline__ uint64_t lookback(unsigned long long* col, uint32_t s
     if (stall) {
       if (++spins > kLookbackSpins) {
         ++timeouts;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  return excl;
-}
-// The same sum with W lanes per column (W = 8, 16, 32 or 64; lane groups aligned
-// inside a wave, all lanes of a group call it together): lane j of the group
-// reads tile q - j, so one round trip covers W predecessors instead of kLbWin.
-// The one-pass mailbox sort runs 16 columns (the stateless view) on its 512
-// threads: 32 lanes each.  Every lane of the group returns the group's sum.
-__device__ __forceinline__ uint64_t lookback_group(unsigned long long* col, uint32_t stride, int64_t q, uint32_t tag,
-                                                   uint32_t W, unsigned long long& timeouts) {
-  const uint32_t lane = lane_id(), j = lane & (W - 1), gbase = lane & ~(W - 1);
-  const uint64_t full = W >= 64 ? ~0ull : (1ull << W) - 1;
-  uint64_t excl = 0;
-  uint32_t spins = 0;
-  for (;;) {
-    const int64_t qq = q - (int64_t)j;
-    const uint64_t x = qq >= 0 ? __hip_atomic_fetch_add(col + (size_t)qq * stride, 0ull, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                               : desc_word(tag, kDescP, 0);  // before tile 0: 0
-    const bool pub = (uint32_t)(x >> 40) == tag;
-    const uint64_t pubm = (__ballot(pub) >> gbase) & full;
-    const uint64_t pm = (__ballot(pub && (x & kDescP)) >> gbase) & full;
-    const uint64_t unpub = ~pubm & full;
-    const uint32_t first_unpub = unpub ? (uint32_t)__builtin_ctzll(unpub) : W;
-    const uint32_t first_p = pm ? (uint32_t)__builtin_ctzll(pm) : W;
-    const bool fin = first_p < first_unpub;
-    const uint32_t n = fin ? first_p + 1 : first_unpub;  // entries summed this round
-    uint64_t v = j < n ? (x & kDescVal) : 0ull;
-    for (uint32_t off = W >> 1; off > 0; off >>= 1) v += __shfl_xor(v, (int)off);
-    excl += v;
-    if (fin) break;
-    q -= (int64_t)n;
-    if (n < W) {  // an unpublished predecessor: poll it again
-      if (++spins > kLookbackSpins) {
-        if (j == 0) ++timeouts;
         break;
       }
       __builtin_amdgcn_s_sleep(1);

@@ -36,7 +36,7 @@ STAT_NAMES = ("enqueued", "overflow", "no_actor", "processed", "failed", "holes"
 SORT_MAX_SHARDS = 1024  # csrc/hip/mailbox.hpp kMboxSortMaxShards
 
 
-SORT_MODES = {"auto": 0, "onepass": 1, "twopass": 2, "ldscount": 3}
+SORT_MODES = {"auto": 0, "onepass": 1, "twopass": 2}
 
 
 def batch_ordered(batch: MsgBatch) -> bool:
@@ -122,8 +122,8 @@ class Mailboxes:
         ring order; otherwise every record runs in parallel.  ``sort`` (default on):
         the sorted epoch kernels (csrc/hip/mailbox_sort.hip: counting-sort enqueue,
         16-B records); off: the tagged reservation kernels of mailbox.hip.
-        ``sort_mode`` (actor sharding): ``"auto"``, ``"onepass"`` (look-back sort),
-        ``"twopass"`` (count + scatter) or ``"ldscount"`` (LDS-table count)."""
+        ``sort_mode`` (actor sharding): ``"auto"``, ``"onepass"`` (run reservations for
+        stateless batches, look-back for ordered ones) or ``"twopass"`` (count + scatter)."""
         M = batch.M
         out_val = torch.empty(M, dtype=torch.int64, device=self.device) if out_val is None else out_val
         out_status = torch.empty(M, dtype=torch.int32, device=self.device) if out_status is None else out_status

@@ -38,13 +38,12 @@ process group's own RCCL communicator and orders the streams with events, so
 the host cost of a step no longer grows by ~100 us of Python per chunk (which
 made multi-GPU steps host-bound).  The Python pipeline below is the same
 schedule over ``torch.distributed`` and serves CPU/gloo groups, and
-``PTYPE_ENGINE=0`` selects it on a GPU for comparison.
+tune ``engine=0`` (ops/tune.py) selects it on a GPU for comparison.
 """
 from __future__ import annotations
 
 import collections
 import math
-import os
 import threading
 from dataclasses import dataclass
 
@@ -52,7 +51,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import batch as B
-from ..ops import raw_stream
+from ..ops import raw_stream, tune
 from ..ops.packed import META_CAP, META_WORDS
 from ..ops.records import STATUS_OVERFLOW, method_ordered
 from ..ops.table import RegistryTable
@@ -174,21 +173,21 @@ class ActorExchange:
         self.state = state
         self.delay_us = delay_us
         self.fmt = fmt  # None: derived per send() from the batch's columns
-        self.use_engine = self.device.type == "cuda" and os.environ.get("PTYPE_ENGINE", "1") != "0"
+        self.use_engine = self.device.type == "cuda" and tune.get("engine") != 0
         # wire format v3 (csrc/hip/packed.hpp): width-adaptive packed records on the
         # all-to-alls, agreed per Send by one 16-word all-reduce (native engine, collectives on)
-        self.packed = os.environ.get("PTYPE_WIRE", "v3") != "v2" if packed is None else bool(packed)
+        self.packed = tune.get("wire") != 2 if packed is None else bool(packed)
         # Adaptive slot capacity (native engine + wire v3): every Send's slots are sized
         # by the node's busiest (rank, destination) bucket, agreed in the layout
         # all-reduce; the buffers hold `skew_room` x the uniform share per peer, so
         # skewed (Zipf) traffic fits without re-send rounds and uniform traffic moves
         # less padding than the static mean + 8 sigma capacity
-        # (PTYPE_ADAPTIVE_C=force: also at world 1 with forced collectives -- runs the
+        # (tune adaptive_c=2: also at world 1 with forced collectives -- runs the
         # counts all-to-all and the grouped ncclSend / ncclRecv on a 1-GPU box)
-        ad = os.environ.get("PTYPE_ADAPTIVE_C", "1")
-        self.adaptive = bool(self.use_engine and self.packed and self.chunks <= 8 and ad != "0"
-                             and (self.world > 1 or (ad == "force" and self.force_collectives)))
-        room = float(os.environ.get("PTYPE_SKEW_ROOM", "4"))
+        ad = tune.get("adaptive_c")
+        self.adaptive = bool(self.use_engine and self.packed and self.chunks <= 8 and ad != 0
+                             and (self.world > 1 or (ad == 2 and self.force_collectives)))
+        room = tune.get("skew_room")
         self.C_alloc = (max(self.C, min(self.max_chunk, int(math.ceil(room * self.max_chunk / self.world))))
                         if self.adaptive else self.C)
         self.bufs = [_ChunkBufs(self.world, self.C_alloc, self.max_chunk, self.device, self.force_collectives,
@@ -207,9 +206,9 @@ class ActorExchange:
         # anyway, and the own slot's replies written from the dispatcher land
         # scattered (message index through the inverse index, ~R messages apart)
         # -- the completion's gather writes them coalesced instead (bench
-        # --loopback 8: 0.360 -> 0.337 ms/step).  PTYPE_DIRECT=0/1 overrides.
-        d = os.environ.get("PTYPE_DIRECT")
-        self.direct = (d != "0") if d is not None else (self.world == 1)
+        # --loopback 8: 0.360 -> 0.337 ms/step).  Tune direct=0/1 overrides.
+        d = tune.get("direct")
+        self.direct = (d != 0) if d >= 0 else (self.world == 1)
         self.counters = EpochStats()
         self._engine = None  # native epoch engine, built on first GPU send
         self._capturing = False  # a captured graph cannot host the v3 agreement (host wait)
@@ -233,7 +232,7 @@ class ActorExchange:
     def _sorted_c_alloc(self) -> int:
         # the sorted exchange's buffers hold 2.5x the uniform share per peer (skewed
         # traffic fits); the start-up capacity is the static mean + 8 sigma
-        room = float(os.environ.get("PTYPE_SORTED_ROOM", "2.5"))
+        room = tune.get("sorted_room")
         return max(64, self.C, min(self.max_chunk, int(math.ceil(room * self.max_chunk / self.world))))
 
     def ipc_cap_bytes(self) -> int:
@@ -322,7 +321,7 @@ class ActorExchange:
         It is the N > 1 path of delivery "mailbox" and of "auto" (Join's default:
         ordered methods keep per-(sender, actor) FIFO through its ordered drain,
         stateless ones run in parallel) -- "direct" keeps the epoch engine's fused
-        dispatch.  PTYPE_SORTED_EXCHANGE=0 keeps the epoch engine everywhere."""
+        dispatch.  Tune sorted_exchange=0 keeps the epoch engine everywhere."""
         if self.delivery == "direct" or not self.use_engine or self.device.type != "cuda":
             return False
         if self.delivery == "auto" and self.world == 1:  # world 1: the fused local pass / world-1 mailboxes
@@ -331,7 +330,7 @@ class ActorExchange:
             return False
         if not (1 < self.world <= 16 or self.force_collectives):
             return False
-        return os.environ.get("PTYPE_SORTED_EXCHANGE", "1") != "0"
+        return tune.get("sorted_exchange") != 0
 
     def _get_sorted(self):
         if self._sorted is None:
@@ -420,7 +419,7 @@ class ActorExchange:
         ``(value int64[M], status int32[M])`` in message order.  Collective:
         every rank of the group must call it (with its own, possibly empty, batch)
         the same number of times."""
-        if self._deferred:  # a deferred Send two Sends old: its agreement buffer is reused by this one
+        if self._deferred and not self._capturing:  # a deferred Send two Sends old: its agreement buffer is reused
             self._resolve_deferred(final=False)
         M = req.M
         if M > self.max_chunk * self.chunks:
@@ -574,7 +573,7 @@ class ActorExchange:
         an outbox whose banks fit one Send."""
         return bool(self.use_engine and self.world == 1 and not self.force_collectives and self.direct
                     and self.delivery != "mailbox" and outbox.cap <= self.max_chunk * self.chunks
-                    and os.environ.get("PTYPE_DEVICE_PUMP", "1") != "0" and os.environ.get("PTYPE_LOCAL", "1") != "0")
+                    and tune.get("device_pump") != 0 and B.hip().tune()["local"] != 0)
 
     def _device_pump_multi_ok(self, outbox) -> bool:
         """Several ranks (RCCL, or FakeComm in-process ranks) on the native engine
@@ -583,7 +582,7 @@ class ActorExchange:
         return bool(self.use_engine and self.device.type == "cuda" and (self.world > 1 or self.force_collectives)
                     and (self.fake is None or not self.fake[0].loopback)
                     and outbox.cap <= self.max_chunk * self.chunks and self.C >= outbox.cap
-                    and os.environ.get("PTYPE_DEVICE_PUMP", "1") != "0")
+                    and tune.get("device_pump") != 0)
 
     def _pump_device_multi(self, outbox, max_epochs: int, check_every: int):
         """Multi-rank pump without a host round trip per epoch.
@@ -722,7 +721,7 @@ class ActorExchange:
             host[h, k:].copy_(start_count[:1], non_blocking=True)  # what is left to pump
             ev[h].record()
 
-        use_graphs = os.environ.get("PTYPE_PUMP_GRAPH", "1") != "0"
+        use_graphs = tune.get("pump_graph") != 0
         epochs = delivered = 0
         launch(0)
         launched, h = k, 1
@@ -770,15 +769,36 @@ class ActorExchange:
         val, st = self.send(req, *(out or ()))
         if self._fits_for_sure():
             return val, st
-        if defer and self._last_sorted and out is None:
+        if defer and self._last_sorted and out is None and not self._keeps_fifo(req):
             self._deferred.append((self._sorted.sends - 1, req, val, st, max_epochs))
             return val, st
         return self._resend_rounds(req, val, st, max_epochs, None)
+
+    def _keeps_fifo(self, req: B.MsgBatch) -> bool:
+        """Whether ``req``'s overflow must be re-sent before the next Send: a batch
+        that may carry an ordered method on actor-sharded delivery keeps per-(sender,
+        actor) FIFO, so its overflowed suffix runs before any later Send's messages
+        to the same actors (a deferred re-send ran them after Send k + 1's).
+        The reference's Call completes before its caller's next one (rpc.go:59-67)."""
+        from ..ops.mailbox import batch_ordered
+
+        return self.mailbox_ordered and batch_ordered(req)
 
     def flush(self) -> None:
         """Resolve every deferred Send (``send_all(defer=True)``): afterwards all
         their outputs are final.  Collective (re-send rounds may run)."""
         self._resolve_deferred(final=True)
+
+    def pending(self) -> int:
+        """Deferred Sends whose overflow is not resolved yet (``flush`` resolves them)."""
+        return len(self._deferred)
+
+    def drop_pending(self) -> int:
+        """Forget deferred Sends without re-sending (their generation failed: the
+        caller re-sends whole batches).  Returns how many were dropped."""
+        n = len(self._deferred)
+        self._deferred.clear()
+        return n
 
     def _resolve_deferred(self, final: bool) -> None:
         # Send k is resolved just before Send k + 2 (its agreement buffer is reused

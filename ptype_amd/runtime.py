@@ -458,6 +458,11 @@ class DeviceRuntime:
         if m is None:
             raise RuntimeError("recover(): this runtime's group was not formed by Join")
         self._abort_generation()
+        if self._exchange is not None and self._exchange.pending():
+            # (elastic Sends never defer; a deferred Send of the failed generation keeps
+            # STATUS_OVERFLOW on its pending messages -- say so instead of dropping it silently)
+            _log.warning("recover: %d deferred Send(s) of generation %d left unresolved (STATUS_OVERFLOW)",
+                         self._exchange.drop_pending(), m["gen"])
         self._exchange = None
         if self._watchdog is not None:
             self._watchdog.reset()
@@ -706,6 +711,13 @@ class DeviceRuntime:
         if self._closed:
             return
         self._closed = True
+        if self._exchange is not None and self._exchange.pending():
+            # deferred re-sends (world > 1) resolve before the group goes away (collective:
+            # every rank closes); a failure here is reported, the teardown goes on
+            try:
+                self._exchange.flush()
+            except Exception as e:  # noqa: BLE001
+                _log.warning("close: deferred re-sends not resolved: %s", str(e)[:300])
         if self._watchdog is not None:
             self._watchdog.close()
         for lease in getattr(self, "_replica_leases", {}).values():

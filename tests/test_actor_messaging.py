@@ -93,8 +93,8 @@ def test_token_ring_on_device(pump, monkeypatch):
     device counter (one host check per 8 epochs; groups after the first replayed
     from a hipGraph, or launched one by one); ``host``: the host reads every
     epoch's count."""
-    monkeypatch.setenv("PTYPE_DEVICE_PUMP", "0" if pump == "host" else "1")
-    monkeypatch.setenv("PTYPE_PUMP_GRAPH", "1" if pump == "graph" else "0")
+    monkeypatch.setenv("PTYPE_TUNE", "device_pump=" + ("0" if pump == "host" else "1") + ",pump_graph="
+                       + ("1" if pump == "graph" else "0"))
     n_per, T, hops, stride = 100_000, 50_000, 20, 7919
     ex, state, starts, epochs, delivered, outbox, n = _ring("cuda", 1, 0, n_per, T, hops, stride)
     torch.cuda.synchronize()

@@ -32,7 +32,7 @@ def test_gpu_engine_matches_python_pipeline(chunks, affine, mixed, local, monkey
     epoch-slot pipeline -- both against the Python slot pipeline."""
     from ptype_amd.parallel.exchange import ActorExchange
 
-    monkeypatch.setenv("PTYPE_LOCAL", local)  # read when the engine is built
+    monkeypatch.setenv("PTYPE_TUNE", f"local={local}")  # read when the engine is built
 
     n, M = 3000, 250_001
     gen = torch.Generator().manual_seed(chunks)

@@ -115,7 +115,7 @@ def test_gpu_engine_loopback(R, chunks, sync, link, monkeypatch):
     with either cross-stream hand-off form and with the modelled link delay."""
     from ptype_amd.parallel.exchange import ActorExchange
 
-    monkeypatch.setenv("PTYPE_STREAM_SYNC", sync)
+    monkeypatch.setenv("PTYPE_TUNE", "stream_sync=" + ("1" if sync == "values" else "0"))
     n, M = 4096 * R, 300_000
     tab = RegistryTable(2 * n, device="cuda")
     ids = torch.arange(n)
@@ -141,7 +141,7 @@ def test_gpu_engine_zipf_skew_no_resend(adaptive, monkeypatch):
     overflows and needs send_all's rounds."""
     from ptype_amd.parallel.exchange import ActorExchange
 
-    monkeypatch.setenv("PTYPE_ADAPTIVE_C", "1" if adaptive else "0")
+    monkeypatch.setenv("PTYPE_TUNE", "adaptive_c=" + ("1" if adaptive else "0"))
     R, n, M = 8, 1 << 15, 200_000
     fc = hip().FakeComm(R)
     out, errors = [None] * R, []

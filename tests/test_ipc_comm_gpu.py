@@ -67,6 +67,15 @@ def test_sorted_exchange_across_processes_seqfold_exactly_once_fifo(R):
     assert out["messages"] == R * 3 * 50_000 and out["actors"] > 0
 
 
+@pytest.mark.parametrize("R", [2, 3])
+def test_ordered_sends_keep_fifo_across_deferred_resends(R):
+    out = _launch("sorted_fold_defer", R)
+    print("fold_defer", out)
+    assert out["messages"] == R * 7 * 60_000 and out["actors"] > 0
+    # re-send rounds ran (skewed start-up capacity, the wide Send), more than one in total
+    assert sum(sum(r) for r in out["rounds"]) > 1, out
+
+
 def test_deferred_resend_has_no_host_wait_on_the_current_send():
     out = _launch("sorted_defer", 2)
     print("defer", out)

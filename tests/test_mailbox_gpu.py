@@ -238,7 +238,7 @@ def test_mailbox_delivery_on_receipt_multirank(R, ordered, packed, monkeypatch):
     from ptype_amd.ops import hip
 
     # the epoch engine's delivery on receipt (the sorted exchange is tested in test_sorted_exchange_gpu.py)
-    monkeypatch.setenv("PTYPE_SORTED_EXCHANGE", "0")
+    monkeypatch.setenv("PTYPE_TUNE", "sorted_exchange=0")
     n, M = 4096, 60_000
     fc = hip().FakeComm(R)
     res, errors = [None] * R, []
@@ -481,8 +481,8 @@ def test_sorted_mailbox_8b_records_spill_what_does_not_fit(fused):
         assert s["overflow"] == 0 and s["spilled"] > 0 and s["processed"] == 3 * M, s
         print("OK", s["spilled"])
     ''')
-    # (PTYPE_MBOX_REC8=1: this batch size would take 16-B records by default)
-    env = dict(os.environ, PTYPE_MBOX_FUSED=fused, PTYPE_MBOX_REC8="1",
+    # (mbox_rec8=1: this batch size would take 16-B records by default)
+    env = dict(os.environ, PTYPE_TUNE=f"mbox_fused={fused},mbox_rec8=1",
                PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "tests")]))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
@@ -566,10 +566,10 @@ def test_live_mailbox_sustained_overload_keeps_consumer_rate():
 
 
 # ---------------------------------------------------------------- sort kernels (mailbox_sort.hip)
-@pytest.mark.parametrize("sort_mode", ["onepass", "twopass", "ldscount"])
+@pytest.mark.parametrize("sort_mode", ["onepass", "twopass"])
 @pytest.mark.parametrize("M", [5000, (1 << 20) + 333])
 def test_sorted_mailbox_sort_modes_exact(sort_mode, M):
-    """Every sort kernel (one-pass look-back, count + scatter, LDS-table count)
+    """Every sort kernel (one pass, count + scatter)
     fills the same per-actor rings: exact replies, misses answered, rings
     consumed, no look-back timeout -- over Sends that reuse the rings."""
     n = 1 << 15
@@ -684,30 +684,36 @@ _ORD_REC8 = textwrap.dedent("""
     for rnd in range(3):
         g = torch.Generator().manual_seed(100 + rnd)
         actor = torch.randint(0, n, (M,), generator=g, dtype=torch.int32)
-        # 16-bit arguments (8-B records), then one argument wider than the widths in force:
-        # it overflows and send_all re-sends it (in whatever records the next Send takes)
+        # 16-bit arguments (8-B records), then arguments wider than the widths in force
+        # (and later messages to the same actors): escape records keep their ring slots,
+        # so nothing overflows and every actor still runs its messages in message order
         a0 = torch.randint(-30000, 30000, (M,), generator=g, dtype=torch.int64)
         if rnd == 2:
             a0[12345] = 1 << 40
+            a0[200000:200064] = -(1 << 50)
         b = B.MsgBatch(actor.to(dev), a0.to(dev), None, None, METHOD_SEQ_FOLD)
         s0 = state.cpu().clone()
+        r0 = ex.counters.resends
         v, st = ex.send_all(b)
         torch.cuda.synchronize()
         s1 = state.cpu().clone()
         ok, info = audit_fold(perm[actor.long()], a0, v.cpu(), st.cpu(), s0, s1)
-        out[rnd] = {"ok": bool(ok), "all_ok": bool((st == STATUS_OK).all()),
+        fifo = bool(ok) and all(seq == sorted(seq) for seq in info.values())
+        out[rnd] = {"ok": bool(ok), "all_ok": bool((st == STATUS_OK).all()), "fifo": fifo,
+                    "resends": int(ex.counters.resends - r0),
                     "rec_bytes": int(ex.mailboxes.last_record_bytes), "info": "" if ok else str(info)[:300]}
     print("RESULT " + json.dumps(out), flush=True)
 """)
 
 
 def test_mailbox_seqfold_in_8b_records_exactly_once_fifo():
-    """Ordered Sends in 8-B records (PTYPE_ORD_REC8=1): each message's place in its
-    tile rides through the ordered drain's reply stage, a message whose argument
-    outgrows the widths in force takes no ring position (no hole the drain could
-    read) and is re-sent -- every actor's replies still chain exactly once, in
-    FIFO order, over three Sends."""
-    env = dict(os.environ, PTYPE_ROOT=ROOT, PTYPE_ORD_REC8="1")
+    """Ordered Sends in 8-B records: each message's place in its tile rides through
+    the ordered drain's reply stage, and a message whose argument outgrows the
+    widths in force keeps its ring slot as an escape record (its fields in a side
+    array) -- ADVICE r5: it used to overflow and be re-sent AFTER later messages of
+    its actor had run.  Every actor's replies chain exactly once and in MESSAGE
+    order (the audit's order checked against the indices), with no re-send round."""
+    env = dict(os.environ, PTYPE_ROOT=ROOT)
     r = subprocess.run([sys.executable, "-c", _ORD_REC8], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
@@ -716,5 +722,6 @@ def test_mailbox_seqfold_in_8b_records_exactly_once_fifo():
 
     out = json.loads(line[0][7:])
     for rnd, o in out.items():
-        assert o["ok"] and o["all_ok"], (rnd, o)
-    assert out["0"]["rec_bytes"] == 8, out  # the ordered Send really took 8-B records
+        assert o["ok"] and o["all_ok"] and o["fifo"], (rnd, o)
+        assert o["resends"] == 0, (rnd, o)  # escapes: no message of an ordered Send overflows
+    assert out["0"]["rec_bytes"] == 8 and out["2"]["rec_bytes"] == 8, out  # the ordered Sends really took 8-B records

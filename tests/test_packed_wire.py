@@ -319,7 +319,7 @@ def test_gpu_engine_packed_rccl_world1(adaptive):
     capacity at world 1, so the exact-size exchange runs on real RCCL -- the
     counts all-to-all and the grouped ncclSend / ncclRecv (to self)."""
     env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1",
-               MASTER_PORT="29563" if adaptive == "1" else "29564", PTYPE_ADAPTIVE_C=adaptive)
+               MASTER_PORT="29563" if adaptive == "1" else "29564", PTYPE_TUNE="adaptive_c=" + ("2" if adaptive == "force" else "1"))
     r = subprocess.run([sys.executable, "-c", _ENGINE_SCRIPT], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]

@@ -23,7 +23,7 @@ def test_default_handoff_under_rocprofv3_kernel_trace(tmp_path):
         pytest.skip("rocprofv3 not installed")
     env = dict(os.environ, TMPDIR="/tmp", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
                HSA_ENABLE_IPC_MODE_LEGACY="0")
-    env.pop("PTYPE_STREAM_SYNC", None)  # the default hand-off
+    env.pop("PTYPE_TUNE", None)  # the default hand-off
     out = tmp_path / "trace"
     cmd = [prof, "--kernel-trace", "--stats", "-d", str(out), "-o", "run", "--output-format", "csv", "--",
            sys.executable, "bench.py", "--force-dist", "--steps", "3", "--warmup", "1", "--rtt-calls", "0",

@@ -204,7 +204,7 @@ def test_sorted_exchange_too_wide_is_overflow_then_resent():
 
 
 def test_sorted_exchange_onepass_epoch_tag_wraps_in_a_subprocess():
-    """the sorted exchange's one-pass sort (PTYPE_SX_SORT=onepass)
+    """the sorted exchange's one-pass look-back sort (tune sx_sort=1)
     across its epoch counter's 24-bit tag wrap: exact replies, no stalled look-back."""
     code = textwrap.dedent("""
         import sys, torch
@@ -235,7 +235,7 @@ def test_sorted_exchange_onepass_epoch_tag_wraps_in_a_subprocess():
         assert all(_run_ranks(R, body))
         print("SUBPROCESS-OK")
     """)
-    env = dict(os.environ, PTYPE_SX_SORT="onepass")
+    env = dict(os.environ, PTYPE_TUNE="sx_sort=1")
     p = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0 and "SUBPROCESS-OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
 
@@ -289,13 +289,13 @@ def test_sorted_exchange_step_captures_into_a_hipgraph():
     records, comm-stream fork / join per chunk, the layout in force -- no host
     wait) captured into a hipGraph and replayed on fresh batches: every reply
     right.  World 1 with the process group up; the all-to-all is a device copy
-    (PTYPE_SX_SELF_COPY) because RCCL collectives issued on the engine's own
+    (tune sx_self_copy) because RCCL collectives issued on the engine's own
     comm stream crash graph instantiation on this ROCm stack (see
     tools/rccl_capture_probe.py -- torch's own captured all_to_all works)."""
     from conftest import free_port
 
     env = dict(os.environ, PTYPE_ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
-               PTYPE_SX_SELF_COPY="1")
+               PTYPE_TUNE="sx_self_copy=1")
     try:
         r = subprocess.run([sys.executable, "-X", "faulthandler", "-c", _GRAPH_SCRIPT], env=env, capture_output=True, text=True,
                            timeout=120)
@@ -308,14 +308,12 @@ def test_sorted_exchange_step_captures_into_a_hipgraph():
     assert all(out["ok"]) and out["engine"] == "sorted" and out["agreed"], out
 
 
-@pytest.mark.parametrize("mbox_sort", ["twopass", "ldscount"])
-def test_alternate_sort_kernels_exact_in_a_subprocess(mbox_sort):
+def test_alternate_sort_kernels_exact_in_a_subprocess():
     """The non-default sort kernels, switched by environment (read once per
-    process): the sorted exchange's one-pass look-back sort (PTYPE_SX_SORT=onepass)
-    at R = 4, and the mailbox's two-pass count + scatter (PTYPE_MBOX_SORT=twopass;
-    ldscount: the count from an LDS shard table, the scatter resolving) with the
-    message-order drain (PTYPE_MBOX_DRAIN=msg) -- replies exact, unknown actors
-    answered STATUS_NO_ACTOR."""
+    process): the sorted exchange's one-pass look-back sort (tune sx_sort=1) at
+    R = 4, and the mailbox's count + scatter (mbox_sort=2) with the message-order
+    drain (mbox_drain_msg=1) -- replies exact, unknown actors answered
+    STATUS_NO_ACTOR."""
     code = textwrap.dedent("""
         import sys, threading, torch
         sys.path.insert(0, sys.argv[1])
@@ -353,6 +351,6 @@ def test_alternate_sort_kernels_exact_in_a_subprocess(mbox_sort):
         assert s["spilled"] > 0 and s["lookback_timeouts"] == 0
         print("SUBPROCESS-OK")
     """)
-    env = dict(os.environ, PTYPE_SX_SORT="onepass", PTYPE_MBOX_SORT=mbox_sort, PTYPE_MBOX_DRAIN="msg")
+    env = dict(os.environ, PTYPE_TUNE="sx_sort=1,mbox_sort=2,mbox_drain_msg=1")
     p = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0 and "SUBPROCESS-OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Host enqueue cost of ActorExchange.send vs its GPU time (single rank, RCCL
 forced on so the collective calls are real), for the native epoch engine and
-the Python pipeline (PTYPE_ENGINE=0 path).  If the enqueue time per step
+the Python pipeline (tune engine=0 path).  If the enqueue time per step
 approaches the GPU time, the multi-GPU step is host-bound.  Also checks that
 both paths return identical results."""
 import json

@@ -1,4 +1,4 @@
-"""Single-call latency vs the dispatcher's polling knobs (PTYPE_POLL_LANES / _FULL /
+"""Single-call latency vs the dispatcher's polling knobs (tune poll_lanes / poll_full /
 _SLEEP, read when a DeviceServer is built), all in one process on one box so the
 variants are comparable.  Prints one JSON line per variant."""
 import json
@@ -16,7 +16,7 @@ VARIANTS = [(64, 1, 1), (64, 0, 1), (16, 1, 1), (16, 0, 1), (1, 1, 1), (64, 1, 8
             (64, 1, 1)]
 state = torch.zeros(1024, dtype=torch.int64, device="cuda")
 for lanes, full, sleep in VARIANTS:
-    os.environ.update(PTYPE_POLL_LANES=str(lanes), PTYPE_POLL_FULL=str(full), PTYPE_POLL_SLEEP=str(sleep))
+    os.environ["PTYPE_TUNE"] = f"poll_lanes={lanes},poll_full={full},poll_sleep={sleep}"
     srv = hip().DeviceServer(0, 4096, state.data_ptr(), 1024, 0, 500.0, 60.0)
     try:
         for i in range(300):

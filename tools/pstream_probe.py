@@ -5,7 +5,7 @@ A DeviceServer wave is made resident (idle exit after IDLE s); then, on each of
 N fresh torch streams, one in-place add runs and that stream is synchronised.
 Prints per-stream wall time and the value each stream reads back, the server's
 running flag, and the totals after a device-wide synchronise.  Compare
-PTYPE_PERSISTENT_STREAM=low (default) / high / cumask / pooled (common.hpp
+PTYPE_TUNE=persistent_stream=low (default) / high / cumask / pooled (common.hpp
 dedicated_stream)."""
 import json
 import os
@@ -28,7 +28,7 @@ def main():
     x = torch.zeros(1024, device=dev)
     torch.cuda.synchronize()
     srv = hip().DeviceServer(0, 256, state.data_ptr(), state.numel(), 0, IDLE_MS, 30.0, "")
-    print(json.dumps({"mode": os.environ.get("PTYPE_PERSISTENT_STREAM", "low"),
+    print(json.dumps({"mode": os.environ.get("PTYPE_TUNE", "persistent_stream=low"),
                       "first_call": list(srv.call(METHOD_CALC_MULTIPLY, 1, 6, 7)), "running": srv.running,
                       "wave_stream_priority": srv.stream_priority}), flush=True)
     rows = []

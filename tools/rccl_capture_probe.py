@@ -15,7 +15,7 @@ import torch.distributed as dist  # noqa: E402
 def main():
     mode = sys.argv[1]
     if mode == "sx1cs":  # the sorted exchange's collectives issued on the capturing stream itself
-        os.environ["PTYPE_SX_COMM_CS"] = "1"
+        os.environ["PTYPE_TUNE"] = "sx_comm_cs=1"
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
