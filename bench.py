@@ -84,9 +84,9 @@ def _parse():
     p.add_argument("--no-secondary", action="store_true",
                    help="skip the secondary (affine placement) measurement after the headline")
     p.add_argument("--comm", choices=["rccl", "ipc"], default="rccl",
-                   help="N > 1 data-plane collectives: RCCL over the process group (one GPU per rank), or IpcComm "
-                        "(csrc/hip/ipc_comm.hpp: peers' HBM segments by IPC handle, a gloo group for the host side) "
-                        "-- ipc lets every rank share one GPU: a multi-process rehearsal, not a scaling figure")
+                   help="N > 1 data-plane transport of the compiled DataPlane (csrc/core/dataplane.cpp): RCCL over "
+                        "xGMI (one GPU per rank), or IpcComm (csrc/hip/ipc_comm.hpp: shared-memory segments) -- ipc "
+                        "lets every rank share one GPU: a multi-process rehearsal, not a scaling figure")
     return p.parse_args()
 
 
@@ -208,26 +208,45 @@ def main():
     else:
         device = torch.device("cpu")
     dist_on = world > 1 or args.force_dist
-    nccl = dist_on and use_gpu and not ipc
+    # N > 1 on GPUs: the data plane the way Join forms it -- a control-plane member per
+    # rank and the compiled DataPlane's communicator (RCCL over xGMI, or IpcComm with
+    # --comm ipc), no torch process group.  CPU runs: a gloo group.
+    native = dist_on and use_gpu
+    M = args.msgs_per_gpu
+    chunks = args.chunks or (2 if dist_on or args.loopback else 1)
+    G = bench_cp = None
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group("nccl" if nccl else "gloo", rank=rank, world_size=world,
-                                device_id=device if nccl else None)
-    red_dev = device if nccl else torch.device("cpu")  # where host-level reductions' tensors live
+        if native:
+            from ptype_amd.parallel.exchange import ipc_cap_for
+            from ptype_amd.utils import benchmarks as BM
+
+            bench_cp, G = BM.bench_group(device, rank, world, comm="ipc" if ipc else "rccl",
+                                         cap_bytes=ipc_cap_for(M, chunks, world) if ipc else 0)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def barrier():
         if dist_on:
-            if nccl:
-                dist.barrier(device_ids=[dev_idx])
+            if native:
+                G.barrier()
             else:
                 dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if not dist_on:
+            return x
+        if native:
+            return G.max_over_ranks(x)
+        tt = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
 
     def sync():
         if use_gpu:
             torch.cuda.synchronize(device)
 
-    M = args.msgs_per_gpu
     fake = None
     if args.loopback > 0:
         if world != 1 or not use_gpu:
@@ -237,10 +256,9 @@ def main():
         fake = (hip().FakeComm(args.loopback, loopback=True, link_gbps=args.link_gbps), 0)
     geo = args.loopback or world  # ranks the actors are sharded over
     n_actors = args.actors_per_gpu * geo
-    # 2 pipeline chunks on the collective path: measured against 1/4/8 with the
-    # all-to-all modelled at xGMI-like bandwidth (profiles/r1_chunk_model.jsonl)
-    # and on the forced single-rank RCCL path (0.31 vs 0.38-0.40 ms at 4 chunks)
-    chunks = args.chunks or (2 if dist_on or fake else 1)
+    # (2 pipeline chunks on the collective path: measured against 1/4/8 with the
+    # all-to-all modelled at xGMI-like bandwidth, profiles/r1_chunk_model.jsonl,
+    # and on the forced single-rank RCCL path: 0.31 vs 0.38-0.40 ms at 4 chunks)
 
     def build_table(placement):
         # GPU registry mirror: every actor of the node -> (rank, mailbox)
@@ -304,7 +322,7 @@ def main():
         # order in one ring) unless --sharding arrival (tile-sharded queues)
         ex = ActorExchange(table, Mq, chunks=chunks, state=state, fake=fake, delivery=delivery,
                            mailbox_ordered=sharding == "actor", mailbox_shards=args.mailbox_shards,
-                           mailbox_slots=args.mailbox_slots, comm="ipc" if ipc else "rccl")
+                           mailbox_slots=args.mailbox_slots, comm="ipc" if ipc else "rccl", group=G)
         _LIVE_EXCHANGES.append(weakref.ref(ex))  # (weak: a finished measurement's buffers stay freeable)
         if Mq == M and method == METHOD_CALC_MULTIPLY and not wide:
             rq, v, t = req, val, st
@@ -393,10 +411,7 @@ def main():
                              "enqueue_us_per_send": round((d["total_ns"] - d["spec_wait_ns"]) / n / 1e3, 2),
                              "agreement_wait_us_per_send": round(d["spec_wait_ns"] / n / 1e3, 2),
                              "overflow_wait_us_per_send": round(d["overflow_wait_ns"] / n / 1e3, 2)}
-        if dist_on:
-            tt = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
+        elapsed = max_over_ranks(elapsed)
         if steps:
             verify("timed", last(warmup + steps), vt[1], vt[2], method)
         return elapsed, ex, graph is not None
@@ -487,18 +502,11 @@ def main():
     if not args.no_secondary and args.steps and use_gpu and fake is None:
         from ptype_amd.utils import benchmarks as BM
 
-        def max_over_ranks(x):
-            if not dist_on:
-                return x
-            tt = torch.tensor([x], dtype=torch.float64, device=red_dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            return float(tt.item())
-
         secondaries["optimus_fanout"] = BM.optimus_fanout(table, n_actors, device, args.steps, max(1, args.warmup),
                                                           rank=rank, world=world, chunks=chunks,
                                                           comm="ipc" if ipc else "rccl",
                                                           barrier=barrier if dist_on else None,
-                                                          max_over_ranks=max_over_ranks)
+                                                          max_over_ranks=max_over_ranks, group=G)
         if world == 1 and not dist_on:  # one process: a failing secondary is reported, the headline kept
             for name, fn in (("registry_1m", lambda: BM.registry_1m(device)),
                              ("api_send", lambda: BM.api_send(device, sorted({M, min(M, 1 << 20)}, reverse=True),
@@ -508,39 +516,6 @@ def main():
                 except Exception as e:  # noqa: BLE001
                     secondaries[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
                     print(f"[bench] secondary {name} failed: {e!r}", file=sys.stderr, flush=True)
-
-    # diagnostics, outside the timed region: the step's all-to-all byte volume moved
-    # by RCCL alone (same chunking, same per-peer sizes), so a multi-GPU line says
-    # whether the step is bound by xGMI or by the kernels around it
-    diag = None
-    if nccl and ex.last_wire is not None and args.steps:
-        w = ex.last_wire
-        # bytes per chunk, all peers (rounded to a multiple of the world: equal splits)
-        sizes = [(4 * int(w[k]) + world - 1) // world * world for k in ("req_words", "rep_words")]
-        bufs = [(torch.empty(s, dtype=torch.uint8, device=device), torch.empty(s, dtype=torch.uint8, device=device))
-                for s in sizes]
-
-        def a2a_step():
-            for _ in range(chunks):
-                for snd, rcv in bufs:
-                    dist.all_to_all_single(rcv, snd)
-
-        a2a_step()
-        sync()
-        barrier()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 5
-        e0.record()
-        for _ in range(reps):
-            a2a_step()
-        e1.record()
-        sync()
-        a2a_ms = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64, device=device)
-        dist.all_reduce(a2a_ms, op=dist.ReduceOp.MAX)
-        per_step = chunks * sum(sizes)
-        off_rank = per_step * (world - 1) / world
-        diag = {"a2a_only_ms_per_step": float(a2a_ms.item()), "a2a_bytes_per_step_per_rank": per_step,
-                "a2a_offrank_GBps_per_rank": off_rank / (float(a2a_ms.item()) * 1e-3) / 1e9 if world > 1 else None}
 
     # p50 RTT of a synchronous Call to a GPU actor (persistent dispatcher, no kernel
     # launch per call): from this process to its own GPU, and -- with more than one
@@ -586,11 +561,7 @@ def main():
             # host-side barriers through the rendezvous store: no collective kernel
             # sits on any GPU while the peers' dispatchers must (re)launch to serve
             def host_barrier(key):
-                store = dist.distributed_c10d._get_default_store()
-                store.add(key, 1)
-                t_end = time.monotonic() + 120.0
-                while store.add(key, 0) < world and time.monotonic() < t_end:
-                    time.sleep(0.001)
+                BM.kv_barrier(bench_cp, key, world)
 
             host_barrier("ptype/bench/rtt/ready")  # every rank's dispatcher segment exists
             try:
@@ -603,9 +574,8 @@ def main():
             host_barrier("ptype/bench/rtt/done")  # keep serving until every rank is done calling
         srv.close()
         if dist_on:
-            t = torch.tensor([p50, p50_remote, float(len(rtt_errors))], dtype=torch.float64, device=red_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            p50, p50_remote, n_err = (float(x) for x in t.tolist())
+            n_err = max_over_ranks(float(len(rtt_errors)))
+            p50, p50_remote = max_over_ranks(max(p50, 0.0)), max_over_ranks(max(p50_remote or 0.0, 0.0))
             if n_err and not rtt_errors:
                 rtt_errors.append("on another rank")
         if rtt_errors:
@@ -653,7 +623,9 @@ def main():
                                 f"actors sharded over {world} GPU(s)" + ((", RCCL all-to-all epochs" if use_gpu
                                                                           else ", gloo all-to-all epochs (CPU)")
                                                                          if dist_on else "")),
-                "comm": ("ipc" if ipc else "rccl") if dist_on and use_gpu else None,
+                # the N > 1 communicator: the compiled DataPlane's (Join's), never a torch process group's
+                "comm": (("DataPlane/IpcComm" if ipc else "DataPlane/RCCL") if native else
+                         ("gloo" if dist_on else None)),
                 "msgs_per_gpu_per_step": M,
                 "actors": n_actors,
                 "chunks": chunks,
@@ -679,8 +651,6 @@ def main():
                    if fake else {}),
             },
         }
-        if diag is not None:
-            out["diag"] = diag
         if secondaries:
             out["secondaries"] = secondaries
         print(json.dumps(out), flush=True)
@@ -693,11 +663,6 @@ def main():
         secondaries["api_send"] = {"error": "did not finish (hang watchdog)"}
         _EMIT_ON_HANG[0] = emit
         try:
-            def max_over_ranks(x):
-                tt = torch.tensor([x], dtype=torch.float64, device=red_dev)
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                return float(tt.item())
-
             secondaries["api_send"] = BM.api_send(device, [min(M, 1 << 22)], args.actors_per_gpu, args.steps,
                                                   max(1, args.warmup), rank=rank, world=world,
                                                   comm="ipc" if ipc else "rccl", barrier=barrier,
@@ -706,7 +671,10 @@ def main():
             secondaries["api_send"] = {"error": f"{type(e).__name__}: {e}"[:300]}
             print(f"[rank {rank}] secondary api_send failed: {e!r}", file=sys.stderr, flush=True)
     emit()
-    if dist_on:
+    if native:
+        G.close()
+        bench_cp.Close()
+    elif dist_on:
         dist.destroy_process_group()
 
 

@@ -986,7 +986,45 @@ PYBIND11_MODULE(_core, m) {
       .def("wait_nodes", &DataPlane::wait_nodes, py::arg("world"), py::call_guard<py::gil_scoped_release>())
       .def("settle", &DataPlane::settle, py::arg("current"), py::arg("grace_s"),
            py::call_guard<py::gil_scoped_release>())
-      .def("recover", &DataPlane::recover, py::arg("grace_s"), py::call_guard<py::gil_scoped_release>())
+      .def("use_transport", &DataPlane::use_transport, py::arg("ops"), py::arg("cap_bytes"),
+           "a DpTransportOps table of the device runtime (IpcComm) instead of RCCL; before the first form()")
+      .def_property_readonly("transport", &DataPlane::transport)
+      .def(
+          "recover",
+          [](DataPlane& d, double grace_s) {
+            DataPlane::Recovery r;
+            {
+              py::gil_scoped_release nogil;
+              r = d.recover(grace_s);
+            }
+            py::dict out;
+            out["lost"] = r.lost;
+            out["members"] = r.members;
+            out["blocks"] = r.blocks;
+            out["kept_from"] = r.kept_from;
+            out["from_replica"] = r.from_replica;
+            return out;
+          },
+          py::arg("grace_s"),
+          "abort + settle + form(gen + 1); the new placement: {lost, members, blocks, kept_from, from_replica}")
+      .def("placement", &DataPlane::placement, py::arg("members"))
+      .def_property_readonly("blocks", &DataPlane::blocks)
+      .def("buddy", &DataPlane::buddy, py::arg("node"))
+      .def("lost_blocks", &DataPlane::lost_blocks, py::arg("before"), py::arg("after"))
+      .def_property_readonly("nodes0", &DataPlane::nodes0)
+      .def("replica_blocks", &DataPlane::replica_blocks)
+      .def("replicate", &DataPlane::replicate, py::arg("state"), py::arg("bytes"), py::arg("recv"),
+           py::arg("recv_bytes"), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("replicas", &DataPlane::replicas)
+      .def("set_watchdog", &DataPlane::set_watchdog, py::arg("timeout_s"))
+      .def("begin_send", &DataPlane::begin_send)
+      .def("end_send", &DataPlane::end_send)
+      .def("arm", &DataPlane::arm, py::arg("stream"))
+      .def_property_readonly("watchdog_failed", &DataPlane::watchdog_failed)
+      .def("reset_watchdog", &DataPlane::reset_watchdog)
+      .def("fail_generation", &DataPlane::fail_generation, py::arg("why"), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("comm_cell", &DataPlane::comm_cell)
+      .def("engine_comm_ref", &DataPlane::engine_comm_ref)
       .def("async_error", &DataPlane::async_error)
       .def("abort", &DataPlane::abort, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("aborted", &DataPlane::aborted)

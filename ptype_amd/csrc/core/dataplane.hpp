@@ -1,39 +1,52 @@
-// The data plane's RCCL communicator lifecycle, compiled (VERDICT r4 Missing #3;
-// SURVEY 3.1 step 5 and 5.3).
+// The data plane's communicator lifecycle and rank-failure handling, compiled
+// (VERDICT r4 Missing #3, r5 #3).
 //
 // The reference's Join is one compiled call that brings a member up, registers
 // it and returns (cluster/cluster.go:28-84, :161-196); a dead member is noticed
 // through its lapsed lease (cluster/registry.go:51-86) and the survivors carry
-// on.  The GPU data plane of a service is an RCCL communicator over the
-// service's nodes, and its whole life runs here, in the control-plane module:
+// on.  The GPU data plane of a service is a communicator over the service's
+// nodes, and its whole life runs here, in the control-plane module:
 //
-//   form(gen, members)   rank 0 (members[0]) draws an ncclUniqueId and publishes
-//                        it with the member list under
-//                        store/_ptype/nccl/<service>/<gen>/uid; every member
-//                        reads it from the replicated store and runs
-//                        ncclCommInitRank on its device (no TCPStore, no torch
-//                        process group);
-//   async_error()        ncclCommGetAsyncError: a peer that died mid-collective;
-//   abort()              ncclCommAbort: nothing of this generation blocks again;
-//   settle(members)      the registry's live nodes (2 s leases): the members
-//                        minus those whose lease lapsed (waited on for at most
-//                        grace_s) -- the next generation's proposal;
-//   recover()            abort + settle + form(gen + 1): the elastic step.
+//   form(gen, members)   the proposal's first node publishes a record (members,
+//                        their registration tags, and for RCCL an ncclUniqueId)
+//                        under store/_ptype/nccl/<service>/<gen>/<node>; the first
+//                        record still current wins, so differing views converge.
+//                        RCCL: ncclCommInitRank, bounded by timeout_s.  IPC
+//                        (DpTransportOps, one GPU shared by processes): every
+//                        member opens its segment under a name derived from the
+//                        record, the members meet at a store barrier, connect,
+//                        meet again and seal -- no torch process group anywhere;
+//   abort()              RCCL: the CommCell is retired (no enqueue in flight) and
+//                        the communicator aborted; IPC: every wait ends at once;
+//   settle(members)      the registry's live nodes (2 s leases): the members minus
+//                        those whose lease lapsed -- the next generation's proposal;
+//   recover()            abort + settle + form(gen + 1), and the placement of the
+//                        new generation: ring adoption of the lost ranks' actor
+//                        blocks (placement(), lost_blocks());
+//   replicate()          buddy replicas: each node's blocks to the node that would
+//                        adopt them, one send / receive pair per neighbour;
+//   watchdog             begin_send / end_send / arm(stream): a thread that fails
+//                        the generation when a Send's host part or device work is
+//                        overdue (RCCL has no timeout of its own) -- it poisons the
+//                        cell and aborts only once no enqueue is in flight.
 //
 // RCCL and HIP are resolved at run time from the libraries the process already
 // loaded (the device runtime's torch / HIP), so this host-only module links
-// neither; without them every call throws.  Host-level agreements of the data
-// plane (a few words, all-reduce MAX) and point-to-point state moves (buddy
-// replicas) go through the same communicator.
+// neither; without them every call throws.
 #pragma once
 #include <stdint.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "api.hpp"
+#include "dp_link.hpp"
 
 namespace ptype {
 
@@ -46,38 +59,73 @@ class DataPlane {
   DataPlane(const DataPlane&) = delete;
   DataPlane& operator=(const DataPlane&) = delete;
 
-  // Generation `gen` over `proposal` (node ids "address:port"): rendezvous -- the
-  // first published record still current wins, so differing views converge -- and
-  // ncclCommInitRank.  Returns this member's rank; throws "excluded" if left out.
+  // The transport: RCCL (default), or a DpTransportOps table (the device runtime's
+  // IpcComm) with `cap_bytes` per peer region.  Before the first form().
+  void use_transport(uintptr_t ops, uint64_t cap_bytes);
+  std::string transport() const { return ops_ ? "ipc" : "rccl"; }
+
+  // Generation `gen` over `proposal` (node ids "address:port").  Returns this
+  // member's rank; throws "excluded" if the winning record left it out.
   int form(uint64_t gen, const std::vector<std::string>& proposal);
   void set_device(int device);  // before the first form() (no communicator yet)
   int device() const { return device_; }
-  // The service's registered nodes with a live lease (sorted "address:port").
   std::vector<std::string> alive_nodes();
-  // Wait until `world` nodes are registered; the first `world` of them (sorted).
   std::vector<std::string> wait_nodes(int world);
-  // The next proposal: `current` minus the nodes whose lease lapsed, waiting at
-  // most grace_s for one to lapse (survivors keep their order).
   std::vector<std::string> settle(const std::vector<std::string>& current, double grace_s);
-  // abort + settle + form(gen + 1); returns the new member list
-  std::vector<std::string> recover(double grace_s);
 
-  int async_error() const;  // ncclResult_t of the communicator (0: fine)
-  void abort();             // ncclCommAbort (idempotent)
-  bool aborted() const { return comm_.load() == nullptr; }
+  // ---- rank failures: abort + settle + form(gen + 1); the original ranks lost
+  struct Recovery {
+    std::vector<int> lost;                   // original ranks whose host is gone
+    std::vector<std::string> members;        // the new generation, in rank order
+    std::vector<int> blocks;                 // original ranks this member hosts now (block order)
+    std::vector<int> kept_from;              // per new block: its index among the old blocks, or -1
+    std::vector<int> from_replica;           // per new block: 1 = resumes from the buddy replica
+  };
+  Recovery recover(double grace_s);
+  // original ranks -> owner (ring adoption over nodes0) for `members`
+  std::map<std::string, std::vector<int>> placement(const std::vector<std::string>& members) const;
+  std::vector<int> blocks() const;                 // this member's original ranks, in block order
+  std::string buddy(const std::string& node) const;  // the next surviving node after `node` (nodes0 ring)
+  std::vector<int> lost_blocks(const std::vector<std::string>& before, const std::vector<std::string>& after) const;
+  const std::vector<std::string>& nodes0() const { return nodes0_; }
+  // Buddy replicas: send this member's blocks (`bytes` at `state`) to its buddy and
+  // receive the blocks of the node whose buddy it is into `recv` (recv_bytes, sized
+  // by replica_blocks()).  Collective over the generation.  Returns those blocks.
+  std::vector<int> replica_blocks() const;
+  std::vector<int> replicate(uintptr_t state, size_t bytes, uintptr_t recv, size_t recv_bytes);
+  const std::vector<int>& replicas() const { return replicas_; }  // blocks held since the last replicate()
+
+  int async_error() const;  // RCCL: ncclResult_t of the communicator; IPC: 1 once failed (0: fine)
+  void abort();             // idempotent
+  bool aborted() const;
 
   // element-wise MAX of `v` over the members (host values; a device round trip)
   std::vector<uint64_t> allreduce_max(const std::vector<uint64_t>& v);
   // the same on n device words in place, enqueued on `stream` (no host wait)
   void allreduce_max_dev(uintptr_t dev, size_t n, uintptr_t stream);
   // grouped send of `sbytes` at device address `send` to rank `dst` and receive of
-  // `rbytes` into `recv` from rank `src` (dst / src < 0: that half skipped); synchronous.
-  // Host waits are bounded by timeout_s: a peer that never answers aborts the
-  // communicator and raises "ncclRemoteError" (a rank failure).
+  // `rbytes` into `recv` from rank `src` (dst / src < 0: that half skipped); synchronous
+  // and bounded by timeout_s (a peer that never answers: abort + "ncclRemoteError").
   void sendrecv(uintptr_t send, size_t sbytes, int dst, uintptr_t recv, size_t rbytes, int src);
   void barrier();
 
-  uintptr_t comm() const { return (uintptr_t)comm_.load(); }
+  // ---- Send watchdog (a thread; off until set_watchdog(t > 0))
+  void set_watchdog(double timeout_s);
+  void begin_send();
+  void end_send();
+  void arm(uintptr_t stream);   // the device work queued on `stream` so far must finish in time
+  std::string watchdog_failed() const;  // why the generation was failed ("" while fine)
+  void reset_watchdog();
+  // Fail the generation now, as the watchdog does (abort; the next Send raises a
+  // rank failure and recovers).  Also the fault-injection hook of the tests.
+  void fail_generation(const std::string& why);
+
+  // What the engines take: RCCL -- the CommCell's address (enter / leave around every
+  // enqueue); IPC -- a new reference to the transport's communicator (the device
+  // runtime's binding adopts it).  0 when the transport is the other one.
+  uintptr_t comm_cell() { return ops_ ? 0 : (uintptr_t)&cell_; }
+  uintptr_t engine_comm_ref();
+  uintptr_t comm() const { return (uintptr_t)cell_.comm.load(); }  // raw ncclComm_t (diagnostics)
   int rank() const { return rank_; }
   int size() const { return (int)members_.size(); }
   uint64_t gen() const { return gen_; }
@@ -87,20 +135,40 @@ class DataPlane {
 
  private:
   void destroy_comm();
-  void* live_comm() const;     // the communicator, or a peer-failure error once aborted
-  void wait_stream(void* comm);  // bounded by timeout_s; a dead peer aborts and raises
+  void* live_comm();                 // the communicator, or a peer-failure error once aborted
+  void wait_stream();                // bounded by timeout_s; a failed peer aborts and raises
+  void form_rccl(const std::string& uid_hex, int rank, int world);
+  void form_ipc(const std::string& pfx, const std::string& nonce, int rank, int world);
+  void store_barrier(const std::string& key_pfx, int world);
+  void ensure_scratch(size_t bytes);
+  void watchdog_loop();
+
   std::shared_ptr<EtcdRegistry> reg_;
   std::shared_ptr<KvClient> kv_;
   std::string service_, me_;
   int device_;
   double timeout_s_;
-  std::atomic<void*> comm_{nullptr};  // ncclComm_t (a watchdog thread may abort it)
-  void* stream_ = nullptr;  // hipStream_t of this object's collectives
-  void* scratch_ = nullptr; // device words for allreduce_max
-  size_t scratch_words_ = 0;
+  CommCell cell_;                     // RCCL
+  const DpTransportOps* ops_ = nullptr;  // IPC
+  void* ep_ = nullptr;                // the transport endpoint of the generation in force
+  std::atomic<bool> ep_failed_{false};
+  uint64_t cap_bytes_ = 0;
+  void* stream_ = nullptr;   // hipStream_t of this object's collectives
+  void* scratch_ = nullptr;  // device bytes for allreduce_max / sendrecv staging
+  size_t scratch_bytes_ = 0;
   int rank_ = -1;
   uint64_t gen_ = 0;
-  std::vector<std::string> members_;
+  std::vector<std::string> members_, nodes0_;
+  std::vector<int> replicas_;
+  // watchdog
+  std::mutex wd_mu_;
+  std::condition_variable wd_cv_;
+  std::thread wd_thread_;
+  bool wd_stop_ = false;
+  double wd_timeout_s_ = 0;
+  double host_deadline_ = 0;  // 0: not inside a Send
+  std::vector<std::pair<void*, double>> armed_;  // (hipEvent_t, deadline)
+  std::string wd_failed_;
 };
 
 }  // namespace ptype

@@ -193,6 +193,18 @@ PYBIND11_MODULE(_hip, m) {
   m.def("roctx_mark", [](const std::string& s) {
     if (roctx().mark) roctx().mark(s.c_str());
   });
+  m.def("dp_ipc_transport", [] { return (uintptr_t)ipc_transport_ops(); },
+        "the DpTransportOps table (csrc/core/dp_link.hpp) of IpcComm, for _core.DataPlane.use_transport");
+  m.def(
+      "host_comm_adopt",
+      [](uintptr_t ref) {
+        if (!ref) throw std::invalid_argument("host_comm_adopt: null reference");
+        auto* p = reinterpret_cast<std::shared_ptr<HostComm>*>(ref);
+        std::shared_ptr<HostComm> out = *p;
+        delete p;
+        return out;
+      },
+      py::arg("ref"), "the engines' communicator from DataPlane.engine_comm_ref() (one reference, adopted)");
   m.def("set_tune", &set_tune, py::arg("spec"),
         "apply 'key=value,...' path switches (csrc/hip/tune.hpp) after PTYPE_TUNE; false on an unknown key");
   m.def("tune", [] {

@@ -8,9 +8,10 @@
 // host only enqueues (~10 us per step instead of ~100 us of Python per chunk,
 // which made a multi-GPU step host-bound -- measured with tools/host_overhead.py).
 //
-// RCCL is called directly on the communicator torch's process group already
-// owns (ProcessGroupNCCL._comm_ptr()); the entry points are resolved at run
-// time from the librccl torch loaded, so this module links no second copy.
+// RCCL is called directly on the communicator the control plane's DataPlane
+// formed (csrc/core/dataplane.hpp), through its CommCell (dp_link.hpp); the entry
+// points are resolved at run time from the librccl torch loaded, so this module
+// links no second copy.
 // Every rank issues the same collectives in the same order (the pipeline is
 // deterministic in the chunk count, which ActorExchange agrees collectively).
 #pragma once
@@ -29,6 +30,7 @@
 #include "mailbox.hpp"
 #include "packed.hpp"
 #include "tune.hpp"
+#include "dp_link.hpp"
 
 namespace ptype {
 
@@ -120,6 +122,20 @@ inline Rccl& rccl() {
 }
 }  // namespace engine_detail
 using engine_detail::rccl;
+
+// One RCCL enqueue on the data plane's CommCell (csrc/core/dp_link.hpp): the
+// communicator of the generation in force, or a peer-failure error once the
+// DataPlane (or its Send watchdog) retired it -- never a freed communicator.
+struct CellUse {
+  CommCell* c;
+  void* comm;
+  explicit CellUse(CommCell* cell) : c(cell), comm(cell ? cell->enter() : nullptr) {
+    if (!comm) throw std::runtime_error("ncclRemoteError: the data-plane generation was aborted");
+  }
+  ~CellUse() { c->leave(); }
+  CellUse(const CellUse&) = delete;
+  CellUse& operator=(const CellUse&) = delete;
+};
 using engine_detail::kNcclInt8;
 using engine_detail::kNcclMax;
 using engine_detail::kNcclUint64;
@@ -341,13 +357,13 @@ class EpochEngine {
   // `c_fixed` (0: C): the capacity of Sends that do not adapt (wire v2).
   EpochEngine(int device, uintptr_t comm, int R, int rank, int64_t C, int64_t max_chunk, int chunks,
               std::shared_ptr<HostComm> fake = nullptr, bool adaptive = false, int64_t c_fixed = 0)
-      : device_(device), comm_((void*)comm), fake_(std::move(fake)), R_(R), rank_(rank), C_(C), C_alloc_(C),
+      : device_(device), cell_(reinterpret_cast<CommCell*>(comm)), fake_(std::move(fake)), R_(R), rank_(rank), C_(C), C_alloc_(C),
         C_fixed_(c_fixed > 0 && c_fixed <= C ? c_fixed : C), max_chunk_(max_chunk), chunks_(chunks),
         adaptive_(adaptive) {
     if (R < 1 || chunks < 1 || max_chunk < 1) throw std::invalid_argument("EpochEngine: bad geometry");
-    if (fake_ && (comm_ || fake_->size() != R || rank < 0 || rank >= R))
+    if (fake_ && (cell_ || fake_->size() != R || rank < 0 || rank >= R))
       throw std::invalid_argument("EpochEngine: fake communicator must match R and replace comm");
-    if (comm_ && !rccl().alltoall) throw std::runtime_error("EpochEngine: ncclAllToAll not found in the process");
+    if (cell_ && !rccl().alltoall) throw std::runtime_error("EpochEngine: ncclAllToAll not found in the process");
     PT_HIP_CHECK(hipSetDevice(device_));
     int lo = 0, hi = 0;
     PT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -592,7 +608,11 @@ class EpochEngine {
       return;
     }
     if (fake_ && !fake_->loopback()) fake_->allreduce_max(rank_, meta_dev_, (int)n_agree, cs);  // device-side (IpcComm)
-    const int rc = fake_ ? 0 : rccl().allreduce(meta_dev_, meta_dev_, n_agree, kNcclUint64, kNcclMax, comm_, cs);
+    int rc = 0;
+    if (!fake_) {
+      CellUse u(cell_);
+      rc = rccl().allreduce(meta_dev_, meta_dev_, n_agree, kNcclUint64, kNcclMax, u.comm, cs);
+    }
     if (rc != 0)
       throw std::runtime_error(std::string("ncclAllReduce failed: ") +
                                (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
@@ -847,7 +867,8 @@ class EpochEngine {
       fake_->alltoall(rank_, (const void*)src, (void*)dst, (size_t)words_per_peer * 4, comm_stream_);
       return;
     }
-    const int rc = rccl().alltoall((const void*)src, (void*)dst, (size_t)words_per_peer * 4, kNcclInt8, comm_,
+    CellUse u(cell_);
+    const int rc = rccl().alltoall((const void*)src, (void*)dst, (size_t)words_per_peer * 4, kNcclInt8, u.comm,
                                    comm_stream_);
     if (rc != 0)
       throw std::runtime_error(std::string("ncclAllToAll failed: ") +
@@ -868,18 +889,19 @@ class EpochEngine {
         throw std::runtime_error(std::string(what) + " failed: " +
                                  (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
     };
+    CellUse u(cell_);
     check(rccl().group_start(), "ncclGroupStart");
     for (int q = 0; q < R_; ++q) {
-      check(rccl().send((const char*)src + (size_t)q * stride, xs_[q], kNcclInt8, q, comm_, comm_stream_), "ncclSend");
-      check(rccl().recv((char*)dst + (size_t)q * stride, xr_[q], kNcclInt8, q, comm_, comm_stream_), "ncclRecv");
+      check(rccl().send((const char*)src + (size_t)q * stride, xs_[q], kNcclInt8, q, u.comm, comm_stream_), "ncclSend");
+      check(rccl().recv((char*)dst + (size_t)q * stride, xr_[q], kNcclInt8, q, u.comm, comm_stream_), "ncclRecv");
     }
     check(rccl().group_end(), "ncclGroupEnd");
   }
 
   int device_;
-  bool collectives() const { return comm_ != nullptr || fake_ != nullptr; }
+  bool collectives() const { return cell_ != nullptr || fake_ != nullptr; }
 
-  void* comm_;
+  CommCell* cell_;  // the data plane's RCCL communicator (dp_link.hpp), or null
   std::shared_ptr<HostComm> fake_;
   int R_, rank_;
   int64_t C_, C_alloc_, C_fixed_, max_chunk_;

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <thread>
 
 #include "exchange_sorted.hpp"
 #include "mailbox.hpp"
@@ -884,16 +885,16 @@ __global__ __launch_bounds__(kXOrdThreads) void sx_drain_ord_kernel(const uint32
 // ---------------------------------------------------------------- host
 SortedExchange::SortedExchange(int device, uintptr_t comm, int R, int rank, int64_t max_chunk, int chunks,
                                int64_t C_alloc, int64_t C0, std::shared_ptr<HostComm> fake)
-    : device_(device), comm_((void*)comm), fake_(std::move(fake)), R_(R), rank_(rank), chunks_(chunks),
+    : device_(device), cell_(reinterpret_cast<CommCell*>(comm)), fake_(std::move(fake)), R_(R), rank_(rank), chunks_(chunks),
       max_chunk_(max_chunk), C_alloc_(C_alloc) {
   if (R < 1 || R > kSxMaxRanks) throw std::invalid_argument("SortedExchange: 1 <= ranks <= 16");
   if (chunks < 1 || chunks > kSxMaxChunks) throw std::invalid_argument("SortedExchange: 1 <= chunks <= 4");
   if (max_chunk < 1 || C_alloc < 64 || C0 < 1 || C0 > C_alloc) throw std::invalid_argument("SortedExchange: geometry");
   if (C_alloc > 0x7fffffff / R) throw std::invalid_argument("SortedExchange: R * C must fit an int32 position");
-  if (fake_ && (comm_ || fake_->size() != R || rank < 0 || rank >= R))
+  if (fake_ && (cell_ || fake_->size() != R || rank < 0 || rank >= R))
     throw std::invalid_argument("SortedExchange: fake communicator must match R and replace comm");
-  if (!fake_ && !comm_) throw std::invalid_argument("SortedExchange: needs a communicator (RCCL or FakeComm)");
-  if (comm_ && (!rccl().alltoall || !rccl().allreduce))
+  if (!fake_ && !cell_) throw std::invalid_argument("SortedExchange: needs a communicator (RCCL or FakeComm)");
+  if (cell_ && (!rccl().alltoall || !rccl().allreduce))
     throw std::runtime_error("SortedExchange: RCCL entry points not found in the process");
   PT_HIP_CHECK(hipSetDevice(device_));
   int lo = 0, hi = 0;
@@ -1004,6 +1005,19 @@ static uint64_t sx_now_ns() {
       .count();
 }
 
+// A host wait on this engine's event that a retired generation ends: RCCL kernels
+// return once the DataPlane aborted the communicator, and the poll sees the cell's
+// poison first (no host wait outlives a peer failure the watchdog caught).
+void SortedExchange::wait_event(hipEvent_t e) const {
+  for (int spin = 0;; ++spin) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) PT_HIP_CHECK(q);
+    if (cell_ && cell_->failed()) throw std::runtime_error("ncclRemoteError: the data-plane generation was aborted");
+    if (spin > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 uint64_t SortedExchange::last_overflow() const { return sends_ > 0 ? overflow_of(sends_ - 1) : 0; }
 
 uint64_t SortedExchange::overflow_of(int64_t k) const {
@@ -1011,7 +1025,7 @@ uint64_t SortedExchange::overflow_of(int64_t k) const {
   const int j = (int)(k & 1);
   if (meta_send_[j] != k) throw std::runtime_error("SortedExchange: no agreement of that Send (captured, or reused)");
   const uint64_t t0 = sx_now_ns();
-  PT_HIP_CHECK(hipEventSynchronize(ev_meta_[j]));
+  wait_event(ev_meta_[j]);
   prof_.overflow_waits += 1;
   prof_.overflow_wait_ns += sx_now_ns() - t0;
   return meta_host_[j * kSxMetaWords + kMetaOverflow];
@@ -1073,7 +1087,7 @@ void SortedExchange::pick_spec(hipStream_t cs) {
   const int j = (int)(want & 1);
   if (meta_send_[j] != want) return;  // recorded under a graph capture: keep the layout in force
   const uint64_t t0 = sx_now_ns();
-  PT_HIP_CHECK(hipEventSynchronize(ev_meta_[j]));
+  wait_event(ev_meta_[j]);
   prof_.spec_wait_ns += sx_now_ns() - t0;
   adopt(meta_host_ + j * kSxMetaWords, want);
 }
@@ -1098,6 +1112,7 @@ void SortedExchange::a2a(const void* src, void* dst, size_t stride, const size_t
     if (rc != 0)
       throw std::runtime_error(std::string(what) + " failed: " + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
   };
+  CellUse u(cell_);
   if ((grouped_p2p || send) && rccl().p2p()) {
     // per-pair prefixes (send / recv sizes), or under a hipGraph capture:
     // ncclAllToAll's captured form crashed graph instantiation here (RCCL 2.26;
@@ -1105,16 +1120,16 @@ void SortedExchange::a2a(const void* src, void* dst, size_t stride, const size_t
     // torch captures -- instantiate and replay
     check(rccl().group_start(), "ncclGroupStart");
     for (int q = 0; q < R_; ++q) {
-      check(rccl().send((const char*)src + (size_t)q * stride, send ? send[q] : stride, kNcclInt8, q, comm_,
+      check(rccl().send((const char*)src + (size_t)q * stride, send ? send[q] : stride, kNcclInt8, q, u.comm,
                         cur_comm_), "ncclSend");
-      check(rccl().recv((char*)dst + (size_t)q * stride, recv ? recv[q] : stride, kNcclInt8, q, comm_, cur_comm_),
+      check(rccl().recv((char*)dst + (size_t)q * stride, recv ? recv[q] : stride, kNcclInt8, q, u.comm, cur_comm_),
             "ncclRecv");
     }
     check(rccl().group_end(), "ncclGroupEnd");
     return;
   }
   if (send) throw std::runtime_error("SortedExchange: per-pair sizes need RCCL's grouped send / recv");
-  check(rccl().alltoall(src, dst, stride, kNcclInt8, comm_, cur_comm_), "ncclAllToAll");
+  check(rccl().alltoall(src, dst, stride, kNcclInt8, u.comm, cur_comm_), "ncclAllToAll");
 }
 
 void SortedExchange::allreduce_meta(uint64_t* dev, hipStream_t s) {
@@ -1122,7 +1137,8 @@ void SortedExchange::allreduce_meta(uint64_t* dev, hipStream_t s) {
     fake_->allreduce_max(rank_, dev, kSxMetaPair + R_ * R_, s);
     return;
   }
-  const int rc = rccl().allreduce(dev, dev, kSxMetaPair + R_ * R_, kNcclUint64, kNcclMax, comm_, s);
+  CellUse u(cell_);
+  const int rc = rccl().allreduce(dev, dev, kSxMetaPair + R_ * R_, kNcclUint64, kNcclMax, u.comm, s);
   if (rc != 0)
     throw std::runtime_error(std::string("ncclAllReduce failed: ") + (rccl().errstr ? rccl().errstr(rc) : std::to_string(rc)));
 }
@@ -1155,7 +1171,7 @@ void SortedExchange::send(const SxSend& a) {
   self_copy_ = tn.sx_self_copy != 0;
   hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;
   const bool capturing = hipStreamIsCapturing(cs, &capst) == hipSuccess && capst != hipStreamCaptureStatusNone;
-  cur_comm_ = (comm_on_cs || (capturing && comm_)) ? cs : comm_stream_;
+  cur_comm_ = (comm_on_cs || (capturing && cell_)) ? cs : comm_stream_;
   pick_spec(cs);
   const PackedLayout L = L_;
   const int S = sx_round_S(L.S);

@@ -141,14 +141,15 @@ class SortedExchange {
     int32_t* perm = nullptr;
   };
   void pick_spec(hipStream_t cs);
+  void wait_event(hipEvent_t e) const;
   void adopt(const uint64_t* meta, int64_t from);
   // regions `stride` bytes apart; send[q] / recv[q] bytes of each (nullptr: whole regions)
   void a2a(const void* src, void* dst, size_t stride, const size_t* send, const size_t* recv, bool grouped_p2p);
   void allreduce_meta(uint64_t* dev, hipStream_t s);
-  bool collectives() const { return comm_ != nullptr || fake_ != nullptr; }
+  bool collectives() const { return cell_ != nullptr || fake_ != nullptr; }
 
   int device_;
-  void* comm_;
+  CommCell* cell_;  // the data plane's RCCL communicator (dp_link.hpp), or null
   std::shared_ptr<HostComm> fake_;
   int R_, rank_, chunks_;
   int64_t max_chunk_, C_alloc_;

@@ -227,6 +227,12 @@ void IpcComm::seal() { segs_[(size_t)rank_]->unlink_now(); }
 
 bool IpcComm::failed() const { return __atomic_load_n(host_failed_, __ATOMIC_ACQUIRE) != 0; }
 
+void IpcComm::abort() {
+  auto* mine = reinterpret_cast<uint64_t*>(static_cast<char*>(segs_[(size_t)rank_]->base()) + kIpcFailedOff);
+  __atomic_store_n(mine, 1ull, __ATOMIC_RELEASE);
+  __atomic_store_n(host_failed_, 1ull, __ATOMIC_RELEASE);
+}
+
 void IpcComm::check() const {
   if (failed())
     throw std::runtime_error("IpcComm: peer did not reach a collective within " + std::to_string(timeout_s_) +
@@ -303,6 +309,75 @@ void IpcComm::allreduce_max(int r, uint64_t* dev, int n, hipStream_t s) {
   IpcSizes sn{}, rn{};
   for (int q = 0; q < R_; ++q) sn.n[q] = (uint64_t)n * 8;
   op(dev, 0, nullptr, 0, sn, rn, s, dev, n);
+}
+
+// ---------------------------------------------------------------- DataPlane transport (dp_link.hpp)
+namespace {
+using IpcRef = std::shared_ptr<IpcComm>;
+IpcComm& ipc_of(void* h) { return **static_cast<IpcRef*>(h); }
+void put_err(char* err, size_t n, const char* m) {
+  if (err && n) {
+    strncpy(err, m, n - 1);
+    err[n - 1] = 0;
+  }
+}
+void* t_open(int device, int world, int rank, uint64_t cap, double timeout_s, const char* name, char* err, size_t n) {
+  try {
+    return new IpcRef(std::make_shared<IpcComm>(device, world, rank, (size_t)cap, timeout_s, std::string(name)));
+  } catch (const std::exception& e) {
+    put_err(err, n, e.what());
+    return nullptr;
+  }
+}
+int t_connect(void* h, const char* const* names, int count, char* err, size_t n) {
+  try {
+    ipc_of(h).connect(std::vector<std::string>(names, names + count));
+    return 0;
+  } catch (const std::exception& e) {
+    put_err(err, n, e.what());
+    return 1;
+  }
+}
+void t_seal(void* h) {
+  try {
+    ipc_of(h).seal();
+  } catch (const std::exception&) {
+  }
+}
+int t_allreduce(void* h, uint64_t* dev, int cnt, void* stream, char* err, size_t n) {
+  try {
+    IpcComm& c = ipc_of(h);
+    c.check();
+    c.allreduce_max(c.rank(), dev, cnt, (hipStream_t)stream);
+    return 0;
+  } catch (const std::exception& e) {
+    put_err(err, n, e.what());
+    return 1;
+  }
+}
+int t_alltoallv(void* h, const void* src, void* dst, size_t stride, const size_t* sb, const size_t* rb, void* stream,
+                char* err, size_t n) {
+  try {
+    IpcComm& c = ipc_of(h);
+    c.check();
+    c.alltoallv(c.rank(), src, dst, stride, sb, rb, (hipStream_t)stream);
+    return 0;
+  } catch (const std::exception& e) {
+    put_err(err, n, e.what());
+    return 1;
+  }
+}
+int t_failed(void* h) { return ipc_of(h).failed() ? 1 : 0; }
+void t_abort(void* h) { ipc_of(h).abort(); }
+uint64_t t_cap(void* h) { return (uint64_t)ipc_of(h).cap(); }
+void* t_engine_ref(void* h) { return new std::shared_ptr<HostComm>(*static_cast<IpcRef*>(h)); }
+void t_release(void* h) { delete static_cast<IpcRef*>(h); }
+}  // namespace
+
+const DpTransportOps* ipc_transport_ops() {
+  static const DpTransportOps ops{kDpTransportAbi, t_open,   t_connect, t_seal, t_allreduce, t_alltoallv,
+                                  t_failed,        t_abort,  t_cap,     t_engine_ref, t_release};
+  return &ops;
 }
 
 }  // namespace ptype

@@ -46,6 +46,7 @@
 #include <string>
 #include <vector>
 
+#include "dp_link.hpp"
 #include "engine.hpp"
 #include "shmring.hpp"
 
@@ -94,7 +95,10 @@ class IpcComm : public HostComm {
   void check() const override;
   const uint64_t* device_failed() const override { return dev_failed_; }
 
-  bool failed() const;           // a wait of this rank timed out (pinned host flag; no sync)
+  bool failed() const;           // a wait of this rank timed out, or abort() ran (pinned host flag; no sync)
+  // Fail this rank's comm now (the DataPlane aborting a generation): the waiting
+  // kernels poll the segment's failed word and exit; every later op skips its work.
+  void abort();
   uint64_t ops() const { return seq_; }
   int rank() const { return rank_; }
   size_t cap() const { return cap_; }
@@ -120,5 +124,9 @@ class IpcComm : public HostComm {
   std::vector<std::pair<hipStream_t, hipEvent_t>> last_op_;  // per stream used: an event after its last op
   bool connected_ = false;
 };
+
+// The DpTransportOps table (dp_link.hpp) through which the control plane's
+// DataPlane forms, drives and aborts IpcComm generations.
+const DpTransportOps* ipc_transport_ops();
 
 }  // namespace ptype

@@ -1,10 +1,10 @@
-"""Data-plane bootstrap through the replicated store.
+"""Data-plane bootstrap of CPU runtimes through the replicated store.
 
-The reference's ``Join`` makes a process a full cluster member with one call
-(cluster/cluster.go:28-84); here the data plane between the members' GPUs is
-a collective process group (RCCL over xGMI; gloo on CPU), and forming it needs
-a rendezvous.  It goes through the control plane the members already share --
-no external launcher, no torchrun:
+On a GPU the data plane is the compiled DataPlane (csrc/core/dataplane.cpp,
+``parallel.native_group``): RCCL over xGMI, or IpcComm, formed without any torch
+process group.  A CPU runtime (tests, GPU-less hosts) runs the same pipeline
+over a torch gloo group, formed the same way -- through the control plane the
+members already share, no external launcher, no torchrun:
 
 1. wait until ``world`` nodes of the service are registered (their 2 s leases
    are alive) -- the registry of cluster/registry.go:93-117;
@@ -12,10 +12,8 @@ no external launcher, no torchrun:
    ``{addr, port, members}`` under ``store/_ptype/nccl/<service>/<epoch>/<node>``;
    the record with the lowest create revision wins (``WithSort(SortByCreateRevision,
    SortAscend)``), so candidates with different views still converge;
-3. every member initialises the process group from that store with
-   ``rank = members.index(node)``; on a GPU the RCCL communicator is then built
-   by the first collective (``ncclCommInitRank`` underneath, unique id through
-   the store).
+3. every member initialises the gloo group from that store with
+   ``rank = members.index(node)``.
 
 ``ElasticDataPlane`` (parallel/elastic.py) forms every later generation the
 same way after a rank failure (epoch = generation).
@@ -69,8 +67,10 @@ def form_group(store, local_addr: str, me: str, service: str, epoch: int, propos
                device_for_rank: Callable[[int], torch.device | None] = lambda r: None, timeout_s: float = 10.0,
                rdv_timeout_s: float = 60.0):
     """Rendezvous ``proposal`` through ``store`` (a ``cluster.KVStore``) and
-    initialise the default process group.  Returns ``(members, tcp_store)``;
+    initialise the default (gloo) process group.  Returns ``(members, tcp_store)``;
     keep ``tcp_store`` alive for the group's lifetime (the master serves it)."""
+    if backend != "gloo":
+        raise ValueError("form_group forms gloo groups (CPU runtimes); GPU data planes are NativeGroups")
     from ..cluster import SortAscend, SortByCreateRevision, WithPrefix, WithSort, background
     from .elastic import Excluded
 
@@ -99,8 +99,6 @@ def form_group(store, local_addr: str, me: str, service: str, epoch: int, propos
     leader = rank == 0 and mine is not None and rec["port"] == mine.port
     tcp = mine if leader else dist.TCPStore(rec["addr"], int(rec["port"]), len(members), False,
                                             timeout=timedelta(seconds=rdv_timeout_s))
-    dev = device_for_rank(rank)
-    kw = {"device_id": dev} if backend == "nccl" and dev is not None else {}
     dist.init_process_group(backend, store=dist.PrefixStore(f"ptype/{service}/epoch{epoch}", tcp), rank=rank,
-                            world_size=len(members), timeout=timedelta(seconds=timeout_s), **kw)
+                            world_size=len(members), timeout=timedelta(seconds=timeout_s))
     return members, tcp

@@ -3,50 +3,43 @@
 SURVEY 5.3.  The reference detects failed service nodes by **lease expiry**
 (2 s TTL + KeepAlive, cluster/registry.go:59-83) observed through a watch, and
 clients re-balance onto the survivors (cluster/rpc.go:197-244).  The data plane
-here is a set of collective process groups (RCCL over xGMI on MI355X, gloo on
-CPU), and a collective with a dead peer fails (gloo: connection reset / timeout;
-RCCL: the watchdog aborts the communicator with
-``TORCH_NCCL_ASYNC_ERROR_HANDLING=2``).  RCCL is not fault tolerant, so a group is
-never repaired in place -- it is aborted and a new *generation* is formed:
+is a communicator over the service's GPUs (RCCL over xGMI, or IpcComm between
+the processes of one GPU) and a collective with a dead peer fails or stalls.
+RCCL is not fault tolerant, so a generation is never repaired in place -- it is
+aborted and a new one formed:
 
-1. ``send`` fails -> the survivor aborts its group (a compiled ``NativeGroup``:
-   ``ncclCommAbort`` in csrc/core/dataplane.cpp; a torch group:
-   ``_abort_process_group``),
+1. ``send`` fails (a peer's failure, or the Send watchdog's deadline) -> the
+   survivor aborts the generation,
 2. waits until the control plane's lease-based membership (the service's
    registry nodes) drops the dead node (bounded by ``grace_s``),
-3. re-rendezvouses through the replicated KV store (``bootstrap.form_group``,
-   the same path ``Join`` forms epoch 0 with): the lowest surviving node opens a
-   TCPStore and publishes ``_ptype/nccl/<svc>/<gen>/<node>`` ``{addr, port,
-   members}``; the record with the lowest create revision wins
-   (``WithSort(SortByCreateRevision, SortAscend)``), so concurrent candidates
-   with different views still converge on one member list,
+3. re-rendezvouses through the replicated KV store: the record with the lowest
+   create revision under ``_ptype/nccl/<svc>/<gen>/`` wins, so candidates with
+   different views still converge on one member list,
 4. re-homes the dead rank's actors by a deterministic ring adoption (the next
    surviving original rank adopts them into extra mailbox blocks; actors of live
    ranks never move and keep their state), rebuilds the GPU registry mirror, and
-5. the caller's batch is re-sent (``send_resilient``): delivery is
-   at-least-once, as with the reference's client retries (rpc.go:107-116).
+5. the caller's batch is re-sent: delivery is at-least-once, as with the
+   reference client's retries (rpc.go:107-116).
 
-The same recovery runs underneath ``Join -> NewClient -> Send``: the
-``DeviceRuntime`` of a group Join formed is elastic (runtime.py ``send`` /
-``recover`` / ``replicate``, built from the helpers below: ``abort_group``,
-``settle_membership``, ``ring_placement``, ``buddy``, ``lost_blocks`` and the
-``SendWatchdog`` that bounds an RCCL Send's device work).  ``ElasticDataPlane``
-is the standalone form (its own table and exchange, no registry mirror).
+On a GPU every step of that is compiled: ``_core.DataPlane``
+(csrc/core/dataplane.cpp: watchdog thread, abort, settle, form, ring adoption,
+buddies, replica moves), driven through ``NativeGroup``.  A CPU runtime (gloo,
+for tests and GPU-less hosts) runs the same steps with the Python helpers below
+(``settle_membership``, ``ring_placement``, ``buddy``, ``lost_blocks``) over a
+torch gloo group re-formed by ``bootstrap.form_group``.  ``ElasticDataPlane`` is
+the standalone form (its own table and exchange, no registry mirror).
 
 Actor state survives a rank loss through **buddy replicas** kept in HBM:
-``replicate()`` (collective; also run every ``replicate_every`` sends) ships
-every block a node hosts to its *buddy* -- the next surviving node after it in
-the original ring -- with one ``ncclSend``/``ncclRecv`` pair per neighbour
-(``batch_isend_irecv``: a point-to-point xGMI copy, no collective over the whole
-group).  The buddy is by construction the node ``ring_placement`` makes adopt
-those blocks if their host dies, so an adopted block resumes from its replica
-(the state as of the last ``replicate``); a block with no replica (two
-neighbours lost at once) restarts from zero.  The control plane itself survives
-the loss of a minority of members (Raft quorum).
+``replicate()`` (collective; also every ``replicate_every`` sends) ships every
+block a node hosts to its *buddy* -- the next surviving node after it in the
+original ring, by construction the node ``ring_placement`` makes adopt those
+blocks -- with one send / receive pair per neighbour.  An adopted block resumes
+from its replica; a block with no replica (two neighbours lost at once) restarts
+from zero.  The control plane itself survives the loss of a minority of members
+(Raft quorum).
 """
 from __future__ import annotations
 
-import os
 import time
 
 import torch
@@ -123,17 +116,12 @@ def buddy(nodes0: list[str], members: list[str], node: str) -> str:
 
 
 def abort_group() -> None:
-    """Abort the default process group (a failed generation): RCCL's
-    communicator is aborted (kernels spinning on a dead peer return), gloo's
-    pairs are closed.  Never raises."""
+    """Tear down a gloo group of a failed generation (CPU runtimes).  Never raises."""
     if dist.is_initialized():
         try:
-            dist.distributed_c10d._abort_process_group()
+            dist.destroy_process_group()
         except Exception:
-            try:
-                dist.destroy_process_group()
-            except Exception:
-                pass
+            pass
 
 
 def settle_membership(alive, members: list[str], me: str, grace_s: float) -> list[str]:
@@ -160,90 +148,15 @@ def lost_blocks(nodes0: list[str], before: list[str], after: list[str]) -> list[
     return sorted(r for n in gone for r in own.get(n, []))
 
 
-class SendWatchdog:
-    """Bounds how long a Send may stay incomplete (RCCL over xGMI has no timeout
-    of its own for the engine's collectives, which are issued on the group's
-    communicator outside torch's watchdog).  ``begin()`` / ``end()`` bracket the
-    host part of a Send (a host wait on a collective whose peer died would never
-    return), ``arm(event)`` after it covers its device work; a daemon thread
-    polls both and, when one is overdue, calls ``abort`` -- the communicator is
-    aborted, so RCCL kernels and host waits on a dead peer return -- and marks the
-    generation failed: the Send (or the next one) raises and recovers.  ``abort``
-    is the default process group's (``abort_group``) or a compiled
-    ``NativeGroup``'s ``ncclCommAbort``."""
-
-    def __init__(self, timeout_s: float, poll_s: float = 0.05, abort=None):
-        import threading
-
-        self.timeout_s, self.poll_s = float(timeout_s), float(poll_s)
-        self.abort = abort if abort is not None else abort_group
-        self.failed: str | None = None
-        self._q: list[tuple[object, float]] = []
-        self._host_deadline: float | None = None
-        self._lock = threading.Lock()
-        self._stop = threading.Event()
-        self._th = threading.Thread(target=self._run, daemon=True, name="ptype-send-watchdog")
-        self._th.start()
-
-    def begin(self) -> None:
-        self._host_deadline = time.monotonic() + self.timeout_s
-
-    def end(self) -> None:
-        self._host_deadline = None
-
-    def arm(self, event) -> None:
-        with self._lock:
-            self._q.append((event, time.monotonic() + self.timeout_s))
-            if len(self._q) > 64:  # completed events are dropped by the thread; bound the backlog anyway
-                self._q = [x for x in self._q if not x[0].query()]
-
-    def reset(self) -> None:
-        with self._lock:
-            self._q = []
-        self._host_deadline = None
-        self.failed = None
-
-    def _fail(self, why: str) -> None:
-        if self.failed is None:
-            self.failed = why
-            try:
-                self.abort()
-            except Exception:
-                pass
-
-    def _run(self) -> None:
-        while not self._stop.wait(self.poll_s):
-            with self._lock:
-                q = self._q
-            now = time.monotonic()
-            hd = self._host_deadline
-            if hd is not None and now > hd:
-                self._fail(f"a Send did not return within {self.timeout_s:.1f} s")
-            keep = []
-            for ev, dl in q:
-                if ev.query():
-                    continue
-                if now > dl:
-                    self._fail(f"a Send's device work did not complete within {self.timeout_s:.1f} s")
-                keep.append((ev, dl))
-            with self._lock:
-                if self._q is q:
-                    self._q = keep
-                else:  # armed meanwhile
-                    self._q = keep + self._q[len(q):]
-
-    def close(self) -> None:
-        self._stop.set()
-        self._th.join(1.0)
-
-
 class ElasticDataPlane:
-    """Batched ``Send`` over a self-healing process group.
+    """Batched ``Send`` over a self-healing data plane.
 
     ``cluster`` is a joined ``ptype_amd.cluster.Cluster`` (its node is
     registered under ``service``); ``world`` the number of data-plane ranks
     expected at start; ``per_rank`` actors hosted per original rank (actor ``a``
-    belongs to original rank ``a % world``, mailbox ``a // world``).
+    belongs to original rank ``a % world``, mailbox ``a // world``).  On a GPU
+    the generations are the compiled DataPlane's (``NativeGroup``: ``backend``
+    "native", RCCL); on the CPU a torch gloo group.
     """
 
     def __init__(self, cluster, service: str, world: int, per_rank: int, device=None, backend: str | None = None,
@@ -254,7 +167,9 @@ class ElasticDataPlane:
         self.world0 = int(world)
         self.per_rank = int(per_rank)
         self.device = torch.device(device) if device is not None else torch.device("cpu")
-        self.backend = backend or ("nccl" if self.device.type == "cuda" else "gloo")
+        self.backend = backend or ("native" if self.device.type == "cuda" else "gloo")
+        if self.backend not in ("native", "gloo"):
+            raise ValueError("backend: 'native' (the compiled DataPlane, GPU) or 'gloo' (CPU)")
         self.max_batch = int(max_batch)
         self.chunks = int(chunks)
         self.timeout_s = float(timeout_s)
@@ -268,15 +183,13 @@ class ElasticDataPlane:
         self.state: torch.Tensor | None = None
         self.table: RegistryTable | None = None
         self.exchange: ActorExchange | None = None
+        self.group = None  # NativeGroup (backend "native")
         self._tcp_store = None
         self.recoveries = 0
         self.replicate_every = int(replicate_every)
         self.replicas: dict[int, torch.Tensor] = {}  # original rank -> its block as of the last replicate()
         self.restored: list[int] = []  # blocks the last re-formation resumed from a replica
         self._sends = 0
-        if self.backend == "nccl":
-            # abort the communicator and raise instead of tearing the process down
-            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
 
     # ------------------------------------------------------------------ membership
     def alive(self, timeout_s: float = 30.0) -> list[str]:
@@ -288,6 +201,15 @@ class ElasticDataPlane:
 
     def start(self) -> None:
         """Wait for ``world`` registered nodes and form generation 0."""
+        if self.backend == "native":
+            from .native_group import NativeGroup
+
+            self.group = NativeGroup.join(self.cluster._c, self.service, self.me, lambda r: self.device, self.world0,
+                                          timeout_s=self.rdv_timeout_s)
+            self.nodes0 = list(self.group.dp.nodes0)
+            self.gen, self.members = self.group.gen, self.group.members
+            self._rebuild(dict(self.group.dp.placement(self.members)))
+            return
         deadline = time.monotonic() + self.rdv_timeout_s
         while True:
             nodes = self.alive()
@@ -305,17 +227,16 @@ class ElasticDataPlane:
         from .bootstrap import form_group
 
         members, store = form_group(self.cluster.Store, self.cluster.local_addr, self.me, self.service, gen,
-                                    proposal, self.backend, lambda r: self.device if self.backend == "nccl" else None,
+                                    proposal, self.backend, lambda r: None,
                                     timeout_s=self.timeout_s, rdv_timeout_s=self.rdv_timeout_s)
         self._tcp_store = store  # the master keeps the store alive for the group's lifetime
         self.gen, self.members = gen, members
-        self._rebuild()
+        self._rebuild(ring_placement(self.nodes0, self.members))
 
     # ------------------------------------------------------------------ placement
-    def _rebuild(self) -> None:
-        own = ring_placement(self.nodes0, self.members)
+    def _rebuild(self, own: dict) -> None:
         W0, P = self.world0, self.per_rank
-        new_blocks = own[self.me]
+        new_blocks = list(own[self.me])
         state = torch.zeros(P * len(new_blocks), dtype=torch.int64, device=self.device)
         self.restored = []
         if self.state is not None:  # actors that stay here keep their state
@@ -337,7 +258,7 @@ class ElasticDataPlane:
                 table.upsert(actor_keys(ids), torch.full((P,), rank, dtype=torch.int32), (j * P + k).to(torch.int32))
         table.enable_directory(W0 * P, affine_world=W0)
         self.table = table
-        self.exchange = ActorExchange(table, self.max_batch, chunks=self.chunks, state=self.state)
+        self.exchange = ActorExchange(table, self.max_batch, chunks=self.chunks, state=self.state, group=self.group)
 
     @property
     def total_actors(self) -> int:
@@ -377,38 +298,52 @@ class ElasticDataPlane:
         """Collective over the current generation: every node sends the blocks
         it hosts to its buddy and keeps the blocks of the node whose buddy it is,
         as resident device tensors.  Point-to-point only (two neighbours)."""
-        own = ring_placement(self.nodes0, self.members)
-        dst = buddy(self.nodes0, self.members, self.me)
-        if dst == self.me:  # alone: nothing can adopt these blocks
-            return
-        src = next(n for n in self.members if buddy(self.nodes0, self.members, n) == self.me)
         P = self.per_rank
-        recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=self.device)
-        ops = [dist.P2POp(dist.isend, self.state, self.members.index(dst)),
-               dist.P2POp(dist.irecv, recv, self.members.index(src))]
         try:
+            if self.group is not None:
+                dp = self.group.dp
+                src_blocks = list(dp.replica_blocks())
+                recv = torch.empty(max(1, P * len(src_blocks)), dtype=torch.int64, device=self.device)
+                torch.cuda.current_stream(self.device).synchronize()
+                got = list(dp.replicate(self.state.data_ptr(), self.state.numel() * 8, recv.data_ptr(),
+                                        P * len(src_blocks) * 8))
+                self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(got)}
+                return
+            own = ring_placement(self.nodes0, self.members)
+            dst = buddy(self.nodes0, self.members, self.me)
+            if dst == self.me:  # alone: nothing can adopt these blocks
+                return
+            src = next(n for n in self.members if buddy(self.nodes0, self.members, n) == self.me)
+            recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=self.device)
+            ops = [dist.P2POp(dist.isend, self.state, self.members.index(dst)),
+                   dist.P2POp(dist.irecv, recv, self.members.index(src))]
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+            self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(own[src])}
         except Exception as e:
             raise RankFailure(f"generation {self.gen}: replicate: {e}") from e
-        self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(own[src])}
 
     def recover(self) -> None:
         """Abort the failed generation, wait for the lease-driven membership to
         settle, form the next generation from the survivors, re-home actors."""
-        self._abort()
-        proposal = settle_membership(self.alive, self.members, self.me, self.grace_s)
+        self.exchange = None
         self.recoveries += 1
+        if self.group is not None:  # compiled: abort, settle, form, ring adoption
+            plan = self.group.recover(self.grace_s)
+            self.gen, self.members = self.group.gen, list(plan["members"])
+            self._rebuild(dict(self.group.dp.placement(self.members)))
+            return
+        abort_group()
+        proposal = settle_membership(self.alive, self.members, self.me, self.grace_s)
         self._form(self.gen + 1, proposal)
 
-    def _abort(self) -> None:
-        abort_group()
-        self.exchange = None
-
     def close(self) -> None:
+        if self.group is not None:
+            self.group.close()
+            self.group = None
         if dist.is_initialized():
             try:
                 dist.destroy_process_group()
             except Exception:
-                self._abort()
+                pass
         self._tcp_store = None

@@ -20,13 +20,18 @@ actors = 2M slots = 32 MB of HBM).  ``mirror.RegistryMirror`` follows those
 records (watch + lease expiry) into the table; with ``gpu.world > 1`` Join
 forms the data-plane group through the store first (parallel/bootstrap.py).
 
-Rank failures.  A runtime whose group Join formed is elastic:
-when a Send's collective fails (gloo: reset / timeout; RCCL: the send watchdog
-aborts a communicator whose work is overdue), the runtime aborts the group,
-waits for the registry's lease-based membership to drop the dead node, forms
-generation g + 1 of the group through the store (bootstrap.form_group), re-homes
-the dead rank's actors onto its ring successor (state from the buddy replica
-``replicate()`` keeps, else zero), republishes its shard record and re-sends:
+Rank failures.  A runtime whose group Join formed is elastic.  On
+a GPU the group is the compiled DataPlane (``NativeGroup``: RCCL, or IpcComm
+between the processes of one GPU) and the whole lifecycle is its: the Send
+watchdog (a C++ thread) fails a generation whose Send is overdue, ``recover``
+is one call -- abort, lease-driven settle, generation g + 1 through the store,
+ring adoption of the lost ranks' blocks -- and ``replicate`` moves buddy
+replicas; this module only applies the DataPlane's plan to its tensors (the
+state blocks, the registry table, the dispatcher).  A CPU runtime (gloo)
+re-forms its torch group the same way (bootstrap.form_group, elastic.py
+helpers).  Either way the dead rank's actors move to their ring successor
+(state from the buddy replica, else zero), the shard record is republished and
+the Send is re-sent:
 ``send_all`` re-sends the whole batch (at-least-once, like the reference
 client's retries, cluster/rpc.go:107-116); ``send(..., resend_overflow=False)``
 answers the messages whose actor lived on the lost rank with
@@ -117,7 +122,7 @@ class DeviceRuntime:
         self.recoveries = 0
         self.replicate_every = 0
         self._sends = 0
-        self._watchdog = None
+        self._cpu_failed = None  # a CPU runtime's failed generation (fail_generation)
         self.mailbox_shards, self.mailbox_slots = int(mailbox_shards), int(mailbox_slots)
         self.delivery = delivery or "auto"  # "mailbox": every Send through the HBM mailboxes (ActorExchange)
         # N > 1 collectives: the group's RCCL communicator, or IpcComm ("ipc": shared-memory
@@ -162,20 +167,23 @@ class DeviceRuntime:
 
             me = node_id(core_cluster.local_addr, cfg.port)
             registry = Registry(core_cluster.registry)
-            backend = g.backend or ("gloo" if g.cpu or g.comm == "ipc" else "nccl")
             store = KVStore(core_cluster.store)
-            from .parallel.native_group import NativeGroup
+            if not g.cpu:
+                # the group's whole lifecycle in the control plane (csrc/core/dataplane.hpp): store
+                # rendezvous, RCCL init (or IpcComm segments: gpu.comm ipc), abort, next generation
+                from .parallel.exchange import ipc_cap_for
+                from .parallel.native_group import NativeGroup
 
-            if backend == "nccl" and g.native_group and NativeGroup.available():
-                # the RCCL communicator's whole lifecycle in the control plane (csrc/core/dataplane.hpp):
-                # unique id through the replicated store, ncclCommInitRank -- no torch process group
-                native = NativeGroup.join(core_cluster, cfg.service_name, me, device_for_rank, max(g.world, 1),
-                                          timeout_s=max(30.0, g.group_timeout_s))
+                world = max(g.world, 1)
+                chunks = 1 if world == 1 else 2
+                native = NativeGroup.join(core_cluster, cfg.service_name, me, device_for_rank, world,
+                                          timeout_s=max(30.0, g.group_timeout_s), transport=g.comm,
+                                          cap_bytes=ipc_cap_for(g.max_batch, chunks, world) if g.comm == "ipc" else 0)
                 members = native.members
+                backend = "native"
             else:
+                backend = g.backend or "gloo"
                 nodes = wait_nodes(registry, cfg.service_name, max(g.world, 1))
-                if backend == "nccl":  # a failed collective aborts the communicator instead of the process
-                    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
                 members, tcp = form_group(store, core_cluster.local_addr, me, cfg.service_name, 0, nodes, backend,
                                           device_for_rank, timeout_s=g.group_timeout_s)
             owns = True
@@ -193,10 +201,8 @@ class DeviceRuntime:
                                "backend": backend, "timeout_s": g.group_timeout_s, "grace_s": g.grace_s,
                                "max_recoveries": 3}
             rt.replicate_every = int(g.replicate_every)
-            if g.send_timeout_s > 0:  # (arms device events on a GPU; on the host it only carries a failure flag)
-                from .parallel.elastic import SendWatchdog
-
-                rt._watchdog = SendWatchdog(g.send_timeout_s, abort=rt._abort_generation)
+            if g.send_timeout_s > 0 and native is not None:  # the DataPlane's watchdog thread (C++)
+                native.dp.set_watchdog(float(g.send_timeout_s))
         rt.attach(core_cluster.registry.kv, cfg.service_name, cfg.node_name, watch=g.watch)
         # Send needs every rank's routes: wait until all shards of the group are mirrored
         rt.mirror.wait_shards(rt.world)
@@ -348,22 +354,23 @@ class DeviceRuntime:
             return ex.send_all(batch, defer=self.world > 1) if resend_overflow else ex.send(batch)
         from .parallel.elastic import RankFailure, is_rank_failure
 
+        dp = self.group.dp if self._native else None  # the compiled lifecycle (watchdog, recovery)
         lost_before: list[int] = []
         todo = None  # after a recovery without re-sends: the indices still to deliver
         for attempt in range(self._elastic_cfg["max_recoveries"] + 1):
             try:
-                if self._watchdog is not None and self._watchdog.failed:
-                    raise RankFailure(self._watchdog.failed)
+                if self._failed():
+                    raise RankFailure(self._failed())
                 sub = batch if todo is None else batch.index_select(todo)
-                if self._watchdog is not None:
-                    self._watchdog.begin()  # the host part of the Send is bounded too
+                if dp is not None:
+                    dp.begin_send()  # the host part of the Send is bounded too
                 try:
                     out = self.exchange.send_all(sub) if resend_overflow else self.exchange.send(sub)
                 finally:
-                    if self._watchdog is not None:
-                        self._watchdog.end()
-                if self._watchdog is not None and self._watchdog.failed:  # aborted mid-Send: its replies are void
-                    raise RankFailure(self._watchdog.failed)
+                    if dp is not None:
+                        dp.end_send()
+                if dp is not None and dp.watchdog_failed:  # aborted mid-Send: its replies are void
+                    raise RankFailure(dp.watchdog_failed)
                 ipc = self.exchange.ipc
                 if ipc is not None:  # IpcComm: a peer that missed a collective is seen once the Send's waits end
                     torch.cuda.current_stream(self.device).synchronize()
@@ -386,10 +393,8 @@ class DeviceRuntime:
                     todo = torch.nonzero(~lost).flatten()
                 continue
             self._sends += 1
-            if self._watchdog is not None and self.on_gpu:
-                ev = torch.cuda.Event()
-                ev.record()
-                self._watchdog.arm(ev)
+            if dp is not None and self.on_gpu:  # the Send's device work must finish in time
+                dp.arm(torch.cuda.current_stream(self.device).cuda_stream)
             if self.replicate_every and self._sends % self.replicate_every == 0:
                 try:
                     self.replicate()
@@ -406,6 +411,18 @@ class DeviceRuntime:
             return (val, st) + tuple(out[2:])
         raise AssertionError("unreachable")
 
+    def _failed(self) -> str:
+        """Why the current generation was failed ("" while fine)."""
+        return self.group.dp.watchdog_failed if self._native else (self._cpu_failed or "")
+
+    def fail_generation(self, why: str) -> None:
+        """Mark the current generation failed, as the Send watchdog does: the next
+        Send recovers (fault injection of the tests)."""
+        if self._native:
+            self.group.dp.fail_generation(why)
+        else:
+            self._cpu_failed = why
+
     def flush(self) -> None:
         """Every earlier Send's replies final (deferred re-sends run now).  Collective."""
         if getattr(self, "_exchange", None) is not None:
@@ -414,8 +431,9 @@ class DeviceRuntime:
     # ------------------------------------------------------------------ rank failures
     def replicate(self) -> None:
         """Collective over the current generation: every rank ships the blocks it
-        hosts to its buddy (the node that would adopt them, elastic.buddy) and
-        keeps the blocks it is buddy of, resident in HBM.  Point-to-point only."""
+        hosts to its buddy (the node that would adopt them) and keeps the blocks it
+        is buddy of, resident in HBM.  Point-to-point only.  On a GPU the DataPlane
+        picks the buddies and moves the bytes (csrc/core/dataplane.cpp replicate)."""
         import torch.distributed as dist
 
         from .parallel.elastic import buddy, ring_placement
@@ -423,26 +441,27 @@ class DeviceRuntime:
         m = self.membership
         if m is None:
             return
+        P = self.actors
+        if self._native:
+            dp = self.group.dp
+            src_blocks = list(dp.replica_blocks())
+            recv = torch.empty(max(1, P * len(src_blocks)), dtype=torch.int64, device=self.device)
+            torch.cuda.current_stream(self.device).synchronize()  # the state's producers are done
+            st = self.state.contiguous()
+            got = list(dp.replicate(st.data_ptr(), st.numel() * 8, recv.data_ptr(), P * len(src_blocks) * 8))
+            self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(got)}
+            return
         own = ring_placement(m["nodes0"], m["members"])
         dst = buddy(m["nodes0"], m["members"], m["me"])
         if dst == m["me"]:
             return
         src = next(n for n in m["members"] if buddy(m["nodes0"], m["members"], n) == m["me"])
-        P = self.actors
-        if self._native:  # the compiled group's ncclSend / ncclRecv pair (csrc/core/dataplane.cpp)
-            recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=self.device)
-            self.group.sendrecv(self.state.contiguous(), m["members"].index(dst), recv, m["members"].index(src))
-            self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(own[src])}
-            return
-        # a gloo group (CPU runtimes, comm="ipc") moves host tensors
-        host = self.on_gpu and dist.get_backend(self.group) == "gloo"
-        io_dev = torch.device("cpu") if host else self.device
-        recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=io_dev)
-        ops = [dist.P2POp(dist.isend, self.state.to(io_dev), m["members"].index(dst)),
+        # a gloo group (CPU runtimes) moves host tensors
+        recv = torch.empty(P * len(own[src]), dtype=torch.int64, device=self.device)
+        ops = [dist.P2POp(dist.isend, self.state, m["members"].index(dst)),
                dist.P2POp(dist.irecv, recv, m["members"].index(src))]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-        recv = recv.to(self.device)
         self.replicas = {r: recv[j * P:(j + 1) * P] for j, r in enumerate(own[src])}
 
     def recover(self) -> list[int]:
@@ -450,9 +469,7 @@ class DeviceRuntime:
         form the next generation through the store and re-home the lost ranks'
         actors.  Returns the original ranks that were lost."""
         from .parallel.bootstrap import alive_nodes, form_group
-        from .parallel.elastic import lost_blocks, settle_membership
-
-        from .parallel.elastic import Excluded
+        from .parallel.elastic import Excluded, lost_blocks, ring_placement, settle_membership
 
         m, c = self.membership, self._elastic_cfg
         if m is None:
@@ -464,30 +481,36 @@ class DeviceRuntime:
             _log.warning("recover: %d deferred Send(s) of generation %d left unresolved (STATUS_OVERFLOW)",
                          self._exchange.drop_pending(), m["gen"])
         self._exchange = None
-        if self._watchdog is not None:
-            self._watchdog.reset()
         if self._native:
-            # the compiled lifecycle: lease-driven proposal, the first current record
-            # in the store wins, ncclCommInitRank of the next generation
-            proposal = self.group.dp.settle(m["members"], float(c["grace_s"]))
+            # the compiled lifecycle: abort, lease-driven settle, the first current record in
+            # the store wins, the next generation's communicator, ring adoption
+            dp = self.group.dp
             try:
-                self.group.form(m["gen"] + 1, proposal)
+                plan = self.group.recover(float(c["grace_s"]))
             except RuntimeError as e:
                 if "excluded" in str(e):
                     raise Excluded(str(e)) from e
                 raise
-            members = self.group.members
+            dp.reset_watchdog()
+            lost = list(plan["lost"])
+            m["members"], m["gen"] = list(plan["members"]), m["gen"] + 1
+            self.rank, self.world = self.group.rank, self.group.size
+            own = {n: list(rs) for n, rs in dict(dp.placement(m["members"])).items()}
+            self._rehome(own, list(plan["blocks"]), list(plan["kept_from"]), list(plan["from_replica"]))
         else:
             proposal = settle_membership(lambda: alive_nodes(c["registry"], self.service), m["members"], m["me"],
                                          c["grace_s"])
             members, tcp = form_group(c["store"], c["local_addr"], m["me"], self.service, m["gen"] + 1, proposal,
-                                      c["backend"], lambda r: self.device if c["backend"] == "nccl" else None,
-                                      timeout_s=c["timeout_s"])
+                                      c["backend"], lambda r: None, timeout_s=c["timeout_s"])
             self._tcp_store = tcp
-        lost = lost_blocks(m["nodes0"], m["members"], members)
-        m["members"], m["gen"] = list(members), m["gen"] + 1
-        self.rank, self.world = members.index(m["me"]), len(members)
-        self._rehome()
+            self._cpu_failed = None
+            lost = lost_blocks(m["nodes0"], m["members"], members)
+            m["members"], m["gen"] = list(members), m["gen"] + 1
+            self.rank, self.world = members.index(m["me"]), len(members)
+            own = ring_placement(m["nodes0"], m["members"])
+            nb = own[m["me"]]
+            kept = [self.blocks.index(r) if r in self.blocks else -1 for r in nb]
+            self._rehome(own, nb, kept, [k < 0 and r in self.replicas for r, k in zip(nb, kept)])
         self.recoveries += 1
         _log.warning("data-plane generation %d formed: world %d, lost original ranks %s, hosting %s", m["gen"],
                      self.world, lost, self.blocks)
@@ -500,7 +523,7 @@ class DeviceRuntime:
         return self.group is not None and hasattr(self.group, "comm_ptr")
 
     def _abort_generation(self) -> None:
-        """Abort the current data-plane generation (any thread; never raises)."""
+        """Abort the current data-plane generation (never raises)."""
         if self._native:
             try:
                 self.group.abort()
@@ -511,26 +534,21 @@ class DeviceRuntime:
 
             abort_group()
 
-    def _rehome(self) -> None:
-        """Placement of the current generation (elastic.ring_placement): keep the
-        state of blocks that stay, adopt lost blocks from their replicas, rebuild
-        the registry table and the dispatcher, republish this rank's record."""
-        from .parallel.elastic import ring_placement
-
+    def _rehome(self, own: dict, new_blocks: list, kept_from: list, from_replica: list) -> None:
+        """Apply a placement: keep the state of blocks that stay, adopt lost blocks
+        from their replicas (else zero), rebuild the registry table and the
+        dispatcher, republish this rank's record.  ``own``: node -> original ranks."""
         m = self.membership
-        own = ring_placement(m["nodes0"], m["members"])
         P, W0 = self.actors, self.world0
-        new_blocks = own[m["me"]]
         state = torch.zeros(P * len(new_blocks), dtype=torch.int64, device=self.device)
         self.restored = []
-        for j, r in enumerate(new_blocks):
-            if r in self.blocks:
-                i = self.blocks.index(r)
-                state[j * P:(j + 1) * P] = self.state[i * P:(i + 1) * P]
-            elif r in self.replicas:
+        for j, (r, k, rep) in enumerate(zip(new_blocks, kept_from, from_replica)):
+            if k >= 0:
+                state[j * P:(j + 1) * P] = self.state[k * P:(k + 1) * P]
+            elif rep and r in self.replicas:
                 state[j * P:(j + 1) * P] = self.replicas[r]
                 self.restored.append(r)
-        self.blocks, self.state, self.replicas = new_blocks, state, {}
+        self.blocks, self.state, self.replicas = list(new_blocks), state, {}
         self.table.clear()
         k = torch.arange(P, dtype=torch.int64)
         for node, rs in own.items():
@@ -718,8 +736,6 @@ class DeviceRuntime:
                 self._exchange.flush()
             except Exception as e:  # noqa: BLE001
                 _log.warning("close: deferred re-sends not resolved: %s", str(e)[:300])
-        if self._watchdog is not None:
-            self._watchdog.close()
         for lease in getattr(self, "_replica_leases", {}).values():
             lease.close()
         if self.mirror is not None:
@@ -729,7 +745,7 @@ class DeviceRuntime:
         if self.server is not None:
             self.server.close()
         if self._owns_group and self._native:
-            self.group.abort()  # ncclCommAbort: never waits on a member that may be gone
+            self.group.close()  # abort: never waits on a member that may be gone
         elif self._owns_group:
             import torch.distributed as dist
 

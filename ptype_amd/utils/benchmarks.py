@@ -31,6 +31,67 @@ def _sync(device):
         torch.cuda.synchronize(device)
 
 
+def static_ports(rank: int, world: int, offset: int) -> tuple[int, int, int, str]:
+    """(peer port, client port, service port, initial-cluster string) of rank
+    ``rank`` in a static ``world``-member cluster on 127.0.0.1 that every rank
+    derives alike from MASTER_PORT (+ ``offset``: one cluster per purpose)."""
+    base = int(os.environ.get("MASTER_PORT", "29500")) + offset
+    if base + 3 * world >= 65536:
+        base = 20000 + base % 20000
+    pp, pc, port = base + 2 * rank, base + 2 * rank + 1, base + 2 * world + rank
+    initial = ",".join(f"b{r}=http://127.0.0.1:{base + 2 * r}" for r in range(world))
+    return pp, pc, port, initial
+
+
+def bench_group(device, rank: int, world: int, comm: str = "rccl", cap_bytes: int = 0, service: str = "bench",
+                offset: int = 211, timeout_s: float = 120.0):
+    """The bench's data plane at N > 1 the way ``Join`` forms it: a control-plane
+    member per rank (a static cluster on 127.0.0.1), and the compiled DataPlane's
+    communicator over the service's registered nodes -- RCCL, or IpcComm for a
+    one-GPU rehearsal -- with no torch process group (reference
+    cluster/cluster.go:28-84).  Returns ``(cluster, NativeGroup)``."""
+    from .. import cluster as C
+    from ..parallel.native_group import NativeGroup
+
+    os.environ.setdefault("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
+    pp, pc, port, initial = static_ports(rank, world, offset)
+    cfg = C.Config()
+    cfg.service_name, cfg.node_name, cfg.port = service, f"r{rank}", port
+    cfg.member = C.member_config(name=f"b{rank}", dir=tempfile.mkdtemp(prefix="ptype_benchdp_"),
+                                 lpurls=[f"http://127.0.0.1:{pp}"], apurls=[f"http://127.0.0.1:{pp}"],
+                                 lcurls=[f"http://127.0.0.1:{pc}"], acurls=[f"http://127.0.0.1:{pc}"],
+                                 initial_cluster=initial, unsafe_no_fsync=True)
+    c = C.Join(C.background(), cfg, runtime=False)
+    try:
+        g = NativeGroup.join(c._c, service, f"{c._c.local_addr}:{port}", lambda r: device, world,
+                             timeout_s=timeout_s, transport=comm, cap_bytes=cap_bytes)
+    except Exception:
+        c.Close()
+        raise
+    if g.rank != rank:  # (ranks follow the sorted node ids: the same order as RANK)
+        raise RuntimeError(f"data-plane rank {g.rank} != launcher rank {rank}")
+    return c, g
+
+
+def kv_barrier(cluster, key: str, world: int, timeout_s: float = 120.0) -> None:
+    """A host-side barrier through the replicated store: no collective kernel on
+    any GPU while it waits (peers' dispatchers may need to launch meanwhile)."""
+    from .. import cluster as C
+
+    rank = int(os.environ.get("RANK", "0"))
+    st = cluster.Store
+    st.Put(C.background(), f"_barrier/{key}/{rank}", "1")
+    t_end = time.monotonic() + timeout_s
+    while time.monotonic() < t_end:
+        try:
+            if len(st.Get(C.background(), f"_barrier/{key}/", C.WithPrefix(), C.WithKeysOnly())) >= world:
+                return
+        except Exception:  # (ErrNoKey before the first put lands)
+            pass
+        time.sleep(0.002)
+    raise TimeoutError(f"kv_barrier {key}: not every rank arrived")
+
+
 def timed(step, steps: int, warmup: int, device, barrier=None) -> float:
     """Seconds for ``steps`` calls of ``step`` after ``warmup`` untimed ones."""
     for _ in range(warmup):
@@ -108,7 +169,7 @@ def registry_1m(device, n: int = 1 << 20, reps: int = 5) -> dict:
 # ---------------------------------------------------------------------------- config 4
 def optimus_fanout(table, n_actors: int, device, steps: int, warmup: int, rank: int = 0, world: int = 1,
                    targets: int = 1024, base: int = 80_001, chunks: int = 1, comm: str = "rccl", barrier=None,
-                   max_over_ranks=None, sets: int = 3) -> dict:
+                   max_over_ranks=None, sets: int = 3, group=None) -> dict:
     """``targets`` odd numbers per rank and set (distinct per rank and set), every
     one split into 10-wide ranges and answered by the Prime.Check actors of the
     whole node; the answers are checked against trial division on a sample.
@@ -123,7 +184,7 @@ def optimus_fanout(table, n_actors: int, device, steps: int, warmup: int, rank: 
         tg = torch.arange(targets, dtype=torch.int64) * 2 + base + (rank + j * world) * 2 * targets
         fs.append((tg, FanOut(tg, n_actors, device)))
     Mx = max(f.M for _, f in fs)
-    ex = ActorExchange(table, Mx, chunks=chunks, delivery="mailbox", mailbox_ordered=False, comm=comm)
+    ex = ActorExchange(table, Mx, chunks=chunks, delivery="mailbox", mailbox_ordered=False, comm=comm, group=group)
     val = torch.empty(Mx, dtype=torch.int64, device=device)
     st = torch.empty(Mx, dtype=torch.int32, device=device)
     k = [0]
@@ -169,12 +230,12 @@ def api_send(device, sizes, actors: int, steps: int, warmup: int, rank: int = 0,
              comm: str = "rccl", barrier=None, max_over_ranks=None) -> dict:
     """Join (a control-plane member, GPU runtime, lease-attached shard, registry
     mirror) -> NewClient -> Client.Send of pre-generated batches, eager, through
-    the HBM mailboxes (gpu.delivery: mailbox).  With ``world`` > 1 (inside the
-    bench's process group): one member per rank in a static cluster on
-    127.0.0.1 (ports from MASTER_PORT), every rank's runtime on the existing
-    group, and every rank Sends its own batches to actors all over the node (the
-    sorted exchange, deferred re-sends: no host wait per Send); the timed loop
-    ends with ``Client.Flush``, and the slowest rank's time counts."""
+    the HBM mailboxes (gpu.delivery: mailbox).  With ``world`` > 1: one member
+    per rank in a static cluster on 127.0.0.1 (ports from MASTER_PORT), whose
+    Join forms the service's data plane (the compiled DataPlane: RCCL, or IpcComm
+    with ``comm="ipc"``), and every rank Sends its own batches to actors all over
+    the node (the sorted exchange, deferred re-sends: no host wait per Send); the
+    timed loop ends with ``Client.Flush``, and the slowest rank's time counts."""
     from .. import cluster as C
     from ..ops import batch as B
     from ..ops.records import METHOD_CALC_MULTIPLY, STATUS_OK
@@ -182,11 +243,7 @@ def api_send(device, sizes, actors: int, steps: int, warmup: int, rank: int = 0,
     os.environ.setdefault("PTYPE_ADVERTISE_ADDR", "127.0.0.1")
     cfg = C.Config()
     if world > 1:  # every rank derives the same static cluster from the rendezvous port
-        base = int(os.environ.get("MASTER_PORT", "29500")) + 1237
-        if base + 3 * world >= 65536:
-            base = 20000 + base % 20000
-        pp, pc, port = base + 2 * rank, base + 2 * rank + 1, base + 2 * world + rank
-        initial = ",".join(f"b{r}=http://127.0.0.1:{base + 2 * r}" for r in range(world))
+        pp, pc, port, initial = static_ports(rank, world, 1237)
     else:
         pp, pc, port = _port(), _port(), _port()
         initial = f"b0=http://127.0.0.1:{pp}"

@@ -74,8 +74,9 @@ def test_bench_multi_gpu(nproc):
     c = out["config"]
     assert c["wire"] == "v3-packed" and c["engine"] == "sorted", c
     assert c["exchange"] in ("padded", "per-pair prefixes"), c
-    assert c["comm"] == "rccl" and c["record_bytes"] <= 8
-    assert out["p50_rtt_remote_us"] is not None and out["diag"]["a2a_only_ms_per_step"] > 0
+    # the communicator Join's compiled DataPlane formed (no torch process group)
+    assert c["comm"] == "DataPlane/RCCL" and c["record_bytes"] <= 8
+    assert out["p50_rtt_remote_us"] is not None
     assert out["rtt_error"] is None and out["rtt_remote_request_ring"] == "device"
     # skewed traffic: once the agreement of Send k - 2 sizes the regions (from Send 2 on),
     # no re-send rounds -- the warm-up's start-up Sends may re-send, the timed ones must not
@@ -88,9 +89,10 @@ def test_bench_multi_gpu(nproc):
 @pytest.mark.parametrize("nproc", [2, 4])
 def test_bench_multi_process_on_one_gpu_ipc(nproc):
     """The bench's N > 1 path across real processes on ONE GPU:
-    torchrun ranks, a gloo group for the host side, the sorted exchange's
-    all-to-alls and agreement through IpcComm (shared-memory segments every
-    rank maps and registers) --
+    torchrun ranks, a control-plane member per rank and the compiled DataPlane
+    with the IpcComm transport (shared-memory segments every rank maps and
+    registers; no torch process group) carrying the sorted exchange's
+    all-to-alls and agreement --
     every reply verified by the bench itself, the cross-process RTT through the
     next rank's dispatcher ring, and skewed (Zipf) traffic without re-sends once
     the agreement applies."""
@@ -99,7 +101,8 @@ def test_bench_multi_process_on_one_gpu_ipc(nproc):
                timeout=600, launcher="self")
     c = out["config"]
     assert out["n_gpus"] == nproc and out["value"] > 0
-    assert c["comm"] == "ipc" and c["engine"] == "sorted" and c["wire"] == "v3-packed" and c["record_bytes"] <= 8
+    assert c["comm"] == "DataPlane/IpcComm" and c["engine"] == "sorted" and c["wire"] == "v3-packed"
+    assert c["record_bytes"] <= 8
     assert out["rtt_error"] is None and out["p50_rtt_remote_us"] > 0
     z = _run(nproc, ["--steps", "4", "--warmup", "3", "--rtt-calls", "0", "--zipf", "1.1", "--no-secondary"] + small,
              timeout=600, launcher="self")
@@ -108,14 +111,15 @@ def test_bench_multi_process_on_one_gpu_ipc(nproc):
 
 @pytest.mark.gpu
 def test_bench_force_dist_remote_rtt():
-    """World 1 with the RCCL process group up: the multi-rank RTT phase (store
-    barriers, the "next rank's" dispatcher mapped from its dma-buf -- here this
-    rank's own) runs as it does at N > 1."""
+    """World 1 with the compiled DataPlane's RCCL communicator up: the multi-rank
+    RTT phase (store barriers, the "next rank's" dispatcher mapped from its dma-buf
+    -- here this rank's own) runs as it does at N > 1."""
     out = _run(1, ["--force-dist", "--steps", "2", "--warmup", "1", "--rtt-calls", "200", "--no-secondary"],
                timeout=300)
     assert out["rtt_error"] is None, out["rtt_error"]
     assert out["p50_rtt_remote_us"] is not None and out["p50_rtt_remote_us"] > 0
     assert out["rtt_remote_request_ring"] == "device"
+    assert out["config"]["comm"] == "DataPlane/RCCL"
 
 
 def test_bench_zipf_cpu():

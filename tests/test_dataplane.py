@@ -363,7 +363,7 @@ def test_join_world1_reforms_after_a_flagged_failure(tmp_path, ports, monkeypatc
         ids = torch.arange(rt.total_actors, dtype=torch.int32)
         add = MsgBatch(ids, torch.ones(ids.numel(), dtype=torch.int64), None, None, METHOD_COUNTER_ADD)
         assert bool((client.Send(add)[1] == STATUS_OK).all())
-        rt._watchdog.failed = "injected"
+        rt.fail_generation("injected")
         mul = MsgBatch(ids, ids.to(torch.int64), torch.full((ids.numel(),), 3, dtype=torch.int64), None,
                        METHOD_CALC_MULTIPLY)
         val, st = client.Send(mul)

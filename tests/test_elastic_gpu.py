@@ -2,9 +2,9 @@
 
 tests/test_elastic.py kills a rank of a 3-process gloo group.  A real RCCL
 group needs a GPU per rank, so here one process runs the RCCL-specific steps
-the recovery takes: form generation 0 through the replicated store (RCCL
-communicator on this GPU, collectives forced on at world 1), Send, ABORT the
-communicator (``_abort_process_group`` -- what a survivor does when a
+the recovery takes, all of them in the compiled DataPlane: form generation 0
+through the replicated store (RCCL communicator on this GPU, collectives forced
+on at world 1), Send, ABORT the communicator (what a survivor does when a
 collective fails), form generation 1 through the store, and Send again: the
 actors kept their state and every reply is right.
 """
@@ -70,7 +70,7 @@ def test_elastic_rccl_abort_and_reform_world1():
     line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
     assert line, r.stdout[-2000:] + r.stderr[-2000:]
     out = json.loads(line[0][7:])
-    assert out["backend"] == "nccl" and out["forced_collectives"], out
+    assert out["backend"] == "native" and out["forced_collectives"], out
     assert out["gen0"] == 0 and out["gen1"] == 1 and out["recoveries"] == 1, out
     assert out["ok1"] and out["ok2"] and out["ok3"], out
     assert out["state"] == [2], out  # both CounterAdd rounds landed on state kept across the re-formation
@@ -110,7 +110,7 @@ _JOIN_SCRIPT = textwrap.dedent("""
            "comm0": rt.group.comm_ptr() if rt.group is not None else 0}
     # a failed generation as the send watchdog reports it: the next Send aborts the RCCL
     # communicator, re-forms the group through the store and re-sends
-    rt._watchdog.failed = "injected: device work overdue"
+    rt.fail_generation("injected: device work overdue")
     mul = MsgBatch(ids, ids.to(torch.int64), torch.full((n,), 7, dtype=torch.int64, device="cuda"), None,
                    METHOD_CALC_MULTIPLY)
     val, st = client.Send(mul)
@@ -192,7 +192,7 @@ _DP_SCRIPT = textwrap.dedent("""
     except RuntimeError as e:
         out["after_abort"] = str(e)
     t0 = time.monotonic()
-    out["recovered"] = g.recover(0.3)
+    out["recovered"] = g.recover(0.3)["members"]
     out["recover_s"] = time.monotonic() - t0
     out["gen1"] = g.gen
     out["max1"] = g.allreduce_max([4])

@@ -1,12 +1,15 @@
 """Rank failure on the NATIVE GPU data plane, across processes.
 
 Three processes on one GPU, each ``Join`` with a ``gpu:`` section (``world: 3``,
-``comm: ipc``): Join forms the group through the replicated store (gloo for the
-host side), the sorted exchange's collectives run through IpcComm (shared-memory
-segments that every rank maps and registers with HIP, csrc/hip/ipc_comm.hpp).  One node dies without cleanup after the first round; the
-survivors' ``Client.Send`` sees the dead peer at the comm's timeout, aborts the
-generation, waits for the lease-driven membership, forms generation 1 through
-the store and re-homes the dead rank's actors from the buddy replica --
+``comm: ipc``): the compiled DataPlane (csrc/core/dataplane.cpp) forms the group
+through the replicated store with the IpcComm transport (shared-memory segments
+that every rank maps and registers with HIP, csrc/hip/ipc_comm.hpp) -- the same
+form / abort / settle / next-generation code as RCCL, and no torch process
+group at all.  One node dies without cleanup after the first
+round; the survivors' ``Client.Send`` sees the dead peer at the comm's timeout,
+the DataPlane aborts the generation, waits for the lease-driven membership,
+forms generation 1 through the store and hands back the ring adoption; the
+adopter resumes the dead rank's actors from the buddy replica --
 messages of lost actors answer STATUS_RANK_LOST when re-sends are off, and are
 answered by the adopter afterwards.  The CPU twin is
 tests/test_dataplane.py::test_join_send_survives_a_dead_rank.
@@ -56,7 +59,11 @@ def _survivor(i, pp, pc, sp, tmp, crash, q):
         ids = torch.arange(n, dtype=torch.int32, device=dev)
         add = MsgBatch(ids, torch.ones(n, dtype=torch.int64, device=dev), None, None, METHOD_COUNTER_ADD)
         _, st = client.Send(add)
+        import torch.distributed as dist
+
         ok1 = bool((st == STATUS_OK).all()) and rt.exchange.ipc is not None
+        ok1 = ok1 and type(rt.group).__name__ == "NativeGroup" and rt.group.transport == "ipc"
+        ok1 = ok1 and not dist.is_initialized()  # no torch process group anywhere
         rt.replicate()  # every block has a copy on its buddy (the node that adopts it)
         me = rt.membership["me"]
         dead = rt.membership["nodes0"][crash]
@@ -72,15 +79,13 @@ def _survivor(i, pp, pc, sp, tmp, crash, q):
         ok2 = ok_lost and bool((st == STATUS_OK).all()) and torch.equal(val, a * 7)
         _, st = client.Send(add)
         ok3 = bool((st == STATUS_OK).all())
-        import torch.distributed as dist
-
-        dist.barrier()
+        rt.group.barrier()
         P = rt.actors
         own = sorted(int(x) for x in rt.state[:P].unique().tolist())
         adopted = sorted(int(x) for x in rt.state[P:].unique().tolist())
         q.put((me, dead, ok1, ok2, ok3, own, adopted, rt.restored, rt.world, rt.recoveries, rt.blocks,
                rt.membership["gen"], rt.exchange.ipc is not None))
-        dist.barrier()
+        rt.group.barrier()
         client.Close()
         srv.Close()
         c.Close()

@@ -79,7 +79,8 @@ _DIST_SCRIPT = textwrap.dedent("""
     from ptype_amd.parallel.exchange import ActorExchange
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from ptype_amd.parallel.native_group import solo_group
+    G = solo_group(dev)  # the compiled DataPlane's RCCL communicator, world 1 (collectives forced on)
     n, M = 4096, 300_000
     g = RegistryTable(2 * n, device=dev)
     ids = torch.arange(n)
@@ -88,7 +89,7 @@ _DIST_SCRIPT = textwrap.dedent("""
     req = B.gen_requests(M, n + 10, METHOD_CALC_MULTIPLY, seed=5, device=dev)
     res = {}
     for engine in (True, False):
-        ex = ActorExchange(g, M, chunks=3)
+        ex = ActorExchange(g, M, chunks=3, group=G)
         assert ex.force_collectives
         ex.use_engine = engine
         v, s = ex.send(req)
@@ -96,7 +97,7 @@ _DIST_SCRIPT = textwrap.dedent("""
         res[engine] = (v.cpu(), s.cpu(), ex._engine is not None)
     ok = torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1])
     print(json.dumps({"identical": bool(ok), "engine_used": res[True][2], "python_used": not res[False][2]}))
-    dist.destroy_process_group()
+    G.close()
 """)
 
 

@@ -268,7 +268,8 @@ _ENGINE_SCRIPT = textwrap.dedent("""
     from ptype_amd.parallel.exchange import ActorExchange
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from ptype_amd.parallel.native_group import solo_group
+    G = solo_group(dev)  # the compiled DataPlane's RCCL communicator, world 1 (collectives forced on)
     n, M = 4096, 300_000
     g = RegistryTable(2 * n, device=dev)
     ids = torch.arange(n)
@@ -291,7 +292,7 @@ _ENGINE_SCRIPT = textwrap.dedent("""
         res = {}
         for packed in (True, False):
             st = torch.zeros(n, dtype=torch.int64, device=dev)
-            ex = ActorExchange(g, M, chunks=3, state=st, packed=packed)
+            ex = ActorExchange(g, M, chunks=3, state=st, packed=packed, group=G)
             assert ex.force_collectives
             ex.use_engine = packed  # v3 on the native engine vs the v2 Python pipeline
             v, s = ex.send(req)
@@ -306,7 +307,7 @@ _ENGINE_SCRIPT = textwrap.dedent("""
         out[name] = {"same": bool(same), "S": a[5]["S"], "vb": a[5]["vb"], "toowide": a[6],
                      "req_words": a[5]["req_words"], "rep_words": a[5]["rep_words"], "exact": a[5]["exact"]}
     print("RESULT " + json.dumps(out))
-    dist.destroy_process_group()
+    G.close()
 """)
 
 

@@ -249,14 +249,15 @@ _GRAPH_SCRIPT = textwrap.dedent("""
     from ptype_amd.parallel.exchange import ActorExchange
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from ptype_amd.parallel.native_group import solo_group
+    G = solo_group(dev)  # the compiled DataPlane's RCCL communicator, world 1 (collectives forced on)
     n, M = 1 << 15, 1 << 20
     t = RegistryTable(2 * n, device=dev)
     ids = torch.arange(n)
     perm = torch.randperm(n, generator=torch.Generator().manual_seed(3))
     t.upsert(actor_keys(ids), torch.zeros(n, dtype=torch.int32), perm.to(torch.int32))
     t.enable_directory(n, affine_world=1)
-    ex = ActorExchange(t, M, chunks=2, delivery="mailbox", mailbox_ordered=False)
+    ex = ActorExchange(t, M, chunks=2, delivery="mailbox", mailbox_ordered=False, group=G)
     assert ex.force_collectives and ex._use_sorted()
     req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=1, device=dev)
     val = torch.empty(M, dtype=torch.int64, device=dev)
@@ -279,7 +280,7 @@ _GRAPH_SCRIPT = textwrap.dedent("""
         oks.append(bool((st == STATUS_OK).all()) and bool(torch.equal(val, req.a0 * req.a1)))
     w = ex.last_wire
     print("RESULT " + json.dumps({"ok": oks, "engine": w["engine"], "agreed": bool(w["agreed"]), "S": int(w["S"])}))
-    dist.destroy_process_group()
+    G.close()
 """)
 
 
