@@ -222,8 +222,13 @@ def main():
             from ptype_amd.parallel.exchange import ipc_cap_for
             from ptype_amd.utils import benchmarks as BM
 
+            # (IpcComm regions: as large as the largest exchange of the run -- the headline's,
+            # or the optimus secondary's fan-out batch)
+            cap = ipc_cap_for(M, chunks, world)
+            if not args.no_secondary:
+                cap = max(cap, ipc_cap_for(BM.optimus_max_batch(world), chunks, world))
             bench_cp, G = BM.bench_group(device, rank, world, comm="ipc" if ipc else "rccl",
-                                         cap_bytes=ipc_cap_for(M, chunks, world) if ipc else 0)
+                                         cap_bytes=cap if ipc else 0)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
 

@@ -167,6 +167,14 @@ def registry_1m(device, n: int = 1 << 20, reps: int = 5) -> dict:
 
 
 # ---------------------------------------------------------------------------- config 4
+def optimus_max_batch(world: int, targets: int = 1024, base: int = 80_001, sets: int = 3) -> int:
+    """The largest batch ``optimus_fanout`` sends on any rank (its exchange's
+    geometry -- e.g. the IpcComm region size a bench group must be formed with):
+    target t is ceil(t / 10) ranges, and the last rank's last set has the largest."""
+    tg = torch.arange(targets, dtype=torch.int64) * 2 + base + ((world - 1) + (sets - 1) * world) * 2 * targets
+    return int(((tg + 9) // 10).sum())
+
+
 def optimus_fanout(table, n_actors: int, device, steps: int, warmup: int, rank: int = 0, world: int = 1,
                    targets: int = 1024, base: int = 80_001, chunks: int = 1, comm: str = "rccl", barrier=None,
                    max_over_ranks=None, sets: int = 3, group=None) -> dict:
