@@ -66,6 +66,10 @@ __device__ __forceinline__ uint32_t* rec_a(const MboxView& mv, uint64_t slot) {
 __device__ __forceinline__ uint32_t* rec_b(const MboxView& mv, uint64_t slot) {
   return mv.planar ? mv.rec + mv.b_off + slot * 4 : mv.rec + slot * 8 + 4;
 }
+// (planar rings) a u16 per slot in plane B's memory: the wide pure records' places
+__device__ __forceinline__ uint16_t* rec_place(const MboxView& mv) {
+  return reinterpret_cast<uint16_t*>(mv.rec + mv.b_off);
+}
 __device__ __forceinline__ uint32_t* rec_at(const MboxView& mv, uint32_t s, uint64_t pos) {
   return rec_a(mv, slot_at(mv, s, pos));
 }

@@ -473,9 +473,10 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   // (in.rec8) the messages whose fields do not fit an 8-B record -- they spill -- and
   // the tile's fields OR-ed (their bit lengths size the next Send's records)
   uint32_t escm = 0;
-  const uint32_t w8 = in.rec8 ? *in.r8w : 0u;  // this Send's 8-B field widths
+  const uint32_t w8 = in.rec8 ? *in.r8w : 0u;  // this Send's 8-B field widths (recw: none, nothing escapes)
   uint64_t or_m = 0, or_0 = 0, or_1 = 0;
-  if (in.rec8) {
+  const bool maxima = in.rec8 || in.recw;  // (wide pure records keep the maxima: back to 8 B once they fit)
+  if (maxima) {
     const uint32_t wm = w8 & 0xffu, w0 = (w8 >> 8) & 0xffu, w1 = (w8 >> 16) & 0xffu;
 #pragma unroll
     for (int k = 0; k < SK; ++k) {
@@ -483,11 +484,11 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
       const uint64_t z0 = ((uint64_t)v0[k] << 1) ^ (uint64_t)(v0[k] >> 63);
       const uint64_t z1 = ((uint64_t)v1[k] << 1) ^ (uint64_t)(v1[k] >> 63);
       or_m |= mb[k], or_0 |= z0, or_1 |= z1;
-      if ((mb[k] >> wm) != 0 || (z0 >> w0) != 0 || (z1 >> w1) != 0) escm |= 1u << k;
+      if (in.rec8 && ((mb[k] >> wm) != 0 || (z0 >> w0) != 0 || (z1 >> w1) != 0)) escm |= 1u << k;
     }
   }
   sp |= escm != 0;
-  if (in.rec8) {  // the tile's field bit lengths (read by thread 0 past the spill barrier)
+  if (maxima) {  // the tile's field bit lengths (read by thread 0 past the spill barrier)
     const uint32_t bm = wave_max_u32(bitlen64(or_m)), b0 = wave_max_u32(bitlen64(or_0)),
                    b1 = wave_max_u32(bitlen64(or_1));
     if (lane == 0) {
@@ -534,7 +535,11 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     const uint64_t slot = slot_at(mv, sh, base[sh] + off);
     if (wsidx) sidx[i] = (uint32_t)slot;
     const uint32_t mt = meth[k];
-    if (in.rec8 && esc) {  // (ordered) escape: the place in the tile + bit 63, the fields aside
+    if (in.recw) {  // wide pure record: {a0, a1} whole, the place in the tile beside it
+      *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
+          u32x4{(uint32_t)v0[k], (uint32_t)((uint64_t)v0[k] >> 32), (uint32_t)v1[k], (uint32_t)((uint64_t)v1[k] >> 32)};
+      rec_place(mv)[slot] = (uint16_t)(i & ((kST * SK) - 1));
+    } else if (in.rec8 && esc) {  // (ordered) escape: the place in the tile + bit 63, the fields aside
       reinterpret_cast<uint64_t*>(mv.rec)[slot] = (uint64_t)(i & ((kST * SK) - 1)) | (1ull << 63);
       *reinterpret_cast<u32x4*>(in.r8esc + 2 * slot) =
           u32x4{(uint32_t)v0[k], (uint32_t)((uint64_t)v0[k] >> 32), mb[k], 0u};
@@ -559,7 +564,7 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   }
   // the tile's field bit lengths, for the next Send's widths (rec8_next): a memory-side write
   // (the fused kernel's last block reads it within the launch: its ticket follows a vmcnt(0) wait)
-  if (in.rec8 && threadIdx.x == 0) (void)atomicExch(&in.r8max[t], tmax[0] | (tmax[1] << 8) | (tmax[2] << 16));
+  if (maxima && threadIdx.x == 0) (void)atomicExch(&in.r8max[t], tmax[0] | (tmax[1] << 8) | (tmax[2] << 16));
   block_add_stats(mv.stats, n_enq, kMbEnqueued, n_ovf, kMbOverflow, n_miss, kMbNoActor);
   __syncthreads();  // block_add_stats' LDS partials are reused
   block_add_stats(mv.stats, n_spill, kMbSpilled, timeouts, kMbLookback, 0, -1);
@@ -625,6 +630,20 @@ __device__ __forceinline__ SortRec decode_rec8(uint64_t r, const SortIn& in, uin
   return x;
 }
 
+// A wide pure record (in.recw): no mailbox -- its method reads none.
+__device__ __forceinline__ SortRec decode_wide(const u32x4& h, const SortIn& in, uint32_t origin) {
+  SortRec x;
+  x.valid = true;
+  x.origin = origin;
+  x.mb = 0;
+  x.method = in.method_uniform;
+  x.flags = 0;
+  x.a0 = (int64_t)(((uint64_t)h.y << 32) | h.x);
+  x.a1 = (int64_t)(((uint64_t)h.w << 32) | h.z);
+  x.a2 = 0;
+  return x;
+}
+
 __device__ __forceinline__ SortRec load_sorted(const MboxView& mv, uint64_t slot) {
   const u32x4 ha = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
   u32x4 hb = {0u, 0u, 0u, 0u};
@@ -679,7 +698,9 @@ __device__ __forceinline__ void epoch_commit(const MboxView& mv, uint32_t s, uin
 // recorded, replies coalesced; a spilled message runs straight from the batch.
 //
 // The last block commits every shard (and clears the group sums).
-template <int FIXED, bool FRESH = false, bool R8 = false, int SK = kSK>
+// RF: the record form -- 0 compact / long (16 / 32 B), 1 the 8-B record, 2 the wide
+// pure record (16 B {a0, a1} + the u16 place)
+template <int FIXED, bool FRESH = false, int RF = 0, int SK = kSK>
 __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t t,
                                                const uint32_t* __restrict__ sidx, const uint32_t* __restrict__ rw,
                                                int64_t* __restrict__ state, uint32_t n_state, uint64_t delay_ticks,
@@ -691,12 +712,12 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
     const int64_t i = tile_index<SK>(t, k);
     sl[k] = i < in.M ? __builtin_nontemporal_load(sidx + i) : kNoSlot;
   }
-  using RecT = typename std::conditional<R8, uint64_t, u32x4>::type;  // the ring record as loaded
-  const uint32_t w8 = R8 ? *in.r8w : 0u;  // the 8-B field widths this Send's sort used
+  using RecT = typename std::conditional<RF == 1, uint64_t, u32x4>::type;  // the ring record as loaded
+  const uint32_t w8 = RF == 1 ? *in.r8w : 0u;  // the 8-B field widths this Send's sort used
   RecT ha[SK];
 #pragma unroll
   for (int k = 0; k < SK; ++k) {
-    if constexpr (R8) {
+    if constexpr (RF == 1) {
       const uint64_t* rp = reinterpret_cast<const uint64_t*>(mv.rec) + (sl[k] < kSpillSlot ? sl[k] : 0);
       ha[k] = sl[k] < kSpillSlot ? (FRESH ? __builtin_nontemporal_load(rp) : *rp) : 0ull;
     } else {
@@ -717,8 +738,10 @@ __device__ __forceinline__ void drain_tile_msg(MboxView mv, SortIn in, uint32_t 
       x.a0 = in.a0[i];
       x.a1 = in.a1 ? in.a1[i] : 0;
       x.a2 = in.a2 ? in.a2[i] : 0;
-    } else if constexpr (R8) {
+    } else if constexpr (RF == 1) {
       x = decode_rec8<FRESH, SK>(ha[k], in, w8, in.origin_base + t * (kST * SK));
+    } else if constexpr (RF == 2) {
+      x = decode_wide(ha[k], in, 0u);
     } else {
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
@@ -840,7 +863,7 @@ struct DrainCounts {
 
 // (views and counts by value: references to a kernel's locals or arguments put
 // them in scratch)
-template <int FIXED, bool NARROW, bool FRESH, bool R8 = false, int SK = kSK>
+template <int FIXED, bool NARROW, bool FRESH, int RF = 0, int SK = kSK>
 __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, uint32_t t,
                                                        const uint32_t* __restrict__ tinfo,
                                                        const uint32_t* __restrict__ sidx,
@@ -864,14 +887,15 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   int spill = 0;
   const uint32_t T = load_tile_runs(mv, tinfo, t, L, spill);
   if (spill) {  // some message of the tile spilled: the scatter left the tile's slot indices
-    drain_tile_msg<FIXED, FRESH, R8, SK>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
+    drain_tile_msg<FIXED, FRESH, RF, SK>(mv, in, t, sidx, rw, state, n_state, delay_ticks, ob, rv, done, failed, holes);
     return DrainCounts{done, failed, holes};
   }
   const uint64_t sbase_mask = (1ull << mv.log_q) - 1;
-  using RecT = typename std::conditional<R8, uint64_t, u32x4>::type;  // the ring record as loaded
-  const uint32_t w8 = R8 ? *in.r8w : 0u;  // the 8-B field widths this Send's sort used
+  using RecT = typename std::conditional<RF == 1, uint64_t, u32x4>::type;  // the ring record as loaded
+  const uint32_t w8 = RF == 1 ? *in.r8w : 0u;  // the 8-B field widths this Send's sort used
   RecT ha[SK];
   uint32_t sl[SK];
+  uint16_t pl[SK];  // (RF 2) the places in the tile
 #pragma unroll
   for (int k = 0; k < SK; ++k) {  // ring order: lane-consecutive entries of the runs
     const uint32_t j = (uint32_t)k * kST + threadIdx.x;
@@ -879,12 +903,16 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
     if (j < T) {
       const uint32_t s = L.owner[j];
       sl[k] = (uint32_t)(((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & sbase_mask));
-      if constexpr (R8) {
+      if constexpr (RF == 1) {
         const uint64_t* rp = reinterpret_cast<const uint64_t*>(mv.rec) + sl[k];
         ha[k] = FRESH ? __builtin_nontemporal_load(rp) : *rp;
       } else {
         const u32x4* rp = reinterpret_cast<const u32x4*>(rec_a(mv, sl[k]));
         ha[k] = FRESH ? __builtin_nontemporal_load(rp) : *rp;
+        if constexpr (RF == 2) {
+          const uint16_t* pp = rec_place(mv) + sl[k];
+          pl[k] = FRESH ? __builtin_nontemporal_load(pp) : *pp;
+        }
       }
     }
   }
@@ -897,8 +925,10 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   for (int k = 0; k < SK; ++k) {
     if (sl[k] == kNoSlot) continue;
     SortRec x;
-    if constexpr (R8) {
+    if constexpr (RF == 1) {
       x = decode_rec8<FRESH, SK>(ha[k], in, w8, in.origin_base + (uint32_t)i0);
+    } else if constexpr (RF == 2) {
+      x = decode_wide(ha[k], in, in.origin_base + (uint32_t)i0 + pl[k]);
     } else {
       u32x4 hb = {0u, 0u, 0u, 0u};
       int64_t a2v = 0;
@@ -934,7 +964,7 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
   return DrainCounts{done, failed, holes};
 }
 
-template <int FIXED, bool NARROW, bool R8, int SK = kSK>
+template <int FIXED, bool NARROW, int RF, int SK = kSK>
 __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring_kernel(MboxView mv, SortIn in, const uint32_t* __restrict__ tinfo,
                                                              const uint32_t* __restrict__ sidx,
                                                              const uint32_t* __restrict__ rw,
@@ -949,7 +979,7 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
   // tiles dealt XCD by XCD like the scatter's blocks (whose writes the XCD's L2 may still hold)
   const uint32_t t = virt_block(blockIdx.x, gridDim.x);
   if (t < in.tiles)
-    dc = drain_ring_tile<FIXED, NARROW, false, R8, SK>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob,
+    dc = drain_ring_tile<FIXED, NARROW, false, RF, SK>(mv, in, t, tinfo, sidx, rw, state, n_state, delay_ticks, ob,
                                                        rv, smem_rd);
   block_add_stats(mv.stats, dc.done, kMbProcessed, dc.failed, kMbFailed, dc.holes, kMbHoles);
   __shared__ bool last;
@@ -958,7 +988,7 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
   if (last) {  // every block's records are read: the rings are consumed
     for (uint32_t s = threadIdx.x; s < S; s += kST) epoch_commit(mv, s, epoch_sum(mv, gsum, ngroups, S, s));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
-    if constexpr (R8) rec8_next(in, const_cast<uint32_t*>(in.r8w), r8host, in.tiles);
+    if constexpr (RF != 0) rec8_next(in, const_cast<uint32_t*>(in.r8w), r8host, in.tiles);
   }
 }
 
@@ -973,7 +1003,7 @@ __global__ __launch_bounds__(kST, (NARROW && FIXED) ? 8 : 1) void mbx_drain_ring
 // waits at a kernel boundary for the slowest tile.  The last block to finish
 // commits every shard's epoch (tail = head = tail + total) and advances the
 // look-back tag.  Tune mbox_fused=0: the separate kernels.
-template <int MODE, bool A2, bool MC, int FIXED, bool R8, int SK = kSK>
+template <int MODE, bool A2, bool MC, int FIXED, int RF, int SK = kSK>
 __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView mv, unsigned long long* __restrict__ desc,
                                                             unsigned* __restrict__ tctr, uint32_t* __restrict__ gsum,
                                                             uint32_t* __restrict__ sidx, uint32_t* __restrict__ tinfo,
@@ -989,7 +1019,7 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
   // every wave's ring stores are out before any wave reads the tile's runs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const DrainCounts dc = drain_ring_tile<FIXED, true, true, R8, SK>(mv, in, t, tinfo, sidx, rw, state, n_state,
+  const DrainCounts dc = drain_ring_tile<FIXED, true, true, RF, SK>(mv, in, t, tinfo, sidx, rw, state, n_state,
                                                                     delay_ticks, ob, rv, smem_sd);
   block_add_stats(mv.stats, dc.done, kMbProcessed, dc.failed, kMbFailed, dc.holes, kMbHoles);
   __shared__ bool last;
@@ -1006,7 +1036,7 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
     for (uint32_t s = threadIdx.x; s < S; s += kST)
       epoch_commit(mv, s, epoch_sum(mv, gsum, 1, S, s));
     if (threadIdx.x == 0) tctr[1] += 1u;  // the next Send's one-pass epoch tag
-    if constexpr (R8) rec8_next(in, const_cast<uint32_t*>(in.r8w), r8host, in.tiles);
+    if constexpr (RF != 0) rec8_next(in, const_cast<uint32_t*>(in.r8w), r8host, in.tiles);
   }
 }
 
@@ -1701,7 +1731,11 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   }
   // fields that outgrew 64 bits (the last Send's widths, bit 31): 16-B records from here on
   const bool r8_on = r8 && !(__atomic_load_n(r8host_, __ATOMIC_RELAXED) & 0x80000000u);
-  last_rec_bytes_ = r8_on ? 8 : ((a.a2 || a.method_col) ? 32 : 16);  // (16: compact unless a value is wide)
+  // fields that outgrew 8 B in a stateless batch of a PURE method (its handler reads no actor):
+  // wide pure records, 16 B {a0, a1} + a u16 place, instead of the 32-B long form (the 8 Mi
+  // full-range int64 step writes and reads 18 B per message, not 32)
+  const bool rw_on = r8 && !r8_on && rank_route;  // (rank routes: stateless methods only)
+  last_rec_bytes_ = r8_on ? 8 : rw_on ? 18 : ((a.a2 || a.method_col) ? 32 : 16);  // (16: compact unless a value is wide)
   if (r8_on && a.ordered && !r8esc_) {  // escape side array: {a0, mailbox} per ring slot
     if (capturing())
       throw std::runtime_error("mailbox send: first ordered 8-B-record Send inside a graph capture (warm up first)");
@@ -1714,7 +1748,12 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     in.r8w = r8w_;
     in.r8max = r8max_;
     in.r8esc = r8esc_;
+  } else if (rw_on) {
+    in.recw = 1;
+    in.r8w = r8w_;
+    in.r8max = r8max_;
   }
+  const int rf = r8_on ? 1 : rw_on ? 2 : 0;
   uint32_t* tinfo = all_sidx ? nullptr : sort_tinfo_;
   if (two_pass) {
 #define PT_COUNT(MO) \
@@ -1736,12 +1775,16 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     const size_t lds = std::max(onesweep_lds_bytes(Sv), ring_drain_lds_bytes(Sv, kSTile));
 #define PT_SD2(MO, A2, MC, FX)                                                                                    \
   do {                                                                                                            \
-    if (!(A2) && !(MC) && r8_on)                                                                                  \
-      hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, false, false, FX, true>), dim3(in.tiles), dim3(kST), lds, st, in, \
+    if (!(A2) && !(MC) && rf == 1)                                                                                \
+      hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, false, false, FX, 1>), dim3(in.tiles), dim3(kST), lds, st, in,  \
+                         mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv,              \
+                         (int64_t*)a.state, a.n_state, a.delay_ticks, ob, sort_ticket_, reserve, r8host_);          \
+    else if (!(A2) && !(MC) && (MO) == 3 && rf == 2)                                                              \
+      hipLaunchKernelGGL((mbx_sortdrain_kernel<3, false, false, FX, 2>), dim3(in.tiles), dim3(kST), lds, st, in,   \
                          mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv,              \
                          (int64_t*)a.state, a.n_state, a.delay_ticks, ob, sort_ticket_, reserve, r8host_);          \
     else                                                                                                          \
-      hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, false>), dim3(in.tiles), dim3(kST), lds, st, in, mv, \
+      hipLaunchKernelGGL((mbx_sortdrain_kernel<MO, A2, MC, FX, 0>), dim3(in.tiles), dim3(kST), lds, st, in, mv, \
                          sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, sort_tinfo_, sort_rw_, rv,                  \
                          (int64_t*)a.state, a.n_state, a.delay_ticks, ob, sort_ticket_, reserve, r8host_);          \
   } while (0)
@@ -1840,17 +1883,19 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #undef PT_DMSG
   } else {
     // the ring-order drain; its LDS stage is sized by the 8-shard view (narrow form)
-#define PT_DRING(FX, R8)                                                                                          \
-  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, true, R8>), dim3(tile_grid), dim3(kST), ring_drain_lds_bytes(Sv, kSTile), \
+#define PT_DRING(FX, RF)                                                                                          \
+  hipLaunchKernelGGL((mbx_drain_ring_kernel<FX, true, RF>), dim3(tile_grid), dim3(kST), ring_drain_lds_bytes(Sv, kSTile), \
                      st, mv, in, (const uint32_t*)sort_tinfo_, (const uint32_t*)sort_sidx_, (const uint32_t*)sort_rw_, \
                      (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_gsum_, ngroups, sort_ticket_,        \
                      sort_tctr_, r8host_)
     if (fixed_mul) {
-      if (r8_on) PT_DRING(kCalculatorMultiply, true);
-      else PT_DRING(kCalculatorMultiply, false);
+      if (rf == 1) PT_DRING(kCalculatorMultiply, 1);
+      else if (rf == 2) PT_DRING(kCalculatorMultiply, 2);
+      else PT_DRING(kCalculatorMultiply, 0);
     } else {
-      if (r8_on) PT_DRING(0, true);
-      else PT_DRING(0, false);
+      if (rf == 1) PT_DRING(0, 1);
+      else if (rf == 2) PT_DRING(0, 2);
+      else PT_DRING(0, 0);
     }
 #undef PT_DRING
   }

@@ -52,6 +52,12 @@ struct SortIn {  // by value
   // ESCAPE record (bit 63 set, place in the tile kept) and its {a0, mailbox} go here,
   // indexed by ring slot -- so the ring stays each actor's FIFO (no overflow, no hole)
   int64_t* r8esc;
+  // wide pure records (a stateless batch of one pure method -- no state, no actor read --
+  // whose arguments outgrew the 8-B fields): plane A holds {a0, a1} whole, and the
+  // message's place in its tile is a u16 at the same slot of plane B's memory (18 B per
+  // message instead of the 32-B long form).  The tile maxima are still kept (r8max), so
+  // the next Send returns to 8-B records once its values fit again.
+  uint32_t recw;
 };
 
 // Block b's range: XCD (b % 8) owns virtual blocks [x * G/8, (x+1) * G/8).

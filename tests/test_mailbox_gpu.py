@@ -488,6 +488,53 @@ def test_sorted_mailbox_8b_records_spill_what_does_not_fit(fused):
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_sorted_mailbox_wide_pure_records_and_back_to_8b(fused):
+    """Full-range int64 arguments of a stateless rank-routed batch: the Send that
+    first meets them spills them (its 8-B widths were narrow), the next ones take
+    the 18-B wide pure records (16 B {a0, a1} + the u16 place; no mailbox -- the
+    methods read none), and once the values are narrow again the batches return to
+    8-B records.  Every reply exact, unknown actors answered, no overflow."""
+    code = textwrap.dedent('''
+        import torch
+        from ptype_amd.ops import batch as B
+        from ptype_amd.ops.mailbox import Mailboxes
+        from ptype_amd.ops.records import METHOD_CALC_MULTIPLY, STATUS_NO_ACTOR, STATUS_OK
+        from ptype_amd.ops.table import RegistryTable, actor_keys
+        n, M = 1 << 14, 600_000
+        t = RegistryTable(4 * n, device="cuda")
+        ids = torch.arange(n)
+        perm = torch.randperm(n, generator=torch.Generator().manual_seed(5))
+        t.upsert(actor_keys(ids), torch.zeros(n, dtype=torch.int32), perm.to(torch.int32))
+        t.enable_directory(n)
+        mb = Mailboxes("cuda", shards=256, slots=16384)
+        seen = []
+        for k, wide in enumerate([False, True, True, True, False, False]):
+            g = torch.Generator().manual_seed(40 + k)
+            actor = torch.randint(0, n + 500, (M,), generator=g, dtype=torch.int32)
+            lo, hi = (-(1 << 63), (1 << 63) - 1) if wide else (-(1 << 15), 1 << 15)
+            a0 = torch.randint(lo, hi, (M,), generator=g, dtype=torch.int64)
+            a1 = torch.randint(lo, hi, (M,), generator=g, dtype=torch.int64)
+            req = B.MsgBatch(actor.cuda(), a0.cuda(), a1.cuda(), None, METHOD_CALC_MULTIPLY)
+            v, st = mb.send(req, t, None, ordered=False)
+            torch.cuda.synchronize()
+            assert mb.last_route == 3
+            known = req.actor < n
+            assert torch.equal(st, torch.where(known, STATUS_OK, STATUS_NO_ACTOR).to(torch.int32)), k
+            assert torch.equal(v[known], (req.a0 * req.a1)[known]), k
+            seen.append(int(mb.last_record_bytes))
+        s = mb.stats()
+        assert s["overflow"] == 0 and s["holes"] == 0, s
+        assert seen == [8, 8, 18, 18, 18, 8], seen
+        print("OK", seen, s["spilled"])
+    ''')
+    # (mbox_rec8=1: this batch size would take 16-B records by default)
+    env = dict(os.environ, PTYPE_TUNE=f"mbox_fused={fused},mbox_rec8=1",
+               PYTHONPATH=os.pathsep.join([ROOT, os.path.join(ROOT, "tests")]))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
 def test_live_mailbox_sustained_overload_keeps_consumer_rate():
     """VERDICT r2 #4: two producer streams keep a persistent consumer ~3x over
     capacity for more than a second.  A full ring reserves nothing (no holes),
