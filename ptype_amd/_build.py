@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import glob
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -67,8 +68,6 @@ def kernel_resources() -> dict:
     """Per-kernel VGPRs / scratch / occupancy from the last hipcc compile of each
     object (``-Rpass-analysis=kernel-resource-usage`` remarks, kept next to the
     objects).  A kernel with scratch > 0 is a performance bug on gfx950."""
-    import re
-
     out = {}
     for res in glob.glob(os.path.join(ROOT, "build", "hip", "*.res")):
         cur = None
@@ -161,7 +160,10 @@ def build_hip(verbose: bool = False) -> str:
         o = os.path.join(objdir, os.path.basename(s) + ".o")
         objs.append(o)
         lang = ["-x", "hip"]
-        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_t):
+        # (a source may include another .hip: mailbox_sort_fused_other.hip)
+        inc = [os.path.join(os.path.dirname(s), m) for m in re.findall(r'#include "([^"]+\.hip)"', open(s).read())]
+        src_t = max([os.path.getmtime(s)] + [os.path.getmtime(i) for i in inc if os.path.exists(i)])
+        if not os.path.exists(o) or os.path.getmtime(o) < max(src_t, hdr_t):
             jobs.append(([hipcc] + lang + flags + ["-Rpass-analysis=kernel-resource-usage", "-c", s, "-o", o],
                          o[:-2] + ".res"))
     _compile_logged(jobs, 8)
@@ -224,8 +226,11 @@ def build_native_test(sanitize: str = "thread", verbose: bool = False) -> str:
 
 
 def build_all(verbose: bool = False) -> None:
-    build_core(verbose)
-    build_hip(verbose)
+    # the two modules share nothing: the host objects compile while hipcc works
+    # through the device runtime (its longest object sets the wall time)
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        for f in [ex.submit(build_core, verbose), ex.submit(build_hip, verbose)]:
+            f.result()
 
 
 if __name__ == "__main__":

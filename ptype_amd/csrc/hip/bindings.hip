@@ -212,7 +212,7 @@ PYBIND11_MODULE(_hip, m) {
     py::dict d;
     d["mbox_fused"] = t.mbox_fused, d["mbox_rec8"] = t.mbox_rec8, d["mbox_sort"] = t.mbox_sort;
     d["mbox_drain_msg"] = t.mbox_drain_msg, d["sx_sort"] = t.sx_sort, d["sx_self_copy"] = t.sx_self_copy;
-    d["sx_comm_cs"] = t.sx_comm_cs, d["sx_graph"] = t.sx_graph, d["stream_sync"] = t.stream_sync;
+    d["sx_comm_cs"] = t.sx_comm_cs, d["stream_sync"] = t.stream_sync;
     d["local"] = t.local, d["persistent_stream"] = t.persistent_stream, d["poll_lanes"] = t.poll_lanes;
     d["poll_full"] = t.poll_full, d["poll_sleep"] = t.poll_sleep;
     return d;

@@ -22,8 +22,6 @@
 //   sx_self_copy      0        world-1 sorted exchange: the all-to-alls as device copies
 //                              (RCCL calls on a forked stream cannot be graph-captured)
 //   sx_comm_cs        0        sorted exchange collectives on the caller's stream
-//   sx_graph          1        sorted exchange Sends replayed from a cached hipGraph
-//                              (0 never, 1 device-side comms, 2 also RCCL)
 //   stream_sync       0        epoch engine hand-offs: 0 events, 1 stream wait-value packets
 //   local             1        world-1 epoch Sends: the fused local pass (0: the slot pipeline)
 //   persistent_stream low      queue of persistent kernels: low / high / cumask / pooled
@@ -45,7 +43,6 @@ struct Tune {
   int sx_sort = 0;
   int sx_self_copy = 0;
   int sx_comm_cs = 0;
-  int sx_graph = 1;
   int stream_sync = 0;
   int local = 1;
   std::string persistent_stream = "low";
@@ -64,7 +61,6 @@ struct Tune {
     if (k == "sx_sort") return i(sx_sort);
     if (k == "sx_self_copy") return i(sx_self_copy);
     if (k == "sx_comm_cs") return i(sx_comm_cs);
-    if (k == "sx_graph") return i(sx_graph);
     if (k == "stream_sync") return i(stream_sync);
     if (k == "local") return i(local);
     if (k == "poll_lanes") return i(poll_lanes);
