@@ -28,6 +28,7 @@
 #include "api.hpp"
 #include "balancer.hpp"
 #include "config.hpp"
+#include "dp_link.hpp"
 #include "kvclient.hpp"
 #include "member.hpp"
 #include "netrpc.hpp"
@@ -417,6 +418,52 @@ void scenario_shm() {
   disp.join();
 }
 
+// The Send watchdog's abort against the engines' enqueues (csrc/core/dp_link.hpp;
+// the watchdog must never free a communicator an engine is inside).
+// Engine threads enter / "enqueue" / leave in a loop while the watchdog retires the
+// cell mid-Send and then "aborts" the communicator: no enqueue may ever see it
+// aborted, retire hands it out once, and every enqueue after the poison is refused.
+void scenario_commcell() {
+  struct Comm {
+    std::atomic<int> alive{1};
+    std::atomic<long> uses{0};
+  };
+  for (int round = 0; round < 24; ++round) {
+    auto* comm = new Comm;
+    CommCell cell;
+    cell.install(comm);
+    std::atomic<int> bad{0};
+    std::atomic<long> refused{0};
+    std::vector<std::thread> engines;
+    for (int t = 0; t < 4; ++t)
+      engines.emplace_back([&, t] {
+        for (int i = 0; i < 4000; ++i) {
+          void* c = cell.enter();
+          if (!c) {
+            refused.fetch_add(1);
+            continue;
+          }
+          auto* cm = static_cast<Comm*>(c);
+          if (!cm->alive.load()) bad.fetch_add(1);
+          cm->uses.fetch_add(1);  // the RCCL enqueue
+          if ((i + t) % 97 == 0) std::this_thread::sleep_for(std::chrono::microseconds(30));
+          if (!cm->alive.load()) bad.fetch_add(1);
+          cell.leave();
+        }
+      });
+    std::this_thread::sleep_for(std::chrono::microseconds(200 + 150 * (round % 8)));
+    void* c = cell.retire(5.0);  // the watchdog, mid-Send
+    CHECK(c == comm);
+    comm->alive.store(0);  // ncclCommAbort: from here any use would be a use after free
+    CHECK(cell.retire(5.0) == nullptr);  // handed out once
+    CHECK(cell.failed() && cell.enter() == nullptr);
+    for (auto& th : engines) th.join();
+    CHECK(bad.load() == 0);
+    CHECK(cell.users.load() == 0);
+    delete comm;
+  }
+}
+
 // Elastic scale-out: a second member joins as a learner through the first one's
 // client URL and is promoted once caught up (cluster/cluster.go:105-147, :183-195).
 void scenario_learner(const std::string& dir) {
@@ -456,7 +503,7 @@ int main(int argc, char** argv) {
   }
   const std::string dir = argv[1];
   std::vector<std::string> want(argv + 2, argv + argc);
-  if (want.empty()) want = {"channel", "raft", "rpc", "api", "learner", "shm"};
+  if (want.empty()) want = {"channel", "raft", "rpc", "api", "learner", "shm", "commcell"};
   std::map<std::string, std::function<void()>> all = {
       {"channel", [] { scenario_channel(); }},
       {"raft", [&] { scenario_raft(dir); }},
@@ -464,6 +511,7 @@ int main(int argc, char** argv) {
       {"api", [&] { scenario_cluster_api(dir); }},
       {"learner", [&] { scenario_learner(dir); }},
       {"shm", [] { scenario_shm(); }},
+      {"commcell", [] { scenario_commcell(); }},
   };
   for (const auto& w : want) {
     auto it = all.find(w);

@@ -8,7 +8,8 @@ each sanitizer -- the sanitizer runtime has to own the process, which a Python
 extension module cannot give it -- and run concurrently-loaded scenarios:
 3-member Raft with concurrent writers, a prefix watch, lease keepalive and a
 leader failover; concurrent Call/Go with retries and a live re-balance; Join ->
-register -> NewClient -> Call -> Close; a learner join + promotion; the same-node shared-memory call path.  Any sanitizer report fails the test.
+register -> NewClient -> Call -> Close; a learner join + promotion; the same-node shared-memory call path;
+the Send watchdog retiring the data plane's communicator while engine threads enqueue.  Any sanitizer report fails the test.
 """
 import os
 import subprocess
@@ -30,5 +31,5 @@ def test_core_under_sanitizer(sanitizer, tmp_path):
     found = [x for x in REPORTS if x in out]
     assert not found, f"{sanitizer} sanitizer reports {found}:\n{out[-6000:]}"
     assert r.returncode == 0, out[-4000:]
-    for s in ("channel", "raft", "rpc", "api", "learner", "shm"):
+    for s in ("channel", "raft", "rpc", "api", "learner", "shm", "commcell"):
         assert f"OK {s}" in r.stdout
