@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void sx_fifo_fixup_kernel(uint32_t* __restrict
 
 // (2048-message tiles and the argument columns loaded with the actors measured no
 // faster: removed, profiles/r5_mailbox_ab.md)
-template <int MODE, int S>
+template <int MODE, int S, int SK>
 __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long long* __restrict__ desc,
                                                  unsigned* __restrict__ tctr, unsigned* __restrict__ ticket,
                                                  uint32_t* __restrict__ sendbuf, int64_t req_stride,
@@ -456,16 +456,16 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
   const uint32_t t = tile_s, tag = tag_s;
   const uint32_t rbits = R > 1 ? 32 - __builtin_clz((uint32_t)R - 1) : 0;
   // phase 1: routes and ranks (a small register file: occupancy hides the gathers)
-  uint32_t pr[kSK], mb[kSK];
+  uint32_t pr[SK], mb[SK];
   uint32_t mbmax = 0;
   {
-    uint32_t a[kSK];
-    int r[kSK];
-    load_actors(in, t, a);
-    resolve_k<MODE>(in, a, r, mb);
+    uint32_t a[SK];
+    int r[SK];
+    load_actors<SK>(in, t, a);
+    resolve_k<MODE, SK>(in, a, r, mb);
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      const bool ok = tile_index(t, k) < in.M && r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
+    for (int k = 0; k < SK; ++k) {
+      const bool ok = tile_index<SK>(t, k) < in.M && r[k] >= 0 && r[k] < R && mb[k] < kMaxMbox;
       if (ok) mbmax = mb[k] > mbmax ? mb[k] : mbmax;
       const uint32_t bk = ok ? (uint32_t)r[k] : 0u;
       const uint64_t peers = match_bits(bk, rbits, __ballot(ok));
@@ -523,8 +523,8 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
   MetaAcc acc;
   uint32_t n_ovf = 0;
 #pragma unroll
-  for (int k = 0; k < kSK; ++k) {
-    const int64_t i = tile_index(t, k);
+  for (int k = 0; k < SK; ++k) {
+    const int64_t i = tile_index<SK>(t, k);
     if (i >= in.M) continue;
     const uint32_t rk = pr[k] & 0xffu;
     if (rk == 0xffu) {
@@ -592,9 +592,11 @@ __device__ __forceinline__ void sx_onesweep_body(SortIn in, int R, unsigned long
       bool reserve, bool reject_ordered
 #define PT_SX_OS_ARGS \
   in, R, desc, tctr, ticket, sendbuf, req_stride, C, caps, hdr_word3, rank_self, L, perm, meta, stats, rcnt, reserve, reject_ordered
-template <int MODE, int S>
+// SK messages per thread: kSK (4096-message tiles), or 2 (1024) for a small chunk -- a
+// 512 Ki chunk is 128 tiles of 4096, a grid that leaves half the CUs idle
+template <int MODE, int S, int SK = kSK>
 __global__ __launch_bounds__(kST) void sx_onesweep_kernel(PT_SX_OS_PARAMS) {
-  sx_onesweep_body<MODE, S>(PT_SX_OS_ARGS);
+  sx_onesweep_body<MODE, S, SK>(PT_SX_OS_ARGS);
 }
 #undef PT_SX_OS_PARAMS
 #undef PT_SX_OS_ARGS
@@ -1159,19 +1161,35 @@ void SortedExchange::send(const SxSend& a) {
   PT_HIP_CHECK(hipSetDevice(device_));
   if (fake_) fake_->check();  // an earlier collective's failure surfaces here (IpcComm: a peer missed one)
   const hipStream_t cs = as_stream(a.stream);
-  // tune sx_comm_cs=1: the collectives on the caller's stream itself (a graph-capture probe:
-  // tools/rccl_capture_probe.py sx1cs) instead of the engine's comm stream
   // Under a hipGraph capture the collectives go on the capturing stream itself: RCCL calls on a
   // stream forked into the capture crash graph instantiation on this stack, issued on the
   // capture stream they instantiate and replay correctly (tools/rccl_capture_probe.py sx1cs,
   // profiles/r3_rccl_capture_probe.txt) -- the captured Send then runs its chunks' collectives in
   // order with their compute instead of beside it.
   const Tune tn = tune();
-  const bool comm_on_cs = tn.sx_comm_cs != 0;
+  // Small Sends put their collectives on the caller's stream: a Send of up to
+  // kSxSmallSend messages is bound by its ~26 HIP calls (~90 us of host time, eight
+  // of them cross-stream event hand-offs), not by its bytes -- on one stream it
+  // issues 15 calls (~31 us) and its GPU side loses the hand-off gaps (loopback-8,
+  // 256 Ki / 1 Mi msgs per rank: 0.120 -> 0.089 / 0.130 -> 0.103 ms per step,
+  // profiles/r6_small_sends.md).  Larger Sends keep the comm stream, whose
+  // all-to-alls overlap the other chunk's kernels.  A per-rank choice: RCCL matches
+  // collectives by their order on the communicator, not by stream (the switch from
+  // the comm stream joins it first, below).
+  // tune sx_comm_cs: -1 auto (the rule above), 0 never, 1 always (a graph-capture probe:
+  // tools/rccl_capture_probe.py sx1cs)
+  const bool comm_on_cs = tn.sx_comm_cs > 0 || (tn.sx_comm_cs < 0 && a.M <= kSxSmallSend);
   self_copy_ = tn.sx_self_copy != 0;
   hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;
   const bool capturing = hipStreamIsCapturing(cs, &capst) == hipSuccess && capst != hipStreamCaptureStatusNone;
   cur_comm_ = (comm_on_cs || (capturing && cell_)) ? cs : comm_stream_;
+  if (cur_comm_ == cs && last_comm_ == comm_stream_ && !capturing) {
+    // the comm stream's last collectives (the previous Send's agreement) ahead of this
+    // Send's on the caller's stream: one communicator, one order of execution
+    PT_HIP_CHECK(hipEventRecord(ev_join_, comm_stream_));
+    PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_join_, 0));
+  }
+  if (!capturing) last_comm_ = cur_comm_ == cs ? nullptr : comm_stream_;
   pick_spec(cs);
   const PackedLayout L = L_;
   const int S = sx_round_S(L.S);
@@ -1274,9 +1292,11 @@ void SortedExchange::send(const SxSend& a) {
     in.tpb = (uint32_t)((tiles + in.G - 1) / in.G);
     return in;
   };
+  // (one stream for both sides: stream order is the hand-off, no events)
+  const bool split = cur_comm_ != cs;
   auto serve = [&](int i) {
     Bufs& b = bufs_[i];
-    PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_req_in_[i], 0));
+    if (split) PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_req_in_[i], 0));
     // ~2048 blocks over the R regions (at least one per region)
     const int64_t per = std::max<int64_t>(1, max_chunk_ / R_);
     constexpr int drain_blocks = 2048, drain_per = 1024;
@@ -1319,10 +1339,12 @@ void SortedExchange::send(const SxSend& a) {
 #undef PT_SX_ORD
     }
     PT_HIP_CHECK(hipGetLastError());
-    PT_HIP_CHECK(hipEventRecord(ev_served_[i], cs));
-    PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_served_[i], 0));
+    if (split) {
+      PT_HIP_CHECK(hipEventRecord(ev_served_[i], cs));
+      PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_served_[i], 0));
+    }
     a2a(b.reply, b.back, (size_t)rp * 4, pairs ? rp_send : nullptr, pairs ? rp_recv : nullptr, capturing);
-    PT_HIP_CHECK(hipEventRecord(ev_rep_in_[i], cur_comm_));
+    if (split) PT_HIP_CHECK(hipEventRecord(ev_rep_in_[i], cur_comm_));
   };
   for (int i = 0; i < chunks_; ++i) {
     Bufs& b = bufs_[i];
@@ -1356,7 +1378,22 @@ void SortedExchange::send(const SxSend& a) {
     case 6: PT_SX_OS(MO, 6); break; \
     default: PT_SX_OS(MO, 8); break; \
   }
-      if (mode == 3) {
+      // a chunk of under 512 tiles: 1024-message tiles (8-B records of the directory routes)
+      const bool small_tiles = reserve && S <= 2 && (mode == 3 || mode == 1) && in.tiles < 512;
+      if (small_tiles) {
+        SortIn in1 = in;
+        in1.tiles = (uint32_t)((m + kST * 2 - 1) / (kST * 2));
+#define PT_SX_OS1(MO, SV)                                                                                        \
+  hipLaunchKernelGGL((sx_onesweep_kernel<MO, SV, 2>), dim3(in1.tiles), dim3(kST), 0, cs, in1, R_, desc_, tctr_,   \
+                     ticket_, b.send, rq, (uint32_t)C, caps_out, hdr3, rank_, L, b.perm,                  \
+                     (unsigned long long*)meta, stats_, rcnt_ + i * kSxMaxRanks, reserve, reject_ordered)
+        if (mode == 3) {
+          if (S == 1) PT_SX_OS1(3, 1); else PT_SX_OS1(3, 2);
+        } else {
+          if (S == 1) PT_SX_OS1(1, 1); else PT_SX_OS1(1, 2);
+        }
+#undef PT_SX_OS1
+      } else if (mode == 3) {
         PT_SX_OS_S(3)
       } else if (mode == 2) {
         PT_SX_OS_S(2)
@@ -1368,10 +1405,12 @@ void SortedExchange::send(const SxSend& a) {
 #undef PT_SX_OS_S
 #undef PT_SX_OS
       PT_HIP_CHECK(hipGetLastError());
-      PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
-      PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
+      if (split) {
+        PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
+        PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
+      }
       a2a(b.send, b.recv, (size_t)rq * 4, pairs ? rq_send : nullptr, pairs ? rq_recv : nullptr, capturing);
-      PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], cur_comm_));
+      if (split) PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], cur_comm_));
       if (i > 0) serve(i - 1);
       continue;
     }
@@ -1419,10 +1458,12 @@ void SortedExchange::send(const SxSend& a) {
 #undef PT_SX_FIX
     }
     PT_HIP_CHECK(hipGetLastError());
-    PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
-    PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
+    if (split) {
+      PT_HIP_CHECK(hipEventRecord(ev_routed_[i], cs));
+      PT_HIP_CHECK(hipStreamWaitEvent(cur_comm_, ev_routed_[i], 0));
+    }
     a2a(b.send, b.recv, (size_t)rq * 4, pairs ? rq_send : nullptr, pairs ? rq_recv : nullptr, capturing);
-    PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], cur_comm_));
+    if (split) PT_HIP_CHECK(hipEventRecord(ev_req_in_[i], cur_comm_));
     if (i > 0) serve(i - 1);
   }
   serve(chunks_ - 1);
@@ -1448,7 +1489,7 @@ void SortedExchange::send(const SxSend& a) {
   for (int i = 0; i < chunks_; ++i) {
     int64_t lo, m;
     (void)chunk_in(i, lo, m);
-    PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_rep_in_[i], 0));
+    if (split) PT_HIP_CHECK(hipStreamWaitEvent(cs, ev_rep_in_[i], 0));
     if (m > 0) {
       // the first completion also clears the agreement buffer of Send + 1 (that of
       // Send - 1, whose copy to the host precedes this Send's reply all-to-alls)

@@ -55,6 +55,7 @@ constexpr int kSxShardBits = 6;  // actor shards per rank on the wire: mailbox &
 constexpr int kSxShards = 1 << kSxShardBits;
 constexpr int kSxMaxRanks = 16;
 constexpr int kSxMaxChunks = 4;
+constexpr int64_t kSxSmallSend = 2 << 20;  // Sends of up to this many messages: collectives on the caller's stream
 constexpr int kSxTableWords = (kSxShards + 1 + 3) & ~3;  // shard table, right after a request region's header
 constexpr int kSxRecOff = 4 + kSxTableWords;             // records start here: a region's used part is a prefix
 // request region words for n records of S dwords: [header 4][shard table][n * S], 16-B padded
@@ -155,6 +156,7 @@ class SortedExchange {
   int64_t max_chunk_, C_alloc_;
   hipStream_t comm_stream_ = nullptr;
   hipStream_t cur_comm_ = nullptr;  // the stream this Send's collectives go on (comm_stream_, or the caller's)
+  hipStream_t last_comm_ = nullptr;  // comm_stream_ when the last eager Send's collectives went there
   Bufs bufs_[kSxMaxChunks];
   uint32_t* hist_ = nullptr;  // [G][R * K] per-block bucket counts -> prefixes (K = 64 or 1)
   uint32_t* boff_ = nullptr;  // [R * K] bucket offsets within their region

@@ -21,7 +21,8 @@
 //                              1 look-back one pass, 2 count + scan + scatter
 //   sx_self_copy      0        world-1 sorted exchange: the all-to-alls as device copies
 //                              (RCCL calls on a forked stream cannot be graph-captured)
-//   sx_comm_cs        0        sorted exchange collectives on the caller's stream
+//   sx_comm_cs        -1       sorted exchange collectives on the caller's stream (-1: Sends
+//                              of up to 2 Mi messages, 0 never, 1 always)
 //   stream_sync       0        epoch engine hand-offs: 0 events, 1 stream wait-value packets
 //   local             1        world-1 epoch Sends: the fused local pass (0: the slot pipeline)
 //   persistent_stream low      queue of persistent kernels: low / high / cumask / pooled
@@ -42,7 +43,7 @@ struct Tune {
   int mbox_drain_msg = 0;
   int sx_sort = 0;
   int sx_self_copy = 0;
-  int sx_comm_cs = 0;
+  int sx_comm_cs = -1;
   int stream_sync = 0;
   int local = 1;
   std::string persistent_stream = "low";

@@ -355,3 +355,28 @@ def test_alternate_sort_kernels_exact_in_a_subprocess():
     env = dict(os.environ, PTYPE_TUNE="sx_sort=1,mbox_sort=2,mbox_drain_msg=1")
     p = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0 and "SUBPROCESS-OK" in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
+
+
+@pytest.mark.parametrize("M", [600_000, 4_500_000])
+def test_sorted_exchange_loopback_both_tile_sizes_exact(M):
+    """The sender's one-pass sort takes 1024-message tiles for a chunk of under 512
+    4096-message tiles and 4096-message tiles above (exchange_sorted.hip): both
+    exact on the loopback R = 8 pipeline (the bench's --loopback stand-in), Send
+    after Send with new batches in the same tensors -- 600 K messages also run their
+    collectives on the caller's stream (a small Send), 4.5 M on the comm stream."""
+    R = 8
+    n = 4096 * R
+    tab, _ = _table(n, R)
+    ex = ActorExchange(tab, M, chunks=2, state=torch.zeros(n // R + 1, dtype=torch.int64, device="cuda"),
+                       fake=(hip().FakeComm(R, loopback=True), 0), delivery="mailbox", mailbox_ordered=False)
+    req = B.MsgBatch(torch.empty(M, dtype=torch.int32, device="cuda"), torch.empty(M, dtype=torch.int64, device="cuda"),
+                     torch.empty(M, dtype=torch.int64, device="cuda"), None, METHOD_CALC_MULTIPLY)
+    val = torch.empty(M, dtype=torch.int64, device="cuda")
+    st = torch.empty(M, dtype=torch.int32, device="cuda")
+    for s in range(5):
+        B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=40 + s, device="cuda", out=req)
+        ex.send_all(req, out=(val, st))
+        torch.cuda.synchronize()
+        assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1), s
+    assert ex.last_wire["S"] == 2 and ex.last_wire["agreed"]
+    assert ex.stats().failed == 0
