@@ -427,7 +427,10 @@ def main():
             return {}
         # mailbox_shards: the rings allocated; ring_view_shards: how the timed Sends used them (stateless
         # batches: a coarser view of the same rings, every actor's messages still in one ring)
-        return {"mailbox_shards": mb.shards, "ring_view_shards": mb.last_view_shards, "mailbox_slots": mb.slots,
+        # sharding_used: the rings the timed Sends took (a batch without ordered methods of up to
+        # 2 Mi messages takes the arrival rings even when actor sharding is asked for)
+        return {"sharding_used": getattr(mb, "last_sharding", None),
+                "mailbox_shards": mb.shards, "ring_view_shards": mb.last_view_shards, "mailbox_slots": mb.slots,
                 "mailbox_ring_bytes": mb.bytes, "mailbox_record_bytes": mb.last_record_bytes,
                 "mailbox_route": mb.last_route}
 

@@ -178,6 +178,29 @@ void Mailboxes::send_sorted(const MboxSend& a) {
   if (a.arrival) {  // fixed positions: enqueue + drain, no count pass
     last_rec_bytes_ = (a.a2 || a.method_col) ? 32 : 16;
     last_view_shards_ = S;
+    last_route_ = mode;
+    if (!a.a2 && !a.method_col && fused_ok(tiles)) {  // both in one launch (mbx_arrival_fused_kernel)
+      // rank byte routes for a stateless method on the directory: the records carry actor ids
+      const bool rank_arr = mode == 1 && a.dir_rank && a.n_dir <= kMaxMbox && method_stateless((uint32_t)a.method_uniform);
+      if (rank_arr) last_route_ = 3;
+#define PT_AFUSED(MO, FX)                                                                                         \
+  hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX>), dim3(tile_grid), dim3(kST), 0, st, in, mv_, (int64_t*)a.state, \
+                     a.n_state, a.delay_ticks, ob, rv, sort_ticket_)
+      if (fixed_mul) {
+        if (rank_arr) PT_AFUSED(3, kCalculatorMultiply);
+        else if (mode == 2) PT_AFUSED(2, kCalculatorMultiply);
+        else if (mode == 1) PT_AFUSED(1, kCalculatorMultiply);
+        else PT_AFUSED(0, kCalculatorMultiply);
+      } else {
+        if (rank_arr) PT_AFUSED(3, 0);
+        else if (mode == 2) PT_AFUSED(2, 0);
+        else if (mode == 1) PT_AFUSED(1, 0);
+        else PT_AFUSED(0, 0);
+      }
+#undef PT_AFUSED
+      PT_HIP_CHECK(hipGetLastError());
+      return;
+    }
 #define PT_AENQ(MO)                                                                                        \
   do {                                                                                                     \
     if (a.a2 && a.method_col)                                                                              \

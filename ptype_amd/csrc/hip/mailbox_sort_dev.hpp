@@ -1151,6 +1151,123 @@ __global__ __launch_bounds__(kST) void mbx_arrival_drain_kernel(MboxView mv, Sor
   }
 }
 
+// Arrival rings, enqueue and drain in ONE launch (batches of up to 512 tiles: at 1 Mi
+// messages the second launch, its ramp and its tail were ~5 of the two kernels' 25 us,
+// profiles/r6_small_sends.md).  Block t writes tile t's records into its run of ring
+// t & (S - 1), exactly as mbx_arrival_enqueue_kernel does, and after a block barrier
+// drains that run: wave w consumes the records wave w ^ 4 wrote -- read back from the
+// ring, decoded, its handler run -- so the ring is the hand-off between the block's
+// waves, as it is between the two kernels (no grid-wide phase is needed: an arrival
+// run belongs to one tile).  Uniform batches of at most two arguments, 16-B compact
+// records (32-B long form for a value past 32 bits); MODE 3 (rank byte routes,
+// stateless methods) carries actor ids.  (8-B records chosen per tile, with the
+// block-wide vote that takes, measured slower: 30.6 vs 33.1 G msg/s per 1 Mi step.)
+template <int MODE, int FIXED>
+__global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxView mv, int64_t* __restrict__ state,
+                                                                uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
+                                                                ReplyView rv, unsigned* __restrict__ ticket) {
+  unsigned long long n_enq = 0, n_miss = 0, n_spill = 0, done = 0, failed = 0;
+  const uint32_t S = 1u << mv.log_s;
+  const uint32_t t = virt_block(blockIdx.x, gridDim.x);
+  if (t < in.tiles) {
+    uint64_t pos0 = 0;
+    const bool fits = arrival_fits(mv, in, t, pos0);
+    const uint32_t s = t & (S - 1);
+    uint32_t a[kSK], mb[kSK];
+    int64_t x0[kSK], x1[kSK];
+    int r[kSK];
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      const int64_t i = tile_index(t, k);
+      const bool ok = i < in.M;
+      a[k] = ok ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
+      x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
+      x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
+    }
+    resolve_k<MODE>(in, a, r, mb);
+    bool live[kSK];
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {  // enqueue: the tile's records at their fixed ring positions
+      const int64_t i = tile_index(t, k);
+      live[k] = false;
+      if (i >= in.M) continue;
+      const uint32_t origin = in.origin_base + (uint32_t)i;
+      const bool ok = r[k] == in.rank_self && mb[k] < kMaxMbox;
+      const uint64_t slot = slot_at(mv, s, pos0 + (uint64_t)(i - (int64_t)t * kSTile));
+      if (!ok) {
+        ++n_miss;
+        write_status(rv, origin, kStatusNoActor);
+        if (fits) *reinterpret_cast<u32x4*>(rec_a(mv, slot)) = u32x4{0u, 0u, 0u, 0u};
+        continue;
+      }
+      live[k] = true;
+      if (!fits) {  // the tile spilled: its messages run from the registers below
+        ++n_spill;
+        continue;
+      }
+      const uint32_t mt = in.method_uniform;
+      if (mt < 128u && fits_i32(x0[k]) && fits_i32(x1[k])) {
+        *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
+            u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)x0[k], (uint32_t)x1[k]};
+      } else {
+        *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
+            u32x4{origin | kCompactMark, mb[k] | kCompactLong, mt & 0xffffu, 0u};
+        *reinterpret_cast<u32x4*>(rec_b(mv, slot)) = u32x4{(uint32_t)x0[k], (uint32_t)((uint64_t)x0[k] >> 32),
+                                                           (uint32_t)x1[k], (uint32_t)((uint64_t)x1[k] >> 32)};
+      }
+      ++n_enq;
+    }
+    __syncthreads();  // the run is in the ring: drain it
+    const uint32_t w2 = (threadIdx.x / kWave) ^ 4u;  // (the wave whose records this one consumes)
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      SortRec x;
+      int64_t i;
+      if (fits) {  // wave w2's k-th record of this lane
+        const uint32_t j = w2 * (kSK * kWave) + (uint32_t)k * kWave + lane_id();
+        i = (int64_t)t * kSTile + j;
+        if (i >= in.M) continue;
+        const uint64_t slot = slot_at(mv, s, pos0 + j);
+        const u32x4 ha = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
+        const u32x4 hb = rec_is_long(ha) ? *reinterpret_cast<const u32x4*>(rec_b(mv, slot)) : u32x4{0u, 0u, 0u, 0u};
+        x = decode_sorted(ha, hb, 0);  // a zero record (no actor): not valid
+        if (!x.valid) continue;
+      } else {  // a spilled tile: this thread's own messages, from its registers
+        if (!live[k]) continue;  // (no actor: answered above)
+        i = tile_index(t, k);
+        x.valid = true, x.mb = mb[k], x.method = in.method_uniform, x.flags = 0;
+        x.a0 = x0[k], x.a1 = x1[k], x.a2 = 0;
+      }
+      MsgRecord m;
+      m.actor = x.mb;
+      m.method = (uint16_t)(FIXED ? FIXED : x.method);
+      m.flags = (uint16_t)x.flags;
+      m.a0 = x.a0, m.a1 = x.a1, m.a2 = 0;
+      const ReplyRecord rr = run_handler(m, state, n_state, delay_ticks, ob);
+      failed += rr.status != kStatusOk;
+      write_reply(rv, in.origin_base + (uint32_t)i, rr);
+      ++done;
+    }
+  }
+  block_add_stats(mv.stats, n_enq, kMbEnqueued, n_miss, kMbNoActor, n_spill, kMbSpilled);
+  __syncthreads();  // block_add_stats' LDS partials are reused
+  block_add_stats(mv.stats, done, kMbProcessed, failed, kMbFailed, 0, -1);
+  __shared__ bool last;
+  if (threadIdx.x == 0) last = last_block_ticket(ticket);
+  __syncthreads();
+  if (last) {  // every tile is read: each shard consumed the positions of its tiles that fit
+    for (uint32_t sh = threadIdx.x; sh < S; sh += kST) {
+      uint64_t used = 0;
+      for (uint32_t tt = sh; tt < in.tiles; tt += S) {
+        uint64_t p0 = 0;
+        if (!arrival_fits(mv, in, tt, p0)) break;  // the spilled suffix
+        used += min((uint64_t)kSTile, (uint64_t)in.M - (uint64_t)tt * kSTile);
+      }
+      epoch_commit(mv, sh, (uint32_t)used);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- K3s ordered drain
 // One block owns shard s: its actors' state is staged in LDS (when it fits), and
 // the shard's records are taken in windows of kOrdWin in ring order.  A window

@@ -54,6 +54,7 @@ class Mailboxes:
         idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self._m = hip().Mailboxes(idx, int(shards), int(slots), bool(with_a2))
         self.shards, self.slots = int(shards), int(slots)
+        self.last_sharding = None  # the rings the last send() took ("actor" / "arrival")
 
     @property
     def bytes(self) -> int:
@@ -133,6 +134,7 @@ class Mailboxes:
             raise ValueError("sharding: 'actor' or 'arrival'")
         ordered = batch_ordered(batch) if ordered is None else bool(ordered)
         arrival = sharding == "arrival"
+        self.last_sharding = sharding
         if arrival and ordered:
             raise ValueError("arrival sharding cannot serve ordered methods (an actor's messages meet in no one ring)")
         # the rings are empty between Sends, so a uniform batch fixes every queued method

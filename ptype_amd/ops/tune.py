@@ -16,6 +16,8 @@ keys (read when an exchange is built or per Send):
   sorted_exchange  1        N > 1 mailbox delivery through the sorted exchange
   device_pump      1        device-counted pump epochs (0: a host round trip per epoch)
   pump_graph       1        world-1 pump groups replayed from a hipGraph
+  auto_arrival     1        world-1 mailbox Sends without ordered methods, up to 2 Mi
+                            messages: arrival rings (0: the actor-sharded sort)
 
 The native keys are listed in csrc/hip/tune.hpp; ``set`` forwards them.
 """
@@ -24,7 +26,8 @@ from __future__ import annotations
 import os
 
 _PY_DEFAULTS = {"engine": 1, "wire": 3, "adaptive_c": 1, "skew_room": 4.0, "sorted_room": 2.5, "direct": -1,
-                "sorted_exchange": 1, "device_pump": 1, "pump_graph": 1}
+                "sorted_exchange": 1, "device_pump": 1, "pump_graph": 1,
+                "auto_arrival": 1}
 _overrides: dict[str, str] = {}
 
 

@@ -772,3 +772,75 @@ def test_mailbox_seqfold_in_8b_records_exactly_once_fifo():
         assert o["ok"] and o["all_ok"] and o["fifo"], (rnd, o)
         assert o["resends"] == 0, (rnd, o)  # escapes: no message of an ordered Send overflows
     assert out["0"]["rec_bytes"] == 8 and out["2"]["rec_bytes"] == 8, out  # the ordered Sends really took 8-B records
+
+
+@pytest.mark.parametrize("M,slots", [(1 << 20, 1 << 16), (300_000, 2048)])
+def test_arrival_fused_enqueue_drain_exact(M, slots):
+    """Arrival rings in one launch (mbx_arrival_fused_kernel: each block writes its
+    tile's records into its ring run, then drains that run): stateless Multiply on
+    rank byte routes (records carry actor ids) with unknown actors, exact -- in 16-B
+    compact records, and 32-B long ones for values past 32 bits; the
+    commutative stateful CounterAdd through the same kernel (hash routes: every
+    actor's count exact); with small rings the tiles past a ring's room spill and
+    run from the batch.  Every ring drained afterwards."""
+    from ptype_amd.ops.records import METHOD_COUNTER_ADD
+
+    n = 1 << 14
+    t, _ = placed_table(n)
+    mb = Mailboxes(DEV, shards=64, slots=slots)
+    g = torch.Generator().manual_seed(21)
+    actor = torch.randint(0, n + 700, (M,), generator=g, dtype=torch.int32).to(DEV)
+    a0 = torch.randint(-(1 << 15), 1 << 15, (M,), generator=g, dtype=torch.int64).to(DEV)
+    a1 = torch.randint(-(1 << 15), 1 << 15, (M,), generator=g, dtype=torch.int64).to(DEV)
+    known = actor < n
+    for k in range(3):
+        if k == 2:  # a wide value in some tiles: those tiles take 16-B (or 32-B long) records
+            a0 = a0.clone()
+            a0[::40_000] = (1 << 40) + 7
+            a1 = a1.clone()
+            a1[5::70_000] = 1 << 21
+        val, st = mb.send(B.MsgBatch(actor, a0, a1, None, METHOD_CALC_MULTIPLY), t, None, ordered=False,
+                          sharding="arrival")
+        torch.cuda.synchronize()
+        assert mb.last_sharding == "arrival" and mb.last_route == 3
+        assert torch.equal(st, torch.where(known, STATUS_OK, STATUS_NO_ACTOR).to(torch.int32)), k
+        assert torch.equal(val[known], (a0 * a1)[known]), k
+    state = torch.zeros(n, dtype=torch.int64, device=DEV)
+    ones = torch.ones(M, dtype=torch.int64, device=DEV)
+    _, st = mb.send(B.MsgBatch(actor, ones, None, None, METHOD_COUNTER_ADD), t, state, ordered=False,
+                    sharding="arrival")
+    torch.cuda.synchronize()
+    assert mb.last_route == 1  # (a stateful method keeps its mailbox route)
+    assert torch.equal(st, torch.where(known, STATUS_OK, STATUS_NO_ACTOR).to(torch.int32))
+    ref = torch.zeros(n, dtype=torch.int64)
+    ref.index_add_(0, actor[known].long().cpu(), torch.ones(int(known.sum()), dtype=torch.int64))
+    _, perm = placed_table(n)
+    got = torch.empty(n, dtype=torch.int64)
+    got[torch.arange(n)] = state.cpu()[perm]  # actor a lives in mailbox perm[a]
+    assert torch.equal(got, ref)
+    s = mb.stats()
+    if slots < M // 64:
+        assert s["spilled"] > 0, s
+    assert s["overflow"] == 0, s
+    ctr = mb.shard_counters()
+    assert (ctr[:, 0] == ctr[:, 2]).all()
+
+
+def test_exchange_takes_arrival_rings_for_small_stateless_sends():
+    """World-1 ActorExchange with actor-sharded mailboxes (the default): a batch
+    without ordered methods of up to 2 Mi messages takes the arrival rings (tune
+    auto_arrival), an ordered one keeps the actor-sharded sort; replies exact."""
+    n, M = 1 << 14, 400_000
+    t, _ = placed_table(n)
+    state = torch.zeros(n, dtype=torch.int64, device=DEV)
+    ex = ActorExchange(t, M, delivery="mailbox", state=state)
+    req = B.gen_requests(M, n, METHOD_CALC_MULTIPLY, seed=5, device=DEV)
+    val, st = ex.send(req)
+    torch.cuda.synchronize()
+    assert ex.mailboxes.last_sharding == "arrival"
+    assert bool((st == STATUS_OK).all()) and torch.equal(val, req.a0 * req.a1)
+    fold = fold_batch(M, n, seed=6)
+    val, st = ex.send(fold)
+    torch.cuda.synchronize()
+    assert ex.mailboxes.last_sharding == "actor"
+    assert bool((st == STATUS_OK).all())
