@@ -496,7 +496,10 @@ def main():
                                  "value": Mq * args.steps / e3 if e3 > 0 else 0.0,
                                  "ms_per_step": e3 / args.steps * 1e3, **mailbox_info(ex3)}
             if kw["delivery"] == "mailbox":
-                secondaries[name]["sharding"] = kw.get("sharding", "actor")
+                asked = kw.get("sharding", "actor")
+                used = secondaries[name].get("sharding_used")
+                secondaries[name]["sharding"] = asked if used in (None, asked) else (
+                    f"{asked} asked; {used} rings used (a batch without ordered methods of <= 2 Mi messages)")
                 secondaries[name]["method"] = "SeqFold (ordered)" if kw.get("method") == METHOD_SEQ_FOLD \
                     else "Calculator.Multiply"
                 secondaries[name]["args"] = "full-range int64" if kw.get("wide") else "A: 16-bit signed, B: 16-bit"
