@@ -179,13 +179,19 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     last_rec_bytes_ = (a.a2 || a.method_col) ? 32 : 16;
     last_view_shards_ = S;
     last_route_ = mode;
-    if (!a.a2 && !a.method_col && fused_ok(tiles)) {  // both in one launch (mbx_arrival_fused_kernel)
+    // both in one launch (mbx_arrival_fused_kernel): an arrival run belongs to one tile, so the
+    // fused form needs no grid-wide phase at any size (tune mbox_fused=0: the two kernels)
+    if (!a.a2 && !a.method_col && tn.mbox_fused != 0) {
       // rank byte routes for a stateless method on the directory: the records carry actor ids
       const bool rank_arr = mode == 1 && a.dir_rank && a.n_dir <= kMaxMbox && method_stateless((uint32_t)a.method_uniform);
       if (rank_arr) last_route_ = 3;
+      // 8-B records past 512 tiles (tune mbox_rec8: the sort's rule; per wave, 16 B when a value
+      // of the wave does not fit)
+      const bool allow8 = mv_.planar && (tn.mbox_rec8 == 1 || (tn.mbox_rec8 < 0 && tiles > 512));
+      if (allow8) last_rec_bytes_ = 8;
 #define PT_AFUSED(MO, FX)                                                                                         \
   hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX>), dim3(tile_grid), dim3(kST), 0, st, in, mv_, (int64_t*)a.state, \
-                     a.n_state, a.delay_ticks, ob, rv, sort_ticket_)
+                     a.n_state, a.delay_ticks, ob, rv, sort_ticket_, allow8)
       if (fixed_mul) {
         if (rank_arr) PT_AFUSED(3, kCalculatorMultiply);
         else if (mode == 2) PT_AFUSED(2, kCalculatorMultiply);

@@ -1151,24 +1151,39 @@ __global__ __launch_bounds__(kST) void mbx_arrival_drain_kernel(MboxView mv, Sor
   }
 }
 
-// Arrival rings, enqueue and drain in ONE launch (batches of up to 512 tiles: at 1 Mi
-// messages the second launch, its ramp and its tail were ~5 of the two kernels' 25 us,
-// profiles/r6_small_sends.md).  Block t writes tile t's records into its run of ring
-// t & (S - 1), exactly as mbx_arrival_enqueue_kernel does, and after a block barrier
-// drains that run: wave w consumes the records wave w ^ 4 wrote -- read back from the
-// ring, decoded, its handler run -- so the ring is the hand-off between the block's
-// waves, as it is between the two kernels (no grid-wide phase is needed: an arrival
-// run belongs to one tile).  Uniform batches of at most two arguments, 16-B compact
-// records (32-B long form for a value past 32 bits); MODE 3 (rank byte routes,
-// stateless methods) carries actor ids.  (8-B records chosen per tile, with the
-// block-wide vote that takes, measured slower: 30.6 vs 33.1 G msg/s per 1 Mi step.)
+// Arrival rings, enqueue and drain in ONE launch.  Block t writes tile t's records
+// into its run of ring t & (S - 1) (the positions mbx_arrival_enqueue_kernel uses) and,
+// after a block barrier, drains that run: wave w consumes the records wave w ^ 4 wrote
+// -- read back from the ring, decoded, its handler run -- so the ring is the hand-off
+// between the block's waves, as it is between the two kernels of the general form (no
+// grid-wide phase is needed: an arrival run belongs to one tile).  Uniform batches of at
+// most two arguments; MODE 3 (rank byte routes, stateless methods) carries actor ids.
+//
+// Record format per WAVE (its producer decides with one ballot and tells its consumer
+// through LDS, across the barrier the hand-off needs anyway; allow8 -- batches past 512
+// tiles, the rule of the sort's 8-B records): 8 B {mailbox 24 | zigzag
+// a0 20 | zigzag a1 20} when every message of the wave fits, in the first half of the
+// wave's own 512 slots (message j in half j & 1 of slot j / 2 of that range: formats
+// never overlap), else the 16-B compact form (32-B long form for a value past 32 bits).
+constexpr int kArr8Mb = 24, kArr8Arg = 20;
+constexpr uint64_t kArr8Null = ~0ull;  // a slot of no actor (mailbox 2^24 - 1 never fits the 8-B form)
+__device__ __forceinline__ bool arr8_fits(uint32_t mb, int64_t x0, int64_t x1) {
+  const uint64_t z0 = ((uint64_t)x0 << 1) ^ (uint64_t)(x0 >> 63), z1 = ((uint64_t)x1 << 1) ^ (uint64_t)(x1 >> 63);
+  return mb < (1u << kArr8Mb) - 1u && (z0 >> kArr8Arg) == 0 && (z1 >> kArr8Arg) == 0;
+}
+__device__ __forceinline__ uint64_t arr8_cell(const MboxView& mv, uint32_t s, uint64_t pos0, uint32_t j) {
+  return 2 * slot_at(mv, s, pos0 + (j & ~(uint32_t)(kSWave - 1)) + ((j & (kSWave - 1)) >> 1)) + (j & 1);
+}
 template <int MODE, int FIXED>
 __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxView mv, int64_t* __restrict__ state,
                                                                 uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
-                                                                ReplyView rv, unsigned* __restrict__ ticket) {
+                                                                ReplyView rv, unsigned* __restrict__ ticket,
+                                                                bool allow8) {
+  __shared__ uint32_t wave_rec8[kST / kWave];
   unsigned long long n_enq = 0, n_miss = 0, n_spill = 0, done = 0, failed = 0;
   const uint32_t S = 1u << mv.log_s;
   const uint32_t t = virt_block(blockIdx.x, gridDim.x);
+  const unsigned w = threadIdx.x / kWave;
   if (t < in.tiles) {
     uint64_t pos0 = 0;
     const bool fits = arrival_fits(mv, in, t, pos0);
@@ -1186,27 +1201,39 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
     }
     resolve_k<MODE>(in, a, r, mb);
     bool live[kSK];
+    bool narrow = allow8 && mv.planar != 0;
+#pragma unroll
+    for (int k = 0; k < kSK; ++k) {
+      live[k] = tile_index(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
+      if (live[k] && !arr8_fits(mb[k], x0[k], x1[k])) narrow = false;
+    }
+    const bool rec8 = __ballot(!narrow) == 0;  // (wave-uniform)
+    if (lane_id() == 0) wave_rec8[w] = rec8;
+    uint64_t* cells = reinterpret_cast<uint64_t*>(mv.rec);
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {  // enqueue: the tile's records at their fixed ring positions
       const int64_t i = tile_index(t, k);
-      live[k] = false;
       if (i >= in.M) continue;
       const uint32_t origin = in.origin_base + (uint32_t)i;
-      const bool ok = r[k] == in.rank_self && mb[k] < kMaxMbox;
-      const uint64_t slot = slot_at(mv, s, pos0 + (uint64_t)(i - (int64_t)t * kSTile));
-      if (!ok) {
+      const uint32_t j = (uint32_t)(i - (int64_t)t * kSTile);
+      const uint64_t slot = slot_at(mv, s, pos0 + j);
+      if (!live[k]) {
         ++n_miss;
         write_status(rv, origin, kStatusNoActor);
-        if (fits) *reinterpret_cast<u32x4*>(rec_a(mv, slot)) = u32x4{0u, 0u, 0u, 0u};
+        if (fits && rec8) cells[arr8_cell(mv, s, pos0, j)] = kArr8Null;
+        else if (fits) *reinterpret_cast<u32x4*>(rec_a(mv, slot)) = u32x4{0u, 0u, 0u, 0u};
         continue;
       }
-      live[k] = true;
       if (!fits) {  // the tile spilled: its messages run from the registers below
         ++n_spill;
         continue;
       }
       const uint32_t mt = in.method_uniform;
-      if (mt < 128u && fits_i32(x0[k]) && fits_i32(x1[k])) {
+      if (rec8) {
+        const uint64_t z0 = ((uint64_t)x0[k] << 1) ^ (uint64_t)(x0[k] >> 63);
+        const uint64_t z1 = ((uint64_t)x1[k] << 1) ^ (uint64_t)(x1[k] >> 63);
+        cells[arr8_cell(mv, s, pos0, j)] = (uint64_t)mb[k] | (z0 << kArr8Mb) | (z1 << (kArr8Mb + kArr8Arg));
+      } else if (mt < 128u && fits_i32(x0[k]) && fits_i32(x1[k])) {
         *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
             u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)x0[k], (uint32_t)x1[k]};
       } else {
@@ -1218,7 +1245,8 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
       ++n_enq;
     }
     __syncthreads();  // the run is in the ring: drain it
-    const uint32_t w2 = (threadIdx.x / kWave) ^ 4u;  // (the wave whose records this one consumes)
+    const uint32_t w2 = w ^ 4u;  // (the wave whose records this one consumes)
+    const bool rec8_2 = wave_rec8[w2] != 0;
 #pragma unroll
     for (int k = 0; k < kSK; ++k) {
       SortRec x;
@@ -1227,11 +1255,21 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
         const uint32_t j = w2 * (kSK * kWave) + (uint32_t)k * kWave + lane_id();
         i = (int64_t)t * kSTile + j;
         if (i >= in.M) continue;
-        const uint64_t slot = slot_at(mv, s, pos0 + j);
-        const u32x4 ha = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
-        const u32x4 hb = rec_is_long(ha) ? *reinterpret_cast<const u32x4*>(rec_b(mv, slot)) : u32x4{0u, 0u, 0u, 0u};
-        x = decode_sorted(ha, hb, 0);  // a zero record (no actor): not valid
-        if (!x.valid) continue;
+        if (rec8_2) {
+          const uint64_t c = cells[arr8_cell(mv, s, pos0, j)];
+          if (c == kArr8Null) continue;  // no actor: answered by the enqueue
+          x.valid = true, x.method = in.method_uniform, x.flags = 0, x.a2 = 0;
+          x.mb = (uint32_t)(c & ((1u << kArr8Mb) - 1));
+          const uint64_t z0 = (c >> kArr8Mb) & ((1ull << kArr8Arg) - 1), z1 = c >> (kArr8Mb + kArr8Arg);
+          x.a0 = (int64_t)(z0 >> 1) ^ -(int64_t)(z0 & 1);
+          x.a1 = (int64_t)(z1 >> 1) ^ -(int64_t)(z1 & 1);
+        } else {
+          const uint64_t slot = slot_at(mv, s, pos0 + j);
+          const u32x4 ha = *reinterpret_cast<const u32x4*>(rec_a(mv, slot));
+          const u32x4 hb = rec_is_long(ha) ? *reinterpret_cast<const u32x4*>(rec_b(mv, slot)) : u32x4{0u, 0u, 0u, 0u};
+          x = decode_sorted(ha, hb, 0);  // a zero record (no actor): not valid
+          if (!x.valid) continue;
+        }
       } else {  // a spilled tile: this thread's own messages, from its registers
         if (!live[k]) continue;  // (no actor: answered above)
         i = tile_index(t, k);

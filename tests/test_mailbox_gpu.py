@@ -774,17 +774,20 @@ def test_mailbox_seqfold_in_8b_records_exactly_once_fifo():
     assert out["0"]["rec_bytes"] == 8 and out["2"]["rec_bytes"] == 8, out  # the ordered Sends really took 8-B records
 
 
+@pytest.mark.parametrize("rec8", ["-1", "1"])
 @pytest.mark.parametrize("M,slots", [(1 << 20, 1 << 16), (300_000, 2048)])
-def test_arrival_fused_enqueue_drain_exact(M, slots):
+def test_arrival_fused_enqueue_drain_exact(M, slots, rec8, monkeypatch):
     """Arrival rings in one launch (mbx_arrival_fused_kernel: each block writes its
     tile's records into its ring run, then drains that run): stateless Multiply on
     rank byte routes (records carry actor ids) with unknown actors, exact -- in 16-B
-    compact records, and 32-B long ones for values past 32 bits; the
+    compact records (8-B ones per wave with tune mbox_rec8=1, the form of batches past
+    512 tiles), and 32-B long ones for values past 32 bits; the
     commutative stateful CounterAdd through the same kernel (hash routes: every
     actor's count exact); with small rings the tiles past a ring's room spill and
     run from the batch.  Every ring drained afterwards."""
     from ptype_amd.ops.records import METHOD_COUNTER_ADD
 
+    monkeypatch.setenv("PTYPE_TUNE", f"mbox_rec8={rec8}")
     n = 1 << 14
     t, _ = placed_table(n)
     mb = Mailboxes(DEV, shards=64, slots=slots)
@@ -803,6 +806,7 @@ def test_arrival_fused_enqueue_drain_exact(M, slots):
                           sharding="arrival")
         torch.cuda.synchronize()
         assert mb.last_sharding == "arrival" and mb.last_route == 3
+        assert mb.last_record_bytes == (8 if rec8 == "1" else 16)
         assert torch.equal(st, torch.where(known, STATUS_OK, STATUS_NO_ACTOR).to(torch.int32)), k
         assert torch.equal(val[known], (a0 * a1)[known]), k
     state = torch.zeros(n, dtype=torch.int64, device=DEV)
