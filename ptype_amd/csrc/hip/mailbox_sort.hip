@@ -189,9 +189,20 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       // of the wave does not fit)
       const bool allow8 = mv_.planar && (tn.mbox_rec8 == 1 || (tn.mbox_rec8 < 0 && tiles > 512));
       if (allow8) last_rec_bytes_ = 8;
-#define PT_AFUSED(MO, FX)                                                                                         \
-  hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX>), dim3(tile_grid), dim3(kST), 0, st, in, mv_, (int64_t*)a.state, \
-                     a.n_state, a.delay_ticks, ob, rv, sort_ticket_, allow8)
+      // batches of up to 512 4096-message tiles: 1024-message tiles (four times the blocks)
+      SortIn in1 = in;
+      const bool small_tiles = tiles <= 512;
+      if (small_tiles) in1.tiles = (uint32_t)((a.M + kST * 2 - 1) / (kST * 2));
+      const uint32_t grid1 = in1.tiles >= 8 ? (in1.tiles + 7) / 8 * 8 : in1.tiles;
+#define PT_AFUSED(MO, FX)                                                                                             \
+  do {                                                                                                                \
+    if (small_tiles)                                                                                                  \
+      hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX, 2>), dim3(grid1), dim3(kST), 0, st, in1, mv_,              \
+                         (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_ticket_, allow8);                  \
+    else                                                                                                              \
+      hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX>), dim3(grid1), dim3(kST), 0, st, in1, mv_, (int64_t*)a.state, \
+                         a.n_state, a.delay_ticks, ob, rv, sort_ticket_, allow8);                                     \
+  } while (0)
       if (fixed_mul) {
         if (rank_arr) PT_AFUSED(3, kCalculatorMultiply);
         else if (mode == 2) PT_AFUSED(2, kCalculatorMultiply);

@@ -997,13 +997,14 @@ __global__ __launch_bounds__(kST) void mbx_sortdrain_kernel(SortIn in, MboxView 
 // written by the enqueue); a tile whose run does not fit the ring's free room
 // spills whole -- the drain runs it straight from the batch, re-resolving each
 // message -- and tiles spill only as a suffix of a shard's sequence.
-__device__ __forceinline__ bool arrival_fits(const MboxView& mv, const SortIn& in, uint32_t t, uint64_t& pos0) {
+__device__ __forceinline__ bool arrival_fits(const MboxView& mv, const SortIn& in, uint32_t t, uint64_t& pos0,
+                                             uint32_t tile = kSTile) {
   const uint32_t s = t & ((1u << mv.log_s) - 1);
   const uint64_t Q = 1ull << mv.log_q;
   const uint64_t tl = *ctr_tail(mv, s), hd = *ctr_head(mv, s);
   const uint64_t room = hd + Q > tl ? hd + Q - tl : 0;
-  const uint64_t off = (uint64_t)(t >> mv.log_s) * kSTile;
-  const uint64_t n_t = min((uint64_t)kSTile, (uint64_t)in.M - (uint64_t)t * kSTile);
+  const uint64_t off = (uint64_t)(t >> mv.log_s) * tile;
+  const uint64_t n_t = min((uint64_t)tile, (uint64_t)in.M - (uint64_t)t * tile);
   pos0 = tl + off;
   return off + n_t <= room;
 }
@@ -1171,10 +1172,14 @@ __device__ __forceinline__ bool arr8_fits(uint32_t mb, int64_t x0, int64_t x1) {
   const uint64_t z0 = ((uint64_t)x0 << 1) ^ (uint64_t)(x0 >> 63), z1 = ((uint64_t)x1 << 1) ^ (uint64_t)(x1 >> 63);
   return mb < (1u << kArr8Mb) - 1u && (z0 >> kArr8Arg) == 0 && (z1 >> kArr8Arg) == 0;
 }
+template <int SK>
 __device__ __forceinline__ uint64_t arr8_cell(const MboxView& mv, uint32_t s, uint64_t pos0, uint32_t j) {
-  return 2 * slot_at(mv, s, pos0 + (j & ~(uint32_t)(kSWave - 1)) + ((j & (kSWave - 1)) >> 1)) + (j & 1);
+  constexpr uint32_t run = SK * kWave;  // a wave's run of the tile
+  return 2 * slot_at(mv, s, pos0 + (j & ~(run - 1)) + ((j & (run - 1)) >> 1)) + (j & 1);
 }
-template <int MODE, int FIXED>
+// SK messages per thread: kSK (4096-message tiles), or 2 (1024) for batches of up to 512
+// 4096-message tiles -- one 8-wave block per CU at 1 Mi messages hid too little latency
+template <int MODE, int FIXED, int SK = kSK>
 __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxView mv, int64_t* __restrict__ state,
                                                                 uint32_t n_state, uint64_t delay_ticks, OutboxView ob,
                                                                 ReplyView rv, unsigned* __restrict__ ticket,
@@ -1186,41 +1191,42 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
   const unsigned w = threadIdx.x / kWave;
   if (t < in.tiles) {
     uint64_t pos0 = 0;
-    const bool fits = arrival_fits(mv, in, t, pos0);
+    constexpr uint32_t kTile = kST * SK;
+    const bool fits = arrival_fits(mv, in, t, pos0, kTile);
     const uint32_t s = t & (S - 1);
-    uint32_t a[kSK], mb[kSK];
-    int64_t x0[kSK], x1[kSK];
-    int r[kSK];
+    uint32_t a[SK], mb[SK];
+    int64_t x0[SK], x1[SK];
+    int r[SK];
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      const int64_t i = tile_index(t, k);
+    for (int k = 0; k < SK; ++k) {
+      const int64_t i = tile_index<SK>(t, k);
       const bool ok = i < in.M;
       a[k] = ok ? __builtin_nontemporal_load(in.actor + i) : 0xffffffffu;
       x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
       x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
     }
-    resolve_k<MODE>(in, a, r, mb);
-    bool live[kSK];
+    resolve_k<MODE, SK>(in, a, r, mb);
+    bool live[SK];
     bool narrow = allow8 && mv.planar != 0;
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
-      live[k] = tile_index(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
+    for (int k = 0; k < SK; ++k) {
+      live[k] = tile_index<SK>(t, k) < in.M && r[k] == in.rank_self && mb[k] < kMaxMbox;
       if (live[k] && !arr8_fits(mb[k], x0[k], x1[k])) narrow = false;
     }
     const bool rec8 = __ballot(!narrow) == 0;  // (wave-uniform)
     if (lane_id() == 0) wave_rec8[w] = rec8;
     uint64_t* cells = reinterpret_cast<uint64_t*>(mv.rec);
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {  // enqueue: the tile's records at their fixed ring positions
-      const int64_t i = tile_index(t, k);
+    for (int k = 0; k < SK; ++k) {  // enqueue: the tile's records at their fixed ring positions
+      const int64_t i = tile_index<SK>(t, k);
       if (i >= in.M) continue;
       const uint32_t origin = in.origin_base + (uint32_t)i;
-      const uint32_t j = (uint32_t)(i - (int64_t)t * kSTile);
+      const uint32_t j = (uint32_t)(i - (int64_t)t * kTile);
       const uint64_t slot = slot_at(mv, s, pos0 + j);
       if (!live[k]) {
         ++n_miss;
         write_status(rv, origin, kStatusNoActor);
-        if (fits && rec8) cells[arr8_cell(mv, s, pos0, j)] = kArr8Null;
+        if (fits && rec8) cells[arr8_cell<SK>(mv, s, pos0, j)] = kArr8Null;
         else if (fits) *reinterpret_cast<u32x4*>(rec_a(mv, slot)) = u32x4{0u, 0u, 0u, 0u};
         continue;
       }
@@ -1232,7 +1238,7 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
       if (rec8) {
         const uint64_t z0 = ((uint64_t)x0[k] << 1) ^ (uint64_t)(x0[k] >> 63);
         const uint64_t z1 = ((uint64_t)x1[k] << 1) ^ (uint64_t)(x1[k] >> 63);
-        cells[arr8_cell(mv, s, pos0, j)] = (uint64_t)mb[k] | (z0 << kArr8Mb) | (z1 << (kArr8Mb + kArr8Arg));
+        cells[arr8_cell<SK>(mv, s, pos0, j)] = (uint64_t)mb[k] | (z0 << kArr8Mb) | (z1 << (kArr8Mb + kArr8Arg));
       } else if (mt < 128u && fits_i32(x0[k]) && fits_i32(x1[k])) {
         *reinterpret_cast<u32x4*>(rec_a(mv, slot)) =
             u32x4{origin | kCompactMark, mb[k] | (mt << 24), (uint32_t)x0[k], (uint32_t)x1[k]};
@@ -1248,15 +1254,15 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
     const uint32_t w2 = w ^ 4u;  // (the wave whose records this one consumes)
     const bool rec8_2 = wave_rec8[w2] != 0;
 #pragma unroll
-    for (int k = 0; k < kSK; ++k) {
+    for (int k = 0; k < SK; ++k) {
       SortRec x;
       int64_t i;
       if (fits) {  // wave w2's k-th record of this lane
-        const uint32_t j = w2 * (kSK * kWave) + (uint32_t)k * kWave + lane_id();
-        i = (int64_t)t * kSTile + j;
+        const uint32_t j = w2 * (SK * kWave) + (uint32_t)k * kWave + lane_id();
+        i = (int64_t)t * kTile + j;
         if (i >= in.M) continue;
         if (rec8_2) {
-          const uint64_t c = cells[arr8_cell(mv, s, pos0, j)];
+          const uint64_t c = cells[arr8_cell<SK>(mv, s, pos0, j)];
           if (c == kArr8Null) continue;  // no actor: answered by the enqueue
           x.valid = true, x.method = in.method_uniform, x.flags = 0, x.a2 = 0;
           x.mb = (uint32_t)(c & ((1u << kArr8Mb) - 1));
@@ -1272,7 +1278,7 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
         }
       } else {  // a spilled tile: this thread's own messages, from its registers
         if (!live[k]) continue;  // (no actor: answered above)
-        i = tile_index(t, k);
+        i = tile_index<SK>(t, k);
         x.valid = true, x.mb = mb[k], x.method = in.method_uniform, x.flags = 0;
         x.a0 = x0[k], x.a1 = x1[k], x.a2 = 0;
       }
@@ -1298,8 +1304,8 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
       uint64_t used = 0;
       for (uint32_t tt = sh; tt < in.tiles; tt += S) {
         uint64_t p0 = 0;
-        if (!arrival_fits(mv, in, tt, p0)) break;  // the spilled suffix
-        used += min((uint64_t)kSTile, (uint64_t)in.M - (uint64_t)tt * kSTile);
+        if (!arrival_fits(mv, in, tt, p0, kST * SK)) break;  // the spilled suffix
+        used += min((uint64_t)(kST * SK), (uint64_t)in.M - (uint64_t)tt * (kST * SK));
       }
       epoch_commit(mv, sh, (uint32_t)used);
     }
