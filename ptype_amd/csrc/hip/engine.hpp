@@ -72,6 +72,8 @@ void launch_dispatch_packed(uintptr_t recv, int R, int64_t C, const PackedLayout
                             uint32_t n_state, uint64_t delay_ticks, uintptr_t stats, int64_t expected_per_rank,
                             const std::vector<uintptr_t>& outbox, uint64_t outbox_cap,
                             const std::vector<uintptr_t>& direct, int self, uintptr_t stream);
+void launch_complete_sx(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
+                        uintptr_t out_st, uintptr_t stream, uintptr_t failed, uintptr_t zero, int64_t zero_words);
 void launch_complete_packed(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
                             uintptr_t out_st, uintptr_t checksum, bool direct, uintptr_t stream, uintptr_t failed = 0,
                             uintptr_t zero = 0, int64_t zero_words = 0);

@@ -1494,10 +1494,10 @@ void SortedExchange::send(const SxSend& a) {
       // the first completion also clears the agreement buffer of Send + 1 (that of
       // Send - 1, whose copy to the host precedes this Send's reply all-to-alls)
       const bool zero = !capturing && !meta_zeroed_[cur ^ 1];
-      launch_complete_packed((uintptr_t)bufs_[i].back, C, R_, L.vb, (uintptr_t)bufs_[i].perm, m,
-                             a.out_val + (uintptr_t)(lo * 8), a.out_st + (uintptr_t)(lo * 4), 0, false,
-                             (uintptr_t)cs, fake_ ? (uintptr_t)fake_->device_failed() : 0,
-                             zero ? (uintptr_t)(meta_dev_ + (cur ^ 1) * kSxMetaWords) : 0, zero ? kSxMetaWords : 0);
+      launch_complete_sx((uintptr_t)bufs_[i].back, C, R_, L.vb, (uintptr_t)bufs_[i].perm, m,
+                         a.out_val + (uintptr_t)(lo * 8), a.out_st + (uintptr_t)(lo * 4), (uintptr_t)cs,
+                         fake_ ? (uintptr_t)fake_->device_failed() : 0,
+                         zero ? (uintptr_t)(meta_dev_ + (cur ^ 1) * kSxMetaWords) : 0, zero ? kSxMetaWords : 0);
       if (zero) meta_zeroed_[cur ^ 1] = true;
     }
   }

@@ -5,6 +5,7 @@
 // Route passes 1 + 2 (route words, histograms, bases, slot headers) are the
 // v2 kernels (batch.hip: route_prep_scan) run with v3 region sizes; only the
 // record writer of the scatter differs (PackedEmit).
+#include <type_traits>
 #include <vector>
 
 #include "common.hpp"
@@ -362,6 +363,94 @@ __global__ __launch_bounds__(256) void complete_packed_kernel(const uint32_t* __
     __syncthreads();
     if (threadIdx.x == 0) atomicAdd(checksum, part[0] + part[1] + part[2] + part[3]);
   }
+}
+
+// The sorted exchange's completion (no checksum, no direct slots): the same gather as
+// complete_packed_kernel with the value width a template parameter -- a third fewer
+// VGPRs, so more waves hide the perm -> reply-gather chain (the kernel waits on memory
+// 77 % of its wave cycles, profiles/r6_pmc_l8.txt).
+template <int VB, int U>
+__global__ __launch_bounds__(256) void complete_sx_kernel(const uint32_t* __restrict__ rep, int64_t rep_words,
+                                                          uint32_t C, int R, const int32_t* __restrict__ perm,
+                                                          int64_t M, int64_t* __restrict__ out_val,
+                                                          int32_t* __restrict__ out_st,
+                                                          const uint64_t* __restrict__ failed,
+                                                          uint64_t* __restrict__ zero, int64_t zero_words) {
+  if (zero)
+    for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < zero_words; w += (int64_t)gridDim.x * blockDim.x)
+      zero[w] = 0;
+  __shared__ uint32_t voff[kMaxRanks];
+  const bool lost = failed && __hip_atomic_load(failed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  for (int d = threadIdx.x; d < R; d += blockDim.x)
+    voff[d] = 4 + (uint32_t)packed_ok_words(std::min<int64_t>(rep[(int64_t)d * rep_words], (int64_t)C));
+  __syncthreads();
+  using VT = typename std::conditional<VB == 1, uint8_t,
+             typename std::conditional<VB == 2, uint16_t,
+             typename std::conditional<VB == 4, uint32_t, uint64_t>::type>::type>::type;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < M; i0 += stride * U) {
+    int32_t p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      p[u] = i < M ? perm[i] : kPastBatch;
+    }
+    uint64_t code[U];
+    uint32_t ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      code[u] = 0;
+      ok[u] = 0;
+      if (p[u] >= 0) {
+        const uint32_t d = (uint32_t)p[u] / C, pos = (uint32_t)p[u] - d * C;
+        const uint32_t* rb = rep + (int64_t)d * rep_words;
+        ok[u] = (uint32_t)(reinterpret_cast<const unsigned long long*>(rb + 4)[pos / kWave] >> (pos % kWave)) & 1u;
+        code[u] = reinterpret_cast<const VT*>(rb + voff[d])[pos];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (p[u] == kPastBatch) continue;
+      int64_t v = 0;
+      int32_t st;
+      if (lost && p[u] >= 0) {
+        st = kStatusNotDelivered;
+      } else if (p[u] >= 0) {
+        if (ok[u]) {
+          v = VB == 8 ? (int64_t)code[u] : zz_dec(code[u]);
+          st = kStatusOk;
+        } else {
+          st = (int32_t)code[u];
+        }
+      } else {
+        st = p[u] == -1 ? kStatusOverflow : kStatusNoActor;
+      }
+      out_val[i] = v;
+      out_st[i] = st;
+    }
+  }
+}
+
+void launch_complete_sx(uintptr_t rep, int64_t C, int R, int vb, uintptr_t perm, int64_t M, uintptr_t out_val,
+                        uintptr_t out_st, uintptr_t stream, uintptr_t failed, uintptr_t zero, int64_t zero_words) {
+  if (M <= 0) return;
+  if (C < 1 || C > 0x7fffffff) throw std::invalid_argument("complete: bad capacity");
+  if (R < 1 || R > kMaxRanks) throw std::invalid_argument("complete: 1 <= R <= 64");
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((M + 256 * 4 - 1) / (256 * 4), 8192));
+#define PT_CSX(VBV)                                                                                                  \
+  hipLaunchKernelGGL((complete_sx_kernel<VBV, 4>), dim3(g), dim3(256), 0, as_stream(stream), (const uint32_t*)rep,   \
+                     packed_rep_words(C, VBV), (uint32_t)C, R, (const int32_t*)perm, M, (int64_t*)out_val,          \
+                     (int32_t*)out_st, (const uint64_t*)failed, (uint64_t*)zero, zero_words)
+  switch (vb) {
+    case 1: PT_CSX(1); break;
+    case 2: PT_CSX(2); break;
+    case 4: PT_CSX(4); break;
+    case 8: PT_CSX(8); break;
+    default: throw std::invalid_argument("complete: vb in {1,2,4,8}");
+  }
+#undef PT_CSX
+  PT_HIP_CHECK(hipGetLastError());
 }
 
 // ---------------------------------------------------------------- launchers
