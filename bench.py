@@ -454,6 +454,9 @@ def main():
     head_mailbox = mailbox_info(ex)
     if head_mailbox.get("mailbox_route") == 3:  # the stateless mailbox Send resolved ranks only
         route_mode = "rank byte gather (1 B per id, from the route directory; stateless records carry the actor id)"
+    elif head_mailbox.get("mailbox_route") == 4:
+        route_mode = ("presence map in LDS (2 bits per id, folded from the route directory's rank bytes each Send; "
+                      "stateless records carry the actor id)")
     secondaries = {}
     if args.placement != "affine" and not args.no_secondary and args.steps:
         # the same step with the strided placement, whose routes need no registry reads

@@ -801,7 +801,7 @@ Mailboxes::~Mailboxes() {
   (void)hipFree(mv_.stats);
   for (void* p : {(void*)sort_hist_, (void*)sort_gsum_, (void*)sort_ticket_, (void*)sort_rw_, (void*)sort_sidx_,
                   (void*)sort_tinfo_, (void*)sort_desc_, (void*)sort_tctr_, stage_rep_,
-                  (void*)r8w_, (void*)r8max_, (void*)r8esc_, (void*)sort_resv_})
+                  (void*)r8w_, (void*)r8max_, (void*)r8esc_, (void*)sort_resv_, (void*)pres_})
     if (p) (void)hipFree(p);
   if (ctrl_) (void)hipHostFree(ctrl_);
   if (r8host_) (void)hipHostFree(r8host_);

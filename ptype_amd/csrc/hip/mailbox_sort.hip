@@ -360,9 +360,38 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     mbx_launch_fused(f);
     return;
   } else {
+    // route mode 4: a rank-routed Send on a directory whose presence map fits LDS
+    const bool pres_route = rank_route && a.n_dir <= kPresMax;
+    if (pres_route) {
+      const uint32_t nw = pres_words(a.n_dir);
+      if (nw > pres_words_) {
+        if (capturing()) throw std::runtime_error("mailbox send: first presence-map Send inside a graph capture (warm up first)");
+        PT_HIP_CHECK(hipStreamSynchronize(st));
+        if (pres_) PT_HIP_CHECK(hipFree(pres_));
+        PT_HIP_CHECK(hipMalloc((void**)&pres_, (size_t)nw * 4));
+        pres_words_ = nw;
+      }
+      hipLaunchKernelGGL(mbx_presence_kernel<>, dim3((nw + 255) / 256), dim3(256), 0, st, (const uint8_t*)a.dir_rank,
+                         a.n_dir, a.rank_self, pres_);
+      PT_HIP_CHECK(hipGetLastError());
+      in.pres = pres_;
+      last_route_ = 4;
+    }
+    const size_t os_lds = pres_route ? ((onesweep_lds_bytes(Sv) + 15) & ~(size_t)15) + (size_t)pres_words(a.n_dir) * 4
+                                     : onesweep_lds_bytes(Sv);
+    if (pres_route) {
+      static bool attr = false;
+      if (!attr) {  // (past the 64 KB default for the largest maps)
+        PT_HIP_CHECK(hipFuncSetAttribute((const void*)mbx_onesweep_kernel<4, false, false>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(((onesweep_lds_bytes(kMboxSortMaxShards) + 15) & ~(size_t)15) +
+                                               (size_t)pres_words(kPresMax) * 4)));
+        attr = true;
+      }
+    }
     // one block per tile, claimed in launch order (the grid is exactly the tile count)
 #define PT_OS1(MO, A2, MC)                                                                                        \
-  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC>), dim3(in.tiles), dim3(kST), onesweep_lds_bytes(Sv), st, in, \
+  hipLaunchKernelGGL((mbx_onesweep_kernel<MO, A2, MC>), dim3(in.tiles), dim3(kST), os_lds, st, in,                 \
                      mv, sort_desc_, sort_tctr_, sort_gsum_, sort_sidx_, tinfo, sort_rw_, rv, !a.ordered, all_sidx,  \
                      reserve)
 #define PT_OS(MO)                                   \
@@ -372,7 +401,8 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     else if (a.method_col) PT_OS1(MO, false, true); \
     else PT_OS1(MO, false, false);                  \
   } while (0)
-    if (rank_route) PT_OS1(3, false, false);
+    if (pres_route) PT_OS1(4, false, false);
+    else if (rank_route) PT_OS1(3, false, false);
     else if (mode == 2) PT_OS(2); else if (mode == 1) PT_OS(1); else PT_OS(0);
 #undef PT_OS
 #undef PT_OS1

@@ -314,6 +314,53 @@ __device__ __forceinline__ void rec8_next_from(const uint32_t* r8max, uint32_t* 
   }
 }
 
+// Route mode 4 (world-1 stateless Sends on a directory of up to kPresMax ids): the
+// directory's rank bytes folded into 2 bits per id for this rank -- 1 here, 2 probe the
+// hash table (a rank past 253), 0 anything else -- so a sort block stages the whole map
+// in LDS (32 KB for 131072 ids) and resolves each message with an LDS read instead of a
+// scattered global gather: 64 lanes gathering from 64 lines kept the sort's address unit
+// stalled by the texture cache half its busy time (profiles/r6_pmc_head.txt).
+constexpr uint32_t kPresMax = 1u << 18;  // ids (64 KB of map)
+__host__ __device__ constexpr uint32_t pres_words(uint32_t n_dir) { return ((n_dir + 15) / 16 + 3) & ~3u; }
+template <int = 0>
+__global__ __launch_bounds__(256) void mbx_presence_kernel(const uint8_t* __restrict__ dirr, uint32_t n_dir,
+                                                           int rank_self, uint32_t* __restrict__ pres) {
+  const uint32_t wi = blockIdx.x * 256u + threadIdx.x;
+  if (wi >= pres_words(n_dir)) return;
+  uint32_t w = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint32_t a = wi * 16 + j;
+    if (a >= n_dir) break;
+    const uint8_t r = dirr[a];
+    const uint32_t st = r == (uint8_t)rank_self ? 1u : r == kRankFallback ? 2u : 0u;
+    w |= st << (2 * j);
+  }
+  pres[wi] = w;
+}
+__device__ __forceinline__ void stage_pres(const SortIn& in, uint32_t* lpres) {
+  const uint32_t nw = pres_words(in.n_dir);
+  for (uint32_t w = threadIdx.x * 4; w < nw; w += blockDim.x * 4)
+    *reinterpret_cast<uint4*>(lpres + w) = *reinterpret_cast<const uint4*>(in.pres + w);
+}
+template <int SK>
+__device__ __forceinline__ void resolve_pres(const SortIn& in, const uint32_t* lpres, const uint32_t (&a)[SK],
+                                             int (&r)[SK], uint32_t (&mb)[SK]) {
+#pragma unroll
+  for (int k = 0; k < SK; ++k) {
+    mb[k] = a[k];
+    if (a[k] < in.n_dir) {
+      const uint32_t st = (lpres[a[k] >> 4] >> ((a[k] & 15) * 2)) & 3u;
+      r[k] = st == 1 ? in.rank_self : -1;
+      if (st == 2) lookup_entry(in.table, in.mask, actor_key(a[k]), r[k], mb[k]);
+    } else if (a[k] != 0xffffffffu) {
+      lookup_entry(in.table, in.mask, actor_key(a[k]), r[k], mb[k]);
+    } else {
+      r[k] = -1;
+    }
+  }
+}
+
 // One tile of the one-pass sort (the block claims it); returns its index.
 //
 // reserve (stateless batches): no look-back.  A stateless record runs on its
@@ -349,6 +396,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
     tile_s = t;
   }
   for (uint32_t s = lane; s < S; s += kWave) wcnt(w, s) = 0;
+  uint32_t* lpres = reinterpret_cast<uint32_t*>(smem_os + ((onesweep_lds_bytes(S) + 15) & ~(size_t)15));
+  if constexpr (MODE == 4) stage_pres(in, lpres);  // (the map, behind the barrier below)
   __syncthreads();
   // (reserve: tiles dealt XCD by XCD, as the ring drain deals them -- its reads of a tile's runs then
   // meet the lines in the L2 that took the sort's stores)
@@ -359,7 +408,8 @@ __device__ __forceinline__ uint32_t onesweep_tile(const SortIn& in, const MboxVi
   int r[SK];
   load_actors<SK>(in, t, a);
   load_cols<A2, MC, SK>(in, t, v0, v1, v2, meth);
-  resolve_k<MODE, SK>(in, a, r, mb);
+  if constexpr (MODE == 4) resolve_pres<SK>(in, lpres, a, r, mb);
+  else resolve_k<MODE, SK>(in, a, r, mb);
   uint32_t wr[SK];
   // (an ordered batch in 8-B records, !spill: a message whose fields do not fit takes its
   // ring position like any other and is written as an escape record below -- FIFO kept)

@@ -34,6 +34,7 @@ struct SortIn {  // by value
   uint64_t mask;
   const uint32_t* dir;
   const uint8_t* dirr;  // MODE 3: the directory's rank byte table (one byte per id: 4x fewer lines than dir)
+  const uint32_t* pres;  // MODE 4: the directory's 2-bit presence map for rank_self (staged in LDS per block)
   uint32_t n_dir;
   uint32_t aw;
   int aw_shift;
