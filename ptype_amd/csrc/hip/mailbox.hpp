@@ -234,6 +234,7 @@ class Mailboxes {
   int last_route_ = -1;
   uint32_t* sort_resv_ = nullptr;   // [S][kResvStride] one-pass run reservations (zero between Sends)
   uint32_t* pres_ = nullptr;        // route mode 4: 2-bit presence map of the route directory (per Send)
+  void build_presence(const MboxSend& a, hipStream_t st);
   uint64_t pres_words_ = 0;
   // 8-B ring records: [0] the field widths in force (device; updated by each Send's
   // last block), per-tile field bit lengths, and a pinned mirror of [0] (bit 31: the

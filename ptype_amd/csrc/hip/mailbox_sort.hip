@@ -76,6 +76,24 @@ static bool fused_ok(int64_t tiles) {
 // drain (233 vs 175 us), 2048-record ordered windows, the ordered drain without the
 // register fold or the prefetched window, 16-B ordered records at 8 Mi, the wide ring
 // drain and the 8 / 16 / 32-shard stateless views other than 8.
+// Route mode 4's presence map of this Send's directory (folded every Send: the
+// directory may have changed since the last one; 128 KB read for 131072 ids).
+void Mailboxes::build_presence(const MboxSend& a, hipStream_t st) {
+  const uint32_t nw = pres_words(a.n_dir);
+  if (nw > pres_words_) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      throw std::runtime_error("mailbox send: first presence-map Send inside a graph capture (warm up first)");
+    PT_HIP_CHECK(hipStreamSynchronize(st));
+    if (pres_) PT_HIP_CHECK(hipFree(pres_));
+    PT_HIP_CHECK(hipMalloc((void**)&pres_, (size_t)nw * 4));
+    pres_words_ = nw;
+  }
+  hipLaunchKernelGGL(mbx_presence_kernel<>, dim3((nw + 255) / 256), dim3(256), 0, st, (const uint8_t*)a.dir_rank,
+                     a.n_dir, a.rank_self, pres_);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
 void Mailboxes::send_sorted(const MboxSend& a) {
   const uint32_t S = shards();
   if (S > (uint32_t)kMboxSortMaxShards) throw std::invalid_argument("sorted mailboxes: at most 1024 shards");
@@ -185,6 +203,26 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       // rank byte routes for a stateless method on the directory: the records carry actor ids
       const bool rank_arr = mode == 1 && a.dir_rank && a.n_dir <= kMaxMbox && method_stateless((uint32_t)a.method_uniform);
       if (rank_arr) last_route_ = 3;
+      // route mode 4 (the directory's presence map in LDS) when it fits -- for batches past 512
+      // tiles: below, the map's staging per block (1024 blocks x 32 KB at 1 Mi) outweighs the
+      // gathers it replaces (config 2: 31.2 vs 29.5 G msg/s)
+      const bool pres_arr = rank_arr && a.n_dir <= kPresMax && tiles > 512;
+      size_t af_lds = 0;
+      if (pres_arr) {
+        build_presence(a, st);
+        in.pres = pres_;
+        last_route_ = 4;
+        af_lds = (size_t)pres_words(a.n_dir) * 4;
+        static bool attr = false;
+        if (!attr) {  // (past the 64 KB default for the largest maps)
+          for (const void* k : {(const void*)mbx_arrival_fused_kernel<4, kCalculatorMultiply, 2>,
+                                (const void*)mbx_arrival_fused_kernel<4, kCalculatorMultiply>,
+                                (const void*)mbx_arrival_fused_kernel<4, 0, 2>, (const void*)mbx_arrival_fused_kernel<4, 0>})
+            PT_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)((size_t)pres_words(kPresMax) * 4)));
+          attr = true;
+        }
+      }
       // 8-B records past 512 tiles (tune mbox_rec8: the sort's rule; per wave, 16 B when a value
       // of the wave does not fit)
       const bool allow8 = mv_.planar && (tn.mbox_rec8 == 1 || (tn.mbox_rec8 < 0 && tiles > 512));
@@ -197,19 +235,21 @@ void Mailboxes::send_sorted(const MboxSend& a) {
 #define PT_AFUSED(MO, FX)                                                                                             \
   do {                                                                                                                \
     if (small_tiles)                                                                                                  \
-      hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX, 2>), dim3(grid1), dim3(kST), 0, st, in1, mv_,              \
+      hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX, 2>), dim3(grid1), dim3(kST), af_lds, st, in1, mv_,         \
                          (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_ticket_, allow8);                  \
     else                                                                                                              \
-      hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX>), dim3(grid1), dim3(kST), 0, st, in1, mv_, (int64_t*)a.state, \
-                         a.n_state, a.delay_ticks, ob, rv, sort_ticket_, allow8);                                     \
+      hipLaunchKernelGGL((mbx_arrival_fused_kernel<MO, FX>), dim3(grid1), dim3(kST), af_lds, st, in1, mv_,            \
+                         (int64_t*)a.state, a.n_state, a.delay_ticks, ob, rv, sort_ticket_, allow8);                  \
   } while (0)
       if (fixed_mul) {
-        if (rank_arr) PT_AFUSED(3, kCalculatorMultiply);
+        if (pres_arr) PT_AFUSED(4, kCalculatorMultiply);
+        else if (rank_arr) PT_AFUSED(3, kCalculatorMultiply);
         else if (mode == 2) PT_AFUSED(2, kCalculatorMultiply);
         else if (mode == 1) PT_AFUSED(1, kCalculatorMultiply);
         else PT_AFUSED(0, kCalculatorMultiply);
       } else {
-        if (rank_arr) PT_AFUSED(3, 0);
+        if (pres_arr) PT_AFUSED(4, 0);
+        else if (rank_arr) PT_AFUSED(3, 0);
         else if (mode == 2) PT_AFUSED(2, 0);
         else if (mode == 1) PT_AFUSED(1, 0);
         else PT_AFUSED(0, 0);
@@ -363,17 +403,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     // route mode 4: a rank-routed Send on a directory whose presence map fits LDS
     const bool pres_route = rank_route && a.n_dir <= kPresMax;
     if (pres_route) {
-      const uint32_t nw = pres_words(a.n_dir);
-      if (nw > pres_words_) {
-        if (capturing()) throw std::runtime_error("mailbox send: first presence-map Send inside a graph capture (warm up first)");
-        PT_HIP_CHECK(hipStreamSynchronize(st));
-        if (pres_) PT_HIP_CHECK(hipFree(pres_));
-        PT_HIP_CHECK(hipMalloc((void**)&pres_, (size_t)nw * 4));
-        pres_words_ = nw;
-      }
-      hipLaunchKernelGGL(mbx_presence_kernel<>, dim3((nw + 255) / 256), dim3(256), 0, st, (const uint8_t*)a.dir_rank,
-                         a.n_dir, a.rank_self, pres_);
-      PT_HIP_CHECK(hipGetLastError());
+      build_presence(a, st);
       in.pres = pres_;
       last_route_ = 4;
     }

@@ -327,13 +327,17 @@ __global__ __launch_bounds__(256) void mbx_presence_kernel(const uint8_t* __rest
                                                            int rank_self, uint32_t* __restrict__ pres) {
   const uint32_t wi = blockIdx.x * 256u + threadIdx.x;
   if (wi >= pres_words(n_dir)) return;
+  alignas(16) uint8_t b[16];
+  if (wi * 16 + 16 <= n_dir) {  // (the table is a whole allocation: 16-B aligned)
+    *reinterpret_cast<uint4*>(b) = *reinterpret_cast<const uint4*>(dirr + (size_t)wi * 16);
+  } else {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) b[j] = wi * 16 + j < n_dir ? dirr[wi * 16 + j] : kRankMissing;
+  }
   uint32_t w = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
-    const uint32_t a = wi * 16 + j;
-    if (a >= n_dir) break;
-    const uint8_t r = dirr[a];
-    const uint32_t st = r == (uint8_t)rank_self ? 1u : r == kRankFallback ? 2u : 0u;
+    const uint32_t st = b[j] == (uint8_t)rank_self ? 1u : b[j] == kRankFallback ? 2u : 0u;
     w |= st << (2 * j);
   }
   pres[wi] = w;
@@ -1235,6 +1239,12 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
                                                                 ReplyView rv, unsigned* __restrict__ ticket,
                                                                 bool allow8) {
   __shared__ uint32_t wave_rec8[kST / kWave];
+  extern __shared__ __align__(16) unsigned char smem_af[];  // MODE 4: the presence map
+  uint32_t* lpres = reinterpret_cast<uint32_t*>(smem_af);
+  if constexpr (MODE == 4) {
+    stage_pres(in, lpres);
+    __syncthreads();
+  }
   unsigned long long n_enq = 0, n_miss = 0, n_spill = 0, done = 0, failed = 0;
   const uint32_t S = 1u << mv.log_s;
   const uint32_t t = virt_block(blockIdx.x, gridDim.x);
@@ -1255,7 +1265,8 @@ __global__ __launch_bounds__(kST) void mbx_arrival_fused_kernel(SortIn in, MboxV
       x0[k] = ok ? __builtin_nontemporal_load(in.a0 + i) : 0;
       x1[k] = ok && in.a1 ? __builtin_nontemporal_load(in.a1 + i) : 0;
     }
-    resolve_k<MODE, SK>(in, a, r, mb);
+    if constexpr (MODE == 4) resolve_pres<SK>(in, lpres, a, r, mb);
+    else resolve_k<MODE, SK>(in, a, r, mb);
     bool live[SK];
     bool narrow = allow8 && mv.planar != 0;
 #pragma unroll

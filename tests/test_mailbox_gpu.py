@@ -782,7 +782,9 @@ def test_mailbox_seqfold_in_8b_records_exactly_once_fifo():
 def test_arrival_fused_enqueue_drain_exact(M, slots, rec8, monkeypatch):
     """Arrival rings in one launch (mbx_arrival_fused_kernel: each block writes its
     tile's records into its ring run, then drains that run): stateless Multiply on
-    rank byte routes (records carry actor ids) with unknown actors, exact -- in 16-B
+    rank byte routes (records carry actor ids; the presence map of route mode 4 is
+    for batches past 512 tiles, test_arrival_fused_big_batch_presence_map) with
+    unknown actors, exact -- in 16-B
     compact records (8-B ones per wave with tune mbox_rec8=1, the form of batches past
     512 tiles), and 32-B long ones for values past 32 bits; the
     commutative stateful CounterAdd through the same kernel (hash routes: every
@@ -808,7 +810,7 @@ def test_arrival_fused_enqueue_drain_exact(M, slots, rec8, monkeypatch):
         val, st = mb.send(B.MsgBatch(actor, a0, a1, None, METHOD_CALC_MULTIPLY), t, None, ordered=False,
                           sharding="arrival")
         torch.cuda.synchronize()
-        assert mb.last_sharding == "arrival" and mb.last_route == 3
+        assert mb.last_sharding == "arrival" and mb.last_route == 3  # (rank bytes: up to 512 tiles)
         assert mb.last_record_bytes == (8 if rec8 == "1" else 16)
         assert torch.equal(st, torch.where(known, STATUS_OK, STATUS_NO_ACTOR).to(torch.int32)), k
         assert torch.equal(val[known], (a0 * a1)[known]), k
@@ -851,3 +853,30 @@ def test_exchange_takes_arrival_rings_for_small_stateless_sends():
     torch.cuda.synchronize()
     assert ex.mailboxes.last_sharding == "actor"
     assert bool((st == STATUS_OK).all())
+
+
+def test_arrival_fused_big_batch_presence_map():
+    """A stateless batch past 512 tiles through the fused arrival Send: the
+    directory's 2-bit presence map staged in LDS (route mode 4), 8-B records per
+    wave; unknown ids (unregistered, past the directory) answered, replies exact."""
+    n, M = 1 << 15, 5 << 20
+    t = RegistryTable(4 * n, device=DEV)
+    ids = torch.cat([torch.arange(n), torch.arange(n + 100, n + 1100)])
+    perm = torch.randperm(ids.numel(), generator=torch.Generator().manual_seed(31))
+    t.upsert(actor_keys(ids), torch.zeros(ids.numel(), dtype=torch.int32), perm.to(torch.int32))
+    t.enable_directory(n + 50)  # ids n..n+49: in the directory, unregistered; n+100..: hash probes
+    g = torch.Generator().manual_seed(32)
+    actor = torch.randint(0, n + 3000, (M,), generator=g, dtype=torch.int32).to(DEV)
+    a0 = torch.randint(-(1 << 15), 1 << 15, (M,), generator=g, dtype=torch.int64).to(DEV)
+    a1 = torch.randint(-(1 << 15), 1 << 15, (M,), generator=g, dtype=torch.int64).to(DEV)
+    mb = Mailboxes(DEV, shards=256, slots=1 << 16)
+    known = (actor < n) | ((actor >= n + 100) & (actor < n + 1100))
+    for _ in range(2):
+        val, st = mb.send(B.MsgBatch(actor, a0, a1, None, METHOD_CALC_MULTIPLY), t, None, ordered=False,
+                          sharding="arrival")
+        torch.cuda.synchronize()
+        assert mb.last_route == 4 and mb.last_record_bytes == 8
+        assert torch.equal(st, torch.where(known, STATUS_OK, STATUS_NO_ACTOR).to(torch.int32))
+        assert torch.equal(val[known], (a0 * a1)[known])
+    ctr = mb.shard_counters()
+    assert (ctr[:, 0] == ctr[:, 2]).all()
