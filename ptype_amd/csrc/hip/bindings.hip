@@ -293,6 +293,10 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("recv"), py::arg("R"), py::arg("C"), py::arg("layout"), py::arg("reply"), py::arg("state"),
       py::arg("n_state"), py::arg("delay_ticks"), py::arg("stats"), py::arg("expected_per_rank"), py::arg("outbox"),
       py::arg("outbox_cap"), py::arg("direct"), py::arg("self"), py::arg("stream"));
+  m.def("presence_words", &presence_words, py::arg("n_dir"),
+        "int32 words of route mode 4's presence map for a directory of n_dir ids (0: too large for LDS)");
+  m.def("presence_build", &launch_presence, py::arg("dir_rank"), py::arg("n_dir"), py::arg("rank"), py::arg("out"),
+        py::arg("stream"), "route mode 4's presence map (2 bits per id: here / probe the table / not here) for rank");
   m.def("complete_packed", &launch_complete_packed, py::arg("rep"), py::arg("C"), py::arg("R"), py::arg("vb"), py::arg("perm"),
         py::arg("M"), py::arg("out_val"), py::arg("out_status"), py::arg("checksum"), py::arg("direct"),
         py::arg("stream"), py::arg("failed") = 0, py::arg("zero") = 0, py::arg("zero_words") = 0);
@@ -495,7 +499,7 @@ PYBIND11_MODULE(_hip, m) {
              uint32_t affine_w, int rank_self, uint32_t origin_base, uintptr_t out_val, uintptr_t out_st,
              uint64_t out_n, uintptr_t state, uint32_t n_state, uint64_t delay_ticks,
              const std::vector<uintptr_t>& outbox, uint64_t outbox_cap, bool arrival, bool ordered,
-             int fixed_method, uintptr_t stream, int sort_mode, uintptr_t dir_rank) {
+             int fixed_method, uintptr_t stream, int sort_mode, uintptr_t dir_rank, uintptr_t pres, int pres_rank) {
             MboxSend a;
             a.actor = actor, a.a0 = a0, a.a1 = a1, a.a2 = a2, a.method_col = method_col;
             a.method_uniform = method_uniform, a.M = M, a.table = table, a.cap = cap, a.dir = dir;
@@ -503,7 +507,7 @@ PYBIND11_MODULE(_hip, m) {
             a.out_val = out_val, a.out_st = out_st, a.out_n = out_n, a.state = state, a.n_state = n_state;
             a.delay_ticks = delay_ticks, a.outbox = outbox, a.outbox_cap = outbox_cap, a.arrival = arrival;
             a.ordered = ordered, a.fixed_method = fixed_method, a.stream = stream, a.sort_mode = sort_mode;
-            a.dir_rank = dir_rank;
+            a.dir_rank = dir_rank, a.pres = pres, a.pres_rank = pres_rank;
             mb.send_sorted(a);
           },
           "epoch Send through the sorted mailboxes: stable counting-sort enqueue + ordered / parallel drain",
@@ -512,7 +516,7 @@ PYBIND11_MODULE(_hip, m) {
           py::arg("affine_w"), py::arg("rank_self"), py::arg("origin_base"), py::arg("out_val"), py::arg("out_st"),
           py::arg("out_n"), py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"), py::arg("outbox"),
           py::arg("outbox_cap"), py::arg("arrival"), py::arg("ordered"), py::arg("fixed_method"), py::arg("stream"),
-          py::arg("sort_mode") = 0, py::arg("dir_rank") = 0)
+          py::arg("sort_mode") = 0, py::arg("dir_rank") = 0, py::arg("pres") = 0, py::arg("pres_rank") = -1)
       .def("start", &Mailboxes::start, py::arg("state"), py::arg("n_state"), py::arg("delay_ticks"),
            py::arg("out_val"), py::arg("out_st"), py::arg("out_n"), py::arg("blocks") = 16, py::arg("idle_ms") = 0.0,
            py::arg("max_s") = 60.0)

@@ -159,7 +159,16 @@ struct MboxSend {
   // resolves only its rank (1 MB at 1 M ids, L2-resident, against the 4 MB
   // directory) and its records carry the actor id, which no stateless handler reads
   uintptr_t dir_rank = 0;
+  // route mode 4's presence map of the directory, kept by the registry mirror for
+  // rank pres_rank (rebuilt with the directory; RegistryTable.presence): used when it is
+  // this Send's rank, else the Send folds its own from dir_rank
+  uintptr_t pres = 0;
+  int pres_rank = -1;
 };
+
+// Route mode 4's presence map: 2 bits per directory id for rank `rank` (mailbox_sort.hip)
+uint32_t presence_words(uint32_t n_dir);
+void launch_presence(uintptr_t dir_rank, uint32_t n_dir, int rank, uintptr_t out, uintptr_t stream);
 
 class Mailboxes {
  public:
@@ -234,6 +243,7 @@ class Mailboxes {
   int last_route_ = -1;
   uint32_t* sort_resv_ = nullptr;   // [S][kResvStride] one-pass run reservations (zero between Sends)
   uint32_t* pres_ = nullptr;        // route mode 4: 2-bit presence map of the route directory (per Send)
+  const uint32_t* pres_view_ = nullptr;  // the map this Send reads (pres_, or the registry mirror's)
   void build_presence(const MboxSend& a, hipStream_t st);
   uint64_t pres_words_ = 0;
   // 8-B ring records: [0] the field widths in force (device; updated by each Send's

@@ -76,9 +76,23 @@ static bool fused_ok(int64_t tiles) {
 // drain (233 vs 175 us), 2048-record ordered windows, the ordered drain without the
 // register fold or the prefetched window, 16-B ordered records at 8 Mi, the wide ring
 // drain and the 8 / 16 / 32-shard stateless views other than 8.
-// Route mode 4's presence map of this Send's directory (folded every Send: the
-// directory may have changed since the last one; 128 KB read for 131072 ids).
+uint32_t presence_words(uint32_t n_dir) { return n_dir <= kPresMax ? pres_words(n_dir) : 0u; }
+void launch_presence(uintptr_t dir_rank, uint32_t n_dir, int rank, uintptr_t out, uintptr_t stream) {
+  if (n_dir == 0 || n_dir > kPresMax || !dir_rank || !out) throw std::invalid_argument("presence: 1 <= n_dir <= 2^18");
+  const uint32_t nw = pres_words(n_dir);
+  hipLaunchKernelGGL(mbx_presence_kernel<>, dim3((nw + 255) / 256), dim3(256), 0, as_stream(stream),
+                     (const uint8_t*)dir_rank, n_dir, rank, (uint32_t*)out);
+  PT_HIP_CHECK(hipGetLastError());
+}
+
+// Route mode 4's presence map of this Send's directory: the registry mirror's (rebuilt
+// with the directory) when it is kept for this Send's rank, else folded here, every Send
+// (the directory may have changed since the last one; 128 KB read for 131072 ids).
 void Mailboxes::build_presence(const MboxSend& a, hipStream_t st) {
+  if (a.pres && a.pres_rank == a.rank_self) {
+    pres_view_ = (const uint32_t*)a.pres;
+    return;
+  }
   const uint32_t nw = pres_words(a.n_dir);
   if (nw > pres_words_) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -89,6 +103,7 @@ void Mailboxes::build_presence(const MboxSend& a, hipStream_t st) {
     PT_HIP_CHECK(hipMalloc((void**)&pres_, (size_t)nw * 4));
     pres_words_ = nw;
   }
+  pres_view_ = pres_;
   hipLaunchKernelGGL(mbx_presence_kernel<>, dim3((nw + 255) / 256), dim3(256), 0, st, (const uint8_t*)a.dir_rank,
                      a.n_dir, a.rank_self, pres_);
   PT_HIP_CHECK(hipGetLastError());
@@ -210,7 +225,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
       size_t af_lds = 0;
       if (pres_arr) {
         build_presence(a, st);
-        in.pres = pres_;
+        in.pres = pres_view_;
         last_route_ = 4;
         af_lds = (size_t)pres_words(a.n_dir) * 4;
         static bool attr = false;
@@ -404,7 +419,7 @@ void Mailboxes::send_sorted(const MboxSend& a) {
     const bool pres_route = rank_route && a.n_dir <= kPresMax;
     if (pres_route) {
       build_presence(a, st);
-      in.pres = pres_;
+      in.pres = pres_view_;
       last_route_ = 4;
     }
     const size_t os_lds = pres_route ? ((onesweep_lds_bytes(Sv) + 15) & ~(size_t)15) + (size_t)pres_words(a.n_dir) * 4

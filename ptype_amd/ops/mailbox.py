@@ -160,7 +160,9 @@ class Mailboxes:
                             affine, int(rank_self), 0, _ptr(out_val), _ptr(out_status), out_val.numel(), _ptr(state),
                             0 if state is None else state.numel(), int(delay_us) * 100, ob, ob_cap, arrival, ordered,
                             fixed, self._stream(), SORT_MODES[sort_mode],
-                            _ptr(table.dir_rank) if d is not None else 0)
+                            _ptr(table.dir_rank) if d is not None else 0,
+                            _ptr(table.presence) if d is not None and table.presence is not None else 0,
+                            table.presence_rank)
         return out_val, out_status
 
     # ---- persistent consumer ("tell" sessions)

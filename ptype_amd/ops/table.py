@@ -83,6 +83,11 @@ class RegistryTable:
         self.affine = 0  # W when the last build verified the rule for every id of the range
         self._astats = None
         self._dir_dirty = True
+        # route mode 4 (csrc/hip/mailbox_sort_dev.hpp): the directory folded into 2 bits
+        # per id for rank `presence_rank` -- here / probe the table / not here -- rebuilt
+        # with the directory, for directories that fit a sort block's LDS (<= 2^18 ids)
+        self.presence = None
+        self.presence_rank = 0
 
     # ------------------------------------------------------------------ directory
     def enable_directory(self, n_ids: int, affine_world: int = 0) -> None:
@@ -107,7 +112,15 @@ class RegistryTable:
         self.dir_rank = torch.empty(self.dir_n, dtype=torch.uint8, device=self.device)
         self.affine_world = int(affine_world)
         self._astats = torch.zeros(2, dtype=torch.int64, device=self.device) if affine_world else None
+        words = int(hip().presence_words(self.dir_n))
+        self.presence = torch.empty(words, dtype=torch.int32, device=self.device) if words else None
         self._dir_dirty = True
+
+    def set_presence_rank(self, rank: int) -> None:
+        """Keep the presence map for ``rank`` (the world-1 runtime's rank 0 by default)."""
+        if int(rank) != self.presence_rank:
+            self.presence_rank = int(rank)
+            self._dir_dirty = True
 
     def directory(self):
         """``(dir tensor | None, n, affine W or 0)`` -- rebuilt on device if the table changed."""
@@ -116,6 +129,9 @@ class RegistryTable:
         if self._dir_dirty:
             hip().table_build_dir(_ptr(self.table), self.cap, _ptr(self.dir), self.dir_n, self.affine_world,
                                   _ptr(self._astats), _stream(self.table), _ptr(self.dir_rank))
+            if self.presence is not None:
+                hip().presence_build(_ptr(self.dir_rank), self.dir_n, self.presence_rank, _ptr(self.presence),
+                                     _stream(self.table))
             self.affine = 0
             if self.affine_world:
                 present, bad = (int(x) for x in self._astats.tolist())  # one sync per rebuild

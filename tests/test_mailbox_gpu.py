@@ -855,12 +855,17 @@ def test_exchange_takes_arrival_rings_for_small_stateless_sends():
     assert bool((st == STATUS_OK).all())
 
 
-def test_arrival_fused_big_batch_presence_map():
+@pytest.mark.parametrize("kept", [True, False])
+def test_arrival_fused_big_batch_presence_map(kept):
     """A stateless batch past 512 tiles through the fused arrival Send: the
     directory's 2-bit presence map staged in LDS (route mode 4), 8-B records per
-    wave; unknown ids (unregistered, past the directory) answered, replies exact."""
+    wave; unknown ids (unregistered, past the directory) answered, replies exact --
+    with the map the registry mirror keeps for this rank, and with one the Send
+    folds itself (the mirror's is kept for another rank)."""
     n, M = 1 << 15, 5 << 20
     t = RegistryTable(4 * n, device=DEV)
+    if not kept:
+        t.set_presence_rank(1)
     ids = torch.cat([torch.arange(n), torch.arange(n + 100, n + 1100)])
     perm = torch.randperm(ids.numel(), generator=torch.Generator().manual_seed(31))
     t.upsert(actor_keys(ids), torch.zeros(ids.numel(), dtype=torch.int32), perm.to(torch.int32))
