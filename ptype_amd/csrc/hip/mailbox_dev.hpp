@@ -134,6 +134,16 @@ __device__ __forceinline__ void put_reply(const ReplyView& rv, uint32_t origin, 
   rv.val[origin] = value;
   rv.st[origin] = status;
 }
+// put_reply for a block's coalesced reply stores: the caller's outputs are not read
+// again by this Send, so the stores stream (non-temporal) instead of filling the L2
+__device__ __forceinline__ void put_reply_nt(const ReplyView& rv, uint32_t origin, int64_t value, int32_t status) {
+  if (rv.slots || (uint64_t)origin >= rv.n) {
+    put_reply(rv, origin, value, status);
+    return;
+  }
+  __builtin_nontemporal_store(value, rv.val + origin);
+  __builtin_nontemporal_store(status, rv.st + origin);
+}
 __device__ __forceinline__ void write_reply(const ReplyView& rv, uint32_t origin, const ReplyRecord& r) {
   put_reply(rv, origin, r.value, r.status);
 }

@@ -956,10 +956,13 @@ __device__ __forceinline__ DrainCounts drain_ring_tile(MboxView mv, SortIn in, u
     ++done;
   }
   __syncthreads();
+  // (non-temporal: 56.4-58.8 vs 54.1-55.7 G on the headline step, one box, alternated; the
+  // same stores measured flat-to-slower in the arrival, SeqFold and N > 1 completions,
+  // which keep plain stores -- profiles/r6_small_sends.md)
 #pragma unroll
   for (int k = 0; k < SK; ++k) {  // the tile's replies, coalesced (misses were answered by the scatter)
     const uint32_t j = (uint32_t)k * kST + threadIdx.x;
-    if (j < n_t && sst[j] != kAbsent) put_reply(rv, in.origin_base + (uint32_t)(i0 + j), sval[j], sst[j]);
+    if (j < n_t && sst[j] != kAbsent) put_reply_nt(rv, in.origin_base + (uint32_t)(i0 + j), sval[j], sst[j]);
   }
   return DrainCounts{done, failed, holes};
 }
