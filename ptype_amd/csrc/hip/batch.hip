@@ -65,7 +65,10 @@ __device__ __forceinline__ uint32_t mod_u64_u32(uint64_t h, uint32_t n, uint64_t
 
 // WIDE: full-range int64 arguments (two more hashes per message) -- values no
 // narrow record holds, for the wide-argument figures (16-B ring records).
-template <bool WIDE>
+// NT: non-temporal stores -- for batches of up to 1 Mi messages (28.8 vs 27.8 G on the 1 Mi
+// step, one box, alternated); an 8 Mi batch keeps plain stores (57.1-57.9 vs 53.6-54.8 G
+// with NT) -- profiles/r6_small_sends.md
+template <bool WIDE, bool NT = false>
 __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict__ actor, int64_t* __restrict__ a0,
                                                            int64_t* __restrict__ a1, int64_t M, uint32_t n_actors,
                                                            uint64_t seed, const uint64_t* __restrict__ seed_ptr,
@@ -82,9 +85,15 @@ __global__ __launch_bounds__(256) void gen_requests_kernel(uint32_t* __restrict_
       x0 = (int64_t)((h >> 20) & 0xffff) - 0x8000;
       x1 = (int64_t)((h >> 40) & 0xffff);
     }
-    actor[i] = ac;
-    a0[i] = x0;
-    if (a1) a1[i] = x1;  // (null: a one-argument batch)
+    if constexpr (NT) {
+      __builtin_nontemporal_store(ac, actor + i);
+      __builtin_nontemporal_store(x0, a0 + i);
+      if (a1) __builtin_nontemporal_store(x1, a1 + i);
+    } else {
+      actor[i] = ac;
+      a0[i] = x0;
+      if (a1) a1[i] = x1;  // (null: a one-argument batch)
+    }
   }
 }
 
@@ -726,12 +735,18 @@ void launch_gen_requests(uintptr_t actor, uintptr_t a0, uintptr_t a1, int64_t M,
   // and grids from 512 to 8192 blocks were no faster -- removed, tools/gen_sweep.py)
   const uint64_t magic = ~0ull / n_actors;
   const dim3 g(grid_cap(M, 256, 8192u));
-  if (wide)
-    hipLaunchKernelGGL(gen_requests_kernel<true>, g, dim3(256), 0, as_stream(stream), (uint32_t*)actor, (int64_t*)a0,
-                       (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr, magic);
-  else
-    hipLaunchKernelGGL(gen_requests_kernel<false>, g, dim3(256), 0, as_stream(stream), (uint32_t*)actor, (int64_t*)a0,
-                       (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr, magic);
+  const bool nt = M <= (1 << 20);
+#define PT_GEN(W, N)                                                                                       \
+  hipLaunchKernelGGL((gen_requests_kernel<W, N>), g, dim3(256), 0, as_stream(stream), (uint32_t*)actor,   \
+                     (int64_t*)a0, (int64_t*)a1, M, n_actors, seed, (const uint64_t*)seed_ptr, magic)
+  if (wide) {
+    if (nt) PT_GEN(true, true);
+    else PT_GEN(true, false);
+  } else {
+    if (nt) PT_GEN(false, true);
+    else PT_GEN(false, false);
+  }
+#undef PT_GEN
   PT_HIP_CHECK(hipGetLastError());
 }
 
