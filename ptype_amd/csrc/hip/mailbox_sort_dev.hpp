@@ -1669,7 +1669,9 @@ __global__ __launch_bounds__(kST) void mbx_complete_ring_kernel(SortIn in, MboxV
     const uint32_t j = (uint32_t)k * kST + threadIdx.x;
     if (j < T) {
       const uint32_t s = L.owner[j];
-      r[k] = srep[((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & qmask)];
+      // (read once: non-temporal -- SeqFold 25.64-25.87 vs 25.22-25.57 G and 25.74-25.85 vs
+      // 25.35-25.52 G in two sessions, alternated; profiles/r6_small_sends.md)
+      r[k] = __builtin_nontemporal_load(srep + (((uint64_t)s << mv.log_q) | ((L.bias[s] + j) & qmask)));
     } else {
       r[k] = u32x4{0u, 0u, 0u, 0xffffffffu};
     }
